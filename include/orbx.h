@@ -1,0 +1,158 @@
+/*
+ * orbx.h -- C ABI of liborbx.so, the MI355X (gfx950) ORB front end that stands
+ * in for ORB-SLAM2's ORBextractor / ORBmatcher hot path
+ * (reference: wjjcdy/orb_slam_2_ros, orb_slam2/include/ORBextractor.h and
+ * orb_slam2/include/ORBmatcher.h).
+ *
+ * Plain C types only: pointers, sizes, status codes.  HIP streams are passed
+ * as `void *` (a hipStream_t, or NULL for the library's own stream).  Every
+ * function returns ORBX_OK (0) or a negative errno-style code; the reference
+ * itself has no error channel, so its silent cases are
+ * mapped explicitly and documented per function.
+ *
+ * The C++ drop-in adapters that re-expose ORB_SLAM2::ORBextractor /
+ * ORB_SLAM2::ORBmatcher over these calls are shown in INTEGRATION.md.
+ */
+#ifndef ORBX_H
+#define ORBX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORBX_OK 0
+#define ORBX_EIO (-5)      /* HIP runtime / kernel failure */
+#define ORBX_ENOMEM (-12)  /* device or host allocation failed */
+#define ORBX_EINVAL (-22)  /* bad argument */
+#define ORBX_ERANGE (-34)  /* output capacity too small (count still reported) */
+#define ORBX_ENODEV (-19)  /* no usable gfx950 device */
+
+/* Same layout and field order as cv::KeyPoint (28 bytes):
+ * pt.x, pt.y, size, angle, response, octave, class_id. */
+typedef struct orbx_keypoint {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} orbx_keypoint;
+
+typedef struct orbx_extractor orbx_extractor;
+
+const char *orbx_strerror(int code);
+int orbx_device_count(void);
+
+/* ---- ORB_SLAM2::ORBextractor ------------------------------------------ */
+
+/* ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST,
+ *              int minThFAST)                         ORBextractor.h:51-52
+ * Returns NULL on bad arguments or when no device is usable. */
+orbx_extractor *orbx_extractor_create(int device, int nfeatures, float scaleFactor,
+                                      int nlevels, int iniThFAST, int minThFAST);
+void orbx_extractor_destroy(orbx_extractor *ex);
+
+/* GetLevels / GetScaleFactor                          ORBextractor.h:63-67 */
+int orbx_extractor_get_levels(const orbx_extractor *ex);
+float orbx_extractor_get_scale_factor(const orbx_extractor *ex);
+/* GetScaleFactors / GetInverseScaleFactors / GetScaleSigmaSquares /
+ * GetInverseScaleSigmaSquares                          ORBextractor.h:69-83
+ * which: 0 = mvScaleFactor, 1 = mvInvScaleFactor, 2 = mvLevelSigma2,
+ * 3 = mvInvLevelSigma2.  Writes min(cap, nlevels) floats, returns nlevels. */
+int orbx_extractor_get_scale_table(const orbx_extractor *ex, int which, float *out, int cap);
+/* mnFeaturesPerLevel (protected in the reference; exposed for tests). */
+int orbx_extractor_get_level_quotas(const orbx_extractor *ex, int32_t *out, int cap);
+
+/* void operator()(InputArray image, InputArray mask, vector<KeyPoint>& kps,
+ *                 OutputArray descriptors)           ORBextractor.h:59-61,
+ *                                                    ORBextractor.cc:1083-1149
+ * Host image in, host keypoints/descriptors out; synchronous.  The mask is
+ * ignored by the reference and is therefore not a parameter.
+ * An empty image (NULL, width or height 0) returns ORBX_OK with *n = -1 and
+ * leaves kps/desc untouched, as the reference does (ORBextractor.cc:1086-1087).
+ * If cap < the keypoint count, returns ORBX_ERANGE with *n = the count. */
+int orbx_extract(orbx_extractor *ex, const uint8_t *image, int width, int height,
+                 size_t pitch, orbx_keypoint *kps, uint8_t *desc, int cap, int *n);
+
+/* std::vector<cv::Mat> mvImagePyramid (public member, ORBextractor.h:85):
+ * host copy of level `level` of the last orbx_extract call (the 19-px border
+ * of the reference's buffers is not materialised).  Writes rows of `w` bytes
+ * at `out_pitch` stride when out != NULL; always reports w, h. */
+int orbx_extractor_pyramid_level(orbx_extractor *ex, int level, uint8_t *out,
+                                 size_t out_pitch, int *w, int *h);
+
+/* ---- batched device API (many cameras / frames per launch) ------------- */
+
+/* Plan buffers for width x height frames, up to max_batch per call. */
+int orbx_extractor_reserve(orbx_extractor *ex, int width, int height, int max_batch);
+/* Keypoint capacity per frame of the current plan (stride of the result arrays). */
+int orbx_extractor_kp_stride(const orbx_extractor *ex);
+/* Extract `batch` device-resident frames (frame b at d_images + b*frame_stride,
+ * rows `pitch` bytes apart) on `stream`; asynchronous.  Results stay on the
+ * device in the current result slot (see orbx_batch_results_device). */
+int orbx_extract_batch_device(orbx_extractor *ex, const uint8_t *d_images,
+                              int64_t frame_stride, int pitch, int batch, void *stream);
+/* Device pointers of the current result slot: frame b's keypoints are
+ * d_kps[b*kp_stride ...], descriptors d_desc[(b*kp_stride + i)*32 ...],
+ * counts d_counts[b]. */
+int orbx_batch_results_device(orbx_extractor *ex, const orbx_keypoint **d_kps,
+                              const uint8_t **d_desc, const int32_t **d_counts);
+/* Synchronous host copy of frame b of the current result slot. */
+int orbx_batch_download(orbx_extractor *ex, int frame, orbx_keypoint *kps, uint8_t *desc,
+                        int cap, int *n);
+
+/* Mono front-end step (the benchmark unit): extract the batch
+ * into the next result slot, then, if the previous slot holds a batch of the
+ * same size, run SearchForInitialization(F1 = previous frame b,
+ * F2 = current frame b, vbPrevMatched = F1 keypoint positions) for every b.
+ * Asynchronous on `stream`. */
+int orbx_mono_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t frame_stride,
+                          int pitch, int batch, int window, float nnratio, int check_ori,
+                          void *stream);
+/* Host copy of frame b's last match result: matches12 (n1 entries, F1 index ->
+ * F2 index or -1), n1, nmatches. */
+int orbx_mono_matches_download(orbx_extractor *ex, int frame, int32_t *matches12, int cap,
+                               int *n1, int *nmatches);
+
+/* Per-stage device time of the last batch (HIP events on the launch stream),
+ * in ms, when profiling is enabled: resize, blur, fast, quadtree, describe,
+ * match.  Returns the number of stages written. */
+int orbx_extractor_set_profiling(orbx_extractor *ex, int on);
+int orbx_extractor_stage_times(orbx_extractor *ex, float *ms, int cap);
+
+/* Debug hooks for stage-level parity tests (current result slot, frame b):
+ * what: 0 = pyramid level, 1 = blurred level (out: w*h bytes, packed rows);
+ *       2 = FAST candidates of the level (out: int32 triples x,y,score in
+ *           reference push order), 3 = quadtree selection of the level (int32
+ *           triples in output order).  Returns element count (bytes for 0/1,
+ *           triples for 2/3) or a negative code; ORBX_ERANGE if cap too small. */
+int orbx_extractor_debug_fetch(orbx_extractor *ex, int frame, int level, int what,
+                               void *out, int64_t cap);
+
+/* ---- ORB_SLAM2::ORBmatcher -------------------------------------------- */
+
+/* static int DescriptorDistance(const cv::Mat &a, const cv::Mat &b)
+ *                                                     ORBmatcher.cc:1649-1665
+ * 32-byte descriptors; host computation (no device round trip). */
+int orbx_descriptor_distance(const uint8_t *a, const uint8_t *b);
+
+/* int SearchForInitialization(Frame &F1, Frame &F2, vector<Point2f>
+ *     &vbPrevMatched, vector<int> &vnMatches12, int windowSize)
+ *                                                     ORBmatcher.cc:406-521
+ * with ORBmatcher(nnratio, checkOri).  Frames are given by their (undistorted)
+ * keypoints and descriptors; the 64x48 grid follows Frame::AssignFeaturesToGrid
+ * for an img_w x img_h image without distortion (Frame.cc:239-256).
+ * prev_xy (2*n1 floats) is vbPrevMatched (read and updated); matches12 (n1)
+ * receives vnMatches12; *nmatches the return value.  Runs on `device`. */
+int orbx_search_for_initialization(int device, const orbx_keypoint *k1, const uint8_t *d1,
+                                   int n1, const orbx_keypoint *k2, const uint8_t *d2, int n2,
+                                   int img_w, int img_h, float *prev_xy, int32_t *matches12,
+                                   int window, float nnratio, int check_ori, int *nmatches);
+
+/* Device evaluation of the restated sincosf / fastAtan2 (test hook). */
+int orbx_debug_trig(int device, const float *angles, float *s, float *c, int n,
+                    const float *ys, const float *xs, float *atan_deg, int m);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ORBX_H */

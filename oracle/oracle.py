@@ -1,0 +1,170 @@
+"""ctypes wrapper of oracle/liborbx_oracle.so -- the CPU restatement.
+
+TEST INFRASTRUCTURE ONLY (see orbx_oracle.h).  Imported by tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg; never by the product
+package.  Parity vs the reference binary: unpinned.
+"""
+from __future__ import annotations
+
+import ctypes
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "liborbx_oracle.so"
+
+KEYPOINT_DTYPE = np.dtype([
+    ("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+    ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4"),
+])
+
+P = ctypes.c_void_p
+I32 = ctypes.c_int
+F32 = ctypes.c_float
+SZ = ctypes.c_size_t
+
+_SIG = {
+    "orbo_cv_round": (I32, [F32]),
+    "orbo_fast_atan2": (F32, [F32, F32]),
+    "orbo_sincosf": (None, [F32, P, P]),
+    "orbo_descriptor_distance": (I32, [P, P]),
+    "orbo_resize_linear": (None, [P, I32, I32, SZ, P, I32, I32, SZ]),
+    "orbo_gauss7": (None, [P, I32, I32, SZ, P, SZ]),
+    "orbo_fast": (I32, [P, I32, I32, SZ, I32, P, I32]),
+    "orbo_levels": (None, [I32, I32, I32, F32, I32, P, P, P, P]),
+    "orbo_pyramid": (SZ, [P, I32, I32, SZ, F32, I32, P]),
+    "orbo_level_candidates": (I32, [P, I32, I32, I32, I32, P, I32]),
+    "orbo_distribute": (I32, [P, I32, I32, I32, I32, P]),
+    "orbo_extract": (I32, [P, I32, I32, SZ, I32, F32, I32, I32, I32, P, P, I32, P]),
+    "orbo_search_for_initialization": (I32, [P, P, I32, P, P, I32, I32, I32, P, P, I32, F32, I32]),
+}
+
+_lib = None
+
+
+def build() -> Path:
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+    return LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            build()
+        l = ctypes.CDLL(str(LIB_PATH))
+        for name, (res, args) in _SIG.items():
+            f = getattr(l, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = l
+    return _lib
+
+
+def _p(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def levels(w, h, nfeatures=1000, scale=1.2, nlevels=8):
+    lw = np.zeros(nlevels, np.int32); lh = np.zeros(nlevels, np.int32)
+    q = np.zeros(nlevels, np.int32); s = np.zeros(nlevels, np.float32)
+    lib().orbo_levels(w, h, nfeatures, scale, nlevels, _p(lw), _p(lh), _p(q), _p(s))
+    return lw, lh, q, s
+
+
+def pyramid(img: np.ndarray, scale=1.2, nlevels=8):
+    img = np.ascontiguousarray(img)
+    h, w = img.shape
+    lw, lh, _, _ = levels(w, h, 1000, scale, nlevels)
+    total = int((lw.astype(np.int64) * lh).sum())
+    out = np.zeros(total, np.uint8)
+    lib().orbo_pyramid(_p(img), w, h, img.strides[0], scale, nlevels, _p(out))
+    res, off = [], 0
+    for l in range(nlevels):
+        n = int(lw[l]) * int(lh[l])
+        res.append(out[off:off + n].reshape(lh[l], lw[l]))
+        off += n
+    return res
+
+
+def resize_linear(src: np.ndarray, dw: int, dh: int) -> np.ndarray:
+    src = np.ascontiguousarray(src)
+    out = np.zeros((dh, dw), np.uint8)
+    lib().orbo_resize_linear(_p(src), src.shape[1], src.shape[0], src.strides[0], _p(out), dw, dh, dw)
+    return out
+
+
+def gauss7(img: np.ndarray) -> np.ndarray:
+    img = np.ascontiguousarray(img)
+    out = np.zeros_like(img)
+    lib().orbo_gauss7(_p(img), img.shape[1], img.shape[0], img.strides[0], _p(out), img.shape[1])
+    return out
+
+
+def fast(img: np.ndarray, threshold: int) -> np.ndarray:
+    img = np.ascontiguousarray(img)
+    cap = img.size
+    out = np.zeros(3 * max(cap, 1), np.int32)
+    n = lib().orbo_fast(_p(img), img.shape[1], img.shape[0], img.strides[0], threshold, _p(out), cap)
+    return out[:3 * n].reshape(n, 3)
+
+
+def level_candidates(lvl: np.ndarray, ini=20, mn=7) -> np.ndarray:
+    lvl = np.ascontiguousarray(lvl)
+    cap = lvl.size
+    out = np.zeros(3 * cap, np.int32)
+    n = lib().orbo_level_candidates(_p(lvl), lvl.shape[1], lvl.shape[0], ini, mn, _p(out), cap)
+    assert n >= 0
+    return out[:3 * n].reshape(n, 3)
+
+
+def distribute(cands: np.ndarray, w: int, h: int, N: int) -> np.ndarray:
+    c = np.ascontiguousarray(cands, dtype=np.int32)
+    sel = np.zeros(max(len(c), 1) + 8, np.int32)
+    n = lib().orbo_distribute(_p(c), len(c), w, h, N, _p(sel))
+    return sel[:n].copy()
+
+
+def extract(img: np.ndarray, nfeatures=1000, scale=1.2, nlevels=8, ini=20, mn=7):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    cap = nfeatures + 16 * nlevels + 64
+    kps = np.zeros(cap, KEYPOINT_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    n = ctypes.c_int(0)
+    rc = lib().orbo_extract(_p(img), w, h, img.strides[0], nfeatures, scale, nlevels, ini, mn,
+                            _p(kps), _p(desc), cap, ctypes.byref(n))
+    if rc != 0:
+        raise RuntimeError(f"oracle extract failed ({rc}, n={n.value})")
+    return kps[:n.value].copy(), desc[:n.value].copy()
+
+
+def search_for_initialization(k1, d1, k2, d2, w, h, prev_xy, window=100, nnratio=0.9, check_ori=True):
+    k1 = np.ascontiguousarray(k1, KEYPOINT_DTYPE); k2 = np.ascontiguousarray(k2, KEYPOINT_DTYPE)
+    d1 = np.ascontiguousarray(d1, np.uint8); d2 = np.ascontiguousarray(d2, np.uint8)
+    prev = np.ascontiguousarray(prev_xy, np.float32).copy()
+    m12 = np.full(max(len(k1), 1), -1, np.int32)
+    nm = lib().orbo_search_for_initialization(_p(k1), _p(d1), len(k1), _p(k2), _p(d2), len(k2), w, h,
+                                              _p(prev), _p(m12), window, nnratio, int(check_ori))
+    return nm, m12[:len(k1)].copy(), prev
+
+
+def fast_atan2(y: float, x: float) -> float:
+    return float(lib().orbo_fast_atan2(y, x))
+
+
+def cv_round(v: float) -> int:
+    return int(lib().orbo_cv_round(v))
+
+
+def sincosf(a: float):
+    s, c = ctypes.c_float(0), ctypes.c_float(0)
+    lib().orbo_sincosf(a, ctypes.byref(s), ctypes.byref(c))
+    return s.value, c.value
+
+
+def descriptor_distance(a, b) -> int:
+    a = np.ascontiguousarray(a, np.uint8); b = np.ascontiguousarray(b, np.uint8)
+    return int(lib().orbo_descriptor_distance(_p(a), _p(b)))

@@ -1,0 +1,770 @@
+/*
+ * orbx_oracle.cpp -- CPU restatement of ORB-SLAM2's ORBextractor / ORBmatcher
+ * hot path, used ONLY as the parity checker and the CPU baseline.
+ *
+ * TEST INFRASTRUCTURE.  Parity vs the reference binary: UNPINNED (see
+ * orbx_oracle.h).  Every function cites the reference line range it restates.
+ * Compile with -ffp-contract=off: the reference (CMake Release, no -march,
+ * CMakeLists.txt:4-6) runs on x86-64 SSE2 without FMA contraction.
+ *
+ * Written as an independent formulation from the HIP kernels: this file follows
+ * the reference's sequential structure (FAST three-row buffers, std::list
+ * quadtree, per-keypoint loops); the kernels use per-pixel arc scores,
+ * round-synchronous node arrays and wave ballots.
+ */
+#include "orbx_oracle.h"
+
+#include <algorithm>
+#include <cfloat>
+#include <climits>
+#include <cmath>
+#include <cstring>
+#include <list>
+#include <vector>
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// OpenCV 3.2 scalar helpers (x86-64): cvRound = cvtss2si/cvtsd2si (half-even).
+// ---------------------------------------------------------------------------
+inline int cv_round(float v) { return (int)std::nearbyint(v); }
+inline int cv_round(double v) { return (int)std::nearbyint(v); }
+inline int cv_floor(float v) { int i = cv_round(v); return i - (float(i) > v ? 1 : 0); }
+inline int cv_floor(double v) { int i = cv_round(v); return i - (double(i) > v ? 1 : 0); }
+inline int cv_ceil(double v) { int i = cv_round(v); return i + (double(i) < v ? 1 : 0); }
+inline short sat_short(float v) {
+    int i = cv_round(v);
+    return (short)std::min(std::max(i, (int)SHRT_MIN), (int)SHRT_MAX);
+}
+inline uint8_t sat_u8(int v) { return (uint8_t)std::min(std::max(v, 0), 255); }
+inline int16_t sat_s16(int v) { return (int16_t)std::min(std::max(v, -32768), 32767); }
+
+// cv::fastAtan2, OpenCV 3.2 core/src/mathfuncs_core.cpp (degrees in [0,360)).
+const float kAtanP1 = 0.9997878412794807f * (float)(180 / M_PI);
+const float kAtanP3 = -0.3258083974640975f * (float)(180 / M_PI);
+const float kAtanP5 = 0.1555786518463281f * (float)(180 / M_PI);
+const float kAtanP7 = -0.04432655554792128f * (float)(180 / M_PI);
+
+float fast_atan2(float y, float x) {
+    float ax = std::fabs(x), ay = std::fabs(y), a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = (((kAtanP7 * c2 + kAtanP5) * c2 + kAtanP3) * c2 + kAtanP1) * c;
+    } else {
+        c = ax / (ay + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = 90.f - (((kAtanP7 * c2 + kAtanP5) * c2 + kAtanP3) * c2 + kAtanP1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+int reflect101(int p, int len) {
+    if (len == 1) return 0;
+    while (p < 0 || p >= len) p = p < 0 ? -p : 2 * len - p - 2;
+    return p;
+}
+
+// ---------------------------------------------------------------------------
+// cv::resize(src, dst, dsize, 0, 0, INTER_LINEAR) for 8UC1, OpenCV 3.2:
+// coefficient tables (resize(), imgwarp.cpp), HResizeLinear<uchar,int,short>
+// and VResizeLinear with the SSE2 VResizeLinearVec_32s8u body for the leading
+// columns and the FixedPtCast<int,uchar,22> scalar tail.
+// Reference call site: ORBextractor.cc:1171.
+// ---------------------------------------------------------------------------
+void resize_linear(const uint8_t *src, int sw, int sh, size_t sstep,
+                   uint8_t *dst, int dw, int dh, size_t dstep) {
+    const double inv_sx = (double)dw / sw, inv_sy = (double)dh / sh;
+    const double scale_x = 1. / inv_sx, scale_y = 1. / inv_sy;
+    std::vector<int> xofs(dw);
+    std::vector<short> ialpha(2 * dw);
+    int xmax = dw;
+    for (int dx = 0; dx < dw; ++dx) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = cv_floor(fx);
+        fx -= sx;
+        if (sx < 0) { fx = 0.f; sx = 0; }
+        if (sx + 1 >= sw) {
+            xmax = std::min(xmax, dx);
+            if (sx >= sw - 1) { fx = 0.f; sx = sw - 1; }
+        }
+        xofs[dx] = sx;
+        ialpha[2 * dx] = sat_short((1.f - fx) * 2048);
+        ialpha[2 * dx + 1] = sat_short(fx * 2048);
+    }
+    // SSE2 vertical pass covers [0, xs); the scalar loop the rest.
+    int xs = 0;
+    while (xs <= dw - 16) xs += 16;
+    while (xs < dw - 4) xs += 4;
+
+    std::vector<int> h0(dw), h1(dw);
+    auto hrow = [&](int r, std::vector<int> &h) {
+        const uint8_t *S = src + (size_t)r * sstep;
+        for (int dx = 0; dx < dw; ++dx) {
+            int sx = xofs[dx];
+            h[dx] = dx < xmax ? S[sx] * ialpha[2 * dx] + S[sx + 1] * ialpha[2 * dx + 1]
+                              : S[sx] * 2048;
+        }
+    };
+    for (int dy = 0; dy < dh; ++dy) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        int sy = cv_floor(fy);
+        fy -= sy;
+        const short b0 = sat_short((1.f - fy) * 2048), b1 = sat_short(fy * 2048);
+        const int r0 = std::min(std::max(sy, 0), sh - 1);
+        const int r1 = std::min(std::max(sy + 1, 0), sh - 1);
+        hrow(r0, h0);
+        hrow(r1, h1);
+        uint8_t *D = dst + (size_t)dy * dstep;
+        for (int x = 0; x < dw; ++x) {
+            if (x < xs) {
+                // _mm_packs_epi32(srai 4) -> _mm_mulhi_epi16 -> _mm_adds_epi16 -> (+2)>>2 -> packus
+                int16_t a = sat_s16(h0[x] >> 4), b = sat_s16(h1[x] >> 4);
+                int16_t p = (int16_t)((a * (int)b0) >> 16), q = (int16_t)((b * (int)b1) >> 16);
+                int16_t s = sat_s16(p + q);
+                s = sat_s16(s + 2);
+                D[x] = sat_u8(s >> 2);
+            } else {
+                D[x] = sat_u8((h0[x] * b0 + h1[x] * b1 + (1 << 21)) >> 22);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// cv::GaussianBlur(img, img, Size(7,7), 2, 2, BORDER_REFLECT_101) for 8UC1,
+// OpenCV 3.2: getGaussianKernel(7, 2, CV_32F) -> fixed-point separable filter
+// (createSeparableLinearFilter: kernels x256 -> int, bits 16): integer row
+// pass, SymmColumnVec_32s8u (SSE2, float accumulation + cvtps rounding) on the
+// leading 4*floor(w/4) columns, FixedPtCastEx<int,uchar>(16) scalar tail.
+// Reference call site: ORBextractor.cc:1129-1130.
+// ---------------------------------------------------------------------------
+void gauss_kernel_int(int k[7]) {
+    float cf[7];
+    double sum = 0;
+    const double sigma = 2.0, scale2X = -0.5 / (sigma * sigma);
+    for (int i = 0; i < 7; ++i) {
+        double x = i - 3.0;
+        cf[i] = (float)std::exp(scale2X * x * x);
+        sum += cf[i];
+    }
+    sum = 1. / sum;
+    for (int i = 0; i < 7; ++i) cf[i] = (float)(cf[i] * sum);
+    for (int i = 0; i < 7; ++i) k[i] = cv_round(cf[i] * 256.f);
+}
+
+void gauss7(const uint8_t *src, int w, int h, size_t sstep, uint8_t *dst, size_t dstep) {
+    int k[7];
+    gauss_kernel_int(k);
+    float kf[4];
+    for (int i = 0; i < 4; ++i) kf[i] = (float)k[3 + i] * (1.f / 65536.f);
+    // Row pass into an int image (exact).
+    std::vector<int> R((size_t)w * h);
+    for (int y = 0; y < h; ++y) {
+        const uint8_t *S = src + (size_t)y * sstep;
+        for (int x = 0; x < w; ++x) {
+            int acc = 0;
+            for (int t = 0; t < 7; ++t) acc += k[t] * S[reflect101(x + t - 3, w)];
+            R[(size_t)y * w + x] = acc;
+        }
+    }
+    const int xs = w & ~3;
+    for (int y = 0; y < h; ++y) {
+        const int *row[7];
+        for (int t = 0; t < 7; ++t) row[t] = &R[(size_t)reflect101(y + t - 3, h) * w];
+        uint8_t *D = dst + (size_t)y * dstep;
+        for (int x = 0; x < w; ++x) {
+            if (x < xs) {
+                float s = (float)row[3][x] * kf[0] + 0.f;
+                for (int t = 1; t <= 3; ++t)
+                    s = s + (float)(row[3 + t][x] + row[3 - t][x]) * kf[t];
+                int v = (int)std::nearbyint(s);  // cvtps_epi32
+                D[x] = sat_u8(sat_s16(v));
+            } else {
+                int s = k[3] * row[3][x];
+                for (int t = 1; t <= 3; ++t) s += k[3 + t] * (row[3 + t][x] + row[3 - t][x]);
+                D[x] = sat_u8((s + (1 << 15)) >> 16);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// cv::FAST(img, kps, th, nonmax=true), TYPE_9_16, OpenCV 3.2 features2d/src/
+// fast.cpp FAST_t<16> + fast_score.cpp cornerScore<16>.  Restated with the
+// three-row score buffers of the original; output order row-major.
+// Reference call sites: ORBextractor.cc:842, 848.
+// ---------------------------------------------------------------------------
+const int kCircle[16][2] = {{0, 3}, {1, 3}, {2, 2}, {3, 1}, {3, 0}, {3, -1}, {2, -2}, {1, -3},
+                            {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
+
+int corner_score16(const uint8_t *p, const int off[25], int threshold) {
+    int v = p[0], d[25];
+    for (int k = 0; k < 25; ++k) d[k] = v - p[off[k]];
+    int a0 = threshold;
+    for (int k = 0; k < 16; k += 2) {
+        int a = std::min(d[k + 1], d[k + 2]);
+        a = std::min(a, d[k + 3]);
+        if (a <= a0) continue;
+        for (int t = 4; t <= 8; ++t) a = std::min(a, d[k + t]);
+        a0 = std::max(a0, std::min(a, d[k]));
+        a0 = std::max(a0, std::min(a, d[k + 9]));
+    }
+    int b0 = -a0;
+    for (int k = 0; k < 16; k += 2) {
+        int b = std::max(d[k + 1], d[k + 2]);
+        b = std::max(b, d[k + 3]);
+        b = std::max(b, d[k + 4]);
+        b = std::max(b, d[k + 5]);
+        if (b >= b0) continue;
+        for (int t = 6; t <= 8; ++t) b = std::max(b, d[k + t]);
+        b0 = std::min(b0, std::max(b, d[k]));
+        b0 = std::min(b0, std::max(b, d[k + 9]));
+    }
+    return -b0 - 1;
+}
+
+struct Corner { int x, y, score; };
+
+void fast9(const uint8_t *img, int w, int h, size_t step, int threshold, std::vector<Corner> &out) {
+    out.clear();
+    threshold = std::min(std::max(threshold, 0), 255);
+    int off[25];
+    for (int k = 0; k < 16; ++k) off[k] = kCircle[k][0] + kCircle[k][1] * (int)step;
+    for (int k = 16; k < 25; ++k) off[k] = off[k - 16];
+    uint8_t tab[512];
+    for (int i = -255; i <= 255; ++i)
+        tab[i + 255] = (uint8_t)(i < -threshold ? 1 : i > threshold ? 2 : 0);
+    std::vector<uint8_t> sbuf(3 * (size_t)std::max(w, 1), 0);
+    std::vector<int> cpos[3];
+    for (int i = 3; i < h - 2; ++i) {
+        uint8_t *curr = &sbuf[(size_t)((i - 3) % 3) * w];
+        std::vector<int> &cp = cpos[(i - 3) % 3];
+        std::memset(curr, 0, w);
+        cp.clear();
+        if (i < h - 3) {
+            for (int j = 3; j < w - 3; ++j) {
+                const uint8_t *p = img + (size_t)i * step + j;
+                const int v = p[0];
+                const uint8_t *t = &tab[255 - v];
+                int d = t[p[off[0]]] | t[p[off[8]]];
+                if (!d) continue;
+                d &= t[p[off[2]]] | t[p[off[10]]];
+                d &= t[p[off[4]]] | t[p[off[12]]];
+                d &= t[p[off[6]]] | t[p[off[14]]];
+                if (!d) continue;
+                d &= t[p[off[1]]] | t[p[off[9]]];
+                d &= t[p[off[3]]] | t[p[off[11]]];
+                d &= t[p[off[5]]] | t[p[off[13]]];
+                d &= t[p[off[7]]] | t[p[off[15]]];
+                for (int pass = 0; pass < 2; ++pass) {
+                    if (!(d & (1 << pass))) continue;
+                    int run = 0;
+                    for (int k = 0; k < 25; ++k) {
+                        int x = p[off[k]];
+                        bool hit = pass == 0 ? x < v - threshold : x > v + threshold;
+                        if (!hit) { run = 0; continue; }
+                        if (++run > 8) {
+                            cp.push_back(j);
+                            curr[j] = (uint8_t)corner_score16(p, off, threshold);
+                            break;
+                        }
+                    }
+                }
+            }
+        }
+        if (i == 3) continue;
+        const uint8_t *prev = &sbuf[(size_t)((i - 4 + 3) % 3) * w];
+        const uint8_t *pprev = &sbuf[(size_t)((i - 5 + 3) % 3) * w];
+        for (int j : cpos[(i - 4 + 3) % 3]) {
+            int s = prev[j];
+            if (s > prev[j + 1] && s > prev[j - 1] && s > pprev[j - 1] && s > pprev[j] &&
+                s > pprev[j + 1] && s > curr[j - 1] && s > curr[j] && s > curr[j + 1])
+                out.push_back({j, i - 1, s});
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// ORBextractor constructor tables (ORBextractor.cc:416-479).
+// ---------------------------------------------------------------------------
+struct Geometry {
+    int nlevels;
+    std::vector<float> scale, inv_scale;
+    std::vector<int> w, h, quota;
+    int umax[16];
+};
+
+Geometry make_geometry(int W, int H, int nfeatures, float scaleFactorF, int nlevels) {
+    Geometry g;
+    g.nlevels = nlevels;
+    const double scaleFactor = scaleFactorF;  // member is double (ORBextractor.h:98)
+    g.scale.assign(nlevels, 1.f);
+    for (int i = 1; i < nlevels; ++i) g.scale[i] = (float)(g.scale[i - 1] * scaleFactor);
+    g.inv_scale.resize(nlevels);
+    for (int i = 0; i < nlevels; ++i) g.inv_scale[i] = 1.0f / g.scale[i];
+    g.quota.assign(nlevels, 0);
+    float factor = (float)(1.0f / scaleFactor);
+    float nDesired = nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)nlevels));
+    int sum = 0;
+    for (int l = 0; l < nlevels - 1; ++l) {
+        g.quota[l] = cv_round(nDesired);
+        sum += g.quota[l];
+        nDesired *= factor;
+    }
+    g.quota[nlevels - 1] = std::max(nfeatures - sum, 0);
+    g.w.resize(nlevels);
+    g.h.resize(nlevels);
+    for (int l = 0; l < nlevels; ++l) {
+        g.w[l] = cv_round((float)W * g.inv_scale[l]);
+        g.h[l] = cv_round((float)H * g.inv_scale[l]);
+    }
+    // umax (ORBextractor.cc:463-478)
+    const int HP = 15;
+    int vmax = cv_floor(HP * std::sqrt(2.f) / 2 + 1);
+    int vmin = cv_ceil(HP * std::sqrt(2.f) / 2);
+    const double hp2 = HP * HP;
+    for (int v = 0; v <= vmax; ++v) g.umax[v] = cv_round(std::sqrt(hp2 - v * v));
+    for (int v = HP, v0 = 0; v >= vmin; --v) {
+        while (g.umax[v0] == g.umax[v0 + 1]) ++v0;
+        g.umax[v] = v0;
+        ++v0;
+    }
+    return g;
+}
+
+// ---------------------------------------------------------------------------
+// Cell loop of ComputeKeyPointsOctTree (ORBextractor.cc:796-863).
+// ---------------------------------------------------------------------------
+void level_candidates(const uint8_t *lvl, int w, int h, size_t step, int iniTh, int minTh,
+                      std::vector<Corner> &cands) {
+    cands.clear();
+    const float W = 30;
+    const int minBX = 19 - 3, minBY = minBX;
+    const int maxBX = w - 19 + 3, maxBY = h - 19 + 3;
+    const float width = (float)(maxBX - minBX), height = (float)(maxBY - minBY);
+    const int nCols = (int)(width / W), nRows = (int)(height / W);
+    if (nCols <= 0 || nRows <= 0) return;
+    const int wCell = (int)std::ceil(width / nCols), hCell = (int)std::ceil(height / nRows);
+    std::vector<Corner> cell;
+    for (int i = 0; i < nRows; ++i) {
+        const float iniY = (float)(minBY + i * hCell);
+        float maxY = iniY + hCell + 6;
+        if (iniY >= maxBY - 3) continue;
+        if (maxY > maxBY) maxY = (float)maxBY;
+        for (int j = 0; j < nCols; ++j) {
+            const float iniX = (float)(minBX + j * wCell);
+            float maxX = iniX + wCell + 6;
+            if (iniX >= maxBX - 6) continue;
+            if (maxX > maxBX) maxX = (float)maxBX;
+            const int y0 = (int)iniY, x0 = (int)iniX;
+            const uint8_t *sub = lvl + (size_t)y0 * step + x0;
+            const int sw = (int)maxX - x0, sh = (int)maxY - y0;
+            fast9(sub, sw, sh, step, iniTh, cell);
+            if (cell.empty()) fast9(sub, sw, sh, step, minTh, cell);
+            for (const Corner &c : cell) cands.push_back({c.x + x0, c.y + y0, c.score});
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// DistributeOctTree (ORBextractor.cc:561-787) + ExtractorNode::DivideNode
+// (ORBextractor.cc:498-554), restated on std::list with the reference's
+// push_front / erase order.  The reference sorts (size, ExtractorNode*) pairs
+// (:705-708), i.e. breaks size ties by heap address; this restatement breaks
+// them by creation number (later-created == larger address), documented in
+// DESIGN.md §3.4.
+// Coordinates are relative to (minBorderX, minBorderY) = (16, 16).
+// ---------------------------------------------------------------------------
+struct QNode {
+    int x0, y0, x1, y1;
+    std::vector<int> keys;
+    bool no_more = false;
+    long seq = 0;
+    std::list<QNode>::iterator self;
+};
+
+void divide(const QNode &p, const std::vector<Corner> &c, QNode ch[4]) {
+    const int hx = (int)std::ceil((float)(p.x1 - p.x0) / 2);
+    const int hy = (int)std::ceil((float)(p.y1 - p.y0) / 2);
+    const int mx = p.x0 + hx, my = p.y0 + hy;
+    ch[0].x0 = p.x0; ch[0].y0 = p.y0; ch[0].x1 = mx;   ch[0].y1 = my;
+    ch[1].x0 = mx;   ch[1].y0 = p.y0; ch[1].x1 = p.x1; ch[1].y1 = my;
+    ch[2].x0 = p.x0; ch[2].y0 = my;   ch[2].x1 = mx;   ch[2].y1 = p.y1;
+    ch[3].x0 = mx;   ch[3].y0 = my;   ch[3].x1 = p.x1; ch[3].y1 = p.y1;
+    for (int q = 0; q < 4; ++q) ch[q].keys.clear();
+    for (int k : p.keys) {
+        const int x = c[k].x - 16, y = c[k].y - 16;
+        int q = (x < mx) ? (y < my ? 0 : 2) : (y < my ? 1 : 3);
+        ch[q].keys.push_back(k);
+    }
+    for (int q = 0; q < 4; ++q) ch[q].no_more = ch[q].keys.size() == 1;
+}
+
+std::vector<int> distribute(const std::vector<Corner> &c, int w, int h, int N) {
+    const int minX = 16, maxX = w - 16, minY = 16, maxY = h - 16;
+    std::vector<int> result;
+    if (c.empty()) return result;
+    const int nIni = (int)std::round((float)(maxX - minX) / (maxY - minY));
+    const float hX = (float)(maxX - minX) / nIni;
+    long seq = 0;
+    std::list<QNode> L;
+    std::vector<QNode *> ini(nIni);
+    for (int i = 0; i < nIni; ++i) {
+        QNode n;
+        n.x0 = (int)(hX * (float)i);
+        n.x1 = (int)(hX * (float)(i + 1));
+        n.y0 = 0;
+        n.y1 = maxY - minY;
+        n.seq = seq++;
+        L.push_back(n);
+        ini[i] = &L.back();
+    }
+    for (size_t k = 0; k < c.size(); ++k) {
+        const float x = (float)(c[k].x - 16);
+        ini[(size_t)(x / hX)]->keys.push_back((int)k);
+    }
+    for (auto it = L.begin(); it != L.end();) {
+        if (it->keys.size() == 1) { it->no_more = true; ++it; }
+        else if (it->keys.empty()) it = L.erase(it);
+        else ++it;
+    }
+
+    struct Expand { int size; long seq; QNode *node; };
+    std::vector<Expand> expand;
+    auto push_children = [&](QNode ch[4], bool count_expand, int *nToExpand) {
+        for (int q = 0; q < 4; ++q) {
+            if (ch[q].keys.empty()) continue;
+            ch[q].seq = seq++;
+            L.push_front(ch[q]);
+            if (ch[q].keys.size() > 1) {
+                if (count_expand) ++*nToExpand;
+                expand.push_back({(int)ch[q].keys.size(), ch[q].seq, &L.front()});
+                L.front().self = L.begin();
+            }
+        }
+    };
+
+    bool finish = false;
+    while (!finish) {
+        const int prevSize = (int)L.size();
+        int nToExpand = 0;
+        expand.clear();
+        for (auto it = L.begin(); it != L.end();) {
+            if (it->no_more) { ++it; continue; }
+            QNode ch[4];
+            divide(*it, c, ch);
+            push_children(ch, true, &nToExpand);
+            it = L.erase(it);
+        }
+        if ((int)L.size() >= N || (int)L.size() == prevSize) {
+            finish = true;
+        } else if ((int)L.size() + nToExpand * 3 > N) {
+            while (!finish) {
+                const int prev = (int)L.size();
+                std::vector<Expand> todo = expand;
+                expand.clear();
+                std::sort(todo.begin(), todo.end(), [](const Expand &a, const Expand &b) {
+                    return a.size != b.size ? a.size < b.size : a.seq < b.seq;
+                });
+                for (int j = (int)todo.size() - 1; j >= 0; --j) {
+                    QNode ch[4];
+                    divide(*todo[j].node, c, ch);
+                    push_children(ch, false, nullptr);
+                    L.erase(todo[j].node->self);
+                    if ((int)L.size() >= N) break;
+                }
+                if ((int)L.size() >= N || (int)L.size() == prev) finish = true;
+            }
+        }
+    }
+    for (const QNode &n : L) {
+        int best = n.keys[0];
+        for (size_t k = 1; k < n.keys.size(); ++k)
+            if (c[n.keys[k]].score > c[best].score) best = n.keys[k];
+        result.push_back(best);
+    }
+    return result;
+}
+
+// IC_Angle (ORBextractor.cc:77-104) on the unblurred level.
+float ic_angle(const uint8_t *lvl, size_t step, int x, int y, const int umax[16]) {
+    const uint8_t *center = lvl + (size_t)y * step + x;
+    int m01 = 0, m10 = 0;
+    for (int u = -15; u <= 15; ++u) m10 += u * center[u];
+    for (int v = 1; v <= 15; ++v) {
+        int vsum = 0;
+        const int d = umax[v];
+        for (int u = -d; u <= d; ++u) {
+            const int plus = center[u + v * (int)step], minus = center[u - v * (int)step];
+            vsum += plus - minus;
+            m10 += u * (plus + minus);
+        }
+        m01 += v * vsum;
+    }
+    return fast_atan2((float)m01, (float)m10);
+}
+
+const int8_t kPattern[512][2] = {
+#define ORBX_PATTERN_BEGIN
+#define ORBX_PATTERN_END
+#include "../orb_slam_2_ros_amd/csrc/orb_pattern.inc"
+#undef ORBX_PATTERN_BEGIN
+#undef ORBX_PATTERN_END
+};
+
+// computeOrbDescriptor (ORBextractor.cc:106-147) on the blurred level.
+void orb_descriptor(const uint8_t *blur, size_t step, int x, int y, float angle_deg, uint8_t *desc) {
+    const float factorPI = (float)(M_PI / 180.f);
+    const float angle = angle_deg * factorPI;
+    const float a = (float)std::cos(angle), b = (float)std::sin(angle);
+    const uint8_t *center = blur + (size_t)y * step + x;
+    auto sample = [&](int idx) {
+        const float px = (float)kPattern[idx][0], py = (float)kPattern[idx][1];
+        const int r = cv_round(px * b + py * a);
+        const int col = cv_round(px * a - py * b);
+        return (int)center[r * (int)step + col];
+    };
+    for (int i = 0; i < 32; ++i) {
+        int val = 0;
+        for (int k = 0; k < 8; ++k) {
+            const int p = 16 * i + 2 * k;
+            val |= (sample(p) < sample(p + 1)) << k;
+        }
+        desc[i] = (uint8_t)val;
+    }
+}
+
+int hamming32(const uint8_t *a, const uint8_t *b) {
+    int dist = 0;
+    for (int i = 0; i < 8; ++i) {
+        uint32_t pa, pb;
+        std::memcpy(&pa, a + 4 * i, 4);
+        std::memcpy(&pb, b + 4 * i, 4);
+        uint32_t v = pa ^ pb;
+        v = v - ((v >> 1) & 0x55555555u);
+        v = (v & 0x33333333u) + ((v >> 2) & 0x33333333u);
+        dist += (int)((((v + (v >> 4)) & 0xF0F0F0Fu) * 0x1010101u) >> 24);
+    }
+    return dist;
+}
+
+struct Pyramid {
+    std::vector<std::vector<uint8_t>> lv;
+};
+
+Pyramid build_pyramid(const uint8_t *img, int W, int H, size_t step, const Geometry &g) {
+    Pyramid p;
+    p.lv.resize(g.nlevels);
+    p.lv[0].resize((size_t)W * H);
+    for (int y = 0; y < H; ++y) std::memcpy(&p.lv[0][(size_t)y * W], img + (size_t)y * step, W);
+    for (int l = 1; l < g.nlevels; ++l) {
+        p.lv[l].resize((size_t)g.w[l] * g.h[l]);
+        resize_linear(p.lv[l - 1].data(), g.w[l - 1], g.h[l - 1], g.w[l - 1],
+                      p.lv[l].data(), g.w[l], g.h[l], g.w[l]);
+    }
+    return p;
+}
+
+}  // namespace
+
+// =============================================================================
+extern "C" {
+
+int orbo_cv_round(float v) { return cv_round(v); }
+float orbo_fast_atan2(float y, float x) { return fast_atan2(y, x); }
+void orbo_sincosf(float a, float *s, float *c) { *c = (float)std::cos(a); *s = (float)std::sin(a); }
+int orbo_descriptor_distance(const uint8_t *a, const uint8_t *b) { return hamming32(a, b); }
+
+void orbo_resize_linear(const uint8_t *src, int sw, int sh, size_t sstep,
+                        uint8_t *dst, int dw, int dh, size_t dstep) {
+    resize_linear(src, sw, sh, sstep, dst, dw, dh, dstep);
+}
+
+void orbo_gauss7(const uint8_t *src, int w, int h, size_t sstep, uint8_t *dst, size_t dstep) {
+    gauss7(src, w, h, sstep, dst, dstep);
+}
+
+int orbo_fast(const uint8_t *img, int w, int h, size_t step, int threshold, int32_t *xys, int cap) {
+    std::vector<Corner> out;
+    fast9(img, w, h, step, threshold, out);
+    int n = (int)out.size();
+    for (int i = 0; i < n && i < cap; ++i) {
+        xys[3 * i] = out[i].x; xys[3 * i + 1] = out[i].y; xys[3 * i + 2] = out[i].score;
+    }
+    return n;
+}
+
+void orbo_levels(int w, int h, int nfeatures, float scaleFactor, int nlevels,
+                 int *lw, int *lh, int *quota, float *scale) {
+    Geometry g = make_geometry(w, h, nfeatures, scaleFactor, nlevels);
+    for (int l = 0; l < nlevels; ++l) {
+        lw[l] = g.w[l]; lh[l] = g.h[l]; quota[l] = g.quota[l]; scale[l] = g.scale[l];
+    }
+}
+
+size_t orbo_pyramid(const uint8_t *img, int w, int h, size_t step, float scaleFactor, int nlevels,
+                    uint8_t *out) {
+    Geometry g = make_geometry(w, h, 1000, scaleFactor, nlevels);
+    Pyramid p = build_pyramid(img, w, h, step, g);
+    size_t off = 0;
+    for (int l = 0; l < nlevels; ++l) {
+        std::memcpy(out + off, p.lv[l].data(), p.lv[l].size());
+        off += p.lv[l].size();
+    }
+    return off;
+}
+
+int orbo_level_candidates(const uint8_t *lvl, int w, int h, int iniTh, int minTh,
+                          int32_t *xys, int cap) {
+    std::vector<Corner> c;
+    level_candidates(lvl, w, h, w, iniTh, minTh, c);
+    const int n = (int)c.size();
+    if (n > cap) return -n;
+    for (int i = 0; i < n; ++i) {
+        xys[3 * i] = c[i].x; xys[3 * i + 1] = c[i].y; xys[3 * i + 2] = c[i].score;
+    }
+    return n;
+}
+
+int orbo_distribute(const int32_t *xys, int n, int w, int h, int N, int32_t *sel) {
+    std::vector<Corner> c(n);
+    for (int i = 0; i < n; ++i) c[i] = {xys[3 * i], xys[3 * i + 1], xys[3 * i + 2]};
+    std::vector<int> r = distribute(c, w, h, N);
+    for (size_t i = 0; i < r.size(); ++i) sel[i] = r[i];
+    return (int)r.size();
+}
+
+int orbo_extract(const uint8_t *img, int w, int h, size_t step,
+                 int nfeatures, float scaleFactor, int nlevels, int iniTh, int minTh,
+                 orbo_keypoint *kps, uint8_t *desc, int cap, int *n_out) {
+    *n_out = 0;
+    if (!img || w <= 0 || h <= 0) return 0;  // empty image: outputs untouched (:1086-1087)
+    Geometry g = make_geometry(w, h, nfeatures, scaleFactor, nlevels);
+    Pyramid p = build_pyramid(img, w, h, step, g);
+    struct LevelOut { std::vector<Corner> keys; std::vector<float> ang; };
+    std::vector<LevelOut> lo(nlevels);
+    int total = 0;
+    std::vector<Corner> cands;
+    for (int l = 0; l < nlevels; ++l) {
+        level_candidates(p.lv[l].data(), g.w[l], g.h[l], g.w[l], iniTh, minTh, cands);
+        std::vector<int> sel = distribute(cands, g.w[l], g.h[l], g.quota[l]);
+        for (int s : sel) lo[l].keys.push_back(cands[s]);
+        for (const Corner &k : lo[l].keys) lo[l].ang.push_back(ic_angle(p.lv[l].data(), g.w[l], k.x, k.y, g.umax));
+        total += (int)sel.size();
+    }
+    *n_out = total;
+    if (total > cap) return -1;
+    int o = 0;
+    std::vector<uint8_t> blur;
+    for (int l = 0; l < nlevels; ++l) {
+        if (lo[l].keys.empty()) continue;
+        blur.resize((size_t)g.w[l] * g.h[l]);
+        gauss7(p.lv[l].data(), g.w[l], g.h[l], g.w[l], blur.data(), g.w[l]);
+        const float size = (float)(int)(31 * g.scale[l]);
+        for (size_t i = 0; i < lo[l].keys.size(); ++i, ++o) {
+            const Corner &k = lo[l].keys[i];
+            orb_descriptor(blur.data(), g.w[l], k.x, k.y, lo[l].ang[i], desc + 32 * (size_t)o);
+            orbo_keypoint &kp = kps[o];
+            kp.x = (float)k.x; kp.y = (float)k.y;
+            if (l != 0) { kp.x *= g.scale[l]; kp.y *= g.scale[l]; }
+            kp.size = size;
+            kp.angle = lo[l].ang[i];
+            kp.response = (float)k.score;
+            kp.octave = l;
+            kp.class_id = -1;
+        }
+    }
+    return 0;
+}
+
+// SearchForInitialization (ORBmatcher.cc:406-521) with Frame grid semantics
+// (Frame.cc:239-256 AssignFeaturesToGrid, :354-412 GetFeaturesInArea,
+// :415-425 PosInGrid) and ComputeThreeMaxima (ORBmatcher.cc:1603-1644).
+int orbo_search_for_initialization(const orbo_keypoint *k1, const uint8_t *d1, int n1,
+                                   const orbo_keypoint *k2, const uint8_t *d2, int n2,
+                                   int img_w, int img_h, float *prev_xy, int32_t *m12,
+                                   int window, float nnratio, int check_ori) {
+    const int GC = 64, GR = 48, HL = 30, TH_LOW = 50;
+    const float minX = 0.f, maxX = (float)img_w, minY = 0.f, maxY = (float)img_h;
+    const float invW = (float)GC / (maxX - minX), invH = (float)GR / (maxY - minY);
+    std::vector<std::vector<int>> grid((size_t)GC * GR);
+    for (int i = 0; i < n2; ++i) {
+        const int px = (int)std::round((k2[i].x - minX) * invW);
+        const int py = (int)std::round((k2[i].y - minY) * invH);
+        if (px < 0 || px >= GC || py < 0 || py >= GR) continue;
+        grid[(size_t)px * GR + py].push_back(i);
+    }
+    for (int i = 0; i < n1; ++i) m12[i] = -1;
+    std::vector<int> rot[HL];
+    const float factor = 1.0f / HL;
+    std::vector<int> matchedDist(n2, INT_MAX), m21(n2, -1);
+    int nmatches = 0;
+    const float r = (float)window;
+    std::vector<int> cand;
+    for (int i1 = 0; i1 < n1; ++i1) {
+        if (k1[i1].octave > 0) continue;
+        const float x = prev_xy[2 * i1], y = prev_xy[2 * i1 + 1];
+        cand.clear();
+        const int cx0 = std::max(0, (int)std::floor((x - minX - r) * invW));
+        const int cx1 = std::min(GC - 1, (int)std::ceil((x - minX + r) * invW));
+        const int cy0 = std::max(0, (int)std::floor((y - minY - r) * invH));
+        const int cy1 = std::min(GR - 1, (int)std::ceil((y - minY + r) * invH));
+        if (cx0 < GC && cx1 >= 0 && cy0 < GR && cy1 >= 0) {
+            for (int ix = cx0; ix <= cx1; ++ix)
+                for (int iy = cy0; iy <= cy1; ++iy)
+                    for (int j : grid[(size_t)ix * GR + iy]) {
+                        if (k2[j].octave < 0 || k2[j].octave > 0) continue;
+                        if (std::fabs(k2[j].x - x) < r && std::fabs(k2[j].y - y) < r) cand.push_back(j);
+                    }
+        }
+        if (cand.empty()) continue;
+        int best = INT_MAX, best2 = INT_MAX, bestIdx = -1;
+        for (int i2 : cand) {
+            const int dist = hamming32(d1 + 32 * (size_t)i1, d2 + 32 * (size_t)i2);
+            if (matchedDist[i2] <= dist) continue;
+            if (dist < best) { best2 = best; best = dist; bestIdx = i2; }
+            else if (dist < best2) best2 = dist;
+        }
+        if (best <= TH_LOW && best < (float)best2 * nnratio) {
+            if (m21[bestIdx] >= 0) { m12[m21[bestIdx]] = -1; --nmatches; }
+            m12[i1] = bestIdx;
+            m21[bestIdx] = i1;
+            matchedDist[bestIdx] = best;
+            ++nmatches;
+            if (check_ori) {
+                float rotv = k1[i1].angle - k2[bestIdx].angle;
+                if (rotv < 0.0) rotv += 360.0f;
+                int bin = (int)std::round(rotv * factor);
+                if (bin == HL) bin = 0;
+                rot[bin].push_back(i1);
+            }
+        }
+    }
+    if (check_ori) {
+        int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+        for (int i = 0; i < HL; ++i) {
+            const int s = (int)rot[i].size();
+            if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
+            else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
+            else if (s > max3) { max3 = s; ind3 = i; }
+        }
+        if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+        else if (max3 < 0.1f * (float)max1) ind3 = -1;
+        for (int i = 0; i < HL; ++i) {
+            if (i == ind1 || i == ind2 || i == ind3) continue;
+            for (int idx1 : rot[i])
+                if (m12[idx1] >= 0) { m12[idx1] = -1; --nmatches; }
+        }
+    }
+    for (int i1 = 0; i1 < n1; ++i1)
+        if (m12[i1] >= 0) {
+            prev_xy[2 * i1] = k2[m12[i1]].x;
+            prev_xy[2 * i1 + 1] = k2[m12[i1]].y;
+        }
+    return nmatches;
+}
+
+}  // extern "C"

@@ -1,0 +1,90 @@
+/*
+ * orbx_oracle.h -- CPU restatement of the ORB-SLAM2 feature hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (orb_slam_2_ros_amd/,
+ * include/) links or calls this library; only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg load it, as the checker / CPU baseline.
+ *
+ * PARITY STATUS: UNPINNED against the reference binary.  The reference
+ * (wjjcdy/orb_slam_2_ros) ships no tests, fixtures or golden vectors, and its
+ * extractor needs OpenCV (not vendored, absent here), so it cannot be built in
+ * this container.  This file restates (a) the reference's own logic from its
+ * sources (file:line cited per function) and (b) the OpenCV 3.2.0 primitives it
+ * calls (x86-64 SSE2 code paths, IPP off: the Ubuntu 18.04 / ROS Melodic build
+ * named by reference docker/melodic/Dockerfile:1), spelled out in DESIGN.md §3.
+ * sinf/cosf are taken from glibc directly, as the reference does.
+ */
+#ifndef ORBX_ORACLE_H
+#define ORBX_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Same 28-byte layout as cv::KeyPoint (pt.x, pt.y, size, angle, response,
+ * octave, class_id) and as orbx_keypoint in include/orbx.h. */
+typedef struct {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} orbo_keypoint;
+
+/* ---- primitives (KAT targets) ---- */
+int   orbo_cv_round(float v);
+float orbo_fast_atan2(float y, float x);
+void  orbo_sincosf(float a, float *s, float *c);
+int   orbo_descriptor_distance(const uint8_t *a, const uint8_t *b);
+/* cv::resize(INTER_LINEAR, 8U) restated (OpenCV 3.2 SSE2). */
+void  orbo_resize_linear(const uint8_t *src, int sw, int sh, size_t sstep,
+                         uint8_t *dst, int dw, int dh, size_t dstep);
+/* cv::GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) on a borderless image. */
+void  orbo_gauss7(const uint8_t *src, int w, int h, size_t sstep,
+                  uint8_t *dst, size_t dstep);
+/* cv::FAST(TYPE_9_16, nonmax=true) on a sub-image; returns #keypoints written
+ * as (x, y, score) triples (row-major order), up to cap. */
+int   orbo_fast(const uint8_t *img, int w, int h, size_t step, int threshold,
+                int32_t *xys, int cap);
+
+/* ---- extractor (ORBextractor) ---- */
+/* Level geometry of ORBextractor(nfeat, scale, nlev, ...): per level the
+ * width, height, feature quota and scale factor (ORBextractor.cc:416-455,
+ * 1157-1159). Arrays have nlevels entries. */
+void  orbo_levels(int w, int h, int nfeatures, float scaleFactor, int nlevels,
+                  int *lw, int *lh, int *quota, float *scale);
+/* ComputePyramid: writes all levels contiguously (level l at sum of previous
+ * w*h, rows packed).  Returns total bytes. */
+size_t orbo_pyramid(const uint8_t *img, int w, int h, size_t step,
+                    float scaleFactor, int nlevels, uint8_t *out);
+/* FAST candidates of one level, cell loop of ComputeKeyPointsOctTree
+ * (ORBextractor.cc:796-863): (x, y, score) in level pixel coordinates, in the
+ * order the reference pushes them.  Returns the count (or -needed if > cap). */
+int   orbo_level_candidates(const uint8_t *lvl, int w, int h, int iniTh, int minTh,
+                            int32_t *xys, int cap);
+/* DistributeOctTree on a candidate list (ORBextractor.cc:561-787): writes the
+ * selected candidate indices in output order; returns the count. */
+int   orbo_distribute(const int32_t *xys, int n, int w, int h, int N, int32_t *sel);
+/* Full operator() (ORBextractor.cc:1083-1149).  Returns 0, or -1 if cap is
+ * too small (then *n_out holds the required count). */
+int   orbo_extract(const uint8_t *img, int w, int h, size_t step,
+                   int nfeatures, float scaleFactor, int nlevels,
+                   int iniThFAST, int minThFAST,
+                   orbo_keypoint *kps, uint8_t *desc, int cap, int *n_out);
+
+/* ---- matcher (ORBmatcher::SearchForInitialization, ORBmatcher.cc:406-521) ----
+ * Frames are described by keypoints (undistorted == distorted, k1 = 0) and
+ * descriptors; the 64x48 grid is built from (img_w, img_h) as
+ * Frame::AssignFeaturesToGrid does (Frame.cc:239-256, 415-425).
+ * prev_xy (2*n1 floats) is read and updated like vbPrevMatched; matches12
+ * (n1 ints) receives vnMatches12.  Returns nmatches. */
+int   orbo_search_for_initialization(const orbo_keypoint *k1, const uint8_t *d1, int n1,
+                                     const orbo_keypoint *k2, const uint8_t *d2, int n2,
+                                     int img_w, int img_h,
+                                     float *prev_xy, int32_t *matches12,
+                                     int window, float nnratio, int check_ori);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,108 @@
+"""ctypes binding of liborbx.so (the C ABI in include/orbx.h).
+
+The library is built in-tree (``orb_slam_2_ros_amd/liborbx.so``) by
+``__graft_entry__.build()`` / ``make -C orb_slam_2_ros_amd/csrc``.  There is no
+fallback: if the library or a gfx950 device is missing, the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import numpy as np
+
+LIB_PATH = Path(__file__).resolve().parent / "liborbx.so"
+
+ORBX_OK = 0
+ORBX_EIO = -5
+ORBX_ENOMEM = -12
+ORBX_EINVAL = -22
+ORBX_ERANGE = -34
+ORBX_ENODEV = -19
+
+# cv::KeyPoint field order (orbx_keypoint, 28 bytes).
+KEYPOINT_DTYPE = np.dtype([
+    ("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+    ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4"),
+])
+assert KEYPOINT_DTYPE.itemsize == 28
+
+
+class OrbxError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        self.code = code
+        msg = _strerror(code) if _LIB is not None else str(code)
+        super().__init__(f"{what}: {msg} ({code})")
+
+
+_LIB = None
+
+P = ctypes.c_void_p
+I32 = ctypes.c_int
+I64 = ctypes.c_int64
+F32 = ctypes.c_float
+SZ = ctypes.c_size_t
+
+_SIGNATURES = {
+    "orbx_strerror": (ctypes.c_char_p, [I32]),
+    "orbx_device_count": (I32, []),
+    "orbx_extractor_create": (P, [I32, I32, F32, I32, I32, I32]),
+    "orbx_extractor_destroy": (None, [P]),
+    "orbx_extractor_get_levels": (I32, [P]),
+    "orbx_extractor_get_scale_factor": (F32, [P]),
+    "orbx_extractor_get_scale_table": (I32, [P, I32, P, I32]),
+    "orbx_extractor_get_level_quotas": (I32, [P, P, I32]),
+    "orbx_extract": (I32, [P, P, I32, I32, SZ, P, P, I32, P]),
+    "orbx_extractor_pyramid_level": (I32, [P, I32, P, SZ, P, P]),
+    "orbx_extractor_reserve": (I32, [P, I32, I32, I32]),
+    "orbx_extractor_kp_stride": (I32, [P]),
+    "orbx_extract_batch_device": (I32, [P, P, I64, I32, I32, P]),
+    "orbx_batch_results_device": (I32, [P, P, P, P]),
+    "orbx_batch_download": (I32, [P, I32, P, P, I32, P]),
+    "orbx_mono_step_device": (I32, [P, P, I64, I32, I32, I32, F32, I32, P]),
+    "orbx_mono_matches_download": (I32, [P, I32, P, I32, P, P]),
+    "orbx_extractor_set_profiling": (I32, [P, I32]),
+    "orbx_extractor_stage_times": (I32, [P, P, I32]),
+    "orbx_extractor_debug_fetch": (I32, [P, I32, I32, I32, P, I64]),
+    "orbx_descriptor_distance": (I32, [P, P]),
+    "orbx_search_for_initialization": (I32, [I32, P, P, I32, P, P, I32, I32, I32, P, P, I32, F32, I32, P]),
+    "orbx_debug_trig": (I32, [I32, P, P, P, I32, P, P, P, I32]),
+}
+
+EXPORTED = tuple(_SIGNATURES)
+
+
+def load(path: os.PathLike | str | None = None) -> ctypes.CDLL:
+    """Load liborbx.so once; raises OSError if it has not been built."""
+    global _LIB
+    if _LIB is not None and path is None:
+        return _LIB
+    p = Path(path) if path is not None else LIB_PATH
+    if not p.exists():
+        raise OSError(f"{p} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = ctypes.CDLL(str(p))
+    for name, (res, args) in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _LIB = lib
+    return lib
+
+
+def _strerror(code: int) -> str:
+    s = load().orbx_strerror(code)
+    return s.decode() if s else str(code)
+
+
+def check(code: int, what: str) -> int:
+    if code < 0:
+        raise OrbxError(code, what)
+    return code
+
+
+def ptr(a: np.ndarray | None) -> ctypes.c_void_p | None:
+    if a is None:
+        return None
+    return ctypes.c_void_p(a.ctypes.data)

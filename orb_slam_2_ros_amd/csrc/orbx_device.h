@@ -1,0 +1,79 @@
+// orbx_device.h -- device-side buffers and kernel launchers (internal).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "orbx_plan.h"
+#include "../../include/orbx.h"
+
+namespace orbx {
+
+// Plan tables resident in device memory (one copy per extractor plan).
+struct DevPlan {
+    const LevelGeom *lv;
+    const Cell *cells;
+    const ResizeTap *xtaps;
+    const ResizeTap *ytaps;
+    const int4 *blur_tiles;   // (level, x0, y0, 0) per 64x16 output tile
+    int nlevels, ncells, nblur_tiles;
+    int gauss[7];
+    int umax[16];
+    int ini_th, min_th;
+    int64_t pyr_bytes, blur_bytes, cand_cap;
+    int out_cap, max_kps;
+    int node_cap;             // quadtree node capacity (max over levels)
+    int node_lds_bytes;       // dynamic LDS of the quadtree kernel
+};
+
+// Per-batch device buffers.  Frame b of a batch uses the b-th slice of each.
+struct FrameBufs {
+    const uint8_t *img0;      // level 0 = caller's images
+    int64_t img0_stride;      // bytes between frames
+    int img0_pitch;           // bytes between rows
+    uint8_t *pyr;             // levels >= 1, B * pyr_bytes
+    uint8_t *blur;            // blurred levels, B * blur_bytes
+    uint32_t *cand;           // per-cell candidate slots, B * cand_cap
+    int32_t *cell_count;      // B * ncells
+    uint32_t *keys;           // per-level compacted candidates, B * cand_cap
+    uint16_t *key_node;       // quadtree scratch, B * cand_cap
+    uint8_t *key_q;           // quadtree scratch, B * cand_cap
+    uint32_t *sel;            // selected keys per level slot, B * out_cap
+    int32_t *level_count;     // B * kMaxLevels
+    orbx_keypoint *kps;       // B * max_kps
+    uint8_t *desc;            // B * max_kps * 32
+    int32_t *nkps;            // B
+};
+
+// Matcher inputs/outputs for a batch of frame pairs (F1[b] -> F2[b]).
+struct MatchBufs {
+    const orbx_keypoint *k1; const uint8_t *d1; const int32_t *n1; int64_t k1_stride;
+    const orbx_keypoint *k2; const uint8_t *d2; const int32_t *n2; int64_t k2_stride;
+    float *prev_xy;           // B * k1_stride * 2, in/out
+    int32_t *matches12;       // B * k1_stride
+    int32_t *nmatches;        // B
+    uint32_t *scratch;        // B * scratch_stride (candidate lists)
+    int64_t scratch_stride;
+    int img_w, img_h, window;
+    float nnratio;
+    int check_ori;
+    int reset_prev;           // 1: prev_xy := F1 keypoint positions before matching
+};
+
+enum Stage { kStageResize = 0, kStageBlur, kStageFast, kStageQuadtree, kStageDescribe, kStageMatch, kNumStages };
+
+hipError_t launch_resize(const DevPlan &p, const Plan &hp, const FrameBufs &fb, int B, hipStream_t s);
+hipError_t launch_blur(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t s);
+hipError_t launch_fast(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t s);
+hipError_t launch_quadtree(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t s);
+hipError_t launch_describe(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t s);
+hipError_t launch_match(const MatchBufs &mb, int B, int n1cap, int n2cap, int maxq, int maxc, hipStream_t s);
+// sincosf restatement and fastAtan2 evaluated on the device over an array
+// (exhaustive-check hook used by the GPU tests).
+hipError_t launch_trig_check(const float *in, float *s, float *c, float *atan_out,
+                             const float *ay, const float *ax, int n, int m, hipStream_t st);
+int match_lds_bytes(int n1cap, int n2cap);
+int quadtree_lds_bytes(int node_cap);
+
+}  // namespace orbx

@@ -1,0 +1,670 @@
+// orbx_runtime.hip -- extractor object, device buffers, streams and the C ABI
+// declared in include/orbx.h.
+//
+// Memory layout per extractor (HBM, all frames of a batch side by side):
+//   pyramid   B x pyr_bytes    levels 1..7, rows padded to 64 B (level 0 is the
+//                              caller's image, read in place)
+//   blurred   B x blur_bytes   levels 0..7
+//   cand      B x cand_cap     per-cell FAST slots (u32 packed x|y<<12|s<<24)
+//   keys etc. B x cand_cap     quadtree scratch (compacted keys, node ids)
+//   results   2 slots x B x kp_stride x (28 + 32) B  keypoints + descriptors
+// The two result slots ping-pong so a mono step can match the previous frame
+// of every stream against the current one without a copy.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "orbx_device.h"
+
+using namespace orbx;
+
+namespace {
+
+template <typename T>
+hipError_t dalloc(T **p, size_t count) {
+    *p = nullptr;
+    if (count == 0) return hipSuccess;
+    return hipMalloc(reinterpret_cast<void **>(p), sizeof(T) * count);
+}
+
+template <typename T>
+void dfree(T *&p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+}
+
+int popcount32(uint32_t v) {
+    v = v - ((v >> 1) & 0x55555555u);
+    v = (v & 0x33333333u) + ((v >> 2) & 0x33333333u);
+    return (int)((((v + (v >> 4)) & 0xF0F0F0Fu) * 0x1010101u) >> 24);
+}
+
+}  // namespace
+
+struct orbx_extractor {
+    int device = 0;
+    int nfeatures = 0, nlevels = 0, ini_th = 0, min_th = 0;
+    float scale_factor = 1.2f;
+    Plan plan;
+    bool planned = false;
+    int max_batch = 0;
+
+    DevPlan dp{};
+    uint8_t *d_tables = nullptr;
+
+    uint8_t *d_pyr = nullptr, *d_blur = nullptr;
+    uint32_t *d_cand = nullptr, *d_keys = nullptr, *d_sel = nullptr;
+    int32_t *d_cell_count = nullptr, *d_level_count = nullptr;
+    uint16_t *d_key_node = nullptr;
+    uint8_t *d_key_q = nullptr;
+
+    struct Slot {
+        orbx_keypoint *kps = nullptr;
+        uint8_t *desc = nullptr;
+        int32_t *nkps = nullptr;
+        int batch = 0;
+        const uint8_t *img0 = nullptr;
+        int64_t img0_stride = 0;
+        int img0_pitch = 0;
+    } slot[2];
+    int cur = 0;
+    int steps = 0;
+
+    // matcher state (results of the last mono step)
+    float *d_prev = nullptr;
+    int32_t *d_m12 = nullptr, *d_nmatch = nullptr;
+    uint32_t *d_scratch = nullptr;
+    int64_t scratch_stride = 0;
+    int match_batch = 0;
+    int l0cap = 0;
+
+    uint8_t *d_img = nullptr;   // staging for the host API
+    size_t d_img_bytes = 0;
+
+    hipStream_t stream = nullptr;
+    bool profiling = false;
+    hipEvent_t ev[kNumStages + 1] = {};
+    float stage_ms[kNumStages] = {0};
+    bool stage_valid[kNumStages] = {false};
+
+    ~orbx_extractor() { release(); if (stream) (void)hipStreamDestroy(stream); for (auto &e : ev) if (e) (void)hipEventDestroy(e); }
+
+    void release() {
+        dfree(d_tables); dfree(d_pyr); dfree(d_blur); dfree(d_cand); dfree(d_keys); dfree(d_sel);
+        dfree(d_cell_count); dfree(d_level_count); dfree(d_key_node); dfree(d_key_q);
+        for (auto &s : slot) { dfree(s.kps); dfree(s.desc); dfree(s.nkps); s.batch = 0; }
+        dfree(d_prev); dfree(d_m12); dfree(d_nmatch); dfree(d_scratch); dfree(d_img);
+        d_img_bytes = 0;
+        planned = false;
+        max_batch = 0;
+        match_batch = 0;
+    }
+};
+
+namespace {
+
+int check(hipError_t e) { return e == hipSuccess ? ORBX_OK : ORBX_EIO; }
+
+hipStream_t stream_of(orbx_extractor *ex, void *s) {
+    return s ? reinterpret_cast<hipStream_t>(s) : ex->stream;
+}
+
+int upload_plan(orbx_extractor *ex) {
+    Plan &p = ex->plan;
+    // blur tile table
+    std::vector<int4> tiles;
+    for (int l = 0; l < p.nlevels; ++l)
+        for (int y = 0; y < p.lv[l].h; y += 16)
+            for (int x = 0; x < p.lv[l].w; x += 64) tiles.push_back(make_int4(l, x, y, 0));
+    const size_t b_lv = sizeof(LevelGeom) * p.lv.size();
+    const size_t b_cells = sizeof(Cell) * p.cells.size();
+    const size_t b_xt = sizeof(ResizeTap) * p.xtaps.size();
+    const size_t b_yt = sizeof(ResizeTap) * p.ytaps.size();
+    const size_t b_tiles = sizeof(int4) * tiles.size();
+    auto al = [](size_t v) { return (v + 255) & ~size_t(255); };
+    const size_t total = al(b_lv) + al(b_cells) + al(b_xt) + al(b_yt) + al(b_tiles) + 256;
+    std::vector<uint8_t> host(total, 0);
+    size_t o = 0;
+    const size_t o_lv = o; std::memcpy(&host[o], p.lv.data(), b_lv); o += al(b_lv);
+    const size_t o_cells = o; if (b_cells) std::memcpy(&host[o], p.cells.data(), b_cells); o += al(b_cells);
+    const size_t o_xt = o; if (b_xt) std::memcpy(&host[o], p.xtaps.data(), b_xt); o += al(b_xt);
+    const size_t o_yt = o; if (b_yt) std::memcpy(&host[o], p.ytaps.data(), b_yt); o += al(b_yt);
+    const size_t o_tiles = o; if (b_tiles) std::memcpy(&host[o], tiles.data(), b_tiles); o += al(b_tiles);
+    if (dalloc(&ex->d_tables, total) != hipSuccess) return ORBX_ENOMEM;
+    if (hipMemcpy(ex->d_tables, host.data(), total, hipMemcpyHostToDevice) != hipSuccess) return ORBX_EIO;
+    DevPlan &d = ex->dp;
+    d.lv = reinterpret_cast<const LevelGeom *>(ex->d_tables + o_lv);
+    d.cells = reinterpret_cast<const Cell *>(ex->d_tables + o_cells);
+    d.xtaps = reinterpret_cast<const ResizeTap *>(ex->d_tables + o_xt);
+    d.ytaps = reinterpret_cast<const ResizeTap *>(ex->d_tables + o_yt);
+    d.blur_tiles = reinterpret_cast<const int4 *>(ex->d_tables + o_tiles);
+    d.nlevels = p.nlevels;
+    d.ncells = (int)p.cells.size();
+    d.nblur_tiles = (int)tiles.size();
+    for (int i = 0; i < 7; ++i) d.gauss[i] = p.gauss[i];
+    for (int i = 0; i < 16; ++i) d.umax[i] = p.umax[i];
+    d.ini_th = std::min(std::max(p.ini_th, 0), 255);
+    d.min_th = std::min(std::max(p.min_th, 0), 255);
+    d.pyr_bytes = p.pyr_bytes;
+    d.blur_bytes = p.blur_bytes;
+    d.cand_cap = p.cand_cap;
+    d.out_cap = p.out_cap;
+    d.max_kps = p.max_kps;
+    int node_cap = 8;
+    for (const LevelGeom &g : p.lv) node_cap = std::max(node_cap, std::max(g.quota, 4 * g.nini) + 4);
+    d.node_cap = node_cap;
+    d.node_lds_bytes = quadtree_lds_bytes(node_cap);
+    if (d.node_lds_bytes > 160 * 1024) return ORBX_EINVAL;
+    return ORBX_OK;
+}
+
+int reserve(orbx_extractor *ex, int w, int h, int max_batch) {
+    if (w < 2 * kEdge + 8 || h < 2 * kEdge + 8 || w > 4095 || h > 4095 || max_batch <= 0) return ORBX_EINVAL;
+    if (ex->planned && ex->plan.width == w && ex->plan.height == h && ex->max_batch >= max_batch) return ORBX_OK;
+    if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
+    (void)hipStreamSynchronize(ex->stream);
+    ex->release();
+    ex->plan = make_plan(w, h, ex->nfeatures, ex->scale_factor, ex->nlevels, ex->ini_th, ex->min_th);
+    for (const LevelGeom &g : ex->plan.lv)
+        if (g.w < 2 * kEdge + 8 || g.h < 2 * kEdge + 8 || g.wcell >= 60 || g.hcell >= 60) return ORBX_EINVAL;
+    int rc = upload_plan(ex);
+    if (rc) return rc;
+    const Plan &p = ex->plan;
+    const size_t B = (size_t)max_batch;
+    bool ok = true;
+    ok &= dalloc(&ex->d_pyr, B * p.pyr_bytes) == hipSuccess;
+    ok &= dalloc(&ex->d_blur, B * p.blur_bytes) == hipSuccess;
+    ok &= dalloc(&ex->d_cand, B * p.cand_cap) == hipSuccess;
+    ok &= dalloc(&ex->d_keys, B * p.cand_cap) == hipSuccess;
+    ok &= dalloc(&ex->d_key_node, B * p.cand_cap) == hipSuccess;
+    ok &= dalloc(&ex->d_key_q, B * p.cand_cap) == hipSuccess;
+    ok &= dalloc(&ex->d_cell_count, B * p.cells.size()) == hipSuccess;
+    ok &= dalloc(&ex->d_sel, B * p.out_cap) == hipSuccess;
+    ok &= dalloc(&ex->d_level_count, B * kMaxLevels) == hipSuccess;
+    for (auto &s : ex->slot) {
+        ok &= dalloc(&s.kps, B * p.max_kps) == hipSuccess;
+        ok &= dalloc(&s.desc, B * p.max_kps * 32) == hipSuccess;
+        ok &= dalloc(&s.nkps, B) == hipSuccess;
+        s.batch = 0;
+    }
+    ex->l0cap = p.lv[0].out_cap;
+    ex->scratch_stride = (int64_t)ex->l0cap * ex->l0cap;
+    ok &= dalloc(&ex->d_prev, B * p.max_kps * 2) == hipSuccess;
+    ok &= dalloc(&ex->d_m12, B * p.max_kps) == hipSuccess;
+    ok &= dalloc(&ex->d_nmatch, B) == hipSuccess;
+    ok &= dalloc(&ex->d_scratch, B * (size_t)ex->scratch_stride) == hipSuccess;
+    if (!ok) { ex->release(); return ORBX_ENOMEM; }
+    ex->planned = true;
+    ex->max_batch = max_batch;
+    ex->cur = 0;
+    return ORBX_OK;
+}
+
+FrameBufs frame_bufs(orbx_extractor *ex, int slot) {
+    FrameBufs fb;
+    const auto &s = ex->slot[slot];
+    fb.img0 = s.img0;
+    fb.img0_stride = s.img0_stride;
+    fb.img0_pitch = s.img0_pitch;
+    fb.pyr = ex->d_pyr;
+    fb.blur = ex->d_blur;
+    fb.cand = ex->d_cand;
+    fb.cell_count = ex->d_cell_count;
+    fb.keys = ex->d_keys;
+    fb.key_node = ex->d_key_node;
+    fb.key_q = ex->d_key_q;
+    fb.sel = ex->d_sel;
+    fb.level_count = ex->d_level_count;
+    fb.kps = s.kps;
+    fb.desc = s.desc;
+    fb.nkps = s.nkps;
+    return fb;
+}
+
+void mark(orbx_extractor *ex, int i, hipStream_t st) {
+    if (ex->profiling) (void)hipEventRecord(ex->ev[i], st);
+}
+
+// Runs the five extractor stages for `batch` frames into result slot `si`.
+int run_extract(orbx_extractor *ex, int si, const uint8_t *d_images, int64_t stride, int pitch, int batch,
+                hipStream_t st) {
+    auto &s = ex->slot[si];
+    s.img0 = d_images;
+    s.img0_stride = stride;
+    s.img0_pitch = pitch;
+    s.batch = batch;
+    const FrameBufs fb = frame_bufs(ex, si);
+    for (int i = 0; i < kNumStages; ++i) ex->stage_valid[i] = false;
+    mark(ex, 0, st);
+    if (launch_resize(ex->dp, ex->plan, fb, batch, st) != hipSuccess) return ORBX_EIO;
+    mark(ex, 1, st);
+    if (launch_blur(ex->dp, fb, batch, st) != hipSuccess) return ORBX_EIO;
+    mark(ex, 2, st);
+    if (launch_fast(ex->dp, fb, batch, st) != hipSuccess) return ORBX_EIO;
+    mark(ex, 3, st);
+    if (launch_quadtree(ex->dp, fb, batch, st) != hipSuccess) return ORBX_EIO;
+    mark(ex, 4, st);
+    if (launch_describe(ex->dp, fb, batch, st) != hipSuccess) return ORBX_EIO;
+    mark(ex, 5, st);
+    for (int i = 0; i < kStageMatch; ++i) ex->stage_valid[i] = ex->profiling;
+    return ORBX_OK;
+}
+
+int validate_batch(orbx_extractor *ex, const uint8_t *d_images, int pitch, int batch) {
+    if (!ex || !ex->planned || !d_images || batch <= 0 || batch > ex->max_batch) return ORBX_EINVAL;
+    if (pitch < ex->plan.width) return ORBX_EINVAL;
+    return ORBX_OK;
+}
+
+}  // namespace
+
+// =============================================================================
+extern "C" {
+
+const char *orbx_strerror(int code) {
+    switch (code) {
+        case ORBX_OK: return "ok";
+        case ORBX_EIO: return "HIP runtime or kernel failure";
+        case ORBX_ENOMEM: return "allocation failed";
+        case ORBX_EINVAL: return "invalid argument";
+        case ORBX_ERANGE: return "output capacity too small";
+        case ORBX_ENODEV: return "no usable device";
+        default: return "unknown error";
+    }
+}
+
+int orbx_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+orbx_extractor *orbx_extractor_create(int device, int nfeatures, float scaleFactor, int nlevels,
+                                      int iniThFAST, int minThFAST) {
+    if (nfeatures < 0 || nlevels < 1 || nlevels > kMaxLevels || !(scaleFactor > 1.0f)) return nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return nullptr;
+    if (hipSetDevice(device) != hipSuccess) return nullptr;
+    orbx_extractor *ex = new (std::nothrow) orbx_extractor();
+    if (!ex) return nullptr;
+    ex->device = device;
+    ex->nfeatures = nfeatures;
+    ex->nlevels = nlevels;
+    ex->scale_factor = scaleFactor;
+    ex->ini_th = iniThFAST;
+    ex->min_th = minThFAST;
+    if (hipStreamCreateWithFlags(&ex->stream, hipStreamNonBlocking) != hipSuccess) { delete ex; return nullptr; }
+    for (auto &e : ex->ev)
+        if (hipEventCreate(&e) != hipSuccess) { delete ex; return nullptr; }
+    // geometry tables for the getters are size independent; plan a nominal size
+    ex->plan = make_plan(640, 480, nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST);
+    return ex;
+}
+
+void orbx_extractor_destroy(orbx_extractor *ex) {
+    if (!ex) return;
+    (void)hipSetDevice(ex->device);
+    if (ex->stream) (void)hipStreamSynchronize(ex->stream);
+    delete ex;
+}
+
+int orbx_extractor_get_levels(const orbx_extractor *ex) { return ex ? ex->nlevels : ORBX_EINVAL; }
+float orbx_extractor_get_scale_factor(const orbx_extractor *ex) {
+    return ex ? (float)(double)ex->scale_factor : 0.f;
+}
+
+int orbx_extractor_get_scale_table(const orbx_extractor *ex, int which, float *out, int cap) {
+    if (!ex || which < 0 || which > 3 || (cap > 0 && !out)) return ORBX_EINVAL;
+    for (int l = 0; l < ex->nlevels && l < cap; ++l) {
+        const LevelGeom &g = ex->plan.lv[l];
+        out[l] = which == 0 ? g.scale : which == 1 ? g.inv_scale : which == 2 ? g.sigma2 : g.inv_sigma2;
+    }
+    return ex->nlevels;
+}
+
+int orbx_extractor_get_level_quotas(const orbx_extractor *ex, int32_t *out, int cap) {
+    if (!ex || (cap > 0 && !out)) return ORBX_EINVAL;
+    for (int l = 0; l < ex->nlevels && l < cap; ++l) out[l] = ex->plan.lv[l].quota;
+    return ex->nlevels;
+}
+
+int orbx_extractor_reserve(orbx_extractor *ex, int width, int height, int max_batch) {
+    if (!ex) return ORBX_EINVAL;
+    if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
+    return reserve(ex, width, height, max_batch);
+}
+
+int orbx_extractor_kp_stride(const orbx_extractor *ex) {
+    return ex && ex->planned ? ex->plan.max_kps : ORBX_EINVAL;
+}
+
+int orbx_extract_batch_device(orbx_extractor *ex, const uint8_t *d_images, int64_t frame_stride, int pitch,
+                              int batch, void *stream) {
+    int rc = validate_batch(ex, d_images, pitch, batch);
+    if (rc) return rc;
+    if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
+    const int next = ex->cur ^ 1;
+    rc = run_extract(ex, next, d_images, frame_stride, pitch, batch, stream_of(ex, stream));
+    if (rc) return rc;
+    ex->cur = next;
+    ex->match_batch = 0;
+    return ORBX_OK;
+}
+
+int orbx_batch_results_device(orbx_extractor *ex, const orbx_keypoint **d_kps, const uint8_t **d_desc,
+                              const int32_t **d_counts) {
+    if (!ex || !ex->planned) return ORBX_EINVAL;
+    const auto &s = ex->slot[ex->cur];
+    if (d_kps) *d_kps = s.kps;
+    if (d_desc) *d_desc = s.desc;
+    if (d_counts) *d_counts = s.nkps;
+    return ORBX_OK;
+}
+
+int orbx_batch_download(orbx_extractor *ex, int frame, orbx_keypoint *kps, uint8_t *desc, int cap, int *n) {
+    if (!ex || !ex->planned || !n) return ORBX_EINVAL;
+    const auto &s = ex->slot[ex->cur];
+    if (frame < 0 || frame >= s.batch) return ORBX_EINVAL;
+    if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
+    if (hipDeviceSynchronize() != hipSuccess) return ORBX_EIO;
+    int32_t cnt = 0;
+    int32_t lc[kMaxLevels];
+    if (hipMemcpy(&cnt, s.nkps + frame, sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess) return ORBX_EIO;
+    if (hipMemcpy(lc, ex->d_level_count + (size_t)frame * kMaxLevels, sizeof(lc), hipMemcpyDeviceToHost) != hipSuccess)
+        return ORBX_EIO;
+    for (int l = 0; l < ex->nlevels; ++l)
+        if (lc[l] < 0) return ORBX_EIO;   // quadtree capacity guard tripped
+    *n = cnt;
+    if (cnt > cap) return ORBX_ERANGE;
+    const size_t base = (size_t)frame * ex->plan.max_kps;
+    if (cnt > 0 && kps &&
+        hipMemcpy(kps, s.kps + base, sizeof(orbx_keypoint) * cnt, hipMemcpyDeviceToHost) != hipSuccess)
+        return ORBX_EIO;
+    if (cnt > 0 && desc && hipMemcpy(desc, s.desc + base * 32, 32 * (size_t)cnt, hipMemcpyDeviceToHost) != hipSuccess)
+        return ORBX_EIO;
+    return ORBX_OK;
+}
+
+int orbx_extract(orbx_extractor *ex, const uint8_t *image, int width, int height, size_t pitch,
+                 orbx_keypoint *kps, uint8_t *desc, int cap, int *n) {
+    if (!ex || !n) return ORBX_EINVAL;
+    if (!image || width <= 0 || height <= 0) { *n = -1; return ORBX_OK; }  // ORBextractor.cc:1086-1087
+    if (pitch < (size_t)width) return ORBX_EINVAL;
+    if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
+    int rc = reserve(ex, width, height, std::max(1, ex->max_batch));
+    if (rc) return rc;
+    const size_t dp = (size_t)pitch_of(width);
+    const size_t need = dp * height;
+    if (ex->d_img_bytes < need) {
+        dfree(ex->d_img);
+        if (dalloc(&ex->d_img, need) != hipSuccess) return ORBX_ENOMEM;
+        ex->d_img_bytes = need;
+    }
+    if (hipMemcpy2DAsync(ex->d_img, dp, image, pitch, width, height, hipMemcpyHostToDevice, ex->stream) != hipSuccess)
+        return ORBX_EIO;
+    rc = orbx_extract_batch_device(ex, ex->d_img, (int64_t)need, (int)dp, 1, nullptr);
+    if (rc) return rc;
+    return orbx_batch_download(ex, 0, kps, desc, cap, n);
+}
+
+int orbx_extractor_pyramid_level(orbx_extractor *ex, int level, uint8_t *out, size_t out_pitch, int *w, int *h) {
+    if (!ex || !ex->planned || level < 0 || level >= ex->nlevels) return ORBX_EINVAL;
+    const LevelGeom &g = ex->plan.lv[level];
+    if (w) *w = g.w;
+    if (h) *h = g.h;
+    if (!out) return ORBX_OK;
+    if (out_pitch < (size_t)g.w) return ORBX_EINVAL;
+    const auto &s = ex->slot[ex->cur];
+    if (s.batch <= 0) return ORBX_EINVAL;
+    if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
+    if (hipDeviceSynchronize() != hipSuccess) return ORBX_EIO;
+    const uint8_t *src = level == 0 ? s.img0 : ex->d_pyr + g.pyr_off;
+    const size_t sp = level == 0 ? (size_t)s.img0_pitch : (size_t)g.pitch;
+    return check(hipMemcpy2D(out, out_pitch, src, sp, g.w, g.h, hipMemcpyDeviceToHost));
+}
+
+int orbx_extractor_debug_fetch(orbx_extractor *ex, int frame, int level, int what, void *out, int64_t cap) {
+    if (!ex || !ex->planned || level < 0 || level >= ex->nlevels || !out) return ORBX_EINVAL;
+    const auto &s = ex->slot[ex->cur];
+    if (frame < 0 || frame >= s.batch) return ORBX_EINVAL;
+    if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
+    if (hipDeviceSynchronize() != hipSuccess) return ORBX_EIO;
+    const Plan &p = ex->plan;
+    const LevelGeom &g = p.lv[level];
+    if (what == 0 || what == 1) {
+        if (cap < (int64_t)g.w * g.h) return ORBX_ERANGE;
+        const uint8_t *src;
+        size_t sp;
+        if (what == 0) {
+            src = level == 0 ? s.img0 + (int64_t)frame * s.img0_stride
+                             : ex->d_pyr + (int64_t)frame * p.pyr_bytes + g.pyr_off;
+            sp = level == 0 ? (size_t)s.img0_pitch : (size_t)g.pitch;
+        } else {
+            src = ex->d_blur + (int64_t)frame * p.blur_bytes + g.blur_off;
+            sp = (size_t)g.pitch;
+        }
+        if (hipMemcpy2D(out, g.w, src, sp, g.w, g.h, hipMemcpyDeviceToHost) != hipSuccess) return ORBX_EIO;
+        return g.w * g.h;
+    }
+    int32_t *o = static_cast<int32_t *>(out);
+    if (what == 2) {
+        const int nc = g.cell_end - g.cell_begin;
+        std::vector<int32_t> counts(nc);
+        if (nc && hipMemcpy(counts.data(), ex->d_cell_count + (size_t)frame * p.cells.size() + g.cell_begin,
+                            sizeof(int32_t) * nc, hipMemcpyDeviceToHost) != hipSuccess)
+            return ORBX_EIO;
+        std::vector<uint32_t> cand(g.cand_cap);
+        if (g.cand_cap && hipMemcpy(cand.data(), ex->d_cand + (size_t)frame * p.cand_cap + g.cand_off,
+                                    sizeof(uint32_t) * g.cand_cap, hipMemcpyDeviceToHost) != hipSuccess)
+            return ORBX_EIO;
+        int64_t k = 0;
+        for (int c = 0; c < nc; ++c) {
+            const Cell &cell = p.cells[g.cell_begin + c];
+            for (int i = 0; i < counts[c]; ++i, ++k) {
+                if (3 * (k + 1) > cap) return ORBX_ERANGE;
+                const uint32_t v = cand[cell.slot - g.cand_off + i];
+                o[3 * k] = (int32_t)(v & 0xFFF);
+                o[3 * k + 1] = (int32_t)((v >> 12) & 0xFFF);
+                o[3 * k + 2] = (int32_t)(v >> 24);
+            }
+        }
+        return (int)k;
+    }
+    if (what == 3) {
+        int32_t cnt = 0;
+        if (hipMemcpy(&cnt, ex->d_level_count + (size_t)frame * kMaxLevels + level, sizeof(int32_t),
+                      hipMemcpyDeviceToHost) != hipSuccess)
+            return ORBX_EIO;
+        if (cnt < 0) return ORBX_EIO;
+        if (3 * (int64_t)cnt > cap) return ORBX_ERANGE;
+        std::vector<uint32_t> sel(cnt);
+        if (cnt && hipMemcpy(sel.data(), ex->d_sel + (size_t)frame * p.out_cap + g.out_off, sizeof(uint32_t) * cnt,
+                             hipMemcpyDeviceToHost) != hipSuccess)
+            return ORBX_EIO;
+        for (int i = 0; i < cnt; ++i) {
+            o[3 * i] = (int32_t)(sel[i] & 0xFFF);
+            o[3 * i + 1] = (int32_t)((sel[i] >> 12) & 0xFFF);
+            o[3 * i + 2] = (int32_t)(sel[i] >> 24);
+        }
+        return cnt;
+    }
+    return ORBX_EINVAL;
+}
+
+int orbx_mono_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t frame_stride, int pitch, int batch,
+                          int window, float nnratio, int check_ori, void *stream) {
+    int rc = validate_batch(ex, d_images, pitch, batch);
+    if (rc) return rc;
+    if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
+    hipStream_t st = stream_of(ex, stream);
+    const int prev = ex->cur, next = ex->cur ^ 1;
+    const bool have_prev = ex->slot[prev].batch == batch && ex->steps > 0;
+    rc = run_extract(ex, next, d_images, frame_stride, pitch, batch, st);
+    if (rc) return rc;
+    ex->cur = next;
+    ++ex->steps;
+    ex->match_batch = 0;
+    if (!have_prev) return ORBX_OK;
+    MatchBufs mb;
+    const auto &s1 = ex->slot[prev];
+    const auto &s2 = ex->slot[next];
+    mb.k1 = s1.kps; mb.d1 = s1.desc; mb.n1 = s1.nkps; mb.k1_stride = ex->plan.max_kps;
+    mb.k2 = s2.kps; mb.d2 = s2.desc; mb.n2 = s2.nkps; mb.k2_stride = ex->plan.max_kps;
+    mb.prev_xy = ex->d_prev;
+    mb.matches12 = ex->d_m12;
+    mb.nmatches = ex->d_nmatch;
+    mb.scratch = ex->d_scratch;
+    mb.scratch_stride = ex->scratch_stride;
+    mb.img_w = ex->plan.width;
+    mb.img_h = ex->plan.height;
+    mb.window = window;
+    mb.nnratio = nnratio;
+    mb.check_ori = check_ori;
+    mb.reset_prev = 1;
+    if (launch_match(mb, batch, ex->plan.max_kps, ex->plan.max_kps, ex->l0cap, ex->l0cap, st) != hipSuccess)
+        return ORBX_EIO;
+    mark(ex, 6, st);
+    ex->stage_valid[kStageMatch] = ex->profiling;
+    ex->match_batch = batch;
+    return ORBX_OK;
+}
+
+int orbx_mono_matches_download(orbx_extractor *ex, int frame, int32_t *matches12, int cap, int *n1, int *nmatches) {
+    if (!ex || !ex->planned || frame < 0 || frame >= ex->match_batch) return ORBX_EINVAL;
+    if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
+    if (hipDeviceSynchronize() != hipSuccess) return ORBX_EIO;
+    const int prev = ex->cur ^ 1;
+    int32_t cnt = 0, nm = 0;
+    if (hipMemcpy(&cnt, ex->slot[prev].nkps + frame, sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess) return ORBX_EIO;
+    if (hipMemcpy(&nm, ex->d_nmatch + frame, sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess) return ORBX_EIO;
+    if (nm < 0) return ORBX_EIO;
+    if (n1) *n1 = cnt;
+    if (nmatches) *nmatches = nm;
+    if (cnt > cap) return ORBX_ERANGE;
+    if (cnt > 0 && matches12 &&
+        hipMemcpy(matches12, ex->d_m12 + (size_t)frame * ex->plan.max_kps, sizeof(int32_t) * cnt,
+                  hipMemcpyDeviceToHost) != hipSuccess)
+        return ORBX_EIO;
+    return ORBX_OK;
+}
+
+int orbx_extractor_set_profiling(orbx_extractor *ex, int on) {
+    if (!ex) return ORBX_EINVAL;
+    ex->profiling = on != 0;
+    return ORBX_OK;
+}
+
+int orbx_extractor_stage_times(orbx_extractor *ex, float *ms, int cap) {
+    if (!ex || (cap > 0 && !ms)) return ORBX_EINVAL;
+    if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
+    int nw = 0;
+    for (int i = 0; i < kNumStages && i < cap; ++i) {
+        float t = -1.f;
+        if (ex->stage_valid[i]) {
+            if (hipEventSynchronize(ex->ev[i + 1]) != hipSuccess) return ORBX_EIO;
+            if (hipEventElapsedTime(&t, ex->ev[i], ex->ev[i + 1]) != hipSuccess) t = -1.f;
+        }
+        ms[i] = t;
+        ++nw;
+    }
+    return nw;
+}
+
+int orbx_descriptor_distance(const uint8_t *a, const uint8_t *b) {
+    if (!a || !b) return ORBX_EINVAL;
+    int dist = 0;
+    for (int i = 0; i < 8; ++i) {
+        uint32_t pa, pb;
+        std::memcpy(&pa, a + 4 * i, 4);
+        std::memcpy(&pb, b + 4 * i, 4);
+        dist += popcount32(pa ^ pb);
+    }
+    return dist;
+}
+
+int orbx_search_for_initialization(int device, const orbx_keypoint *k1, const uint8_t *d1, int n1,
+                                   const orbx_keypoint *k2, const uint8_t *d2, int n2, int img_w, int img_h,
+                                   float *prev_xy, int32_t *matches12, int window, float nnratio, int check_ori,
+                                   int *nmatches) {
+    if (n1 < 0 || n2 < 0 || n1 > 32767 || n2 > 32767 || img_w <= 0 || img_h <= 0 || !nmatches) return ORBX_EINVAL;
+    if ((n1 && (!k1 || !d1 || !prev_xy || !matches12)) || (n2 && (!k2 || !d2))) return ORBX_EINVAL;
+    if (hipSetDevice(device) != hipSuccess) return ORBX_ENODEV;
+    if (match_lds_bytes(std::max(n1, 1), std::max(n2, 1)) > 160 * 1024) return ORBX_EINVAL;
+    int q = 0, c = 0;
+    for (int i = 0; i < n1; ++i) q += k1[i].octave == 0;
+    for (int i = 0; i < n2; ++i) c += k2[i].octave == 0;
+    q = std::max(q, 1);
+    c = std::max(c, 1);
+    const int n1c = std::max(n1, 1), n2c = std::max(n2, 1);
+    orbx_keypoint *dk1 = nullptr, *dk2 = nullptr;
+    uint8_t *dd1 = nullptr, *dd2 = nullptr;
+    int32_t *dn = nullptr, *dm = nullptr, *dnm = nullptr;
+    float *dprev = nullptr;
+    uint32_t *dscr = nullptr;
+    int rc = ORBX_OK;
+    bool ok = dalloc(&dk1, n1c) == hipSuccess && dalloc(&dk2, n2c) == hipSuccess &&
+              dalloc(&dd1, 32 * (size_t)n1c) == hipSuccess && dalloc(&dd2, 32 * (size_t)n2c) == hipSuccess &&
+              dalloc(&dn, 2) == hipSuccess && dalloc(&dm, n1c) == hipSuccess && dalloc(&dnm, 1) == hipSuccess &&
+              dalloc(&dprev, 2 * (size_t)n1c) == hipSuccess && dalloc(&dscr, (size_t)q * c) == hipSuccess;
+    if (!ok) rc = ORBX_ENOMEM;
+    int32_t ns[2] = {n1, n2};
+    if (!rc && n1) ok = hipMemcpy(dk1, k1, sizeof(orbx_keypoint) * n1, hipMemcpyHostToDevice) == hipSuccess &&
+                        hipMemcpy(dd1, d1, 32 * (size_t)n1, hipMemcpyHostToDevice) == hipSuccess &&
+                        hipMemcpy(dprev, prev_xy, 8 * (size_t)n1, hipMemcpyHostToDevice) == hipSuccess;
+    if (!rc && n2) ok = ok && hipMemcpy(dk2, k2, sizeof(orbx_keypoint) * n2, hipMemcpyHostToDevice) == hipSuccess &&
+                        hipMemcpy(dd2, d2, 32 * (size_t)n2, hipMemcpyHostToDevice) == hipSuccess;
+    if (!rc) ok = ok && hipMemcpy(dn, ns, sizeof(ns), hipMemcpyHostToDevice) == hipSuccess;
+    if (!rc && !ok) rc = ORBX_EIO;
+    if (!rc) {
+        MatchBufs mb;
+        mb.k1 = dk1; mb.d1 = dd1; mb.n1 = dn; mb.k1_stride = n1c;
+        mb.k2 = dk2; mb.d2 = dd2; mb.n2 = dn + 1; mb.k2_stride = n2c;
+        mb.prev_xy = dprev; mb.matches12 = dm; mb.nmatches = dnm;
+        mb.scratch = dscr; mb.scratch_stride = (int64_t)q * c;
+        mb.img_w = img_w; mb.img_h = img_h; mb.window = window; mb.nnratio = nnratio;
+        mb.check_ori = check_ori; mb.reset_prev = 0;
+        if (launch_match(mb, 1, n1c, n2c, q, c, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+            rc = ORBX_EIO;
+    }
+    int32_t nm = 0;
+    if (!rc) {
+        ok = hipMemcpy(&nm, dnm, sizeof(int32_t), hipMemcpyDeviceToHost) == hipSuccess;
+        if (ok && n1) ok = hipMemcpy(matches12, dm, sizeof(int32_t) * n1, hipMemcpyDeviceToHost) == hipSuccess &&
+                           hipMemcpy(prev_xy, dprev, 8 * (size_t)n1, hipMemcpyDeviceToHost) == hipSuccess;
+        if (!ok) rc = ORBX_EIO;
+        else if (nm < 0) rc = ORBX_EIO;
+        else *nmatches = nm;
+    }
+    dfree(dk1); dfree(dk2); dfree(dd1); dfree(dd2); dfree(dn); dfree(dm); dfree(dnm); dfree(dprev); dfree(dscr);
+    return rc;
+}
+
+int orbx_debug_trig(int device, const float *angles, float *s, float *c, int n, const float *ys, const float *xs,
+                    float *atan_deg, int m) {
+    if (n < 0 || m < 0) return ORBX_EINVAL;
+    if (hipSetDevice(device) != hipSuccess) return ORBX_ENODEV;
+    float *da = nullptr, *ds = nullptr, *dc = nullptr, *dy = nullptr, *dx = nullptr, *dt = nullptr;
+    const size_t nn = std::max(n, 1), mm = std::max(m, 1);
+    int rc = ORBX_OK;
+    if (dalloc(&da, nn) || dalloc(&ds, nn) || dalloc(&dc, nn) || dalloc(&dy, mm) || dalloc(&dx, mm) || dalloc(&dt, mm))
+        rc = ORBX_ENOMEM;
+    if (!rc && n && hipMemcpy(da, angles, 4 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess) rc = ORBX_EIO;
+    if (!rc && m && (hipMemcpy(dy, ys, 4 * (size_t)m, hipMemcpyHostToDevice) != hipSuccess ||
+                     hipMemcpy(dx, xs, 4 * (size_t)m, hipMemcpyHostToDevice) != hipSuccess))
+        rc = ORBX_EIO;
+    if (!rc && (launch_trig_check(da, ds, dc, dt, dy, dx, n, m, nullptr) != hipSuccess ||
+                hipDeviceSynchronize() != hipSuccess))
+        rc = ORBX_EIO;
+    if (!rc && n && (hipMemcpy(s, ds, 4 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess ||
+                     hipMemcpy(c, dc, 4 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess))
+        rc = ORBX_EIO;
+    if (!rc && m && hipMemcpy(atan_deg, dt, 4 * (size_t)m, hipMemcpyDeviceToHost) != hipSuccess) rc = ORBX_EIO;
+    dfree(da); dfree(ds); dfree(dc); dfree(dy); dfree(dx); dfree(dt);
+    return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,65 @@
+"""Host mirror of ``ORB_SLAM2::ORBmatcher`` (and the Frame data it reads).
+
+Reference interface: orb_slam2/include/ORBmatcher.h:36-106,
+orb_slam2/src/ORBmatcher.cc:37-43 (constants, constructor), :406-521
+(SearchForInitialization), :1649-1665 (DescriptorDistance).
+
+``Frame`` carries what the matcher reads from ORB_SLAM2::Frame: the undistorted
+keypoints (mvKeysUn; distortion-free cameras, so equal to mvKeys), the
+descriptors (mDescriptors) and the image bounds that size the 64x48 grid
+(Frame.cc:218-220).  SearchForInitialization runs on the GPU through
+liborbx.so; DescriptorDistance is a host popcount (no device round trip).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import KEYPOINT_DTYPE, check, ptr
+
+
+class Frame:
+    def __init__(self, keypoints: np.ndarray, descriptors: np.ndarray, width: int, height: int):
+        self.mvKeysUn = np.ascontiguousarray(keypoints, dtype=KEYPOINT_DTYPE)
+        self.mvKeys = self.mvKeysUn
+        self.mDescriptors = np.ascontiguousarray(descriptors, dtype=np.uint8).reshape(-1, 32)
+        if len(self.mvKeysUn) != len(self.mDescriptors):
+            raise ValueError("keypoints and descriptors differ in length")
+        self.N = len(self.mvKeysUn)
+        self.width, self.height = int(width), int(height)
+
+
+class ORBmatcher:
+    TH_HIGH = 100
+    TH_LOW = 50
+    HISTO_LENGTH = 30
+
+    def __init__(self, nnratio: float = 0.6, checkOri: bool = True, device: int = 0):
+        self._lib = _lib.load()
+        self.mfNNratio = float(nnratio)
+        self.mbCheckOrientation = bool(checkOri)
+        self.device = device
+
+    @staticmethod
+    def DescriptorDistance(a: np.ndarray, b: np.ndarray) -> int:
+        a = np.ascontiguousarray(a, dtype=np.uint8).reshape(32)
+        b = np.ascontiguousarray(b, dtype=np.uint8).reshape(32)
+        return int(_lib.load().orbx_descriptor_distance(ptr(a), ptr(b)))
+
+    def SearchForInitialization(self, F1: Frame, F2: Frame, vbPrevMatched: np.ndarray,
+                                windowSize: int = 10):
+        """Returns (nmatches, vnMatches12); vbPrevMatched (N1 x 2 float32) is
+        updated in place like the reference's vector<cv::Point2f>&."""
+        if vbPrevMatched.dtype != np.float32 or vbPrevMatched.shape != (F1.N, 2) or \
+                not vbPrevMatched.flags.c_contiguous:
+            raise ValueError("vbPrevMatched must be a C-contiguous (N1, 2) float32 array")
+        m12 = np.full(max(F1.N, 1), -1, dtype=np.int32)
+        nm = ctypes.c_int(0)
+        check(self._lib.orbx_search_for_initialization(
+            self.device, ptr(F1.mvKeysUn), ptr(F1.mDescriptors), F1.N,
+            ptr(F2.mvKeysUn), ptr(F2.mDescriptors), F2.N, F2.width, F2.height,
+            ptr(vbPrevMatched), ptr(m12), int(windowSize), ctypes.c_float(self.mfNNratio),
+            int(self.mbCheckOrientation), ctypes.byref(nm)), "SearchForInitialization")
+        return nm.value, m12[:F1.N].copy()
