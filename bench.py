@@ -1,0 +1,229 @@
+#!/usr/bin/env python3
+"""Benchmark: frames/s of the ORB front end (extract + SearchForInitialization
+against the previous frame of the same stream), 1000 kp, 8 levels, VGA mono
+(BASELINE.json configs[1]) on N MI355X GPUs, one process per GPU.
+
+Unit of work: one frame = ORBextractor::operator() on a
+640x480 u8 image + ORBmatcher::SearchForInitialization(F1 = that stream's
+previous frame, F2 = this frame, vbPrevMatched = F1 keypoints, window 100,
+nnratio 0.9, checkOri).  A step processes one new frame for each of the B
+streams a GPU owns (streams are independent: weak scaling, no collective on
+the data path; RCCL is used only for the barrier / max-time reduction).
+
+Inputs are synthetic (orb_slam_2_ros_amd.synth) and resident in HBM before
+the timed region.  Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "frames/sec ORB extract+match (1000 kp, 8 lvl) @640x480 & 1920x1080, 1-GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+FRAMES_PER_STREAM = 4  # resident frames per stream, stepped cyclically
+UNIQUE_SCENES = 32
+
+
+def level_geometry(w: int, h: int, nfeatures: int):
+    """Level sizes / quotas exactly as the extractor computes them (host copy of
+    ORBextractor.cc:416-455,1157-1159 semantics via the library's getters)."""
+    from orb_slam_2_ros_amd import ORBextractor
+    ex = ORBextractor(nfeatures, 1.2, 8, 20, 7)
+    inv = ex.GetInverseScaleFactors()
+    sizes = [(int(np.rint(np.float32(w) * np.float32(s))), int(np.rint(np.float32(h) * np.float32(s)))) for s in inv]
+    ex.close()
+    return sizes
+
+
+def algorithmic_bytes(sizes, nkp: float, stage: str) -> float:
+    """Compulsory HBM bytes per frame of one stage."""
+    p0 = sizes[0][0] * sizes[0][1]
+    p = sum(a * b for a, b in sizes)
+    if stage == "resize":      # read levels 0..6, write levels 1..7
+        return float(p - sizes[-1][0] * sizes[-1][1]) + float(p - p0)
+    if stage == "blur":        # read every level, write its blurred copy
+        return 2.0 * p
+    if stage == "fast":        # read every level once
+        return float(p)
+    if stage == "describe":    # 31x31 disc + 37x37 blurred patch reads, 60 B written per kp
+        return nkp * (961 + 1369 + 60)
+    if stage == "match":       # both frames' descriptors + keypoints read, matches written
+        return nkp * (2 * 32 + 2 * 28 + 4)
+    if stage == "quadtree":    # candidates in, selection out (counted in the kernel)
+        return 0.0
+    if stage == "frame":       # SURVEY.md §8(d) compulsory figure
+        return float(p0 + 2 * (p - p0)) + nkp * 60 + nkp * (2 * 32 + 4)
+    raise ValueError(stage)
+
+
+def cpu_baseline(w: int, h: int, nfeatures: int, budget_s: float):
+    """The oracle (C++ restatement of the reference, 1 thread) on the same
+    workload: extract + SearchForInitialization vs the previous frame."""
+    from oracle import oracle
+    from orb_slam_2_ros_amd import synth
+    frames = synth.frames(w, h, 4242, 8)
+    prev = oracle.extract(frames[0], nfeatures)
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        img = frames[(n + 1) % len(frames)]
+        k2, d2 = oracle.extract(img, nfeatures)
+        k1, d1 = prev
+        pxy = np.ascontiguousarray(np.stack([k1["x"], k1["y"]], 1).astype(np.float32))
+        oracle.search_for_initialization(k1, d1, k2, d2, w, h, pxy, 100, 0.9, True)
+        prev = (k2, d2)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": n / el, "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{n} consecutive {w}x{h} synthetic frames ({el:.1f} s), oracle/liborbx_oracle.so, 1 thread"}
+
+
+def run_config(torch, dist, rank, world, dev, w, h, nfeatures, batch, steps, warmup, profile):
+    from orb_slam_2_ros_amd import ORBextractor, synth
+    ex = ORBextractor(nfeatures, 1.2, 8, 20, 7, device=dev.index)
+    ex.reserve(w, h, batch)
+    # resident input: [FRAMES_PER_STREAM, batch, h, w]
+    nsc = min(UNIQUE_SCENES, batch)
+    scenes = [synth.frames(w, h, 7000 + 97 * rank + s, FRAMES_PER_STREAM) for s in range(nsc)]
+    host = np.empty((FRAMES_PER_STREAM, batch, h, w), np.uint8)
+    for b in range(batch):
+        host[:, b] = scenes[b % nsc]
+    frames = torch.from_numpy(host).to(dev)
+    del host
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+    fstride = h * w
+
+    def step(k):
+        t = k % FRAMES_PER_STREAM
+        ex.mono_step_device(frames[t].data_ptr(), fstride, w, batch, 100, 0.9, True, sp)
+
+    k = 0
+    for _ in range(max(warmup, 2)):
+        step(k); k += 1
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    ex.set_profiling(profile)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(k); k += 1
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    stages = ex.stage_times() if profile else None
+    ex.set_profiling(False)
+    # sanity: last step produced keypoints and matches on every stream
+    kp, _ = ex.batch_download(0)
+    m12, nm = ex.mono_matches_download(0)
+    t_el = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t_el, op=dist.ReduceOp.MAX)
+    ex.close()
+    return float(t_el.item()), stages, len(kp), nm
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256, help="streams (frames per step) per GPU")
+    ap.add_argument("--width", type=int, default=640)
+    ap.add_argument("--height", type=int, default=480)
+    ap.add_argument("--nfeatures", type=int, default=1000)
+    ap.add_argument("--fhd-batch", type=int, default=64, help="also measure 1920x1080 (0 = skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-profile", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    profile = not args.no_profile
+
+    w, h, nf, B = args.width, args.height, args.nfeatures, args.batch
+    el, stages, nkp_last, nm_last = run_config(torch, dist, rank, world, dev, w, h, nf, B, args.steps,
+                                               args.warmup, profile)
+    frames_total = world * B * args.steps
+    value = frames_total / el
+    ms_per_step = 1000.0 * el / args.steps
+
+    fhd = None
+    if args.fhd_batch > 0:
+        el2, st2, _, _ = run_config(torch, dist, rank, world, dev, 1920, 1080, nf, args.fhd_batch,
+                                    max(5, args.steps // 4), 2, profile)
+        fhd = {"value": world * args.fhd_batch * max(5, args.steps // 4) / el2, "unit": "frames/s",
+               "batch_per_gpu": args.fhd_batch, "stage_ms": st2}
+
+    if rank == 0:
+        sizes = level_geometry(w, h, nf)
+        names = ["resize", "blur", "fast", "quadtree", "describe", "match"]
+        roof = None
+        stage_ms = None
+        if stages:
+            stage_ms = dict(zip(names, [round(s, 4) for s in stages]))
+            # dominant HBM-streaming kernel by time among the stages with an algorithmic byte count
+            cand = {n: s for n, s in stage_ms.items() if s and s > 0 and algorithmic_bytes(sizes, nkp_last, n) > 0}
+            dom = max(cand, key=cand.get)
+            bytes_launch = algorithmic_bytes(sizes, nkp_last, dom) * B
+            achieved = bytes_launch / (cand[dom] * 1e-3) / 1e9
+            roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                    "bytes_per_launch": bytes_launch}
+            frame_bytes = algorithmic_bytes(sizes, nkp_last, "frame")
+            roof["pipeline_GBs"] = round(frame_bytes * value / world / 1e9, 2)
+            roof["pipeline_frac"] = round(frame_bytes * value / world / 1e9 / HBM_PEAK_GBS, 5)
+        cpu = cpu_baseline(w, h, nf, args.cpu_seconds) if (world == 1 and args.cpu_seconds > 0) else None
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (orb_slam_2_ros_amd.synth: value-noise + shapes, 4 resident frames per stream)",
+            "config": {"workload": f"mono {w}x{h}, {nf} kp, 8 lvl, scale 1.2, FAST 20/7: ORBextractor + "
+                                   "SearchForInitialization(prev frame, window 100, nnratio 0.9, checkOri)",
+                       "streams_per_gpu": B, "global_batch": B * world, "parallelism": f"replicas x{world}",
+                       "kps_last_frame": nkp_last, "matches_last_frame": nm_last},
+            "roofline": roof,
+            "stage_ms_per_step": stage_ms,
+            "cpu_baseline": cpu,
+            "fhd_1920x1080": fhd,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

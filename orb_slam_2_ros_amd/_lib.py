@@ -81,6 +81,14 @@ def load(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     p = Path(path) if path is not None else LIB_PATH
     if not p.exists():
         raise OSError(f"{p} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    # torch-ROCm bundles its own libamdhip64.so.7 (same SONAME as /opt/rocm's).
+    # Loading torch first makes liborbx bind to that one copy, so a process that
+    # uses both has a single HIP runtime (the other order leaves torch without
+    # devices).  Without torch, liborbx uses /opt/rocm's runtime via its RUNPATH.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(str(p))
     for name, (res, args) in _SIGNATURES.items():
         fn = getattr(lib, name)

@@ -196,8 +196,8 @@ inline Plan make_plan(int width, int height, int nfeatures, float scale_factor_f
         // FAST cell grid (ORBextractor.cc:796-817); interiors tile [19, dim-19).
         const int maxbx = g.w - kEdge + 3, maxby = g.h - kEdge + 3;
         const float width_f = (float)(maxbx - kBorder), height_f = (float)(maxby - kBorder);
-        g.ncols = (int)(width_f / kFastCell);
-        g.nrows = (int)(height_f / kFastCell);
+        g.ncols = std::max(0, (int)(width_f / kFastCell));
+        g.nrows = std::max(0, (int)(height_f / kFastCell));
         g.wcell = g.ncols > 0 ? (int)std::ceil(width_f / g.ncols) : 0;
         g.hcell = g.nrows > 0 ? (int)std::ceil(height_f / g.nrows) : 0;
         g.cell_begin = (int)p.cells.size();

@@ -86,12 +86,27 @@ struct orbx_extractor {
     size_t d_img_bytes = 0;
 
     hipStream_t stream = nullptr;
-    bool profiling = false;
-    hipEvent_t ev[kNumStages + 1] = {};
-    float stage_ms[kNumStages] = {0};
-    bool stage_valid[kNumStages] = {false};
 
-    ~orbx_extractor() { release(); if (stream) (void)hipStreamDestroy(stream); for (auto &e : ev) if (e) (void)hipEventDestroy(e); }
+    // Stage profiling: a ring of event sets, one set per step, folded into
+    // per-stage sums lazily so the timed loop never waits on the host.
+    static constexpr int kRing = 64;
+    bool profiling = false;
+    hipEvent_t ev[kRing][kNumStages + 1] = {};
+    bool pending[kRing] = {false};
+    bool valid[kRing][kNumStages] = {};
+    int ring_pos = 0;
+    double stage_sum[kNumStages] = {0};
+    long stage_cnt[kNumStages] = {0};
+    hipEvent_t *cur_ev = nullptr;
+    bool *cur_valid = nullptr;
+
+    ~orbx_extractor() {
+        release();
+        if (stream) (void)hipStreamDestroy(stream);
+        for (auto &set : ev)
+            for (auto &e : set)
+                if (e) (void)hipEventDestroy(e);
+    }
 
     void release() {
         dfree(d_tables); dfree(d_pyr); dfree(d_blur); dfree(d_cand); dfree(d_keys); dfree(d_sel);
@@ -163,14 +178,20 @@ int upload_plan(orbx_extractor *ex) {
 }
 
 int reserve(orbx_extractor *ex, int w, int h, int max_batch) {
-    if (w < 2 * kEdge + 8 || h < 2 * kEdge + 8 || w > 4095 || h > 4095 || max_batch <= 0) return ORBX_EINVAL;
+    if (w < 8 || h < 8 || w > 4095 || h > 4095 || max_batch <= 0) return ORBX_EINVAL;
     if (ex->planned && ex->plan.width == w && ex->plan.height == h && ex->max_batch >= max_batch) return ORBX_OK;
     if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
     (void)hipStreamSynchronize(ex->stream);
     ex->release();
     ex->plan = make_plan(w, h, ex->nfeatures, ex->scale_factor, ex->nlevels, ex->ini_th, ex->min_th);
-    for (const LevelGeom &g : ex->plan.lv)
-        if (g.w < 2 * kEdge + 8 || g.h < 2 * kEdge + 8 || g.wcell >= 60 || g.hcell >= 60) return ORBX_EINVAL;
+    // Levels too small for a FAST cell grid yield no keypoints, as in the reference
+    // (nCols or nRows == 0 skips its cell loop).  Rejected: levels under 4 px (the
+    // blur's reflect-101 halo needs them) and a quadtree with cells but nIni == 0
+    // (w/h < 0.5: the reference divides by zero at ORBextractor.cc:568).
+    for (const LevelGeom &g : ex->plan.lv) {
+        if (g.w < 4 || g.h < 4 || g.wcell >= 60 || g.hcell >= 60) return ORBX_EINVAL;
+        if (g.ncols > 0 && g.nrows > 0 && g.nini <= 0) return ORBX_EINVAL;
+    }
     int rc = upload_plan(ex);
     if (rc) return rc;
     const Plan &p = ex->plan;
@@ -225,8 +246,43 @@ FrameBufs frame_bufs(orbx_extractor *ex, int slot) {
     return fb;
 }
 
+void fold(orbx_extractor *ex, int set) {
+    if (!ex->pending[set]) return;
+    (void)hipEventSynchronize(ex->ev[set][kNumStages]);
+    for (int i = 0; i < kNumStages; ++i) {
+        if (!ex->valid[set][i]) continue;
+        float t = 0.f;
+        if (hipEventElapsedTime(&t, ex->ev[set][i], ex->ev[set][i + 1]) == hipSuccess) {
+            ex->stage_sum[i] += t;
+            ex->stage_cnt[i] += 1;
+        }
+    }
+    ex->pending[set] = false;
+}
+
+// Starts a profiled step: picks the next event set (folding it first if it
+// still holds an unread step).
+void prof_begin(orbx_extractor *ex) {
+    ex->cur_ev = nullptr;
+    ex->cur_valid = nullptr;
+    if (!ex->profiling) return;
+    const int set = ex->ring_pos;
+    ex->ring_pos = (ex->ring_pos + 1) % orbx_extractor::kRing;
+    fold(ex, set);
+    for (auto &e : ex->ev[set])
+        if (!e && hipEventCreate(&e) != hipSuccess) return;
+    for (int i = 0; i < kNumStages; ++i) ex->valid[set][i] = false;
+    ex->cur_ev = ex->ev[set];
+    ex->cur_valid = ex->valid[set];
+    ex->pending[set] = true;
+}
+
 void mark(orbx_extractor *ex, int i, hipStream_t st) {
-    if (ex->profiling) (void)hipEventRecord(ex->ev[i], st);
+    if (ex->cur_ev) (void)hipEventRecord(ex->cur_ev[i], st);
+}
+
+void mark_valid(orbx_extractor *ex, int stage) {
+    if (ex->cur_valid) ex->cur_valid[stage] = true;
 }
 
 // Runs the five extractor stages for `batch` frames into result slot `si`.
@@ -238,7 +294,6 @@ int run_extract(orbx_extractor *ex, int si, const uint8_t *d_images, int64_t str
     s.img0_pitch = pitch;
     s.batch = batch;
     const FrameBufs fb = frame_bufs(ex, si);
-    for (int i = 0; i < kNumStages; ++i) ex->stage_valid[i] = false;
     mark(ex, 0, st);
     if (launch_resize(ex->dp, ex->plan, fb, batch, st) != hipSuccess) return ORBX_EIO;
     mark(ex, 1, st);
@@ -250,7 +305,7 @@ int run_extract(orbx_extractor *ex, int si, const uint8_t *d_images, int64_t str
     mark(ex, 4, st);
     if (launch_describe(ex->dp, fb, batch, st) != hipSuccess) return ORBX_EIO;
     mark(ex, 5, st);
-    for (int i = 0; i < kStageMatch; ++i) ex->stage_valid[i] = ex->profiling;
+    for (int i = 0; i < kStageMatch; ++i) mark_valid(ex, i);
     return ORBX_OK;
 }
 
@@ -298,8 +353,6 @@ orbx_extractor *orbx_extractor_create(int device, int nfeatures, float scaleFact
     ex->ini_th = iniThFAST;
     ex->min_th = minThFAST;
     if (hipStreamCreateWithFlags(&ex->stream, hipStreamNonBlocking) != hipSuccess) { delete ex; return nullptr; }
-    for (auto &e : ex->ev)
-        if (hipEventCreate(&e) != hipSuccess) { delete ex; return nullptr; }
     // geometry tables for the getters are size independent; plan a nominal size
     ex->plan = make_plan(640, 480, nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST);
     return ex;
@@ -348,8 +401,11 @@ int orbx_extract_batch_device(orbx_extractor *ex, const uint8_t *d_images, int64
     if (rc) return rc;
     if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
     const int next = ex->cur ^ 1;
-    rc = run_extract(ex, next, d_images, frame_stride, pitch, batch, stream_of(ex, stream));
+    hipStream_t st = stream_of(ex, stream);
+    prof_begin(ex);
+    rc = run_extract(ex, next, d_images, frame_stride, pitch, batch, st);
     if (rc) return rc;
+    mark(ex, kNumStages, st);
     ex->cur = next;
     ex->match_batch = 0;
     return ORBX_OK;
@@ -503,12 +559,16 @@ int orbx_mono_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t f
     hipStream_t st = stream_of(ex, stream);
     const int prev = ex->cur, next = ex->cur ^ 1;
     const bool have_prev = ex->slot[prev].batch == batch && ex->steps > 0;
+    prof_begin(ex);
     rc = run_extract(ex, next, d_images, frame_stride, pitch, batch, st);
     if (rc) return rc;
     ex->cur = next;
     ++ex->steps;
     ex->match_batch = 0;
-    if (!have_prev) return ORBX_OK;
+    if (!have_prev) {
+        mark(ex, kNumStages, st);
+        return ORBX_OK;
+    }
     MatchBufs mb;
     const auto &s1 = ex->slot[prev];
     const auto &s2 = ex->slot[next];
@@ -527,8 +587,8 @@ int orbx_mono_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t f
     mb.reset_prev = 1;
     if (launch_match(mb, batch, ex->plan.max_kps, ex->plan.max_kps, ex->l0cap, ex->l0cap, st) != hipSuccess)
         return ORBX_EIO;
-    mark(ex, 6, st);
-    ex->stage_valid[kStageMatch] = ex->profiling;
+    mark(ex, kNumStages, st);
+    mark_valid(ex, kStageMatch);
     ex->match_batch = batch;
     return ORBX_OK;
 }
@@ -554,6 +614,9 @@ int orbx_mono_matches_download(orbx_extractor *ex, int frame, int32_t *matches12
 
 int orbx_extractor_set_profiling(orbx_extractor *ex, int on) {
     if (!ex) return ORBX_EINVAL;
+    if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
+    for (int s = 0; s < orbx_extractor::kRing; ++s) fold(ex, s);
+    for (int i = 0; i < kNumStages; ++i) { ex->stage_sum[i] = 0; ex->stage_cnt[i] = 0; }
     ex->profiling = on != 0;
     return ORBX_OK;
 }
@@ -561,14 +624,10 @@ int orbx_extractor_set_profiling(orbx_extractor *ex, int on) {
 int orbx_extractor_stage_times(orbx_extractor *ex, float *ms, int cap) {
     if (!ex || (cap > 0 && !ms)) return ORBX_EINVAL;
     if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
+    for (int s = 0; s < orbx_extractor::kRing; ++s) fold(ex, s);
     int nw = 0;
     for (int i = 0; i < kNumStages && i < cap; ++i) {
-        float t = -1.f;
-        if (ex->stage_valid[i]) {
-            if (hipEventSynchronize(ex->ev[i + 1]) != hipSuccess) return ORBX_EIO;
-            if (hipEventElapsedTime(&t, ex->ev[i], ex->ev[i + 1]) != hipSuccess) t = -1.f;
-        }
-        ms[i] = t;
+        ms[i] = ex->stage_cnt[i] ? (float)(ex->stage_sum[i] / ex->stage_cnt[i]) : -1.f;
         ++nw;
     }
     return nw;

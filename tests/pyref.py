@@ -1,0 +1,331 @@
+"""Pure-Python restatements of the reference hot path for SMALL inputs.
+
+A third, independent formulation next to the C++ oracle (oracle/) and the HIP
+kernels, written straight from the reference sources and the OpenCV 3.2
+semantics in DESIGN.md §3; used only to cross-check the oracle on small
+seeded cases (the reference itself ships no test vectors: SURVEY.md §4).
+numpy float32 scalars are used wherever the reference computes in float.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+f32 = np.float32
+
+
+def cv_round(v) -> int:
+    return int(np.rint(v))  # half-to-even, as x86 cvRound
+
+
+def cv_floor(v) -> int:
+    return int(math.floor(float(v)))
+
+
+# ---- cv::resize INTER_LINEAR 8U, OpenCV 3.2 (ORBextractor.cc:1171) -----------
+def resize_linear(src: np.ndarray, dw: int, dh: int) -> np.ndarray:
+    sh, sw = src.shape
+    scale_x, scale_y = 1.0 / (dw / sw), 1.0 / (dh / sh)
+
+    def taps(ssize, dsize, scale, is_x):
+        out, xmax = [], dsize
+        for d in range(dsize):
+            f = f32((d + 0.5) * scale - 0.5)
+            s = cv_floor(f)
+            f = f32(f - f32(s))
+            if is_x:
+                if s < 0:
+                    f, s = f32(0), 0
+                if s + 1 >= ssize:
+                    xmax = min(xmax, d)
+                    if s >= ssize - 1:
+                        f, s = f32(0), ssize - 1
+            a0 = max(-32768, min(32767, cv_round(f32(f32(1) - f) * f32(2048))))
+            a1 = max(-32768, min(32767, cv_round(f * f32(2048))))
+            out.append((s, a0, a1))
+        return out, xmax
+
+    xt, xmax = taps(sw, dw, scale_x, True)
+    yt, _ = taps(sh, dh, scale_y, False)
+    xs = 0
+    while xs <= dw - 16:
+        xs += 16
+    while xs < dw - 4:
+        xs += 4
+    dst = np.zeros((dh, dw), np.uint8)
+    src = src.astype(np.int64)
+    for dy, (sy, b0, b1) in enumerate(yt):
+        r0, r1 = min(max(sy, 0), sh - 1), min(max(sy + 1, 0), sh - 1)
+        for dx, (sx, a0, a1) in enumerate(xt):
+            if dx < xmax:
+                h0 = src[r0, sx] * a0 + src[r0, sx + 1] * a1
+                h1 = src[r1, sx] * a0 + src[r1, sx + 1] * a1
+            else:
+                h0, h1 = src[r0, sx] * 2048, src[r1, sx] * 2048
+            if dx < xs:
+                v = ((((h0 >> 4) * b0) >> 16) + (((h1 >> 4) * b1) >> 16) + 2) >> 2
+            else:
+                v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22
+            dst[dy, dx] = min(max(v, 0), 255)
+    return dst
+
+
+# ---- GaussianBlur 7x7 sigma 2 REFLECT_101, OpenCV 3.2 (ORBextractor.cc:1130) --
+def gauss_taps() -> list:
+    cf = [f32(math.exp(-0.5 / 4.0 * (i - 3) ** 2)) for i in range(7)]
+    s = 0.0
+    for c in cf:
+        s += float(c)
+    s = 1.0 / s
+    cf = [f32(float(c) * s) for c in cf]
+    return [cv_round(f32(c) * f32(256)) for c in cf]
+
+
+def gauss7(img: np.ndarray) -> np.ndarray:
+    h, w = img.shape
+    k = gauss_taps()
+
+    def r101(p, n):
+        while p < 0 or p >= n:
+            p = -p if p < 0 else 2 * n - p - 2
+        return p
+
+    src = img.astype(np.int64)
+    rows = np.zeros((h, w), np.int64)
+    for y in range(h):
+        for x in range(w):
+            rows[y, x] = sum(k[t] * src[y, r101(x + t - 3, w)] for t in range(7))
+    xs = w & ~3
+    kf = [f32(f32(k[3 + i]) * f32(1.0 / 65536.0)) for i in range(4)]
+    out = np.zeros((h, w), np.uint8)
+    for y in range(h):
+        R = [rows[r101(y + t - 3, h)] for t in range(7)]
+        for x in range(w):
+            if x < xs:
+                s = f32(f32(R[3][x]) * kf[0]) + f32(0)
+                for t in range(1, 4):
+                    s = f32(s + f32(f32(R[3 + t][x] + R[3 - t][x]) * kf[t]))
+                v = cv_round(s)
+                out[y, x] = min(max(v, 0), 255)
+            else:
+                s = k[3] * R[3][x] + sum(k[3 + t] * (R[3 + t][x] + R[3 - t][x]) for t in range(1, 4))
+                out[y, x] = min(max((s + (1 << 15)) >> 16, 0), 255)
+    return out
+
+
+# ---- FAST-9 arc score (cv::FAST TYPE_9_16 + cornerScore<16>) ----------------
+CIRCLE = [(0, 3), (1, 3), (2, 2), (3, 1), (3, 0), (3, -1), (2, -2), (1, -3),
+          (0, -3), (-1, -3), (-2, -2), (-3, -1), (-3, 0), (-3, 1), (-2, 2), (-1, 3)]
+
+
+def arc_score(img: np.ndarray, x: int, y: int) -> int:
+    v = int(img[y, x])
+    d = [v - int(img[y + dy, x + dx]) for dx, dy in CIRCLE]
+    best = -10 ** 9
+    for k in range(16):
+        arc = [d[(k + i) % 16] for i in range(9)]
+        best = max(best, min(arc), min(-a for a in arc))
+    return best
+
+
+def fast_cell(img: np.ndarray, threshold: int) -> list:
+    """cv::FAST(img, kps, threshold, nonmax=true) on a whole (sub)image."""
+    h, w = img.shape
+    sc = np.zeros((h, w), np.int64)
+    for y in range(3, h - 3):
+        for x in range(3, w - 3):
+            s = arc_score(img, x, y)
+            if s > threshold:
+                sc[y, x] = s - 1
+    out = []
+    for y in range(3, h - 3):
+        for x in range(3, w - 3):
+            s = sc[y, x]
+            if s and all(s > sc[y + dy, x + dx] for dy in (-1, 0, 1) for dx in (-1, 0, 1) if dx or dy):
+                out.append((x, y, int(s)))
+    return out
+
+
+# ---- DistributeOctTree (ORBextractor.cc:561-787), literal list semantics -----
+class _Node:
+    __slots__ = ("x0", "y0", "x1", "y1", "keys", "no_more", "seq")
+
+    def __init__(self, x0, y0, x1, y1, seq=0):
+        self.x0, self.y0, self.x1, self.y1 = x0, y0, x1, y1
+        self.keys, self.no_more, self.seq = [], False, seq
+
+
+def distribute(cands, w: int, h: int, N: int) -> list:
+    """cands: list of (x, y, score) in level coordinates; returns indices."""
+    if not cands:
+        return []
+    minx, maxx, miny, maxy = 16, w - 16, 16, h - 16
+    nini = round_half_away(f32(f32(maxx - minx) / f32(maxy - miny)))
+    hx = f32(f32(maxx - minx) / f32(nini))
+    seq = [0]
+    nodes = []
+    for i in range(nini):
+        nodes.append(_Node(int(f32(hx * f32(i))), 0, int(f32(hx * f32(i + 1))), maxy - miny))
+    for k, (x, y, _) in enumerate(cands):
+        nodes[int(f32(f32(x - 16) / hx))].keys.append(k)
+    lst = [n for n in nodes if n.keys]
+    for n in lst:
+        n.no_more = len(n.keys) == 1
+
+    def divide(n):
+        hxx = int(math.ceil((n.x1 - n.x0) / 2))
+        hyy = int(math.ceil((n.y1 - n.y0) / 2))
+        mx, my = n.x0 + hxx, n.y0 + hyy
+        ch = [_Node(n.x0, n.y0, mx, my), _Node(mx, n.y0, n.x1, my),
+              _Node(n.x0, my, mx, n.y1), _Node(mx, my, n.x1, n.y1)]
+        for k in n.keys:
+            x, y = cands[k][0] - 16, cands[k][1] - 16
+            q = (0 if y < my else 2) if x < mx else (1 if y < my else 3)
+            ch[q].keys.append(k)
+        for c in ch:
+            c.no_more = len(c.keys) == 1
+        return ch
+
+    finish = False
+    expand = []
+    while not finish:
+        prev = len(lst)
+        n_to_expand = 0
+        expand = []
+        i = 0
+        while i < len(lst):
+            n = lst[i]
+            if n.no_more:
+                i += 1
+                continue
+            for c in divide(n):
+                if c.keys:
+                    c.seq = seq[0]
+                    seq[0] += 1
+                    lst.insert(0, c)
+                    i += 1
+                    if len(c.keys) > 1:
+                        n_to_expand += 1
+                        expand.append(c)
+            del lst[i]
+        if len(lst) >= N or len(lst) == prev:
+            finish = True
+        elif len(lst) + n_to_expand * 3 > N:
+            while not finish:
+                prev = len(lst)
+                todo = sorted(expand, key=lambda n: (len(n.keys), n.seq))
+                expand = []
+                for n in reversed(todo):
+                    for c in divide(n):
+                        if c.keys:
+                            c.seq = seq[0]
+                            seq[0] += 1
+                            lst.insert(0, c)
+                            if len(c.keys) > 1:
+                                expand.append(c)
+                    lst.remove(n)
+                    if len(lst) >= N:
+                        break
+                if len(lst) >= N or len(lst) == prev:
+                    finish = True
+    res = []
+    for n in lst:
+        best = n.keys[0]
+        for k in n.keys[1:]:
+            if cands[k][2] > cands[best][2]:
+                best = k
+        res.append(best)
+    return res
+
+
+# ---- SearchForInitialization (ORBmatcher.cc:406-521) ------------------------
+def hamming(a: np.ndarray, b: np.ndarray) -> int:
+    return int(np.unpackbits(np.bitwise_xor(a, b)).sum())
+
+
+def search_for_initialization(k1, d1, k2, d2, w, h, prev, window, nnratio, check_ori):
+    GC, GR, HL = 64, 48, 30
+    invw, invh = f32(f32(GC) / f32(w)), f32(f32(GR) / f32(h))
+    grid = {}
+    for i, kp in enumerate(k2):
+        px = int(round_half_away(f32(kp["x"] * invw)))
+        py = int(round_half_away(f32(kp["y"] * invh)))
+        if 0 <= px < GC and 0 <= py < GR:
+            grid.setdefault((px, py), []).append(i)
+    m12 = [-1] * len(k1)
+    m21 = [-1] * len(k2)
+    mdist = [2 ** 31 - 1] * len(k2)
+    rot = [[] for _ in range(HL)]
+    r = f32(window)
+    factor = f32(f32(1.0) / f32(HL))
+    for i1 in range(len(k1)):
+        if k1[i1]["octave"] > 0:
+            continue
+        x, y = f32(prev[i1, 0]), f32(prev[i1, 1])
+        cx0 = max(0, math.floor(f32(f32(x - r) * invw)))
+        cx1 = min(GC - 1, math.ceil(f32(f32(x + r) * invw)))
+        cy0 = max(0, math.floor(f32(f32(y - r) * invh)))
+        cy1 = min(GR - 1, math.ceil(f32(f32(y + r) * invh)))
+        cand = []
+        if cx0 < GC and cx1 >= 0 and cy0 < GR and cy1 >= 0:
+            for ix in range(cx0, cx1 + 1):
+                for iy in range(cy0, cy1 + 1):
+                    for j in grid.get((ix, iy), []):
+                        if k2[j]["octave"] != 0:
+                            continue
+                        if abs(f32(k2[j]["x"] - x)) < r and abs(f32(k2[j]["y"] - y)) < r:
+                            cand.append(j)
+        if not cand:
+            continue
+        best, best2, bi = 2 ** 31 - 1, 2 ** 31 - 1, -1
+        for i2 in cand:
+            dist = hamming(d1[i1], d2[i2])
+            if mdist[i2] <= dist:
+                continue
+            if dist < best:
+                best2, best, bi = best, dist, i2
+            elif dist < best2:
+                best2 = dist
+        if best <= 50 and f32(best) < f32(f32(best2) * f32(nnratio)):
+            if m21[bi] >= 0:
+                m12[m21[bi]] = -1
+            m12[i1], m21[bi], mdist[bi] = bi, i1, best
+            if check_ori:
+                rv = f32(k1[i1]["angle"] - k2[bi]["angle"])
+                if rv < 0.0:
+                    rv = f32(rv + f32(360.0))
+                b = int(round_half_away(f32(rv * factor)))
+                if b == HL:
+                    b = 0
+                rot[b].append(i1)
+    if check_ori:
+        sizes = [len(b) for b in rot]
+        m1 = m2 = m3 = 0
+        i1_ = i2_ = i3_ = -1
+        for i, s in enumerate(sizes):
+            if s > m1:
+                m3, m2, m1, i3_, i2_, i1_ = m2, m1, s, i2_, i1_, i
+            elif s > m2:
+                m3, m2, i3_, i2_ = m2, s, i2_, i
+            elif s > m3:
+                m3, i3_ = s, i
+        if f32(m2) < f32(f32(0.1) * f32(m1)):
+            i2_ = i3_ = -1
+        elif f32(m3) < f32(f32(0.1) * f32(m1)):
+            i3_ = -1
+        for i, b in enumerate(rot):
+            if i in (i1_, i2_, i3_):
+                continue
+            for idx in b:
+                m12[idx] = -1
+    prev = prev.copy()
+    for i1, m in enumerate(m12):
+        if m >= 0:
+            prev[i1, 0], prev[i1, 1] = k2[m]["x"], k2[m]["y"]
+    return sum(1 for m in m12 if m >= 0), np.array(m12, np.int32), prev
+
+
+def round_half_away(v) -> int:
+    v = float(v)
+    return int(math.floor(v + 0.5)) if v >= 0 else -int(math.floor(-v + 0.5))
