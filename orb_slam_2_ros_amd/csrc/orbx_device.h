@@ -23,6 +23,8 @@ struct DevPlan {
     int ini_th, min_th;
     int64_t pyr_bytes, blur_bytes, cand_cap;
     int out_cap, max_kps;
+    int cell_max_w, cell_max_h;   // largest FAST cell interior (sizes k_fast's LDS)
+    int fast_patch_stride, fast_patch_bytes, fast_score_bytes, fast_lds_per_wave;
     int node_cap;             // quadtree node capacity (max over levels)
     int node_lds_bytes;       // dynamic LDS of the quadtree kernel
 };
@@ -34,7 +36,8 @@ struct FrameBufs {
     int img0_pitch;           // bytes between rows
     uint8_t *pyr;             // levels >= 1, B * pyr_bytes
     uint8_t *blur;            // blurred levels, B * blur_bytes
-    uint32_t *cand;           // per-cell candidate slots, B * cand_cap
+    uint32_t *cand;           // per-cell candidate slots (iniThFAST lists), B * cand_cap
+    uint32_t *cand2;          // same slots for the minThFAST lists
     int32_t *cell_count;      // B * ncells
     uint32_t *keys;           // per-level compacted candidates, B * cand_cap
     uint16_t *key_node;       // quadtree scratch, B * cand_cap
@@ -73,7 +76,8 @@ hipError_t launch_match(const MatchBufs &mb, int B, int n1cap, int n2cap, int ma
 // (exhaustive-check hook used by the GPU tests).
 hipError_t launch_trig_check(const float *in, float *s, float *c, float *atan_out,
                              const float *ay, const float *ax, int n, int m, hipStream_t st);
-int match_lds_bytes(int n1cap, int n2cap);
+int match_lds_bytes(int n1cap, int n2cap, int maxq, int maxc);
 int quadtree_lds_bytes(int node_cap);
+bool resize_window_fits(const Plan &hp);
 
 }  // namespace orbx

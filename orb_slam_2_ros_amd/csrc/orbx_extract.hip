@@ -119,51 +119,111 @@ __device__ int block_excl_scan_i32(int v, int *total, int *ws) {
 }
 
 // ===========================================================================
+// Wave-cooperative staging of an image rectangle into LDS with aligned dword
+// loads, 8 in flight per lane before any LDS store.  Pixel (r, c) of the
+// rectangle lands at dst[r * ds + o + c]; returns o = x0 & 3.  The caller
+// guarantees a 4-aligned image base and pitch and that the aligned span
+// [x0 & ~3, x0 + nc rounded up to 4) lies inside the row's pitch.
+// ===========================================================================
+__device__ inline int wave_stage_rect(uint8_t *dst, int ds, const uint8_t *img, int pitch, int y0, int x0,
+                                      int nr, int nc, int lane) {
+    const int xa = x0 & ~3, o = x0 - xa;
+    const int nd = (o + nc + 3) >> 2;
+    const int total = nr * nd;
+    const int dr = 64 / nd, dk = 64 - dr * nd;
+    const int r_l = lane / nd, k_l = lane - r_l * nd;
+    const uint8_t *base = img + (int64_t)y0 * pitch + xa;
+    for (int i0 = 0, r0 = r_l, k0 = k_l; i0 < total; i0 += 64 * 8) {
+        uint32_t v[8];
+        int r = r0, k = k0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (i0 + 64 * j + lane < total) v[j] = *reinterpret_cast<const uint32_t *>(base + (int64_t)r * pitch + 4 * k);
+            r += dr; k += dk; if (k >= nd) { k -= nd; ++r; }
+        }
+        r = r0; k = k0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (i0 + 64 * j + lane < total) *reinterpret_cast<uint32_t *>(dst + r * ds + 4 * k) = v[j];
+            r += dr; k += dk; if (k >= nd) { k -= nd; ++r; }
+        }
+        r0 = r; k0 = k;
+    }
+    return o;
+}
+
+__device__ inline void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// ===========================================================================
 // K1: bilinear level l from level l-1 (cv::resize INTER_LINEAR 8U, OpenCV 3.2
 // fixed point; SSE2 vertical rounding on the leading columns, scalar tail).
-// Thread = 4 consecutive output pixels; block = 256 x 4 pixels.
+// Block = 256 x 8 output pixels; the source window it needs (<= kResRows x
+// kResCols bytes, checked on the host) is staged in LDS by coalesced loads.
+// Thread = 4 consecutive columns x 2 rows, one u32 store per row.
 // ===========================================================================
+constexpr int kResTW = 256, kResTH = 8, kResRows = 24, kResCols = 544;
+
 __global__ __launch_bounds__(kThreads) void k_resize(DevPlan p, FrameBufs fb, int l) {
+    __shared__ uint8_t win[kResRows * kResCols];
     const LevelGeom g = p.lv[l];
     const LevelGeom gs = p.lv[l - 1];
-    const int b = blockIdx.z;
-    const int x4 = (blockIdx.x * 64 + (threadIdx.x & 63)) * 4;
-    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
-    if (y >= g.h || x4 >= g.w) return;
+    const int b = blockIdx.z, tid = threadIdx.x;
+    const int x0 = blockIdx.x * kResTW, y0 = blockIdx.y * kResTH;
+    const ResizeTap *xt = p.xtaps + g.xtab_off;
+    const ResizeTap *yt = p.ytaps + g.ytab_off;
+    const int xl = min(x0 + kResTW, g.w) - 1, yl = min(y0 + kResTH, g.h) - 1;
+    const int c_lo = xt[x0].src, c_hi = min((int)xt[xl].src + 1, gs.w - 1);
+    const int r_lo = min(max((int)yt[y0].src, 0), gs.h - 1);
+    const int r_hi = min(max((int)yt[yl].src + 1, 0), gs.h - 1);
+    const int nc = c_hi - c_lo + 1, nr = r_hi - r_lo + 1;
     int spitch;
     const uint8_t *src = level_ptr(p, fb, gs, l - 1, b, spitch);
+    // each wave stages a quarter of the window's rows (aligned dword loads)
+    const int wv = tid >> 6;
+    const int ra = (nr * wv) >> 2, rb = (nr * (wv + 1)) >> 2;
+    int o = c_lo & 3;
+    if (rb > ra) o = wave_stage_rect(win + ra * kResCols, kResCols, src, spitch, r_lo + ra, c_lo, rb - ra, nc, tid & 63);
+    __syncthreads();
+    const int xb = x0 + 4 * (tid & 63);
+    if (xb >= g.w) return;
     uint8_t *dst = fb.pyr + (int64_t)b * p.pyr_bytes + g.pyr_off;
-    const ResizeTap ty = p.ytaps[g.ytab_off + y];
-    const int r0 = min(max((int)ty.src, 0), gs.h - 1);
-    const int r1 = min(max((int)ty.src + 1, 0), gs.h - 1);
-    const uint8_t *S0 = src + (int64_t)r0 * spitch;
-    const uint8_t *S1 = src + (int64_t)r1 * spitch;
-    const int b0 = ty.a0, b1 = ty.a1;
-    uint32_t packed = 0;
+    ResizeTap tx[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int x = x4 + k;
-        if (x >= g.w) break;
-        const ResizeTap tx = p.xtaps[g.xtab_off + x];
-        int h0, h1;
-        if (tx.mode & 1) {
-            h0 = S0[tx.src] * tx.a0 + S0[tx.src + 1] * tx.a1;
-            h1 = S1[tx.src] * tx.a0 + S1[tx.src + 1] * tx.a1;
-        } else {
-            h0 = S0[tx.src] * 2048;
-            h1 = S1[tx.src] * 2048;
+    for (int k = 0; k < 4; ++k) tx[k] = xt[min(xb + k, g.w - 1)];
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+        const int y = y0 + 2 * (tid >> 6) + rr;
+        if (y >= g.h) break;
+        const ResizeTap ty = yt[y];
+        const uint8_t *S0 = win + (min(max((int)ty.src, 0), gs.h - 1) - r_lo) * kResCols + o - c_lo;
+        const uint8_t *S1 = win + (min(max((int)ty.src + 1, 0), gs.h - 1) - r_lo) * kResCols + o - c_lo;
+        const int b0 = ty.a0, b1 = ty.a1;
+        uint32_t packed = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int sx = tx[k].src;
+            int h0, h1;
+            if (tx[k].mode & 1) {
+                h0 = S0[sx] * tx[k].a0 + S0[sx + 1] * tx[k].a1;
+                h1 = S1[sx] * tx[k].a0 + S1[sx + 1] * tx[k].a1;
+            } else {
+                h0 = S0[sx] * 2048;
+                h1 = S1[sx] * 2048;
+            }
+            int v;
+            if (tx[k].mode & 2) {
+                // _mm_packs_epi32(h>>4) ; _mm_mulhi_epi16 ; _mm_adds_epi16 ; +2 ; >>2 ; packus
+                v = ((((h0 >> 4) * b0) >> 16) + (((h1 >> 4) * b1) >> 16) + 2) >> 2;
+            } else {
+                v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
+            }
+            packed |= (uint32_t)min(max(v, 0), 255) << (8 * k);
         }
-        int v;
-        if (tx.mode & 2) {
-            // _mm_packs_epi32(h>>4) ; _mm_mulhi_epi16 ; _mm_adds_epi16 ; +2 ; >>2 ; packus
-            v = ((((h0 >> 4) * b0) >> 16) + (((h1 >> 4) * b1) >> 16) + 2) >> 2;
-        } else {
-            v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
-        }
-        v = min(max(v, 0), 255);
-        packed |= (uint32_t)v << (8 * k);
+        *reinterpret_cast<uint32_t *>(dst + (int64_t)y * g.pitch + xb) = packed;
     }
-    *reinterpret_cast<uint32_t *>(dst + (int64_t)y * g.pitch + x4) = packed;
 }
 
 // ===========================================================================
@@ -218,112 +278,174 @@ __global__ __launch_bounds__(kThreads) void k_blur(DevPlan p, FrameBufs fb) {
 }
 
 // ===========================================================================
-// K3: per-cell FAST-9 with the reference's cell semantics.  For each interior
-// pixel the arc score S = max over the 16 nine-pixel arcs of
+// K3: per-cell FAST-9 with the reference's cell semantics, one wave per cell
+// (no workgroup barriers: each wave owns its cell's LDS slice).
+// For each interior pixel the arc score S = max over the 16 nine-pixel arcs of
 // max(min(v - p), min(p - v)); the pixel is a corner at threshold t iff S > t
-// and cv::FAST's cornerScore is S - 1.  NMS is the strict 3x3 test inside the
-// cell (outside neighbours count 0, as FAST on the cell sub-image sees them).
-// If no keypoint survives at iniThFAST the cell is redone at minThFAST.
-// Output: the cell's keypoints in row-major order, packed (x | y<<12 | s<<24).
+// and cv::FAST's cornerScore is S - 1.  S is evaluated only
+// where a 16-bit brighter/darker mask at minThFAST holds a 9-run, i.e. only
+// for corners.  NMS is the strict 3x3 test inside the cell (outside
+// neighbours count 0, as FAST on the cell sub-image sees them).  The iniThFAST
+// and minThFAST keypoint lists are compacted in one pass into two slot
+// arrays; the count word says which one the cell uses (bit 31 = minThFAST:
+// no keypoint survived at iniThFAST, ORBextractor.cc:846-850).
+// Output: keypoints in row-major order, packed (x | y<<12 | s<<24).
 // ===========================================================================
-constexpr int kCellMax = 64;                 // wCell/hCell < 60 by construction
-constexpr int kPatchW = kCellMax + 6;
-constexpr int kScoreW = kCellMax + 2;
-
-__device__ inline int arc_score(const uint8_t *c, int stride) {
-    const int v = c[0];
-    int d[16];
-    d[0] = v - c[3 * stride];      d[1] = v - c[3 * stride + 1];
-    d[2] = v - c[2 * stride + 2];  d[3] = v - c[stride + 3];
-    d[4] = v - c[3];               d[5] = v - c[-stride + 3];
-    d[6] = v - c[-2 * stride + 2]; d[7] = v - c[-3 * stride + 1];
-    d[8] = v - c[-3 * stride];     d[9] = v - c[-3 * stride - 1];
-    d[10] = v - c[-2 * stride - 2]; d[11] = v - c[-stride - 3];
-    d[12] = v - c[-3];             d[13] = v - c[stride - 3];
-    d[14] = v - c[2 * stride - 2]; d[15] = v - c[3 * stride - 1];
-    int mn[16], mx[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) { mn[k] = min(d[k], d[(k + 1) & 15]); mx[k] = max(d[k], d[(k + 1) & 15]); }
-    int mn4[16], mx4[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) { mn4[k] = min(mn[k], mn[(k + 2) & 15]); mx4[k] = max(mx[k], mx[(k + 2) & 15]); }
-    int dark = -1024, bright = 1024;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int a8 = min(mn4[k], mn4[(k + 4) & 15]);
-        const int b8 = max(mx4[k], mx4[(k + 4) & 15]);
-        dark = max(dark, min(a8, d[(k + 8) & 15]));
-        bright = min(bright, max(b8, d[(k + 8) & 15]));
-    }
-    return max(dark, -bright);
+__device__ inline bool has_run9(uint32_t m16) {
+    const uint32_t m = m16 | (m16 << 16);
+    uint32_t a = m & (m >> 1);
+    a &= a >> 2;
+    a &= a >> 4;
+    a &= m >> 8;
+    return (a & 0xFFFFu) != 0;
 }
 
-__device__ inline bool nms_keep(const uint8_t *sc, int idx) {
+// max over the 16 arcs of 9 of max(min d, min -d), d[k] = v - circle[k]:
+// the order of OpenCV's cornerScore<16> (arcs anchored at even k).
+__device__ inline int arc_score16(const int d[16]) {
+    int q0 = -1000, q1 = 1000;
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) {
+        int a = min(d[(k + 1) & 15], d[(k + 2) & 15]);
+        int b = max(d[(k + 1) & 15], d[(k + 2) & 15]);
+#pragma unroll
+        for (int t = 3; t <= 8; ++t) {
+            a = min(a, d[(k + t) & 15]);
+            b = max(b, d[(k + t) & 15]);
+        }
+        q0 = max(q0, max(min(a, d[k & 15]), min(a, d[(k + 9) & 15])));
+        q1 = min(q1, min(max(b, d[k & 15]), max(b, d[(k + 9) & 15])));
+    }
+    return max(q0, -q1);
+}
+
+__device__ inline bool nms_keep(const uint8_t *sc, int idx, int sw) {
     const int s = sc[idx];
     return s > sc[idx - 1] && s > sc[idx + 1] &&
-           s > sc[idx - kScoreW - 1] && s > sc[idx - kScoreW] && s > sc[idx - kScoreW + 1] &&
-           s > sc[idx + kScoreW - 1] && s > sc[idx + kScoreW] && s > sc[idx + kScoreW + 1];
+           s > sc[idx - sw - 1] && s > sc[idx - sw] && s > sc[idx - sw + 1] &&
+           s > sc[idx + sw - 1] && s > sc[idx + sw] && s > sc[idx + sw + 1];
 }
 
 __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb) {
-    const int ci = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+    extern __shared__ __align__(16) uint8_t lds[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int ci = blockIdx.x * 4 + wave, b = blockIdx.y;
+    if (ci >= p.ncells) return;
     const Cell c = p.cells[ci];
     int32_t *count_out = fb.cell_count + (int64_t)b * p.ncells + ci;
     const int cw = c.x1 - c.x0, ch = c.y1 - c.y0;
     if (cw <= 0 || ch <= 0) {
-        if (tid == 0) *count_out = 0;
+        if (lane == 0) *count_out = 0;
         return;
     }
+    const int PS = p.fast_patch_stride, SW = p.cell_max_w + 2;
+    uint8_t *patch = lds + (size_t)wave * p.fast_lds_per_wave;
+    uint8_t *sci = patch + p.fast_patch_bytes;
+    uint8_t *scm = sci + p.fast_score_bytes;
+    uint16_t *list = reinterpret_cast<uint16_t *>(scm + p.fast_score_bytes);   // (yy << 8 | xx), row-major
     const LevelGeom g = p.lv[c.level];
     int spitch;
-    const uint8_t *src = level_ptr(p, fb, g, c.level, b, spitch);
-    __shared__ uint8_t patch[(kCellMax + 6) * kPatchW];
-    __shared__ uint8_t sc_ini[(kCellMax + 2) * kScoreW];
-    __shared__ uint8_t sc_min[(kCellMax + 2) * kScoreW];
-    __shared__ int ws[4];
-    __shared__ int any_ini;
-    const int pw = cw + 6, ph = ch + 6;
-    for (int i = tid; i < pw * ph; i += kThreads) {
-        const int r = i / pw, col = i - r * pw;
-        patch[r * kPatchW + col] = src[(int64_t)(c.y0 - 3 + r) * spitch + (c.x0 - 3 + col)];
+    const uint8_t *img = level_ptr(p, fb, g, c.level, b, spitch);
+    const int o = wave_stage_rect(patch, PS, img, spitch, c.y0 - 3, c.x0 - 3, ch + 6, cw + 6, lane);
+    {
+        uint32_t *z0 = reinterpret_cast<uint32_t *>(sci);
+        const int nz = (2 * p.fast_score_bytes) >> 2;   // both score maps, in dwords
+        for (int i = lane; i < nz; i += 64) z0[i] = 0;
     }
-    for (int i = tid; i < (ch + 2) * kScoreW; i += kThreads) { sc_ini[i] = 0; sc_min[i] = 0; }
-    if (tid == 0) any_ini = 0;
-    __syncthreads();
+    wave_lds_fence();
+    const uint8_t *pc = patch + 3 * PS + o + 3;         // interior pixel (0, 0)
+    const int ini = p.ini_th, mnt = p.min_th;
     const int npx = cw * ch;
-    for (int i = tid; i < npx; i += kThreads) {
-        const int yy = i / cw, xx = i - yy * cw;
-        const int s = arc_score(&patch[(yy + 3) * kPatchW + xx + 3], kPatchW);
-        const int si = (yy + 1) * kScoreW + xx + 1;
-        sc_ini[si] = s > p.ini_th ? (uint8_t)(s - 1) : 0;
-        sc_min[si] = s > p.min_th ? (uint8_t)(s - 1) : 0;
-    }
-    __syncthreads();
-    int found = 0;
-    for (int i = tid; i < npx; i += kThreads) {
-        const int yy = i / cw, xx = i - yy * cw;
-        found |= nms_keep(sc_ini, (yy + 1) * kScoreW + xx + 1);
-    }
-    if (found) any_ini = 1;
-    __syncthreads();
-    const uint8_t *sc = any_ini ? sc_ini : sc_min;
-    uint32_t *out = fb.cand + (int64_t)b * p.cand_cap + c.slot;
-    int base = 0;
-    for (int r0 = 0; r0 < npx; r0 += kThreads) {
-        const int i = r0 + tid;
-        int keep = 0, yy = 0, xx = 0;
-        if (i < npx) {
-            yy = i / cw;
-            xx = i - yy * cw;
-            keep = nms_keep(sc, (yy + 1) * kScoreW + xx + 1);
+    const uint64_t below = (1ull << lane) - 1;
+
+    // A. compass pre-test at minThFAST: an arc of 9 covers two cyclically
+    //    adjacent points of {0, 4, 8, 12}, so pixels without such a pair are
+    //    not corners at any threshold >= minThFAST.  Survivors are compacted.
+    const int dyc = 64 / cw, dxc = 64 - dyc * cw;
+    int yy = lane / cw, xx = lane - yy * cw;
+    int nsurv = 0;
+    for (int i0 = 0; i0 < npx; i0 += 64) {
+        bool surv = false;
+        if (i0 + lane < npx) {
+            const uint8_t *q = pc + yy * PS + xx;
+            const int v = q[0];
+            const int a0 = q[3 * PS], a4 = q[3], a8 = q[-3 * PS], a12 = q[-3];
+            const uint32_t br = (uint32_t)(a0 - v > mnt) | ((uint32_t)(a4 - v > mnt) << 1) |
+                                ((uint32_t)(a8 - v > mnt) << 2) | ((uint32_t)(a12 - v > mnt) << 3);
+            const uint32_t dk = (uint32_t)(v - a0 > mnt) | ((uint32_t)(v - a4 > mnt) << 1) |
+                                ((uint32_t)(v - a8 > mnt) << 2) | ((uint32_t)(v - a12 > mnt) << 3);
+            surv = ((br & ((br >> 1) | (br << 3))) | (dk & ((dk >> 1) | (dk << 3)))) != 0;
         }
-        int total;
-        const int pos = base + block_excl_scan_i32(keep, &total, ws);
-        if (keep && pos < c.cap)
-            out[pos] = pack_key(c.x0 + xx, c.y0 + yy, sc[(yy + 1) * kScoreW + xx + 1]);
-        base += total;
+        const uint64_t m = __ballot(surv);
+        if (surv) list[nsurv + __popcll(m & below)] = (uint16_t)((yy << 8) | xx);
+        nsurv += __popcll(m);
+        yy += dyc; xx += dxc;
+        if (xx >= cw) { xx -= cw; ++yy; }
     }
-    if (tid == 0) *count_out = min(base, c.cap);
+    wave_lds_fence();
+
+    // B. full 16-point test on survivors; corners get their arc score S and are
+    //    compacted in place (a corner's slot never passes the survivors read).
+    int ncorner = 0;
+    for (int i0 = 0; i0 < nsurv; i0 += 64) {
+        bool corner = false;
+        int e = 0;
+        if (i0 + lane < nsurv) {
+            e = list[i0 + lane];
+            const int ey = e >> 8, ex = e & 0xFF;
+            const uint8_t *q = pc + ey * PS + ex;
+            const int v = q[0];
+            int d[16];
+            d[0] = v - q[3 * PS];       d[1] = v - q[3 * PS + 1];  d[2] = v - q[2 * PS + 2];  d[3] = v - q[PS + 3];
+            d[4] = v - q[3];            d[5] = v - q[-PS + 3];     d[6] = v - q[-2 * PS + 2]; d[7] = v - q[-3 * PS + 1];
+            d[8] = v - q[-3 * PS];      d[9] = v - q[-3 * PS - 1]; d[10] = v - q[-2 * PS - 2]; d[11] = v - q[-PS - 3];
+            d[12] = v - q[-3];          d[13] = v - q[PS - 3];     d[14] = v - q[2 * PS - 2]; d[15] = v - q[3 * PS - 1];
+            uint32_t dark = 0, bright = 0;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                dark |= (uint32_t)(d[k] > mnt) << k;
+                bright |= (uint32_t)(d[k] < -mnt) << k;
+            }
+            if (has_run9(dark) || has_run9(bright)) {
+                corner = true;
+                const int s = arc_score16(d);
+                const int si = (ey + 1) * SW + ex + 1;
+                scm[si] = (uint8_t)(s - 1);
+                sci[si] = s > ini ? (uint8_t)(s - 1) : 0;
+            }
+        }
+        const uint64_t m = __ballot(corner);
+        wave_lds_fence();   // all survivor reads of this chunk precede the in-place writes
+        if (corner) list[ncorner + __popcll(m & below)] = (uint16_t)e;
+        ncorner += __popcll(m);
+    }
+    wave_lds_fence();
+
+    // C. NMS on the corners (non-corners score 0 and can never be kept), both
+    //    thresholds at once, compacted in row-major order into the two lists.
+    uint32_t *out_i = fb.cand + (int64_t)b * p.cand_cap + c.slot;
+    uint32_t *out_m = fb.cand2 + (int64_t)b * p.cand_cap + c.slot;
+    int base_i = 0, base_m = 0;
+    for (int i0 = 0; i0 < ncorner; i0 += 64) {
+        bool ki = false, km = false;
+        int ey = 0, ex = 0, si = 0;
+        if (i0 + lane < ncorner) {
+            const int e = list[i0 + lane];
+            ey = e >> 8;
+            ex = e & 0xFF;
+            si = (ey + 1) * SW + ex + 1;
+            ki = nms_keep(sci, si, SW);
+            km = nms_keep(scm, si, SW);
+        }
+        const uint64_t mi = __ballot(ki), mm = __ballot(km);
+        const int pi = base_i + __popcll(mi & below), pm = base_m + __popcll(mm & below);
+        if (ki && pi < c.cap) out_i[pi] = pack_key(c.x0 + ex, c.y0 + ey, sci[si]);
+        if (km && pm < c.cap) out_m[pm] = pack_key(c.x0 + ex, c.y0 + ey, scm[si]);
+        base_i += __popcll(mi);
+        base_m += __popcll(mm);
+    }
+    if (lane == 0)
+        *count_out = base_i > 0 ? min(base_i, c.cap) : (int32_t)(0x80000000u | (uint32_t)min(base_m, c.cap));
 }
 
 // ===========================================================================
@@ -453,11 +575,13 @@ __global__ __launch_bounds__(kThreads) void k_quadtree(DevPlan p, FrameBufs fb) 
     int base = 0;
     for (int c0 = 0; c0 < ncell; c0 += kThreads) {
         const int c = c0 + tid;
-        const int cnt = c < ncell ? fb.cell_count[(int64_t)b * p.ncells + g.cell_begin + c] : 0;
+        const int word = c < ncell ? fb.cell_count[(int64_t)b * p.ncells + g.cell_begin + c] : 0;
+        const int cnt = word & 0x7FFFFFFF;
         int tot;
         const int ex = block_excl_scan_i32(cnt, &tot, ws32);
         if (cnt > 0) {
-            const uint32_t *src = fb.cand + (int64_t)b * p.cand_cap + p.cells[g.cell_begin + c].slot;
+            const uint32_t *src = (word < 0 ? fb.cand2 : fb.cand) + (int64_t)b * p.cand_cap +
+                                  p.cells[g.cell_begin + c].slot;
             for (int k = 0; k < cnt; ++k) keys[base + ex + k] = src[k];
         }
         base += tot;
@@ -666,8 +790,24 @@ __global__ __launch_bounds__(kThreads) void k_quadtree(DevPlan p, FrameBufs fb) 
 
 // ===========================================================================
 // K5: orientation + rBRIEF + keypoint record, one wave per selected key.
+// The wave stages the 43x43 neighbourhood of its keypoint (radius 21, with the
+// level's reflect-101 at the borders) in LDS once; from it come the integer
+// IC moments (radius-15 disc, unblurred), the 37x37 Gaussian-blurred patch
+// (the 7x7 s=2 blur of the whole level restricted to the pixels the rotated
+// pattern can reach: |offset| <= 18) and the 512 pattern samples.  No blurred
+// pyramid is written to HBM.
 // ===========================================================================
+constexpr int kDescR = 21;                  // patch radius = 18 (samples) + 3 (blur taps)
+constexpr int kDescP = 2 * kDescR + 1;      // 43
+constexpr int kDescPS = 48;                 // patch row stride (bytes, dword rows + align offset)
+constexpr int kBlurR = 18;
+constexpr int kBlurN = 2 * kBlurR + 1;      // 37
+constexpr int kBlurS = 40;                  // blurred patch row stride (bytes)
+constexpr int kRowS = 38;                   // row-pass stride (u16)
+constexpr int kDescWaveLds = kDescP * kDescPS + kDescP * kRowS * 2 + kBlurN * kBlurS;   // 6640 B
+
 __global__ __launch_bounds__(kThreads) void k_describe(DevPlan p, FrameBufs fb) {
+    __shared__ __align__(16) uint8_t lds[4 * ((kDescWaveLds + 15) & ~15)];
     const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int32_t *lc = fb.level_count + (int64_t)b * kMaxLevels;
     if (blockIdx.x == 0 && tid == 0) {
@@ -687,10 +827,31 @@ __global__ __launch_bounds__(kThreads) void k_describe(DevPlan p, FrameBufs fb) 
     const uint32_t key = fb.sel[(int64_t)b * p.out_cap + slot];
     const int x = (int)(key & 0xFFF), y = (int)((key >> 12) & 0xFFF), score = (int)(key >> 24);
 
-    // IC_Angle on the unblurred level (ORBextractor.cc:77-104): exact integer moments.
+    uint8_t *lbase = lds + wave * ((kDescWaveLds + 15) & ~15);
+    uint16_t *rowp = reinterpret_cast<uint16_t *>(lbase + kDescP * kDescPS);
+    uint8_t *blur = lbase + kDescP * kDescPS + kDescP * kRowS * 2;
+
+    // 1. stage the 43x43 unblurred neighbourhood: aligned dword loads when it
+    //    lies inside the level, else byte loads with reflect-101 at the borders
     int spitch;
     const uint8_t *img = level_ptr(p, fb, g, l, b, spitch);
-    const uint8_t *center = img + (int64_t)y * spitch + x;
+    const int px0 = x - kDescR, py0 = y - kDescR;
+    int o = 0;
+    if (px0 >= 0 && py0 >= 0 && x + kDescR < g.w && y + kDescR < g.h &&
+        (px0 & ~3) + 4 * (((px0 & 3) + kDescP + 3) >> 2) <= spitch) {
+        o = wave_stage_rect(lbase, kDescPS, img, spitch, py0, px0, kDescP, kDescP, lane);
+    } else {
+        for (int e = lane; e < kDescP * kDescP; e += 64) {
+            const int r = e / kDescP, c = e - r * kDescP;
+            const int yy = reflect101(py0 + r, g.h), xx = reflect101(px0 + c, g.w);
+            lbase[r * kDescPS + c] = img[(int64_t)yy * spitch + xx];
+        }
+    }
+    const uint8_t *patch = lbase + o;
+    wave_lds_fence();
+
+    // 2. IC_Angle (ORBextractor.cc:77-104): exact integer moments on the disc.
+    const uint8_t *center = patch + kDescR * kDescPS + kDescR;
     const int u = (lane & 31) - 15;
     const int half = lane >> 5;
     int m10 = 0, m01 = 0;
@@ -699,7 +860,7 @@ __global__ __launch_bounds__(kThreads) void k_describe(DevPlan p, FrameBufs fb) 
             if (half == 1 && v == 0) continue;
             const int row = half ? -v : v;
             if (abs(u) <= p.umax[v]) {
-                const int val = center[(int64_t)row * spitch + u];
+                const int val = center[row * kDescPS + u];
                 m10 += u * val;
                 m01 += row * val;
             }
@@ -709,12 +870,54 @@ __global__ __launch_bounds__(kThreads) void k_describe(DevPlan p, FrameBufs fb) 
     m01 = wave_sum_i32(m01);
     const float angle = fast_atan2_deg((float)m01, (float)m10);
 
-    // computeOrbDescriptor on the blurred level (ORBextractor.cc:106-147).
+    // 3. Gaussian 7x7 restricted to the 37x37 sample window: row pass over all
+    //    43 rows (8-wide segments slide along a row), then the column pass with
+    //    OpenCV 3.2's per-column rounding (half-even below w & ~3, else half-up).
+    const int k0 = p.gauss[0], k1 = p.gauss[1], k2 = p.gauss[2], k3 = p.gauss[3];
+    for (int t = lane; t < kDescP * 5; t += 64) {
+        const int r = t / 5, seg = t - r * 5;
+        const int c0 = seg * 8, n = min(8, kBlurN - c0);
+        const uint8_t *q = patch + r * kDescPS + c0;   // patch col (3 + c) - 3 = c for blur col c
+        int w[14];
+#pragma unroll
+        for (int j = 0; j < 14; ++j) w[j] = j < n + 6 ? q[j] : 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (j < n)
+                rowp[r * kRowS + c0 + j] = (uint16_t)(k0 * (w[j] + w[j + 6]) + k1 * (w[j + 1] + w[j + 5]) +
+                                                      k2 * (w[j + 2] + w[j + 4]) + k3 * w[j + 3]);
+    }
+    wave_lds_fence();
+    const int xs = g.w & ~3;
+    for (int t = lane; t < kBlurN * 5; t += 64) {
+        const int c = t / 5, seg = t - c * 5;
+        const int r0 = seg * 8, n = min(8, kBlurN - r0);
+        const int ax = x - kBlurR + c;                 // absolute column of this blurred pixel
+        int w[14];
+#pragma unroll
+        for (int j = 0; j < 14; ++j) w[j] = j < n + 6 ? rowp[(r0 + j) * kRowS + c] : 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (j >= n) break;
+            const int sum = k3 * w[j + 3] + k2 * (w[j + 2] + w[j + 4]) + k1 * (w[j + 1] + w[j + 5]) +
+                            k0 * (w[j] + w[j + 6]);
+            int qv = sum >> 16;
+            if (ax < xs) {
+                const int rem = sum & 0xFFFF;
+                qv += (rem > 0x8000) | ((rem == 0x8000) & (qv & 1));
+            } else {
+                qv = (sum + (1 << 15)) >> 16;
+            }
+            blur[(r0 + j) * kBlurS + c] = (uint8_t)min(qv, 255);
+        }
+    }
+    wave_lds_fence();
+
+    // 4. computeOrbDescriptor (ORBextractor.cc:106-147) on the blurred patch.
     const float factor_pi = (float)(3.14159265358979323846 / 180.f);
     float sa, ca;
     glibc_sincosf(__fmul_rn(angle, factor_pi), &sa, &ca);
-    const uint8_t *blur = fb.blur + (int64_t)b * p.blur_bytes + g.blur_off;
-    const uint8_t *bc = blur + (int64_t)y * g.pitch + x;
+    const uint8_t *bc = blur + kBlurR * kBlurS + kBlurR;
     const int64_t kp_index = (int64_t)b * p.max_kps + off + i;
     uint64_t *dout = reinterpret_cast<uint64_t *>(fb.desc + kp_index * 32);
 #pragma unroll
@@ -726,7 +929,7 @@ __global__ __launch_bounds__(kThreads) void k_describe(DevPlan p, FrameBufs fb) 
             const float px = (float)c_pattern[2 * j + e][0], py = (float)c_pattern[2 * j + e][1];
             const int r = __float2int_rn(__fadd_rn(__fmul_rn(px, sa), __fmul_rn(py, ca)));
             const int cc = __float2int_rn(__fsub_rn(__fmul_rn(px, ca), __fmul_rn(py, sa)));
-            val[e] = bc[(int64_t)r * g.pitch + cc];
+            val[e] = bc[r * kBlurS + cc];
         }
         const uint64_t m = __ballot(val[0] < val[1]);
         if (lane == 0) dout[grp] = m;
@@ -759,7 +962,7 @@ __global__ void k_trig(const float *in, float *so, float *co, int n, const float
 hipError_t launch_resize(const DevPlan &p, const Plan &hp, const FrameBufs &fb, int B, hipStream_t st) {
     for (int l = 1; l < hp.nlevels; ++l) {
         const LevelGeom &g = hp.lv[l];
-        dim3 grid((g.w + 255) / 256, (g.h + 3) / 4, B);
+        dim3 grid((g.w + kResTW - 1) / kResTW, (g.h + kResTH - 1) / kResTH, B);
         hipLaunchKernelGGL(k_resize, grid, dim3(kThreads), 0, st, p, fb, l);
     }
     return hipGetLastError();
@@ -771,11 +974,20 @@ hipError_t launch_blur(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t
 }
 
 hipError_t launch_fast(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t st) {
-    hipLaunchKernelGGL(k_fast, dim3(p.ncells, B), dim3(kThreads), 0, st, p, fb);
+    hipLaunchKernelGGL(k_fast, dim3((p.ncells + 3) / 4, B), dim3(kThreads), 4 * p.fast_lds_per_wave, st, p, fb);
     return hipGetLastError();
 }
 
+// Dynamic LDS above 64 KiB must be opted into per kernel.
+template <typename K>
+hipError_t allow_lds(K kernel, int bytes) {
+    if (bytes <= 64 * 1024) return hipSuccess;
+    return hipFuncSetAttribute(reinterpret_cast<const void *>(kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
+
 hipError_t launch_quadtree(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t st) {
+    if (allow_lds(k_quadtree, p.node_lds_bytes) != hipSuccess) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_quadtree, dim3(p.nlevels, B), dim3(kThreads), p.node_lds_bytes, st, p, fb);
     return hipGetLastError();
 }
@@ -791,6 +1003,21 @@ hipError_t launch_trig_check(const float *in, float *s, float *c, float *atan_ou
     if (total <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_trig, dim3((total + 255) / 256), dim3(256), 0, st, in, s, c, n, ay, ax, atan_out, m);
     return hipGetLastError();
+}
+
+bool resize_window_fits(const Plan &hp) {
+    for (int l = 1; l < hp.nlevels; ++l) {
+        const LevelGeom &g = hp.lv[l];
+        for (int x0 = 0; x0 < g.w; x0 += kResTW) {
+            const int xl = std::min(x0 + kResTW, g.w) - 1;
+            if (hp.xtaps[g.xtab_off + xl].src + 8 - hp.xtaps[g.xtab_off + x0].src > kResCols) return false;
+        }
+        for (int y0 = 0; y0 < g.h; y0 += kResTH) {
+            const int yl = std::min(y0 + kResTH, g.h) - 1;
+            if (hp.ytaps[g.ytab_off + yl].src + 2 - hp.ytaps[g.ytab_off + y0].src > kResRows) return false;
+        }
+    }
+    return true;
 }
 
 int quadtree_lds_bytes(int node_cap) {

@@ -8,9 +8,12 @@
 // dependency -- grid build, window enumeration, filters, all Hamming distances
 // -- runs on every wave; the reference's greedy loop (its vMatchedDistance /
 // vnMatches21 state makes query i1 depend on every earlier one) is replayed in
-// order by a single wave that evaluates each query's candidates 64 at a time
-// with ballot/min reductions, keeping the exact tie semantics (first minimum
-// wins; second-best is the multiset second minimum).
+// order by a single wave.  Each query's 4 smallest (distance, position)
+// entries are found in the parallel phase; the replay only checks their
+// vMatchedDistance validity, falling back to a 64-wide ballot/min scan of the
+// whole list when fewer than two of the four are still valid.  Tie semantics
+// are the reference's: first minimum wins; second-best is the multiset second
+// minimum.
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -25,14 +28,8 @@ constexpr int kGridCells = kGridCols * kGridRows;
 constexpr int kHisto = 30;                      // ORBmatcher::HISTO_LENGTH
 constexpr int kThLow = 50;                      // ORBmatcher::TH_LOW
 constexpr int kSkip = 0xFFFF;
-
-__device__ inline int hamming(const uint8_t *a, const uint8_t *b) {
-    const uint4 *pa = reinterpret_cast<const uint4 *>(a);
-    const uint4 *pb = reinterpret_cast<const uint4 *>(b);
-    const uint4 x0 = pa[0], x1 = pa[1], y0 = pb[0], y1 = pb[1];
-    return __popc(x0.x ^ y0.x) + __popc(x0.y ^ y0.y) + __popc(x0.z ^ y0.z) + __popc(x0.w ^ y0.w) +
-           __popc(x1.x ^ y1.x) + __popc(x1.y ^ y1.y) + __popc(x1.z ^ y1.z) + __popc(x1.w ^ y1.w);
-}
+constexpr int kMT = 1024;                       // threads per frame pair
+constexpr int kMW = kMT / 64;                   // waves
 
 __device__ inline int wave_incl_scan_i32(int v) {
     const int lane = threadIdx.x & 63;
@@ -55,20 +52,71 @@ __device__ inline uint64_t wave_min_u64(uint64_t v) {
     return v;
 }
 
+// LDS layout of one frame pair (16-B aligned arrays first).
 struct MLds {
-    int *gstart;    // kGridCells + 1
-    int *gfill;     // kGridCells
-    int16_t *glist; // n2cap
-    int16_t *kcell_or_rank;
-    int *mdist;     // n2cap
-    int *m21;       // n2cap
-    int *m12;       // n1cap
-    int8_t *rbin;   // n1cap
-    int *qrank;     // n1cap (rank among octave-0 queries, or -1)
-    int *qcount;    // n1cap
+    uint4 *gd;       // maxc x 2: F2 octave-0 descriptors in grid order
+    uint4 *qd;       // maxq x 2: F1 octave-0 (query) descriptors in query order
+    float2 *gxy;     // maxc: F2 positions in grid order
+    float2 *qxy;     // maxq: query centres (vbPrevMatched)
+    int *gstart;     // kGridCells + 1
+    int *gfill;      // kGridCells
+    int *mdist;      // n2cap: vMatchedDistance
+    int *m21;        // n2cap: vnMatches21
+    int *m12;        // n1cap: vnMatches12
+    int *qrank;      // n1cap: rank among octave-0 queries, or -1
+    int *qcount;     // maxq: candidate-list length
+    uint32_t *top4;  // maxq x 4: (i2 << 16 | dist) of the 4 smallest (dist, position)
+    int16_t *kcell;  // n2cap: grid cell of each F2 keypoint (-1: none)
+    int16_t *glist;  // maxc: F2 index by grid position
+    int16_t *qidx;   // maxq: F1 index of each query
+    int16_t *acc;    // n1cap: F2 index accepted for query i1 (-1: none)
+    int8_t *rbin;    // n1cap: rotation bin of accepted queries (-1: none)
 };
 
-__global__ __launch_bounds__(256) void k_search_init(MatchBufs mb, int n1cap, int n2cap, int maxq, int maxc) {
+__device__ inline MLds carve(uint8_t *ptr, int n1cap, int n2cap, int maxq, int maxc) {
+    MLds s;
+    s.gd = reinterpret_cast<uint4 *>(ptr); ptr += sizeof(uint4) * 2 * maxc;
+    s.qd = reinterpret_cast<uint4 *>(ptr); ptr += sizeof(uint4) * 2 * maxq;
+    s.gxy = reinterpret_cast<float2 *>(ptr); ptr += sizeof(float2) * maxc;
+    s.qxy = reinterpret_cast<float2 *>(ptr); ptr += sizeof(float2) * maxq;
+    s.gstart = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * (kGridCells + 1);
+    s.gfill = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * kGridCells;
+    s.mdist = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * n2cap;
+    s.m21 = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * n2cap;
+    s.m12 = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * n1cap;
+    s.qrank = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * n1cap;
+    s.qcount = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * maxq;
+    s.top4 = reinterpret_cast<uint32_t *>(ptr); ptr += sizeof(uint32_t) * 4 * maxq;
+    s.kcell = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * n2cap;
+    s.glist = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * ((maxc + 1) & ~1);
+    s.qidx = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * ((maxq + 1) & ~1);
+    s.acc = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * ((n1cap + 1) & ~1);
+    s.rbin = reinterpret_cast<int8_t *>(ptr);
+    return s;
+}
+
+__device__ inline int hamming_regs(const uint4 a0, const uint4 a1, const uint4 b0, const uint4 b1) {
+    return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+           __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+// Exclusive scan of one int per thread over the block.
+__device__ inline int block_scan_i32(int v, int *total, int *ws) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int incl = wave_incl_scan_i32(v);
+    if (lane == 63) ws[wave] = incl;
+    __syncthreads();
+    int base = 0, tot = 0;
+    for (int w = 0; w < kMW; ++w) {
+        if (w < wave) base += ws[w];
+        tot += ws[w];
+    }
+    __syncthreads();
+    *total = tot;
+    return base + incl - v;
+}
+
+__global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, int n2cap, int maxq, int maxc) {
     extern __shared__ __align__(16) uint8_t lds[];
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const orbx_keypoint *k1 = mb.k1 + (int64_t)b * mb.k1_stride;
@@ -79,23 +127,11 @@ __global__ __launch_bounds__(256) void k_search_init(MatchBufs mb, int n1cap, in
     float *prev = mb.prev_xy + (int64_t)b * mb.k1_stride * 2;
     int32_t *out12 = mb.matches12 + (int64_t)b * mb.k1_stride;
     uint32_t *scratch = mb.scratch + (int64_t)b * mb.scratch_stride;
-
-    MLds s;
-    uint8_t *ptr = lds;
-    s.gstart = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * (kGridCells + 1);
-    s.gfill = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * kGridCells;
-    s.mdist = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * n2cap;
-    s.m21 = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * n2cap;
-    s.m12 = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * n1cap;
-    s.qrank = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * n1cap;
-    s.qcount = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * n1cap;
-    s.glist = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * n2cap;
-    s.kcell_or_rank = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * n2cap;
-    s.rbin = reinterpret_cast<int8_t *>(ptr); ptr += n1cap;
+    const MLds s = carve(lds, n1cap, n2cap, maxq, maxc);
     __shared__ int hist[kHisto];
-    __shared__ int ws[4];
+    __shared__ int ws[kMW];
     __shared__ int sh_top[3];
-    __shared__ int sh_err;
+    __shared__ int sh_err, sh_nq;
 
     // Frame grid constants for an undistorted img_w x img_h image
     // (Frame.cc:218-220, ComputeImageBounds with k1 == 0).
@@ -105,19 +141,19 @@ __global__ __launch_bounds__(256) void k_search_init(MatchBufs mb, int n1cap, in
     const float r = (float)mb.window;
 
     // ---- 0. init
-    for (int i = tid; i <= kGridCells; i += 256) s.gstart[i] = 0;
-    for (int i = tid; i < kGridCells; i += 256) s.gfill[i] = 0;
-    for (int i = tid; i < n2; i += 256) { s.mdist[i] = INT_MAX; s.m21[i] = -1; }
-    for (int i = tid; i < n1; i += 256) { s.m12[i] = -1; s.rbin[i] = -1; s.qcount[i] = 0; }
+    for (int i = tid; i <= kGridCells; i += kMT) s.gstart[i] = 0;
+    for (int i = tid; i < kGridCells; i += kMT) s.gfill[i] = 0;
+    for (int i = tid; i < n2; i += kMT) { s.mdist[i] = INT_MAX; s.m21[i] = -1; }
+    for (int i = tid; i < n1; i += kMT) { s.m12[i] = -1; s.rbin[i] = -1; s.acc[i] = -1; }
     if (tid < kHisto) hist[tid] = 0;
     if (tid == 0) sh_err = 0;
     if (mb.reset_prev) {
-        for (int i = tid; i < n1; i += 256) { prev[2 * i] = k1[i].x; prev[2 * i + 1] = k1[i].y; }
+        for (int i = tid; i < n1; i += kMT) { prev[2 * i] = k1[i].x; prev[2 * i + 1] = k1[i].y; }
     }
     __syncthreads();
 
-    // ---- 1. grid of F2's octave-0 keypoints (PosInGrid uses round(), Frame.cc:417-418)
-    for (int i = tid; i < n2; i += 256) {
+    // ---- 1. F2 grid of octave-0 keypoints (PosInGrid uses round(), Frame.cc:417-418)
+    for (int i = tid; i < n2; i += kMT) {
         int cell = -1;
         if (k2[i].octave == 0) {
             const int px = (int)roundf(__fmul_rn(__fsub_rn(k2[i].x, minX), invW));
@@ -127,39 +163,36 @@ __global__ __launch_bounds__(256) void k_search_init(MatchBufs mb, int n1cap, in
                 atomicAdd(&s.gstart[cell], 1);
             }
         }
-        s.kcell_or_rank[i] = (int16_t)cell;
+        s.kcell[i] = (int16_t)cell;
     }
     __syncthreads();
     {
-        // exclusive scan of the 3072 counts (12 per thread, contiguous)
-        const int per = kGridCells / 256;
+        const int per = kGridCells / kMT;   // 3 cells per thread, contiguous
         int local = 0;
         for (int i = 0; i < per; ++i) local += s.gstart[tid * per + i];
-        const int incl = wave_incl_scan_i32(local);
-        if (lane == 63) ws[wave] = incl;
-        __syncthreads();
-        int base = 0;
-        for (int w = 0; w < wave; ++w) base += ws[w];
-        int run = base + incl - local;
+        int tot;
+        int run = block_scan_i32(local, &tot, ws);
         for (int i = 0; i < per; ++i) {
             const int v = s.gstart[tid * per + i];
             s.gstart[tid * per + i] = run;
             run += v;
         }
-        if (tid == 255) s.gstart[kGridCells] = run;
+        if (tid == kMT - 1) s.gstart[kGridCells] = run;
+        if (tid == 0 && tot > maxc) sh_err = 1;
         __syncthreads();
     }
-    for (int i = tid; i < n2; i += 256) {
-        const int cell = s.kcell_or_rank[i];
+    const int ngrid = min(s.gstart[kGridCells], maxc);
+    for (int i = tid; i < n2; i += kMT) {
+        const int cell = s.kcell[i];
         if (cell >= 0) {
-            const int pos = atomicAdd(&s.gfill[cell], 1);
-            s.glist[s.gstart[cell] + pos] = (int16_t)i;
+            const int pos = s.gstart[cell] + atomicAdd(&s.gfill[cell], 1);
+            if (pos < maxc) s.glist[pos] = (int16_t)i;
         }
     }
     __syncthreads();
-    // keep each cell's list in keypoint-index order (mGrid push_back order)
-    for (int c = tid; c < kGridCells; c += 256) {
-        const int st = s.gstart[c], en = s.gstart[c + 1];
+    // each cell's list in keypoint-index order (mGrid push_back order)
+    for (int c = tid; c < kGridCells; c += kMT) {
+        const int st = s.gstart[c], en = min(s.gstart[c + 1], maxc);
         for (int a = st + 1; a < en; ++a) {
             const int16_t v = s.glist[a];
             int j = a - 1;
@@ -167,104 +200,158 @@ __global__ __launch_bounds__(256) void k_search_init(MatchBufs mb, int n1cap, in
             s.glist[j + 1] = v;
         }
     }
-    // rank of each octave-0 query in F1 (scratch row index)
+    __syncthreads();
+    for (int pos = tid; pos < ngrid; pos += kMT) {
+        const int i2 = s.glist[pos];
+        s.gxy[pos] = make_float2(k2[i2].x, k2[i2].y);
+        const uint4 *dp = reinterpret_cast<const uint4 *>(d2 + (int64_t)i2 * 32);
+        s.gd[2 * pos] = dp[0];
+        s.gd[2 * pos + 1] = dp[1];
+    }
+    // queries: F1 octave-0 keypoints in index order
     {
-        const int per = (n1 + 255) / 256;
+        const int per = (n1 + kMT - 1) / kMT;
         const int st = min(tid * per, n1), en = min(st + per, n1);
         int local = 0;
         for (int i = st; i < en; ++i) local += k1[i].octave == 0;
-        const int incl = wave_incl_scan_i32(local);
-        if (lane == 63) ws[wave] = incl;
-        __syncthreads();
-        int base = 0;
-        for (int w = 0; w < wave; ++w) base += ws[w];
-        int run = base + incl - local;
+        int tot;
+        int run = block_scan_i32(local, &tot, ws);
         for (int i = st; i < en; ++i) {
-            s.qrank[i] = k1[i].octave == 0 ? run : -1;
-            run += k1[i].octave == 0;
+            const bool isq = k1[i].octave == 0;
+            s.qrank[i] = isq && run < maxq ? run : -1;
+            if (isq && run < maxq) {
+                s.qidx[run] = (int16_t)i;
+                s.qxy[run] = make_float2(prev[2 * i], prev[2 * i + 1]);
+                const uint4 *dp = reinterpret_cast<const uint4 *>(d1 + (int64_t)i * 32);
+                s.qd[2 * run] = dp[0];
+                s.qd[2 * run + 1] = dp[1];
+            }
+            run += isq;
         }
-        __syncthreads();
+        if (tid == 0) { sh_nq = min(tot, maxq); if (tot > maxq) sh_err = 1; }
     }
+    __syncthreads();
+    const int nq = sh_nq;
 
-    // ---- 2. candidate lists + distances (GetFeaturesInArea order: ix outer,
-    //         iy inner, cell insertion order; |dx| < r and |dy| < r).
-    for (int i1 = wave; i1 < n1; i1 += 4) {
-        const int q = s.qrank[i1];
-        if (q < 0) continue;
-        if (q >= maxq) { if (lane == 0) sh_err = 1; continue; }
-        const float x = prev[2 * i1], y = prev[2 * i1 + 1];
+    // ---- 2. candidate lists + distances, all from LDS.  GetFeaturesInArea
+    //         visits ix outer, iy inner, then cell insertion order; glist is
+    //         sorted by cell = ix * 48 + iy and index, so the window's list is
+    //         one contiguous glist range per grid column ix.  Lane = column.
+    for (int q = wave; q < nq; q += kMW) {
+        const float2 c = s.qxy[q];
+        const float x = c.x, y = c.y;
         const int cx0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(x, minX), r), invW)));
         const int cx1 = min(kGridCols - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(x, minX), r), invW)));
         const int cy0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(y, minY), r), invH)));
         const int cy1 = min(kGridRows - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(y, minY), r), invH)));
-        if (cx0 >= kGridCols || cx1 < 0 || cy0 >= kGridRows || cy1 < 0 || cx1 < cx0 || cy1 < cy0) continue;
-        const int ncy = cy1 - cy0 + 1;
-        const int ncells = (cx1 - cx0 + 1) * ncy;
-        const uint8_t *q1 = d1 + (int64_t)i1 * 32;
-        uint32_t *list = scratch + (int64_t)q * maxc;
         int written = 0;
-        for (int c0 = 0; c0 < ncells; c0 += 64) {
-            const int cidx = c0 + lane;
+        uint64_t t4[4] = {~0ull, ~0ull, ~0ull, ~0ull};   // this lane's 4 smallest (dist, position, i2)
+        if (!(cx0 >= kGridCols || cx1 < 0 || cy0 >= kGridRows || cy1 < 0 || cx1 < cx0 || cy1 < cy0)) {
+            const uint4 qa = s.qd[2 * q], qb = s.qd[2 * q + 1];
+            uint32_t *list = scratch + (int64_t)q * maxc;
+            const int ncx = cx1 - cx0 + 1;   // <= 64 grid columns
             int st = 0, cnt = 0;
-            if (cidx < ncells) {
-                const int ix = cx0 + cidx / ncy, iy = cy0 + cidx % ncy;
-                const int cell = ix * kGridRows + iy;
-                st = s.gstart[cell];
-                cnt = s.gstart[cell + 1] - st;
+            if (lane < ncx) {
+                const int col = (cx0 + lane) * kGridRows;
+                st = s.gstart[col + cy0];
+                cnt = max(min(s.gstart[col + cy1 + 1], maxc) - st, 0);
             }
             const int incl = wave_incl_scan_i32(cnt);
-            const int tot = __shfl(incl, 63, 64);
-            const int pos0 = written + incl - cnt;
+            const int pos0 = incl - cnt;
+            written = __shfl(incl, 63, 64);
             for (int e = 0; e < cnt; ++e) {
-                const int i2 = s.glist[st + e];
-                const float dx = __fsub_rn(k2[i2].x, x), dy = __fsub_rn(k2[i2].y, y);
+                const int gp = st + e;
+                const int i2 = s.glist[gp];
+                const float2 kp = s.gxy[gp];
+                const float dx = __fsub_rn(kp.x, x), dy = __fsub_rn(kp.y, y);
                 int dist = kSkip;
-                if (fabsf(dx) < r && fabsf(dy) < r) dist = hamming(q1, d2 + (int64_t)i2 * 32);
+                if (fabsf(dx) < r && fabsf(dy) < r) dist = hamming_regs(qa, qb, s.gd[2 * gp], s.gd[2 * gp + 1]);
                 if (pos0 + e < maxc) list[pos0 + e] = ((uint32_t)i2 << 16) | (uint32_t)dist;
+                if (dist != kSkip) {
+                    uint64_t k = ((uint64_t)dist << 32) | ((uint64_t)(pos0 + e) << 16) | (uint32_t)i2;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        if (k < t4[j]) { const uint64_t tmp = t4[j]; t4[j] = k; k = tmp; }
+                    }
+                }
             }
-            written += tot;
         }
         if (written > maxc) { if (lane == 0) sh_err = 1; written = maxc; }
-        if (lane == 0) s.qcount[i1] = written;
+        // wave-wide 4 smallest: pop the minimum head four times
+        for (int j = 0; j < 4; ++j) {
+            const uint64_t mn = wave_min_u64(t4[0]);
+            if (t4[0] == mn && mn != ~0ull) { t4[0] = t4[1]; t4[1] = t4[2]; t4[2] = t4[3]; t4[3] = ~0ull; }
+            if (lane == 0)
+                s.top4[4 * q + j] = mn == ~0ull ? 0xFFFFFFFFu
+                                                : (((uint32_t)mn & 0xFFFFu) << 16) | (uint32_t)(mn >> 32);
+        }
+        if (lane == 0) s.qcount[q] = written;
     }
     __syncthreads();
 
-    // ---- 3. ordered greedy replay (ORBmatcher.cc:425-491), wave 0 only
+    // ---- 3. ordered greedy replay (ORBmatcher.cc:425-491), wave 0 only.
+    // The valid entries (vMatchedDistance[i2] > dist) among a query's 4
+    // smallest (dist, position) entries, in order, are the smallest valid ones
+    // of its whole list: two found decide (best, best2); a list that fits in 4
+    // is decided too; otherwise the list is scanned 64 entries at a time.
     if (wave == 0) {
-        const float factor = 1.0f / kHisto;
-        for (int i1 = 0; i1 < n1; ++i1) {
-            const int q = s.qrank[i1];
-            if (q < 0 || q >= maxq) continue;
-            const int cnt = s.qcount[i1];
+        for (int g0 = 0; g0 < nq; g0 += 64) {
+          // this group's static query data, one query per lane
+          const int gq = min(g0 + lane, nq - 1);
+          const uint32_t r0 = s.top4[4 * gq], r1 = s.top4[4 * gq + 1], r2 = s.top4[4 * gq + 2],
+                         r3 = s.top4[4 * gq + 3];
+          const int rc = s.qcount[gq], ri = s.qidx[gq];
+          const int gn = min(64, nq - g0);
+          for (int j = 0; j < gn; ++j) {
+            const int q = g0 + j;
+            const int cnt = __builtin_amdgcn_readlane(rc, j);
             if (cnt == 0) continue;
-            const uint32_t *list = scratch + (int64_t)q * maxc;
+            const int i1 = __builtin_amdgcn_readlane(ri, j);
+            const uint32_t e4[4] = {(uint32_t)__builtin_amdgcn_readlane((int)r0, j),
+                                    (uint32_t)__builtin_amdgcn_readlane((int)r1, j),
+                                    (uint32_t)__builtin_amdgcn_readlane((int)r2, j),
+                                    (uint32_t)__builtin_amdgcn_readlane((int)r3, j)};
+            int md[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) md[t] = e4[t] == 0xFFFFFFFFu ? 0 : s.mdist[e4[t] >> 16];
             int best = INT_MAX, best2 = INT_MAX, best_i2 = -1;
-            for (int c0 = 0; c0 < cnt; c0 += 64) {
-                const int e = c0 + lane;
-                uint64_t key = ~0ull;
-                int dist = INT_MAX, i2 = -1;
-                if (e < cnt) {
-                    const uint32_t v = list[e];
-                    i2 = (int)(v >> 16);
-                    dist = (int)(v & 0xFFFF);
-                    if (dist == kSkip || s.mdist[i2] <= dist) dist = INT_MAX;
-                    else key = ((uint64_t)dist << 32) | (uint32_t)e;
+            int found = 0;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                if (e4[t] == 0xFFFFFFFFu || found == 2) continue;
+                const int i2 = (int)(e4[t] >> 16), dist = (int)(e4[t] & 0xFFFF);
+                if (md[t] <= dist) continue;
+                if (found == 0) { best = dist; best_i2 = i2; }
+                else best2 = dist;
+                ++found;
+            }
+            if (!(found == 2 || e4[3] == 0xFFFFFFFFu)) {
+                best = INT_MAX; best2 = INT_MAX; best_i2 = -1;
+                const uint32_t *list = scratch + (int64_t)q * maxc;
+                for (int c0 = 0; c0 < cnt; c0 += 64) {
+                    const int e = c0 + lane;
+                    uint64_t key = ~0ull;
+                    int dist = INT_MAX, i2 = -1;
+                    if (e < cnt) {
+                        const uint32_t v = list[e];
+                        i2 = (int)(v >> 16);
+                        dist = (int)(v & 0xFFFF);
+                        if (dist == kSkip || s.mdist[i2] <= dist) dist = INT_MAX;
+                        else key = ((uint64_t)dist << 32) | (uint32_t)e;
+                    }
+                    const uint64_t mn = wave_min_u64(key);
+                    if (mn == ~0ull) continue;
+                    const int cb = (int)(mn >> 32);
+                    const int cb_lane = (int)(mn & 0xFFFFFFFF) - c0;
+                    const int cb_i2 = __shfl(i2, cb_lane, 64);
+                    const uint64_t key2 = (lane == cb_lane || dist == INT_MAX) ? ~0ull : (uint64_t)dist;
+                    const uint64_t mn2 = wave_min_u64(key2);
+                    const int cs = mn2 == ~0ull ? INT_MAX : (int)mn2;
+                    const int hi = best <= cb ? cb : best;
+                    best2 = min(hi, min(best2, cs));
+                    if (cb < best) best_i2 = cb_i2;
+                    best = best <= cb ? best : cb;
                 }
-                const uint64_t mn = wave_min_u64(key);
-                if (mn == ~0ull) continue;
-                const int cb = (int)(mn >> 32);
-                const int cb_lane = (int)(mn & 0xFFFFFFFF) - c0;
-                const int cb_i2 = __shfl(i2, cb_lane, 64);
-                // second smallest of this chunk's valid distances (multiset)
-                const uint64_t key2 = (lane == cb_lane || dist == INT_MAX) ? ~0ull : (uint64_t)dist;
-                const uint64_t mn2 = wave_min_u64(key2);
-                const int cs = mn2 == ~0ull ? INT_MAX : (int)mn2;
-                // merge (running result precedes this chunk)
-                const int nb = best <= cb ? best : cb;
-                const int hi = best <= cb ? cb : best;
-                best2 = min(hi, min(best2, cs));
-                if (cb < best) best_i2 = cb_i2;
-                best = nb;
             }
             if (best <= kThLow && (float)best < __fmul_rn((float)best2, mb.nnratio)) {
                 if (lane == 0) {
@@ -273,20 +360,34 @@ __global__ __launch_bounds__(256) void k_search_init(MatchBufs mb, int n1cap, in
                     s.m12[i1] = best_i2;
                     s.m21[best_i2] = i1;
                     s.mdist[best_i2] = best;
-                    if (mb.check_ori) {
-                        float rot = __fsub_rn(k1[i1].angle, k2[best_i2].angle);
-                        if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
-                        int bin = (int)roundf(__fmul_rn(rot, factor));
-                        if (bin == kHisto) bin = 0;
-                        s.rbin[i1] = (int8_t)bin;
-                        hist[bin] += 1;
-                    }
+                    s.acc[i1] = (int16_t)best_i2;   // binned in phase 4 (stolen pairs keep their bin)
                 }
-                __builtin_amdgcn_s_waitcnt(0);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                 __builtin_amdgcn_wave_barrier();
             }
+          }
         }
-        if (lane == 0 && mb.check_ori) {
+    }
+    __syncthreads();
+
+    // ---- 4. rotation histogram of every accepted pair (rotHist, ORBmatcher.cc:475-483),
+    //         ComputeThreeMaxima, consistency filter and outputs (:494-520)
+    if (mb.check_ori) {
+        const float factor = 1.0f / kHisto;
+        for (int i1 = tid; i1 < n1; i1 += kMT) {
+            const int a = s.acc[i1];
+            if (a < 0) continue;
+            float rot = __fsub_rn(k1[i1].angle, k2[a].angle);
+            if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
+            int bin = (int)roundf(__fmul_rn(rot, factor));
+            if (bin == kHisto) bin = 0;
+            s.rbin[i1] = (int8_t)bin;
+            atomicAdd(&hist[bin], 1);
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        if (mb.check_ori) {
             int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
             for (int i = 0; i < kHisto; ++i) {
                 const int sz = hist[i];
@@ -300,10 +401,8 @@ __global__ __launch_bounds__(256) void k_search_init(MatchBufs mb, int n1cap, in
         }
     }
     __syncthreads();
-
-    // ---- 4. rotation-consistency filter and outputs (ORBmatcher.cc:494-520)
     int local = 0;
-    for (int i1 = tid; i1 < n1; i1 += 256) {
+    for (int i1 = tid; i1 < n1; i1 += kMT) {
         int m = s.m12[i1];
         if (mb.check_ori && m >= 0) {
             const int bin = s.rbin[i1];
@@ -316,22 +415,26 @@ __global__ __launch_bounds__(256) void k_search_init(MatchBufs mb, int n1cap, in
             ++local;
         }
     }
-    local = wave_incl_scan_i32(local);
-    if (lane == 63) ws[wave] = local;
-    __syncthreads();
-    if (tid == 0) mb.nmatches[b] = sh_err ? -1 : ws[0] + ws[1] + ws[2] + ws[3];
+    int total;
+    block_scan_i32(local, &total, ws);
+    if (tid == 0) mb.nmatches[b] = sh_err ? -1 : total;
 }
 
 }  // namespace
 
-int match_lds_bytes(int n1cap, int n2cap) {
-    return (int)(sizeof(int) * (2 * kGridCells + 1) + sizeof(int) * 2 * n2cap + sizeof(int) * 3 * n1cap +
-                 sizeof(int16_t) * 2 * n2cap + n1cap + 64);
+int match_lds_bytes(int n1cap, int n2cap, int maxq, int maxc) {
+    return (int)(32 * (maxc + maxq) + 8 * (maxc + maxq) + sizeof(int) * (2 * kGridCells + 1) +
+                 sizeof(int) * (2 * n2cap + 2 * n1cap) + sizeof(int) * 5 * maxq + sizeof(int16_t) * n2cap +
+                 sizeof(int16_t) * ((maxc + 1) & ~1) + sizeof(int16_t) * ((maxq + 1) & ~1) + sizeof(int16_t) * ((n1cap + 1) & ~1) + n1cap + 64);
 }
 
 hipError_t launch_match(const MatchBufs &mb, int B, int n1cap, int n2cap, int maxq, int maxc, hipStream_t st) {
-    const int bytes = match_lds_bytes(n1cap, n2cap);
-    hipLaunchKernelGGL(k_search_init, dim3(B), dim3(256), bytes, st, mb, n1cap, n2cap, maxq, maxc);
+    const int bytes = match_lds_bytes(n1cap, n2cap, maxq, maxc);
+    if (bytes > 64 * 1024 &&
+        hipFuncSetAttribute(reinterpret_cast<const void *>(k_search_init),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_search_init, dim3(B), dim3(kMT), bytes, st, mb, n1cap, n2cap, maxq, maxc);
     return hipGetLastError();
 }
 

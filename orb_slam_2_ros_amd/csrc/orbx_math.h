@@ -45,24 +45,18 @@ __device__ inline float fast_atan2_deg(float y, float x) {
 // |x| < 120 range (angles here are in [0, 2*pi)); the FMA form equals the
 // non-FMA form bit for bit over every float in [0, 6.2832] and equals this
 // container's glibc 2.35 sincosf there (exhaustive check).
-struct SinCosTab {
-    double sign[4];
-    double hpi_inv, hpi, c0, c1, c2, c3, c4, s1, s2, s3;
-};
-
 __device__ inline void glibc_sincosf(float y, float *sinp, float *cosp) {
-    const SinCosTab t0 = {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0,
-                          0x1p0, -0x1.ffffffd0c621cp-2, 0x1.55553e1068f19p-5,
-                          -0x1.6c087e89a359dp-10, 0x1.99343027bf8c3p-16,
-                          -0x1.555545995a603p-3, 0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13};
-    const SinCosTab t1 = {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0,
-                          -0x1p0, 0x1.ffffffd0c621cp-2, -0x1.55553e1068f19p-5,
-                          0x1.6c087e89a359dp-10, -0x1.99343027bf8c3p-16,
-                          -0x1.555545995a603p-3, 0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13};
+    // __sincosf_table[0] / [1] differ only in the sign of the cos polynomial
+    // (c0..c4); the sign is selected arithmetically (x * +-1 is exact) so no
+    // table lives in per-lane scratch.
+    constexpr double kHpiInv = 0x1.45F306DC9C883p+23, kHpi = 0x1.921FB54442D18p0;
+    constexpr double kC0 = 0x1p0, kC1 = -0x1.ffffffd0c621cp-2, kC2 = 0x1.55553e1068f19p-5,
+                     kC3 = -0x1.6c087e89a359dp-10, kC4 = 0x1.99343027bf8c3p-16;
+    constexpr double kS1 = -0x1.555545995a603p-3, kS2 = 0x1.1107605230bc4p-7, kS3 = -0x1.994eb3774cf24p-13;
     const uint32_t top = (__float_as_uint(y) >> 20) & 0x7ff;
     double x = y;
     int n = 0;
-    const SinCosTab *p = &t0;
+    double csign = 1.0;
     if (top < 0x3f4u) {            // |y| < pi/4 (top-12-bit compare, as glibc)
         if (top < 0x398u) {        // |y| < 2^-12
             *sinp = y;
@@ -70,23 +64,24 @@ __device__ inline void glibc_sincosf(float y, float *sinp, float *cosp) {
             return;
         }
     } else {
-        const double r = __dmul_rn(x, p->hpi_inv);
+        const double r = __dmul_rn(x, kHpiInv);
         n = ((int32_t)r + 0x800000) >> 24;
-        x = __fma_rn(-(double)n, p->hpi, x);
-        const double s = p->sign[n & 3];
-        if (n & 2) p = &t1;
-        x = __dmul_rn(x, s);
+        x = __fma_rn(-(double)n, kHpi, x);
+        const double sgn = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0;   // sign[n & 3]
+        if (n & 2) csign = -1.0;                                           // table [1]
+        x = __dmul_rn(x, sgn);
     }
+    const double c0 = kC0 * csign, c1 = kC1 * csign, c2c = kC2 * csign, c3 = kC3 * csign, c4 = kC4 * csign;
     const double x2 = __dmul_rn(x, x);
     const double x4 = __dmul_rn(x2, x2);
     const double x3 = __dmul_rn(x2, x);
-    const double c2 = __fma_rn(x2, p->c4, p->c3);
-    const double s1 = __fma_rn(x2, p->s3, p->s2);
-    const double c1 = __fma_rn(x2, p->c1, p->c0);
+    const double c2 = __fma_rn(x2, c4, c3);
+    const double s1 = __fma_rn(x2, kS3, kS2);
+    const double c1v = __fma_rn(x2, c1, c0);
     const double x5 = __dmul_rn(x3, x2);
     const double x6 = __dmul_rn(x4, x2);
-    const double s = __fma_rn(x3, p->s1, x);
-    const double c = __fma_rn(x4, p->c2, c1);
+    const double s = __fma_rn(x3, kS1, x);
+    const double c = __fma_rn(x4, c2c, c1v);
     const float sv = (float)__fma_rn(x5, s1, s);
     const float cv = (float)__fma_rn(x6, c2, c);
     if (n & 1) { *sinp = cv; *cosp = sv; }

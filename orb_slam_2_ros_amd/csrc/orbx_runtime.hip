@@ -57,7 +57,7 @@ struct orbx_extractor {
     uint8_t *d_tables = nullptr;
 
     uint8_t *d_pyr = nullptr, *d_blur = nullptr;
-    uint32_t *d_cand = nullptr, *d_keys = nullptr, *d_sel = nullptr;
+    uint32_t *d_cand = nullptr, *d_cand2 = nullptr, *d_keys = nullptr, *d_sel = nullptr;
     int32_t *d_cell_count = nullptr, *d_level_count = nullptr;
     uint16_t *d_key_node = nullptr;
     uint8_t *d_key_q = nullptr;
@@ -109,7 +109,7 @@ struct orbx_extractor {
     }
 
     void release() {
-        dfree(d_tables); dfree(d_pyr); dfree(d_blur); dfree(d_cand); dfree(d_keys); dfree(d_sel);
+        dfree(d_tables); dfree(d_pyr); dfree(d_blur); dfree(d_cand); dfree(d_cand2); dfree(d_keys); dfree(d_sel);
         dfree(d_cell_count); dfree(d_level_count); dfree(d_key_node); dfree(d_key_q);
         for (auto &s : slot) { dfree(s.kps); dfree(s.desc); dfree(s.nkps); s.batch = 0; }
         dfree(d_prev); dfree(d_m12); dfree(d_nmatch); dfree(d_scratch); dfree(d_img);
@@ -172,6 +172,16 @@ int upload_plan(orbx_extractor *ex) {
     int node_cap = 8;
     for (const LevelGeom &g : p.lv) node_cap = std::max(node_cap, std::max(g.quota, 4 * g.nini) + 4);
     d.node_cap = node_cap;
+    int mw = 1, mh = 1;
+    for (const Cell &c : p.cells) { mw = std::max(mw, c.x1 - c.x0); mh = std::max(mh, c.y1 - c.y0); }
+    d.cell_max_w = mw;
+    d.cell_max_h = mh;
+    d.fast_patch_stride = (mw + 6 + 3 + 3) & ~3;      // + alignment offset, dword rows
+    d.fast_patch_bytes = (d.fast_patch_stride * (mh + 6) + 15) & ~15;
+    d.fast_score_bytes = ((mw + 2) * (mh + 2) + 15) & ~15;
+    d.fast_lds_per_wave = d.fast_patch_bytes + 2 * d.fast_score_bytes + ((2 * mw * mh + 15) & ~15);
+    if (mw > 255 || mh > 255) return ORBX_EINVAL;   // survivor list packs (y << 8 | x)
+    if (4 * d.fast_lds_per_wave > 64 * 1024) return ORBX_EINVAL;
     d.node_lds_bytes = quadtree_lds_bytes(node_cap);
     if (d.node_lds_bytes > 160 * 1024) return ORBX_EINVAL;
     return ORBX_OK;
@@ -192,6 +202,7 @@ int reserve(orbx_extractor *ex, int w, int h, int max_batch) {
         if (g.w < 4 || g.h < 4 || g.wcell >= 60 || g.hcell >= 60) return ORBX_EINVAL;
         if (g.ncols > 0 && g.nrows > 0 && g.nini <= 0) return ORBX_EINVAL;
     }
+    if (!resize_window_fits(ex->plan)) return ORBX_EINVAL;
     int rc = upload_plan(ex);
     if (rc) return rc;
     const Plan &p = ex->plan;
@@ -200,6 +211,7 @@ int reserve(orbx_extractor *ex, int w, int h, int max_batch) {
     ok &= dalloc(&ex->d_pyr, B * p.pyr_bytes) == hipSuccess;
     ok &= dalloc(&ex->d_blur, B * p.blur_bytes) == hipSuccess;
     ok &= dalloc(&ex->d_cand, B * p.cand_cap) == hipSuccess;
+    ok &= dalloc(&ex->d_cand2, B * p.cand_cap) == hipSuccess;
     ok &= dalloc(&ex->d_keys, B * p.cand_cap) == hipSuccess;
     ok &= dalloc(&ex->d_key_node, B * p.cand_cap) == hipSuccess;
     ok &= dalloc(&ex->d_key_q, B * p.cand_cap) == hipSuccess;
@@ -234,6 +246,7 @@ FrameBufs frame_bufs(orbx_extractor *ex, int slot) {
     fb.pyr = ex->d_pyr;
     fb.blur = ex->d_blur;
     fb.cand = ex->d_cand;
+    fb.cand2 = ex->d_cand2;
     fb.cell_count = ex->d_cell_count;
     fb.keys = ex->d_keys;
     fb.key_node = ex->d_key_node;
@@ -297,21 +310,45 @@ int run_extract(orbx_extractor *ex, int si, const uint8_t *d_images, int64_t str
     mark(ex, 0, st);
     if (launch_resize(ex->dp, ex->plan, fb, batch, st) != hipSuccess) return ORBX_EIO;
     mark(ex, 1, st);
-    if (launch_blur(ex->dp, fb, batch, st) != hipSuccess) return ORBX_EIO;
-    mark(ex, 2, st);
+    mark(ex, 2, st);   // the blur is fused into k_describe (patch-local); stage 1 stays empty
     if (launch_fast(ex->dp, fb, batch, st) != hipSuccess) return ORBX_EIO;
     mark(ex, 3, st);
     if (launch_quadtree(ex->dp, fb, batch, st) != hipSuccess) return ORBX_EIO;
     mark(ex, 4, st);
     if (launch_describe(ex->dp, fb, batch, st) != hipSuccess) return ORBX_EIO;
     mark(ex, 5, st);
-    for (int i = 0; i < kStageMatch; ++i) mark_valid(ex, i);
+    for (int i = 0; i < kStageMatch; ++i)
+        if (i != kStageBlur) mark_valid(ex, i);
     return ORBX_OK;
 }
 
 int validate_batch(orbx_extractor *ex, const uint8_t *d_images, int pitch, int batch) {
     if (!ex || !ex->planned || !d_images || batch <= 0 || batch > ex->max_batch) return ORBX_EINVAL;
     if (pitch < ex->plan.width) return ORBX_EINVAL;
+    return ORBX_OK;
+}
+
+// The kernels stage level 0 with aligned dword loads: base, pitch and frame
+// stride must be multiples of 4.  Other layouts are first copied (on the
+// stream) into an aligned staging buffer.
+int align_level0(orbx_extractor *ex, const uint8_t **d_images, int64_t *stride, int *pitch, int batch,
+                 hipStream_t st) {
+    if ((((uintptr_t)*d_images) | (uintptr_t)*stride | (uintptr_t)*pitch) % 4 == 0) return ORBX_OK;
+    const int w = ex->plan.width, h = ex->plan.height;
+    const size_t dp = (size_t)pitch_of(w), fs = dp * h, need = fs * batch;
+    if (ex->d_img_bytes < need) {
+        (void)hipStreamSynchronize(st);
+        dfree(ex->d_img);
+        if (dalloc(&ex->d_img, need) != hipSuccess) return ORBX_ENOMEM;
+        ex->d_img_bytes = need;
+    }
+    for (int b = 0; b < batch; ++b)
+        if (hipMemcpy2DAsync(ex->d_img + fs * b, dp, *d_images + *stride * b, *pitch, w, h, hipMemcpyDeviceToDevice,
+                             st) != hipSuccess)
+            return ORBX_EIO;
+    *d_images = ex->d_img;
+    *stride = (int64_t)fs;
+    *pitch = (int)dp;
     return ORBX_OK;
 }
 
@@ -402,6 +439,8 @@ int orbx_extract_batch_device(orbx_extractor *ex, const uint8_t *d_images, int64
     if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
     const int next = ex->cur ^ 1;
     hipStream_t st = stream_of(ex, stream);
+    rc = align_level0(ex, &d_images, &frame_stride, &pitch, batch, st);
+    if (rc) return rc;
     prof_begin(ex);
     rc = run_extract(ex, next, d_images, frame_stride, pitch, batch, st);
     if (rc) return rc;
@@ -500,6 +539,11 @@ int orbx_extractor_debug_fetch(orbx_extractor *ex, int frame, int level, int wha
                              : ex->d_pyr + (int64_t)frame * p.pyr_bytes + g.pyr_off;
             sp = level == 0 ? (size_t)s.img0_pitch : (size_t)g.pitch;
         } else {
+            // the hot path blurs patch-locally inside k_describe; materialise the
+            // full blurred pyramid on demand with the standalone kernel
+            if (launch_blur(ex->dp, frame_bufs(ex, ex->cur), s.batch, ex->stream) != hipSuccess ||
+                hipStreamSynchronize(ex->stream) != hipSuccess)
+                return ORBX_EIO;
             src = ex->d_blur + (int64_t)frame * p.blur_bytes + g.blur_off;
             sp = (size_t)g.pitch;
         }
@@ -513,16 +557,20 @@ int orbx_extractor_debug_fetch(orbx_extractor *ex, int frame, int level, int wha
         if (nc && hipMemcpy(counts.data(), ex->d_cell_count + (size_t)frame * p.cells.size() + g.cell_begin,
                             sizeof(int32_t) * nc, hipMemcpyDeviceToHost) != hipSuccess)
             return ORBX_EIO;
-        std::vector<uint32_t> cand(g.cand_cap);
-        if (g.cand_cap && hipMemcpy(cand.data(), ex->d_cand + (size_t)frame * p.cand_cap + g.cand_off,
-                                    sizeof(uint32_t) * g.cand_cap, hipMemcpyDeviceToHost) != hipSuccess)
+        std::vector<uint32_t> cand(g.cand_cap), cand2(g.cand_cap);
+        if (g.cand_cap && (hipMemcpy(cand.data(), ex->d_cand + (size_t)frame * p.cand_cap + g.cand_off,
+                                     sizeof(uint32_t) * g.cand_cap, hipMemcpyDeviceToHost) != hipSuccess ||
+                           hipMemcpy(cand2.data(), ex->d_cand2 + (size_t)frame * p.cand_cap + g.cand_off,
+                                     sizeof(uint32_t) * g.cand_cap, hipMemcpyDeviceToHost) != hipSuccess))
             return ORBX_EIO;
         int64_t k = 0;
         for (int c = 0; c < nc; ++c) {
             const Cell &cell = p.cells[g.cell_begin + c];
-            for (int i = 0; i < counts[c]; ++i, ++k) {
+            const std::vector<uint32_t> &src = counts[c] < 0 ? cand2 : cand;
+            const int cnt = counts[c] & 0x7FFFFFFF;
+            for (int i = 0; i < cnt; ++i, ++k) {
                 if (3 * (k + 1) > cap) return ORBX_ERANGE;
-                const uint32_t v = cand[cell.slot - g.cand_off + i];
+                const uint32_t v = src[cell.slot - g.cand_off + i];
                 o[3 * k] = (int32_t)(v & 0xFFF);
                 o[3 * k + 1] = (int32_t)((v >> 12) & 0xFFF);
                 o[3 * k + 2] = (int32_t)(v >> 24);
@@ -557,6 +605,8 @@ int orbx_mono_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t f
     if (rc) return rc;
     if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
     hipStream_t st = stream_of(ex, stream);
+    rc = align_level0(ex, &d_images, &frame_stride, &pitch, batch, st);
+    if (rc) return rc;
     const int prev = ex->cur, next = ex->cur ^ 1;
     const bool have_prev = ex->slot[prev].batch == batch && ex->steps > 0;
     prof_begin(ex);
@@ -652,12 +702,12 @@ int orbx_search_for_initialization(int device, const orbx_keypoint *k1, const ui
     if (n1 < 0 || n2 < 0 || n1 > 32767 || n2 > 32767 || img_w <= 0 || img_h <= 0 || !nmatches) return ORBX_EINVAL;
     if ((n1 && (!k1 || !d1 || !prev_xy || !matches12)) || (n2 && (!k2 || !d2))) return ORBX_EINVAL;
     if (hipSetDevice(device) != hipSuccess) return ORBX_ENODEV;
-    if (match_lds_bytes(std::max(n1, 1), std::max(n2, 1)) > 160 * 1024) return ORBX_EINVAL;
     int q = 0, c = 0;
     for (int i = 0; i < n1; ++i) q += k1[i].octave == 0;
     for (int i = 0; i < n2; ++i) c += k2[i].octave == 0;
     q = std::max(q, 1);
     c = std::max(c, 1);
+    if (match_lds_bytes(std::max(n1, 1), std::max(n2, 1), q, c) > 160 * 1024) return ORBX_EINVAL;
     const int n1c = std::max(n1, 1), n2c = std::max(n2, 1);
     orbx_keypoint *dk1 = nullptr, *dk2 = nullptr;
     uint8_t *dd1 = nullptr, *dd2 = nullptr;

@@ -127,3 +127,36 @@ def test_trig_restatements_on_device(oracle_mod):
     ato = np.array([oracle_mod.fast_atan2(float(y), float(x)) for y, x in zip(ys[:20000], xs[:20000])], np.float32)
     assert np.array_equal(at[:20000], ato)
     del s_ref
+
+
+@pytest.mark.parametrize("seed,pool,window", [(0, 4, 100), (1, 16, 60), (2, 2, 200), (3, 64, 30)])
+def test_matcher_ties_and_contention(seed, pool, window, oracle_mod):
+    """Descriptors from a tiny pool: equal distances everywhere, many queries
+    competing for the same candidates (steals, vMatchedDistance filtering and
+    the full-list fallback of the replay), random angles for the histogram."""
+    from orb_slam_2_ros_amd import KEYPOINT_DTYPE
+    rng = np.random.default_rng(seed)
+    w, h = 640, 480
+    n1, n2 = 400, 450
+    base = rng.integers(0, 256, (pool, 32)).astype(np.uint8)
+
+    def frame(n):
+        k = np.zeros(n, KEYPOINT_DTYPE)
+        k["x"] = rng.integers(0, w, n).astype(np.float32) + rng.choice([0, 0.5], n).astype(np.float32)
+        k["y"] = rng.integers(0, h, n).astype(np.float32)
+        k["octave"] = rng.choice([0, 0, 0, 1, 2], n)
+        k["angle"] = rng.uniform(0, 360, n).astype(np.float32)
+        k["class_id"] = -1
+        d = base[rng.integers(0, pool, n)].copy()
+        flip = rng.integers(0, 32, n)
+        d[np.arange(n), flip] ^= rng.integers(0, 4, n).astype(np.uint8)   # small perturbations
+        return k, d
+
+    k1, d1 = frame(n1)
+    k2, d2 = frame(n2)
+    for ratio, ori in [(0.9, True), (1.0, True), (0.6, False)]:
+        prev = np.ascontiguousarray(np.stack([k1["x"], k1["y"]], 1).astype(np.float32))
+        nm_o, m_o, prev_o = oracle_mod.search_for_initialization(k1, d1, k2, d2, w, h, prev, window, ratio, ori)
+        nm_g, m_g = ORBmatcher(ratio, ori).SearchForInitialization(Frame(k1, d1, w, h), Frame(k2, d2, w, h), prev,
+                                                                  window)
+        assert nm_g == nm_o and np.array_equal(m_g, m_o) and np.array_equal(prev, prev_o)

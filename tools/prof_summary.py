@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 rocpd databases (kernel trace + PMC passes) into the
+text files committed under profiles/.
+
+usage: prof_summary.py --trace gpurun_out/prof_r1/trace_results.db
+                       [--fetch gpurun_out/pmc_fetch/pmc_results.db]
+                       [--write gpurun_out/pmc_write/pmc_results.db]
+                       --out profiles/r01_bench_vga_b256
+
+FETCH_SIZE / WRITE_SIZE are reported in KB per dispatch as rocprofv3 gives
+them, plus the gfx950 correction of MI355X_MICROARCH.md §HBM: FETCH_SIZE is
+doubled (wide coalesced reads are tallied at half their bytes); WRITE_SIZE is
+taken as is.  Both are per-dispatch averages over every dispatch of a kernel.
+"""
+import argparse
+import re
+import sqlite3
+from collections import defaultdict
+
+
+def short(name: str) -> str:
+    m = re.search(r"(\w+)\(", name)
+    return m.group(1) if m else name
+
+
+def kernel_stats(db):
+    con = sqlite3.connect(db)
+    rows = con.execute("select name, total_calls, total_duration, average, percentage from top_kernels").fetchall()
+    return [(short(r[0]), int(r[1]), float(r[2]), float(r[3]), float(r[4])) for r in rows]
+
+
+def pmc(db, counter):
+    con = sqlite3.connect(db)
+    acc = defaultdict(list)
+    for name, val in con.execute("select kernel_name, value from counters_collection where counter_name = ?",
+                                 (counter,)):
+        acc[short(name)].append(float(val))
+    return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--trace", required=True)
+    ap.add_argument("--fetch")
+    ap.add_argument("--write")
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--title", default="")
+    a = ap.parse_args()
+    lines = []
+    if a.title:
+        lines.append(f"# {a.title}")
+    lines.append("## rocprofv3 --kernel-trace --stats (durations in ms)")
+    lines.append(f"{'kernel':<20} {'calls':>6} {'total_ms':>12} {'avg_ms':>10} {'pct':>7}")
+    for n, c, tot, avg, pct in kernel_stats(a.trace):
+        lines.append(f"{n:<20} {c:>6} {tot / 1e3:>12.1f} {avg / 1e3:>10.2f} {pct:>7.2f}")
+    if a.fetch or a.write:
+        f = pmc(a.fetch, "FETCH_SIZE") if a.fetch else {}
+        w = pmc(a.write, "WRITE_SIZE") if a.write else {}
+        lines.append("")
+        lines.append("## PMC per dispatch (separate --pmc passes; KB as reported, FETCH x2 = gfx950-corrected)")
+        lines.append(f"{'kernel':<20} {'dispatches':>10} {'FETCH_KB':>12} {'FETCHx2_MB':>11} {'WRITE_KB':>12} "
+                     f"{'HBM_MB':>9}")
+        for k in sorted(set(f) | set(w)):
+            fk, fn = f.get(k, (float('nan'), 0))
+            wk, _ = w.get(k, (float('nan'), 0))
+            hbm = (2 * fk + wk) / 1024.0
+            lines.append(f"{k:<20} {fn:>10} {fk:>12.1f} {2 * fk / 1024:>11.2f} {wk:>12.1f} {hbm:>9.2f}")
+    text = "\n".join(lines) + "\n"
+    with open(a.out, "w") as fh:
+        fh.write(text)
+    print(text)
+
+
+if __name__ == "__main__":
+    main()
