@@ -1,0 +1,171 @@
+// orbx_orbslam2.hpp -- header-only drop-in for ORB_SLAM2::ORBextractor and
+// ORB_SLAM2::ORBmatcher::{DescriptorDistance, SearchForInitialization} over
+// liborbx.so (include/orbx.h).
+//
+// Reference interfaces reproduced (wjjcdy/orb_slam_2_ros):
+//   orb_slam2/include/ORBextractor.h:45-111  (class ORBextractor)
+//   orb_slam2/include/ORBmatcher.h:46,65     (DescriptorDistance, SearchForInitialization)
+//
+// Use: replace `#include "ORBextractor.h"` by this header in Frame.h /
+// Tracking.h (or add the GPU class beside the CPU one) and
+// link liborbx.so.  The types are OpenCV's; nothing here includes HIP.
+#pragma once
+
+#include <cassert>
+#include <cstdint>
+#include <cstdlib>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include <opencv2/core/core.hpp>
+
+#include "orbx.h"
+
+namespace ORB_SLAM2 {
+
+namespace orbx_detail {
+inline int device_index() {
+    const char *s = std::getenv("ORBX_DEVICE");
+    return s ? std::atoi(s) : 0;
+}
+inline void check(int rc, const char *what) {
+    if (rc < 0) throw std::runtime_error(std::string(what) + ": " + orbx_strerror(rc));
+}
+}  // namespace orbx_detail
+
+class ORBextractor {
+public:
+    enum { HARRIS_SCORE = 0, FAST_SCORE = 1 };
+
+    ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST)
+        : nfeatures_(nfeatures), nlevels_(nlevels) {
+        h_ = orbx_extractor_create(orbx_detail::device_index(), nfeatures, scaleFactor, nlevels, iniThFAST,
+                                   minThFAST);
+        if (!h_) throw std::runtime_error("orbx_extractor_create failed (no gfx950 device or bad parameters)");
+        scaleFactor_ = orbx_extractor_get_scale_factor(h_);
+        mvScaleFactor = table(0);
+        mvInvScaleFactor = table(1);
+        mvLevelSigma2 = table(2);
+        mvInvLevelSigma2 = table(3);
+        mvImagePyramid.resize(nlevels);
+    }
+    ~ORBextractor() { orbx_extractor_destroy(h_); }
+    ORBextractor(const ORBextractor &) = delete;
+    ORBextractor &operator=(const ORBextractor &) = delete;
+
+    // ORBextractor.cc:1083-1149.  The mask is ignored, as in the reference.
+    void operator()(cv::InputArray _image, cv::InputArray /*mask*/, std::vector<cv::KeyPoint> &_keypoints,
+                    cv::OutputArray _descriptors) {
+        if (_image.empty()) return;   // outputs untouched (ORBextractor.cc:1086-1087)
+        cv::Mat image = _image.getMat();
+        assert(image.type() == CV_8UC1);
+        int cap = nfeatures_ + 16 * nlevels_ + 64;
+        std::vector<orbx_keypoint> kps;
+        cv::Mat desc;
+        int n = 0;
+        for (;;) {
+            kps.resize(cap);
+            desc.create(cap, 32, CV_8U);
+            const int rc = orbx_extract(h_, image.data, image.cols, image.rows, image.step, kps.data(), desc.data,
+                                        cap, &n);
+            if (rc == ORBX_ERANGE) { cap = n; continue; }
+            orbx_detail::check(rc, "ORBextractor::operator()");
+            break;
+        }
+        _keypoints.clear();
+        _keypoints.reserve(n);
+        for (int i = 0; i < n; ++i) {
+            const orbx_keypoint &k = kps[i];
+            _keypoints.push_back(cv::KeyPoint(cv::Point2f(k.x, k.y), k.size, k.angle, k.response, k.octave,
+                                              k.class_id));
+        }
+        if (n == 0) {
+            _descriptors.release();
+        } else {
+            _descriptors.create(n, 32, CV_8U);
+            desc.rowRange(0, n).copyTo(_descriptors.getMat());
+        }
+        fill_pyramid();
+    }
+
+    int inline GetLevels() { return nlevels_; }
+    float inline GetScaleFactor() { return scaleFactor_; }
+    std::vector<float> inline GetScaleFactors() { return mvScaleFactor; }
+    std::vector<float> inline GetInverseScaleFactors() { return mvInvScaleFactor; }
+    std::vector<float> inline GetScaleSigmaSquares() { return mvLevelSigma2; }
+    std::vector<float> inline GetInverseScaleSigmaSquares() { return mvInvLevelSigma2; }
+
+    // ORBextractor.h:85 -- each level as an ROI of a buffer with a 19-px
+    // reflect-101 border, as ComputePyramid builds it (ORBextractor.cc:1152-1185);
+    // Frame::ComputeStereoMatches reads it (Frame.cc:509, 599-616).
+    std::vector<cv::Mat> mvImagePyramid;
+
+protected:
+    std::vector<float> table(int which) {
+        std::vector<float> v(nlevels_);
+        orbx_detail::check(orbx_extractor_get_scale_table(h_, which, v.data(), nlevels_), "scale table");
+        return v;
+    }
+
+    void fill_pyramid() {
+        const int E = 19;   // EDGE_THRESHOLD
+        for (int l = 0; l < nlevels_; ++l) {
+            int w = 0, h = 0;
+            orbx_detail::check(orbx_extractor_pyramid_level(h_, l, nullptr, 0, &w, &h), "pyramid level");
+            cv::Mat whole(h + 2 * E, w + 2 * E, CV_8U);
+            cv::Mat roi = whole(cv::Rect(E, E, w, h));
+            orbx_detail::check(orbx_extractor_pyramid_level(h_, l, roi.data, roi.step, nullptr, nullptr),
+                               "pyramid level");
+            cv::copyMakeBorder(roi, whole, E, E, E, E, cv::BORDER_REFLECT_101 + cv::BORDER_ISOLATED);
+            mvImagePyramid[l] = roi;
+        }
+    }
+
+    orbx_extractor *h_ = nullptr;
+    int nfeatures_;
+    int nlevels_;
+    float scaleFactor_ = 1.2f;
+    std::vector<float> mvScaleFactor, mvInvScaleFactor, mvLevelSigma2, mvInvLevelSigma2;
+};
+
+// Free-function forms of the two ORBmatcher members this tier accelerates; the
+// reference class keeps its other members (see INTEGRATION.md for the patch).
+struct OrbxMatcher {
+    // ORBmatcher.cc:1649-1665
+    static int DescriptorDistance(const cv::Mat &a, const cv::Mat &b) {
+        return orbx_descriptor_distance(a.ptr<uint8_t>(), b.ptr<uint8_t>());
+    }
+
+    // ORBmatcher.cc:406-521 for frames given by (mvKeysUn, mDescriptors) and the
+    // undistorted image size that sizes Frame's 64x48 grid.
+    static int SearchForInitialization(const std::vector<cv::KeyPoint> &keys1, const cv::Mat &desc1,
+                                       const std::vector<cv::KeyPoint> &keys2, const cv::Mat &desc2, int img_w,
+                                       int img_h, std::vector<cv::Point2f> &vbPrevMatched,
+                                       std::vector<int> &vnMatches12, int windowSize, float nnratio,
+                                       bool checkOri) {
+        auto pack = [](const std::vector<cv::KeyPoint> &ks) {
+            std::vector<orbx_keypoint> out(ks.size());
+            for (size_t i = 0; i < ks.size(); ++i)
+                out[i] = {ks[i].pt.x, ks[i].pt.y, ks[i].size, ks[i].angle, ks[i].response, ks[i].octave,
+                          ks[i].class_id};
+            return out;
+        };
+        const std::vector<orbx_keypoint> k1 = pack(keys1), k2 = pack(keys2);
+        const cv::Mat d1 = desc1.isContinuous() ? desc1 : desc1.clone();
+        const cv::Mat d2 = desc2.isContinuous() ? desc2 : desc2.clone();
+        std::vector<float> prev(2 * keys1.size());
+        for (size_t i = 0; i < keys1.size(); ++i) { prev[2 * i] = vbPrevMatched[i].x; prev[2 * i + 1] = vbPrevMatched[i].y; }
+        vnMatches12.assign(keys1.size(), -1);
+        int nm = 0;
+        orbx_detail::check(orbx_search_for_initialization(orbx_detail::device_index(), k1.data(), d1.data,
+                                                          (int)k1.size(), k2.data(), d2.data, (int)k2.size(),
+                                                          img_w, img_h, prev.data(), vnMatches12.data(),
+                                                          windowSize, nnratio, checkOri ? 1 : 0, &nm),
+                           "SearchForInitialization");
+        for (size_t i = 0; i < keys1.size(); ++i) vbPrevMatched[i] = cv::Point2f(prev[2 * i], prev[2 * i + 1]);
+        return nm;
+    }
+};
+
+}  // namespace ORB_SLAM2

@@ -1,0 +1,70 @@
+// Exercises include/orbx_orbslam2.hpp (the ORB_SLAM2:: drop-in) through its
+// reference-shaped signatures.
+//   adapter_test probe                      -> prints "nodevice" if construction fails
+//   adapter_test run W H img0.raw img1.raw out.bin
+//        extracts both frames, matches them (window 100, 0.9, checkOri) and
+//        writes: n0, kps0 (28 B each), desc0, n1, kps1, desc1, nm, matches12,
+//        prev (2 floats per F1 keypoint), pyramid level 1 with its 19-px border.
+#include <cstdio>
+#include <fstream>
+#include <iostream>
+#include <string>
+
+#include "orbx_orbslam2.hpp"
+
+using namespace ORB_SLAM2;
+
+static cv::Mat load(const char *path, int w, int h) {
+    cv::Mat m(h, w, CV_8U);
+    std::ifstream f(path, std::ios::binary);
+    f.read(reinterpret_cast<char *>(m.data), (std::streamsize)w * h);
+    return m;
+}
+
+int main(int argc, char **argv) {
+    if (argc >= 2 && std::string(argv[1]) == "probe") {
+        try {
+            ORBextractor ex(1000, 1.2f, 8, 20, 7);
+            std::cout << "levels " << ex.GetLevels() << " scale " << ex.GetScaleFactor() << "\n";
+        } catch (const std::runtime_error &e) {
+            std::cout << "nodevice\n";
+        }
+        return 0;
+    }
+    if (argc != 7 || std::string(argv[1]) != "run") return 2;
+    const int w = std::atoi(argv[2]), h = std::atoi(argv[3]);
+    cv::Mat im0 = load(argv[4], w, h), im1 = load(argv[5], w, h);
+    ORBextractor ex(1000, 1.2f, 8, 20, 7);
+    std::vector<cv::KeyPoint> k0, k1;
+    cv::Mat d0, d1;
+    ex(im0, cv::Mat(), k0, d0);
+    ex(im1, cv::Mat(), k1, d1);
+    std::vector<cv::Point2f> prev(k0.size());
+    for (size_t i = 0; i < k0.size(); ++i) prev[i] = k0[i].pt;
+    std::vector<int> m12;
+    const int nm = OrbxMatcher::SearchForInitialization(k0, d0, k1, d1, w, h, prev, m12, 100, 0.9f, true);
+    std::ofstream out(argv[6], std::ios::binary);
+    auto put_kps = [&](const std::vector<cv::KeyPoint> &ks, const cv::Mat &d) {
+        const int n = (int)ks.size();
+        out.write(reinterpret_cast<const char *>(&n), 4);
+        for (const auto &k : ks) {
+            const float f[5] = {k.pt.x, k.pt.y, k.size, k.angle, k.response};
+            const int i[2] = {k.octave, k.class_id};
+            out.write(reinterpret_cast<const char *>(f), 20);
+            out.write(reinterpret_cast<const char *>(i), 8);
+        }
+        for (int r = 0; r < n; ++r) out.write(reinterpret_cast<const char *>(d.ptr<uint8_t>(r)), 32);
+    };
+    put_kps(k0, d0);
+    put_kps(k1, d1);
+    out.write(reinterpret_cast<const char *>(&nm), 4);
+    out.write(reinterpret_cast<const char *>(m12.data()), 4 * m12.size());
+    for (const auto &p : prev) { out.write(reinterpret_cast<const char *>(&p.x), 4); out.write(reinterpret_cast<const char *>(&p.y), 4); }
+    const cv::Mat &l1 = ex.mvImagePyramid[1];
+    const int bw = l1.cols + 38, bh = l1.rows + 38;
+    out.write(reinterpret_cast<const char *>(&bw), 4);
+    out.write(reinterpret_cast<const char *>(&bh), 4);
+    const uint8_t *base = l1.data - 19 * l1.step - 19;
+    for (int y = 0; y < bh; ++y) out.write(reinterpret_cast<const char *>(base + y * l1.step), bw);
+    return 0;
+}

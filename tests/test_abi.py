@@ -57,3 +57,28 @@ def test_no_device_fails_loudly():
     from orb_slam_2_ros_amd import ORBextractor, OrbxError
     with pytest.raises(OrbxError):
         ORBextractor(1000, 1.2, 8, 20, 7)
+
+
+def test_cpp_dropin_adapter_compiles_and_links():
+    """include/orbx_orbslam2.hpp keeps ORB_SLAM2::ORBextractor's signatures; it
+    must compile, link against liborbx.so and, without a device, fail loudly."""
+    import subprocess
+    import torch
+    from cxx_build import build_adapter_test
+    exe = build_adapter_test()
+    out = subprocess.run([str(exe), "probe"], capture_output=True, text=True, check=True).stdout
+    if not torch.cuda.is_available():
+        assert out.strip() == "nodevice"
+    else:
+        assert out.startswith("levels 8")
+
+
+def test_pattern_stays_inside_blur_window():
+    """k_describe blurs only the 37x37 window (|offset| <= 18) around a key:
+    every rotated sample cvRound(x*b + y*a) must land inside it for every angle,
+    i.e. every pattern point lies strictly within radius 18.5."""
+    import re as _re
+    txt = (ROOT / "orb_slam_2_ros_amd" / "csrc" / "orb_pattern.inc").read_text()
+    pts = np.array([[int(a), int(b)] for a, b in _re.findall(r"\{\s*(-?\d+),\s*(-?\d+)\}", txt)])
+    assert pts.shape == (512, 2)
+    assert float(np.sqrt((pts.astype(float) ** 2).sum(1)).max()) < 18.5 - 1e-3

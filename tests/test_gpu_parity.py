@@ -160,3 +160,47 @@ def test_matcher_ties_and_contention(seed, pool, window, oracle_mod):
         nm_g, m_g = ORBmatcher(ratio, ori).SearchForInitialization(Frame(k1, d1, w, h), Frame(k2, d2, w, h), prev,
                                                                   window)
         assert nm_g == nm_o and np.array_equal(m_g, m_o) and np.array_equal(prev, prev_o)
+
+
+def test_cpp_dropin_adapter_end_to_end(tmp_path, oracle_mod):
+    """The C++ ORB_SLAM2:: adapter (include/orbx_orbslam2.hpp) driven through
+    the reference-shaped calls: keypoints, descriptors, SearchForInitialization
+    and mvImagePyramid (with its 19-px reflect-101 border) vs the oracle."""
+    import subprocess
+    from cxx_build import build_adapter_test
+    from orb_slam_2_ros_amd import KEYPOINT_DTYPE
+    w, h = 640, 480
+    fr = synth.frames(w, h, 777, 2)
+    p0, p1, out = tmp_path / "f0.raw", tmp_path / "f1.raw", tmp_path / "out.bin"
+    fr[0].tofile(p0)
+    fr[1].tofile(p1)
+    exe = build_adapter_test()
+    subprocess.run([str(exe), "run", str(w), str(h), str(p0), str(p1), str(out)], check=True)
+    buf = out.read_bytes()
+    off = 0
+
+    def take(dtype, count):
+        nonlocal off
+        a = np.frombuffer(buf, dtype=dtype, count=count, offset=off)
+        off += a.nbytes
+        return a
+
+    res = []
+    for _ in range(2):
+        n = int(take(np.int32, 1)[0])
+        res.append((take(KEYPOINT_DTYPE, n), take(np.uint8, 32 * n).reshape(n, 32)))
+    nm = int(take(np.int32, 1)[0])
+    m12 = take(np.int32, len(res[0][0]))
+    prev = take(np.float32, 2 * len(res[0][0])).reshape(-1, 2)
+    bw, bh = take(np.int32, 2)
+    lvl1 = take(np.uint8, int(bw) * int(bh)).reshape(int(bh), int(bw))
+    for t in range(2):
+        ko, do = oracle_mod.extract(fr[t])
+        assert (res[t][0] == ko).all() and np.array_equal(res[t][1], do)
+    k0, d0 = res[0]
+    k1, d1 = res[1]
+    pv = np.ascontiguousarray(np.stack([k0["x"], k0["y"]], 1).astype(np.float32))
+    nm_o, m_o, prev_o = oracle_mod.search_for_initialization(k0, d0, k1, d1, w, h, pv, 100, 0.9, True)
+    assert nm == nm_o and np.array_equal(m12, m_o) and np.array_equal(prev, prev_o)
+    ref1 = np.pad(oracle_mod.pyramid(fr[1])[1], 19, mode="reflect")   # numpy "reflect" == REFLECT_101
+    assert np.array_equal(lvl1, ref1)
