@@ -118,6 +118,15 @@ __device__ int block_excl_scan_i32(int v, int *total, int *ws) {
     return base + incl - v;
 }
 
+// Unsigned 24-bit multiply (v_mul_u32_u24, full rate); both operands must be
+// in [0, 2^24), which every use below guarantees.
+__device__ inline int mul24u(int a, int b) { return (int)(((uint32_t)a & 0xFFFFFFu) * ((uint32_t)b & 0xFFFFFFu)); }
+
+// Small exact integer division for the index walks (a < 2^15, b <= 255).
+__device__ inline int div_small(int a, int b) {
+    return (int)(((float)a + 0.5f) * __builtin_amdgcn_rcpf((float)b));
+}
+
 // ===========================================================================
 // Wave-cooperative staging of an image rectangle into LDS with aligned dword
 // loads, 8 in flight per lane before any LDS store.  Pixel (r, c) of the
@@ -130,21 +139,21 @@ __device__ inline int wave_stage_rect(uint8_t *dst, int ds, const uint8_t *img, 
     const int xa = x0 & ~3, o = x0 - xa;
     const int nd = (o + nc + 3) >> 2;
     const int total = nr * nd;
-    const int dr = 64 / nd, dk = 64 - dr * nd;
-    const int r_l = lane / nd, k_l = lane - r_l * nd;
+    const int dr = div_small(64, nd), dk = 64 - dr * nd;
+    const int r_l = div_small(lane, nd), k_l = lane - r_l * nd;
     const uint8_t *base = img + (int64_t)y0 * pitch + xa;
     for (int i0 = 0, r0 = r_l, k0 = k_l; i0 < total; i0 += 64 * 8) {
         uint32_t v[8];
         int r = r0, k = k0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            if (i0 + 64 * j + lane < total) v[j] = *reinterpret_cast<const uint32_t *>(base + (int64_t)r * pitch + 4 * k);
+            if (i0 + 64 * j + lane < total) v[j] = *reinterpret_cast<const uint32_t *>(base + mul24u(r, pitch) + 4 * k);
             r += dr; k += dk; if (k >= nd) { k -= nd; ++r; }
         }
         r = r0; k = k0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            if (i0 + 64 * j + lane < total) *reinterpret_cast<uint32_t *>(dst + r * ds + 4 * k) = v[j];
+            if (i0 + 64 * j + lane < total) *reinterpret_cast<uint32_t *>(dst + mul24u(r, ds) + 4 * k) = v[j];
             r += dr; k += dk; if (k >= nd) { k -= nd; ++r; }
         }
         r0 = r; k0 = k;
@@ -164,7 +173,9 @@ __device__ inline void wave_lds_fence() {
 // kResCols bytes, checked on the host) is staged in LDS by coalesced loads.
 // Thread = 4 consecutive columns x 2 rows, one u32 store per row.
 // ===========================================================================
-constexpr int kResTW = 256, kResTH = 8, kResRows = 24, kResCols = 544;
+constexpr int kResTW = 256, kResTH = 16, kResRows = 32, kResCols = 544;
+typedef __attribute__((address_space(3))) uint8_t lds_u8;   // LDS byte (keeps ds_read_u8)
+constexpr int kResRowsPerThread = kResTH / 4;
 
 __global__ __launch_bounds__(kThreads) void k_resize(DevPlan p, FrameBufs fb, int l) {
     __shared__ uint8_t win[kResRows * kResCols];
@@ -174,6 +185,15 @@ __global__ __launch_bounds__(kThreads) void k_resize(DevPlan p, FrameBufs fb, in
     const int x0 = blockIdx.x * kResTW, y0 = blockIdx.y * kResTH;
     const ResizeTap *xt = p.xtaps + g.xtab_off;
     const ResizeTap *yt = p.ytaps + g.ytab_off;
+    // this thread's taps: 4 columns x kResRowsPerThread rows, fetched before the
+    // window so their latency overlaps the staging loads
+    const int xb = x0 + 4 * (tid & 63);
+    const int yb = y0 + kResRowsPerThread * (tid >> 6);
+    ResizeTap tx[4], ty[kResRowsPerThread];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tx[k] = xt[min(xb + k, g.w - 1)];
+#pragma unroll
+    for (int k = 0; k < kResRowsPerThread; ++k) ty[k] = yt[min(yb + k, g.h - 1)];
     const int xl = min(x0 + kResTW, g.w) - 1, yl = min(y0 + kResTH, g.h) - 1;
     const int c_lo = xt[x0].src, c_hi = min((int)xt[xl].src + 1, gs.w - 1);
     const int r_lo = min(max((int)yt[y0].src, 0), gs.h - 1);
@@ -187,42 +207,35 @@ __global__ __launch_bounds__(kThreads) void k_resize(DevPlan p, FrameBufs fb, in
     int o = c_lo & 3;
     if (rb > ra) o = wave_stage_rect(win + ra * kResCols, kResCols, src, spitch, r_lo + ra, c_lo, rb - ra, nc, tid & 63);
     __syncthreads();
-    const int xb = x0 + 4 * (tid & 63);
     if (xb >= g.w) return;
     uint8_t *dst = fb.pyr + (int64_t)b * p.pyr_bytes + g.pyr_off;
-    ResizeTap tx[4];
+    // An opaque 1: stops the load vectorizer from fusing the tap pair S[sx],
+    // S[sx+1] into one unaligned ds_read_u16 (LDS unaligned-access stalls).
+    int one = 1;
+    asm volatile("" : "+s"(one));
 #pragma unroll
-    for (int k = 0; k < 4; ++k) tx[k] = xt[min(xb + k, g.w - 1)];
-#pragma unroll
-    for (int rr = 0; rr < 2; ++rr) {
-        const int y = y0 + 2 * (tid >> 6) + rr;
+    for (int rr = 0; rr < kResRowsPerThread; ++rr) {
+        const int y = yb + rr;
         if (y >= g.h) break;
-        const ResizeTap ty = yt[y];
-        const uint8_t *S0 = win + (min(max((int)ty.src, 0), gs.h - 1) - r_lo) * kResCols + o - c_lo;
-        const uint8_t *S1 = win + (min(max((int)ty.src + 1, 0), gs.h - 1) - r_lo) * kResCols + o - c_lo;
-        const int b0 = ty.a0, b1 = ty.a1;
+        const lds_u8 *S0 = (const lds_u8 *)(win + mul24u(min(max((int)ty[rr].src, 0), gs.h - 1) - r_lo, kResCols) + o - c_lo);
+        const lds_u8 *S1 = (const lds_u8 *)(win + mul24u(min(max((int)ty[rr].src + 1, 0), gs.h - 1) - r_lo, kResCols) + o - c_lo);
+        const int b0 = ty[rr].a0, b1 = ty[rr].a1;
         uint32_t packed = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int sx = tx[k].src;
-            int h0, h1;
-            if (tx[k].mode & 1) {
-                h0 = S0[sx] * tx[k].a0 + S0[sx + 1] * tx[k].a1;
-                h1 = S1[sx] * tx[k].a0 + S1[sx + 1] * tx[k].a1;
-            } else {
-                h0 = S0[sx] * 2048;
-                h1 = S1[sx] * 2048;
-            }
-            int v;
-            if (tx[k].mode & 2) {
-                // _mm_packs_epi32(h>>4) ; _mm_mulhi_epi16 ; _mm_adds_epi16 ; +2 ; >>2 ; packus
-                v = ((((h0 >> 4) * b0) >> 16) + (((h1 >> 4) * b1) >> 16) + 2) >> 2;
-            } else {
-                v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
-            }
+            // Branch-free: tail columns carry coefficients (2048, 0) (orbx_plan.h);
+            // every product fits 24-bit operands (S <= 255, a <= 2048, h < 2^20).
+            const int sx = tx[k].src, sx1 = sx + one;
+            const int h0 = mul24u(S0[sx], tx[k].a0) + mul24u(S0[sx1], tx[k].a1);
+            const int h1 = mul24u(S1[sx], tx[k].a0) + mul24u(S1[sx1], tx[k].a1);
+            // SSE2 columns: _mm_packs_epi32(h>>4); _mm_mulhi_epi16; _mm_adds_epi16; +2; >>2; packus
+            const int v_simd = ((mul24u(h0 >> 4, b0) >> 16) + (mul24u(h1 >> 4, b1) >> 16) + 2) >> 2;
+            // scalar tail: FixedPtCast<int, uchar, 22>
+            const int v_tail = (mul24u(h0, b0) + mul24u(h1, b1) + (1 << 21)) >> 22;
+            const int v = (tx[k].mode & 2) ? v_simd : v_tail;
             packed |= (uint32_t)min(max(v, 0), 255) << (8 * k);
         }
-        *reinterpret_cast<uint32_t *>(dst + (int64_t)y * g.pitch + xb) = packed;
+        *reinterpret_cast<uint32_t *>(dst + mul24u(y, g.pitch) + xb) = packed;
     }
 }
 
@@ -301,22 +314,24 @@ __device__ inline bool has_run9(uint32_t m16) {
 }
 
 // max over the 16 arcs of 9 of max(min d, min -d), d[k] = v - circle[k]:
-// the order of OpenCV's cornerScore<16> (arcs anchored at even k).
+// the order of OpenCV's cornerScore<16> (arcs anchored at even k).  Dark and
+// bright arcs run side by side as packed 16-bit lanes (d, -d).
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
 __device__ inline int arc_score16(const int d[16]) {
-    int q0 = -1000, q1 = 1000;
+    s16x2 e[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) e[k] = (s16x2){(short)d[k], (short)(-d[k])};
+    s16x2 q0 = (s16x2){-1000, -1000};
 #pragma unroll
     for (int k = 0; k < 16; k += 2) {
-        int a = min(d[(k + 1) & 15], d[(k + 2) & 15]);
-        int b = max(d[(k + 1) & 15], d[(k + 2) & 15]);
+        s16x2 a = __builtin_elementwise_min(e[(k + 1) & 15], e[(k + 2) & 15]);
 #pragma unroll
-        for (int t = 3; t <= 8; ++t) {
-            a = min(a, d[(k + t) & 15]);
-            b = max(b, d[(k + t) & 15]);
-        }
-        q0 = max(q0, max(min(a, d[k & 15]), min(a, d[(k + 9) & 15])));
-        q1 = min(q1, min(max(b, d[k & 15]), max(b, d[(k + 9) & 15])));
+        for (int t = 3; t <= 8; ++t) a = __builtin_elementwise_min(a, e[(k + t) & 15]);
+        q0 = __builtin_elementwise_max(q0, __builtin_elementwise_max(__builtin_elementwise_min(a, e[k & 15]),
+                                                                     __builtin_elementwise_min(a, e[(k + 9) & 15])));
     }
-    return max(q0, -q1);
+    return max((int)q0.x, (int)q0.y);
 }
 
 __device__ inline bool nms_keep(const uint8_t *sc, int idx, int sw) {
@@ -361,8 +376,8 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb) {
     // A. compass pre-test at minThFAST: an arc of 9 covers two cyclically
     //    adjacent points of {0, 4, 8, 12}, so pixels without such a pair are
     //    not corners at any threshold >= minThFAST.  Survivors are compacted.
-    const int dyc = 64 / cw, dxc = 64 - dyc * cw;
-    int yy = lane / cw, xx = lane - yy * cw;
+    const int dyc = div_small(64, cw), dxc = 64 - dyc * cw;
+    int yy = div_small(lane, cw), xx = lane - yy * cw;
     int nsurv = 0;
     for (int i0 = 0; i0 < npx; i0 += 64) {
         bool surv = false;
@@ -384,41 +399,53 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb) {
     }
     wave_lds_fence();
 
-    // B. full 16-point test on survivors; corners get their arc score S and are
-    //    compacted in place (a corner's slot never passes the survivors read).
+    // B1. full 16-point test on survivors; corners are compacted in place
+    //     (a corner's slot never passes the survivors already read).
+#define ORBX_CIRCLE_DIFFS(q, v, d)                                                                    \
+    d[0] = v - q[3 * PS];       d[1] = v - q[3 * PS + 1];  d[2] = v - q[2 * PS + 2];  d[3] = v - q[PS + 3];  \
+    d[4] = v - q[3];            d[5] = v - q[-PS + 3];     d[6] = v - q[-2 * PS + 2]; d[7] = v - q[-3 * PS + 1]; \
+    d[8] = v - q[-3 * PS];      d[9] = v - q[-3 * PS - 1]; d[10] = v - q[-2 * PS - 2]; d[11] = v - q[-PS - 3]; \
+    d[12] = v - q[-3];          d[13] = v - q[PS - 3];     d[14] = v - q[2 * PS - 2]; d[15] = v - q[3 * PS - 1];
     int ncorner = 0;
     for (int i0 = 0; i0 < nsurv; i0 += 64) {
         bool corner = false;
         int e = 0;
         if (i0 + lane < nsurv) {
             e = list[i0 + lane];
-            const int ey = e >> 8, ex = e & 0xFF;
-            const uint8_t *q = pc + ey * PS + ex;
+            const uint8_t *q = pc + (e >> 8) * PS + (e & 0xFF);
             const int v = q[0];
             int d[16];
-            d[0] = v - q[3 * PS];       d[1] = v - q[3 * PS + 1];  d[2] = v - q[2 * PS + 2];  d[3] = v - q[PS + 3];
-            d[4] = v - q[3];            d[5] = v - q[-PS + 3];     d[6] = v - q[-2 * PS + 2]; d[7] = v - q[-3 * PS + 1];
-            d[8] = v - q[-3 * PS];      d[9] = v - q[-3 * PS - 1]; d[10] = v - q[-2 * PS - 2]; d[11] = v - q[-PS - 3];
-            d[12] = v - q[-3];          d[13] = v - q[PS - 3];     d[14] = v - q[2 * PS - 2]; d[15] = v - q[3 * PS - 1];
+            ORBX_CIRCLE_DIFFS(q, v, d)
             uint32_t dark = 0, bright = 0;
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
                 dark |= (uint32_t)(d[k] > mnt) << k;
                 bright |= (uint32_t)(d[k] < -mnt) << k;
             }
-            if (has_run9(dark) || has_run9(bright)) {
-                corner = true;
-                const int s = arc_score16(d);
-                const int si = (ey + 1) * SW + ex + 1;
-                scm[si] = (uint8_t)(s - 1);
-                sci[si] = s > ini ? (uint8_t)(s - 1) : 0;
-            }
+            corner = has_run9(dark) || has_run9(bright);
         }
         const uint64_t m = __ballot(corner);
         wave_lds_fence();   // all survivor reads of this chunk precede the in-place writes
         if (corner) list[ncorner + __popcll(m & below)] = (uint16_t)e;
         ncorner += __popcll(m);
     }
+    wave_lds_fence();
+    // B2. arc score S of each corner (dense: one corner per lane)
+    for (int i0 = 0; i0 < ncorner; i0 += 64) {
+        if (i0 + lane < ncorner) {
+            const int e = list[i0 + lane];
+            const int ey = e >> 8, ex = e & 0xFF;
+            const uint8_t *q = pc + ey * PS + ex;
+            const int v = q[0];
+            int d[16];
+            ORBX_CIRCLE_DIFFS(q, v, d)
+            const int sc = arc_score16(d);
+            const int si = (ey + 1) * SW + ex + 1;
+            scm[si] = (uint8_t)(sc - 1);
+            sci[si] = sc > ini ? (uint8_t)(sc - 1) : 0;
+        }
+    }
+#undef ORBX_CIRCLE_DIFFS
     wave_lds_fence();
 
     // C. NMS on the corners (non-corners score 0 and can never be kept), both
@@ -873,7 +900,8 @@ __global__ __launch_bounds__(kThreads) void k_describe(DevPlan p, FrameBufs fb) 
     // 3. Gaussian 7x7 restricted to the 37x37 sample window: row pass over all
     //    43 rows (8-wide segments slide along a row), then the column pass with
     //    OpenCV 3.2's per-column rounding (half-even below w & ~3, else half-up).
-    const int k0 = p.gauss[0], k1 = p.gauss[1], k2 = p.gauss[2], k3 = p.gauss[3];
+    // taps of getGaussianKernel(7, 2) x256 (checked against the plan on the host)
+    constexpr int k0 = kGaussTaps[0], k1 = kGaussTaps[1], k2 = kGaussTaps[2], k3 = kGaussTaps[3];
     for (int t = lane; t < kDescP * 5; t += 64) {
         const int r = t / 5, seg = t - r * 5;
         const int c0 = seg * 8, n = min(8, kBlurN - c0);
@@ -884,8 +912,8 @@ __global__ __launch_bounds__(kThreads) void k_describe(DevPlan p, FrameBufs fb) 
 #pragma unroll
         for (int j = 0; j < 8; ++j)
             if (j < n)
-                rowp[r * kRowS + c0 + j] = (uint16_t)(k0 * (w[j] + w[j + 6]) + k1 * (w[j + 1] + w[j + 5]) +
-                                                      k2 * (w[j + 2] + w[j + 4]) + k3 * w[j + 3]);
+                rowp[r * kRowS + c0 + j] = (uint16_t)(mul24u(k0, w[j] + w[j + 6]) + mul24u(k1, w[j + 1] + w[j + 5]) +
+                                                      mul24u(k2, w[j + 2] + w[j + 4]) + mul24u(k3, w[j + 3]));
     }
     wave_lds_fence();
     const int xs = g.w & ~3;
@@ -899,8 +927,8 @@ __global__ __launch_bounds__(kThreads) void k_describe(DevPlan p, FrameBufs fb) 
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             if (j >= n) break;
-            const int sum = k3 * w[j + 3] + k2 * (w[j + 2] + w[j + 4]) + k1 * (w[j + 1] + w[j + 5]) +
-                            k0 * (w[j] + w[j + 6]);
+            const int sum = mul24u(k3, w[j + 3]) + mul24u(k2, w[j + 2] + w[j + 4]) +
+                            mul24u(k1, w[j + 1] + w[j + 5]) + mul24u(k0, w[j] + w[j + 6]);
             int qv = sum >> 16;
             if (ax < xs) {
                 const int rem = sum & 0xFFFF;

@@ -26,6 +26,9 @@ constexpr int kMaxLevels = 16;
 constexpr int kEdge = 19;          // EDGE_THRESHOLD, ORBextractor.cc:71
 constexpr int kBorder = kEdge - 3; // minBorderX/Y, ORBextractor.cc:796-797
 constexpr int kFastCell = 30;      // W, ORBextractor.cc:788
+// cvRound(256 * getGaussianKernel(7, 2, CV_32F)) = {18, 34, 49, 55, 49, 34, 18};
+// make_gauss_taps recomputes it from the OpenCV formula and the runtime checks both agree.
+constexpr int kGaussTaps[7] = {18, 34, 49, 55, 49, 34, 18};
 
 // x86-64 cvRound (cvtss2si / cvtsd2si): round half to even.
 inline int round_even(float v) { return (int)std::nearbyint(v); }
@@ -131,8 +134,12 @@ inline void make_resize_taps(int ssize, int dsize, bool is_x, std::vector<Resize
         int xs = 0;
         while (xs <= dsize - 16) xs += 16;
         while (xs < dsize - 4) xs += 4;
-        for (int d = 0; d < dsize; ++d)
+        for (int d = 0; d < dsize; ++d) {
             t[d].mode = (int16_t)((d < xmax ? 1 : 0) | (d < xs ? 2 : 0));
+            // From xmax on, HResizeLinear stores S[sx]*2048: the same value as the
+            // two-tap form with coefficients (2048, 0), which keeps the kernel branch-free.
+            if (d >= xmax) { t[d].a0 = 2048; t[d].a1 = 0; }
+        }
     }
     out.insert(out.end(), t.begin(), t.end());
 }

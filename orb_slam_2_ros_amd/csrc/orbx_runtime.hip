@@ -160,7 +160,10 @@ int upload_plan(orbx_extractor *ex) {
     d.nlevels = p.nlevels;
     d.ncells = (int)p.cells.size();
     d.nblur_tiles = (int)tiles.size();
-    for (int i = 0; i < 7; ++i) d.gauss[i] = p.gauss[i];
+    for (int i = 0; i < 7; ++i) {
+        d.gauss[i] = p.gauss[i];
+        if (p.gauss[i] != kGaussTaps[i]) return ORBX_EINVAL;   // kernels use the constant taps
+    }
     for (int i = 0; i < 16; ++i) d.umax[i] = p.umax[i];
     d.ini_th = std::min(std::max(p.ini_th, 0), 255);
     d.min_th = std::min(std::max(p.min_th, 0), 255);
