@@ -334,13 +334,6 @@ __device__ inline int arc_score16(const int d[16]) {
     return max((int)q0.x, (int)q0.y);
 }
 
-__device__ inline bool nms_keep(const uint8_t *sc, int idx, int sw) {
-    const int s = sc[idx];
-    return s > sc[idx - 1] && s > sc[idx + 1] &&
-           s > sc[idx - sw - 1] && s > sc[idx - sw] && s > sc[idx - sw + 1] &&
-           s > sc[idx + sw - 1] && s > sc[idx + sw] && s > sc[idx + sw + 1];
-}
-
 __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb) {
     extern __shared__ __align__(16) uint8_t lds[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -355,27 +348,27 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb) {
     }
     const int PS = p.fast_patch_stride, SW = p.cell_max_w + 2;
     uint8_t *patch = lds + (size_t)wave * p.fast_lds_per_wave;
-    uint8_t *sci = patch + p.fast_patch_bytes;
-    uint8_t *scm = sci + p.fast_score_bytes;
+    uint8_t *scm = patch + p.fast_patch_bytes;   // S-1 of corners at min(ini, min) threshold, 0 elsewhere
     uint16_t *list = reinterpret_cast<uint16_t *>(scm + p.fast_score_bytes);   // (yy << 8 | xx), row-major
     const LevelGeom g = p.lv[c.level];
     int spitch;
     const uint8_t *img = level_ptr(p, fb, g, c.level, b, spitch);
     const int o = wave_stage_rect(patch, PS, img, spitch, c.y0 - 3, c.x0 - 3, ch + 6, cw + 6, lane);
     {
-        uint32_t *z0 = reinterpret_cast<uint32_t *>(sci);
-        const int nz = (2 * p.fast_score_bytes) >> 2;   // both score maps, in dwords
+        uint32_t *z0 = reinterpret_cast<uint32_t *>(scm);
+        const int nz = p.fast_score_bytes >> 2;
         for (int i = lane; i < nz; i += 64) z0[i] = 0;
     }
     wave_lds_fence();
     const uint8_t *pc = patch + 3 * PS + o + 3;         // interior pixel (0, 0)
     const int ini = p.ini_th, mnt = p.min_th;
+    const int lo = min(ini, mnt);   // corners at either threshold are corners at lo
     const int npx = cw * ch;
     const uint64_t below = (1ull << lane) - 1;
 
-    // A. compass pre-test at minThFAST: an arc of 9 covers two cyclically
+    // A. compass pre-test at the lower threshold: an arc of 9 covers two cyclically
     //    adjacent points of {0, 4, 8, 12}, so pixels without such a pair are
-    //    not corners at any threshold >= minThFAST.  Survivors are compacted.
+    //    not corners at any threshold >= the lower threshold.  Survivors are compacted.
     const int dyc = div_small(64, cw), dxc = 64 - dyc * cw;
     int yy = div_small(lane, cw), xx = lane - yy * cw;
     int nsurv = 0;
@@ -385,10 +378,10 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb) {
             const uint8_t *q = pc + yy * PS + xx;
             const int v = q[0];
             const int a0 = q[3 * PS], a4 = q[3], a8 = q[-3 * PS], a12 = q[-3];
-            const uint32_t br = (uint32_t)(a0 - v > mnt) | ((uint32_t)(a4 - v > mnt) << 1) |
-                                ((uint32_t)(a8 - v > mnt) << 2) | ((uint32_t)(a12 - v > mnt) << 3);
-            const uint32_t dk = (uint32_t)(v - a0 > mnt) | ((uint32_t)(v - a4 > mnt) << 1) |
-                                ((uint32_t)(v - a8 > mnt) << 2) | ((uint32_t)(v - a12 > mnt) << 3);
+            const uint32_t br = (uint32_t)(a0 - v > lo) | ((uint32_t)(a4 - v > lo) << 1) |
+                                ((uint32_t)(a8 - v > lo) << 2) | ((uint32_t)(a12 - v > lo) << 3);
+            const uint32_t dk = (uint32_t)(v - a0 > lo) | ((uint32_t)(v - a4 > lo) << 1) |
+                                ((uint32_t)(v - a8 > lo) << 2) | ((uint32_t)(v - a12 > lo) << 3);
             surv = ((br & ((br >> 1) | (br << 3))) | (dk & ((dk >> 1) | (dk << 3)))) != 0;
         }
         const uint64_t m = __ballot(surv);
@@ -419,8 +412,8 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb) {
             uint32_t dark = 0, bright = 0;
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
-                dark |= (uint32_t)(d[k] > mnt) << k;
-                bright |= (uint32_t)(d[k] < -mnt) << k;
+                dark |= (uint32_t)(d[k] > lo) << k;
+                bright |= (uint32_t)(d[k] < -lo) << k;
             }
             corner = has_run9(dark) || has_run9(bright);
         }
@@ -439,35 +432,42 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb) {
             const int v = q[0];
             int d[16];
             ORBX_CIRCLE_DIFFS(q, v, d)
-            const int sc = arc_score16(d);
-            const int si = (ey + 1) * SW + ex + 1;
-            scm[si] = (uint8_t)(sc - 1);
-            sci[si] = sc > ini ? (uint8_t)(sc - 1) : 0;
+            scm[(ey + 1) * SW + ex + 1] = (uint8_t)(arc_score16(d) - 1);
         }
     }
 #undef ORBX_CIRCLE_DIFFS
     wave_lds_fence();
 
-    // C. NMS on the corners (non-corners score 0 and can never be kept), both
-    //    thresholds at once, compacted in row-major order into the two lists.
+    // C. NMS on the corners, both thresholds at once, compacted in row-major
+    //    order into the two lists.  At threshold t >= lo a pixel's FAST score is
+    //    S-1 if S-1 >= t and 0 otherwise (a non-corner), so one score map serves
+    //    both thresholds.
     uint32_t *out_i = fb.cand + (int64_t)b * p.cand_cap + c.slot;
     uint32_t *out_m = fb.cand2 + (int64_t)b * p.cand_cap + c.slot;
     int base_i = 0, base_m = 0;
     for (int i0 = 0; i0 < ncorner; i0 += 64) {
         bool ki = false, km = false;
-        int ey = 0, ex = 0, si = 0;
+        int ey = 0, ex = 0, sv = 0;
         if (i0 + lane < ncorner) {
             const int e = list[i0 + lane];
             ey = e >> 8;
             ex = e & 0xFF;
-            si = (ey + 1) * SW + ex + 1;
-            ki = nms_keep(sci, si, SW);
-            km = nms_keep(scm, si, SW);
+            const int si = (ey + 1) * SW + ex + 1;
+            sv = scm[si];
+            const int nb[8] = {scm[si - 1], scm[si + 1], scm[si - SW - 1], scm[si - SW],
+                               scm[si - SW + 1], scm[si + SW - 1], scm[si + SW], scm[si + SW + 1]};
+            ki = sv >= ini;
+            km = sv >= mnt;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                ki &= sv > (nb[t] >= ini ? nb[t] : 0);
+                km &= sv > (nb[t] >= mnt ? nb[t] : 0);
+            }
         }
         const uint64_t mi = __ballot(ki), mm = __ballot(km);
         const int pi = base_i + __popcll(mi & below), pm = base_m + __popcll(mm & below);
-        if (ki && pi < c.cap) out_i[pi] = pack_key(c.x0 + ex, c.y0 + ey, sci[si]);
-        if (km && pm < c.cap) out_m[pm] = pack_key(c.x0 + ex, c.y0 + ey, scm[si]);
+        if (ki && pi < c.cap) out_i[pi] = pack_key(c.x0 + ex, c.y0 + ey, sv);
+        if (km && pm < c.cap) out_m[pm] = pack_key(c.x0 + ex, c.y0 + ey, sv);
         base_i += __popcll(mi);
         base_m += __popcll(mm);
     }
@@ -819,19 +819,19 @@ __global__ __launch_bounds__(kThreads) void k_quadtree(DevPlan p, FrameBufs fb) 
 // K5: orientation + rBRIEF + keypoint record, one wave per selected key.
 // The wave stages the 43x43 neighbourhood of its keypoint (radius 21, with the
 // level's reflect-101 at the borders) in LDS once; from it come the integer
-// IC moments (radius-15 disc, unblurred), the 37x37 Gaussian-blurred patch
-// (the 7x7 s=2 blur of the whole level restricted to the pixels the rotated
-// pattern can reach: |offset| <= 18) and the 512 pattern samples.  No blurred
-// pyramid is written to HBM.
+// IC moments (radius-15 disc, unblurred), the horizontal pass of the 7x7 s=2
+// Gaussian over the window the rotated pattern can reach (|offset| <= 18), and
+// each of the 512 samples as the vertical pass at that pixel.  Identical to
+// sampling the blurred level (same taps, same per-column rounding); no
+// blurred pyramid is written to HBM.
 // ===========================================================================
 constexpr int kDescR = 21;                  // patch radius = 18 (samples) + 3 (blur taps)
 constexpr int kDescP = 2 * kDescR + 1;      // 43
 constexpr int kDescPS = 48;                 // patch row stride (bytes, dword rows + align offset)
 constexpr int kBlurR = 18;
 constexpr int kBlurN = 2 * kBlurR + 1;      // 37
-constexpr int kBlurS = 40;                  // blurred patch row stride (bytes)
 constexpr int kRowS = 38;                   // row-pass stride (u16)
-constexpr int kDescWaveLds = kDescP * kDescPS + kDescP * kRowS * 2 + kBlurN * kBlurS;   // 6640 B
+constexpr int kDescWaveLds = kDescP * kDescPS + kDescP * kRowS * 2;   // 5332 B
 
 __global__ __launch_bounds__(kThreads) void k_describe(DevPlan p, FrameBufs fb) {
     __shared__ __align__(16) uint8_t lds[4 * ((kDescWaveLds + 15) & ~15)];
@@ -856,7 +856,6 @@ __global__ __launch_bounds__(kThreads) void k_describe(DevPlan p, FrameBufs fb) 
 
     uint8_t *lbase = lds + wave * ((kDescWaveLds + 15) & ~15);
     uint16_t *rowp = reinterpret_cast<uint16_t *>(lbase + kDescP * kDescPS);
-    uint8_t *blur = lbase + kDescP * kDescPS + kDescP * kRowS * 2;
 
     // 1. stage the 43x43 unblurred neighbourhood: aligned dword loads when it
     //    lies inside the level, else byte loads with reflect-101 at the borders
@@ -916,36 +915,28 @@ __global__ __launch_bounds__(kThreads) void k_describe(DevPlan p, FrameBufs fb) 
                                                       mul24u(k2, w[j + 2] + w[j + 4]) + mul24u(k3, w[j + 3]));
     }
     wave_lds_fence();
-    const int xs = g.w & ~3;
-    for (int t = lane; t < kBlurN * 5; t += 64) {
-        const int c = t / 5, seg = t - c * 5;
-        const int r0 = seg * 8, n = min(8, kBlurN - r0);
-        const int ax = x - kBlurR + c;                 // absolute column of this blurred pixel
-        int w[14];
-#pragma unroll
-        for (int j = 0; j < 14; ++j) w[j] = j < n + 6 ? rowp[(r0 + j) * kRowS + c] : 0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            if (j >= n) break;
-            const int sum = mul24u(k3, w[j + 3]) + mul24u(k2, w[j + 2] + w[j + 4]) +
-                            mul24u(k1, w[j + 1] + w[j + 5]) + mul24u(k0, w[j] + w[j + 6]);
-            int qv = sum >> 16;
-            if (ax < xs) {
-                const int rem = sum & 0xFFFF;
-                qv += (rem > 0x8000) | ((rem == 0x8000) & (qv & 1));
-            } else {
-                qv = (sum + (1 << 15)) >> 16;
-            }
-            blur[(r0 + j) * kBlurS + c] = (uint8_t)min(qv, 255);
-        }
-    }
-    wave_lds_fence();
 
-    // 4. computeOrbDescriptor (ORBextractor.cc:106-147) on the blurred patch.
+    // 4. computeOrbDescriptor (ORBextractor.cc:106-147) on the blurred level:
+    //    each sample's blurred value is the column pass evaluated at that pixel
+    //    from the row-pass buffer, with OpenCV 3.2's per-column rounding
+    //    (half-even below w & ~3, else half-up).
     const float factor_pi = (float)(3.14159265358979323846 / 180.f);
     float sa, ca;
     glibc_sincosf(__fmul_rn(angle, factor_pi), &sa, &ca);
-    const uint8_t *bc = blur + kBlurR * kBlurS + kBlurR;
+    const int xs = g.w & ~3;
+    auto blurred = [&](int r, int c) {   // r, c in [-18, 18]
+        const uint16_t *w = rowp + (r + kBlurR) * kRowS + (c + kBlurR);
+        const int sum = mul24u(k3, w[3 * kRowS]) + mul24u(k2, w[2 * kRowS] + w[4 * kRowS]) +
+                        mul24u(k1, w[kRowS] + w[5 * kRowS]) + mul24u(k0, w[0] + w[6 * kRowS]);
+        int qv = sum >> 16;
+        if (x + c < xs) {
+            const int rem = sum & 0xFFFF;
+            qv += (rem > 0x8000) | ((rem == 0x8000) & (qv & 1));
+        } else {
+            qv = (sum + (1 << 15)) >> 16;
+        }
+        return min(qv, 255);
+    };
     const int64_t kp_index = (int64_t)b * p.max_kps + off + i;
     uint64_t *dout = reinterpret_cast<uint64_t *>(fb.desc + kp_index * 32);
 #pragma unroll
@@ -957,7 +948,7 @@ __global__ __launch_bounds__(kThreads) void k_describe(DevPlan p, FrameBufs fb) 
             const float px = (float)c_pattern[2 * j + e][0], py = (float)c_pattern[2 * j + e][1];
             const int r = __float2int_rn(__fadd_rn(__fmul_rn(px, sa), __fmul_rn(py, ca)));
             const int cc = __float2int_rn(__fsub_rn(__fmul_rn(px, ca), __fmul_rn(py, sa)));
-            val[e] = bc[r * kBlurS + cc];
+            val[e] = blurred(r, cc);
         }
         const uint64_t m = __ballot(val[0] < val[1]);
         if (lane == 0) dout[grp] = m;

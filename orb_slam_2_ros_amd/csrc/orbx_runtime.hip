@@ -182,7 +182,7 @@ int upload_plan(orbx_extractor *ex) {
     d.fast_patch_stride = (mw + 6 + 3 + 3) & ~3;      // + alignment offset, dword rows
     d.fast_patch_bytes = (d.fast_patch_stride * (mh + 6) + 15) & ~15;
     d.fast_score_bytes = ((mw + 2) * (mh + 2) + 15) & ~15;
-    d.fast_lds_per_wave = d.fast_patch_bytes + 2 * d.fast_score_bytes + ((2 * mw * mh + 15) & ~15);
+    d.fast_lds_per_wave = d.fast_patch_bytes + d.fast_score_bytes + ((2 * mw * mh + 15) & ~15);
     if (mw > 255 || mh > 255) return ORBX_EINVAL;   // survivor list packs (y << 8 | x)
     if (4 * d.fast_lds_per_wave > 64 * 1024) return ORBX_EINVAL;
     d.node_lds_bytes = quadtree_lds_bytes(node_cap);

@@ -64,6 +64,27 @@ def test_stages_bit_exact(w, h, nfeat, seed, extractors, oracle_mod):
     assert np.array_equal(dg, do), f"descriptors differ at {_first_diff(dg, do)}"
 
 
+PARAM_VARIANTS = [
+    # (w, h, nfeatures, scale, nlevels, iniThFAST, minThFAST, seed)
+    (640, 480, 1000, 1.2, 8, 7, 20, 31),     # ini < min: corners found at the lower threshold
+    (640, 480, 1500, 1.2, 8, 12, 12, 32),    # equal thresholds
+    (752, 480, 800, 1.5, 6, 40, 3, 33),      # sparse ini pass, min fallback common
+    (512, 384, 2000, 1.1, 10, 0, 0, 34),     # threshold 0
+]
+
+
+@pytest.mark.parametrize("w,h,nfeat,scale,nlev,ini,mn,seed", PARAM_VARIANTS)
+def test_extract_parameter_variants(w, h, nfeat, scale, nlev, ini, mn, seed, extractors, oracle_mod):
+    img = synth.frame(w, h, seed)
+    ex = extractors(nfeat, scale, nlev, ini, mn)
+    kg, dg = ex(img)
+    ko, do = oracle_mod.extract(img, nfeat, scale, nlev, ini, mn)
+    assert len(kg) == len(ko)
+    for f in ko.dtype.names:
+        assert np.array_equal(kg[f], ko[f]), f"keypoint field {f} differs at {_first_diff(kg[f], ko[f])}"
+    assert np.array_equal(dg, do), f"descriptors differ at {_first_diff(dg, do)}"
+
+
 @pytest.mark.parametrize("w,h,nfeat,seed", CONFIGS[:4])
 def test_search_for_initialization(w, h, nfeat, seed, extractors, oracle_mod):
     fr = synth.frames(w, h, seed + 100, 2)
