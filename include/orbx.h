@@ -128,6 +128,51 @@ int orbx_extractor_stage_times(orbx_extractor *ex, float *ms, int cap);
 int orbx_extractor_debug_fetch(orbx_extractor *ex, int frame, int level, int what,
                                void *out, int64_t cap);
 
+/* ---- ORB_SLAM2::Frame depth: stereo and RGB-D ------------------------- */
+
+/* void Frame::ComputeStereoMatches()                      Frame.cc:502-676
+ * For the rectified pair last extracted by `left` and `right` (orbx_extract on
+ * each, or frame 0 of each one's current batch): kl/dl/nl are mvKeys /
+ * mDescriptors and kr/dr/nr mvKeysRight / mDescriptorsRight as those calls
+ * returned them; mbf and mb as the Frame holds them (maxD = mbf / mb).
+ * uright / depth (nl floats) receive mvuRight / mvDepth, -1 where there is no
+ * match; *nkept = the number of depths kept after the median cut.  Both
+ * extractors must share parameters and image size.  Synchronous.
+ * Where the reference has undefined behaviour or raises cv::Exception (a band
+ * row outside the image, an SAD window outside the level) the keypoint gets
+ * no match. */
+int orbx_compute_stereo_matches(orbx_extractor *left, orbx_extractor *right,
+                                const orbx_keypoint *kl, const uint8_t *dl, int nl,
+                                const orbx_keypoint *kr, const uint8_t *dr, int nr,
+                                float mbf, float mb, float *uright, float *depth, int *nkept);
+
+/* Stereo front-end step (config C3/C4 unit): frames 2p (left) and 2p+1
+ * (right) of d_images, p < pairs, are extracted, then ComputeStereoMatches
+ * runs for every pair on the device.  Needs max_batch >= 2 * pairs.
+ * Asynchronous on `stream`; results via orbx_depth_download. */
+int orbx_stereo_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t frame_stride,
+                            int pitch, int pairs, float mbf, float mb, void *stream);
+
+/* RGB-D front-end step: extract `batch` frames, then
+ * Frame::ComputeStereoFromRGBD (Frame.cc:679-701) against float32 depth maps
+ * (frame b at d_depth + b * depth_stride bytes, rows depth_pitch bytes apart;
+ * undistorted cameras, mvKeysUn == mvKeys).  Asynchronous. */
+int orbx_rgbd_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t frame_stride,
+                          int pitch, int batch, const float *d_depth, int64_t depth_stride,
+                          int depth_pitch, float mbf, void *stream);
+
+/* Host copy of the last stereo (index = pair) or RGB-D (index = frame) step:
+ * mvuRight / mvDepth of the left frame's n keypoints, and the kept count. */
+int orbx_depth_download(orbx_extractor *ex, int index, float *uright, float *depth, int cap,
+                        int *n, int *nkept);
+
+/* void Frame::ComputeStereoFromRGBD(const cv::Mat &imDepth) Frame.cc:679-701
+ * Host keypoints (mvKeys; mvKeysUn = kps_un, or kps when NULL) and CV_32F
+ * depth image in, mvuRight / mvDepth out; computed on `device`. */
+int orbx_stereo_from_rgbd(int device, const orbx_keypoint *kps, const orbx_keypoint *kps_un, int n,
+                          const float *depth_map, int width, int height, size_t pitch, float mbf,
+                          float *uright, float *depth, int *nkept);
+
 /* ---- ORB_SLAM2::ORBmatcher -------------------------------------------- */
 
 /* static int DescriptorDistance(const cv::Mat &a, const cv::Mat &b)

@@ -39,6 +39,8 @@ _SIG = {
     "orbo_distribute": (I32, [P, I32, I32, I32, I32, P]),
     "orbo_extract": (I32, [P, I32, I32, SZ, I32, F32, I32, I32, I32, P, P, I32, P]),
     "orbo_search_for_initialization": (I32, [P, P, I32, P, P, I32, I32, I32, P, P, I32, F32, I32]),
+    "orbo_compute_stereo_matches": (I32, [P, P, P, P, I32, P, P, P, P, I32, P, P, I32, F32, F32, P, P]),
+    "orbo_stereo_from_rgbd": (None, [P, P, I32, P, I32, I32, SZ, F32, P, P]),
 }
 
 _lib = None
@@ -168,3 +170,45 @@ def sincosf(a: float):
 def descriptor_distance(a, b) -> int:
     a = np.ascontiguousarray(a, np.uint8); b = np.ascontiguousarray(b, np.uint8)
     return int(lib().orbo_descriptor_distance(_p(a), _p(b)))
+
+
+def scale_tables(scale=1.2, nlevels=8):
+    """mvScaleFactor / mvInvScaleFactor (ORBextractor.cc:424-438): float
+    products computed in double (member scaleFactor is a double)."""
+    sf = np.zeros(nlevels, np.float32)
+    sf[0] = 1.0
+    for i in range(1, nlevels):
+        sf[i] = np.float32(float(sf[i - 1]) * float(np.float32(scale)))
+    inv = (np.float32(1.0) / sf).astype(np.float32)
+    return sf, inv
+
+
+def compute_stereo_matches(pyr_l, pyr_r, kl, dl, kr, dr, mbf, mb, scale=1.2):
+    """Frame::ComputeStereoMatches on oracle pyramids (lists of levels).
+    Returns (uright, depth, kept)."""
+    nlev = len(pyr_l)
+    lw = np.array([p.shape[1] for p in pyr_l], np.int32)
+    lh = np.array([p.shape[0] for p in pyr_l], np.int32)
+    bl = np.ascontiguousarray(np.concatenate([p.ravel() for p in pyr_l]))
+    br = np.ascontiguousarray(np.concatenate([p.ravel() for p in pyr_r]))
+    sf, inv = scale_tables(scale, nlev)
+    kl = np.ascontiguousarray(kl, KEYPOINT_DTYPE); kr = np.ascontiguousarray(kr, KEYPOINT_DTYPE)
+    dl = np.ascontiguousarray(dl, np.uint8); dr = np.ascontiguousarray(dr, np.uint8)
+    ur = np.zeros(max(len(kl), 1), np.float32)
+    dp = np.zeros(max(len(kl), 1), np.float32)
+    kept = lib().orbo_compute_stereo_matches(_p(bl), _p(br), _p(lw), _p(lh), nlev, _p(sf), _p(inv),
+                                             _p(kl), _p(dl), len(kl), _p(kr), _p(dr), len(kr),
+                                             mbf, mb, _p(ur), _p(dp))
+    return ur[:len(kl)].copy(), dp[:len(kl)].copy(), kept
+
+
+def stereo_from_rgbd(kps, dmap, mbf, kps_un=None):
+    """Frame::ComputeStereoFromRGBD; dmap is float32 (h, w)."""
+    kps = np.ascontiguousarray(kps, KEYPOINT_DTYPE)
+    kun = kps if kps_un is None else np.ascontiguousarray(kps_un, KEYPOINT_DTYPE)
+    dmap = np.ascontiguousarray(dmap, np.float32)
+    ur = np.zeros(max(len(kps), 1), np.float32)
+    dp = np.zeros(max(len(kps), 1), np.float32)
+    lib().orbo_stereo_from_rgbd(_p(kps), _p(kun), len(kps), _p(dmap), dmap.shape[1], dmap.shape[0],
+                                dmap.strides[0], mbf, _p(ur), _p(dp))
+    return ur[:len(kps)].copy(), dp[:len(kps)].copy()

@@ -768,3 +768,124 @@ int orbo_search_for_initialization(const orbo_keypoint *k1, const uint8_t *d1, i
 }
 
 }  // extern "C"
+
+// Frame::ComputeStereoMatches (Frame.cc:502-676).  Row table Frame.cc:512-529,
+// band search :540-585, SAD window + parabola :587-660, median cut :662-675.
+// Where the reference has undefined behaviour or raises cv::Exception (row
+// table or row index out of range; an SAD window outside the level, which
+// Mat::rowRange/colRange assert on) this restatement reports "no match" for
+// that keypoint; the product kernel does the same.
+int orbo_compute_stereo_matches(const uint8_t *pyrL, const uint8_t *pyrR, const int *lw, const int *lh,
+                                int nlevels, const float *scale, const float *inv_scale,
+                                const orbo_keypoint *kl, const uint8_t *dl, int nl,
+                                const orbo_keypoint *kr, const uint8_t *dr, int nr,
+                                float mbf, float mb, float *uright, float *depth) {
+    std::vector<size_t> off(nlevels + 1, 0);
+    for (int l = 0; l < nlevels; ++l) off[l + 1] = off[l] + (size_t)lw[l] * lh[l];
+    for (int i = 0; i < nl; ++i) { uright[i] = -1.0f; depth[i] = -1.0f; }
+    const int TH_HIGH = 100, TH_LOW = 50, thOrbDist = (TH_HIGH + TH_LOW) / 2;
+    const int nRows = lh[0];
+    std::vector<std::vector<int>> rows(nRows);
+    for (int iR = 0; iR < nr; ++iR) {
+        const float y = kr[iR].y;
+        const float r = 2.0f * scale[kr[iR].octave];
+        const int maxr = (int)std::ceil(y + r), minr = (int)std::floor(y - r);
+        for (int yi = minr; yi <= maxr; ++yi)
+            if (yi >= 0 && yi < nRows) rows[yi].push_back(iR);
+    }
+    const float minZ = mb, minD = 0.f, maxD = mbf / minZ;
+    std::vector<std::pair<int, int>> distIdx;
+    for (int iL = 0; iL < nl; ++iL) {
+        const orbo_keypoint &kL = kl[iL];
+        const int levelL = kL.octave;
+        const float vL = kL.y, uL = kL.x;
+        if (!(vL >= 0.f) || vL >= (float)nRows) continue;
+        const std::vector<int> &cands = rows[(size_t)vL];
+        if (cands.empty()) continue;
+        const float minU = uL - maxD, maxU = uL - minD;
+        if (maxU < 0) continue;
+        int bestDist = TH_HIGH;
+        int bestIdxR = 0;
+        for (int iR : cands) {
+            if (kr[iR].octave < levelL - 1 || kr[iR].octave > levelL + 1) continue;
+            const float uR = kr[iR].x;
+            if (uR >= minU && uR <= maxU) {
+                const int dist = hamming32(dl + 32 * (size_t)iL, dr + 32 * (size_t)iR);
+                if (dist < bestDist) { bestDist = dist; bestIdxR = iR; }
+            }
+        }
+        if (bestDist >= thOrbDist) continue;
+        const float uR0 = kr[bestIdxR].x;
+        const float sf = inv_scale[levelL];
+        const float suL = std::round(uL * sf), svL = std::round(vL * sf), suR0 = std::round(uR0 * sf);
+        const int W = 5, L = 5;
+        const int cols = lw[levelL], nrows = lh[levelL];
+        const int r0 = (int)(svL - W), cL0 = (int)(suL - W);
+        if (svL - W < 0 || svL + W + 1 > nrows || suL - W < 0 || suL + W + 1 > cols) continue;  // cv assert
+        const float iniu = suR0 + L - W, endu = suR0 + L + W + 1;
+        if (iniu < 0 || endu >= cols) continue;
+        if (suR0 - L - W < 0) continue;                                                        // cv assert
+        const uint8_t *IL = pyrL + off[levelL], *IR = pyrR + off[levelL];
+        const int cR0 = (int)suR0;
+        const float cl = (float)IL[(size_t)(r0 + W) * cols + cL0 + W];
+        int bestSad = INT_MAX, bestInc = 0;
+        float dists[2 * L + 1];
+        for (int inc = -L; inc <= L; ++inc) {
+            const int c0 = cR0 + inc - W;
+            const float cr = (float)IR[(size_t)(r0 + W) * cols + c0 + W];
+            double acc = 0;   // cv::norm(NORM_L1) of CV_32F accumulates in double
+            for (int r = 0; r < 2 * W + 1; ++r)
+                for (int c = 0; c < 2 * W + 1; ++c) {
+                    const float a = (float)IL[(size_t)(r0 + r) * cols + cL0 + c] - cl;
+                    const float b = (float)IR[(size_t)(r0 + r) * cols + c0 + c] - cr;
+                    acc += std::fabs((double)a - (double)b);
+                }
+            const float dist = (float)acc;
+            if (dist < (float)bestSad) { bestSad = (int)dist; bestInc = inc; }
+            dists[L + inc] = dist;
+        }
+        if (bestInc == -L || bestInc == L) continue;
+        const float d1 = dists[L + bestInc - 1], d2 = dists[L + bestInc], d3 = dists[L + bestInc + 1];
+        const float deltaR = (d1 - d3) / (2.0f * (d1 + d3 - 2.0f * d2));
+        if (deltaR < -1 || deltaR > 1) continue;
+        float bestuR = scale[levelL] * ((float)suR0 + (float)bestInc + deltaR);
+        float disparity = uL - bestuR;
+        if (disparity >= minD && disparity < maxD) {
+            if (disparity <= 0) {
+                disparity = 0.01;
+                bestuR = uL - 0.01;
+            }
+            depth[iL] = mbf / disparity;
+            uright[iL] = bestuR;
+            distIdx.push_back(std::make_pair(bestSad, iL));
+        }
+    }
+    if (distIdx.empty()) return 0;   // the reference reads distIdx[0] of an empty vector here
+    std::sort(distIdx.begin(), distIdx.end());
+    const float median = (float)distIdx[distIdx.size() / 2].first;
+    const float thDist = 1.5f * 1.4f * median;
+    int kept = (int)distIdx.size();
+    for (int i = (int)distIdx.size() - 1; i >= 0; --i) {
+        if ((float)distIdx[i].first < thDist) break;
+        uright[distIdx[i].second] = -1;
+        depth[distIdx[i].second] = -1;
+        --kept;
+    }
+    return kept;
+}
+
+// Frame::ComputeStereoFromRGBD (Frame.cc:679-701): depth looked up at the
+// (truncated) distorted keypoint, uRight from the undistorted one.
+void orbo_stereo_from_rgbd(const orbo_keypoint *kps, const orbo_keypoint *kps_un, int n, const float *dmap,
+                           int w, int h, size_t pitch_bytes, float mbf, float *uright, float *depth) {
+    for (int i = 0; i < n; ++i) {
+        uright[i] = -1; depth[i] = -1;
+        const int v = (int)kps[i].y, u = (int)kps[i].x;
+        if (v < 0 || v >= h || u < 0 || u >= w) continue;   // reference: unchecked Mat::at
+        const float d = *(const float *)((const uint8_t *)dmap + (size_t)v * pitch_bytes + 4 * (size_t)u);
+        if (d > 0) {
+            depth[i] = d;
+            uright[i] = kps_un[i].x - mbf / d;
+        }
+    }
+}

@@ -84,6 +84,20 @@ int   orbo_search_for_initialization(const orbo_keypoint *k1, const uint8_t *d1,
                                      float *prev_xy, int32_t *matches12,
                                      int window, float nnratio, int check_ori);
 
+/* ---- stereo (Frame::ComputeStereoMatches, Frame.cc:502-676) ----
+ * pyrL / pyrR: all levels packed as orbo_pyramid writes them, level sizes
+ * lw/lh; scale / inv_scale = mvScaleFactors / mvInvScaleFactors.  uright and
+ * depth (nl floats) receive mvuRight / mvDepth.  Returns the count kept. */
+int   orbo_compute_stereo_matches(const uint8_t *pyrL, const uint8_t *pyrR, const int *lw, const int *lh,
+                                  int nlevels, const float *scale, const float *inv_scale,
+                                  const orbo_keypoint *kl, const uint8_t *dl, int nl,
+                                  const orbo_keypoint *kr, const uint8_t *dr, int nr,
+                                  float mbf, float mb, float *uright, float *depth);
+/* Frame::ComputeStereoFromRGBD (Frame.cc:679-701); dmap is CV_32F. */
+void  orbo_stereo_from_rgbd(const orbo_keypoint *kps, const orbo_keypoint *kps_un, int n,
+                            const float *dmap, int w, int h, size_t pitch_bytes, float mbf,
+                            float *uright, float *depth);
+
 #ifdef __cplusplus
 }
 #endif

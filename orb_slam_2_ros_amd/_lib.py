@@ -65,6 +65,11 @@ _SIGNATURES = {
     "orbx_extractor_set_profiling": (I32, [P, I32]),
     "orbx_extractor_stage_times": (I32, [P, P, I32]),
     "orbx_extractor_debug_fetch": (I32, [P, I32, I32, I32, P, I64]),
+    "orbx_compute_stereo_matches": (I32, [P, P, P, P, I32, P, P, I32, F32, F32, P, P, P]),
+    "orbx_stereo_step_device": (I32, [P, P, I64, I32, I32, F32, F32, P]),
+    "orbx_rgbd_step_device": (I32, [P, P, I64, I32, I32, P, I64, I32, F32, P]),
+    "orbx_depth_download": (I32, [P, I32, P, P, I32, P, P]),
+    "orbx_stereo_from_rgbd": (I32, [I32, P, P, I32, P, I32, I32, SZ, F32, P, P, P]),
     "orbx_descriptor_distance": (I32, [P, P]),
     "orbx_search_for_initialization": (I32, [I32, P, P, I32, P, P, I32, I32, I32, P, P, I32, F32, I32, P]),
     "orbx_debug_trig": (I32, [I32, P, P, P, I32, P, P, P, I32]),

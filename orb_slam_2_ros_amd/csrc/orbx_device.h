@@ -64,6 +64,28 @@ struct MatchBufs {
     int reset_prev;           // 1: prev_xy := F1 keypoint positions before matching
 };
 
+// Where a frame's pyramid lives: level 0 is the caller's image, levels >= 1
+// are in the extractor's pyramid block (frame f at pyr + f * pyr_bytes).
+struct PyrView {
+    const uint8_t *img0; int64_t img0_stride; int img0_pitch;
+    const uint8_t *pyr; int64_t pyr_bytes;
+};
+
+// Stereo matching of a batch of rectified pairs (Frame::ComputeStereoMatches).
+// Pair b: left frame left_f0 + b*fstep of `left`, right frame right_f0 + b*fstep
+// of `right`; keypoints kl/kr + b*kstride (descriptors likewise, 32 B each),
+// counts nl/nr[b*nstride]; outputs ur/depth/sad + b*ostride, nkept[b].
+struct StereoBufs {
+    const LevelGeom *lv; int nlevels; int rows;   // rows: level-0 height (nRows)
+    PyrView left, right; int left_f0, right_f0, fstep;
+    const orbx_keypoint *kl; const uint8_t *dl; const int32_t *nl;
+    const orbx_keypoint *kr; const uint8_t *dr; const int32_t *nr;
+    int64_t kstride; int64_t nstride;
+    int nr_cap;               // right keypoints indexed per pair (LDS capacity)
+    float mbf, maxd;          // maxD = mbf / mb (Frame.cc:532-534)
+    float *ur, *depth; int32_t *sad; int64_t ostride; int32_t *nkept;
+};
+
 enum Stage { kStageResize = 0, kStageBlur, kStageFast, kStageQuadtree, kStageDescribe, kStageMatch, kNumStages };
 
 hipError_t launch_resize(const DevPlan &p, const Plan &hp, const FrameBufs &fb, int B, hipStream_t s);
@@ -76,6 +98,11 @@ hipError_t launch_match(const MatchBufs &mb, int B, int n1cap, int n2cap, int ma
 // (exhaustive-check hook used by the GPU tests).
 hipError_t launch_trig_check(const float *in, float *s, float *c, float *atan_out,
                              const float *ay, const float *ax, int n, int m, hipStream_t st);
+hipError_t launch_stereo(const StereoBufs &a, int pairs, int nl_cap, hipStream_t s);
+int stereo_lds_bytes(int rows, int nr_cap);
+hipError_t launch_rgbd(const orbx_keypoint *kps, const orbx_keypoint *kun, const int32_t *nkps, int64_t kstride,
+                       int kcap, const float *dmap, int64_t dstride, int dpitch, int w, int h, float mbf, float *ur,
+                       float *depth, int64_t ostride, int32_t *nkept, int B, hipStream_t s);
 int match_lds_bytes(int n1cap, int n2cap, int maxq, int maxc);
 int quadtree_lds_bytes(int node_cap);
 bool resize_window_fits(const Plan &hp);

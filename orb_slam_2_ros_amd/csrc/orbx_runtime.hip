@@ -82,6 +82,12 @@ struct orbx_extractor {
     int match_batch = 0;
     int l0cap = 0;
 
+    // depth results of the last stereo / RGB-D step (per pair or per frame)
+    float *d_ur = nullptr, *d_depth = nullptr;
+    int32_t *d_sad = nullptr, *d_nkept = nullptr;
+    int depth_mode = 0;         // 0 none, 1 stereo (index = pair), 2 RGB-D (index = frame)
+    int depth_count = 0;
+
     uint8_t *d_img = nullptr;   // staging for the host API
     size_t d_img_bytes = 0;
 
@@ -113,6 +119,9 @@ struct orbx_extractor {
         dfree(d_cell_count); dfree(d_level_count); dfree(d_key_node); dfree(d_key_q);
         for (auto &s : slot) { dfree(s.kps); dfree(s.desc); dfree(s.nkps); s.batch = 0; }
         dfree(d_prev); dfree(d_m12); dfree(d_nmatch); dfree(d_scratch); dfree(d_img);
+        dfree(d_ur); dfree(d_depth); dfree(d_sad); dfree(d_nkept);
+        depth_mode = 0;
+        depth_count = 0;
         d_img_bytes = 0;
         planned = false;
         max_batch = 0;
@@ -233,6 +242,10 @@ int reserve(orbx_extractor *ex, int w, int h, int max_batch) {
     ok &= dalloc(&ex->d_m12, B * p.max_kps) == hipSuccess;
     ok &= dalloc(&ex->d_nmatch, B) == hipSuccess;
     ok &= dalloc(&ex->d_scratch, B * (size_t)ex->scratch_stride) == hipSuccess;
+    ok &= dalloc(&ex->d_ur, B * p.max_kps) == hipSuccess;
+    ok &= dalloc(&ex->d_depth, B * p.max_kps) == hipSuccess;
+    ok &= dalloc(&ex->d_sad, B * p.max_kps) == hipSuccess;
+    ok &= dalloc(&ex->d_nkept, B) == hipSuccess;
     if (!ok) { ex->release(); return ORBX_ENOMEM; }
     ex->planned = true;
     ex->max_batch = max_batch;
@@ -260,6 +273,20 @@ FrameBufs frame_bufs(orbx_extractor *ex, int slot) {
     fb.desc = s.desc;
     fb.nkps = s.nkps;
     return fb;
+}
+
+PyrView pyr_view(const orbx_extractor *ex, int slot) {
+    const auto &s = ex->slot[slot];
+    return PyrView{s.img0, s.img0_stride, s.img0_pitch, ex->d_pyr, ex->plan.pyr_bytes};
+}
+
+bool same_geometry(const Plan &a, const Plan &b) {
+    if (a.width != b.width || a.height != b.height || a.nlevels != b.nlevels) return false;
+    for (int l = 0; l < a.nlevels; ++l)
+        if (a.lv[l].w != b.lv[l].w || a.lv[l].h != b.lv[l].h || a.lv[l].scale != b.lv[l].scale ||
+            a.lv[l].inv_scale != b.lv[l].inv_scale)
+            return false;
+    return true;
 }
 
 void fold(orbx_extractor *ex, int set) {
@@ -684,6 +711,179 @@ int orbx_extractor_stage_times(orbx_extractor *ex, float *ms, int cap) {
         ++nw;
     }
     return nw;
+}
+
+int orbx_compute_stereo_matches(orbx_extractor *left, orbx_extractor *right, const orbx_keypoint *kl,
+                                const uint8_t *dl, int nl, const orbx_keypoint *kr, const uint8_t *dr, int nr,
+                                float mbf, float mb, float *uright, float *depth, int *nkept) {
+    if (!left || !right || !left->planned || !right->planned || !nkept) return ORBX_EINVAL;
+    if (nl < 0 || nr < 0 || nr > 65535 || (nl && (!kl || !dl || !uright || !depth)) || (nr && (!kr || !dr)))
+        return ORBX_EINVAL;
+    if (left->device != right->device || !same_geometry(left->plan, right->plan)) return ORBX_EINVAL;
+    if (left->slot[left->cur].batch <= 0 || right->slot[right->cur].batch <= 0) return ORBX_EINVAL;
+    *nkept = 0;
+    if (nl == 0) return ORBX_OK;
+    const int rows = left->plan.height;
+    const int ncap = std::max(nr, 1);
+    if (stereo_lds_bytes(rows, ncap) > 160 * 1024) return ORBX_EINVAL;
+    if (hipSetDevice(left->device) != hipSuccess) return ORBX_ENODEV;
+    if (hipStreamSynchronize(right->stream) != hipSuccess || hipStreamSynchronize(left->stream) != hipSuccess)
+        return ORBX_EIO;
+    orbx_keypoint *dkl = nullptr, *dkr = nullptr;
+    uint8_t *ddl = nullptr, *ddr = nullptr;
+    int32_t *dn = nullptr, *dsad = nullptr, *dnk = nullptr;
+    float *dur = nullptr, *ddp = nullptr;
+    int rc = ORBX_OK;
+    const bool ok = dalloc(&dkl, nl) == hipSuccess && dalloc(&dkr, ncap) == hipSuccess &&
+                    dalloc(&ddl, 32 * (size_t)nl) == hipSuccess && dalloc(&ddr, 32 * (size_t)ncap) == hipSuccess &&
+                    dalloc(&dn, 2) == hipSuccess && dalloc(&dsad, nl) == hipSuccess && dalloc(&dnk, 1) == hipSuccess &&
+                    dalloc(&dur, nl) == hipSuccess && dalloc(&ddp, nl) == hipSuccess;
+    if (!ok) rc = ORBX_ENOMEM;
+    const int32_t ns[2] = {nl, nr};
+    if (!rc && (hipMemcpy(dkl, kl, sizeof(orbx_keypoint) * nl, hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(ddl, dl, 32 * (size_t)nl, hipMemcpyHostToDevice) != hipSuccess ||
+                (nr && hipMemcpy(dkr, kr, sizeof(orbx_keypoint) * nr, hipMemcpyHostToDevice) != hipSuccess) ||
+                (nr && hipMemcpy(ddr, dr, 32 * (size_t)nr, hipMemcpyHostToDevice) != hipSuccess) ||
+                hipMemcpy(dn, ns, sizeof(ns), hipMemcpyHostToDevice) != hipSuccess))
+        rc = ORBX_EIO;
+    if (!rc) {
+        StereoBufs a{};
+        a.lv = left->dp.lv; a.nlevels = left->nlevels; a.rows = rows;
+        a.left = pyr_view(left, left->cur); a.right = pyr_view(right, right->cur);
+        a.left_f0 = 0; a.right_f0 = 0; a.fstep = 0;
+        a.kl = dkl; a.dl = ddl; a.nl = dn; a.kr = dkr; a.dr = ddr; a.nr = dn + 1;
+        a.kstride = 0; a.nstride = 0; a.nr_cap = ncap;
+        a.mbf = mbf; a.maxd = mbf / mb;
+        a.ur = dur; a.depth = ddp; a.sad = dsad; a.ostride = 0; a.nkept = dnk;
+        if (launch_stereo(a, 1, nl, left->stream) != hipSuccess || hipStreamSynchronize(left->stream) != hipSuccess)
+            rc = ORBX_EIO;
+    }
+    if (!rc && (hipMemcpy(uright, dur, 4 * (size_t)nl, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(depth, ddp, 4 * (size_t)nl, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(nkept, dnk, sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess))
+        rc = ORBX_EIO;
+    dfree(dkl); dfree(dkr); dfree(ddl); dfree(ddr); dfree(dn); dfree(dsad); dfree(dnk); dfree(dur); dfree(ddp);
+    return rc;
+}
+
+int orbx_stereo_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t frame_stride, int pitch, int pairs,
+                            float mbf, float mb, void *stream) {
+    if (pairs <= 0) return ORBX_EINVAL;
+    int rc = validate_batch(ex, d_images, pitch, 2 * pairs);
+    if (rc) return rc;
+    const int kcap = ex->plan.max_kps;
+    if (kcap > 65535 || stereo_lds_bytes(ex->plan.height, kcap) > 160 * 1024) return ORBX_EINVAL;
+    if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
+    hipStream_t st = stream_of(ex, stream);
+    rc = align_level0(ex, &d_images, &frame_stride, &pitch, 2 * pairs, st);
+    if (rc) return rc;
+    const int next = ex->cur ^ 1;
+    prof_begin(ex);
+    rc = run_extract(ex, next, d_images, frame_stride, pitch, 2 * pairs, st);
+    if (rc) return rc;
+    ex->cur = next;
+    ++ex->steps;
+    ex->match_batch = 0;
+    const auto &s = ex->slot[next];
+    StereoBufs a{};
+    a.lv = ex->dp.lv; a.nlevels = ex->nlevels; a.rows = ex->plan.height;
+    a.left = a.right = pyr_view(ex, next);
+    a.left_f0 = 0; a.right_f0 = 1; a.fstep = 2;
+    a.kl = s.kps; a.dl = s.desc; a.nl = s.nkps;
+    a.kr = s.kps + kcap; a.dr = s.desc + (size_t)kcap * 32; a.nr = s.nkps + 1;
+    a.kstride = 2 * (int64_t)kcap; a.nstride = 2; a.nr_cap = kcap;
+    a.mbf = mbf; a.maxd = mbf / mb;
+    a.ur = ex->d_ur; a.depth = ex->d_depth; a.sad = ex->d_sad; a.ostride = kcap; a.nkept = ex->d_nkept;
+    if (launch_stereo(a, pairs, kcap, st) != hipSuccess) return ORBX_EIO;
+    mark(ex, kNumStages, st);
+    mark_valid(ex, kStageMatch);
+    ex->depth_mode = 1;
+    ex->depth_count = pairs;
+    return ORBX_OK;
+}
+
+int orbx_rgbd_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t frame_stride, int pitch, int batch,
+                          const float *d_depth, int64_t depth_stride, int depth_pitch, float mbf, void *stream) {
+    int rc = validate_batch(ex, d_images, pitch, batch);
+    if (rc) return rc;
+    if (!d_depth || depth_pitch < 4 * ex->plan.width || (depth_pitch & 3) || (depth_stride & 3) ||
+        (reinterpret_cast<uintptr_t>(d_depth) & 3))
+        return ORBX_EINVAL;
+    if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
+    hipStream_t st = stream_of(ex, stream);
+    rc = align_level0(ex, &d_images, &frame_stride, &pitch, batch, st);
+    if (rc) return rc;
+    const int next = ex->cur ^ 1;
+    prof_begin(ex);
+    rc = run_extract(ex, next, d_images, frame_stride, pitch, batch, st);
+    if (rc) return rc;
+    ex->cur = next;
+    ++ex->steps;
+    ex->match_batch = 0;
+    const auto &s = ex->slot[next];
+    const int kcap = ex->plan.max_kps;
+    if (launch_rgbd(s.kps, nullptr, s.nkps, kcap, kcap, d_depth, depth_stride, depth_pitch, ex->plan.width,
+                    ex->plan.height, mbf, ex->d_ur, ex->d_depth, kcap, ex->d_nkept, batch, st) != hipSuccess)
+        return ORBX_EIO;
+    mark(ex, kNumStages, st);
+    mark_valid(ex, kStageMatch);
+    ex->depth_mode = 2;
+    ex->depth_count = batch;
+    return ORBX_OK;
+}
+
+int orbx_depth_download(orbx_extractor *ex, int index, float *uright, float *depth, int cap, int *n, int *nkept) {
+    if (!ex || !ex->planned || !n || ex->depth_mode == 0 || index < 0 || index >= ex->depth_count) return ORBX_EINVAL;
+    if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
+    if (hipDeviceSynchronize() != hipSuccess) return ORBX_EIO;
+    const int frame = ex->depth_mode == 1 ? 2 * index : index;
+    int32_t cnt = 0, nk = 0;
+    if (hipMemcpy(&cnt, ex->slot[ex->cur].nkps + frame, sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(&nk, ex->d_nkept + index, sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
+        return ORBX_EIO;
+    *n = cnt;
+    if (nkept) *nkept = nk;
+    if (cnt > cap) return ORBX_ERANGE;
+    const size_t base = (size_t)index * ex->plan.max_kps;
+    if (cnt > 0 && uright && hipMemcpy(uright, ex->d_ur + base, 4 * (size_t)cnt, hipMemcpyDeviceToHost) != hipSuccess)
+        return ORBX_EIO;
+    if (cnt > 0 && depth && hipMemcpy(depth, ex->d_depth + base, 4 * (size_t)cnt, hipMemcpyDeviceToHost) != hipSuccess)
+        return ORBX_EIO;
+    return ORBX_OK;
+}
+
+int orbx_stereo_from_rgbd(int device, const orbx_keypoint *kps, const orbx_keypoint *kps_un, int n,
+                          const float *depth_map, int width, int height, size_t pitch, float mbf, float *uright,
+                          float *depth, int *nkept) {
+    if (n < 0 || width <= 0 || height <= 0 || pitch < 4 * (size_t)width || (pitch & 3) || !depth_map || !nkept)
+        return ORBX_EINVAL;
+    if (n && (!kps || !uright || !depth)) return ORBX_EINVAL;
+    *nkept = 0;
+    if (n == 0) return ORBX_OK;
+    if (hipSetDevice(device) != hipSuccess) return ORBX_ENODEV;
+    orbx_keypoint *dk = nullptr, *dku = nullptr;
+    float *dmap = nullptr, *dur = nullptr, *ddp = nullptr;
+    int32_t *dn = nullptr, *dnk = nullptr;
+    int rc = ORBX_OK;
+    const bool ok = dalloc(&dk, n) == hipSuccess && dalloc(&dku, n) == hipSuccess &&
+                    dalloc(&dmap, (pitch / 4) * (size_t)height) == hipSuccess && dalloc(&dur, n) == hipSuccess &&
+                    dalloc(&ddp, n) == hipSuccess && dalloc(&dn, 1) == hipSuccess && dalloc(&dnk, 1) == hipSuccess;
+    if (!ok) rc = ORBX_ENOMEM;
+    if (!rc && (hipMemcpy(dk, kps, sizeof(orbx_keypoint) * n, hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(dku, kps_un ? kps_un : kps, sizeof(orbx_keypoint) * n, hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(dmap, depth_map, pitch * (size_t)height, hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(dn, &n, sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess))
+        rc = ORBX_EIO;
+    if (!rc && (launch_rgbd(dk, dku, dn, n, n, dmap, 0, (int)pitch, width, height, mbf, dur, ddp, n, dnk, 1,
+                            nullptr) != hipSuccess ||
+                hipDeviceSynchronize() != hipSuccess))
+        rc = ORBX_EIO;
+    if (!rc && (hipMemcpy(uright, dur, 4 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(depth, ddp, 4 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(nkept, dnk, sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess))
+        rc = ORBX_EIO;
+    dfree(dk); dfree(dku); dfree(dmap); dfree(dur); dfree(ddp); dfree(dn); dfree(dnk);
+    return rc;
 }
 
 int orbx_descriptor_distance(const uint8_t *a, const uint8_t *b) {

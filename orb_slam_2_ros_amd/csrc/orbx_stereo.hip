@@ -1,0 +1,386 @@
+// orbx_stereo.hip -- depth for stereo and RGB-D frames, per keypoint:
+//
+//   k_stereo_band    Frame::ComputeStereoMatches (Frame.cc:502-660): row-band
+//                    Hamming search over the right keypoints, 11x11 SAD over 11
+//                    offsets on the unblurred pyramid level, parabola fit.
+//   k_stereo_cut     the median cut of Frame.cc:662-675.
+//   k_rgbd_depth     Frame::ComputeStereoFromRGBD (Frame.cc:679-701).
+//
+// One block of k_stereo_band covers 256 left keypoints of one stereo pair.  It
+// first counting-sorts the pair's right keypoints by the first row of their
+// band (vRowIndices of Frame.cc:512-529 without the per-row copies) into LDS,
+// then every thread walks the bands that can contain its keypoint's row.  The
+// reference keeps the first strictly smaller distance in candidate (= right
+// index) order, i.e. the lexicographic minimum of (distance, index), which is
+// what the walk computes in any order.
+#include <hip/hip_runtime.h>
+
+#include "orbx_device.h"
+
+namespace orbx {
+namespace {
+
+constexpr int kST = 256;
+constexpr int kThOrbDist = (100 + 50) / 2;   // (TH_HIGH + TH_LOW) / 2, Frame.cc:507
+constexpr int kSadW = 5, kSadL = 5;          // Frame.cc:597, 607
+
+__device__ inline const uint8_t *view_level(const PyrView &v, const LevelGeom &g, int l, int f, int &pitch) {
+    if (l == 0) {
+        pitch = v.img0_pitch;
+        return v.img0 + (int64_t)f * v.img0_stride;
+    }
+    pitch = g.pitch;
+    return v.pyr + (int64_t)f * v.pyr_bytes + g.pyr_off;
+}
+
+__device__ inline int hamming(const uint32_t a[8], const uint8_t *d) {
+    const uint4 q0 = *reinterpret_cast<const uint4 *>(d);
+    const uint4 q1 = *reinterpret_cast<const uint4 *>(d + 16);
+    return __popc(a[0] ^ q0.x) + __popc(a[1] ^ q0.y) + __popc(a[2] ^ q0.z) + __popc(a[3] ^ q0.w) +
+           __popc(a[4] ^ q1.x) + __popc(a[5] ^ q1.y) + __popc(a[6] ^ q1.z) + __popc(a[7] ^ q1.w);
+}
+
+// In-place exclusive scan of n ints in LDS by the whole block; returns the total.
+__device__ int block_scan_lds(int *a, int n, int *ws) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int per = (n + kST - 1) / kST;
+    const int lo = min(n, tid * per), hi = min(n, lo + per);
+    int s = 0;
+    for (int i = lo; i < hi; ++i) s += a[i];
+    int incl = s;
+    for (int d = 1; d < 64; d <<= 1) {
+        const int t = __shfl_up(incl, d);
+        if (lane >= d) incl += t;
+    }
+    if (lane == 63) ws[wv] = incl;
+    __syncthreads();
+    int base = 0;
+    for (int w = 0; w < wv; ++w) base += ws[w];
+    const int total = ws[0] + ws[1] + ws[2] + ws[3];
+    int run = base + incl - s;
+    for (int i = lo; i < hi; ++i) {
+        const int v = a[i];
+        a[i] = run;
+        run += v;
+    }
+    __syncthreads();
+    return total;
+}
+
+// Bytes [o, o + 4*N) of the dwords d[] as N dwords (v_alignbyte).
+template <int N>
+__device__ inline void realign(const uint32_t *d, uint32_t o, uint32_t *e) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) e[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], o);
+}
+
+__device__ inline int byte_of(const uint32_t *e, int j) { return (e[j >> 2] >> (8 * (j & 3))) & 0xFF; }
+
+// Left row (11 px from column c0) and right row (21 px from column c0r) of
+// one SAD window row, from dword-aligned loads.
+__device__ inline void load_rows(const uint8_t *lrow, int c0, const uint8_t *rrow, int c0r, int l[11], int r[21]) {
+    {
+        const uint32_t o = (uint32_t)(reinterpret_cast<uintptr_t>(lrow + c0) & 3);
+        const uint32_t *p = reinterpret_cast<const uint32_t *>(lrow + c0 - o);
+        uint32_t d[4], e[3];
+        d[0] = p[0]; d[1] = p[1]; d[2] = p[2];
+        d[3] = o >= 2 ? p[3] : 0u;   // byte o + 10 lies in dword 3 only then
+        realign<3>(d, o, e);
+#pragma unroll
+        for (int j = 0; j < 11; ++j) l[j] = byte_of(e, j);
+    }
+    {
+        const uint32_t o = (uint32_t)(reinterpret_cast<uintptr_t>(rrow + c0r) & 3);
+        const uint32_t *p = reinterpret_cast<const uint32_t *>(rrow + c0r - o);
+        uint32_t d[7], e[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) d[k] = p[k];
+        d[6] = 0u;                   // byte o + 20 always lies in dword 5
+        realign<6>(d, o, e);
+#pragma unroll
+        for (int j = 0; j < 21; ++j) r[j] = byte_of(e, j);
+    }
+}
+
+__global__ __launch_bounds__(kST) void k_stereo_band(StereoBufs a) {
+    extern __shared__ __align__(16) uint8_t lds[];
+    __shared__ int ws[4];
+    __shared__ int s_span;
+    const int b = blockIdx.y, tid = threadIdx.x;
+    const int nl = a.nl[(int64_t)b * a.nstride];
+    const int i0 = blockIdx.x * kST;
+    if (i0 >= nl) return;
+    const int nr = min(a.nr[(int64_t)b * a.nstride], a.nr_cap);
+    const int H = a.rows;
+    const orbx_keypoint *kl = a.kl + (int64_t)b * a.kstride;
+    const orbx_keypoint *kr = a.kr + (int64_t)b * a.kstride;
+    const uint8_t *dl = a.dl + (int64_t)b * a.kstride * 32;
+    const uint8_t *dr = a.dr + (int64_t)b * a.kstride * 32;
+
+    int *rend = reinterpret_cast<int *>(lds);                       // H + 1 counters / bucket ends
+    float *sx = reinterpret_cast<float *>(rend + H + 1);            // right u, by band order
+    int16_t *smaxr = reinterpret_cast<int16_t *>(sx + a.nr_cap);    // last row of the band
+    uint16_t *sidx = reinterpret_cast<uint16_t *>(smaxr + a.nr_cap);
+    int8_t *soct = reinterpret_cast<int8_t *>(sidx + a.nr_cap);
+
+    // 1. vRowIndices (Frame.cc:517-529): right keypoint iR lies in rows
+    //    [floor(y - r), ceil(y + r)], r = 2 * scale[octave].  Rows outside the
+    //    image (undefined behaviour in the reference) are dropped.
+    for (int i = tid; i <= H; i += kST) rend[i] = 0;
+    if (tid == 0) s_span = 0;
+    __syncthreads();
+    int span = 0;
+    for (int iR = tid; iR < nr; iR += kST) {
+        const orbx_keypoint k = kr[iR];
+        if (k.octave < 0 || k.octave >= a.nlevels) continue;
+        const float r = __fmul_rn(2.0f, a.lv[k.octave].scale);
+        const int maxr = (int)ceilf(__fadd_rn(k.y, r)), minr = (int)floorf(__fsub_rn(k.y, r));
+        const int lo = max(minr, 0), hi = min(maxr, H - 1);
+        if (lo > hi) continue;
+        atomicAdd(&rend[lo], 1);
+        span = max(span, hi - lo);
+    }
+    atomicMax(&s_span, span);
+    __syncthreads();
+    block_scan_lds(rend, H + 1, ws);
+    for (int iR = tid; iR < nr; iR += kST) {
+        const orbx_keypoint k = kr[iR];
+        if (k.octave < 0 || k.octave >= a.nlevels) continue;
+        const float r = __fmul_rn(2.0f, a.lv[k.octave].scale);
+        const int maxr = (int)ceilf(__fadd_rn(k.y, r)), minr = (int)floorf(__fsub_rn(k.y, r));
+        const int lo = max(minr, 0), hi = min(maxr, H - 1);
+        if (lo > hi) continue;
+        const int pos = atomicAdd(&rend[lo], 1);   // afterwards rend[m] = end of band m
+        sx[pos] = k.x;
+        smaxr[pos] = (int16_t)hi;
+        sidx[pos] = (uint16_t)iR;
+        soct[pos] = (int8_t)k.octave;
+    }
+    __syncthreads();
+    span = s_span;
+
+    const int iL = i0 + tid;
+    if (iL >= nl) return;
+    float *ur_out = a.ur + (int64_t)b * a.ostride;
+    float *dp_out = a.depth + (int64_t)b * a.ostride;
+    int32_t *sad_out = a.sad + (int64_t)b * a.ostride;
+    ur_out[iL] = -1.0f;
+    dp_out[iL] = -1.0f;
+    sad_out[iL] = -1;
+    const orbx_keypoint kL = kl[iL];
+    const float vL = kL.y, uL = kL.x;
+    const int levelL = kL.octave;
+    if (!(vL >= 0.0f) || vL >= (float)H || levelL < 0 || levelL >= a.nlevels) return;
+    const int v = (int)vL;
+    const float minU = __fsub_rn(uL, a.maxd), maxU = uL;   // uL - minD, minD = 0
+    if (maxU < 0.0f) return;
+
+    // 2. best Hamming distance over the band (Frame.cc:556-585)
+    uint32_t q[8];
+    {
+        const uint4 q0 = *reinterpret_cast<const uint4 *>(dl + 32 * (int64_t)iL);
+        const uint4 q1 = *reinterpret_cast<const uint4 *>(dl + 32 * (int64_t)iL + 16);
+        q[0] = q0.x; q[1] = q0.y; q[2] = q0.z; q[3] = q0.w;
+        q[4] = q1.x; q[5] = q1.y; q[6] = q1.z; q[7] = q1.w;
+    }
+    int best = 100, bidx = 0;   // TH_HIGH
+    for (int m = max(0, v - span); m <= v; ++m) {
+        const int e = rend[m];
+        for (int pos = m ? rend[m - 1] : 0; pos < e; ++pos) {
+            if (smaxr[pos] < v) continue;
+            const int o = soct[pos];
+            if (o < levelL - 1 || o > levelL + 1) continue;
+            const float uR = sx[pos];
+            if (!(uR >= minU && uR <= maxU)) continue;
+            const int iR = sidx[pos];
+            const int dist = hamming(q, dr + 32 * (int64_t)iR);
+            if (dist < best || (dist == best && iR < bidx)) { best = dist; bidx = iR; }
+        }
+    }
+    if (best >= kThOrbDist) return;
+
+    // 3. SAD over 11 offsets (Frame.cc:587-629).  Windows the reference's
+    //    Mat::rowRange / colRange would assert on are reported as no match.
+    const LevelGeom g = a.lv[levelL];
+    const float sf = g.inv_scale;
+    const float suL = roundf(__fmul_rn(uL, sf)), svL = roundf(__fmul_rn(vL, sf));
+    const float suR0 = roundf(__fmul_rn(kr[bidx].x, sf));
+    if (svL - kSadW < 0.0f || svL + kSadW + 1 > (float)g.h || suL - kSadW < 0.0f || suL + kSadW + 1 > (float)g.w)
+        return;
+    const float iniu = suR0 + kSadL - kSadW, endu = suR0 + kSadL + kSadW + 1;
+    if (iniu < 0.0f || endu >= (float)g.w) return;
+    if (suR0 - kSadL - kSadW < 0.0f) return;
+    int lp, rp;
+    const uint8_t *IL = view_level(a.left, g, levelL, a.left_f0 + b * a.fstep, lp);
+    const uint8_t *IR = view_level(a.right, g, levelL, a.right_f0 + b * a.fstep, rp);
+    const int r0 = (int)svL - kSadW, cl0 = (int)suL - kSadW, cr0 = (int)suR0 - kSadL - kSadW;
+    int l[11], r[21];
+    load_rows(IL + (int64_t)(r0 + kSadW) * lp, cl0, IR + (int64_t)(r0 + kSadW) * rp, cr0, l, r);
+    int kc[11];   // center difference IL(w,w) - IR(w,w) per offset
+#pragma unroll
+    for (int i = 0; i < 11; ++i) kc[i] = l[kSadW] - r[i + kSadW];
+    int sad[11];
+#pragma unroll
+    for (int i = 0; i < 11; ++i) sad[i] = 0;
+    for (int rr = 0; rr < 2 * kSadW + 1; ++rr) {
+        load_rows(IL + (int64_t)(r0 + rr) * lp, cl0, IR + (int64_t)(r0 + rr) * rp, cr0, l, r);
+#pragma unroll
+        for (int i = 0; i < 11; ++i)
+#pragma unroll
+            for (int c = 0; c < 11; ++c) sad[i] += abs(l[c] - r[c + i] - kc[i]);
+    }
+    int bestSad = sad[0], bestInc = 0;   // first strict minimum (exact integer floats)
+#pragma unroll
+    for (int i = 1; i < 11; ++i)
+        if (sad[i] < bestSad) { bestSad = sad[i]; bestInc = i; }
+    if (bestInc == 0 || bestInc == 2 * kSadL) return;
+    float d1 = 0.f, d2 = 0.f, d3 = 0.f;
+#pragma unroll
+    for (int i = 1; i < 10; ++i)
+        if (i == bestInc) { d1 = (float)sad[i - 1]; d2 = (float)sad[i]; d3 = (float)sad[i + 1]; }
+    // 4. parabola fit and depth (Frame.cc:631-657)
+    const float deltaR = __fdiv_rn(__fsub_rn(d1, d3), __fmul_rn(2.0f, __fsub_rn(__fadd_rn(d1, d3), __fmul_rn(2.0f, d2))));
+    if (deltaR < -1.0f || deltaR > 1.0f) return;
+    float bestuR = __fmul_rn(g.scale, __fadd_rn(__fadd_rn(suR0, (float)(bestInc - kSadL)), deltaR));
+    float disparity = __fsub_rn(uL, bestuR);
+    if (disparity >= 0.0f && disparity < a.maxd) {
+        if (disparity <= 0.0f) {
+            disparity = 0.01f;                         // (float)0.01
+            bestuR = (float)__dsub_rn((double)uL, 0.01);   // uL - 0.01 in double
+        }
+        dp_out[iL] = __fdiv_rn(a.mbf, disparity);
+        ur_out[iL] = bestuR;
+        sad_out[iL] = bestSad;
+    }
+}
+
+// Median cut (Frame.cc:662-675): entries with SAD >= 1.5f*1.4f*median are
+// dropped; the median is element size/2 of the ascending SAD order.  SADs are
+// < 2^16 (121 * 510), so the median is a two-pass 8-bit radix select.
+__global__ __launch_bounds__(kST) void k_stereo_cut(StereoBufs a) {
+    __shared__ int hist[256];
+    __shared__ int s_sel, s_rank, s_kept;
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const int nl = a.nl[(int64_t)b * a.nstride];
+    float *ur = a.ur + (int64_t)b * a.ostride;
+    float *dp = a.depth + (int64_t)b * a.ostride;
+    const int32_t *sad = a.sad + (int64_t)b * a.ostride;
+    int cnt = 0;
+    hist[tid] = 0;
+    __syncthreads();
+    for (int i = tid; i < nl; i += kST) {
+        const int s = sad[i];
+        if (s >= 0) { ++cnt; atomicAdd(&hist[s >> 8], 1); }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int total = 0;
+        for (int i = 0; i < 256; ++i) total += hist[i];
+        const int k = total / 2;
+        int acc = 0, sel = -1;
+        for (int i = 0; i < 256 && sel < 0; ++i) {
+            if (acc + hist[i] > k) sel = i;
+            else acc += hist[i];
+        }
+        s_sel = sel;
+        s_rank = k - acc;
+        s_kept = total;
+    }
+    __syncthreads();
+    if (s_sel < 0) {   // no depth at all: nothing to cut (the reference reads an empty vector)
+        if (tid == 0) a.nkept[b] = 0;
+        return;
+    }
+    const int hi = s_sel, rank = s_rank;
+    __syncthreads();
+    hist[tid] = 0;
+    __syncthreads();
+    for (int i = tid; i < nl; i += kST) {
+        const int s = sad[i];
+        if (s >= 0 && (s >> 8) == hi) atomicAdd(&hist[s & 0xFF], 1);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int acc = 0, sel = 0;
+        for (int i = 0; i < 256; ++i) {
+            if (acc + hist[i] > rank) { sel = i; break; }
+            acc += hist[i];
+        }
+        s_sel = (hi << 8) | sel;
+    }
+    __syncthreads();
+    constexpr float kCut = 1.5f * 1.4f;   // folded in float, as the reference's constant product
+    const float thDist = __fmul_rn(kCut, (float)s_sel);
+    int dropped = 0;
+    for (int i = tid; i < nl; i += kST) {
+        const int s = sad[i];
+        if (s >= 0 && !((float)s < thDist)) {
+            ur[i] = -1.0f;
+            dp[i] = -1.0f;
+            ++dropped;
+        }
+    }
+    (void)cnt;
+    if (dropped) atomicSub(&s_kept, dropped);
+    __syncthreads();
+    if (tid == 0) a.nkept[b] = s_kept;
+}
+
+// Frame::ComputeStereoFromRGBD (Frame.cc:679-701) for undistorted frames
+// (mvKeysUn == mvKeys when k1 == 0, Frame.cc:440-444).
+__global__ __launch_bounds__(kST) void k_rgbd_depth(const orbx_keypoint *kps, const orbx_keypoint *kun,
+                                                    const int32_t *nkps, int64_t kstride, const float *dmap,
+                                                    int64_t dstride, int dpitch, int w, int h, float mbf, float *ur,
+                                                    float *depth, int64_t ostride, int32_t *nkept) {
+    const int b = blockIdx.y, i = blockIdx.x * kST + threadIdx.x;
+    const bool live = i < nkps[b];
+    bool got = false;
+    if (live) {
+    const orbx_keypoint k = kps[(int64_t)b * kstride + i];
+    float u_out = -1.0f, d_out = -1.0f;
+    const int v = (int)k.y, u = (int)k.x;
+    if (v >= 0 && v < h && u >= 0 && u < w) {
+        const float d = *reinterpret_cast<const float *>(reinterpret_cast<const uint8_t *>(dmap) + (int64_t)b * dstride +
+                                                         (int64_t)v * dpitch + 4 * (int64_t)u);
+        if (d > 0.0f) {
+            d_out = d;
+            u_out = __fsub_rn(kun[(int64_t)b * kstride + i].x, __fdiv_rn(mbf, d));
+            got = true;
+        }
+    }
+    ur[(int64_t)b * ostride + i] = u_out;
+    depth[(int64_t)b * ostride + i] = d_out;
+    }
+    const uint64_t m = __ballot(got);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(&nkept[b], __popcll(m));
+}
+
+}  // namespace
+
+int stereo_lds_bytes(int rows, int nr_cap) {
+    return ((rows + 1) * 4 + nr_cap * (4 + 2 + 2 + 1) + 15) & ~15;
+}
+
+hipError_t launch_stereo(const StereoBufs &a, int pairs, int nl_cap, hipStream_t st) {
+    if (pairs <= 0) return hipSuccess;
+    const int bytes = stereo_lds_bytes(a.rows, a.nr_cap);
+    if (bytes > 64 * 1024 &&
+        hipFuncSetAttribute(reinterpret_cast<const void *>(k_stereo_band), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            bytes) != hipSuccess)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_stereo_band, dim3((nl_cap + kST - 1) / kST, pairs), dim3(kST), bytes, st, a);
+    hipLaunchKernelGGL(k_stereo_cut, dim3(pairs), dim3(kST), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_rgbd(const orbx_keypoint *kps, const orbx_keypoint *kun, const int32_t *nkps, int64_t kstride,
+                       int kcap, const float *dmap, int64_t dstride, int dpitch, int w, int h, float mbf, float *ur,
+                       float *depth, int64_t ostride, int32_t *nkept, int B, hipStream_t st) {
+    if (B <= 0) return hipSuccess;
+    if (hipMemsetAsync(nkept, 0, sizeof(int32_t) * B, st) != hipSuccess) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_rgbd_depth, dim3((kcap + kST - 1) / kST, B), dim3(kST), 0, st, kps, kun ? kun : kps, nkps,
+                       kstride, dmap, dstride, dpitch, w, h, mbf, ur, depth, ostride, nkept);
+    return hipGetLastError();
+}
+
+}  // namespace orbx

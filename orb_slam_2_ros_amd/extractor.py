@@ -138,6 +138,30 @@ class ORBextractor:
                                               window, ctypes.c_float(nnratio), int(check_ori),
                                               ctypes.c_void_p(stream or 0)), "mono_step_device")
 
+    def stereo_step_device(self, d_images: int, frame_stride: int, pitch: int, pairs: int, mbf: float,
+                           mb: float, stream: int | None = None) -> None:
+        """Frames 2p / 2p+1 are the left / right images of pair p."""
+        check(self._lib.orbx_stereo_step_device(self._h, ctypes.c_void_p(d_images), frame_stride, pitch, pairs,
+                                                ctypes.c_float(mbf), ctypes.c_float(mb),
+                                                ctypes.c_void_p(stream or 0)), "stereo_step_device")
+
+    def rgbd_step_device(self, d_images: int, frame_stride: int, pitch: int, batch: int, d_depth: int,
+                         depth_stride: int, depth_pitch: int, mbf: float, stream: int | None = None) -> None:
+        check(self._lib.orbx_rgbd_step_device(self._h, ctypes.c_void_p(d_images), frame_stride, pitch, batch,
+                                              ctypes.c_void_p(d_depth), depth_stride, depth_pitch,
+                                              ctypes.c_float(mbf), ctypes.c_void_p(stream or 0)),
+              "rgbd_step_device")
+
+    def depth_download(self, index: int):
+        """(mvuRight, mvDepth, nkept) of pair / frame `index` of the last stereo / RGB-D step."""
+        cap = self.kp_stride()
+        ur = np.zeros(cap, dtype=np.float32)
+        dp = np.zeros(cap, dtype=np.float32)
+        n, nk = ctypes.c_int(0), ctypes.c_int(0)
+        check(self._lib.orbx_depth_download(self._h, index, ptr(ur), ptr(dp), cap, ctypes.byref(n),
+                                            ctypes.byref(nk)), "depth_download")
+        return ur[:n.value].copy(), dp[:n.value].copy(), nk.value
+
     def batch_download(self, frame: int):
         cap = self.kp_stride()
         kps = np.zeros(cap, dtype=KEYPOINT_DTYPE)

@@ -84,3 +84,26 @@ def frames(width: int, height: int, seed: int, count: int) -> np.ndarray:
     for t in range(count):
         out[t] = frame_from_canvas(canvas, width, height, t, seed * 7919 + t)
     return out
+
+
+def stereo_pair(width: int, height: int, seed: int, t: int = 0, disparity: int = 20):
+    """Rectified (left, right) pair of stream `seed` at time t: the right image
+    is the left crop shifted by `disparity` px (u_R = u_L - disparity), with
+    its own noise."""
+    canvas = stream_canvas(width, height, seed)
+    left = frame_from_canvas(canvas, width, height, t, seed * 7919 + t)
+    right = frame_from_canvas(canvas, width, height, t, seed * 7919 + t + 500009, disparity=disparity)
+    return np.ascontiguousarray(left), np.ascontiguousarray(right)
+
+
+def depth_map(width: int, height: int, seed: int, z: float = 1.5) -> np.ndarray:
+    """float32 depth image: a plane at z metres with a tilted patch and a few
+    invalid (0 / NaN) pixels, as an RGB-D sensor delivers."""
+    rng = np.random.default_rng(seed)
+    d = np.full((height, width), z, np.float32)
+    yy, xx = np.mgrid[0:height, 0:width]
+    d += (0.0005 * (xx - width / 2) + 0.0003 * (yy - height / 2)).astype(np.float32)
+    holes = rng.random((height, width)) < 0.02
+    d[holes] = 0.0
+    d[rng.random((height, width)) < 0.005] = np.nan
+    return d

@@ -329,3 +329,91 @@ def search_for_initialization(k1, d1, k2, d2, w, h, prev, window, nnratio, check
 def round_half_away(v) -> int:
     v = float(v)
     return int(math.floor(v + 0.5)) if v >= 0 else -int(math.floor(-v + 0.5))
+
+
+# ---- Frame::ComputeStereoMatches (Frame.cc:502-676) --------------------------
+def compute_stereo_matches(pyr_l, pyr_r, scale, inv_scale, kl, dl, kr, dr, mbf, mb):
+    """Straight transcription of the reference loop (vRowIndices as lists,
+    candidates in right-index order); returns (uright, depth, kept)."""
+    n = len(kl)
+    ur = np.full(n, -1, np.float32)
+    dp = np.full(n, -1, np.float32)
+    nrows = pyr_l[0].shape[0]
+    rows = [[] for _ in range(nrows)]
+    for iR in range(len(kr)):
+        y = f32(kr["y"][iR])
+        r = f32(f32(2.0) * f32(scale[kr["octave"][iR]]))
+        maxr, minr = int(math.ceil(f32(y + r))), int(math.floor(f32(y - r)))
+        for yi in range(minr, maxr + 1):
+            if 0 <= yi < nrows:
+                rows[yi].append(iR)
+    mbf, mb = f32(mbf), f32(mb)
+    maxD = f32(mbf / mb)
+    dist_idx = []
+    for iL in range(n):
+        uL, vL, lvl = f32(kl["x"][iL]), f32(kl["y"][iL]), int(kl["octave"][iL])
+        if not (0 <= vL < nrows):
+            continue
+        cands = rows[int(vL)]
+        if not cands:
+            continue
+        minU, maxU = f32(uL - maxD), uL
+        if maxU < 0:
+            continue
+        best, bidx = 100, 0
+        for iR in cands:
+            if kr["octave"][iR] < lvl - 1 or kr["octave"][iR] > lvl + 1:
+                continue
+            uR = f32(kr["x"][iR])
+            if minU <= uR <= maxU:
+                d = hamming(dl[iL], dr[iR])
+                if d < best:
+                    best, bidx = d, iR
+        if best >= 75:
+            continue
+        sf = f32(inv_scale[lvl])
+        suL = f32(round_half_away(f32(uL * sf)))
+        svL = f32(round_half_away(f32(vL * sf)))
+        suR0 = f32(round_half_away(f32(f32(kr["x"][bidx]) * sf)))
+        IL, IR = pyr_l[lvl].astype(np.int64), pyr_r[lvl].astype(np.int64)
+        h, w = IL.shape
+        if svL - 5 < 0 or svL + 6 > h or suL - 5 < 0 or suL + 6 > w:
+            continue
+        if suR0 < 0 or suR0 + 11 >= w or suR0 - 10 < 0:
+            continue
+        r0, c0 = int(svL) - 5, int(suL) - 5
+        wl = IL[r0:r0 + 11, c0:c0 + 11]
+        wl = wl - wl[5, 5]
+        sads = []
+        for inc in range(-5, 6):
+            cr = int(suR0) + inc - 5
+            wr = IR[r0:r0 + 11, cr:cr + 11]
+            sads.append(int(np.abs(wl - (wr - wr[5, 5])).sum()))
+        bi = int(np.argmin(sads))     # first minimum
+        if bi in (0, 10):
+            continue
+        d1, d2, d3 = f32(sads[bi - 1]), f32(sads[bi]), f32(sads[bi + 1])
+        delta = f32(f32(d1 - d3) / f32(f32(2.0) * f32(f32(d1 + d3) - f32(f32(2.0) * d2))))
+        if delta < -1 or delta > 1:
+            continue
+        bestuR = f32(f32(scale[lvl]) * f32(f32(suR0 + f32(bi - 5)) + delta))
+        disp = f32(uL - bestuR)
+        if 0 <= disp < maxD:
+            if disp <= 0:
+                disp = f32(0.01)
+                bestuR = f32(float(uL) - 0.01)
+            dp[iL] = f32(mbf / disp)
+            ur[iL] = bestuR
+            dist_idx.append((sads[bi], iL))
+    if not dist_idx:
+        return ur, dp, 0
+    dist_idx.sort()
+    median = f32(dist_idx[len(dist_idx) // 2][0])
+    th = f32(f32(f32(1.5) * f32(1.4)) * median)
+    kept = len(dist_idx)
+    for d, i in reversed(dist_idx):
+        if f32(d) < th:
+            break
+        ur[i] = dp[i] = -1
+        kept -= 1
+    return ur, dp, kept

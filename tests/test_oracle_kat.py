@@ -169,3 +169,73 @@ def test_matcher_vs_python(seed, oracle_mod):
         nm_p, m12_p, p2_p = pyref.search_for_initialization(k1, d1, k2, d2, w, h, prev, window, ratio, ori)
         assert nm == nm_p and np.array_equal(m12, m12_p) and np.array_equal(p2, p2_p)
     assert nm > 0
+
+
+def _stereo_inputs(oracle_mod, w, h, nf, seed, disparity):
+    L, R = synth.stereo_pair(w, h, seed, 0, disparity)
+    kl, dl = oracle_mod.extract(L, nf)
+    kr, dr = oracle_mod.extract(R, nf)
+    return oracle_mod.pyramid(L), oracle_mod.pyramid(R), kl, dl, kr, dr
+
+
+def _edge_keypoints(pyr, n, rng, nlev=8):
+    """Random keypoints anywhere on random levels (incl. the borders the
+    reference would assert on), in level-0 coordinates like the extractor's."""
+    sf, _ = __import__("oracle.oracle", fromlist=["x"]).scale_tables(1.2, nlev)
+    k = np.zeros(n, dtype=[("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+    oc = rng.integers(0, nlev, n)
+    for i in range(n):
+        hh, ww = pyr[oc[i]].shape
+        k["x"][i] = np.float32(rng.integers(0, ww)) * sf[oc[i]]
+        k["y"][i] = np.float32(rng.integers(0, hh)) * sf[oc[i]]
+    k["octave"] = oc
+    k["class_id"] = -1
+    return k
+
+
+@pytest.mark.parametrize("w,h,nf,seed,disp", [(320, 240, 500, 41, 12), (400, 200, 400, 42, 3)])
+def test_stereo_vs_python(w, h, nf, seed, disp, oracle_mod):
+    pl, pr, kl, dl, kr, dr = _stereo_inputs(oracle_mod, w, h, nf, seed, disp)
+    sf, inv = oracle_mod.scale_tables()
+    mbf, mb = 40.0, float(np.float32(40.0) / np.float32(300.0))
+    ur, dp, kept = oracle_mod.compute_stereo_matches(pl, pr, kl, dl, kr, dr, mbf, mb)
+    pur, pdp, pkept = pyref.compute_stereo_matches(pl, pr, sf, inv, kl, dl, kr, dr, mbf, mb)
+    assert kept == pkept and kept > 0.3 * len(kl)
+    assert np.array_equal(ur, pur) and np.array_equal(dp, pdp)
+    v = ur >= 0
+    assert abs(np.median(kl["x"][v] - ur[v]) - disp) < 0.5
+
+
+def test_stereo_edge_keypoints_vs_python(oracle_mod):
+    rng = np.random.default_rng(43)
+    pl, pr, _, _, _, _ = _stereo_inputs(oracle_mod, 320, 240, 300, 43, 8)
+    kl = _edge_keypoints(pl, 300, rng)
+    kr = kl.copy()
+    kr["x"] -= np.float32(8.0)
+    dl = rng.integers(0, 256, (300, 32)).astype(np.uint8)
+    dr = dl.copy()
+    flips = rng.integers(0, 256, (300, 32)).astype(np.uint8) & rng.integers(0, 256, (300, 32)).astype(np.uint8) \
+        & rng.integers(0, 256, (300, 32)).astype(np.uint8)
+    dr ^= flips   # ~1/8 of the bits differ: some pairs pass TH 75, some do not
+    sf, inv = oracle_mod.scale_tables()
+    for mbf, mb in [(40.0, 0.1), (40.0, 1e9), (1e6, 0.5)]:
+        ur, dp, kept = oracle_mod.compute_stereo_matches(pl, pr, kl, dl, kr, dr, mbf, mb)
+        pur, pdp, pkept = pyref.compute_stereo_matches(pl, pr, sf, inv, kl, dl, kr, dr, mbf, mb)
+        assert kept == pkept and np.array_equal(ur, pur) and np.array_equal(dp, pdp)
+
+
+def test_stereo_from_rgbd_oracle(oracle_mod):
+    rng = np.random.default_rng(44)
+    d = synth.depth_map(160, 120, 44)
+    k = np.zeros(500, oracle_mod.KEYPOINT_DTYPE)
+    k["x"] = rng.uniform(-2, 162, 500).astype(np.float32)
+    k["y"] = rng.uniform(-2, 122, 500).astype(np.float32)
+    ur, dp = oracle_mod.stereo_from_rgbd(k, d, 40.0)
+    for i in range(500):
+        u, v = int(k["x"][i]), int(k["y"][i])
+        z = d[v, u] if (0 <= u < 160 and 0 <= v < 120) else np.float32(np.nan)
+        if z > 0:
+            assert dp[i] == z and ur[i] == np.float32(k["x"][i] - np.float32(np.float32(40.0) / z))
+        else:
+            assert dp[i] == -1 and ur[i] == -1
