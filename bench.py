@@ -10,6 +10,11 @@ nnratio 0.9, checkOri).  A step processes one new frame for each of the B
 streams a GPU owns (streams are independent: weak scaling, no collective on
 the data path; RCCL is used only for the barrier / max-time reduction).
 
+Secondary configurations (reported under "extras", not the headline value):
+FHD mono, and the stereo / RGB-D units of SURVEY.md §8(d) -- a stereo pair =
+extract left + right + Frame::ComputeStereoMatches (C3 EuRoC 752x480 1200 kp,
+C4 KITTI 1241x376 2000 kp, FHD); an RGB-D frame = extract + ComputeStereoFromRGBD.
+
 Inputs are synthetic (orb_slam_2_ros_amd.synth) and resident in HBM before
 the timed region.  Prints ONE JSON line on rank 0.
 """
@@ -89,25 +94,56 @@ def cpu_baseline(w: int, h: int, nfeatures: int, budget_s: float):
             "sample": f"{n} consecutive {w}x{h} synthetic frames ({el:.1f} s), oracle/liborbx_oracle.so, 1 thread"}
 
 
-def run_config(torch, dist, rank, world, dev, w, h, nfeatures, batch, steps, warmup, profile):
-    from orb_slam_2_ros_amd import ORBextractor, synth
-    ex = ORBextractor(nfeatures, 1.2, 8, 20, 7, device=dev.index)
-    ex.reserve(w, h, batch)
-    # resident input: [FRAMES_PER_STREAM, batch, h, w]
+def _resident_frames(mode, w, h, batch, rank):
+    """Host array [FRAMES_PER_STREAM, frames_per_step, h, w] (+ depth maps for RGB-D)."""
+    from orb_slam_2_ros_amd import synth
     nsc = min(UNIQUE_SCENES, batch)
-    scenes = [synth.frames(w, h, 7000 + 97 * rank + s, FRAMES_PER_STREAM) for s in range(nsc)]
-    host = np.empty((FRAMES_PER_STREAM, batch, h, w), np.uint8)
-    for b in range(batch):
-        host[:, b] = scenes[b % nsc]
+    depth = None
+    if mode == "stereo":
+        host = np.empty((FRAMES_PER_STREAM, 2 * batch, h, w), np.uint8)
+        for s in range(nsc):
+            seed = 7000 + 97 * rank + s
+            canvas = synth.stream_canvas(w, h, seed)
+            for t in range(FRAMES_PER_STREAM):
+                L = synth.frame_from_canvas(canvas, w, h, t, seed * 7919 + t)
+                R = synth.frame_from_canvas(canvas, w, h, t, seed * 7919 + t + 500009, disparity=20)
+                for b in range(s, batch, nsc):
+                    host[t, 2 * b], host[t, 2 * b + 1] = L, R
+    else:
+        host = np.empty((FRAMES_PER_STREAM, batch, h, w), np.uint8)
+        scenes = [synth.frames(w, h, 7000 + 97 * rank + s, FRAMES_PER_STREAM) for s in range(nsc)]
+        for b in range(batch):
+            host[:, b] = scenes[b % nsc]
+        if mode == "rgbd":
+            dm = [synth.depth_map(w, h, 7000 + s) for s in range(min(nsc, 8))]
+            depth = np.stack([dm[b % len(dm)] for b in range(batch)])
+    return host, depth
+
+
+def run_config(torch, dist, rank, world, dev, w, h, nfeatures, batch, steps, warmup, profile, mode="mono"):
+    """Times `steps` front-end steps of `batch` streams (mono / RGB-D frames or
+    stereo pairs) per GPU; returns (max-over-ranks seconds, stage ms, sanity)."""
+    from orb_slam_2_ros_amd import ORBextractor
+    ex = ORBextractor(nfeatures, 1.2, 8, 20, 7, device=dev.index)
+    ex.reserve(w, h, 2 * batch if mode == "stereo" else batch)
+    host, depth = _resident_frames(mode, w, h, batch, rank)
     frames = torch.from_numpy(host).to(dev)
-    del host
+    dmaps = torch.from_numpy(depth).to(dev) if depth is not None else None
+    del host, depth
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
     fstride = h * w
+    bf, fx = 47.9, 435.2                       # EuRoC-like rig: mbf, fx (mb = mbf / fx)
+    mb = float(np.float32(bf) / np.float32(fx))
 
     def step(k):
         t = k % FRAMES_PER_STREAM
-        ex.mono_step_device(frames[t].data_ptr(), fstride, w, batch, 100, 0.9, True, sp)
+        if mode == "mono":
+            ex.mono_step_device(frames[t].data_ptr(), fstride, w, batch, 100, 0.9, True, sp)
+        elif mode == "stereo":
+            ex.stereo_step_device(frames[t].data_ptr(), fstride, w, batch, bf, mb, sp)
+        else:
+            ex.rgbd_step_device(frames[t].data_ptr(), fstride, w, batch, dmaps.data_ptr(), 4 * fstride, 4 * w, bf, sp)
 
     k = 0
     for _ in range(max(warmup, 2)):
@@ -128,14 +164,27 @@ def run_config(torch, dist, rank, world, dev, w, h, nfeatures, batch, steps, war
     el = time.perf_counter() - t0
     stages = ex.stage_times() if profile else None
     ex.set_profiling(False)
-    # sanity: last step produced keypoints and matches on every stream
+    # sanity: the last step produced keypoints and matches / depths on stream 0
     kp, _ = ex.batch_download(0)
-    m12, nm = ex.mono_matches_download(0)
+    if mode == "mono":
+        _, sane = ex.mono_matches_download(0)
+    else:
+        _, _, sane = ex.depth_download(0)
     t_el = torch.tensor([el], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t_el, op=dist.ReduceOp.MAX)
     ex.close()
-    return float(t_el.item()), stages, len(kp), nm
+    return float(t_el.item()), stages, len(kp), sane
+
+
+EXTRAS = [
+    # key, mode, w, h, nfeatures, streams per GPU, unit
+    ("fhd_1920x1080", "mono", 1920, 1080, 1000, 64, "frames/s"),
+    ("stereo_euroc_752x480", "stereo", 752, 480, 1200, 128, "stereo pairs/s"),
+    ("stereo_kitti_1241x376", "stereo", 1241, 376, 2000, 96, "stereo pairs/s"),
+    ("stereo_fhd_1920x1080", "stereo", 1920, 1080, 1000, 32, "stereo pairs/s"),
+    ("rgbd_fhd_1920x1080", "rgbd", 1920, 1080, 1000, 64, "frames/s"),
+]
 
 
 def main() -> int:
@@ -147,7 +196,8 @@ def main() -> int:
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--nfeatures", type=int, default=1000)
-    ap.add_argument("--fhd-batch", type=int, default=64, help="also measure 1920x1080 (0 = skip)")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the secondary FHD / stereo / RGB-D configurations")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-profile", action="store_true")
     args = ap.parse_args()
@@ -171,12 +221,14 @@ def main() -> int:
     value = frames_total / el
     ms_per_step = 1000.0 * el / args.steps
 
-    fhd = None
-    if args.fhd_batch > 0:
-        el2, st2, _, _ = run_config(torch, dist, rank, world, dev, 1920, 1080, nf, args.fhd_batch,
-                                    max(5, args.steps // 4), 2, profile)
-        fhd = {"value": world * args.fhd_batch * max(5, args.steps // 4) / el2, "unit": "frames/s",
-               "batch_per_gpu": args.fhd_batch, "stage_ms": st2}
+    extras = {}
+    if not args.no_extras:
+        for key, mode, ew, eh, enf, eb, unit in EXTRAS:
+            es = max(5, args.steps // 4)
+            el2, st2, nk2, sane2 = run_config(torch, dist, rank, world, dev, ew, eh, enf, eb, es, 2, profile, mode)
+            extras[key] = {"value": round(world * eb * es / el2, 2), "unit": unit, "mode": mode,
+                           "streams_per_gpu": eb, "nfeatures": enf, "stage_ms": st2,
+                           "kps_last_frame": nk2, ("matches" if mode == "mono" else "depths") + "_last_frame": sane2}
 
     if rank == 0:
         sizes = level_geometry(w, h, nf)
@@ -217,7 +269,7 @@ def main() -> int:
             "roofline": roof,
             "stage_ms_per_step": stage_ms,
             "cpu_baseline": cpu,
-            "fhd_1920x1080": fhd,
+            "extras": extras,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
