@@ -5,6 +5,7 @@
 // Reference interfaces reproduced (wjjcdy/orb_slam_2_ros):
 //   orb_slam2/include/ORBextractor.h:45-111  (class ORBextractor)
 //   orb_slam2/include/ORBmatcher.h:46,65     (DescriptorDistance, SearchForInitialization)
+//   orb_slam2/src/Frame.cc:502-676,679-701   (ComputeStereoMatches, ComputeStereoFromRGBD)
 //
 // Use: replace `#include "ORBextractor.h"` by this header in Frame.h /
 // Tracking.h (or add the GPU class beside the CPU one) and
@@ -31,6 +32,12 @@ inline int device_index() {
 }
 inline void check(int rc, const char *what) {
     if (rc < 0) throw std::runtime_error(std::string(what) + ": " + orbx_strerror(rc));
+}
+inline std::vector<orbx_keypoint> pack(const std::vector<cv::KeyPoint> &ks) {
+    std::vector<orbx_keypoint> out(ks.size());
+    for (size_t i = 0; i < ks.size(); ++i)
+        out[i] = {ks[i].pt.x, ks[i].pt.y, ks[i].size, ks[i].angle, ks[i].response, ks[i].octave, ks[i].class_id};
+    return out;
 }
 }  // namespace orbx_detail
 
@@ -90,6 +97,8 @@ public:
     }
 
     int inline GetLevels() { return nlevels_; }
+    // The liborbx handle (device pyramid of the last call), for OrbxFrame.
+    orbx_extractor *handle() const { return h_; }
     float inline GetScaleFactor() { return scaleFactor_; }
     std::vector<float> inline GetScaleFactors() { return mvScaleFactor; }
     std::vector<float> inline GetInverseScaleFactors() { return mvInvScaleFactor; }
@@ -144,14 +153,7 @@ struct OrbxMatcher {
                                        int img_h, std::vector<cv::Point2f> &vbPrevMatched,
                                        std::vector<int> &vnMatches12, int windowSize, float nnratio,
                                        bool checkOri) {
-        auto pack = [](const std::vector<cv::KeyPoint> &ks) {
-            std::vector<orbx_keypoint> out(ks.size());
-            for (size_t i = 0; i < ks.size(); ++i)
-                out[i] = {ks[i].pt.x, ks[i].pt.y, ks[i].size, ks[i].angle, ks[i].response, ks[i].octave,
-                          ks[i].class_id};
-            return out;
-        };
-        const std::vector<orbx_keypoint> k1 = pack(keys1), k2 = pack(keys2);
+        const std::vector<orbx_keypoint> k1 = orbx_detail::pack(keys1), k2 = orbx_detail::pack(keys2);
         const cv::Mat d1 = desc1.isContinuous() ? desc1 : desc1.clone();
         const cv::Mat d2 = desc2.isContinuous() ? desc2 : desc2.clone();
         std::vector<float> prev(2 * keys1.size());
@@ -165,6 +167,46 @@ struct OrbxMatcher {
                            "SearchForInitialization");
         for (size_t i = 0; i < keys1.size(); ++i) vbPrevMatched[i] = cv::Point2f(prev[2 * i], prev[2 * i + 1]);
         return nm;
+    }
+};
+
+// The two Frame depth steps this tier accelerates, as free functions over the
+// Frame members they read and write (see INTEGRATION.md for the Frame.cc patch).
+struct OrbxFrame {
+    // Frame::ComputeStereoMatches (Frame.cc:502-676): left / right are the
+    // extractors that produced mvKeys / mvKeysRight in this frame (their device
+    // pyramids are the mvImagePyramid the reference reads).  Returns the number
+    // of depths kept.
+    static int ComputeStereoMatches(ORBextractor &left, ORBextractor &right, const std::vector<cv::KeyPoint> &mvKeys,
+                                    const cv::Mat &mDescriptors, const std::vector<cv::KeyPoint> &mvKeysRight,
+                                    const cv::Mat &mDescriptorsRight, float mbf, float mb,
+                                    std::vector<float> &mvuRight, std::vector<float> &mvDepth) {
+        const std::vector<orbx_keypoint> kl = orbx_detail::pack(mvKeys), kr = orbx_detail::pack(mvKeysRight);
+        const cv::Mat dl = mDescriptors.isContinuous() ? mDescriptors : mDescriptors.clone();
+        const cv::Mat dr = mDescriptorsRight.isContinuous() ? mDescriptorsRight : mDescriptorsRight.clone();
+        mvuRight.assign(kl.size(), -1.0f);
+        mvDepth.assign(kl.size(), -1.0f);
+        int kept = 0;
+        orbx_detail::check(orbx_compute_stereo_matches(left.handle(), right.handle(), kl.data(), dl.data, (int)kl.size(),
+                                                       kr.data(), dr.data, (int)kr.size(), mbf, mb, mvuRight.data(),
+                                                       mvDepth.data(), &kept),
+                           "ComputeStereoMatches");
+        return kept;
+    }
+
+    // Frame::ComputeStereoFromRGBD (Frame.cc:679-701); imDepth is CV_32F.
+    static void ComputeStereoFromRGBD(const std::vector<cv::KeyPoint> &mvKeys,
+                                      const std::vector<cv::KeyPoint> &mvKeysUn, const cv::Mat &imDepth, float mbf,
+                                      std::vector<float> &mvuRight, std::vector<float> &mvDepth) {
+        assert(imDepth.type() == CV_32F);
+        const std::vector<orbx_keypoint> k = orbx_detail::pack(mvKeys), ku = orbx_detail::pack(mvKeysUn);
+        mvuRight.assign(k.size(), -1.0f);
+        mvDepth.assign(k.size(), -1.0f);
+        int kept = 0;
+        orbx_detail::check(orbx_stereo_from_rgbd(orbx_detail::device_index(), k.data(), ku.data(), (int)k.size(),
+                                                 imDepth.ptr<float>(), imDepth.cols, imDepth.rows, imDepth.step,
+                                                 mbf, mvuRight.data(), mvDepth.data(), &kept),
+                           "ComputeStereoFromRGBD");
     }
 };
 

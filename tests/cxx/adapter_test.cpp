@@ -5,6 +5,13 @@
 //        extracts both frames, matches them (window 100, 0.9, checkOri) and
 //        writes: n0, kps0 (28 B each), desc0, n1, kps1, desc1, nm, matches12,
 //        prev (2 floats per F1 keypoint), pyramid level 1 with its 19-px border.
+//   adapter_test stereo W H left.raw right.raw mbf mb out.bin
+//        extracts both images with two extractors, runs
+//        OrbxFrame::ComputeStereoMatches and writes: nl, kps, desc, nr, kps,
+//        desc, nkept, mvuRight, mvDepth.
+//   adapter_test rgbd W H img.raw depth.raw mbf out.bin
+//        extracts the image and runs OrbxFrame::ComputeStereoFromRGBD:
+//        n, kps, desc, mvuRight, mvDepth.
 #include <cstdio>
 #include <fstream>
 #include <iostream>
@@ -21,6 +28,18 @@ static cv::Mat load(const char *path, int w, int h) {
     return m;
 }
 
+static void put_kps(std::ofstream &out, const std::vector<cv::KeyPoint> &ks, const cv::Mat &d) {
+    const int n = (int)ks.size();
+    out.write(reinterpret_cast<const char *>(&n), 4);
+    for (const auto &k : ks) {
+        const float f[5] = {k.pt.x, k.pt.y, k.size, k.angle, k.response};
+        const int i[2] = {k.octave, k.class_id};
+        out.write(reinterpret_cast<const char *>(f), 20);
+        out.write(reinterpret_cast<const char *>(i), 8);
+    }
+    for (int r = 0; r < n; ++r) out.write(reinterpret_cast<const char *>(d.ptr<uint8_t>(r)), 32);
+}
+
 int main(int argc, char **argv) {
     if (argc >= 2 && std::string(argv[1]) == "probe") {
         try {
@@ -29,6 +48,43 @@ int main(int argc, char **argv) {
         } catch (const std::runtime_error &e) {
             std::cout << "nodevice\n";
         }
+        return 0;
+    }
+    if (argc == 9 && std::string(argv[1]) == "stereo") {
+        const int w = std::atoi(argv[2]), h = std::atoi(argv[3]);
+        cv::Mat il = load(argv[4], w, h), ir = load(argv[5], w, h);
+        ORBextractor exl(1000, 1.2f, 8, 20, 7), exr(1000, 1.2f, 8, 20, 7);
+        std::vector<cv::KeyPoint> kl, kr;
+        cv::Mat dl, dr;
+        exl(il, cv::Mat(), kl, dl);
+        exr(ir, cv::Mat(), kr, dr);
+        std::vector<float> ur, dp;
+        const int kept = OrbxFrame::ComputeStereoMatches(exl, exr, kl, dl, kr, dr, (float)std::atof(argv[6]),
+                                                         (float)std::atof(argv[7]), ur, dp);
+        std::ofstream out(argv[8], std::ios::binary);
+        put_kps(out, kl, dl);
+        put_kps(out, kr, dr);
+        out.write(reinterpret_cast<const char *>(&kept), 4);
+        out.write(reinterpret_cast<const char *>(ur.data()), 4 * ur.size());
+        out.write(reinterpret_cast<const char *>(dp.data()), 4 * dp.size());
+        return 0;
+    }
+    if (argc == 8 && std::string(argv[1]) == "rgbd") {
+        const int w = std::atoi(argv[2]), h = std::atoi(argv[3]);
+        cv::Mat im = load(argv[4], w, h);
+        cv::Mat depth(h, w, CV_32F);
+        std::ifstream f(argv[5], std::ios::binary);
+        f.read(reinterpret_cast<char *>(depth.data), (std::streamsize)4 * w * h);
+        ORBextractor ex(1000, 1.2f, 8, 20, 7);
+        std::vector<cv::KeyPoint> k;
+        cv::Mat d;
+        ex(im, cv::Mat(), k, d);
+        std::vector<float> ur, dp;
+        OrbxFrame::ComputeStereoFromRGBD(k, k, depth, (float)std::atof(argv[6]), ur, dp);
+        std::ofstream out(argv[7], std::ios::binary);
+        put_kps(out, k, d);
+        out.write(reinterpret_cast<const char *>(ur.data()), 4 * ur.size());
+        out.write(reinterpret_cast<const char *>(dp.data()), 4 * dp.size());
         return 0;
     }
     if (argc != 7 || std::string(argv[1]) != "run") return 2;
@@ -44,19 +100,8 @@ int main(int argc, char **argv) {
     std::vector<int> m12;
     const int nm = OrbxMatcher::SearchForInitialization(k0, d0, k1, d1, w, h, prev, m12, 100, 0.9f, true);
     std::ofstream out(argv[6], std::ios::binary);
-    auto put_kps = [&](const std::vector<cv::KeyPoint> &ks, const cv::Mat &d) {
-        const int n = (int)ks.size();
-        out.write(reinterpret_cast<const char *>(&n), 4);
-        for (const auto &k : ks) {
-            const float f[5] = {k.pt.x, k.pt.y, k.size, k.angle, k.response};
-            const int i[2] = {k.octave, k.class_id};
-            out.write(reinterpret_cast<const char *>(f), 20);
-            out.write(reinterpret_cast<const char *>(i), 8);
-        }
-        for (int r = 0; r < n; ++r) out.write(reinterpret_cast<const char *>(d.ptr<uint8_t>(r)), 32);
-    };
-    put_kps(k0, d0);
-    put_kps(k1, d1);
+    put_kps(out, k0, d0);
+    put_kps(out, k1, d1);
     out.write(reinterpret_cast<const char *>(&nm), 4);
     out.write(reinterpret_cast<const char *>(m12.data()), 4 * m12.size());
     for (const auto &p : prev) { out.write(reinterpret_cast<const char *>(&p.x), 4); out.write(reinterpret_cast<const char *>(&p.y), 4); }

@@ -10,6 +10,7 @@
 
 #define CV_8U 0
 #define CV_8UC1 0
+#define CV_32F 5
 
 namespace cv {
 enum { BORDER_REFLECT_101 = 4, BORDER_ISOLATED = 16 };
@@ -37,24 +38,36 @@ public:
     int rows = 0, cols = 0;
     size_t step = 0;
     uint8_t *data = nullptr;
+    int type_ = CV_8U;
     std::shared_ptr<std::vector<uint8_t>> buf;
     Mat() = default;
-    Mat(int r, int c, int) { create(r, c, CV_8U); }
-    void create(int r, int c, int) {
-        if (rows == r && cols == c && data) return;
-        buf = std::make_shared<std::vector<uint8_t>>((size_t)r * c);
-        rows = r; cols = c; step = c; data = buf->data();
+    Mat(int r, int c, int t) { create(r, c, t); }
+    size_t elemSize() const { return type_ == CV_32F ? 4 : 1; }
+    void create(int r, int c, int t) {
+        if (rows == r && cols == c && type_ == t && data) return;
+        type_ = t;
+        buf = std::make_shared<std::vector<uint8_t>>((size_t)r * c * elemSize());
+        rows = r; cols = c; step = c * elemSize(); data = buf->data();
     }
     void release() { buf.reset(); data = nullptr; rows = cols = 0; step = 0; }
     bool empty() const { return !data || rows == 0 || cols == 0; }
-    int type() const { return CV_8U; }
-    bool isContinuous() const { return step == (size_t)cols; }
+    int type() const { return type_; }
+    bool isContinuous() const { return step == (size_t)cols * elemSize(); }
     template <typename T> T *ptr(int r = 0) { return reinterpret_cast<T *>(data + r * step); }
     template <typename T> const T *ptr(int r = 0) const { return reinterpret_cast<const T *>(data + r * step); }
+    template <typename T> const T &at(int r, int c) const { return ptr<T>(r)[c]; }
     Mat rowRange(int a, int b) const { Mat m = *this; m.data = data + a * step; m.rows = b - a; return m; }
-    Mat operator()(Rect r) const { Mat m = *this; m.data = data + r.y * step + r.x; m.rows = r.height; m.cols = r.width; return m; }
-    Mat clone() const { Mat m(rows, cols, CV_8U); for (int i = 0; i < rows; ++i) std::memcpy(m.data + i * m.step, data + i * step, cols); return m; }
-    void copyTo(Mat dst) const { for (int i = 0; i < rows; ++i) std::memcpy(dst.data + i * dst.step, data + i * step, cols); }
+    Mat operator()(Rect r) const {
+        Mat m = *this; m.data = data + r.y * step + r.x * elemSize(); m.rows = r.height; m.cols = r.width; return m;
+    }
+    Mat clone() const {
+        Mat m(rows, cols, type_);
+        for (int i = 0; i < rows; ++i) std::memcpy(m.data + i * m.step, data + i * step, cols * elemSize());
+        return m;
+    }
+    void copyTo(Mat dst) const {
+        for (int i = 0; i < rows; ++i) std::memcpy(dst.data + i * dst.step, data + i * step, cols * elemSize());
+    }
 };
 
 class _InputArray {

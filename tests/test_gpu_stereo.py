@@ -160,3 +160,54 @@ def test_stereo_from_rgbd_host_and_batch(oracle_mod):
         assert np.array_equal(ur.view(np.uint32), our.view(np.uint32))
         assert np.array_equal(dp.view(np.uint32), odp.view(np.uint32))
         assert kept == int((odp > 0).sum())
+
+
+def _read_kps(buf, off):
+    from orb_slam_2_ros_amd import KEYPOINT_DTYPE
+    n = int(np.frombuffer(buf, np.int32, 1, off)[0])
+    off += 4
+    k = np.frombuffer(buf, KEYPOINT_DTYPE, n, off)
+    off += 28 * n
+    d = np.frombuffer(buf, np.uint8, 32 * n, off).reshape(n, 32)
+    return k, d, off + 32 * n
+
+
+def test_cpp_adapter_stereo_and_rgbd(tmp_path, oracle_mod):
+    """OrbxFrame::ComputeStereoMatches / ComputeStereoFromRGBD of the C++
+    drop-in (include/orbx_orbslam2.hpp) vs the oracle."""
+    import subprocess
+    from cxx_build import build_adapter_test
+    exe = build_adapter_test()
+    w, h, bf, fx = 752, 480, 47.9, 435.2
+    L, R = synth.stereo_pair(w, h, 80, 0, 20)
+    (tmp_path / "l.raw").write_bytes(L.tobytes())
+    (tmp_path / "r.raw").write_bytes(R.tobytes())
+    mb = _mb(bf, fx)
+    subprocess.run([str(exe), "stereo", str(w), str(h), str(tmp_path / "l.raw"), str(tmp_path / "r.raw"), repr(bf),
+                    repr(mb), str(tmp_path / "s.bin")], check=True)
+    buf = (tmp_path / "s.bin").read_bytes()
+    kl, dl, off = _read_kps(buf, 0)
+    kr, dr, off = _read_kps(buf, off)
+    kept = int(np.frombuffer(buf, np.int32, 1, off)[0])
+    ur = np.frombuffer(buf, np.float32, len(kl), off + 4)
+    dp = np.frombuffer(buf, np.float32, len(kl), off + 4 + 4 * len(kl))
+    # the adapter parses mbf / mb with atof -> float, as the test does
+    our, odp, okept = oracle_mod.compute_stereo_matches(oracle_mod.pyramid(L), oracle_mod.pyramid(R), kl, dl, kr, dr,
+                                                        float(np.float32(bf)), float(np.float32(mb)))
+    assert kept == okept and kept > 0
+    assert np.array_equal(ur.view(np.uint32), our.view(np.uint32))
+    assert np.array_equal(dp.view(np.uint32), odp.view(np.uint32))
+
+    img = synth.frame(w, h, 81)
+    dm = synth.depth_map(w, h, 81)
+    (tmp_path / "i.raw").write_bytes(img.tobytes())
+    (tmp_path / "d.raw").write_bytes(dm.tobytes())
+    subprocess.run([str(exe), "rgbd", str(w), str(h), str(tmp_path / "i.raw"), str(tmp_path / "d.raw"), repr(bf),
+                    str(tmp_path / "g.bin")], check=True)
+    buf = (tmp_path / "g.bin").read_bytes()
+    k, _, off = _read_kps(buf, 0)
+    ur = np.frombuffer(buf, np.float32, len(k), off)
+    dp = np.frombuffer(buf, np.float32, len(k), off + 4 * len(k))
+    our, odp = oracle_mod.stereo_from_rgbd(k, dm, float(np.float32(bf)))
+    assert np.array_equal(ur.view(np.uint32), our.view(np.uint32))
+    assert np.array_equal(dp.view(np.uint32), odp.view(np.uint32))
