@@ -94,6 +94,37 @@ def cpu_baseline(w: int, h: int, nfeatures: int, budget_s: float):
             "sample": f"{n} consecutive {w}x{h} synthetic frames ({el:.1f} s), oracle/liborbx_oracle.so, 1 thread"}
 
 
+def timed_region(step, steps, warmup, sync, dist, world, on_start=None):
+    """W untimed warmup steps, then EXACTLY `steps` timed steps bracketed by a
+    barrier + device sync on both sides.  Returns this rank's elapsed seconds."""
+    k = 0
+    for _ in range(warmup):
+        step(k); k += 1
+    sync()
+    if world > 1:
+        dist.barrier()
+    if on_start is not None:
+        on_start()
+    sync()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(k); k += 1
+    sync()
+    if world > 1:
+        dist.barrier()
+    return time.perf_counter() - t0
+
+
+def max_over_ranks(torch, dist, world, el, device):
+    """The slowest rank's elapsed time (whole-job throughput divides by it)."""
+    t = torch.tensor([el], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def _resident_frames(mode, w, h, batch, rank):
     """Host array [FRAMES_PER_STREAM, frames_per_step, h, w] (+ depth maps for RGB-D)."""
     from orb_slam_2_ros_amd import synth
@@ -145,23 +176,9 @@ def run_config(torch, dist, rank, world, dev, w, h, nfeatures, batch, steps, war
         else:
             ex.rgbd_step_device(frames[t].data_ptr(), fstride, w, batch, dmaps.data_ptr(), 4 * fstride, 4 * w, bf, sp)
 
-    k = 0
-    for _ in range(max(warmup, 2)):
-        step(k); k += 1
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    ex.set_profiling(profile)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step(k); k += 1
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
+    sync = lambda: torch.cuda.synchronize(dev)   # noqa: E731
+    el = timed_region(step, steps, max(warmup, 2), sync, dist, world,
+                      on_start=lambda: ex.set_profiling(profile))
     stages = ex.stage_times() if profile else None
     ex.set_profiling(False)
     # sanity: the last step produced keypoints and matches / depths on stream 0
@@ -170,11 +187,9 @@ def run_config(torch, dist, rank, world, dev, w, h, nfeatures, batch, steps, war
         _, sane = ex.mono_matches_download(0)
     else:
         _, _, sane = ex.depth_download(0)
-    t_el = torch.tensor([el], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t_el, op=dist.ReduceOp.MAX)
+    el = max_over_ranks(torch, dist, world, el, dev)
     ex.close()
-    return float(t_el.item()), stages, len(kp), sane
+    return el, stages, len(kp), sane
 
 
 EXTRAS = [
