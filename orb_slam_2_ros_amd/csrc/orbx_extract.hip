@@ -304,34 +304,28 @@ __global__ __launch_bounds__(kThreads) void k_blur(DevPlan p, FrameBufs fb) {
 // no keypoint survived at iniThFAST, ORBextractor.cc:846-850).
 // Output: keypoints in row-major order, packed (x | y<<12 | s<<24).
 // ===========================================================================
-__device__ inline bool has_run9(uint32_t m16) {
-    const uint32_t m = m16 | (m16 << 16);
-    uint32_t a = m & (m >> 1);
-    a &= a >> 2;
-    a &= a >> 4;
-    a &= m >> 8;
-    return (a & 0xFFFFu) != 0;
-}
+// max over the 16 arcs of 9 of max(min(p) - v, v - max(p)) for circle bytes p.
+// Lane pair (p, 255 - p): the minimum of the second half is 255 - max(p).
+// Equal to OpenCV's cornerScore<16> arc order (its even-anchored pairs of
+// arcs cover all 16 starts); min / max are exact, so any order agrees.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
-// max over the 16 arcs of 9 of max(min d, min -d), d[k] = v - circle[k]:
-// the order of OpenCV's cornerScore<16> (arcs anchored at even k).  Dark and
-// bright arcs run side by side as packed 16-bit lanes (d, -d).
-typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ inline u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
 
-__device__ inline int arc_score16(const int d[16]) {
-    s16x2 e[16];
+__device__ inline int arc_score_bytes(const int p[16], int v) {
+    u16x2 e[16], m2[16], m4[16], m8[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) e[k] = (s16x2){(short)d[k], (short)(-d[k])};
-    s16x2 q0 = (s16x2){-1000, -1000};
+    for (int k = 0; k < 16; ++k) e[k] = as_u16x2((uint32_t)p[k] + ((uint32_t)(255 - p[k]) << 16));
 #pragma unroll
-    for (int k = 0; k < 16; k += 2) {
-        s16x2 a = __builtin_elementwise_min(e[(k + 1) & 15], e[(k + 2) & 15]);
+    for (int k = 0; k < 16; ++k) m2[k] = __builtin_elementwise_min(e[k], e[(k + 1) & 15]);
 #pragma unroll
-        for (int t = 3; t <= 8; ++t) a = __builtin_elementwise_min(a, e[(k + t) & 15]);
-        q0 = __builtin_elementwise_max(q0, __builtin_elementwise_max(__builtin_elementwise_min(a, e[k & 15]),
-                                                                     __builtin_elementwise_min(a, e[(k + 9) & 15])));
-    }
-    return max((int)q0.x, (int)q0.y);
+    for (int k = 0; k < 16; ++k) m4[k] = __builtin_elementwise_min(m2[k], m2[(k + 2) & 15]);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) m8[k] = __builtin_elementwise_min(m4[k], m4[(k + 4) & 15]);
+    u16x2 best = __builtin_elementwise_min(m8[0], e[8]);
+#pragma unroll
+    for (int k = 1; k < 16; ++k) best = __builtin_elementwise_max(best, __builtin_elementwise_min(m8[k], e[(k + 8) & 15]));
+    return max((int)best.x - v, v - (255 - (int)best.y));
 }
 
 __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb) {
@@ -367,8 +361,9 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb) {
     const uint64_t below = (1ull << lane) - 1;
 
     // A. compass pre-test at the lower threshold: an arc of 9 covers two cyclically
-    //    adjacent points of {0, 4, 8, 12}, so pixels without such a pair are
-    //    not corners at any threshold >= the lower threshold.  Survivors are compacted.
+    //    adjacent points of {0, 4, 8, 12}, so a pixel is a corner candidate only if
+    //    some adjacent pair is all brighter (min of the pair > v + lo) or all
+    //    darker (max of the pair < v - lo).  Survivors are compacted.
     const int dyc = div_small(64, cw), dxc = 64 - dyc * cw;
     int yy = div_small(lane, cw), xx = lane - yy * cw;
     int nsurv = 0;
@@ -378,11 +373,9 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb) {
             const uint8_t *q = pc + yy * PS + xx;
             const int v = q[0];
             const int a0 = q[3 * PS], a4 = q[3], a8 = q[-3 * PS], a12 = q[-3];
-            const uint32_t br = (uint32_t)(a0 - v > lo) | ((uint32_t)(a4 - v > lo) << 1) |
-                                ((uint32_t)(a8 - v > lo) << 2) | ((uint32_t)(a12 - v > lo) << 3);
-            const uint32_t dk = (uint32_t)(v - a0 > lo) | ((uint32_t)(v - a4 > lo) << 1) |
-                                ((uint32_t)(v - a8 > lo) << 2) | ((uint32_t)(v - a12 > lo) << 3);
-            surv = ((br & ((br >> 1) | (br << 3))) | (dk & ((dk >> 1) | (dk << 3)))) != 0;
+            const int hi_pair = max(max(min(a0, a4), min(a8, a12)), max(min(a4, a8), min(a12, a0)));
+            const int lo_pair = min(min(max(a0, a4), max(a8, a12)), min(max(a4, a8), max(a12, a0)));
+            surv = (hi_pair > v + lo) | (lo_pair < v - lo);
         }
         const uint64_t m = __ballot(surv);
         if (surv) list[nsurv + __popcll(m & below)] = (uint16_t)((yy << 8) | xx);
@@ -392,50 +385,34 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb) {
     }
     wave_lds_fence();
 
-    // B1. full 16-point test on survivors; corners are compacted in place
-    //     (a corner's slot never passes the survivors already read).
-#define ORBX_CIRCLE_DIFFS(q, v, d)                                                                    \
-    d[0] = v - q[3 * PS];       d[1] = v - q[3 * PS + 1];  d[2] = v - q[2 * PS + 2];  d[3] = v - q[PS + 3];  \
-    d[4] = v - q[3];            d[5] = v - q[-PS + 3];     d[6] = v - q[-2 * PS + 2]; d[7] = v - q[-3 * PS + 1]; \
-    d[8] = v - q[-3 * PS];      d[9] = v - q[-3 * PS - 1]; d[10] = v - q[-2 * PS - 2]; d[11] = v - q[-PS - 3]; \
-    d[12] = v - q[-3];          d[13] = v - q[PS - 3];     d[14] = v - q[2 * PS - 2]; d[15] = v - q[3 * PS - 1];
+    // B. arc score of every survivor: S = max(M1 - v, v - M2), M1 = max over the
+    //    16 nine-pixel arcs of the arc's minimum, M2 = min over arcs of the arc's
+    //    maximum.  Both run side by side as packed u16 lanes (p, 255 - p) through
+    //    sliding-window minima (2, 4, 8, 9).  The pixel is a corner at lo iff
+    //    S > lo; its score S - 1 goes to the map and corners are compacted in
+    //    place (a corner's slot never passes the survivors already read).
     int ncorner = 0;
     for (int i0 = 0; i0 < nsurv; i0 += 64) {
         bool corner = false;
         int e = 0;
         if (i0 + lane < nsurv) {
             e = list[i0 + lane];
-            const uint8_t *q = pc + (e >> 8) * PS + (e & 0xFF);
+            const int ey = e >> 8, ex = e & 0xFF;
+            const uint8_t *q = pc + ey * PS + ex;
             const int v = q[0];
-            int d[16];
-            ORBX_CIRCLE_DIFFS(q, v, d)
-            uint32_t dark = 0, bright = 0;
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                dark |= (uint32_t)(d[k] > lo) << k;
-                bright |= (uint32_t)(d[k] < -lo) << k;
-            }
-            corner = has_run9(dark) || has_run9(bright);
+            const int pr[16] = {q[3 * PS],  q[3 * PS + 1],  q[2 * PS + 2],  q[PS + 3],
+                                q[3],       q[-PS + 3],     q[-2 * PS + 2], q[-3 * PS + 1],
+                                q[-3 * PS], q[-3 * PS - 1], q[-2 * PS - 2], q[-PS - 3],
+                                q[-3],      q[PS - 3],      q[2 * PS - 2],  q[3 * PS - 1]};
+            const int S = arc_score_bytes(pr, v);
+            corner = S > lo;
+            if (corner) scm[(ey + 1) * SW + ex + 1] = (uint8_t)(S - 1);
         }
         const uint64_t m = __ballot(corner);
         wave_lds_fence();   // all survivor reads of this chunk precede the in-place writes
         if (corner) list[ncorner + __popcll(m & below)] = (uint16_t)e;
         ncorner += __popcll(m);
     }
-    wave_lds_fence();
-    // B2. arc score S of each corner (dense: one corner per lane)
-    for (int i0 = 0; i0 < ncorner; i0 += 64) {
-        if (i0 + lane < ncorner) {
-            const int e = list[i0 + lane];
-            const int ey = e >> 8, ex = e & 0xFF;
-            const uint8_t *q = pc + ey * PS + ex;
-            const int v = q[0];
-            int d[16];
-            ORBX_CIRCLE_DIFFS(q, v, d)
-            scm[(ey + 1) * SW + ex + 1] = (uint8_t)(arc_score16(d) - 1);
-        }
-    }
-#undef ORBX_CIRCLE_DIFFS
     wave_lds_fence();
 
     // C. NMS on the corners, both thresholds at once, compacted in row-major
