@@ -804,11 +804,11 @@ __global__ __launch_bounds__(kThreads) void k_quadtree(DevPlan p, FrameBufs fb) 
 // ===========================================================================
 constexpr int kDescR = 21;                  // patch radius = 18 (samples) + 3 (blur taps)
 constexpr int kDescP = 2 * kDescR + 1;      // 43
-constexpr int kDescPS = 48;                 // patch row stride (bytes, dword rows + align offset)
+constexpr int kDescPS = 52;                 // patch row stride (bytes): 43 + align offset + row-pass overread
 constexpr int kBlurR = 18;
-constexpr int kBlurN = 2 * kBlurR + 1;      // 37
-constexpr int kRowS = 38;                   // row-pass stride (u16)
-constexpr int kDescWaveLds = kDescP * kDescPS + kDescP * kRowS * 2;   // 5332 B
+constexpr int kRowS = 40;                   // row-pass stride (u16): 10 groups of 4 outputs
+constexpr int kDescRowOff = (kDescP * kDescPS + 15) & ~15;          // row-pass buffer, 16-aligned
+constexpr int kDescWaveLds = kDescRowOff + kDescP * kRowS * 2;        // 5680 B
 
 __global__ __launch_bounds__(kThreads) void k_describe(DevPlan p, FrameBufs fb) {
     __shared__ __align__(16) uint8_t lds[4 * ((kDescWaveLds + 15) & ~15)];
@@ -832,7 +832,7 @@ __global__ __launch_bounds__(kThreads) void k_describe(DevPlan p, FrameBufs fb) 
     const int x = (int)(key & 0xFFF), y = (int)((key >> 12) & 0xFFF), score = (int)(key >> 24);
 
     uint8_t *lbase = lds + wave * ((kDescWaveLds + 15) & ~15);
-    uint16_t *rowp = reinterpret_cast<uint16_t *>(lbase + kDescP * kDescPS);
+    uint16_t *rowp = reinterpret_cast<uint16_t *>(lbase + kDescRowOff);
 
     // 1. stage the 43x43 unblurred neighbourhood: aligned dword loads when it
     //    lies inside the level, else byte loads with reflect-101 at the borders
@@ -878,18 +878,29 @@ __global__ __launch_bounds__(kThreads) void k_describe(DevPlan p, FrameBufs fb) 
     //    OpenCV 3.2's per-column rounding (half-even below w & ~3, else half-up).
     // taps of getGaussianKernel(7, 2) x256 (checked against the plan on the host)
     constexpr int k0 = kGaussTaps[0], k1 = kGaussTaps[1], k2 = kGaussTaps[2], k3 = kGaussTaps[3];
-    for (int t = lane; t < kDescP * 5; t += 64) {
-        const int r = t / 5, seg = t - r * 5;
-        const int c0 = seg * 8, n = min(8, kBlurN - c0);
-        const uint8_t *q = patch + r * kDescPS + c0;   // patch col (3 + c) - 3 = c for blur col c
-        int w[14];
+    // Taps as byte vectors for v_dot4_u32_u8: out[j] = dot4(px[j..j+3], W0) + dot4(px[j+4..j+7], W1).
+    constexpr uint32_t kW0 = (uint32_t)kGaussTaps[0] | (uint32_t)kGaussTaps[1] << 8 |
+                             (uint32_t)kGaussTaps[2] << 16 | (uint32_t)kGaussTaps[3] << 24;
+    constexpr uint32_t kW1 = (uint32_t)kGaussTaps[4] | (uint32_t)kGaussTaps[5] << 8 | (uint32_t)kGaussTaps[6] << 16;
+    // One task = 4 consecutive outputs (columns 4s..4s+3) of one row: three
+    // realigned dwords hold the 10 source bytes; outputs 37..39 are padding.
+    for (int t = lane; t < kDescP * 10; t += 64) {
+        const int r = (t * 205) >> 11, sgi = t - r * 10;   // t / 10 for t < 1024
+        const uint32_t *ap = reinterpret_cast<const uint32_t *>(lbase + r * kDescPS + 4 * sgi);
+        const uint32_t d0 = ap[0], d1 = ap[1], d2 = ap[2], d3 = ap[3];
+        const uint32_t e0 = __builtin_amdgcn_alignbyte(d1, d0, o), e1 = __builtin_amdgcn_alignbyte(d2, d1, o),
+                       e2 = __builtin_amdgcn_alignbyte(d3, d2, o);
+        uint32_t out[4];
 #pragma unroll
-        for (int j = 0; j < 14; ++j) w[j] = j < n + 6 ? q[j] : 0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            if (j < n)
-                rowp[r * kRowS + c0 + j] = (uint16_t)(mul24u(k0, w[j] + w[j + 6]) + mul24u(k1, w[j + 1] + w[j + 5]) +
-                                                      mul24u(k2, w[j + 2] + w[j + 4]) + mul24u(k3, w[j + 3]));
+        for (int m = 0; m < 4; ++m) {
+            const uint32_t lo4 = m ? __builtin_amdgcn_alignbyte(e1, e0, m) : e0;
+            const uint32_t hi4 = m ? __builtin_amdgcn_alignbyte(e2, e1, m) : e1;
+            out[m] = __builtin_amdgcn_udot4(lo4, kW0, __builtin_amdgcn_udot4(hi4, kW1, 0u, false), false);
+        }
+        uint2 packed;
+        packed.x = out[0] | (out[1] << 16);
+        packed.y = out[2] | (out[3] << 16);
+        *reinterpret_cast<uint2 *>(rowp + r * kRowS + 4 * sgi) = packed;
     }
     wave_lds_fence();
 
