@@ -62,6 +62,7 @@ struct MatchBufs {
     float nnratio;
     int check_ori;
     int reset_prev;           // 1: prev_xy := F1 keypoint positions before matching
+    long long *clocks;        // debug: phase timestamps of pair 0 (nullptr = off)
 };
 
 // Where a frame's pyramid lives: level 0 is the caller's image, levels >= 1

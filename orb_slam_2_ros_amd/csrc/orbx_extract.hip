@@ -13,6 +13,7 @@
 
 #include "orbx_device.h"
 #include "orbx_math.h"
+#include "orbx_wave.h"
 
 namespace orbx {
 
@@ -38,6 +39,24 @@ __device__ inline const uint8_t *level_ptr(const DevPlan &p, const FrameBufs &fb
     return fb.pyr + (int64_t)b * p.pyr_bytes + g.pyr_off;
 }
 
+// The dispatcher hands workgroup j (linear, x fastest) to XCD j % 8.  This
+// maps j to a logical block index so that each XCD runs a contiguous range of
+// logical blocks: consecutive blocks of one frame then share an XCD's L2
+// (overlapping cell rings / keypoint patches hit instead of refetching).
+constexpr int kXcds = 8;
+__device__ inline int xcd_logical_block(int j, int n) {
+    const int per = n / kXcds, rem = n % kXcds, xcd = j % kXcds, idx = j / kXcds;
+    return xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
+}
+
+// (x, y) of the logical block of a 2-D grid.
+__device__ inline void xcd_block_2d(int &bx, int &by) {
+    const int n = gridDim.x * gridDim.y;
+    const int L = xcd_logical_block(blockIdx.y * gridDim.x + blockIdx.x, n);
+    by = L / gridDim.x;
+    bx = L - by * gridDim.x;
+}
+
 __device__ inline int reflect101(int v, int n) {
     // BORDER_REFLECT_101 for the 3-px halo of a >= 4 px image.
     v = v < 0 ? -v : v;
@@ -49,28 +68,6 @@ __device__ inline uint32_t pack_key(int x, int y, int score) {
 }
 
 // ---- wave / block helpers (wave64) ----------------------------------------
-__device__ inline uint64_t shfl_up_u64(uint64_t v, int d) {
-    const int lo = __shfl_up((int)(uint32_t)v, d, 64);
-    const int hi = __shfl_up((int)(uint32_t)(v >> 32), d, 64);
-    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
-}
-
-__device__ inline uint64_t wave_incl_scan_u64(uint64_t v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t o = shfl_up_u64(v, d);
-        if (lane >= d) v += o;
-    }
-    return v;
-}
-
-__device__ inline int wave_sum_i32(int v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-    return v;
-}
-
 // Exclusive scan of a[0..m) (uint64) in LDS by the whole 256-thread block.
 // ws: 4 uint64 of LDS scratch.  Returns the total.  Ends with a barrier.
 __device__ uint64_t block_excl_scan_u64(uint64_t *a, int m, uint64_t *ws) {
@@ -100,12 +97,7 @@ __device__ uint64_t block_excl_scan_u64(uint64_t *a, int m, uint64_t *ws) {
 // Exclusive scan of one int per thread across the block; returns total.
 __device__ int block_excl_scan_i32(int v, int *total, int *ws) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    int incl = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int o = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += o;
-    }
+    const int incl = wave_incl_scan_i32(v);
     if (lane == 63) ws[wave] = incl;
     __syncthreads();
     int base = 0, tot = 0;
@@ -181,8 +173,11 @@ __global__ __launch_bounds__(kThreads) void k_resize(DevPlan p, FrameBufs fb, in
     __shared__ uint8_t win[kResRows * kResCols];
     const LevelGeom g = p.lv[l];
     const LevelGeom gs = p.lv[l - 1];
-    const int b = blockIdx.z, tid = threadIdx.x;
-    const int x0 = blockIdx.x * kResTW, y0 = blockIdx.y * kResTH;
+    const int tid = threadIdx.x;
+    const int L = xcd_logical_block((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x,
+                                    gridDim.x * gridDim.y * gridDim.z);
+    const int bxy = L % (gridDim.x * gridDim.y), b = L / (gridDim.x * gridDim.y);
+    const int x0 = (bxy % gridDim.x) * kResTW, y0 = (bxy / gridDim.x) * kResTH;
     const ResizeTap *xt = p.xtaps + g.xtab_off;
     const ResizeTap *yt = p.ytaps + g.ytab_off;
     // this thread's taps: 4 columns x kResRowsPerThread rows, fetched before the
@@ -331,7 +326,9 @@ __device__ inline int arc_score_bytes(const int p[16], int v) {
 __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb) {
     extern __shared__ __align__(16) uint8_t lds[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int ci = blockIdx.x * 4 + wave, b = blockIdx.y;
+    int bx, b;
+    xcd_block_2d(bx, b);
+    const int ci = bx * 4 + wave;
     if (ci >= p.ncells) return;
     const Cell c = p.cells[ci];
     int32_t *count_out = fb.cell_count + (int64_t)b * p.ncells + ci;
@@ -812,14 +809,16 @@ constexpr int kDescWaveLds = kDescRowOff + kDescP * kRowS * 2;        // 5680 B
 
 __global__ __launch_bounds__(kThreads) void k_describe(DevPlan p, FrameBufs fb) {
     __shared__ __align__(16) uint8_t lds[4 * ((kDescWaveLds + 15) & ~15)];
-    const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int bx, b;
+    xcd_block_2d(bx, b);
     const int32_t *lc = fb.level_count + (int64_t)b * kMaxLevels;
-    if (blockIdx.x == 0 && tid == 0) {
+    if (bx == 0 && tid == 0) {
         int total = 0;
         for (int l = 0; l < p.nlevels; ++l) total += max(lc[l], 0);
         fb.nkps[b] = total;
     }
-    const int slot = blockIdx.x * 4 + wave;
+    const int slot = bx * 4 + wave;
     if (slot >= p.out_cap) return;
     int l = 0;
     while (l + 1 < p.nlevels && slot >= p.lv[l + 1].out_off) ++l;

@@ -16,9 +16,11 @@
 // minimum.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <climits>
 
 #include "orbx_device.h"
+#include "orbx_wave.h"
 
 namespace orbx {
 namespace {
@@ -30,27 +32,6 @@ constexpr int kThLow = 50;                      // ORBmatcher::TH_LOW
 constexpr int kSkip = 0xFFFF;
 constexpr int kMT = 1024;                       // threads per frame pair
 constexpr int kMW = kMT / 64;                   // waves
-
-__device__ inline int wave_incl_scan_i32(int v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int o = __shfl_up(v, d, 64);
-        if (lane >= d) v += o;
-    }
-    return v;
-}
-
-__device__ inline uint64_t wave_min_u64(uint64_t v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, d, 64);
-        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), d, 64);
-        const uint64_t o = ((uint64_t)hi << 32) | lo;
-        v = o < v ? o : v;
-    }
-    return v;
-}
 
 // LDS layout of one frame pair (16-B aligned arrays first).
 struct MLds {
@@ -66,6 +47,8 @@ struct MLds {
     int *qrank;      // n1cap: rank among octave-0 queries, or -1
     int *qcount;     // maxq: candidate-list length
     uint32_t *top4;  // maxq x 4: (i2 << 16 | dist) of the 4 smallest (dist, position)
+    int *qbase;      // maxq: list start in `pool`, or -1 when the list lives in global scratch
+    uint32_t *pool;  // pool_cap candidate-list entries (i2 << 16 | dist)
     int16_t *kcell;  // n2cap: grid cell of each F2 keypoint (-1: none)
     int16_t *glist;  // maxc: F2 index by grid position
     int16_t *qidx;   // maxq: F1 index of each query
@@ -73,7 +56,7 @@ struct MLds {
     int8_t *rbin;    // n1cap: rotation bin of accepted queries (-1: none)
 };
 
-__device__ inline MLds carve(uint8_t *ptr, int n1cap, int n2cap, int maxq, int maxc) {
+__device__ inline MLds carve(uint8_t *ptr, int n1cap, int n2cap, int maxq, int maxc, int pool_cap) {
     MLds s;
     s.gd = reinterpret_cast<uint4 *>(ptr); ptr += sizeof(uint4) * 2 * maxc;
     s.qd = reinterpret_cast<uint4 *>(ptr); ptr += sizeof(uint4) * 2 * maxq;
@@ -87,6 +70,8 @@ __device__ inline MLds carve(uint8_t *ptr, int n1cap, int n2cap, int maxq, int m
     s.qrank = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * n1cap;
     s.qcount = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * maxq;
     s.top4 = reinterpret_cast<uint32_t *>(ptr); ptr += sizeof(uint32_t) * 4 * maxq;
+    s.qbase = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * maxq;
+    s.pool = reinterpret_cast<uint32_t *>(ptr); ptr += sizeof(uint32_t) * pool_cap;
     s.kcell = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * n2cap;
     s.glist = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * ((maxc + 1) & ~1);
     s.qidx = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * ((maxq + 1) & ~1);
@@ -116,7 +101,8 @@ __device__ inline int block_scan_i32(int v, int *total, int *ws) {
     return base + incl - v;
 }
 
-__global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, int n2cap, int maxq, int maxc) {
+__global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, int n2cap, int maxq, int maxc,
+                                                     int pool_cap) {
     extern __shared__ __align__(16) uint8_t lds[];
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const orbx_keypoint *k1 = mb.k1 + (int64_t)b * mb.k1_stride;
@@ -127,11 +113,11 @@ __global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, i
     float *prev = mb.prev_xy + (int64_t)b * mb.k1_stride * 2;
     int32_t *out12 = mb.matches12 + (int64_t)b * mb.k1_stride;
     uint32_t *scratch = mb.scratch + (int64_t)b * mb.scratch_stride;
-    const MLds s = carve(lds, n1cap, n2cap, maxq, maxc);
+    const MLds s = carve(lds, n1cap, n2cap, maxq, maxc, pool_cap);
     __shared__ int hist[kHisto];
     __shared__ int ws[kMW];
     __shared__ int sh_top[3];
-    __shared__ int sh_err, sh_nq;
+    __shared__ int sh_err, sh_nq, sh_pool;
 
     // Frame grid constants for an undistorted img_w x img_h image
     // (Frame.cc:218-220, ComputeImageBounds with k1 == 0).
@@ -139,6 +125,8 @@ __global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, i
     const float invW = __fdiv_rn((float)kGridCols, __fsub_rn(maxX, minX));
     const float invH = __fdiv_rn((float)kGridRows, __fsub_rn(maxY, minY));
     const float r = (float)mb.window;
+    const bool clk = mb.clocks && b == 0 && tid == 0;
+    if (clk) { mb.clocks[0] = clock64(); mb.clocks[6] = 0; mb.clocks[7] = 0; }
 
     // ---- 0. init
     for (int i = tid; i <= kGridCells; i += kMT) s.gstart[i] = 0;
@@ -146,11 +134,12 @@ __global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, i
     for (int i = tid; i < n2; i += kMT) { s.mdist[i] = INT_MAX; s.m21[i] = -1; }
     for (int i = tid; i < n1; i += kMT) { s.m12[i] = -1; s.rbin[i] = -1; s.acc[i] = -1; }
     if (tid < kHisto) hist[tid] = 0;
-    if (tid == 0) sh_err = 0;
+    if (tid == 0) { sh_err = 0; sh_pool = 0; }
     if (mb.reset_prev) {
         for (int i = tid; i < n1; i += kMT) { prev[2 * i] = k1[i].x; prev[2 * i + 1] = k1[i].y; }
     }
     __syncthreads();
+    if (clk) mb.clocks[1] = clock64();
 
     // ---- 1. F2 grid of octave-0 keypoints (PosInGrid uses round(), Frame.cc:417-418)
     for (int i = tid; i < n2; i += kMT) {
@@ -232,11 +221,13 @@ __global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, i
     }
     __syncthreads();
     const int nq = sh_nq;
+    if (clk) mb.clocks[2] = clock64();
 
     // ---- 2. candidate lists + distances, all from LDS.  GetFeaturesInArea
     //         visits ix outer, iy inner, then cell insertion order; glist is
     //         sorted by cell = ix * 48 + iy and index, so the window's list is
     //         one contiguous glist range per grid column ix.  Lane = column.
+    //         A list goes to the LDS pool when it fits, else to global scratch.
     for (int q = wave; q < nq; q += kMW) {
         const float2 c = s.qxy[q];
         const float x = c.x, y = c.y;
@@ -244,21 +235,30 @@ __global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, i
         const int cx1 = min(kGridCols - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(x, minX), r), invW)));
         const int cy0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(y, minY), r), invH)));
         const int cy1 = min(kGridRows - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(y, minY), r), invH)));
-        int written = 0;
-        uint64_t t4[4] = {~0ull, ~0ull, ~0ull, ~0ull};   // this lane's 4 smallest (dist, position, i2)
-        if (!(cx0 >= kGridCols || cx1 < 0 || cy0 >= kGridRows || cy1 < 0 || cx1 < cx0 || cy1 < cy0)) {
+        const bool empty = cx0 >= kGridCols || cx1 < 0 || cy0 >= kGridRows || cy1 < 0 || cx1 < cx0 || cy1 < cy0;
+        const int ncx = cx1 - cx0 + 1;   // <= 64 grid columns
+        int st = 0, cnt = 0;
+        if (!empty && lane < ncx) {
+            const int col = (cx0 + lane) * kGridRows;
+            st = s.gstart[col + cy0];
+            cnt = max(min(s.gstart[col + cy1 + 1], maxc) - st, 0);
+        }
+        const int incl = wave_incl_scan_i32(cnt);
+        const int pos0 = incl - cnt;
+        int written = __builtin_amdgcn_readlane(incl, 63);
+        if (written > maxc) { if (lane == 0) sh_err = 1; written = maxc; }
+        int base = -1;
+        if (lane == 0 && written > 0) {
+            base = atomicAdd(&sh_pool, written);
+            if (base + written > pool_cap) base = -1;
+        }
+        base = __builtin_amdgcn_readfirstlane(base);
+        uint32_t *list = base >= 0 ? s.pool + base : scratch + (int64_t)q * maxc;
+        // this lane's 4 smallest (dist << 16 | list position) and their i2
+        uint32_t tk[4] = {~0u, ~0u, ~0u, ~0u};
+        int ti[4] = {0, 0, 0, 0};
+        if (cnt > 0) {
             const uint4 qa = s.qd[2 * q], qb = s.qd[2 * q + 1];
-            uint32_t *list = scratch + (int64_t)q * maxc;
-            const int ncx = cx1 - cx0 + 1;   // <= 64 grid columns
-            int st = 0, cnt = 0;
-            if (lane < ncx) {
-                const int col = (cx0 + lane) * kGridRows;
-                st = s.gstart[col + cy0];
-                cnt = max(min(s.gstart[col + cy1 + 1], maxc) - st, 0);
-            }
-            const int incl = wave_incl_scan_i32(cnt);
-            const int pos0 = incl - cnt;
-            written = __shfl(incl, 63, 64);
             for (int e = 0; e < cnt; ++e) {
                 const int gp = st + e;
                 const int i2 = s.glist[gp];
@@ -268,44 +268,54 @@ __global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, i
                 if (fabsf(dx) < r && fabsf(dy) < r) dist = hamming_regs(qa, qb, s.gd[2 * gp], s.gd[2 * gp + 1]);
                 if (pos0 + e < maxc) list[pos0 + e] = ((uint32_t)i2 << 16) | (uint32_t)dist;
                 if (dist != kSkip) {
-                    uint64_t k = ((uint64_t)dist << 32) | ((uint64_t)(pos0 + e) << 16) | (uint32_t)i2;
+                    uint32_t k = ((uint32_t)dist << 16) | (uint32_t)(pos0 + e);
+                    int ki = i2;
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        if (k < t4[j]) { const uint64_t tmp = t4[j]; t4[j] = k; k = tmp; }
+                        if (k < tk[j]) {
+                            const uint32_t t = tk[j]; tk[j] = k; k = t;
+                            const int u = ti[j]; ti[j] = ki; ki = u;
+                        }
                     }
                 }
             }
         }
-        if (written > maxc) { if (lane == 0) sh_err = 1; written = maxc; }
         // wave-wide 4 smallest: pop the minimum head four times
         for (int j = 0; j < 4; ++j) {
-            const uint64_t mn = wave_min_u64(t4[0]);
-            if (t4[0] == mn && mn != ~0ull) { t4[0] = t4[1]; t4[1] = t4[2]; t4[2] = t4[3]; t4[3] = ~0ull; }
-            if (lane == 0)
-                s.top4[4 * q + j] = mn == ~0ull ? 0xFFFFFFFFu
-                                                : (((uint32_t)mn & 0xFFFFu) << 16) | (uint32_t)(mn >> 32);
+            const uint32_t mn = wave_min_u32(tk[0]);
+            const bool mine = tk[0] == mn && mn != ~0u;
+            const uint64_t who = __ballot(mine);
+            int i2 = 0;
+            if (who) i2 = __builtin_amdgcn_readlane(ti[0], (int)__builtin_ctzll(who));
+            if (mine) { tk[0] = tk[1]; tk[1] = tk[2]; tk[2] = tk[3]; tk[3] = ~0u; ti[0] = ti[1]; ti[1] = ti[2]; ti[2] = ti[3]; }
+            if (lane == 0) s.top4[4 * q + j] = mn == ~0u ? 0xFFFFFFFFu : ((uint32_t)i2 << 16) | (mn >> 16);
         }
-        if (lane == 0) s.qcount[q] = written;
+        if (lane == 0) { s.qcount[q] = written; s.qbase[q] = base; }
     }
     __syncthreads();
+    if (clk) mb.clocks[3] = clock64();
 
     // ---- 3. ordered greedy replay (ORBmatcher.cc:425-491), wave 0 only.
     // The valid entries (vMatchedDistance[i2] > dist) among a query's 4
     // smallest (dist, position) entries, in order, are the smallest valid ones
     // of its whole list: two found decide (best, best2); a list that fits in 4
     // is decided too; otherwise the list is scanned 64 entries at a time.
+    // Queries whose smallest distance exceeds TH_LOW can never be accepted and
+    // change no state, so they are skipped.
     if (wave == 0) {
         for (int g0 = 0; g0 < nq; g0 += 64) {
           // this group's static query data, one query per lane
           const int gq = min(g0 + lane, nq - 1);
           const uint32_t r0 = s.top4[4 * gq], r1 = s.top4[4 * gq + 1], r2 = s.top4[4 * gq + 2],
                          r3 = s.top4[4 * gq + 3];
-          const int rc = s.qcount[gq], ri = s.qidx[gq];
-          const int gn = min(64, nq - g0);
-          for (int j = 0; j < gn; ++j) {
+          const int rc = s.qcount[gq], ri = s.qidx[gq], rb = s.qbase[gq];
+          const bool live = g0 + lane < nq && rc > 0 && r0 != 0xFFFFFFFFu && (int)(r0 & 0xFFFF) <= kThLow;
+          uint64_t todo = __ballot(live);
+          while (todo) {
+            const int j = (int)__builtin_ctzll(todo);
+            todo &= todo - 1;
             const int q = g0 + j;
             const int cnt = __builtin_amdgcn_readlane(rc, j);
-            if (cnt == 0) continue;
             const int i1 = __builtin_amdgcn_readlane(ri, j);
             const uint32_t e4[4] = {(uint32_t)__builtin_amdgcn_readlane((int)r0, j),
                                     (uint32_t)__builtin_amdgcn_readlane((int)r1, j),
@@ -313,7 +323,7 @@ __global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, i
                                     (uint32_t)__builtin_amdgcn_readlane((int)r3, j)};
             int md[4];
 #pragma unroll
-            for (int t = 0; t < 4; ++t) md[t] = e4[t] == 0xFFFFFFFFu ? 0 : s.mdist[e4[t] >> 16];
+            for (int t = 0; t < 4; ++t) md[t] = s.mdist[e4[t] == 0xFFFFFFFFu ? 0 : (e4[t] >> 16)];
             int best = INT_MAX, best2 = INT_MAX, best_i2 = -1;
             int found = 0;
 #pragma unroll
@@ -327,26 +337,27 @@ __global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, i
             }
             if (!(found == 2 || e4[3] == 0xFFFFFFFFu)) {
                 best = INT_MAX; best2 = INT_MAX; best_i2 = -1;
-                const uint32_t *list = scratch + (int64_t)q * maxc;
+                const int qb = __builtin_amdgcn_readlane(rb, j);
+                const uint32_t *list = qb >= 0 ? s.pool + qb : scratch + (int64_t)q * maxc;
                 for (int c0 = 0; c0 < cnt; c0 += 64) {
                     const int e = c0 + lane;
-                    uint64_t key = ~0ull;
-                    int dist = INT_MAX, i2 = -1;
+                    uint32_t key = ~0u;
+                    int dist = INT_MAX, i2 = 0;
                     if (e < cnt) {
                         const uint32_t v = list[e];
                         i2 = (int)(v >> 16);
                         dist = (int)(v & 0xFFFF);
                         if (dist == kSkip || s.mdist[i2] <= dist) dist = INT_MAX;
-                        else key = ((uint64_t)dist << 32) | (uint32_t)e;
+                        else key = ((uint32_t)dist << 16) | (uint32_t)e;
                     }
-                    const uint64_t mn = wave_min_u64(key);
-                    if (mn == ~0ull) continue;
-                    const int cb = (int)(mn >> 32);
-                    const int cb_lane = (int)(mn & 0xFFFFFFFF) - c0;
-                    const int cb_i2 = __shfl(i2, cb_lane, 64);
-                    const uint64_t key2 = (lane == cb_lane || dist == INT_MAX) ? ~0ull : (uint64_t)dist;
-                    const uint64_t mn2 = wave_min_u64(key2);
-                    const int cs = mn2 == ~0ull ? INT_MAX : (int)mn2;
+                    const uint32_t mn = wave_min_u32(key);
+                    if (mn == ~0u) continue;
+                    const int cb = (int)(mn >> 16);
+                    const int cb_lane = (int)(mn & 0xFFFF) - c0;
+                    const int cb_i2 = __builtin_amdgcn_readlane(i2, cb_lane);
+                    const uint32_t key2 = (lane == cb_lane || dist == INT_MAX) ? ~0u : (uint32_t)dist;
+                    const uint32_t mn2 = wave_min_u32(key2);
+                    const int cs = mn2 == ~0u ? INT_MAX : (int)mn2;
                     const int hi = best <= cb ? cb : best;
                     best2 = min(hi, min(best2, cs));
                     if (cb < best) best_i2 = cb_i2;
@@ -369,6 +380,7 @@ __global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, i
         }
     }
     __syncthreads();
+    if (clk) mb.clocks[4] = clock64();
 
     // ---- 4. rotation histogram of every accepted pair (rotHist, ORBmatcher.cc:475-483),
     //         ComputeThreeMaxima, consistency filter and outputs (:494-520)
@@ -418,23 +430,32 @@ __global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, i
     int total;
     block_scan_i32(local, &total, ws);
     if (tid == 0) mb.nmatches[b] = sh_err ? -1 : total;
+    if (clk) mb.clocks[5] = clock64();
 }
 
 }  // namespace
 
+// LDS of everything but the candidate-list pool.
 int match_lds_bytes(int n1cap, int n2cap, int maxq, int maxc) {
     return (int)(32 * (maxc + maxq) + 8 * (maxc + maxq) + sizeof(int) * (2 * kGridCells + 1) +
-                 sizeof(int) * (2 * n2cap + 2 * n1cap) + sizeof(int) * 5 * maxq + sizeof(int16_t) * n2cap +
-                 sizeof(int16_t) * ((maxc + 1) & ~1) + sizeof(int16_t) * ((maxq + 1) & ~1) + sizeof(int16_t) * ((n1cap + 1) & ~1) + n1cap + 64);
+                 sizeof(int) * (2 * n2cap + 2 * n1cap) + sizeof(int) * 6 * maxq + sizeof(int16_t) * n2cap +
+                 sizeof(int16_t) * ((maxc + 1) & ~1) + sizeof(int16_t) * ((maxq + 1) & ~1) +
+                 sizeof(int16_t) * ((n1cap + 1) & ~1) + n1cap + 64);
 }
 
+constexpr int kMatchLdsMax = 160 * 1024 - 1024;   // dynamic LDS; the kernel's static LDS needs < 1 KiB
+
 hipError_t launch_match(const MatchBufs &mb, int B, int n1cap, int n2cap, int maxq, int maxc, hipStream_t st) {
-    const int bytes = match_lds_bytes(n1cap, n2cap, maxq, maxc);
+    const int fixed = match_lds_bytes(n1cap, n2cap, maxq, maxc);
+    if (fixed > kMatchLdsMax) return hipErrorInvalidValue;
+    // candidate-list pool: the rest of the CU's LDS, at most every list at full length
+    const int pool_cap = (int)std::min<int64_t>((int64_t)maxq * maxc, (kMatchLdsMax - fixed) / 4);
+    const int bytes = fixed + 4 * pool_cap;
     if (bytes > 64 * 1024 &&
         hipFuncSetAttribute(reinterpret_cast<const void *>(k_search_init),
                             hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_search_init, dim3(B), dim3(kMT), bytes, st, mb, n1cap, n2cap, maxq, maxc);
+    hipLaunchKernelGGL(k_search_init, dim3(B), dim3(kMT), bytes, st, mb, n1cap, n2cap, maxq, maxc, pool_cap);
     return hipGetLastError();
 }
 

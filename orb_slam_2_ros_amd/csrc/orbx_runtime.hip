@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -665,8 +666,22 @@ int orbx_mono_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t f
     mb.nnratio = nnratio;
     mb.check_ori = check_ori;
     mb.reset_prev = 1;
+    mb.clocks = nullptr;
+    static const bool dbg_clocks = std::getenv("ORBX_MATCH_CLOCKS") != nullptr;
+    long long *dclk = nullptr;
+    if (dbg_clocks && hipMalloc(reinterpret_cast<void **>(&dclk), 8 * sizeof(long long)) == hipSuccess)
+        mb.clocks = dclk;
     if (launch_match(mb, batch, ex->plan.max_kps, ex->plan.max_kps, ex->l0cap, ex->l0cap, st) != hipSuccess)
         return ORBX_EIO;
+    if (dclk) {   // debug: phase cycle counts of pair 0
+        long long c[8] = {};
+        if (hipStreamSynchronize(st) == hipSuccess &&
+            hipMemcpy(c, dclk, sizeof(c), hipMemcpyDeviceToHost) == hipSuccess)
+            std::fprintf(stderr, "match phases (cycles): init %lld grid+queries %lld lists %lld replay %lld tail %lld; "
+                         "queries %lld fallbacks %lld\n",
+                         c[1] - c[0], c[2] - c[1], c[3] - c[2], c[4] - c[3], c[5] - c[4], c[7], c[6]);
+        (void)hipFree(dclk);
+    }
     mark(ex, kNumStages, st);
     mark_valid(ex, kStageMatch);
     ex->match_batch = batch;
@@ -938,7 +953,7 @@ int orbx_search_for_initialization(int device, const orbx_keypoint *k1, const ui
         mb.prev_xy = dprev; mb.matches12 = dm; mb.nmatches = dnm;
         mb.scratch = dscr; mb.scratch_stride = (int64_t)q * c;
         mb.img_w = img_w; mb.img_h = img_h; mb.window = window; mb.nnratio = nnratio;
-        mb.check_ori = check_ori; mb.reset_prev = 0;
+        mb.check_ori = check_ori; mb.reset_prev = 0; mb.clocks = nullptr;
         if (launch_match(mb, 1, n1c, n2c, q, c, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
             rc = ORBX_EIO;
     }

@@ -1,0 +1,56 @@
+// orbx_wave.h -- wave64 cross-lane primitives on DPP (row_shr / row_bcast),
+// which stay in the VALU instead of round-tripping through LDS the way
+// ds_bpermute-based shuffles do.  All require every lane of the wave active.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace orbx {
+
+template <int Ctrl, int RowMask = 0xF>
+__device__ inline uint32_t dpp_or(uint32_t old, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, Ctrl, RowMask, 0xF, false);
+}
+
+constexpr int kRowShr1 = 0x111, kRowShr2 = 0x112, kRowShr4 = 0x114, kRowShr8 = 0x118;
+constexpr int kRowBcast15 = 0x142, kRowBcast31 = 0x143;
+
+// Inclusive prefix sum over the 64 lanes.
+__device__ inline int wave_incl_scan_i32(int v) {
+    uint32_t u = (uint32_t)v;
+    u += dpp_or<kRowShr1>(0u, u);
+    u += dpp_or<kRowShr2>(0u, u);
+    u += dpp_or<kRowShr4>(0u, u);
+    u += dpp_or<kRowShr8>(0u, u);
+    u += dpp_or<kRowBcast15, 0xA>(0u, u);
+    u += dpp_or<kRowBcast31, 0xC>(0u, u);
+    return (int)u;
+}
+
+// Inclusive prefix sum of packed pairs of 32-bit counters (the halves are
+// scanned independently: callers pack counts that never carry into bit 32).
+__device__ inline uint64_t wave_incl_scan_u64(uint64_t v) {
+    const uint32_t lo = (uint32_t)wave_incl_scan_i32((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)wave_incl_scan_i32((int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Sum over the wave, returned in every lane.
+__device__ inline int wave_sum_i32(int v) {
+    return __builtin_amdgcn_readlane(wave_incl_scan_i32(v), 63);
+}
+
+// Minimum over the wave, returned in every lane.
+__device__ inline uint32_t wave_min_u32(uint32_t v) {
+    v = min(v, dpp_or<kRowShr1>(~0u, v));
+    v = min(v, dpp_or<kRowShr2>(~0u, v));
+    v = min(v, dpp_or<kRowShr4>(~0u, v));
+    v = min(v, dpp_or<kRowShr8>(~0u, v));
+    v = min(v, dpp_or<kRowBcast15, 0xA>(~0u, v));
+    v = min(v, dpp_or<kRowBcast31, 0xC>(~0u, v));
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+}  // namespace orbx

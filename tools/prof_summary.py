@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--trace", required=True)
     ap.add_argument("--fetch")
     ap.add_argument("--write")
+    ap.add_argument("--sq", help="pmc db with SQ_* counters")
     ap.add_argument("--out", required=True)
     ap.add_argument("--title", default="")
     a = ap.parse_args()
@@ -65,6 +66,22 @@ def main():
             wk, _ = w.get(k, (float('nan'), 0))
             hbm = (2 * fk + wk) / 1024.0
             lines.append(f"{k:<20} {fn:>10} {fk:>12.1f} {2 * fk / 1024:>11.2f} {wk:>12.1f} {hbm:>9.2f}")
+    if a.sq:
+        names = ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY",
+                 "SQ_WAIT_INST_ANY", "SQ_BUSY_CYCLES"]
+        c = {n: pmc(a.sq, n) for n in names}
+        lines.append("")
+        lines.append("## SQ counters per dispatch (per-wave instruction counts; cycle shares of SQ_WAVE_CYCLES)")
+        lines.append(f"{'kernel':<20} {'waves':>9} {'VALU/w':>8} {'SALU/w':>8} {'LDS/w':>7} {'wait_any':>9} "
+                     f"{'wait_inst':>9}")
+        for k in sorted(c["SQ_WAVES"]):
+            wv = c["SQ_WAVES"][k][0]
+            if wv <= 0:
+                continue
+            g = lambda n: c[n].get(k, (float("nan"), 0))[0]   # noqa: E731
+            wc = g("SQ_WAVE_CYCLES")
+            lines.append(f"{k:<20} {wv:>9.0f} {g('SQ_INSTS_VALU') / wv:>8.0f} {g('SQ_INSTS_SALU') / wv:>8.0f} "
+                         f"{g('SQ_INSTS_LDS') / wv:>7.0f} {g('SQ_WAIT_ANY') / wc:>9.2f} {g('SQ_WAIT_INST_ANY') / wc:>9.2f}")
     text = "\n".join(lines) + "\n"
     with open(a.out, "w") as fh:
         fh.write(text)
