@@ -10,8 +10,18 @@
 
 namespace orbx {
 
+// The per-level fields the per-keypoint / per-cell kernels need first, as a
+// kernel-argument copy: they come from the scalar cache with the other
+// arguments instead of a dependent load from the device tables.
+struct LevelArgs {
+    int w, h, pitch, out_off;
+    int64_t pyr_off;
+    float scale, patch_size;
+};
+
 // Plan tables resident in device memory (one copy per extractor plan).
 struct DevPlan {
+    LevelArgs la[kMaxLevels];
     const LevelGeom *lv;
     const Cell *cells;
     const ResizeTap *xtaps;

@@ -39,6 +39,15 @@ __device__ inline const uint8_t *level_ptr(const DevPlan &p, const FrameBufs &fb
     return fb.pyr + (int64_t)b * p.pyr_bytes + g.pyr_off;
 }
 
+__device__ inline const uint8_t *level_ptr(const DevPlan &p, const FrameBufs &fb, int l, int b, int &pitch) {
+    if (l == 0) {
+        pitch = fb.img0_pitch;
+        return fb.img0 + (int64_t)b * fb.img0_stride;
+    }
+    pitch = p.la[l].pitch;
+    return fb.pyr + (int64_t)b * p.pyr_bytes + p.la[l].pyr_off;
+}
+
 // The dispatcher hands workgroup j (linear, x fastest) to XCD j % 8.  This
 // maps j to a logical block index so that each XCD runs a contiguous range of
 // logical blocks: consecutive blocks of one frame then share an XCD's L2
@@ -341,9 +350,8 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb) {
     uint8_t *patch = lds + (size_t)wave * p.fast_lds_per_wave;
     uint8_t *scm = patch + p.fast_patch_bytes;   // S-1 of corners at min(ini, min) threshold, 0 elsewhere
     uint16_t *list = reinterpret_cast<uint16_t *>(scm + p.fast_score_bytes);   // (yy << 8 | xx), row-major
-    const LevelGeom g = p.lv[c.level];
     int spitch;
-    const uint8_t *img = level_ptr(p, fb, g, c.level, b, spitch);
+    const uint8_t *img = level_ptr(p, fb, c.level, b, spitch);
     const int o = wave_stage_rect(patch, PS, img, spitch, c.y0 - 3, c.x0 - 3, ch + 6, cw + 6, lane);
     {
         uint32_t *z0 = reinterpret_cast<uint32_t *>(scm);
@@ -813,21 +821,32 @@ __global__ __launch_bounds__(kThreads) void k_describe(DevPlan p, FrameBufs fb) 
     int bx, b;
     xcd_block_2d(bx, b);
     const int32_t *lc = fb.level_count + (int64_t)b * kMaxLevels;
+    const int slot = bx * 4 + wave;
+    // level of this slot from the kernel-argument offsets; the key and the
+    // level counts are independent loads issued together
+    int l = 0;
+#pragma unroll
+    for (int q = 1; q < kMaxLevels; ++q) l += (q < p.nlevels && slot >= p.la[q].out_off) ? 1 : 0;
+    const uint32_t key = slot < p.out_cap ? fb.sel[(int64_t)b * p.out_cap + slot] : 0u;
+    int cnt[kMaxLevels];
+#pragma unroll
+    for (int q = 0; q < kMaxLevels; ++q) cnt[q] = q < p.nlevels ? max(lc[q], 0) : 0;
     if (bx == 0 && tid == 0) {
         int total = 0;
-        for (int l = 0; l < p.nlevels; ++l) total += max(lc[l], 0);
+#pragma unroll
+        for (int q = 0; q < kMaxLevels; ++q) total += cnt[q];
         fb.nkps[b] = total;
     }
-    const int slot = bx * 4 + wave;
     if (slot >= p.out_cap) return;
-    int l = 0;
-    while (l + 1 < p.nlevels && slot >= p.lv[l + 1].out_off) ++l;
-    const LevelGeom g = p.lv[l];
+    const LevelArgs g = p.la[l];
     const int i = slot - g.out_off;
-    if (i >= lc[l]) return;
-    int off = 0;
-    for (int q = 0; q < l; ++q) off += max(lc[q], 0);
-    const uint32_t key = fb.sel[(int64_t)b * p.out_cap + slot];
+    int off = 0, cl = 0;
+#pragma unroll
+    for (int q = 0; q < kMaxLevels; ++q) {
+        off += q < l ? cnt[q] : 0;
+        cl = q == l ? cnt[q] : cl;
+    }
+    if (i >= cl) return;
     const int x = (int)(key & 0xFFF), y = (int)((key >> 12) & 0xFFF), score = (int)(key >> 24);
 
     uint8_t *lbase = lds + wave * ((kDescWaveLds + 15) & ~15);
@@ -836,7 +855,7 @@ __global__ __launch_bounds__(kThreads) void k_describe(DevPlan p, FrameBufs fb) 
     // 1. stage the 43x43 unblurred neighbourhood: aligned dword loads when it
     //    lies inside the level, else byte loads with reflect-101 at the borders
     int spitch;
-    const uint8_t *img = level_ptr(p, fb, g, l, b, spitch);
+    const uint8_t *img = level_ptr(p, fb, l, b, spitch);
     const int px0 = x - kDescR, py0 = y - kDescR;
     int o = 0;
     if (px0 >= 0 && py0 >= 0 && x + kDescR < g.w && y + kDescR < g.h &&

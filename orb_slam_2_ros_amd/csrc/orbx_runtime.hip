@@ -168,6 +168,14 @@ int upload_plan(orbx_extractor *ex) {
     d.ytaps = reinterpret_cast<const ResizeTap *>(ex->d_tables + o_yt);
     d.blur_tiles = reinterpret_cast<const int4 *>(ex->d_tables + o_tiles);
     d.nlevels = p.nlevels;
+    for (int l = 0; l < kMaxLevels; ++l) {
+        LevelArgs &a = d.la[l];
+        a = LevelArgs{};
+        if (l >= p.nlevels) continue;
+        const LevelGeom &g = p.lv[l];
+        a.w = g.w; a.h = g.h; a.pitch = g.pitch; a.out_off = g.out_off;
+        a.pyr_off = g.pyr_off; a.scale = g.scale; a.patch_size = g.patch_size;
+    }
     d.ncells = (int)p.cells.size();
     d.nblur_tiles = (int)tiles.size();
     for (int i = 0; i < 7; ++i) {
