@@ -6,7 +6,7 @@ against the previous frame of the same stream), 1000 kp, 8 levels, VGA mono
 Unit of work (SURVEY.md §8(d)): one frame = ORBextractor::operator() on a
 640x480 u8 image + ORBmatcher::SearchForInitialization(F1 = that stream's
 previous frame, F2 = this frame, vbPrevMatched = F1 keypoints, window 100,
-nnratio 0.9, checkOri).  A step processes one new frame for each of the B
+nnratio 0.9, checkOri).  A step processes one new frame for each of the B = 512
 streams a GPU owns (streams are independent: weak scaling, no collective on
 the data path; RCCL is used only for the barrier / max-time reduction).
 
@@ -68,6 +68,24 @@ def algorithmic_bytes(sizes, nkp: float, stage: str) -> float:
     if stage == "frame":       # SURVEY.md §8(d) compulsory figure
         return float(p0 + 2 * (p - p0)) + nkp * 60 + nkp * (2 * 32 + 4)
     raise ValueError(stage)
+
+
+TRAFFIC_FILE = ROOT / "profiles" / "traffic_vga.json"
+STAGE_KERNEL = {"resize": "k_resize", "fast": "k_fast", "quadtree": "k_quadtree", "describe": "k_describe",
+                "match": "k_search_init"}
+
+
+def measured_traffic(stage: str, frames_per_launch: float):
+    """HBM bytes per launch of the stage's kernel from the committed rocprofv3
+    PMC passes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, MI355X_MICROARCH.md),
+    scaled from the profiled dispatch's frame count; (None, None) if absent."""
+    try:
+        prof = json.loads(TRAFFIC_FILE.read_text())
+        k = prof["kernels"][STAGE_KERNEL[stage]]
+        per_frame = k["hbm_bytes_per_dispatch"] / prof["frames_per_dispatch"]
+        return round(per_frame * frames_per_launch), str(TRAFFIC_FILE.relative_to(ROOT))
+    except (OSError, KeyError, ValueError, ZeroDivisionError):
+        return None, None
 
 
 def cpu_baseline(w: int, h: int, nfeatures: int, budget_s: float):
@@ -188,8 +206,9 @@ def run_config(torch, dist, rank, world, dev, w, h, nfeatures, batch, steps, war
     else:
         _, _, sane = ex.depth_download(0)
     el = max_over_ranks(torch, dist, world, el, dev)
+    parts = ex.split() if (mode == "mono" and batch >= 64) else 1
     ex.close()
-    return el, stages, len(kp), sane
+    return el, stages, len(kp), sane, batch / parts
 
 
 EXTRAS = [
@@ -207,7 +226,7 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=256, help="streams (frames per step) per GPU")
+    ap.add_argument("--batch", type=int, default=512, help="streams (frames per step) per GPU")
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--nfeatures", type=int, default=1000)
@@ -230,7 +249,7 @@ def main() -> int:
     profile = not args.no_profile
 
     w, h, nf, B = args.width, args.height, args.nfeatures, args.batch
-    el, stages, nkp_last, nm_last = run_config(torch, dist, rank, world, dev, w, h, nf, B, args.steps,
+    el, stages, nkp_last, nm_last, frames_per_launch = run_config(torch, dist, rank, world, dev, w, h, nf, B, args.steps,
                                                args.warmup, profile)
     frames_total = world * B * args.steps
     value = frames_total / el
@@ -240,7 +259,7 @@ def main() -> int:
     if not args.no_extras:
         for key, mode, ew, eh, enf, eb, unit in EXTRAS:
             es = max(5, args.steps // 4)
-            el2, st2, nk2, sane2 = run_config(torch, dist, rank, world, dev, ew, eh, enf, eb, es, 2, profile, mode)
+            el2, st2, nk2, sane2, _ = run_config(torch, dist, rank, world, dev, ew, eh, enf, eb, es, 2, profile, mode)
             extras[key] = {"value": round(world * eb * es / el2, 2), "unit": unit, "mode": mode,
                            "streams_per_gpu": eb, "nfeatures": enf, "stage_ms": st2,
                            "kps_last_frame": nk2, ("matches" if mode == "mono" else "depths") + "_last_frame": sane2}
@@ -255,11 +274,15 @@ def main() -> int:
             # dominant HBM-streaming kernel by time among the stages with an algorithmic byte count
             cand = {n: s for n, s in stage_ms.items() if s and s > 0 and algorithmic_bytes(sizes, nkp_last, n) > 0}
             dom = max(cand, key=cand.get)
-            bytes_launch = algorithmic_bytes(sizes, nkp_last, dom) * B
+            # one launch covers one part of the split batch; its duration is the
+            # part-0 stage time (the parts' launches overlap on the GPU)
+            bytes_launch = algorithmic_bytes(sizes, nkp_last, dom) * frames_per_launch
             achieved = bytes_launch / (cand[dom] * 1e-3) / 1e9
+            traffic, tsrc = measured_traffic(dom, frames_per_launch)
             roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                    "bytes_per_launch": bytes_launch}
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                    "traffic_source": tsrc, "bytes_per_launch": bytes_launch,
+                    "frames_per_launch": frames_per_launch}
             frame_bytes = algorithmic_bytes(sizes, nkp_last, "frame")
             roof["pipeline_GBs"] = round(frame_bytes * value / world / 1e9, 2)
             roof["pipeline_frac"] = round(frame_bytes * value / world / 1e9 / HBM_PEAK_GBS, 5)

@@ -113,6 +113,12 @@ int orbx_mono_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t f
 int orbx_mono_matches_download(orbx_extractor *ex, int frame, int32_t *matches12, int cap,
                                int *n1, int *nmatches);
 
+/* Batch split: a step's batch runs as up to `parts` interleaved sub-batches
+ * on internal streams forked from and joined to the launch stream (latency-
+ * bound kernels of one part overlap the other's).  parts 1 or 2; 0 queries.
+ * Returns the current setting.  Batches under 64 frames are never split. */
+int orbx_extractor_split(orbx_extractor *ex, int parts);
+
 /* Per-stage device time of the last batch (HIP events on the launch stream),
  * in ms, when profiling is enabled: resize, blur, fast, quadtree, describe,
  * match.  Returns the number of stages written. */

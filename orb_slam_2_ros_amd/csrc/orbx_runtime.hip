@@ -94,6 +94,14 @@ struct orbx_extractor {
 
     hipStream_t stream = nullptr;
 
+    // Batch split: a large batch runs as `split` interleaved sub-batches on
+    // their own streams (forked from / joined to the launch stream), so the
+    // latency-bound kernels of one half overlap the other half's work.
+    static constexpr int kMaxParts = 2;
+    int split = 1;   // orbx_extractor_split / ORBX_SPLIT=2 turn it on
+    hipStream_t part_stream[kMaxParts] = {};
+    hipEvent_t fork_ev = nullptr, done_ev[kMaxParts] = {};
+
     // Stage profiling: a ring of event sets, one set per step, folded into
     // per-stage sums lazily so the timed loop never waits on the host.
     static constexpr int kRing = 64;
@@ -110,6 +118,11 @@ struct orbx_extractor {
     ~orbx_extractor() {
         release();
         if (stream) (void)hipStreamDestroy(stream);
+        for (auto &ps : part_stream)
+            if (ps) (void)hipStreamDestroy(ps);
+        if (fork_ev) (void)hipEventDestroy(fork_ev);
+        for (auto &e : done_ev)
+            if (e) (void)hipEventDestroy(e);
         for (auto &set : ev)
             for (auto &e : set)
                 if (e) (void)hipEventDestroy(e);
@@ -298,6 +311,77 @@ bool same_geometry(const Plan &a, const Plan &b) {
     return true;
 }
 
+// The same buffers seen from frame b0 on.
+FrameBufs offset_frames(const orbx_extractor *ex, FrameBufs fb, int b0) {
+    const Plan &p = ex->plan;
+    fb.img0 += (int64_t)b0 * fb.img0_stride;
+    fb.pyr += (int64_t)b0 * p.pyr_bytes;
+    fb.blur += (int64_t)b0 * p.blur_bytes;
+    fb.cand += (int64_t)b0 * p.cand_cap;
+    fb.cand2 += (int64_t)b0 * p.cand_cap;
+    fb.cell_count += (int64_t)b0 * p.cells.size();
+    fb.keys += (int64_t)b0 * p.cand_cap;
+    fb.key_node += (int64_t)b0 * p.cand_cap;
+    fb.key_q += (int64_t)b0 * p.cand_cap;
+    fb.sel += (int64_t)b0 * p.out_cap;
+    fb.level_count += (int64_t)b0 * kMaxLevels;
+    fb.kps += (int64_t)b0 * p.max_kps;
+    fb.desc += (int64_t)b0 * p.max_kps * 32;
+    fb.nkps += b0;
+    return fb;
+}
+
+MatchBufs offset_pairs(MatchBufs mb, int b0) {
+    mb.k1 += b0 * mb.k1_stride; mb.d1 += b0 * mb.k1_stride * 32; mb.n1 += b0;
+    mb.k2 += b0 * mb.k2_stride; mb.d2 += b0 * mb.k2_stride * 32; mb.n2 += b0;
+    mb.prev_xy += b0 * mb.k1_stride * 2;
+    mb.matches12 += b0 * mb.k1_stride;
+    mb.nmatches += b0;
+    mb.scratch += b0 * mb.scratch_stride;
+    return mb;
+}
+
+struct Parts {
+    int n = 1;
+    int b0[orbx_extractor::kMaxParts] = {0, 0};
+    int nb[orbx_extractor::kMaxParts] = {0, 0};
+    hipStream_t s[orbx_extractor::kMaxParts] = {};
+};
+
+// Splits `batch` into sub-batches on the part streams (forked from st), or a
+// single part on st itself.
+Parts fork_parts(orbx_extractor *ex, hipStream_t st, int batch) {
+    Parts P;
+    P.nb[0] = batch;
+    P.s[0] = st;
+    constexpr int kMinPart = 32;   // orbx.h: batches under 64 frames are never split
+    if (ex->split < 2 || batch < 2 * kMinPart) return P;
+    if (!ex->fork_ev) {
+        bool ok = hipEventCreateWithFlags(&ex->fork_ev, hipEventDisableTiming) == hipSuccess;
+        for (int k = 0; k < orbx_extractor::kMaxParts && ok; ++k)
+            ok = hipStreamCreateWithFlags(&ex->part_stream[k], hipStreamNonBlocking) == hipSuccess &&
+                 hipEventCreateWithFlags(&ex->done_ev[k], hipEventDisableTiming) == hipSuccess;
+        if (!ok) { ex->split = 1; return P; }
+    }
+    if (hipEventRecord(ex->fork_ev, st) != hipSuccess) return P;
+    P.n = orbx_extractor::kMaxParts;
+    for (int k = 0; k < P.n; ++k) {
+        P.b0[k] = batch * k / P.n;
+        P.nb[k] = batch * (k + 1) / P.n - P.b0[k];
+        P.s[k] = ex->part_stream[k];
+        (void)hipStreamWaitEvent(P.s[k], ex->fork_ev, 0);
+    }
+    return P;
+}
+
+int join_parts(orbx_extractor *ex, hipStream_t st, const Parts &P) {
+    if (P.n < 2) return ORBX_OK;
+    for (int k = 0; k < P.n; ++k)
+        if (hipEventRecord(ex->done_ev[k], P.s[k]) != hipSuccess || hipStreamWaitEvent(st, ex->done_ev[k], 0) != hipSuccess)
+            return ORBX_EIO;
+    return ORBX_OK;
+}
+
 void fold(orbx_extractor *ex, int set) {
     if (!ex->pending[set]) return;
     (void)hipEventSynchronize(ex->ev[set][kNumStages]);
@@ -337,28 +421,44 @@ void mark_valid(orbx_extractor *ex, int stage) {
     if (ex->cur_valid) ex->cur_valid[stage] = true;
 }
 
-// Runs the five extractor stages for `batch` frames into result slot `si`.
+// Runs the five extractor stages for `batch` frames into result slot `si`,
+// stage by stage across the parts (profiling marks on part 0's stream).
 int run_extract(orbx_extractor *ex, int si, const uint8_t *d_images, int64_t stride, int pitch, int batch,
-                hipStream_t st) {
+                const Parts &P) {
     auto &s = ex->slot[si];
     s.img0 = d_images;
     s.img0_stride = stride;
     s.img0_pitch = pitch;
     s.batch = batch;
     const FrameBufs fb = frame_bufs(ex, si);
-    mark(ex, 0, st);
-    if (launch_resize(ex->dp, ex->plan, fb, batch, st) != hipSuccess) return ORBX_EIO;
-    mark(ex, 1, st);
-    mark(ex, 2, st);   // the blur is fused into k_describe (patch-local); stage 1 stays empty
-    if (launch_fast(ex->dp, fb, batch, st) != hipSuccess) return ORBX_EIO;
-    mark(ex, 3, st);
-    if (launch_quadtree(ex->dp, fb, batch, st) != hipSuccess) return ORBX_EIO;
-    mark(ex, 4, st);
-    if (launch_describe(ex->dp, fb, batch, st) != hipSuccess) return ORBX_EIO;
-    mark(ex, 5, st);
+    FrameBufs pf[orbx_extractor::kMaxParts];
+    for (int k = 0; k < P.n; ++k) pf[k] = offset_frames(ex, fb, P.b0[k]);
+    const hipStream_t m = P.s[0];
+    mark(ex, 0, m);
+    for (int k = 0; k < P.n; ++k)
+        if (launch_resize(ex->dp, ex->plan, pf[k], P.nb[k], P.s[k]) != hipSuccess) return ORBX_EIO;
+    mark(ex, 1, m);
+    mark(ex, 2, m);   // the blur is fused into k_describe (patch-local); stage 1 stays empty
+    for (int k = 0; k < P.n; ++k)
+        if (launch_fast(ex->dp, pf[k], P.nb[k], P.s[k]) != hipSuccess) return ORBX_EIO;
+    mark(ex, 3, m);
+    for (int k = 0; k < P.n; ++k)
+        if (launch_quadtree(ex->dp, pf[k], P.nb[k], P.s[k]) != hipSuccess) return ORBX_EIO;
+    mark(ex, 4, m);
+    for (int k = 0; k < P.n; ++k)
+        if (launch_describe(ex->dp, pf[k], P.nb[k], P.s[k]) != hipSuccess) return ORBX_EIO;
+    mark(ex, 5, m);
     for (int i = 0; i < kStageMatch; ++i)
         if (i != kStageBlur) mark_valid(ex, i);
     return ORBX_OK;
+}
+
+int run_extract(orbx_extractor *ex, int si, const uint8_t *d_images, int64_t stride, int pitch, int batch,
+                hipStream_t st) {
+    Parts P;
+    P.nb[0] = batch;
+    P.s[0] = st;
+    return run_extract(ex, si, d_images, stride, pitch, batch, P);
 }
 
 int validate_batch(orbx_extractor *ex, const uint8_t *d_images, int pitch, int batch) {
@@ -429,6 +529,7 @@ orbx_extractor *orbx_extractor_create(int device, int nfeatures, float scaleFact
     ex->ini_th = iniThFAST;
     ex->min_th = minThFAST;
     if (hipStreamCreateWithFlags(&ex->stream, hipStreamNonBlocking) != hipSuccess) { delete ex; return nullptr; }
+    if (const char *sp = std::getenv("ORBX_SPLIT")) ex->split = std::max(1, std::min(std::atoi(sp), orbx_extractor::kMaxParts));
     // geometry tables for the getters are size independent; plan a nominal size
     ex->plan = make_plan(640, 480, nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST);
     return ex;
@@ -649,12 +750,14 @@ int orbx_mono_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t f
     const int prev = ex->cur, next = ex->cur ^ 1;
     const bool have_prev = ex->slot[prev].batch == batch && ex->steps > 0;
     prof_begin(ex);
-    rc = run_extract(ex, next, d_images, frame_stride, pitch, batch, st);
+    const Parts P = fork_parts(ex, st, batch);
+    rc = run_extract(ex, next, d_images, frame_stride, pitch, batch, P);
     if (rc) return rc;
     ex->cur = next;
     ++ex->steps;
     ex->match_batch = 0;
     if (!have_prev) {
+        if ((rc = join_parts(ex, st, P))) return rc;
         mark(ex, kNumStages, st);
         return ORBX_OK;
     }
@@ -679,8 +782,13 @@ int orbx_mono_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t f
     long long *dclk = nullptr;
     if (dbg_clocks && hipMalloc(reinterpret_cast<void **>(&dclk), 8 * sizeof(long long)) == hipSuccess)
         mb.clocks = dclk;
-    if (launch_match(mb, batch, ex->plan.max_kps, ex->plan.max_kps, ex->l0cap, ex->l0cap, st) != hipSuccess)
-        return ORBX_EIO;
+    for (int k = 0; k < P.n; ++k) {
+        MatchBufs pm = offset_pairs(mb, P.b0[k]);
+        if (k > 0) pm.clocks = nullptr;
+        if (launch_match(pm, P.nb[k], ex->plan.max_kps, ex->plan.max_kps, ex->l0cap, ex->l0cap, P.s[k]) != hipSuccess)
+            return ORBX_EIO;
+    }
+    if ((rc = join_parts(ex, st, P))) return rc;
     if (dclk) {   // debug: phase cycle counts of pair 0
         long long c[8] = {};
         if (hipStreamSynchronize(st) == hipSuccess &&
@@ -713,6 +821,12 @@ int orbx_mono_matches_download(orbx_extractor *ex, int frame, int32_t *matches12
                   hipMemcpyDeviceToHost) != hipSuccess)
         return ORBX_EIO;
     return ORBX_OK;
+}
+
+int orbx_extractor_split(orbx_extractor *ex, int parts) {
+    if (!ex || parts < 0 || parts > orbx_extractor::kMaxParts) return ORBX_EINVAL;
+    if (parts > 0) ex->split = parts;
+    return ex->split;
 }
 
 int orbx_extractor_set_profiling(orbx_extractor *ex, int on) {

@@ -179,6 +179,10 @@ class ORBextractor:
                                                    ctypes.byref(nm)), "mono_matches_download")
         return m[:n1.value].copy(), nm.value
 
+    def split(self, parts: int = 0) -> int:
+        """Batch split into sub-batches on internal streams (0 = query)."""
+        return check(self._lib.orbx_extractor_split(self._h, int(parts)), "split")
+
     def set_profiling(self, on: bool) -> None:
         check(self._lib.orbx_extractor_set_profiling(self._h, int(on)), "set_profiling")
 

@@ -44,6 +44,8 @@ def main():
     ap.add_argument("--fetch")
     ap.add_argument("--write")
     ap.add_argument("--sq", help="pmc db with SQ_* counters")
+    ap.add_argument("--json", help="also write per-kernel HBM bytes per dispatch here")
+    ap.add_argument("--frames-per-dispatch", type=float, default=0.0)
     ap.add_argument("--out", required=True)
     ap.add_argument("--title", default="")
     a = ap.parse_args()
@@ -82,6 +84,16 @@ def main():
             wc = g("SQ_WAVE_CYCLES")
             lines.append(f"{k:<20} {wv:>9.0f} {g('SQ_INSTS_VALU') / wv:>8.0f} {g('SQ_INSTS_SALU') / wv:>8.0f} "
                          f"{g('SQ_INSTS_LDS') / wv:>7.0f} {g('SQ_WAIT_ANY') / wc:>9.2f} {g('SQ_WAIT_INST_ANY') / wc:>9.2f}")
+    if a.json and a.fetch and a.write:
+        import json
+        f = pmc(a.fetch, "FETCH_SIZE")
+        w = pmc(a.write, "WRITE_SIZE")
+        out = {"source": a.out, "frames_per_dispatch": a.frames_per_dispatch,
+               "note": "FETCH_SIZE x2 (gfx950) + WRITE_SIZE, KB x 1024, averaged over dispatches",
+               "kernels": {k: {"hbm_bytes_per_dispatch": (2 * f[k][0] + w.get(k, (0.0, 0))[0]) * 1024.0,
+                               "fetch_kb": f[k][0], "write_kb": w.get(k, (0.0, 0))[0]} for k in f}}
+        with open(a.json, "w") as fh:
+            json.dump(out, fh, indent=1)
     text = "\n".join(lines) + "\n"
     with open(a.out, "w") as fh:
         fh.write(text)
