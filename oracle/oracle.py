@@ -212,3 +212,35 @@ def stereo_from_rgbd(kps, dmap, mbf, kps_un=None):
     lib().orbo_stereo_from_rgbd(_p(kps), _p(kun), len(kps), _p(dmap), dmap.shape[1], dmap.shape[0],
                                 dmap.strides[0], mbf, _p(ur), _p(dp))
     return ur[:len(kps)].copy(), dp[:len(kps)].copy()
+
+
+PROJ_QUERY_DTYPE = np.dtype([
+    ("u", "<f4"), ("v", "<f4"), ("radius", "<f4"), ("ur", "<f4"), ("ur_tol", "<f4"),
+    ("min_level", "<i4"), ("max_level", "<i4"), ("angle", "<f4"), ("flags", "<i4"),
+])
+PROJ_VARIANTS = {"localmap": 0, "lastframe": 1, "keyframe": 2, "sim3": 3, "fuse": 4, "fuse_sim3": 5}
+
+
+def search_by_projection(variant, keys, desc, queries, qdesc, bounds, uright=None, mp_state=None,
+                         inv_sigma2=None, th_dist=100, nnratio=0.6, check_ori=True):
+    """ORBmatcher::SearchByProjection x4 / Fuse x2 (search part) on a query
+    table.  Returns (nmatches, q_idx, q_dist, kp_final)."""
+    lib().orbo_search_by_projection.restype = I32
+    lib().orbo_search_by_projection.argtypes = [I32, P, P, P, P, P, I32, F32, F32, F32, F32, P, P, I32, I32,
+                                                F32, I32, P, P, P]
+    keys = np.ascontiguousarray(keys, KEYPOINT_DTYPE)
+    desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    q = np.ascontiguousarray(queries, PROJ_QUERY_DTYPE)
+    qd = np.ascontiguousarray(qdesc, np.uint8).reshape(-1, 32)
+    ur = None if uright is None else np.ascontiguousarray(uright, np.float32)
+    ms = None if mp_state is None else np.ascontiguousarray(mp_state, np.uint8)
+    isg = None if inv_sigma2 is None else np.ascontiguousarray(inv_sigma2, np.float32)
+    qi = np.full(max(len(q), 1), -1, np.int32)
+    qdist = np.full(max(len(q), 1), -1, np.int32)
+    kf = np.full(max(len(keys), 1), -1, np.int32)
+    v = PROJ_VARIANTS[variant] if isinstance(variant, str) else int(variant)
+    nm = lib().orbo_search_by_projection(v, _p(keys), _p(desc), None if ur is None else _p(ur),
+                                         None if ms is None else _p(ms), None if isg is None else _p(isg),
+                                         len(keys), *[float(b) for b in bounds], _p(q), _p(qd), len(q),
+                                         int(th_dist), float(nnratio), int(check_ori), _p(qi), _p(qdist), _p(kf))
+    return nm, qi[:len(q)].copy(), qdist[:len(q)].copy(), kf[:len(keys)].copy()

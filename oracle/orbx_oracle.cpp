@@ -889,3 +889,170 @@ void orbo_stereo_from_rgbd(const orbo_keypoint *kps, const orbo_keypoint *kps_un
         }
     }
 }
+
+// ---- projection matchers (ORBmatcher::SearchByProjection x4, Fuse x2 search) ----
+namespace {
+
+// Frame / KeyFrame 64x48 feature grid (Frame.cc:239-256, 415-425).
+struct FeatureGrid {
+    static constexpr int GC = 64, GR = 48;
+    float minX, minY, invW, invH;
+    std::vector<std::vector<int>> cells;
+    FeatureGrid(const orbo_keypoint *k, int n, float min_x, float max_x, float min_y, float max_y)
+        : minX(min_x), minY(min_y), invW((float)GC / (max_x - min_x)), invH((float)GR / (max_y - min_y)),
+          cells((size_t)GC * GR) {
+        for (int i = 0; i < n; ++i) {
+            const int px = (int)std::round((k[i].x - minX) * invW);
+            const int py = (int)std::round((k[i].y - minY) * invH);
+            if (px < 0 || px >= GC || py < 0 || py >= GR) continue;
+            cells[(size_t)px * GR + py].push_back(i);
+        }
+    }
+    // Frame::GetFeaturesInArea (Frame.cc:354-412); KeyFrame's (KeyFrame.cc:700-739)
+    // is the same walk without the level filter (minLevel = maxLevel = -1 here).
+    std::vector<int> area(const orbo_keypoint *k, float x, float y, float r, int minLevel, int maxLevel) const {
+        std::vector<int> out;
+        const int nMinCellX = std::max(0, (int)std::floor((x - minX - r) * invW));
+        if (nMinCellX >= GC) return out;
+        const int nMaxCellX = std::min(GC - 1, (int)std::ceil((x - minX + r) * invW));
+        if (nMaxCellX < 0) return out;
+        const int nMinCellY = std::max(0, (int)std::floor((y - minY - r) * invH));
+        if (nMinCellY >= GR) return out;
+        const int nMaxCellY = std::min(GR - 1, (int)std::ceil((y - minY + r) * invH));
+        if (nMaxCellY < 0) return out;
+        const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+        for (int ix = nMinCellX; ix <= nMaxCellX; ix++)
+            for (int iy = nMinCellY; iy <= nMaxCellY; iy++)
+                for (int j : cells[(size_t)ix * GR + iy]) {
+                    if (bCheckLevels) {
+                        if (k[j].octave < minLevel) continue;
+                        if (maxLevel >= 0 && k[j].octave > maxLevel) continue;
+                    }
+                    const float distx = k[j].x - x, disty = k[j].y - y;
+                    if (std::fabs(distx) < r && std::fabs(disty) < r) out.push_back(j);
+                }
+        return out;
+    }
+};
+
+// ComputeThreeMaxima (ORBmatcher.cc:1603-1644) on bin sizes.
+void three_maxima(const int *sizes, int L, int &ind1, int &ind2, int &ind3) {
+    int max1 = 0, max2 = 0, max3 = 0;
+    ind1 = ind2 = ind3 = -1;
+    for (int i = 0; i < L; i++) {
+        const int s = sizes[i];
+        if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
+        else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
+        else if (s > max3) { max3 = s; ind3 = i; }
+    }
+    if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+    else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+}
+
+}  // namespace
+
+int orbo_search_by_projection(int variant, const orbo_keypoint *keys, const uint8_t *desc, const float *uright,
+                              const uint8_t *mp_state, const float *inv_sigma2, int n, float min_x, float max_x,
+                              float min_y, float max_y, const orbo_proj_query *q, const uint8_t *qdesc, int nq,
+                              int th_dist, float nnratio, int check_ori, int32_t *q_idx, int32_t *q_dist,
+                              int32_t *kp_final) {
+    const FeatureGrid grid(keys, n, min_x, max_x, min_y, max_y);
+    const int HL = 30;
+    const float factor = 1.0f / HL;
+    std::vector<int> rotHist[HL];   // accepted queries per bin (the reference keeps their keypoints)
+    // mvpMapPoints as (non-NULL, Observations() > 0) and which query put it there
+    std::vector<uint8_t> has(n), obs(n);
+    for (int i = 0; i < n; ++i) { has[i] = mp_state ? (mp_state[i] & 1) : 0; obs[i] = mp_state ? ((mp_state[i] >> 1) & 1) : 0; }
+    for (int i = 0; i < n; ++i) kp_final[i] = -1;
+    int nmatches = 0;
+    for (int iq = 0; iq < nq; ++iq) {
+        q_idx[iq] = -1;
+        q_dist[iq] = -1;
+        const orbo_proj_query &Q = q[iq];
+        if (!(Q.flags & 1)) continue;
+        const uint8_t *dq = qdesc + 32 * (size_t)iq;
+        const std::vector<int> cand = grid.area(keys, Q.u, Q.v, Q.radius, Q.min_level, Q.max_level);
+        if (cand.empty()) continue;
+        if (variant == ORBO_PROJ_LOCALMAP) {
+            // ORBmatcher.cc:45-129
+            int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+            for (int idx : cand) {
+                if (has[idx] && obs[idx]) continue;
+                if (uright && uright[idx] > 0) {
+                    const float er = std::fabs(Q.ur - uright[idx]);
+                    if (er > Q.ur_tol) continue;
+                }
+                const int dist = hamming32(dq, desc + 32 * (size_t)idx);
+                if (dist < bestDist) {
+                    bestDist2 = bestDist; bestDist = dist;
+                    bestLevel2 = bestLevel; bestLevel = keys[idx].octave;
+                    bestIdx = idx;
+                } else if (dist < bestDist2) {
+                    bestLevel2 = keys[idx].octave; bestDist2 = dist;
+                }
+            }
+            if (bestDist <= th_dist) {
+                if (bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) continue;
+                has[bestIdx] = 1; obs[bestIdx] = (Q.flags >> 1) & 1;
+                kp_final[bestIdx] = iq;
+                q_idx[iq] = bestIdx; q_dist[iq] = bestDist;
+                nmatches++;
+            }
+            continue;
+        }
+        // best-only variants
+        const bool fuse = variant == ORBO_PROJ_FUSE || variant == ORBO_PROJ_FUSE_SIM3;
+        int bestDist = variant == ORBO_PROJ_FUSE_SIM3 ? INT_MAX : 256, bestIdx = -1;
+        for (int idx : cand) {
+            if (variant == ORBO_PROJ_LASTFRAME) {             // ORBmatcher.cc:1403-1413
+                if (has[idx] && obs[idx]) continue;
+                if (uright && uright[idx] > 0) {
+                    const float er = std::fabs(Q.ur - uright[idx]);
+                    if (er > Q.ur_tol) continue;
+                }
+            } else if (variant == ORBO_PROJ_KEYFRAME || variant == ORBO_PROJ_SIM3) {   // :1546-1548, :371-372
+                if (has[idx]) continue;
+            } else if (variant == ORBO_PROJ_FUSE) {           // :903-932
+                const orbo_keypoint &kp = keys[idx];
+                const int kpLevel = kp.octave;
+                if (uright && uright[idx] >= 0) {
+                    const float ex = Q.u - kp.x, ey = Q.v - kp.y, er = Q.ur - uright[idx];
+                    const float e2 = ex * ex + ey * ey + er * er;
+                    if (e2 * inv_sigma2[kpLevel] > 7.8) continue;
+                } else {
+                    const float ex = Q.u - kp.x, ey = Q.v - kp.y;
+                    const float e2 = ex * ex + ey * ey;
+                    if (e2 * inv_sigma2[kpLevel] > 5.99) continue;
+                }
+            }
+            const int dist = hamming32(dq, desc + 32 * (size_t)idx);
+            if (dist < bestDist) { bestDist = dist; bestIdx = idx; }
+        }
+        if (bestDist <= th_dist) {
+            q_idx[iq] = bestIdx;
+            q_dist[iq] = bestDist;
+            if (fuse) { nmatches++; continue; }   // actions on the map stay with the caller
+            has[bestIdx] = 1; obs[bestIdx] = (Q.flags >> 1) & 1;
+            kp_final[bestIdx] = iq;
+            nmatches++;
+            if (check_ori && (variant == ORBO_PROJ_LASTFRAME || variant == ORBO_PROJ_KEYFRAME)) {
+                float rot = Q.angle - keys[bestIdx].angle;
+                if (rot < 0.0) rot += 360.0f;
+                int bin = (int)std::round(rot * factor);
+                if (bin == HL) bin = 0;
+                rotHist[bin].push_back(iq);
+            }
+        }
+    }
+    if (check_ori && (variant == ORBO_PROJ_LASTFRAME || variant == ORBO_PROJ_KEYFRAME)) {
+        int sizes[HL];
+        for (int i = 0; i < HL; ++i) sizes[i] = (int)rotHist[i].size();
+        int ind1, ind2, ind3;
+        three_maxima(sizes, HL, ind1, ind2, ind3);
+        for (int i = 0; i < HL; i++) {
+            if (i == ind1 || i == ind2 || i == ind3) continue;
+            for (int iq : rotHist[i]) { kp_final[q_idx[iq]] = -2; q_idx[iq] = -1; nmatches--; }
+        }
+    }
+    return nmatches;
+}

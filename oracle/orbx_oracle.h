@@ -98,6 +98,32 @@ void  orbo_stereo_from_rgbd(const orbo_keypoint *kps, const orbo_keypoint *kps_u
                             const float *dmap, int w, int h, size_t pitch_bytes, float mbf,
                             float *uright, float *depth);
 
+/* ---- projection matchers (ORBmatcher.cc:45-129, 291-404, 827-1102, 1330-1601) ----
+ * Queries carry the projection the reference computes in the caller or at
+ * the top of each loop body (u, v, window radius, stereo u, level range of
+ * GetFeaturesInArea, the query keypoint's angle).  flags: bit0 = query taken
+ * (the reference's own skip tests passed), bit1 = assigning it blocks the
+ * keypoint for later queries (its Observations() > 0).  mp_state per
+ * keypoint: bit0 = mvpMapPoints[i] / vpMatched[i] non-NULL, bit1 = that point's
+ * Observations() > 0.  Outputs: q_idx / q_dist per query (the keypoint it was
+ * assigned, -1 if none or if the rotation check dropped its bin), kp_final per
+ * keypoint (query whose point it holds at the end, -1 untouched, -2 cleared
+ * by the rotation check; untouched by the Fuse variants, whose map updates
+ * stay with the caller).  Returns nmatches / nFused as the reference counts. */
+typedef struct {
+    float u, v, radius, ur, ur_tol;
+    int32_t min_level, max_level;
+    float angle;
+    int32_t flags;
+} orbo_proj_query;
+enum { ORBO_PROJ_LOCALMAP = 0, ORBO_PROJ_LASTFRAME = 1, ORBO_PROJ_KEYFRAME = 2, ORBO_PROJ_SIM3 = 3,
+       ORBO_PROJ_FUSE = 4, ORBO_PROJ_FUSE_SIM3 = 5 };
+int   orbo_search_by_projection(int variant, const orbo_keypoint *keys, const uint8_t *desc, const float *uright,
+                                const uint8_t *mp_state, const float *inv_sigma2, int n, float min_x, float max_x,
+                                float min_y, float max_y, const orbo_proj_query *q, const uint8_t *qdesc, int nq,
+                                int th_dist, float nnratio, int check_ori, int32_t *q_idx, int32_t *q_dist,
+                                int32_t *kp_final);
+
 #ifdef __cplusplus
 }
 #endif

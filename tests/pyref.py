@@ -417,3 +417,143 @@ def compute_stereo_matches(pyr_l, pyr_r, scale, inv_scale, kl, dl, kr, dr, mbf, 
         ur[i] = dp[i] = -1
         kept -= 1
     return ur, dp, kept
+
+
+# ---- ORBmatcher::SearchByProjection x4 / Fuse x2 search (ORBmatcher.cc) -------
+def _grid(keys, bounds):
+    minX, maxX, minY, maxY = [f32(b) for b in bounds]
+    invW, invH = f32(f32(64) / f32(maxX - minX)), f32(f32(48) / f32(maxY - minY))
+    cells = {}
+    for i in range(len(keys)):
+        px = round_half_away(f32(f32(f32(keys["x"][i]) - minX) * invW))
+        py = round_half_away(f32(f32(f32(keys["y"][i]) - minY) * invH))
+        if 0 <= px < 64 and 0 <= py < 48:
+            cells.setdefault((px, py), []).append(i)
+    return minX, minY, invW, invH, cells
+
+
+def _area(keys, g, x, y, r, min_level, max_level):
+    minX, minY, invW, invH, cells = g
+    x, y, r = f32(x), f32(y), f32(r)
+    c0 = max(0, math.floor(f32(f32(f32(x - minX) - r) * invW)))
+    if c0 >= 64:
+        return []
+    c1 = min(63, math.ceil(f32(f32(f32(x - minX) + r) * invW)))
+    if c1 < 0:
+        return []
+    r0 = max(0, math.floor(f32(f32(f32(y - minY) - r) * invH)))
+    if r0 >= 48:
+        return []
+    r1 = min(47, math.ceil(f32(f32(f32(y - minY) + r) * invH)))
+    if r1 < 0:
+        return []
+    check = min_level > 0 or max_level >= 0
+    out = []
+    for ix in range(c0, c1 + 1):
+        for iy in range(r0, r1 + 1):
+            for j in cells.get((ix, iy), []):
+                if check and (keys["octave"][j] < min_level or (max_level >= 0 and keys["octave"][j] > max_level)):
+                    continue
+                if abs(f32(f32(keys["x"][j]) - x)) < r and abs(f32(f32(keys["y"][j]) - y)) < r:
+                    out.append(j)
+    return out
+
+
+def search_by_projection(variant, keys, desc, q, qdesc, bounds, uright=None, mp_state=None, inv_sigma2=None,
+                         th_dist=100, nnratio=0.6, check_ori=True):
+    g = _grid(keys, bounds)
+    n = len(keys)
+    has = [bool(mp_state[i] & 1) if mp_state is not None else False for i in range(n)]
+    obs = [bool(mp_state[i] & 2) if mp_state is not None else False for i in range(n)]
+    q_idx, q_dist, kp_final = [-1] * len(q), [-1] * len(q), [-1] * n
+    hist = [[] for _ in range(30)]
+    nm = 0
+    use_ori = check_ori and variant in ("lastframe", "keyframe")
+    for iq in range(len(q)):
+        Q = q[iq]
+        if not (Q["flags"] & 1):
+            continue
+        cand = _area(keys, g, Q["u"], Q["v"], Q["radius"], int(Q["min_level"]), int(Q["max_level"]))
+        if not cand:
+            continue
+        if variant == "localmap":                      # ORBmatcher.cc:45-129
+            bd, bl, bd2, bl2, bi = 256, -1, 256, -1, -1
+            for idx in cand:
+                if has[idx] and obs[idx]:
+                    continue
+                if uright is not None and uright[idx] > 0 and abs(f32(Q["ur"] - uright[idx])) > Q["ur_tol"]:
+                    continue
+                d = hamming(qdesc[iq], desc[idx])
+                if d < bd:
+                    bd2, bd, bl2, bl, bi = bd, d, bl, int(keys["octave"][idx]), idx
+                elif d < bd2:
+                    bl2, bd2 = int(keys["octave"][idx]), d
+            if bd <= th_dist:
+                if bl == bl2 and f32(bd) > f32(f32(nnratio) * f32(bd2)):
+                    continue
+                has[bi], obs[bi] = True, bool(Q["flags"] & 2)
+                kp_final[bi], q_idx[iq], q_dist[iq] = iq, bi, bd
+                nm += 1
+            continue
+        bd, bi = (2 ** 31 - 1 if variant == "fuse_sim3" else 256), -1
+        for idx in cand:
+            if variant == "lastframe":                 # :1403-1413
+                if has[idx] and obs[idx]:
+                    continue
+                if uright is not None and uright[idx] > 0 and abs(f32(Q["ur"] - uright[idx])) > Q["ur_tol"]:
+                    continue
+            elif variant in ("keyframe", "sim3"):      # :1546-1548, :371-372
+                if has[idx]:
+                    continue
+            elif variant == "fuse":                    # :903-932
+                lvl = int(keys["octave"][idx])
+                ex = f32(Q["u"] - keys["x"][idx])
+                ey = f32(Q["v"] - keys["y"][idx])
+                if uright is not None and uright[idx] >= 0:
+                    er = f32(Q["ur"] - uright[idx])
+                    e2 = f32(f32(f32(ex * ex) + f32(ey * ey)) + f32(er * er))
+                    if float(f32(e2 * inv_sigma2[lvl])) > 7.8:
+                        continue
+                else:
+                    e2 = f32(f32(ex * ex) + f32(ey * ey))
+                    if float(f32(e2 * inv_sigma2[lvl])) > 5.99:
+                        continue
+            d = hamming(qdesc[iq], desc[idx])
+            if d < bd:
+                bd, bi = d, idx
+        if bd <= th_dist:
+            q_idx[iq], q_dist[iq] = bi, bd
+            nm += 1
+            if variant in ("fuse", "fuse_sim3"):
+                continue
+            has[bi], obs[bi] = True, bool(Q["flags"] & 2)
+            kp_final[bi] = iq
+            if use_ori:
+                rot = f32(Q["angle"] - keys["angle"][bi])
+                if rot < 0:
+                    rot = f32(rot + f32(360))
+                b = round_half_away(f32(rot * f32(f32(1) / f32(30))))
+                hist[0 if b == 30 else b].append(iq)
+    if use_ori:
+        sizes = [len(h) for h in hist]
+        m1 = m2 = m3 = 0
+        i1 = i2 = i3 = -1
+        for i, s in enumerate(sizes):
+            if s > m1:
+                m3, m2, m1, i3, i2, i1 = m2, m1, s, i2, i1, i
+            elif s > m2:
+                m3, m2, i3, i2 = m2, s, i2, i
+            elif s > m3:
+                m3, i3 = s, i
+        if m2 < f32(0.1) * f32(m1):
+            i2 = i3 = -1
+        elif m3 < f32(0.1) * f32(m1):
+            i3 = -1
+        for i in range(30):
+            if i in (i1, i2, i3):
+                continue
+            for iq in hist[i]:
+                kp_final[q_idx[iq]] = -2
+                q_idx[iq] = -1
+                nm -= 1
+    return nm, np.array(q_idx, np.int32), np.array(q_dist, np.int32), np.array(kp_final, np.int32)

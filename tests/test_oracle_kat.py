@@ -239,3 +239,18 @@ def test_stereo_from_rgbd_oracle(oracle_mod):
             assert dp[i] == z and ur[i] == np.float32(k["x"][i] - np.float32(np.float32(40.0) / z))
         else:
             assert dp[i] == -1 and ur[i] == -1
+
+
+@pytest.mark.parametrize("variant", ["localmap", "lastframe", "keyframe", "sim3", "fuse", "fuse_sim3"])
+@pytest.mark.parametrize("seed,stereo", [(81, False), (82, True)])
+def test_projection_matchers_vs_python(variant, seed, stereo, oracle_mod):
+    from proj_cases import VARIANT_ARGS, make_case
+    th, ratio, ori, wth = VARIANT_ARGS[variant]
+    c = make_case(seed, variant, n=900, nq=700, stereo=stereo, th=wth)
+    a = oracle_mod.search_by_projection(variant, c["keys"], c["desc"], c["queries"], c["qdesc"], c["bounds"],
+                                        c["uright"], c["mp_state"], c["inv_sigma2"], th, ratio, ori)
+    b = pyref.search_by_projection(variant, c["keys"], c["desc"], c["queries"], c["qdesc"], c["bounds"],
+                                   c["uright"], c["mp_state"], c["inv_sigma2"], th, ratio, ori)
+    assert a[0] == b[0] and a[0] > 20
+    for x, y in zip(a[1:], b[1:]):
+        assert np.array_equal(x, y)
