@@ -199,6 +199,60 @@ int orbx_search_for_initialization(int device, const orbx_keypoint *k1, const ui
                                    int img_w, int img_h, float *prev_xy, int32_t *matches12,
                                    int window, float nnratio, int check_ori, int *nmatches);
 
+/* ORBmatcher projection searches: SearchByProjection x4 and the candidate
+ * search of Fuse x2 (ORBmatcher.cc:45-129, 291-404, 827-1102, 1330-1601).
+ * The caller projects its map points (the pose algebra stays in the host, on
+ * the caller's cv::Mat types) and passes one row per point, in the
+ * reference's loop order; the device runs the window search, the Hamming
+ * distances, the reference's greedy keypoint assignment and the rotation
+ * check. */
+typedef struct orbx_match_frame {
+    const orbx_keypoint *keys;  /* mvKeysUn (grid position, octave, angle) */
+    const uint8_t *desc;        /* mDescriptors, 32-byte rows */
+    const float *uright;        /* mvuRight, or NULL (monocular) */
+    const uint8_t *mp_state;    /* mvpMapPoints / vpMatched per keypoint: bit0 non-NULL,
+                                   bit1 its Observations() > 0; NULL = all NULL */
+    const float *inv_sigma2;    /* mvInvLevelSigma2 (Fuse's reprojection test) or NULL */
+    int n;
+    int nlevels;                /* entries of inv_sigma2 */
+    float min_x, max_x, min_y, max_y;   /* mnMinX, mnMaxX, mnMinY, mnMaxY: the 64 x 48 grid */
+} orbx_match_frame;
+
+typedef struct orbx_proj_query {
+    float u, v;          /* projection */
+    float radius;        /* GetFeaturesInArea half-size */
+    float ur;            /* projected right u (mTrackProjXR, u - mbf * invz) */
+    float ur_tol;        /* stereo gate |ur - mvuRight| > ur_tol (SearchByProjection) */
+    int32_t min_level;   /* GetFeaturesInArea level arguments, reference semantics */
+    int32_t max_level;
+    float angle;         /* the query keypoint's angle (rotation check) */
+    int32_t flags;       /* ORBX_QUERY_ACTIVE | ORBX_QUERY_BLOCKS */
+} orbx_proj_query;
+
+#define ORBX_QUERY_ACTIVE 1   /* the reference's per-point skip tests passed */
+#define ORBX_QUERY_BLOCKS 2   /* its map point has Observations() > 0 */
+
+#define ORBX_PROJ_LOCALMAP 0  /* SearchByProjection(Frame&, const vector<MapPoint*>&, th)       :45  */
+#define ORBX_PROJ_LASTFRAME 1 /* SearchByProjection(Frame&, const Frame&, th, bMono)            :1330 */
+#define ORBX_PROJ_KEYFRAME 2  /* SearchByProjection(Frame&, KeyFrame*, set, th, ORBdist)        :1474 */
+#define ORBX_PROJ_SIM3 3      /* SearchByProjection(KeyFrame*, Scw, vpPoints, vpMatched, th)    :291 */
+#define ORBX_PROJ_FUSE 4      /* Fuse(KeyFrame*, vpMapPoints, th): candidate search             :827 */
+#define ORBX_PROJ_FUSE_SIM3 5 /* Fuse(KeyFrame*, Scw, vpPoints, th, vpReplacePoint): search     :979 */
+
+/* th_dist: TH_HIGH / ORBdist / TH_LOW as the variant's reference uses;
+ * nnratio and check_ori: the ORBmatcher's.  Outputs (host arrays):
+ *   q_idx[nq]   keypoint assigned to the query (the variant's bestIdx when it
+ *               passes), -1 none or dropped by the rotation check;
+ *   q_dist[nq]  its distance (-1 none);
+ *   kp_final[n] query whose point the keypoint holds afterwards, -1 untouched,
+ *               -2 cleared by the rotation check (search variants only);
+ *   *nmatches   the reference's return value (nmatches / nFused).
+ * Synchronous. */
+int orbx_search_by_projection(int device, int variant, const orbx_match_frame *frame,
+                              const orbx_proj_query *queries, const uint8_t *qdesc, int nq,
+                              int th_dist, float nnratio, int check_ori, int32_t *q_idx,
+                              int32_t *q_dist, int32_t *kp_final, int *nmatches);
+
 /* Device evaluation of the restated sincosf / fastAtan2 (test hook). */
 int orbx_debug_trig(int device, const float *angles, float *s, float *c, int n,
                     const float *ys, const float *xs, float *atan_deg, int m);

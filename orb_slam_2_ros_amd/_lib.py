@@ -28,6 +28,21 @@ KEYPOINT_DTYPE = np.dtype([
 ])
 assert KEYPOINT_DTYPE.itemsize == 28
 
+# orbx_proj_query (36 bytes)
+PROJ_QUERY_DTYPE = np.dtype([
+    ("u", "<f4"), ("v", "<f4"), ("radius", "<f4"), ("ur", "<f4"), ("ur_tol", "<f4"),
+    ("min_level", "<i4"), ("max_level", "<i4"), ("angle", "<f4"), ("flags", "<i4"),
+])
+assert PROJ_QUERY_DTYPE.itemsize == 36
+
+
+class MatchFrame(ctypes.Structure):
+    """orbx_match_frame"""
+    _fields_ = [("keys", ctypes.c_void_p), ("desc", ctypes.c_void_p), ("uright", ctypes.c_void_p),
+                ("mp_state", ctypes.c_void_p), ("inv_sigma2", ctypes.c_void_p), ("n", ctypes.c_int),
+                ("nlevels", ctypes.c_int), ("min_x", ctypes.c_float), ("max_x", ctypes.c_float),
+                ("min_y", ctypes.c_float), ("max_y", ctypes.c_float)]
+
 
 class OrbxError(RuntimeError):
     def __init__(self, code: int, what: str):
@@ -71,6 +86,7 @@ _SIGNATURES = {
     "orbx_rgbd_step_device": (I32, [P, P, I64, I32, I32, P, I64, I32, F32, P]),
     "orbx_depth_download": (I32, [P, I32, P, P, I32, P, P]),
     "orbx_stereo_from_rgbd": (I32, [I32, P, P, I32, P, I32, I32, SZ, F32, P, P, P]),
+    "orbx_search_by_projection": (I32, [I32, I32, P, P, P, I32, I32, F32, I32, P, P, P, P]),
     "orbx_descriptor_distance": (I32, [P, P]),
     "orbx_search_for_initialization": (I32, [I32, P, P, I32, P, P, I32, I32, I32, P, P, I32, F32, I32, P]),
     "orbx_debug_trig": (I32, [I32, P, P, P, I32, P, P, P, I32]),

@@ -97,6 +97,21 @@ struct StereoBufs {
     float *ur, *depth; int32_t *sad; int64_t ostride; int32_t *nkept;
 };
 
+// Projection searches (ORBmatcher SearchByProjection x4, Fuse x2): one frame
+// per launch, query table in reference loop order.
+struct ProjBufs {
+    const orbx_keypoint *keys; const uint8_t *desc; const float *uright; const uint8_t *mp_state;
+    const float *inv_sigma2;
+    int n, nlevels;
+    float min_x, max_x, min_y, max_y;
+    const orbx_proj_query *q; const uint8_t *qdesc; int nq;
+    int variant, th_dist; float nnratio; int check_ori;
+    int32_t *q_idx, *q_dist, *kp_final, *nmatches;
+    uint32_t *qtop; int32_t *qlen, *qbase;   // per query: 4 kept entries (16-B aligned), list length, pool base
+    uint32_t *spill; int64_t spill_stride;   // lists that do not fit the LDS pool: nq x spill_stride
+    int pool_cap;
+};
+
 enum Stage { kStageResize = 0, kStageBlur, kStageFast, kStageQuadtree, kStageDescribe, kStageMatch, kNumStages };
 
 hipError_t launch_resize(const DevPlan &p, const Plan &hp, const FrameBufs &fb, int B, hipStream_t s);
@@ -114,6 +129,8 @@ int stereo_lds_bytes(int rows, int nr_cap);
 hipError_t launch_rgbd(const orbx_keypoint *kps, const orbx_keypoint *kun, const int32_t *nkps, int64_t kstride,
                        int kcap, const float *dmap, int64_t dstride, int dpitch, int w, int h, float mbf, float *ur,
                        float *depth, int64_t ostride, int32_t *nkept, int B, hipStream_t s);
+hipError_t launch_proj(const ProjBufs &a, hipStream_t s);
+int proj_pool_cap(int n, int nq);   // -1: the frame does not fit the kernel's LDS
 int match_lds_bytes(int n1cap, int n2cap, int maxq, int maxc);
 int quadtree_lds_bytes(int node_cap);
 bool resize_window_fits(const Plan &hp);

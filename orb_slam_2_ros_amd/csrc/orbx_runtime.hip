@@ -1092,6 +1092,73 @@ int orbx_search_for_initialization(int device, const orbx_keypoint *k1, const ui
     return rc;
 }
 
+int orbx_search_by_projection(int device, int variant, const orbx_match_frame *F, const orbx_proj_query *queries,
+                              const uint8_t *qdesc, int nq, int th_dist, float nnratio, int check_ori,
+                              int32_t *q_idx, int32_t *q_dist, int32_t *kp_final, int *nmatches) {
+    if (!F || !nmatches || variant < ORBX_PROJ_LOCALMAP || variant > ORBX_PROJ_FUSE_SIM3) return ORBX_EINVAL;
+    const int n = F->n;
+    if (n < 0 || n > 32767 || nq < 0 || th_dist < 0 || th_dist > 255) return ORBX_EINVAL;
+    if ((n && (!F->keys || !F->desc || !kp_final)) || (nq && (!queries || !qdesc || !q_idx || !q_dist)))
+        return ORBX_EINVAL;
+    if (variant == ORBX_PROJ_FUSE && (!F->inv_sigma2 || F->nlevels <= 0 || F->nlevels > kMaxLevels)) return ORBX_EINVAL;
+    if (!(F->max_x > F->min_x) || !(F->max_y > F->min_y)) return ORBX_EINVAL;
+    *nmatches = 0;
+    if (n == 0 || nq == 0) {
+        for (int i = 0; i < nq; ++i) { q_idx[i] = -1; q_dist[i] = -1; }
+        for (int i = 0; i < n; ++i) kp_final[i] = -1;
+        return ORBX_OK;
+    }
+    const int pool_cap = proj_pool_cap(n, nq);
+    if (pool_cap < 0) return ORBX_EINVAL;
+    if (hipSetDevice(device) != hipSuccess) return ORBX_ENODEV;
+    const bool spill = (int64_t)nq * n > pool_cap;
+    orbx_keypoint *dk = nullptr;
+    uint8_t *dd = nullptr, *dms = nullptr, *dqd = nullptr;
+    float *dur = nullptr, *disg = nullptr;
+    orbx_proj_query *dq = nullptr;
+    int32_t *dqi = nullptr, *dqdist = nullptr, *dkf = nullptr, *dnm = nullptr, *dqlen = nullptr, *dqbase = nullptr;
+    uint32_t *dqtop = nullptr, *dspill = nullptr;
+    int rc = ORBX_OK;
+    bool ok = dalloc(&dk, n) == hipSuccess && dalloc(&dd, 32 * (size_t)n) == hipSuccess &&
+              dalloc(&dq, nq) == hipSuccess && dalloc(&dqd, 32 * (size_t)nq) == hipSuccess &&
+              dalloc(&dqi, nq) == hipSuccess && dalloc(&dqdist, nq) == hipSuccess && dalloc(&dkf, n) == hipSuccess &&
+              dalloc(&dnm, 1) == hipSuccess && dalloc(&dqtop, 4 * (size_t)nq) == hipSuccess &&
+              dalloc(&dqlen, nq) == hipSuccess && dalloc(&dqbase, nq) == hipSuccess;
+    if (ok && F->uright) ok = dalloc(&dur, n) == hipSuccess;
+    if (ok && F->mp_state) ok = dalloc(&dms, n) == hipSuccess;
+    if (ok && F->inv_sigma2 && F->nlevels > 0) ok = dalloc(&disg, F->nlevels) == hipSuccess;
+    if (ok && spill) ok = dalloc(&dspill, (size_t)nq * n) == hipSuccess;
+    if (!ok) rc = ORBX_ENOMEM;
+    if (!rc && (hipMemcpy(dk, F->keys, sizeof(orbx_keypoint) * n, hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(dd, F->desc, 32 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(dq, queries, sizeof(orbx_proj_query) * nq, hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(dqd, qdesc, 32 * (size_t)nq, hipMemcpyHostToDevice) != hipSuccess ||
+                (dur && hipMemcpy(dur, F->uright, 4 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess) ||
+                (dms && hipMemcpy(dms, F->mp_state, (size_t)n, hipMemcpyHostToDevice) != hipSuccess) ||
+                (disg && hipMemcpy(disg, F->inv_sigma2, 4 * (size_t)F->nlevels, hipMemcpyHostToDevice) != hipSuccess)))
+        rc = ORBX_EIO;
+    if (!rc) {
+        ProjBufs a{};
+        a.keys = dk; a.desc = dd; a.uright = dur; a.mp_state = dms; a.inv_sigma2 = disg;
+        a.n = n; a.nlevels = F->nlevels;
+        a.min_x = F->min_x; a.max_x = F->max_x; a.min_y = F->min_y; a.max_y = F->max_y;
+        a.q = dq; a.qdesc = dqd; a.nq = nq;
+        a.variant = variant; a.th_dist = th_dist; a.nnratio = nnratio; a.check_ori = check_ori;
+        a.q_idx = dqi; a.q_dist = dqdist; a.kp_final = dkf; a.nmatches = dnm;
+        a.qtop = dqtop; a.qlen = dqlen; a.qbase = dqbase;
+        a.spill = dspill; a.spill_stride = n; a.pool_cap = pool_cap;
+        if (launch_proj(a, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = ORBX_EIO;
+    }
+    if (!rc && (hipMemcpy(q_idx, dqi, 4 * (size_t)nq, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(q_dist, dqdist, 4 * (size_t)nq, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(kp_final, dkf, 4 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(nmatches, dnm, sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess))
+        rc = ORBX_EIO;
+    dfree(dk); dfree(dd); dfree(dms); dfree(dqd); dfree(dur); dfree(disg); dfree(dq); dfree(dqi); dfree(dqdist);
+    dfree(dkf); dfree(dnm); dfree(dqtop); dfree(dqlen); dfree(dqbase); dfree(dspill);
+    return rc;
+}
+
 int orbx_debug_trig(int device, const float *angles, float *s, float *c, int n, const float *ys, const float *xs,
                     float *atan_deg, int m) {
     if (n < 0 || m < 0) return ORBX_EINVAL;

@@ -17,7 +17,10 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import KEYPOINT_DTYPE, check, ptr
+from ._lib import KEYPOINT_DTYPE, PROJ_QUERY_DTYPE, MatchFrame, check, ptr
+
+# orbx_search_by_projection variants (include/orbx.h)
+PROJ_VARIANTS = {"localmap": 0, "lastframe": 1, "keyframe": 2, "sim3": 3, "fuse": 4, "fuse_sim3": 5}
 
 
 class Frame:
@@ -63,3 +66,37 @@ class ORBmatcher:
             ptr(vbPrevMatched), ptr(m12), int(windowSize), ctypes.c_float(self.mfNNratio),
             int(self.mbCheckOrientation), ctypes.byref(nm)), "SearchForInitialization")
         return nm.value, m12[:F1.N].copy()
+
+    # -- projection searches (ORBmatcher.cc:45-129, 291-404, 827-1102, 1330-1601) --
+    def search_by_projection(self, variant, keys, desc, queries, qdesc, bounds, uright=None, mp_state=None,
+                             inv_sigma2=None, th_dist=None):
+        """One of SearchByProjection x4 / Fuse x2 (search part) on a query table
+        (PROJ_QUERY_DTYPE rows in the reference's loop order; the caller
+        projects its map points).  variant: "localmap" (Frame&, vector<MapPoint*>&),
+        "lastframe" (Frame&, const Frame&), "keyframe" (Frame&, KeyFrame*, set),
+        "sim3" (KeyFrame*, Scw, ...), "fuse", "fuse_sim3".  th_dist defaults to
+        the reference's constant (TH_HIGH for localmap/lastframe, TH_LOW else).
+        Returns (nmatches, q_idx, q_dist, kp_final), see include/orbx.h."""
+        v = PROJ_VARIANTS[variant] if isinstance(variant, str) else int(variant)
+        if th_dist is None:
+            th_dist = self.TH_HIGH if v in (0, 1) else self.TH_LOW
+        keys = np.ascontiguousarray(keys, KEYPOINT_DTYPE)
+        desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        q = np.ascontiguousarray(queries, PROJ_QUERY_DTYPE)
+        qd = np.ascontiguousarray(qdesc, np.uint8).reshape(-1, 32)
+        if len(keys) != len(desc) or len(q) != len(qd):
+            raise ValueError("rows of keys/desc or queries/qdesc differ")
+        ur = None if uright is None else np.ascontiguousarray(uright, np.float32)
+        ms = None if mp_state is None else np.ascontiguousarray(mp_state, np.uint8)
+        isg = None if inv_sigma2 is None else np.ascontiguousarray(inv_sigma2, np.float32)
+        f = MatchFrame(ptr(keys), ptr(desc), ptr(ur), ptr(ms), ptr(isg), len(keys),
+                       0 if isg is None else len(isg), *[float(b) for b in bounds])
+        qi = np.full(max(len(q), 1), -1, np.int32)
+        qdist = np.full(max(len(q), 1), -1, np.int32)
+        kf = np.full(max(len(keys), 1), -1, np.int32)
+        nm = ctypes.c_int(0)
+        check(self._lib.orbx_search_by_projection(self.device, v, ctypes.byref(f), ptr(q), ptr(qd), len(q),
+                                                  int(th_dist), ctypes.c_float(self.mfNNratio),
+                                                  int(self.mbCheckOrientation), ptr(qi), ptr(qdist), ptr(kf),
+                                                  ctypes.byref(nm)), "SearchByProjection")
+        return nm.value, qi[:len(q)].copy(), qdist[:len(q)].copy(), kf[:len(keys)].copy()

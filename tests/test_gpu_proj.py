@@ -1,0 +1,68 @@
+"""GPU parity of the projection matchers (SURVEY.md §8 a15 SearchByProjection
+x4, a18 Fuse x2 search) against the CPU oracle on the same query tables:
+nmatches, per-query assignment and distance, and the final keypoint
+ownership must agree exactly."""
+import numpy as np
+import pytest
+
+from orb_slam_2_ros_amd import ORBmatcher
+
+pytestmark = pytest.mark.gpu
+
+VARIANTS = ["localmap", "lastframe", "keyframe", "sim3", "fuse", "fuse_sim3"]
+
+
+def _check(c, variant, oracle_mod, th=None):
+    from proj_cases import VARIANT_ARGS
+    th_dist, ratio, ori, _ = VARIANT_ARGS[variant]
+    if th is not None:
+        th_dist = th
+    g = ORBmatcher(ratio, ori).search_by_projection(variant, c["keys"], c["desc"], c["queries"], c["qdesc"],
+                                                    c["bounds"], c["uright"], c["mp_state"], c["inv_sigma2"],
+                                                    th_dist)
+    o = oracle_mod.search_by_projection(variant, c["keys"], c["desc"], c["queries"], c["qdesc"], c["bounds"],
+                                        c["uright"], c["mp_state"], c["inv_sigma2"], th_dist, ratio, ori)
+    assert g[0] == o[0], f"nmatches {g[0]} vs {o[0]}"
+    for name, x, y in zip(("q_idx", "q_dist", "kp_final"), g[1:], o[1:]):
+        bad = np.nonzero(x != y)[0]
+        assert len(bad) == 0, f"{name} differs at {bad[:5]}: {x[bad[:5]]} vs {y[bad[:5]]}"
+    return o[0]
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("seed,n,nq,stereo", [(91, 1000, 800, False), (92, 2500, 2000, True)])
+def test_projection_matchers_bit_exact(variant, seed, n, nq, stereo, oracle_mod):
+    from proj_cases import VARIANT_ARGS, make_case
+    c = make_case(seed, variant, n=n, nq=nq, stereo=stereo, th=VARIANT_ARGS[variant][3])
+    assert _check(c, variant, oracle_mod) > 0
+
+
+@pytest.mark.parametrize("variant", ["localmap", "lastframe", "keyframe"])
+def test_projection_matchers_contention(variant, oracle_mod):
+    """Wide windows over a dense frame with many near-duplicate descriptors:
+    long candidate lists (LDS pool overflow into global scratch), frequent
+    keypoint contention and full-list fallbacks in the greedy replay."""
+    from proj_cases import make_case
+    c = make_case(93, variant, n=6000, nq=3000, stereo=True, th=40.0)
+    rng = np.random.default_rng(5)
+    base = c["desc"][:40].copy()
+    c["desc"][:] = base[rng.integers(0, 40, len(c["desc"]))]
+    c["desc"] ^= (rng.integers(0, 256, c["desc"].shape) & rng.integers(0, 256, c["desc"].shape)
+                  & rng.integers(0, 256, c["desc"].shape) & rng.integers(0, 256, c["desc"].shape)).astype(np.uint8)
+    c["qdesc"][:] = base[rng.integers(0, 40, len(c["qdesc"]))]
+    _check(c, variant, oracle_mod)
+
+
+def test_projection_matchers_empty_and_edges(oracle_mod):
+    from proj_cases import make_case
+    c = make_case(94, "localmap", n=300, nq=200)
+    m = ORBmatcher(0.8, False)
+    nm, qi, qd, kf = m.search_by_projection("localmap", c["keys"][:0], c["desc"][:0], c["queries"], c["qdesc"],
+                                            c["bounds"])
+    assert nm == 0 and (qi == -1).all()
+    nm, qi, qd, kf = m.search_by_projection("localmap", c["keys"], c["desc"], c["queries"][:0], c["qdesc"][:0],
+                                            c["bounds"])
+    assert nm == 0 and (kf == -1).all()
+    q = c["queries"].copy()
+    q["flags"] = 0                      # every point skipped by the caller's own tests
+    assert _check(dict(c, queries=q), "localmap", oracle_mod) == 0
