@@ -244,3 +244,30 @@ def search_by_projection(variant, keys, desc, queries, qdesc, bounds, uright=Non
                                          len(keys), *[float(b) for b in bounds], _p(q), _p(qd), len(q),
                                          int(th_dist), float(nnratio), int(check_ori), _p(qi), _p(qdist), _p(kf))
     return nm, qi[:len(q)].copy(), qdist[:len(q)].copy(), kf[:len(keys)].copy()
+
+
+BOW_VARIANTS = {"kf_frame": 0, "kf_kf": 1, "triangulation": 2}
+
+
+def search_by_bow(variant, A, B, nnratio=0.6, check_ori=True, tri=None, nlevels=8):
+    """SearchByBoW(KF, F) / SearchByBoW(KF1, KF2) / SearchForTriangulation.
+    A, B: dicts with keys, desc, flags (u8), ids (u32, ascending), off (i32),
+    feat (i32).  Returns (nmatches, match_a, match_b)."""
+    f = lib().orbo_search_by_bow
+    f.restype = I32
+    f.argtypes = [I32, P, P, P, I32, P, P, P, I32, P, P, P, I32, P, P, P, I32, F32, I32, P, I32, P, P]
+
+    def side(S):
+        return (np.ascontiguousarray(S["keys"], KEYPOINT_DTYPE), np.ascontiguousarray(S["desc"], np.uint8),
+                np.ascontiguousarray(S["flags"], np.uint8), np.ascontiguousarray(S["ids"], np.uint32),
+                np.ascontiguousarray(S["off"], np.int32), np.ascontiguousarray(S["feat"], np.int32))
+    ka, da, fa, ia, oa, fea = side(A)
+    kb, db, fb, ib, ob, feb = side(B)
+    t = None if tri is None else np.ascontiguousarray(tri, np.float32)
+    ma = np.full(max(len(ka), 1), -1, np.int32)
+    mb = np.full(max(len(kb), 1), -1, np.int32)
+    v = BOW_VARIANTS[variant] if isinstance(variant, str) else int(variant)
+    nm = f(v, _p(ka), _p(da), _p(fa), len(ka), _p(ia), _p(oa), _p(fea), len(ia),
+           _p(kb), _p(db), _p(fb), len(kb), _p(ib), _p(ob), _p(feb), len(ib),
+           float(nnratio), int(check_ori), None if t is None else _p(t), int(nlevels), _p(ma), _p(mb))
+    return nm, ma[:len(ka)].copy(), mb[:len(kb)].copy()

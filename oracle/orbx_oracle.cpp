@@ -1056,3 +1056,129 @@ int orbo_search_by_projection(int variant, const orbo_keypoint *keys, const uint
     }
     return nmatches;
 }
+
+// ---- BoW matchers: SearchByBoW x2 (ORBmatcher.cc:160-289, 524-657) and
+//      SearchForTriangulation (:659-825 with CheckDistEpipolarLine :140-157) ----
+namespace {
+
+struct BowView {   // DBoW2::FeatureVector as CSR
+    const uint32_t *ids; const int32_t *off; const int32_t *feat; int nn;
+};
+
+// Common nodes in ascending id order (the reference's lower_bound merge join).
+template <typename F>
+void for_common_nodes(const BowView &A, const BowView &B, F f) {
+    int i = 0, j = 0;
+    while (i < A.nn && j < B.nn) {
+        if (A.ids[i] == B.ids[j]) { f(i, j); ++i; ++j; }
+        else if (A.ids[i] < B.ids[j]) { while (i < A.nn && A.ids[i] < B.ids[j]) ++i; }
+        else { while (j < B.nn && B.ids[j] < A.ids[i]) ++j; }
+    }
+}
+
+bool check_dist_epipolar_line(const orbo_keypoint &kp1, const orbo_keypoint &kp2, const float *F12,
+                              const float *sigma2_2) {
+    const float a = kp1.x * F12[0] + kp1.y * F12[3] + F12[6];
+    const float b = kp1.x * F12[1] + kp1.y * F12[4] + F12[7];
+    const float c = kp1.x * F12[2] + kp1.y * F12[5] + F12[8];
+    const float num = a * kp2.x + b * kp2.y + c;
+    const float den = a * a + b * b;
+    if (den == 0) return false;
+    const float dsqr = num * num / den;
+    return dsqr < 3.84 * sigma2_2[kp2.octave];
+}
+
+}  // namespace
+
+int orbo_search_by_bow(int variant, const orbo_keypoint *ka, const uint8_t *da, const uint8_t *fa, int na,
+                       const uint32_t *ida, const int32_t *offa, const int32_t *feata, int nna,
+                       const orbo_keypoint *kb, const uint8_t *db, const uint8_t *fb, int nb,
+                       const uint32_t *idb, const int32_t *offb, const int32_t *featb, int nnb,
+                       float nnratio, int check_ori, const float *tri, int nlevels,
+                       int32_t *match_a, int32_t *match_b) {
+    const int HL = 30, TH_LOW = 50;
+    const float factor = 1.0f / HL;
+    std::vector<int> rotHist[HL];
+    for (int i = 0; i < na; ++i) match_a[i] = -1;
+    for (int i = 0; i < nb; ++i) match_b[i] = -1;
+    std::vector<char> matched2(nb, 0);
+    int nmatches = 0;
+    const BowView A{ida, offa, feata, nna}, B{idb, offb, featb, nnb};
+    // triangulation parameters: F12 (row-major 3x3), epipole (ex, ey), then
+    // KF2's mvScaleFactors[nlevels] and mvLevelSigma2[nlevels]
+    const float *F12 = tri, *scale2 = tri ? tri + 11 : nullptr, *sigma2 = tri ? tri + 11 + nlevels : nullptr;
+    const float ex = tri ? tri[9] : 0.f, ey = tri ? tri[10] : 0.f;
+    for_common_nodes(A, B, [&](int na_i, int nb_i) {
+        for (int p = A.off[na_i]; p < A.off[na_i + 1]; ++p) {
+            const int i1 = A.feat[p];
+            if (!(fa[i1] & 1)) continue;
+            if (variant == ORBO_BOW_TRIANGULATION) {
+                const bool bStereo1 = (fa[i1] >> 1) & 1;
+                int bestDist = TH_LOW, bestIdx2 = -1;
+                for (int q = B.off[nb_i]; q < B.off[nb_i + 1]; ++q) {
+                    const int i2 = B.feat[q];
+                    if (matched2[i2] || !(fb[i2] & 1)) continue;
+                    const bool bStereo2 = (fb[i2] >> 1) & 1;
+                    const int dist = hamming32(da + 32 * (size_t)i1, db + 32 * (size_t)i2);
+                    if (dist > TH_LOW || dist > bestDist) continue;
+                    const orbo_keypoint &kp2 = kb[i2];
+                    if (!bStereo1 && !bStereo2) {
+                        const float distex = ex - kp2.x, distey = ey - kp2.y;
+                        if (distex * distex + distey * distey < 100 * scale2[kp2.octave]) continue;
+                    }
+                    if (check_dist_epipolar_line(ka[i1], kp2, F12, sigma2)) { bestIdx2 = i2; bestDist = dist; }
+                }
+                if (bestIdx2 >= 0) {
+                    match_a[i1] = bestIdx2;
+                    nmatches++;
+                    if (check_ori) {
+                        float rot = ka[i1].angle - kb[bestIdx2].angle;
+                        if (rot < 0.0) rot += 360.0f;
+                        int bin = (int)std::round(rot * factor);
+                        if (bin == HL) bin = 0;
+                        rotHist[bin].push_back(i1);
+                    }
+                }
+                continue;
+            }
+            int bestDist1 = 256, bestIdx2 = -1, bestDist2 = 256;
+            for (int q = B.off[nb_i]; q < B.off[nb_i + 1]; ++q) {
+                const int i2 = B.feat[q];
+                if (variant == ORBO_BOW_KF_FRAME) { if (match_b[i2] >= 0) continue; }
+                else if (matched2[i2] || !(fb[i2] & 1)) continue;
+                const int dist = hamming32(da + 32 * (size_t)i1, db + 32 * (size_t)i2);
+                if (dist < bestDist1) { bestDist2 = bestDist1; bestDist1 = dist; bestIdx2 = i2; }
+                else if (dist < bestDist2) { bestDist2 = dist; }
+            }
+            const bool pass = variant == ORBO_BOW_KF_FRAME ? bestDist1 <= TH_LOW : bestDist1 < TH_LOW;
+            if (pass && static_cast<float>(bestDist1) < nnratio * static_cast<float>(bestDist2)) {
+                match_a[i1] = bestIdx2;
+                match_b[bestIdx2] = i1;
+                matched2[bestIdx2] = 1;
+                if (check_ori) {
+                    float rot = ka[i1].angle - kb[bestIdx2].angle;
+                    if (rot < 0.0) rot += 360.0f;
+                    int bin = (int)std::round(rot * factor);
+                    if (bin == HL) bin = 0;
+                    rotHist[bin].push_back(i1);
+                }
+                nmatches++;
+            }
+        }
+    });
+    if (check_ori) {
+        int sizes[HL];
+        for (int i = 0; i < HL; ++i) sizes[i] = (int)rotHist[i].size();
+        int ind1, ind2, ind3;
+        three_maxima(sizes, HL, ind1, ind2, ind3);
+        for (int i = 0; i < HL; i++) {
+            if (i == ind1 || i == ind2 || i == ind3) continue;
+            for (int i1 : rotHist[i]) {
+                if (match_a[i1] >= 0 && variant != ORBO_BOW_TRIANGULATION) match_b[match_a[i1]] = -1;
+                match_a[i1] = -1;
+                nmatches--;
+            }
+        }
+    }
+    return nmatches;
+}

@@ -124,6 +124,23 @@ int   orbo_search_by_projection(int variant, const orbo_keypoint *keys, const ui
                                 int th_dist, float nnratio, int check_ori, int32_t *q_idx, int32_t *q_dist,
                                 int32_t *kp_final);
 
+/* ---- BoW matchers (ORBmatcher.cc:160-289, 524-657, 659-825) ----
+ * Side A = pKF / pKF1 (the outer loop), side B = F / pKF2.  Each side: keys,
+ * descriptors, per-feature flags (bit0 usable: A of the SearchByBoW variants =
+ * has a good map point; B of KF_FRAME = 1; B of KF_KF = has a good map point;
+ * triangulation = no map point yet [and stereo when bOnlyStereo]; bit1 =
+ * mvuRight >= 0), and the FeatureVector as CSR (ascending node ids, offsets,
+ * feature indices).  tri (triangulation only): F12 row-major [9], epipole
+ * ex, ey, then pKF2->mvScaleFactors[nlevels], pKF2->mvLevelSigma2[nlevels].
+ * match_a[na] / match_b[nb] receive the pairs (-1 none); returns nmatches. */
+enum { ORBO_BOW_KF_FRAME = 0, ORBO_BOW_KF_KF = 1, ORBO_BOW_TRIANGULATION = 2 };
+int   orbo_search_by_bow(int variant, const orbo_keypoint *ka, const uint8_t *da, const uint8_t *fa, int na,
+                         const uint32_t *ida, const int32_t *offa, const int32_t *feata, int nna,
+                         const orbo_keypoint *kb, const uint8_t *db, const uint8_t *fb, int nb,
+                         const uint32_t *idb, const int32_t *offb, const int32_t *featb, int nnb,
+                         float nnratio, int check_ori, const float *tri, int nlevels,
+                         int32_t *match_a, int32_t *match_b);
+
 #ifdef __cplusplus
 }
 #endif

@@ -557,3 +557,112 @@ def search_by_projection(variant, keys, desc, q, qdesc, bounds, uright=None, mp_
                 q_idx[iq] = -1
                 nm -= 1
     return nm, np.array(q_idx, np.int32), np.array(q_dist, np.int32), np.array(kp_final, np.int32)
+
+
+# ---- SearchByBoW x2 / SearchForTriangulation (ORBmatcher.cc:160-289, 524-825) ----
+def search_by_bow(variant, A, B, nnratio=0.6, check_ori=True, tri=None, nlevels=8):
+    na, nb = len(A["keys"]), len(B["keys"])
+    ma, mb = [-1] * na, [-1] * nb
+    hist = [[] for _ in range(30)]
+    nm = 0
+    idsB = {int(x): j for j, x in enumerate(B["ids"])}
+    if tri is not None:
+        F = [f32(x) for x in tri[:9]]
+        ex, ey = f32(tri[9]), f32(tri[10])
+        scale2, sigma2 = tri[11:11 + nlevels], tri[11 + nlevels:11 + 2 * nlevels]
+
+    def epi_ok(k1, k2):
+        x1, y1 = f32(k1["x"]), f32(k1["y"])
+        a = f32(f32(f32(x1 * F[0]) + f32(y1 * F[3])) + F[6])
+        b = f32(f32(f32(x1 * F[1]) + f32(y1 * F[4])) + F[7])
+        c = f32(f32(f32(x1 * F[2]) + f32(y1 * F[5])) + F[8])
+        num = f32(f32(f32(a * f32(k2["x"])) + f32(b * f32(k2["y"]))) + c)
+        den = f32(f32(a * a) + f32(b * b))
+        if den == 0:
+            return False
+        dsqr = f32(f32(num * num) / den)
+        return float(dsqr) < 3.84 * float(f32(sigma2[k2["octave"]]))
+
+    for i, nid in enumerate(A["ids"]):
+        j = idsB.get(int(nid))
+        if j is None:
+            continue
+        for p in range(A["off"][i], A["off"][i + 1]):
+            i1 = int(A["feat"][p])
+            if not (A["flags"][i1] & 1):
+                continue
+            if variant == "triangulation":
+                st1 = bool(A["flags"][i1] & 2)
+                bd, bi = 50, -1
+                for q in range(B["off"][j], B["off"][j + 1]):
+                    i2 = int(B["feat"][q])
+                    if not (B["flags"][i2] & 1):
+                        continue
+                    st2 = bool(B["flags"][i2] & 2)
+                    d = hamming(A["desc"][i1], B["desc"][i2])
+                    if d > 50 or d > bd:
+                        continue
+                    k2 = B["keys"][i2]
+                    if not st1 and not st2:
+                        dx, dy = f32(ex - f32(k2["x"])), f32(ey - f32(k2["y"]))
+                        if f32(f32(dx * dx) + f32(dy * dy)) < f32(f32(100) * f32(scale2[k2["octave"]])):
+                            continue
+                    if epi_ok(A["keys"][i1], k2):
+                        bi, bd = i2, d
+                if bi >= 0:
+                    ma[i1] = bi
+                    nm += 1
+                    if check_ori:
+                        rot = f32(f32(A["keys"]["angle"][i1]) - f32(B["keys"]["angle"][bi]))
+                        if rot < 0:
+                            rot = f32(rot + f32(360))
+                        b_ = round_half_away(f32(rot * f32(f32(1) / f32(30))))
+                        hist[0 if b_ == 30 else b_].append(i1)
+                continue
+            bd1, bi, bd2 = 256, -1, 256
+            for q in range(B["off"][j], B["off"][j + 1]):
+                i2 = int(B["feat"][q])
+                if variant == "kf_frame":
+                    if mb[i2] >= 0:
+                        continue
+                elif mb[i2] >= 0 or not (B["flags"][i2] & 1):
+                    continue
+                d = hamming(A["desc"][i1], B["desc"][i2])
+                if d < bd1:
+                    bd2, bd1, bi = bd1, d, i2
+                elif d < bd2:
+                    bd2 = d
+            ok = bd1 <= 50 if variant == "kf_frame" else bd1 < 50
+            if ok and f32(bd1) < f32(f32(nnratio) * f32(bd2)):
+                ma[i1], mb[bi] = bi, i1
+                nm += 1
+                if check_ori:
+                    rot = f32(f32(A["keys"]["angle"][i1]) - f32(B["keys"]["angle"][bi]))
+                    if rot < 0:
+                        rot = f32(rot + f32(360))
+                    b_ = round_half_away(f32(rot * f32(f32(1) / f32(30))))
+                    hist[0 if b_ == 30 else b_].append(i1)
+    if check_ori:
+        sizes = [len(h) for h in hist]
+        m1 = m2 = m3 = 0
+        i1_ = i2_ = i3_ = -1
+        for i, s in enumerate(sizes):
+            if s > m1:
+                m3, m2, m1, i3_, i2_, i1_ = m2, m1, s, i2_, i1_, i
+            elif s > m2:
+                m3, m2, i3_, i2_ = m2, s, i2_, i
+            elif s > m3:
+                m3, i3_ = s, i
+        if m2 < f32(0.1) * f32(m1):
+            i2_ = i3_ = -1
+        elif m3 < f32(0.1) * f32(m1):
+            i3_ = -1
+        for i in range(30):
+            if i in (i1_, i2_, i3_):
+                continue
+            for a in hist[i]:
+                if ma[a] >= 0 and variant != "triangulation":
+                    mb[ma[a]] = -1
+                ma[a] = -1
+                nm -= 1
+    return nm, np.array(ma, np.int32), np.array(mb, np.int32)

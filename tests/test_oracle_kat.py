@@ -254,3 +254,15 @@ def test_projection_matchers_vs_python(variant, seed, stereo, oracle_mod):
     assert a[0] == b[0] and a[0] > 20
     for x, y in zip(a[1:], b[1:]):
         assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("variant", ["kf_frame", "kf_kf", "triangulation"])
+@pytest.mark.parametrize("seed,ori", [(101, True), (102, False)])
+def test_bow_matchers_vs_python(variant, seed, ori, oracle_mod):
+    from bow_cases import VARIANT_ARGS, make_case
+    A, B, tri = make_case(seed, variant, na=700, nb=650)
+    ratio, _ = VARIANT_ARGS[variant]
+    a = oracle_mod.search_by_bow(variant, A, B, ratio, ori, tri)
+    b = pyref.search_by_bow(variant, A, B, ratio, ori, tri)
+    assert a[0] == b[0] and a[0] > 20
+    assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
