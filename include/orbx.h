@@ -253,6 +253,38 @@ int orbx_search_by_projection(int device, int variant, const orbx_match_frame *f
                               int th_dist, float nnratio, int check_ori, int32_t *q_idx,
                               int32_t *q_dist, int32_t *kp_final, int *nmatches);
 
+/* ORBmatcher vocabulary-node searches (ORBmatcher.cc:160-289, 524-657,
+ * 659-825).  Each side is a keyframe / frame with its DBoW2::FeatureVector
+ * given as CSR: ascending node ids, offsets (nnodes + 1), and the feature
+ * indices of every node in the vector's order.  flags per feature: bit0 =
+ * usable as the reference tests it (side A of SearchByBoW: has a map point
+ * that is not bad; side B of the KF-KF search: the same; both sides of
+ * SearchForTriangulation: no map point yet, and stereo if bOnlyStereo;
+ * side B of the KF-Frame search: ignored), bit1 = mvuRight >= 0. */
+typedef struct orbx_bow_side {
+    const orbx_keypoint *keys;   /* mvKeysUn (angles; positions for triangulation) */
+    const uint8_t *desc;
+    const uint8_t *flags;
+    int n;
+    const uint32_t *node_ids;
+    const int32_t *node_offsets;
+    const int32_t *node_features;
+    int nnodes;
+} orbx_bow_side;
+
+#define ORBX_BOW_KF_FRAME 0      /* SearchByBoW(KeyFrame* A, Frame& B, vpMapPointMatches)      :160 */
+#define ORBX_BOW_KF_KF 1         /* SearchByBoW(KeyFrame* A, KeyFrame* B, vpMatches12)         :524 */
+#define ORBX_BOW_TRIANGULATION 2 /* SearchForTriangulation(KeyFrame* A, KeyFrame* B, F12, ...)  :659 */
+
+/* tri (triangulation only): F12 row-major [9], the epipole (ex, ey) in B,
+ * then B's mvScaleFactors[nlevels] and mvLevelSigma2[nlevels].
+ * match_a[a.n] / match_b[b.n]: the pairs (-1 none; match_b unused by
+ * triangulation, whose pairs are (i, match_a[i]) in index order);
+ * *nmatches: the reference's return value.  Synchronous. */
+int orbx_search_by_bow(int device, int variant, const orbx_bow_side *a, const orbx_bow_side *b,
+                       float nnratio, int check_ori, const float *tri, int nlevels,
+                       int32_t *match_a, int32_t *match_b, int *nmatches);
+
 /* Device evaluation of the restated sincosf / fastAtan2 (test hook). */
 int orbx_debug_trig(int device, const float *angles, float *s, float *c, int n,
                     const float *ys, const float *xs, float *atan_deg, int m);

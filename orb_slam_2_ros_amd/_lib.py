@@ -36,6 +36,13 @@ PROJ_QUERY_DTYPE = np.dtype([
 assert PROJ_QUERY_DTYPE.itemsize == 36
 
 
+class BowSide(ctypes.Structure):
+    """orbx_bow_side"""
+    _fields_ = [("keys", ctypes.c_void_p), ("desc", ctypes.c_void_p), ("flags", ctypes.c_void_p),
+                ("n", ctypes.c_int), ("node_ids", ctypes.c_void_p), ("node_offsets", ctypes.c_void_p),
+                ("node_features", ctypes.c_void_p), ("nnodes", ctypes.c_int)]
+
+
 class MatchFrame(ctypes.Structure):
     """orbx_match_frame"""
     _fields_ = [("keys", ctypes.c_void_p), ("desc", ctypes.c_void_p), ("uright", ctypes.c_void_p),
@@ -87,6 +94,7 @@ _SIGNATURES = {
     "orbx_depth_download": (I32, [P, I32, P, P, I32, P, P]),
     "orbx_stereo_from_rgbd": (I32, [I32, P, P, I32, P, I32, I32, SZ, F32, P, P, P]),
     "orbx_search_by_projection": (I32, [I32, I32, P, P, P, I32, I32, F32, I32, P, P, P, P]),
+    "orbx_search_by_bow": (I32, [I32, I32, P, P, F32, I32, P, I32, P, P, P]),
     "orbx_descriptor_distance": (I32, [P, P]),
     "orbx_search_for_initialization": (I32, [I32, P, P, I32, P, P, I32, I32, I32, P, P, I32, F32, I32, P]),
     "orbx_debug_trig": (I32, [I32, P, P, P, I32, P, P, P, I32]),

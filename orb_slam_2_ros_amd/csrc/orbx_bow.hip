@@ -1,0 +1,223 @@
+// orbx_bow.hip -- ORBmatcher's vocabulary-node matchers on gfx950:
+// SearchByBoW(KeyFrame*, Frame&) (ORBmatcher.cc:160-289), SearchByBoW(KeyFrame*,
+// KeyFrame*) (:524-657) and SearchForTriangulation (:659-825, epipolar test
+// CheckDistEpipolarLine :140-157).
+//
+// The reference merge-joins the two FeatureVectors (node id -> feature
+// indices) and compares only features that share a node.  A feature belongs
+// to exactly one node, so the greedy "already matched" state of the two
+// SearchByBoW variants never crosses nodes: nodes are independent.  One wave
+// takes one node of side A, finds it in side B (binary search over the
+// ascending ids) and walks A's features in order; for each, the lanes hold
+// B's features of the node, compute the distances and reduce (distance,
+// position) minima with DPP.  Accepted B positions are flagged in the wave's
+// LDS.  SearchForTriangulation never sets its vbMatched2 (the reference
+// leaves it false), so there every A feature is independent; its update rule
+// (dist <= bestDist, after the epipolar tests) keeps the LAST minimum.
+// The rotation-consistency pass runs in a second single-block kernel.
+#include <hip/hip_runtime.h>
+
+#include "orbx_device.h"
+#include "orbx_wave.h"
+
+namespace orbx {
+namespace {
+
+constexpr int kBT = 256;
+constexpr int kHist = 30;
+constexpr int kThLow = 50;
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+__device__ inline int hamming_rr(const uint4 a0, const uint4 a1, const uint4 b0, const uint4 b1) {
+    return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+           __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+__device__ inline int rot_bin(float a1, float a2) {
+    float rot = __fsub_rn(a1, a2);
+    if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
+    int bin = (int)roundf(__fmul_rn(rot, 1.0f / kHist));
+    return bin == kHist ? 0 : bin;
+}
+
+// CheckDistEpipolarLine (ORBmatcher.cc:140-157); F row-major.
+__device__ inline bool epipolar_ok(float x1, float y1, float x2, float y2, const float *F, float sigma2) {
+    const float a = __fadd_rn(__fadd_rn(__fmul_rn(x1, F[0]), __fmul_rn(y1, F[3])), F[6]);
+    const float b = __fadd_rn(__fadd_rn(__fmul_rn(x1, F[1]), __fmul_rn(y1, F[4])), F[7]);
+    const float c = __fadd_rn(__fadd_rn(__fmul_rn(x1, F[2]), __fmul_rn(y1, F[5])), F[8]);
+    const float num = __fadd_rn(__fadd_rn(__fmul_rn(a, x2), __fmul_rn(b, y2)), c);
+    const float den = __fadd_rn(__fmul_rn(a, a), __fmul_rn(b, b));
+    if (den == 0.0f) return false;
+    const float dsqr = __fdiv_rn(__fmul_rn(num, num), den);
+    return (double)dsqr < __dmul_rn(3.84, (double)sigma2);
+}
+
+__global__ __launch_bounds__(kBT) void k_bow_match(BowBufs a) {
+    __shared__ uint8_t matched[kBT / 64][kBowNodeCap];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int na_node = blockIdx.x * (kBT / 64) + wave;
+    if (na_node >= a.A.nnodes) return;
+    // the node in side B
+    const uint32_t id = a.A.node_ids[na_node];
+    int lo = 0, hi = a.B.nnodes - 1, nb_node = -1;
+    while (lo <= hi) {
+        const int mid = (lo + hi) >> 1;
+        const uint32_t v = a.B.node_ids[mid];
+        if (v == id) { nb_node = mid; break; }
+        if (v < id) lo = mid + 1; else hi = mid - 1;
+    }
+    if (nb_node < 0) return;
+    const int a0 = a.A.node_offsets[na_node], a1 = a.A.node_offsets[na_node + 1];
+    const int b0 = a.B.node_offsets[nb_node], nbk = a.B.node_offsets[nb_node + 1] - b0;
+    const bool tri = a.variant == ORBX_BOW_TRIANGULATION;
+    uint8_t *mflag = matched[wave];
+    for (int p = lane; p < nbk; p += 64) mflag[p] = 0;
+    // the first 64 B features stay in registers
+    int i2r = -1, fbr = 0, octr = 0;
+    uint4 d0r = make_uint4(0, 0, 0, 0), d1r = d0r;
+    float xr = 0.f, yr = 0.f;
+    if (lane < nbk) {
+        i2r = a.B.node_features[b0 + lane];
+        fbr = a.B.flags[i2r];
+        const uint4 *dp = reinterpret_cast<const uint4 *>(a.B.desc + 32 * (int64_t)i2r);
+        d0r = dp[0]; d1r = dp[1];
+        const orbx_keypoint k = a.B.keys[i2r];
+        xr = k.x; yr = k.y; octr = k.octave;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const float *F = a.tri;
+    for (int p = a0; p < a1; ++p) {
+        const int i1 = a.A.node_features[p];
+        const int fa = a.A.flags[i1];
+        if (!(fa & 1)) continue;
+        const uint4 *ap = reinterpret_cast<const uint4 *>(a.A.desc + 32 * (int64_t)i1);
+        const uint4 qa = ap[0], qb = ap[1];
+        const orbx_keypoint k1 = a.A.keys[i1];
+        const bool st1 = (fa >> 1) & 1;
+        uint32_t k_1 = kNone, k_2 = kNone;   // running (dist << 16 | position) smallest two
+        int x_1 = -1;                         // B feature of k_1
+        for (int c0 = 0; c0 < nbk; c0 += 64) {
+            const int pos = c0 + lane;
+            int i2 = -1, fb = 0, oct = 0;
+            uint4 e0, e1;
+            float x2 = 0.f, y2 = 0.f;
+            if (c0 == 0) {
+                i2 = i2r; fb = fbr; e0 = d0r; e1 = d1r; x2 = xr; y2 = yr; oct = octr;
+            } else if (pos < nbk) {
+                i2 = a.B.node_features[b0 + pos];
+                fb = a.B.flags[i2];
+                const uint4 *dp = reinterpret_cast<const uint4 *>(a.B.desc + 32 * (int64_t)i2);
+                e0 = dp[0]; e1 = dp[1];
+                const orbx_keypoint k = a.B.keys[i2];
+                x2 = k.x; y2 = k.y; oct = k.octave;
+            }
+            uint32_t key = kNone;
+            if (pos < nbk) {
+                const bool usable = a.variant == ORBX_BOW_KF_FRAME ? true : (fb & 1);
+                if (usable && !(tri ? false : mflag[pos])) {
+                    const int dist = hamming_rr(qa, qb, e0, e1);
+                    if (!tri) {
+                        key = ((uint32_t)dist << 16) | (uint32_t)pos;
+                    } else if (dist <= kThLow) {
+                        bool ok = true;
+                        const bool st2 = (fb >> 1) & 1;
+                        const bool lv = oct >= 0 && oct < a.nlevels;
+                        if (!st1 && !st2) {
+                            const float dx = __fsub_rn(a.ex, x2), dy = __fsub_rn(a.ey, y2);
+                            const float sc = lv ? F[11 + oct] : 0.0f;
+                            if (__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)) < __fmul_rn(100.0f, sc)) ok = false;
+                        }
+                        if (ok && epipolar_ok(k1.x, k1.y, x2, y2, F, lv ? F[11 + a.nlevels + oct] : 0.0f))
+                            key = ((uint32_t)dist << 16) | (uint32_t)(0xFFFF - pos);   // last minimum wins
+                    }
+                }
+            }
+            const uint32_t m1 = wave_min_u32(key);
+            if (m1 == kNone) continue;
+            const int l1 = tri ? (int)(0xFFFF - (m1 & 0xFFFF)) - c0 : (int)(m1 & 0xFFFF) - c0;
+            const int w1 = __builtin_amdgcn_readlane(i2, l1);
+            if (tri) {
+                if (m1 < k_1) { k_1 = m1; x_1 = w1; }
+                continue;
+            }
+            const uint32_t m2 = wave_min_u32(lane == l1 ? kNone : key);
+            if (m1 < k_1) {
+                k_2 = m2 < k_1 ? m2 : k_1;
+                k_1 = m1;
+                x_1 = w1;
+            } else if (m1 < k_2) {
+                k_2 = m1;
+            }
+        }
+        if (k_1 == kNone) continue;
+        const int best1 = (int)(k_1 >> 16);
+        if (!tri) {
+            const int best2 = k_2 == kNone ? 256 : (int)(k_2 >> 16);
+            const bool pass = a.variant == ORBX_BOW_KF_FRAME ? best1 <= kThLow : best1 < kThLow;
+            if (!(pass && (float)best1 < __fmul_rn(a.nnratio, (float)best2))) continue;
+            if (lane == 0) mflag[k_1 & 0xFFFF] = 1;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        if (lane == 0) {
+            a.match_a[i1] = x_1;
+            if (!tri) a.match_b[x_1] = i1;
+            if (a.check_ori) {
+                const int bin = rot_bin(k1.angle, a.B.keys[x_1].angle);
+                a.bin_a[i1] = (int8_t)bin;
+                atomicAdd(&a.hist[bin], 1);
+            }
+            atomicAdd(&a.counts[0], 1);
+        }
+    }
+}
+
+// ComputeThreeMaxima + removal of the matches outside the three main bins.
+__global__ __launch_bounds__(1024) void k_bow_finish(BowBufs a) {
+    __shared__ int top[3];
+    __shared__ int removed;
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        removed = 0;
+        int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+        for (int i = 0; i < kHist; ++i) {
+            const int sz = a.hist[i];
+            if (sz > max1) { max3 = max2; max2 = max1; max1 = sz; ind3 = ind2; ind2 = ind1; ind1 = i; }
+            else if (sz > max2) { max3 = max2; max2 = sz; ind3 = ind2; ind2 = i; }
+            else if (sz > max3) { max3 = sz; ind3 = i; }
+        }
+        if ((float)max2 < __fmul_rn(0.1f, (float)max1)) { ind2 = -1; ind3 = -1; }
+        else if ((float)max3 < __fmul_rn(0.1f, (float)max1)) { ind3 = -1; }
+        top[0] = ind1; top[1] = ind2; top[2] = ind3;
+    }
+    __syncthreads();
+    if (a.check_ori) {
+        int local = 0;
+        for (int i1 = tid; i1 < a.A.n; i1 += blockDim.x) {
+            const int m = a.match_a[i1];
+            if (m < 0) continue;
+            const int bin = a.bin_a[i1];
+            if (bin == top[0] || bin == top[1] || bin == top[2]) continue;
+            a.match_a[i1] = -1;
+            if (a.variant != ORBX_BOW_TRIANGULATION) a.match_b[m] = -1;
+            ++local;
+        }
+        if (local) atomicAdd(&removed, local);
+    }
+    __syncthreads();
+    if (tid == 0) a.counts[1] = a.counts[0] - removed;
+}
+
+}  // namespace
+
+hipError_t launch_bow(const BowBufs &a, hipStream_t st) {
+    if (a.A.nnodes > 0)
+        hipLaunchKernelGGL(k_bow_match, dim3((a.A.nnodes + kBT / 64 - 1) / (kBT / 64)), dim3(kBT), 0, st, a);
+    hipLaunchKernelGGL(k_bow_finish, dim3(1), dim3(1024), 0, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace orbx

@@ -112,6 +112,23 @@ struct ProjBufs {
     int pool_cap;
 };
 
+// Vocabulary-node matchers (SearchByBoW x2, SearchForTriangulation).
+constexpr int kBowNodeCap = 2048;   // largest side-B node (features) a wave handles
+struct BowSideDev {
+    const orbx_keypoint *keys; const uint8_t *desc; const uint8_t *flags; int n;
+    const uint32_t *node_ids; const int32_t *node_offsets; const int32_t *node_features; int nnodes;
+};
+struct BowBufs {
+    BowSideDev A, B;
+    int variant; float nnratio; int check_ori;
+    const float *tri;   // F12[9], ex, ey, scale2[nlevels], sigma2[nlevels] (triangulation)
+    float ex, ey; int nlevels;
+    int32_t *match_a, *match_b;
+    int8_t *bin_a;      // rotation bin per accepted A feature
+    int32_t *hist;      // 30 bins
+    int32_t *counts;    // [0] accepted, [1] nmatches after the rotation check
+};
+
 enum Stage { kStageResize = 0, kStageBlur, kStageFast, kStageQuadtree, kStageDescribe, kStageMatch, kNumStages };
 
 hipError_t launch_resize(const DevPlan &p, const Plan &hp, const FrameBufs &fb, int B, hipStream_t s);
@@ -131,6 +148,7 @@ hipError_t launch_rgbd(const orbx_keypoint *kps, const orbx_keypoint *kun, const
                        float *depth, int64_t ostride, int32_t *nkept, int B, hipStream_t s);
 hipError_t launch_proj(const ProjBufs &a, hipStream_t s);
 int proj_pool_cap(int n, int nq);   // -1: the frame does not fit the kernel's LDS
+hipError_t launch_bow(const BowBufs &a, hipStream_t s);
 int match_lds_bytes(int n1cap, int n2cap, int maxq, int maxc);
 int quadtree_lds_bytes(int node_cap);
 bool resize_window_fits(const Plan &hp);

@@ -118,7 +118,13 @@ __global__ __launch_bounds__(kPT) void k_proj_match(ProjBufs a) {
         s.state[i] = a.mp_state ? (a.mp_state[i] & 3) : 0;
         a.kp_final[i] = -1;
     }
-    for (int i = tid; i < nq; i += kPT) { a.q_idx[i] = -1; a.q_dist[i] = -1; }
+    for (int i = tid; i < nq; i += kPT) {
+        a.q_idx[i] = -1;
+        a.q_dist[i] = -1;
+        a.qlen[i] = 0;   // queries with an empty window never reach phase 2's stores
+        a.qbase[i] = -1;
+        reinterpret_cast<uint4 *>(a.qtop)[i] = make_uint4(kNone, kNone, kNone, kNone);
+    }
     if (tid < kHist) hist[tid] = 0;
     if (tid == 0) { sh_pool = 0; sh_acc = 0; sh_removed = 0; }
     __syncthreads();

@@ -1159,6 +1159,82 @@ int orbx_search_by_projection(int device, int variant, const orbx_match_frame *F
     return rc;
 }
 
+int orbx_search_by_bow(int device, int variant, const orbx_bow_side *A, const orbx_bow_side *B, float nnratio,
+                       int check_ori, const float *tri, int nlevels, int32_t *match_a, int32_t *match_b,
+                       int *nmatches) {
+    if (!A || !B || !nmatches || variant < ORBX_BOW_KF_FRAME || variant > ORBX_BOW_TRIANGULATION) return ORBX_EINVAL;
+    if (A->n < 0 || B->n < 0 || A->nnodes < 0 || B->nnodes < 0 || (A->n && !match_a) || (B->n && !match_b))
+        return ORBX_EINVAL;
+    if (variant == ORBX_BOW_TRIANGULATION && (!tri || nlevels <= 0 || nlevels > kMaxLevels)) return ORBX_EINVAL;
+    for (const orbx_bow_side *S : {A, B}) {
+        if (S->n && (!S->keys || !S->desc || !S->flags)) return ORBX_EINVAL;
+        if (S->nnodes && (!S->node_ids || !S->node_offsets || !S->node_features)) return ORBX_EINVAL;
+        for (int k = 0; k < S->nnodes; ++k) {   // ascending ids, sane offsets, indices in range
+            if (k > 0 && S->node_ids[k] <= S->node_ids[k - 1]) return ORBX_EINVAL;
+            if (S->node_offsets[k + 1] < S->node_offsets[k]) return ORBX_EINVAL;
+        }
+        const int nf = S->nnodes ? S->node_offsets[S->nnodes] : 0;
+        if (S->nnodes && S->node_offsets[0] != 0) return ORBX_EINVAL;
+        for (int k = 0; k < nf; ++k)
+            if (S->node_features[k] < 0 || S->node_features[k] >= S->n) return ORBX_EINVAL;
+    }
+    for (int k = 0; k < B->nnodes; ++k)
+        if (B->node_offsets[k + 1] - B->node_offsets[k] > kBowNodeCap) return ORBX_EINVAL;
+    *nmatches = 0;
+    for (int i = 0; i < A->n; ++i) match_a[i] = -1;
+    for (int i = 0; i < B->n; ++i) match_b[i] = -1;
+    if (A->n == 0 || B->n == 0 || A->nnodes == 0 || B->nnodes == 0) return ORBX_OK;
+    if (hipSetDevice(device) != hipSuccess) return ORBX_ENODEV;
+    const int nfa = A->node_offsets[A->nnodes], nfb = B->node_offsets[B->nnodes];
+    orbx_keypoint *dka = nullptr, *dkb = nullptr;
+    uint8_t *dda = nullptr, *ddb = nullptr, *dfa = nullptr, *dfb = nullptr;
+    uint32_t *dia = nullptr, *dib = nullptr;
+    int32_t *doa = nullptr, *dob = nullptr, *dea = nullptr, *deb = nullptr, *dma = nullptr, *dmb = nullptr;
+    int32_t *dhist = nullptr;
+    int8_t *dbin = nullptr;
+    float *dtri = nullptr;
+    const int ntri = variant == ORBX_BOW_TRIANGULATION ? 11 + 2 * nlevels : 0;
+    int rc = ORBX_OK;
+    bool ok = dalloc(&dka, A->n) == hipSuccess && dalloc(&dkb, B->n) == hipSuccess &&
+              dalloc(&dda, 32 * (size_t)A->n) == hipSuccess && dalloc(&ddb, 32 * (size_t)B->n) == hipSuccess &&
+              dalloc(&dfa, A->n) == hipSuccess && dalloc(&dfb, B->n) == hipSuccess &&
+              dalloc(&dia, A->nnodes) == hipSuccess && dalloc(&dib, B->nnodes) == hipSuccess &&
+              dalloc(&doa, A->nnodes + 1) == hipSuccess && dalloc(&dob, B->nnodes + 1) == hipSuccess &&
+              dalloc(&dea, std::max(nfa, 1)) == hipSuccess && dalloc(&deb, std::max(nfb, 1)) == hipSuccess &&
+              dalloc(&dma, A->n) == hipSuccess && dalloc(&dmb, B->n) == hipSuccess &&
+              dalloc(&dhist, 32 + 2) == hipSuccess && dalloc(&dbin, A->n) == hipSuccess;
+    if (ok && ntri) ok = dalloc(&dtri, ntri) == hipSuccess;
+    if (!ok) rc = ORBX_ENOMEM;
+    auto up = [](void *d, const void *h, size_t b) { return b == 0 || hipMemcpy(d, h, b, hipMemcpyHostToDevice) == hipSuccess; };
+    if (!rc && !(up(dka, A->keys, sizeof(orbx_keypoint) * A->n) && up(dkb, B->keys, sizeof(orbx_keypoint) * B->n) &&
+                 up(dda, A->desc, 32 * (size_t)A->n) && up(ddb, B->desc, 32 * (size_t)B->n) &&
+                 up(dfa, A->flags, A->n) && up(dfb, B->flags, B->n) && up(dia, A->node_ids, 4 * (size_t)A->nnodes) &&
+                 up(dib, B->node_ids, 4 * (size_t)B->nnodes) && up(doa, A->node_offsets, 4 * (size_t)(A->nnodes + 1)) &&
+                 up(dob, B->node_offsets, 4 * (size_t)(B->nnodes + 1)) && up(dea, A->node_features, 4 * (size_t)nfa) &&
+                 up(deb, B->node_features, 4 * (size_t)nfb) && up(dma, match_a, 4 * (size_t)A->n) &&
+                 up(dmb, match_b, 4 * (size_t)B->n) && up(dtri, tri, 4 * (size_t)ntri) &&
+                 hipMemset(dhist, 0, 4 * (32 + 2)) == hipSuccess))
+        rc = ORBX_EIO;
+    if (!rc) {
+        BowBufs a{};
+        a.A = BowSideDev{dka, dda, dfa, A->n, dia, doa, dea, A->nnodes};
+        a.B = BowSideDev{dkb, ddb, dfb, B->n, dib, dob, deb, B->nnodes};
+        a.variant = variant; a.nnratio = nnratio; a.check_ori = check_ori;
+        a.tri = dtri; a.ex = ntri ? tri[9] : 0.f; a.ey = ntri ? tri[10] : 0.f; a.nlevels = nlevels;
+        a.match_a = dma; a.match_b = dmb; a.bin_a = dbin; a.hist = dhist; a.counts = dhist + 32;
+        if (launch_bow(a, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = ORBX_EIO;
+    }
+    int32_t counts[2] = {0, 0};
+    if (!rc && (hipMemcpy(match_a, dma, 4 * (size_t)A->n, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(match_b, dmb, 4 * (size_t)B->n, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(counts, dhist + 32, sizeof(counts), hipMemcpyDeviceToHost) != hipSuccess))
+        rc = ORBX_EIO;
+    if (!rc) *nmatches = counts[1];
+    dfree(dka); dfree(dkb); dfree(dda); dfree(ddb); dfree(dfa); dfree(dfb); dfree(dia); dfree(dib); dfree(doa);
+    dfree(dob); dfree(dea); dfree(deb); dfree(dma); dfree(dmb); dfree(dhist); dfree(dbin); dfree(dtri);
+    return rc;
+}
+
 int orbx_debug_trig(int device, const float *angles, float *s, float *c, int n, const float *ys, const float *xs,
                     float *atan_deg, int m) {
     if (n < 0 || m < 0) return ORBX_EINVAL;

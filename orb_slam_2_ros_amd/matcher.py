@@ -17,10 +17,12 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import KEYPOINT_DTYPE, PROJ_QUERY_DTYPE, MatchFrame, check, ptr
+from ._lib import KEYPOINT_DTYPE, PROJ_QUERY_DTYPE, BowSide, MatchFrame, check, ptr
 
 # orbx_search_by_projection variants (include/orbx.h)
 PROJ_VARIANTS = {"localmap": 0, "lastframe": 1, "keyframe": 2, "sim3": 3, "fuse": 4, "fuse_sim3": 5}
+# orbx_search_by_bow variants
+BOW_VARIANTS = {"kf_frame": 0, "kf_kf": 1, "triangulation": 2}
 
 
 class Frame:
@@ -100,3 +102,31 @@ class ORBmatcher:
                                                   int(self.mbCheckOrientation), ptr(qi), ptr(qdist), ptr(kf),
                                                   ctypes.byref(nm)), "SearchByProjection")
         return nm.value, qi[:len(q)].copy(), qdist[:len(q)].copy(), kf[:len(keys)].copy()
+
+    # -- vocabulary-node searches (ORBmatcher.cc:160-289, 524-657, 659-825) --
+    def search_by_bow(self, variant, A, B, tri=None, nlevels=8):
+        """SearchByBoW(KF, F) ("kf_frame"), SearchByBoW(KF1, KF2) ("kf_kf") or
+        SearchForTriangulation ("triangulation").  A, B: dicts with keys, desc,
+        flags (see include/orbx.h), ids / off / feat (the FeatureVector as CSR).
+        tri: F12[9], ex, ey, B's scale factors and sigma2 (triangulation).
+        Returns (nmatches, match_a, match_b)."""
+        v = BOW_VARIANTS[variant] if isinstance(variant, str) else int(variant)
+        keep = []
+
+        def side(S):
+            arrs = (np.ascontiguousarray(S["keys"], KEYPOINT_DTYPE), np.ascontiguousarray(S["desc"], np.uint8),
+                    np.ascontiguousarray(S["flags"], np.uint8), np.ascontiguousarray(S["ids"], np.uint32),
+                    np.ascontiguousarray(S["off"], np.int32), np.ascontiguousarray(S["feat"], np.int32))
+            keep.append(arrs)
+            k, d, f, i, o, e = arrs
+            return BowSide(ptr(k), ptr(d), ptr(f), len(k), ptr(i), ptr(o), ptr(e), len(i))
+        sa, sb = side(A), side(B)
+        t = None if tri is None else np.ascontiguousarray(tri, np.float32)
+        na, nb = len(keep[0][0]), len(keep[1][0])
+        ma = np.full(max(na, 1), -1, np.int32)
+        mb = np.full(max(nb, 1), -1, np.int32)
+        nm = ctypes.c_int(0)
+        check(self._lib.orbx_search_by_bow(self.device, v, ctypes.byref(sa), ctypes.byref(sb),
+                                           ctypes.c_float(self.mfNNratio), int(self.mbCheckOrientation), ptr(t),
+                                           int(nlevels), ptr(ma), ptr(mb), ctypes.byref(nm)), "SearchByBoW")
+        return nm.value, ma[:na].copy(), mb[:nb].copy()
