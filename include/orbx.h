@@ -253,6 +253,20 @@ int orbx_search_by_projection(int device, int variant, const orbx_match_frame *f
                               int th_dist, float nnratio, int check_ori, int32_t *q_idx,
                               int32_t *q_dist, int32_t *kp_final, int *nmatches);
 
+/* int SearchBySim3(KeyFrame *pKF1, KeyFrame *pKF2, vector<MapPoint*> &vpMatches12,
+ *                  const float &s12, const cv::Mat &R12, const cv::Mat &t12, th)
+ *                                                     ORBmatcher.cc:1104-1328
+ * q1: one row per pKF1 map-point slot, its projection into pKF2 (inactive for
+ * NULL / bad / already matched / rejected points); q2 likewise for pKF2 into
+ * pKF1; each row's level window is [pred - 1, pred].  Two independent window
+ * searches (best only, TH_HIGH = th_dist) on the device, then the agreement
+ * check: matches12[kf1->n] = the KF2 index of each newly agreed pair (-1
+ * none; the caller sets vpMatches12[i1] = vpMapPoints2[matches12[i1]]).
+ * *nfound = the reference's return value.  Synchronous. */
+int orbx_search_by_sim3(int device, const orbx_match_frame *kf1, const orbx_match_frame *kf2,
+                        const orbx_proj_query *q1, const uint8_t *qdesc1, const orbx_proj_query *q2,
+                        const uint8_t *qdesc2, int th_dist, int32_t *matches12, int *nfound);
+
 /* ORBmatcher vocabulary-node searches (ORBmatcher.cc:160-289, 524-657,
  * 659-825).  Each side is a keyframe / frame with its DBoW2::FeatureVector
  * given as CSR: ascending node ids, offsets (nnodes + 1), and the feature

@@ -271,3 +271,18 @@ def search_by_bow(variant, A, B, nnratio=0.6, check_ori=True, tri=None, nlevels=
            _p(kb), _p(db), _p(fb), len(kb), _p(ib), _p(ob), _p(feb), len(ib),
            float(nnratio), int(check_ori), None if t is None else _p(t), int(nlevels), _p(ma), _p(mb))
     return nm, ma[:len(ka)].copy(), mb[:len(kb)].copy()
+
+
+def search_by_sim3(k1, d1, b1, k2, d2, b2, q1, qd1, q2, qd2, th_dist=100):
+    """SearchBySim3 on per-slot query tables; returns (nfound, matches12)."""
+    f = lib().orbo_search_by_sim3
+    f.restype = I32
+    f.argtypes = [P, P, I32, P, P, I32] + [F32] * 8 + [P, P, P, P, I32, P]
+    k1 = np.ascontiguousarray(k1, KEYPOINT_DTYPE); k2 = np.ascontiguousarray(k2, KEYPOINT_DTYPE)
+    d1 = np.ascontiguousarray(d1, np.uint8); d2 = np.ascontiguousarray(d2, np.uint8)
+    q1 = np.ascontiguousarray(q1, PROJ_QUERY_DTYPE); q2 = np.ascontiguousarray(q2, PROJ_QUERY_DTYPE)
+    qd1 = np.ascontiguousarray(qd1, np.uint8); qd2 = np.ascontiguousarray(qd2, np.uint8)
+    m = np.full(max(len(k1), 1), -1, np.int32)
+    nf = f(_p(k1), _p(d1), len(k1), _p(k2), _p(d2), len(k2), *[float(x) for x in b1], *[float(x) for x in b2],
+           _p(q1), _p(qd1), _p(q2), _p(qd2), int(th_dist), _p(m))
+    return nf, m[:len(k1)].copy()

@@ -1182,3 +1182,35 @@ int orbo_search_by_bow(int variant, const orbo_keypoint *ka, const uint8_t *da, 
     }
     return nmatches;
 }
+
+// SearchBySim3 (ORBmatcher.cc:1104-1328): two independent best-only window
+// searches (INT_MAX start, octave in [pred-1, pred], TH_HIGH) and the
+// agreement check.  q1 / q2 carry one row per keyframe map-point slot.
+int orbo_search_by_sim3(const orbo_keypoint *k1, const uint8_t *dsc1, int n1, const orbo_keypoint *k2,
+                        const uint8_t *dsc2, int n2, float minx1, float maxx1, float miny1, float maxy1,
+                        float minx2, float maxx2, float miny2, float maxy2, const orbo_proj_query *q1,
+                        const uint8_t *qd1, const orbo_proj_query *q2, const uint8_t *qd2, int th_dist,
+                        int32_t *matches12) {
+    const FeatureGrid g1(k1, n1, minx1, maxx1, miny1, maxy1), g2(k2, n2, minx2, maxx2, miny2, maxy2);
+    auto search = [&](const FeatureGrid &g, const orbo_keypoint *k, const uint8_t *dsc, const orbo_proj_query &Q,
+                      const uint8_t *dq) {
+        if (!(Q.flags & 1)) return -1;
+        int bestDist = INT_MAX, bestIdx = -1;
+        for (int idx : g.area(k, Q.u, Q.v, Q.radius, -1, -1)) {
+            if (k[idx].octave < Q.min_level || k[idx].octave > Q.max_level) continue;
+            const int dist = hamming32(dq, dsc + 32 * (size_t)idx);
+            if (dist < bestDist) { bestDist = dist; bestIdx = idx; }
+        }
+        return bestDist <= th_dist ? bestIdx : -1;
+    };
+    std::vector<int> m1(n1, -1), m2(n2, -1);
+    for (int i1 = 0; i1 < n1; ++i1) m1[i1] = search(g2, k2, dsc2, q1[i1], qd1 + 32 * (size_t)i1);
+    for (int i2 = 0; i2 < n2; ++i2) m2[i2] = search(g1, k1, dsc1, q2[i2], qd2 + 32 * (size_t)i2);
+    int nFound = 0;
+    for (int i1 = 0; i1 < n1; ++i1) {
+        matches12[i1] = -1;
+        const int idx2 = m1[i1];
+        if (idx2 >= 0 && m2[idx2] == i1) { matches12[i1] = idx2; nFound++; }
+    }
+    return nFound;
+}

@@ -124,6 +124,16 @@ int   orbo_search_by_projection(int variant, const orbo_keypoint *keys, const ui
                                 int th_dist, float nnratio, int check_ori, int32_t *q_idx, int32_t *q_dist,
                                 int32_t *kp_final);
 
+/* SearchBySim3 (ORBmatcher.cc:1104-1328): q1 has one row per KF1 map-point
+ * slot (its projection into KF2), q2 one per KF2 slot (into KF1); the query's
+ * level window is [min_level, max_level] = [pred-1, pred].  matches12[n1] = the
+ * agreed KF2 index (-1 none).  Returns nFound. */
+int   orbo_search_by_sim3(const orbo_keypoint *k1, const uint8_t *dsc1, int n1, const orbo_keypoint *k2,
+                          const uint8_t *dsc2, int n2, float minx1, float maxx1, float miny1, float maxy1,
+                          float minx2, float maxx2, float miny2, float maxy2, const orbo_proj_query *q1,
+                          const uint8_t *qd1, const orbo_proj_query *q2, const uint8_t *qd2, int th_dist,
+                          int32_t *matches12);
+
 /* ---- BoW matchers (ORBmatcher.cc:160-289, 524-657, 659-825) ----
  * Side A = pKF / pKF1 (the outer loop), side B = F / pKF2.  Each side: keys,
  * descriptors, per-feature flags (bit0 usable: A of the SearchByBoW variants =

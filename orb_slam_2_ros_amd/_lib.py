@@ -94,6 +94,7 @@ _SIGNATURES = {
     "orbx_depth_download": (I32, [P, I32, P, P, I32, P, P]),
     "orbx_stereo_from_rgbd": (I32, [I32, P, P, I32, P, I32, I32, SZ, F32, P, P, P]),
     "orbx_search_by_projection": (I32, [I32, I32, P, P, P, I32, I32, F32, I32, P, P, P, P]),
+    "orbx_search_by_sim3": (I32, [I32, P, P, P, P, P, P, I32, P, P]),
     "orbx_search_by_bow": (I32, [I32, I32, P, P, F32, I32, P, I32, P, P, P]),
     "orbx_descriptor_distance": (I32, [P, P]),
     "orbx_search_for_initialization": (I32, [I32, P, P, I32, P, P, I32, I32, I32, P, P, I32, F32, I32, P]),

@@ -1235,6 +1235,31 @@ int orbx_search_by_bow(int device, int variant, const orbx_bow_side *A, const or
     return rc;
 }
 
+int orbx_search_by_sim3(int device, const orbx_match_frame *kf1, const orbx_match_frame *kf2,
+                        const orbx_proj_query *q1, const uint8_t *qdesc1, const orbx_proj_query *q2,
+                        const uint8_t *qdesc2, int th_dist, int32_t *matches12, int *nfound) {
+    if (!kf1 || !kf2 || !nfound || kf1->n < 0 || kf2->n < 0 || (kf1->n && !matches12)) return ORBX_EINVAL;
+    const int n1 = kf1->n, n2 = kf2->n;
+    std::vector<int32_t> m1(n1), d1(n1), m2(n2), d2(n2), f1(n1), f2(n2);
+    int nm = 0;
+    // pKF1's points into pKF2, then pKF2's into pKF1 (ORBmatcher.cc:1147-1219, 1222-1294)
+    int rc = orbx_search_by_projection(device, ORBX_PROJ_FUSE_SIM3, kf2, q1, qdesc1, n1, th_dist, 1.0f, 0,
+                                       m1.data(), d1.data(), f2.data(), &nm);
+    if (rc) return rc;
+    rc = orbx_search_by_projection(device, ORBX_PROJ_FUSE_SIM3, kf1, q2, qdesc2, n2, th_dist, 1.0f, 0, m2.data(),
+                                   d2.data(), f1.data(), &nm);
+    if (rc) return rc;
+    // agreement check (:1297-1315)
+    int found = 0;
+    for (int i1 = 0; i1 < n1; ++i1) {
+        const int idx2 = m1[i1];
+        matches12[i1] = -1;
+        if (idx2 >= 0 && idx2 < n2 && m2[idx2] == i1) { matches12[i1] = idx2; ++found; }
+    }
+    *nfound = found;
+    return ORBX_OK;
+}
+
 int orbx_debug_trig(int device, const float *angles, float *s, float *c, int n, const float *ys, const float *xs,
                     float *atan_deg, int m) {
     if (n < 0 || m < 0) return ORBX_EINVAL;

@@ -130,3 +130,27 @@ class ORBmatcher:
                                            ctypes.c_float(self.mfNNratio), int(self.mbCheckOrientation), ptr(t),
                                            int(nlevels), ptr(ma), ptr(mb), ctypes.byref(nm)), "SearchByBoW")
         return nm.value, ma[:na].copy(), mb[:nb].copy()
+
+    def search_by_sim3(self, kf1, kf2, q1, qdesc1, q2, qdesc2, th_dist=None):
+        """SearchBySim3 (ORBmatcher.cc:1104-1328) on per-slot query tables.
+        kf1 / kf2: dicts with keys, desc, bounds.  Returns (nfound, matches12)."""
+        th_dist = self.TH_HIGH if th_dist is None else th_dist
+        arrs = []
+
+        def frame(K):
+            k = np.ascontiguousarray(K["keys"], KEYPOINT_DTYPE)
+            d = np.ascontiguousarray(K["desc"], np.uint8).reshape(-1, 32)
+            arrs.extend([k, d])
+            return MatchFrame(ptr(k), ptr(d), None, None, None, len(k), 0, *[float(b) for b in K["bounds"]])
+        f1, f2 = frame(kf1), frame(kf2)
+        a1 = np.ascontiguousarray(q1, PROJ_QUERY_DTYPE); a2 = np.ascontiguousarray(q2, PROJ_QUERY_DTYPE)
+        b1 = np.ascontiguousarray(qdesc1, np.uint8).reshape(-1, 32)
+        b2 = np.ascontiguousarray(qdesc2, np.uint8).reshape(-1, 32)
+        if len(a1) != f1.n or len(a2) != f2.n:
+            raise ValueError("one query row per keyframe map-point slot")
+        m = np.full(max(f1.n, 1), -1, np.int32)
+        nf = ctypes.c_int(0)
+        check(self._lib.orbx_search_by_sim3(self.device, ctypes.byref(f1), ctypes.byref(f2), ptr(a1), ptr(b1),
+                                            ptr(a2), ptr(b2), int(th_dist), ptr(m), ctypes.byref(nf)),
+              "SearchBySim3")
+        return nf.value, m[:f1.n].copy()

@@ -87,3 +87,31 @@ VARIANT_ARGS = {
     "fuse": (50, 0.6, False, 3.0),         # LocalMapping::SearchInNeighbors: th 3, TH_LOW
     "fuse_sim3": (50, 0.8, False, 4.0),    # LoopClosing::SearchAndFuse: th 4, TH_LOW
 }
+
+
+def make_sim3_case(seed, n1=900, n2=850, w=640, h=480, th=7.5):
+    """Two keyframes that see overlapping points: slot i of KF1 projects near
+    its partner's keypoint in KF2 and vice versa (plus random slots)."""
+    rng = np.random.default_rng(seed)
+    sf, _ = scale_tables(1.2, 8)
+    c1 = make_case(seed, "sim3", n=n1, nq=n2, th=th)      # KF1's frame data, queries = KF2 slots -> KF1
+    c2 = make_case(seed + 1, "sim3", n=n2, nq=n1, th=th)  # KF2's frame data, queries = KF1 slots -> KF2
+    # tie the two tables: KF1 slot i's descriptor matches KF2 keypoint partner[i] and vice versa
+    partner = rng.permutation(n2)[:min(n1, n2)]
+    for i1, i2 in enumerate(partner[:n1]):
+        if rng.random() < 0.7:
+            c2["qdesc"][i1] = c2["desc"][i2]
+            c2["queries"]["u"][i1] = c2["keys"]["x"][i2] + np.float32(rng.normal(0, 1))
+            c2["queries"]["v"][i1] = c2["keys"]["y"][i2] + np.float32(rng.normal(0, 1))
+            lv = int(c2["keys"]["octave"][i2])
+            c2["queries"]["min_level"][i1], c2["queries"]["max_level"][i1] = lv - 1, lv
+            c2["queries"]["radius"][i1] = np.float32(th) * sf[lv]
+            c1["qdesc"][i2] = c1["desc"][i1]
+            c1["queries"]["u"][i2] = c1["keys"]["x"][i1] + np.float32(rng.normal(0, 1))
+            c1["queries"]["v"][i2] = c1["keys"]["y"][i1] + np.float32(rng.normal(0, 1))
+            lv1 = int(c1["keys"]["octave"][i1])
+            c1["queries"]["min_level"][i2], c1["queries"]["max_level"][i2] = lv1 - 1, lv1
+            c1["queries"]["radius"][i2] = np.float32(th) * sf[lv1]
+    kf1 = dict(keys=c1["keys"], desc=c1["desc"], bounds=c1["bounds"])
+    kf2 = dict(keys=c2["keys"], desc=c2["desc"], bounds=c2["bounds"])
+    return kf1, kf2, c2["queries"], c2["qdesc"], c1["queries"], c1["qdesc"]

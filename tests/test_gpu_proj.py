@@ -66,3 +66,14 @@ def test_projection_matchers_empty_and_edges(oracle_mod):
     q = c["queries"].copy()
     q["flags"] = 0                      # every point skipped by the caller's own tests
     assert _check(dict(c, queries=q), "localmap", oracle_mod) == 0
+
+
+@pytest.mark.parametrize("seed", [95, 96])
+def test_search_by_sim3_bit_exact(seed, oracle_mod):
+    from proj_cases import make_sim3_case
+    kf1, kf2, q1, qd1, q2, qd2 = make_sim3_case(seed)
+    nf, m = ORBmatcher(0.75, False).search_by_sim3(kf1, kf2, q1, qd1, q2, qd2)
+    onf, om = oracle_mod.search_by_sim3(kf1["keys"], kf1["desc"], kf1["bounds"], kf2["keys"], kf2["desc"],
+                                        kf2["bounds"], q1, qd1, q2, qd2, 100)
+    assert nf == onf and onf > 50
+    assert np.array_equal(m, om)

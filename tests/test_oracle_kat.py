@@ -266,3 +266,18 @@ def test_bow_matchers_vs_python(variant, seed, ori, oracle_mod):
     b = pyref.search_by_bow(variant, A, B, ratio, ori, tri)
     assert a[0] == b[0] and a[0] > 20
     assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
+
+
+def test_search_by_sim3_vs_python(oracle_mod):
+    from proj_cases import make_sim3_case
+    kf1, kf2, q1, qd1, q2, qd2 = make_sim3_case(97, n1=500, n2=480)
+    nf, m = oracle_mod.search_by_sim3(kf1["keys"], kf1["desc"], kf1["bounds"], kf2["keys"], kf2["desc"],
+                                      kf2["bounds"], q1, qd1, q2, qd2, 100)
+    # two best-only searches (INT_MAX start, TH_HIGH) + agreement, from the pure-Python restatement
+    _, m1, _, _ = pyref.search_by_projection("fuse_sim3", kf2["keys"], kf2["desc"], q1, qd1, kf2["bounds"],
+                                             th_dist=100)
+    _, m2, _, _ = pyref.search_by_projection("fuse_sim3", kf1["keys"], kf1["desc"], q2, qd2, kf1["bounds"],
+                                             th_dist=100)
+    want = np.array([i2 if i2 >= 0 and m2[i2] == i1 else -1 for i1, i2 in enumerate(m1)], np.int32)
+    assert nf == int((want >= 0).sum()) and nf > 30
+    assert np.array_equal(m, want)
