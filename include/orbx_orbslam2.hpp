@@ -138,8 +138,8 @@ protected:
     std::vector<float> mvScaleFactor, mvInvScaleFactor, mvLevelSigma2, mvInvLevelSigma2;
 };
 
-// Free-function forms of the two ORBmatcher members this tier accelerates; the
-// reference class keeps its other members (see INTEGRATION.md for the patch).
+// Free-function forms of the ORBmatcher members this tier accelerates; the
+// reference class keeps its signatures and forwards to these.
 struct OrbxMatcher {
     // ORBmatcher.cc:1649-1665
     static int DescriptorDistance(const cv::Mat &a, const cv::Mat &b) {
@@ -166,6 +166,65 @@ struct OrbxMatcher {
                                                           windowSize, nnratio, checkOri ? 1 : 0, &nm),
                            "SearchForInitialization");
         for (size_t i = 0; i < keys1.size(); ++i) vbPrevMatched[i] = cv::Point2f(prev[2 * i], prev[2 * i + 1]);
+        return nm;
+    }
+
+    // The searched frame / keyframe of a projection search: mvKeysUn,
+    // mDescriptors, mvuRight (may be empty), the current mvpMapPoints /
+    // vpMatched as per-keypoint flags (bit0 non-NULL, bit1 Observations() > 0),
+    // mvInvLevelSigma2 (Fuse) and the grid bounds mnMinX..mnMaxY.
+    struct ProjFrame {
+        const std::vector<cv::KeyPoint> *keys = nullptr;
+        const cv::Mat *desc = nullptr;
+        const std::vector<float> *uright = nullptr;
+        const std::vector<uint8_t> *mp_state = nullptr;
+        const std::vector<float> *inv_sigma2 = nullptr;
+        float min_x = 0, max_x = 0, min_y = 0, max_y = 0;
+    };
+
+    // SearchByProjection x4 / Fuse x2 (search part), ORBmatcher.cc:45-129,
+    // 291-404, 827-1102, 1330-1601: one query row per point in the reference's
+    // loop order (orbx_proj_query), descriptors as an nq x 32 Mat.  Returns the
+    // reference's count; q_idx / kp_final as in include/orbx.h.
+    static int SearchByProjectionTable(int variant, const ProjFrame &F, const std::vector<orbx_proj_query> &q,
+                                       const cv::Mat &qdesc, int th_dist, float nnratio, bool checkOri,
+                                       std::vector<int> &q_idx, std::vector<int> &q_dist,
+                                       std::vector<int> &kp_final) {
+        const std::vector<orbx_keypoint> k = orbx_detail::pack(*F.keys);
+        const cv::Mat d = F.desc->isContinuous() ? *F.desc : F.desc->clone();
+        const cv::Mat qd = qdesc.isContinuous() ? qdesc : qdesc.clone();
+        orbx_match_frame mf{};
+        mf.keys = k.data();
+        mf.desc = d.data;
+        mf.uright = F.uright && !F.uright->empty() ? F.uright->data() : nullptr;
+        mf.mp_state = F.mp_state && !F.mp_state->empty() ? F.mp_state->data() : nullptr;
+        mf.inv_sigma2 = F.inv_sigma2 ? F.inv_sigma2->data() : nullptr;
+        mf.n = (int)k.size();
+        mf.nlevels = F.inv_sigma2 ? (int)F.inv_sigma2->size() : 0;
+        mf.min_x = F.min_x; mf.max_x = F.max_x; mf.min_y = F.min_y; mf.max_y = F.max_y;
+        q_idx.assign(q.size(), -1);
+        q_dist.assign(q.size(), -1);
+        kp_final.assign(k.size(), -1);
+        int nm = 0;
+        orbx_detail::check(orbx_search_by_projection(orbx_detail::device_index(), variant, &mf, q.data(), qd.data,
+                                                     (int)q.size(), th_dist, nnratio, checkOri ? 1 : 0, q_idx.data(),
+                                                     q_dist.data(), kp_final.data(), &nm),
+                           "SearchByProjection");
+        return nm;
+    }
+
+    // SearchByBoW x2 / SearchForTriangulation (ORBmatcher.cc:160-289, 524-825)
+    // on two sides given as orbx_bow_side (FeatureVector as CSR).
+    static int SearchByBoWTable(int variant, const orbx_bow_side &A, const orbx_bow_side &B, float nnratio,
+                                bool checkOri, const std::vector<float> &tri, int nlevels,
+                                std::vector<int> &match_a, std::vector<int> &match_b) {
+        match_a.assign(A.n, -1);
+        match_b.assign(B.n, -1);
+        int nm = 0;
+        orbx_detail::check(orbx_search_by_bow(orbx_detail::device_index(), variant, &A, &B, nnratio, checkOri ? 1 : 0,
+                                              tri.empty() ? nullptr : tri.data(), nlevels, match_a.data(),
+                                              match_b.data(), &nm),
+                           "SearchByBoW");
         return nm;
     }
 };

@@ -9,6 +9,9 @@
 //        extracts both images with two extractors, runs
 //        OrbxFrame::ComputeStereoMatches and writes: nl, kps, desc, nr, kps,
 //        desc, nkept, mvuRight, mvDepth.
+//   adapter_test proj variant th ratio ori frame.bin queries.bin out.bin
+//        OrbxMatcher::SearchByProjectionTable on raw tables (see test): writes
+//        nmatches, q_idx, q_dist, kp_final.
 //   adapter_test rgbd W H img.raw depth.raw mbf out.bin
 //        extracts the image and runs OrbxFrame::ComputeStereoFromRGBD:
 //        n, kps, desc, mvuRight, mvDepth.
@@ -67,6 +70,47 @@ int main(int argc, char **argv) {
         out.write(reinterpret_cast<const char *>(&kept), 4);
         out.write(reinterpret_cast<const char *>(ur.data()), 4 * ur.size());
         out.write(reinterpret_cast<const char *>(dp.data()), 4 * dp.size());
+        return 0;
+    }
+    if (argc == 9 && std::string(argv[1]) == "proj") {
+        // frame.bin: n, min_x, max_x, min_y, max_y, n x 28 B keys, n x 32 B desc, n floats uright, n u8 state,
+        //            nlev, nlev floats inv_sigma2;  queries.bin: nq, nq x 36 B rows, nq x 32 B desc
+        std::ifstream ff(argv[6], std::ios::binary), fq(argv[7], std::ios::binary);
+        int n = 0, nq = 0, nlev = 0;
+        float b[4];
+        ff.read(reinterpret_cast<char *>(&n), 4);
+        ff.read(reinterpret_cast<char *>(b), 16);
+        std::vector<orbx_keypoint> kr(n);
+        ff.read(reinterpret_cast<char *>(kr.data()), 28 * (std::streamsize)n);
+        std::vector<cv::KeyPoint> keys;
+        for (const auto &k : kr)
+            keys.push_back(cv::KeyPoint(cv::Point2f(k.x, k.y), k.size, k.angle, k.response, k.octave, k.class_id));
+        cv::Mat desc(n, 32, CV_8U);
+        ff.read(reinterpret_cast<char *>(desc.data), 32 * (std::streamsize)n);
+        std::vector<float> ur(n);
+        ff.read(reinterpret_cast<char *>(ur.data()), 4 * (std::streamsize)n);
+        std::vector<uint8_t> st(n);
+        ff.read(reinterpret_cast<char *>(st.data()), n);
+        ff.read(reinterpret_cast<char *>(&nlev), 4);
+        std::vector<float> isg(nlev);
+        ff.read(reinterpret_cast<char *>(isg.data()), 4 * (std::streamsize)nlev);
+        fq.read(reinterpret_cast<char *>(&nq), 4);
+        std::vector<orbx_proj_query> q(nq);
+        fq.read(reinterpret_cast<char *>(q.data()), sizeof(orbx_proj_query) * (std::streamsize)nq);
+        cv::Mat qd(nq, 32, CV_8U);
+        fq.read(reinterpret_cast<char *>(qd.data), 32 * (std::streamsize)nq);
+        OrbxMatcher::ProjFrame F;
+        F.keys = &keys; F.desc = &desc; F.uright = &ur; F.mp_state = &st; F.inv_sigma2 = &isg;
+        F.min_x = b[0]; F.max_x = b[1]; F.min_y = b[2]; F.max_y = b[3];
+        std::vector<int> qi, qdist, kf;
+        const int nm = OrbxMatcher::SearchByProjectionTable(std::atoi(argv[2]), F, q, qd, std::atoi(argv[3]),
+                                                            (float)std::atof(argv[4]), std::atoi(argv[5]) != 0, qi,
+                                                            qdist, kf);
+        std::ofstream out(argv[8], std::ios::binary);
+        out.write(reinterpret_cast<const char *>(&nm), 4);
+        out.write(reinterpret_cast<const char *>(qi.data()), 4 * qi.size());
+        out.write(reinterpret_cast<const char *>(qdist.data()), 4 * qdist.size());
+        out.write(reinterpret_cast<const char *>(kf.data()), 4 * kf.size());
         return 0;
     }
     if (argc == 8 && std::string(argv[1]) == "rgbd") {

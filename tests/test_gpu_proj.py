@@ -77,3 +77,33 @@ def test_search_by_sim3_bit_exact(seed, oracle_mod):
                                         kf2["bounds"], q1, qd1, q2, qd2, 100)
     assert nf == onf and onf > 50
     assert np.array_equal(m, om)
+
+
+def test_cpp_adapter_projection_table(tmp_path, oracle_mod):
+    """OrbxMatcher::SearchByProjectionTable of the C++ drop-in header driven
+    through its cv-typed signature (local-map variant, stereo) vs the oracle."""
+    import subprocess
+    from cxx_build import build_adapter_test
+    from proj_cases import VARIANT_ARGS, make_case
+    c = make_case(98, "localmap", n=1200, nq=900, stereo=True, th=3.0)
+    th, ratio, ori, _ = VARIANT_ARGS["localmap"]
+    n, nq = len(c["keys"]), len(c["queries"])
+    with open(tmp_path / "f.bin", "wb") as f:
+        f.write(np.int32(n).tobytes()); f.write(np.array(c["bounds"], np.float32).tobytes())
+        f.write(c["keys"].tobytes()); f.write(c["desc"].tobytes()); f.write(c["uright"].astype(np.float32).tobytes())
+        f.write(c["mp_state"].tobytes()); f.write(np.int32(len(c["inv_sigma2"])).tobytes())
+        f.write(c["inv_sigma2"].tobytes())
+    with open(tmp_path / "q.bin", "wb") as f:
+        f.write(np.int32(nq).tobytes()); f.write(c["queries"].tobytes()); f.write(c["qdesc"].tobytes())
+    exe = build_adapter_test()
+    subprocess.run([str(exe), "proj", "0", str(th), repr(ratio), str(int(ori)), str(tmp_path / "f.bin"),
+                    str(tmp_path / "q.bin"), str(tmp_path / "o.bin")], check=True)
+    buf = (tmp_path / "o.bin").read_bytes()
+    nm = int(np.frombuffer(buf, np.int32, 1, 0)[0])
+    qi = np.frombuffer(buf, np.int32, nq, 4)
+    qd = np.frombuffer(buf, np.int32, nq, 4 + 4 * nq)
+    kf = np.frombuffer(buf, np.int32, n, 4 + 8 * nq)
+    o = oracle_mod.search_by_projection("localmap", c["keys"], c["desc"], c["queries"], c["qdesc"], c["bounds"],
+                                        c["uright"], c["mp_state"], c["inv_sigma2"], th, np.float32(ratio), ori)
+    assert nm == o[0] and nm > 0
+    assert np.array_equal(qi, o[1]) and np.array_equal(qd, o[2]) and np.array_equal(kf, o[3])
