@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -42,6 +43,63 @@ int popcount32(uint32_t v) {
     v = v - ((v >> 1) & 0x55555555u);
     v = (v & 0x33333333u) + ((v >> 2) & 0x33333333u);
     return (int)((((v + (v >> 4)) & 0xF0F0F0Fu) * 0x1010101u) >> 24);
+}
+
+// Workspace of the synchronous host entry points (the drop-in matchers and
+// depth calls): per device one grow-only device arena, one pinned staging
+// arena, a stream and a mutex -- the reference calls its matchers from the
+// Tracking, LocalMapping and LoopClosing threads concurrently.  A call packs
+// its inputs into the staging arena, moves them with one copy, runs, and
+// brings every output back with one copy.
+struct CallWs {
+    std::mutex mu;
+    hipStream_t st = nullptr;
+    uint8_t *dev = nullptr, *host = nullptr;
+    size_t cap = 0;
+};
+
+CallWs &call_ws(int device) {
+    static CallWs ws[64];
+    return ws[device & 63];
+}
+
+struct Layout {
+    size_t size = 0;
+    size_t add(size_t bytes) {
+        const size_t o = size;
+        size += (bytes + 255) & ~size_t(255);
+        return o;
+    }
+};
+
+// Ensures stream and capacity (caller holds ws.mu and has set the device).
+int ws_reserve(CallWs &ws, size_t bytes) {
+    if (!ws.st && hipStreamCreateWithFlags(&ws.st, hipStreamNonBlocking) != hipSuccess) return ORBX_EIO;
+    if (ws.cap >= bytes) return ORBX_OK;
+    (void)hipStreamSynchronize(ws.st);
+    if (ws.dev) (void)hipFree(ws.dev);
+    if (ws.host) (void)hipHostFree(ws.host);
+    ws.dev = ws.host = nullptr;
+    ws.cap = 0;
+    const size_t cap = std::max(bytes, size_t(1) << 20) * 3 / 2;
+    if (hipMalloc(reinterpret_cast<void **>(&ws.dev), cap) != hipSuccess) return ORBX_ENOMEM;
+    if (hipHostMalloc(reinterpret_cast<void **>(&ws.host), cap, hipHostMallocDefault) != hipSuccess) {
+        (void)hipFree(ws.dev);
+        ws.dev = nullptr;
+        return ORBX_ENOMEM;
+    }
+    ws.cap = cap;
+    return ORBX_OK;
+}
+
+template <typename T>
+T *at(uint8_t *base, size_t off) { return reinterpret_cast<T *>(base + off); }
+
+void put(CallWs &ws, size_t off, const void *src, size_t bytes) {
+    if (bytes && src) std::memcpy(ws.host + off, src, bytes);
+}
+void get(CallWs &ws, size_t off, void *dst, size_t bytes) {
+    if (bytes && dst) std::memcpy(dst, ws.host + off, bytes);
 }
 
 }  // namespace
@@ -1049,47 +1107,45 @@ int orbx_search_for_initialization(int device, const orbx_keypoint *k1, const ui
     c = std::max(c, 1);
     if (match_lds_bytes(std::max(n1, 1), std::max(n2, 1), q, c) > 160 * 1024) return ORBX_EINVAL;
     const int n1c = std::max(n1, 1), n2c = std::max(n2, 1);
-    orbx_keypoint *dk1 = nullptr, *dk2 = nullptr;
-    uint8_t *dd1 = nullptr, *dd2 = nullptr;
-    int32_t *dn = nullptr, *dm = nullptr, *dnm = nullptr;
-    float *dprev = nullptr;
-    uint32_t *dscr = nullptr;
-    int rc = ORBX_OK;
-    bool ok = dalloc(&dk1, n1c) == hipSuccess && dalloc(&dk2, n2c) == hipSuccess &&
-              dalloc(&dd1, 32 * (size_t)n1c) == hipSuccess && dalloc(&dd2, 32 * (size_t)n2c) == hipSuccess &&
-              dalloc(&dn, 2) == hipSuccess && dalloc(&dm, n1c) == hipSuccess && dalloc(&dnm, 1) == hipSuccess &&
-              dalloc(&dprev, 2 * (size_t)n1c) == hipSuccess && dalloc(&dscr, (size_t)q * c) == hipSuccess;
-    if (!ok) rc = ORBX_ENOMEM;
-    int32_t ns[2] = {n1, n2};
-    if (!rc && n1) ok = hipMemcpy(dk1, k1, sizeof(orbx_keypoint) * n1, hipMemcpyHostToDevice) == hipSuccess &&
-                        hipMemcpy(dd1, d1, 32 * (size_t)n1, hipMemcpyHostToDevice) == hipSuccess &&
-                        hipMemcpy(dprev, prev_xy, 8 * (size_t)n1, hipMemcpyHostToDevice) == hipSuccess;
-    if (!rc && n2) ok = ok && hipMemcpy(dk2, k2, sizeof(orbx_keypoint) * n2, hipMemcpyHostToDevice) == hipSuccess &&
-                        hipMemcpy(dd2, d2, 32 * (size_t)n2, hipMemcpyHostToDevice) == hipSuccess;
-    if (!rc) ok = ok && hipMemcpy(dn, ns, sizeof(ns), hipMemcpyHostToDevice) == hipSuccess;
-    if (!rc && !ok) rc = ORBX_EIO;
-    if (!rc) {
-        MatchBufs mb;
-        mb.k1 = dk1; mb.d1 = dd1; mb.n1 = dn; mb.k1_stride = n1c;
-        mb.k2 = dk2; mb.d2 = dd2; mb.n2 = dn + 1; mb.k2_stride = n2c;
-        mb.prev_xy = dprev; mb.matches12 = dm; mb.nmatches = dnm;
-        mb.scratch = dscr; mb.scratch_stride = (int64_t)q * c;
-        mb.img_w = img_w; mb.img_h = img_h; mb.window = window; mb.nnratio = nnratio;
-        mb.check_ori = check_ori; mb.reset_prev = 0; mb.clocks = nullptr;
-        if (launch_match(mb, 1, n1c, n2c, q, c, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
-            rc = ORBX_EIO;
-    }
+    Layout L;
+    const size_t o_k1 = L.add(sizeof(orbx_keypoint) * n1c), o_d1 = L.add(32 * (size_t)n1c),
+                 o_k2 = L.add(sizeof(orbx_keypoint) * n2c), o_d2 = L.add(32 * (size_t)n2c), o_ns = L.add(8);
+    const size_t o_prev = L.add(8 * (size_t)n1c);   // in / out
+    const size_t in_bytes = L.size;
+    const size_t o_m = L.add(4 * (size_t)n1c), o_nm = L.add(4);
+    const size_t out_end = L.size;
+    const size_t o_scr = L.add(4 * (size_t)q * c);
+    CallWs &ws = call_ws(device);
+    std::lock_guard<std::mutex> lock(ws.mu);
+    int rc = ws_reserve(ws, L.size);
+    if (rc) return rc;
+    const int32_t ns[2] = {n1, n2};
+    put(ws, o_k1, k1, sizeof(orbx_keypoint) * n1);
+    put(ws, o_d1, d1, 32 * (size_t)n1);
+    put(ws, o_k2, k2, sizeof(orbx_keypoint) * n2);
+    put(ws, o_d2, d2, 32 * (size_t)n2);
+    put(ws, o_ns, ns, sizeof(ns));
+    put(ws, o_prev, prev_xy, 8 * (size_t)n1);
+    uint8_t *D = ws.dev;
+    if (hipMemcpyAsync(D, ws.host, in_bytes, hipMemcpyHostToDevice, ws.st) != hipSuccess) return ORBX_EIO;
+    MatchBufs mb;
+    mb.k1 = at<orbx_keypoint>(D, o_k1); mb.d1 = D + o_d1; mb.n1 = at<int32_t>(D, o_ns); mb.k1_stride = n1c;
+    mb.k2 = at<orbx_keypoint>(D, o_k2); mb.d2 = D + o_d2; mb.n2 = at<int32_t>(D, o_ns) + 1; mb.k2_stride = n2c;
+    mb.prev_xy = at<float>(D, o_prev); mb.matches12 = at<int32_t>(D, o_m); mb.nmatches = at<int32_t>(D, o_nm);
+    mb.scratch = at<uint32_t>(D, o_scr); mb.scratch_stride = (int64_t)q * c;
+    mb.img_w = img_w; mb.img_h = img_h; mb.window = window; mb.nnratio = nnratio;
+    mb.check_ori = check_ori; mb.reset_prev = 0; mb.clocks = nullptr;
+    if (launch_match(mb, 1, n1c, n2c, q, c, ws.st) != hipSuccess ||
+        hipMemcpyAsync(ws.host + o_prev, D + o_prev, out_end - o_prev, hipMemcpyDeviceToHost, ws.st) != hipSuccess ||
+        hipStreamSynchronize(ws.st) != hipSuccess)
+        return ORBX_EIO;
     int32_t nm = 0;
-    if (!rc) {
-        ok = hipMemcpy(&nm, dnm, sizeof(int32_t), hipMemcpyDeviceToHost) == hipSuccess;
-        if (ok && n1) ok = hipMemcpy(matches12, dm, sizeof(int32_t) * n1, hipMemcpyDeviceToHost) == hipSuccess &&
-                           hipMemcpy(prev_xy, dprev, 8 * (size_t)n1, hipMemcpyDeviceToHost) == hipSuccess;
-        if (!ok) rc = ORBX_EIO;
-        else if (nm < 0) rc = ORBX_EIO;
-        else *nmatches = nm;
-    }
-    dfree(dk1); dfree(dk2); dfree(dd1); dfree(dd2); dfree(dn); dfree(dm); dfree(dnm); dfree(dprev); dfree(dscr);
-    return rc;
+    get(ws, o_nm, &nm, 4);
+    if (nm < 0) return ORBX_EIO;
+    get(ws, o_m, matches12, 4 * (size_t)n1);
+    get(ws, o_prev, prev_xy, 8 * (size_t)n1);
+    *nmatches = nm;
+    return ORBX_OK;
 }
 
 int orbx_search_by_projection(int device, int variant, const orbx_match_frame *F, const orbx_proj_query *queries,
@@ -1112,51 +1168,53 @@ int orbx_search_by_projection(int device, int variant, const orbx_match_frame *F
     if (pool_cap < 0) return ORBX_EINVAL;
     if (hipSetDevice(device) != hipSuccess) return ORBX_ENODEV;
     const bool spill = (int64_t)nq * n > pool_cap;
-    orbx_keypoint *dk = nullptr;
-    uint8_t *dd = nullptr, *dms = nullptr, *dqd = nullptr;
-    float *dur = nullptr, *disg = nullptr;
-    orbx_proj_query *dq = nullptr;
-    int32_t *dqi = nullptr, *dqdist = nullptr, *dkf = nullptr, *dnm = nullptr, *dqlen = nullptr, *dqbase = nullptr;
-    uint32_t *dqtop = nullptr, *dspill = nullptr;
-    int rc = ORBX_OK;
-    bool ok = dalloc(&dk, n) == hipSuccess && dalloc(&dd, 32 * (size_t)n) == hipSuccess &&
-              dalloc(&dq, nq) == hipSuccess && dalloc(&dqd, 32 * (size_t)nq) == hipSuccess &&
-              dalloc(&dqi, nq) == hipSuccess && dalloc(&dqdist, nq) == hipSuccess && dalloc(&dkf, n) == hipSuccess &&
-              dalloc(&dnm, 1) == hipSuccess && dalloc(&dqtop, 4 * (size_t)nq) == hipSuccess &&
-              dalloc(&dqlen, nq) == hipSuccess && dalloc(&dqbase, nq) == hipSuccess;
-    if (ok && F->uright) ok = dalloc(&dur, n) == hipSuccess;
-    if (ok && F->mp_state) ok = dalloc(&dms, n) == hipSuccess;
-    if (ok && F->inv_sigma2 && F->nlevels > 0) ok = dalloc(&disg, F->nlevels) == hipSuccess;
-    if (ok && spill) ok = dalloc(&dspill, (size_t)nq * n) == hipSuccess;
-    if (!ok) rc = ORBX_ENOMEM;
-    if (!rc && (hipMemcpy(dk, F->keys, sizeof(orbx_keypoint) * n, hipMemcpyHostToDevice) != hipSuccess ||
-                hipMemcpy(dd, F->desc, 32 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
-                hipMemcpy(dq, queries, sizeof(orbx_proj_query) * nq, hipMemcpyHostToDevice) != hipSuccess ||
-                hipMemcpy(dqd, qdesc, 32 * (size_t)nq, hipMemcpyHostToDevice) != hipSuccess ||
-                (dur && hipMemcpy(dur, F->uright, 4 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess) ||
-                (dms && hipMemcpy(dms, F->mp_state, (size_t)n, hipMemcpyHostToDevice) != hipSuccess) ||
-                (disg && hipMemcpy(disg, F->inv_sigma2, 4 * (size_t)F->nlevels, hipMemcpyHostToDevice) != hipSuccess)))
-        rc = ORBX_EIO;
-    if (!rc) {
-        ProjBufs a{};
-        a.keys = dk; a.desc = dd; a.uright = dur; a.mp_state = dms; a.inv_sigma2 = disg;
-        a.n = n; a.nlevels = F->nlevels;
-        a.min_x = F->min_x; a.max_x = F->max_x; a.min_y = F->min_y; a.max_y = F->max_y;
-        a.q = dq; a.qdesc = dqd; a.nq = nq;
-        a.variant = variant; a.th_dist = th_dist; a.nnratio = nnratio; a.check_ori = check_ori;
-        a.q_idx = dqi; a.q_dist = dqdist; a.kp_final = dkf; a.nmatches = dnm;
-        a.qtop = dqtop; a.qlen = dqlen; a.qbase = dqbase;
-        a.spill = dspill; a.spill_stride = n; a.pool_cap = pool_cap;
-        if (launch_proj(a, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = ORBX_EIO;
-    }
-    if (!rc && (hipMemcpy(q_idx, dqi, 4 * (size_t)nq, hipMemcpyDeviceToHost) != hipSuccess ||
-                hipMemcpy(q_dist, dqdist, 4 * (size_t)nq, hipMemcpyDeviceToHost) != hipSuccess ||
-                hipMemcpy(kp_final, dkf, 4 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess ||
-                hipMemcpy(nmatches, dnm, sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess))
-        rc = ORBX_EIO;
-    dfree(dk); dfree(dd); dfree(dms); dfree(dqd); dfree(dur); dfree(disg); dfree(dq); dfree(dqi); dfree(dqdist);
-    dfree(dkf); dfree(dnm); dfree(dqtop); dfree(dqlen); dfree(dqbase); dfree(dspill);
-    return rc;
+    const int nlev = F->inv_sigma2 ? std::max(F->nlevels, 0) : 0;
+    Layout L;   // inputs, then outputs, then device-only scratch
+    const size_t o_k = L.add(sizeof(orbx_keypoint) * n), o_d = L.add(32 * (size_t)n),
+                 o_ur = F->uright ? L.add(4 * (size_t)n) : 0, o_ms = F->mp_state ? L.add((size_t)n) : 0,
+                 o_isg = nlev ? L.add(4 * (size_t)nlev) : 0, o_q = L.add(sizeof(orbx_proj_query) * nq),
+                 o_qd = L.add(32 * (size_t)nq);
+    const size_t in_bytes = L.size;
+    const size_t o_qi = L.add(4 * (size_t)nq), o_qdist = L.add(4 * (size_t)nq), o_kf = L.add(4 * (size_t)n),
+                 o_nm = L.add(4);
+    const size_t out_end = L.size;
+    const size_t o_top = L.add(16 * (size_t)nq), o_len = L.add(4 * (size_t)nq), o_base = L.add(4 * (size_t)nq),
+                 o_sp = spill ? L.add(4 * (size_t)nq * n) : 0;
+    CallWs &ws = call_ws(device);
+    std::lock_guard<std::mutex> lock(ws.mu);
+    int rc = ws_reserve(ws, L.size);
+    if (rc) return rc;
+    put(ws, o_k, F->keys, sizeof(orbx_keypoint) * n);
+    put(ws, o_d, F->desc, 32 * (size_t)n);
+    if (F->uright) put(ws, o_ur, F->uright, 4 * (size_t)n);
+    if (F->mp_state) put(ws, o_ms, F->mp_state, (size_t)n);
+    if (nlev) put(ws, o_isg, F->inv_sigma2, 4 * (size_t)nlev);
+    put(ws, o_q, queries, sizeof(orbx_proj_query) * nq);
+    put(ws, o_qd, qdesc, 32 * (size_t)nq);
+    if (hipMemcpyAsync(ws.dev, ws.host, in_bytes, hipMemcpyHostToDevice, ws.st) != hipSuccess) return ORBX_EIO;
+    ProjBufs a{};
+    uint8_t *D = ws.dev;
+    a.keys = at<orbx_keypoint>(D, o_k); a.desc = D + o_d;
+    a.uright = F->uright ? at<float>(D, o_ur) : nullptr;
+    a.mp_state = F->mp_state ? D + o_ms : nullptr;
+    a.inv_sigma2 = nlev ? at<float>(D, o_isg) : nullptr;
+    a.n = n; a.nlevels = nlev;
+    a.min_x = F->min_x; a.max_x = F->max_x; a.min_y = F->min_y; a.max_y = F->max_y;
+    a.q = at<orbx_proj_query>(D, o_q); a.qdesc = D + o_qd; a.nq = nq;
+    a.variant = variant; a.th_dist = th_dist; a.nnratio = nnratio; a.check_ori = check_ori;
+    a.q_idx = at<int32_t>(D, o_qi); a.q_dist = at<int32_t>(D, o_qdist); a.kp_final = at<int32_t>(D, o_kf);
+    a.nmatches = at<int32_t>(D, o_nm);
+    a.qtop = at<uint32_t>(D, o_top); a.qlen = at<int32_t>(D, o_len); a.qbase = at<int32_t>(D, o_base);
+    a.spill = spill ? at<uint32_t>(D, o_sp) : nullptr; a.spill_stride = n; a.pool_cap = pool_cap;
+    if (launch_proj(a, ws.st) != hipSuccess ||
+        hipMemcpyAsync(ws.host + o_qi, D + o_qi, out_end - o_qi, hipMemcpyDeviceToHost, ws.st) != hipSuccess ||
+        hipStreamSynchronize(ws.st) != hipSuccess)
+        return ORBX_EIO;
+    get(ws, o_qi, q_idx, 4 * (size_t)nq);
+    get(ws, o_qdist, q_dist, 4 * (size_t)nq);
+    get(ws, o_kf, kp_final, 4 * (size_t)n);
+    get(ws, o_nm, nmatches, 4);
+    return ORBX_OK;
 }
 
 int orbx_search_by_bow(int device, int variant, const orbx_bow_side *A, const orbx_bow_side *B, float nnratio,
@@ -1186,53 +1244,69 @@ int orbx_search_by_bow(int device, int variant, const orbx_bow_side *A, const or
     if (A->n == 0 || B->n == 0 || A->nnodes == 0 || B->nnodes == 0) return ORBX_OK;
     if (hipSetDevice(device) != hipSuccess) return ORBX_ENODEV;
     const int nfa = A->node_offsets[A->nnodes], nfb = B->node_offsets[B->nnodes];
-    orbx_keypoint *dka = nullptr, *dkb = nullptr;
-    uint8_t *dda = nullptr, *ddb = nullptr, *dfa = nullptr, *dfb = nullptr;
-    uint32_t *dia = nullptr, *dib = nullptr;
-    int32_t *doa = nullptr, *dob = nullptr, *dea = nullptr, *deb = nullptr, *dma = nullptr, *dmb = nullptr;
-    int32_t *dhist = nullptr;
-    int8_t *dbin = nullptr;
-    float *dtri = nullptr;
     const int ntri = variant == ORBX_BOW_TRIANGULATION ? 11 + 2 * nlevels : 0;
-    int rc = ORBX_OK;
-    bool ok = dalloc(&dka, A->n) == hipSuccess && dalloc(&dkb, B->n) == hipSuccess &&
-              dalloc(&dda, 32 * (size_t)A->n) == hipSuccess && dalloc(&ddb, 32 * (size_t)B->n) == hipSuccess &&
-              dalloc(&dfa, A->n) == hipSuccess && dalloc(&dfb, B->n) == hipSuccess &&
-              dalloc(&dia, A->nnodes) == hipSuccess && dalloc(&dib, B->nnodes) == hipSuccess &&
-              dalloc(&doa, A->nnodes + 1) == hipSuccess && dalloc(&dob, B->nnodes + 1) == hipSuccess &&
-              dalloc(&dea, std::max(nfa, 1)) == hipSuccess && dalloc(&deb, std::max(nfb, 1)) == hipSuccess &&
-              dalloc(&dma, A->n) == hipSuccess && dalloc(&dmb, B->n) == hipSuccess &&
-              dalloc(&dhist, 32 + 2) == hipSuccess && dalloc(&dbin, A->n) == hipSuccess;
-    if (ok && ntri) ok = dalloc(&dtri, ntri) == hipSuccess;
-    if (!ok) rc = ORBX_ENOMEM;
-    auto up = [](void *d, const void *h, size_t b) { return b == 0 || hipMemcpy(d, h, b, hipMemcpyHostToDevice) == hipSuccess; };
-    if (!rc && !(up(dka, A->keys, sizeof(orbx_keypoint) * A->n) && up(dkb, B->keys, sizeof(orbx_keypoint) * B->n) &&
-                 up(dda, A->desc, 32 * (size_t)A->n) && up(ddb, B->desc, 32 * (size_t)B->n) &&
-                 up(dfa, A->flags, A->n) && up(dfb, B->flags, B->n) && up(dia, A->node_ids, 4 * (size_t)A->nnodes) &&
-                 up(dib, B->node_ids, 4 * (size_t)B->nnodes) && up(doa, A->node_offsets, 4 * (size_t)(A->nnodes + 1)) &&
-                 up(dob, B->node_offsets, 4 * (size_t)(B->nnodes + 1)) && up(dea, A->node_features, 4 * (size_t)nfa) &&
-                 up(deb, B->node_features, 4 * (size_t)nfb) && up(dma, match_a, 4 * (size_t)A->n) &&
-                 up(dmb, match_b, 4 * (size_t)B->n) && up(dtri, tri, 4 * (size_t)ntri) &&
-                 hipMemset(dhist, 0, 4 * (32 + 2)) == hipSuccess))
-        rc = ORBX_EIO;
-    if (!rc) {
-        BowBufs a{};
-        a.A = BowSideDev{dka, dda, dfa, A->n, dia, doa, dea, A->nnodes};
-        a.B = BowSideDev{dkb, ddb, dfb, B->n, dib, dob, deb, B->nnodes};
-        a.variant = variant; a.nnratio = nnratio; a.check_ori = check_ori;
-        a.tri = dtri; a.ex = ntri ? tri[9] : 0.f; a.ey = ntri ? tri[10] : 0.f; a.nlevels = nlevels;
-        a.match_a = dma; a.match_b = dmb; a.bin_a = dbin; a.hist = dhist; a.counts = dhist + 32;
-        if (launch_bow(a, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = ORBX_EIO;
+    Layout L;
+    size_t o_side[2][6];
+    for (int k = 0; k < 2; ++k) {
+        const orbx_bow_side *S = k ? B : A;
+        const int nf = k ? nfb : nfa;
+        o_side[k][0] = L.add(sizeof(orbx_keypoint) * S->n);
+        o_side[k][1] = L.add(32 * (size_t)S->n);
+        o_side[k][2] = L.add((size_t)S->n);
+        o_side[k][3] = L.add(4 * (size_t)S->nnodes);
+        o_side[k][4] = L.add(4 * (size_t)(S->nnodes + 1));
+        o_side[k][5] = L.add(4 * (size_t)std::max(nf, 1));
     }
-    int32_t counts[2] = {0, 0};
-    if (!rc && (hipMemcpy(match_a, dma, 4 * (size_t)A->n, hipMemcpyDeviceToHost) != hipSuccess ||
-                hipMemcpy(match_b, dmb, 4 * (size_t)B->n, hipMemcpyDeviceToHost) != hipSuccess ||
-                hipMemcpy(counts, dhist + 32, sizeof(counts), hipMemcpyDeviceToHost) != hipSuccess))
-        rc = ORBX_EIO;
-    if (!rc) *nmatches = counts[1];
-    dfree(dka); dfree(dkb); dfree(dda); dfree(ddb); dfree(dfa); dfree(dfb); dfree(dia); dfree(dib); dfree(doa);
-    dfree(dob); dfree(dea); dfree(deb); dfree(dma); dfree(dmb); dfree(dhist); dfree(dbin); dfree(dtri);
-    return rc;
+    const size_t o_tri = ntri ? L.add(4 * (size_t)ntri) : 0;
+    const size_t o_ma = L.add(4 * (size_t)A->n), o_mb = L.add(4 * (size_t)B->n);
+    const size_t in_bytes = L.size;   // match arrays start as -1 (host copies)
+    const size_t o_cnt = L.add(4 * 34);   // hist[32] + counts[2]
+    const size_t out_end = L.size;
+    const size_t o_bin = L.add((size_t)A->n);
+    CallWs &ws = call_ws(device);
+    std::lock_guard<std::mutex> lock(ws.mu);
+    int rc = ws_reserve(ws, L.size);
+    if (rc) return rc;
+    for (int k = 0; k < 2; ++k) {
+        const orbx_bow_side *S = k ? B : A;
+        const int nf = k ? nfb : nfa;
+        put(ws, o_side[k][0], S->keys, sizeof(orbx_keypoint) * S->n);
+        put(ws, o_side[k][1], S->desc, 32 * (size_t)S->n);
+        put(ws, o_side[k][2], S->flags, (size_t)S->n);
+        put(ws, o_side[k][3], S->node_ids, 4 * (size_t)S->nnodes);
+        put(ws, o_side[k][4], S->node_offsets, 4 * (size_t)(S->nnodes + 1));
+        put(ws, o_side[k][5], S->node_features, 4 * (size_t)nf);
+    }
+    if (ntri) put(ws, o_tri, tri, 4 * (size_t)ntri);
+    put(ws, o_ma, match_a, 4 * (size_t)A->n);
+    put(ws, o_mb, match_b, 4 * (size_t)B->n);
+    uint8_t *D = ws.dev;
+    if (hipMemcpyAsync(D, ws.host, in_bytes, hipMemcpyHostToDevice, ws.st) != hipSuccess ||
+        hipMemsetAsync(D + o_cnt, 0, 4 * 34, ws.st) != hipSuccess)
+        return ORBX_EIO;
+    BowBufs a{};
+    for (int k = 0; k < 2; ++k) {
+        const orbx_bow_side *S = k ? B : A;
+        BowSideDev &d = k ? a.B : a.A;
+        d = BowSideDev{at<orbx_keypoint>(D, o_side[k][0]), D + o_side[k][1], D + o_side[k][2], S->n,
+                       at<uint32_t>(D, o_side[k][3]), at<int32_t>(D, o_side[k][4]), at<int32_t>(D, o_side[k][5]),
+                       S->nnodes};
+    }
+    a.variant = variant; a.nnratio = nnratio; a.check_ori = check_ori;
+    a.tri = ntri ? at<float>(D, o_tri) : nullptr; a.ex = ntri ? tri[9] : 0.f; a.ey = ntri ? tri[10] : 0.f;
+    a.nlevels = nlevels;
+    a.match_a = at<int32_t>(D, o_ma); a.match_b = at<int32_t>(D, o_mb); a.bin_a = at<int8_t>(D, o_bin);
+    a.hist = at<int32_t>(D, o_cnt); a.counts = at<int32_t>(D, o_cnt) + 32;
+    if (launch_bow(a, ws.st) != hipSuccess ||
+        hipMemcpyAsync(ws.host + o_ma, D + o_ma, out_end - o_ma, hipMemcpyDeviceToHost, ws.st) != hipSuccess ||
+        hipStreamSynchronize(ws.st) != hipSuccess)
+        return ORBX_EIO;
+    get(ws, o_ma, match_a, 4 * (size_t)A->n);
+    get(ws, o_mb, match_b, 4 * (size_t)B->n);
+    int32_t counts[2];
+    get(ws, o_cnt + 4 * 32, counts, sizeof(counts));
+    *nmatches = counts[1];
+    return ORBX_OK;
 }
 
 int orbx_search_by_sim3(int device, const orbx_match_frame *kf1, const orbx_match_frame *kf2,
