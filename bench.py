@@ -143,6 +143,48 @@ def max_over_ranks(torch, dist, world, el, device):
     return float(t.item())
 
 
+def matcher_latencies(reps: int = 20):
+    """Per-call latency of the drop-in ORBmatcher searches (host arrays in and
+    out, as Tracking / LocalMapping / LoopClosing call them) next to the
+    oracle's single-thread time on the same inputs."""
+    from oracle import oracle
+    from orb_slam_2_ros_amd import ORBmatcher
+    from orb_slam_2_ros_amd.synth_match import (BOW_VARIANT_ARGS, PROJ_VARIANT_ARGS, make_bow_case,
+                                                make_proj_case)
+
+    def timed(fn, k):
+        ts = []
+        for _ in range(k):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return 1e3 * float(np.median(ts))
+
+    out = {}
+    for variant, n, nq in [("localmap", 2000, 2500), ("lastframe", 2000, 1500), ("keyframe", 2000, 1000),
+                           ("fuse", 2000, 2000)]:
+        th, ratio, ori, wth = PROJ_VARIANT_ARGS[variant]
+        c = make_proj_case(1234, variant, n=n, nq=nq, stereo=variant != "keyframe", th=wth)
+        m = ORBmatcher(ratio, ori)
+        args = (variant, c["keys"], c["desc"], c["queries"], c["qdesc"], c["bounds"], c["uright"], c["mp_state"],
+                c["inv_sigma2"])
+        m.search_by_projection(*args, th)
+        out[f"SearchByProjection_{variant}" if "fuse" not in variant else "Fuse"] = {
+            "keypoints": n, "points": nq,
+            "gpu_ms": round(timed(lambda: m.search_by_projection(*args, th), reps), 4),
+            "cpu_ms": round(timed(lambda: oracle.search_by_projection(*args, th, ratio, ori), 5), 4)}
+    for variant, na in [("kf_frame", 2000), ("triangulation", 2000)]:
+        ratio, ori = BOW_VARIANT_ARGS[variant]
+        A, B, tri = make_bow_case(4321, variant, na=na, nb=na, nodes=200)
+        m = ORBmatcher(ratio, ori)
+        m.search_by_bow(variant, A, B, tri)
+        name = "SearchByBoW_kf_frame" if variant == "kf_frame" else "SearchForTriangulation"
+        out[name] = {"features": na,
+                     "gpu_ms": round(timed(lambda: m.search_by_bow(variant, A, B, tri), reps), 4),
+                     "cpu_ms": round(timed(lambda: oracle.search_by_bow(variant, A, B, ratio, ori, tri), 5), 4)}
+    return out
+
+
 def _resident_frames(mode, w, h, batch, rank):
     """Host array [FRAMES_PER_STREAM, frames_per_step, h, w] (+ depth maps for RGB-D)."""
     from orb_slam_2_ros_amd import synth
@@ -287,6 +329,7 @@ def main() -> int:
             roof["pipeline_GBs"] = round(frame_bytes * value / world / 1e9, 2)
             roof["pipeline_frac"] = round(frame_bytes * value / world / 1e9 / HBM_PEAK_GBS, 5)
         cpu = cpu_baseline(w, h, nf, args.cpu_seconds) if (world == 1 and args.cpu_seconds > 0) else None
+        matchers = matcher_latencies() if (world == 1 and not args.no_extras) else None
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -308,6 +351,7 @@ def main() -> int:
             "stage_ms_per_step": stage_ms,
             "cpu_baseline": cpu,
             "extras": extras,
+            "matchers_per_call": matchers,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -107,3 +107,14 @@ def depth_map(width: int, height: int, seed: int, z: float = 1.5) -> np.ndarray:
     d[holes] = 0.0
     d[rng.random((height, width)) < 0.005] = np.nan
     return d
+
+
+def scale_tables(scale=1.2, nlevels=8):
+    """mvScaleFactor / mvInvScaleFactor (ORBextractor.cc:424-438): float
+    products computed in double (the member scaleFactor is a double)."""
+    sf = np.zeros(nlevels, np.float32)
+    sf[0] = 1.0
+    for i in range(1, nlevels):
+        sf[i] = np.float32(float(sf[i - 1]) * float(np.float32(scale)))
+    inv = (np.float32(1.0) / sf).astype(np.float32)
+    return sf, inv
