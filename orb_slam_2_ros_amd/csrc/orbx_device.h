@@ -108,8 +108,13 @@ struct ProjBufs {
     int variant, th_dist; float nnratio; int check_ori;
     int32_t *q_idx, *q_dist, *kp_final, *nmatches;
     uint32_t *qtop; int32_t *qlen, *qbase;   // per query: 4 kept entries (16-B aligned), list length, pool base
-    uint32_t *spill; int64_t spill_stride;   // lists that do not fit the LDS pool: nq x spill_stride
-    int pool_cap;
+    uint32_t *pool; int64_t pool_cap;        // candidate lists of all queries (global)
+    // zeroed by the caller before a launch: list-pool counter (> pool_cap:
+    // rerun with more) and count of `hard` claims
+    unsigned long long *pool_top; uint32_t *hard_cnt;
+    uint2 *hard; int hard_cap;               // (keypoint, query) claims past a query's 4 kept entries
+    uint8_t *und;                            // nq: 0 decided, 1 open, 2 left to the in-order replay
+    int32_t *stats;                          // optional: rounds, queries replayed in order
 };
 
 // Vocabulary-node matchers (SearchByBoW x2, SearchForTriangulation).
@@ -147,7 +152,7 @@ hipError_t launch_rgbd(const orbx_keypoint *kps, const orbx_keypoint *kun, const
                        int kcap, const float *dmap, int64_t dstride, int dpitch, int w, int h, float mbf, float *ur,
                        float *depth, int64_t ostride, int32_t *nkept, int B, hipStream_t s);
 hipError_t launch_proj(const ProjBufs &a, hipStream_t s);
-int proj_pool_cap(int n, int nq);   // -1: the frame does not fit the kernel's LDS
+bool proj_fits(int n);   // the frame's grid fits the search kernel's LDS
 hipError_t launch_bow(const BowBufs &a, hipStream_t s);
 int match_lds_bytes(int n1cap, int n2cap, int maxq, int maxc);
 int quadtree_lds_bytes(int node_cap);

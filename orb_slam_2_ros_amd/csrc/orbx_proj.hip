@@ -3,19 +3,24 @@
 // (ORBmatcher.cc:45-129, 291-404, 827-1102, 1330-1601; GetFeaturesInArea
 // Frame.cc:354-412 / KeyFrame.cc:700-739; ComputeThreeMaxima :1603-1644).
 //
-// One 1024-thread workgroup per call.  The frame's 64x48 grid (positions,
-// octaves, mvuRight, map-point state) is built in LDS.  Every wave then takes
-// queries in turn and expands the query's window into candidate entries, one
-// lane per entry.  The static filters (level range, window, stereo gate, Fuse's
+// k_proj_search: many 1024-thread workgroups; each builds the frame's 64x48
+// grid (positions, octaves, mvuRight) in its LDS and takes a slice of the
+// queries, one wave per query, expanding the query's window into candidate
+// entries, one lane per entry.  The static filters (level range, window, stereo gate, Fuse's
 // reprojection test) and the Hamming distances are evaluated here, and the
-// query's 4 smallest (distance, candidate position) entries are kept.
+// query's 4 smallest (distance, candidate position) entries are kept; the full
+// list goes to a global pool.
 //
 // The reference assigns keypoints greedily in query order: a keypoint taken by
-// an earlier point is skipped by later ones.  That dependency is replayed by
-// wave 0 in query order; each query needs only its first one (best-only
-// variants) or two (SearchByProjection(Frame&, vector<MapPoint*>&)) still-free
-// entries in (distance, position) order.  Those come from the 4 kept entries,
-// or from a 64-wide scan of the query's full list when too few are free.
+// an earlier point is skipped by later ones.  Each query needs only its first
+// one (best-only variants) or two (SearchByProjection(Frame&,
+// vector<MapPoint*>&)) still-free entries in (distance, position) order.
+// k_proj_replay (one workgroup) decides the queries in rounds: an open query
+// none of whose examined entries can still be taken by an earlier open query
+// sees what the in-order loop would see, and is decided in parallel.  What the
+// rounds leave (chains of contention, or more than the 4 kept entries needed)
+// is replayed by wave 0 in query order, from the 4 kept entries or a 64-wide
+// scan of the full list.
 // Fuse has no such dependency (its map edits stay with the caller), so its
 // queries finish in the parallel phase.
 #include <hip/hip_runtime.h>
@@ -32,9 +37,11 @@ namespace {
 constexpr int kPT = 1024, kPW = kPT / 64;
 constexpr int kGC = 64, kGR = 48, kCells = kGC * kGR;
 constexpr int kHist = 30;
+constexpr int kKPer = 8;                  // keypoints per thread in the grid build (n <= 8192)
 constexpr int kEnt = 512;                 // per-wave entry map (candidate -> grid column)
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr int kBadDist = 0x1FF;           // entry failed a static filter
+constexpr int kProjLdsMax = 160 * 1024 - 1024;   // dynamic LDS; the static part needs < 1 KiB
 
 // list entry: keypoint index | octave << 16 | distance << 20
 __device__ inline uint32_t entry(int idx, int oct, int dist) {
@@ -50,14 +57,12 @@ struct PLds {
     float2 *gxy;      // n, by grid position
     float *gur;       // n, mvuRight by grid position
     int16_t *glist;   // n, keypoint index by grid position
-    int16_t *kcell;   // n
+    int16_t *gtmp;    // n, keypoint index by grid position, unordered inside a cell
     int8_t *goct;     // n, octave by grid position
-    uint8_t *state;   // n, by keypoint index: bit0 has a point, bit1 it blocks
     uint8_t *entmap;  // kPW x kEnt
-    uint32_t *pool;   // pool_cap list entries
 };
 
-__device__ inline PLds carve(uint8_t *p, int n, int pool_cap) {
+__device__ inline PLds carve(uint8_t *p, int n) {
     PLds s;
     auto take = [&](size_t bytes) { uint8_t *r = p; p += (bytes + 15) & ~size_t(15); return r; };
     s.gstart = reinterpret_cast<int *>(take(4 * (kCells + 1)));
@@ -65,11 +70,9 @@ __device__ inline PLds carve(uint8_t *p, int n, int pool_cap) {
     s.gxy = reinterpret_cast<float2 *>(take(8 * (size_t)n));
     s.gur = reinterpret_cast<float *>(take(4 * (size_t)n));
     s.glist = reinterpret_cast<int16_t *>(take(2 * (size_t)n));
-    s.kcell = reinterpret_cast<int16_t *>(take(2 * (size_t)n));
+    s.gtmp = reinterpret_cast<int16_t *>(take(2 * (size_t)n));
     s.goct = reinterpret_cast<int8_t *>(take((size_t)n));
-    s.state = reinterpret_cast<uint8_t *>(take((size_t)n));
     s.entmap = take((size_t)kPW * kEnt);
-    s.pool = reinterpret_cast<uint32_t *>(take(4 * (size_t)pool_cap));
     return s;
 }
 
@@ -95,51 +98,41 @@ __device__ inline int block_scan(int v, int *total, int *ws) {
     return base + incl - v;
 }
 
-__global__ __launch_bounds__(kPT) void k_proj_match(ProjBufs a) {
+__global__ __launch_bounds__(kPT) void k_proj_search(ProjBufs a) {
     extern __shared__ __align__(16) uint8_t lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int n = a.n, nq = a.nq;
-    const PLds s = carve(lds, n, a.pool_cap);
+    const PLds s = carve(lds, n);
     __shared__ int ws[kPW];
-    __shared__ int hist[kHist];
-    __shared__ int sh_pool, sh_acc, sh_removed, sh_top[3];
     const int V = a.variant;
     const bool fuse = V == ORBX_PROJ_FUSE || V == ORBX_PROJ_FUSE_SIM3;
-    const bool occ_obs = V == ORBX_PROJ_LOCALMAP || V == ORBX_PROJ_LASTFRAME;   // skip: has && Observations() > 0
-    const bool ratio = V == ORBX_PROJ_LOCALMAP;
-    const bool use_ori = a.check_ori && (V == ORBX_PROJ_LASTFRAME || V == ORBX_PROJ_KEYFRAME);
     const float invW = __fdiv_rn((float)kGC, __fsub_rn(a.max_x, a.min_x));
     const float invH = __fdiv_rn((float)kGR, __fsub_rn(a.max_y, a.min_y));
 
     // ---- 0. init
     for (int i = tid; i <= kCells; i += kPT) s.gstart[i] = 0;
     for (int i = tid; i < kCells; i += kPT) s.gfill[i] = 0;
-    for (int i = tid; i < n; i += kPT) {
-        s.state[i] = a.mp_state ? (a.mp_state[i] & 3) : 0;
-        a.kp_final[i] = -1;
-    }
-    for (int i = tid; i < nq; i += kPT) {
-        a.q_idx[i] = -1;
-        a.q_dist[i] = -1;
-        a.qlen[i] = 0;   // queries with an empty window never reach phase 2's stores
-        a.qbase[i] = -1;
-        reinterpret_cast<uint4 *>(a.qtop)[i] = make_uint4(kNone, kNone, kNone, kNone);
-    }
-    if (tid < kHist) hist[tid] = 0;
-    if (tid == 0) { sh_pool = 0; sh_acc = 0; sh_removed = 0; }
     __syncthreads();
 
-    // ---- 1. grid: counting sort by cell, then index order inside each cell
-    for (int i = tid; i < n; i += kPT) {
-        const orbx_keypoint k = a.keys[i];
-        const int px = (int)roundf(__fmul_rn(__fsub_rn(k.x, a.min_x), invW));
-        const int py = (int)roundf(__fmul_rn(__fsub_rn(k.y, a.min_y), invH));
-        int cell = -1;
-        if (px >= 0 && px < kGC && py >= 0 && py < kGR) {
-            cell = px * kGR + py;
-            atomicAdd(&s.gstart[cell], 1);
+    // ---- 1. grid: counting sort by cell, index order inside each cell.  Each
+    // thread keeps its keypoints in registers and places them by rank.
+    float kx[kKPer], ky[kKPer], kur[kKPer];
+    int koc[kKPer], kc[kKPer];
+#pragma unroll
+    for (int r = 0; r < kKPer; ++r) {
+        const int i = tid + r * kPT;
+        kc[r] = -1;
+        if (i < n) {
+            const orbx_keypoint k = a.keys[i];
+            kx[r] = k.x; ky[r] = k.y; koc[r] = k.octave;
+            kur[r] = a.uright ? a.uright[i] : -1.0f;
+            const int px = (int)roundf(__fmul_rn(__fsub_rn(k.x, a.min_x), invW));
+            const int py = (int)roundf(__fmul_rn(__fsub_rn(k.y, a.min_y), invH));
+            if (px >= 0 && px < kGC && py >= 0 && py < kGR) {
+                kc[r] = px * kGR + py;
+                atomicAdd(&s.gstart[kc[r]], 1);
+            }
         }
-        s.kcell[i] = (int16_t)cell;
     }
     __syncthreads();
     {
@@ -156,64 +149,87 @@ __global__ __launch_bounds__(kPT) void k_proj_match(ProjBufs a) {
         if (tid == kPT - 1) s.gstart[kCells] = run;
         __syncthreads();
     }
-    for (int i = tid; i < n; i += kPT) {
-        const int cell = s.kcell[i];
-        if (cell >= 0) s.glist[s.gstart[cell] + atomicAdd(&s.gfill[cell], 1)] = (int16_t)i;
-    }
+#pragma unroll
+    for (int r = 0; r < kKPer; ++r)
+        if (kc[r] >= 0) s.gtmp[s.gstart[kc[r]] + atomicAdd(&s.gfill[kc[r]], 1)] = (int16_t)(tid + r * kPT);
     __syncthreads();
-    for (int c = tid; c < kCells; c += kPT) {
-        const int st = s.gstart[c], en = s.gstart[c + 1];
-        for (int x = st + 1; x < en; ++x) {
-            const int16_t v = s.glist[x];
-            int j = x - 1;
-            while (j >= st && s.glist[j] > v) { s.glist[j + 1] = s.glist[j]; --j; }
-            s.glist[j + 1] = v;
-        }
-    }
-    __syncthreads();
-    const int ngrid = s.gstart[kCells];
-    for (int g = tid; g < ngrid; g += kPT) {
-        const int i = s.glist[g];
-        const orbx_keypoint k = a.keys[i];
-        s.gxy[g] = make_float2(k.x, k.y);
-        s.goct[g] = (int8_t)k.octave;
-        s.gur[g] = a.uright ? a.uright[i] : -1.0f;
+#pragma unroll
+    for (int r = 0; r < kKPer; ++r) {
+        if (kc[r] < 0) continue;
+        const int i = tid + r * kPT;
+        const int st = s.gstart[kc[r]], en = s.gstart[kc[r] + 1];
+        int pos = st;
+        for (int x = st; x < en; ++x) pos += s.gtmp[x] < i;
+        s.glist[pos] = (int16_t)i;
+        s.gxy[pos] = make_float2(kx[r], ky[r]);
+        s.goct[pos] = (int8_t)koc[r];
+        s.gur[pos] = kur[r];
     }
     __syncthreads();
 
+    for (int i = blockIdx.x * kPT + tid; i < n; i += gridDim.x * kPT) a.kp_final[i] = -1;
+
     // ---- 2. window expansion, static filters, distances, 4 smallest per query
     uint8_t *emap = s.entmap + wave * kEnt;
-    for (int q = wave; q < nq; q += kPW) {
-        const orbx_proj_query Q = a.q[q];
-        if (!(Q.flags & ORBX_QUERY_ACTIVE)) continue;
-        const float x = Q.u, y = Q.v, r = Q.radius;
-        // Frame::GetFeaturesInArea cell range (float, as the reference)
-        const int cx0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(x, a.min_x), r), invW)));
-        const int cx1 = min(kGC - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(x, a.min_x), r), invW)));
-        const int cy0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(y, a.min_y), r), invH)));
-        const int cy1 = min(kGR - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(y, a.min_y), r), invH)));
-        if (cx0 >= kGC || cx1 < 0 || cy0 >= kGR || cy1 < 0 || cx1 < cx0 || cy1 < cy0) continue;
-        const int ncx = cx1 - cx0 + 1;   // <= 64
-        int st = 0, cnt = 0;
-        if (lane < ncx) {
-            const int col = (cx0 + lane) * kGR;
-            st = s.gstart[col + cy0];
-            cnt = s.gstart[col + cy1 + 1] - st;
+    const bool occ_obs = V == ORBX_PROJ_LOCALMAP || V == ORBX_PROJ_LASTFRAME;
+    __shared__ int sh_T[kPW], sh_base;
+    // uniform trip count: the waves of a block allocate their lists together
+    for (int q0 = blockIdx.x * kPW; q0 < nq; q0 += gridDim.x * kPW) {
+        const int q = q0 + wave;
+        orbx_proj_query Q{};
+        int T = 0, st = 0, cnt = 0, pos0 = 0;
+        float x = 0.f, y = 0.f, r = 0.f;
+        if (q < nq) {
+            if (lane == 0) {   // this wave owns query q: default results
+                a.qlen[q] = 0;
+                a.qbase[q] = -1;
+                reinterpret_cast<uint4 *>(a.qtop)[q] = make_uint4(kNone, kNone, kNone, kNone);
+                a.q_idx[q] = -1;
+                a.q_dist[q] = -1;
+            }
+            Q = a.q[q];
+            x = Q.u; y = Q.v; r = Q.radius;
+            // Frame::GetFeaturesInArea cell range (float, as the reference)
+            const int cx0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(x, a.min_x), r), invW)));
+            const int cx1 = min(kGC - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(x, a.min_x), r), invW)));
+            const int cy0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(y, a.min_y), r), invH)));
+            const int cy1 = min(kGR - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(y, a.min_y), r), invH)));
+            const bool win = (Q.flags & ORBX_QUERY_ACTIVE) && !(cx0 >= kGC || cx1 < 0 || cy0 >= kGR || cy1 < 0 ||
+                                                                 cx1 < cx0 || cy1 < cy0);
+            const int ncx = cx1 - cx0 + 1;   // <= 64
+            if (win && lane < ncx) {
+                const int col = (cx0 + lane) * kGR;
+                st = s.gstart[col + cy0];
+                cnt = s.gstart[col + cy1 + 1] - st;
+            }
+            const int incl = wave_incl_scan_i32(cnt);
+            pos0 = incl - cnt;
+            T = __builtin_amdgcn_readlane(incl, 63);
         }
-        const int incl = wave_incl_scan_i32(cnt);
-        const int pos0 = incl - cnt;
-        const int T = __builtin_amdgcn_readlane(incl, 63);
+        // the replay kernel needs the whole lists: one slice of the global
+        // pool per block and pass (Fuse decides from the 4 smallest alone)
+        if (lane == 0) sh_T[wave] = fuse ? 0 : T;
+        __syncthreads();
+        if (tid == 0) {
+            int tot = 0;
+            for (int w = 0; w < kPW; ++w) { const int t = sh_T[w]; sh_T[w] = tot; tot += t; }
+            int b = -1;
+            if (tot > 0) {
+                const unsigned long long g = atomicAdd(a.pool_top, (unsigned long long)tot);
+                if (g + tot <= (unsigned long long)a.pool_cap) b = (int)g;   // overflow: the host reruns larger
+            }
+            sh_base = b;
+        }
+        __syncthreads();
+        const int base = fuse || sh_base < 0 ? -1 : sh_base + sh_T[wave];
+        __syncthreads();   // sh_T / sh_base are rewritten by the next pass
         if (T == 0) continue;
-        int base = -1;
-        if (lane == 0) {
-            base = atomicAdd(&sh_pool, T);
-            if (base + T > a.pool_cap) base = -1;
-        }
-        base = __builtin_amdgcn_readfirstlane(base);
-        uint32_t *list = base >= 0 ? s.pool + base : a.spill + (int64_t)q * a.spill_stride;
+        uint32_t *list = base >= 0 ? a.pool + base : nullptr;
         const uint4 qa = *reinterpret_cast<const uint4 *>(a.qdesc + 32 * (int64_t)q);
         const uint4 qb = *reinterpret_cast<const uint4 *>(a.qdesc + 32 * (int64_t)q + 16);
         const bool check_lv = Q.min_level > 0 || Q.max_level >= 0;
+        // a keypoint q takes is closed to later queries when q blocks it
+        const bool claims = !fuse && (!occ_obs || (Q.flags & ORBX_QUERY_BLOCKS));
         uint32_t tk[4] = {kNone, kNone, kNone, kNone};   // (dist << 16 | position) of this lane's 4 smallest
         uint32_t te[4] = {0, 0, 0, 0};                   // their entries
         for (int E0 = 0; E0 < T; E0 += kEnt) {
@@ -260,7 +276,7 @@ __global__ __launch_bounds__(kPT) void k_proj_match(ProjBufs a) {
                     }
                     const int dist = ok ? hamming_q(qa, qb, a.desc + 32 * (int64_t)i2) : kBadDist;
                     ent = entry(i2, oct, dist);
-                    list[t] = ent;
+                    if (list) list[t] = ent;
                     if (ok) {
                         uint32_t k = ((uint32_t)dist << 16) | (uint32_t)t;
                         uint32_t ke = ent;
@@ -294,7 +310,19 @@ __global__ __launch_bounds__(kPT) void k_proj_match(ProjBufs a) {
                 a.q_idx[q] = e_idx(top[0]);
                 a.q_dist[q] = e_dist(top[0]);
             }
-        } else if (lane == 0) {
+        } else {
+            if (claims && top[3] != kNone && e_dist(top[3]) <= a.th_dist && list) {
+                // more possible takes than the 4 kept: register them all (rare)
+                __threadfence();
+                for (int t = lane; t < T; t += 64) {
+                    const uint32_t ent = __hip_atomic_load(list + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (e_dist(ent) <= a.th_dist) {
+                        const uint32_t h = atomicAdd(a.hard_cnt, 1u);
+                        if (h < (uint32_t)a.hard_cap) a.hard[h] = make_uint2((uint32_t)e_idx(ent), (uint32_t)q);
+                    }
+                }
+            }
+            if (lane != 0) continue;
             uint4 t4;
             t4.x = top[0]; t4.y = top[1]; t4.z = top[2]; t4.w = top[3];
             reinterpret_cast<uint4 *>(a.qtop)[q] = t4;
@@ -302,28 +330,260 @@ __global__ __launch_bounds__(kPT) void k_proj_match(ProjBufs a) {
             a.qbase[q] = base;
         }
     }
-    __syncthreads();
+}
 
-    // ---- 3. greedy assignment in query order (wave 0)
-    if (!fuse && wave == 0) {
+__device__ inline bool taken_static(int st, bool occ_obs) { return occ_obs ? st == 3 : (st & 1); }
+
+constexpr int kFQ = 512;   // full-list queries a round hands to the waves
+
+// Keypoint state seen by query q in the replay.
+struct RState {
+    const uint8_t *state;   // initial map-point state
+    uint32_t *blk;          // first blocking taker so far
+    const uint32_t *opn;    // first open claimer this round
+    const uint32_t *hard;   // first claimer with claims past its 4 kept entries
+    bool occ_obs;
+    __device__ bool taken(int k, uint32_t q) const { return taken_static(state[k], occ_obs) || blk[k] < q; }
+    // an earlier query that is still open may take it
+    __device__ bool contended(int k, uint32_t q) const { return opn[k] < q || hard[k] < q; }
+};
+
+// The two smallest not-taken entries of a query's full candidate list, by
+// (distance, position in the list); wave-uniform arguments and results.
+__device__ inline void wave_two_free(const uint32_t *list, int cnt, uint32_t q, const RState &r, int lane,
+                                     uint32_t &x1, uint32_t &x2) {
+    uint32_t k1 = kNone, k2 = kNone;
+    x1 = x2 = kNone;
+    for (int c0 = 0; c0 < cnt; c0 += 64) {
+        const int e = c0 + lane;
+        uint32_t key = kNone, ent = kNone;
+        if (e < cnt) {
+            ent = list[e];
+            if (e_dist(ent) != kBadDist && !r.taken(e_idx(ent), q)) key = ((uint32_t)e_dist(ent) << 16) | (uint32_t)e;
+        }
+        const uint32_t m1 = wave_min_u32(key);
+        if (m1 == kNone) continue;
+        const int l1 = (int)(m1 & 0xFFFF) - c0;
+        const uint32_t ent1 = (uint32_t)__builtin_amdgcn_readlane((int)ent, l1);
+        const uint32_t m2 = wave_min_u32(lane == l1 ? kNone : key);
+        uint32_t ent2 = kNone;
+        if (m2 != kNone) ent2 = (uint32_t)__builtin_amdgcn_readlane((int)ent, (int)(m2 & 0xFFFF) - c0);
+        // merge (m1, m2) into the running two smallest
+        if (m1 < k1) {
+            if (m2 < k1) { k2 = m2; x2 = ent2; } else { k2 = k1; x2 = x1; }
+            k1 = m1; x1 = ent1;
+        } else if (m1 < k2) {
+            k2 = m1; x2 = ent1;
+        }
+    }
+}
+
+// ORBmatcher's acceptance of the best (and, with the ratio test, second)
+// free entry; records the take.  True when q takes a keypoint.
+__device__ inline bool accept(const ProjBufs &a, bool ratio, int q, const uint32_t got[2], bool blocks, uint32_t *blk) {
+    if (got[0] == kNone) return false;
+    const int bestDist = e_dist(got[0]);
+    // bestDist starts at 256 and only strictly smaller distances replace it
+    if (bestDist > a.th_dist || bestDist >= 256) return false;
+    if (ratio) {
+        // best and second of ORBmatcher.cc:98-112, with their octaves; a 256
+        // never becomes second (bestDist2 = 256, bestLevel2 = -1)
+        const bool has2 = got[1] != kNone && e_dist(got[1]) < 256;
+        const int bestDist2 = has2 ? e_dist(got[1]) : 256;
+        const int lv1 = e_oct(got[0]), lv2 = has2 ? e_oct(got[1]) : -1;
+        if (lv1 == lv2 && (float)bestDist > __fmul_rn(a.nnratio, (float)bestDist2)) return false;
+    }
+    const int idx = e_idx(got[0]);
+    a.q_idx[q] = idx;
+    a.q_dist[q] = bestDist;
+    atomicMax(&a.kp_final[idx], q);   // a non-blocking take leaves it to later queries
+    if (blocks) atomicMin(&blk[idx], (uint32_t)q);
+    return true;
+}
+
+// The greedy assignment (ORBmatcher.cc:45-129, 1330-1601), then the rotation
+// check and the count.  One block.
+//
+// A query examines its entries in (distance, position) order until it has the
+// one (two, with the ratio test) not yet taken.  An entry is taken at query q
+// when its initial state says so or a blocking take by a query < q made it
+// so; only entries within th_dist of a query ("claims", all among its 4 kept
+// entries unless `hard` has them) can ever be taken by it.  Rounds: every open
+// query registers its claims (minimum open claimer per keypoint); an open
+// query none of whose examined entries has an open claimer < q sees exactly
+// what the in-order loop would, and is decided (by a thread from its 4 kept
+// entries, or by a wave from its full list when those are not enough).  The
+// rounds stop when none progresses; what is left (contention chains through
+// `hard` claims) is replayed by wave 0 in query order.
+template <bool QL>   // per-query data in LDS (else global; one instantiation each keeps ds_* loads ds_*)
+__global__ __launch_bounds__(kPT) void k_proj_replay(ProjBufs a) {
+    extern __shared__ __align__(16) uint8_t lds[];
+    const uint64_t c0 = wall_clock64();
+    const int n = a.n, nq = a.nq;
+    const int V = a.variant;
+    const bool fuse = V == ORBX_PROJ_FUSE || V == ORBX_PROJ_FUSE_SIM3;
+    const bool occ_obs = V == ORBX_PROJ_LOCALMAP || V == ORBX_PROJ_LASTFRAME;   // skip: has && Observations() > 0
+    const bool ratio = V == ORBX_PROJ_LOCALMAP;
+    const bool use_ori = a.check_ori && (V == ORBX_PROJ_LASTFRAME || V == ORBX_PROJ_KEYFRAME);
+    const int need = ratio ? 2 : 1;
+    // LDS: per keypoint blk / opn / hard (u32) and state (u8), the full-list
+    // queue; per query the 4 kept entries and a status byte, in LDS when they
+    // fit (else in global memory)
+    constexpr bool q_in_lds = QL;
+    uint32_t *blk = reinterpret_cast<uint32_t *>(lds);
+    uint32_t *opn = blk + n;
+    uint32_t *hard = opn + n;
+    int32_t *fq = reinterpret_cast<int32_t *>(hard + n);
+    uint8_t *p8 = lds + ((12 * (size_t)n + 12 * kFQ + 15) & ~size_t(15));
+    uint4 *qt = q_in_lds ? reinterpret_cast<uint4 *>(p8) : reinterpret_cast<uint4 *>(a.qtop);
+    if (q_in_lds) p8 += 16 * (size_t)nq;
+    uint8_t *state = p8;
+    // per query: bits 0-1 status (0 decided, 1 open), bit 2 blocks
+    uint8_t *qs = q_in_lds ? p8 + n : a.und;
+    const RState rs{state, blk, opn, hard, occ_obs};
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    __shared__ int ws[kPW];
+    __shared__ int hist[kHist];
+    __shared__ int sh_acc, sh_removed, sh_top[3], sh_prog[2], sh_fq;
+    if (!fuse) {
+        for (int i = tid; i < n; i += kPT) {
+            state[i] = a.mp_state ? (a.mp_state[i] & 3) : 0;
+            blk[i] = kNone;
+            hard[i] = kNone;
+        }
+        for (int q = tid; q < nq; q += kPT) {
+            const uint4 t4 = reinterpret_cast<const uint4 *>(a.qtop)[q];
+            const int fl = a.q[q].flags;
+            if (q_in_lds) qt[q] = t4;
+            // open: some entry within th_dist (else no take is possible)
+            const bool open = (fl & ORBX_QUERY_ACTIVE) && t4.x != kNone && e_dist(t4.x) <= a.th_dist;
+            const bool blocks = !occ_obs || (fl & ORBX_QUERY_BLOCKS);
+            qs[q] = (uint8_t)((open ? 1 : 0) | (blocks ? 4 : 0));
+        }
+    }
+    if (tid < kHist) hist[tid] = 0;
+    if (tid == 0) { sh_acc = 0; sh_removed = 0; }
+    __syncthreads();
+    const uint32_t nhard = fuse ? 0 : *a.hard_cnt;
+    for (uint32_t h = tid; h < min(nhard, (uint32_t)a.hard_cap); h += kPT) {
+        const uint2 c = a.hard[h];
+        atomicMin(&hard[c.x], c.y);
+    }
+    __syncthreads();
+    if (a.stats && tid == 0) a.stats[2] = (int)(wall_clock64() - c0);
+
+    // ---- 3a. rounds of order-independent decisions
+    // (claims lost to a full `hard` list: everything goes in order)
+    if (!fuse && nhard <= (uint32_t)a.hard_cap) {
         int accepted = 0;
-        for (int g0 = 0; g0 < nq; g0 += 64) {
-            const int gq = g0 + lane;
-            uint4 t4 = make_uint4(kNone, kNone, kNone, kNone);
-            int len = 0, qb = -1, qblk = 0;
-            bool live = false;
-            if (gq < nq) {
-                const orbx_proj_query Q = a.q[gq];
-                qblk = (Q.flags & ORBX_QUERY_BLOCKS) ? 2 : 0;
-                if (Q.flags & ORBX_QUERY_ACTIVE) {
-                    t4 = reinterpret_cast<const uint4 *>(a.qtop)[gq];
-                    len = a.qlen[gq];
-                    qb = a.qbase[gq];
-                    // nothing at or under th_dist: no state change possible
-                    live = len > 0 && t4.x != kNone && e_dist(t4.x) <= a.th_dist;
+        for (int round = 0; round < 64; ++round) {
+            for (int i = tid; i < n; i += kPT) opn[i] = kNone;
+            if (tid == 0) { sh_prog[round & 1] = 0; sh_fq = 0; }
+            int any_open = 0;
+            for (int q = tid; q < nq && !any_open; q += kPT) any_open = (qs[q] & 3) == 1;
+            if (!__syncthreads_or(any_open)) {
+                if (a.stats && tid == 0) a.stats[0] = round;
+                break;
+            }
+            for (int q = tid; q < nq; q += kPT) {
+                if (qs[q] != (1 | 4)) continue;   // open and blocking (other takes close nothing)
+                const uint4 t4 = qt[q];
+                const uint32_t e4[4] = {t4.x, t4.y, t4.z, t4.w};
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    if (e4[t] == kNone || e_dist(e4[t]) > a.th_dist) break;
+                    const int k = e_idx(e4[t]);
+                    if (!taken_static(state[k], occ_obs)) atomicMin(&opn[k], (uint32_t)q);
                 }
             }
-            uint64_t todo = __ballot(live);
+            __syncthreads();
+            int prog = 0;
+            for (int q = tid; q < nq; q += kPT) {
+                const int st = qs[q];
+                if ((st & 3) != 1) continue;
+                const uint4 t4 = qt[q];
+                const uint32_t e4[4] = {t4.x, t4.y, t4.z, t4.w};
+                // all four entries' state at once (independent LDS reads)
+                bool tk[4], ct[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int k = e4[t] == kNone ? 0 : e_idx(e4[t]);
+                    tk[t] = rs.taken(k, q);
+                    ct[t] = rs.contended(k, q);
+                }
+                uint32_t got[2] = {kNone, kNone};
+                int found = 0;
+                bool stuck = false;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    if (found == need || stuck || e4[t] == kNone) continue;
+                    if (tk[t]) continue;
+                    if (ct[t]) { stuck = true; continue; }
+                    got[found++] = e4[t];
+                }
+                if (stuck) continue;
+                if (found < need && e4[3] != kNone) {
+                    // past the 4 kept entries: a wave scans the full list below
+                    const int slot = atomicAdd(&sh_fq, 1);
+                    if (slot < kFQ) {   // (a full queue leaves q open for the next round)
+                        fq[3 * slot] = q;
+                        fq[3 * slot + 1] = a.qbase[q];
+                        fq[3 * slot + 2] = a.qlen[q];
+                    }
+                    continue;
+                }
+                qs[q] = (uint8_t)(st & 4);
+                prog = 1;
+                accepted += accept(a, ratio, q, got, st & 4, blk);
+            }
+            __syncthreads();
+            const int nfq = min(sh_fq, kFQ);
+            for (int i = wave; i < nfq; i += kPW) {
+                const int q = fq[3 * i], qb = fq[3 * i + 1], len = fq[3 * i + 2];
+                const int st = qs[q];
+                prog = 1;
+                if (qb < 0) {   // the pool overflowed: the host runs the call again
+                    if (lane == 0) qs[q] = (uint8_t)(st & 4);
+                    continue;
+                }
+                uint32_t got[2];
+                wave_two_free(a.pool + qb, len, q, rs, lane, got[0], got[1]);
+                if (need == 1) got[1] = kNone;
+                bool stuck = false;
+                for (int t = 0; t < 2; ++t)
+                    if (got[t] != kNone && rs.contended(e_idx(got[t]), q)) stuck = true;
+                if (stuck) continue;
+                if (lane == 0) {
+                    qs[q] = (uint8_t)(st & 4);
+                    accepted += accept(a, ratio, q, got, st & 4, blk);
+                }
+            }
+            if (prog) sh_prog[round & 1] = 1;
+            __syncthreads();
+            if (!sh_prog[round & 1]) {   // (the next round resets the other flag)
+                if (a.stats && tid == 0) a.stats[0] = round + 1;
+                break;
+            }
+        }
+        const int tot = wave_sum_i32(accepted);
+        if (lane == 0 && tot) atomicAdd(&sh_acc, tot);
+        __syncthreads();
+    }
+    if (a.stats && tid == 0) a.stats[3] = (int)(wall_clock64() - c0);
+
+    // ---- 3b. what is left, in query order (wave 0)
+    int left = 0;
+    if (!fuse)
+        for (int q = tid; q < nq && !left; q += kPT) left = (qs[q] & 3) != 0;
+    if (__syncthreads_or(left) && wave == 0) {
+        int accepted = 0, nserial = 0;
+        for (int g0 = 0; g0 < nq; g0 += 64) {
+            const int gq = g0 + lane;
+            const int st = gq < nq ? qs[gq] : 0;
+            uint64_t todo = __ballot((st & 3) != 0);
+            if (!todo) continue;
+            nserial += __popcll(todo);
+            const uint4 t4 = (st & 3) ? qt[gq] : make_uint4(kNone, kNone, kNone, kNone);
             while (todo) {
                 const int j = (int)__builtin_ctzll(todo);
                 todo &= todo - 1;
@@ -332,84 +592,34 @@ __global__ __launch_bounds__(kPT) void k_proj_match(ProjBufs a) {
                                         (uint32_t)__builtin_amdgcn_readlane((int)t4.y, j),
                                         (uint32_t)__builtin_amdgcn_readlane((int)t4.z, j),
                                         (uint32_t)__builtin_amdgcn_readlane((int)t4.w, j)};
-                const int blocks = __builtin_amdgcn_readlane(qblk, j);
-                int st4[4];
-#pragma unroll
-                for (int t = 0; t < 4; ++t) st4[t] = e4[t] == kNone ? 0 : s.state[e_idx(e4[t])];
-                const int need = ratio ? 2 : 1;
+                const bool blocks = __builtin_amdgcn_readlane(st, j) & 4;
                 uint32_t got[2] = {kNone, kNone};
                 int found = 0;
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
                     if (e4[t] == kNone || found == need) continue;
-                    const bool taken = occ_obs ? (st4[t] == 3) : (st4[t] & 1);
-                    if (taken) continue;
+                    if (rs.taken(e_idx(e4[t]), q)) continue;
                     got[found++] = e4[t];
                 }
                 if (found < need && e4[3] != kNone) {
                     // more entries than the 4 kept: scan the whole list
-                    const int cnt = __builtin_amdgcn_readlane(len, j);
-                    const int lb = __builtin_amdgcn_readlane(qb, j);
-                    const uint32_t *list = lb >= 0 ? s.pool + lb : a.spill + (int64_t)q * a.spill_stride;
-                    uint32_t k1 = kNone, k2 = kNone;   // (dist << 16 | position), two smallest free
-                    uint32_t x1 = kNone, x2 = kNone;
-                    for (int c0 = 0; c0 < cnt; c0 += 64) {
-                        const int e = c0 + lane;
-                        uint32_t key = kNone, ent = kNone;
-                        if (e < cnt) {
-                            ent = list[e];
-                            const int d = e_dist(ent);
-                            const int stt = s.state[e_idx(ent)];
-                            const bool taken = occ_obs ? (stt == 3) : (stt & 1);
-                            if (d != kBadDist && !taken) key = ((uint32_t)d << 16) | (uint32_t)e;
-                        }
-                        const uint32_t m1 = wave_min_u32(key);
-                        if (m1 == kNone) continue;
-                        const int l1 = (int)(m1 & 0xFFFF) - c0;
-                        const uint32_t ent1 = (uint32_t)__builtin_amdgcn_readlane((int)ent, l1);
-                        const uint32_t m2 = wave_min_u32(lane == l1 ? kNone : key);
-                        uint32_t ent2 = kNone;
-                        if (m2 != kNone) ent2 = (uint32_t)__builtin_amdgcn_readlane((int)ent, (int)(m2 & 0xFFFF) - c0);
-                        // merge (m1, m2) into the running two smallest
-                        if (m1 < k1) {
-                            if (m2 < k1) { k2 = m2; x2 = ent2; } else { k2 = k1; x2 = x1; }
-                            k1 = m1; x1 = ent1;
-                        } else if (m1 < k2) {
-                            k2 = m1; x2 = ent1;
-                        }
-                    }
-                    got[0] = x1;
-                    got[1] = x2;
-                    found = (x1 != kNone) + (x2 != kNone);
+                    const int qb = a.qbase[q];
+                    if (qb < 0) continue;   // the pool overflowed: the host runs the call again
+                    wave_two_free(a.pool + qb, a.qlen[q], q, rs, lane, got[0], got[1]);
+                    if (need == 1) got[1] = kNone;
                 }
-                if (got[0] == kNone) continue;
-                const int bestDist = e_dist(got[0]);
-                // bestDist starts at 256 and only strictly smaller distances replace it
-                if (bestDist > a.th_dist || bestDist >= 256) continue;
-                if (ratio) {
-                    // best and second of ORBmatcher.cc:98-112: the first two free
-                    // entries in (distance, position) order, with their octaves; a
-                    // 256 never becomes second (bestDist2 = 256, bestLevel2 = -1)
-                    const bool has2 = got[1] != kNone && e_dist(got[1]) < 256;
-                    const int bestDist2 = has2 ? e_dist(got[1]) : 256;
-                    const int lv1 = e_oct(got[0]), lv2 = has2 ? e_oct(got[1]) : -1;
-                    if (lv1 == lv2 && (float)bestDist > __fmul_rn(a.nnratio, (float)bestDist2)) continue;
-                }
-                const int idx = e_idx(got[0]);
-                if (lane == 0) {
-                    s.state[idx] = (uint8_t)(1 | blocks);
-                    a.kp_final[idx] = q;
-                    a.q_idx[q] = idx;
-                    a.q_dist[q] = bestDist;
-                }
-                ++accepted;
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                bool took = false;
+                if (lane == 0) took = accept(a, ratio, q, got, blocks, blk);
+                accepted += __builtin_amdgcn_readfirstlane((int)took);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");
                 __builtin_amdgcn_wave_barrier();
             }
         }
-        if (lane == 0) sh_acc = accepted;
+        if (lane == 0) sh_acc += accepted;
+        if (a.stats && lane == 0) a.stats[1] = nserial;
     }
     __syncthreads();
+    if (a.stats && tid == 0) a.stats[5] = (int)(wall_clock64() - c0);
 
     // ---- 4. rotation consistency (ORBmatcher.cc:1434-1469, 1568-1598)
     if (use_ori) {
@@ -469,28 +679,40 @@ __global__ __launch_bounds__(kPT) void k_proj_match(ProjBufs a) {
 
 }  // namespace
 
-int proj_lds_bytes(int n, int pool_cap) {
+int proj_lds_bytes(int n) {
     auto al = [](size_t b) { return (int)((b + 15) & ~size_t(15)); };
     return al(4 * (kCells + 1)) + al(4 * kCells) + al(8 * (size_t)n) + al(4 * (size_t)n) + al(2 * (size_t)n) +
-           al(2 * (size_t)n) + al((size_t)n) + al((size_t)n) + al((size_t)kPW * kEnt) + al(4 * (size_t)pool_cap);
+           al(2 * (size_t)n) + al((size_t)n) + al((size_t)kPW * kEnt);
 }
 
-constexpr int kProjLdsMax = 160 * 1024 - 1024;   // dynamic LDS; the static part needs < 1 KiB
 
-int proj_pool_cap(int n, int nq) {
-    const int fixed = proj_lds_bytes(n, 0);
-    if (fixed > kProjLdsMax) return -1;
-    return (int)std::min<int64_t>((int64_t)std::max(nq, 1) * std::max(n, 1), (kProjLdsMax - fixed) / 4);
+int proj_replay_lds_bytes(int n, int nq, bool q_in_lds) {
+    return 13 * n + 12 * kFQ + (q_in_lds ? 17 * nq : 0) + 64;
 }
+
+bool proj_fits(int n) { return n <= kKPer * kPT && proj_lds_bytes(n) <= kProjLdsMax && proj_replay_lds_bytes(n, 0, false) <= kProjLdsMax; }
 
 hipError_t launch_proj(const ProjBufs &a, hipStream_t st) {
-    const int bytes = proj_lds_bytes(a.n, a.pool_cap);
+    const int bytes = proj_lds_bytes(a.n);
     if (bytes > kProjLdsMax) return hipErrorInvalidValue;
     if (bytes > 64 * 1024 &&
-        hipFuncSetAttribute(reinterpret_cast<const void *>(k_proj_match), hipFuncAttributeMaxDynamicSharedMemorySize,
+        hipFuncSetAttribute(reinterpret_cast<const void *>(k_proj_search), hipFuncAttributeMaxDynamicSharedMemorySize,
                             bytes) != hipSuccess)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_proj_match, dim3(1), dim3(kPT), bytes, st, a);
+    // spread the queries over the chip, one per wave up to two blocks per CU
+    const int blocks = std::max(1, std::min(512, (a.nq + kPW - 1) / kPW));
+    hipLaunchKernelGGL(k_proj_search, dim3(blocks), dim3(kPT), bytes, st, a);
+    const bool q_in_lds = proj_replay_lds_bytes(a.n, a.nq, true) <= kProjLdsMax;
+    if (proj_replay_lds_bytes(a.n, a.nq, q_in_lds) > kProjLdsMax) return hipErrorInvalidValue;
+    const int rbytes = proj_replay_lds_bytes(a.n, a.nq, q_in_lds);
+    const void *rk = q_in_lds ? reinterpret_cast<const void *>(k_proj_replay<true>)
+                              : reinterpret_cast<const void *>(k_proj_replay<false>);
+    if (rbytes > 64 * 1024 && hipFuncSetAttribute(rk, hipFuncAttributeMaxDynamicSharedMemorySize, rbytes) != hipSuccess)
+        return hipErrorInvalidValue;
+    if (q_in_lds)
+        hipLaunchKernelGGL(k_proj_replay<true>, dim3(1), dim3(kPT), rbytes, st, a);
+    else
+        hipLaunchKernelGGL(k_proj_replay<false>, dim3(1), dim3(kPT), rbytes, st, a);
     return hipGetLastError();
 }
 

@@ -56,6 +56,7 @@ struct CallWs {
     hipStream_t st = nullptr;
     uint8_t *dev = nullptr, *host = nullptr;
     size_t cap = 0;
+    int64_t proj_pool = 0;   // projection candidate-list entries the last calls needed
 };
 
 CallWs &call_ws(int device) {
@@ -1164,57 +1165,83 @@ int orbx_search_by_projection(int device, int variant, const orbx_match_frame *F
         for (int i = 0; i < n; ++i) kp_final[i] = -1;
         return ORBX_OK;
     }
-    const int pool_cap = proj_pool_cap(n, nq);
-    if (pool_cap < 0) return ORBX_EINVAL;
+    if (!proj_fits(n)) return ORBX_EINVAL;
     if (hipSetDevice(device) != hipSuccess) return ORBX_ENODEV;
-    const bool spill = (int64_t)nq * n > pool_cap;
+    const bool fuse = variant == ORBX_PROJ_FUSE || variant == ORBX_PROJ_FUSE_SIM3;
     const int nlev = F->inv_sigma2 ? std::max(F->nlevels, 0) : 0;
-    Layout L;   // inputs, then outputs, then device-only scratch
-    const size_t o_k = L.add(sizeof(orbx_keypoint) * n), o_d = L.add(32 * (size_t)n),
-                 o_ur = F->uright ? L.add(4 * (size_t)n) : 0, o_ms = F->mp_state ? L.add((size_t)n) : 0,
-                 o_isg = nlev ? L.add(4 * (size_t)nlev) : 0, o_q = L.add(sizeof(orbx_proj_query) * nq),
-                 o_qd = L.add(32 * (size_t)nq);
-    const size_t in_bytes = L.size;
-    const size_t o_qi = L.add(4 * (size_t)nq), o_qdist = L.add(4 * (size_t)nq), o_kf = L.add(4 * (size_t)n),
-                 o_nm = L.add(4);
-    const size_t out_end = L.size;
-    const size_t o_top = L.add(16 * (size_t)nq), o_len = L.add(4 * (size_t)nq), o_base = L.add(4 * (size_t)nq),
-                 o_sp = spill ? L.add(4 * (size_t)nq * n) : 0;
     CallWs &ws = call_ws(device);
     std::lock_guard<std::mutex> lock(ws.mu);
-    int rc = ws_reserve(ws, L.size);
-    if (rc) return rc;
-    put(ws, o_k, F->keys, sizeof(orbx_keypoint) * n);
-    put(ws, o_d, F->desc, 32 * (size_t)n);
-    if (F->uright) put(ws, o_ur, F->uright, 4 * (size_t)n);
-    if (F->mp_state) put(ws, o_ms, F->mp_state, (size_t)n);
-    if (nlev) put(ws, o_isg, F->inv_sigma2, 4 * (size_t)nlev);
-    put(ws, o_q, queries, sizeof(orbx_proj_query) * nq);
-    put(ws, o_qd, qdesc, 32 * (size_t)nq);
-    if (hipMemcpyAsync(ws.dev, ws.host, in_bytes, hipMemcpyHostToDevice, ws.st) != hipSuccess) return ORBX_EIO;
-    ProjBufs a{};
-    uint8_t *D = ws.dev;
-    a.keys = at<orbx_keypoint>(D, o_k); a.desc = D + o_d;
-    a.uright = F->uright ? at<float>(D, o_ur) : nullptr;
-    a.mp_state = F->mp_state ? D + o_ms : nullptr;
-    a.inv_sigma2 = nlev ? at<float>(D, o_isg) : nullptr;
-    a.n = n; a.nlevels = nlev;
-    a.min_x = F->min_x; a.max_x = F->max_x; a.min_y = F->min_y; a.max_y = F->max_y;
-    a.q = at<orbx_proj_query>(D, o_q); a.qdesc = D + o_qd; a.nq = nq;
-    a.variant = variant; a.th_dist = th_dist; a.nnratio = nnratio; a.check_ori = check_ori;
-    a.q_idx = at<int32_t>(D, o_qi); a.q_dist = at<int32_t>(D, o_qdist); a.kp_final = at<int32_t>(D, o_kf);
-    a.nmatches = at<int32_t>(D, o_nm);
-    a.qtop = at<uint32_t>(D, o_top); a.qlen = at<int32_t>(D, o_len); a.qbase = at<int32_t>(D, o_base);
-    a.spill = spill ? at<uint32_t>(D, o_sp) : nullptr; a.spill_stride = n; a.pool_cap = pool_cap;
-    if (launch_proj(a, ws.st) != hipSuccess ||
-        hipMemcpyAsync(ws.host + o_qi, D + o_qi, out_end - o_qi, hipMemcpyDeviceToHost, ws.st) != hipSuccess ||
-        hipStreamSynchronize(ws.st) != hipSuccess)
-        return ORBX_EIO;
-    get(ws, o_qi, q_idx, 4 * (size_t)nq);
-    get(ws, o_qdist, q_dist, 4 * (size_t)nq);
-    get(ws, o_kf, kp_final, 4 * (size_t)n);
-    get(ws, o_nm, nmatches, 4);
-    return ORBX_OK;
+    // candidate lists of all queries share one pool; its size is learnt: a
+    // call that overflows it reports the total it needed and runs again
+    int64_t pool = fuse ? 1 : std::max<int64_t>({ws.proj_pool, 64 * (int64_t)nq, 1 << 16});
+    const int hard_cap = 4 * nq + 4096;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        Layout L;   // inputs, then outputs, then device-only scratch
+        const size_t o_k = L.add(sizeof(orbx_keypoint) * n), o_d = L.add(32 * (size_t)n),
+                     o_ur = F->uright ? L.add(4 * (size_t)n) : 0, o_ms = F->mp_state ? L.add((size_t)n) : 0,
+                     o_isg = nlev ? L.add(4 * (size_t)nlev) : 0, o_q = L.add(sizeof(orbx_proj_query) * nq),
+                     o_qd = L.add(32 * (size_t)nq);
+        const size_t o_ptop = L.add(16);   // pool_top, hard_cnt: zeros from the host, read back after
+        const size_t in_bytes = L.size;
+        const size_t o_qi = L.add(4 * (size_t)nq), o_qdist = L.add(4 * (size_t)nq), o_kf = L.add(4 * (size_t)n),
+                     o_nm = L.add(4);
+        const size_t out_end = L.size;
+        const size_t o_top = L.add(16 * (size_t)nq), o_len = L.add(4 * (size_t)nq), o_base = L.add(4 * (size_t)nq),
+                     o_pool = L.add(4 * (size_t)pool), o_hard = L.add(8 * (size_t)hard_cap), o_und = L.add((size_t)nq), o_stats = L.add(64);
+        int rc = ws_reserve(ws, L.size);
+        if (rc) return rc;
+        put(ws, o_k, F->keys, sizeof(orbx_keypoint) * n);
+        put(ws, o_d, F->desc, 32 * (size_t)n);
+        if (F->uright) put(ws, o_ur, F->uright, 4 * (size_t)n);
+        if (F->mp_state) put(ws, o_ms, F->mp_state, (size_t)n);
+        if (nlev) put(ws, o_isg, F->inv_sigma2, 4 * (size_t)nlev);
+        put(ws, o_q, queries, sizeof(orbx_proj_query) * nq);
+        put(ws, o_qd, qdesc, 32 * (size_t)nq);
+        std::memset(ws.host + o_ptop, 0, 16);
+        if (hipMemcpyAsync(ws.dev, ws.host, in_bytes, hipMemcpyHostToDevice, ws.st) != hipSuccess) return ORBX_EIO;
+        ProjBufs a{};
+        uint8_t *D = ws.dev;
+        a.keys = at<orbx_keypoint>(D, o_k); a.desc = D + o_d;
+        a.uright = F->uright ? at<float>(D, o_ur) : nullptr;
+        a.mp_state = F->mp_state ? D + o_ms : nullptr;
+        a.inv_sigma2 = nlev ? at<float>(D, o_isg) : nullptr;
+        a.n = n; a.nlevels = nlev;
+        a.min_x = F->min_x; a.max_x = F->max_x; a.min_y = F->min_y; a.max_y = F->max_y;
+        a.q = at<orbx_proj_query>(D, o_q); a.qdesc = D + o_qd; a.nq = nq;
+        a.variant = variant; a.th_dist = th_dist; a.nnratio = nnratio; a.check_ori = check_ori;
+        a.q_idx = at<int32_t>(D, o_qi); a.q_dist = at<int32_t>(D, o_qdist); a.kp_final = at<int32_t>(D, o_kf);
+        a.nmatches = at<int32_t>(D, o_nm);
+        a.qtop = at<uint32_t>(D, o_top); a.qlen = at<int32_t>(D, o_len); a.qbase = at<int32_t>(D, o_base);
+        a.pool = at<uint32_t>(D, o_pool); a.pool_cap = pool;
+        a.pool_top = at<unsigned long long>(D, o_ptop); a.hard_cnt = at<uint32_t>(D, o_ptop + 8);
+        a.hard = at<uint2>(D, o_hard); a.hard_cap = hard_cap; a.und = D + o_und;
+        static const bool dbg_stats = std::getenv("ORBX_PROJ_STATS") != nullptr;
+        a.stats = dbg_stats ? at<int32_t>(D, o_stats) : nullptr;
+        if (launch_proj(a, ws.st) != hipSuccess ||
+            hipMemcpyAsync(ws.host + o_ptop, D + o_ptop, out_end - o_ptop, hipMemcpyDeviceToHost, ws.st) != hipSuccess ||
+            hipStreamSynchronize(ws.st) != hipSuccess)
+            return ORBX_EIO;
+        unsigned long long used = 0;
+        get(ws, o_ptop, &used, 8);
+        if (a.stats) {
+            int32_t st2[6] = {};
+            if (hipMemcpy(st2, a.stats, sizeof(st2), hipMemcpyDeviceToHost) == hipSuccess)
+                std::fprintf(stderr, "orbx proj: variant %d nq %d rounds %d in-order %d pool %llu | 10ns: init %d rounds %d end %d\n",
+                             variant, nq, st2[0], st2[1], used, st2[2], st2[3], st2[5]);
+        }
+        if (!fuse) ws.proj_pool = std::max<int64_t>(ws.proj_pool, (int64_t)used);
+        if (!fuse && (int64_t)used > pool) {
+            if (used > (unsigned long long)INT32_MAX) return ORBX_ENOMEM;
+            pool = (int64_t)used;
+            continue;
+        }
+        get(ws, o_qi, q_idx, 4 * (size_t)nq);
+        get(ws, o_qdist, q_dist, 4 * (size_t)nq);
+        get(ws, o_kf, kp_final, 4 * (size_t)n);
+        get(ws, o_nm, nmatches, 4);
+        return ORBX_OK;
+    }
+    return ORBX_EIO;
 }
 
 int orbx_search_by_bow(int device, int variant, const orbx_bow_side *A, const orbx_bow_side *B, float nnratio,

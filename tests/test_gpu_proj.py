@@ -107,3 +107,22 @@ def test_cpp_adapter_projection_table(tmp_path, oracle_mod):
                                         c["uright"], c["mp_state"], c["inv_sigma2"], th, np.float32(ratio), ori)
     assert nm == o[0] and nm > 0
     assert np.array_equal(qi, o[1]) and np.array_equal(qd, o[2]) and np.array_equal(kf, o[3])
+
+
+def test_projection_pool_growth(oracle_mod):
+    """Very wide windows over the largest frame the grid LDS holds: the
+    candidate lists total millions of entries, more than the pool the earlier
+    calls sized, so the call overflows it, learns the size and runs again."""
+    from proj_cases import make_case
+    c = make_case(97, "localmap", n=7000, nq=600, stereo=False, th=60.0)
+    assert _check(c, "localmap", oracle_mod) > 0
+    assert _check(c, "lastframe", oracle_mod, th=255) > 0
+
+
+@pytest.mark.parametrize("variant", ["localmap", "keyframe"])
+def test_projection_many_points(variant, oracle_mod):
+    """More map points than the replay keeps in LDS (their kept entries and
+    status stay in global memory)."""
+    from proj_cases import VARIANT_ARGS, make_case
+    c = make_case(98, variant, n=3000, nq=9000, stereo=True, th=VARIANT_ARGS[variant][3])
+    assert _check(c, variant, oracle_mod) > 0

@@ -1,0 +1,15 @@
+"""Median duration (us) per kernel name from a rocprofv3 rocpd database, in
+dispatch order groups: tools/kernel_times.py DB [GROUPS]"""
+import sqlite3
+import sys
+
+import numpy as np
+
+db = sys.argv[1]
+groups = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+rows = sqlite3.connect(db).execute("select name, start, end from kernels order by start").fetchall()
+names = sorted({r[0] for r in rows})
+for nm in names:
+    d = [(r[2] - r[1]) / 1e3 for r in rows if r[0] == nm]
+    k = max(1, len(d) // groups)
+    print(f"{nm[:40]:40s} n={len(d):5d} " + " ".join(f"{np.median(d[i * k:(i + 1) * k]):8.1f}" for i in range(groups)))
