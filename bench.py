@@ -185,6 +185,52 @@ def matcher_latencies(reps: int = 20):
     return out
 
 
+def bow_transform_throughput(torch, frames=512, nfeat=1000, reps=20):
+    """DBoW2 transform of `frames` x `nfeat` device-resident
+    descriptors through a synthetic ORBvoc-shaped vocabulary (k=10, L=6,
+    1.1M nodes; ORBvoc.txt itself is not in the repository), levelsup 4 as
+    Frame::ComputeBoW.  The per-feature descent only (word, weight, node per
+    descriptor); the CPU oracle is timed on 20 frames with its tree prebuilt."""
+    from oracle import oracle
+    from orb_slam_2_ros_amd.synth_vocab import features_near_leaves, make_vocab
+    from orb_slam_2_ros_amd.vocabulary import ORBVocabulary
+    voc = make_vocab(k=10, L=6, seed=5)
+    v = ORBVocabulary.from_arrays(10, 6, 0, 0, voc["parent"], voc["is_leaf"], voc["desc"], voc["weight"])
+    n = frames * nfeat
+    feats = features_near_leaves(voc, n, seed=9, noise=30)
+    d = torch.from_numpy(feats).cuda()
+    word = torch.empty(n, dtype=torch.int32, device="cuda")
+    wt = torch.empty(n, dtype=torch.float64, device="cuda")
+    node = torch.empty(n, dtype=torch.int32, device="cuda")
+    st = torch.cuda.Stream()   # a real stream handle (NULL would mean the library's own stream)
+    st.wait_stream(torch.cuda.current_stream())
+
+    def run():
+        v.transform_device(d.data_ptr(), n, 4, word.data_ptr(), wt.data_ptr(), node.data_ptr(), st.cuda_stream)
+    for _ in range(3):
+        run()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(st)
+    for _ in range(reps):
+        run()
+    e1.record(st)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    pv = oracle.PreparedVocab(voc)
+    sample = feats[:20 * nfeat]
+    pv.transform(sample[:nfeat])
+    t0 = time.perf_counter()
+    for f in range(20):
+        pv.transform(sample[f * nfeat:(f + 1) * nfeat])
+    cpu_ms = 1e3 * (time.perf_counter() - t0) / 20
+    # L2/MALL-resident tree: per feature L levels x (k x 32 B child rows + 16 B node)
+    return {"value": round(n / (ms * 1e-3), 1), "unit": "features/s", "frames_per_launch": frames,
+            "features_per_frame": nfeat, "ms_per_launch": round(ms, 4), "frame_equiv_per_s": round(frames / (ms * 1e-3), 1),
+            "bytes_per_feature_from_cache": 6 * (10 * 32 + 16),
+            "cpu_ms_per_frame": round(cpu_ms, 4), "cpu_kind": "port, 1 thread, tree prebuilt"}
+
+
 def _resident_frames(mode, w, h, batch, rank):
     """Host array [FRAMES_PER_STREAM, frames_per_step, h, w] (+ depth maps for RGB-D)."""
     from orb_slam_2_ros_amd import synth
@@ -330,6 +376,8 @@ def main() -> int:
             roof["pipeline_frac"] = round(frame_bytes * value / world / 1e9 / HBM_PEAK_GBS, 5)
         cpu = cpu_baseline(w, h, nf, args.cpu_seconds) if (world == 1 and args.cpu_seconds > 0) else None
         matchers = matcher_latencies() if (world == 1 and not args.no_extras) else None
+        if world == 1 and not args.no_extras:
+            extras["bow_transform_orbvoc"] = bow_transform_throughput(torch)
         line = {
             "metric": METRIC,
             "value": round(value, 2),

@@ -299,6 +299,57 @@ int orbx_search_by_bow(int device, int variant, const orbx_bow_side *a, const or
                        float nnratio, int check_ori, const float *tri, int nlevels,
                        int32_t *match_a, int32_t *match_b, int *nmatches);
 
+/* ---- DBoW2 vocabulary ----
+ * ORBVocabulary = DBoW2::TemplatedVocabulary<FORB::TDescriptor, FORB>
+ * (ORBVocabulary.h).  The tree is held as loadFromTextFile /
+ * loadFromBinFile build it (TemplatedVocabulary.h:1351-1425 / 1473-1547):
+ * node 0 the root, nodes 1..n_nodes-1 in file order with parent (< own
+ * index), the file's leaf flag, a 32-byte descriptor and a weight (double);
+ * children in file order, word ids in the order of the leaf flags.
+ * scoring / weighting are DBoW2's ScoringType (L1_NORM 0 .. DOT_PRODUCT 5) /
+ * WeightingType (TF_IDF 0, TF 1, IDF 2, BINARY 3).  Creation and loading are
+ * host-only; the first transform uploads the tree to `device`. */
+typedef struct orbx_vocab orbx_vocab;
+
+/* From arrays (row 0 of desc / weight / parent / is_leaf is the root's and
+ * ignored).  k = the header's branching factor (informational; the tree's
+ * own child counts are used, up to 64). */
+int orbx_vocab_create(int device, int k, int L, int scoring, int weighting, int n_nodes,
+                      const int32_t *parent, const uint8_t *is_leaf, const uint8_t *desc,
+                      const double *weight, orbx_vocab **out);
+/* loadFromTextFile (format 0: "k L scoring weighting" then one
+ * "parent isLeaf d0 .. d31 weight" line per node; blank lines skipped) or
+ * loadFromBinFile (format 1: int32 k, L, scoring, weighting, then per node
+ * int32 parent, u8 isLeaf, 32 B, f64 weight, up to (k^(L+1)-1)/(k-1) nodes).
+ * Header checks as the reference: 0<=k<=20, 1<=L<=10, scoring 0..5,
+ * weighting 0..3, else ORBX_EINVAL. */
+int orbx_vocab_load(int device, const char *path, int format, orbx_vocab **out);
+void orbx_vocab_destroy(orbx_vocab *v);
+/* header and sizes; any pointer may be NULL. */
+int orbx_vocab_info(const orbx_vocab *v, int *k, int *L, int *scoring, int *weighting, int *n_nodes,
+                    int *n_words);
+/* The tree back as arrays of n_nodes (cap >= n_nodes, else ORBX_ERANGE). */
+int orbx_vocab_export(const orbx_vocab *v, int32_t *parent, uint8_t *is_leaf, uint8_t *desc,
+                      double *weight, int cap);
+
+/* TemplatedVocabulary::transform(features, BowVector&, FeatureVector&,
+ * levelsup) (TemplatedVocabulary.h:1140-1207), as Frame::ComputeBoW
+ * (Frame.cc:428-435) and KeyFrame::ComputeBoW (KeyFrame.cc:68-77, levelsup 4)
+ * call it.  desc: n rows of 32 B.  BowVector out as ascending (word, value)
+ * pairs (capacity n); FeatureVector out as ascending node ids with per-node
+ * feature lists: fv_offsets[n_fv + 1] (capacity n + 1), fv_features
+ * (capacity n) -- the layout orbx_bow_side takes.  A leaf above level
+ * L - levelsup (the reference leaves its node unset) files the feature under
+ * the leaf.  An empty vocabulary clears both.  Synchronous. */
+int orbx_vocab_transform(orbx_vocab *v, const uint8_t *desc, int n, int levelsup,
+                         uint32_t *bow_words, double *bow_values, int *n_bow,
+                         uint32_t *fv_nodes, int32_t *fv_offsets, int32_t *fv_features, int *n_fv);
+/* Per-feature descent on device buffers, ordered on `stream` (NULL: the
+ * vocabulary's own stream, as the extractor's): word id, weight (0: a
+ * stopped word the vectors skip) and FeatureVector node of each row. */
+int orbx_vocab_transform_device(orbx_vocab *v, const uint8_t *d_desc, int n, int levelsup,
+                                uint32_t *d_word, double *d_weight, uint32_t *d_node, void *stream);
+
 /* Device evaluation of the restated sincosf / fastAtan2 (test hook). */
 int orbx_debug_trig(int device, const float *angles, float *s, float *c, int n,
                     const float *ys, const float *xs, float *atan_deg, int m);

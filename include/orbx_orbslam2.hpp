@@ -15,6 +15,7 @@
 #include <cassert>
 #include <cstdint>
 #include <cstdlib>
+#include <cstring>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -267,6 +268,60 @@ struct OrbxFrame {
                                                  mbf, mvuRight.data(), mvDepth.data(), &kept),
                            "ComputeStereoFromRGBD");
     }
+};
+
+// ORBVocabulary = DBoW2::TemplatedVocabulary<FORB::TDescriptor, FORB> for the
+// parts the per-frame path uses: the two loaders and transform(features, v,
+// fv, levelsup) (TemplatedVocabulary.h:1140-1207, 1351-1547).  BowVector /
+// FeatureVector are DBoW2's (std::map<WordId, WordValue> and
+// std::map<NodeId, std::vector<unsigned int>>); any map-like types with
+// clear() / operator[] work, so this header needs no DBoW2 include.
+class OrbxVocabulary {
+public:
+    OrbxVocabulary() = default;
+    OrbxVocabulary(const OrbxVocabulary &) = delete;
+    OrbxVocabulary &operator=(const OrbxVocabulary &) = delete;
+    ~OrbxVocabulary() { orbx_vocab_destroy(v_); }
+
+    bool loadFromTextFile(const std::string &filename) { return load(filename, 0); }
+    bool loadFromBinFile(const std::string &filename) { return load(filename, 1); }
+
+    bool empty() const { return size() == 0; }
+    unsigned int size() const {
+        int nw = 0;
+        if (v_) orbx_vocab_info(v_, nullptr, nullptr, nullptr, nullptr, nullptr, &nw);
+        return (unsigned int)nw;
+    }
+
+    template <class BowVector, class FeatureVector>
+    void transform(const std::vector<cv::Mat> &features, BowVector &v, FeatureVector &fv, int levelsup) const {
+        v.clear();
+        fv.clear();
+        if (!v_ || features.empty()) return;
+        const int n = (int)features.size();
+        std::vector<uint8_t> desc(32 * (size_t)n);
+        for (int i = 0; i < n; ++i) std::memcpy(&desc[32 * (size_t)i], features[i].ptr<uint8_t>(), 32);
+        std::vector<uint32_t> bw(n), fn(n);
+        std::vector<double> bv(n);
+        std::vector<int32_t> fo(n + 1), ff(n);
+        int nb = 0, nf = 0;
+        orbx_detail::check(orbx_vocab_transform(v_, desc.data(), n, levelsup, bw.data(), bv.data(), &nb, fn.data(),
+                                                fo.data(), ff.data(), &nf),
+                           "ORBVocabulary::transform");
+        for (int i = 0; i < nb; ++i) v[bw[i]] = bv[i];
+        for (int j = 0; j < nf; ++j)
+            for (int t = fo[j]; t < fo[j + 1]; ++t) fv[fn[j]].push_back((unsigned int)ff[t]);
+    }
+
+    orbx_vocab *handle() const { return v_; }
+
+private:
+    bool load(const std::string &filename, int format) {
+        orbx_vocab_destroy(v_);
+        v_ = nullptr;
+        return orbx_vocab_load(orbx_detail::device_index(), filename.c_str(), format, &v_) == ORBX_OK;
+    }
+    orbx_vocab *v_ = nullptr;
 };
 
 }  // namespace ORB_SLAM2

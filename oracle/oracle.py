@@ -286,3 +286,68 @@ def search_by_sim3(k1, d1, b1, k2, d2, b2, q1, qd1, q2, qd2, th_dist=100):
     nf = f(_p(k1), _p(d1), len(k1), _p(k2), _p(d2), len(k2), *[float(x) for x in b1], *[float(x) for x in b2],
            _p(q1), _p(qd1), _p(q2), _p(qd2), int(th_dist), _p(m))
     return nf, m[:len(k1)].copy()
+
+
+def vocab_transform(voc, features, levelsup=4):
+    """DBoW2 TemplatedVocabulary::transform on a vocabulary dict (L, scoring,
+    weighting, parent i32, is_leaf u8, desc (n,32) u8, weight f64; node 0 the
+    root).  Returns (bow: dict word -> value, fv: dict node -> [features],
+    per-feature (word, weight, node))."""
+    f = lib().orbo_vocab_transform
+    f.restype = I32
+    f.argtypes = [I32, I32, I32, I32, P, P, P, P, P, I32, I32, P, P, P, P, P, P, P, P, P, P]
+    par = np.ascontiguousarray(voc["parent"], np.int32)
+    leaf = np.ascontiguousarray(voc["is_leaf"], np.uint8)
+    desc = np.ascontiguousarray(voc["desc"], np.uint8).reshape(-1, 32)
+    wt = np.ascontiguousarray(voc["weight"], np.float64)
+    feats = np.ascontiguousarray(features, np.uint8).reshape(-1, 32)
+    n = len(feats)
+    m = max(n, 1)
+    bw = np.zeros(m, np.uint32); bv = np.zeros(m, np.float64)
+    fn = np.zeros(m, np.uint32); fo = np.zeros(m + 1, np.int32); ff = np.zeros(m, np.int32)
+    fw = np.zeros(m, np.uint32); fwt = np.zeros(m, np.float64); fnd = np.zeros(m, np.uint32)
+    nb = ctypes.c_int(0); nf = ctypes.c_int(0)
+    f(int(voc["L"]), int(voc["scoring"]), int(voc["weighting"]), len(par), _p(par), _p(leaf), _p(desc), _p(wt),
+      _p(feats), n, int(levelsup), _p(bw), _p(bv), ctypes.byref(nb), _p(fn), _p(fo), _p(ff), ctypes.byref(nf),
+      _p(fw), _p(fwt), _p(fnd))
+    bow = {int(bw[i]): float(bv[i]) for i in range(nb.value)}
+    fv = {int(fn[j]): [int(x) for x in ff[fo[j]:fo[j + 1]]] for j in range(nf.value)}
+    return bow, fv, (fw[:n].copy(), fwt[:n].copy(), fnd[:n].copy())
+
+
+class PreparedVocab:
+    """The oracle's tree built once (for timing the per-frame descent)."""
+
+    def __init__(self, voc):
+        l = lib()
+        l.orbo_vocab_prepare.restype = P
+        l.orbo_vocab_prepare.argtypes = [I32, P, P]
+        l.orbo_vocab_release.restype = None
+        l.orbo_vocab_release.argtypes = [P]
+        l.orbo_vocab_transform_prepared.restype = I32
+        l.orbo_vocab_transform_prepared.argtypes = [P, I32, I32, I32, P, P, P, I32, I32] + [P] * 10
+        self.voc = voc
+        self.par = np.ascontiguousarray(voc["parent"], np.int32)
+        self.leaf = np.ascontiguousarray(voc["is_leaf"], np.uint8)
+        self.desc = np.ascontiguousarray(voc["desc"], np.uint8).reshape(-1, 32)
+        self.wt = np.ascontiguousarray(voc["weight"], np.float64)
+        self.h = l.orbo_vocab_prepare(len(self.par), _p(self.par), _p(self.leaf))
+
+    def transform(self, features, levelsup=4):
+        feats = np.ascontiguousarray(features, np.uint8).reshape(-1, 32)
+        n = len(feats)
+        m = max(n, 1)
+        bw = np.zeros(m, np.uint32); bv = np.zeros(m, np.float64)
+        fn = np.zeros(m, np.uint32); fo = np.zeros(m + 1, np.int32); ff = np.zeros(m, np.int32)
+        nb = ctypes.c_int(0); nf = ctypes.c_int(0)
+        lib().orbo_vocab_transform_prepared(self.h, int(self.voc["L"]), int(self.voc["scoring"]),
+                                            int(self.voc["weighting"]), _p(self.desc), _p(self.wt), _p(feats), n,
+                                            int(levelsup), _p(bw), _p(bv), ctypes.byref(nb), _p(fn), _p(fo), _p(ff),
+                                            ctypes.byref(nf), None, None, None)
+        return nb.value, nf.value
+
+    def __del__(self):
+        try:
+            lib().orbo_vocab_release(self.h)
+        except Exception:
+            pass

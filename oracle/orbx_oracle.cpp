@@ -20,6 +20,7 @@
 #include <cmath>
 #include <cstring>
 #include <list>
+#include <map>
 #include <vector>
 
 namespace {
@@ -1213,4 +1214,119 @@ int orbo_search_by_sim3(const orbo_keypoint *k1, const uint8_t *dsc1, int n1, co
         if (idx2 >= 0 && m2[idx2] == i1) { matches12[i1] = idx2; nFound++; }
     }
     return nFound;
+}
+
+// ---------------------------------------------------------------------------
+// DBoW2 vocabulary transform (TemplatedVocabulary.h:1140-1272).
+struct OrboVocab {
+    std::vector<std::vector<int>> children;
+    std::vector<uint32_t> word_id;
+    int nwords = 0;
+};
+
+// The loaders' tree: children in file order, word ids in leaf-flag order.
+void *orbo_vocab_prepare(int n_nodes, const int32_t *parent, const uint8_t *is_leaf) {
+    OrboVocab *t = new OrboVocab;
+    t->children.resize(n_nodes);
+    t->word_id.assign(n_nodes, 0);   // Node(): word_id(0)
+    for (int i = 1; i < n_nodes; ++i) {
+        t->children[parent[i]].push_back(i);
+        if (is_leaf[i]) t->word_id[i] = (uint32_t)t->nwords++;
+    }
+    return t;
+}
+
+void orbo_vocab_release(void *t) { delete static_cast<OrboVocab *>(t); }
+
+int orbo_vocab_transform(int L, int scoring, int weighting, int n_nodes, const int32_t *parent,
+                         const uint8_t *is_leaf, const uint8_t *desc, const double *weight,
+                         const uint8_t *features, int n, int levelsup,
+                         uint32_t *bow_words, double *bow_values, int *n_bow,
+                         uint32_t *fv_nodes, int32_t *fv_offsets, int32_t *fv_features, int *n_fv,
+                         uint32_t *f_word, double *f_weight, uint32_t *f_node) {
+    OrboVocab *t = static_cast<OrboVocab *>(orbo_vocab_prepare(n_nodes, parent, is_leaf));
+    const int r = orbo_vocab_transform_prepared(t, L, scoring, weighting, desc, weight, features, n, levelsup,
+                                                bow_words, bow_values, n_bow, fv_nodes, fv_offsets, fv_features,
+                                                n_fv, f_word, f_weight, f_node);
+    delete t;
+    return r;
+}
+
+int orbo_vocab_transform_prepared(void *tree, int L, int scoring, int weighting, const uint8_t *desc,
+                                  const double *weight, const uint8_t *features, int n, int levelsup,
+                                  uint32_t *bow_words, double *bow_values, int *n_bow,
+                                  uint32_t *fv_nodes, int32_t *fv_offsets, int32_t *fv_features, int *n_fv,
+                                  uint32_t *f_word, double *f_weight, uint32_t *f_node) {
+    const OrboVocab &T = *static_cast<const OrboVocab *>(tree);
+    const std::vector<std::vector<int>> &children = T.children;
+    const std::vector<uint32_t> &word_id = T.word_id;
+    const int nwords = T.nwords;
+    *n_bow = 0;
+    *n_fv = 0;
+    if (fv_offsets) fv_offsets[0] = 0;
+    if (nwords == 0) return 0;   // empty()
+    // normalisation of the scoring object (ScoringObject.h:74-89)
+    const bool must = scoring != 5;              // DOT_PRODUCT does not normalise
+    const bool l2 = scoring == 1;                // L2_NORM; the others are L1
+    std::map<uint32_t, double> bow;
+    std::map<uint32_t, std::vector<int>> fv;
+    const int nid_level = L - levelsup;
+    for (int f = 0; f < n; ++f) {
+        const uint8_t *fd = features + 32 * (size_t)f;
+        uint32_t nid = 0;   // (set at nid_level; a shallower leaf keeps the leaf, see header)
+        int final_id = 0, level = 0;
+        bool nid_set = nid_level <= 0;
+        do {
+            ++level;
+            const std::vector<int> &nodes = children[final_id];
+            final_id = nodes[0];
+            double best_d = hamming32(fd, desc + 32 * (size_t)final_id);
+            for (size_t c = 1; c < nodes.size(); ++c) {
+                const double d = hamming32(fd, desc + 32 * (size_t)nodes[c]);
+                if (d < best_d) { best_d = d; final_id = nodes[c]; }
+            }
+            if (level == nid_level) { nid = (uint32_t)final_id; nid_set = true; }
+        } while (!children[final_id].empty());
+        if (!nid_set) nid = (uint32_t)final_id;
+        const uint32_t wid = word_id[final_id];
+        const double w = weight[final_id];
+        if (f_word) f_word[f] = wid;
+        if (f_weight) f_weight[f] = w;
+        if (f_node) f_node[f] = nid;
+        if (w > 0) {
+            if (weighting == 0 || weighting == 1) {   // TF_IDF, TF: addWeight
+                auto it = bow.find(wid);
+                if (it == bow.end()) bow.emplace(wid, w); else it->second += w;
+            } else {                                  // IDF, BINARY: addIfNotExist
+                bow.emplace(wid, w);
+            }
+            fv[nid].push_back(f);
+        }
+    }
+    if ((weighting == 0 || weighting == 1) && !bow.empty() && !must) {
+        const double nd = (double)bow.size();
+        for (auto &kv : bow) kv.second /= nd;
+    }
+    if (must) {
+        double norm = 0.0;
+        if (!l2) {
+            for (auto &kv : bow) norm += std::fabs(kv.second);
+        } else {
+            for (auto &kv : bow) norm += kv.second * kv.second;
+            norm = std::sqrt(norm);
+        }
+        if (norm > 0.0)
+            for (auto &kv : bow) kv.second /= norm;
+    }
+    int i = 0;
+    for (auto &kv : bow) { bow_words[i] = kv.first; bow_values[i] = kv.second; ++i; }
+    *n_bow = i;
+    int j = 0, t = 0;
+    for (auto &kv : fv) {
+        fv_nodes[j] = kv.first;
+        for (int x : kv.second) fv_features[t++] = x;
+        fv_offsets[++j] = t;
+    }
+    *n_fv = j;
+    return nwords;
 }

@@ -151,6 +151,36 @@ int   orbo_search_by_bow(int variant, const orbo_keypoint *ka, const uint8_t *da
                          float nnratio, int check_ori, const float *tri, int nlevels,
                          int32_t *match_a, int32_t *match_b);
 
+/* DBoW2 TemplatedVocabulary<FORB>::transform(features, BowVector&,
+ * FeatureVector&, levelsup) (TemplatedVocabulary.h:1140-1207, per feature
+ * :1231-1272; BowVector::addWeight / addIfNotExist / normalize
+ * BowVector.cpp; FeatureVector::addFeature FeatureVector.cpp:31-45).  The
+ * vocabulary is given as loadFromTextFile / loadFromBinFile build it
+ * (TemplatedVocabulary.h:1351-1425, 1473-1547): node 0 is the root, nodes
+ * 1..n_nodes-1 in file order with parent (< own index), file leaf flag,
+ * 32-B descriptor (row 0 unused) and weight; children in file order; word ids
+ * in order of the leaf flags.  scoring / weighting are DBoW2's ScoringType /
+ * WeightingType values.  Outputs: the BowVector as ascending (word, value);
+ * the FeatureVector as ascending node ids with per-node feature lists (CSR,
+ * fv_offsets[n_fv] = total).  Optional per-feature word / weight / node
+ * (nullable).  A leaf shallower than L - levelsup leaves the reference's nid
+ * unset (undefined); here it is the leaf.  Returns the number of words
+ * (0 for an empty vocabulary: outputs cleared). */
+int   orbo_vocab_transform(int L, int scoring, int weighting, int n_nodes, const int32_t *parent,
+                           const uint8_t *is_leaf, const uint8_t *desc, const double *weight,
+                           const uint8_t *features, int n, int levelsup,
+                           uint32_t *bow_words, double *bow_values, int *n_bow,
+                           uint32_t *fv_nodes, int32_t *fv_offsets, int32_t *fv_features, int *n_fv,
+                           uint32_t *f_word, double *f_weight, uint32_t *f_node);
+/* The same with the tree built once (CPU-baseline timing). */
+void *orbo_vocab_prepare(int n_nodes, const int32_t *parent, const uint8_t *is_leaf);
+void  orbo_vocab_release(void *tree);
+int   orbo_vocab_transform_prepared(void *tree, int L, int scoring, int weighting, const uint8_t *desc,
+                                    const double *weight, const uint8_t *features, int n, int levelsup,
+                                    uint32_t *bow_words, double *bow_values, int *n_bow,
+                                    uint32_t *fv_nodes, int32_t *fv_offsets, int32_t *fv_features, int *n_fv,
+                                    uint32_t *f_word, double *f_weight, uint32_t *f_node);
+
 #ifdef __cplusplus
 }
 #endif

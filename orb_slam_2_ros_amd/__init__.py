@@ -2,7 +2,8 @@
 
 The hot path of wjjcdy/orb_slam_2_ros (ORBextractor: pyramid, per-cell FAST-9,
 quadtree distribution, orientation, rBRIEF; ORBmatcher::SearchForInitialization;
-Frame's stereo / RGB-D depth association)
+Frame's stereo / RGB-D depth association; the other ORBmatcher searches; the
+DBoW2 vocabulary transform)
 as hand-written HIP kernels for gfx950 behind a C ABI (include/orbx.h,
 liborbx.so), with host mirrors of the reference's classes.
 """
@@ -10,6 +11,7 @@ from ._lib import KEYPOINT_DTYPE, OrbxError, load  # noqa: F401
 from .extractor import ORBextractor  # noqa: F401
 from .matcher import Frame, ORBmatcher  # noqa: F401
 from .depth import compute_stereo_matches, stereo_from_rgbd  # noqa: F401
+from .vocabulary import ORBVocabulary  # noqa: F401
 
 __all__ = ["KEYPOINT_DTYPE", "OrbxError", "load", "ORBextractor", "ORBmatcher", "Frame",
-           "compute_stereo_matches", "stereo_from_rgbd"]
+           "compute_stereo_matches", "stereo_from_rgbd", "ORBVocabulary"]

@@ -99,6 +99,13 @@ _SIGNATURES = {
     "orbx_descriptor_distance": (I32, [P, P]),
     "orbx_search_for_initialization": (I32, [I32, P, P, I32, P, P, I32, I32, I32, P, P, I32, F32, I32, P]),
     "orbx_debug_trig": (I32, [I32, P, P, P, I32, P, P, P, I32]),
+    "orbx_vocab_create": (I32, [I32, I32, I32, I32, I32, I32, P, P, P, P, P]),
+    "orbx_vocab_load": (I32, [I32, ctypes.c_char_p, I32, P]),
+    "orbx_vocab_destroy": (None, [P]),
+    "orbx_vocab_info": (I32, [P, P, P, P, P, P, P]),
+    "orbx_vocab_export": (I32, [P, P, P, P, P, I32]),
+    "orbx_vocab_transform": (I32, [P, P, I32, I32, P, P, P, P, P, P, P]),
+    "orbx_vocab_transform_device": (I32, [P, P, I32, I32, P, P, P, P]),
 }
 
 EXPORTED = tuple(_SIGNATURES)

@@ -154,6 +154,21 @@ hipError_t launch_rgbd(const orbx_keypoint *kps, const orbx_keypoint *kun, const
 hipError_t launch_proj(const ProjBufs &a, hipStream_t s);
 bool proj_fits(int n);   // the frame's grid fits the search kernel's LDS
 hipError_t launch_bow(const BowBufs &a, hipStream_t s);
+
+// DBoW2 vocabulary in slot order: the children of a node occupy consecutive
+// slots (root = slot 0).  16 B per slot + 32-B descriptor + weight.
+struct VocabNode {
+    int32_t first;    // slot of the first child
+    int32_t nchild;   // 0: a leaf (DBoW2's isLeaf() = children.empty())
+    uint32_t word;    // word id (0 for a node without the file's leaf flag, as Node())
+    uint32_t id;      // node id (file order)
+};
+struct VocabDev {
+    const VocabNode *nodes; const uint8_t *desc; const double *weight;
+    int k;            // largest child count
+};
+hipError_t launch_vocab_transform(const VocabDev &v, const uint8_t *feat, int n, int nid_level, uint32_t *o_word,
+                                  double *o_weight, uint32_t *o_node, hipStream_t s);
 int match_lds_bytes(int n1cap, int n2cap, int maxq, int maxc);
 int quadtree_lds_bytes(int node_cap);
 bool resize_window_fits(const Plan &hp);

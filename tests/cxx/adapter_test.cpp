@@ -15,7 +15,12 @@
 //   adapter_test rgbd W H img.raw depth.raw mbf out.bin
 //        extracts the image and runs OrbxFrame::ComputeStereoFromRGBD:
 //        n, kps, desc, mvuRight, mvDepth.
+//   adapter_test vocab voc.txt feats.raw n levelsup out.bin
+//        OrbxVocabulary::loadFromTextFile + transform into std::map
+//        BowVector / FeatureVector: nb, (word u32, value f64) x nb, nf,
+//        (node u32, count i32, features i32 x count) x nf.
 #include <cstdio>
+#include <map>
 #include <fstream>
 #include <iostream>
 #include <string>
@@ -129,6 +134,36 @@ int main(int argc, char **argv) {
         put_kps(out, k, d);
         out.write(reinterpret_cast<const char *>(ur.data()), 4 * ur.size());
         out.write(reinterpret_cast<const char *>(dp.data()), 4 * dp.size());
+        return 0;
+    }
+    if (argc == 7 && std::string(argv[1]) == "vocab") {
+        OrbxVocabulary voc;
+        if (!voc.loadFromTextFile(argv[2])) return 3;
+        const int n = std::atoi(argv[4]), levelsup = std::atoi(argv[5]);
+        std::ifstream f(argv[3], std::ios::binary);
+        std::vector<cv::Mat> feats;
+        for (int i = 0; i < n; ++i) {
+            cv::Mat d(1, 32, CV_8U);
+            f.read(reinterpret_cast<char *>(d.data), 32);
+            feats.push_back(d);
+        }
+        std::map<unsigned int, double> bow;
+        std::map<unsigned int, std::vector<unsigned int>> fv;
+        voc.transform(feats, bow, fv, levelsup);
+        std::ofstream out(argv[6], std::ios::binary);
+        const int nb = (int)bow.size(), nf = (int)fv.size();
+        out.write(reinterpret_cast<const char *>(&nb), 4);
+        for (const auto &kv : bow) {
+            out.write(reinterpret_cast<const char *>(&kv.first), 4);
+            out.write(reinterpret_cast<const char *>(&kv.second), 8);
+        }
+        out.write(reinterpret_cast<const char *>(&nf), 4);
+        for (const auto &kv : fv) {
+            const int c = (int)kv.second.size();
+            out.write(reinterpret_cast<const char *>(&kv.first), 4);
+            out.write(reinterpret_cast<const char *>(&c), 4);
+            out.write(reinterpret_cast<const char *>(kv.second.data()), 4 * (std::streamsize)c);
+        }
         return 0;
     }
     if (argc != 7 || std::string(argv[1]) != "run") return 2;

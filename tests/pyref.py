@@ -666,3 +666,62 @@ def search_by_bow(variant, A, B, nnratio=0.6, check_ori=True, tri=None, nlevels=
                 ma[a] = -1
                 nm -= 1
     return nm, np.array(ma, np.int32), np.array(mb, np.int32)
+
+
+def vocab_transform(voc, features, levelsup=4):
+    """TemplatedVocabulary::transform (TemplatedVocabulary.h:1140-1272) with
+    the loaders' tree (children in file order, word ids in leaf-flag order),
+    restated independently for the oracle's KAT: (bow dict, fv dict)."""
+    n_nodes = len(voc["parent"])
+    children = [[] for _ in range(n_nodes)]
+    word_id = [0] * n_nodes
+    nw = 0
+    for i in range(1, n_nodes):
+        children[int(voc["parent"][i])].append(i)
+        if voc["is_leaf"][i]:
+            word_id[i] = nw
+            nw += 1
+    if nw == 0:
+        return {}, {}
+    scoring, weighting = int(voc["scoring"]), int(voc["weighting"])
+    must = scoring != 5
+    nid_level = int(voc["L"]) - levelsup
+    bow, fv = {}, {}
+    for f, fd in enumerate(np.asarray(features, np.uint8).reshape(-1, 32)):
+        nid = 0 if nid_level <= 0 else None
+        node, level = 0, 0
+        while children[node]:
+            level += 1
+            kids = children[node]
+            best, best_d = kids[0], hamming(fd, voc["desc"][kids[0]])
+            for c in kids[1:]:
+                d = hamming(fd, voc["desc"][c])
+                if d < best_d:
+                    best, best_d = c, d
+            node = best
+            if level == nid_level:
+                nid = node
+        if nid is None:
+            nid = node
+        w = float(voc["weight"][node])
+        if w > 0:
+            wid = word_id[node]
+            if weighting in (0, 1):
+                bow[wid] = bow[wid] + w if wid in bow else w
+            elif wid not in bow:
+                bow[wid] = w
+            fv.setdefault(nid, []).append(f)
+    bow = dict(sorted(bow.items()))
+    if weighting in (0, 1) and bow and not must:
+        nd = float(len(bow))
+        bow = {k: v / nd for k, v in bow.items()}
+    if must:
+        if scoring == 1:
+            norm = math.sqrt(sum(v * v for v in bow.values()))
+        else:
+            norm = 0.0
+            for v in bow.values():
+                norm += abs(v)
+        if norm > 0:
+            bow = {k: v / norm for k, v in bow.items()}
+    return bow, dict(sorted(fv.items()))

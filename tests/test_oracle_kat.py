@@ -281,3 +281,33 @@ def test_search_by_sim3_vs_python(oracle_mod):
     want = np.array([i2 if i2 >= 0 and m2[i2] == i1 else -1 for i1, i2 in enumerate(m1)], np.int32)
     assert nf == int((want >= 0).sum()) and nf > 30
     assert np.array_equal(m, want)
+
+
+@pytest.mark.parametrize("irregular", [False, True])
+@pytest.mark.parametrize("scoring,weighting", [(0, 0), (1, 1), (5, 0), (5, 2), (0, 3), (2, 1)])
+@pytest.mark.parametrize("levelsup", [0, 2, 4, 9])
+def test_vocab_transform_vs_python(irregular, scoring, weighting, levelsup, oracle_mod):
+    """DBoW2 transform: the oracle against an independent restatement, on
+    small synthetic trees (regular and with early leaves), every weighting and
+    normalisation path, FeatureVector levels from the root to the leaves."""
+    from orb_slam_2_ros_amd.synth_vocab import features_near_leaves, make_vocab
+    voc = make_vocab(k=6 if irregular else 5, L=4, seed=3 + irregular, irregular=irregular, stop_frac=0.1,
+                     scoring=scoring, weighting=weighting)
+    feats = features_near_leaves(voc, 300, seed=7)
+    feats[5] = feats[4]                                  # repeated words
+    bow, fv, _ = oracle_mod.vocab_transform(voc, feats, levelsup)
+    pbow, pfv = pyref.vocab_transform(voc, feats, levelsup)
+    assert list(bow) == list(pbow) and list(fv) == list(pfv)
+    assert all(bow[k] == pbow[k] for k in bow)           # bit-exact doubles
+    assert fv == pfv
+    assert len(bow) > 10
+
+
+def test_vocab_transform_empty_oracle(oracle_mod):
+    from orb_slam_2_ros_amd.synth_vocab import make_vocab
+    voc = make_vocab(k=4, L=2, seed=1)
+    bow, fv, _ = oracle_mod.vocab_transform(voc, np.zeros((0, 32), np.uint8), 1)
+    assert bow == {} and fv == {}
+    voc["is_leaf"][:] = 0                                # no words: empty()
+    bow, fv, _ = oracle_mod.vocab_transform(voc, np.ones((3, 32), np.uint8), 1)
+    assert bow == {} and fv == {}
