@@ -350,6 +350,47 @@ int orbx_vocab_transform(orbx_vocab *v, const uint8_t *desc, int n, int levelsup
 int orbx_vocab_transform_device(orbx_vocab *v, const uint8_t *d_desc, int n, int levelsup,
                                 uint32_t *d_word, double *d_weight, uint32_t *d_node, void *stream);
 
+/* ---- per-frame neighbours ----
+ * The *_device forms run on `stream` (a hipStream_t; NULL = the current
+ * device's default stream) over device buffers; the others are synchronous
+ * over host buffers. */
+
+/* MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:288-361) for a batch of
+ * map points: point p's usable observation descriptors (the reference skips
+ * bad keyframes) are rows offsets[p] .. offsets[p+1]-1 of desc (32 B each,
+ * in the observation map's order; at most 65535 per point).  best[p] = the
+ * row (relative to offsets[p]) with the least median Hamming distance to the
+ * point's rows, the first on ties -- mDescriptor = that row; -1 when the
+ * point has none (the reference returns without change). */
+int orbx_distinctive_descriptors(int device, const uint8_t *desc, const int32_t *offsets, int npoints,
+                                 int32_t *best);
+int orbx_distinctive_descriptors_device(const uint8_t *d_desc, const int32_t *d_offsets, int npoints,
+                                        int32_t *d_best, void *stream);
+
+/* Frame::UndistortKeyPoints (Frame.cc:438-469): cv::undistortPoints(mK,
+ * mDistCoef, R = I, P = mK).  K: row-major 3x3 (mK, CV_32F); dist: k1 k2 p1
+ * p2 [k3 ...] (ncoef 4..8).  dist[0] == 0: a copy, as the reference.  Only
+ * pt.x / pt.y change. */
+int orbx_undistort_keypoints(int device, const orbx_keypoint *kps, int n, const float *K, const float *dist,
+                             int ncoef, orbx_keypoint *kps_un);
+/* The same on device (x, y) float pairs. */
+int orbx_undistort_points_device(const float *d_xy, int n, const float *K, const float *dist, int ncoef,
+                                 float *d_xy_un, void *stream);
+
+/* cv::cvtColor(CV_RGB2GRAY / CV_BGR2GRAY / CV_RGBA2GRAY / CV_BGRA2GRAY) of
+ * 8-bit images (Tracking.cc:179-264): channels 3 or 4, rgb 1 when the first
+ * channel is red (mbRGB). */
+int orbx_cvt_gray(int device, const uint8_t *src, int width, int height, size_t pitch, int channels, int rgb,
+                  uint8_t *dst, size_t dst_pitch);
+int orbx_cvt_gray_device(const uint8_t *d_src, int64_t src_frame_stride, int src_pitch, int channels, int rgb,
+                         int width, int height, int batch, uint8_t *d_dst, int64_t dst_frame_stride,
+                         int dst_pitch, void *stream);
+/* imDepth.convertTo(imDepth, CV_32F, mDepthMapFactor) of 16-bit depth
+ * (Tracking.cc:228-229): dst = (float)src * scale. */
+int orbx_depth_to_float_device(const uint16_t *d_src, int64_t src_frame_stride, int src_pitch, int width,
+                               int height, int batch, float scale, float *d_dst, int64_t dst_frame_stride,
+                               int dst_pitch, void *stream);
+
 /* Device evaluation of the restated sincosf / fastAtan2 (test hook). */
 int orbx_debug_trig(int device, const float *angles, float *s, float *c, int n,
                     const float *ys, const float *xs, float *atan_deg, int m);

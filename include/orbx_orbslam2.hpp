@@ -12,6 +12,7 @@
 // link liborbx.so.  The types are OpenCV's; nothing here includes HIP.
 #pragma once
 
+#include <algorithm>
 #include <cassert>
 #include <cstdint>
 #include <cstdlib>
@@ -267,6 +268,59 @@ struct OrbxFrame {
                                                  imDepth.ptr<float>(), imDepth.cols, imDepth.rows, imDepth.step,
                                                  mbf, mvuRight.data(), mvDepth.data(), &kept),
                            "ComputeStereoFromRGBD");
+    }
+};
+
+// The per-frame neighbours as free functions over the members
+// they read and write (INTEGRATION.md shows the one-line forwarders).
+struct OrbxFrameAux {
+    // Frame::UndistortKeyPoints (Frame.cc:438-469); mK CV_32F 3x3, mDistCoef
+    // CV_32F 4x1 or 5x1.
+    static void UndistortKeyPoints(const std::vector<cv::KeyPoint> &mvKeys, const cv::Mat &mK,
+                                   const cv::Mat &mDistCoef, std::vector<cv::KeyPoint> &mvKeysUn) {
+        assert(mK.type() == CV_32F && mDistCoef.type() == CV_32F);
+        const std::vector<orbx_keypoint> k = orbx_detail::pack(mvKeys);
+        std::vector<orbx_keypoint> ku(k.size());
+        float K[9], D[8];
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) K[3 * r + c] = mK.at<float>(r, c);
+        const int nc = std::min(mDistCoef.rows * mDistCoef.cols, 8);
+        for (int i = 0; i < nc; ++i) D[i] = mDistCoef.ptr<float>(0)[i];
+        orbx_detail::check(orbx_undistort_keypoints(orbx_detail::device_index(), k.data(), (int)k.size(), K, D, nc,
+                                                    ku.data()),
+                           "UndistortKeyPoints");
+        mvKeysUn = mvKeys;
+        for (size_t i = 0; i < ku.size(); ++i) { mvKeysUn[i].pt.x = ku[i].x; mvKeysUn[i].pt.y = ku[i].y; }
+    }
+
+    // MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:288-361) for a batch
+    // of map points: vvDescriptors[p] = point p's usable observation rows (1x32
+    // CV_8U), in its observation order.  Returns each point's chosen row (-1:
+    // none, mDescriptor unchanged).
+    static std::vector<int> DistinctiveDescriptors(const std::vector<std::vector<cv::Mat>> &vvDescriptors) {
+        std::vector<int32_t> off(vvDescriptors.size() + 1, 0);
+        for (size_t p = 0; p < vvDescriptors.size(); ++p) off[p + 1] = off[p] + (int32_t)vvDescriptors[p].size();
+        std::vector<uint8_t> desc(32 * (size_t)off.back());
+        size_t r = 0;
+        for (const auto &v : vvDescriptors)
+            for (const cv::Mat &d : v) std::memcpy(&desc[32 * r++], d.ptr<uint8_t>(), 32);
+        std::vector<int32_t> best(vvDescriptors.size(), -1);
+        orbx_detail::check(orbx_distinctive_descriptors(orbx_detail::device_index(), desc.data(), off.data(),
+                                                        (int)vvDescriptors.size(), best.data()),
+                           "ComputeDistinctiveDescriptors");
+        return std::vector<int>(best.begin(), best.end());
+    }
+
+    // Tracking::GrabImage* colour conversion (Tracking.cc:179-264): 3- or
+    // 4-channel 8-bit input to gray in place; other input is left as is.
+    static void ToGray(cv::Mat &im, bool mbRGB) {
+        const int cn = im.channels();
+        if (cn != 3 && cn != 4) return;
+        cv::Mat gray(im.rows, im.cols, CV_8U);
+        orbx_detail::check(orbx_cvt_gray(orbx_detail::device_index(), im.data, im.cols, im.rows, im.step, cn,
+                                         mbRGB ? 1 : 0, gray.data, gray.step),
+                           "cvtColor");
+        im = gray;
     }
 };
 

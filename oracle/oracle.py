@@ -351,3 +351,49 @@ class PreparedVocab:
             lib().orbo_vocab_release(self.h)
         except Exception:
             pass
+
+
+def distinctive_descriptors(desc, offsets):
+    f = lib().orbo_distinctive_descriptors
+    f.restype = None
+    f.argtypes = [P, P, I32, P]
+    desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    offsets = np.ascontiguousarray(offsets, np.int32)
+    npts = len(offsets) - 1
+    best = np.full(max(npts, 1), -1, np.int32)
+    f(_p(desc), _p(offsets), npts, _p(best))
+    return best[:npts]
+
+
+def undistort_points(xy, K, dist):
+    f = lib().orbo_undistort_points
+    f.restype = None
+    f.argtypes = [P, I32, P, P, I32, P]
+    xy = np.ascontiguousarray(xy, np.float32).reshape(-1, 2)
+    K = np.ascontiguousarray(K, np.float32).reshape(9)
+    dist = np.ascontiguousarray(dist, np.float32).reshape(-1)
+    out = np.empty_like(xy)
+    f(_p(xy), len(xy), _p(K), _p(dist), len(dist), _p(out))
+    return out
+
+
+def cvt_gray(img, rgb=True):
+    f = lib().orbo_cvt_gray
+    f.restype = None
+    f.argtypes = [P, I32, I32, SZ, I32, I32, P, SZ]
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w, cn = img.shape
+    out = np.empty((h, w), np.uint8)
+    f(_p(img), w, h, w * cn, cn, int(bool(rgb)), _p(out), w)
+    return out
+
+
+def depth_to_float(d16, scale):
+    f = lib().orbo_depth_to_float
+    f.restype = None
+    f.argtypes = [P, I32, I32, SZ, F32, P, SZ]
+    d16 = np.ascontiguousarray(d16, np.uint16)
+    h, w = d16.shape
+    out = np.empty((h, w), np.float32)
+    f(_p(d16), w, h, 2 * w, float(scale), _p(out), 4 * w)
+    return out

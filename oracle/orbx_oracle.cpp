@@ -1330,3 +1330,85 @@ int orbo_vocab_transform_prepared(void *tree, int L, int scoring, int weighting,
     *n_fv = j;
     return nwords;
 }
+
+// ---------------------------------------------------------------------------
+// MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:288-361).
+void orbo_distinctive_descriptors(const uint8_t *desc, const int32_t *offsets, int np, int32_t *best) {
+    for (int p = 0; p < np; ++p) {
+        const int o = offsets[p];
+        const size_t N = (size_t)(offsets[p + 1] - o);
+        if (N == 0) { best[p] = -1; continue; }
+        std::vector<float> D(N * N);
+        for (size_t i = 0; i < N; i++) {
+            D[i * N + i] = 0;
+            for (size_t j = i + 1; j < N; j++) {
+                const int distij = hamming32(desc + 32 * (size_t)(o + i), desc + 32 * (size_t)(o + j));
+                D[i * N + j] = (float)distij;
+                D[j * N + i] = (float)distij;
+            }
+        }
+        int BestMedian = INT_MAX, BestIdx = 0;
+        for (size_t i = 0; i < N; i++) {
+            std::vector<int> v(D.begin() + i * N, D.begin() + (i + 1) * N);
+            std::sort(v.begin(), v.end());
+            const int median = v[(size_t)(0.5 * (N - 1))];
+            if (median < BestMedian) { BestMedian = median; BestIdx = (int)i; }
+        }
+        best[p] = BestIdx;
+    }
+}
+
+// cv::undistortPoints (OpenCV 3.2 cvUndistortPoints, modules/imgproc/src/
+// undistort.cpp) with R = I and P = K, as Frame::UndistortKeyPoints calls it.
+void orbo_undistort_points(const float *xy_in, int n, const float *K, const float *dist, int ncoef, float *xy_out) {
+    if (dist[0] == 0.0f) {   // Frame.cc:441: mvKeysUn = mvKeys
+        std::memcpy(xy_out, xy_in, sizeof(float) * 2 * (size_t)n);
+        return;
+    }
+    double k[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < ncoef && i < 8; ++i) k[i] = dist[i];
+    const double fx = K[0], fy = K[4], cx = K[2], cy = K[5];
+    const double ifx = 1. / fx, ify = 1. / fy;
+    // RR = P * I = K (cvMatMul of exact 0/1 entries)
+    const double RR[3][3] = {{K[0], K[1], K[2]}, {K[3], K[4], K[5]}, {K[6], K[7], K[8]}};
+    for (int i = 0; i < n; i++) {
+        double x = xy_in[2 * i], y = xy_in[2 * i + 1], x0, y0;
+        x0 = x = (x - cx) * ifx;
+        y0 = y = (y - cy) * ify;
+        for (int j = 0; j < 5; j++) {
+            const double r2 = x * x + y * y;
+            const double icdist = (1 + ((k[7] * r2 + k[6]) * r2 + k[5]) * r2) / (1 + ((k[4] * r2 + k[1]) * r2 + k[0]) * r2);
+            const double deltaX = 2 * k[2] * x * y + k[3] * (r2 + 2 * x * x);
+            const double deltaY = k[2] * (r2 + 2 * y * y) + 2 * k[3] * x * y;
+            x = (x0 - deltaX) * icdist;
+            y = (y0 - deltaY) * icdist;
+        }
+        const double xx = RR[0][0] * x + RR[0][1] * y + RR[0][2];
+        const double yy = RR[1][0] * x + RR[1][1] * y + RR[1][2];
+        const double ww = 1. / (RR[2][0] * x + RR[2][1] * y + RR[2][2]);
+        xy_out[2 * i] = (float)(xx * ww);
+        xy_out[2 * i + 1] = (float)(yy * ww);
+    }
+}
+
+// cvtColor *2GRAY for 8U (OpenCV 3.2 RGB2Gray<uchar>: 14-bit fixed point).
+void orbo_cvt_gray(const uint8_t *src, int w, int h, size_t spitch, int channels, int rgb, uint8_t *dst,
+                   size_t dpitch) {
+    const int R2Y = 4899, G2Y = 9617, B2Y = 1868, shift = 14;
+    const int bidx = rgb ? 2 : 0;
+    for (int y = 0; y < h; ++y)
+        for (int x = 0; x < w; ++x) {
+            const uint8_t *s = src + y * spitch + (size_t)x * channels;
+            dst[y * dpitch + x] =
+                (uint8_t)((s[bidx] * B2Y + s[1] * G2Y + s[bidx ^ 2] * R2Y + (1 << (shift - 1))) >> shift);
+        }
+}
+
+// Mat::convertTo(CV_32F, scale) from 16U.
+void orbo_depth_to_float(const uint16_t *src, int w, int h, size_t spitch, float scale, float *dst, size_t dpitch) {
+    for (int y = 0; y < h; ++y) {
+        const uint16_t *s = reinterpret_cast<const uint16_t *>(reinterpret_cast<const uint8_t *>(src) + y * spitch);
+        float *d = reinterpret_cast<float *>(reinterpret_cast<uint8_t *>(dst) + y * dpitch);
+        for (int x = 0; x < w; ++x) d[x] = (float)s[x] * scale;
+    }
+}

@@ -181,6 +181,29 @@ int   orbo_vocab_transform_prepared(void *tree, int L, int scoring, int weightin
                                     uint32_t *fv_nodes, int32_t *fv_offsets, int32_t *fv_features, int *n_fv,
                                     uint32_t *f_word, double *f_weight, uint32_t *f_node);
 
+/* ---- per-frame neighbours ---- */
+/* MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:288-361) for np
+ * points: point p's observation descriptors are rows offsets[p] ..
+ * offsets[p+1]-1 of desc.  best[p] = the index (within the point's rows) of
+ * the descriptor with the least median distance to the others (first on
+ * ties), -1 for a point without descriptors. */
+void  orbo_distinctive_descriptors(const uint8_t *desc, const int32_t *offsets, int np, int32_t *best);
+/* Frame::UndistortKeyPoints (Frame.cc:438-469): cv::undistortPoints(K, D,
+ * R = I, P = K) as OpenCV 3.2 computes it in double (5 fixed iterations;
+ * coefficients k1 k2 p1 p2 [k3], ncoef 4 or 5).  k1 == 0: a plain copy.
+ * xy in / out: n (x, y) float pairs. */
+void  orbo_undistort_points(const float *xy_in, int n, const float *K /* row-major 3x3 */,
+                            const float *dist, int ncoef, float *xy_out);
+/* cv::cvtColor(CV_RGB2GRAY / BGR2GRAY / RGBA2GRAY / BGRA2GRAY) for 8U
+ * (Tracking.cc:179-264): 14-bit fixed point, coefficients 4899 (R), 9617 (G),
+ * 1868 (B), rounding 1 << 13.  channels 3 or 4; rgb 1 = R first. */
+void  orbo_cvt_gray(const uint8_t *src, int w, int h, size_t spitch, int channels, int rgb,
+                    uint8_t *dst, size_t dpitch);
+/* Mat::convertTo(CV_32F, scale) of a 16U depth image (Tracking.cc:228-229):
+ * dst = (float)src * scale in float. */
+void  orbo_depth_to_float(const uint16_t *src, int w, int h, size_t spitch, float scale, float *dst,
+                          size_t dpitch);
+
 #ifdef __cplusplus
 }
 #endif

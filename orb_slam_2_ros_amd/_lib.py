@@ -106,6 +106,13 @@ _SIGNATURES = {
     "orbx_vocab_export": (I32, [P, P, P, P, P, I32]),
     "orbx_vocab_transform": (I32, [P, P, I32, I32, P, P, P, P, P, P, P]),
     "orbx_vocab_transform_device": (I32, [P, P, I32, I32, P, P, P, P]),
+    "orbx_distinctive_descriptors": (I32, [I32, P, P, I32, P]),
+    "orbx_distinctive_descriptors_device": (I32, [P, P, I32, P, P]),
+    "orbx_undistort_keypoints": (I32, [I32, P, I32, P, P, I32, P]),
+    "orbx_undistort_points_device": (I32, [P, I32, P, P, I32, P, P]),
+    "orbx_cvt_gray": (I32, [I32, P, I32, I32, SZ, I32, I32, P, SZ]),
+    "orbx_cvt_gray_device": (I32, [P, I64, I32, I32, I32, I32, I32, I32, P, I64, I32, P]),
+    "orbx_depth_to_float_device": (I32, [P, I64, I32, I32, I32, I32, F32, P, I64, I32, P]),
 }
 
 EXPORTED = tuple(_SIGNATURES)

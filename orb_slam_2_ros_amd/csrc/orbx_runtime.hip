@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "orbx_device.h"
+#include "orbx_ws.h"
 
 using namespace orbx;
 
@@ -43,64 +44,6 @@ int popcount32(uint32_t v) {
     v = v - ((v >> 1) & 0x55555555u);
     v = (v & 0x33333333u) + ((v >> 2) & 0x33333333u);
     return (int)((((v + (v >> 4)) & 0xF0F0F0Fu) * 0x1010101u) >> 24);
-}
-
-// Workspace of the synchronous host entry points (the drop-in matchers and
-// depth calls): per device one grow-only device arena, one pinned staging
-// arena, a stream and a mutex -- the reference calls its matchers from the
-// Tracking, LocalMapping and LoopClosing threads concurrently.  A call packs
-// its inputs into the staging arena, moves them with one copy, runs, and
-// brings every output back with one copy.
-struct CallWs {
-    std::mutex mu;
-    hipStream_t st = nullptr;
-    uint8_t *dev = nullptr, *host = nullptr;
-    size_t cap = 0;
-    int64_t proj_pool = 0;   // projection candidate-list entries the last calls needed
-};
-
-CallWs &call_ws(int device) {
-    static CallWs ws[64];
-    return ws[device & 63];
-}
-
-struct Layout {
-    size_t size = 0;
-    size_t add(size_t bytes) {
-        const size_t o = size;
-        size += (bytes + 255) & ~size_t(255);
-        return o;
-    }
-};
-
-// Ensures stream and capacity (caller holds ws.mu and has set the device).
-int ws_reserve(CallWs &ws, size_t bytes) {
-    if (!ws.st && hipStreamCreateWithFlags(&ws.st, hipStreamNonBlocking) != hipSuccess) return ORBX_EIO;
-    if (ws.cap >= bytes) return ORBX_OK;
-    (void)hipStreamSynchronize(ws.st);
-    if (ws.dev) (void)hipFree(ws.dev);
-    if (ws.host) (void)hipHostFree(ws.host);
-    ws.dev = ws.host = nullptr;
-    ws.cap = 0;
-    const size_t cap = std::max(bytes, size_t(1) << 20) * 3 / 2;
-    if (hipMalloc(reinterpret_cast<void **>(&ws.dev), cap) != hipSuccess) return ORBX_ENOMEM;
-    if (hipHostMalloc(reinterpret_cast<void **>(&ws.host), cap, hipHostMallocDefault) != hipSuccess) {
-        (void)hipFree(ws.dev);
-        ws.dev = nullptr;
-        return ORBX_ENOMEM;
-    }
-    ws.cap = cap;
-    return ORBX_OK;
-}
-
-template <typename T>
-T *at(uint8_t *base, size_t off) { return reinterpret_cast<T *>(base + off); }
-
-void put(CallWs &ws, size_t off, const void *src, size_t bytes) {
-    if (bytes && src) std::memcpy(ws.host + off, src, bytes);
-}
-void get(CallWs &ws, size_t off, void *dst, size_t bytes) {
-    if (bytes && dst) std::memcpy(dst, ws.host + off, bytes);
 }
 
 }  // namespace

@@ -19,7 +19,12 @@
 //        OrbxVocabulary::loadFromTextFile + transform into std::map
 //        BowVector / FeatureVector: nb, (word u32, value f64) x nb, nf,
 //        (node u32, count i32, features i32 x count) x nf.
+//   adapter_test aux W H rgb.raw kps.bin out.bin
+//        OrbxFrameAux::ToGray (3-channel RGB image) and UndistortKeyPoints
+//        (TUM1 camera) of the keypoints file (n, then n x 28 B): writes the
+//        gray image (W x H) and the undistorted (x, y) pairs.
 #include <cstdio>
+#include <cstring>
 #include <map>
 #include <fstream>
 #include <iostream>
@@ -163,6 +168,38 @@ int main(int argc, char **argv) {
             out.write(reinterpret_cast<const char *>(&kv.first), 4);
             out.write(reinterpret_cast<const char *>(&c), 4);
             out.write(reinterpret_cast<const char *>(kv.second.data()), 4 * (std::streamsize)c);
+        }
+        return 0;
+    }
+    if (argc == 7 && std::string(argv[1]) == "aux") {
+        const int w = std::atoi(argv[2]), h = std::atoi(argv[3]);
+        cv::Mat im(h, w, CV_8UC3);
+        std::ifstream fi(argv[4], std::ios::binary);
+        fi.read(reinterpret_cast<char *>(im.data), (std::streamsize)w * h * 3);
+        OrbxFrameAux::ToGray(im, true);
+        std::ifstream fk(argv[5], std::ios::binary);
+        int n = 0;
+        fk.read(reinterpret_cast<char *>(&n), 4);
+        std::vector<cv::KeyPoint> kps(n);
+        for (auto &k : kps) {
+            float f[5];
+            int i[2];
+            fk.read(reinterpret_cast<char *>(f), 20);
+            fk.read(reinterpret_cast<char *>(i), 8);
+            k = cv::KeyPoint(cv::Point2f(f[0], f[1]), f[2], f[3], f[4], i[0], i[1]);
+        }
+        cv::Mat K(3, 3, CV_32F), D(5, 1, CV_32F);
+        const float kv[9] = {517.306408f, 0, 318.643040f, 0, 516.469215f, 255.313989f, 0, 0, 1};
+        const float dv[5] = {0.262383f, -0.953104f, -0.005358f, 0.002628f, 1.163314f};
+        std::memcpy(K.data, kv, sizeof(kv));
+        std::memcpy(D.data, dv, sizeof(dv));
+        std::vector<cv::KeyPoint> un;
+        OrbxFrameAux::UndistortKeyPoints(kps, K, D, un);
+        std::ofstream out(argv[6], std::ios::binary);
+        out.write(reinterpret_cast<const char *>(im.data), (std::streamsize)w * h);
+        for (const auto &k : un) {
+            out.write(reinterpret_cast<const char *>(&k.pt.x), 4);
+            out.write(reinterpret_cast<const char *>(&k.pt.y), 4);
         }
         return 0;
     }

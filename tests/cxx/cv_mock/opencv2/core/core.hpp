@@ -10,6 +10,8 @@
 
 #define CV_8U 0
 #define CV_8UC1 0
+#define CV_8UC3 16
+#define CV_8UC4 24
 #define CV_32F 5
 
 namespace cv {
@@ -42,7 +44,8 @@ public:
     std::shared_ptr<std::vector<uint8_t>> buf;
     Mat() = default;
     Mat(int r, int c, int t) { create(r, c, t); }
-    size_t elemSize() const { return type_ == CV_32F ? 4 : 1; }
+    size_t elemSize() const { return type_ == CV_32F ? 4 : (size_t)channels(); }
+    int channels() const { return type_ == CV_32F ? 1 : (type_ >> 3) + 1; }
     void create(int r, int c, int t) {
         if (rows == r && cols == c && type_ == t && data) return;
         type_ = t;

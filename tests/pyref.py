@@ -725,3 +725,52 @@ def vocab_transform(voc, features, levelsup=4):
         if norm > 0:
             bow = {k: v / norm for k, v in bow.items()}
     return bow, dict(sorted(fv.items()))
+
+
+def distinctive_descriptors(desc, offsets):
+    """MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:288-361) per point."""
+    out = []
+    for p in range(len(offsets) - 1):
+        rows = desc[offsets[p]:offsets[p + 1]]
+        N = len(rows)
+        if N == 0:
+            out.append(-1)
+            continue
+        D = [[0] * N for _ in range(N)]
+        for i in range(N):
+            for j in range(i + 1, N):
+                D[i][j] = D[j][i] = hamming(rows[i], rows[j])
+        best_med, best_idx = 2 ** 31 - 1, 0
+        for i in range(N):
+            med = sorted(D[i])[int(0.5 * (N - 1))]
+            if med < best_med:
+                best_med, best_idx = med, i
+        out.append(best_idx)
+    return np.array(out, np.int32)
+
+
+def undistort_points(xy, K, dist):
+    """cv::undistortPoints(K, D, R=I, P=K) in Python doubles, OpenCV 3.2 order."""
+    K = [float(v) for v in np.asarray(K, np.float32).reshape(9)]
+    d = [float(v) for v in np.asarray(dist, np.float32).reshape(-1)]
+    if d[0] == 0.0:
+        return np.asarray(xy, np.float32).copy()
+    k = (d + [0.0] * 8)[:8]
+    fx, fy, cx, cy = K[0], K[4], K[2], K[5]
+    ifx, ify = 1.0 / fx, 1.0 / fy
+    out = np.empty((len(xy), 2), np.float32)
+    for i, (u, v) in enumerate(np.asarray(xy, np.float32)):
+        x = x0 = (float(u) - cx) * ifx
+        y = y0 = (float(v) - cy) * ify
+        for _ in range(5):
+            r2 = x * x + y * y
+            icdist = (1 + ((k[7] * r2 + k[6]) * r2 + k[5]) * r2) / (1 + ((k[4] * r2 + k[1]) * r2 + k[0]) * r2)
+            dx = 2 * k[2] * x * y + k[3] * (r2 + 2 * x * x)
+            dy = k[2] * (r2 + 2 * y * y) + 2 * k[3] * x * y
+            x = (x0 - dx) * icdist
+            y = (y0 - dy) * icdist
+        xx = K[0] * x + K[1] * y + K[2]
+        yy = K[3] * x + K[4] * y + K[5]
+        ww = 1.0 / (K[6] * x + K[7] * y + K[8])
+        out[i] = (np.float32(xx * ww), np.float32(yy * ww))
+    return out

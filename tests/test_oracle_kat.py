@@ -311,3 +311,66 @@ def test_vocab_transform_empty_oracle(oracle_mod):
     voc["is_leaf"][:] = 0                                # no words: empty()
     bow, fv, _ = oracle_mod.vocab_transform(voc, np.ones((3, 32), np.uint8), 1)
     assert bow == {} and fv == {}
+
+
+def _obs_descs(seed, npts, maxn):
+    rng = np.random.default_rng(seed)
+    sizes = rng.integers(0, maxn + 1, npts)
+    sizes[0] = 0
+    sizes[1] = 1
+    offsets = np.zeros(npts + 1, np.int32)
+    offsets[1:] = np.cumsum(sizes)
+    base = rng.integers(0, 256, (npts, 32)).astype(np.uint8)
+    desc = np.repeat(base, sizes, axis=0)
+    noise = (rng.integers(0, 256, desc.shape) & rng.integers(0, 256, desc.shape)
+             & rng.integers(0, 256, desc.shape)).astype(np.uint8)
+    desc ^= noise
+    dup = rng.random(len(desc)) < 0.1                       # repeated rows: median ties
+    desc[dup] = desc[np.maximum(np.nonzero(dup)[0] - 1, 0)]
+    return desc, offsets
+
+
+def test_distinctive_descriptors_vs_python(oracle_mod):
+    desc, offsets = _obs_descs(3, 60, 25)
+    assert np.array_equal(oracle_mod.distinctive_descriptors(desc, offsets),
+                          pyref.distinctive_descriptors(desc, offsets))
+
+
+CAMERAS = {   # fx fy cx cy, k1 k2 p1 p2 [k3]: TUM1 / EuRoC / KITTI-like settings files
+    "tum1": ((517.306408, 516.469215, 318.643040, 255.313989), (0.262383, -0.953104, -0.005358, 0.002628, 1.163314)),
+    "euroc": ((458.654, 457.296, 367.215, 248.375), (-0.28340811, 0.07395907, 0.00019359, 1.76187114e-05)),
+    "none": ((718.856, 718.856, 607.1928, 185.2157), (0.0, 0.0, 0.0, 0.0)),
+}
+
+
+def _K(c):
+    fx, fy, cx, cy = c
+    return np.array([[fx, 0, cx], [0, fy, cy], [0, 0, 1]], np.float32)
+
+
+@pytest.mark.parametrize("cam", sorted(CAMERAS))
+def test_undistort_vs_python(cam, oracle_mod):
+    c, d = CAMERAS[cam]
+    rng = np.random.default_rng(4)
+    xy = np.stack([rng.uniform(0, 752, 400), rng.uniform(0, 480, 400)], 1).astype(np.float32)
+    o = oracle_mod.undistort_points(xy, _K(c), d)
+    p = pyref.undistort_points(xy, _K(c), d)
+    assert np.array_equal(o.view(np.uint32), p.view(np.uint32))
+    if cam == "none":
+        assert np.array_equal(o, xy)
+    else:
+        assert np.abs(o - xy).max() > 1.0
+
+
+def test_cvt_gray_and_depth_oracle(oracle_mod):
+    rng = np.random.default_rng(5)
+    img = rng.integers(0, 256, (37, 53, 4)).astype(np.uint8)
+    i32 = img.astype(np.int64)
+    for cn in (3, 4):
+        for rgb in (True, False):
+            r, b = (i32[..., 0], i32[..., 2]) if rgb else (i32[..., 2], i32[..., 0])
+            ref = ((r * 4899 + i32[..., 1] * 9617 + b * 1868 + 8192) >> 14).astype(np.uint8)
+            assert np.array_equal(oracle_mod.cvt_gray(img[..., :cn], rgb), ref)
+    d16 = rng.integers(0, 65536, (21, 33)).astype(np.uint16)
+    scale = np.float32(1.0) / np.float32(5000.0)
+    assert np.array_equal(oracle_mod.depth_to_float(d16, scale), d16.astype(np.float32) * scale)
