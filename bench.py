@@ -231,6 +231,57 @@ def bow_transform_throughput(torch, frames=512, nfeat=1000, reps=20):
             "cpu_ms_per_frame": round(cpu_ms, 4), "cpu_kind": "port, 1 thread, tree prebuilt"}
 
 
+def kfdb_latency(n_kf=10000, words=1000, reps=10):
+    """KeyFrameDatabase::DetectLoopCandidates over a 10,000-keyframe database
+    (64 streams x ~150 keyframes; synthetic BowVectors of 1,000 words of a
+    1M-word vocabulary), GPU vs the oracle's literal inverted-file walk."""
+    from oracle import oracle
+    from orb_slam_2_ros_amd.keyframe_db import KeyFrameDatabase
+    from orb_slam_2_ros_amd.synth_vocab import make_keyframe_bows
+    bows, covis = make_keyframe_bows(n_kf=n_kf + reps, n_words=1000000, words_per_kf=words, seed=11, loop_every=500)
+    g, o = KeyFrameDatabase(), oracle.KeyFrameDB(1000000)
+    for i in range(n_kf):
+        g.add(i, *bows[i])
+        o.add(i, *bows[i])
+    cv = lambda k: covis.get(k, [])   # noqa: E731
+    tg, to = [], []
+    for r in range(reps):
+        q = n_kf + r
+        t0 = time.perf_counter()
+        a = g.DetectLoopCandidates(q, *bows[q], covis[q], 0.01, cv)
+        tg.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        b = o.detect(False, q, *bows[q], covis[q], 0.01, cv)
+        to.append(time.perf_counter() - t0)
+        assert a == b
+    return {"keyframes": n_kf, "words_per_keyframe": words, "gpu_ms": round(1e3 * float(np.median(tg)), 4),
+            "cpu_ms": round(1e3 * float(np.median(to)), 4), "cpu_kind": "port, 1 thread, inverted file"}
+
+
+def keyframe_exchange(torch, dist, world, dev, kfs_per_rank=8, nkp=1000, reps=10):
+    """The C5 cross-stream keyframe all-gather: every
+    rank publishes kfs_per_rank new keyframes (BowVector of ~nkp words,
+    nkp keypoints + descriptors) and receives everyone's, over RCCL."""
+    from orb_slam_2_ros_amd import KEYPOINT_DTYPE
+    from orb_slam_2_ros_amd.keyframe_db import all_gather_keyframes
+    rng = np.random.default_rng(dist.get_rank() if world > 1 else 0)
+    recs = []
+    for i in range(kfs_per_rank):
+        recs.append({"kf_id": i, "words": np.sort(rng.choice(1000000, nkp, replace=False)).astype(np.uint32),
+                     "values": rng.random(nkp), "keys": np.zeros(nkp, KEYPOINT_DTYPE),
+                     "desc": rng.integers(0, 256, (nkp, 32)).astype(np.uint8)})
+    all_gather_keyframes(recs, dist, dev)
+    ts = []
+    for _ in range(reps):
+        dist.barrier()
+        t0 = time.perf_counter()
+        got = all_gather_keyframes(recs, dist, dev)
+        ts.append(time.perf_counter() - t0)
+    assert len(got) == world * kfs_per_rank
+    return {"ranks": world, "keyframes_per_rank": kfs_per_rank, "bytes_per_rank": int(sum(
+        12 * len(r["words"]) + 60 * len(r["keys"]) + 16 for r in recs)), "ms": round(1e3 * float(np.median(ts)), 4)}
+
+
 def _resident_frames(mode, w, h, batch, rank):
     """Host array [FRAMES_PER_STREAM, frames_per_step, h, w] (+ depth maps for RGB-D)."""
     from orb_slam_2_ros_amd import synth
@@ -352,6 +403,8 @@ def main() -> int:
                            "streams_per_gpu": eb, "nfeatures": enf, "stage_ms": st2,
                            "kps_last_frame": nk2, ("matches" if mode == "mono" else "depths") + "_last_frame": sane2}
 
+    exchange = keyframe_exchange(torch, dist, world, dev) if (world > 1 and not args.no_extras) else None
+
     if rank == 0:
         sizes = level_geometry(w, h, nf)
         names = ["resize", "blur", "fast", "quadtree", "describe", "match"]
@@ -378,6 +431,9 @@ def main() -> int:
         matchers = matcher_latencies() if (world == 1 and not args.no_extras) else None
         if world == 1 and not args.no_extras:
             extras["bow_transform_orbvoc"] = bow_transform_throughput(torch)
+            extras["keyframe_db_loop_query"] = kfdb_latency()
+        if exchange is not None:
+            extras["keyframe_all_gather"] = exchange
         line = {
             "metric": METRIC,
             "value": round(value, 2),

@@ -391,6 +391,41 @@ int orbx_depth_to_float_device(const uint16_t *d_src, int64_t src_frame_stride, 
                                int height, int batch, float scale, float *d_dst, int64_t dst_frame_stride,
                                int dst_pitch, void *stream);
 
+/* ---- keyframe database ----
+ * KeyFrameDatabase (KeyFrameDatabase.cc:31-236) over keyframes named by 64-bit
+ * ids, BowVectors as ascending (word, value) arrays (orbx_vocab_transform's
+ * output).  The per-keyframe query state of the reference (mnLoopQuery,
+ * mnLoopWords, mLoopScore, mnRelocQuery, mnRelocWords, mRelocScore) lives in
+ * the database and persists across queries, erase and re-add; the scores the
+ * reference leaves uninitialised start at 0.  Scoring is L1 (ORBvoc's
+ * L1_NORM).  Covisibility (KeyFrame::GetBestCovisibilityKeyFrames(10)) comes
+ * from the caller's callback, which writes up to cap ids and returns the
+ * count. */
+typedef struct orbx_kfdb orbx_kfdb;
+typedef int (*orbx_covis_fn)(void *ctx, uint64_t kf_id, uint64_t *out, int cap);
+int orbx_kfdb_create(int device, orbx_kfdb **out);
+void orbx_kfdb_destroy(orbx_kfdb *db);
+/* add (:37-44) / erase (:46-67) / clear (:69-73).  Adding an id that is in the
+ * database is ORBX_EINVAL (the reference would list it twice). */
+int orbx_kfdb_add(orbx_kfdb *db, uint64_t kf_id, const uint32_t *words, const double *values, int n);
+int orbx_kfdb_erase(orbx_kfdb *db, uint64_t kf_id);
+int orbx_kfdb_clear(orbx_kfdb *db);
+int orbx_kfdb_size(const orbx_kfdb *db);
+/* DetectLoopCandidates(pKF, minScore) (:76-236): query = pKF's id and
+ * BowVector, connected = pKF->GetConnectedKeyFrames().  out: candidate ids in
+ * the reference's order; ORBX_ERANGE (with *n_out) if cap is too small. */
+int orbx_kfdb_detect_loop_candidates(orbx_kfdb *db, uint64_t query_id, const uint32_t *words,
+                                     const double *values, int n, const uint64_t *connected, int n_connected,
+                                     float min_score, orbx_covis_fn covis, void *ctx, uint64_t *out, int cap,
+                                     int *n_out);
+/* DetectRelocalizationCandidates(F) (:238-330): frame id and BowVector. */
+int orbx_kfdb_detect_relocalization_candidates(orbx_kfdb *db, uint64_t frame_id, const uint32_t *words,
+                                               const double *values, int n, orbx_covis_fn covis, void *ctx,
+                                               uint64_t *out, int cap, int *n_out);
+/* L1Scoring::score (ScoringObject.cpp:23-66), host. */
+int orbx_bow_score_l1(const uint32_t *w1, const double *v1, int n1, const uint32_t *w2, const double *v2, int n2,
+                      double *score);
+
 /* Device evaluation of the restated sincosf / fastAtan2 (test hook). */
 int orbx_debug_trig(int device, const float *angles, float *s, float *c, int n,
                     const float *ys, const float *xs, float *atan_deg, int m);

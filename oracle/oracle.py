@@ -397,3 +397,69 @@ def depth_to_float(d16, scale):
     out = np.empty((h, w), np.float32)
     f(_p(d16), w, h, 2 * w, float(scale), _p(out), 4 * w)
     return out
+
+
+_COVIS = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
+                          ctypes.c_int)
+
+
+class KeyFrameDB:
+    """The oracle's literal KeyFrameDatabase (inverted lists, per-keyframe
+    query state)."""
+
+    def __init__(self, n_words):
+        l = lib()
+        l.orbo_kfdb_create.restype = P
+        l.orbo_kfdb_create.argtypes = [I32]
+        l.orbo_kfdb_destroy.restype = None
+        l.orbo_kfdb_destroy.argtypes = [P]
+        l.orbo_kfdb_add.restype = None
+        l.orbo_kfdb_add.argtypes = [P, ctypes.c_uint64, P, P, I32]
+        l.orbo_kfdb_erase.restype = None
+        l.orbo_kfdb_erase.argtypes = [P, ctypes.c_uint64]
+        l.orbo_kfdb_clear.restype = None
+        l.orbo_kfdb_clear.argtypes = [P]
+        l.orbo_kfdb_detect.restype = I32
+        l.orbo_kfdb_detect.argtypes = [P, I32, ctypes.c_uint64, P, P, I32, P, I32, F32, _COVIS, P, P, I32]
+        l.orbo_bow_score_l1.restype = ctypes.c_double
+        l.orbo_bow_score_l1.argtypes = [P, P, I32, P, P, I32]
+        self.h = l.orbo_kfdb_create(int(n_words))
+
+    def add(self, kf_id, words, values):
+        w = np.ascontiguousarray(words, np.uint32); v = np.ascontiguousarray(values, np.float64)
+        lib().orbo_kfdb_add(self.h, int(kf_id), _p(w), _p(v), len(w))
+
+    def erase(self, kf_id):
+        lib().orbo_kfdb_erase(self.h, int(kf_id))
+
+    def clear(self):
+        lib().orbo_kfdb_clear(self.h)
+
+    def detect(self, reloc, qid, words, values, connected, min_score, covis):
+        w = np.ascontiguousarray(words, np.uint32); v = np.ascontiguousarray(values, np.float64)
+        conn = np.ascontiguousarray(sorted(connected or []), np.uint64)
+
+        def cb(_c, kf, out, cap):
+            ids = list(covis(int(kf)))[:cap]
+            for i, k in enumerate(ids):
+                out[i] = int(k)
+            return len(ids)
+        fn = _COVIS(cb)
+        out = np.zeros(4096, np.uint64)
+        n = lib().orbo_kfdb_detect(self.h, int(reloc), int(qid), _p(w), _p(v), len(w), _p(conn), len(conn),
+                                   float(min_score), fn, None, _p(out), len(out))
+        return [int(x) for x in out[:n]]
+
+    def __del__(self):
+        try:
+            lib().orbo_kfdb_destroy(self.h)
+        except Exception:
+            pass
+
+
+def bow_score_l1(w1, v1, w2, v2):
+    lib().orbo_bow_score_l1.restype = ctypes.c_double
+    lib().orbo_bow_score_l1.argtypes = [P, P, I32, P, P, I32]
+    a = np.ascontiguousarray(w1, np.uint32); b = np.ascontiguousarray(v1, np.float64)
+    c = np.ascontiguousarray(w2, np.uint32); d = np.ascontiguousarray(v2, np.float64)
+    return lib().orbo_bow_score_l1(_p(a), _p(b), len(a), _p(c), _p(d), len(c))

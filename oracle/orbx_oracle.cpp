@@ -21,6 +21,8 @@
 #include <cstring>
 #include <list>
 #include <map>
+#include <set>
+#include <unordered_map>
 #include <vector>
 
 namespace {
@@ -1411,4 +1413,178 @@ void orbo_depth_to_float(const uint16_t *src, int w, int h, size_t spitch, float
         float *d = reinterpret_cast<float *>(reinterpret_cast<uint8_t *>(dst) + y * dpitch);
         for (int x = 0; x < w; ++x) d[x] = (float)s[x] * scale;
     }
+}
+
+// ---------------------------------------------------------------------------
+// KeyFrameDatabase (KeyFrameDatabase.cc:31-236) over named keyframes.
+namespace {
+struct OrboKF {
+    uint64_t id;
+    std::vector<uint32_t> words;
+    std::vector<double> values;
+    uint64_t mnLoopQuery = 0, mnRelocQuery = 0;   // KeyFrame.cc:41
+    int mnLoopWords = 0, mnRelocWords = 0;
+    float mLoopScore = 0, mRelocScore = 0;        // uninitialised in the reference
+};
+struct OrboKFDB {
+    std::vector<std::list<OrboKF *>> inv;
+    std::unordered_map<uint64_t, OrboKF *> kfs;
+    std::vector<OrboKF *> owned;
+};
+
+// L1Scoring::score (ScoringObject.cpp:23-66): merge with lower_bound jumps;
+// only common words add, in ascending word order.
+double l1_score(const uint32_t *w1, const double *v1, int n1, const uint32_t *w2, const double *v2, int n2) {
+    int i = 0, j = 0;
+    double score = 0;
+    while (i < n1 && j < n2) {
+        const double vi = v1[i], wi = v2[j];
+        if (w1[i] == w2[j]) {
+            score += std::fabs(vi - wi) - std::fabs(vi) - std::fabs(wi);
+            ++i;
+            ++j;
+        } else if (w1[i] < w2[j]) {
+            i = (int)(std::lower_bound(w1, w1 + n1, w2[j]) - w1);
+        } else {
+            j = (int)(std::lower_bound(w2, w2 + n2, w1[i]) - w2);
+        }
+    }
+    return -score / 2.0;
+}
+}  // namespace
+
+double orbo_bow_score_l1(const uint32_t *w1, const double *v1, int n1, const uint32_t *w2, const double *v2, int n2) {
+    return l1_score(w1, v1, n1, w2, v2, n2);
+}
+
+void *orbo_kfdb_create(int n_words) {
+    OrboKFDB *db = new OrboKFDB;
+    db->inv.resize(n_words);
+    return db;
+}
+
+void orbo_kfdb_destroy(void *p) {
+    OrboKFDB *db = static_cast<OrboKFDB *>(p);
+    for (OrboKF *k : db->owned) delete k;
+    delete db;
+}
+
+void orbo_kfdb_add(void *p, uint64_t kf_id, const uint32_t *words, const double *values, int n) {
+    OrboKFDB *db = static_cast<OrboKFDB *>(p);
+    OrboKF *k;
+    auto it = db->kfs.find(kf_id);
+    if (it != db->kfs.end()) {
+        k = it->second;
+    } else {
+        k = new OrboKF;
+        k->id = kf_id;
+        k->words.assign(words, words + n);
+        k->values.assign(values, values + n);
+        db->kfs[kf_id] = k;
+        db->owned.push_back(k);
+    }
+    for (int i = 0; i < n; ++i) db->inv[words[i]].push_back(k);
+}
+
+void orbo_kfdb_erase(void *p, uint64_t kf_id) {
+    OrboKFDB *db = static_cast<OrboKFDB *>(p);
+    auto it = db->kfs.find(kf_id);
+    if (it == db->kfs.end()) return;
+    OrboKF *k = it->second;
+    for (uint32_t w : k->words) {
+        std::list<OrboKF *> &l = db->inv[w];
+        for (auto lit = l.begin(); lit != l.end(); ++lit)
+            if (*lit == k) { l.erase(lit); break; }
+    }
+}
+
+void orbo_kfdb_clear(void *p) {
+    OrboKFDB *db = static_cast<OrboKFDB *>(p);
+    const size_t nw = db->inv.size();
+    db->inv.clear();
+    db->inv.resize(nw);
+}
+
+int orbo_kfdb_detect(void *p, int reloc, uint64_t qid, const uint32_t *words, const double *values, int n,
+                     const uint64_t *connected, int n_connected, float minScore, orbo_covis_fn covis, void *ctx,
+                     uint64_t *out, int cap) {
+    OrboKFDB *db = static_cast<OrboKFDB *>(p);
+    std::set<uint64_t> conn(connected, connected + (reloc ? 0 : n_connected));
+    std::list<OrboKF *> sharing;
+    for (int i = 0; i < n; ++i) {
+        for (OrboKF *k : db->inv[words[i]]) {
+            if (!reloc) {
+                if (k->mnLoopQuery != qid) {
+                    k->mnLoopWords = 0;
+                    if (!conn.count(k->id)) {
+                        k->mnLoopQuery = qid;
+                        sharing.push_back(k);
+                    }
+                }
+                k->mnLoopWords++;
+            } else {
+                if (k->mnRelocQuery != qid) {
+                    k->mnRelocWords = 0;
+                    k->mnRelocQuery = qid;
+                    sharing.push_back(k);
+                }
+                k->mnRelocWords++;
+            }
+        }
+    }
+    if (sharing.empty()) return 0;
+    int maxCommonWords = 0;
+    for (OrboKF *k : sharing) maxCommonWords = std::max(maxCommonWords, reloc ? k->mnRelocWords : k->mnLoopWords);
+    const int minCommonWords = maxCommonWords * 0.8f;
+    std::list<std::pair<float, OrboKF *>> scored;
+    for (OrboKF *k : sharing) {
+        if ((reloc ? k->mnRelocWords : k->mnLoopWords) > minCommonWords) {
+            const float si = (float)l1_score(words, values, n, k->words.data(), k->values.data(), (int)k->words.size());
+            if (reloc) {
+                k->mRelocScore = si;
+                scored.push_back(std::make_pair(si, k));
+            } else {
+                k->mLoopScore = si;
+                if (si >= minScore) scored.push_back(std::make_pair(si, k));
+            }
+        }
+    }
+    if (scored.empty()) return 0;
+    std::list<std::pair<float, OrboKF *>> acc;
+    float bestAccScore = reloc ? 0 : minScore;
+    uint64_t neigh[64];
+    for (auto &sm : scored) {
+        OrboKF *ki = sm.second;
+        const int nn = covis(ctx, ki->id, neigh, 10);
+        float bestScore = sm.first, accScore = sm.first;
+        OrboKF *best = ki;
+        for (int t = 0; t < nn; ++t) {
+            auto it = db->kfs.find(neigh[t]);
+            if (it == db->kfs.end()) continue;   // (a neighbour never added holds no query state)
+            OrboKF *k2 = it->second;
+            if (!reloc) {
+                if (k2->mnLoopQuery == qid && k2->mnLoopWords > minCommonWords) {
+                    accScore += k2->mLoopScore;
+                    if (k2->mLoopScore > bestScore) { best = k2; bestScore = k2->mLoopScore; }
+                }
+            } else {
+                if (k2->mnRelocQuery != qid) continue;
+                accScore += k2->mRelocScore;
+                if (k2->mRelocScore > bestScore) { best = k2; bestScore = k2->mRelocScore; }
+            }
+        }
+        acc.push_back(std::make_pair(accScore, best));
+        if (accScore > bestAccScore) bestAccScore = accScore;
+    }
+    const float minScoreToRetain = 0.75f * bestAccScore;
+    std::set<OrboKF *> added;
+    int m = 0;
+    for (auto &a : acc) {
+        if (a.first > minScoreToRetain && !added.count(a.second)) {
+            if (m < cap) out[m] = a.second->id;
+            ++m;
+            added.insert(a.second);
+        }
+    }
+    return m;
 }

@@ -204,6 +204,24 @@ void  orbo_cvt_gray(const uint8_t *src, int w, int h, size_t spitch, int channel
 void  orbo_depth_to_float(const uint16_t *src, int w, int h, size_t spitch, float scale, float *dst,
                           size_t dpitch);
 
+/* ---- keyframe database: KeyFrameDatabase.cc:31-236 restated
+ * literally -- inverted file of std::lists in add order, the per-keyframe
+ * query state (mnLoopQuery / mnLoopWords / mLoopScore and the reloc trio)
+ * persisting across queries, L1Scoring::score (ScoringObject.cpp:23-66).
+ * Keyframes are named by 64-bit ids; covisibility (GetBestCovisibilityKeyFrames
+ * (10)) comes from a callback.  Scores the reference leaves uninitialised
+ * start at 0 here. */
+typedef int (*orbo_covis_fn)(void *ctx, uint64_t kf_id, uint64_t *out, int cap);
+void *orbo_kfdb_create(int n_words);
+void  orbo_kfdb_destroy(void *db);
+void  orbo_kfdb_add(void *db, uint64_t kf_id, const uint32_t *words, const double *values, int n);
+void  orbo_kfdb_erase(void *db, uint64_t kf_id);
+void  orbo_kfdb_clear(void *db);
+int   orbo_kfdb_detect(void *db, int reloc, uint64_t query_id, const uint32_t *words, const double *values, int n,
+                       const uint64_t *connected, int n_connected, float min_score, orbo_covis_fn covis, void *ctx,
+                       uint64_t *out, int cap);
+double orbo_bow_score_l1(const uint32_t *w1, const double *v1, int n1, const uint32_t *w2, const double *v2, int n2);
+
 #ifdef __cplusplus
 }
 #endif

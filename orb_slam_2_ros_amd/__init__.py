@@ -13,7 +13,8 @@ from .matcher import Frame, ORBmatcher  # noqa: F401
 from .depth import compute_stereo_matches, stereo_from_rgbd  # noqa: F401
 from .vocabulary import ORBVocabulary  # noqa: F401
 from .frame_aux import compute_distinctive_descriptors, cvt_gray, undistort_keypoints  # noqa: F401
+from .keyframe_db import KeyFrameDatabase  # noqa: F401
 
 __all__ = ["KEYPOINT_DTYPE", "OrbxError", "load", "ORBextractor", "ORBmatcher", "Frame",
            "compute_stereo_matches", "stereo_from_rgbd", "ORBVocabulary",
-           "compute_distinctive_descriptors", "cvt_gray", "undistort_keypoints"]
+           "compute_distinctive_descriptors", "cvt_gray", "undistort_keypoints", "KeyFrameDatabase"]

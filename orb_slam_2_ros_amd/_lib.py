@@ -113,7 +113,20 @@ _SIGNATURES = {
     "orbx_cvt_gray": (I32, [I32, P, I32, I32, SZ, I32, I32, P, SZ]),
     "orbx_cvt_gray_device": (I32, [P, I64, I32, I32, I32, I32, I32, I32, P, I64, I32, P]),
     "orbx_depth_to_float_device": (I32, [P, I64, I32, I32, I32, I32, F32, P, I64, I32, P]),
+    "orbx_kfdb_create": (I32, [I32, P]),
+    "orbx_kfdb_destroy": (None, [P]),
+    "orbx_kfdb_add": (I32, [P, ctypes.c_uint64, P, P, I32]),
+    "orbx_kfdb_erase": (I32, [P, ctypes.c_uint64]),
+    "orbx_kfdb_clear": (I32, [P]),
+    "orbx_kfdb_size": (I32, [P]),
+    "orbx_kfdb_detect_loop_candidates": (I32, [P, ctypes.c_uint64, P, P, I32, P, I32, F32, P, P, P, I32, P]),
+    "orbx_kfdb_detect_relocalization_candidates": (I32, [P, ctypes.c_uint64, P, P, I32, P, P, P, I32, P]),
+    "orbx_bow_score_l1": (I32, [P, P, I32, P, P, I32, P]),
 }
+
+# orbx_covis_fn
+COVIS_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
+                            ctypes.c_int)
 
 EXPORTED = tuple(_SIGNATURES)
 

@@ -123,3 +123,28 @@ def write_binary(voc, path):
             f.write(struct.pack("<iB", int(voc["parent"][i]), int(voc["is_leaf"][i])))
             f.write(voc["desc"][i].tobytes())
             f.write(struct.pack("<d", float(voc["weight"][i])))
+
+
+def make_keyframe_bows(n_kf=300, n_words=100000, words_per_kf=500, seed=0, loop_every=60):
+    """Synthetic keyframe BowVectors along a trajectory with revisits: a
+    keyframe keeps ~70% of the previous one's words; every `loop_every`
+    keyframes the trajectory returns near an earlier place (a loop).  Values
+    are positive and L1-normalised (TF-IDF with L1 scoring).  Returns a list of
+    (words u32 ascending, values f64) and the covisibility order (each
+    keyframe's up-to-10 neighbours, nearest first)."""
+    rng = np.random.default_rng(seed)
+    bows = []
+    cur = np.sort(rng.choice(n_words, words_per_kf, replace=False))
+    for i in range(n_kf):
+        if i and i % loop_every == 0 and i > 2 * loop_every // 3:
+            j = int(rng.integers(0, i - loop_every // 2))
+            cur = bows[j][0].copy()                                # back at keyframe j's place
+        keep = cur[rng.random(len(cur)) < 0.7]
+        new = rng.choice(n_words, words_per_kf - len(keep), replace=False)
+        cur = np.unique(np.concatenate([keep, new]).astype(np.uint32))
+        vals = rng.uniform(0.1, 5.0, len(cur))
+        vals /= np.abs(vals).sum()
+        bows.append((cur.astype(np.uint32), vals))
+    covis = {i: [j for j in sorted(range(max(0, i - 5), min(n_kf, i + 6)), key=lambda j: (abs(j - i), j))
+                 if j != i][:10] for i in range(n_kf)}
+    return bows, covis

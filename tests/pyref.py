@@ -774,3 +774,90 @@ def undistort_points(xy, K, dist):
         ww = 1.0 / (K[6] * x + K[7] * y + K[8])
         out[i] = (np.float32(xx * ww), np.float32(yy * ww))
     return out
+
+
+def l1_score(w1, v1, w2, v2):
+    """L1Scoring::score (ScoringObject.cpp:23-66)."""
+    d2 = dict(zip((int(x) for x in w2), (float(x) for x in v2)))
+    s = 0.0
+    for w, vi in zip(w1, v1):
+        wi = d2.get(int(w))
+        if wi is not None:
+            vi = float(vi)
+            s += abs(vi - wi) - abs(vi) - abs(wi)
+    return -s / 2.0
+
+
+class KeyFrameDB:
+    """KeyFrameDatabase (KeyFrameDatabase.cc:31-330) restated literally in
+    Python: inverted lists in add order, per-keyframe query state."""
+
+    def __init__(self):
+        self.inv = {}
+        self.bow = {}
+        self.st = {}
+
+    def add(self, k, words, values):
+        self.bow[k] = (np.asarray(words), np.asarray(values))
+        self.st.setdefault(k, dict(lq=0, lw=0, ls=np.float32(0), rq=0, rw=0, rs=np.float32(0)))
+        for w in words:
+            self.inv.setdefault(int(w), []).append(k)
+
+    def erase(self, k):
+        for w in self.bow.get(k, ([], []))[0]:
+            lst = self.inv.get(int(w), [])
+            if k in lst:
+                lst.remove(k)
+
+    def detect(self, reloc, qid, words, values, connected, min_score, covis):
+        conn = set(connected or [])
+        sharing = []
+        q, wk, sk = ("rq", "rw", "rs") if reloc else ("lq", "lw", "ls")
+        for w in words:
+            for k in self.inv.get(int(w), []):
+                s = self.st[k]
+                if s[q] != qid:
+                    s[wk] = 0
+                    if reloc or k not in conn:
+                        s[q] = qid
+                        sharing.append(k)
+                s[wk] += 1
+        if not sharing:
+            return []
+        max_common = max(self.st[k][wk] for k in sharing)
+        min_common = int(np.float32(max_common) * np.float32(0.8))
+        scored = []
+        for k in sharing:
+            if self.st[k][wk] > min_common:
+                si = np.float32(l1_score(words, values, *self.bow[k]))
+                self.st[k][sk] = si
+                if reloc or si >= np.float32(min_score):
+                    scored.append((si, k))
+        if not scored:
+            return []
+        acc = []
+        best_acc = np.float32(0) if reloc else np.float32(min_score)
+        for si, k in scored:
+            best_s, acc_s, best_k = si, si, k
+            for k2 in list(covis(k))[:10]:
+                s2 = self.st.get(k2)
+                if s2 is None:
+                    continue
+                if reloc:
+                    if s2[q] != qid:
+                        continue
+                elif not (s2[q] == qid and s2[wk] > min_common):
+                    continue
+                acc_s = np.float32(acc_s + s2[sk])
+                if s2[sk] > best_s:
+                    best_k, best_s = k2, s2[sk]
+            acc.append((acc_s, best_k))
+            if acc_s > best_acc:
+                best_acc = acc_s
+        keep = np.float32(np.float32(0.75) * best_acc)
+        out, seen = [], set()
+        for a, k in acc:
+            if a > keep and k not in seen:
+                out.append(k)
+                seen.add(k)
+        return out

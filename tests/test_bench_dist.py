@@ -59,3 +59,34 @@ def test_timed_region_two_ranks_gloo():
         assert mx == pytest.approx(max(gathered))    # max over ranks, identical on both
         assert mx >= 6 * 0.02 * 0.9                  # bounded below by the slow rank's work
     assert res[0][2] == res[1][2]
+
+
+def _exchange_worker(rank, world, port, out):
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, str(ROOT))
+    import bench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    r = bench.keyframe_exchange(torch, dist, world, None, kfs_per_rank=2, nkp=50, reps=2)
+    dist.destroy_process_group()
+    out.put((rank, r))
+
+
+def test_keyframe_exchange_two_ranks_gloo():
+    """bench.keyframe_exchange (the C5 keyframe all-gather extra) runs on every
+    rank and each receives world x keyframes_per_rank keyframes."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(2):
+        assert res[r]["ranks"] == 2 and res[r]["keyframes_per_rank"] == 2 and res[r]["ms"] > 0

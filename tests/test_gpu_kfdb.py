@@ -1,0 +1,62 @@
+"""GPU keyframe database against the oracle's literal
+KeyFrameDatabase over a query script: loop and relocalisation candidates in
+the reference's order, with the per-keyframe query state carried across
+queries, an erase / re-add and a repeated query id."""
+import numpy as np
+import pytest
+
+from orb_slam_2_ros_amd.keyframe_db import KeyFrameDatabase, bow_score_l1
+
+pytestmark = pytest.mark.gpu
+
+
+def test_kfdb_bit_exact_vs_oracle(oracle_mod):
+    from test_oracle_kat import _kfdb_script, _run_kfdb
+    ops, covis = _kfdb_script()
+    o = _run_kfdb(oracle_mod.KeyFrameDB(20000), ops, covis,
+                  lambda db, r, q, w, v, c, m, cv: db.detect(r, q, w, v, c, m, cv))
+
+    def gdetect(db, r, q, w, v, c, m, cv):
+        return db.DetectRelocalizationCandidates(q, w, v, cv) if r else db.DetectLoopCandidates(q, w, v, c, m, cv)
+    g = _run_kfdb(KeyFrameDatabase(), ops, covis, gdetect)
+    assert g == o
+    assert sum(len(x) > 0 for x in g) > 10
+
+
+def test_kfdb_large_database(oracle_mod):
+    """2,000 keyframes of 1,000 words (past the LDS-staged query size only
+    for the query side cases below), a loop query per 100 keyframes."""
+    from orb_slam_2_ros_amd.synth_vocab import make_keyframe_bows
+    bows, covis = make_keyframe_bows(n_kf=2000, n_words=100000, words_per_kf=1000, seed=9, loop_every=150)
+    g, o = KeyFrameDatabase(), oracle_mod.KeyFrameDB(100000)
+    cv = lambda k: covis.get(k, [])   # noqa: E731
+    for i, (w, v) in enumerate(bows):
+        if i and i % 100 == 0:
+            a = g.DetectLoopCandidates(i, w, v, covis[i], 0.01, cv)
+            b = o.detect(False, i, w, v, covis[i], 0.01, cv)
+            assert a == b
+        g.add(i, w, v)
+        o.add(i, w, v)
+    # a query with more words than the kernels stage in LDS
+    w = np.unique(np.concatenate([bows[5][0], np.arange(50000, 60000, dtype=np.uint32)]))
+    v = np.full(len(w), 1.0 / len(w))
+    assert g.DetectRelocalizationCandidates(777777, w, v, cv) == o.detect(True, 777777, w, v, None, 0.0, cv)
+
+
+def test_bow_score_l1_host(oracle_mod):
+    from orb_slam_2_ros_amd.synth_vocab import make_keyframe_bows
+    bows, _ = make_keyframe_bows(n_kf=10, n_words=3000, words_per_kf=200, seed=3)
+    assert bow_score_l1(*bows[1], *bows[2]) == oracle_mod.bow_score_l1(*bows[1], *bows[2])
+
+
+def test_kfdb_add_rejects_duplicates():
+    from orb_slam_2_ros_amd import OrbxError
+    db = KeyFrameDatabase()
+    db.add(7, np.array([1, 5, 9], np.uint32), np.array([0.2, 0.3, 0.5]))
+    with pytest.raises(OrbxError):
+        db.add(7, np.array([1], np.uint32), np.array([1.0]))
+    with pytest.raises(OrbxError):   # words must ascend
+        db.add(8, np.array([5, 1], np.uint32), np.array([0.5, 0.5]))
+    db.erase(7)
+    db.add(7, np.array([2], np.uint32), np.array([1.0]))
+    assert db.size() == 1

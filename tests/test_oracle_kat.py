@@ -374,3 +374,56 @@ def test_cvt_gray_and_depth_oracle(oracle_mod):
     d16 = rng.integers(0, 65536, (21, 33)).astype(np.uint16)
     scale = np.float32(1.0) / np.float32(5000.0)
     assert np.array_equal(oracle_mod.depth_to_float(d16, scale), d16.astype(np.float32) * scale)
+
+
+def _kfdb_script():
+    """A query script over synthetic keyframes: add along the trajectory,
+    loop queries (connected = covisible neighbours), relocalisation queries,
+    an erase + re-add, and a repeated query id."""
+    from orb_slam_2_ros_amd.synth_vocab import make_keyframe_bows
+    bows, covis = make_keyframe_bows(n_kf=240, n_words=20000, words_per_kf=300, seed=5, loop_every=50)
+    ops = []
+    for i, (w, v) in enumerate(bows):
+        if i >= 20 and i % 7 == 0:
+            ops.append(("loop", i, w, v, covis[i], 0.01))
+        if i >= 20 and i % 11 == 0:
+            ops.append(("reloc", 10000 + i, w, v, None, 0.0))
+        ops.append(("add", i, w, v))
+        if i == 120:
+            ops.append(("erase", 60))
+        if i == 160:
+            ops.append(("add", 60, *bows[60]))
+        if i == 200:
+            ops.append(("loop", 196, w, v, covis[196], 0.005))   # a query id met before
+    return ops, covis
+
+
+def _run_kfdb(db, ops, covis, detect):
+    out = []
+    for op in ops:
+        if op[0] == "add":
+            db.add(op[1], op[2], op[3])
+        elif op[0] == "erase":
+            db.erase(op[1])
+        else:
+            kind, qid, w, v, conn, ms = op
+            out.append(detect(db, kind == "reloc", qid, w, v, conn, ms, lambda k: covis.get(k, [])))
+    return out
+
+
+def test_kfdb_oracle_vs_python(oracle_mod):
+    ops, covis = _kfdb_script()
+    o = _run_kfdb(oracle_mod.KeyFrameDB(20000), ops, covis,
+                  lambda db, r, q, w, v, c, m, cv: db.detect(r, q, w, v, c, m, cv))
+    p = _run_kfdb(pyref.KeyFrameDB(), ops, covis,
+                  lambda db, r, q, w, v, c, m, cv: db.detect(r, q, w, v, c, m, cv))
+    assert o == p
+    assert sum(len(x) > 0 for x in o) > 10
+
+
+def test_bow_score_l1_oracle(oracle_mod):
+    from orb_slam_2_ros_amd.synth_vocab import make_keyframe_bows
+    bows, _ = make_keyframe_bows(n_kf=30, n_words=3000, words_per_kf=200, seed=2)
+    for a in range(0, 30, 3):
+        for b in range(1, 30, 4):
+            assert oracle_mod.bow_score_l1(*bows[a], *bows[b]) == pyref.l1_score(*bows[a], *bows[b])
