@@ -258,6 +258,30 @@ def kfdb_latency(n_kf=10000, words=1000, reps=10):
             "cpu_ms": round(1e3 * float(np.median(to)), 4), "cpu_kind": "port, 1 thread, inverted file"}
 
 
+def local_ba_latency(reps=3):
+    """Optimizer::LocalBundleAdjustment (config C4, KITTI-like stereo: 20
+    local + 4 fixed keyframes, 3,000 map points, ~25k observations; 5 + 10 LM
+    iterations), GPU vs the oracle's single-thread restatement."""
+    from oracle import oracle
+    from orb_slam_2_ros_amd.optimizer import local_bundle_adjustment
+    from orb_slam_2_ros_amd.synth_ba import make_ba_problem
+    P = make_ba_problem(n_local=20, n_fixed=4, n_points=3000, seed=2)
+    args = (P["Tcw"], P["fixed"], P["Xw"], P["edges"])
+    local_bundle_adjustment(*args)
+    tg, to = [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        g = local_bundle_adjustment(*args)
+        tg.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        o = oracle.local_ba(*args)
+        to.append(time.perf_counter() - t0)
+    assert np.array_equal(g[0], o[0]) and np.array_equal(g[2], o[2])
+    return {"keyframes": 24, "points": 3000, "observations": int(len(P["edges"])), "lm_iterations": list(g[3]),
+            "gpu_ms": round(1e3 * float(np.median(tg)), 3), "cpu_ms": round(1e3 * float(np.median(to)), 3),
+            "cpu_kind": "port, 1 thread, same summation order"}
+
+
 def keyframe_exchange(torch, dist, world, dev, kfs_per_rank=8, nkp=1000, reps=10):
     """The C5 cross-stream keyframe all-gather: every
     rank publishes kfs_per_rank new keyframes (BowVector of ~nkp words,
@@ -432,6 +456,7 @@ def main() -> int:
         if world == 1 and not args.no_extras:
             extras["bow_transform_orbvoc"] = bow_transform_throughput(torch)
             extras["keyframe_db_loop_query"] = kfdb_latency()
+            extras["local_ba_kitti"] = local_ba_latency()
         if exchange is not None:
             extras["keyframe_all_gather"] = exchange
         line = {

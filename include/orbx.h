@@ -426,6 +426,39 @@ int orbx_kfdb_detect_relocalization_candidates(orbx_kfdb *db, uint64_t frame_id,
 int orbx_bow_score_l1(const uint32_t *w1, const double *v1, int n1, const uint32_t *w2, const double *v2, int n2,
                       double *score);
 
+/* ---- local bundle adjustment ----
+ * Optimizer::LocalBundleAdjustment (Optimizer.cc:517-900) on the graph the
+ * caller collected: cameras (local keyframes + fixed cameras) and local map
+ * points, one edge per observation.  Runs g2o's Levenberg-Marquardt over a
+ * 6/3 block solver with the Schur complement: iters1 iterations with Huber
+ * kernels (delta sqrt(5.991) mono, sqrt(7.815) stereo), then the outliers
+ * (chi2 > 5.991 / 7.815 or point behind the camera) leave, the kernels are
+ * dropped and iters2 more iterations run (the reference: 5 and 10). */
+typedef struct orbx_ba_edge {
+    int32_t cam, point;       /* indices into the camera / point arrays */
+    float u, v;               /* mvKeysUn[idx].pt */
+    float ur;                 /* mvuRight[idx]; < 0: monocular edge */
+    float inv_sigma2;         /* mvInvLevelSigma2[octave] */
+    float fx, fy, cx, cy, bf; /* the keyframe's intrinsics (bf stereo only) */
+} orbx_ba_edge;
+
+/* Tcw: ncam row-major 3x4 float poses (KeyFrame::GetPose()), fixed[c] != 0
+ * for fixed vertices (mnId == 0 and the fixed cameras); Xw: npt x 3 float
+ * (MapPoint::GetWorldPos()).  Out: Tcw_out / Xw_out as Converter::toCvMat
+ * casts them back; outlier[e] = the reference's final check (chi2 over the
+ * threshold or depth not positive: the observation is erased);
+ * iterations[2] (nullable) = LM iterations run per pass.  At most 170 free
+ * cameras.  Synchronous. */
+int orbx_local_ba(int device, const float *Tcw, const uint8_t *fixed, int ncam, const float *Xw, int npt,
+                  const orbx_ba_edge *edges, int ne, int iters1, int iters2, float *Tcw_out, float *Xw_out,
+                  uint8_t *outlier, int *iterations);
+/* One LM linear system of the first pass at the given lambda: x (6 per free
+ * camera, then 3 per point) and the robust chi2; *solved = 0 when the
+ * reduced system is not positive definite.  Test hook. */
+int orbx_ba_debug_step(int device, const float *Tcw, const uint8_t *fixed, int ncam, const float *Xw, int npt,
+                       const orbx_ba_edge *edges, int ne, int robust, double lambda, double *x_out,
+                       double *chi2_out, int *solved);
+
 /* Device evaluation of the restated sincosf / fastAtan2 (test hook). */
 int orbx_debug_trig(int device, const float *angles, float *s, float *c, int n,
                     const float *ys, const float *xs, float *atan_deg, int m);

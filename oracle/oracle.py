@@ -463,3 +463,36 @@ def bow_score_l1(w1, v1, w2, v2):
     a = np.ascontiguousarray(w1, np.uint32); b = np.ascontiguousarray(v1, np.float64)
     c = np.ascontiguousarray(w2, np.uint32); d = np.ascontiguousarray(v2, np.float64)
     return lib().orbo_bow_score_l1(_p(a), _p(b), len(a), _p(c), _p(d), len(c))
+
+
+def local_ba(Tcw, fixed, Xw, edges, iters=(5, 10)):
+    from orb_slam_2_ros_amd.synth_ba import BA_EDGE_DTYPE
+    f = lib().orbo_local_ba
+    f.restype = I32
+    f.argtypes = [P, P, I32, P, I32, P, I32, I32, I32, P, P, P, P]
+    T = np.ascontiguousarray(Tcw, np.float32).reshape(-1, 3, 4)
+    F = np.ascontiguousarray(fixed, np.uint8)
+    X = np.ascontiguousarray(Xw, np.float32).reshape(-1, 3)
+    E = np.ascontiguousarray(edges, BA_EDGE_DTYPE)
+    To, Xo = np.empty_like(T), np.empty_like(X)
+    out = np.zeros(max(len(E), 1), np.uint8)
+    its = np.zeros(2, np.int32)
+    f(_p(T), _p(F), len(T), _p(X), len(X), _p(E), len(E), int(iters[0]), int(iters[1]), _p(To), _p(Xo), _p(out),
+      _p(its))
+    return To, Xo, out[:len(E)].astype(bool), (int(its[0]), int(its[1]))
+
+
+def ba_debug_step(Tcw, fixed, Xw, edges, robust=True, lam=1e-3):
+    from orb_slam_2_ros_amd.synth_ba import BA_EDGE_DTYPE
+    f = lib().orbo_ba_debug_step
+    f.restype = I32
+    f.argtypes = [P, P, I32, P, I32, P, I32, I32, ctypes.c_double, P, P]
+    T = np.ascontiguousarray(Tcw, np.float32).reshape(-1, 3, 4)
+    F = np.ascontiguousarray(fixed, np.uint8)
+    X = np.ascontiguousarray(Xw, np.float32).reshape(-1, 3)
+    E = np.ascontiguousarray(edges, BA_EDGE_DTYPE)
+    n = 6 * int((F == 0).sum()) + 3 * len(X)
+    x = np.zeros(max(n, 1), np.float64)
+    chi2 = ctypes.c_double(0)
+    ok = f(_p(T), _p(F), len(T), _p(X), len(X), _p(E), len(E), int(robust), float(lam), _p(x), ctypes.byref(chi2))
+    return x[:n], chi2.value, bool(ok)

@@ -1588,3 +1588,518 @@ int orbo_kfdb_detect(void *p, int reloc, uint64_t qid, const uint32_t *words, co
     }
     return m;
 }
+
+// ---------------------------------------------------------------------------
+// Local bundle adjustment (Optimizer.cc:517-900 over g2o).
+namespace {
+struct BQ { double q[4], t[3]; int f; };   // SE3Quat (x y z w), free index or -1
+
+void bq_rot(const double *q, const double *v, double *o) {   // Eigen _transformVector
+    double uv[3] = {q[1] * v[2] - q[2] * v[1], q[2] * v[0] - q[0] * v[2], q[0] * v[1] - q[1] * v[0]};
+    for (int i = 0; i < 3; ++i) uv[i] = uv[i] + uv[i];
+    const double c[3] = {q[1] * uv[2] - q[2] * uv[1], q[2] * uv[0] - q[0] * uv[2], q[0] * uv[1] - q[1] * uv[0]};
+    for (int i = 0; i < 3; ++i) o[i] = v[i] + q[3] * uv[i] + c[i];
+}
+void bq_R(const double *q, double *R) {   // toRotationMatrix
+    const double tx = 2 * q[0], ty = 2 * q[1], tz = 2 * q[2];
+    const double twx = tx * q[3], twy = ty * q[3], twz = tz * q[3];
+    const double txx = tx * q[0], txy = ty * q[0], txz = tz * q[0];
+    const double tyy = ty * q[1], tyz = tz * q[1], tzz = tz * q[2];
+    const double r[9] = {1 - (tyy + tzz), txy - twz, txz + twy, txy + twz, 1 - (txx + tzz), tyz - twx,
+                         txz - twy, tyz + twx, 1 - (txx + tyy)};
+    std::memcpy(R, r, sizeof(r));
+}
+void bq_fromR(const double *m, double *q) {   // Quaternion(Matrix3d)
+    const double tr = m[0] + m[4] + m[8];
+    if (tr > 0) {
+        double t = std::sqrt(tr + 1.0);
+        q[3] = 0.5 * t;
+        t = 0.5 / t;
+        q[0] = (m[7] - m[5]) * t;
+        q[1] = (m[2] - m[6]) * t;
+        q[2] = (m[3] - m[1]) * t;
+    } else {
+        int i = 0;
+        if (m[4] > m[0]) i = 1;
+        if (m[8] > m[3 * i + i]) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        double t = std::sqrt(m[3 * i + i] - m[3 * j + j] - m[3 * k + k] + 1.0);
+        q[i] = 0.5 * t;
+        t = 0.5 / t;
+        q[3] = (m[3 * k + j] - m[3 * j + k]) * t;
+        q[j] = (m[3 * j + i] + m[3 * i + j]) * t;
+        q[k] = (m[3 * k + i] + m[3 * i + k]) * t;
+    }
+}
+void bq_norm(double *q) {   // normalizeRotation
+    if (q[3] < 0)
+        for (int i = 0; i < 4; ++i) q[i] *= -1;
+    const double n = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    for (int i = 0; i < 4; ++i) q[i] = q[i] / n;
+}
+void bq_mul(const double *a, const double *b, double *o) {
+    o[3] = a[3] * b[3] - a[0] * b[0] - a[1] * b[1] - a[2] * b[2];
+    o[0] = a[3] * b[0] + a[0] * b[3] + a[1] * b[2] - a[2] * b[1];
+    o[1] = a[3] * b[1] + a[1] * b[3] + a[2] * b[0] - a[0] * b[2];
+    o[2] = a[3] * b[2] + a[2] * b[3] + a[0] * b[1] - a[1] * b[0];
+}
+
+struct OBA {
+    int ncam, npt, ne, nf;
+    std::vector<BQ> T;
+    std::vector<double> X;
+    const orbo_ba_edge *E;
+    std::vector<double> delta, err, chi2, rho0, rho1;
+    std::vector<uint8_t> act, front;
+    std::vector<std::vector<int>> pe;     // edges per point, by camera
+    std::vector<std::vector<int>> ce;     // edges per free camera, edge order
+    // system
+    std::vector<double> Hpp, bp, Hll, bl, hpp_e, hll_e, hpl_e, bp_e, bl_e, x;
+    bool robust = true;
+
+    void proj(int e, double *p) const {
+        const BQ &t = T[E[e].cam];
+        bq_rot(t.q, &X[3 * (size_t)E[e].point], p);
+        for (int i = 0; i < 3; ++i) p[i] = p[i] + t.t[i];
+    }
+    void fronts() {   // isDepthPositive() at the current estimate, errors untouched
+        for (int e = 0; e < ne; ++e) {
+            double p[3];
+            proj(e, p);
+            front[e] = p[2] > 0.0;
+        }
+    }
+    double errors() {
+        double s = 0;
+        for (int e = 0; e < ne; ++e) {
+            double p[3];
+            proj(e, p);
+            front[e] = p[2] > 0.0;
+            if (!act[e]) continue;
+            const orbo_ba_edge &d = E[e];
+            const bool st = d.ur >= 0;
+            double r[3];
+            if (!st) {
+                const double u = p[0] / p[2], v = p[1] / p[2];
+                r[0] = (double)d.u - (u * (double)d.fx + (double)d.cx);
+                r[1] = (double)d.v - (v * (double)d.fy + (double)d.cy);
+                r[2] = 0;
+            } else {
+                const double invz = (double)(float)(1.0 / p[2]);
+                const double r0 = p[0] * invz * (double)d.fx + (double)d.cx;
+                const double r1 = p[1] * invz * (double)d.fy + (double)d.cy;
+                r[0] = (double)d.u - r0;
+                r[1] = (double)d.v - r1;
+                r[2] = (double)d.ur - (r0 - (double)d.bf * invz);
+            }
+            const double om = d.inv_sigma2;
+            double c = 0;
+            for (int k = 0; k < (st ? 3 : 2); ++k) c = c + r[k] * (om * r[k]);
+            double a0 = c, a1 = 1.0;
+            if (robust) {
+                const double dsqr = delta[e] * delta[e];
+                if (!(c <= dsqr)) {
+                    const double sq = std::sqrt(c);
+                    a0 = 2 * sq * delta[e] - dsqr;
+                    a1 = delta[e] / sq;
+                }
+            }
+            for (int k = 0; k < 3; ++k) err[3 * (size_t)e + k] = r[k];
+            chi2[e] = c;
+            rho0[e] = a0;
+            rho1[e] = a1;
+            s += a0;
+        }
+        return s;
+    }
+    void linearize(int e) {
+        const orbo_ba_edge &d = E[e];
+        const bool st = d.ur >= 0;
+        const double fx = d.fx, fy = d.fy, bf = d.bf;
+        double p[3];
+        proj(e, p);
+        const double x = p[0], y = p[1], z = p[2], z_2 = z * z;
+        double R[9];
+        bq_R(T[d.cam].q, R);
+        double A[3][3], B[3][6];
+        if (!st) {
+            const double tmp[2][3] = {{fx, 0, -x / z * fx}, {0, fy, -y / z * fy}};
+            const double s = -1. / z;
+            for (int r = 0; r < 2; ++r)
+                for (int c = 0; c < 3; ++c) {
+                    double acc = 0;
+                    for (int k = 0; k < 3; ++k) acc = acc + (s * tmp[r][k]) * R[3 * k + c];
+                    A[r][c] = acc;
+                }
+        } else {
+            for (int c = 0; c < 3; ++c) {
+                A[0][c] = -fx * R[c] / z + fx * x * R[6 + c] / z_2;
+                A[1][c] = -fy * R[3 + c] / z + fy * y * R[6 + c] / z_2;
+                A[2][c] = A[0][c] - bf * R[6 + c] / z_2;
+            }
+        }
+        B[0][0] = x * y / z_2 * fx; B[0][1] = -(1 + (x * x / z_2)) * fx; B[0][2] = y / z * fx;
+        B[0][3] = -1. / z * fx; B[0][4] = 0; B[0][5] = x / z_2 * fx;
+        B[1][0] = (1 + y * y / z_2) * fy; B[1][1] = -x * y / z_2 * fy; B[1][2] = -x / z * fy;
+        B[1][3] = 0; B[1][4] = -1. / z * fy; B[1][5] = y / z_2 * fy;
+        if (st) {
+            B[2][0] = B[0][0] - bf * y / z_2; B[2][1] = B[0][1] + bf * x / z_2; B[2][2] = B[0][2];
+            B[2][3] = B[0][3]; B[2][4] = 0; B[2][5] = B[0][5] - bf / z_2;
+        }
+        const int D = st ? 3 : 2;
+        const double w = rho1[e] * (double)d.inv_sigma2;
+        double omr[3];
+        for (int k = 0; k < D; ++k) omr[k] = -((double)d.inv_sigma2 * err[3 * (size_t)e + k]) * rho1[e];
+        const bool pf = T[d.cam].f >= 0;
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) {
+                double acc = 0;
+                for (int k = 0; k < D; ++k) acc = acc + (A[k][a] * w) * A[k][b];
+                hll_e[9 * (size_t)e + 3 * a + b] = acc;
+            }
+        for (int a = 0; a < 6; ++a) {
+            for (int b = 0; b < 6; ++b) {
+                double acc = 0;
+                if (pf)
+                    for (int k = 0; k < D; ++k) acc = acc + (B[k][a] * w) * B[k][b];
+                hpp_e[36 * (size_t)e + 6 * a + b] = acc;
+            }
+            for (int c = 0; c < 3; ++c) {
+                double acc = 0;
+                if (pf)
+                    for (int k = 0; k < D; ++k) acc = acc + (A[k][c] * w) * B[k][a];
+                hpl_e[18 * (size_t)e + 3 * a + c] = acc;
+            }
+            double acc = 0;
+            if (pf)
+                for (int k = 0; k < D; ++k) acc = acc + B[k][a] * omr[k];
+            bp_e[6 * (size_t)e + a] = acc;
+        }
+        for (int c = 0; c < 3; ++c) {
+            double acc = 0;
+            for (int k = 0; k < D; ++k) acc = acc + A[k][c] * omr[k];
+            bl_e[3 * (size_t)e + c] = acc;
+        }
+    }
+    void build() {
+        for (int e = 0; e < ne; ++e)
+            if (act[e]) linearize(e);
+        Hpp.assign(36 * (size_t)nf, 0); bp.assign(6 * (size_t)nf, 0);
+        Hll.assign(9 * (size_t)npt, 0); bl.assign(3 * (size_t)npt, 0);
+        for (int f = 0; f < nf; ++f)
+            for (int e : ce[f]) {
+                if (!act[e]) continue;
+                for (int k = 0; k < 36; ++k) Hpp[36 * (size_t)f + k] = Hpp[36 * (size_t)f + k] + hpp_e[36 * (size_t)e + k];
+                for (int k = 0; k < 6; ++k) bp[6 * (size_t)f + k] = bp[6 * (size_t)f + k] + bp_e[6 * (size_t)e + k];
+            }
+        for (int p = 0; p < npt; ++p)
+            for (int e : pe[p]) {
+                if (!act[e]) continue;
+                for (int k = 0; k < 9; ++k) Hll[9 * (size_t)p + k] = Hll[9 * (size_t)p + k] + hll_e[9 * (size_t)e + k];
+                for (int k = 0; k < 3; ++k) bl[3 * (size_t)p + k] = bl[3 * (size_t)p + k] + bl_e[3 * (size_t)e + k];
+            }
+    }
+    double max_diag() const {
+        double m = 0.;
+        for (int f = 0; f < nf; ++f)
+            for (int j = 0; j < 6; ++j) m = std::max(std::fabs(Hpp[36 * (size_t)f + 7 * j]), m);
+        for (int p = 0; p < npt; ++p)
+            for (int j = 0; j < 3; ++j) m = std::max(std::fabs(Hll[9 * (size_t)p + 4 * j]), m);
+        return m;
+    }
+    static double cof(const double *m, int i, int j) {
+        const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+        return m[3 * i1 + j1] * m[3 * i2 + j2] - m[3 * i1 + j2] * m[3 * i2 + j1];
+    }
+    bool usable(int e) const { return act[e] && T[E[e].cam].f >= 0; }
+    bool solve(double lambda) {
+        const int n = 6 * nf;
+        std::vector<double> S((size_t)n * n, 0.0), bs(n), dinv(9 * (size_t)npt), bdinv(18 * (size_t)ne),
+            bdb(6 * (size_t)ne);
+        for (int p = 0; p < npt; ++p) {
+            double m[9];
+            for (int k = 0; k < 9; ++k) m[k] = Hll[9 * (size_t)p + k];
+            for (int k = 0; k < 3; ++k) m[4 * k] = m[4 * k] + lambda;
+            const double c0 = cof(m, 0, 0), c1 = cof(m, 1, 0), c2 = cof(m, 2, 0);
+            const double det = c0 * m[0] + c1 * m[3] + c2 * m[6];
+            const double invdet = 1.0 / det;
+            double *D = &dinv[9 * (size_t)p];
+            D[0] = c0 * invdet; D[1] = c1 * invdet; D[2] = c2 * invdet;
+            D[3] = cof(m, 0, 1) * invdet; D[4] = cof(m, 1, 1) * invdet; D[5] = cof(m, 2, 1) * invdet;
+            D[6] = cof(m, 0, 2) * invdet; D[7] = cof(m, 1, 2) * invdet; D[8] = cof(m, 2, 2) * invdet;
+            double db[3];
+            for (int r = 0; r < 3; ++r) {
+                double acc = 0;
+                for (int c = 0; c < 3; ++c) acc = acc + D[3 * r + c] * bl[3 * (size_t)p + c];
+                db[r] = acc;
+            }
+            for (int e : pe[p]) {
+                if (!usable(e)) continue;
+                const double *Bm = &hpl_e[18 * (size_t)e];
+                for (int r = 0; r < 6; ++r) {
+                    for (int c = 0; c < 3; ++c) {
+                        double acc = 0;
+                        for (int k = 0; k < 3; ++k) acc = acc + Bm[3 * r + k] * D[3 * k + c];
+                        bdinv[18 * (size_t)e + 3 * r + c] = acc;
+                    }
+                    double acc = 0;
+                    for (int k = 0; k < 3; ++k) acc = acc + Bm[3 * r + k] * db[k];
+                    bdb[6 * (size_t)e + r] = acc;
+                }
+            }
+        }
+        // camera lists of usable edges in ascending point order
+        std::vector<std::vector<int>> cl(nf);
+        for (int p = 0; p < npt; ++p)
+            for (int e : pe[p])
+                if (usable(e)) cl[T[E[e].cam].f].push_back(e);
+        for (int i1 = 0; i1 < nf; ++i1)
+            for (int i2 = i1; i2 < nf; ++i2)
+                for (int r = 0; r < 6; ++r)
+                    for (int c = 0; c < 6; ++c) {
+                        double acc = 0;
+                        if (i1 == i2) {
+                            acc = Hpp[36 * (size_t)i1 + 6 * r + c];
+                            if (r == c) acc = acc + lambda;
+                        }
+                        size_t a = 0, b = 0;
+                        while (a < cl[i1].size() && b < cl[i2].size()) {
+                            const int pa = E[cl[i1][a]].point, pb = E[cl[i2][b]].point;
+                            if (pa < pb) { ++a; continue; }
+                            if (pb < pa) { ++b; continue; }
+                            double s = 0;
+                            for (int k = 0; k < 3; ++k)
+                                s = s + bdinv[18 * (size_t)cl[i1][a] + 3 * r + k] * hpl_e[18 * (size_t)cl[i2][b] + 3 * c + k];
+                            acc = acc - s;
+                            ++a;
+                            ++b;
+                        }
+                        S[(size_t)(6 * i1 + r) * n + 6 * i2 + c] = acc;
+                        S[(size_t)(6 * i2 + c) * n + 6 * i1 + r] = acc;
+                    }
+        for (int i = 0; i < n; ++i) {
+            double coef = 0;
+            for (int e : cl[i / 6]) coef = coef + bdb[6 * (size_t)e + i % 6];
+            bs[i] = bp[i] - coef;
+        }
+        x.assign(n + 3 * (size_t)npt, 0.0);
+        for (int j = 0; j < n; ++j) {   // dense Cholesky, column by column
+            double d = S[(size_t)j * n + j];
+            for (int k = 0; k < j; ++k) d = d - S[(size_t)j * n + k] * S[(size_t)j * n + k];
+            if (!(d > 0)) return false;
+            const double dg = std::sqrt(d);
+            S[(size_t)j * n + j] = dg;
+            for (int i = j + 1; i < n; ++i) {
+                double s2 = S[(size_t)i * n + j];
+                for (int k = 0; k < j; ++k) s2 = s2 - S[(size_t)i * n + k] * S[(size_t)j * n + k];
+                S[(size_t)i * n + j] = s2 / dg;
+            }
+        }
+        for (int i = 0; i < n; ++i) {
+            double s2 = bs[i];
+            for (int k = 0; k < i; ++k) s2 = s2 - S[(size_t)i * n + k] * x[k];
+            x[i] = s2 / S[(size_t)i * n + i];
+        }
+        for (int i = n - 1; i >= 0; --i) {
+            double s2 = x[i];
+            for (int k = i + 1; k < n; ++k) s2 = s2 - S[(size_t)k * n + i] * x[k];
+            x[i] = s2 / S[(size_t)i * n + i];
+        }
+        for (int p = 0; p < npt; ++p) {
+            double c3[3];
+            for (int k = 0; k < 3; ++k) c3[k] = bl[3 * (size_t)p + k];
+            for (int e : pe[p]) {
+                if (!usable(e)) continue;
+                const int f = T[E[e].cam].f;
+                const double *Bm = &hpl_e[18 * (size_t)e];
+                for (int c = 0; c < 3; ++c) {
+                    double s2 = 0;
+                    for (int r = 0; r < 6; ++r) s2 = s2 + Bm[3 * r + c] * -x[6 * f + r];
+                    c3[c] = c3[c] + s2;
+                }
+            }
+            const double *D = &dinv[9 * (size_t)p];
+            for (int r = 0; r < 3; ++r) {
+                double acc = 0;
+                for (int c = 0; c < 3; ++c) acc = acc + D[3 * r + c] * c3[c];
+                x[n + 3 * (size_t)p + r] = acc;
+            }
+        }
+        return true;
+    }
+    double scale(double lambda) const {
+        const int n = 6 * nf;
+        double s2 = 0.;
+        for (int j = 0; j < n; ++j) s2 += x[j] * (lambda * x[j] + bp[j]);
+        for (int j = 0; j < 3 * npt; ++j) s2 += x[n + j] * (lambda * x[n + j] + bl[j]);
+        return s2;
+    }
+    void update() {
+        const int n = 6 * nf;
+        for (int c = 0; c < ncam; ++c) {
+            BQ &t = T[c];
+            if (t.f < 0) continue;
+            const double *u = &x[6 * (size_t)t.f];
+            const double w[3] = {u[0], u[1], u[2]}, ups[3] = {u[3], u[4], u[5]};
+            const double theta = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+            const double Om[9] = {0, -w[2], w[1], w[2], 0, -w[0], -w[1], w[0], 0};
+            double O2[9], R[9], V[9];
+            for (int r = 0; r < 3; ++r)
+                for (int cc = 0; cc < 3; ++cc) {
+                    double acc = 0;
+                    for (int k = 0; k < 3; ++k) acc = acc + Om[3 * r + k] * Om[3 * k + cc];
+                    O2[3 * r + cc] = acc;
+                }
+            if (theta < 0.00001) {
+                for (int k = 0; k < 9; ++k) R[k] = ((k % 4 == 0) ? 1.0 : 0.0) + Om[k] + O2[k];
+                for (int k = 0; k < 9; ++k) V[k] = R[k];
+            } else {
+                const double a = std::sin(theta) / theta, b = (1 - std::cos(theta)) / (theta * theta);
+                const double cc = (theta - std::sin(theta)) / std::pow(theta, 3);
+                for (int k = 0; k < 9; ++k) {
+                    R[k] = ((k % 4 == 0) ? 1.0 : 0.0) + a * Om[k] + b * O2[k];
+                    V[k] = ((k % 4 == 0) ? 1.0 : 0.0) + b * Om[k] + cc * O2[k];
+                }
+            }
+            double qe[4], te[3], rt[3], qn[4];
+            bq_fromR(R, qe);
+            for (int r = 0; r < 3; ++r) te[r] = V[3 * r] * ups[0] + V[3 * r + 1] * ups[1] + V[3 * r + 2] * ups[2];
+            bq_norm(qe);
+            bq_rot(qe, t.t, rt);
+            for (int k = 0; k < 3; ++k) t.t[k] = te[k] + rt[k];
+            bq_mul(qe, t.q, qn);
+            bq_norm(qn);
+            std::memcpy(t.q, qn, sizeof(qn));
+        }
+        for (int i = 0; i < 3 * npt; ++i) X[i] = X[i] + x[n + i];
+    }
+    int optimize(int iters) {   // OptimizationAlgorithmLevenberg::solve, `iters` times
+        double lambda = 0, ni = 2;
+        int nBad = 0, it = 0;
+        for (; it < iters; ++it) {
+            double currentChi = errors();
+            build();
+            const double iniChi = currentChi;
+            if (it == 0) {
+                lambda = 1e-5 * max_diag();
+                ni = 2;
+                nBad = 0;
+            }
+            double rho = 0;
+            int qmax = 0;
+            do {
+                const std::vector<BQ> Tb = T;
+                const std::vector<double> Xb = X;
+                const bool ok = solve(lambda);
+                double tempChi;
+                if (ok) {
+                    update();
+                    tempChi = errors();
+                } else {
+                    tempChi = DBL_MAX;
+                }
+                rho = currentChi - tempChi;
+                double sc = ok ? scale(lambda) : 0.0;
+                sc += 1e-3;
+                rho /= sc;
+                if (rho > 0 && std::isfinite(tempChi)) {
+                    double alpha = 1. - std::pow((2 * rho - 1), 3);
+                    alpha = std::min(alpha, 2. / 3.);
+                    lambda *= std::max(1. / 3., alpha);
+                    ni = 2;
+                    currentChi = tempChi;
+                } else {
+                    lambda *= ni;
+                    ni *= 2;
+                    T = Tb;
+                    X = Xb;
+                }
+                qmax++;
+            } while (rho < 0 && qmax < 10);
+            if (qmax == 10 || rho == 0) return it + 1;
+            if ((iniChi - currentChi) * 1e3 < iniChi) nBad++;
+            else nBad = 0;
+            if (nBad >= 3) return it + 1;
+        }
+        return it;
+    }
+};
+
+void oba_init(OBA &o, const float *Tcw, const uint8_t *fixed, int ncam, const float *Xw, int npt,
+              const orbo_ba_edge *edges, int ne) {
+    o.ncam = ncam; o.npt = npt; o.ne = ne; o.E = edges;
+    o.T.resize(ncam);
+    int nf = 0;
+    for (int c = 0; c < ncam; ++c) {
+        double R[9];
+        for (int r = 0; r < 3; ++r)
+            for (int k = 0; k < 3; ++k) R[3 * r + k] = Tcw[12 * (size_t)c + 4 * r + k];
+        bq_fromR(R, o.T[c].q);
+        bq_norm(o.T[c].q);
+        for (int r = 0; r < 3; ++r) o.T[c].t[r] = Tcw[12 * (size_t)c + 4 * r + 3];
+        o.T[c].f = fixed[c] ? -1 : nf++;
+    }
+    o.nf = nf;
+    o.X.assign(Xw, Xw + 3 * (size_t)npt);
+    const double thMono = (double)(float)std::sqrt(5.991), thStereo = (double)(float)std::sqrt(7.815);
+    o.delta.resize(ne);
+    for (int e = 0; e < ne; ++e) o.delta[e] = edges[e].ur >= 0 ? thStereo : thMono;
+    o.err.assign(3 * (size_t)ne, 0); o.chi2.assign(ne, 0); o.rho0.assign(ne, 0); o.rho1.assign(ne, 0);
+    o.act.assign(ne, 1); o.front.assign(ne, 0);
+    o.hpp_e.assign(36 * (size_t)ne, 0); o.hll_e.assign(9 * (size_t)ne, 0); o.hpl_e.assign(18 * (size_t)ne, 0);
+    o.bp_e.assign(6 * (size_t)ne, 0); o.bl_e.assign(3 * (size_t)ne, 0);
+    o.pe.assign(npt, {});
+    for (int e = 0; e < ne; ++e) o.pe[edges[e].point].push_back(e);
+    for (auto &l : o.pe) std::stable_sort(l.begin(), l.end(), [&](int a, int b) { return edges[a].cam < edges[b].cam; });
+    o.ce.assign(nf, {});
+    for (int e = 0; e < ne; ++e)
+        if (o.T[edges[e].cam].f >= 0) o.ce[o.T[edges[e].cam].f].push_back(e);
+}
+}  // namespace
+
+int orbo_local_ba(const float *Tcw, const uint8_t *fixed, int ncam, const float *Xw, int npt,
+                  const orbo_ba_edge *edges, int ne, int iters1, int iters2, float *Tcw_out, float *Xw_out,
+                  uint8_t *outlier, int *iterations) {
+    OBA o;
+    oba_init(o, Tcw, fixed, ncam, Xw, npt, edges, ne);
+    o.robust = true;
+    const int it1 = o.optimize(iters1);
+    int it2 = 0;
+    if (iters2 > 0) {
+        o.fronts();   // e->chi2() as last computed, isDepthPositive() now
+        for (int e = 0; e < ne; ++e) {
+            const double th = edges[e].ur >= 0 ? 7.815 : 5.991;
+            if (o.chi2[e] > th || !o.front[e]) o.act[e] = 0;
+        }
+        o.robust = false;
+        it2 = o.optimize(iters2);
+    }
+    o.fronts();
+    for (int e = 0; e < ne; ++e) {
+        const double th = edges[e].ur >= 0 ? 7.815 : 5.991;
+        outlier[e] = o.chi2[e] > th || !o.front[e];
+    }
+    for (int c = 0; c < ncam; ++c) {
+        double R[9];
+        bq_R(o.T[c].q, R);
+        for (int r = 0; r < 3; ++r) {
+            for (int k = 0; k < 3; ++k) Tcw_out[12 * (size_t)c + 4 * r + k] = (float)R[3 * r + k];
+            Tcw_out[12 * (size_t)c + 4 * r + 3] = (float)o.T[c].t[r];
+        }
+    }
+    for (int i = 0; i < 3 * npt; ++i) Xw_out[i] = (float)o.X[i];
+    if (iterations) { iterations[0] = it1; iterations[1] = it2; }
+    return 0;
+}
+
+int orbo_ba_debug_step(const float *Tcw, const uint8_t *fixed, int ncam, const float *Xw, int npt,
+                       const orbo_ba_edge *edges, int ne, int robust, double lambda, double *x_out, double *chi2_out) {
+    OBA o;
+    oba_init(o, Tcw, fixed, ncam, Xw, npt, edges, ne);
+    o.robust = robust != 0;
+    *chi2_out = o.errors();
+    o.build();
+    const bool ok = o.solve(lambda);
+    if (ok) std::copy(o.x.begin(), o.x.end(), x_out);
+    return ok ? 1 : 0;
+}

@@ -222,6 +222,27 @@ int   orbo_kfdb_detect(void *db, int reloc, uint64_t query_id, const uint32_t *w
                        uint64_t *out, int cap);
 double orbo_bow_score_l1(const uint32_t *w1, const double *v1, int n1, const uint32_t *w2, const double *v2, int n2);
 
+/* ---- local bundle adjustment ----
+ * Optimizer::LocalBundleAdjustment's optimisation (Optimizer.cc:517-900)
+ * restated over g2o's Levenberg (optimization_algorithm_levenberg.cpp:60-160),
+ * BlockSolver_6_3 with the Schur complement (block_solver.hpp:354-484), the
+ * two projection edges (types_six_dof_expmap.cpp:109-230), Huber
+ * (robust_kernel_impl.cpp:65-91) and SE3Quat (se3quat.h).  The sums follow a
+ * fixed order (edge order per vertex, ascending point per camera pair, a dense
+ * Cholesky of the reduced system): g2o's own order is unspecified (it sorts
+ * edges of equal ids) and Eigen's sparse LDLT differs, so parity with g2o is
+ * to rounding -- unpinned.  Edge layout as orbx_ba_edge in include/orbx.h. */
+typedef struct {
+    int32_t cam, point;
+    float u, v, ur, inv_sigma2, fx, fy, cx, cy, bf;
+} orbo_ba_edge;
+int   orbo_local_ba(const float *Tcw, const uint8_t *fixed, int ncam, const float *Xw, int npt,
+                    const orbo_ba_edge *edges, int ne, int iters1, int iters2, float *Tcw_out, float *Xw_out,
+                    uint8_t *outlier, int *iterations);
+int   orbo_ba_debug_step(const float *Tcw, const uint8_t *fixed, int ncam, const float *Xw, int npt,
+                         const orbo_ba_edge *edges, int ne, int robust, double lambda, double *x_out,
+                         double *chi2_out);
+
 #ifdef __cplusplus
 }
 #endif

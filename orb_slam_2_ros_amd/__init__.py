@@ -14,7 +14,9 @@ from .depth import compute_stereo_matches, stereo_from_rgbd  # noqa: F401
 from .vocabulary import ORBVocabulary  # noqa: F401
 from .frame_aux import compute_distinctive_descriptors, cvt_gray, undistort_keypoints  # noqa: F401
 from .keyframe_db import KeyFrameDatabase  # noqa: F401
+from .optimizer import local_bundle_adjustment  # noqa: F401
 
 __all__ = ["KEYPOINT_DTYPE", "OrbxError", "load", "ORBextractor", "ORBmatcher", "Frame",
            "compute_stereo_matches", "stereo_from_rgbd", "ORBVocabulary",
-           "compute_distinctive_descriptors", "cvt_gray", "undistort_keypoints", "KeyFrameDatabase"]
+           "compute_distinctive_descriptors", "cvt_gray", "undistort_keypoints", "KeyFrameDatabase",
+           "local_bundle_adjustment"]

@@ -122,6 +122,8 @@ _SIGNATURES = {
     "orbx_kfdb_detect_loop_candidates": (I32, [P, ctypes.c_uint64, P, P, I32, P, I32, F32, P, P, P, I32, P]),
     "orbx_kfdb_detect_relocalization_candidates": (I32, [P, ctypes.c_uint64, P, P, I32, P, P, P, I32, P]),
     "orbx_bow_score_l1": (I32, [P, P, I32, P, P, I32, P]),
+    "orbx_local_ba": (I32, [I32, P, P, I32, P, I32, P, I32, I32, I32, P, P, P, P]),
+    "orbx_ba_debug_step": (I32, [I32, P, P, I32, P, I32, P, I32, I32, ctypes.c_double, P, P, P]),
 }
 
 # orbx_covis_fn

@@ -1,0 +1,972 @@
+// orbx_ba.hip -- Optimizer::LocalBundleAdjustment (Optimizer.cc:517-900) on
+// gfx950: g2o's Levenberg-Marquardt (optimization_algorithm_levenberg.cpp:
+// 60-160) over a BlockSolver_6_3 (block_solver.hpp: buildSystem, Schur
+// complement :354-484) with EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ
+// (types_six_dof_expmap.cpp:109-230) and Huber kernels (robust_kernel_impl.
+// cpp:78-91).  SURVEY.md §8 f2, config C4.
+//
+// Device work per LM trial, all FP64:
+//   k_ba_errors      thread per edge: error, chi2, Huber rho (computeActiveErrors)
+//   k_ba_linearize   thread per edge: Jacobians and the edge's J^T W J / J^T W r blocks
+//   k_ba_reduce      wave per vertex: sums of its edges' blocks, in edge order
+//   k_ba_point       thread per point: (Hll + lambda I)^-1, db, then per edge B Dinv and B db
+//   k_ba_pairs       wave per camera pair: S_ij -= B_i Dinv B_j^T over shared points, point order
+//   k_ba_chol        one workgroup: dense Cholesky of the reduced camera system and the solve
+//   k_ba_backsub     thread per point: xl = Dinv (bl - sum_e B_e^T xp)
+//   k_ba_update      poses exp(dx) * T (SE3Quat), points += dx
+// Every sum runs in a fixed order (edge order per vertex, ascending point per
+// camera pair, ascending column in the Cholesky), so a run is deterministic
+// and matches the oracle's CPU restatement of the same order.  g2o's own order
+// is unspecified (it sorts edges with equal ids), so parity with it is to
+// rounding only.  The LM control (lambda, rho, trials, termination) runs on
+// the host as in the reference.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <set>
+#include <vector>
+
+#include "orbx_device.h"
+#include "orbx_wave.h"
+#include "orbx_ws.h"
+
+namespace orbx {
+namespace {
+
+struct Pose {      // SE3Quat: q = (x, y, z, w), t
+    double q[4];
+    double t[3];
+    int32_t free_idx;   // -1: fixed
+    int32_t pad;
+};
+
+struct EdgeD {     // one observation, device copy
+    int32_t cam, point, stereo, pad;
+    double obs[3];
+    double omega;   // information = omega * I
+    double fx, fy, cx, cy, bf;
+    double delta;   // Huber delta
+};
+
+struct EdgeOut {   // per edge, per linearization
+    double hpp[36], hll[9], hpl[18];   // hpl: 6 x 3 (pose rows, point cols)
+    double bp[6], bl[3];
+};
+
+// Eigen's q * v (Quaternion::_transformVector): uv = 2 (q.vec x v); v + w uv + q.vec x uv
+__host__ __device__ inline void quat_rotate(const double *q, const double *v, double *o) {
+    double uv[3] = {q[1] * v[2] - q[2] * v[1], q[2] * v[0] - q[0] * v[2], q[0] * v[1] - q[1] * v[0]};
+    for (int i = 0; i < 3; ++i) uv[i] = uv[i] + uv[i];
+    const double c[3] = {q[1] * uv[2] - q[2] * uv[1], q[2] * uv[0] - q[0] * uv[2], q[0] * uv[1] - q[1] * uv[0]};
+    for (int i = 0; i < 3; ++i) o[i] = v[i] + q[3] * uv[i] + c[i];
+}
+
+__host__ __device__ inline void se3_map(const Pose &T, const double *X, double *o) {
+    quat_rotate(T.q, X, o);
+    for (int i = 0; i < 3; ++i) o[i] = o[i] + T.t[i];
+}
+
+// Eigen's Quaternion::toRotationMatrix
+__host__ __device__ inline void quat_to_R(const double *q, double *R) {
+    const double tx = 2 * q[0], ty = 2 * q[1], tz = 2 * q[2];
+    const double twx = tx * q[3], twy = ty * q[3], twz = tz * q[3];
+    const double txx = tx * q[0], txy = ty * q[0], txz = tz * q[0];
+    const double tyy = ty * q[1], tyz = tz * q[1], tzz = tz * q[2];
+    R[0] = 1 - (tyy + tzz); R[1] = txy - twz; R[2] = txz + twy;
+    R[3] = txy + twz; R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy; R[7] = tyz + twx; R[8] = 1 - (txx + tyy);
+}
+
+// Eigen's Quaternion(const Matrix3&) (quaternion_base_assign_impl)
+__host__ __device__ inline void R_to_quat(const double *m, double *q) {
+    const double tr = m[0] + m[4] + m[8];
+    if (tr > 0) {
+        double t = sqrt(tr + 1.0);
+        q[3] = 0.5 * t;
+        t = 0.5 / t;
+        q[0] = (m[7] - m[5]) * t;
+        q[1] = (m[2] - m[6]) * t;
+        q[2] = (m[3] - m[1]) * t;
+    } else {
+        int i = 0;
+        if (m[4] > m[0]) i = 1;
+        if (m[8] > m[3 * i + i]) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        double t = sqrt(m[3 * i + i] - m[3 * j + j] - m[3 * k + k] + 1.0);
+        q[i] = 0.5 * t;
+        t = 0.5 / t;
+        q[3] = (m[3 * k + j] - m[3 * j + k]) * t;
+        q[j] = (m[3 * j + i] + m[3 * i + j]) * t;
+        q[k] = (m[3 * k + i] + m[3 * i + k]) * t;
+    }
+}
+
+// SE3Quat::normalizeRotation: w >= 0, unit norm
+__host__ __device__ inline void quat_normalize(double *q) {
+    if (q[3] < 0)
+        for (int i = 0; i < 4; ++i) q[i] *= -1;
+    const double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    for (int i = 0; i < 4; ++i) q[i] = q[i] / n;
+}
+
+// Eigen's quaternion product a * b
+__host__ __device__ inline void quat_mul(const double *a, const double *b, double *o) {
+    o[3] = a[3] * b[3] - a[0] * b[0] - a[1] * b[1] - a[2] * b[2];
+    o[0] = a[3] * b[0] + a[0] * b[3] + a[1] * b[2] - a[2] * b[1];
+    o[1] = a[3] * b[1] + a[1] * b[3] + a[2] * b[0] - a[0] * b[2];
+    o[2] = a[3] * b[2] + a[2] * b[3] + a[0] * b[1] - a[1] * b[0];
+}
+
+// error of an edge (computeError) and whether the point is in front
+__device__ inline void edge_error(const EdgeD &e, const Pose &T, const double *X, double *err, bool *front) {
+    double p[3];
+    se3_map(T, X, p);
+    *front = p[2] > 0.0;
+    if (!e.stereo) {
+        const double u = p[0] / p[2], v = p[1] / p[2];
+        err[0] = e.obs[0] - (u * e.fx + e.cx);
+        err[1] = e.obs[1] - (v * e.fy + e.cy);
+        err[2] = 0;
+    } else {
+        const double invz = (double)(float)(1.0 / p[2]);   // const float invz = 1.0f/trans_xyz[2]
+        const double r0 = p[0] * invz * e.fx + e.cx;
+        const double r1 = p[1] * invz * e.fy + e.cy;
+        err[0] = e.obs[0] - r0;
+        err[1] = e.obs[1] - r1;
+        err[2] = e.obs[2] - (r0 - e.bf * invz);
+    }
+}
+
+__global__ void k_ba_errors(const Pose *poses, const double *pts, const EdgeD *edges, int ne, const uint8_t *active,
+                            int robust, int front_only, double *err_out, double *chi2_out, double *rho_out,
+                            uint8_t *front_out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ne) return;
+    const EdgeD e = edges[i];
+    double err[3];
+    bool front;
+    edge_error(e, poses[e.cam], pts + 3 * (int64_t)e.point, err, &front);
+    front_out[i] = front;   // isDepthPositive() at the current estimate
+    if (front_only || !active[i]) return;   // computeActiveErrors leaves inactive edges' errors as they were
+    const int D = e.stereo ? 3 : 2;
+    double chi2 = 0;
+    for (int k = 0; k < D; ++k) chi2 = chi2 + err[k] * (e.omega * err[k]);
+    double rho0 = chi2, rho1 = 1.0;
+    if (robust) {
+        const double dsqr = e.delta * e.delta;
+        if (!(chi2 <= dsqr)) {
+            const double s = sqrt(chi2);
+            rho0 = 2 * s * e.delta - dsqr;
+            rho1 = e.delta / s;
+        }
+    }
+    for (int k = 0; k < 3; ++k) err_out[3 * (int64_t)i + k] = err[k];
+    chi2_out[i] = chi2;
+    rho_out[2 * (int64_t)i] = rho0;
+    rho_out[2 * (int64_t)i + 1] = rho1;
+}
+
+__global__ void k_ba_linearize(const Pose *poses, const double *pts, const EdgeD *edges, int ne, const uint8_t *active,
+                               const double *err_in, const double *rho_in, EdgeOut *out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ne || !active[i]) return;
+    const EdgeD e = edges[i];
+    const Pose T = poses[e.cam];
+    double p[3];
+    se3_map(T, pts + 3 * (int64_t)e.point, p);
+    const double x = p[0], y = p[1], z = p[2], z_2 = z * z;
+    double R[9];
+    quat_to_R(T.q, R);
+    double A[3][3], B[3][6];   // d e / d point, d e / d pose (rows: error components)
+    if (!e.stereo) {
+        const double tmp[2][3] = {{e.fx, 0, -x / z * e.fx}, {0, e.fy, -y / z * e.fy}};
+        const double s = -1. / z;
+        for (int r = 0; r < 2; ++r)
+            for (int c = 0; c < 3; ++c) {
+                double acc = 0;
+                for (int k = 0; k < 3; ++k) acc = acc + (s * tmp[r][k]) * R[3 * k + c];
+                A[r][c] = acc;
+            }
+    } else {
+        for (int c = 0; c < 3; ++c) {
+            A[0][c] = -e.fx * R[c] / z + e.fx * x * R[6 + c] / z_2;
+            A[1][c] = -e.fy * R[3 + c] / z + e.fy * y * R[6 + c] / z_2;
+            A[2][c] = A[0][c] - e.bf * R[6 + c] / z_2;
+        }
+    }
+    B[0][0] = x * y / z_2 * e.fx;
+    B[0][1] = -(1 + (x * x / z_2)) * e.fx;
+    B[0][2] = y / z * e.fx;
+    B[0][3] = -1. / z * e.fx;
+    B[0][4] = 0;
+    B[0][5] = x / z_2 * e.fx;
+    B[1][0] = (1 + y * y / z_2) * e.fy;
+    B[1][1] = -x * y / z_2 * e.fy;
+    B[1][2] = -x / z * e.fy;
+    B[1][3] = 0;
+    B[1][4] = -1. / z * e.fy;
+    B[1][5] = y / z_2 * e.fy;
+    if (e.stereo) {
+        B[2][0] = B[0][0] - e.bf * y / z_2;
+        B[2][1] = B[0][1] + e.bf * x / z_2;
+        B[2][2] = B[0][2];
+        B[2][3] = B[0][3];
+        B[2][4] = 0;
+        B[2][5] = B[0][5] - e.bf / z_2;
+    }
+    const int D = e.stereo ? 3 : 2;
+    const double rho1 = rho_in[2 * (int64_t)i + 1];
+    const double w = rho1 * e.omega;   // robustInformation = rho[1] * information (rho1 = 1 without a kernel)
+    double omr[3];
+    for (int k = 0; k < D; ++k) omr[k] = -(e.omega * err_in[3 * (int64_t)i + k]) * rho1;
+    EdgeOut o;
+    for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) {
+            double acc = 0;
+            for (int k = 0; k < D; ++k) acc = acc + (A[k][a] * w) * A[k][b];
+            o.hll[3 * a + b] = acc;
+        }
+    const bool pose_free = T.free_idx >= 0;
+    for (int a = 0; a < 6; ++a) {
+        for (int b = 0; b < 6; ++b) {
+            double acc = 0;
+            if (pose_free)
+                for (int k = 0; k < D; ++k) acc = acc + (B[k][a] * w) * B[k][b];
+            o.hpp[6 * a + b] = acc;
+        }
+        for (int c = 0; c < 3; ++c) {   // (A^T W B)^T: pose row a, point column c
+            double acc = 0;
+            if (pose_free)
+                for (int k = 0; k < D; ++k) acc = acc + (A[k][c] * w) * B[k][a];
+            o.hpl[3 * a + c] = acc;
+        }
+        double acc = 0;
+        if (pose_free)
+            for (int k = 0; k < D; ++k) acc = acc + B[k][a] * omr[k];
+        o.bp[a] = acc;
+    }
+    for (int c = 0; c < 3; ++c) {
+        double acc = 0;
+        for (int k = 0; k < D; ++k) acc = acc + A[k][c] * omr[k];
+        o.bl[c] = acc;
+    }
+    out[i] = o;
+}
+
+// Vertex blocks: wave per vertex, lane = one matrix entry, edges in order.
+// kind 0: cameras (36 + 6 entries from hpp / bp), 1: points (9 + 3 from hll / bl).
+__global__ void k_ba_reduce(const EdgeOut *eo, const int32_t *offs, const int32_t *list, const uint8_t *active,
+                            int nv, int kind, double *H, double *b) {
+    const int lane = threadIdx.x & 63;
+    const int v = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    if (v >= nv) return;
+    const int nh = kind ? 9 : 36, nb = kind ? 3 : 6;
+    if (lane >= nh + nb) return;
+    double acc = 0;
+    for (int t = offs[v]; t < offs[v + 1]; ++t) {
+        const int ei = list[t];
+        if (!active[ei]) continue;
+        const EdgeOut &o = eo[ei];
+        acc = acc + (lane < nh ? (kind ? o.hll[lane] : o.hpp[lane]) : (kind ? o.bl[lane - nh] : o.bp[lane - nh]));
+    }
+    if (lane < nh) H[(int64_t)v * nh + lane] = acc;
+    else b[(int64_t)v * nb + lane - nh] = acc;
+}
+
+// Per point: Dinv = (Hll + lambda I)^-1 (Eigen's 3x3 cofactor inverse),
+// db = Dinv bl, then for each of its active free-camera edges B Dinv and B db.
+__device__ inline double cof(const double *m, int i, int j) {
+    const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+    return m[3 * i1 + j1] * m[3 * i2 + j2] - m[3 * i1 + j2] * m[3 * i2 + j1];
+}
+
+__global__ void k_ba_point(const double *Hll, const double *bl, int npt, double lambda, const EdgeOut *eo,
+                           const int32_t *offs, const int32_t *list, const uint8_t *usable, double *dinv_out,
+                           double *bdinv, double *bdb) {
+    const int pt = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pt >= npt) return;
+    double m[9];
+    for (int k = 0; k < 9; ++k) m[k] = Hll[9 * (int64_t)pt + k];
+    for (int k = 0; k < 3; ++k) m[4 * k] = m[4 * k] + lambda;
+    const double c0 = cof(m, 0, 0), c1 = cof(m, 1, 0), c2 = cof(m, 2, 0);
+    const double det = c0 * m[0] + c1 * m[3] + c2 * m[6];
+    const double invdet = 1.0 / det;
+    double D[9];
+    D[0] = c0 * invdet; D[1] = c1 * invdet; D[2] = c2 * invdet;
+    D[3] = cof(m, 0, 1) * invdet; D[4] = cof(m, 1, 1) * invdet; D[5] = cof(m, 2, 1) * invdet;
+    D[6] = cof(m, 0, 2) * invdet; D[7] = cof(m, 1, 2) * invdet; D[8] = cof(m, 2, 2) * invdet;
+    for (int k = 0; k < 9; ++k) dinv_out[9 * (int64_t)pt + k] = D[k];
+    double db[3];
+    for (int r = 0; r < 3; ++r) {
+        double acc = 0;
+        for (int c = 0; c < 3; ++c) acc = acc + D[3 * r + c] * bl[3 * (int64_t)pt + c];
+        db[r] = acc;
+    }
+    for (int t = offs[pt]; t < offs[pt + 1]; ++t) {
+        const int ei = list[t];
+        if (!usable[ei]) continue;
+        const double *B = eo[ei].hpl;
+        for (int r = 0; r < 6; ++r) {
+            for (int c = 0; c < 3; ++c) {
+                double acc = 0;
+                for (int k = 0; k < 3; ++k) acc = acc + B[3 * r + k] * D[3 * k + c];
+                bdinv[18 * (int64_t)ei + 3 * r + c] = acc;
+            }
+            double acc = 0;
+            for (int k = 0; k < 3; ++k) acc = acc + B[3 * r + k] * db[k];
+            bdb[6 * (int64_t)ei + r] = acc;
+        }
+    }
+}
+
+// S block (i1, i2), i1 <= i2: Hpp(+lambda on the diagonal) - sum over shared
+// points (ascending) of BDinv_e1 * B_e2^T.  Wave per pair, lane per entry.
+// Camera lists hold the usable edges sorted by point.
+__global__ void k_ba_pairs(const int2 *pairs, int npairs, const int32_t *coffs, const int32_t *clist,
+                           const int32_t *epoint, const EdgeOut *eo, const double *bdinv, const double *Hpp,
+                           double lambda, int nf, double *S) {
+    const int lane = threadIdx.x & 63;
+    const int pi = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    if (pi >= npairs || lane >= 36) return;
+    const int i1 = pairs[pi].x, i2 = pairs[pi].y;
+    const int r = lane / 6, c = lane % 6;
+    double acc = 0;
+    if (i1 == i2) {
+        acc = Hpp[36 * (int64_t)i1 + lane];
+        if (r == c) acc = acc + lambda;
+    }
+    int a = coffs[i1], ae = coffs[i1 + 1], b = coffs[i2], be = coffs[i2 + 1];
+    while (a < ae && b < be) {
+        const int pa = epoint[clist[a]], pb = epoint[clist[b]];
+        if (pa < pb) { ++a; continue; }
+        if (pb < pa) { ++b; continue; }
+        const int e1 = clist[a], e2 = clist[b];
+        double s = 0;
+        for (int k = 0; k < 3; ++k) s = s + bdinv[18 * (int64_t)e1 + 3 * r + k] * eo[e2].hpl[3 * c + k];
+        acc = acc - s;
+        ++a;
+        ++b;
+    }
+    const int n = 6 * nf;
+    S[(int64_t)(6 * i1 + r) * n + 6 * i2 + c] = acc;
+    S[(int64_t)(6 * i2 + c) * n + 6 * i1 + r] = acc;   // mirror (the solver reads the full matrix)
+}
+
+// bschur = bp - sum over the camera's usable edges (point order) of B db.
+__global__ void k_ba_bschur(const double *bp, const int32_t *coffs, const int32_t *clist, const double *bdb, int nf,
+                            double *bs) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 6 * nf) return;
+    const int cam = i / 6, r = i % 6;
+    double coef = 0;
+    for (int t = coffs[cam]; t < coffs[cam + 1]; ++t) coef = coef + bdb[6 * (int64_t)clist[t] + r];
+    bs[i] = bp[i] - coef;
+}
+
+// Dense Cholesky S = L L^T (lower, in place, column by column) and the two
+// triangular solves for x; one workgroup.  ok = 0 if S is not positive definite.
+__global__ __launch_bounds__(1024) void k_ba_chol(double *S, int n, const double *bs, double *x, int *ok) {
+    __shared__ double diag;
+    __shared__ int bad;
+    const int tid = threadIdx.x;
+    if (tid == 0) bad = 0;
+    __syncthreads();
+    for (int j = 0; j < n; ++j) {
+        if (tid == 0) {
+            double d = S[(int64_t)j * n + j];
+            for (int k = 0; k < j; ++k) d = d - S[(int64_t)j * n + k] * S[(int64_t)j * n + k];
+            if (!(d > 0)) bad = 1;
+            diag = sqrt(d);
+            S[(int64_t)j * n + j] = diag;
+        }
+        __syncthreads();
+        if (bad) break;
+        for (int i = j + 1 + tid; i < n; i += blockDim.x) {
+            double s = S[(int64_t)i * n + j];
+            for (int k = 0; k < j; ++k) s = s - S[(int64_t)i * n + k] * S[(int64_t)j * n + k];
+            S[(int64_t)i * n + j] = s / diag;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        *ok = !bad;
+        if (!bad) {
+            for (int i = 0; i < n; ++i) {   // L y = b
+                double s = bs[i];
+                for (int k = 0; k < i; ++k) s = s - S[(int64_t)i * n + k] * x[k];
+                x[i] = s / S[(int64_t)i * n + i];
+            }
+            for (int i = n - 1; i >= 0; --i) {   // L^T x = y
+                double s = x[i];
+                for (int k = i + 1; k < n; ++k) s = s - S[(int64_t)k * n + i] * x[k];
+                x[i] = s / S[(int64_t)i * n + i];
+            }
+        }
+    }
+}
+
+// xl = Dinv (bl - sum over the point's usable edges (camera order) of B^T xp)
+__global__ void k_ba_backsub(const double *dinv, const double *bl, int npt, const EdgeOut *eo, const int32_t *offs,
+                             const int32_t *list, const uint8_t *usable, const EdgeD *edges, const Pose *poses,
+                             const double *xp, double *xl) {
+    const int pt = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pt >= npt) return;
+    double cl[3];
+    for (int k = 0; k < 3; ++k) cl[k] = bl[3 * (int64_t)pt + k];
+    for (int t = offs[pt]; t < offs[pt + 1]; ++t) {
+        const int ei = list[t];
+        if (!usable[ei]) continue;
+        const int f = poses[edges[ei].cam].free_idx;
+        const double *B = eo[ei].hpl;
+        for (int c = 0; c < 3; ++c) {
+            double s = 0;
+            for (int r = 0; r < 6; ++r) s = s + B[3 * r + c] * -xp[6 * f + r];
+            cl[c] = cl[c] + s;
+        }
+    }
+    const double *D = dinv + 9 * (int64_t)pt;
+    for (int r = 0; r < 3; ++r) {
+        double acc = 0;
+        for (int c = 0; c < 3; ++c) acc = acc + D[3 * r + c] * cl[c];
+        xl[3 * (int64_t)pt + r] = acc;
+    }
+}
+
+// SE3Quat::exp(update) * estimate (se3quat.h:223-258, :104-110); points += dx
+__global__ void k_ba_update(Pose *poses, int ncam, double *pts, int npt, const double *xp, const double *xl) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < npt)
+        for (int k = 0; k < 3; ++k) pts[3 * (int64_t)i + k] = pts[3 * (int64_t)i + k] + xl[3 * (int64_t)i + k];
+    if (i < ncam && poses[i].free_idx >= 0) {
+        Pose &T = poses[i];
+        const double *u = xp + 6 * T.free_idx;
+        const double w[3] = {u[0], u[1], u[2]}, ups[3] = {u[3], u[4], u[5]};
+        const double theta = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+        const double Om[9] = {0, -w[2], w[1], w[2], 0, -w[0], -w[1], w[0], 0};
+        double O2[9];
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) {
+                double acc = 0;
+                for (int k = 0; k < 3; ++k) acc = acc + Om[3 * r + k] * Om[3 * k + c];
+                O2[3 * r + c] = acc;
+            }
+        double R[9], V[9];
+        if (theta < 0.00001) {
+            for (int k = 0; k < 9; ++k) R[k] = ((k % 4 == 0) ? 1.0 : 0.0) + Om[k] + O2[k];
+            for (int k = 0; k < 9; ++k) V[k] = R[k];
+        } else {
+            const double a = sin(theta) / theta, b = (1 - cos(theta)) / (theta * theta);
+            const double c = (theta - sin(theta)) / pow(theta, 3);
+            for (int k = 0; k < 9; ++k) {
+                R[k] = ((k % 4 == 0) ? 1.0 : 0.0) + a * Om[k] + b * O2[k];
+                V[k] = ((k % 4 == 0) ? 1.0 : 0.0) + b * Om[k] + c * O2[k];
+            }
+        }
+        double qe[4], te[3];
+        R_to_quat(R, qe);
+        for (int r = 0; r < 3; ++r) te[r] = V[3 * r] * ups[0] + V[3 * r + 1] * ups[1] + V[3 * r + 2] * ups[2];
+        quat_normalize(qe);   // SE3Quat(q, t) constructor
+        // (qe, te) * (T.q, T.t): t = te + qe * T.t, q = qe * T.q, normalised
+        double rt[3], qn[4];
+        quat_rotate(qe, T.t, rt);
+        for (int k = 0; k < 3; ++k) T.t[k] = te[k] + rt[k];
+        quat_mul(qe, T.q, qn);
+        quat_normalize(qn);
+        for (int k = 0; k < 4; ++k) T.q[k] = qn[k];
+    }
+}
+
+}  // namespace
+}  // namespace orbx
+
+using namespace orbx;
+
+namespace {
+
+// Converter::toSE3Quat (Converter.cc:37-47): SE3Quat(R, t) from a float Tcw
+void pose_from_cv(const float *T, Pose &p) {
+    double R[9];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) R[3 * r + c] = T[4 * r + c];
+    R_to_quat(R, p.q);
+    quat_normalize(p.q);
+    for (int r = 0; r < 3; ++r) p.t[r] = T[4 * r + 3];
+}
+
+// Converter::toCvMat(SE3Quat): rotation matrix and translation as float
+void pose_to_cv(const Pose &p, float *T) {
+    double R[9];
+    quat_to_R(p.q, R);
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) T[4 * r + c] = (float)R[3 * r + c];
+        T[4 * r + 3] = (float)p.t[r];
+    }
+}
+
+struct Dev {
+    uint8_t *base = nullptr;
+    size_t cap = 0;
+};
+
+template <typename T>
+T *carve(uint8_t *&p, size_t n) {
+    T *r = reinterpret_cast<T *>(p);
+    p += (sizeof(T) * n + 255) & ~size_t(255);
+    return r;
+}
+
+struct Graph {
+    int ncam, npt, ne, nf;
+    std::vector<Pose> poses;
+    std::vector<EdgeD> edges;
+    std::vector<int32_t> coffs, clist, poffs, plist, epoint;   // camera lists: usable edges by point; point lists: edges by camera
+};
+
+class BA {
+public:
+    explicit BA(Graph &g, hipStream_t st) : g_(g), st_(st) {}
+    int alloc();
+    int upload(const double *pts);
+    void set_active(const std::vector<uint8_t> &act);
+    int errors(bool robust, double *chi_sum);
+    int build();
+    int max_diag(double *m);
+    int solve(double lambda, int *ok);
+    double scale(double lambda);
+    int update();
+    int push();
+    int pop();
+    int download(double *pts, std::vector<double> &chi2, std::vector<uint8_t> &front);
+    ~BA() { if (buf_) (void)hipFree(buf_); }
+
+    Graph &g_;
+    hipStream_t st_;
+    uint8_t *buf_ = nullptr;
+    Pose *d_pose = nullptr, *d_pose_bk = nullptr;
+    double *d_pts = nullptr, *d_pts_bk = nullptr;
+    EdgeD *d_edges = nullptr;
+    uint8_t *d_active = nullptr, *d_usable = nullptr, *d_front = nullptr;
+    double *d_err = nullptr, *d_chi2 = nullptr, *d_rho = nullptr;
+    EdgeOut *d_eo = nullptr;
+    int32_t *d_coffs = nullptr, *d_clist = nullptr, *d_poffs = nullptr, *d_plist = nullptr, *d_epoint = nullptr,
+            *d_cvoffs = nullptr, *d_cvlist = nullptr;
+    int2 *d_pairs = nullptr;
+    int npairs = 0;
+    double *d_Hpp = nullptr, *d_bp = nullptr, *d_Hll = nullptr, *d_bl = nullptr, *d_dinv = nullptr,
+           *d_bdinv = nullptr, *d_bdb = nullptr, *d_S = nullptr, *d_bs = nullptr, *d_x = nullptr;
+    int *d_ok = nullptr;
+    std::vector<uint8_t> act_;
+    std::vector<int32_t> cv_offs_, cv_list_;   // all edges per free camera (reduce), edge order
+};
+
+int BA::alloc() {
+    const Graph &g = g_;
+    const size_t ne = std::max(g.ne, 1), nc = std::max(g.ncam, 1), np = std::max(g.npt, 1), nf = std::max(g.nf, 1);
+    // the camera-pair list: free cameras sharing a point (structure of the reduced system)
+    std::set<std::pair<int, int>> pairset;
+    std::vector<int> fcams;
+    for (int p = 0; p < g.npt; ++p) {
+        fcams.clear();
+        for (int t = g.poffs[p]; t < g.poffs[p + 1]; ++t) {
+            const int f = g.poses[g.edges[g.plist[t]].cam].free_idx;
+            if (f >= 0) fcams.push_back(f);
+        }
+        for (size_t a = 0; a < fcams.size(); ++a)
+            for (size_t b = 0; b < fcams.size(); ++b)
+                if (fcams[a] <= fcams[b]) pairset.insert({fcams[a], fcams[b]});
+    }
+    for (int f = 0; f < g.nf; ++f) pairset.insert({f, f});
+    std::vector<int2> pairs;
+    for (auto &pr : pairset) pairs.push_back(make_int2(pr.first, pr.second));
+    npairs = (int)pairs.size();
+    // all edges of each free camera in edge order (for Hpp / bp)
+    cv_offs_.assign(g.nf + 1, 0);
+    for (int e = 0; e < g.ne; ++e) {
+        const int f = g.poses[g.edges[e].cam].free_idx;
+        if (f >= 0) ++cv_offs_[f + 1];
+    }
+    for (int f = 0; f < g.nf; ++f) cv_offs_[f + 1] += cv_offs_[f];
+    cv_list_.assign(std::max(cv_offs_[g.nf], 1), 0);
+    {
+        std::vector<int> fill(cv_offs_.begin(), cv_offs_.end() - 1);
+        for (int e = 0; e < g.ne; ++e) {
+            const int f = g.poses[g.edges[e].cam].free_idx;
+            if (f >= 0) cv_list_[fill[f]++] = e;
+        }
+    }
+    const size_t n = 6 * nf;
+    const size_t bytes = 256 * 40 + sizeof(Pose) * nc * 2 + 8 * 3 * np * 2 + sizeof(EdgeD) * ne + 3 * ne +
+                         8 * ne * 6 + sizeof(EdgeOut) * ne + 4 * (nf + 1 + ne + np + 1 + ne + ne + nf + 1 + ne) +
+                         sizeof(int2) * std::max(npairs, 1) + 8 * (36 * nf + 6 * nf + 9 * np + 3 * np + 9 * np +
+                                                                   18 * ne + 6 * ne + n * n + n + n + 3 * np) + 256;
+    if (hipMalloc(reinterpret_cast<void **>(&buf_), bytes) != hipSuccess) return ORBX_ENOMEM;
+    uint8_t *p = buf_;
+    d_pose = carve<Pose>(p, nc); d_pose_bk = carve<Pose>(p, nc);
+    d_pts = carve<double>(p, 3 * np); d_pts_bk = carve<double>(p, 3 * np);
+    d_edges = carve<EdgeD>(p, ne);
+    d_active = carve<uint8_t>(p, ne); d_usable = carve<uint8_t>(p, ne); d_front = carve<uint8_t>(p, ne);
+    d_err = carve<double>(p, 3 * ne); d_chi2 = carve<double>(p, ne); d_rho = carve<double>(p, 2 * ne);
+    d_eo = carve<EdgeOut>(p, ne);
+    d_coffs = carve<int32_t>(p, nf + 1); d_clist = carve<int32_t>(p, ne);
+    d_poffs = carve<int32_t>(p, np + 1); d_plist = carve<int32_t>(p, ne); d_epoint = carve<int32_t>(p, ne);
+    d_cvoffs = carve<int32_t>(p, nf + 1); d_cvlist = carve<int32_t>(p, ne);
+    d_pairs = carve<int2>(p, std::max(npairs, 1));
+    d_Hpp = carve<double>(p, 36 * nf); d_bp = carve<double>(p, 6 * nf);
+    d_Hll = carve<double>(p, 9 * np); d_bl = carve<double>(p, 3 * np); d_dinv = carve<double>(p, 9 * np);
+    d_bdinv = carve<double>(p, 18 * ne); d_bdb = carve<double>(p, 6 * ne);
+    d_S = carve<double>(p, n * n); d_bs = carve<double>(p, n); d_x = carve<double>(p, n + 3 * np);
+    d_ok = carve<int>(p, 1);
+    if ((size_t)(p - buf_) > bytes) return ORBX_ENOMEM;
+    auto up = [&](void *d, const void *h, size_t b) {
+        return b == 0 || hipMemcpyAsync(d, h, b, hipMemcpyHostToDevice, st_) == hipSuccess;
+    };
+    std::vector<int32_t> ep(g.ne);
+    for (int e = 0; e < g.ne; ++e) ep[e] = g.edges[e].point;
+    if (!up(d_edges, g.edges.data(), sizeof(EdgeD) * g.ne) || !up(d_poffs, g.poffs.data(), 4 * (g.npt + 1)) ||
+        !up(d_plist, g.plist.data(), 4 * g.ne) || !up(d_epoint, ep.data(), 4 * g.ne) ||
+        !up(d_pairs, pairs.data(), sizeof(int2) * npairs) || !up(d_cvoffs, cv_offs_.data(), 4 * (g.nf + 1)) ||
+        !up(d_cvlist, cv_list_.data(), 4 * cv_list_.size()) || hipStreamSynchronize(st_) != hipSuccess)
+        return ORBX_EIO;
+    return ORBX_OK;
+}
+
+int BA::upload(const double *pts) {
+    if (hipMemcpyAsync(d_pose, g_.poses.data(), sizeof(Pose) * g_.ncam, hipMemcpyHostToDevice, st_) != hipSuccess ||
+        (g_.npt && hipMemcpyAsync(d_pts, pts, 24 * (size_t)g_.npt, hipMemcpyHostToDevice, st_) != hipSuccess))
+        return ORBX_EIO;
+    return ORBX_OK;
+}
+
+// active edges; usable = active with a free camera, sorted per camera by point
+void BA::set_active(const std::vector<uint8_t> &act) {
+    act_ = act;
+    const Graph &g = g_;
+    std::vector<uint8_t> usable(g.ne);
+    for (int e = 0; e < g.ne; ++e) usable[e] = act[e] && g.poses[g.edges[e].cam].free_idx >= 0;
+    std::vector<int32_t> coffs(g.nf + 1, 0), clist;
+    for (int e = 0; e < g.ne; ++e)
+        if (usable[e]) ++coffs[g.poses[g.edges[e].cam].free_idx + 1];
+    for (int f = 0; f < g.nf; ++f) coffs[f + 1] += coffs[f];
+    clist.assign(std::max(coffs[g.nf], 1), 0);
+    std::vector<int> fill(coffs.begin(), coffs.end() - 1);
+    // point-major walk: each camera's list comes out in ascending point order
+    for (int p = 0; p < g.npt; ++p)
+        for (int t = g.poffs[p]; t < g.poffs[p + 1]; ++t) {
+            const int e = g.plist[t];
+            if (usable[e]) clist[fill[g.poses[g.edges[e].cam].free_idx]++] = e;
+        }
+    (void)hipMemcpyAsync(d_active, act.data(), g.ne, hipMemcpyHostToDevice, st_);
+    (void)hipMemcpyAsync(d_usable, usable.data(), g.ne, hipMemcpyHostToDevice, st_);
+    (void)hipMemcpyAsync(d_coffs, coffs.data(), 4 * (g.nf + 1), hipMemcpyHostToDevice, st_);
+    (void)hipMemcpyAsync(d_clist, clist.data(), 4 * clist.size(), hipMemcpyHostToDevice, st_);
+    (void)hipStreamSynchronize(st_);
+}
+
+int BA::errors(bool robust, double *chi_sum) {
+    const int ne = g_.ne;
+    if (ne) hipLaunchKernelGGL(k_ba_errors, dim3((ne + 255) / 256), dim3(256), 0, st_, d_pose, d_pts, d_edges, ne,
+                               d_active, robust ? 1 : 0, 0, d_err, d_chi2, d_rho, d_front);
+    std::vector<double> rho(2 * (size_t)std::max(ne, 1));
+    if (hipGetLastError() != hipSuccess ||
+        (ne && hipMemcpyAsync(rho.data(), d_rho, 16 * (size_t)ne, hipMemcpyDeviceToHost, st_) != hipSuccess) ||
+        hipStreamSynchronize(st_) != hipSuccess)
+        return ORBX_EIO;
+    double s = 0;   // activeRobustChi2: active edges in order
+    for (int e = 0; e < ne; ++e)
+        if (act_[e]) s += rho[2 * (size_t)e];
+    *chi_sum = s;
+    return ORBX_OK;
+}
+
+int BA::build() {
+    const Graph &g = g_;
+    if (g.ne) hipLaunchKernelGGL(k_ba_linearize, dim3((g.ne + 255) / 256), dim3(256), 0, st_, d_pose, d_pts, d_edges,
+                                 g.ne, d_active, d_err, d_rho, d_eo);
+    if (g.nf) hipLaunchKernelGGL(k_ba_reduce, dim3((g.nf + 3) / 4), dim3(256), 0, st_, d_eo, d_cvoffs, d_cvlist,
+                                 d_active, g.nf, 0, d_Hpp, d_bp);
+    if (g.npt) hipLaunchKernelGGL(k_ba_reduce, dim3((g.npt + 3) / 4), dim3(256), 0, st_, d_eo, d_poffs, d_plist,
+                                  d_active, g.npt, 1, d_Hll, d_bl);
+    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
+}
+
+// computeLambdaInit: max |diagonal| over the free vertices
+int BA::max_diag(double *m) {
+    std::vector<double> hpp(36 * (size_t)std::max(g_.nf, 1)), hll(9 * (size_t)std::max(g_.npt, 1));
+    if ((g_.nf && hipMemcpyAsync(hpp.data(), d_Hpp, 8 * 36 * (size_t)g_.nf, hipMemcpyDeviceToHost, st_) != hipSuccess) ||
+        (g_.npt && hipMemcpyAsync(hll.data(), d_Hll, 8 * 9 * (size_t)g_.npt, hipMemcpyDeviceToHost, st_) != hipSuccess) ||
+        hipStreamSynchronize(st_) != hipSuccess)
+        return ORBX_EIO;
+    double mx = 0.;
+    for (int f = 0; f < g_.nf; ++f)
+        for (int j = 0; j < 6; ++j) mx = std::max(std::fabs(hpp[36 * (size_t)f + 7 * j]), mx);
+    for (int p = 0; p < g_.npt; ++p)
+        for (int j = 0; j < 3; ++j) mx = std::max(std::fabs(hll[9 * (size_t)p + 4 * j]), mx);
+    *m = mx;
+    return ORBX_OK;
+}
+
+int BA::solve(double lambda, int *ok) {
+    const Graph &g = g_;
+    const int n = 6 * g.nf;
+    // (the previous factorisation left L in place, also outside the pair blocks)
+    if (n && hipMemsetAsync(d_S, 0, 8 * (size_t)n * n, st_) != hipSuccess) return ORBX_EIO;
+    if (g.npt) hipLaunchKernelGGL(k_ba_point, dim3((g.npt + 255) / 256), dim3(256), 0, st_, d_Hll, d_bl, g.npt, lambda,
+                                  d_eo, d_poffs, d_plist, d_usable, d_dinv, d_bdinv, d_bdb);
+    if (g.nf) {
+        hipLaunchKernelGGL(k_ba_pairs, dim3((npairs + 3) / 4), dim3(256), 0, st_, d_pairs, npairs, d_coffs, d_clist,
+                           d_epoint, d_eo, d_bdinv, d_Hpp, lambda, g.nf, d_S);
+        hipLaunchKernelGGL(k_ba_bschur, dim3((n + 255) / 256), dim3(256), 0, st_, d_bp, d_coffs, d_clist, d_bdb, g.nf,
+                           d_bs);
+        // (blocks of camera pairs without a shared point stay as the memset left them)
+        hipLaunchKernelGGL(k_ba_chol, dim3(1), dim3(1024), 0, st_, d_S, n, d_bs, d_x, d_ok);
+    }
+    if (g.npt) hipLaunchKernelGGL(k_ba_backsub, dim3((g.npt + 255) / 256), dim3(256), 0, st_, d_dinv, d_bl, g.npt,
+                                  d_eo, d_poffs, d_plist, d_usable, d_edges, d_pose, d_x, d_x + n);
+    int okv = 1;
+    if (hipGetLastError() != hipSuccess ||
+        (g.nf && hipMemcpyAsync(&okv, d_ok, 4, hipMemcpyDeviceToHost, st_) != hipSuccess) ||
+        hipStreamSynchronize(st_) != hipSuccess)
+        return ORBX_EIO;
+    *ok = okv;
+    return ORBX_OK;
+}
+
+// computeScale: sum over the solution of x (lambda x + b), poses then points
+double BA::scale(double lambda) {
+    const int n = 6 * g_.nf, m = n + 3 * g_.npt;
+    std::vector<double> x(std::max(m, 1)), b(std::max(m, 1));
+    (void)hipMemcpyAsync(x.data(), d_x, 8 * (size_t)m, hipMemcpyDeviceToHost, st_);
+    if (n) (void)hipMemcpyAsync(b.data(), d_bp, 8 * (size_t)n, hipMemcpyDeviceToHost, st_);
+    if (g_.npt) (void)hipMemcpyAsync(b.data() + n, d_bl, 8 * 3 * (size_t)g_.npt, hipMemcpyDeviceToHost, st_);
+    (void)hipStreamSynchronize(st_);
+    double s = 0.;
+    for (int j = 0; j < m; ++j) s += x[j] * (lambda * x[j] + b[j]);
+    return s;
+}
+
+int BA::update() {
+    const int n = std::max(g_.ncam, g_.npt);
+    hipLaunchKernelGGL(k_ba_update, dim3((n + 255) / 256), dim3(256), 0, st_, d_pose, g_.ncam, d_pts, g_.npt, d_x,
+                       d_x + 6 * g_.nf);
+    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
+}
+
+int BA::push() {
+    if (hipMemcpyAsync(d_pose_bk, d_pose, sizeof(Pose) * g_.ncam, hipMemcpyDeviceToDevice, st_) != hipSuccess ||
+        (g_.npt && hipMemcpyAsync(d_pts_bk, d_pts, 24 * (size_t)g_.npt, hipMemcpyDeviceToDevice, st_) != hipSuccess))
+        return ORBX_EIO;
+    return ORBX_OK;
+}
+
+int BA::pop() {
+    if (hipMemcpyAsync(d_pose, d_pose_bk, sizeof(Pose) * g_.ncam, hipMemcpyDeviceToDevice, st_) != hipSuccess ||
+        (g_.npt && hipMemcpyAsync(d_pts, d_pts_bk, 24 * (size_t)g_.npt, hipMemcpyDeviceToDevice, st_) != hipSuccess))
+        return ORBX_EIO;
+    return ORBX_OK;
+}
+
+// chi2 as last computed (an edge's error is only refreshed while active, and
+// a rejected trial's errors stay), the depth test at the current estimate
+int BA::download(double *pts, std::vector<double> &chi2, std::vector<uint8_t> &front) {
+    if (g_.ne) hipLaunchKernelGGL(k_ba_errors, dim3((g_.ne + 255) / 256), dim3(256), 0, st_, d_pose, d_pts, d_edges,
+                                  g_.ne, d_active, 0, 1, d_err, d_chi2, d_rho, d_front);
+    chi2.resize(std::max(g_.ne, 1));
+    front.resize(std::max(g_.ne, 1));
+    if (hipMemcpyAsync(g_.poses.data(), d_pose, sizeof(Pose) * g_.ncam, hipMemcpyDeviceToHost, st_) != hipSuccess ||
+        (g_.npt && hipMemcpyAsync(pts, d_pts, 24 * (size_t)g_.npt, hipMemcpyDeviceToHost, st_) != hipSuccess) ||
+        (g_.ne && hipMemcpyAsync(chi2.data(), d_chi2, 8 * (size_t)g_.ne, hipMemcpyDeviceToHost, st_) != hipSuccess) ||
+        (g_.ne && hipMemcpyAsync(front.data(), d_front, g_.ne, hipMemcpyDeviceToHost, st_) != hipSuccess) ||
+        hipStreamSynchronize(st_) != hipSuccess)
+        return ORBX_EIO;
+    return ORBX_OK;
+}
+
+// OptimizationAlgorithmLevenberg::solve over `iters` iterations
+// (optimization_algorithm_levenberg.cpp:60-145); returns iterations run.
+int lm_optimize(BA &ba, int iters, bool robust, int *rc_out) {
+    double lambda = 0, ni = 2;
+    int nBad = 0, it = 0;
+    *rc_out = ORBX_OK;
+    for (; it < iters; ++it) {
+        double currentChi = 0;
+        int rc = ba.errors(robust, &currentChi);
+        if (!rc) rc = ba.build();
+        if (rc) { *rc_out = rc; return it; }
+        const double iniChi = currentChi;
+        if (it == 0) {
+            double md = 0;
+            if ((rc = ba.max_diag(&md))) { *rc_out = rc; return it; }
+            lambda = 1e-5 * md;   // _tau * maxDiagonal
+            ni = 2;
+            nBad = 0;
+        }
+        double rho = 0;
+        int qmax = 0;
+        do {
+            int ok = 0;
+            if ((rc = ba.push()) || (rc = ba.solve(lambda, &ok))) { *rc_out = rc; return it; }
+            double tempChi = 0;
+            if (ok) {
+                if ((rc = ba.update()) || (rc = ba.errors(robust, &tempChi))) { *rc_out = rc; return it; }
+            } else {
+                tempChi = DBL_MAX;   // (the reference updates with an unsolved x; the step is rejected either way)
+            }
+            rho = currentChi - tempChi;
+            double sc = ok ? ba.scale(lambda) : 0.0;
+            sc += 1e-3;
+            rho /= sc;
+            if (rho > 0 && std::isfinite(tempChi)) {
+                double alpha = 1. - std::pow((2 * rho - 1), 3);
+                alpha = std::min(alpha, 2. / 3.);
+                const double scaleFactor = std::max(1. / 3., alpha);
+                lambda *= scaleFactor;
+                ni = 2;
+                currentChi = tempChi;
+            } else {
+                lambda *= ni;
+                ni *= 2;
+                if ((rc = ba.pop())) { *rc_out = rc; return it; }
+            }
+            qmax++;
+        } while (rho < 0 && qmax < 10);
+        if (qmax == 10 || rho == 0) return it + 1;   // Terminate
+        if ((iniChi - currentChi) * 1e3 < iniChi) nBad++;
+        else nBad = 0;
+        if (nBad >= 3) return it + 1;
+    }
+    return it;
+}
+
+int build_graph(const float *Tcw, const uint8_t *fixed, int ncam, int npt, const orbx_ba_edge *edges, int ne,
+                Graph &g) {
+    g.ncam = ncam; g.npt = npt; g.ne = ne;
+    g.poses.resize(ncam);
+    int nf = 0;
+    for (int c = 0; c < ncam; ++c) {
+        pose_from_cv(Tcw + 12 * (size_t)c, g.poses[c]);
+        g.poses[c].free_idx = fixed[c] ? -1 : nf++;
+        g.poses[c].pad = 0;
+    }
+    g.nf = nf;
+    g.edges.resize(ne);
+    const double thMono = (double)(float)std::sqrt(5.991), thStereo = (double)(float)std::sqrt(7.815);
+    for (int e = 0; e < ne; ++e) {
+        const orbx_ba_edge &s = edges[e];
+        if (s.cam < 0 || s.cam >= ncam || s.point < 0 || s.point >= npt) return ORBX_EINVAL;
+        EdgeD &d = g.edges[e];
+        d.cam = s.cam; d.point = s.point; d.stereo = s.ur >= 0 ? 1 : 0; d.pad = 0;
+        d.obs[0] = s.u; d.obs[1] = s.v; d.obs[2] = d.stereo ? s.ur : 0.0;
+        d.omega = s.inv_sigma2;
+        d.fx = s.fx; d.fy = s.fy; d.cx = s.cx; d.cy = s.cy; d.bf = s.bf;
+        d.delta = d.stereo ? thStereo : thMono;
+    }
+    // edges per point, by camera index (stable)
+    g.poffs.assign(npt + 1, 0);
+    for (int e = 0; e < ne; ++e) ++g.poffs[edges[e].point + 1];
+    for (int p = 0; p < npt; ++p) g.poffs[p + 1] += g.poffs[p];
+    g.plist.assign(std::max(ne, 1), 0);
+    std::vector<int> fill(g.poffs.begin(), g.poffs.end() - 1);
+    for (int e = 0; e < ne; ++e) g.plist[fill[edges[e].point]++] = e;
+    for (int p = 0; p < npt; ++p)
+        std::stable_sort(g.plist.begin() + g.poffs[p], g.plist.begin() + g.poffs[p + 1],
+                         [&](int a, int b) { return edges[a].cam < edges[b].cam; });
+    return ORBX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int orbx_local_ba(int device, const float *Tcw, const uint8_t *fixed, int ncam, const float *Xw, int npt,
+                  const orbx_ba_edge *edges, int ne, int iters1, int iters2, float *Tcw_out, float *Xw_out,
+                  uint8_t *outlier, int *iterations) {
+    if (ncam < 0 || npt < 0 || ne < 0 || iters1 < 0 || iters2 < 0 || (ncam && (!Tcw || !fixed || !Tcw_out)) ||
+        (npt && (!Xw || !Xw_out)) || (ne && (!edges || !outlier)))
+        return ORBX_EINVAL;
+    Graph g;
+    int rc = build_graph(Tcw, fixed, ncam, npt, edges, ne, g);
+    if (rc) return rc;
+    if (g.nf > 170) return ORBX_EINVAL;   // dense reduced system: 6 x 170 rows in one workgroup
+    if (hipSetDevice(device) != hipSuccess) return ORBX_ENODEV;
+    hipStream_t st;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return ORBX_EIO;
+    std::vector<double> pts(3 * (size_t)std::max(npt, 1));
+    for (size_t i = 0; i < 3 * (size_t)npt; ++i) pts[i] = Xw[i];
+    std::vector<uint8_t> out_flags(std::max(ne, 1), 0);
+    int its[2] = {0, 0};
+    {
+        BA ba(g, st);
+        if ((rc = ba.alloc()) || (rc = ba.upload(pts.data()))) { (void)hipStreamDestroy(st); return rc; }
+        (void)hipMemsetAsync(ba.d_chi2, 0, 8 * (size_t)std::max(ne, 1), st);
+        (void)hipMemsetAsync(ba.d_rho, 0, 16 * (size_t)std::max(ne, 1), st);
+        (void)hipMemsetAsync(ba.d_err, 0, 24 * (size_t)std::max(ne, 1), st);
+        // optimizer.optimize(5) with Huber kernels on every edge (Optimizer.cc:779-781)
+        std::vector<uint8_t> act(std::max(ne, 1), 1);
+        ba.set_active(act);
+        its[0] = lm_optimize(ba, iters1, true, &rc);
+        std::vector<double> chi2;
+        std::vector<uint8_t> front;
+        if (!rc) rc = ba.download(pts.data(), chi2, front);
+        if (!rc && iters2 > 0) {
+            // outliers leave the second pass (setLevel(1)); every kernel is dropped (:791-826)
+            for (int e = 0; e < ne; ++e) {
+                const double th = g.edges[e].stereo ? 7.815 : 5.991;
+                if (chi2[e] > th || !front[e]) act[e] = 0;
+            }
+            ba.set_active(act);
+            its[1] = lm_optimize(ba, iters2, false, &rc);
+            if (!rc) rc = ba.download(pts.data(), chi2, front);
+        }
+        if (!rc)   // the inlier check of :838-870 (an inactive edge keeps its last error)
+            for (int e = 0; e < ne; ++e) {
+                const double th = g.edges[e].stereo ? 7.815 : 5.991;
+                out_flags[e] = chi2[e] > th || !front[e];
+            }
+    }
+    (void)hipStreamDestroy(st);
+    if (rc) return rc;
+    for (int c = 0; c < ncam; ++c) pose_to_cv(g.poses[c], Tcw_out + 12 * (size_t)c);
+    for (size_t i = 0; i < 3 * (size_t)npt; ++i) Xw_out[i] = (float)pts[i];
+    if (ne) std::memcpy(outlier, out_flags.data(), ne);
+    if (iterations) { iterations[0] = its[0]; iterations[1] = its[1]; }
+    return ORBX_OK;
+}
+
+// One linear system of the first pass: computeActiveErrors, buildSystem,
+// setLambda(lambda), solve -- the step x (poses, then points) and the robust
+// chi2, without the update (test hook for the oracle's identical step).
+int orbx_ba_debug_step(int device, const float *Tcw, const uint8_t *fixed, int ncam, const float *Xw, int npt,
+                       const orbx_ba_edge *edges, int ne, int robust, double lambda, double *x_out, double *chi2_out,
+                       int *solved) {
+    if (ncam < 0 || npt < 0 || ne < 0 || !x_out || !chi2_out || !solved || (ncam && (!Tcw || !fixed)) ||
+        (npt && !Xw) || (ne && !edges))
+        return ORBX_EINVAL;
+    Graph g;
+    int rc = build_graph(Tcw, fixed, ncam, npt, edges, ne, g);
+    if (rc) return rc;
+    if (g.nf > 170) return ORBX_EINVAL;
+    if (hipSetDevice(device) != hipSuccess) return ORBX_ENODEV;
+    hipStream_t st;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return ORBX_EIO;
+    std::vector<double> pts(3 * (size_t)std::max(npt, 1));
+    for (size_t i = 0; i < 3 * (size_t)npt; ++i) pts[i] = Xw[i];
+    {
+        BA ba(g, st);
+        std::vector<uint8_t> act(std::max(ne, 1), 1);
+        if (!(rc = ba.alloc()) && !(rc = ba.upload(pts.data()))) {
+            ba.set_active(act);
+            if (!(rc = ba.errors(robust != 0, chi2_out)) && !(rc = ba.build()) && !(rc = ba.solve(lambda, solved))) {
+                const size_t m = 6 * (size_t)g.nf + 3 * (size_t)npt;
+                if (m && (hipMemcpy(x_out, ba.d_x, 8 * m, hipMemcpyDeviceToHost) != hipSuccess)) rc = ORBX_EIO;
+            }
+        }
+    }
+    (void)hipStreamDestroy(st);
+    return rc;
+}
+
+}  // extern "C"

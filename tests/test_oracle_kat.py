@@ -427,3 +427,88 @@ def test_bow_score_l1_oracle(oracle_mod):
     for a in range(0, 30, 3):
         for b in range(1, 30, 4):
             assert oracle_mod.bow_score_l1(*bows[a], *bows[b]) == pyref.l1_score(*bows[a], *bows[b])
+
+
+def _reproj_median(T, X, E):
+    Xc = np.einsum("eij,ej->ei", T[E["cam"], :, :3].astype(np.float64), X[E["point"]].astype(np.float64)) \
+        + T[E["cam"], :, 3]
+    u = E["fx"] * Xc[:, 0] / Xc[:, 2] + E["cx"]
+    v = E["fy"] * Xc[:, 1] / Xc[:, 2] + E["cy"]
+    return float(np.median(np.hypot(u - E["u"], v - E["v"])))
+
+
+def test_local_ba_oracle_converges_and_flags_outliers(oracle_mod):
+    """The restated LocalBundleAdjustment reduces the reprojection error,
+    brings the free poses toward the truth, keeps the fixed ones, and marks
+    the injected gross outliers for erasure."""
+    from orb_slam_2_ros_amd.synth_ba import make_ba_problem
+    P = make_ba_problem(n_local=6, n_fixed=2, n_points=600, seed=3, outlier_frac=0.04)
+    To, Xo, out, its = oracle_mod.local_ba(P["Tcw"], P["fixed"], P["Xw"], P["edges"])
+    assert its[0] >= 1 and its[1] >= 1
+    assert _reproj_median(To, Xo, P["edges"]) < 0.6 * _reproj_median(P["Tcw"], P["Xw"], P["edges"])
+    free = P["fixed"] == 0
+    assert np.abs(To[free] - P["Tcw_true"][free]).max() < 0.5 * np.abs(P["Tcw"][free] - P["Tcw_true"][free]).max()
+    assert np.array_equal(To[~free], P["Tcw"][~free])
+    E = P["edges"]
+    Xc = np.einsum("eij,ej->ei", P["Tcw_true"][E["cam"], :, :3], P["Xw_true"][E["point"]]) + P["Tcw_true"][E["cam"], :, 3]
+    gross = np.hypot(E["fx"] * Xc[:, 0] / Xc[:, 2] + E["cx"] - E["u"], E["fy"] * Xc[:, 1] / Xc[:, 2] + E["cy"] - E["v"]) > 14
+    assert out[gross].mean() > 0.95
+
+
+def test_local_ba_step_solves_the_normal_equations(oracle_mod):
+    """The Schur-reduced step equals the solution of the full damped normal
+    equations (H + lambda I) x = b built from numerical Jacobians of the
+    reprojection error under g2o's left SE3 / additive point perturbations."""
+    from orb_slam_2_ros_amd.synth_ba import make_ba_problem
+    P = make_ba_problem(n_local=3, n_fixed=1, n_points=40, seed=4, outlier_frac=0.0, stereo_frac=0.5)
+    T, F, X, E = P["Tcw"].astype(np.float64), P["fixed"], P["Xw"].astype(np.float64), P["edges"]
+    lam = 1e-2
+    x, chi2, ok = oracle_mod.ba_debug_step(P["Tcw"], F, P["Xw"], E, robust=False, lam=lam)
+    assert ok
+    free = np.nonzero(F == 0)[0]
+    nf, npt = len(free), len(X)
+    fidx = {c: i for i, c in enumerate(free)}
+
+    def expm(w6):
+        R = pyref_rot(w6[:3])
+        return R, w6[3:]
+
+    def pyref_rot(w):
+        th = np.linalg.norm(w)
+        K = np.array([[0, -w[2], w[1]], [w[2], 0, -w[0]], [-w[1], w[0], 0]])
+        if th < 1e-12:
+            return np.eye(3) + K
+        return np.eye(3) + np.sin(th) / th * K + (1 - np.cos(th)) / th ** 2 * K @ K
+
+    def resid(Tc, Xp, e):
+        Xc = Tc[:, :3] @ Xp + Tc[:, 3]
+        u = e["fx"] * Xc[0] / Xc[2] + e["cx"]
+        v = e["fy"] * Xc[1] / Xc[2] + e["cy"]
+        r = [e["u"] - u, e["v"] - v]
+        if e["ur"] >= 0:
+            r.append(e["ur"] - (u - e["bf"] / Xc[2]))
+        return np.array(r)
+
+    n = 6 * nf + 3 * npt
+    H, b = np.zeros((n, n)), np.zeros(n)
+    for e in E:
+        c, p = int(e["cam"]), int(e["point"])
+        r0 = resid(T[c], X[p], e)
+        cols, J = [], []
+        if c in fidx:
+            for k in range(6):
+                d = np.zeros(6); d[k] = 1e-6
+                R, t = expm(d)
+                Tn = np.hstack([R @ T[c][:, :3], (R @ T[c][:, 3] + t)[:, None]])
+                J.append((resid(Tn, X[p], e) - r0) / 1e-6)
+                cols.append(6 * fidx[c] + k)
+        for k in range(3):
+            d = np.zeros(3); d[k] = 1e-6
+            J.append((resid(T[c], X[p] + d, e) - r0) / 1e-6)
+            cols.append(6 * nf + 3 * p + k)
+        J = np.array(J).T
+        w = float(e["inv_sigma2"])
+        H[np.ix_(cols, cols)] += w * J.T @ J
+        b[cols] += -w * J.T @ r0
+    xr = np.linalg.solve(H + lam * np.eye(n), b)
+    assert np.allclose(x, xr, rtol=2e-3, atol=2e-5 * np.abs(xr).max())
