@@ -300,12 +300,12 @@ __global__ __launch_bounds__(kThreads) void k_blur(DevPlan p, FrameBufs fb) {
 // For each interior pixel the arc score S = max over the 16 nine-pixel arcs of
 // max(min(v - p), min(p - v)); the pixel is a corner at threshold t iff S > t
 // and cv::FAST's cornerScore is S - 1.  S is evaluated only
-// where a 16-bit brighter/darker mask at minThFAST holds a 9-run, i.e. only
-// for corners.  NMS is the strict 3x3 test inside the cell (outside
-// neighbours count 0, as FAST on the cell sub-image sees them).  The iniThFAST
-// and minThFAST keypoint lists are compacted in one pass into two slot
-// arrays; the count word says which one the cell uses (bit 31 = minThFAST:
-// no keypoint survived at iniThFAST, ORBextractor.cc:846-850).
+// for pixels that pass a compass pre-test at the pass's threshold.  NMS is the
+// strict 3x3 test inside the cell (outside neighbours count 0, as FAST on the
+// cell sub-image sees them).  As the reference, a pass at iniThFAST comes
+// first and a pass at minThFAST only for a cell it left empty (about one cell
+// in eight); the count word says which list the cell uses (bit 31 =
+// minThFAST, ORBextractor.cc:846-850).
 // Output: keypoints in row-major order, packed (x | y<<12 | s<<24).
 // ===========================================================================
 // max over the 16 arcs of 9 of max(min(p) - v, v - max(p)) for circle bytes p.
@@ -348,113 +348,111 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb) {
     }
     const int PS = p.fast_patch_stride, SW = p.cell_max_w + 2;
     uint8_t *patch = lds + (size_t)wave * p.fast_lds_per_wave;
-    uint8_t *scm = patch + p.fast_patch_bytes;   // S-1 of corners at min(ini, min) threshold, 0 elsewhere
+    uint8_t *scm = patch + p.fast_patch_bytes;   // S-1 of the pass's corners, 0 elsewhere
     uint16_t *list = reinterpret_cast<uint16_t *>(scm + p.fast_score_bytes);   // (yy << 8 | xx), row-major
     int spitch;
     const uint8_t *img = level_ptr(p, fb, c.level, b, spitch);
     const int o = wave_stage_rect(patch, PS, img, spitch, c.y0 - 3, c.x0 - 3, ch + 6, cw + 6, lane);
-    {
-        uint32_t *z0 = reinterpret_cast<uint32_t *>(scm);
-        const int nz = p.fast_score_bytes >> 2;
-        for (int i = lane; i < nz; i += 64) z0[i] = 0;
-    }
-    wave_lds_fence();
     const uint8_t *pc = patch + 3 * PS + o + 3;         // interior pixel (0, 0)
-    const int ini = p.ini_th, mnt = p.min_th;
-    const int lo = min(ini, mnt);   // corners at either threshold are corners at lo
     const int npx = cw * ch;
     const uint64_t below = (1ull << lane) - 1;
-
-    // A. compass pre-test at the lower threshold: an arc of 9 covers two cyclically
-    //    adjacent points of {0, 4, 8, 12}, so a pixel is a corner candidate only if
-    //    some adjacent pair is all brighter (min of the pair > v + lo) or all
-    //    darker (max of the pair < v - lo).  Survivors are compacted.
     const int dyc = div_small(64, cw), dxc = 64 - dyc * cw;
-    int yy = div_small(lane, cw), xx = lane - yy * cw;
-    int nsurv = 0;
-    for (int i0 = 0; i0 < npx; i0 += 64) {
-        bool surv = false;
-        if (i0 + lane < npx) {
-            const uint8_t *q = pc + yy * PS + xx;
-            const int v = q[0];
-            const int a0 = q[3 * PS], a4 = q[3], a8 = q[-3 * PS], a12 = q[-3];
-            const int hi_pair = max(max(min(a0, a4), min(a8, a12)), max(min(a4, a8), min(a12, a0)));
-            const int lo_pair = min(min(max(a0, a4), max(a8, a12)), min(max(a4, a8), max(a12, a0)));
-            surv = (hi_pair > v + lo) | (lo_pair < v - lo);
-        }
-        const uint64_t m = __ballot(surv);
-        if (surv) list[nsurv + __popcll(m & below)] = (uint16_t)((yy << 8) | xx);
-        nsurv += __popcll(m);
-        yy += dyc; xx += dxc;
-        if (xx >= cw) { xx -= cw; ++yy; }
-    }
-    wave_lds_fence();
-
-    // B. arc score of every survivor: S = max(M1 - v, v - M2), M1 = max over the
-    //    16 nine-pixel arcs of the arc's minimum, M2 = min over arcs of the arc's
-    //    maximum.  Both run side by side as packed u16 lanes (p, 255 - p) through
-    //    sliding-window minima (2, 4, 8, 9).  The pixel is a corner at lo iff
-    //    S > lo; its score S - 1 goes to the map and corners are compacted in
-    //    place (a corner's slot never passes the survivors already read).
-    int ncorner = 0;
-    for (int i0 = 0; i0 < nsurv; i0 += 64) {
-        bool corner = false;
-        int e = 0;
-        if (i0 + lane < nsurv) {
-            e = list[i0 + lane];
-            const int ey = e >> 8, ex = e & 0xFF;
-            const uint8_t *q = pc + ey * PS + ex;
-            const int v = q[0];
-            const int pr[16] = {q[3 * PS],  q[3 * PS + 1],  q[2 * PS + 2],  q[PS + 3],
-                                q[3],       q[-PS + 3],     q[-2 * PS + 2], q[-3 * PS + 1],
-                                q[-3 * PS], q[-3 * PS - 1], q[-2 * PS - 2], q[-PS - 3],
-                                q[-3],      q[PS - 3],      q[2 * PS - 2],  q[3 * PS - 1]};
-            const int S = arc_score_bytes(pr, v);
-            corner = S > lo;
-            if (corner) scm[(ey + 1) * SW + ex + 1] = (uint8_t)(S - 1);
-        }
-        const uint64_t m = __ballot(corner);
-        wave_lds_fence();   // all survivor reads of this chunk precede the in-place writes
-        if (corner) list[ncorner + __popcll(m & below)] = (uint16_t)e;
-        ncorner += __popcll(m);
-    }
-    wave_lds_fence();
-
-    // C. NMS on the corners, both thresholds at once, compacted in row-major
-    //    order into the two lists.  At threshold t >= lo a pixel's FAST score is
-    //    S-1 if S-1 >= t and 0 otherwise (a non-corner), so one score map serves
-    //    both thresholds.
     uint32_t *out_i = fb.cand + (int64_t)b * p.cand_cap + c.slot;
     uint32_t *out_m = fb.cand2 + (int64_t)b * p.cand_cap + c.slot;
-    int base_i = 0, base_m = 0;
-    for (int i0 = 0; i0 < ncorner; i0 += 64) {
-        bool ki = false, km = false;
-        int ey = 0, ex = 0, sv = 0;
-        if (i0 + lane < ncorner) {
-            const int e = list[i0 + lane];
-            ey = e >> 8;
-            ex = e & 0xFF;
-            const int si = (ey + 1) * SW + ex + 1;
-            sv = scm[si];
-            const int nb[8] = {scm[si - 1], scm[si + 1], scm[si - SW - 1], scm[si - SW],
-                               scm[si - SW + 1], scm[si + SW - 1], scm[si + SW], scm[si + SW + 1]};
-            ki = sv >= ini;
-            km = sv >= mnt;
-#pragma unroll
-            for (int t = 0; t < 8; ++t) {
-                ki &= sv > (nb[t] >= ini ? nb[t] : 0);
-                km &= sv > (nb[t] >= mnt ? nb[t] : 0);
-            }
+
+    // One FAST pass at threshold th: returns the keypoints kept after NMS,
+    // written to out.  The reference runs iniThFAST first and minThFAST only
+    // for a cell where that found nothing (ORBextractor.cc:842-850).
+    auto pass = [&](int th, uint32_t *out) -> int {
+        {
+            uint32_t *z0 = reinterpret_cast<uint32_t *>(scm);
+            const int nz = p.fast_score_bytes >> 2;
+            for (int i = lane; i < nz; i += 64) z0[i] = 0;
         }
-        const uint64_t mi = __ballot(ki), mm = __ballot(km);
-        const int pi = base_i + __popcll(mi & below), pm = base_m + __popcll(mm & below);
-        if (ki && pi < c.cap) out_i[pi] = pack_key(c.x0 + ex, c.y0 + ey, sv);
-        if (km && pm < c.cap) out_m[pm] = pack_key(c.x0 + ex, c.y0 + ey, sv);
-        base_i += __popcll(mi);
-        base_m += __popcll(mm);
+        wave_lds_fence();
+        // A. compass pre-test: an arc of 9 covers two cyclically adjacent points
+        //    of {0, 4, 8, 12}, so a pixel is a corner candidate only if some
+        //    adjacent pair is all brighter (min of the pair > v + th) or all
+        //    darker (max of the pair < v - th).  Survivors are compacted.
+        int yy = div_small(lane, cw), xx = lane - yy * cw;
+        int nsurv = 0;
+        for (int i0 = 0; i0 < npx; i0 += 64) {
+            bool surv = false;
+            if (i0 + lane < npx) {
+                const uint8_t *q = pc + yy * PS + xx;
+                const int v = q[0];
+                const int a0 = q[3 * PS], a4 = q[3], a8 = q[-3 * PS], a12 = q[-3];
+                const int hi_pair = max(max(min(a0, a4), min(a8, a12)), max(min(a4, a8), min(a12, a0)));
+                const int lo_pair = min(min(max(a0, a4), max(a8, a12)), min(max(a4, a8), max(a12, a0)));
+                surv = (hi_pair > v + th) | (lo_pair < v - th);
+            }
+            const uint64_t m = __ballot(surv);
+            if (surv) list[nsurv + __popcll(m & below)] = (uint16_t)((yy << 8) | xx);
+            nsurv += __popcll(m);
+            yy += dyc; xx += dxc;
+            if (xx >= cw) { xx -= cw; ++yy; }
+        }
+        wave_lds_fence();
+        // B. arc score of every survivor: S = max(M1 - v, v - M2), M1 = max over
+        //    the 16 nine-pixel arcs of the arc's minimum, M2 = min over arcs of the
+        //    arc's maximum, side by side as packed u16 lanes (p, 255 - p) through
+        //    sliding-window minima (2, 4, 8, 9).  A corner at th iff S > th; its
+        //    FAST score S - 1 goes to the map, corners compacted in place.
+        int ncorner = 0;
+        for (int i0 = 0; i0 < nsurv; i0 += 64) {
+            bool corner = false;
+            int e = 0;
+            if (i0 + lane < nsurv) {
+                e = list[i0 + lane];
+                const int ey = e >> 8, ex = e & 0xFF;
+                const uint8_t *q = pc + ey * PS + ex;
+                const int v = q[0];
+                const int pr[16] = {q[3 * PS],  q[3 * PS + 1],  q[2 * PS + 2],  q[PS + 3],
+                                    q[3],       q[-PS + 3],     q[-2 * PS + 2], q[-3 * PS + 1],
+                                    q[-3 * PS], q[-3 * PS - 1], q[-2 * PS - 2], q[-PS - 3],
+                                    q[-3],      q[PS - 3],      q[2 * PS - 2],  q[3 * PS - 1]};
+                const int S = arc_score_bytes(pr, v);
+                corner = S > th;
+                if (corner) scm[(ey + 1) * SW + ex + 1] = (uint8_t)(S - 1);
+            }
+            const uint64_t m = __ballot(corner);
+            wave_lds_fence();   // all survivor reads of this chunk precede the in-place writes
+            if (corner) list[ncorner + __popcll(m & below)] = (uint16_t)e;
+            ncorner += __popcll(m);
+        }
+        wave_lds_fence();
+        // C. strict 3x3 NMS inside the cell (outside neighbours and non-corners
+        //    score 0), compacted in row-major order.
+        int base = 0;
+        for (int i0 = 0; i0 < ncorner; i0 += 64) {
+            bool keep = false;
+            int ey = 0, ex = 0, sv = 0;
+            if (i0 + lane < ncorner) {
+                const int e = list[i0 + lane];
+                ey = e >> 8;
+                ex = e & 0xFF;
+                const int si = (ey + 1) * SW + ex + 1;
+                sv = scm[si];
+                keep = sv > scm[si - 1] && sv > scm[si + 1] && sv > scm[si - SW - 1] && sv > scm[si - SW] &&
+                       sv > scm[si - SW + 1] && sv > scm[si + SW - 1] && sv > scm[si + SW] && sv > scm[si + SW + 1];
+            }
+            const uint64_t mk = __ballot(keep);
+            const int pk = base + __popcll(mk & below);
+            if (keep && pk < c.cap) out[pk] = pack_key(c.x0 + ex, c.y0 + ey, sv);
+            base += __popcll(mk);
+        }
+        return base;
+    };
+    const int n_ini = pass(p.ini_th, out_i);
+    int32_t cnt;
+    if (n_ini > 0) {
+        cnt = min(n_ini, c.cap);
+    } else {
+        wave_lds_fence();
+        const int n_min = pass(p.min_th, out_m);
+        cnt = (int32_t)(0x80000000u | (uint32_t)min(n_min, c.cap));
     }
-    if (lane == 0)
-        *count_out = base_i > 0 ? min(base_i, c.cap) : (int32_t)(0x80000000u | (uint32_t)min(base_m, c.cap));
+    if (lane == 0) *count_out = cnt;
 }
 
 // ===========================================================================
