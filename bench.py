@@ -59,8 +59,8 @@ def algorithmic_bytes(sizes, nkp: float, stage: str) -> float:
         return 2.0 * p
     if stage == "fast":        # read every level once
         return float(p)
-    if stage == "describe":    # 31x31 disc + 37x37 blurred patch reads, 60 B written per kp
-        return nkp * (961 + 1369 + 60)
+    if stage == "describe":    # the keypoints' neighbourhoods cover the levels: each pixel once, 60 B per kp out
+        return float(p) + nkp * 60
     if stage == "match":       # both frames' descriptors + keypoints read, matches written
         return nkp * (2 * 32 + 2 * 28 + 4)
     if stage == "quadtree":    # candidates in, selection out (counted in the kernel)

@@ -354,9 +354,7 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb) {
     const uint8_t *img = level_ptr(p, fb, c.level, b, spitch);
     const int o = wave_stage_rect(patch, PS, img, spitch, c.y0 - 3, c.x0 - 3, ch + 6, cw + 6, lane);
     const uint8_t *pc = patch + 3 * PS + o + 3;         // interior pixel (0, 0)
-    const int npx = cw * ch;
     const uint64_t below = (1ull << lane) - 1;
-    const int dyc = div_small(64, cw), dxc = 64 - dyc * cw;
     uint32_t *out_i = fb.cand + (int64_t)b * p.cand_cap + c.slot;
     uint32_t *out_m = fb.cand2 + (int64_t)b * p.cand_cap + c.slot;
 
@@ -373,24 +371,43 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb) {
         // A. compass pre-test: an arc of 9 covers two cyclically adjacent points
         //    of {0, 4, 8, 12}, so a pixel is a corner candidate only if some
         //    adjacent pair is all brighter (min of the pair > v + th) or all
-        //    darker (max of the pair < v - th).  Survivors are compacted.
-        int yy = div_small(lane, cw), xx = lane - yy * cw;
+        //    darker (max of the pair < v - th).  A lane tests two horizontally
+        //    adjacent pixels at once in packed u16 halves; survivors are
+        //    compacted in row-major order.
         int nsurv = 0;
-        for (int i0 = 0; i0 < npx; i0 += 64) {
-            bool surv = false;
-            if (i0 + lane < npx) {
-                const uint8_t *q = pc + yy * PS + xx;
-                const int v = q[0];
-                const int a0 = q[3 * PS], a4 = q[3], a8 = q[-3 * PS], a12 = q[-3];
-                const int hi_pair = max(max(min(a0, a4), min(a8, a12)), max(min(a4, a8), min(a12, a0)));
-                const int lo_pair = min(min(max(a0, a4), max(a8, a12)), min(max(a4, a8), max(a12, a0)));
-                surv = (hi_pair > v + th) | (lo_pair < v - th);
+        {
+            const int hw = (cw + 1) >> 1;             // pixel pairs per row
+            const int npairs = hw * ch;
+            const int dyp = div_small(64, hw), dxp = 64 - dyp * hw;
+            int yy = div_small(lane, hw), px = lane - yy * hw;
+            const u16x2 thv = {(unsigned short)th, (unsigned short)th};
+            for (int i0 = 0; i0 < npairs; i0 += 64) {
+                bool s0 = false, s1 = false;
+                const int xx = 2 * px;
+                if (i0 + lane < npairs) {
+                    const uint8_t *q = pc + yy * PS + xx;
+                    auto pr = [&](int d) { return as_u16x2((uint32_t)q[d] | ((uint32_t)q[d + 1] << 16)); };
+                    const u16x2 v = pr(0), a0 = pr(3 * PS), a4 = pr(3), a8 = pr(-3 * PS), a12 = pr(-3);
+                    const u16x2 hi = __builtin_elementwise_max(
+                        __builtin_elementwise_max(__builtin_elementwise_min(a0, a4), __builtin_elementwise_min(a8, a12)),
+                        __builtin_elementwise_max(__builtin_elementwise_min(a4, a8), __builtin_elementwise_min(a12, a0)));
+                    const u16x2 lo = __builtin_elementwise_min(
+                        __builtin_elementwise_min(__builtin_elementwise_max(a0, a4), __builtin_elementwise_max(a8, a12)),
+                        __builtin_elementwise_min(__builtin_elementwise_max(a4, a8), __builtin_elementwise_max(a12, a0)));
+                    // hi > v + th  or  lo + th < v, as saturating differences
+                    const u16x2 d = __builtin_elementwise_sub_sat(hi, v + thv) | __builtin_elementwise_sub_sat(v, lo + thv);
+                    s0 = d.x != 0;
+                    s1 = d.y != 0 && xx + 1 < cw;
+                }
+                const uint64_t m0 = __ballot(s0), m1 = __ballot(s1);
+                const int pos = nsurv + __popcll(m0 & below) + __popcll(m1 & below);
+                const uint16_t e0 = (uint16_t)((yy << 8) | xx);
+                if (s0) list[pos] = e0;
+                if (s1) list[pos + s0] = (uint16_t)(e0 + 1);
+                nsurv += __popcll(m0) + __popcll(m1);
+                yy += dyp; px += dxp;
+                if (px >= hw) { px -= hw; ++yy; }
             }
-            const uint64_t m = __ballot(surv);
-            if (surv) list[nsurv + __popcll(m & below)] = (uint16_t)((yy << 8) | xx);
-            nsurv += __popcll(m);
-            yy += dyc; xx += dxc;
-            if (xx >= cw) { xx -= cw; ++yy; }
         }
         wave_lds_fence();
         // B. arc score of every survivor: S = max(M1 - v, v - M2), M1 = max over
@@ -870,20 +887,29 @@ __global__ __launch_bounds__(kThreads) void k_describe(DevPlan p, FrameBufs fb) 
     wave_lds_fence();
 
     // 2. IC_Angle (ORBextractor.cc:77-104): exact integer moments on the disc.
+    //    A task = 4 consecutive disc columns of one row (31 rows x 8 groups,
+    //    columns -16..15): m10 += sum((u + 16) * I) - 16 sum(I), m01 += v sum(I),
+    //    with v_dot4 on the realigned dword and the bytes outside the row's
+    //    |u| <= umax[|v|] masked off.
     const uint8_t *center = patch + kDescR * kDescPS + kDescR;
-    const int u = (lane & 31) - 15;
-    const int half = lane >> 5;
     int m10 = 0, m01 = 0;
-    if (u <= 15) {
-        for (int v = 0; v <= 15; ++v) {
-            if (half == 1 && v == 0) continue;
-            const int row = half ? -v : v;
-            if (abs(u) <= p.umax[v]) {
-                const int val = center[row * kDescPS + u];
-                m10 += u * val;
-                m01 += row * val;
-            }
-        }
+    for (int t = lane; t < 31 * 8; t += 64) {
+        const int ri = t >> 3, g4 = t & 7;
+        const int v = ri - 15, u0 = 4 * g4 - 16;
+        const int um = p.umax[abs(v)];
+        const int addr = (int)(center - lbase) + v * kDescPS + u0;   // byte offset of column u0
+        const uint32_t *ap = reinterpret_cast<const uint32_t *>(lbase + (addr & ~3));
+        const uint32_t px = __builtin_amdgcn_alignbyte(ap[1], ap[0], addr & 3);
+        // byte k (column u0 + k) kept iff |u0 + k| <= um
+        uint32_t keep = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) keep |= (abs(u0 + k) <= um ? 0xFFu : 0u) << (8 * k);
+        const uint32_t pm = px & keep;
+        const uint32_t wu = (uint32_t)(u0 + 16) | (uint32_t)(u0 + 17) << 8 | (uint32_t)(u0 + 18) << 16 |
+                            (uint32_t)(u0 + 19) << 24;
+        const int sumI = (int)__builtin_amdgcn_udot4(pm, 0x01010101u, 0u, false);
+        m10 += (int)__builtin_amdgcn_udot4(pm, wu, 0u, false) - 16 * sumI;
+        m01 += v * sumI;
     }
     m10 = wave_sum_i32(m10);
     m01 = wave_sum_i32(m01);
@@ -928,12 +954,18 @@ __global__ __launch_bounds__(kThreads) void k_describe(DevPlan p, FrameBufs fb) 
     float sa, ca;
     glibc_sincosf(__fmul_rn(angle, factor_pi), &sa, &ca);
     const int xs = g.w & ~3;
+    // whole sample window left of w & ~3 (almost every keypoint): half-even
+    // rounding everywhere, (s + 0x7FFF + bit16) >> 16, no per-column test
+    const bool all_even = x + kBlurR < xs;
     auto blurred = [&](int r, int c) {   // r, c in [-18, 18]
         const uint16_t *w = rowp + (r + kBlurR) * kRowS + (c + kBlurR);
         const int sum = mul24u(k3, w[3 * kRowS]) + mul24u(k2, w[2 * kRowS] + w[4 * kRowS]) +
                         mul24u(k1, w[kRowS] + w[5 * kRowS]) + mul24u(k0, w[0] + w[6 * kRowS]);
-        int qv = sum >> 16;
-        if (x + c < xs) {
+        int qv;
+        if (all_even) {
+            qv = (sum + 0x7FFF + ((sum >> 16) & 1)) >> 16;
+        } else if (x + c < xs) {
+            qv = sum >> 16;
             const int rem = sum & 0xFFFF;
             qv += (rem > 0x8000) | ((rem == 0x8000) & (qv & 1));
         } else {
