@@ -172,5 +172,6 @@ hipError_t launch_vocab_transform(const VocabDev &v, const uint8_t *feat, int n,
 int match_lds_bytes(int n1cap, int n2cap, int maxq, int maxc);
 int quadtree_lds_bytes(int node_cap);
 bool resize_window_fits(const Plan &hp);
+bool plan_resize_waves(Plan &hp);   // fills hp.rw, or leaves it empty (block kernel)
 
 }  // namespace orbx

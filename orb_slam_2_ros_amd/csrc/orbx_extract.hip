@@ -244,6 +244,117 @@ __global__ __launch_bounds__(kThreads) void k_resize(DevPlan p, FrameBufs fb, in
 }
 
 // ===========================================================================
+// K1 (wave tiles): the same resize with every wave independent.  A wave owns
+// a 4*twg x (64/twg)*kResizeK output tile (ResizeWave, chosen per level so
+// narrow levels waste few lanes), stages the source window it needs in its
+// own LDS slice and writes 4 columns x kResizeK rows per lane.  The window
+// bounds come from the same double/float arithmetic as the tap tables, so the
+// staging loads and the tap loads go out together.  Per source row a lane
+// reads 3 dwords, realigns them, gathers each column's pixel pair (S[sx],
+// S[sx+1]) with one v_perm and applies the horizontal taps with one
+// v_dot2_u32_u16; the vertical pass is OpenCV's fixed point as above.
+// ===========================================================================
+typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+
+__host__ __device__ inline int resize_src_raw(int d, double scale) {
+#ifdef __HIP_DEVICE_COMPILE__
+    const float f = __double2float_rn(__dsub_rn(__dmul_rn(__dadd_rn((double)d, 0.5), scale), 0.5));
+    return (int)floorf(f);
+#else
+    const float f = (float)((d + 0.5) * scale - 0.5);
+    return floor_i(f);
+#endif
+}
+
+__global__ __launch_bounds__(kThreads) void k_resize_w(DevPlan p, FrameBufs fb, int l, ResizeWave a, int B) {
+    extern __shared__ __align__(16) uint8_t lds[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int L = xcd_logical_block(blockIdx.x, gridDim.x);
+    const int t = L * 4 + wave;
+    if (t >= a.ntiles * B) return;
+    const int b = t / a.ntiles, tile = t - b * a.ntiles;
+    const int ty = tile / a.ntx, tx = tile - ty * a.ntx;
+    const LevelArgs g = p.la[l], gs = p.la[l - 1];
+    const int twg = a.twg, lr = lane >> a.twg_shift, lg = lane & (twg - 1);
+    const int TH = (64 >> a.twg_shift) * kResizeK;
+    const int x0 = tx * 4 * twg, y0 = ty * TH;
+    const int xb = x0 + 4 * lg, yb = y0 + lr * kResizeK;
+    // taps of this lane's 4 columns and kResizeK rows (independent of the window loads)
+    const ResizeTap *xt = p.xtaps + p.lv[l].xtab_off;
+    const ResizeTap *yt = p.ytaps + p.lv[l].ytab_off;
+    ResizeTap txk[4], tyk[kResizeK];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) txk[k] = xt[min(xb + k, g.w - 1)];
+#pragma unroll
+    for (int k = 0; k < kResizeK; ++k) tyk[k] = yt[min(yb + k, g.h - 1)];
+    // the source window: columns [c_lo, c_hi], rows [r_lo, r_hi] (as the tables)
+    const int xl = min(x0 + 4 * twg, g.w) - 1, yl = min(y0 + TH, g.h) - 1;
+    const int c_lo = min(max(resize_src_raw(x0, a.sx), 0), gs.w - 1);
+    const int c_hi = min(max(resize_src_raw(xl, a.sx), 0) + 1, gs.w - 1);
+    const int r_lo = min(max(resize_src_raw(y0, a.sy), 0), gs.h - 1);
+    const int r_hi = min(max(resize_src_raw(yl, a.sy) + 1, 0), gs.h - 1);
+    int spitch;
+    const uint8_t *src = level_ptr(p, fb, l - 1, b, spitch);
+    uint8_t *win = lds + wave * a.win_bytes;
+    wave_stage_rect(win, a.win_stride, src, spitch, r_lo, c_lo, r_hi - r_lo + 1, c_hi - c_lo + 1, lane);
+    // per-lane column constants: dword of the first source pixel, realignment,
+    // and the v_perm selectors of the 4 pixel pairs (S[sx_k], S[sx_k + 1])
+    const int rel0 = txk[0].src - (c_lo & ~3);
+    const int q4 = (rel0 >> 2) * 4, o = rel0 & 3;
+    uint32_t sel[4], coef[4];
+    bool simd_all = true;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t r = (uint32_t)(txk[k].src - txk[0].src);
+        sel[k] = r | 0x0C00u | ((r + 1) << 16) | 0x0C000000u;
+        coef[k] = (uint32_t)(uint16_t)txk[k].a0 | ((uint32_t)(uint16_t)txk[k].a1 << 16);
+        simd_all &= (txk[k].mode & 2) != 0;
+    }
+    wave_lds_fence();
+    if (xb >= g.w) return;
+    uint8_t *dst = fb.pyr + (int64_t)b * p.pyr_bytes + g.pyr_off;
+    auto hrow = [&](int row, uint32_t h[4]) {
+        const uint32_t *ap = reinterpret_cast<const uint32_t *>(win + mul24u(row - r_lo, a.win_stride) + q4);
+        const uint32_t d0 = ap[0], d1 = ap[1], d2 = ap[2];
+        const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, o), w1 = __builtin_amdgcn_alignbyte(d2, d1, o);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t pr = __builtin_amdgcn_perm(w1, w0, sel[k]);
+            h[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, pr), __builtin_bit_cast(u16x2_t, coef[k]), 0u,
+                                          false);
+        }
+    };
+#pragma unroll
+    for (int j = 0; j < kResizeK; ++j) {
+        const int y = yb + j;
+        if (y >= g.h) break;
+        const int s0 = min(max((int)tyk[j].src, 0), gs.h - 1), s1 = min(max((int)tyk[j].src + 1, 0), gs.h - 1);
+        const int b0 = tyk[j].a0, b1 = tyk[j].a1;
+        uint32_t h0[4], h1[4];
+        hrow(s0, h0);
+        hrow(s1, h1);
+        // SSE2 columns: _mm_packs_epi32(h>>4); _mm_mulhi_epi16; _mm_adds_epi16; +2; >>2
+        // (h <= 255 * 2048: no saturation, result <= 255); the last < 16 columns
+        // are the scalar tail FixedPtCast<int, uchar, 22>
+        uint32_t packed = 0;
+        if (simd_all) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                packed |= (((mul24u(h0[k] >> 4, b0) >> 16) + (mul24u(h1[k] >> 4, b1) >> 16) + 2) >> 2) << (8 * k);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t v = (txk[k].mode & 2)
+                                       ? ((mul24u(h0[k] >> 4, b0) >> 16) + (mul24u(h1[k] >> 4, b1) >> 16) + 2) >> 2
+                                       : (mul24u(h0[k], b0) + mul24u(h1[k], b1) + (1 << 21)) >> 22;
+                packed |= v << (8 * k);
+            }
+        }
+        *reinterpret_cast<uint32_t *>(dst + mul24u(y, g.pitch) + xb) = packed;
+    }
+}
+
+// ===========================================================================
 // K2: Gaussian 7x7, sigma 2, BORDER_REFLECT_101 on each level (OpenCV 3.2
 // fixed-point separable filter).  The SSE2 column pass accumulates exactly in
 // float and rounds half-to-even; the scalar tail adds 2^15 and shifts: both are
@@ -1015,6 +1126,14 @@ __global__ void k_trig(const float *in, float *so, float *co, int n, const float
 
 // ---------------------------------------------------------------------------
 hipError_t launch_resize(const DevPlan &p, const Plan &hp, const FrameBufs &fb, int B, hipStream_t st) {
+    if (!hp.rw.empty()) {
+        for (int l = 1; l < hp.nlevels; ++l) {
+            const ResizeWave &a = hp.rw[l];
+            const int waves = a.ntiles * B;
+            hipLaunchKernelGGL(k_resize_w, dim3((waves + 3) / 4), dim3(kThreads), 4 * a.win_bytes, st, p, fb, l, a, B);
+        }
+        return hipGetLastError();
+    }
     for (int l = 1; l < hp.nlevels; ++l) {
         const LevelGeom &g = hp.lv[l];
         dim3 grid((g.w + kResTW - 1) / kResTW, (g.h + kResTH - 1) / kResTH, B);
@@ -1058,6 +1177,63 @@ hipError_t launch_trig_check(const float *in, float *s, float *c, float *atan_ou
     if (total <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_trig, dim3((total + 255) / 256), dim3(256), 0, st, in, s, c, n, ay, ax, atan_out, m);
     return hipGetLastError();
+}
+
+// Wave-tile geometry of every level (ResizeWave).  False when some level does
+// not fit the wave kernel (a column group spanning more than 7 source bytes,
+// i.e. scale factors above ~2.3, or a window over the LDS budget); the block
+// kernel k_resize then runs instead.
+bool plan_resize_waves(Plan &hp) {
+    hp.rw.assign(hp.nlevels, ResizeWave{});
+    for (int l = 1; l < hp.nlevels; ++l) {
+        const LevelGeom &g = hp.lv[l], &gs = hp.lv[l - 1];
+        const ResizeTap *xt = hp.xtaps.data() + g.xtab_off;
+        const ResizeTap *yt = hp.ytaps.data() + g.ytab_off;
+        ResizeWave a;
+        a.sx = 1. / ((double)g.w / gs.w);
+        a.sy = 1. / ((double)g.h / gs.h);
+        int best = -1;
+        for (int sh = 6; sh >= 4; --sh) {
+            const int cols = 4 << sh, n = (g.w + cols - 1) / cols;
+            if (best < 0 || n * cols < best) { best = n * cols; a.twg_shift = sh; }
+        }
+        a.twg = 1 << a.twg_shift;
+        const int TW = 4 * a.twg, TH = (64 >> a.twg_shift) * kResizeK;
+        a.ntx = (g.w + TW - 1) / TW;
+        const int nty = (g.h + TH - 1) / TH;
+        a.ntiles = a.ntx * nty;
+        int nd_max = 0;
+        for (int tx = 0; tx < a.ntx; ++tx) {
+            const int x0 = tx * TW, xl = std::min(x0 + TW, g.w) - 1;
+            const int c_lo = std::min(std::max(resize_src_raw(x0, a.sx), 0), gs.w - 1);
+            const int c_hi = std::min(std::max(resize_src_raw(xl, a.sx), 0) + 1, gs.w - 1);
+            // the kernel's arithmetic bounds must be the tables' (and cover them)
+            if (c_lo != xt[x0].src || c_hi < std::min((int)xt[xl].src + 1, gs.w - 1)) return false;
+            nd_max = std::max(nd_max, ((c_lo & 3) + c_hi - c_lo + 1 + 3) >> 2);
+            for (int xb = x0; xb <= xl; xb += 4) {
+                const int s0 = xt[xb].src, s3 = xt[std::min(xb + 3, g.w - 1)].src;
+                if (s3 - s0 + 1 > 7) return false;   // pair bytes within the 8 realigned ones
+                nd_max = std::max(nd_max, ((s0 - (c_lo & ~3)) >> 2) + 3);
+            }
+        }
+        int nr_max = 0;
+        for (int ty = 0; ty < nty; ++ty) {
+            const int y0 = ty * TH, yl = std::min(y0 + TH, g.h) - 1;
+            const int r_lo = std::min(std::max(resize_src_raw(y0, a.sy), 0), gs.h - 1);
+            const int r_hi = std::min(std::max(resize_src_raw(yl, a.sy) + 1, 0), gs.h - 1);
+            for (int y = y0; y <= yl; ++y) {
+                const int s0 = std::min(std::max((int)yt[y].src, 0), gs.h - 1);
+                const int s1 = std::min(std::max((int)yt[y].src + 1, 0), gs.h - 1);
+                if (s0 < r_lo || s1 > r_hi) return false;
+            }
+            nr_max = std::max(nr_max, r_hi - r_lo + 1);
+        }
+        a.win_stride = 4 * nd_max;
+        a.win_bytes = (nr_max * a.win_stride + 15) & ~15;
+        if (4 * a.win_bytes > 64 * 1024) return false;
+        hp.rw[l] = a;
+    }
+    return true;
 }
 
 bool resize_window_fits(const Plan &hp) {

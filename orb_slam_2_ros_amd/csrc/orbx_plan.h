@@ -74,6 +74,19 @@ struct LevelGeom {
     int xtab_off, ytab_off;          // into the plan's resize tap tables (levels >= 1)
 };
 
+// Wave-tile geometry of one pyramid level's resize (k_resize): a wave owns
+// 4*twg columns x (64/twg)*kResizeK rows; lane (lr, lg) writes columns
+// x0 + 4 lg .. + 3 of rows y0 + lr kResizeK + j.  twg in {16, 32, 64} is chosen
+// per level to waste the fewest columns at the right edge.
+constexpr int kResizeK = 4;
+struct ResizeWave {
+    double sx = 0, sy = 0;     // source / destination size ratio, as make_resize_taps
+    int twg = 64, twg_shift = 6;
+    int ntx = 0, ntiles = 0;   // tiles per row of tiles, per frame
+    int win_stride = 0;        // LDS bytes per window row (dword multiple)
+    int win_bytes = 0;         // LDS bytes per wave (16-B multiple)
+};
+
 struct Plan {
     int width = 0, height = 0;
     int nfeatures = 0, nlevels = 0, ini_th = 0, min_th = 0;
@@ -89,6 +102,7 @@ struct Plan {
     int out_cap = 0;          // staging slots per frame (sum of level out_cap)
     int max_kps = 0;          // keypoint capacity per frame
     int max_quota = 0;
+    std::vector<ResizeWave> rw;   // per level (index 0 unused); empty: k_resize_lds path
 };
 
 inline int pitch_of(int w) { return (w + 63) & ~63; }

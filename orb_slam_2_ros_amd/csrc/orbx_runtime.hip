@@ -239,6 +239,7 @@ int reserve(orbx_extractor *ex, int w, int h, int max_batch) {
         if (g.ncols > 0 && g.nrows > 0 && g.nini <= 0) return ORBX_EINVAL;
     }
     if (!resize_window_fits(ex->plan)) return ORBX_EINVAL;
+    if (!plan_resize_waves(ex->plan) || std::getenv("ORBX_RESIZE_BLOCKS")) ex->plan.rw.clear();
     int rc = upload_plan(ex);
     if (rc) return rc;
     const Plan &p = ex->plan;

@@ -64,6 +64,33 @@ def test_stages_bit_exact(w, h, nfeat, seed, extractors, oracle_mod):
     assert np.array_equal(dg, do), f"descriptors differ at {_first_diff(dg, do)}"
 
 
+PYRAMID_CASES = [
+    # (w, h, scale, nlevels, seed): odd sizes, narrow / wide levels, every wave-tile width
+    # (16 / 32 / 64 column groups) and scale 2.0 (7-byte column spans)
+    (97, 71, 1.2, 4, 41),
+    (1023, 767, 1.2, 8, 42),
+    (480, 700, 1.2, 8, 43),
+    (1280, 720, 1.3, 8, 44),
+    (640, 480, 2.0, 4, 45),
+    (1920, 1080, 1.2, 8, 47),
+]
+
+
+@pytest.mark.parametrize("w,h,scale,nlev,seed", PYRAMID_CASES)
+@pytest.mark.parametrize("blocks", [False, True])
+def test_pyramid_sizes_and_scales(w, h, scale, nlev, seed, blocks, oracle_mod, monkeypatch):
+    """cv::resize chain (k_resize_w wave tiles, or the k_resize block kernel) vs the oracle."""
+    if blocks:
+        monkeypatch.setenv("ORBX_RESIZE_BLOCKS", "1")
+    img = synth.frame(w, h, seed)
+    ex = ORBextractor(500, scale, nlev, 20, 7)
+    ex(img)
+    pyr = oracle_mod.pyramid(img, scale, nlev)
+    for l in range(nlev):
+        gp = ex.debug_fetch(0, l, 0)
+        assert np.array_equal(gp, pyr[l]), f"pyramid level {l} differs at {_first_diff(gp, pyr[l])}"
+
+
 PARAM_VARIANTS = [
     # (w, h, nfeatures, scale, nlevels, iniThFAST, minThFAST, seed)
     (640, 480, 1000, 1.2, 8, 7, 20, 31),     # ini < min: corners found at the lower threshold
