@@ -17,7 +17,7 @@
 
 namespace orbx {
 
-__constant__ int8_t c_pattern[512][2] = {
+__constant__ __attribute__((aligned(16))) int8_t c_pattern[512][2] = {
 #define ORBX_PATTERN_BEGIN
 #define ORBX_PATTERN_END
 #include "orb_pattern.inc"
@@ -65,6 +65,11 @@ __device__ inline void xcd_block_2d(int &bx, int &by) {
     by = L / gridDim.x;
     bx = L - by * gridDim.x;
 }
+
+// The wave's index in its workgroup as a scalar: the compiler cannot prove
+// threadIdx.x >> 6 wave-uniform, so everything derived from it would live in
+// VGPRs and branch per lane.
+__device__ inline int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
 __device__ inline int reflect101(int v, int n) {
     // BORDER_REFLECT_101 for the 3-px halo of a >= 4 px image.
@@ -130,11 +135,13 @@ __device__ inline int div_small(int a, int b) {
 
 // ===========================================================================
 // Wave-cooperative staging of an image rectangle into LDS with aligned dword
-// loads, 8 in flight per lane before any LDS store.  Pixel (r, c) of the
+// loads, NB in flight per lane before any LDS store (a rectangle of up to
+// 64 * NB dwords costs one global round trip).  Pixel (r, c) of the
 // rectangle lands at dst[r * ds + o + c]; returns o = x0 & 3.  The caller
 // guarantees a 4-aligned image base and pitch and that the aligned span
 // [x0 & ~3, x0 + nc rounded up to 4) lies inside the row's pitch.
 // ===========================================================================
+template <int NB = 8>
 __device__ inline int wave_stage_rect(uint8_t *dst, int ds, const uint8_t *img, int pitch, int y0, int x0,
                                       int nr, int nc, int lane) {
     const int xa = x0 & ~3, o = x0 - xa;
@@ -143,17 +150,17 @@ __device__ inline int wave_stage_rect(uint8_t *dst, int ds, const uint8_t *img, 
     const int dr = div_small(64, nd), dk = 64 - dr * nd;
     const int r_l = div_small(lane, nd), k_l = lane - r_l * nd;
     const uint8_t *base = img + (int64_t)y0 * pitch + xa;
-    for (int i0 = 0, r0 = r_l, k0 = k_l; i0 < total; i0 += 64 * 8) {
-        uint32_t v[8];
+    for (int i0 = 0, r0 = r_l, k0 = k_l; i0 < total; i0 += 64 * NB) {
+        uint32_t v[NB];
         int r = r0, k = k0;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < NB; ++j) {
             if (i0 + 64 * j + lane < total) v[j] = *reinterpret_cast<const uint32_t *>(base + mul24u(r, pitch) + 4 * k);
             r += dr; k += dk; if (k >= nd) { k -= nd; ++r; }
         }
         r = r0; k = k0;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < NB; ++j) {
             if (i0 + 64 * j + lane < total) *reinterpret_cast<uint32_t *>(dst + mul24u(r, ds) + 4 * k) = v[j];
             r += dr; k += dk; if (k >= nd) { k -= nd; ++r; }
         }
@@ -266,9 +273,10 @@ __host__ __device__ inline int resize_src_raw(int d, double scale) {
 #endif
 }
 
+template <int NB>
 __global__ __launch_bounds__(kThreads) void k_resize_w(DevPlan p, FrameBufs fb, int l, ResizeWave a, int B) {
     extern __shared__ __align__(16) uint8_t lds[];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = wave_id(), lane = threadIdx.x & 63;
     const int L = xcd_logical_block(blockIdx.x, gridDim.x);
     const int t = L * 4 + wave;
     if (t >= a.ntiles * B) return;
@@ -296,7 +304,7 @@ __global__ __launch_bounds__(kThreads) void k_resize_w(DevPlan p, FrameBufs fb, 
     int spitch;
     const uint8_t *src = level_ptr(p, fb, l - 1, b, spitch);
     uint8_t *win = lds + wave * a.win_bytes;
-    wave_stage_rect(win, a.win_stride, src, spitch, r_lo, c_lo, r_hi - r_lo + 1, c_hi - c_lo + 1, lane);
+    wave_stage_rect<NB>(win, a.win_stride, src, spitch, r_lo, c_lo, r_hi - r_lo + 1, c_hi - c_lo + 1, lane);
     // per-lane column constants: dword of the first source pixel, realignment,
     // and the v_perm selectors of the 4 pixel pairs (S[sx_k], S[sx_k + 1])
     const int rel0 = txk[0].src - (c_lo & ~3);
@@ -445,7 +453,7 @@ __device__ inline int arc_score_bytes(const int p[16], int v) {
 
 __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb) {
     extern __shared__ __align__(16) uint8_t lds[];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = wave_id(), lane = threadIdx.x & 63;
     int bx, b;
     xcd_block_2d(bx, b);
     const int ci = bx * 4 + wave;
@@ -941,9 +949,14 @@ constexpr int kRowS = 40;                   // row-pass stride (u16): 10 groups 
 constexpr int kDescRowOff = (kDescP * kDescPS + 15) & ~15;          // row-pass buffer, 16-aligned
 constexpr int kDescWaveLds = kDescRowOff + kDescP * kRowS * 2;        // 5680 B
 
-__global__ __launch_bounds__(kThreads) void k_describe(DevPlan p, FrameBufs fb) {
+__global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs fb) {
     __shared__ __align__(16) uint8_t lds[4 * ((kDescWaveLds + 15) & ~15)];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+    // this lane's 4 pattern pairs (bytes x0 y0 x1 y1 of pairs 2j, 2j + 1,
+    // j = 64 grp + lane), fetched first so the loads overlap the staging
+    uint32_t pat[4];
+#pragma unroll
+    for (int grp = 0; grp < 4; ++grp) pat[grp] = reinterpret_cast<const uint32_t *>(c_pattern)[grp * 64 + lane];
     int bx, b;
     xcd_block_2d(bx, b);
     const int32_t *lc = fb.level_count + (int64_t)b * kMaxLevels;
@@ -953,7 +966,7 @@ __global__ __launch_bounds__(kThreads) void k_describe(DevPlan p, FrameBufs fb) 
     int l = 0;
 #pragma unroll
     for (int q = 1; q < kMaxLevels; ++q) l += (q < p.nlevels && slot >= p.la[q].out_off) ? 1 : 0;
-    const uint32_t key = slot < p.out_cap ? fb.sel[(int64_t)b * p.out_cap + slot] : 0u;
+    const uint32_t key = slot < p.out_cap ? __builtin_amdgcn_readfirstlane(fb.sel[(int64_t)b * p.out_cap + slot]) : 0u;
     int cnt[kMaxLevels];
 #pragma unroll
     for (int q = 0; q < kMaxLevels; ++q) cnt[q] = q < p.nlevels ? max(lc[q], 0) : 0;
@@ -986,7 +999,8 @@ __global__ __launch_bounds__(kThreads) void k_describe(DevPlan p, FrameBufs fb) 
     int o = 0;
     if (px0 >= 0 && py0 >= 0 && x + kDescR < g.w && y + kDescR < g.h &&
         (px0 & ~3) + 4 * (((px0 & 3) + kDescP + 3) >> 2) <= spitch) {
-        o = wave_stage_rect(lbase, kDescPS, img, spitch, py0, px0, kDescP, kDescP, lane);
+        o = wave_stage_rect<(kDescP * ((kDescP + 6) / 4) + 63) / 64>(lbase, kDescPS, img, spitch, py0, px0, kDescP, kDescP,
+                                                                   lane);
     } else {
         for (int e = lane; e < kDescP * kDescP; e += 64) {
             const int r = e / kDescP, c = e - r * kDescP;
@@ -1068,37 +1082,47 @@ __global__ __launch_bounds__(kThreads) void k_describe(DevPlan p, FrameBufs fb) 
     // whole sample window left of w & ~3 (almost every keypoint): half-even
     // rounding everywhere, (s + 0x7FFF + bit16) >> 16, no per-column test
     const bool all_even = x + kBlurR < xs;
-    auto blurred = [&](int r, int c) {   // r, c in [-18, 18]
-        const uint16_t *w = rowp + (r + kBlurR) * kRowS + (c + kBlurR);
-        const int sum = mul24u(k3, w[3 * kRowS]) + mul24u(k2, w[2 * kRowS] + w[4 * kRowS]) +
-                        mul24u(k1, w[kRowS] + w[5 * kRowS]) + mul24u(k0, w[0] + w[6 * kRowS]);
-        int qv;
-        if (all_even) {
-            qv = (sum + 0x7FFF + ((sum >> 16) & 1)) >> 16;
-        } else if (x + c < xs) {
-            qv = sum >> 16;
-            const int rem = sum & 0xFFFF;
-            qv += (rem > 0x8000) | ((rem == 0x8000) & (qv & 1));
-        } else {
-            qv = (sum + (1 << 15)) >> 16;
+    // all 8 of the lane's samples: offsets, then every column-pass read in
+    // flight at once, then the rounding
+    int sums[8], cols[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t pw = pat[k >> 1] >> (16 * (k & 1));
+        const float px = (float)(int8_t)pw, py = (float)(int8_t)(pw >> 8);
+        const int r = __float2int_rn(__fadd_rn(__fmul_rn(px, sa), __fmul_rn(py, ca)));
+        const int cc = __float2int_rn(__fsub_rn(__fmul_rn(px, ca), __fmul_rn(py, sa)));
+        cols[k] = cc;
+        const uint16_t *w = rowp + (r + kBlurR) * kRowS + (cc + kBlurR);   // r, cc in [-18, 18]
+        sums[k] = mul24u(k3, w[3 * kRowS]) + mul24u(k2, w[2 * kRowS] + w[4 * kRowS]) +
+                  mul24u(k1, w[kRowS] + w[5 * kRowS]) + mul24u(k0, w[0] + w[6 * kRowS]);
+    }
+    int val[8];
+    if (all_even) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) val[k] = min((sums[k] + 0x7FFF + ((sums[k] >> 16) & 1)) >> 16, 255);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int sum = sums[k];
+            int qv;
+            if (x + cols[k] < xs) {
+                qv = sum >> 16;
+                const int rem = sum & 0xFFFF;
+                qv += (rem > 0x8000) | ((rem == 0x8000) & (qv & 1));
+            } else {
+                qv = (sum + (1 << 15)) >> 16;
+            }
+            val[k] = min(qv, 255);
         }
-        return min(qv, 255);
-    };
+    }
     const int64_t kp_index = (int64_t)b * p.max_kps + off + i;
-    uint64_t *dout = reinterpret_cast<uint64_t *>(fb.desc + kp_index * 32);
+    uint64_t m[4];
 #pragma unroll
-    for (int grp = 0; grp < 4; ++grp) {
-        const int j = grp * 64 + lane;
-        int val[2];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const float px = (float)c_pattern[2 * j + e][0], py = (float)c_pattern[2 * j + e][1];
-            const int r = __float2int_rn(__fadd_rn(__fmul_rn(px, sa), __fmul_rn(py, ca)));
-            const int cc = __float2int_rn(__fsub_rn(__fmul_rn(px, ca), __fmul_rn(py, sa)));
-            val[e] = blurred(r, cc);
-        }
-        const uint64_t m = __ballot(val[0] < val[1]);
-        if (lane == 0) dout[grp] = m;
+    for (int grp = 0; grp < 4; ++grp) m[grp] = __ballot(val[2 * grp] < val[2 * grp + 1]);
+    if (lane == 0) {
+        ulonglong2 *dout = reinterpret_cast<ulonglong2 *>(fb.desc + kp_index * 32);
+        dout[0] = make_ulonglong2(m[0], m[1]);
+        dout[1] = make_ulonglong2(m[2], m[3]);
     }
     if (lane == 0) {
         orbx_keypoint kp;
@@ -1130,7 +1154,12 @@ hipError_t launch_resize(const DevPlan &p, const Plan &hp, const FrameBufs &fb, 
         for (int l = 1; l < hp.nlevels; ++l) {
             const ResizeWave &a = hp.rw[l];
             const int waves = a.ntiles * B;
-            hipLaunchKernelGGL(k_resize_w, dim3((waves + 3) / 4), dim3(kThreads), 4 * a.win_bytes, st, p, fb, l, a, B);
+            // one global round trip for the whole window when it fits 64 x 9 / 64 x 16 dwords
+            if (a.win_dwords <= 64 * 9)
+                hipLaunchKernelGGL(k_resize_w<9>, dim3((waves + 3) / 4), dim3(kThreads), 4 * a.win_bytes, st, p, fb, l, a, B);
+            else
+                hipLaunchKernelGGL(k_resize_w<16>, dim3((waves + 3) / 4), dim3(kThreads), 4 * a.win_bytes, st, p, fb, l, a,
+                                   B);
         }
         return hipGetLastError();
     }
@@ -1202,14 +1231,15 @@ bool plan_resize_waves(Plan &hp) {
         a.ntx = (g.w + TW - 1) / TW;
         const int nty = (g.h + TH - 1) / TH;
         a.ntiles = a.ntx * nty;
-        int nd_max = 0;
+        int nd_max = 0, nd_win = 0;
         for (int tx = 0; tx < a.ntx; ++tx) {
             const int x0 = tx * TW, xl = std::min(x0 + TW, g.w) - 1;
             const int c_lo = std::min(std::max(resize_src_raw(x0, a.sx), 0), gs.w - 1);
             const int c_hi = std::min(std::max(resize_src_raw(xl, a.sx), 0) + 1, gs.w - 1);
             // the kernel's arithmetic bounds must be the tables' (and cover them)
             if (c_lo != xt[x0].src || c_hi < std::min((int)xt[xl].src + 1, gs.w - 1)) return false;
-            nd_max = std::max(nd_max, ((c_lo & 3) + c_hi - c_lo + 1 + 3) >> 2);
+            nd_win = std::max(nd_win, ((c_lo & 3) + c_hi - c_lo + 1 + 3) >> 2);
+            nd_max = std::max(nd_max, nd_win);
             for (int xb = x0; xb <= xl; xb += 4) {
                 const int s0 = xt[xb].src, s3 = xt[std::min(xb + 3, g.w - 1)].src;
                 if (s3 - s0 + 1 > 7) return false;   // pair bytes within the 8 realigned ones
@@ -1229,6 +1259,7 @@ bool plan_resize_waves(Plan &hp) {
             nr_max = std::max(nr_max, r_hi - r_lo + 1);
         }
         a.win_stride = 4 * nd_max;
+        a.win_dwords = nr_max * nd_win;
         a.win_bytes = (nr_max * a.win_stride + 15) & ~15;
         if (4 * a.win_bytes > 64 * 1024) return false;
         hp.rw[l] = a;

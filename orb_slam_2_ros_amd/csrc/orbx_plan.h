@@ -78,13 +78,14 @@ struct LevelGeom {
 // 4*twg columns x (64/twg)*kResizeK rows; lane (lr, lg) writes columns
 // x0 + 4 lg .. + 3 of rows y0 + lr kResizeK + j.  twg in {16, 32, 64} is chosen
 // per level to waste the fewest columns at the right edge.
-constexpr int kResizeK = 4;
+constexpr int kResizeK = 8;
 struct ResizeWave {
     double sx = 0, sy = 0;     // source / destination size ratio, as make_resize_taps
     int twg = 64, twg_shift = 6;
     int ntx = 0, ntiles = 0;   // tiles per row of tiles, per frame
     int win_stride = 0;        // LDS bytes per window row (dword multiple)
     int win_bytes = 0;         // LDS bytes per wave (16-B multiple)
+    int win_dwords = 0;        // largest window, in staged dwords
 };
 
 struct Plan {
