@@ -358,10 +358,23 @@ def run_config(torch, dist, rank, world, dev, w, h, nfeatures, batch, steps, war
             ex.rgbd_step_device(frames[t].data_ptr(), fstride, w, batch, dmaps.data_ptr(), 4 * fstride, 4 * w, bf, sp)
 
     sync = lambda: torch.cuda.synchronize(dev)   # noqa: E731
-    el = timed_region(step, steps, max(warmup, 2), sync, dist, world,
-                      on_start=lambda: ex.set_profiling(profile))
-    stages = ex.stage_times() if profile else None
-    ex.set_profiling(False)
+    el = timed_region(step, steps, max(warmup, 2), sync, dist, world)
+    stages = None
+    if profile:
+        # per-stage launch durations (HIP events on the launch stream) from a
+        # separate untimed pass with the level pipeline off (if it was on), so
+        # each stage is one whole-batch launch that overlaps nothing
+        piped = ex.pipeline()
+        ex.pipeline(0)
+        step(steps)
+        sync()
+        ex.set_profiling(True)
+        for k in range(max(5, steps // 5)):
+            step(steps + 1 + k)
+        sync()
+        stages = ex.stage_times()
+        ex.set_profiling(False)
+        ex.pipeline(piped)
     # sanity: the last step produced keypoints and matches / depths on stream 0
     kp, _ = ex.batch_download(0)
     if mode == "mono":
@@ -397,6 +410,7 @@ def main() -> int:
                     help="skip the secondary FHD / stereo / RGB-D configurations")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--extra", default=None, help="time only this EXTRAS config (diagnostics; prints its dict)")
     args = ap.parse_args()
 
     import torch
@@ -410,6 +424,16 @@ def main() -> int:
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     profile = not args.no_profile
+
+    if args.extra:
+        for key, mode, ew, eh, enf, eb, unit in EXTRAS:
+            if key == args.extra:
+                el2, st2, nk2, sane2, _ = run_config(torch, dist, rank, world, dev, ew, eh, enf, eb, args.steps,
+                                                     args.warmup, profile, mode)
+                if rank == 0:
+                    print(json.dumps({"extra": key, "value": round(world * eb * args.steps / el2, 2), "unit": unit,
+                                      "stage_ms": st2, "kps_last_frame": nk2}), flush=True)
+        return 0
 
     w, h, nf, B = args.width, args.height, args.nfeatures, args.batch
     el, stages, nkp_last, nm_last, frames_per_launch = run_config(torch, dist, rank, world, dev, w, h, nf, B, args.steps,

@@ -119,6 +119,15 @@ int orbx_mono_matches_download(orbx_extractor *ex, int frame, int32_t *matches12
  * Returns the current setting.  Batches under 64 frames are never split. */
 int orbx_extractor_split(orbx_extractor *ex, int parts);
 
+/* Level pipeline (default off): a step's extraction runs in two level groups
+ * on internal streams forked from and joined to the launch stream -- level 0's
+ * FAST, quadtree and describe beside the resize chain and levels 1.. -- so
+ * level 0's work overlaps the latency-bound resize chain.  Outputs are
+ * identical either way.  on: 1 / 0 sets, -1 queries; returns the current
+ * setting.  Stage times (orbx_extractor_stage_times) cover the extractor
+ * stages only with the pipeline off. */
+int orbx_extractor_pipeline(orbx_extractor *ex, int on);
+
 /* Per-stage device time of the last batch (HIP events on the launch stream),
  * in ms, when profiling is enabled: resize, blur, fast, quadtree, describe,
  * match.  Returns the number of stages written. */

@@ -137,6 +137,13 @@ struct BowBufs {
 enum Stage { kStageResize = 0, kStageBlur, kStageFast, kStageQuadtree, kStageDescribe, kStageMatch, kNumStages };
 
 hipError_t launch_resize(const DevPlan &p, const Plan &hp, const FrameBufs &fb, int B, hipStream_t s);
+// Per-level launches of the level-pipelined step (orbx_extractor_pipeline).
+hipError_t launch_resize_level(const DevPlan &p, const Plan &hp, const FrameBufs &fb, int B, hipStream_t s, int l);
+// (levels [l, l_end))
+hipError_t launch_fast_level(const DevPlan &p, const Plan &hp, const FrameBufs &fb, int B, hipStream_t s, int l, int l_end);
+hipError_t launch_quadtree_level(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t s, int l, int l_end);
+hipError_t launch_describe_level(const DevPlan &p, const Plan &hp, const FrameBufs &fb, int B, hipStream_t s, int l,
+                                 int l_end);
 hipError_t launch_blur(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t s);
 hipError_t launch_fast(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t s);
 hipError_t launch_quadtree(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t s);

@@ -451,13 +451,16 @@ __device__ inline int arc_score_bytes(const int p[16], int v) {
     return max((int)best.x - v, v - (255 - (int)best.y));
 }
 
-__global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb) {
+// PIPE: a level's cells in a level-pipelined step (a distinct instantiation so
+// profiles tell per-level launches from whole-batch ones).
+template <bool PIPE>
+__global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int c0, int nc) {
     extern __shared__ __align__(16) uint8_t lds[];
     const int wave = wave_id(), lane = threadIdx.x & 63;
     int bx, b;
     xcd_block_2d(bx, b);
-    const int ci = bx * 4 + wave;
-    if (ci >= p.ncells) return;
+    if (bx * 4 + wave >= nc) return;
+    const int ci = c0 + bx * 4 + wave;
     const Cell c = p.cells[ci];
     int32_t *count_out = fb.cell_count + (int64_t)b * p.ncells + ci;
     const int cw = c.x1 - c.x0, ch = c.y1 - c.y0;
@@ -684,9 +687,10 @@ __device__ void bitonic_desc(uint64_t *a, int np2) {
     }
 }
 
-__global__ __launch_bounds__(kThreads) void k_quadtree(DevPlan p, FrameBufs fb) {
+template <bool PIPE>
+__global__ __launch_bounds__(kThreads) void k_quadtree(DevPlan p, FrameBufs fb, int l0) {
     extern __shared__ __align__(16) uint8_t lds[];
-    const int l = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+    const int l = l0 + blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
     const LevelGeom g = p.lv[l];
     const int N = g.quota, NC = p.node_cap;
     QLds s;
@@ -949,7 +953,8 @@ constexpr int kRowS = 40;                   // row-pass stride (u16): 10 groups 
 constexpr int kDescRowOff = (kDescP * kDescPS + 15) & ~15;          // row-pass buffer, 16-aligned
 constexpr int kDescWaveLds = kDescRowOff + kDescP * kRowS * 2;        // 5680 B
 
-__global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs fb) {
+template <bool PIPE>
+__global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs fb, int s0, int ns, int write_total) {
     __shared__ __align__(16) uint8_t lds[4 * ((kDescWaveLds + 15) & ~15)];
     const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
     // this lane's 4 pattern pairs (bytes x0 y0 x1 y1 of pairs 2j, 2j + 1,
@@ -960,7 +965,7 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
     int bx, b;
     xcd_block_2d(bx, b);
     const int32_t *lc = fb.level_count + (int64_t)b * kMaxLevels;
-    const int slot = bx * 4 + wave;
+    const int slot = s0 + bx * 4 + wave;
     // level of this slot from the kernel-argument offsets; the key and the
     // level counts are independent loads issued together
     int l = 0;
@@ -970,13 +975,13 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
     int cnt[kMaxLevels];
 #pragma unroll
     for (int q = 0; q < kMaxLevels; ++q) cnt[q] = q < p.nlevels ? max(lc[q], 0) : 0;
-    if (bx == 0 && tid == 0) {
+    if (write_total && bx == 0 && tid == 0) {
         int total = 0;
 #pragma unroll
         for (int q = 0; q < kMaxLevels; ++q) total += cnt[q];
         fb.nkps[b] = total;
     }
-    if (slot >= p.out_cap) return;
+    if (slot >= p.out_cap || bx * 4 + wave >= ns) return;
     const LevelArgs g = p.la[l];
     const int i = slot - g.out_off;
     int off = 0, cl = 0;
@@ -1149,26 +1154,27 @@ __global__ void k_trig(const float *in, float *so, float *co, int n, const float
 }  // namespace
 
 // ---------------------------------------------------------------------------
-hipError_t launch_resize(const DevPlan &p, const Plan &hp, const FrameBufs &fb, int B, hipStream_t st) {
+hipError_t launch_resize_level(const DevPlan &p, const Plan &hp, const FrameBufs &fb, int B, hipStream_t st, int l) {
     if (!hp.rw.empty()) {
-        for (int l = 1; l < hp.nlevels; ++l) {
-            const ResizeWave &a = hp.rw[l];
-            const int waves = a.ntiles * B;
-            // one global round trip for the whole window when it fits 64 x 9 / 64 x 16 dwords
-            if (a.win_dwords <= 64 * 9)
-                hipLaunchKernelGGL(k_resize_w<9>, dim3((waves + 3) / 4), dim3(kThreads), 4 * a.win_bytes, st, p, fb, l, a, B);
-            else
-                hipLaunchKernelGGL(k_resize_w<16>, dim3((waves + 3) / 4), dim3(kThreads), 4 * a.win_bytes, st, p, fb, l, a,
-                                   B);
-        }
+        const ResizeWave &a = hp.rw[l];
+        const int waves = a.ntiles * B;
+        // one global round trip for the whole window when it fits 64 x 9 / 64 x 16 dwords
+        if (a.win_dwords <= 64 * 9)
+            hipLaunchKernelGGL(k_resize_w<9>, dim3((waves + 3) / 4), dim3(kThreads), 4 * a.win_bytes, st, p, fb, l, a, B);
+        else
+            hipLaunchKernelGGL(k_resize_w<16>, dim3((waves + 3) / 4), dim3(kThreads), 4 * a.win_bytes, st, p, fb, l, a, B);
         return hipGetLastError();
     }
-    for (int l = 1; l < hp.nlevels; ++l) {
-        const LevelGeom &g = hp.lv[l];
-        dim3 grid((g.w + kResTW - 1) / kResTW, (g.h + kResTH - 1) / kResTH, B);
-        hipLaunchKernelGGL(k_resize, grid, dim3(kThreads), 0, st, p, fb, l);
-    }
+    const LevelGeom &g = hp.lv[l];
+    dim3 grid((g.w + kResTW - 1) / kResTW, (g.h + kResTH - 1) / kResTH, B);
+    hipLaunchKernelGGL(k_resize, grid, dim3(kThreads), 0, st, p, fb, l);
     return hipGetLastError();
+}
+
+hipError_t launch_resize(const DevPlan &p, const Plan &hp, const FrameBufs &fb, int B, hipStream_t st) {
+    for (int l = 1; l < hp.nlevels; ++l)
+        if (launch_resize_level(p, hp, fb, B, st, l) != hipSuccess) return hipErrorLaunchFailure;
+    return hipSuccess;
 }
 
 hipError_t launch_blur(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t st) {
@@ -1177,7 +1183,16 @@ hipError_t launch_blur(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t
 }
 
 hipError_t launch_fast(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t st) {
-    hipLaunchKernelGGL(k_fast, dim3((p.ncells + 3) / 4, B), dim3(kThreads), 4 * p.fast_lds_per_wave, st, p, fb);
+    hipLaunchKernelGGL(k_fast<false>, dim3((p.ncells + 3) / 4, B), dim3(kThreads), 4 * p.fast_lds_per_wave, st, p, fb, 0,
+                       p.ncells);
+    return hipGetLastError();
+}
+
+hipError_t launch_fast_level(const DevPlan &p, const Plan &hp, const FrameBufs &fb, int B, hipStream_t st, int l,
+                             int l_end) {
+    const int c0 = hp.lv[l].cell_begin, nc = hp.lv[l_end - 1].cell_end - c0;
+    if (nc <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fast<true>, dim3((nc + 3) / 4, B), dim3(kThreads), 4 * p.fast_lds_per_wave, st, p, fb, c0, nc);
     return hipGetLastError();
 }
 
@@ -1190,13 +1205,29 @@ hipError_t allow_lds(K kernel, int bytes) {
 }
 
 hipError_t launch_quadtree(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t st) {
-    if (allow_lds(k_quadtree, p.node_lds_bytes) != hipSuccess) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_quadtree, dim3(p.nlevels, B), dim3(kThreads), p.node_lds_bytes, st, p, fb);
+    if (allow_lds(k_quadtree<false>, p.node_lds_bytes) != hipSuccess) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_quadtree<false>, dim3(p.nlevels, B), dim3(kThreads), p.node_lds_bytes, st, p, fb, 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_quadtree_level(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t st, int l, int l_end) {
+    if (allow_lds(k_quadtree<true>, p.node_lds_bytes) != hipSuccess) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_quadtree<true>, dim3(l_end - l, B), dim3(kThreads), p.node_lds_bytes, st, p, fb, l);
     return hipGetLastError();
 }
 
 hipError_t launch_describe(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t st) {
-    hipLaunchKernelGGL(k_describe, dim3((p.out_cap + 3) / 4, B), dim3(kThreads), 0, st, p, fb);
+    hipLaunchKernelGGL(k_describe<false>, dim3((p.out_cap + 3) / 4, B), dim3(kThreads), 0, st, p, fb, 0, p.out_cap, 1);
+    return hipGetLastError();
+}
+
+// Levels [l, l_end)'s keypoints; the launch with the last level also writes each
+// frame's keypoint total (every level's count is final by then).
+hipError_t launch_describe_level(const DevPlan &p, const Plan &hp, const FrameBufs &fb, int B, hipStream_t st, int l,
+                                 int l_end) {
+    const int s0 = hp.lv[l].out_off, ns = hp.lv[l_end - 1].out_off + hp.lv[l_end - 1].out_cap - s0;
+    hipLaunchKernelGGL(k_describe<true>, dim3((ns + 3) / 4, B), dim3(kThreads), 0, st, p, fb, s0, ns,
+                       l_end == hp.nlevels ? 1 : 0);
     return hipGetLastError();
 }
 

@@ -183,6 +183,10 @@ class ORBextractor:
         """Batch split into sub-batches on internal streams (0 = query)."""
         return check(self._lib.orbx_extractor_split(self._h, int(parts)), "split")
 
+    def pipeline(self, on: int = -1) -> int:
+        """Level-pipelined extraction on internal streams (1 on, 0 off, -1 query)."""
+        return check(self._lib.orbx_extractor_pipeline(self._h, int(on)), "pipeline")
+
     def set_profiling(self, on: bool) -> None:
         check(self._lib.orbx_extractor_set_profiling(self._h, int(on)), "set_profiling")
 

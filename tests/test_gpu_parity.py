@@ -129,11 +129,19 @@ def test_search_for_initialization(w, h, nfeat, seed, extractors, oracle_mod):
         assert nm_g > 0
 
 
-def test_batch_and_mono_step_match_single(extractors, oracle_mod):
+@pytest.mark.parametrize("pipeline,split", [(1, 1), (0, 1), (0, 2), (1, 2)])
+def test_batch_and_mono_step_match_single(pipeline, split, extractors, oracle_mod):
+    """A batched mono step (level pipeline on / off, batch split in 1 or 2
+    parts) gives every stream the oracle's keypoints, descriptors and matches."""
     import torch
-    w, h, B = 640, 480, 4
+    w, h = 640, 480
+    B = 4 if split == 1 else 64    # batches under 64 frames are never split
     ex = ORBextractor(1000, 1.2, 8, 20, 7)
-    seqs = [synth.frames(w, h, 500 + s, 2) for s in range(B)]
+    ex.pipeline(pipeline)
+    ex.split(split)
+    assert ex.pipeline() == pipeline and ex.split() == split
+    seqs = [synth.frames(w, h, 500 + s, 2) for s in range(min(B, 6))]
+    seqs = [seqs[b % len(seqs)] for b in range(B)]
     ex.reserve(w, h, B)
     dev = torch.device("cuda:0")
     t0 = torch.from_numpy(np.stack([s[0] for s in seqs])).to(dev)
@@ -141,7 +149,7 @@ def test_batch_and_mono_step_match_single(extractors, oracle_mod):
     torch.cuda.synchronize()
     ex.mono_step_device(t0.data_ptr(), w * h, w, B)
     ex.mono_step_device(t1.data_ptr(), w * h, w, B)
-    for b in range(B):
+    for b in sorted({0, 1, 2, 3, B // 2 - 1, B // 2, B - 1}):
         kg, dg = ex.batch_download(b)
         ko, do = oracle_mod.extract(seqs[b][1])
         assert len(kg) == len(ko) and (kg == ko).all() and np.array_equal(dg, do)
