@@ -25,6 +25,25 @@ __constant__ __attribute__((aligned(16))) int8_t c_pattern[512][2] = {
 #undef ORBX_PATTERN_END
 };
 
+// c_disc_mask[ri][g]: byte k kept iff column 4g - 16 + k lies in row ri - 15
+// of the orientation disc (kUmax, orbx_plan.h).
+struct DiscMask {
+    uint32_t m[32][8];
+    constexpr DiscMask() : m() {
+        for (int ri = 0; ri < 32; ++ri)
+            for (int g = 0; g < 8; ++g) {
+                uint32_t keep = 0;
+                const int v = ri - 15, av = v < 0 ? -v : v;
+                for (int k = 0; k < 4; ++k) {
+                    const int u = 4 * g - 16 + k, au = u < 0 ? -u : u;
+                    if (ri < 31 && au <= kUmax[av]) keep |= 0xFFu << (8 * k);
+                }
+                m[ri][g] = keep;
+            }
+    }
+};
+__constant__ DiscMask c_disc_mask = DiscMask();
+
 namespace {
 
 constexpr int kThreads = 256;
@@ -959,9 +978,11 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
     const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
     // this lane's 4 pattern pairs (bytes x0 y0 x1 y1 of pairs 2j, 2j + 1,
     // j = 64 grp + lane), fetched first so the loads overlap the staging
-    uint32_t pat[4];
+    uint32_t pat[4], dmask[4];
 #pragma unroll
     for (int grp = 0; grp < 4; ++grp) pat[grp] = reinterpret_cast<const uint32_t *>(c_pattern)[grp * 64 + lane];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dmask[i] = c_disc_mask.m[(lane >> 3) + 8 * i][lane & 7];
     int bx, b;
     xcd_block_2d(bx, b);
     const int32_t *lc = fb.level_count + (int64_t)b * kMaxLevels;
@@ -1021,25 +1042,29 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
     //    columns -16..15): m10 += sum((u + 16) * I) - 16 sum(I), m01 += v sum(I),
     //    with v_dot4 on the realigned dword and the bytes outside the row's
     //    |u| <= umax[|v|] masked off.
+    // The lane's column group g = lane & 7 is the same in every iteration (row
+    // ri = lane / 8 + 8 i), so the weights and the LDS offsets are fixed.
     const uint8_t *center = patch + kDescR * kDescPS + kDescR;
-    int m10 = 0, m01 = 0;
-    for (int t = lane; t < 31 * 8; t += 64) {
-        const int ri = t >> 3, g4 = t & 7;
-        const int v = ri - 15, u0 = 4 * g4 - 16;
-        const int um = p.umax[abs(v)];
-        const int addr = (int)(center - lbase) + v * kDescPS + u0;   // byte offset of column u0
-        const uint32_t *ap = reinterpret_cast<const uint32_t *>(lbase + (addr & ~3));
-        const uint32_t px = __builtin_amdgcn_alignbyte(ap[1], ap[0], addr & 3);
-        // byte k (column u0 + k) kept iff |u0 + k| <= um
-        uint32_t keep = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) keep |= (abs(u0 + k) <= um ? 0xFFu : 0u) << (8 * k);
-        const uint32_t pm = px & keep;
+    int m10, m01 = 0;
+    {
+        const int g4 = lane & 7, u0 = 4 * g4 - 16, r0 = lane >> 3;
         const uint32_t wu = (uint32_t)(u0 + 16) | (uint32_t)(u0 + 17) << 8 | (uint32_t)(u0 + 18) << 16 |
                             (uint32_t)(u0 + 19) << 24;
-        const int sumI = (int)__builtin_amdgcn_udot4(pm, 0x01010101u, 0u, false);
-        m10 += (int)__builtin_amdgcn_udot4(pm, wu, 0u, false) - 16 * sumI;
-        m01 += v * sumI;
+        const int addr = (int)(center - lbase) + (r0 - 15) * kDescPS + u0;   // byte offset of column u0, row r0 - 15
+        const uint32_t *ap = reinterpret_cast<const uint32_t *>(lbase + (addr & ~3));
+        const int sh = addr & 3;
+        uint32_t s1 = 0, s0 = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int ri = r0 + 8 * i;   // < 32; row 31 has an all-zero mask
+            const uint32_t px = __builtin_amdgcn_alignbyte(ap[i * 2 * kDescPS + 1], ap[i * 2 * kDescPS], sh);
+            const uint32_t pm = px & dmask[i];
+            const uint32_t si = __builtin_amdgcn_udot4(pm, 0x01010101u, 0u, false);
+            s1 = __builtin_amdgcn_udot4(pm, wu, s1, false);
+            s0 += si;
+            m01 += (ri - 15) * (int)si;
+        }
+        m10 = (int)s1 - 16 * (int)s0;
     }
     m10 = wave_sum_i32(m10);
     m01 = wave_sum_i32(m01);
@@ -1097,7 +1122,7 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
         const int r = __float2int_rn(__fadd_rn(__fmul_rn(px, sa), __fmul_rn(py, ca)));
         const int cc = __float2int_rn(__fsub_rn(__fmul_rn(px, ca), __fmul_rn(py, sa)));
         cols[k] = cc;
-        const uint16_t *w = rowp + (r + kBlurR) * kRowS + (cc + kBlurR);   // r, cc in [-18, 18]
+        const uint16_t *w = rowp + mul24u(r + kBlurR, kRowS) + (cc + kBlurR);   // r, cc in [-18, 18]
         sums[k] = mul24u(k3, w[3 * kRowS]) + mul24u(k2, w[2 * kRowS] + w[4 * kRowS]) +
                   mul24u(k1, w[kRowS] + w[5 * kRowS]) + mul24u(k0, w[0] + w[6 * kRowS]);
     }

@@ -29,6 +29,9 @@ constexpr int kFastCell = 30;      // W, ORBextractor.cc:788
 // cvRound(256 * getGaussianKernel(7, 2, CV_32F)) = {18, 34, 49, 55, 49, 34, 18};
 // make_gauss_taps recomputes it from the OpenCV formula and the runtime checks both agree.
 constexpr int kGaussTaps[7] = {18, 34, 49, 55, 49, 34, 18};
+// umax of the orientation disc (HALF_PATCH_SIZE 15, ORBextractor.cc:461-478);
+// make_plan recomputes it and the runtime checks both agree.
+constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
 
 // x86-64 cvRound (cvtss2si / cvtsd2si): round half to even.
 inline int round_even(float v) { return (int)std::nearbyint(v); }

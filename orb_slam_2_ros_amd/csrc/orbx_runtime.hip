@@ -215,6 +215,8 @@ int upload_plan(orbx_extractor *ex) {
         if (p.gauss[i] != kGaussTaps[i]) return ORBX_EINVAL;   // kernels use the constant taps
     }
     for (int i = 0; i < 16; ++i) d.umax[i] = p.umax[i];
+    for (int i = 0; i < 16; ++i)
+        if (p.umax[i] != kUmax[i]) return ORBX_EINVAL;   // k_describe's disc masks are built from kUmax
     d.ini_th = std::min(std::max(p.ini_th, 0), 255);
     d.min_th = std::min(std::max(p.min_th, 0), 255);
     d.pyr_bytes = p.pyr_bytes;
