@@ -1079,19 +1079,19 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
     constexpr uint32_t kW0 = (uint32_t)kGaussTaps[0] | (uint32_t)kGaussTaps[1] << 8 |
                              (uint32_t)kGaussTaps[2] << 16 | (uint32_t)kGaussTaps[3] << 24;
     constexpr uint32_t kW1 = (uint32_t)kGaussTaps[4] | (uint32_t)kGaussTaps[5] << 8 | (uint32_t)kGaussTaps[6] << 16;
-    // One task = 4 consecutive outputs (columns 4s..4s+3) of one row: three
-    // realigned dwords hold the 10 source bytes; outputs 37..39 are padding.
+    // One task = 4 consecutive outputs of one row at patch-aligned columns
+    // 4s..4s+3 (window column = patch column - o): the 10 source bytes lie in
+    // three aligned dwords.  Window columns 0..36 are patch columns o..o+36,
+    // within the 40 computed; the others are padding.
     for (int t = lane; t < kDescP * 10; t += 64) {
         const int r = (t * 205) >> 11, sgi = t - r * 10;   // t / 10 for t < 1024
         const uint32_t *ap = reinterpret_cast<const uint32_t *>(lbase + r * kDescPS + 4 * sgi);
-        const uint32_t d0 = ap[0], d1 = ap[1], d2 = ap[2], d3 = ap[3];
-        const uint32_t e0 = __builtin_amdgcn_alignbyte(d1, d0, o), e1 = __builtin_amdgcn_alignbyte(d2, d1, o),
-                       e2 = __builtin_amdgcn_alignbyte(d3, d2, o);
+        const uint32_t d0 = ap[0], d1 = ap[1], d2 = ap[2];
         uint32_t out[4];
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
-            const uint32_t lo4 = m ? __builtin_amdgcn_alignbyte(e1, e0, m) : e0;
-            const uint32_t hi4 = m ? __builtin_amdgcn_alignbyte(e2, e1, m) : e1;
+            const uint32_t lo4 = m ? __builtin_amdgcn_alignbyte(d1, d0, m) : d0;
+            const uint32_t hi4 = m ? __builtin_amdgcn_alignbyte(d2, d1, m) : d1;
             out[m] = __builtin_amdgcn_udot4(lo4, kW0, __builtin_amdgcn_udot4(hi4, kW1, 0u, false), false);
         }
         uint2 packed;
@@ -1122,7 +1122,7 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
         const int r = __float2int_rn(__fadd_rn(__fmul_rn(px, sa), __fmul_rn(py, ca)));
         const int cc = __float2int_rn(__fsub_rn(__fmul_rn(px, ca), __fmul_rn(py, sa)));
         cols[k] = cc;
-        const uint16_t *w = rowp + mul24u(r + kBlurR, kRowS) + (cc + kBlurR);   // r, cc in [-18, 18]
+        const uint16_t *w = rowp + mul24u(r + kBlurR, kRowS) + (cc + kBlurR + o);   // r, cc in [-18, 18]
         sums[k] = mul24u(k3, w[3 * kRowS]) + mul24u(k2, w[2 * kRowS] + w[4 * kRowS]) +
                   mul24u(k1, w[kRowS] + w[5 * kRowS]) + mul24u(k0, w[0] + w[6 * kRowS]);
     }
