@@ -664,22 +664,63 @@ struct QLds {
     int np2;
 };
 
-__device__ void child_stats(const QLds &s, int S, const uint32_t *keys, const uint16_t *knode,
-                            uint8_t *kq, int n) {
+// The level's keys, each with its node index and quadrant.  R > 0: thread t
+// holds keys t + 256 j (j < R) in registers for the whole distribution (the
+// rounds then touch no global memory); R == 0: they stay in global scratch.
+constexpr int kQRegKeys = 8;
+template <int R>
+struct QKeys {
+    uint32_t key[R > 0 ? R : 1];
+    uint32_t nq[R > 0 ? R : 1];   // node | quadrant << 16
+    uint32_t *gkeys;
+    uint16_t *gnode;
+    uint8_t *gq;
+    int n;
+    template <typename F>
+    __device__ inline void each(F f) {
+        if constexpr (R > 0) {
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                const int k = (int)threadIdx.x + j * kThreads;
+                if (k < n) f(j, k);
+            }
+        } else {
+            for (int k = threadIdx.x; k < n; k += kThreads) f(0, k);
+        }
+    }
+    __device__ inline uint32_t get_key(int j, int k) const {
+        if constexpr (R > 0) return key[j]; else return gkeys[k];
+    }
+    __device__ inline int node(int j, int k) const {
+        if constexpr (R > 0) return (int)(nq[j] & 0xFFFF); else return gnode[k];
+    }
+    __device__ inline int quad(int j, int k) const {
+        if constexpr (R > 0) return (int)(nq[j] >> 16); else return gq[k];
+    }
+    __device__ inline void set_node(int j, int k, int nd) {
+        if constexpr (R > 0) nq[j] = (nq[j] & 0xFFFF0000u) | (uint32_t)nd; else gnode[k] = (uint16_t)nd;
+    }
+    __device__ inline void set_quad(int j, int k, int q) {
+        if constexpr (R > 0) nq[j] = (nq[j] & 0xFFFFu) | ((uint32_t)q << 16); else gq[k] = (uint8_t)q;
+    }
+};
+
+template <int R>
+__device__ void child_stats(const QLds &s, int S, QKeys<R> &K) {
     const int tid = threadIdx.x;
     for (int i = tid; i < 4 * S; i += kThreads) { s.ccnt[i] = 0; s.cbest[i] = 0; }
     __syncthreads();
-    for (int k = tid; k < n; k += kThreads) {
-        const int nd = knode[k];
+    K.each([&](int j, int k) {
+        const int nd = K.node(j, k);
         const QNode node = s.cur[nd];
         if (node.count > 1) {
-            const uint32_t key = keys[k];
+            const uint32_t key = K.get_key(j, k);
             const int q = quadrant_of(node, key);
-            kq[k] = (uint8_t)q;
+            K.set_quad(j, k, q);
             atomicAdd(&s.ccnt[4 * nd + q], 1u);
             atomicMax(&s.cbest[4 * nd + q], best_pack(key, k));
         }
-    }
+    });
     __syncthreads();
 }
 
@@ -706,72 +747,30 @@ __device__ void bitonic_desc(uint64_t *a, int np2) {
     }
 }
 
-template <bool PIPE>
-__global__ __launch_bounds__(kThreads) void k_quadtree(DevPlan p, FrameBufs fb, int l0) {
-    extern __shared__ __align__(16) uint8_t lds[];
-    const int l = l0 + blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
-    const LevelGeom g = p.lv[l];
+// Phases 2-5 of k_quadtree on the gathered keys (ORBextractor.cc:566-784).
+template <int NR>
+__device__ void quadtree_rounds(const DevPlan &p, const FrameBufs &fb, QLds &s, const LevelGeom &g, int b, int l,
+                                QKeys<NR> &K) {
+    const int tid = threadIdx.x;
     const int N = g.quota, NC = p.node_cap;
-    QLds s;
-    s.np2 = 1;
-    while (s.np2 < NC) s.np2 <<= 1;
-    uint8_t *ptr = lds;
-    s.a64 = reinterpret_cast<uint64_t *>(ptr); ptr += sizeof(uint64_t) * s.np2;
-    s.b64 = reinterpret_cast<uint64_t *>(ptr); ptr += sizeof(uint64_t) * s.np2;
-    s.cur = reinterpret_cast<QNode *>(ptr); ptr += sizeof(QNode) * NC;
-    s.nxt = reinterpret_cast<QNode *>(ptr); ptr += sizeof(QNode) * NC;
-    s.ccnt = reinterpret_cast<uint32_t *>(ptr); ptr += sizeof(uint32_t) * 4 * NC;
-    s.cbest = reinterpret_cast<uint32_t *>(ptr); ptr += sizeof(uint32_t) * 4 * NC;
-    s.nidx_c = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * 4 * NC;
-    s.nidx_s = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * NC;
-    s.mark = ptr;
-    __shared__ uint64_t ws64[4];
-    __shared__ int ws32[4];
-    __shared__ int sh_S, sh_R;
-
-    const int64_t kbase = (int64_t)b * p.cand_cap + g.cand_off;
-    uint32_t *keys = fb.keys + kbase;
-    uint16_t *knode = fb.key_node + kbase;
-    uint8_t *kq = fb.key_q + kbase;
+    const uint32_t *keys = K.gkeys;
     int32_t *level_count = fb.level_count + (int64_t)b * kMaxLevels + l;
-
-    // ---- 1. gather the level's candidates in cell order (the order the
-    //         reference pushes them into vToDistributeKeys)
-    const int ncell = g.cell_end - g.cell_begin;
-    int base = 0;
-    for (int c0 = 0; c0 < ncell; c0 += kThreads) {
-        const int c = c0 + tid;
-        const int word = c < ncell ? fb.cell_count[(int64_t)b * p.ncells + g.cell_begin + c] : 0;
-        const int cnt = word & 0x7FFFFFFF;
-        int tot;
-        const int ex = block_excl_scan_i32(cnt, &tot, ws32);
-        if (cnt > 0) {
-            const uint32_t *src = (word < 0 ? fb.cand2 : fb.cand) + (int64_t)b * p.cand_cap +
-                                  p.cells[g.cell_begin + c].slot;
-            for (int k = 0; k < cnt; ++k) keys[base + ex + k] = src[k];
-        }
-        base += tot;
-    }
-    const int n = base;
-    __syncthreads();
-    if (n == 0 || g.nini <= 0) {
-        if (tid == 0) *level_count = 0;
-        return;
-    }
+    __shared__ uint64_t ws64[4];
+    __shared__ int sh_S, sh_R;
 
     // ---- 2. root nodes (ORBextractor.cc:566-613)
     const int nini = g.nini;
     for (int i = tid; i < nini; i += kThreads) { s.ccnt[i] = 0; s.cbest[i] = 0; }
     __syncthreads();
-    for (int k = tid; k < n; k += kThreads) {
-        const uint32_t key = keys[k];
+    K.each([&](int j, int k) {
+        const uint32_t key = K.get_key(j, k);
         const float rx = (float)((int)(key & 0xFFF) - kBorder);
         int r = (int)__fdiv_rn(rx, g.hx);
         r = min(r, nini - 1);
-        knode[k] = (uint16_t)r;
+        K.set_node(j, k, r);
         atomicAdd(&s.ccnt[r], 1u);
         atomicMax(&s.cbest[r], best_pack(key, k));
-    }
+    });
     __syncthreads();
     if (tid == 0) {
         int S = 0;
@@ -792,14 +791,14 @@ __global__ __launch_bounds__(kThreads) void k_quadtree(DevPlan p, FrameBufs fb, 
         sh_S = S;
     }
     __syncthreads();
-    for (int k = tid; k < n; k += kThreads) knode[k] = (uint16_t)s.nidx_s[knode[k]];
+    K.each([&](int j, int k) { K.set_node(j, k, s.nidx_s[K.node(j, k)]); });
     __syncthreads();
 
     // ---- 3. full rounds (ORBextractor.cc:618-696)
     bool final_phase = false;
     while (true) {
         const int S = sh_S;
-        child_stats(s, S, keys, knode, kq, n);
+        child_stats(s, S, K);
         for (int i = tid; i < S; i += kThreads) {
             uint64_t v = 0;
             if (s.cur[i].count > 1) {
@@ -839,10 +838,10 @@ __global__ __launch_bounds__(kThreads) void k_quadtree(DevPlan p, FrameBufs fb, 
             }
         }
         __syncthreads();
-        for (int k = tid; k < n; k += kThreads) {
-            const int nd = knode[k];
-            knode[k] = (uint16_t)(s.cur[nd].count > 1 ? s.nidx_c[4 * nd + kq[k]] : s.nidx_s[nd]);
-        }
+        K.each([&](int j, int k) {
+            const int nd = K.node(j, k);
+            K.set_node(j, k, s.cur[nd].count > 1 ? s.nidx_c[4 * nd + K.quad(j, k)] : s.nidx_s[nd]);
+        });
         {
             QNode *t = s.cur; s.cur = s.nxt; s.nxt = t;
         }
@@ -855,7 +854,7 @@ __global__ __launch_bounds__(kThreads) void k_quadtree(DevPlan p, FrameBufs fb, 
     // ---- 4. final phase (ORBextractor.cc:697-762)
     while (final_phase) {
         const int S = sh_S;
-        child_stats(s, S, keys, knode, kq, n);
+        child_stats(s, S, K);
         for (int i = tid; i < s.np2; i += kThreads) {
             uint64_t v = 0;
             if (i < S && s.cur[i].count > 1)
@@ -931,10 +930,10 @@ __global__ __launch_bounds__(kThreads) void k_quadtree(DevPlan p, FrameBufs fb, 
             s.nidx_s[i] = (int16_t)ni;
         }
         __syncthreads();
-        for (int k = tid; k < n; k += kThreads) {
-            const int nd = knode[k];
-            knode[k] = (uint16_t)(s.mark[nd] ? s.nidx_c[4 * nd + kq[k]] : s.nidx_s[nd]);
-        }
+        K.each([&](int j, int k) {
+            const int nd = K.node(j, k);
+            K.set_node(j, k, s.mark[nd] ? s.nidx_c[4 * nd + K.quad(j, k)] : s.nidx_s[nd]);
+        });
         {
             QNode *t = s.cur; s.cur = s.nxt; s.nxt = t;
         }
@@ -952,6 +951,69 @@ __global__ __launch_bounds__(kThreads) void k_quadtree(DevPlan p, FrameBufs fb, 
         sel[i] = keys[k];
     }
     if (tid == 0) *level_count = S <= g.out_cap ? S : -1;
+}
+
+template <bool PIPE>
+__global__ __launch_bounds__(kThreads) void k_quadtree(DevPlan p, FrameBufs fb, int l0) {
+    extern __shared__ __align__(16) uint8_t lds[];
+    const int l = l0 + blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+    const LevelGeom g = p.lv[l];
+    const int NC = p.node_cap;
+    QLds s;
+    s.np2 = 1;
+    while (s.np2 < NC) s.np2 <<= 1;
+    uint8_t *ptr = lds;
+    s.a64 = reinterpret_cast<uint64_t *>(ptr); ptr += sizeof(uint64_t) * s.np2;
+    s.b64 = reinterpret_cast<uint64_t *>(ptr); ptr += sizeof(uint64_t) * s.np2;
+    s.cur = reinterpret_cast<QNode *>(ptr); ptr += sizeof(QNode) * NC;
+    s.nxt = reinterpret_cast<QNode *>(ptr); ptr += sizeof(QNode) * NC;
+    s.ccnt = reinterpret_cast<uint32_t *>(ptr); ptr += sizeof(uint32_t) * 4 * NC;
+    s.cbest = reinterpret_cast<uint32_t *>(ptr); ptr += sizeof(uint32_t) * 4 * NC;
+    s.nidx_c = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * 4 * NC;
+    s.nidx_s = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * NC;
+    s.mark = ptr;
+    __shared__ int ws32[4];
+
+    const int64_t kbase = (int64_t)b * p.cand_cap + g.cand_off;
+    uint32_t *keys = fb.keys + kbase;
+    uint16_t *knode = fb.key_node + kbase;
+    uint8_t *kq = fb.key_q + kbase;
+    int32_t *level_count = fb.level_count + (int64_t)b * kMaxLevels + l;
+
+    // ---- 1. gather the level's candidates in cell order (the order the
+    //         reference pushes them into vToDistributeKeys)
+    const int ncell = g.cell_end - g.cell_begin;
+    int base = 0;
+    for (int c0 = 0; c0 < ncell; c0 += kThreads) {
+        const int c = c0 + tid;
+        const int word = c < ncell ? fb.cell_count[(int64_t)b * p.ncells + g.cell_begin + c] : 0;
+        const int cnt = word & 0x7FFFFFFF;
+        int tot;
+        const int ex = block_excl_scan_i32(cnt, &tot, ws32);
+        if (cnt > 0) {
+            const uint32_t *src = (word < 0 ? fb.cand2 : fb.cand) + (int64_t)b * p.cand_cap +
+                                  p.cells[g.cell_begin + c].slot;
+            for (int k = 0; k < cnt; ++k) keys[base + ex + k] = src[k];
+        }
+        base += tot;
+    }
+    const int n = base;
+    __syncthreads();
+    if (n == 0 || g.nini <= 0) {
+        if (tid == 0) *level_count = 0;
+        return;
+    }
+    // up to kQRegKeys keys per thread stay in registers through the rounds
+    if (n <= kQRegKeys * kThreads) {
+        QKeys<kQRegKeys> K;
+        K.gkeys = keys; K.gnode = knode; K.gq = kq; K.n = n;
+        K.each([&](int j, int k) { K.key[j] = keys[k]; K.nq[j] = 0; });
+        quadtree_rounds(p, fb, s, g, b, l, K);
+    } else {
+        QKeys<0> K;
+        K.gkeys = keys; K.gnode = knode; K.gq = kq; K.n = n;
+        quadtree_rounds(p, fb, s, g, b, l, K);
+    }
 }
 
 // ===========================================================================
