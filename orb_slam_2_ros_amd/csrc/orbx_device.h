@@ -37,6 +37,7 @@ struct DevPlan {
     int fast_patch_stride, fast_patch_bytes, fast_score_bytes, fast_lds_per_wave;
     int node_cap;             // quadtree node capacity (max over levels)
     int node_lds_bytes;       // dynamic LDS of the quadtree kernel
+    int dbg_stop;             // diagnostics only (ORBX_DBG_STOP): end k_quadtree after phase n (0 = off)
 };
 
 // Per-batch device buffers.  Frame b of a batch uses the b-th slice of each.

@@ -794,6 +794,7 @@ __device__ void quadtree_rounds(const DevPlan &p, const FrameBufs &fb, QLds &s, 
     K.each([&](int j, int k) { K.set_node(j, k, s.nidx_s[K.node(j, k)]); });
     __syncthreads();
 
+    if (p.dbg_stop == 2) return;
     // ---- 3. full rounds (ORBextractor.cc:618-696)
     bool final_phase = false;
     while (true) {
@@ -851,6 +852,7 @@ __device__ void quadtree_rounds(const DevPlan &p, const FrameBufs &fb, QLds &s, 
         if (S2 + nexp * 3 > N) { final_phase = true; break; }
     }
 
+    if (p.dbg_stop == 3) return;
     // ---- 4. final phase (ORBextractor.cc:697-762)
     while (final_phase) {
         const int S = sh_S;
@@ -946,15 +948,23 @@ __device__ void quadtree_rounds(const DevPlan &p, const FrameBufs &fb, QLds &s, 
     const int S = sh_S;
     uint32_t *sel = fb.sel + (int64_t)b * p.out_cap + g.out_off;
     const int S_out = min(S, g.out_cap);
-    for (int i = tid; i < S_out; i += kThreads) {
-        const int k = 0xFFFFFF - (int)(s.cur[i].best & 0xFFFFFF);
-        sel[i] = keys[k];
+    if constexpr (NR > 0) {
+        // the owner of each node's best key writes it (keys live in registers)
+        K.each([&](int j, int k) {
+            const int nd = K.node(j, k);
+            if (nd < S_out && 0xFFFFFF - (int)(s.cur[nd].best & 0xFFFFFF) == k) sel[nd] = K.key[j];
+        });
+    } else {
+        for (int i = tid; i < S_out; i += kThreads) {
+            const int k = 0xFFFFFF - (int)(s.cur[i].best & 0xFFFFFF);
+            sel[i] = keys[k];
+        }
     }
     if (tid == 0) *level_count = S <= g.out_cap ? S : -1;
 }
 
 template <bool PIPE>
-__global__ __launch_bounds__(kThreads) void k_quadtree(DevPlan p, FrameBufs fb, int l0) {
+__global__ __launch_bounds__(kThreads, 6) void k_quadtree(DevPlan p, FrameBufs fb, int l0) {
     extern __shared__ __align__(16) uint8_t lds[];
     const int l = l0 + blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
     const LevelGeom g = p.lv[l];
@@ -981,8 +991,11 @@ __global__ __launch_bounds__(kThreads) void k_quadtree(DevPlan p, FrameBufs fb, 
     int32_t *level_count = fb.level_count + (int64_t)b * kMaxLevels + l;
 
     // ---- 1. gather the level's candidates in cell order (the order the
-    //         reference pushes them into vToDistributeKeys)
+    //         reference pushes them into vToDistributeKeys): per-cell start
+    //         offsets and sources in LDS (the node arrays are free until phase 2)
     const int ncell = g.cell_end - g.cell_begin;
+    int *cell_off = reinterpret_cast<int *>(lds);            // ncell + 1
+    int *cell_src = cell_off + ncell + 1;                    // slot | bit 31: minThFAST list
     int base = 0;
     for (int c0 = 0; c0 < ncell; c0 += kThreads) {
         const int c = c0 + tid;
@@ -990,28 +1003,43 @@ __global__ __launch_bounds__(kThreads) void k_quadtree(DevPlan p, FrameBufs fb, 
         const int cnt = word & 0x7FFFFFFF;
         int tot;
         const int ex = block_excl_scan_i32(cnt, &tot, ws32);
-        if (cnt > 0) {
-            const uint32_t *src = (word < 0 ? fb.cand2 : fb.cand) + (int64_t)b * p.cand_cap +
-                                  p.cells[g.cell_begin + c].slot;
-            for (int k = 0; k < cnt; ++k) keys[base + ex + k] = src[k];
+        if (c < ncell) {
+            cell_off[c] = base + ex;
+            cell_src[c] = p.cells[g.cell_begin + c].slot | (word < 0 ? (int)0x80000000 : 0);
         }
         base += tot;
     }
     const int n = base;
+    if (tid == 0) cell_off[ncell] = n;
     __syncthreads();
+    if (p.dbg_stop == 1) return;
     if (n == 0 || g.nini <= 0) {
         if (tid == 0) *level_count = 0;
         return;
     }
+    const uint32_t *cand = fb.cand + (int64_t)b * p.cand_cap, *cand2 = fb.cand2 + (int64_t)b * p.cand_cap;
+    // key k: the cell whose range [off[c], off[c+1]) holds it, by bisection
+    auto fetch = [&](int k) {
+        int lo = 0, hi = ncell - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (cell_off[mid] <= k) lo = mid; else hi = mid - 1;
+        }
+        const int src = cell_src[lo];
+        return ((src < 0) ? cand2 : cand)[(src & 0x7FFFFFFF) + (k - cell_off[lo])];
+    };
     // up to kQRegKeys keys per thread stay in registers through the rounds
     if (n <= kQRegKeys * kThreads) {
         QKeys<kQRegKeys> K;
-        K.gkeys = keys; K.gnode = knode; K.gq = kq; K.n = n;
-        K.each([&](int j, int k) { K.key[j] = keys[k]; K.nq[j] = 0; });
+        K.gkeys = nullptr; K.gnode = knode; K.gq = kq; K.n = n;
+        K.each([&](int j, int k) { K.key[j] = fetch(k); K.nq[j] = 0; });
+        __syncthreads();   // the cell tables are dead from here
         quadtree_rounds(p, fb, s, g, b, l, K);
     } else {
         QKeys<0> K;
         K.gkeys = keys; K.gnode = knode; K.gq = kq; K.n = n;
+        for (int k = tid; k < n; k += kThreads) keys[k] = fetch(k);
+        __syncthreads();
         quadtree_rounds(p, fb, s, g, b, l, K);
     }
 }
