@@ -67,8 +67,6 @@ struct MatchBufs {
     float *prev_xy;           // B * k1_stride * 2, in/out
     int32_t *matches12;       // B * k1_stride
     int32_t *nmatches;        // B
-    uint32_t *scratch;        // B * scratch_stride (candidate lists)
-    int64_t scratch_stride;
     int img_w, img_h, window;
     float nnratio;
     int check_ori;

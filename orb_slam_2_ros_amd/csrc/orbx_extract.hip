@@ -188,10 +188,6 @@ __device__ inline int wave_stage_rect(uint8_t *dst, int ds, const uint8_t *img, 
     return o;
 }
 
-__device__ inline void wave_lds_fence() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
 
 // ===========================================================================
 // K1: bilinear level l from level l-1 (cv::resize INTER_LINEAR 8U, OpenCV 3.2

@@ -46,9 +46,9 @@ struct MLds {
     int *m12;        // n1cap: vnMatches12
     int *qrank;      // n1cap: rank among octave-0 queries, or -1
     int *qcount;     // maxq: candidate-list length
+    uint32_t *claim; // n2cap: (replay batch << 16 | (255 - lane) << 8 | dist) of a batch's first acceptor of i2
+    int16_t *live;   // maxq: queries that can be accepted, in order
     uint32_t *top4;  // maxq x 4: (i2 << 16 | dist) of the 4 smallest (dist, position)
-    int *qbase;      // maxq: list start in `pool`, or -1 when the list lives in global scratch
-    uint32_t *pool;  // pool_cap candidate-list entries (i2 << 16 | dist)
     int16_t *kcell;  // n2cap: grid cell of each F2 keypoint (-1: none)
     int16_t *glist;  // maxc: F2 index by grid position
     int16_t *qidx;   // maxq: F1 index of each query
@@ -56,7 +56,7 @@ struct MLds {
     int8_t *rbin;    // n1cap: rotation bin of accepted queries (-1: none)
 };
 
-__device__ inline MLds carve(uint8_t *ptr, int n1cap, int n2cap, int maxq, int maxc, int pool_cap) {
+__device__ inline MLds carve(uint8_t *ptr, int n1cap, int n2cap, int maxq, int maxc) {
     MLds s;
     s.gd = reinterpret_cast<uint4 *>(ptr); ptr += sizeof(uint4) * 2 * maxc;
     s.qd = reinterpret_cast<uint4 *>(ptr); ptr += sizeof(uint4) * 2 * maxq;
@@ -70,11 +70,11 @@ __device__ inline MLds carve(uint8_t *ptr, int n1cap, int n2cap, int maxq, int m
     s.qrank = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * n1cap;
     s.qcount = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * maxq;
     s.top4 = reinterpret_cast<uint32_t *>(ptr); ptr += sizeof(uint32_t) * 4 * maxq;
-    s.qbase = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * maxq;
-    s.pool = reinterpret_cast<uint32_t *>(ptr); ptr += sizeof(uint32_t) * pool_cap;
+    s.claim = reinterpret_cast<uint32_t *>(ptr); ptr += sizeof(uint32_t) * n2cap;
     s.kcell = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * n2cap;
     s.glist = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * ((maxc + 1) & ~1);
     s.qidx = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * ((maxq + 1) & ~1);
+    s.live = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * ((maxq + 1) & ~1);
     s.acc = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * ((n1cap + 1) & ~1);
     s.rbin = reinterpret_cast<int8_t *>(ptr);
     return s;
@@ -101,8 +101,7 @@ __device__ inline int block_scan_i32(int v, int *total, int *ws) {
     return base + incl - v;
 }
 
-__global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, int n2cap, int maxq, int maxc,
-                                                     int pool_cap) {
+__global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, int n2cap, int maxq, int maxc) {
     extern __shared__ __align__(16) uint8_t lds[];
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const orbx_keypoint *k1 = mb.k1 + (int64_t)b * mb.k1_stride;
@@ -112,12 +111,11 @@ __global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, i
     const int n1 = min(mb.n1[b], n1cap), n2 = min(mb.n2[b], n2cap);
     float *prev = mb.prev_xy + (int64_t)b * mb.k1_stride * 2;
     int32_t *out12 = mb.matches12 + (int64_t)b * mb.k1_stride;
-    uint32_t *scratch = mb.scratch + (int64_t)b * mb.scratch_stride;
-    const MLds s = carve(lds, n1cap, n2cap, maxq, maxc, pool_cap);
+    const MLds s = carve(lds, n1cap, n2cap, maxq, maxc);
     __shared__ int hist[kHisto];
     __shared__ int ws[kMW];
     __shared__ int sh_top[3];
-    __shared__ int sh_err, sh_nq, sh_pool;
+    __shared__ int sh_err, sh_nq;
 
     // Frame grid constants for an undistorted img_w x img_h image
     // (Frame.cc:218-220, ComputeImageBounds with k1 == 0).
@@ -131,10 +129,10 @@ __global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, i
     // ---- 0. init
     for (int i = tid; i <= kGridCells; i += kMT) s.gstart[i] = 0;
     for (int i = tid; i < kGridCells; i += kMT) s.gfill[i] = 0;
-    for (int i = tid; i < n2; i += kMT) { s.mdist[i] = INT_MAX; s.m21[i] = -1; }
+    for (int i = tid; i < n2; i += kMT) { s.mdist[i] = INT_MAX; s.m21[i] = -1; s.claim[i] = 0; }
     for (int i = tid; i < n1; i += kMT) { s.m12[i] = -1; s.rbin[i] = -1; s.acc[i] = -1; }
     if (tid < kHisto) hist[tid] = 0;
-    if (tid == 0) { sh_err = 0; sh_pool = 0; }
+    if (tid == 0) sh_err = 0;
     if (mb.reset_prev) {
         for (int i = tid; i < n1; i += kMT) { prev[2 * i] = k1[i].x; prev[2 * i + 1] = k1[i].y; }
     }
@@ -223,12 +221,14 @@ __global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, i
     const int nq = sh_nq;
     if (clk) mb.clocks[2] = clock64();
 
-    // ---- 2. candidate lists + distances, all from LDS.  GetFeaturesInArea
-    //         visits ix outer, iy inner, then cell insertion order; glist is
-    //         sorted by cell = ix * 48 + iy and index, so the window's list is
-    //         one contiguous glist range per grid column ix.  Lane = column.
-    //         A list goes to the LDS pool when it fits, else to global scratch.
-    for (int q = wave; q < nq; q += kMW) {
+    // ---- 2. candidate distances, all from LDS.  GetFeaturesInArea visits
+    //         ix outer, iy inner, then cell insertion order; glist is sorted by
+    //         cell = ix * 48 + iy and index, so the window's list is one
+    //         contiguous glist range per grid column ix.  Lane = column; a
+    //         candidate's list position is its column's base + its rank.
+    //         Only each query's 4 smallest (dist, position) entries are kept;
+    //         the rare replay that needs more walks the window again.
+    auto window = [&](int q, int &st, int &cnt, int &pos0) {
         const float2 c = s.qxy[q];
         const float x = c.x, y = c.y;
         const int cx0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(x, minX), r), invW)));
@@ -237,39 +237,38 @@ __global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, i
         const int cy1 = min(kGridRows - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(y, minY), r), invH)));
         const bool empty = cx0 >= kGridCols || cx1 < 0 || cy0 >= kGridRows || cy1 < 0 || cx1 < cx0 || cy1 < cy0;
         const int ncx = cx1 - cx0 + 1;   // <= 64 grid columns
-        int st = 0, cnt = 0;
+        st = 0; cnt = 0;
         if (!empty && lane < ncx) {
             const int col = (cx0 + lane) * kGridRows;
             st = s.gstart[col + cy0];
             cnt = max(min(s.gstart[col + cy1 + 1], maxc) - st, 0);
         }
         const int incl = wave_incl_scan_i32(cnt);
-        const int pos0 = incl - cnt;
-        int written = __builtin_amdgcn_readlane(incl, 63);
+        pos0 = incl - cnt;
+        return __builtin_amdgcn_readlane(incl, 63);   // list length
+    };
+    // distance of list entry (column lane, rank e) to query q; kSkip outside the window
+    auto entry_dist = [&](int gp, float x, float y, const uint4 &qa, const uint4 &qb) {
+        const float2 kp = s.gxy[gp];
+        const float dx = __fsub_rn(kp.x, x), dy = __fsub_rn(kp.y, y);
+        return (fabsf(dx) < r && fabsf(dy) < r) ? hamming_regs(qa, qb, s.gd[2 * gp], s.gd[2 * gp + 1]) : kSkip;
+    };
+    for (int q = wave; q < nq; q += kMW) {
+        int st, cnt, pos0;
+        int written = window(q, st, cnt, pos0);
         if (written > maxc) { if (lane == 0) sh_err = 1; written = maxc; }
-        int base = -1;
-        if (lane == 0 && written > 0) {
-            base = atomicAdd(&sh_pool, written);
-            if (base + written > pool_cap) base = -1;
-        }
-        base = __builtin_amdgcn_readfirstlane(base);
-        uint32_t *list = base >= 0 ? s.pool + base : scratch + (int64_t)q * maxc;
         // this lane's 4 smallest (dist << 16 | list position) and their i2
         uint32_t tk[4] = {~0u, ~0u, ~0u, ~0u};
         int ti[4] = {0, 0, 0, 0};
         if (cnt > 0) {
+            const float2 c = s.qxy[q];
             const uint4 qa = s.qd[2 * q], qb = s.qd[2 * q + 1];
             for (int e = 0; e < cnt; ++e) {
                 const int gp = st + e;
-                const int i2 = s.glist[gp];
-                const float2 kp = s.gxy[gp];
-                const float dx = __fsub_rn(kp.x, x), dy = __fsub_rn(kp.y, y);
-                int dist = kSkip;
-                if (fabsf(dx) < r && fabsf(dy) < r) dist = hamming_regs(qa, qb, s.gd[2 * gp], s.gd[2 * gp + 1]);
-                if (pos0 + e < maxc) list[pos0 + e] = ((uint32_t)i2 << 16) | (uint32_t)dist;
-                if (dist != kSkip) {
+                const int dist = entry_dist(gp, c.x, c.y, qa, qb);
+                if (dist != kSkip && pos0 + e < maxc) {
                     uint32_t k = ((uint32_t)dist << 16) | (uint32_t)(pos0 + e);
-                    int ki = i2;
+                    int ki = s.glist[gp];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         if (k < tk[j]) {
@@ -290,7 +289,7 @@ __global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, i
             if (mine) { tk[0] = tk[1]; tk[1] = tk[2]; tk[2] = tk[3]; tk[3] = ~0u; ti[0] = ti[1]; ti[1] = ti[2]; ti[2] = ti[3]; }
             if (lane == 0) s.top4[4 * q + j] = mn == ~0u ? 0xFFFFFFFFu : ((uint32_t)i2 << 16) | (mn >> 16);
         }
-        if (lane == 0) { s.qcount[q] = written; s.qbase[q] = base; }
+        if (lane == 0) s.qcount[q] = written;
     }
     __syncthreads();
     if (clk) mb.clocks[3] = clock64();
@@ -299,85 +298,141 @@ __global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, i
     // The valid entries (vMatchedDistance[i2] > dist) among a query's 4
     // smallest (dist, position) entries, in order, are the smallest valid ones
     // of its whole list: two found decide (best, best2); a list that fits in 4
-    // is decided too; otherwise the list is scanned 64 entries at a time.
-    // Queries whose smallest distance exceeds TH_LOW can never be accepted and
-    // change no state, so they are skipped.
+    // is decided too; otherwise the whole list is walked again.  Queries whose
+    // smallest distance exceeds TH_LOW can never be accepted and change no
+    // state, so only the others ("live") are replayed, 64 consecutive ones per
+    // batch, one per lane, each against the state left by the committed ones.
+    // A lane's decision is the in-order one unless an earlier lane of the
+    // batch accepts a keypoint among the entries it examined (the only state
+    // its decision reads): the batch commits up to the first such lane (or the
+    // first lane that needs its whole list, which then runs alone) and the
+    // next batch starts there.  Lane 0 of a batch always commits.
     if (wave == 0) {
+        // the replay is the block's serial critical path: let it issue ahead
+        // of the co-resident block's waves
+        __builtin_amdgcn_s_setprio(3);
+        int nlive = 0;
         for (int g0 = 0; g0 < nq; g0 += 64) {
-          // this group's static query data, one query per lane
-          const int gq = min(g0 + lane, nq - 1);
-          const uint32_t r0 = s.top4[4 * gq], r1 = s.top4[4 * gq + 1], r2 = s.top4[4 * gq + 2],
-                         r3 = s.top4[4 * gq + 3];
-          const int rc = s.qcount[gq], ri = s.qidx[gq], rb = s.qbase[gq];
-          const bool live = g0 + lane < nq && rc > 0 && r0 != 0xFFFFFFFFu && (int)(r0 & 0xFFFF) <= kThLow;
-          uint64_t todo = __ballot(live);
-          while (todo) {
-            const int j = (int)__builtin_ctzll(todo);
-            todo &= todo - 1;
-            const int q = g0 + j;
-            const int cnt = __builtin_amdgcn_readlane(rc, j);
-            const int i1 = __builtin_amdgcn_readlane(ri, j);
-            const uint32_t e4[4] = {(uint32_t)__builtin_amdgcn_readlane((int)r0, j),
-                                    (uint32_t)__builtin_amdgcn_readlane((int)r1, j),
-                                    (uint32_t)__builtin_amdgcn_readlane((int)r2, j),
-                                    (uint32_t)__builtin_amdgcn_readlane((int)r3, j)};
+            const int q = g0 + lane;
+            const uint32_t r0 = q < nq ? s.top4[4 * q] : 0xFFFFFFFFu;
+            const bool live = q < nq && s.qcount[q] > 0 && r0 != 0xFFFFFFFFu && (int)(r0 & 0xFFFF) <= kThLow;
+            const uint64_t m = __ballot(live);
+            if (live) s.live[nlive + __popcll(m & ((1ull << lane) - 1))] = (int16_t)q;
+            nlive += __popcll(m);
+        }
+        wave_lds_fence();
+        if (clk) mb.clocks[7] = nlive;
+        const float nnr = mb.nnratio;
+        uint32_t batch = 0;
+        for (int P = 0; P < nlive;) {
+            ++batch;
+            const int idx = P + lane;
+            const bool act = idx < nlive;
+            const int q = act ? s.live[idx] : 0;
+            uint32_t e4[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) e4[t] = act ? s.top4[4 * q + t] : 0xFFFFFFFFu;
             int md[4];
 #pragma unroll
             for (int t = 0; t < 4; ++t) md[t] = s.mdist[e4[t] == 0xFFFFFFFFu ? 0 : (e4[t] >> 16)];
-            int best = INT_MAX, best2 = INT_MAX, best_i2 = -1;
-            int found = 0;
+            int best = INT_MAX, best2 = INT_MAX, best_i2 = -1, found = 0, ne = 0;
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
                 if (e4[t] == 0xFFFFFFFFu || found == 2) continue;
+                ne = t + 1;
                 const int i2 = (int)(e4[t] >> 16), dist = (int)(e4[t] & 0xFFFF);
                 if (md[t] <= dist) continue;
                 if (found == 0) { best = dist; best_i2 = i2; }
                 else best2 = dist;
                 ++found;
             }
-            if (!(found == 2 || e4[3] == 0xFFFFFFFFu)) {
-                best = INT_MAX; best2 = INT_MAX; best_i2 = -1;
-                const int qb = __builtin_amdgcn_readlane(rb, j);
-                const uint32_t *list = qb >= 0 ? s.pool + qb : scratch + (int64_t)q * maxc;
-                for (int c0 = 0; c0 < cnt; c0 += 64) {
-                    const int e = c0 + lane;
-                    uint32_t key = ~0u;
-                    int dist = INT_MAX, i2 = 0;
-                    if (e < cnt) {
-                        const uint32_t v = list[e];
-                        i2 = (int)(v >> 16);
-                        dist = (int)(v & 0xFFFF);
-                        if (dist == kSkip || s.mdist[i2] <= dist) dist = INT_MAX;
-                        else key = ((uint32_t)dist << 16) | (uint32_t)e;
-                    }
-                    const uint32_t mn = wave_min_u32(key);
-                    if (mn == ~0u) continue;
-                    const int cb = (int)(mn >> 16);
-                    const int cb_lane = (int)(mn & 0xFFFF) - c0;
-                    const int cb_i2 = __builtin_amdgcn_readlane(i2, cb_lane);
-                    const uint32_t key2 = (lane == cb_lane || dist == INT_MAX) ? ~0u : (uint32_t)dist;
-                    const uint32_t mn2 = wave_min_u32(key2);
-                    const int cs = mn2 == ~0u ? INT_MAX : (int)mn2;
-                    const int hi = best <= cb ? cb : best;
-                    best2 = min(hi, min(best2, cs));
-                    if (cb < best) best_i2 = cb_i2;
-                    best = best <= cb ? best : cb;
+            const bool fb = act && !(found == 2 || e4[3] == 0xFFFFFFFFu);
+            const bool ok = act && !fb && best <= kThLow && (float)best < __fmul_rn((float)best2, nnr);
+            const uint64_t fbm = __ballot(fb);
+            const int f = fbm ? (int)__builtin_ctzll(fbm) : 64;
+            // claim = batch << 16 | (255 - lane) << 8 | best: the earliest
+            // accepting lane of the batch and the vMatchedDistance it leaves
+            if (ok && lane < f)
+                atomicMax(&s.claim[best_i2], (batch << 16) | ((uint32_t)(255 - lane) << 8) | (uint32_t)best);
+            wave_lds_fence();
+            // An entry the lane found valid (md > dist) turns invalid iff an
+            // earlier lane accepts its keypoint with best <= dist; an invalid
+            // one stays invalid (the acceptor saw md > best).  Accepting a
+            // keypoint an earlier lane accepts (a steal within the batch) also
+            // ends the commit, so each keypoint has one acceptor per batch and
+            // the claim's distance is what that acceptor leaves.
+            bool inval = false;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                if (t < ne && act && lane < f) {
+                    const uint32_t c = s.claim[e4[t] >> 16];
+                    const int dist = (int)(e4[t] & 0xFFFF);
+                    const bool earlier = (c >> 16) == batch && 255 - (int)((c >> 8) & 0xFF) < lane;
+                    inval |= earlier && ((md[t] > dist && (int)(c & 0xFF) <= dist) ||
+                                         (ok && (int)(e4[t] >> 16) == best_i2));
                 }
             }
-            if (best <= kThLow && (float)best < __fmul_rn((float)best2, mb.nnratio)) {
-                if (lane == 0) {
-                    const int old = s.m21[best_i2];
+            const uint64_t im = __ballot(inval);
+            const int cut = min(min(im ? (int)__builtin_ctzll(im) : 64, f), nlive - P);
+            if (ok && lane < cut) {
+                const int i1 = s.qidx[q];
+                const int old = s.m21[best_i2];
+                if (old >= 0) s.m12[old] = -1;
+                s.m12[i1] = best_i2;
+                s.m21[best_i2] = i1;
+                s.mdist[best_i2] = best;
+                s.acc[i1] = (int16_t)best_i2;   // binned in phase 4 (stolen pairs keep their bin)
+            }
+            wave_lds_fence();
+            if (clk) mb.clocks[6] += 1;
+            P += cut;
+            if (cut == f && P < nlive) {
+                // lane f's query needs its whole list: walk the window again;
+                // each lane keeps its column's smallest valid (dist, position)
+                // key and its second distance
+                const int qf = s.live[P];
+                int st, cc, pos0;
+                window(qf, st, cc, pos0);
+                const float2 c = s.qxy[qf];
+                const uint4 qa = s.qd[2 * qf], qb = s.qd[2 * qf + 1];
+                uint32_t k1 = ~0u;
+                int d2 = INT_MAX, i2a = 0;
+                for (int e = 0; e < cc; ++e) {
+                    const int gp = st + e;
+                    if (pos0 + e >= maxc) break;
+                    const int dist = entry_dist(gp, c.x, c.y, qa, qb);
+                    const int i2 = s.glist[gp];
+                    if (dist == kSkip || s.mdist[i2] <= dist) continue;
+                    const uint32_t k = ((uint32_t)dist << 16) | (uint32_t)(pos0 + e);
+                    if (k < k1) { d2 = k1 == ~0u ? INT_MAX : (int)(k1 >> 16); k1 = k; i2a = i2; }
+                    else d2 = min(d2, dist);
+                }
+                const uint32_t mn = wave_min_u32(k1);
+                int fbest = INT_MAX, fbest2 = INT_MAX, fi2 = -1;
+                if (mn != ~0u) {
+                    const uint64_t who = __ballot(k1 == mn);
+                    const int wl = (int)__builtin_ctzll(who);
+                    fbest = (int)(mn >> 16);
+                    fi2 = __builtin_amdgcn_readlane(i2a, wl);
+                    // multiset second: the best lane's second, every other lane's first
+                    const uint32_t cand2 = lane == wl ? (uint32_t)d2 : (k1 == ~0u ? ~0u : (k1 >> 16));
+                    const uint32_t m2 = wave_min_u32(cand2);
+                    fbest2 = m2 >= (uint32_t)INT_MAX ? INT_MAX : (int)m2;
+                }
+                if (fbest <= kThLow && (float)fbest < __fmul_rn((float)fbest2, nnr) && lane == 0) {
+                    const int i1 = s.qidx[qf];
+                    const int old = s.m21[fi2];
                     if (old >= 0) s.m12[old] = -1;
-                    s.m12[i1] = best_i2;
-                    s.m21[best_i2] = i1;
-                    s.mdist[best_i2] = best;
-                    s.acc[i1] = (int16_t)best_i2;   // binned in phase 4 (stolen pairs keep their bin)
+                    s.m12[i1] = fi2;
+                    s.m21[fi2] = i1;
+                    s.mdist[fi2] = fbest;
+                    s.acc[i1] = (int16_t)fi2;
                 }
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                __builtin_amdgcn_wave_barrier();
+                wave_lds_fence();
+                ++P;
             }
-          }
         }
+        __builtin_amdgcn_s_setprio(0);
     }
     __syncthreads();
     if (clk) mb.clocks[4] = clock64();
@@ -435,27 +490,24 @@ __global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, i
 
 }  // namespace
 
-// LDS of everything but the candidate-list pool.
+// LDS of one frame pair.
 int match_lds_bytes(int n1cap, int n2cap, int maxq, int maxc) {
     return (int)(32 * (maxc + maxq) + 8 * (maxc + maxq) + sizeof(int) * (2 * kGridCells + 1) +
-                 sizeof(int) * (2 * n2cap + 2 * n1cap) + sizeof(int) * 6 * maxq + sizeof(int16_t) * n2cap +
-                 sizeof(int16_t) * ((maxc + 1) & ~1) + sizeof(int16_t) * ((maxq + 1) & ~1) +
+                 sizeof(int) * (3 * n2cap + 2 * n1cap) + sizeof(int) * 5 * maxq + sizeof(int16_t) * n2cap +
+                 sizeof(int16_t) * ((maxc + 1) & ~1) + 2 * sizeof(int16_t) * ((maxq + 1) & ~1) +
                  sizeof(int16_t) * ((n1cap + 1) & ~1) + n1cap + 64);
 }
 
 constexpr int kMatchLdsMax = 160 * 1024 - 1024;   // dynamic LDS; the kernel's static LDS needs < 1 KiB
 
 hipError_t launch_match(const MatchBufs &mb, int B, int n1cap, int n2cap, int maxq, int maxc, hipStream_t st) {
-    const int fixed = match_lds_bytes(n1cap, n2cap, maxq, maxc);
-    if (fixed > kMatchLdsMax) return hipErrorInvalidValue;
-    // candidate-list pool: the rest of the CU's LDS, at most every list at full length
-    const int pool_cap = (int)std::min<int64_t>((int64_t)maxq * maxc, (kMatchLdsMax - fixed) / 4);
-    const int bytes = fixed + 4 * pool_cap;
+    const int bytes = match_lds_bytes(n1cap, n2cap, maxq, maxc);
+    if (bytes > kMatchLdsMax) return hipErrorInvalidValue;
     if (bytes > 64 * 1024 &&
         hipFuncSetAttribute(reinterpret_cast<const void *>(k_search_init),
                             hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_search_init, dim3(B), dim3(kMT), bytes, st, mb, n1cap, n2cap, maxq, maxc, pool_cap);
+    hipLaunchKernelGGL(k_search_init, dim3(B), dim3(kMT), bytes, st, mb, n1cap, n2cap, maxq, maxc);
     return hipGetLastError();
 }
 

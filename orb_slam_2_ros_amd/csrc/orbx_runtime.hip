@@ -80,8 +80,6 @@ struct orbx_extractor {
     // matcher state (results of the last mono step)
     float *d_prev = nullptr;
     int32_t *d_m12 = nullptr, *d_nmatch = nullptr;
-    uint32_t *d_scratch = nullptr;
-    int64_t scratch_stride = 0;
     int match_batch = 0;
     int l0cap = 0;
 
@@ -151,7 +149,7 @@ struct orbx_extractor {
         dfree(d_tables); dfree(d_pyr); dfree(d_blur); dfree(d_cand); dfree(d_cand2); dfree(d_keys); dfree(d_sel);
         dfree(d_cell_count); dfree(d_level_count); dfree(d_key_node); dfree(d_key_q);
         for (auto &s : slot) { dfree(s.kps); dfree(s.desc); dfree(s.nkps); s.batch = 0; }
-        dfree(d_prev); dfree(d_m12); dfree(d_nmatch); dfree(d_scratch); dfree(d_img);
+        dfree(d_prev); dfree(d_m12); dfree(d_nmatch); dfree(d_img);
         dfree(d_ur); dfree(d_depth); dfree(d_sad); dfree(d_nkept);
         depth_mode = 0;
         depth_count = 0;
@@ -285,11 +283,9 @@ int reserve(orbx_extractor *ex, int w, int h, int max_batch) {
         s.batch = 0;
     }
     ex->l0cap = p.lv[0].out_cap;
-    ex->scratch_stride = (int64_t)ex->l0cap * ex->l0cap;
     ok &= dalloc(&ex->d_prev, B * p.max_kps * 2) == hipSuccess;
     ok &= dalloc(&ex->d_m12, B * p.max_kps) == hipSuccess;
     ok &= dalloc(&ex->d_nmatch, B) == hipSuccess;
-    ok &= dalloc(&ex->d_scratch, B * (size_t)ex->scratch_stride) == hipSuccess;
     ok &= dalloc(&ex->d_ur, B * p.max_kps) == hipSuccess;
     ok &= dalloc(&ex->d_depth, B * p.max_kps) == hipSuccess;
     ok &= dalloc(&ex->d_sad, B * p.max_kps) == hipSuccess;
@@ -363,7 +359,6 @@ MatchBufs offset_pairs(MatchBufs mb, int b0) {
     mb.prev_xy += b0 * mb.k1_stride * 2;
     mb.matches12 += b0 * mb.k1_stride;
     mb.nmatches += b0;
-    mb.scratch += b0 * mb.scratch_stride;
     return mb;
 }
 
@@ -848,8 +843,6 @@ int orbx_mono_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t f
     mb.prev_xy = ex->d_prev;
     mb.matches12 = ex->d_m12;
     mb.nmatches = ex->d_nmatch;
-    mb.scratch = ex->d_scratch;
-    mb.scratch_stride = ex->scratch_stride;
     mb.img_w = ex->plan.width;
     mb.img_h = ex->plan.height;
     mb.window = window;
@@ -873,7 +866,7 @@ int orbx_mono_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t f
         if (hipStreamSynchronize(st) == hipSuccess &&
             hipMemcpy(c, dclk, sizeof(c), hipMemcpyDeviceToHost) == hipSuccess)
             std::fprintf(stderr, "match phases (cycles): init %lld grid+queries %lld lists %lld replay %lld tail %lld; "
-                         "queries %lld fallbacks %lld\n",
+                         "live queries %lld replay batches %lld\n",
                          c[1] - c[0], c[2] - c[1], c[3] - c[2], c[4] - c[3], c[5] - c[4], c[7], c[6]);
         (void)hipFree(dclk);
     }
@@ -1141,7 +1134,6 @@ int orbx_search_for_initialization(int device, const orbx_keypoint *k1, const ui
     const size_t in_bytes = L.size;
     const size_t o_m = L.add(4 * (size_t)n1c), o_nm = L.add(4);
     const size_t out_end = L.size;
-    const size_t o_scr = L.add(4 * (size_t)q * c);
     CallWs &ws = call_ws(device);
     std::lock_guard<std::mutex> lock(ws.mu);
     int rc = ws_reserve(ws, L.size);
@@ -1159,7 +1151,6 @@ int orbx_search_for_initialization(int device, const orbx_keypoint *k1, const ui
     mb.k1 = at<orbx_keypoint>(D, o_k1); mb.d1 = D + o_d1; mb.n1 = at<int32_t>(D, o_ns); mb.k1_stride = n1c;
     mb.k2 = at<orbx_keypoint>(D, o_k2); mb.d2 = D + o_d2; mb.n2 = at<int32_t>(D, o_ns) + 1; mb.k2_stride = n2c;
     mb.prev_xy = at<float>(D, o_prev); mb.matches12 = at<int32_t>(D, o_m); mb.nmatches = at<int32_t>(D, o_nm);
-    mb.scratch = at<uint32_t>(D, o_scr); mb.scratch_stride = (int64_t)q * c;
     mb.img_w = img_w; mb.img_h = img_h; mb.window = window; mb.nnratio = nnratio;
     mb.check_ori = check_ori; mb.reset_prev = 0; mb.clocks = nullptr;
     if (launch_match(mb, 1, n1c, n2c, q, c, ws.st) != hipSuccess ||

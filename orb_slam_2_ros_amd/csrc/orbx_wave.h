@@ -14,6 +14,13 @@ __device__ inline uint32_t dpp_or(uint32_t old, uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, Ctrl, RowMask, 0xF, false);
 }
 
+// Orders this wave's LDS accesses: everything before is visible to every lane
+// after (no workgroup barrier).
+__device__ inline void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
 constexpr int kRowShr1 = 0x111, kRowShr2 = 0x112, kRowShr4 = 0x114, kRowShr8 = 0x118;
 constexpr int kRowBcast15 = 0x142, kRowBcast31 = 0x143;
 
