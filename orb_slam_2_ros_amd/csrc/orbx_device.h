@@ -19,6 +19,15 @@ struct LevelArgs {
     float scale, patch_size;
 };
 
+// LDS layout of one k_fast launch (per wave), sized by the largest cell of the
+// levels it covers.
+struct FastLds {
+    int ps;            // patch row stride (dword multiple)
+    int patch_bytes, score_bytes, per_wave;
+    int sw;            // score-map row stride (largest cell width + 2)
+};
+FastLds fast_lds(int mw, int mh);
+
 // Plan tables resident in device memory (one copy per extractor plan).
 struct DevPlan {
     LevelArgs la[kMaxLevels];
@@ -33,8 +42,6 @@ struct DevPlan {
     int ini_th, min_th;
     int64_t pyr_bytes, blur_bytes, cand_cap;
     int out_cap, max_kps;
-    int cell_max_w, cell_max_h;   // largest FAST cell interior (sizes k_fast's LDS)
-    int fast_patch_stride, fast_patch_bytes, fast_score_bytes, fast_lds_per_wave;
     int node_cap;             // quadtree node capacity (max over levels)
     int node_lds_bytes;       // dynamic LDS of the quadtree kernel
     int dbg_stop;             // diagnostics only (ORBX_DBG_STOP): end k_quadtree after phase n (0 = off)
@@ -144,7 +151,7 @@ hipError_t launch_quadtree_level(const DevPlan &p, const FrameBufs &fb, int B, h
 hipError_t launch_describe_level(const DevPlan &p, const Plan &hp, const FrameBufs &fb, int B, hipStream_t s, int l,
                                  int l_end);
 hipError_t launch_blur(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t s);
-hipError_t launch_fast(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t s);
+hipError_t launch_fast(const DevPlan &p, const Plan &hp, const FrameBufs &fb, int B, hipStream_t s);
 hipError_t launch_quadtree(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t s);
 hipError_t launch_describe(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t s);
 hipError_t launch_match(const MatchBufs &mb, int B, int n1cap, int n2cap, int maxq, int maxc, hipStream_t s);

@@ -469,7 +469,7 @@ __device__ inline int arc_score_bytes(const int p[16], int v) {
 // PIPE: a level's cells in a level-pipelined step (a distinct instantiation so
 // profiles tell per-level launches from whole-batch ones).
 template <bool PIPE>
-__global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int c0, int nc) {
+__global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int c0, int nc, FastLds fl) {
     extern __shared__ __align__(16) uint8_t lds[];
     const int wave = wave_id(), lane = threadIdx.x & 63;
     int bx, b;
@@ -483,10 +483,10 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
         if (lane == 0) *count_out = 0;
         return;
     }
-    const int PS = p.fast_patch_stride, SW = p.cell_max_w + 2;
-    uint8_t *patch = lds + (size_t)wave * p.fast_lds_per_wave;
-    uint8_t *scm = patch + p.fast_patch_bytes;   // S-1 of the pass's corners, 0 elsewhere
-    uint16_t *list = reinterpret_cast<uint16_t *>(scm + p.fast_score_bytes);   // (yy << 8 | xx), row-major
+    const int PS = fl.ps, SW = fl.sw;
+    uint8_t *patch = lds + (size_t)wave * fl.per_wave;
+    uint8_t *scm = patch + fl.patch_bytes;   // S-1 of the pass's corners, 0 elsewhere
+    uint16_t *list = reinterpret_cast<uint16_t *>(scm + fl.score_bytes);   // (yy << 8 | xx), row-major
     int spitch;
     const uint8_t *img = level_ptr(p, fb, c.level, b, spitch);
     const int o = wave_stage_rect(patch, PS, img, spitch, c.y0 - 3, c.x0 - 3, ch + 6, cw + 6, lane);
@@ -501,7 +501,7 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
     auto pass = [&](int th, uint32_t *out) -> int {
         {
             uint32_t *z0 = reinterpret_cast<uint32_t *>(scm);
-            const int nz = p.fast_score_bytes >> 2;
+            const int nz = fl.score_bytes >> 2;
             for (int i = lane; i < nz; i += 64) z0[i] = 0;
         }
         wave_lds_fence();
@@ -1293,18 +1293,60 @@ hipError_t launch_blur(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t
     return hipGetLastError();
 }
 
-hipError_t launch_fast(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t st) {
-    hipLaunchKernelGGL(k_fast<false>, dim3((p.ncells + 3) / 4, B), dim3(kThreads), 4 * p.fast_lds_per_wave, st, p, fb, 0,
-                       p.ncells);
+FastLds fast_lds(int mw, int mh) {
+    FastLds f;
+    f.ps = (mw + 6 + 3 + 3) & ~3;   // + alignment offset, dword rows
+    f.patch_bytes = (f.ps * (mh + 6) + 15) & ~15;
+    f.score_bytes = ((mw + 2) * (mh + 2) + 15) & ~15;
+    f.per_wave = f.patch_bytes + f.score_bytes + ((2 * mw * mh + 15) & ~15);
+    f.sw = mw + 2;
+    return f;
+}
+
+namespace {
+// The levels [l0, l1)'s cells with LDS sized by their largest cell.
+template <bool PIPE>
+hipError_t launch_fast_range(const DevPlan &p, const Plan &hp, const FrameBufs &fb, int B, hipStream_t st, int l0,
+                             int l1) {
+    const int c0 = hp.lv[l0].cell_begin, nc = hp.lv[l1 - 1].cell_end - c0;
+    if (nc <= 0) return hipSuccess;
+    int mw = 1, mh = 1;
+    for (int c = c0; c < c0 + nc; ++c) {
+        mw = std::max(mw, hp.cells[c].x1 - hp.cells[c].x0);
+        mh = std::max(mh, hp.cells[c].y1 - hp.cells[c].y0);
+    }
+    const FastLds fl = fast_lds(mw, mh);
+    hipLaunchKernelGGL(k_fast<PIPE>, dim3((nc + 3) / 4, B), dim3(kThreads), 4 * fl.per_wave, st, p, fb, c0, nc, fl);
     return hipGetLastError();
+}
+
+// Workgroups of 4 waves one CU holds at a time for a level's largest cell.
+int fast_blocks_per_cu(const Plan &hp, int l) {
+    int mw = 1, mh = 1;
+    for (int c = hp.lv[l].cell_begin; c < hp.lv[l].cell_end; ++c) {
+        mw = std::max(mw, hp.cells[c].x1 - hp.cells[c].x0);
+        mh = std::max(mh, hp.cells[c].y1 - hp.cells[c].y0);
+    }
+    return std::min(8, 160 * 1024 / (4 * fast_lds(mw, mh).per_wave));
+}
+}  // namespace
+
+// Consecutive levels whose cells give the same occupancy share a launch, so a
+// level of large cells (the last level's few columns) does not size the LDS
+// of all the others.
+hipError_t launch_fast(const DevPlan &p, const Plan &hp, const FrameBufs &fb, int B, hipStream_t st) {
+    for (int l0 = 0; l0 < hp.nlevels;) {
+        int l1 = l0 + 1;
+        while (l1 < hp.nlevels && fast_blocks_per_cu(hp, l1) == fast_blocks_per_cu(hp, l0)) ++l1;
+        if (launch_fast_range<false>(p, hp, fb, B, st, l0, l1) != hipSuccess) return hipErrorLaunchFailure;
+        l0 = l1;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_fast_level(const DevPlan &p, const Plan &hp, const FrameBufs &fb, int B, hipStream_t st, int l,
                              int l_end) {
-    const int c0 = hp.lv[l].cell_begin, nc = hp.lv[l_end - 1].cell_end - c0;
-    if (nc <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_fast<true>, dim3((nc + 3) / 4, B), dim3(kThreads), 4 * p.fast_lds_per_wave, st, p, fb, c0, nc);
-    return hipGetLastError();
+    return launch_fast_range<true>(p, hp, fb, B, st, l, l_end);
 }
 
 // Dynamic LDS above 64 KiB must be opted into per kernel.

@@ -227,14 +227,8 @@ int upload_plan(orbx_extractor *ex) {
     d.node_cap = node_cap;
     int mw = 1, mh = 1;
     for (const Cell &c : p.cells) { mw = std::max(mw, c.x1 - c.x0); mh = std::max(mh, c.y1 - c.y0); }
-    d.cell_max_w = mw;
-    d.cell_max_h = mh;
-    d.fast_patch_stride = (mw + 6 + 3 + 3) & ~3;      // + alignment offset, dword rows
-    d.fast_patch_bytes = (d.fast_patch_stride * (mh + 6) + 15) & ~15;
-    d.fast_score_bytes = ((mw + 2) * (mh + 2) + 15) & ~15;
-    d.fast_lds_per_wave = d.fast_patch_bytes + d.fast_score_bytes + ((2 * mw * mh + 15) & ~15);
     if (mw > 255 || mh > 255) return ORBX_EINVAL;   // survivor list packs (y << 8 | x)
-    if (4 * d.fast_lds_per_wave > 64 * 1024) return ORBX_EINVAL;
+    if (4 * fast_lds(mw, mh).per_wave > 64 * 1024) return ORBX_EINVAL;   // k_fast's LDS for the largest cell
     d.node_lds_bytes = quadtree_lds_bytes(node_cap);
     // phase 1 of k_quadtree keeps two ints per cell of a level in the same LDS
     for (const LevelGeom &g : p.lv)
@@ -513,7 +507,7 @@ int run_extract(orbx_extractor *ex, int si, const uint8_t *d_images, int64_t str
     mark(ex, 1, m);
     mark(ex, 2, m);   // the blur is fused into k_describe (patch-local); stage 1 stays empty
     for (int k = 0; k < P.n; ++k)
-        if (launch_fast(ex->dp, pf[k], P.nb[k], P.s[k]) != hipSuccess) return ORBX_EIO;
+        if (launch_fast(ex->dp, ex->plan, pf[k], P.nb[k], P.s[k]) != hipSuccess) return ORBX_EIO;
     mark(ex, 3, m);
     for (int k = 0; k < P.n; ++k)
         if (launch_quadtree(ex->dp, pf[k], P.nb[k], P.s[k]) != hipSuccess) return ORBX_EIO;
