@@ -288,14 +288,12 @@ __host__ __device__ inline int resize_src_raw(int d, double scale) {
 #endif
 }
 
+// One wave tile (ResizeWave) of level l of frame b; `win` is the wave's LDS
+// slice (a.win_bytes).
 template <int NB>
-__global__ __launch_bounds__(kThreads) void k_resize_w(DevPlan p, FrameBufs fb, int l, ResizeWave a, int B) {
-    extern __shared__ __align__(16) uint8_t lds[];
-    const int wave = wave_id(), lane = threadIdx.x & 63;
-    const int L = xcd_logical_block(blockIdx.x, gridDim.x);
-    const int t = L * 4 + wave;
-    if (t >= a.ntiles * B) return;
-    const int b = t / a.ntiles, tile = t - b * a.ntiles;
+__device__ inline void resize_tile(const DevPlan &p, const FrameBufs &fb, int l, const ResizeWave &a, int b, int tile,
+                                   int lane, uint8_t *win) {
+    wave_lds_fence();   // the slice's previous window is consumed
     const int ty = tile / a.ntx, tx = tile - ty * a.ntx;
     const LevelArgs g = p.la[l], gs = p.la[l - 1];
     const int twg = a.twg, lr = lane >> a.twg_shift, lg = lane & (twg - 1);
@@ -303,8 +301,8 @@ __global__ __launch_bounds__(kThreads) void k_resize_w(DevPlan p, FrameBufs fb, 
     const int x0 = tx * 4 * twg, y0 = ty * TH;
     const int xb = x0 + 4 * lg, yb = y0 + lr * kResizeK;
     // taps of this lane's 4 columns and kResizeK rows (independent of the window loads)
-    const ResizeTap *xt = p.xtaps + p.lv[l].xtab_off;
-    const ResizeTap *yt = p.ytaps + p.lv[l].ytab_off;
+    const ResizeTap *xt = p.xtaps + a.xtab_off;
+    const ResizeTap *yt = p.ytaps + a.ytab_off;
     ResizeTap txk[4], tyk[kResizeK];
 #pragma unroll
     for (int k = 0; k < 4; ++k) txk[k] = xt[min(xb + k, g.w - 1)];
@@ -318,7 +316,6 @@ __global__ __launch_bounds__(kThreads) void k_resize_w(DevPlan p, FrameBufs fb, 
     const int r_hi = min(max(resize_src_raw(yl, a.sy) + 1, 0), gs.h - 1);
     int spitch;
     const uint8_t *src = level_ptr(p, fb, l - 1, b, spitch);
-    uint8_t *win = lds + wave * a.win_bytes;
     wave_stage_rect<NB>(win, a.win_stride, src, spitch, r_lo, c_lo, r_hi - r_lo + 1, c_hi - c_lo + 1, lane);
     // per-lane column constants: dword of the first source pixel, realignment,
     // and the v_perm selectors of the 4 pixel pairs (S[sx_k], S[sx_k + 1])
@@ -375,6 +372,17 @@ __global__ __launch_bounds__(kThreads) void k_resize_w(DevPlan p, FrameBufs fb, 
         }
         *reinterpret_cast<uint32_t *>(dst + mul24u(y, g.pitch) + xb) = packed;
     }
+}
+
+template <int NB>
+__global__ __launch_bounds__(kThreads) void k_resize_w(DevPlan p, FrameBufs fb, int l, ResizeWave a, int B) {
+    extern __shared__ __align__(16) uint8_t lds[];
+    const int wave = wave_id(), lane = threadIdx.x & 63;
+    const int L = xcd_logical_block(blockIdx.x, gridDim.x);
+    const int t = L * 4 + wave;
+    if (t >= a.ntiles * B) return;
+    const int b = t / a.ntiles;
+    resize_tile<NB>(p, fb, l, a, b, t - b * a.ntiles, lane, lds + wave * a.win_bytes);
 }
 
 // ===========================================================================
@@ -1403,6 +1411,8 @@ bool plan_resize_waves(Plan &hp) {
         const ResizeTap *xt = hp.xtaps.data() + g.xtab_off;
         const ResizeTap *yt = hp.ytaps.data() + g.ytab_off;
         ResizeWave a;
+        a.xtab_off = g.xtab_off;
+        a.ytab_off = g.ytab_off;
         a.sx = 1. / ((double)g.w / gs.w);
         a.sy = 1. / ((double)g.h / gs.h);
         int best = -1;

@@ -77,10 +77,11 @@ PYRAMID_CASES = [
 
 
 @pytest.mark.parametrize("w,h,scale,nlev,seed", PYRAMID_CASES)
-@pytest.mark.parametrize("blocks", [False, True])
-def test_pyramid_sizes_and_scales(w, h, scale, nlev, seed, blocks, oracle_mod, monkeypatch):
-    """cv::resize chain (k_resize_w wave tiles, or the k_resize block kernel) vs the oracle."""
-    if blocks:
+@pytest.mark.parametrize("path", ["waves", "blocks"])
+def test_pyramid_sizes_and_scales(w, h, scale, nlev, seed, path, oracle_mod, monkeypatch):
+    """cv::resize chain vs the oracle: per-level wave tiles (k_resize_w) and the
+    block kernel (k_resize)."""
+    if path == "blocks":
         monkeypatch.setenv("ORBX_RESIZE_BLOCKS", "1")
     img = synth.frame(w, h, seed)
     ex = ORBextractor(500, scale, nlev, 20, 7)
