@@ -81,10 +81,15 @@ def measured_traffic(stage: str, frames_per_launch: float):
     scaled from the profiled dispatch's frame count; (None, None) if absent."""
     try:
         prof = json.loads(TRAFFIC_FILE.read_text())
-        k = prof["kernels"][STAGE_KERNEL[stage]]
+        name = STAGE_KERNEL[stage]
+        # template instantiations are listed as k_name<args>; the whole-batch
+        # launch is the <false> one
+        keys = [k for k in prof["kernels"] if k == name or k.startswith(name + "<") or k.startswith(name + "_w<")]
+        keys.sort(key=lambda k: "<false>" not in k)
+        k = prof["kernels"][keys[0]]
         per_frame = k["hbm_bytes_per_dispatch"] / prof["frames_per_dispatch"]
         return round(per_frame * frames_per_launch), str(TRAFFIC_FILE.relative_to(ROOT))
-    except (OSError, KeyError, ValueError, ZeroDivisionError):
+    except (OSError, KeyError, ValueError, ZeroDivisionError, IndexError):
         return None, None
 
 

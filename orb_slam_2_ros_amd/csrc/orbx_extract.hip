@@ -1328,28 +1328,12 @@ hipError_t launch_fast_range(const DevPlan &p, const Plan &hp, const FrameBufs &
     return hipGetLastError();
 }
 
-// Workgroups of 4 waves one CU holds at a time for a level's largest cell.
-int fast_blocks_per_cu(const Plan &hp, int l) {
-    int mw = 1, mh = 1;
-    for (int c = hp.lv[l].cell_begin; c < hp.lv[l].cell_end; ++c) {
-        mw = std::max(mw, hp.cells[c].x1 - hp.cells[c].x0);
-        mh = std::max(mh, hp.cells[c].y1 - hp.cells[c].y0);
-    }
-    return std::min(8, 160 * 1024 / (4 * fast_lds(mw, mh).per_wave));
-}
 }  // namespace
 
-// Consecutive levels whose cells give the same occupancy share a launch, so a
-// level of large cells (the last level's few columns) does not size the LDS
-// of all the others.
+// All cells of all levels in one launch (one dispatch per stage keeps the
+// per-launch roofline figure clean; splitting by cell size measured +1 %).
 hipError_t launch_fast(const DevPlan &p, const Plan &hp, const FrameBufs &fb, int B, hipStream_t st) {
-    for (int l0 = 0; l0 < hp.nlevels;) {
-        int l1 = l0 + 1;
-        while (l1 < hp.nlevels && fast_blocks_per_cu(hp, l1) == fast_blocks_per_cu(hp, l0)) ++l1;
-        if (launch_fast_range<false>(p, hp, fb, B, st, l0, l1) != hipSuccess) return hipErrorLaunchFailure;
-        l0 = l1;
-    }
-    return hipSuccess;
+    return launch_fast_range<false>(p, hp, fb, B, st, 0, hp.nlevels);
 }
 
 hipError_t launch_fast_level(const DevPlan &p, const Plan &hp, const FrameBufs &fb, int B, hipStream_t st, int l,

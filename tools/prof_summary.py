@@ -19,7 +19,7 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    m = re.search(r"(\w+)\(", name)
+    m = re.search(r"(k_\w+(?:<[^>]*>)?)\(", name) or re.search(r"(\w+)\(", name)
     return m.group(1) if m else name
 
 
