@@ -117,6 +117,41 @@ def cpu_baseline(w: int, h: int, nfeatures: int, budget_s: float):
             "sample": f"{n} consecutive {w}x{h} synthetic frames ({el:.1f} s), oracle/liborbx_oracle.so, 1 thread"}
 
 
+def cpu_baseline_threads(w: int, h: int, nfeatures: int, budget_s: float, threads: int):
+    """The same oracle workload on `threads` host threads at once, one stream
+    per thread (ORB-SLAM2 runs one extraction per std::thread, Frame.cc:79-82);
+    ctypes drops the GIL inside each call.  Whole-host frames/s."""
+    import threading
+    from oracle import oracle
+    from orb_slam_2_ros_amd import synth
+    frames = synth.frames(w, h, 4242, 8)
+    counts = [0] * threads
+    stop = time.perf_counter() + budget_s
+
+    def worker(t):
+        prev = oracle.extract(frames[t % len(frames)], nfeatures)
+        n = 0
+        while time.perf_counter() < stop:
+            img = frames[(t + n + 1) % len(frames)]
+            k2, d2 = oracle.extract(img, nfeatures)
+            k1, d1 = prev
+            pxy = np.ascontiguousarray(np.stack([k1["x"], k1["y"]], 1).astype(np.float32))
+            oracle.search_for_initialization(k1, d1, k2, d2, w, h, pxy, 100, 0.9, True)
+            prev = (k2, d2)
+            n += 1
+        counts[t] = n
+
+    t0 = time.perf_counter()
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    el = time.perf_counter() - t0
+    return {"value": sum(counts) / el, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{sum(counts)} {w}x{h} synthetic frames on {threads} threads ({el:.1f} s)"}
+
+
 def timed_region(step, steps, warmup, sync, dist, world, on_start=None):
     """W untimed warmup steps, then EXACTLY `steps` timed steps bracketed by a
     barrier + device sync on both sides.  Returns this rank's elapsed seconds."""
@@ -481,6 +516,10 @@ def main() -> int:
             roof["pipeline_GBs"] = round(frame_bytes * value / world / 1e9, 2)
             roof["pipeline_frac"] = round(frame_bytes * value / world / 1e9 / HBM_PEAK_GBS, 5)
         cpu = cpu_baseline(w, h, nf, args.cpu_seconds) if (world == 1 and args.cpu_seconds > 0) else None
+        if cpu is not None:
+            # the host's share of cores (OMP_NUM_THREADS on the GPU box), all at once
+            nthr = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1), 64))
+            cpu["all_cores"] = cpu_baseline_threads(w, h, nf, max(2.0, args.cpu_seconds / 2), nthr)
         matchers = matcher_latencies() if (world == 1 and not args.no_extras) else None
         if world == 1 and not args.no_extras:
             extras["bow_transform_orbvoc"] = bow_transform_throughput(torch)
