@@ -429,11 +429,11 @@ def run_config(torch, dist, rank, world, dev, w, h, nfeatures, batch, steps, war
 
 EXTRAS = [
     # key, mode, w, h, nfeatures, streams per GPU, unit
-    ("fhd_1920x1080", "mono", 1920, 1080, 1000, 64, "frames/s"),
+    ("fhd_1920x1080", "mono", 1920, 1080, 1000, 128, "frames/s"),
     ("stereo_euroc_752x480", "stereo", 752, 480, 1200, 128, "stereo pairs/s"),
     ("stereo_kitti_1241x376", "stereo", 1241, 376, 2000, 96, "stereo pairs/s"),
     ("stereo_fhd_1920x1080", "stereo", 1920, 1080, 1000, 32, "stereo pairs/s"),
-    ("rgbd_fhd_1920x1080", "rgbd", 1920, 1080, 1000, 64, "frames/s"),
+    ("rgbd_fhd_1920x1080", "rgbd", 1920, 1080, 1000, 128, "frames/s"),
 ]
 
 
@@ -442,7 +442,7 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=512, help="streams (frames per step) per GPU")
+    ap.add_argument("--batch", type=int, default=1024, help="streams (frames per step) per GPU")
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--nfeatures", type=int, default=1000)
