@@ -266,12 +266,29 @@ __global__ void k_ba_reduce(const EdgeOut *eo, const int32_t *offs, const int32_
     if (v >= nv) return;
     const int nh = kind ? 9 : 36, nb = kind ? 3 : 6;
     if (lane >= nh + nb) return;
+    // the field this lane sums, as a double offset into EdgeOut
+    const int fo = lane < nh ? (kind ? 36 + lane : lane) : (kind ? 63 + 6 + lane - nh : 63 + lane - nh);
+    const double *base = reinterpret_cast<const double *>(eo) + fo;
+    constexpr int kEo = sizeof(EdgeOut) / sizeof(double);
     double acc = 0;
-    for (int t = offs[v]; t < offs[v + 1]; ++t) {
+    // 8 edges' loads in flight, then their sum in edge order
+    int t = offs[v];
+    const int te = offs[v + 1];
+    for (; t + 8 <= te; t += 8) {
+        int ei[8];
+        double val[8];
+        uint8_t a[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ei[j] = list[t + j];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { a[j] = active[ei[j]]; val[j] = base[(int64_t)ei[j] * kEo]; }
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (a[j]) acc = acc + val[j];
+    }
+    for (; t < te; ++t) {
         const int ei = list[t];
-        if (!active[ei]) continue;
-        const EdgeOut &o = eo[ei];
-        acc = acc + (lane < nh ? (kind ? o.hll[lane] : o.hpp[lane]) : (kind ? o.bl[lane - nh] : o.bp[lane - nh]));
+        if (active[ei]) acc = acc + base[(int64_t)ei * kEo];
     }
     if (lane < nh) H[(int64_t)v * nh + lane] = acc;
     else b[(int64_t)v * nb + lane - nh] = acc;
@@ -356,6 +373,66 @@ __global__ void k_ba_pairs(const int2 *pairs, int npairs, const int32_t *coffs, 
     S[(int64_t)(6 * i2 + c) * n + 6 * i1 + r] = acc;   // mirror (the solver reads the full matrix)
 }
 
+// The same blocks with the shared points found lane-parallel: a wave walks
+// camera i1's list 64 entries at a time and looks each point up in camera
+// i2's point -> list-position map (cmap, -1: not observed).  Each matched
+// lane copies its operands (B Dinv and B rows) into LDS at its rank, so one
+// global round trip serves the chunk; the 36 entry lanes then subtract the
+// shared points in ascending point order.  Needs each (camera, point)
+// observed at most once (checked on the host).
+__global__ __launch_bounds__(256) void k_ba_pairs_map(const int2 *pairs, int npairs, const int32_t *coffs,
+                                                      const int32_t *clist, const int32_t *epoint, const int32_t *cmap,
+                                                      int npt, const EdgeOut *eo, const double *bdinv,
+                                                      const double *Hpp, double lambda, int nf, double *S) {
+    // per wave: the chunk's matched B Dinv (6x3) and B (hpl, 6x3) rows
+    __shared__ double ops[4][64][36];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int pi = blockIdx.x * (blockDim.x / 64) + w;
+    if (pi >= npairs) return;
+    const int i1 = pairs[pi].x, i2 = pairs[pi].y;
+    const int r = min(lane, 35) / 6, c = min(lane, 35) % 6;
+    double acc = 0;
+    if (i1 == i2) {
+        acc = Hpp[36 * (int64_t)i1 + min(lane, 35)];
+        if (r == c) acc = acc + lambda;
+    }
+    const int32_t *map2 = cmap + (int64_t)i2 * npt;
+    constexpr int kEo = sizeof(EdgeOut) / sizeof(double);
+    double (*op)[36] = ops[w];
+    for (int a0 = coffs[i1]; a0 < coffs[i1 + 1]; a0 += 64) {
+        const int a = a0 + lane;
+        int e1 = -1, e2 = -1;
+        if (a < coffs[i1 + 1]) {
+            e1 = clist[a];
+            const int pos = map2[epoint[e1]];
+            if (pos >= 0) e2 = clist[pos];
+        }
+        const uint64_t m = __ballot(e2 >= 0);
+        const int nm = __popcll(m);
+        if (e2 >= 0) {   // this lane's match goes to slot = its rank (point order)
+            const int slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            const double *bd = bdinv + 18 * (int64_t)e1;
+            const double *hp = reinterpret_cast<const double *>(eo) + (int64_t)e2 * kEo + 45;   // EdgeOut::hpl
+#pragma unroll
+            for (int k = 0; k < 18; ++k) { op[slot][k] = bd[k]; op[slot][18 + k] = hp[k]; }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        // S_rc -= sum_k BDinv_1[r][k] B_2[c][k], shared points in ascending order
+        for (int t = 0; t < nm; ++t) {
+            double sj = 0;
+            for (int k = 0; k < 3; ++k) sj = sj + op[t][3 * r + k] * op[t][18 + 3 * c + k];
+            acc = acc - sj;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (lane >= 36) return;
+    const int n = 6 * nf;
+    S[(int64_t)(6 * i1 + r) * n + 6 * i2 + c] = acc;
+    S[(int64_t)(6 * i2 + c) * n + 6 * i1 + r] = acc;   // mirror (the solver reads the full matrix)
+}
+
 // bschur = bp - sum over the camera's usable edges (point order) of B db.
 __global__ void k_ba_bschur(const double *bp, const int32_t *coffs, const int32_t *clist, const double *bdb, int nf,
                             double *bs) {
@@ -363,7 +440,16 @@ __global__ void k_ba_bschur(const double *bp, const int32_t *coffs, const int32_
     if (i >= 6 * nf) return;
     const int cam = i / 6, r = i % 6;
     double coef = 0;
-    for (int t = coffs[cam]; t < coffs[cam + 1]; ++t) coef = coef + bdb[6 * (int64_t)clist[t] + r];
+    int t = coffs[cam];
+    const int te = coffs[cam + 1];
+    for (; t + 8 <= te; t += 8) {   // 8 loads in flight, summed in order
+        double val[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) val[j] = bdb[6 * (int64_t)clist[t + j] + r];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) coef = coef + val[j];
+    }
+    for (; t < te; ++t) coef = coef + bdb[6 * (int64_t)clist[t] + r];
     bs[i] = bp[i] - coef;
 }
 
@@ -407,6 +493,60 @@ __global__ __launch_bounds__(1024) void k_ba_chol(double *S, int n, const double
             }
         }
     }
+}
+
+// The same factorisation and solves with S held in LDS (n <= kCholLds): the
+// same operations in the same order, without a global round trip per term.
+constexpr int kCholLds = 128;
+__global__ __launch_bounds__(1024) void k_ba_chol_lds(double *S, int n, const double *bs, double *x, int *ok) {
+    extern __shared__ double L[];   // n x n, then x (n)
+    double *xs = L + n * n;
+    __shared__ double diag;
+    __shared__ int bad;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < n * n; i += blockDim.x) L[i] = S[i];
+    if (tid == 0) bad = 0;
+    __syncthreads();
+    for (int j = 0; j < n; ++j) {
+        if (tid == 0) {
+            double d = L[j * n + j];
+#pragma unroll 8
+            for (int k = 0; k < j; ++k) d = d - L[j * n + k] * L[j * n + k];
+            if (!(d > 0)) bad = 1;
+            diag = sqrt(d);
+            L[j * n + j] = diag;
+        }
+        __syncthreads();
+        if (bad) break;
+        for (int i = j + 1 + tid; i < n; i += blockDim.x) {
+            double s = L[i * n + j];
+#pragma unroll 8
+            for (int k = 0; k < j; ++k) s = s - L[i * n + k] * L[j * n + k];
+            L[i * n + j] = s / diag;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        *ok = !bad;
+        if (!bad) {
+            for (int i = 0; i < n; ++i) {   // L y = b
+                double s = bs[i];
+#pragma unroll 8
+                for (int k = 0; k < i; ++k) s = s - L[i * n + k] * xs[k];
+                xs[i] = s / L[i * n + i];
+            }
+            for (int i = n - 1; i >= 0; --i) {   // L^T x = y
+                double s = xs[i];
+#pragma unroll 8
+                for (int k = i + 1; k < n; ++k) s = s - L[k * n + i] * xs[k];
+                xs[i] = s / L[i * n + i];
+            }
+        }
+    }
+    __syncthreads();
+    if (!bad)
+        for (int i = tid; i < n; i += blockDim.x) x[i] = xs[i];
+    for (int i = tid; i < n * n; i += blockDim.x) S[i] = L[i];   // the (partial) factor, as k_ba_chol leaves it
 }
 
 // xl = Dinv (bl - sum over the point's usable edges (camera order) of B^T xp)
@@ -559,6 +699,8 @@ public:
     double *d_Hpp = nullptr, *d_bp = nullptr, *d_Hll = nullptr, *d_bl = nullptr, *d_dinv = nullptr,
            *d_bdinv = nullptr, *d_bdb = nullptr, *d_S = nullptr, *d_bs = nullptr, *d_x = nullptr;
     int *d_ok = nullptr;
+    int32_t *d_cmap = nullptr;   // free camera x point -> position in its usable list (-1)
+    bool use_map = false;        // every (camera, point) observed at most once
     std::vector<uint8_t> act_;
     std::vector<int32_t> cv_offs_, cv_list_;   // all edges per free camera (reduce), edge order
 };
@@ -602,7 +744,8 @@ int BA::alloc() {
     const size_t bytes = 256 * 40 + sizeof(Pose) * nc * 2 + 8 * 3 * np * 2 + sizeof(EdgeD) * ne + 3 * ne +
                          8 * ne * 6 + sizeof(EdgeOut) * ne + 4 * (nf + 1 + ne + np + 1 + ne + ne + nf + 1 + ne) +
                          sizeof(int2) * std::max(npairs, 1) + 8 * (36 * nf + 6 * nf + 9 * np + 3 * np + 9 * np +
-                                                                   18 * ne + 6 * ne + n * n + n + n + 3 * np) + 256;
+                                                                   18 * ne + 6 * ne + n * n + n + n + 3 * np) +
+                         4 * nf * np + 256 * 2;
     if (hipMalloc(reinterpret_cast<void **>(&buf_), bytes) != hipSuccess) return ORBX_ENOMEM;
     uint8_t *p = buf_;
     d_pose = carve<Pose>(p, nc); d_pose_bk = carve<Pose>(p, nc);
@@ -620,6 +763,7 @@ int BA::alloc() {
     d_bdinv = carve<double>(p, 18 * ne); d_bdb = carve<double>(p, 6 * ne);
     d_S = carve<double>(p, n * n); d_bs = carve<double>(p, n); d_x = carve<double>(p, n + 3 * np);
     d_ok = carve<int>(p, 1);
+    d_cmap = carve<int32_t>(p, nf * np);
     if ((size_t)(p - buf_) > bytes) return ORBX_ENOMEM;
     auto up = [&](void *d, const void *h, size_t b) {
         return b == 0 || hipMemcpyAsync(d, h, b, hipMemcpyHostToDevice, st_) == hipSuccess;
@@ -659,10 +803,21 @@ void BA::set_active(const std::vector<uint8_t> &act) {
             const int e = g.plist[t];
             if (usable[e]) clist[fill[g.poses[g.edges[e].cam].free_idx]++] = e;
         }
+    // point -> list position per free camera, for k_ba_pairs_map
+    std::vector<int32_t> cmap((size_t)g.nf * g.npt, -1);
+    use_map = true;
+    for (int f = 0; f < g.nf && use_map; ++f)
+        for (int t = coffs[f]; t < coffs[f + 1]; ++t) {
+            int32_t &m = cmap[(size_t)f * g.npt + g.edges[clist[t]].point];
+            if (m >= 0) { use_map = false; break; }   // a point seen twice by one camera: merge kernel
+            m = t;
+        }
     (void)hipMemcpyAsync(d_active, act.data(), g.ne, hipMemcpyHostToDevice, st_);
     (void)hipMemcpyAsync(d_usable, usable.data(), g.ne, hipMemcpyHostToDevice, st_);
     (void)hipMemcpyAsync(d_coffs, coffs.data(), 4 * (g.nf + 1), hipMemcpyHostToDevice, st_);
     (void)hipMemcpyAsync(d_clist, clist.data(), 4 * clist.size(), hipMemcpyHostToDevice, st_);
+    if (use_map && !cmap.empty())
+        (void)hipMemcpyAsync(d_cmap, cmap.data(), 4 * cmap.size(), hipMemcpyHostToDevice, st_);
     (void)hipStreamSynchronize(st_);
 }
 
@@ -717,12 +872,24 @@ int BA::solve(double lambda, int *ok) {
     if (g.npt) hipLaunchKernelGGL(k_ba_point, dim3((g.npt + 255) / 256), dim3(256), 0, st_, d_Hll, d_bl, g.npt, lambda,
                                   d_eo, d_poffs, d_plist, d_usable, d_dinv, d_bdinv, d_bdb);
     if (g.nf) {
-        hipLaunchKernelGGL(k_ba_pairs, dim3((npairs + 3) / 4), dim3(256), 0, st_, d_pairs, npairs, d_coffs, d_clist,
-                           d_epoint, d_eo, d_bdinv, d_Hpp, lambda, g.nf, d_S);
+        if (use_map)
+            hipLaunchKernelGGL(k_ba_pairs_map, dim3((npairs + 3) / 4), dim3(256), 0, st_, d_pairs, npairs, d_coffs,
+                               d_clist, d_epoint, d_cmap, g.npt, d_eo, d_bdinv, d_Hpp, lambda, g.nf, d_S);
+        else
+            hipLaunchKernelGGL(k_ba_pairs, dim3((npairs + 3) / 4), dim3(256), 0, st_, d_pairs, npairs, d_coffs,
+                               d_clist, d_epoint, d_eo, d_bdinv, d_Hpp, lambda, g.nf, d_S);
         hipLaunchKernelGGL(k_ba_bschur, dim3((n + 255) / 256), dim3(256), 0, st_, d_bp, d_coffs, d_clist, d_bdb, g.nf,
                            d_bs);
         // (blocks of camera pairs without a shared point stay as the memset left them)
-        hipLaunchKernelGGL(k_ba_chol, dim3(1), dim3(1024), 0, st_, d_S, n, d_bs, d_x, d_ok);
+        if (n <= kCholLds) {
+            const int lb = 8 * (n * n + n);
+            if (lb > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void *>(k_ba_chol_lds),
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize, lb) != hipSuccess)
+                return ORBX_EIO;
+            hipLaunchKernelGGL(k_ba_chol_lds, dim3(1), dim3(1024), lb, st_, d_S, n, d_bs, d_x, d_ok);
+        } else {
+            hipLaunchKernelGGL(k_ba_chol, dim3(1), dim3(1024), 0, st_, d_S, n, d_bs, d_x, d_ok);
+        }
     }
     if (g.npt) hipLaunchKernelGGL(k_ba_backsub, dim3((g.npt + 255) / 256), dim3(256), 0, st_, d_dinv, d_bl, g.npt,
                                   d_eo, d_poffs, d_plist, d_usable, d_edges, d_pose, d_x, d_x + n);
