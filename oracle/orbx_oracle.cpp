@@ -1902,7 +1902,7 @@ struct OBA {
         }
         for (int i = n - 1; i >= 0; --i) {
             double s2 = x[i];
-            for (int k = i + 1; k < n; ++k) s2 = s2 - S[(size_t)k * n + i] * x[k];
+            for (int k = n - 1; k > i; --k) s2 = s2 - S[(size_t)k * n + i] * x[k];
             x[i] = s2 / S[(size_t)i * n + i];
         }
         for (int p = 0; p < npt; ++p) {

@@ -229,7 +229,9 @@ double orbo_bow_score_l1(const uint32_t *w1, const double *v1, int n1, const uin
  * two projection edges (types_six_dof_expmap.cpp:109-230), Huber
  * (robust_kernel_impl.cpp:65-91) and SE3Quat (se3quat.h).  The sums follow a
  * fixed order (edge order per vertex, ascending point per camera pair, a dense
- * Cholesky of the reduced system): g2o's own order is unspecified (it sorts
+ * Cholesky of the reduced system with k-ascending dot products, the
+ * forward solve's terms k-ascending and the backward solve's k-descending):
+ * g2o's own order is unspecified (it sorts
  * edges of equal ids) and Eigen's sparse LDLT differs, so parity with g2o is
  * to rounding -- unpinned.  Edge layout as orbx_ba_edge in include/orbx.h. */
 typedef struct {

@@ -488,65 +488,85 @@ __global__ __launch_bounds__(1024) void k_ba_chol(double *S, int n, const double
             }
             for (int i = n - 1; i >= 0; --i) {   // L^T x = y
                 double s = x[i];
-                for (int k = i + 1; k < n; ++k) s = s - S[(int64_t)k * n + i] * x[k];
+                for (int k = n - 1; k > i; --k) s = s - S[(int64_t)k * n + i] * x[k];
                 x[i] = s / S[(int64_t)i * n + i];
             }
         }
     }
 }
 
-// The same factorisation and solves with S held in LDS (n <= kCholLds): the
-// same operations in the same order, without a global round trip per term.
+__device__ inline double readlane_f64(double v, int l) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+// The same factorisation and solves with S held in LDS (n <= kCholLds), with
+// the work spread over the workgroup instead of one thread:
+//  - right-looking: at column k every wave scales the column in registers
+//    (lane t holds L(k+1+t, k)) and the trailing lower triangle is updated
+//    row per wave, lane per column.  Each entry still receives its terms
+//    L(i,m) L(j,m) in ascending m, so the factor equals the column-by-column
+//    one bit for bit; one barrier per column.  Column k of L is kept in the
+//    upper triangle's row k (untouched by the trailing updates), the
+//    diagonal in dg[].
+//  - the solves run column-sweep in one wave (lane r owns rows r and r+64):
+//    the forward terms arrive in ascending k as in the row loop, the
+//    backward terms in descending k (the order the oracle uses).
+// Row stride n+1 keeps the backward solve's column reads off one bank.
 constexpr int kCholLds = 128;
-__global__ __launch_bounds__(1024) void k_ba_chol_lds(double *S, int n, const double *bs, double *x, int *ok) {
-    extern __shared__ double L[];   // n x n, then x (n)
-    double *xs = L + n * n;
-    __shared__ double diag;
-    __shared__ int bad;
-    const int tid = threadIdx.x;
-    for (int i = tid; i < n * n; i += blockDim.x) L[i] = S[i];
-    if (tid == 0) bad = 0;
+__global__ __launch_bounds__(512) void k_ba_chol_lds(const double *S, int n, const double *bs, double *x, int *ok) {
+    extern __shared__ double L[];   // n rows of n+1, then dg (n)
+    const int ld = n + 1;
+    double *dg = L + n * ld;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
+    for (int r = w; r < n; r += nw)
+        for (int c = lane; c <= r; c += 64) L[r * ld + c] = S[(int64_t)r * n + c];
     __syncthreads();
-    for (int j = 0; j < n; ++j) {
-        if (tid == 0) {
-            double d = L[j * n + j];
-#pragma unroll 8
-            for (int k = 0; k < j; ++k) d = d - L[j * n + k] * L[j * n + k];
-            if (!(d > 0)) bad = 1;
-            diag = sqrt(d);
-            L[j * n + j] = diag;
+    bool good = true;
+    const int i0 = lane, i1 = lane + 64;   // (rows relative to k + 1)
+    for (int k = 0; k < n; ++k) {
+        const double d = L[k * ld + k];
+        if (!(d > 0)) {   // (every thread reads the same d: the break is uniform)
+            good = false;
+            break;
         }
-        __syncthreads();
-        if (bad) break;
-        for (int i = j + 1 + tid; i < n; i += blockDim.x) {
-            double s = L[i * n + j];
-#pragma unroll 8
-            for (int k = 0; k < j; ++k) s = s - L[i * n + k] * L[j * n + k];
-            L[i * n + j] = s / diag;
+        const double g = sqrt(d);
+        const int r0 = k + 1 + i0, r1 = k + 1 + i1;
+        const double a0 = r0 < n ? L[r0 * ld + k] / g : 0.0;
+        const double a1 = r1 < n ? L[r1 * ld + k] / g : 0.0;
+        if (w == 0) {
+            if (lane == 0) dg[k] = g;
+            if (r0 < n) L[k * ld + r0] = a0;
+            if (r1 < n) L[k * ld + r1] = a1;
+        }
+        for (int i = k + 1 + w; i < n; i += nw) {
+            const int t = i - k - 1;
+            const double ai = t < 64 ? readlane_f64(a0, t) : readlane_f64(a1, t - 64);
+            if (r0 <= i) L[i * ld + r0] = L[i * ld + r0] - ai * a0;
+            if (r1 <= i) L[i * ld + r1] = L[i * ld + r1] - ai * a1;
         }
         __syncthreads();
     }
-    if (tid == 0) {
-        *ok = !bad;
-        if (!bad) {
-            for (int i = 0; i < n; ++i) {   // L y = b
-                double s = bs[i];
-#pragma unroll 8
-                for (int k = 0; k < i; ++k) s = s - L[i * n + k] * xs[k];
-                xs[i] = s / L[i * n + i];
-            }
-            for (int i = n - 1; i >= 0; --i) {   // L^T x = y
-                double s = xs[i];
-#pragma unroll 8
-                for (int k = i + 1; k < n; ++k) s = s - L[k * n + i] * xs[k];
-                xs[i] = s / L[i * n + i];
-            }
-        }
+    if (w != 0) return;
+    if (lane == 0) *ok = good;
+    if (!good) return;
+    double s0 = i0 < n ? bs[i0] : 0.0, s1 = i1 < n ? bs[i1] : 0.0;
+    for (int k = 0; k < n; ++k) {   // L y = b
+        const double yk = (k < 64 ? readlane_f64(s0, k) : readlane_f64(s1, k - 64)) / dg[k];
+        if (lane == (k & 63)) (k < 64 ? s0 : s1) = yk;
+        if (i0 > k && i0 < n) s0 = s0 - L[k * ld + i0] * yk;
+        if (i1 > k && i1 < n) s1 = s1 - L[k * ld + i1] * yk;
     }
-    __syncthreads();
-    if (!bad)
-        for (int i = tid; i < n; i += blockDim.x) x[i] = xs[i];
-    for (int i = tid; i < n * n; i += blockDim.x) S[i] = L[i];   // the (partial) factor, as k_ba_chol leaves it
+    for (int k = n - 1; k >= 0; --k) {   // L^T x = y
+        const double xk = (k < 64 ? readlane_f64(s0, k) : readlane_f64(s1, k - 64)) / dg[k];
+        if (lane == (k & 63)) (k < 64 ? s0 : s1) = xk;
+        if (i0 < k) s0 = s0 - L[i0 * ld + k] * xk;
+        if (i1 < k) s1 = s1 - L[i1 * ld + k] * xk;
+    }
+    if (i0 < n) x[i0] = s0;
+    if (i1 < n) x[i1] = s1;
 }
 
 // xl = Dinv (bl - sum over the point's usable edges (camera order) of B^T xp)
@@ -882,11 +902,11 @@ int BA::solve(double lambda, int *ok) {
                            d_bs);
         // (blocks of camera pairs without a shared point stay as the memset left them)
         if (n <= kCholLds) {
-            const int lb = 8 * (n * n + n);
+            const int lb = 8 * (n * (n + 1) + n);
             if (lb > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void *>(k_ba_chol_lds),
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, lb) != hipSuccess)
                 return ORBX_EIO;
-            hipLaunchKernelGGL(k_ba_chol_lds, dim3(1), dim3(1024), lb, st_, d_S, n, d_bs, d_x, d_ok);
+            hipLaunchKernelGGL(k_ba_chol_lds, dim3(1), dim3(512), lb, st_, d_S, n, d_bs, d_x, d_ok);
         } else {
             hipLaunchKernelGGL(k_ba_chol, dim3(1), dim3(1024), 0, st_, d_S, n, d_bs, d_x, d_ok);
         }
