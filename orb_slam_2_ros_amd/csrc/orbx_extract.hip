@@ -189,6 +189,31 @@ __device__ inline int wave_stage_rect(uint8_t *dst, int ds, const uint8_t *img, 
 }
 
 
+// The same staging for rectangles of at most 64 dwords per row: lane =
+// (row in pass, dword), 64 / nd rows per pass, so each load's address is one
+// uniform row offset plus a fixed per-lane offset (no per-load index walk).
+template <int NB = 8>
+__device__ inline int wave_stage_rows(uint8_t *dst, int ds, const uint8_t *img, int pitch, int y0, int x0, int nr,
+                                      int nc, int lane) {
+    const int xa = x0 & ~3, o = x0 - xa;
+    const int nd = (o + nc + 3) >> 2;
+    const int R = div_small(64, nd);   // rows per pass
+    const int rl = div_small(lane, nd), k = lane - rl * nd;
+    const uint8_t *src = img + (int64_t)y0 * pitch + xa;
+    const int voff = mul24u(rl, pitch) + 4 * k, loff = mul24u(rl, ds) + 4 * k;
+    const int rmax = rl < R ? nr - rl : 0;   // this lane loads rows r0 + j R < rmax
+    for (int r0 = 0; r0 < nr; r0 += NB * R) {
+        uint32_t v[NB];
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+            if (r0 + j * R < rmax) v[j] = *reinterpret_cast<const uint32_t *>(src + mul24u(r0 + j * R, pitch) + voff);
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+            if (r0 + j * R < rmax) *reinterpret_cast<uint32_t *>(dst + mul24u(r0 + j * R, ds) + loff) = v[j];
+    }
+    return o;
+}
+
 // ===========================================================================
 // K1: bilinear level l from level l-1 (cv::resize INTER_LINEAR 8U, OpenCV 3.2
 // fixed point; SSE2 vertical rounding on the leading columns, scalar tail).
@@ -497,7 +522,7 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
     uint16_t *list = reinterpret_cast<uint16_t *>(scm + fl.score_bytes);   // (yy << 8 | xx), row-major
     int spitch;
     const uint8_t *img = level_ptr(p, fb, c.level, b, spitch);
-    const int o = wave_stage_rect(patch, PS, img, spitch, c.y0 - 3, c.x0 - 3, ch + 6, cw + 6, lane);
+    const int o = wave_stage_rows(patch, PS, img, spitch, c.y0 - 3, c.x0 - 3, ch + 6, cw + 6, lane);
     const uint8_t *pc = patch + 3 * PS + o + 3;         // interior pixel (0, 0)
     const uint64_t below = (1ull << lane) - 1;
     uint32_t *out_i = fb.cand + (int64_t)b * p.cand_cap + c.slot;
@@ -516,42 +541,76 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
         // A. compass pre-test: an arc of 9 covers two cyclically adjacent points
         //    of {0, 4, 8, 12}, so a pixel is a corner candidate only if some
         //    adjacent pair is all brighter (min of the pair > v + th) or all
-        //    darker (max of the pair < v - th).  A lane tests two horizontally
-        //    adjacent pixels at once in packed u16 halves; survivors are
-        //    compacted in row-major order.
+        //    darker (max of the pair < v - th).  A lane tests a dword-aligned
+        //    quad of 4 pixels from 5 aligned LDS dwords (the +-3 column
+        //    neighbours by byte alignment), as two packed u16 pairs (even and
+        //    odd pixels); survivors are compacted in row-major order.
         int nsurv = 0;
         {
-            const int hw = (cw + 1) >> 1;             // pixel pairs per row
-            const int npairs = hw * ch;
-            const int dyp = div_small(64, hw), dxp = 64 - dyp * hw;
-            int yy = div_small(lane, hw), px = lane - yy * hw;
+            // lane = (row in pass, quad of the row), 64 / nq rows per pass: a
+            // lane keeps its quad column, so its interior mask is fixed
+            const int qc0 = (o + 3) & ~3;                           // patch column of the first quad
+            const int nq = ((o + 2 + cw) >> 2) - (qc0 >> 2) + 1;   // quads per row
+            const int R = div_small(64, nq);
+            const int rl = div_small(lane, nq), qi = lane - rl * nq;
+            const int xx0 = qc0 - o - 3 + 4 * qi;   // interior x of the quad's byte 0
+            // candidate word: pixel j of the quad at bit 16 (j >> 1) + (j & 1)
+            uint32_t vmask = 0;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+                if (xx0 + jj >= 0 && xx0 + jj < cw) vmask |= 1u << (16 * (jj >> 1) + (jj & 1));
+            if (rl >= R) vmask = 0;   // (tail lanes: rows of the next pass)
+            const uint8_t *q0 = patch + mul24u(3 + rl, PS) + qc0 + 4 * qi;
             const u16x2 thv = {(unsigned short)th, (unsigned short)th};
-            for (int i0 = 0; i0 < npairs; i0 += 64) {
-                bool s0 = false, s1 = false;
-                const int xx = 2 * px;
-                if (i0 + lane < npairs) {
-                    const uint8_t *q = pc + yy * PS + xx;
-                    auto pr = [&](int d) { return as_u16x2((uint32_t)q[d] | ((uint32_t)q[d + 1] << 16)); };
-                    const u16x2 v = pr(0), a0 = pr(3 * PS), a4 = pr(3), a8 = pr(-3 * PS), a12 = pr(-3);
-                    const u16x2 hi = __builtin_elementwise_max(
-                        __builtin_elementwise_max(__builtin_elementwise_min(a0, a4), __builtin_elementwise_min(a8, a12)),
-                        __builtin_elementwise_max(__builtin_elementwise_min(a4, a8), __builtin_elementwise_min(a12, a0)));
-                    const u16x2 lo = __builtin_elementwise_min(
-                        __builtin_elementwise_min(__builtin_elementwise_max(a0, a4), __builtin_elementwise_max(a8, a12)),
-                        __builtin_elementwise_min(__builtin_elementwise_max(a4, a8), __builtin_elementwise_max(a12, a0)));
-                    // hi > v + th  or  lo + th < v, as saturating differences
-                    const u16x2 d = __builtin_elementwise_sub_sat(hi, v + thv) | __builtin_elementwise_sub_sat(v, lo + thv);
-                    s0 = d.x != 0;
-                    s1 = d.y != 0 && xx + 1 < cw;
+            int e = (rl << 8) + xx0;
+            for (int y0 = 0; y0 < ch; y0 += R, e += R << 8) {
+                uint32_t cand = 0;
+                if (rl + y0 < ch) {
+                    const uint8_t *q = q0 + mul24u(y0, PS);
+                    const uint32_t c = *reinterpret_cast<const uint32_t *>(q);
+                    const uint32_t l = *reinterpret_cast<const uint32_t *>(q - 4);
+                    const uint32_t r = *reinterpret_cast<const uint32_t *>(q + 4);
+                    const uint32_t up = *reinterpret_cast<const uint32_t *>(q - 3 * PS);
+                    const uint32_t dn = *reinterpret_cast<const uint32_t *>(q + 3 * PS);
+                    const uint32_t w4 = __builtin_amdgcn_alignbyte(r, c, 3);    // pixel j's x + 3
+                    const uint32_t w12 = __builtin_amdgcn_alignbyte(c, l, 1);   // pixel j's x - 3
+                    auto half = [&](uint32_t sel) -> u16x2 {   // 1 per candidate pixel of the pair
+                        const u16x2 v = as_u16x2(__builtin_amdgcn_perm(0u, c, sel));
+                        const u16x2 a0 = as_u16x2(__builtin_amdgcn_perm(0u, dn, sel));
+                        const u16x2 a4 = as_u16x2(__builtin_amdgcn_perm(0u, w4, sel));
+                        const u16x2 a8 = as_u16x2(__builtin_amdgcn_perm(0u, up, sel));
+                        const u16x2 a12 = as_u16x2(__builtin_amdgcn_perm(0u, w12, sel));
+                        // max over the cyclic pairs of the pair's min, and min of the max:
+                        // max(min(a,b), min(b,c), min(c,d), min(d,a)) = min(max(a,c), max(b,d))
+                        const u16x2 hi = __builtin_elementwise_min(__builtin_elementwise_max(a0, a8),
+                                                                   __builtin_elementwise_max(a4, a12));
+                        const u16x2 lo = __builtin_elementwise_max(__builtin_elementwise_min(a0, a8),
+                                                                   __builtin_elementwise_min(a4, a12));
+                        // hi > v + th  or  lo + th < v, as saturating differences
+                        const u16x2 d = __builtin_elementwise_sub_sat(hi, v + thv) | __builtin_elementwise_sub_sat(v, lo + thv);
+                        u16x2 m;   // min(d, 1) per half, kept one packed op
+                        asm("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(d), "s"(0x00010001u));
+                        return m;
+                    };
+                    cand = (__builtin_bit_cast(uint32_t, half(0x0c020c00u)) |
+                            (__builtin_bit_cast(uint32_t, half(0x0c030c01u)) << 1)) & vmask;
                 }
-                const uint64_t m0 = __ballot(s0), m1 = __ballot(s1);
-                const int pos = nsurv + __popcll(m0 & below) + __popcll(m1 & below);
-                const uint16_t e0 = (uint16_t)((yy << 8) | xx);
-                if (s0) list[pos] = e0;
-                if (s1) list[pos + s0] = (uint16_t)(e0 + 1);
-                nsurv += __popcll(m0) + __popcll(m1);
-                yy += dyp; px += dxp;
-                if (px >= hw) { px -= hw; ++yy; }
+                // compaction in row-major order: the lanes' counts (0..4) by their
+                // binary digits, one ballot each, then each lane's bits
+                const int cnt = __builtin_popcount(cand);
+                const uint64_t c1 = __ballot(cnt & 1), c2 = __ballot(cnt & 2), c4 = __ballot(cnt & 4);
+                if (c1 | c2 | c4) {
+                    auto below_cnt = [&](uint64_t m) {
+                        return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    };
+                    int pos = nsurv + below_cnt(c1) + 2 * below_cnt(c2) + 4 * below_cnt(c4);
+                    while (cand) {
+                        const int bt = __builtin_ctz(cand);
+                        list[pos++] = (uint16_t)(e + ((bt >> 3) | (bt & 1)));
+                        cand &= cand - 1u;
+                    }
+                    nsurv += __popcll(c1) + 2 * __popcll(c2) + 4 * __popcll(c4);
+                }
             }
         }
         wave_lds_fence();
