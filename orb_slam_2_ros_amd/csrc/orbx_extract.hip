@@ -1146,9 +1146,13 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
 #pragma unroll
     for (int q = 1; q < kMaxLevels; ++q) l += (q < p.nlevels && slot >= p.la[q].out_off) ? 1 : 0;
     const uint32_t key = slot < p.out_cap ? __builtin_amdgcn_readfirstlane(fb.sel[(int64_t)b * p.out_cap + slot]) : 0u;
+    // all kMaxLevels counts loaded unconditionally (one scalar burst, no
+    // load-wait chain), the levels past nlevels masked afterwards
     int cnt[kMaxLevels];
 #pragma unroll
-    for (int q = 0; q < kMaxLevels; ++q) cnt[q] = q < p.nlevels ? max(lc[q], 0) : 0;
+    for (int q = 0; q < kMaxLevels; ++q) cnt[q] = lc[q];
+#pragma unroll
+    for (int q = 0; q < kMaxLevels; ++q) cnt[q] = q < p.nlevels ? max(cnt[q], 0) : 0;
     if (write_total && bx == 0 && tid == 0) {
         int total = 0;
 #pragma unroll
@@ -1178,8 +1182,7 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
     int o = 0;
     if (px0 >= 0 && py0 >= 0 && x + kDescR < g.w && y + kDescR < g.h &&
         (px0 & ~3) + 4 * (((px0 & 3) + kDescP + 3) >> 2) <= spitch) {
-        o = wave_stage_rect<(kDescP * ((kDescP + 6) / 4) + 63) / 64>(lbase, kDescPS, img, spitch, py0, px0, kDescP, kDescP,
-                                                                   lane);
+        o = wave_stage_rows<(kDescP + 4) / 5>(lbase, kDescPS, img, spitch, py0, px0, kDescP, kDescP, lane);   // 5 rows a pass
     } else {
         for (int e = lane; e < kDescP * kDescP; e += 64) {
             const int r = e / kDescP, c = e - r * kDescP;
@@ -1232,6 +1235,7 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
     constexpr uint32_t kW0 = (uint32_t)kGaussTaps[0] | (uint32_t)kGaussTaps[1] << 8 |
                              (uint32_t)kGaussTaps[2] << 16 | (uint32_t)kGaussTaps[3] << 24;
     constexpr uint32_t kW1 = (uint32_t)kGaussTaps[4] | (uint32_t)kGaussTaps[5] << 8 | (uint32_t)kGaussTaps[6] << 16;
+    constexpr u16x2 kK01 = {(unsigned short)k0, (unsigned short)k1}, kK23 = {(unsigned short)k2, (unsigned short)k3};
     // One task = 4 consecutive outputs of one row at patch-aligned columns
     // 4s..4s+3 (window column = patch column - o): the 10 source bytes lie in
     // three aligned dwords.  Window columns 0..36 are patch columns o..o+36,
@@ -1276,8 +1280,12 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
         const int cc = __float2int_rn(__fsub_rn(__fmul_rn(px, ca), __fmul_rn(py, sa)));
         cols[k] = cc;
         const uint16_t *w = rowp + mul24u(r + kBlurR, kRowS) + (cc + kBlurR + o);   // r, cc in [-18, 18]
-        sums[k] = mul24u(k3, w[3 * kRowS]) + mul24u(k2, w[2 * kRowS] + w[4 * kRowS]) +
-                  mul24u(k1, w[kRowS] + w[5 * kRowS]) + mul24u(k0, w[0] + w[6 * kRowS]);
+        // k0 (w0 + w6) + k1 (w1 + w5) + k2 (w2 + w4) + k3 w3 as three u16-pair dot products
+        // (the pairs are loaded straight into register halves)
+        const u16x2 r01 = {w[0], w[kRowS]}, r65 = {w[6 * kRowS], w[5 * kRowS]}, r23 = {w[2 * kRowS], w[3 * kRowS]};
+        sums[k] = (int)__builtin_amdgcn_udot2(
+            r01, kK01, __builtin_amdgcn_udot2(r65, kK01, __builtin_amdgcn_udot2(r23, kK23, mul24u(k2, w[4 * kRowS]), false), false),
+            false);
     }
     int val[8];
     if (all_even) {
