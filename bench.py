@@ -93,6 +93,27 @@ def measured_traffic(stage: str, frames_per_launch: float):
         return None, None
 
 
+# VALU issue peak: 1024 SIMDs / 1.728 ns per wave-instruction per SIMD, the best
+# rate tools/ubench/valu_rate.hip measured on MI355X (profiles/r01_valu_issue_rate.txt)
+VALU_PEAK_GINST = 592.6
+VALU_PEAK_SOURCE = "profiles/r01_valu_issue_rate.txt"
+
+
+def measured_valu(stage: str, frames_per_launch: float):
+    """VALU wave-instructions per launch of the stage's kernel (SQ_INSTS_VALU
+    from the committed PMC pass, scaled from the profiled dispatch's frame
+    count); None if absent."""
+    try:
+        prof = json.loads(TRAFFIC_FILE.read_text())
+        name = STAGE_KERNEL[stage]
+        keys = [k for k in prof["kernels"] if k == name or k.startswith(name + "<") or k.startswith(name + "_w<")]
+        keys.sort(key=lambda k: "<false>" not in k)
+        k = prof["kernels"][keys[0]]
+        return round(k["valu_insts_per_dispatch"] / prof["frames_per_dispatch"] * frames_per_launch)
+    except (OSError, KeyError, ValueError, ZeroDivisionError, IndexError):
+        return None
+
+
 def cpu_baseline(w: int, h: int, nfeatures: int, budget_s: float):
     """The oracle (C++ restatement of the reference, 1 thread) on the same
     workload: extract + SearchForInitialization vs the previous frame."""
@@ -512,6 +533,13 @@ def main() -> int:
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                     "traffic_source": tsrc, "bytes_per_launch": bytes_launch,
                     "frames_per_launch": frames_per_launch}
+            valu = measured_valu(dom, frames_per_launch)
+            if valu:
+                # the same kernel against the VALU issue rate (its actual bound)
+                ach = valu / (cand[dom] * 1e-3) / 1e9
+                roof["issue"] = {"bound": "valu", "achieved": round(ach, 1), "peak": VALU_PEAK_GINST,
+                                 "unit": "G wave-instr/s", "frac": round(ach / VALU_PEAK_GINST, 4),
+                                 "insts_per_launch": valu, "source": tsrc, "peak_source": VALU_PEAK_SOURCE}
             frame_bytes = algorithmic_bytes(sizes, nkp_last, "frame")
             roof["pipeline_GBs"] = round(frame_bytes * value / world / 1e9, 2)
             roof["pipeline_frac"] = round(frame_bytes * value / world / 1e9 / HBM_PEAK_GBS, 5)

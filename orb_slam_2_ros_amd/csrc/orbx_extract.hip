@@ -189,14 +189,32 @@ __device__ inline int wave_stage_rect(uint8_t *dst, int ds, const uint8_t *img, 
 }
 
 
-// The same staging for rectangles of at most 64 dwords per row: lane =
-// (row in pass, dword), 64 / nd rows per pass, so each load's address is one
-// uniform row offset plus a fixed per-lane offset (no per-load index walk).
+// The same staging with a fixed lane -> (row in pass, dword) map, so each
+// load's address is one uniform row offset plus a fixed per-lane offset (no
+// per-load index walk): rows of at most 64 dwords go 64 / nd rows per pass;
+// wider rows one row per pass in 64-dword chunks, NB rows per round.
 template <int NB = 8>
 __device__ inline int wave_stage_rows(uint8_t *dst, int ds, const uint8_t *img, int pitch, int y0, int x0, int nr,
                                       int nc, int lane) {
     const int xa = x0 & ~3, o = x0 - xa;
     const int nd = (o + nc + 3) >> 2;
+    if (nd > 64) {
+        const uint8_t *src = img + (int64_t)y0 * pitch + xa;
+        for (int c0 = 0; c0 < nd; c0 += 64) {
+            const bool on = c0 + lane < nd;
+            const int voff = 4 * (c0 + lane);
+            for (int r0 = 0; r0 < nr; r0 += NB) {
+                uint32_t v[NB];
+#pragma unroll
+                for (int j = 0; j < NB; ++j)
+                    if (on && r0 + j < nr) v[j] = *reinterpret_cast<const uint32_t *>(src + mul24u(r0 + j, pitch) + voff);
+#pragma unroll
+                for (int j = 0; j < NB; ++j)
+                    if (on && r0 + j < nr) *reinterpret_cast<uint32_t *>(dst + mul24u(r0 + j, ds) + voff) = v[j];
+            }
+        }
+        return o;
+    }
     const int R = div_small(64, nd);   // rows per pass
     const int rl = div_small(lane, nd), k = lane - rl * nd;
     const uint8_t *src = img + (int64_t)y0 * pitch + xa;
@@ -341,7 +359,7 @@ __device__ inline void resize_tile(const DevPlan &p, const FrameBufs &fb, int l,
     const int r_hi = min(max(resize_src_raw(yl, a.sy) + 1, 0), gs.h - 1);
     int spitch;
     const uint8_t *src = level_ptr(p, fb, l - 1, b, spitch);
-    wave_stage_rect<NB>(win, a.win_stride, src, spitch, r_lo, c_lo, r_hi - r_lo + 1, c_hi - c_lo + 1, lane);
+    wave_stage_rows<NB>(win, a.win_stride, src, spitch, r_lo, c_lo, r_hi - r_lo + 1, c_hi - c_lo + 1, lane);
     // per-lane column constants: dword of the first source pixel, realignment,
     // and the v_perm selectors of the 4 pixel pairs (S[sx_k], S[sx_k + 1])
     const int rel0 = txk[0].src - (c_lo & ~3);
@@ -1344,11 +1362,13 @@ hipError_t launch_resize_level(const DevPlan &p, const Plan &hp, const FrameBufs
     if (!hp.rw.empty()) {
         const ResizeWave &a = hp.rw[l];
         const int waves = a.ntiles * B;
-        // one global round trip for the whole window when it fits 64 x 9 / 64 x 16 dwords
-        if (a.win_dwords <= 64 * 9)
+        // one global round trip for the whole window: NB >= the staging's row passes
+        if (a.stage_passes <= 9)
             hipLaunchKernelGGL(k_resize_w<9>, dim3((waves + 3) / 4), dim3(kThreads), 4 * a.win_bytes, st, p, fb, l, a, B);
-        else
+        else if (a.stage_passes <= 16)
             hipLaunchKernelGGL(k_resize_w<16>, dim3((waves + 3) / 4), dim3(kThreads), 4 * a.win_bytes, st, p, fb, l, a, B);
+        else
+            hipLaunchKernelGGL(k_resize_w<24>, dim3((waves + 3) / 4), dim3(kThreads), 4 * a.win_bytes, st, p, fb, l, a, B);
         return hipGetLastError();
     }
     const LevelGeom &g = hp.lv[l];
@@ -1505,6 +1525,7 @@ bool plan_resize_waves(Plan &hp) {
         }
         a.win_stride = 4 * nd_max;
         a.win_dwords = nr_max * nd_win;
+        a.stage_passes = nd_win <= 64 ? (nr_max + 64 / nd_win - 1) / (64 / nd_win) : nr_max;
         a.win_bytes = (nr_max * a.win_stride + 15) & ~15;
         if (4 * a.win_bytes > 64 * 1024) return false;
         hp.rw[l] = a;

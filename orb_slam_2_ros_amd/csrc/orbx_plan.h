@@ -89,6 +89,7 @@ struct ResizeWave {
     int win_stride = 0;        // LDS bytes per window row (dword multiple)
     int win_bytes = 0;         // LDS bytes per wave (16-B multiple)
     int win_dwords = 0;        // largest window, in staged dwords
+    int stage_passes = 0;      // row passes of the window staging (wave_stage_rows)
     int xtab_off = 0, ytab_off = 0;   // the level's tap tables
 };
 

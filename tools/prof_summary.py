@@ -92,6 +92,11 @@ def main():
                "note": "FETCH_SIZE x2 (gfx950) + WRITE_SIZE, KB x 1024, averaged over dispatches",
                "kernels": {k: {"hbm_bytes_per_dispatch": (2 * f[k][0] + w.get(k, (0.0, 0))[0]) * 1024.0,
                                "fetch_kb": f[k][0], "write_kb": w.get(k, (0.0, 0))[0]} for k in f}}
+        if a.sq:   # VALU wave-instructions per dispatch (whole device), for the issue roofline
+            vi = pmc(a.sq, "SQ_INSTS_VALU")
+            for k, d in out["kernels"].items():
+                if k in vi:
+                    d["valu_insts_per_dispatch"] = vi[k][0]
         with open(a.json, "w") as fh:
             json.dump(out, fh, indent=1)
     text = "\n".join(lines) + "\n"
