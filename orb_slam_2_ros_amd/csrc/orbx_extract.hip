@@ -590,28 +590,30 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
                     const uint32_t r = *reinterpret_cast<const uint32_t *>(q + 4);
                     const uint32_t up = *reinterpret_cast<const uint32_t *>(q - 3 * PS);
                     const uint32_t dn = *reinterpret_cast<const uint32_t *>(q + 3 * PS);
-                    const uint32_t w4 = __builtin_amdgcn_alignbyte(r, c, 3);    // pixel j's x + 3
-                    const uint32_t w12 = __builtin_amdgcn_alignbyte(c, l, 1);   // pixel j's x - 3
-                    auto half = [&](uint32_t sel) -> u16x2 {   // 1 per candidate pixel of the pair
+                    // pixel pairs (0, 2) and (1, 3) of the quad as u16 halves, straight from
+                    // the aligned dwords: v_perm picks any two bytes of (lo, hi) dword pairs
+                    auto half = [&](uint32_t sel, uint32_t sel4, uint32_t sel12) -> u16x2 {   // 1: candidate
                         const u16x2 v = as_u16x2(__builtin_amdgcn_perm(0u, c, sel));
                         const u16x2 a0 = as_u16x2(__builtin_amdgcn_perm(0u, dn, sel));
-                        const u16x2 a4 = as_u16x2(__builtin_amdgcn_perm(0u, w4, sel));
+                        const u16x2 a4 = as_u16x2(__builtin_amdgcn_perm(r, c, sel4));     // x + 3
                         const u16x2 a8 = as_u16x2(__builtin_amdgcn_perm(0u, up, sel));
-                        const u16x2 a12 = as_u16x2(__builtin_amdgcn_perm(0u, w12, sel));
+                        const u16x2 a12 = as_u16x2(__builtin_amdgcn_perm(c, l, sel12));   // x - 3
                         // max over the cyclic pairs of the pair's min, and min of the max:
                         // max(min(a,b), min(b,c), min(c,d), min(d,a)) = min(max(a,c), max(b,d))
                         const u16x2 hi = __builtin_elementwise_min(__builtin_elementwise_max(a0, a8),
                                                                    __builtin_elementwise_max(a4, a12));
                         const u16x2 lo = __builtin_elementwise_max(__builtin_elementwise_min(a0, a8),
                                                                    __builtin_elementwise_min(a4, a12));
-                        // hi > v + th  or  lo + th < v, as saturating differences
-                        const u16x2 d = __builtin_elementwise_sub_sat(hi, v + thv) | __builtin_elementwise_sub_sat(v, lo + thv);
+                        // hi > v + th  or  lo + th < v  <=>  max(hi - v, v - lo) > th (saturating)
+                        const u16x2 d = __builtin_elementwise_sub_sat(
+                            __builtin_elementwise_max(__builtin_elementwise_sub_sat(hi, v), __builtin_elementwise_sub_sat(v, lo)),
+                            thv);
                         u16x2 m;   // min(d, 1) per half, kept one packed op
                         asm("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(d), "s"(0x00010001u));
                         return m;
                     };
-                    cand = (__builtin_bit_cast(uint32_t, half(0x0c020c00u)) |
-                            (__builtin_bit_cast(uint32_t, half(0x0c030c01u)) << 1)) & vmask;
+                    cand = (__builtin_bit_cast(uint32_t, half(0x0c020c00u, 0x0c050c03u, 0x0c030c01u)) |
+                            (__builtin_bit_cast(uint32_t, half(0x0c030c01u, 0x0c060c04u, 0x0c040c02u)) << 1)) & vmask;
                 }
                 // compaction in row-major order: the lanes' counts (0..4) by their
                 // binary digits, one ballot each, then each lane's bits
