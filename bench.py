@@ -399,6 +399,10 @@ def run_config(torch, dist, rank, world, dev, w, h, nfeatures, batch, steps, war
     from orb_slam_2_ros_amd import ORBextractor
     ex = ORBextractor(nfeatures, 1.2, 8, 20, 7, device=dev.index)
     ex.reserve(w, h, 2 * batch if mode == "stereo" else batch)
+    if mode == "mono" and batch >= 64 and "ORBX_SPLIT" not in os.environ:
+        # two half-batches on forked streams: one half's latency-bound quadtree /
+        # matcher launches overlap the other half's VALU-bound ones
+        ex.split(2)
     host, depth = _resident_frames(mode, w, h, batch, rank)
     frames = torch.from_numpy(host).to(dev)
     dmaps = torch.from_numpy(depth).to(dev) if depth is not None else None
@@ -425,8 +429,9 @@ def run_config(torch, dist, rank, world, dev, w, h, nfeatures, batch, steps, war
         # per-stage launch durations (HIP events on the launch stream) from a
         # separate untimed pass with the level pipeline off (if it was on), so
         # each stage is one whole-batch launch that overlaps nothing
-        piped = ex.pipeline()
+        piped, parts = ex.pipeline(), ex.split()
         ex.pipeline(0)
+        ex.split(1)
         step(steps)
         sync()
         ex.set_profiling(True)
@@ -436,6 +441,7 @@ def run_config(torch, dist, rank, world, dev, w, h, nfeatures, batch, steps, war
         stages = ex.stage_times()
         ex.set_profiling(False)
         ex.pipeline(piped)
+        ex.split(parts)
     # sanity: the last step produced keypoints and matches / depths on stream 0
     kp, _ = ex.batch_download(0)
     if mode == "mono":
@@ -443,9 +449,8 @@ def run_config(torch, dist, rank, world, dev, w, h, nfeatures, batch, steps, war
     else:
         _, _, sane = ex.depth_download(0)
     el = max_over_ranks(torch, dist, world, el, dev)
-    parts = ex.split() if (mode == "mono" and batch >= 64) else 1
     ex.close()
-    return el, stages, len(kp), sane, batch / parts
+    return el, stages, len(kp), sane, float(batch)   # the profiled launches cover the whole batch
 
 
 EXTRAS = [
@@ -524,8 +529,8 @@ def main() -> int:
             # dominant HBM-streaming kernel by time among the stages with an algorithmic byte count
             cand = {n: s for n, s in stage_ms.items() if s and s > 0 and algorithmic_bytes(sizes, nkp_last, n) > 0}
             dom = max(cand, key=cand.get)
-            # one launch covers one part of the split batch; its duration is the
-            # part-0 stage time (the parts' launches overlap on the GPU)
+            # stage times come from the profiling pass: one whole-batch launch per
+            # stage, unsplit and unpipelined, overlapping nothing
             bytes_launch = algorithmic_bytes(sizes, nkp_last, dom) * frames_per_launch
             achieved = bytes_launch / (cand[dom] * 1e-3) / 1e9
             traffic, tsrc = measured_traffic(dom, frames_per_launch)
