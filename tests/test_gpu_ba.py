@@ -25,7 +25,9 @@ def test_ba_step_matches_oracle(robust, lam, oracle_mod):
     assert np.abs(xg - xo).max() <= 1e-12 * scale, np.abs(xg - xo).max() / scale
 
 
-@pytest.mark.parametrize("seed,n_local,n_points", [(1, 10, 1500), (2, 20, 3000), (3, 4, 300)])
+# (the reduced camera system: n <= 128 unknowns is factored in LDS, 30 local
+# keyframes take the global-memory Cholesky)
+@pytest.mark.parametrize("seed,n_local,n_points", [(1, 10, 1500), (2, 20, 3000), (3, 4, 300), (4, 30, 2500)])
 def test_local_ba_matches_oracle(seed, n_local, n_points, oracle_mod):
     P = make_ba_problem(n_local=n_local, n_fixed=4, n_points=n_points, seed=seed)
     Tg, Xg, og, ig = local_bundle_adjustment(P["Tcw"], P["fixed"], P["Xw"], P["edges"])
@@ -46,3 +48,14 @@ def test_local_ba_mono_only_and_empty(oracle_mod):
     e = P["edges"][:0]
     Tg, Xg, og, ig = local_bundle_adjustment(P["Tcw"], P["fixed"], P["Xw"], e)
     assert len(og) == 0
+
+
+def test_local_ba_repeated_observation(oracle_mod):
+    """A (camera, point) pair observed twice: the Schur pairs leave the
+    per-camera point maps for the merge walk, still identical to the oracle."""
+    P = make_ba_problem(n_local=6, n_fixed=2, n_points=600, seed=9)
+    e = np.concatenate([P["edges"], P["edges"][5:6], P["edges"][40:41]])
+    Tg, Xg, og, ig = local_bundle_adjustment(P["Tcw"], P["fixed"], P["Xw"], e)
+    To, Xo, oo, io = oracle_mod.local_ba(P["Tcw"], P["fixed"], P["Xw"], e)
+    assert ig == io and np.array_equal(og, oo)
+    assert np.array_equal(Tg, To) and np.array_equal(Xg, Xo)
