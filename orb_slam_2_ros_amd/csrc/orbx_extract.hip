@@ -196,6 +196,10 @@ __device__ inline int wave_stage_rect(uint8_t *dst, int ds, const uint8_t *img, 
 template <int NB = 8>
 __device__ inline int wave_stage_rows(uint8_t *dst, int ds, const uint8_t *img, int pitch, int y0, int x0, int nr,
                                       int nc, int lane) {
+    // (all wave-uniform: row offsets then come from the scalar unit)
+    pitch = __builtin_amdgcn_readfirstlane(pitch);
+    ds = __builtin_amdgcn_readfirstlane(ds);
+    nr = __builtin_amdgcn_readfirstlane(nr);
     const int xa = x0 & ~3, o = x0 - xa;
     const int nd = (o + nc + 3) >> 2;
     if (nd > 64) {
@@ -215,8 +219,8 @@ __device__ inline int wave_stage_rows(uint8_t *dst, int ds, const uint8_t *img, 
         }
         return o;
     }
-    const int R = div_small(64, nd);   // rows per pass
-    const int rl = div_small(lane, nd), k = lane - rl * nd;
+    const int R = __builtin_amdgcn_readfirstlane(div_small(64, nd));   // rows per pass (wave-uniform: SALU)
+    const int rl = div_small(lane, nd), k = lane - mul24u(rl, nd);
     const uint8_t *src = img + (int64_t)y0 * pitch + xa;
     const int voff = mul24u(rl, pitch) + 4 * k, loff = mul24u(rl, ds) + 4 * k;
     const int rmax = rl < R ? nr - rl : 0;   // this lane loads rows r0 + j R < rmax
@@ -569,8 +573,8 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
             // lane keeps its quad column, so its interior mask is fixed
             const int qc0 = (o + 3) & ~3;                           // patch column of the first quad
             const int nq = ((o + 2 + cw) >> 2) - (qc0 >> 2) + 1;   // quads per row
-            const int R = div_small(64, nq);
-            const int rl = div_small(lane, nq), qi = lane - rl * nq;
+            const int R = __builtin_amdgcn_readfirstlane(div_small(64, nq));
+            const int rl = div_small(lane, nq), qi = lane - mul24u(rl, nq);
             const int xx0 = qc0 - o - 3 + 4 * qi;   // interior x of the quad's byte 0
             // candidate word: pixel j of the quad at bit 16 (j >> 1) + (j & 1)
             uint32_t vmask = 0;
@@ -646,7 +650,7 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
             if (i0 + lane < nsurv) {
                 e = list[i0 + lane];
                 const int ey = e >> 8, ex = e & 0xFF;
-                const uint8_t *q = pc + ey * PS + ex;
+                const uint8_t *q = pc + mul24u(ey, PS) + ex;
                 const int v = q[0];
                 const int pr[16] = {q[3 * PS],  q[3 * PS + 1],  q[2 * PS + 2],  q[PS + 3],
                                     q[3],       q[-PS + 3],     q[-2 * PS + 2], q[-3 * PS + 1],
@@ -654,7 +658,7 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
                                     q[-3],      q[PS - 3],      q[2 * PS - 2],  q[3 * PS - 1]};
                 const int S = arc_score_bytes(pr, v);
                 corner = S > th;
-                if (corner) scm[(ey + 1) * SW + ex + 1] = (uint8_t)(S - 1);
+                if (corner) scm[mul24u(ey + 1, SW) + ex + 1] = (uint8_t)(S - 1);
             }
             const uint64_t m = __ballot(corner);
             wave_lds_fence();   // all survivor reads of this chunk precede the in-place writes
@@ -672,7 +676,7 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
                 const int e = list[i0 + lane];
                 ey = e >> 8;
                 ex = e & 0xFF;
-                const int si = (ey + 1) * SW + ex + 1;
+                const int si = mul24u(ey + 1, SW) + ex + 1;
                 sv = scm[si];
                 keep = sv > scm[si - 1] && sv > scm[si + 1] && sv > scm[si - SW - 1] && sv > scm[si - SW] &&
                        sv > scm[si - SW + 1] && sv > scm[si + SW - 1] && sv > scm[si + SW] && sv > scm[si + SW + 1];
@@ -1238,7 +1242,7 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
             const uint32_t si = __builtin_amdgcn_udot4(pm, 0x01010101u, 0u, false);
             s1 = __builtin_amdgcn_udot4(pm, wu, s1, false);
             s0 += si;
-            m01 += (ri - 15) * (int)si;
+            m01 += __mul24(ri - 15, (int)si);   // |ri - 15| <= 16, si <= 1020: 24-bit multiply
         }
         m10 = (int)s1 - 16 * (int)s0;
     }
