@@ -1208,10 +1208,16 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
         (px0 & ~3) + 4 * (((px0 & 3) + kDescP + 3) >> 2) <= spitch) {
         o = wave_stage_rows<(kDescP + 4) / 5>(lbase, kDescPS, img, spitch, py0, px0, kDescP, kDescP, lane);   // 5 rows a pass
     } else {
-        for (int e = lane; e < kDescP * kDescP; e += 64) {
-            const int r = e / kDescP, c = e - r * kDescP;
-            const int yy = reflect101(py0 + r, g.h), xx = reflect101(px0 + c, g.w);
-            lbase[r * kDescPS + c] = img[(int64_t)yy * spitch + xx];
+        // near a level border: lane = patch column (its reflect-101 column fixed),
+        // the rows in turn (the row's reflection is wave-uniform)
+        const int c = min(lane, kDescP - 1);
+        const int xx = reflect101(px0 + c, g.w);
+        const int sp = __builtin_amdgcn_readfirstlane(spitch);
+#pragma unroll 11
+        for (int r = 0; r < kDescP; ++r) {
+            const int yy = reflect101(py0 + r, g.h);
+            const uint8_t v = img[(int64_t)yy * sp + xx];
+            if (lane < kDescP) lbase[r * kDescPS + lane] = v;
         }
     }
     const uint8_t *patch = lbase + o;
