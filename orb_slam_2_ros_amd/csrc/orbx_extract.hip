@@ -1266,25 +1266,28 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
                              (uint32_t)kGaussTaps[2] << 16 | (uint32_t)kGaussTaps[3] << 24;
     constexpr uint32_t kW1 = (uint32_t)kGaussTaps[4] | (uint32_t)kGaussTaps[5] << 8 | (uint32_t)kGaussTaps[6] << 16;
     constexpr u16x2 kK01 = {(unsigned short)k0, (unsigned short)k1}, kK23 = {(unsigned short)k2, (unsigned short)k3};
-    // One task = 4 consecutive outputs of one row at patch-aligned columns
-    // 4s..4s+3 (window column = patch column - o): the 10 source bytes lie in
-    // three aligned dwords.  Window columns 0..36 are patch columns o..o+36,
-    // within the 40 computed; the others are padding.
-    for (int t = lane; t < kDescP * 10; t += 64) {
-        const int r = (t * 205) >> 11, sgi = t - r * 10;   // t / 10 for t < 1024
-        const uint32_t *ap = reinterpret_cast<const uint32_t *>(lbase + r * kDescPS + 4 * sgi);
-        const uint32_t d0 = ap[0], d1 = ap[1], d2 = ap[2];
-        uint32_t out[4];
+    // One task = 8 consecutive outputs of one row at patch-aligned columns
+    // 8s..8s+7 (window column = patch column - o): the 14 source bytes lie in
+    // four aligned dwords, every 4-byte window of them one v_alignbyte.
+    // Window columns 0..36 are patch columns o..o+36, within the 40 computed;
+    // the others are padding.
+    for (int t = lane; t < kDescP * 5; t += 64) {
+        const int r = (t * 205) >> 10, sgi = t - r * 5;   // t / 5 for t < 215
+        const uint32_t *ap = reinterpret_cast<const uint32_t *>(lbase + r * kDescPS + 8 * sgi);
+        const uint32_t d[4] = {ap[0], ap[1], ap[2], ap[3]};
+        auto win = [&](int k) {   // source bytes k..k+3
+            return (k & 3) ? __builtin_amdgcn_alignbyte(d[(k >> 2) + 1], d[k >> 2], k & 3) : d[k >> 2];
+        };
+        uint32_t out[8];
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            const uint32_t lo4 = m ? __builtin_amdgcn_alignbyte(d1, d0, m) : d0;
-            const uint32_t hi4 = m ? __builtin_amdgcn_alignbyte(d2, d1, m) : d1;
-            out[m] = __builtin_amdgcn_udot4(lo4, kW0, __builtin_amdgcn_udot4(hi4, kW1, 0u, false), false);
-        }
-        uint2 packed;
+        for (int m = 0; m < 8; ++m)
+            out[m] = __builtin_amdgcn_udot4(win(m), kW0, __builtin_amdgcn_udot4(win(m + 4), kW1, 0u, false), false);
+        uint4 packed;
         packed.x = out[0] | (out[1] << 16);
         packed.y = out[2] | (out[3] << 16);
-        *reinterpret_cast<uint2 *>(rowp + r * kRowS + 4 * sgi) = packed;
+        packed.z = out[4] | (out[5] << 16);
+        packed.w = out[6] | (out[7] << 16);
+        *reinterpret_cast<uint4 *>(rowp + r * kRowS + 8 * sgi) = packed;
     }
     wave_lds_fence();
 
