@@ -24,6 +24,14 @@ __constant__ __attribute__((aligned(16))) int8_t c_pattern[512][2] = {
 #undef ORBX_PATTERN_BEGIN
 #undef ORBX_PATTERN_END
 };
+// the same points as floats (the descriptor's rotation multiplies them in float)
+__constant__ __attribute__((aligned(16))) float c_pattern_f[512][2] = {
+#define ORBX_PATTERN_BEGIN
+#define ORBX_PATTERN_END
+#include "orb_pattern.inc"
+#undef ORBX_PATTERN_BEGIN
+#undef ORBX_PATTERN_END
+};
 
 // c_disc_mask[ri][g]: byte k kept iff column 4g - 16 + k lies in row ri - 15
 // of the orientation disc (kUmax, orbx_plan.h).
@@ -1155,9 +1163,10 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
     const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
     // this lane's 4 pattern pairs (bytes x0 y0 x1 y1 of pairs 2j, 2j + 1,
     // j = 64 grp + lane), fetched first so the loads overlap the staging
-    uint32_t pat[4], dmask[4];
+    float4 pat[4];
+    uint32_t dmask[4];
 #pragma unroll
-    for (int grp = 0; grp < 4; ++grp) pat[grp] = reinterpret_cast<const uint32_t *>(c_pattern)[grp * 64 + lane];
+    for (int grp = 0; grp < 4; ++grp) pat[grp] = reinterpret_cast<const float4 *>(c_pattern_f)[grp * 64 + lane];
 #pragma unroll
     for (int i = 0; i < 4; ++i) dmask[i] = c_disc_mask.m[(lane >> 3) + 8 * i][lane & 7];
     int bx, b;
@@ -1307,12 +1316,17 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
     int sums[8], cols[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        const uint32_t pw = pat[k >> 1] >> (16 * (k & 1));
-        const float px = (float)(int8_t)pw, py = (float)(int8_t)(pw >> 8);
-        const int r = __float2int_rn(__fadd_rn(__fmul_rn(px, sa), __fmul_rn(py, ca)));
-        const int cc = __float2int_rn(__fsub_rn(__fmul_rn(px, ca), __fmul_rn(py, sa)));
+        const float px = (k & 1) ? pat[k >> 1].z : pat[k >> 1].x, py = (k & 1) ? pat[k >> 1].w : pat[k >> 1].y;
+        // cvRound by the 1.5 * 2^23 bias: the float add rounds to the nearest
+        // integer, ties to even, and the bits are then 0x4B400000 + n (|n| < 2^22)
+        constexpr float kRndBias = 12582912.f;
+        const int rb = __float_as_int(__fadd_rn(__fadd_rn(__fmul_rn(px, sa), __fmul_rn(py, ca)), kRndBias));
+        const int cb = __float_as_int(__fadd_rn(__fsub_rn(__fmul_rn(px, ca), __fmul_rn(py, sa)), kRndBias));
+        const int cc = cb - 0x4B400000;
         cols[k] = cc;
-        const uint16_t *w = rowp + mul24u(r + kBlurR, kRowS) + (cc + kBlurR + o);   // r, cc in [-18, 18]
+        // mul24u sees the low 24 bits of rb + kBlurR: 0x400000 + r + kBlurR (r, cc in [-18, 18])
+        const int roff = (int)mul24u(rb + kBlurR, kRowS) - kRowS * 0x400000;
+        const uint16_t *w = rowp + roff + (cc + kBlurR + o);
         // k0 (w0 + w6) + k1 (w1 + w5) + k2 (w2 + w4) + k3 w3 as three u16-pair dot products
         // (the pairs are loaded straight into register halves)
         const u16x2 r01 = {w[0], w[kRowS]}, r65 = {w[6 * kRowS], w[5 * kRowS]}, r23 = {w[2 * kRowS], w[3 * kRowS]};
