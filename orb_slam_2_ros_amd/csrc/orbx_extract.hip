@@ -500,8 +500,8 @@ __global__ __launch_bounds__(kThreads) void k_blur(DevPlan p, FrameBufs fb) {
 // for pixels that pass a compass pre-test at the pass's threshold.  NMS is the
 // strict 3x3 test inside the cell (outside neighbours count 0, as FAST on the
 // cell sub-image sees them).  As the reference, a pass at iniThFAST comes
-// first and a pass at minThFAST only for a cell it left empty (about one cell
-// in eight); the count word says which list the cell uses (bit 31 =
+// first and a pass at minThFAST only for a cell it left empty (27 % of the
+// level-0 cells of the bench frames); the count word says which list the cell uses (bit 31 =
 // minThFAST, ORBextractor.cc:846-850).
 // Output: keypoints in row-major order, packed (x | y<<12 | s<<24).
 // ===========================================================================
