@@ -89,8 +89,10 @@ __device__ inline int xcd_logical_block(int j, int n) {
 __device__ inline void xcd_block_2d(int &bx, int &by) {
     const int n = gridDim.x * gridDim.y;
     const int L = xcd_logical_block(blockIdx.y * gridDim.x + blockIdx.x, n);
-    by = L / gridDim.x;
-    bx = L - by * gridDim.x;
+    // (the division runs on the VALU; readfirstlane hands the wave-uniform
+    // results back to the scalar unit, so the code that depends on them stays SALU)
+    by = __builtin_amdgcn_readfirstlane(L / gridDim.x);
+    bx = __builtin_amdgcn_readfirstlane(L - by * gridDim.x);
 }
 
 // The wave's index in its workgroup as a scalar: the compiler cannot prove
@@ -227,7 +229,7 @@ __device__ inline int wave_stage_rows(uint8_t *dst, int ds, const uint8_t *img, 
         }
         return o;
     }
-    const int R = __builtin_amdgcn_readfirstlane(div_small(64, nd));   // rows per pass (wave-uniform: SALU)
+    const int R = __builtin_amdgcn_readfirstlane(div_small(64, nd));   // rows per pass (wave-uniform)
     const int rl = div_small(lane, nd), k = lane - mul24u(rl, nd);
     const uint8_t *src = img + (int64_t)y0 * pitch + xa;
     const int voff = mul24u(rl, pitch) + 4 * k, loff = mul24u(rl, ds) + 4 * k;
@@ -1175,9 +1177,16 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
     const int slot = s0 + bx * 4 + wave;
     // level of this slot from the kernel-argument offsets; the key and the
     // level counts are independent loads issued together
+    // (scalar compare-selects: the compiler turns `(a && b) ? 1 : 0` on
+    // wave-uniform values into lane masks and v_cndmask + readfirstlane)
+    auto s_ge = [](int a, int b) {
+        int r;
+        asm("s_cmp_ge_i32 %1, %2\n\ts_cselect_b32 %0, 1, 0" : "=s"(r) : "s"(a), "s"(b) : "scc");
+        return r;
+    };
     int l = 0;
 #pragma unroll
-    for (int q = 1; q < kMaxLevels; ++q) l += (q < p.nlevels && slot >= p.la[q].out_off) ? 1 : 0;
+    for (int q = 1; q < kMaxLevels; ++q) l += s_ge(p.nlevels - 1, q) & s_ge(slot, p.la[q].out_off);
     const uint32_t key = slot < p.out_cap ? __builtin_amdgcn_readfirstlane(fb.sel[(int64_t)b * p.out_cap + slot]) : 0u;
     // all kMaxLevels counts loaded unconditionally (one scalar burst, no
     // load-wait chain), the levels past nlevels masked afterwards
