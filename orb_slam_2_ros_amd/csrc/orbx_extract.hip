@@ -565,9 +565,9 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
     // for a cell where that found nothing (ORBextractor.cc:842-850).
     auto pass = [&](int th, uint32_t *out) -> int {
         {
-            uint32_t *z0 = reinterpret_cast<uint32_t *>(scm);
-            const int nz = fl.score_bytes >> 2;
-            for (int i = lane; i < nz; i += 64) z0[i] = 0;
+            uint4 *z0 = reinterpret_cast<uint4 *>(scm);   // (16-B aligned; score_bytes a multiple of 16)
+            const int nz = fl.score_bytes >> 4;
+            for (int i = lane; i < nz; i += 64) z0[i] = make_uint4(0u, 0u, 0u, 0u);
         }
         wave_lds_fence();
         // A. compass pre-test: an arc of 9 covers two cyclically adjacent points
