@@ -17,14 +17,7 @@
 
 namespace orbx {
 
-__constant__ __attribute__((aligned(16))) int8_t c_pattern[512][2] = {
-#define ORBX_PATTERN_BEGIN
-#define ORBX_PATTERN_END
-#include "orb_pattern.inc"
-#undef ORBX_PATTERN_BEGIN
-#undef ORBX_PATTERN_END
-};
-// the same points as floats (the descriptor's rotation multiplies them in float)
+// rBRIEF sampling points as floats (the descriptor's rotation multiplies them in float)
 __constant__ __attribute__((aligned(16))) float c_pattern_f[512][2] = {
 #define ORBX_PATTERN_BEGIN
 #define ORBX_PATTERN_END
