@@ -96,6 +96,15 @@ int orbx_extract_batch_device(orbx_extractor *ex, const uint8_t *d_images,
  * counts d_counts[b]. */
 int orbx_batch_results_device(orbx_extractor *ex, const orbx_keypoint **d_kps,
                               const uint8_t **d_desc, const int32_t **d_counts);
+/* Keyframe publication for the cross-stream exchange (config C5; the
+ * reference's analogue is KeyFrameDatabase::add, KeyFrameDatabase.cc:41-48,
+ * fed by LoopClosing::InsertKeyFrame, LoopClosing.cc:96): copies the current result slot into
+ * one contiguous device buffer, ready for an RCCL all-gather --
+ *   int32 counts[B] (padded to 64 B) | orbx_keypoint [B][kp_stride] |
+ *   uint8 desc [B][kp_stride][32]
+ * *bytes = the size of that layout (d_out may be NULL to query it).
+ * Asynchronous on `stream`; ORBX_ERANGE if cap < *bytes. */
+int orbx_batch_pack_device(orbx_extractor *ex, void *d_out, int64_t cap, int64_t *bytes, void *stream);
 /* Synchronous host copy of frame b of the current result slot. */
 int orbx_batch_download(orbx_extractor *ex, int frame, orbx_keypoint *kps, uint8_t *desc,
                         int cap, int *n);

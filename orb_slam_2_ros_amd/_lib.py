@@ -81,6 +81,7 @@ _SIGNATURES = {
     "orbx_extractor_kp_stride": (I32, [P]),
     "orbx_extract_batch_device": (I32, [P, P, I64, I32, I32, P]),
     "orbx_batch_results_device": (I32, [P, P, P, P]),
+    "orbx_batch_pack_device": (I32, [P, P, I64, P, P]),
     "orbx_batch_download": (I32, [P, I32, P, P, I32, P]),
     "orbx_mono_step_device": (I32, [P, P, I64, I32, I32, I32, F32, I32, P]),
     "orbx_mono_matches_download": (I32, [P, I32, P, I32, P, P]),

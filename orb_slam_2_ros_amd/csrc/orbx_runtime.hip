@@ -668,6 +668,27 @@ int orbx_batch_results_device(orbx_extractor *ex, const orbx_keypoint **d_kps, c
     return ORBX_OK;
 }
 
+int orbx_batch_pack_device(orbx_extractor *ex, void *d_out, int64_t cap, int64_t *bytes, void *stream) {
+    if (!ex || !ex->planned || !bytes) return ORBX_EINVAL;
+    const auto &s = ex->slot[ex->cur];
+    const int64_t B = s.batch, K = ex->plan.max_kps;
+    const int64_t head = (4 * B + 63) / 64 * 64;
+    const int64_t need = head + B * K * (int64_t)sizeof(orbx_keypoint) + B * K * 32;
+    *bytes = need;
+    if (B <= 0) return ORBX_EINVAL;
+    if (!d_out) return ORBX_OK;
+    if (cap < need) return ORBX_ERANGE;
+    if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
+    hipStream_t st = stream_of(ex, stream);
+    auto *o = static_cast<uint8_t *>(d_out);
+    if (hipMemcpyAsync(o, s.nkps, 4 * B, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(o + head, s.kps, B * K * sizeof(orbx_keypoint), hipMemcpyDeviceToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(o + head + B * K * (int64_t)sizeof(orbx_keypoint), s.desc, B * K * 32,
+                       hipMemcpyDeviceToDevice, st) != hipSuccess)
+        return ORBX_EIO;
+    return ORBX_OK;
+}
+
 int orbx_batch_download(orbx_extractor *ex, int frame, orbx_keypoint *kps, uint8_t *desc, int cap, int *n) {
     if (!ex || !ex->planned || !n) return ORBX_EINVAL;
     const auto &s = ex->slot[ex->cur];

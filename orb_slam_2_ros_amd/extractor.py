@@ -162,6 +162,20 @@ class ORBextractor:
                                             ctypes.byref(nk)), "depth_download")
         return ur[:n.value].copy(), dp[:n.value].copy(), nk.value
 
+    def pack_bytes(self) -> int:
+        """Size of the orbx_batch_pack_device layout for the current batch."""
+        nb = ctypes.c_int64(0)
+        check(self._lib.orbx_batch_pack_device(self._h, None, 0, ctypes.byref(nb), None), "pack size")
+        return nb.value
+
+    def pack_device(self, d_out: int, cap: int, stream: int | None = None) -> int:
+        """Copy the current results (counts | keypoints | descriptors) into a
+        device buffer for the keyframe all-gather; returns the bytes written."""
+        nb = ctypes.c_int64(0)
+        check(self._lib.orbx_batch_pack_device(self._h, ctypes.c_void_p(d_out), cap, ctypes.byref(nb),
+                                               ctypes.c_void_p(stream or 0)), "pack_device")
+        return nb.value
+
     def batch_download(self, frame: int):
         cap = self.kp_stride()
         kps = np.zeros(cap, dtype=KEYPOINT_DTYPE)
