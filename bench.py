@@ -93,10 +93,17 @@ def measured_traffic(stage: str, frames_per_launch: float):
         return None, None
 
 
-# VALU issue peak: 1024 SIMDs / 1.728 ns per wave-instruction per SIMD, the best
-# rate tools/ubench/valu_rate.hip measured on MI355X (profiles/r01_valu_issue_rate.txt)
-VALU_PEAK_GINST = 592.6
-VALU_PEAK_SOURCE = "profiles/r01_valu_issue_rate.txt"
+# VALU issue ceilings measured on MI355X with the clock each launch held
+# (s_memtime / s_memrealtime; profiles/r02_valu_rate_clock.txt, r02_valu_ops.txt):
+# - full rate: v_add/sub/and/or/xor/lshrrev_b32, 16-bit VOP2 min/max/sub, f32
+#   add/mul/fma, mov -- 0.908 ns per wave-instruction per SIMD at 16 waves/SIMD
+#   (2.14 cycles at 2.36 GHz): 1024 SIMDs / 0.908 ns = 1128 G wave-instr/s;
+# - half rate: u32 min/max, every 3-operand integer op, v_perm / alignbyte /
+#   bfe, packed 16-bit, dot2/dot4, DPP, cvt, any op with an SGPR operand --
+#   1.727 ns (4.15 cycles): 593 G wave-instr/s.
+VALU_PEAK_GINST = 1127.8
+VALU_HALF_RATE_GINST = 592.9
+VALU_PEAK_SOURCE = "profiles/r02_valu_rate_clock.txt, profiles/r02_valu_ops.txt"
 
 
 def measured_valu(stage: str, frames_per_launch: float):
@@ -114,11 +121,24 @@ def measured_valu(stage: str, frames_per_launch: float):
         return None
 
 
+def cpu_model() -> str:
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(w: int, h: int, nfeatures: int, budget_s: float):
-    """The oracle (C++ restatement of the reference, 1 thread) on the same
-    workload: extract + SearchForInitialization vs the previous frame."""
+    """The oracle (C++ restatement of the reference, scalar primitives as
+    written -- not OpenCV-SIMD/IPP) on the same workload, 1 thread: extract +
+    SearchForInitialization vs the previous frame.  Timed on the oracle's
+    -O3 -march=native build (oracle.use_timing_build)."""
     from oracle import oracle
     from orb_slam_2_ros_amd import synth
+    build = oracle.use_timing_build()
     frames = synth.frames(w, h, 4242, 8)
     prev = oracle.extract(frames[0], nfeatures)
     n = 0
@@ -135,7 +155,9 @@ def cpu_baseline(w: int, h: int, nfeatures: int, budget_s: float):
         if el >= budget_s:
             break
     return {"value": n / el, "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"{n} consecutive {w}x{h} synthetic frames ({el:.1f} s), oracle/liborbx_oracle.so, 1 thread"}
+            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "build": build,
+            "sample": f"{n} consecutive {w}x{h} synthetic frames ({el:.1f} s), oracle timing build, 1 thread; "
+                      "restated reference, scalar primitives (not OpenCV-SIMD/IPP)"}
 
 
 def cpu_baseline_threads(w: int, h: int, nfeatures: int, budget_s: float, threads: int):
@@ -367,48 +389,227 @@ def keyframe_exchange(torch, dist, world, dev, kfs_per_rank=8, nkp=1000, reps=10
         12 * len(r["words"]) + 60 * len(r["keys"]) + 16 for r in recs)), "ms": round(1e3 * float(np.median(ts)), 4)}
 
 
-def _resident_frames(mode, w, h, batch, rank):
-    """Host array [FRAMES_PER_STREAM, frames_per_step, h, w] (+ depth maps for RGB-D)."""
+def stream_partition(total: int, world: int, rank: int) -> list:
+    """Global stream ids a rank owns: stream s -> rank s mod G (SURVEY.md §8(e),
+    stream-affine; a stereo pair is one stream and stays on one GPU)."""
+    return list(range(rank, total, world))
+
+
+def stream_scene(s: int) -> int:
+    """Synthetic scene of global stream s: the content is a function of the
+    stream id alone, so a stream's frames (and outputs) do not depend on how
+    many ranks share the job.  UNIQUE_SCENES distinct scenes keep the set-up
+    cheap at 1024 streams per GPU."""
+    return s % UNIQUE_SCENES
+
+
+def scene_frames(mode, w, h, scene):
+    """The FRAMES_PER_STREAM resident frames of one scene: [T, h, w] (mono /
+    RGB-D) or [T, 2, h, w] (stereo L/R, 20-px disparity)."""
     from orb_slam_2_ros_amd import synth
-    nsc = min(UNIQUE_SCENES, batch)
+    seed = 7000 + scene
+    if mode == "stereo":
+        canvas = synth.stream_canvas(w, h, seed)
+        out = np.empty((FRAMES_PER_STREAM, 2, h, w), np.uint8)
+        for t in range(FRAMES_PER_STREAM):
+            out[t, 0] = synth.frame_from_canvas(canvas, w, h, t, seed * 7919 + t)
+            out[t, 1] = synth.frame_from_canvas(canvas, w, h, t, seed * 7919 + t + 500009, disparity=20)
+        return out
+    return synth.frames(w, h, seed, FRAMES_PER_STREAM)
+
+
+def dropin_latency(torch, dev, reps=30):
+    """The drop-in path as ORB-SLAM2 drives it, one frame per call:
+    - `ORBextractor::operator()` on a host image (Frame::ExtractORB,
+      Frame.cc:259-265, from Tracking::GrabImage*, Tracking.cc:247-276),
+      host keypoints/descriptors out, synchronous -- VGA, HD and FHD;
+    - a stereo pair: two extractors (Frame.cc:79-82 runs them on two threads)
+      + Frame::ComputeStereoMatches (Frame.cc:502-676), EuRoC size;
+    - the batched device step at B in {1, 8, 64, 256} VGA frames per launch;
+    next to the oracle's single-thread latency on the same frames."""
+    from oracle import oracle
+    from orb_slam_2_ros_amd import ORBextractor, synth
+    from orb_slam_2_ros_amd.depth import compute_stereo_matches
+
+    def med(fn, k):
+        ts = []
+        for _ in range(k):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return 1e3 * float(np.median(ts))
+
+    out = {}
+    for key, w, h in (("vga", 640, 480), ("hd", 1280, 720), ("fhd", 1920, 1080)):
+        img = synth.frame(w, h, 4242)
+        ex = ORBextractor(1000, 1.2, 8, 20, 7, device=dev.index)
+        ex(img)
+        out[f"extract_host_{key}"] = {"gpu_ms": round(med(lambda: ex(img), reps), 4),
+                                      "cpu_ms": round(med(lambda: oracle.extract(img), 3), 3)}
+        ex.close()
+    w, h = 752, 480
+    L, R = synth.stereo_pair(w, h, 4243)
+    exl, exr = ORBextractor(1200, 1.2, 8, 20, 7, device=dev.index), ORBextractor(1200, 1.2, 8, 20, 7, device=dev.index)
+    bf, fx = 47.9, 435.2
+    mb = float(np.float32(bf) / np.float32(fx))
+
+    def pair():
+        kl, dl = exl(L)
+        kr, dr = exr(R)
+        return compute_stereo_matches(exl, exr, kl, dl, kr, dr, bf, mb)
+
+    def pair_cpu():
+        kl, dl = oracle.extract(L, 1200)
+        kr, dr = oracle.extract(R, 1200)
+        return oracle.compute_stereo_matches(oracle.pyramid(L), oracle.pyramid(R), kl, dl, kr, dr, bf, mb)
+
+    pair()
+    out["stereo_pair_host_euroc"] = {"gpu_ms": round(med(pair, reps), 4), "cpu_ms": round(med(pair_cpu, 3), 3)}
+    exl.close()
+    exr.close()
+    # batched device step, VGA mono (extract + SearchForInitialization)
+    w, h = 640, 480
+    base = synth.frames(w, h, 4244, FRAMES_PER_STREAM)
+    sweep = {}
+    sp = torch.cuda.current_stream(dev).cuda_stream
+    for B in (1, 8, 64, 256):
+        ex = ORBextractor(1000, 1.2, 8, 20, 7, device=dev.index)
+        ex.reserve(w, h, B)
+        fr = torch.from_numpy(np.ascontiguousarray(np.repeat(base[:, None], B, axis=1))).to(dev)
+        k = [0]
+
+        def step():
+            ex.mono_step_device(fr[k[0] % FRAMES_PER_STREAM].data_ptr(), w * h, w, B, 100, 0.9, True, sp)
+            k[0] += 1
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize(dev)
+        n = 20
+        t0 = time.perf_counter()
+        for _ in range(n):
+            step()
+        torch.cuda.synchronize(dev)
+        ms = 1e3 * (time.perf_counter() - t0) / n
+        sweep[str(B)] = {"ms_per_step": round(ms, 4), "frames_per_s": round(B / (ms * 1e-3), 1),
+                         "us_per_frame": round(1e3 * ms / B, 3)}
+        ex.close()
+        del fr
+    out["mono_step_device_vga_batch_sweep"] = sweep
+    return out
+
+
+def _resident_frames(mode, w, h, streams):
+    """Host array [FRAMES_PER_STREAM, frames_per_step, h, w] for this rank's
+    global stream ids (+ float32 depth maps for RGB-D): local slot b holds
+    stream streams[b] (stereo: slots 2b / 2b+1 its left / right image)."""
+    from orb_slam_2_ros_amd import synth
+    batch = len(streams)
+    cache = {}
     depth = None
     if mode == "stereo":
         host = np.empty((FRAMES_PER_STREAM, 2 * batch, h, w), np.uint8)
-        for s in range(nsc):
-            seed = 7000 + 97 * rank + s
-            canvas = synth.stream_canvas(w, h, seed)
-            for t in range(FRAMES_PER_STREAM):
-                L = synth.frame_from_canvas(canvas, w, h, t, seed * 7919 + t)
-                R = synth.frame_from_canvas(canvas, w, h, t, seed * 7919 + t + 500009, disparity=20)
-                for b in range(s, batch, nsc):
-                    host[t, 2 * b], host[t, 2 * b + 1] = L, R
     else:
         host = np.empty((FRAMES_PER_STREAM, batch, h, w), np.uint8)
-        scenes = [synth.frames(w, h, 7000 + 97 * rank + s, FRAMES_PER_STREAM) for s in range(nsc)]
-        for b in range(batch):
-            host[:, b] = scenes[b % nsc]
-        if mode == "rgbd":
-            dm = [synth.depth_map(w, h, 7000 + s) for s in range(min(nsc, 8))]
-            depth = np.stack([dm[b % len(dm)] for b in range(batch)])
+    for b, s in enumerate(streams):
+        sc = stream_scene(s)
+        if sc not in cache:
+            cache[sc] = scene_frames(mode, w, h, sc)
+        if mode == "stereo":
+            host[:, 2 * b], host[:, 2 * b + 1] = cache[sc][:, 0], cache[sc][:, 1]
+        else:
+            host[:, b] = cache[sc]
+    if mode == "rgbd":
+        dm = {}
+        for s in streams:
+            dm.setdefault(stream_scene(s) % 8, None)
+        dm = {k: synth.depth_map(w, h, 7000 + k) for k in dm}
+        depth = np.stack([dm[stream_scene(s) % 8] for s in streams])
     return host, depth
 
 
-def run_config(torch, dist, rank, world, dev, w, h, nfeatures, batch, steps, warmup, profile, mode="mono"):
-    """Times `steps` front-end steps of `batch` streams (mono / RGB-D frames or
-    stereo pairs) per GPU; returns (max-over-ranks seconds, stage ms, sanity)."""
-    from orb_slam_2_ros_amd import ORBextractor
-    ex = ORBextractor(nfeatures, 1.2, 8, 20, 7, device=dev.index)
+class StubExtractor:
+    """Stands in for ORBextractor under `bench.py --stub` (CPU, gloo): records
+    what each step hands the library -- batch size and a checksum of every
+    frame of the batch -- so the launcher, the stream partition and the batch
+    shapes are testable without a GPU (tests/test_bench_dist.py)."""
+
+    def __init__(self, w, h):
+        self.w, self.h = w, h
+        self.batches = []
+        self.checksums = None
+        self._t = 0
+
+    def _record(self, ptr, fstride, batch):
+        import ctypes
+        buf = np.ctypeslib.as_array((ctypes.c_uint8 * (fstride * batch)).from_address(ptr))
+        sums = [int(buf[i * fstride:(i + 1) * fstride].astype(np.uint64).sum()) for i in range(batch)]
+        if self.checksums is None:
+            self.checksums = sums
+        self.batches.append(batch)
+
+    def reserve(self, w, h, b):
+        pass
+
+    def split(self, parts=0):
+        return 1
+
+    def pipeline(self, on=-1):
+        return 0
+
+    def mono_step_device(self, ptr, fstride, pitch, batch, *a):
+        self._record(ptr, fstride, batch)
+
+    def stereo_step_device(self, ptr, fstride, pitch, pairs, *a):
+        self._record(ptr, fstride, 2 * pairs)
+
+    def rgbd_step_device(self, ptr, fstride, pitch, batch, *a):
+        self._record(ptr, fstride, batch)
+
+    def set_profiling(self, on):
+        pass
+
+    def stage_times(self):
+        return [0.0] * 6
+
+    def batch_download(self, b):
+        return np.zeros(1), None
+
+    def mono_matches_download(self, b):
+        return None, 0
+
+    def depth_download(self, b):
+        return None, None, 0
+
+    def pack_bytes(self):
+        return 64
+
+    def close(self):
+        pass
+
+
+def run_config(torch, dist, rank, world, dev, w, h, nfeatures, streams, steps, warmup, profile, mode="mono",
+               stub=None):
+    """Times `steps` front-end steps of this rank's `streams` (global stream
+    ids: mono / RGB-D frames or stereo pairs, one per stream per step); returns
+    (max-over-ranks seconds, stage ms, kps, sanity, frames per launch, extractor)."""
+    batch = len(streams)
+    if stub is not None:
+        ex = stub
+    else:
+        from orb_slam_2_ros_amd import ORBextractor
+        ex = ORBextractor(nfeatures, 1.2, 8, 20, 7, device=dev.index)
     ex.reserve(w, h, 2 * batch if mode == "stereo" else batch)
     if mode == "mono" and batch >= 64 and "ORBX_SPLIT" not in os.environ:
         # two half-batches on forked streams: one half's latency-bound quadtree /
         # matcher launches overlap the other half's VALU-bound ones (DESIGN.md §6)
         ex.split(2)
-    host, depth = _resident_frames(mode, w, h, batch, rank)
+    host, depth = _resident_frames(mode, w, h, streams)
     frames = torch.from_numpy(host).to(dev)
     dmaps = torch.from_numpy(depth).to(dev) if depth is not None else None
     del host, depth
-    stream = torch.cuda.current_stream(dev)
-    sp = stream.cuda_stream
+    on_gpu = dev.type == "cuda"
+    stream = torch.cuda.current_stream(dev) if on_gpu else None
+    sp = stream.cuda_stream if on_gpu else 0
     fstride = h * w
     bf, fx = 47.9, 435.2                       # EuRoC-like rig: mbf, fx (mb = mbf / fx)
     mb = float(np.float32(bf) / np.float32(fx))
@@ -422,10 +623,10 @@ def run_config(torch, dist, rank, world, dev, w, h, nfeatures, batch, steps, war
         else:
             ex.rgbd_step_device(frames[t].data_ptr(), fstride, w, batch, dmaps.data_ptr(), 4 * fstride, 4 * w, bf, sp)
 
-    sync = lambda: torch.cuda.synchronize(dev)   # noqa: E731
+    sync = (lambda: torch.cuda.synchronize(dev)) if on_gpu else (lambda: None)
     el = timed_region(step, steps, max(warmup, 2), sync, dist, world)
     stages = None
-    if profile:
+    if profile and stub is None:
         # per-stage launch durations (HIP events on the launch stream) from a
         # separate untimed pass with the level pipeline off (if it was on), so
         # each stage is one whole-batch launch that overlaps nothing
@@ -449,18 +650,111 @@ def run_config(torch, dist, rank, world, dev, w, h, nfeatures, batch, steps, war
     else:
         _, _, sane = ex.depth_download(0)
     el = max_over_ranks(torch, dist, world, el, dev)
-    ex.close()
-    return el, stages, len(kp), sane, float(batch)   # the profiled launches cover the whole batch
+    return el, stages, len(kp), sane, float(batch), ex   # the profiled launches cover the whole batch
 
 
 EXTRAS = [
     # key, mode, w, h, nfeatures, streams per GPU, unit
     ("fhd_1920x1080", "mono", 1920, 1080, 1000, 128, "frames/s"),
+    ("hd_1280x720", "mono", 1280, 720, 1000, 256, "frames/s"),
     ("stereo_euroc_752x480", "stereo", 752, 480, 1200, 128, "stereo pairs/s"),
     ("stereo_kitti_1241x376", "stereo", 1241, 376, 2000, 96, "stereo pairs/s"),
     ("stereo_fhd_1920x1080", "stereo", 1920, 1080, 1000, 32, "stereo pairs/s"),
     ("rgbd_fhd_1920x1080", "rgbd", 1920, 1080, 1000, 128, "frames/s"),
 ]
+
+# Config C5 (BASELINE.json configs[4]): 64 FHD RGB-D streams over the job's
+# GPUs (stream s -> rank s mod G), plus the cross-stream keyframe exchange.
+C5_STREAMS = 64
+
+
+def keyframe_publish(torch, dist, world, dev, ex, reps=10):
+    """C5's one collective (reference analogue
+    KeyFrameDatabase::add / DetectLoopCandidates, KeyFrameDatabase.cc:41,82):
+    every rank packs its streams' newest keypoints + descriptors on the device
+    (orbx_batch_pack_device) and all-gathers them over RCCL, so every GPU
+    holds every stream's keyframe.  Times pack + all-gather, median of reps."""
+    nb = ex.pack_bytes()
+    sizes = [nb] * world
+    if world > 1:
+        t = torch.tensor([nb], dtype=torch.int64, device=dev)
+        g = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(g, t)
+        sizes = [int(x.item()) for x in g]
+    cap = max(sizes)
+    buf = torch.zeros(cap, dtype=torch.uint8, device=dev)
+    out = torch.empty(world * cap, dtype=torch.uint8, device=dev)
+    on_gpu = dev.type == "cuda"
+    sp = torch.cuda.current_stream(dev).cuda_stream if on_gpu else 0
+
+    def once():
+        if on_gpu:
+            ex.pack_device(buf.data_ptr(), cap, sp)
+        if world > 1 and on_gpu:
+            dist.all_gather_into_tensor(out, buf)
+        elif world > 1:                      # gloo (CPU tests): list form
+            dist.all_gather(list(out.view(world, cap).unbind(0)), buf)
+        else:
+            out.copy_(buf)
+        if on_gpu:
+            torch.cuda.synchronize(dev)
+
+    once()
+    ts = []
+    for _ in range(reps):
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        once()
+        ts.append(time.perf_counter() - t0)
+    ms = 1e3 * float(np.median(ts))
+    if world > 1:
+        m = torch.tensor([ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(m, op=dist.ReduceOp.MAX)
+        ms = float(m.item())
+    # every gathered block carries its rank's per-stream keypoint counts
+    counts = []
+    if on_gpu:
+        for r in range(world):
+            nst = len(stream_partition(C5_STREAMS, world, r))
+            counts += out[r * cap:r * cap + 4 * nst].view(torch.int32).tolist()
+    return {"ranks": world, "bytes_per_rank": int(nb), "bytes_gathered": int(world * cap), "ms": round(ms, 4),
+            "GB_per_s_received": round(world * cap / (ms * 1e-3) / 1e9, 2) if ms > 0 else None,
+            "streams_received": len(counts), "min_keypoints_per_stream": min(counts) if counts else None}
+
+
+def c5_config(torch, dist, rank, world, dev, steps, warmup, profile, stub=None, w=1920, h=1080):
+    """C5 as configured: 64 FHD RGB-D streams in total, s -> rank s mod G, one
+    extract + ComputeStereoFromRGBD per stream per step (strong scaling inside
+    the config: the stream count is fixed); then the keyframe all-gather."""
+    streams = stream_partition(C5_STREAMS, world, rank)
+    el, st, nk, sane, _, ex = run_config(torch, dist, rank, world, dev, w, h, 1000, streams, steps, warmup,
+                                         profile, "rgbd", stub)
+    xchg = keyframe_publish(torch, dist, world, dev, ex)
+    ex.close()
+    return {"value": round(C5_STREAMS * steps / el, 2), "unit": "frames/s", "mode": "rgbd", "streams_total": C5_STREAMS,
+            "streams_per_gpu": len(streams), "workload": f"rgbd {w}x{h}", "scaling": "strong", "stage_ms": st, "kps_last_frame": nk,
+            "depths_last_frame": sane, "keyframe_all_gather": xchg}
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv: list) -> int:
+    """`bench.py --gpus N` outside a launcher: start N ranks (one process per
+    GPU) under torch.distributed.run and return its exit code.  This parent
+    never touches HIP -- it runs before torch is imported -- and the ranks are
+    child processes, not an exec of this one."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", str(Path(__file__).resolve())] + argv
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def main() -> int:
@@ -473,11 +767,16 @@ def main() -> int:
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--nfeatures", type=int, default=1000)
     ap.add_argument("--no-extras", action="store_true",
-                    help="skip the secondary FHD / stereo / RGB-D configurations")
+                    help="skip the secondary FHD / stereo / RGB-D / C5 configurations")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-profile", action="store_true")
-    ap.add_argument("--extra", default=None, help="time only this EXTRAS config (diagnostics; prints its dict)")
+    ap.add_argument("--extra", default=None, help="time only this EXTRAS config or 'c5' (diagnostics; prints its dict)")
+    ap.add_argument("--stub", action="store_true",
+                    help="CPU / gloo dry run of the launcher, stream partition and batch shapes (tests)")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args.gpus, sys.argv[1:])
 
     import torch
     import torch.distributed as dist
@@ -485,42 +784,80 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-    profile = not args.no_profile
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
+    if args.stub:
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
+    else:
+        if world > 1:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+    profile = not args.no_profile and not args.stub
+    stub = (lambda w, h: StubExtractor(w, h)) if args.stub else (lambda w, h: None)
+    # the stub keeps C5's stream count but not its frame size
+    c5_args = (stub(args.width, args.height), args.width, args.height) if args.stub else (None,)
 
     if args.extra:
+        res = None
+        if args.extra == "c5":
+            res = c5_config(torch, dist, rank, world, dev, args.steps, args.warmup, profile, *c5_args)
         for key, mode, ew, eh, enf, eb, unit in EXTRAS:
             if key == args.extra:
-                el2, st2, nk2, sane2, _ = run_config(torch, dist, rank, world, dev, ew, eh, enf, eb, args.steps,
-                                                     args.warmup, profile, mode)
-                if rank == 0:
-                    print(json.dumps({"extra": key, "value": round(world * eb * args.steps / el2, 2), "unit": unit,
-                                      "stage_ms": st2, "kps_last_frame": nk2}), flush=True)
+                streams = stream_partition(eb * world, world, rank)
+                el2, st2, nk2, sane2, _, ex2 = run_config(torch, dist, rank, world, dev, ew, eh, enf, streams,
+                                                          args.steps, args.warmup, profile, mode, stub(ew, eh))
+                ex2.close()
+                res = {"value": round(world * eb * args.steps / el2, 2), "unit": unit, "stage_ms": st2,
+                       "kps_last_frame": nk2}
+        if rank == 0:
+            print(json.dumps({"extra": args.extra, **(res or {"error": "unknown extra"})}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
         return 0
 
     w, h, nf, B = args.width, args.height, args.nfeatures, args.batch
-    el, stages, nkp_last, nm_last, frames_per_launch = run_config(torch, dist, rank, world, dev, w, h, nf, B, args.steps,
-                                               args.warmup, profile)
+    streams = stream_partition(B * world, world, rank)          # weak scaling: B streams per GPU
+    el, stages, nkp_last, nm_last, frames_per_launch, ex = run_config(
+        torch, dist, rank, world, dev, w, h, nf, streams, args.steps, args.warmup, profile, "mono", stub(w, h))
+    ex.close()
     frames_total = world * B * args.steps
     value = frames_total / el
     ms_per_step = 1000.0 * el / args.steps
+    stub_report = None
+    if args.stub:
+        mine = {"rank": rank, "streams": streams, "batches": sorted(set(ex.batches)), "calls": len(ex.batches),
+                "checksums": ex.checksums}
+        allr = [None] * world
+        if world > 1:
+            dist.all_gather_object(allr, mine)
+        else:
+            allr = [mine]
+        stub_report = allr
 
     extras = {}
     if not args.no_extras:
         for key, mode, ew, eh, enf, eb, unit in EXTRAS:
+            if args.stub:
+                continue
             es = max(5, args.steps // 4)
-            el2, st2, nk2, sane2, _ = run_config(torch, dist, rank, world, dev, ew, eh, enf, eb, es, 2, profile, mode)
+            est = stream_partition(eb * world, world, rank)
+            el2, st2, nk2, sane2, _, ex2 = run_config(torch, dist, rank, world, dev, ew, eh, enf, est, es, 2, profile,
+                                                      mode)
+            ex2.close()
             extras[key] = {"value": round(world * eb * es / el2, 2), "unit": unit, "mode": mode,
                            "streams_per_gpu": eb, "nfeatures": enf, "stage_ms": st2,
                            "kps_last_frame": nk2, ("matches" if mode == "mono" else "depths") + "_last_frame": sane2}
-
-    exchange = keyframe_exchange(torch, dist, world, dev) if (world > 1 and not args.no_extras) else None
+        c5 = c5_config(torch, dist, rank, world, dev, max(5, args.steps // 4), 2, profile, *c5_args)
+        extras["c5_rgbd_fhd_64_streams"] = c5
+        if world > 1 and not args.stub:
+            extras["keyframe_bow_all_gather"] = keyframe_exchange(torch, dist, world, dev)
 
     if rank == 0:
-        sizes = level_geometry(w, h, nf)
+        sizes = level_geometry(w, h, nf) if not args.stub else [(w, h)]
         names = ["resize", "blur", "fast", "quadtree", "describe", "match"]
         roof = None
         stage_ms = None
@@ -544,22 +881,26 @@ def main() -> int:
                 ach = valu / (cand[dom] * 1e-3) / 1e9
                 roof["issue"] = {"bound": "valu", "achieved": round(ach, 1), "peak": VALU_PEAK_GINST,
                                  "unit": "G wave-instr/s", "frac": round(ach / VALU_PEAK_GINST, 4),
+                                 "half_rate_peak": VALU_HALF_RATE_GINST,
+                                 "frac_of_half_rate": round(ach / VALU_HALF_RATE_GINST, 4),
                                  "insts_per_launch": valu, "source": tsrc, "peak_source": VALU_PEAK_SOURCE}
             frame_bytes = algorithmic_bytes(sizes, nkp_last, "frame")
             roof["pipeline_GBs"] = round(frame_bytes * value / world / 1e9, 2)
             roof["pipeline_frac"] = round(frame_bytes * value / world / 1e9 / HBM_PEAK_GBS, 5)
-        cpu = cpu_baseline(w, h, nf, args.cpu_seconds) if (world == 1 and args.cpu_seconds > 0) else None
+        run_cpu = world == 1 and args.cpu_seconds > 0 and not args.stub
+        cpu = cpu_baseline(w, h, nf, args.cpu_seconds) if run_cpu else None
         if cpu is not None:
             # the host's share of cores (OMP_NUM_THREADS on the GPU box), all at once
             nthr = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1), 64))
             cpu["all_cores"] = cpu_baseline_threads(w, h, nf, max(2.0, args.cpu_seconds / 2), nthr)
-        matchers = matcher_latencies() if (world == 1 and not args.no_extras) else None
-        if world == 1 and not args.no_extras:
+            # the timing build stays selected: every CPU time in extras uses it too
+        full = world == 1 and not args.no_extras and not args.stub
+        matchers = matcher_latencies() if full else None
+        if full:
+            extras["dropin_latency"] = dropin_latency(torch, dev)
             extras["bow_transform_orbvoc"] = bow_transform_throughput(torch)
             extras["keyframe_db_loop_query"] = kfdb_latency()
             extras["local_ba_kitti"] = local_ba_latency()
-        if exchange is not None:
-            extras["keyframe_all_gather"] = exchange
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -576,6 +917,7 @@ def main() -> int:
             "config": {"workload": f"mono {w}x{h}, {nf} kp, 8 lvl, scale 1.2, FAST 20/7: ORBextractor + "
                                    "SearchForInitialization(prev frame, window 100, nnratio 0.9, checkOri)",
                        "streams_per_gpu": B, "global_batch": B * world, "parallelism": f"replicas x{world}",
+                       "stream_partition": "global stream s -> rank s mod G",
                        "kps_last_frame": nkp_last, "matches_last_frame": nm_last},
             "roofline": roof,
             "stage_ms_per_step": stage_ms,
@@ -583,6 +925,8 @@ def main() -> int:
             "extras": extras,
             "matchers_per_call": matchers,
         }
+        if stub_report is not None:
+            line["stub"] = stub_report
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

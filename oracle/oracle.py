@@ -56,13 +56,48 @@ def lib() -> ctypes.CDLL:
     if _lib is None:
         if not LIB_PATH.exists():
             build()
-        l = ctypes.CDLL(str(LIB_PATH))
-        for name, (res, args) in _SIG.items():
-            f = getattr(l, name)
-            f.restype = res
-            f.argtypes = args
-        _lib = l
+        _lib = _bind(LIB_PATH)
     return _lib
+
+
+def _bind(path: Path) -> ctypes.CDLL:
+    l = ctypes.CDLL(str(path))
+    for name, (res, args) in _SIG.items():
+        f = getattr(l, name)
+        f.restype = res
+        f.argtypes = args
+    return l
+
+
+def use_timing_build(timeout_s: float = 240.0) -> str:
+    """Switch this process to the oracle's timing build (bench.py's
+    cpu_baseline leg; SURVEY.md §8(d): -O3 -march=native).  The native build is
+    compiled on the host that runs the bench (`make native`, so -march=native
+    means that host); if that fails, the portable -O3 -march=x86-64-v3 build
+    shipped in-tree is used.  Both keep -ffp-contract=off and no fast-math, so
+    results are identical to the checker build.  Returns a description;
+    use_checker_build() switches back."""
+    global _lib
+    desc = None
+    try:
+        r = subprocess.run(["make", "-s", "-C", str(HERE), "native"], timeout=timeout_s, capture_output=True)
+        if r.returncode == 0 and (HERE / "_timing" / "liborbx_oracle_native.so").exists():
+            _lib = _bind(HERE / "_timing" / "liborbx_oracle_native.so")
+            desc = "g++ -O3 -march=native -ffp-contract=off (built on this host)"
+    except (OSError, subprocess.TimeoutExpired):
+        pass
+    if desc is None:
+        p = HERE / "liborbx_oracle_v3.so"
+        if not p.exists():
+            subprocess.run(["make", "-s", "-C", str(HERE), "liborbx_oracle_v3.so"], check=True)
+        _lib = _bind(p)
+        desc = "g++ -O3 -march=x86-64-v3 -ffp-contract=off (prebuilt; native build unavailable)"
+    return desc
+
+
+def use_checker_build() -> None:
+    global _lib
+    _lib = None
 
 
 def _p(a):

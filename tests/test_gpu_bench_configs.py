@@ -1,0 +1,188 @@
+"""The timed kernels are the tested kernels: bench.py's own configurations,
+at the batch sizes it times, checked against the oracle on
+sampled streams -- first, last, both sides of the split boundary and one
+stream in each XCD's frame range -- plus two size-independent properties:
+every stream's output equals that of the stream showing the same scene (the
+bench's 32 unique scenes), and sharding a stream set over ranks changes no
+stream's output (SURVEY.md §8(e) scaling check, 1x16 vs 2x8).
+
+Reference: ORBextractor.cc:1083-1149, ORBmatcher.cc:406-521,
+Frame.cc:502-676 (stereo), Frame.cc:679-701 (RGB-D)."""
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from orb_slam_2_ros_amd import ORBextractor
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+import bench  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+BF, FX = 47.9, 435.2                               # bench.py's rig
+MB = float(np.float32(BF) / np.float32(FX))
+
+
+def _samples(n):
+    """First, last, the split-2 boundary, and the first/last frame of every
+    eighth of the batch (the XCD-contiguous frame ranges of the remap)."""
+    s = {0, 1, n - 1, n // 2 - 1, n // 2}
+    for x in range(8):
+        s.add(x * n // 8)
+        s.add(max(0, (x + 1) * n // 8 - 1))
+    return sorted(i for i in s if 0 <= i < n)
+
+
+def _kp_equal(a, b):
+    return len(a) == len(b) and all(np.array_equal(a[f], b[f]) for f in a.dtype.names)
+
+
+def _frames(torch, mode, w, h, streams):
+    host, depth = bench._resident_frames(mode, w, h, streams)
+    dev = torch.device("cuda:0")
+    fr = torch.from_numpy(host).to(dev)
+    dm = torch.from_numpy(depth).to(dev) if depth is not None else None
+    torch.cuda.synchronize()
+    return host, depth, fr, dm
+
+
+def test_mono_bench_config_b1024_split2(oracle_mod):
+    """The headline timed region: 1024 VGA streams, split 2, two steps (the
+    second matches against the first)."""
+    import torch
+    w, h, B = 640, 480, 1024
+    streams = list(range(B))
+    host, _, fr, _ = _frames(torch, "mono", w, h, streams)
+    ex = ORBextractor(1000, 1.2, 8, 20, 7)
+    ex.reserve(w, h, B)
+    ex.split(2)
+    assert ex.split() == 2
+    for t in range(2):
+        ex.mono_step_device(fr[t].data_ptr(), w * h, w, B, 100, 0.9, True)
+    torch.cuda.synchronize()
+    outs = [ex.batch_download(b) for b in range(B)]
+    matches = [ex.mono_matches_download(b) for b in range(B)]
+    # every stream equals the stream that shows the same scene
+    for b in range(B):
+        r = bench.stream_scene(b)
+        assert _kp_equal(outs[b][0], outs[r][0]) and np.array_equal(outs[b][1], outs[r][1]), f"stream {b}"
+        assert matches[b][1] == matches[r][1] and np.array_equal(matches[b][0], matches[r][0]), f"stream {b}"
+    for b in _samples(B):
+        k1, d1 = oracle_mod.extract(host[0, b])
+        k2, d2 = oracle_mod.extract(host[1, b])
+        assert _kp_equal(outs[b][0], k2) and np.array_equal(outs[b][1], d2), f"stream {b} extract"
+        prev = np.ascontiguousarray(np.stack([k1["x"], k1["y"]], 1).astype(np.float32))
+        nm, m12, _ = oracle_mod.search_for_initialization(k1, d1, k2, d2, w, h, prev, 100, 0.9, True)
+        assert matches[b][1] == nm and np.array_equal(matches[b][0], m12), f"stream {b} matches"
+        assert nm > 0
+    ex.close()
+
+
+STEREO_CONFIGS = [   # bench.py EXTRAS: (w, h, nfeatures, pairs)
+    (752, 480, 1200, 128),
+    (1241, 376, 2000, 96),
+    (1920, 1080, 1000, 32),
+]
+
+
+@pytest.mark.parametrize("w,h,nf,P", STEREO_CONFIGS)
+def test_stereo_bench_configs(w, h, nf, P, oracle_mod):
+    import torch
+    streams = list(range(P))
+    host, _, fr, _ = _frames(torch, "stereo", w, h, streams)
+    ex = ORBextractor(nf, 1.2, 8, 20, 7)
+    ex.reserve(w, h, 2 * P)
+    ex.stereo_step_device(fr[1].data_ptr(), w * h, w, P, BF, MB)
+    torch.cuda.synchronize()
+    deps = [ex.depth_download(p) for p in range(P)]
+    for p in range(P):
+        r = bench.stream_scene(p)
+        assert np.array_equal(deps[p][0], deps[r][0]) and deps[p][2] == deps[r][2]
+    samples = _samples(P) if w < 1920 else [0, 1, P // 2, P - 1]
+    for p in samples:
+        L, R = host[1, 2 * p], host[1, 2 * p + 1]
+        kl, dl = ex.batch_download(2 * p)
+        kr, dr = ex.batch_download(2 * p + 1)
+        ko, do = oracle_mod.extract(L, nf)
+        kro, dro = oracle_mod.extract(R, nf)
+        assert _kp_equal(kl, ko) and np.array_equal(dl, do), f"pair {p} left"
+        assert _kp_equal(kr, kro) and np.array_equal(dr, dro), f"pair {p} right"
+        our, odp, okept = oracle_mod.compute_stereo_matches(oracle_mod.pyramid(L), oracle_mod.pyramid(R), ko, do,
+                                                            kro, dro, BF, MB)
+        ur, dp, kept = deps[p]
+        assert kept == okept and kept > 0, f"pair {p}"
+        assert np.array_equal(ur.view(np.uint32), our.view(np.uint32)), f"pair {p} mvuRight"
+        assert np.array_equal(dp.view(np.uint32), odp.view(np.uint32)), f"pair {p} mvDepth"
+    ex.close()
+
+
+@pytest.mark.parametrize("B", [128, 64])
+def test_rgbd_fhd_bench_configs(B, oracle_mod):
+    """RGB-D FHD at the bench's 128 streams per GPU, and C5's 64 streams as
+    one GPU runs them."""
+    import torch
+    w, h = 1920, 1080
+    streams = list(range(B))
+    host, depth, fr, dm = _frames(torch, "rgbd", w, h, streams)
+    ex = ORBextractor(1000, 1.2, 8, 20, 7)
+    ex.reserve(w, h, B)
+    ex.rgbd_step_device(fr[2].data_ptr(), w * h, w, B, dm.data_ptr(), 4 * w * h, 4 * w, BF)
+    torch.cuda.synchronize()
+    for b in [0, 1, B // 2 - 1, B // 2, B - 1]:
+        kg, dg = ex.batch_download(b)
+        ko, do = oracle_mod.extract(host[2, b])
+        assert _kp_equal(kg, ko) and np.array_equal(dg, do), f"frame {b}"
+        ur, dp, kept = ex.depth_download(b)
+        our, odp = oracle_mod.stereo_from_rgbd(ko, depth[b], BF)
+        assert np.array_equal(ur.view(np.uint32), our.view(np.uint32))
+        assert np.array_equal(dp.view(np.uint32), odp.view(np.uint32))
+        assert kept == int((odp > 0).sum()) and kept > 0
+    ex.close()
+
+
+def _run_streams(torch, mode, w, h, nf, streams, steps):
+    """One extractor (one 'rank') stepping its streams; per-stream outputs."""
+    host, depth, fr, dm = _frames(torch, mode, w, h, streams)
+    n = len(streams)
+    ex = ORBextractor(nf, 1.2, 8, 20, 7)
+    ex.reserve(w, h, 2 * n if mode == "stereo" else n)
+    for t in range(steps):
+        if mode == "mono":
+            ex.mono_step_device(fr[t].data_ptr(), w * h, w, n, 100, 0.9, True)
+        else:
+            ex.stereo_step_device(fr[t].data_ptr(), w * h, w, n, BF, MB)
+    torch.cuda.synchronize()
+    out = {}
+    for b, s in enumerate(streams):
+        if mode == "mono":
+            k, d = ex.batch_download(b)
+            m, nm = ex.mono_matches_download(b)
+            out[s] = (k.tobytes(), d.tobytes(), m.tobytes(), nm)
+        else:
+            k, d = ex.batch_download(2 * b)
+            ur, dp, kept = ex.depth_download(b)
+            out[s] = (k.tobytes(), d.tobytes(), ur.tobytes(), dp.tobytes(), kept)
+    ex.close()
+    return out
+
+
+@pytest.mark.parametrize("mode,w,h,nf,total,world", [("mono", 640, 480, 1000, 16, 2),
+                                                      ("mono", 640, 480, 1000, 16, 4),
+                                                      ("stereo", 752, 480, 1200, 8, 2)])
+def test_sharding_changes_no_stream(mode, w, h, nf, total, world):
+    """per-frame outputs at G ranks are byte-identical to
+    G = 1.  Each rank's share (stream s -> rank s mod G, bench.stream_partition)
+    runs as its own batch, as bench.py's ranks run it; streams are distinct
+    scenes."""
+    import torch
+    assert total <= bench.UNIQUE_SCENES
+    whole = _run_streams(torch, mode, w, h, nf, list(range(total)), 3)
+    for r in range(world):
+        part = bench.stream_partition(total, world, r)
+        got = _run_streams(torch, mode, w, h, nf, part, 3)
+        for s in part:
+            assert got[s] == whole[s], f"stream {s} differs on rank {r} of {world}"
+    assert len({v[0] for v in whole.values()}) == total       # the streams really are distinct

@@ -14,6 +14,8 @@ STEREO = [
     # (w, h, nfeatures, seed, disparity, fx, bf)   C3 EuRoC, C4 KITTI + small/odd
     (752, 480, 1200, 51, 20, 435.2, 47.9),
     (1241, 376, 2000, 52, 20, 718.856, 386.1448),
+    (1920, 1080, 1000, 57, 20, 1050.0, 126.0),      # north_star FHD stereo (largest bands / SAD levels)
+    (1920, 1080, 2000, 58, 41, 1050.0, 126.0),
     (640, 480, 1000, 53, 7, 517.3, 40.0),
     (333, 250, 500, 54, 13, 300.0, 30.0),
 ]
