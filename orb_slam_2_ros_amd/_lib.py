@@ -140,7 +140,9 @@ def load(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     global _LIB
     if _LIB is not None and path is None:
         return _LIB
-    p = Path(path) if path is not None else LIB_PATH
+    # ORBX_LIB: an alternative build of the same ABI (the phase-profiling
+    # diagnostic build, tools/phase_prof.py); never set by tests or the bench
+    p = Path(path) if path is not None else Path(os.environ.get("ORBX_LIB", LIB_PATH))
     if not p.exists():
         raise OSError(f"{p} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
     # torch-ROCm bundles its own libamdhip64.so.7 (same SONAME as /opt/rocm's).

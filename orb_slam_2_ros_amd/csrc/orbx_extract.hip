@@ -45,6 +45,27 @@ struct DiscMask {
 };
 __constant__ DiscMask c_disc_mask = DiscMask();
 
+// Phase profiling (diagnostic build only, -DORBX_PHASE_PROF: tools/phase_prof.py):
+// each wave adds the s_memtime cycles of its phases to g_phase[kernel][phase]
+// (lane 0, vector atomics).  The product build compiles the marks away.
+#ifdef ORBX_PHASE_PROF
+// (256 slots per counter, by workgroup: one shared address per counter would
+// serialise every wave's atomic at one L2 channel)
+__device__ unsigned long long g_phase[2][8][256];
+#define PHASE_START() uint64_t phase_t_ = __builtin_amdgcn_s_memtime()
+#define PHASE_MARK(K, I)                                                                  \
+    do {                                                                                  \
+        const uint64_t phase_n_ = __builtin_amdgcn_s_memtime();                          \
+        if ((threadIdx.x & 63) == 0)                                                      \
+            atomicAdd(&g_phase[K][I][(blockIdx.x + 37 * blockIdx.y) & 255],              \
+                      (unsigned long long)(phase_n_ - phase_t_));                         \
+        phase_t_ = phase_n_;                                                              \
+    } while (0)
+#else
+#define PHASE_START() (void)0
+#define PHASE_MARK(K, I) (void)0
+#endif
+
 namespace {
 
 constexpr int kThreads = 256;
@@ -192,11 +213,30 @@ __device__ inline int wave_stage_rect(uint8_t *dst, int ds, const uint8_t *img, 
 }
 
 
+// A raw buffer resource over a wave-uniform base: loads through it take a
+// 32-bit per-lane offset plus a scalar offset, so no 64-bit address
+// arithmetic runs on the VALU (2 VALU per global_load otherwise).  The range
+// check is left open (the callers never read past their rectangles).
+__device__ inline __amdgpu_buffer_rsrc_t wave_rsrc(const void *base) {
+    const uint64_t a = reinterpret_cast<uint64_t>(base);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), (short)0,
+                                             0x7FFFFFF0, 0x00020000);
+}
+
+__device__ inline uint32_t buf_ld32(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0);
+}
+
 // The same staging with a fixed lane -> (row in pass, dword) map, so each
 // load's address is one uniform row offset plus a fixed per-lane offset (no
 // per-load index walk): rows of at most 64 dwords go 64 / nd rows per pass;
-// wider rows one row per pass in 64-dword chunks, NB rows per round.
-template <int NB = 8>
+// wider rows one row per pass in 64-dword chunks, NB rows per round.  BUF:
+// buffer loads, the row offset a scalar operand and the lane offset a 32-bit
+// VGPR (k_fast, k_describe: -2 % time); the resize windows (up to 24
+// rows in flight) measured 2 % slower that way and keep global loads.
+template <int NB = 8, bool BUF = true>
 __device__ inline int wave_stage_rows(uint8_t *dst, int ds, const uint8_t *img, int pitch, int y0, int x0, int nr,
                                       int nc, int lane) {
     // (all wave-uniform: row offsets then come from the scalar unit)
@@ -205,8 +245,13 @@ __device__ inline int wave_stage_rows(uint8_t *dst, int ds, const uint8_t *img, 
     nr = __builtin_amdgcn_readfirstlane(nr);
     const int xa = x0 & ~3, o = x0 - xa;
     const int nd = (o + nc + 3) >> 2;
+    const uint8_t *gsrc = img + (int64_t)y0 * pitch + xa;
+    const __amdgpu_buffer_rsrc_t src = wave_rsrc(gsrc);
+    auto load = [&](int voff, int row) -> uint32_t {
+        if constexpr (BUF) return buf_ld32(src, voff, __builtin_amdgcn_readfirstlane(row * pitch));
+        else return *reinterpret_cast<const uint32_t *>(gsrc + mul24u(row, pitch) + voff);
+    };
     if (nd > 64) {
-        const uint8_t *src = img + (int64_t)y0 * pitch + xa;
         for (int c0 = 0; c0 < nd; c0 += 64) {
             const bool on = c0 + lane < nd;
             const int voff = 4 * (c0 + lane);
@@ -214,7 +259,7 @@ __device__ inline int wave_stage_rows(uint8_t *dst, int ds, const uint8_t *img, 
                 uint32_t v[NB];
 #pragma unroll
                 for (int j = 0; j < NB; ++j)
-                    if (on && r0 + j < nr) v[j] = *reinterpret_cast<const uint32_t *>(src + mul24u(r0 + j, pitch) + voff);
+                    if (on && r0 + j < nr) v[j] = load(voff, r0 + j);
 #pragma unroll
                 for (int j = 0; j < NB; ++j)
                     if (on && r0 + j < nr) *reinterpret_cast<uint32_t *>(dst + mul24u(r0 + j, ds) + voff) = v[j];
@@ -224,14 +269,13 @@ __device__ inline int wave_stage_rows(uint8_t *dst, int ds, const uint8_t *img, 
     }
     const int R = __builtin_amdgcn_readfirstlane(div_small(64, nd));   // rows per pass (wave-uniform)
     const int rl = div_small(lane, nd), k = lane - mul24u(rl, nd);
-    const uint8_t *src = img + (int64_t)y0 * pitch + xa;
     const int voff = mul24u(rl, pitch) + 4 * k, loff = mul24u(rl, ds) + 4 * k;
     const int rmax = rl < R ? nr - rl : 0;   // this lane loads rows r0 + j R < rmax
     for (int r0 = 0; r0 < nr; r0 += NB * R) {
         uint32_t v[NB];
 #pragma unroll
         for (int j = 0; j < NB; ++j)
-            if (r0 + j * R < rmax) v[j] = *reinterpret_cast<const uint32_t *>(src + mul24u(r0 + j * R, pitch) + voff);
+            if (r0 + j * R < rmax) v[j] = load(voff, r0 + j * R);
 #pragma unroll
         for (int j = 0; j < NB; ++j)
             if (r0 + j * R < rmax) *reinterpret_cast<uint32_t *>(dst + mul24u(r0 + j * R, ds) + loff) = v[j];
@@ -366,7 +410,7 @@ __device__ inline void resize_tile(const DevPlan &p, const FrameBufs &fb, int l,
     const int r_hi = min(max(resize_src_raw(yl, a.sy) + 1, 0), gs.h - 1);
     int spitch;
     const uint8_t *src = level_ptr(p, fb, l - 1, b, spitch);
-    wave_stage_rows<NB>(win, a.win_stride, src, spitch, r_lo, c_lo, r_hi - r_lo + 1, c_hi - c_lo + 1, lane);
+    wave_stage_rows<NB, false>(win, a.win_stride, src, spitch, r_lo, c_lo, r_hi - r_lo + 1, c_hi - c_lo + 1, lane);
     // per-lane column constants: dword of the first source pixel, realignment,
     // and the v_perm selectors of the 4 pixel pairs (S[sx_k], S[sx_k + 1])
     const int rel0 = txk[0].src - (c_lo & ~3);
@@ -529,6 +573,7 @@ __device__ inline int arc_score_bytes(const int p[16], int v) {
 template <bool PIPE>
 __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int c0, int nc, FastLds fl) {
     extern __shared__ __align__(16) uint8_t lds[];
+    PHASE_START();
     const int wave = wave_id(), lane = threadIdx.x & 63;
     int bx, b;
     xcd_block_2d(bx, b);
@@ -550,13 +595,14 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
     const int o = wave_stage_rows(patch, PS, img, spitch, c.y0 - 3, c.x0 - 3, ch + 6, cw + 6, lane);
     const uint8_t *pc = patch + 3 * PS + o + 3;         // interior pixel (0, 0)
     const uint64_t below = (1ull << lane) - 1;
+    PHASE_MARK(0, 0);   // prologue + staging
     uint32_t *out_i = fb.cand + (int64_t)b * p.cand_cap + c.slot;
     uint32_t *out_m = fb.cand2 + (int64_t)b * p.cand_cap + c.slot;
 
     // One FAST pass at threshold th: returns the keypoints kept after NMS,
     // written to out.  The reference runs iniThFAST first and minThFAST only
     // for a cell where that found nothing (ORBextractor.cc:842-850).
-    auto pass = [&](int th, uint32_t *out) -> int {
+    auto pass = [&](int th, uint32_t *out, int ph) -> int {
         {
             uint4 *z0 = reinterpret_cast<uint4 *>(scm);   // (16-B aligned; score_bytes a multiple of 16)
             const int nz = fl.score_bytes >> 4;
@@ -641,6 +687,7 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
             }
         }
         wave_lds_fence();
+        PHASE_MARK(0, ph);       // score-map zeroing + compass pre-test + compaction
         // B. arc score of every survivor: S = max(M1 - v, v - M2), M1 = max over
         //    the 16 nine-pixel arcs of the arc's minimum, M2 = min over arcs of the
         //    arc's maximum, side by side as packed u16 lanes (p, 255 - p) through
@@ -669,6 +716,7 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
             ncorner += __popcll(m);
         }
         wave_lds_fence();
+        PHASE_MARK(0, ph + 1);   // arc scores
         // C. strict 3x3 NMS inside the cell (outside neighbours and non-corners
         //    score 0), compacted in row-major order.
         int base = 0;
@@ -689,15 +737,16 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
             if (keep && pk < c.cap) out[pk] = pack_key(c.x0 + ex, c.y0 + ey, sv);
             base += __popcll(mk);
         }
+        PHASE_MARK(0, ph + 2);   // NMS + output
         return base;
     };
-    const int n_ini = pass(p.ini_th, out_i);
+    const int n_ini = pass(p.ini_th, out_i, 1);
     int32_t cnt;
     if (n_ini > 0) {
         cnt = min(n_ini, c.cap);
     } else {
         wave_lds_fence();
-        const int n_min = pass(p.min_th, out_m);
+        const int n_min = pass(p.min_th, out_m, 4);
         cnt = (int32_t)(0x80000000u | (uint32_t)min(n_min, c.cap));
     }
     if (lane == 0) *count_out = cnt;
@@ -1155,6 +1204,7 @@ constexpr int kDescWaveLds = kDescRowOff + kDescP * kRowS * 2;        // 5680 B
 template <bool PIPE>
 __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs fb, int s0, int ns, int write_total) {
     __shared__ __align__(16) uint8_t lds[4 * ((kDescWaveLds + 15) & ~15)];
+    PHASE_START();
     const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
     // this lane's 4 pattern pairs (bytes x0 y0 x1 y1 of pairs 2j, 2j + 1,
     // j = 64 grp + lane), fetched first so the loads overlap the staging
@@ -1233,6 +1283,7 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
     }
     const uint8_t *patch = lbase + o;
     wave_lds_fence();
+    PHASE_MARK(1, 0);   // prologue + staging
 
     // 2. IC_Angle (ORBextractor.cc:77-104): exact integer moments on the disc.
     //    A task = 4 consecutive disc columns of one row (31 rows x 8 groups,
@@ -1266,6 +1317,7 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
     m10 = wave_sum_i32(m10);
     m01 = wave_sum_i32(m01);
     const float angle = fast_atan2_deg((float)m01, (float)m10);
+    PHASE_MARK(1, 1);   // moments + atan
 
     // 3. Gaussian 7x7 restricted to the 37x37 sample window: row pass over all
     //    43 rows (8-wide segments slide along a row), then the column pass with
@@ -1301,6 +1353,7 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
         *reinterpret_cast<uint4 *>(rowp + r * kRowS + 8 * sgi) = packed;
     }
     wave_lds_fence();
+    PHASE_MARK(1, 2);   // row pass
 
     // 4. computeOrbDescriptor (ORBextractor.cc:106-147) on the blurred level:
     //    each sample's blurred value is the column pass evaluated at that pixel
@@ -1336,6 +1389,7 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
             r01, kK01, __builtin_amdgcn_udot2(r65, kK01, __builtin_amdgcn_udot2(r23, kK23, mul24u(k2, w[4 * kRowS]), false), false),
             false);
     }
+    PHASE_MARK(1, 3);   // sincos + sample offsets + column pass
     int val[8];
     if (all_even) {
 #pragma unroll
@@ -1377,6 +1431,7 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
         kp.class_id = -1;
         fb.kps[kp_index] = kp;
     }
+    PHASE_MARK(1, 4);   // rounding + ballots + records
 }
 
 __global__ void k_trig(const float *in, float *so, float *co, int n, const float *ay, const float *ax,
@@ -1578,6 +1633,23 @@ bool resize_window_fits(const Plan &hp) {
     }
     return true;
 }
+
+#ifdef ORBX_PHASE_PROF
+extern "C" int orbx_debug_phase_cycles(unsigned long long *out, int cap, int reset) {
+    static unsigned long long h[16 * 256];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase), sizeof(h)) != hipSuccess) return -5;
+    for (int i = 0; i < 16 && i < cap; ++i) {
+        unsigned long long t = 0;
+        for (int j = 0; j < 256; ++j) t += h[256 * i + j];
+        out[i] = t;
+    }
+    if (reset) {
+        static unsigned long long z[16 * 256];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)) != hipSuccess) return -5;
+    }
+    return 16;
+}
+#endif
 
 int quadtree_lds_bytes(int node_cap) {
     int np2 = 1;
