@@ -51,7 +51,7 @@ __constant__ DiscMask c_disc_mask = DiscMask();
 #ifdef ORBX_PHASE_PROF
 // (256 slots per counter, by workgroup: one shared address per counter would
 // serialise every wave's atomic at one L2 channel)
-__device__ unsigned long long g_phase[2][8][256];
+__device__ unsigned long long g_phase[3][8][256];
 #define PHASE_START() uint64_t phase_t_ = __builtin_amdgcn_s_memtime()
 #define PHASE_MARK(K, I)                                                                  \
     do {                                                                                  \
@@ -62,7 +62,7 @@ __device__ unsigned long long g_phase[2][8][256];
         phase_t_ = phase_n_;                                                              \
     } while (0)
 #else
-#define PHASE_START() (void)0
+#define PHASE_START() uint64_t phase_t_ = 0; (void)phase_t_
 #define PHASE_MARK(K, I) (void)0
 #endif
 
@@ -806,7 +806,7 @@ struct QLds {
 // The level's keys, each with its node index and quadrant.  R > 0: thread t
 // holds keys t + 256 j (j < R) in registers for the whole distribution (the
 // rounds then touch no global memory); R == 0: they stay in global scratch.
-constexpr int kQRegKeys = 8;
+constexpr int kQRegKeys = kQuadRegKeys / kThreads;
 template <int R>
 struct QKeys {
     uint32_t key[R > 0 ? R : 1];
@@ -844,11 +844,11 @@ struct QKeys {
     }
 };
 
+// Child counts / best keys of the splittable nodes.  ccnt / cbest[0, 4S)
+// were zeroed by the step that produced the current nodes (zero_children),
+// ordered by that step's closing barrier.  Ends with a barrier.
 template <int R>
-__device__ void child_stats(const QLds &s, int S, QKeys<R> &K) {
-    const int tid = threadIdx.x;
-    for (int i = tid; i < 4 * S; i += kThreads) { s.ccnt[i] = 0; s.cbest[i] = 0; }
-    __syncthreads();
+__device__ void child_stats(const QLds &s, QKeys<R> &K) {
     K.each([&](int j, int k) {
         const int nd = K.node(j, k);
         const QNode node = s.cur[nd];
@@ -863,6 +863,10 @@ __device__ void child_stats(const QLds &s, int S, QKeys<R> &K) {
     __syncthreads();
 }
 
+__device__ inline void zero_children(const QLds &s, int S) {
+    for (int i = threadIdx.x; i < 4 * S; i += kThreads) { s.ccnt[i] = 0; s.cbest[i] = 0; }
+}
+
 __device__ inline QNode make_child(const QLds &s, const QNode &parent, int i, int q, int seq) {
     QNode c = child_of(parent, q);
     c.count = (int32_t)s.ccnt[4 * i + q];
@@ -871,45 +875,43 @@ __device__ inline QNode make_child(const QLds &s, const QNode &parent, int i, in
     return c;
 }
 
-__device__ void bitonic_desc(uint64_t *a, int np2) {
-    for (int size = 2; size <= np2; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int i = threadIdx.x; i < (np2 >> 1); i += kThreads) {
-                const int lo = 2 * stride * (i / stride) + (i % stride);
-                const int hi = lo + stride;
-                const bool up = (lo & size) == 0;
-                const uint64_t x = a[lo], y = a[hi];
-                if (up ? (x < y) : (x > y)) { a[lo] = y; a[hi] = x; }
-            }
-            __syncthreads();
-        }
-    }
-}
-
 // Phases 2-5 of k_quadtree on the gathered keys (ORBextractor.cc:566-784).
 template <int NR>
 __device__ void quadtree_rounds(const DevPlan &p, const FrameBufs &fb, QLds &s, const LevelGeom &g, int b, int l,
-                                QKeys<NR> &K) {
+                                QKeys<NR> &K, uint64_t &phase_t_) {
     const int tid = threadIdx.x;
     const int N = g.quota, NC = p.node_cap;
     const uint32_t *keys = K.gkeys;
     int32_t *level_count = fb.level_count + (int64_t)b * kMaxLevels + l;
     __shared__ uint64_t ws64[4];
-    __shared__ int sh_S, sh_R;
+    __shared__ int sh_S, sh_R, sh_nv;
 
     // ---- 2. root nodes (ORBextractor.cc:566-613)
     const int nini = g.nini;
     for (int i = tid; i < nini; i += kThreads) { s.ccnt[i] = 0; s.cbest[i] = 0; }
     __syncthreads();
-    K.each([&](int j, int k) {
-        const uint32_t key = K.get_key(j, k);
-        const float rx = (float)((int)(key & 0xFFF) - kBorder);
-        int r = (int)__fdiv_rn(rx, g.hx);
-        r = min(r, nini - 1);
-        K.set_node(j, k, r);
-        atomicAdd(&s.ccnt[r], 1u);
-        atomicMax(&s.cbest[r], best_pack(key, k));
-    });
+    if (nini == 1) {
+        // one root (every 4:3 or squarer level): its count is the key count and
+        // its best key a block maximum, no per-key atomics on one address
+        uint32_t bm = 0;
+        K.each([&](int j, int k) {
+            K.set_node(j, k, 0);
+            bm = max(bm, best_pack(K.get_key(j, k), k));
+        });
+        bm = wave_max_u32(bm);
+        if ((tid & 63) == 0) atomicMax(&s.cbest[0], bm);
+        if (tid == 0) s.ccnt[0] = (uint32_t)K.n;
+    } else {
+        K.each([&](int j, int k) {
+            const uint32_t key = K.get_key(j, k);
+            const float rx = (float)((int)(key & 0xFFF) - kBorder);
+            int r = (int)__fdiv_rn(rx, g.hx);
+            r = min(r, nini - 1);
+            K.set_node(j, k, r);
+            atomicAdd(&s.ccnt[r], 1u);
+            atomicMax(&s.cbest[r], best_pack(key, k));
+        });
+    }
     __syncthreads();
     if (tid == 0) {
         int S = 0;
@@ -931,27 +933,41 @@ __device__ void quadtree_rounds(const DevPlan &p, const FrameBufs &fb, QLds &s, 
     }
     __syncthreads();
     K.each([&](int j, int k) { K.set_node(j, k, s.nidx_s[K.node(j, k)]); });
+    zero_children(s, sh_S);   // (the roots' counts were read before the barrier above)
     __syncthreads();
+    PHASE_MARK(2, 1);   // roots
 
     if (p.dbg_stop == 2) return;
     // ---- 3. full rounds (ORBextractor.cc:618-696)
     bool final_phase = false;
     while (true) {
         const int S = sh_S;
-        child_stats(s, S, K);
-        for (int i = tid; i < S; i += kThreads) {
-            uint64_t v = 0;
+        child_stats(s, K);
+        PHASE_MARK(2, 2);   // full rounds: child counts
+        // per node: (non-empty children | single-key parents << 21 | children
+        // with more than one key << 42), scanned over a contiguous node range
+        // per thread, so each thread reads back only its own entries
+        const int per = (S + kThreads - 1) / kThreads;
+        const int i0 = min(tid * per, S), i1 = min(i0 + per, S);
+        uint64_t local = 0;
+        for (int i = i0; i < i1; ++i) {
+            uint64_t v = 1ull << 21;
             if (s.cur[i].count > 1) {
                 uint64_t nc = 0, ex = 0;
                 for (int q = 0; q < 4; ++q) { nc += s.ccnt[4 * i + q] > 0; ex += s.ccnt[4 * i + q] > 1; }
                 v = nc | (ex << 42);
-            } else {
-                v = 1ull << 21;
             }
             s.a64[i] = v;
+            local += v;
         }
+        const uint64_t incl = wave_incl_scan_u64(local);
+        if ((tid & 63) == 63) ws64[tid >> 6] = incl;
         __syncthreads();
-        const uint64_t tot = block_excl_scan_u64(s.a64, S, ws64);
+        uint64_t run = incl - local, tot = 0;
+        for (int w = 0; w < kThreads / 64; ++w) {
+            if (w < (tid >> 6)) run += ws64[w];
+            tot += ws64[w];
+        }
         const int C = (int)(tot & 0x1FFFFF), singles = (int)((tot >> 21) & 0x1FFFFF);
         const int nexp = (int)(tot >> 42);
         const int S2 = C + singles;
@@ -959,8 +975,9 @@ __device__ void quadtree_rounds(const DevPlan &p, const FrameBufs &fb, QLds &s, 
             if (tid == 0) *level_count = -1;
             return;
         }
-        for (int i = tid; i < S; i += kThreads) {
-            const uint64_t pre = s.a64[i];
+        for (int i = i0; i < i1; ++i) {
+            const uint64_t pre = run;
+            run += s.a64[i];
             const QNode nd = s.cur[i];
             if (nd.count > 1) {
                 int pos = (int)(pre & 0x1FFFFF);
@@ -982,11 +999,13 @@ __device__ void quadtree_rounds(const DevPlan &p, const FrameBufs &fb, QLds &s, 
             const int nd = K.node(j, k);
             K.set_node(j, k, s.cur[nd].count > 1 ? s.nidx_c[4 * nd + K.quad(j, k)] : s.nidx_s[nd]);
         });
+        zero_children(s, S2);
         {
             QNode *t = s.cur; s.cur = s.nxt; s.nxt = t;
         }
         if (tid == 0) sh_S = S2;
         __syncthreads();
+        PHASE_MARK(2, 3);   // full rounds: scan + children
         if (S2 >= N || S2 == S) break;
         if (S2 + nexp * 3 > N) { final_phase = true; break; }
     }
@@ -995,16 +1014,43 @@ __device__ void quadtree_rounds(const DevPlan &p, const FrameBufs &fb, QLds &s, 
     // ---- 4. final phase (ORBextractor.cc:697-762)
     while (final_phase) {
         const int S = sh_S;
-        child_stats(s, S, K);
-        for (int i = tid; i < s.np2; i += kThreads) {
-            uint64_t v = 0;
-            if (i < S && s.cur[i].count > 1)
-                v = ((uint64_t)s.cur[i].count << 40) | ((uint64_t)s.cur[i].seq << 16) | (uint64_t)i;
-            s.a64[i] = v;
+        if (tid == 0) sh_nv = 0;   // (ordered by child_stats' barrier)
+        child_stats(s, K);
+        {
+            int nz = 0;
+            for (int i = tid; i < s.np2; i += kThreads) {
+                uint64_t v = 0;
+                if (i < S && s.cur[i].count > 1)
+                    v = ((uint64_t)s.cur[i].count << 40) | ((uint64_t)s.cur[i].seq << 16) | (uint64_t)i;
+                s.a64[i] = v;
+                s.b64[i] = 0;
+                nz += v != 0;
+            }
+            nz = wave_sum_i32(nz);
+            if ((tid & 63) == 0 && nz) atomicAdd(&sh_nv, nz);
         }
         for (int i = tid; i < S; i += kThreads) s.mark[i] = 0;
         __syncthreads();
-        bitonic_desc(s.a64, s.np2);
+        PHASE_MARK(2, 4);   // final: child counts
+        // descending order of the splittable nodes' (count, seq, index) keys
+        // (all distinct) by rank counting: one barrier instead of a bitonic
+        // network's log^2 stages; zeros (unsplittable) stay behind, in b64
+        {
+            const int S2r = (S + 1) & ~1;   // a64[S] is 0 when S is odd (np2 is an even power of two)
+            for (int i = tid; i < S; i += kThreads) {
+                const uint64_t v = s.a64[i];
+                if (v == 0) continue;
+                int r = 0;
+                for (int j = 0; j < S2r; j += 2) {
+                    const ulonglong2 w = *reinterpret_cast<const ulonglong2 *>(s.a64 + j);
+                    r += (w.x > v) + (w.y > v);
+                }
+                s.b64[r] = v;
+            }
+            __syncthreads();
+            uint64_t *t = s.a64; s.a64 = s.b64; s.b64 = t;
+        }
+        PHASE_MARK(2, 5);   // final: sort
         // per rank: number of non-empty children (nc) and gain (nc - 1)
         for (int r = tid; r < s.np2; r += kThreads) {
             uint64_t v = 0;
@@ -1018,8 +1064,7 @@ __device__ void quadtree_rounds(const DevPlan &p, const FrameBufs &fb, QLds &s, 
         }
         if (tid == 0) sh_R = -1;
         __syncthreads();
-        int nv = 0;
-        for (int r = 0; r < s.np2; ++r) nv += s.a64[r] != 0;   // uniform, small
+        const int nv = sh_nv;
         block_excl_scan_u64(s.b64, s.np2, ws64);
         for (int r = tid; r < nv; r += kThreads) {
             const int i = (int)(s.a64[r] & 0xFFFF);
@@ -1075,11 +1120,13 @@ __device__ void quadtree_rounds(const DevPlan &p, const FrameBufs &fb, QLds &s, 
             const int nd = K.node(j, k);
             K.set_node(j, k, s.mark[nd] ? s.nidx_c[4 * nd + K.quad(j, k)] : s.nidx_s[nd]);
         });
+        zero_children(s, S2);
         {
             QNode *t = s.cur; s.cur = s.nxt; s.nxt = t;
         }
         if (tid == 0) sh_S = S2;
         __syncthreads();
+        PHASE_MARK(2, 6);   // final: splits
         if (S2 >= N || S2 == S) break;
     }
 
@@ -1100,11 +1147,13 @@ __device__ void quadtree_rounds(const DevPlan &p, const FrameBufs &fb, QLds &s, 
         }
     }
     if (tid == 0) *level_count = S <= g.out_cap ? S : -1;
+    PHASE_MARK(2, 7);   // output
 }
 
 template <bool PIPE>
 __global__ __launch_bounds__(kThreads, 6) void k_quadtree(DevPlan p, FrameBufs fb, int l0) {
     extern __shared__ __align__(16) uint8_t lds[];
+    PHASE_START();
     const int l = l0 + blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
     const LevelGeom g = p.lv[l];
     const int NC = p.node_cap;
@@ -1169,17 +1218,30 @@ __global__ __launch_bounds__(kThreads, 6) void k_quadtree(DevPlan p, FrameBufs f
     };
     // up to kQRegKeys keys per thread stay in registers through the rounds
     if (n <= kQRegKeys * kThreads) {
+        // key k -> its cell by a scatter of the cell ranges (u16 per key)
+        // instead of a bisection per key
+        uint16_t *kcell = reinterpret_cast<uint16_t *>(cell_src + ncell);
+        for (int c = tid; c < ncell; c += kThreads)
+            for (int k = cell_off[c]; k < cell_off[c + 1]; ++k) kcell[k] = (uint16_t)c;
+        __syncthreads();
         QKeys<kQRegKeys> K;
         K.gkeys = nullptr; K.gnode = knode; K.gq = kq; K.n = n;
-        K.each([&](int j, int k) { K.key[j] = fetch(k); K.nq[j] = 0; });
+        K.each([&](int j, int k) {
+            const int c = kcell[k];
+            const int src = cell_src[c];
+            K.key[j] = ((src < 0) ? cand2 : cand)[(src & 0x7FFFFFFF) + (k - cell_off[c])];
+            K.nq[j] = 0;
+        });
         __syncthreads();   // the cell tables are dead from here
-        quadtree_rounds(p, fb, s, g, b, l, K);
+        PHASE_MARK(2, 0);   // gather
+        quadtree_rounds(p, fb, s, g, b, l, K, phase_t_);
     } else {
         QKeys<0> K;
         K.gkeys = keys; K.gnode = knode; K.gq = kq; K.n = n;
         for (int k = tid; k < n; k += kThreads) keys[k] = fetch(k);
         __syncthreads();
-        quadtree_rounds(p, fb, s, g, b, l, K);
+        PHASE_MARK(2, 0);
+        quadtree_rounds(p, fb, s, g, b, l, K, phase_t_);
     }
 }
 
@@ -1636,18 +1698,18 @@ bool resize_window_fits(const Plan &hp) {
 
 #ifdef ORBX_PHASE_PROF
 extern "C" int orbx_debug_phase_cycles(unsigned long long *out, int cap, int reset) {
-    static unsigned long long h[16 * 256];
+    static unsigned long long h[24 * 256];
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase), sizeof(h)) != hipSuccess) return -5;
-    for (int i = 0; i < 16 && i < cap; ++i) {
+    for (int i = 0; i < 24 && i < cap; ++i) {
         unsigned long long t = 0;
         for (int j = 0; j < 256; ++j) t += h[256 * i + j];
         out[i] = t;
     }
     if (reset) {
-        static unsigned long long z[16 * 256];
+        static unsigned long long z[24 * 256];
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)) != hipSuccess) return -5;
     }
-    return 16;
+    return 24;
 }
 #endif
 

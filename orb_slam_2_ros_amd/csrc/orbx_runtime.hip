@@ -112,6 +112,11 @@ struct orbx_extractor {
     int split = 1;   // orbx_extractor_split / ORBX_SPLIT=2 turn it on
     hipStream_t part_stream[kMaxParts] = {};
     hipEvent_t fork_ev = nullptr, done_ev[kMaxParts] = {};
+    // Stagger (ORBX_STAGGER=s, s in 1..3): part 1 starts after part 0's first
+    // s stages (resize, FAST, quadtree), so the parts' latency-bound kernels
+    // meet the other part's VALU-bound ones instead of each other.
+    int stagger = 0;
+    hipEvent_t stag_ev = nullptr;
 
     // Stage profiling: a ring of event sets, one set per step, folded into
     // per-stage sums lazily so the timed loop never waits on the host.
@@ -132,6 +137,7 @@ struct orbx_extractor {
         for (auto &ps : part_stream)
             if (ps) (void)hipStreamDestroy(ps);
         if (fork_ev) (void)hipEventDestroy(fork_ev);
+        if (stag_ev) (void)hipEventDestroy(stag_ev);
         for (auto &e : done_ev)
             if (e) (void)hipEventDestroy(e);
         for (auto &set : ev)
@@ -230,9 +236,10 @@ int upload_plan(orbx_extractor *ex) {
     if (mw > 255 || mh > 255) return ORBX_EINVAL;   // survivor list packs (y << 8 | x)
     if (4 * fast_lds(mw, mh).per_wave > 64 * 1024) return ORBX_EINVAL;   // k_fast's LDS for the largest cell
     d.node_lds_bytes = quadtree_lds_bytes(node_cap);
-    // phase 1 of k_quadtree keeps two ints per cell of a level in the same LDS
+    // phase 1 of k_quadtree keeps two ints per cell of a level and a u16 cell
+    // index per register-held key (kQuadRegKeys per thread) in the same LDS
     for (const LevelGeom &g : p.lv)
-        d.node_lds_bytes = std::max(d.node_lds_bytes, (int)(8 * (g.cell_end - g.cell_begin) + 16));
+        d.node_lds_bytes = std::max(d.node_lds_bytes, (int)(8 * (g.cell_end - g.cell_begin) + 16 + 2 * kQuadRegKeys));
     d.dbg_stop = std::getenv("ORBX_DBG_STOP") ? std::atoi(std::getenv("ORBX_DBG_STOP")) : 0;
     if (d.node_lds_bytes > 160 * 1024) return ORBX_EINVAL;
     return ORBX_OK;
@@ -501,6 +508,27 @@ int run_extract(orbx_extractor *ex, int si, const uint8_t *d_images, int64_t str
         }
         return ORBX_OK;
     }
+    auto stage = [&](int k, int st) -> bool {
+        switch (st) {
+            case 0: return launch_resize(ex->dp, ex->plan, pf[k], P.nb[k], P.s[k]) == hipSuccess;
+            case 1: return launch_fast(ex->dp, ex->plan, pf[k], P.nb[k], P.s[k]) == hipSuccess;
+            case 2: return launch_quadtree(ex->dp, pf[k], P.nb[k], P.s[k]) == hipSuccess;
+            default: return launch_describe(ex->dp, pf[k], P.nb[k], P.s[k]) == hipSuccess;
+        }
+    };
+    if (P.n == 2 && ex->stagger > 0 &&
+        (ex->stag_ev || hipEventCreateWithFlags(&ex->stag_ev, hipEventDisableTiming) == hipSuccess)) {
+        const int sg = std::min(ex->stagger, 3);
+        for (int st = 0; st < 4; ++st) {
+            if (!stage(0, st)) return ORBX_EIO;
+            if (st == sg - 1 && (hipEventRecord(ex->stag_ev, P.s[0]) != hipSuccess ||
+                                 hipStreamWaitEvent(P.s[1], ex->stag_ev, 0) != hipSuccess))
+                return ORBX_EIO;
+        }
+        for (int st = 0; st < 4; ++st)
+            if (!stage(1, st)) return ORBX_EIO;
+        return ORBX_OK;   // (no stage marks: stage times come from unsplit runs)
+    }
     mark(ex, 0, m);
     for (int k = 0; k < P.n; ++k)
         if (launch_resize(ex->dp, ex->plan, pf[k], P.nb[k], P.s[k]) != hipSuccess) return ORBX_EIO;
@@ -598,6 +626,7 @@ orbx_extractor *orbx_extractor_create(int device, int nfeatures, float scaleFact
     if (hipStreamCreateWithFlags(&ex->stream, hipStreamNonBlocking) != hipSuccess) { delete ex; return nullptr; }
     if (const char *sp = std::getenv("ORBX_SPLIT")) ex->split = std::max(1, std::min(std::atoi(sp), orbx_extractor::kMaxParts));
     if (const char *pp = std::getenv("ORBX_PIPELINE")) ex->pipeline = std::atoi(pp) != 0;
+    if (const char *sg = std::getenv("ORBX_STAGGER")) ex->stagger = std::max(0, std::min(std::atoi(sg), 3));
     // geometry tables for the getters are size independent; plan a nominal size
     ex->plan = make_plan(640, 480, nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST);
     return ex;

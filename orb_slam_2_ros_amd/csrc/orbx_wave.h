@@ -60,4 +60,15 @@ __device__ inline uint32_t wave_min_u32(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
+// Maximum over the wave, returned in every lane.
+__device__ inline uint32_t wave_max_u32(uint32_t v) {
+    v = max(v, dpp_or<kRowShr1>(0u, v));
+    v = max(v, dpp_or<kRowShr2>(0u, v));
+    v = max(v, dpp_or<kRowShr4>(0u, v));
+    v = max(v, dpp_or<kRowShr8>(0u, v));
+    v = max(v, dpp_or<kRowBcast15, 0xA>(0u, v));
+    v = max(v, dpp_or<kRowBcast31, 0xC>(0u, v));
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 }  // namespace orbx

@@ -1,4 +1,4 @@
-"""Per-phase cycle breakdown of k_fast and k_describe (diagnostic build with
+"""Per-phase cycle breakdown of k_fast, k_describe and k_quadtree (diagnostic build with
 s_memtime marks, -DORBX_PHASE_PROF):
     make -C orb_slam_2_ros_amd/csrc prof
     ORBX_LIB=orb_slam_2_ros_amd/liborbx_prof.so python tools/phase_prof.py [W H B]
@@ -24,7 +24,7 @@ lib = _lib.load()
 fn = lib.orbx_debug_phase_cycles
 fn.restype = ctypes.c_int
 fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
-buf = np.zeros(16, np.uint64)
+buf = np.zeros(24, np.uint64)
 host, _ = bench._resident_frames("mono", w, h, list(range(B)))
 fr = torch.from_numpy(host).cuda()
 ex = ORBextractor(1000, 1.2, 8, 20, 7)
@@ -33,17 +33,19 @@ ex.split(1)
 for t in range(3):
     ex.mono_step_device(fr[t % 4].data_ptr(), w * h, w, B, 100, 0.9, True)
 torch.cuda.synchronize()
-fn(buf.ctypes.data, 16, 1)
+fn(buf.ctypes.data, 24, 1)
 reps = 5
 for t in range(reps):
     ex.mono_step_device(fr[t % 4].data_ptr(), w * h, w, B, 100, 0.9, True)
 torch.cuda.synchronize()
-fn(buf.ctypes.data, 16, 1)
+fn(buf.ctypes.data, 24, 1)
 names = {0: ["prologue+stage", "ini: zero+compass+compact", "ini: arc scores", "ini: NMS+out",
              "min: zero+compass+compact", "min: arc scores", "min: NMS+out", "-"],
          1: ["prologue+stage", "moments+atan", "row pass", "sincos+offsets+column pass", "round+ballot+write",
-             "-", "-", "-"]}
-for k, kname in ((0, "k_fast"), (1, "k_describe")):
+             "-", "-", "-"],
+         2: ["gather", "roots", "full: child counts", "full: scan+children", "final: child counts",
+             "final: sort", "final: splits", "output"]}
+for k, kname in ((0, "k_fast"), (1, "k_describe"), (2, "k_quadtree")):
     v = buf[8 * k:8 * k + 8].astype(np.float64) / reps
     tot = v.sum()
     print(f"{kname} ({w}x{h}, B={B}): {tot / 1e9:.3f} G wave-cycles per launch")
