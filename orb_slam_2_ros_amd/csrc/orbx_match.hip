@@ -5,10 +5,10 @@
 // GetFeaturesInArea (Frame.cc:239-256, 415-425, 354-412).
 //
 // One 256-thread workgroup per frame pair.  The work that carries no
-// dependency -- grid build, window enumeration, filters, all Hamming distances
-// -- runs on every wave; the reference's greedy loop (its vMatchedDistance /
-// vnMatches21 state makes query i1 depend on every earlier one) is replayed in
-// order by a single wave.  Each query's 4 smallest (distance, position)
+// dependency -- grid build, window enumeration (a lane per query), filters,
+// all Hamming distances -- runs on every wave; the reference's greedy loop
+// (its vMatchedDistance / vnMatches21 state makes query i1 depend on every
+// earlier one) is replayed in order by a single wave.  Each query's 4 smallest (distance, position)
 // entries are found in the parallel phase; the replay only checks their
 // vMatchedDistance validity, falling back to a 64-wide ballot/min scan of the
 // whole list when fewer than two of the four are still valid.  Tie semantics
@@ -30,52 +30,47 @@ constexpr int kGridCells = kGridCols * kGridRows;
 constexpr int kHisto = 30;                      // ORBmatcher::HISTO_LENGTH
 constexpr int kThLow = 50;                      // ORBmatcher::TH_LOW
 constexpr int kSkip = 0xFFFF;
-constexpr int kMT = 1024;                       // threads per frame pair
+constexpr int kMT = 256;                        // threads per frame pair
 constexpr int kMW = kMT / 64;                   // waves
 
-// LDS layout of one frame pair (16-B aligned arrays first).
+// LDS layout of one frame pair, indexed by grid position (F2 octave-0
+// keypoints, < maxc) or query rank (F1 octave-0 keypoints, < maxq) only, so a
+// pair needs ~40 KB at VGA and four pairs share a CU (16-B aligned arrays first).
 struct MLds {
     uint4 *gd;       // maxc x 2: F2 octave-0 descriptors in grid order
     uint4 *qd;       // maxq x 2: F1 octave-0 (query) descriptors in query order
     float2 *gxy;     // maxc: F2 positions in grid order
     float2 *qxy;     // maxq: query centres (vbPrevMatched)
-    int *gstart;     // kGridCells + 1
-    int *gfill;      // kGridCells
-    int *mdist;      // n2cap: vMatchedDistance
-    int *m21;        // n2cap: vnMatches21
-    int *m12;        // n1cap: vnMatches12
-    int *qrank;      // n1cap: rank among octave-0 queries, or -1
-    int *qcount;     // maxq: candidate-list length
-    uint32_t *claim; // n2cap: (replay batch << 16 | (255 - lane) << 8 | dist) of a batch's first acceptor of i2
-    int16_t *live;   // maxq: queries that can be accepted, in order
-    uint32_t *top4;  // maxq x 4: (i2 << 16 | dist) of the 4 smallest (dist, position)
-    int16_t *kcell;  // n2cap: grid cell of each F2 keypoint (-1: none)
+    uint32_t *top4;  // maxq x 4: (grid position << 16 | dist) of the 4 smallest (dist, list position)
+    int *gstart;     // kGridCells + 1: first grid position of each cell
+    int *mdist;      // maxc: vMatchedDistance by grid position
+    int *m21;        // maxc: vnMatches21 (query rank) by grid position
+    uint32_t *claim; // maxc: (replay batch << 16 | (255 - lane) << 8 | dist) of a batch's first acceptor
+    int *m12;        // maxq: vnMatches12 (grid position) by query rank
     int16_t *glist;  // maxc: F2 index by grid position
     int16_t *qidx;   // maxq: F1 index of each query
-    int16_t *acc;    // n1cap: F2 index accepted for query i1 (-1: none)
-    int8_t *rbin;    // n1cap: rotation bin of accepted queries (-1: none)
+    int16_t *live;   // maxq: queries that can be accepted, in order
+    int16_t *acc;    // maxq: grid position accepted by each query (-1: none)
+    int8_t *rbin;    // maxq: rotation bin of accepted queries (-1: none)
 };
 
-__device__ inline MLds carve(uint8_t *ptr, int n1cap, int n2cap, int maxq, int maxc) {
+__device__ inline MLds carve(uint8_t *ptr, int maxq, int maxc) {
     MLds s;
     s.gd = reinterpret_cast<uint4 *>(ptr); ptr += sizeof(uint4) * 2 * maxc;
     s.qd = reinterpret_cast<uint4 *>(ptr); ptr += sizeof(uint4) * 2 * maxq;
     s.gxy = reinterpret_cast<float2 *>(ptr); ptr += sizeof(float2) * maxc;
     s.qxy = reinterpret_cast<float2 *>(ptr); ptr += sizeof(float2) * maxq;
-    s.gstart = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * (kGridCells + 1);
-    s.gfill = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * kGridCells;
-    s.mdist = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * n2cap;
-    s.m21 = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * n2cap;
-    s.m12 = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * n1cap;
-    s.qrank = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * n1cap;
-    s.qcount = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * maxq;
+    ptr += 8 * ((maxc + maxq) & 1);   // top4 rows are read as uint4
     s.top4 = reinterpret_cast<uint32_t *>(ptr); ptr += sizeof(uint32_t) * 4 * maxq;
-    s.claim = reinterpret_cast<uint32_t *>(ptr); ptr += sizeof(uint32_t) * n2cap;
-    s.kcell = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * n2cap;
+    s.gstart = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * (kGridCells + 1);
+    s.mdist = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * maxc;
+    s.m21 = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * maxc;
+    s.claim = reinterpret_cast<uint32_t *>(ptr); ptr += sizeof(uint32_t) * maxc;
+    s.m12 = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * maxq;
     s.glist = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * ((maxc + 1) & ~1);
     s.qidx = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * ((maxq + 1) & ~1);
     s.live = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * ((maxq + 1) & ~1);
-    s.acc = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * ((n1cap + 1) & ~1);
+    s.acc = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * ((maxq + 1) & ~1);
     s.rbin = reinterpret_cast<int8_t *>(ptr);
     return s;
 }
@@ -101,82 +96,96 @@ __device__ inline int block_scan_i32(int v, int *total, int *ws) {
     return base + incl - v;
 }
 
-__global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, int n2cap, int maxq, int maxc) {
+// PosInGrid (Frame.cc:415-425) for an undistorted image: round(), cell
+// ix * 48 + iy, or -1 outside the grid.
+__device__ inline int grid_cell(float x, float y, float invW, float invH) {
+    const int px = (int)roundf(__fmul_rn(x, invW));
+    const int py = (int)roundf(__fmul_rn(y, invH));
+    return (px >= 0 && px < kGridCols && py >= 0 && py < kGridRows) ? px * kGridRows + py : -1;
+}
+
+__global__ __launch_bounds__(kMT) void k_search_init(MatchBufs mb, int maxq, int maxc) {
     extern __shared__ __align__(16) uint8_t lds[];
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const orbx_keypoint *k1 = mb.k1 + (int64_t)b * mb.k1_stride;
     const orbx_keypoint *k2 = mb.k2 + (int64_t)b * mb.k2_stride;
     const uint8_t *d1 = mb.d1 + (int64_t)b * mb.k1_stride * 32;
     const uint8_t *d2 = mb.d2 + (int64_t)b * mb.k2_stride * 32;
-    const int n1 = min(mb.n1[b], n1cap), n2 = min(mb.n2[b], n2cap);
+    const int n1 = mb.n1[b], n2 = mb.n2[b];
     float *prev = mb.prev_xy + (int64_t)b * mb.k1_stride * 2;
     int32_t *out12 = mb.matches12 + (int64_t)b * mb.k1_stride;
-    const MLds s = carve(lds, n1cap, n2cap, maxq, maxc);
+    const MLds s = carve(lds, maxq, maxc);
     __shared__ int hist[kHisto];
     __shared__ int ws[kMW];
     __shared__ int sh_top[3];
     __shared__ int sh_err, sh_nq;
 
     // Frame grid constants for an undistorted img_w x img_h image
-    // (Frame.cc:218-220, ComputeImageBounds with k1 == 0).
-    const float minX = 0.f, maxX = (float)mb.img_w, minY = 0.f, maxY = (float)mb.img_h;
-    const float invW = __fdiv_rn((float)kGridCols, __fsub_rn(maxX, minX));
-    const float invH = __fdiv_rn((float)kGridRows, __fsub_rn(maxY, minY));
+    // (Frame.cc:218-220, ComputeImageBounds with k1 == 0: minX = minY = 0).
+    const float invW = __fdiv_rn((float)kGridCols, (float)mb.img_w);
+    const float invH = __fdiv_rn((float)kGridRows, (float)mb.img_h);
     const float r = (float)mb.window;
     const bool clk = mb.clocks && b == 0 && tid == 0;
     if (clk) { mb.clocks[0] = clock64(); mb.clocks[6] = 0; mb.clocks[7] = 0; }
 
-    // ---- 0. init
+    // ---- 0. init; every output defaults to "no match"
     for (int i = tid; i <= kGridCells; i += kMT) s.gstart[i] = 0;
-    for (int i = tid; i < kGridCells; i += kMT) s.gfill[i] = 0;
-    for (int i = tid; i < n2; i += kMT) { s.mdist[i] = INT_MAX; s.m21[i] = -1; s.claim[i] = 0; }
-    for (int i = tid; i < n1; i += kMT) { s.m12[i] = -1; s.rbin[i] = -1; s.acc[i] = -1; }
+    for (int i = tid; i < maxc; i += kMT) { s.mdist[i] = INT_MAX; s.m21[i] = -1; s.claim[i] = 0; }
+    for (int i = tid; i < maxq; i += kMT) { s.m12[i] = -1; s.rbin[i] = -1; s.acc[i] = -1; }
+    for (int i = tid; i < n1; i += kMT) {
+        out12[i] = -1;
+        if (mb.reset_prev) { prev[2 * i] = k1[i].x; prev[2 * i + 1] = k1[i].y; }
+    }
     if (tid < kHisto) hist[tid] = 0;
     if (tid == 0) sh_err = 0;
-    if (mb.reset_prev) {
-        for (int i = tid; i < n1; i += kMT) { prev[2 * i] = k1[i].x; prev[2 * i + 1] = k1[i].y; }
-    }
     __syncthreads();
     if (clk) mb.clocks[1] = clock64();
 
-    // ---- 1. F2 grid of octave-0 keypoints (PosInGrid uses round(), Frame.cc:417-418)
+    // ---- 1. F2 grid of octave-0 keypoints: counts, exclusive scan, then
+    //         placement by a second atomic pass on the starts (which leaves
+    //         gstart[c] at the end of cell c, i.e. the start of c + 1)
     for (int i = tid; i < n2; i += kMT) {
-        int cell = -1;
-        if (k2[i].octave == 0) {
-            const int px = (int)roundf(__fmul_rn(__fsub_rn(k2[i].x, minX), invW));
-            const int py = (int)roundf(__fmul_rn(__fsub_rn(k2[i].y, minY), invH));
-            if (px >= 0 && px < kGridCols && py >= 0 && py < kGridRows) {
-                cell = px * kGridRows + py;
-                atomicAdd(&s.gstart[cell], 1);
-            }
-        }
-        s.kcell[i] = (int16_t)cell;
+        if (k2[i].octave != 0) continue;
+        const int cell = grid_cell(k2[i].x, k2[i].y, invW, invH);
+        if (cell >= 0) atomicAdd(&s.gstart[cell], 1);
     }
     __syncthreads();
+    constexpr int kPer = kGridCells / kMT;   // 12 cells per thread, contiguous
     {
-        const int per = kGridCells / kMT;   // 3 cells per thread, contiguous
         int local = 0;
-        for (int i = 0; i < per; ++i) local += s.gstart[tid * per + i];
+        for (int i = 0; i < kPer; ++i) local += s.gstart[tid * kPer + i];
         int tot;
         int run = block_scan_i32(local, &tot, ws);
-        for (int i = 0; i < per; ++i) {
-            const int v = s.gstart[tid * per + i];
-            s.gstart[tid * per + i] = run;
+        for (int i = 0; i < kPer; ++i) {
+            const int v = s.gstart[tid * kPer + i];
+            s.gstart[tid * kPer + i] = run;
             run += v;
         }
         if (tid == kMT - 1) s.gstart[kGridCells] = run;
         if (tid == 0 && tot > maxc) sh_err = 1;
         __syncthreads();
     }
-    const int ngrid = min(s.gstart[kGridCells], maxc);
     for (int i = tid; i < n2; i += kMT) {
-        const int cell = s.kcell[i];
+        if (k2[i].octave != 0) continue;
+        const int cell = grid_cell(k2[i].x, k2[i].y, invW, invH);
         if (cell >= 0) {
-            const int pos = s.gstart[cell] + atomicAdd(&s.gfill[cell], 1);
+            const int pos = atomicAdd(&s.gstart[cell], 1);
             if (pos < maxc) s.glist[pos] = (int16_t)i;
         }
     }
     __syncthreads();
+    {   // shift back: start(c) = end(c - 1)
+        int v[kPer];
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            const int c = tid * kPer + i;
+            v[i] = c == 0 ? 0 : s.gstart[c - 1];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) s.gstart[tid * kPer + i] = v[i];
+        __syncthreads();
+    }
     // each cell's list in keypoint-index order (mGrid push_back order)
     for (int c = tid; c < kGridCells; c += kMT) {
         const int st = s.gstart[c], en = min(s.gstart[c + 1], maxc);
@@ -188,6 +197,7 @@ __global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, i
         }
     }
     __syncthreads();
+    const int ngrid = min(s.gstart[kGridCells], maxc);
     for (int pos = tid; pos < ngrid; pos += kMT) {
         const int i2 = s.glist[pos];
         s.gxy[pos] = make_float2(k2[i2].x, k2[i2].y);
@@ -204,16 +214,15 @@ __global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, i
         int tot;
         int run = block_scan_i32(local, &tot, ws);
         for (int i = st; i < en; ++i) {
-            const bool isq = k1[i].octave == 0;
-            s.qrank[i] = isq && run < maxq ? run : -1;
-            if (isq && run < maxq) {
+            if (k1[i].octave != 0) continue;
+            if (run < maxq) {
                 s.qidx[run] = (int16_t)i;
                 s.qxy[run] = make_float2(prev[2 * i], prev[2 * i + 1]);
                 const uint4 *dp = reinterpret_cast<const uint4 *>(d1 + (int64_t)i * 32);
                 s.qd[2 * run] = dp[0];
                 s.qd[2 * run + 1] = dp[1];
             }
-            run += isq;
+            ++run;
         }
         if (tid == 0) { sh_nq = min(tot, maxq); if (tot > maxq) sh_err = 1; }
     }
@@ -221,84 +230,67 @@ __global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, i
     const int nq = sh_nq;
     if (clk) mb.clocks[2] = clock64();
 
-    // ---- 2. candidate distances, all from LDS.  GetFeaturesInArea visits
-    //         ix outer, iy inner, then cell insertion order; glist is sorted by
-    //         cell = ix * 48 + iy and index, so the window's list is one
-    //         contiguous glist range per grid column ix.  Lane = column; a
-    //         candidate's list position is its column's base + its rank.
-    //         Only each query's 4 smallest (dist, position) entries are kept;
-    //         the rare replay that needs more walks the window again.
-    auto window = [&](int q, int &st, int &cnt, int &pos0) {
-        const float2 c = s.qxy[q];
-        const float x = c.x, y = c.y;
-        const int cx0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(x, minX), r), invW)));
-        const int cx1 = min(kGridCols - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(x, minX), r), invW)));
-        const int cy0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(y, minY), r), invH)));
-        const int cy1 = min(kGridRows - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(y, minY), r), invH)));
-        const bool empty = cx0 >= kGridCols || cx1 < 0 || cy0 >= kGridRows || cy1 < 0 || cx1 < cx0 || cy1 < cy0;
-        const int ncx = cx1 - cx0 + 1;   // <= 64 grid columns
-        st = 0; cnt = 0;
-        if (!empty && lane < ncx) {
-            const int col = (cx0 + lane) * kGridRows;
-            st = s.gstart[col + cy0];
-            cnt = max(min(s.gstart[col + cy1 + 1], maxc) - st, 0);
-        }
-        const int incl = wave_incl_scan_i32(cnt);
-        pos0 = incl - cnt;
-        return __builtin_amdgcn_readlane(incl, 63);   // list length
+    // GetFeaturesInArea's cell window (Frame.cc:354-412) of a query centre
+    auto cells_of = [&](float x, float y, int &cx0, int &cx1, int &cy0, int &cy1) {
+        cx0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(x, r), invW)));
+        cx1 = min(kGridCols - 1, (int)ceilf(__fmul_rn(__fadd_rn(x, r), invW)));
+        cy0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(y, r), invH)));
+        cy1 = min(kGridRows - 1, (int)ceilf(__fmul_rn(__fadd_rn(y, r), invH)));
+        return !(cx0 >= kGridCols || cx1 < 0 || cy0 >= kGridRows || cy1 < 0 || cx1 < cx0 || cy1 < cy0);
     };
-    // distance of list entry (column lane, rank e) to query q; kSkip outside the window
+    // distance of grid entry gp to query q's descriptor; kSkip outside the window
     auto entry_dist = [&](int gp, float x, float y, const uint4 &qa, const uint4 &qb) {
         const float2 kp = s.gxy[gp];
         const float dx = __fsub_rn(kp.x, x), dy = __fsub_rn(kp.y, y);
         return (fabsf(dx) < r && fabsf(dy) < r) ? hamming_regs(qa, qb, s.gd[2 * gp], s.gd[2 * gp + 1]) : kSkip;
     };
-    for (int q = wave; q < nq; q += kMW) {
-        int st, cnt, pos0;
-        int written = window(q, st, cnt, pos0);
-        if (written > maxc) { if (lane == 0) sh_err = 1; written = maxc; }
-        // this lane's 4 smallest (dist << 16 | list position) and their i2
+
+    // ---- 2. candidate distances, one lane per query.  GetFeaturesInArea
+    //         visits ix outer, iy inner, then cell insertion order; the grid
+    //         is sorted by cell = ix * 48 + iy and index, so the window's list
+    //         is one contiguous grid range per column ix and a candidate's list
+    //         position is a running count over the columns.  Each query keeps
+    //         its 4 smallest (dist, position) entries; the rare replay that
+    //         needs more walks the window again.
+    for (int q = tid; q < nq; q += kMT) {
         uint32_t tk[4] = {~0u, ~0u, ~0u, ~0u};
-        int ti[4] = {0, 0, 0, 0};
-        if (cnt > 0) {
-            const float2 c = s.qxy[q];
+        int tg[4] = {0, 0, 0, 0};
+        int cx0, cx1, cy0, cy1;
+        const float2 c = s.qxy[q];
+        if (cells_of(c.x, c.y, cx0, cx1, cy0, cy1)) {
             const uint4 qa = s.qd[2 * q], qb = s.qd[2 * q + 1];
-            for (int e = 0; e < cnt; ++e) {
-                const int gp = st + e;
-                const int dist = entry_dist(gp, c.x, c.y, qa, qb);
-                if (dist != kSkip && pos0 + e < maxc) {
-                    uint32_t k = ((uint32_t)dist << 16) | (uint32_t)(pos0 + e);
-                    int ki = s.glist[gp];
+            int pos = 0;
+            for (int ix = cx0; ix <= cx1; ++ix) {
+                const int col = ix * kGridRows;
+                const int st = s.gstart[col + cy0], en = min(s.gstart[col + cy1 + 1], maxc);
+                for (int gp = st; gp < en; ++gp, ++pos) {
+                    const int dist = entry_dist(gp, c.x, c.y, qa, qb);
+                    if (dist == kSkip || pos >= maxc) continue;
+                    uint32_t k = ((uint32_t)dist << 16) | (uint32_t)pos;
+                    int kg = gp;
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         if (k < tk[j]) {
                             const uint32_t t = tk[j]; tk[j] = k; k = t;
-                            const int u = ti[j]; ti[j] = ki; ki = u;
+                            const int u = tg[j]; tg[j] = kg; kg = u;
                         }
                     }
                 }
             }
+            if (pos > maxc) sh_err = 1;
         }
-        // wave-wide 4 smallest: pop the minimum head four times
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t mn = wave_min_u32(tk[0]);
-            const bool mine = tk[0] == mn && mn != ~0u;
-            const uint64_t who = __ballot(mine);
-            int i2 = 0;
-            if (who) i2 = __builtin_amdgcn_readlane(ti[0], (int)__builtin_ctzll(who));
-            if (mine) { tk[0] = tk[1]; tk[1] = tk[2]; tk[2] = tk[3]; tk[3] = ~0u; ti[0] = ti[1]; ti[1] = ti[2]; ti[2] = ti[3]; }
-            if (lane == 0) s.top4[4 * q + j] = mn == ~0u ? 0xFFFFFFFFu : ((uint32_t)i2 << 16) | (mn >> 16);
-        }
-        if (lane == 0) s.qcount[q] = written;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            s.top4[4 * q + j] = tk[j] == ~0u ? 0xFFFFFFFFu : ((uint32_t)tg[j] << 16) | (tk[j] >> 16);
     }
     __syncthreads();
     if (clk) mb.clocks[3] = clock64();
 
     // ---- 3. ordered greedy replay (ORBmatcher.cc:425-491), wave 0 only.
-    // The valid entries (vMatchedDistance[i2] > dist) among a query's 4
-    // smallest (dist, position) entries, in order, are the smallest valid ones
-    // of its whole list: two found decide (best, best2); a list that fits in 4
-    // is decided too; otherwise the whole list is walked again.  Queries whose
+    // The valid entries (vMatchedDistance > dist) among a query's 4 smallest
+    // (dist, position) entries, in order, are the smallest valid ones of its
+    // whole list: two found decide (best, best2); a list that fits in 4 is
+    // decided too; otherwise the whole list is walked again.  Queries whose
     // smallest distance exceeds TH_LOW can never be accepted and change no
     // state, so only the others ("live") are replayed, 64 consecutive ones per
     // batch, one per lane, each against the state left by the committed ones.
@@ -309,13 +301,13 @@ __global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, i
     // next batch starts there.  Lane 0 of a batch always commits.
     if (wave == 0) {
         // the replay is the block's serial critical path: let it issue ahead
-        // of the co-resident block's waves
+        // of the co-resident blocks' waves
         __builtin_amdgcn_s_setprio(3);
         int nlive = 0;
         for (int g0 = 0; g0 < nq; g0 += 64) {
             const int q = g0 + lane;
             const uint32_t r0 = q < nq ? s.top4[4 * q] : 0xFFFFFFFFu;
-            const bool live = q < nq && s.qcount[q] > 0 && r0 != 0xFFFFFFFFu && (int)(r0 & 0xFFFF) <= kThLow;
+            const bool live = r0 != 0xFFFFFFFFu && (int)(r0 & 0xFFFF) <= kThLow;
             const uint64_t m = __ballot(live);
             if (live) s.live[nlive + __popcll(m & ((1ull << lane) - 1))] = (int16_t)q;
             nlive += __popcll(m);
@@ -330,19 +322,22 @@ __global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, i
             const bool act = idx < nlive;
             const int q = act ? s.live[idx] : 0;
             uint32_t e4[4];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) e4[t] = act ? s.top4[4 * q + t] : 0xFFFFFFFFu;
+            {
+                const uint4 t4 = act ? *reinterpret_cast<const uint4 *>(s.top4 + 4 * q)
+                                     : make_uint4(~0u, ~0u, ~0u, ~0u);
+                e4[0] = t4.x; e4[1] = t4.y; e4[2] = t4.z; e4[3] = t4.w;
+            }
             int md[4];
 #pragma unroll
             for (int t = 0; t < 4; ++t) md[t] = s.mdist[e4[t] == 0xFFFFFFFFu ? 0 : (e4[t] >> 16)];
-            int best = INT_MAX, best2 = INT_MAX, best_i2 = -1, found = 0, ne = 0;
+            int best = INT_MAX, best2 = INT_MAX, best_g = -1, found = 0, ne = 0;
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
                 if (e4[t] == 0xFFFFFFFFu || found == 2) continue;
                 ne = t + 1;
-                const int i2 = (int)(e4[t] >> 16), dist = (int)(e4[t] & 0xFFFF);
+                const int g = (int)(e4[t] >> 16), dist = (int)(e4[t] & 0xFFFF);
                 if (md[t] <= dist) continue;
-                if (found == 0) { best = dist; best_i2 = i2; }
+                if (found == 0) { best = dist; best_g = g; }
                 else best2 = dist;
                 ++found;
             }
@@ -353,7 +348,7 @@ __global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, i
             // claim = batch << 16 | (255 - lane) << 8 | best: the earliest
             // accepting lane of the batch and the vMatchedDistance it leaves
             if (ok && lane < f)
-                atomicMax(&s.claim[best_i2], (batch << 16) | ((uint32_t)(255 - lane) << 8) | (uint32_t)best);
+                atomicMax(&s.claim[best_g], (batch << 16) | ((uint32_t)(255 - lane) << 8) | (uint32_t)best);
             wave_lds_fence();
             // An entry the lane found valid (md > dist) turns invalid iff an
             // earlier lane accepts its keypoint with best <= dist; an invalid
@@ -369,64 +364,66 @@ __global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, i
                     const int dist = (int)(e4[t] & 0xFFFF);
                     const bool earlier = (c >> 16) == batch && 255 - (int)((c >> 8) & 0xFF) < lane;
                     inval |= earlier && ((md[t] > dist && (int)(c & 0xFF) <= dist) ||
-                                         (ok && (int)(e4[t] >> 16) == best_i2));
+                                         (ok && (int)(e4[t] >> 16) == best_g));
                 }
             }
             const uint64_t im = __ballot(inval);
             const int cut = min(min(im ? (int)__builtin_ctzll(im) : 64, f), nlive - P);
             if (ok && lane < cut) {
-                const int i1 = s.qidx[q];
-                const int old = s.m21[best_i2];
+                const int old = s.m21[best_g];
                 if (old >= 0) s.m12[old] = -1;
-                s.m12[i1] = best_i2;
-                s.m21[best_i2] = i1;
-                s.mdist[best_i2] = best;
-                s.acc[i1] = (int16_t)best_i2;   // binned in phase 4 (stolen pairs keep their bin)
+                s.m12[q] = best_g;
+                s.m21[best_g] = q;
+                s.mdist[best_g] = best;
+                s.acc[q] = (int16_t)best_g;   // binned in phase 4 (stolen pairs keep their bin)
             }
             wave_lds_fence();
             if (clk) mb.clocks[6] += 1;
             P += cut;
             if (cut == f && P < nlive) {
-                // lane f's query needs its whole list: walk the window again;
-                // each lane keeps its column's smallest valid (dist, position)
-                // key and its second distance
+                // lane f's query needs its whole list: walk the window again,
+                // lane = grid column; each lane keeps its column's smallest
+                // valid (dist, position) key and its second distance
                 const int qf = s.live[P];
-                int st, cc, pos0;
-                window(qf, st, cc, pos0);
                 const float2 c = s.qxy[qf];
+                int cx0, cx1, cy0, cy1, st = 0, cc = 0;
+                if (cells_of(c.x, c.y, cx0, cx1, cy0, cy1) && lane < cx1 - cx0 + 1) {
+                    const int col = (cx0 + lane) * kGridRows;
+                    st = s.gstart[col + cy0];
+                    cc = max(min(s.gstart[col + cy1 + 1], maxc) - st, 0);
+                }
+                const int pos0 = wave_incl_scan_i32(cc) - cc;
                 const uint4 qa = s.qd[2 * qf], qb = s.qd[2 * qf + 1];
                 uint32_t k1 = ~0u;
-                int d2 = INT_MAX, i2a = 0;
+                int d2 = INT_MAX, ga = 0;
                 for (int e = 0; e < cc; ++e) {
                     const int gp = st + e;
                     if (pos0 + e >= maxc) break;
                     const int dist = entry_dist(gp, c.x, c.y, qa, qb);
-                    const int i2 = s.glist[gp];
-                    if (dist == kSkip || s.mdist[i2] <= dist) continue;
+                    if (dist == kSkip || s.mdist[gp] <= dist) continue;
                     const uint32_t k = ((uint32_t)dist << 16) | (uint32_t)(pos0 + e);
-                    if (k < k1) { d2 = k1 == ~0u ? INT_MAX : (int)(k1 >> 16); k1 = k; i2a = i2; }
+                    if (k < k1) { d2 = k1 == ~0u ? INT_MAX : (int)(k1 >> 16); k1 = k; ga = gp; }
                     else d2 = min(d2, dist);
                 }
                 const uint32_t mn = wave_min_u32(k1);
-                int fbest = INT_MAX, fbest2 = INT_MAX, fi2 = -1;
+                int fbest = INT_MAX, fbest2 = INT_MAX, fg = -1;
                 if (mn != ~0u) {
                     const uint64_t who = __ballot(k1 == mn);
                     const int wl = (int)__builtin_ctzll(who);
                     fbest = (int)(mn >> 16);
-                    fi2 = __builtin_amdgcn_readlane(i2a, wl);
+                    fg = __builtin_amdgcn_readlane(ga, wl);
                     // multiset second: the best lane's second, every other lane's first
                     const uint32_t cand2 = lane == wl ? (uint32_t)d2 : (k1 == ~0u ? ~0u : (k1 >> 16));
                     const uint32_t m2 = wave_min_u32(cand2);
                     fbest2 = m2 >= (uint32_t)INT_MAX ? INT_MAX : (int)m2;
                 }
                 if (fbest <= kThLow && (float)fbest < __fmul_rn((float)fbest2, nnr) && lane == 0) {
-                    const int i1 = s.qidx[qf];
-                    const int old = s.m21[fi2];
+                    const int old = s.m21[fg];
                     if (old >= 0) s.m12[old] = -1;
-                    s.m12[i1] = fi2;
-                    s.m21[fi2] = i1;
-                    s.mdist[fi2] = fbest;
-                    s.acc[i1] = (int16_t)fi2;
+                    s.m12[qf] = fg;
+                    s.m21[fg] = qf;
+                    s.mdist[fg] = fbest;
+                    s.acc[qf] = (int16_t)fg;
                 }
                 wave_lds_fence();
                 ++P;
@@ -441,14 +438,14 @@ __global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, i
     //         ComputeThreeMaxima, consistency filter and outputs (:494-520)
     if (mb.check_ori) {
         const float factor = 1.0f / kHisto;
-        for (int i1 = tid; i1 < n1; i1 += kMT) {
-            const int a = s.acc[i1];
+        for (int q = tid; q < nq; q += kMT) {
+            const int a = s.acc[q];
             if (a < 0) continue;
-            float rot = __fsub_rn(k1[i1].angle, k2[a].angle);
+            float rot = __fsub_rn(k1[s.qidx[q]].angle, k2[s.glist[a]].angle);
             if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
             int bin = (int)roundf(__fmul_rn(rot, factor));
             if (bin == kHisto) bin = 0;
-            s.rbin[i1] = (int8_t)bin;
+            s.rbin[q] = (int8_t)bin;
             atomicAdd(&hist[bin], 1);
         }
     }
@@ -469,18 +466,18 @@ __global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, i
     }
     __syncthreads();
     int local = 0;
-    for (int i1 = tid; i1 < n1; i1 += kMT) {
-        int m = s.m12[i1];
-        if (mb.check_ori && m >= 0) {
-            const int bin = s.rbin[i1];
-            if (bin >= 0 && bin != sh_top[0] && bin != sh_top[1] && bin != sh_top[2]) m = -1;
+    for (int q = tid; q < nq; q += kMT) {
+        const int g = s.m12[q];
+        if (g < 0) continue;
+        if (mb.check_ori) {
+            const int bin = s.rbin[q];
+            if (bin >= 0 && bin != sh_top[0] && bin != sh_top[1] && bin != sh_top[2]) continue;
         }
-        out12[i1] = m;
-        if (m >= 0) {
-            prev[2 * i1] = k2[m].x;
-            prev[2 * i1 + 1] = k2[m].y;
-            ++local;
-        }
+        const int i1 = s.qidx[q], i2 = s.glist[g];
+        out12[i1] = i2;
+        prev[2 * i1] = s.gxy[g].x;
+        prev[2 * i1 + 1] = s.gxy[g].y;
+        ++local;
     }
     int total;
     block_scan_i32(local, &total, ws);
@@ -490,12 +487,12 @@ __global__ __launch_bounds__(1024) void k_search_init(MatchBufs mb, int n1cap, i
 
 }  // namespace
 
-// LDS of one frame pair.
+// LDS of one frame pair (n1cap / n2cap: kept for the callers; the layout
+// is indexed by query rank and grid position only).
 int match_lds_bytes(int n1cap, int n2cap, int maxq, int maxc) {
-    return (int)(32 * (maxc + maxq) + 8 * (maxc + maxq) + sizeof(int) * (2 * kGridCells + 1) +
-                 sizeof(int) * (3 * n2cap + 2 * n1cap) + sizeof(int) * 5 * maxq + sizeof(int16_t) * n2cap +
-                 sizeof(int16_t) * ((maxc + 1) & ~1) + 2 * sizeof(int16_t) * ((maxq + 1) & ~1) +
-                 sizeof(int16_t) * ((n1cap + 1) & ~1) + n1cap + 64);
+    (void)n1cap; (void)n2cap;
+    return (int)(40 * (maxc + maxq) + 8 + 16 * maxq + sizeof(int) * (kGridCells + 1) + 12 * maxc + 4 * maxq +
+                 sizeof(int16_t) * (((maxc + 1) & ~1) + 3 * ((maxq + 1) & ~1)) + maxq + 64);
 }
 
 constexpr int kMatchLdsMax = 160 * 1024 - 1024;   // dynamic LDS; the kernel's static LDS needs < 1 KiB
@@ -507,7 +504,7 @@ hipError_t launch_match(const MatchBufs &mb, int B, int n1cap, int n2cap, int ma
         hipFuncSetAttribute(reinterpret_cast<const void *>(k_search_init),
                             hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_search_init, dim3(B), dim3(kMT), bytes, st, mb, n1cap, n2cap, maxq, maxc);
+    hipLaunchKernelGGL(k_search_init, dim3(B), dim3(kMT), bytes, st, mb, maxq, maxc);
     return hipGetLastError();
 }
 
