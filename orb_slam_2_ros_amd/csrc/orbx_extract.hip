@@ -570,7 +570,10 @@ __device__ inline int arc_score_bytes(const int p[16], int v) {
 
 // PIPE: a level's cells in a level-pipelined step (a distinct instantiation so
 // profiles tell per-level launches from whole-batch ones).
-template <bool PIPE>
+// PSC: the patch / score-map row stride as a compile-time constant (48 or 64:
+// every circle, ring and NMS neighbour offset becomes an LDS immediate), or 0
+// for the launch's runtime stride.
+template <bool PIPE, int PSC>
 __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int c0, int nc, FastLds fl) {
     extern __shared__ __align__(16) uint8_t lds[];
     PHASE_START();
@@ -586,7 +589,7 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
         if (lane == 0) *count_out = 0;
         return;
     }
-    const int PS = fl.ps, SW = fl.sw;
+    const int PS = PSC ? PSC : fl.ps, SW = PSC ? PSC : fl.sw;
     uint8_t *patch = lds + (size_t)wave * fl.per_wave;
     uint8_t *scm = patch + fl.patch_bytes;   // S-1 of the pass's corners, 0 elsewhere
     uint16_t *list = reinterpret_cast<uint16_t *>(scm + fl.score_bytes);   // (yy << 8 | xx), row-major
@@ -1539,10 +1542,11 @@ hipError_t launch_blur(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t
 FastLds fast_lds(int mw, int mh) {
     FastLds f;
     f.ps = (mw + 6 + 3 + 3) & ~3;   // + alignment offset, dword rows
-    f.patch_bytes = (f.ps * (mh + 6) + 15) & ~15;
-    f.score_bytes = ((mw + 2) * (mh + 2) + 15) & ~15;
-    f.per_wave = f.patch_bytes + f.score_bytes + ((2 * mw * mh + 15) & ~15);
     f.sw = mw + 2;
+    if (f.ps <= 64) f.ps = f.sw = f.ps <= 48 ? 48 : 64;   // k_fast's constant-stride instantiations
+    f.patch_bytes = (f.ps * (mh + 6) + 15) & ~15;
+    f.score_bytes = (f.sw * (mh + 2) + 15) & ~15;
+    f.per_wave = f.patch_bytes + f.score_bytes + ((2 * mw * mh + 15) & ~15);
     return f;
 }
 
@@ -1559,7 +1563,13 @@ hipError_t launch_fast_range(const DevPlan &p, const Plan &hp, const FrameBufs &
         mh = std::max(mh, hp.cells[c].y1 - hp.cells[c].y0);
     }
     const FastLds fl = fast_lds(mw, mh);
-    hipLaunchKernelGGL(k_fast<PIPE>, dim3((nc + 3) / 4, B), dim3(kThreads), 4 * fl.per_wave, st, p, fb, c0, nc, fl);
+    const dim3 grid((nc + 3) / 4, B);
+    if (fl.ps == 48 && fl.sw == 48)
+        hipLaunchKernelGGL((k_fast<PIPE, 48>), grid, dim3(kThreads), 4 * fl.per_wave, st, p, fb, c0, nc, fl);
+    else if (fl.ps == 64 && fl.sw == 64)
+        hipLaunchKernelGGL((k_fast<PIPE, 64>), grid, dim3(kThreads), 4 * fl.per_wave, st, p, fb, c0, nc, fl);
+    else
+        hipLaunchKernelGGL((k_fast<PIPE, 0>), grid, dim3(kThreads), 4 * fl.per_wave, st, p, fb, c0, nc, fl);
     return hipGetLastError();
 }
 
