@@ -265,6 +265,72 @@ def matcher_latencies(reps: int = 20):
         out[name] = {"features": na,
                      "gpu_ms": round(timed(lambda: m.search_by_bow(variant, A, B, tri), reps), 4),
                      "cpu_ms": round(timed(lambda: oracle.search_by_bow(variant, A, B, ratio, ori, tri), 5), 4)}
+    out["local_mapping_20_neighbours"] = local_mapping_matchers(reps)
+    return out
+
+
+def local_mapping_matchers(reps: int = 10, nn: int = 20):
+    """The matcher work LocalMapping does per new keyframe over its nn = 20
+    covisible neighbours: SearchForTriangulation against each
+    (CreateNewMapPoints, LocalMapping.cc:276-315, ORBmatcher(0.6, false)) and
+    Fuse of its map points into each (SearchInNeighbors, :537-548), plus
+    relocalisation's SearchByProjection over 10 candidates (Tracking.cc:1667).
+    Batched (one launch pair per loop) vs one drop-in call per neighbour vs
+    the oracle's single thread."""
+    from oracle import oracle
+    from orb_slam_2_ros_amd import ORBmatcher
+    from orb_slam_2_ros_amd.synth_match import (BOW_VARIANT_ARGS, PROJ_VARIANT_ARGS, make_bow_case,
+                                                make_proj_case)
+
+    def timed(fn, k):
+        ts = []
+        for _ in range(k):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return 1e3 * float(np.median(ts))
+
+    out = {}
+    ratio, ori = BOW_VARIANT_ARGS["triangulation"]
+    A, B, tri = make_bow_case(777, "triangulation", na=2000, nb=2000, nodes=200)
+    rng = np.random.default_rng(778)
+    probs = []
+    for _ in range(nn):
+        d = B["desc"].copy()
+        flip = rng.random(d.shape) < 0.03
+        d[flip] ^= (1 << rng.integers(0, 8, flip.sum())).astype(np.uint8)
+        probs.append({"A": A, "B": dict(B, desc=d), "tri": tri})
+    m = ORBmatcher(ratio, ori)
+    m.search_by_bow_batch("triangulation", probs)
+    out["SearchForTriangulation"] = {
+        "features": 2000, "neighbours": nn,
+        "gpu_batched_ms": round(timed(lambda: m.search_by_bow_batch("triangulation", probs), reps), 4),
+        "gpu_per_call_ms": round(timed(lambda: [m.search_by_bow("triangulation", P["A"], P["B"], P["tri"])
+                                                for P in probs], max(3, reps // 3)), 4),
+        "cpu_ms": round(timed(lambda: [oracle.search_by_bow("triangulation", P["A"], P["B"], ratio, ori, P["tri"])
+                                       for P in probs], 3), 4)}
+    for variant, key, count, n, nq in [("fuse", "Fuse", nn, 2000, 1500), ("keyframe", "reloc_SearchByProjection", 10,
+                                                                          2000, 1000)]:
+        th, ratio, ori, wth = PROJ_VARIANT_ARGS[variant]
+        cases = [make_proj_case(900 + k, variant, n=n, nq=nq, stereo=variant == "fuse", th=wth) for k in range(count)]
+        if variant == "keyframe":   # one current frame, each candidate's points
+            cases = [dict(cases[0], queries=c["queries"], qdesc=c["qdesc"]) for c in cases]
+        m = ORBmatcher(ratio, ori)
+        m.search_by_projection_batch(variant, cases, th)
+
+        def per_call(cs=cases, mm=m, v=variant, t=th):
+            for c in cs:
+                mm.search_by_projection(v, c["keys"], c["desc"], c["queries"], c["qdesc"], c["bounds"], c["uright"],
+                                        c["mp_state"], c["inv_sigma2"], t)
+
+        def cpu(cs=cases, v=variant, t=th, r=ratio, o=ori):
+            for c in cs:
+                oracle.search_by_projection(v, c["keys"], c["desc"], c["queries"], c["qdesc"], c["bounds"],
+                                            c["uright"], c["mp_state"], c["inv_sigma2"], t, r, o)
+        out[key] = {"keypoints": n, "points": nq, "problems": count,
+                    "gpu_batched_ms": round(timed(lambda: m.search_by_projection_batch(variant, cases, th), reps), 4),
+                    "gpu_per_call_ms": round(timed(per_call, max(3, reps // 3)), 4),
+                    "cpu_ms": round(timed(cpu, 3), 4)}
     return out
 
 

@@ -271,6 +271,34 @@ int orbx_search_by_projection(int device, int variant, const orbx_match_frame *f
                               int th_dist, float nnratio, int check_ori, int32_t *q_idx,
                               int32_t *q_dist, int32_t *kp_final, int *nmatches);
 
+/* Several independent projection searches of one variant in one pair of
+ * launches and one round trip -- the reference's per-keyframe loops:
+ *   LocalMapping::SearchInNeighbors, Fuse(pKFi, vpMapPointMatches) for every
+ *     neighbour (LocalMapping.cc:537-548; ORBX_PROJ_FUSE);
+ *   Tracking::Relocalization, SearchByProjection(mCurrentFrame,
+ *     vpCandidateKFs[i], sFound, 10, 100) for every candidate that reached it
+ *     (Tracking.cc:1667, 1685; ORBX_PROJ_KEYFRAME).
+ * Each problem is exactly one orbx_search_by_projection call (same inputs,
+ * same outputs, filled in place including nmatches); problems may share a
+ * frame's arrays (uploaded once).  Fuse's candidate search reads no map
+ * state, so a neighbour's results stay exact when the caller applies the map
+ * edits neighbour by neighbour and re-checks pMP->isBad() / IsInKeyFrame()
+ * before each edit, as Fuse itself does at the top of its loop.
+ * Synchronous. */
+typedef struct orbx_proj_problem {
+    orbx_match_frame frame;
+    const orbx_proj_query *queries;
+    const uint8_t *qdesc;
+    int nq;
+    int32_t *q_idx;      /* [nq] */
+    int32_t *q_dist;     /* [nq] */
+    int32_t *kp_final;   /* [frame.n] */
+    int nmatches;        /* out */
+} orbx_proj_problem;
+
+int orbx_search_by_projection_batch(int device, int variant, orbx_proj_problem *problems, int nproblems,
+                                    int th_dist, float nnratio, int check_ori);
+
 /* int SearchBySim3(KeyFrame *pKF1, KeyFrame *pKF2, vector<MapPoint*> &vpMatches12,
  *                  const float &s12, const cv::Mat &R12, const cv::Mat &t12, th)
  *                                                     ORBmatcher.cc:1104-1328
@@ -316,6 +344,41 @@ typedef struct orbx_bow_side {
 int orbx_search_by_bow(int device, int variant, const orbx_bow_side *a, const orbx_bow_side *b,
                        float nnratio, int check_ori, const float *tri, int nlevels,
                        int32_t *match_a, int32_t *match_b, int *nmatches);
+
+/* Several vocabulary-node searches of one variant in one pair of launches
+ * and one round trip: LocalMapping::CreateNewMapPoints' SearchForTriangulation
+ * of the new keyframe against each covisible neighbour (LocalMapping.cc:
+ * 276-315), or any set of SearchByBoW calls.  Each problem is exactly one
+ * orbx_search_by_bow call with the same inputs (tri: its own 11 + 2 nlevels
+ * floats; match arrays and nmatches filled in place).
+ * The reference runs the neighbours in order and each one's triangulations
+ * give keyframe A new map points, which bar those features from the next
+ * neighbour's search (side A flags).  A feature's search never depends on the
+ * other A features (SearchForTriangulation sets no vbMatched2), so a batch
+ * run with the flags at the start stays exact: the caller drops, neighbour by
+ * neighbour, the pairs whose A feature got a map point from an earlier
+ * neighbour -- with check_ori = 0, as LocalMapping's ORBmatcher(0.6, false)
+ * has it; with check_ori = 1 run orbx_rotation_filter over the survivors
+ * (pass check_ori = 0 to the batch and keep its raw pairs).
+ * Synchronous. */
+typedef struct orbx_bow_problem {
+    orbx_bow_side a, b;
+    const float *tri;    /* triangulation only */
+    int32_t *match_a;    /* [a.n] */
+    int32_t *match_b;    /* [b.n] (unused by triangulation) */
+    int nmatches;        /* out */
+} orbx_bow_problem;
+
+int orbx_search_by_bow_batch(int device, int variant, orbx_bow_problem *problems, int nproblems,
+                             float nnratio, int check_ori, int nlevels);
+
+/* The reference's rotation-consistency pass (rotHist + ComputeThreeMaxima +
+ * removal, ORBmatcher.cc:1603-1644 and e.g. :800-818) over pairs
+ * (i, match_a[i] >= 0) of keypoints ka / kb, skipping A features with
+ * exclude[i] != 0 (NULL: none), in place; *nmatches = the pairs kept.  Host
+ * only. */
+int orbx_rotation_filter(const orbx_keypoint *ka, const orbx_keypoint *kb, int32_t *match_a, int na,
+                         const uint8_t *exclude, int *nmatches);
 
 /* ---- DBoW2 vocabulary ----
  * ORBVocabulary = DBoW2::TemplatedVocabulary<FORB::TDescriptor, FORB>

@@ -51,6 +51,19 @@ class MatchFrame(ctypes.Structure):
                 ("min_y", ctypes.c_float), ("max_y", ctypes.c_float)]
 
 
+class ProjProblem(ctypes.Structure):
+    """orbx_proj_problem"""
+    _fields_ = [("frame", MatchFrame), ("queries", ctypes.c_void_p), ("qdesc", ctypes.c_void_p),
+                ("nq", ctypes.c_int), ("q_idx", ctypes.c_void_p), ("q_dist", ctypes.c_void_p),
+                ("kp_final", ctypes.c_void_p), ("nmatches", ctypes.c_int)]
+
+
+class BowProblem(ctypes.Structure):
+    """orbx_bow_problem"""
+    _fields_ = [("a", BowSide), ("b", BowSide), ("tri", ctypes.c_void_p), ("match_a", ctypes.c_void_p),
+                ("match_b", ctypes.c_void_p), ("nmatches", ctypes.c_int)]
+
+
 class OrbxError(RuntimeError):
     def __init__(self, code: int, what: str):
         self.code = code
@@ -96,7 +109,10 @@ _SIGNATURES = {
     "orbx_depth_download": (I32, [P, I32, P, P, I32, P, P]),
     "orbx_stereo_from_rgbd": (I32, [I32, P, P, I32, P, I32, I32, SZ, F32, P, P, P]),
     "orbx_search_by_projection": (I32, [I32, I32, P, P, P, I32, I32, F32, I32, P, P, P, P]),
+    "orbx_search_by_projection_batch": (I32, [I32, I32, P, I32, I32, F32, I32]),
     "orbx_search_by_sim3": (I32, [I32, P, P, P, P, P, P, I32, P, P]),
+    "orbx_search_by_bow_batch": (I32, [I32, I32, P, I32, F32, I32, I32]),
+    "orbx_rotation_filter": (I32, [P, P, P, I32, P, P]),
     "orbx_search_by_bow": (I32, [I32, I32, P, P, F32, I32, P, I32, P, P, P]),
     "orbx_descriptor_distance": (I32, [P, P]),
     "orbx_search_for_initialization": (I32, [I32, P, P, I32, P, P, I32, I32, I32, P, P, I32, F32, I32, P]),

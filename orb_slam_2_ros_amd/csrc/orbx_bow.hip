@@ -17,6 +17,8 @@
 // The rotation-consistency pass runs in a second single-block kernel.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "orbx_device.h"
 #include "orbx_wave.h"
 
@@ -52,8 +54,10 @@ __device__ inline bool epipolar_ok(float x1, float y1, float x2, float y2, const
     return (double)dsqr < __dmul_rn(3.84, (double)sigma2);
 }
 
-__global__ __launch_bounds__(kBT) void k_bow_match(BowBufs a) {
+// Grid (nodes of the largest side A / 4, problems).
+__global__ __launch_bounds__(kBT) void k_bow_match(const BowBufs *pa) {
     __shared__ uint8_t matched[kBT / 64][kBowNodeCap];
+    const BowBufs a = pa[blockIdx.y];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int na_node = blockIdx.x * (kBT / 64) + wave;
     if (na_node >= a.A.nnodes) return;
@@ -176,8 +180,9 @@ __global__ __launch_bounds__(kBT) void k_bow_match(BowBufs a) {
 }
 
 // ComputeThreeMaxima + removal of the matches outside the three main bins.
-__global__ __launch_bounds__(1024) void k_bow_finish(BowBufs a) {
+__global__ __launch_bounds__(1024) void k_bow_finish(const BowBufs *pa) {   // one block per problem
     __shared__ int top[3];
+    const BowBufs a = pa[blockIdx.x];
     __shared__ int removed;
     const int tid = threadIdx.x;
     if (tid == 0) {
@@ -213,10 +218,13 @@ __global__ __launch_bounds__(1024) void k_bow_finish(BowBufs a) {
 
 }  // namespace
 
-hipError_t launch_bow(const BowBufs &a, hipStream_t st) {
-    if (a.A.nnodes > 0)
-        hipLaunchKernelGGL(k_bow_match, dim3((a.A.nnodes + kBT / 64 - 1) / (kBT / 64)), dim3(kBT), 0, st, a);
-    hipLaunchKernelGGL(k_bow_finish, dim3(1), dim3(1024), 0, st, a);
+hipError_t launch_bow(const BowBufs *h, const BowBufs *d, int np, hipStream_t st) {
+    if (np <= 0) return hipSuccess;
+    int nodes = 0;
+    for (int k = 0; k < np; ++k) nodes = std::max(nodes, h[k].A.nnodes);
+    if (nodes > 0)
+        hipLaunchKernelGGL(k_bow_match, dim3((nodes + kBT / 64 - 1) / (kBT / 64), np), dim3(kBT), 0, st, d);
+    hipLaunchKernelGGL(k_bow_finish, dim3(np), dim3(1024), 0, st, d);
     return hipGetLastError();
 }
 

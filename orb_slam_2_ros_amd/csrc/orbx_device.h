@@ -121,6 +121,7 @@ struct ProjBufs {
     uint2 *hard; int hard_cap;               // (keypoint, query) claims past a query's 4 kept entries
     uint8_t *und;                            // nq: 0 decided, 1 open, 2 left to the in-order replay
     int32_t *stats;                          // optional: rounds, queries replayed in order
+    int nblk;                                // search blocks of this problem (proj_blocks(nq))
 };
 
 // Vocabulary-node matchers (SearchByBoW x2, SearchForTriangulation).
@@ -164,9 +165,11 @@ int stereo_lds_bytes(int rows, int nr_cap);
 hipError_t launch_rgbd(const orbx_keypoint *kps, const orbx_keypoint *kun, const int32_t *nkps, int64_t kstride,
                        int kcap, const float *dmap, int64_t dstride, int dpitch, int w, int h, float mbf, float *ur,
                        float *depth, int64_t ostride, int32_t *nkept, int B, hipStream_t s);
-hipError_t launch_proj(const ProjBufs &a, hipStream_t s);
+// A batch of independent problems: h on the host, d the same array on the device.
+hipError_t launch_proj(const ProjBufs *h, const ProjBufs *d, int np, hipStream_t s);
+int proj_blocks(int nq);
 bool proj_fits(int n);   // the frame's grid fits the search kernel's LDS
-hipError_t launch_bow(const BowBufs &a, hipStream_t s);
+hipError_t launch_bow(const BowBufs *h, const BowBufs *d, int np, hipStream_t s);
 
 // DBoW2 vocabulary in slot order: the children of a node occupy consecutive
 // slots (root = slot 0).  16 B per slot + 32-B descriptor + weight.

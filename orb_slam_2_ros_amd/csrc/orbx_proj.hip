@@ -98,8 +98,11 @@ __device__ inline int block_scan(int v, int *total, int *ws) {
     return base + incl - v;
 }
 
-__global__ __launch_bounds__(kPT) void k_proj_search(ProjBufs a) {
+// Grid (max nblk, problems): problem blockIdx.y, its first a.nblk blocks.
+__global__ __launch_bounds__(kPT) void k_proj_search(const ProjBufs *pa) {
     extern __shared__ __align__(16) uint8_t lds[];
+    const ProjBufs a = pa[blockIdx.y];
+    if ((int)blockIdx.x >= a.nblk) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int n = a.n, nq = a.nq;
     const PLds s = carve(lds, n);
@@ -167,14 +170,14 @@ __global__ __launch_bounds__(kPT) void k_proj_search(ProjBufs a) {
     }
     __syncthreads();
 
-    for (int i = blockIdx.x * kPT + tid; i < n; i += gridDim.x * kPT) a.kp_final[i] = -1;
+    for (int i = blockIdx.x * kPT + tid; i < n; i += a.nblk * kPT) a.kp_final[i] = -1;
 
     // ---- 2. window expansion, static filters, distances, 4 smallest per query
     uint8_t *emap = s.entmap + wave * kEnt;
     const bool occ_obs = V == ORBX_PROJ_LOCALMAP || V == ORBX_PROJ_LASTFRAME;
     __shared__ int sh_T[kPW], sh_base;
     // uniform trip count: the waves of a block allocate their lists together
-    for (int q0 = blockIdx.x * kPW; q0 < nq; q0 += gridDim.x * kPW) {
+    for (int q0 = blockIdx.x * kPW; q0 < nq; q0 += a.nblk * kPW) {
         const int q = q0 + wave;
         orbx_proj_query Q{};
         int T = 0, st = 0, cnt = 0, pos0 = 0;
@@ -416,8 +419,9 @@ __device__ inline bool accept(const ProjBufs &a, bool ratio, int q, const uint32
 // rounds stop when none progresses; what is left (contention chains through
 // `hard` claims) is replayed by wave 0 in query order.
 template <bool QL>   // per-query data in LDS (else global; one instantiation each keeps ds_* loads ds_*)
-__global__ __launch_bounds__(kPT) void k_proj_replay(ProjBufs a) {
+__global__ __launch_bounds__(kPT) void k_proj_replay(const ProjBufs *pa) {   // one block per problem
     extern __shared__ __align__(16) uint8_t lds[];
+    const ProjBufs a = pa[blockIdx.x];
     const uint64_t c0 = wall_clock64();
     const int n = a.n, nq = a.nq;
     const int V = a.variant;
@@ -692,27 +696,36 @@ int proj_replay_lds_bytes(int n, int nq, bool q_in_lds) {
 
 bool proj_fits(int n) { return n <= kKPer * kPT && proj_lds_bytes(n) <= kProjLdsMax && proj_replay_lds_bytes(n, 0, false) <= kProjLdsMax; }
 
-hipError_t launch_proj(const ProjBufs &a, hipStream_t st) {
-    const int bytes = proj_lds_bytes(a.n);
+int proj_blocks(int nq) { return std::max(1, std::min(512, (nq + kPW - 1) / kPW)); }
+
+// h: the problems' buffers on the host, d: the same array in device memory.
+hipError_t launch_proj(const ProjBufs *h, const ProjBufs *d, int np, hipStream_t st) {
+    if (np <= 0) return hipSuccess;
+    int bytes = 0, nblk = 1;
+    bool q_in_lds = true;
+    for (int k = 0; k < np; ++k) {
+        bytes = std::max(bytes, proj_lds_bytes(h[k].n));
+        nblk = std::max(nblk, h[k].nblk);
+        q_in_lds = q_in_lds && proj_replay_lds_bytes(h[k].n, h[k].nq, true) <= kProjLdsMax;
+    }
     if (bytes > kProjLdsMax) return hipErrorInvalidValue;
     if (bytes > 64 * 1024 &&
         hipFuncSetAttribute(reinterpret_cast<const void *>(k_proj_search), hipFuncAttributeMaxDynamicSharedMemorySize,
                             bytes) != hipSuccess)
         return hipErrorInvalidValue;
-    // spread the queries over the chip, one per wave up to two blocks per CU
-    const int blocks = std::max(1, std::min(512, (a.nq + kPW - 1) / kPW));
-    hipLaunchKernelGGL(k_proj_search, dim3(blocks), dim3(kPT), bytes, st, a);
-    const bool q_in_lds = proj_replay_lds_bytes(a.n, a.nq, true) <= kProjLdsMax;
-    if (proj_replay_lds_bytes(a.n, a.nq, q_in_lds) > kProjLdsMax) return hipErrorInvalidValue;
-    const int rbytes = proj_replay_lds_bytes(a.n, a.nq, q_in_lds);
+    // each problem's queries spread over up to 512 blocks, one query per wave
+    hipLaunchKernelGGL(k_proj_search, dim3(nblk, np), dim3(kPT), bytes, st, d);
+    int rbytes = 0;
+    for (int k = 0; k < np; ++k) rbytes = std::max(rbytes, proj_replay_lds_bytes(h[k].n, h[k].nq, q_in_lds));
+    if (rbytes > kProjLdsMax) return hipErrorInvalidValue;
     const void *rk = q_in_lds ? reinterpret_cast<const void *>(k_proj_replay<true>)
                               : reinterpret_cast<const void *>(k_proj_replay<false>);
     if (rbytes > 64 * 1024 && hipFuncSetAttribute(rk, hipFuncAttributeMaxDynamicSharedMemorySize, rbytes) != hipSuccess)
         return hipErrorInvalidValue;
     if (q_in_lds)
-        hipLaunchKernelGGL(k_proj_replay<true>, dim3(1), dim3(kPT), rbytes, st, a);
+        hipLaunchKernelGGL(k_proj_replay<true>, dim3(np), dim3(kPT), rbytes, st, d);
     else
-        hipLaunchKernelGGL(k_proj_replay<false>, dim3(1), dim3(kPT), rbytes, st, a);
+        hipLaunchKernelGGL(k_proj_replay<false>, dim3(np), dim3(kPT), rbytes, st, d);
     return hipGetLastError();
 }
 

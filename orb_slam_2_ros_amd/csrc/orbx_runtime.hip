@@ -1210,9 +1210,11 @@ int orbx_search_for_initialization(int device, const orbx_keypoint *k1, const ui
     return ORBX_OK;
 }
 
-int orbx_search_by_projection(int device, int variant, const orbx_match_frame *F, const orbx_proj_query *queries,
-                              const uint8_t *qdesc, int nq, int th_dist, float nnratio, int check_ori,
-                              int32_t *q_idx, int32_t *q_dist, int32_t *kp_final, int *nmatches) {
+namespace {
+
+// Checks one projection problem; 1 = nothing to search (outputs filled here).
+int proj_check(int variant, const orbx_match_frame *F, const orbx_proj_query *queries, const uint8_t *qdesc, int nq,
+               int th_dist, int32_t *q_idx, int32_t *q_dist, int32_t *kp_final, int *nmatches) {
     if (!F || !nmatches || variant < ORBX_PROJ_LOCALMAP || variant > ORBX_PROJ_FUSE_SIM3) return ORBX_EINVAL;
     const int n = F->n;
     if (n < 0 || n > 32767 || nq < 0 || th_dist < 0 || th_dist > 255) return ORBX_EINVAL;
@@ -1224,71 +1226,131 @@ int orbx_search_by_projection(int device, int variant, const orbx_match_frame *F
     if (n == 0 || nq == 0) {
         for (int i = 0; i < nq; ++i) { q_idx[i] = -1; q_dist[i] = -1; }
         for (int i = 0; i < n; ++i) kp_final[i] = -1;
-        return ORBX_OK;
+        return 1;
     }
-    if (!proj_fits(n)) return ORBX_EINVAL;
+    return proj_fits(n) ? ORBX_OK : ORBX_EINVAL;
+}
+
+// Host arrays several problems share (a frame searched with several query
+// sets) go up once: offsets by (pointer, bytes).
+struct Dedup {
+    struct E { const void *p; size_t bytes, off; };
+    std::vector<E> v;
+    size_t add(Layout &L, const void *p, size_t bytes, bool &fresh) {
+        for (const E &e : v)
+            if (e.p == p && e.bytes == bytes) { fresh = false; return e.off; }
+        fresh = true;
+        v.push_back({p, bytes, L.add(bytes)});
+        return v.back().off;
+    }
+};
+
+// Runs the problems (all of one variant) in one pair of launches.
+int proj_run(int device, int variant, orbx_proj_problem *P, int np, int th_dist, float nnratio, int check_ori) {
+    if (np < 0 || (np && !P)) return ORBX_EINVAL;
+    std::vector<int> live;
+    for (int k = 0; k < np; ++k) {
+        const int rc = proj_check(variant, &P[k].frame, P[k].queries, P[k].qdesc, P[k].nq, th_dist, P[k].q_idx,
+                                  P[k].q_dist, P[k].kp_final, &P[k].nmatches);
+        if (rc < 0) return rc;
+        if (rc == 0) live.push_back(k);
+    }
+    if (live.empty()) return ORBX_OK;
     if (hipSetDevice(device) != hipSuccess) return ORBX_ENODEV;
     const bool fuse = variant == ORBX_PROJ_FUSE || variant == ORBX_PROJ_FUSE_SIM3;
-    const int nlev = F->inv_sigma2 ? std::max(F->nlevels, 0) : 0;
+    const int nl = (int)live.size();
+    int64_t nq_tot = 0;
+    for (int k : live) nq_tot += P[k].nq;
     CallWs &ws = call_ws(device);
     std::lock_guard<std::mutex> lock(ws.mu);
     // candidate lists of all queries share one pool; its size is learnt: a
     // call that overflows it reports the total it needed and runs again
-    int64_t pool = fuse ? 1 : std::max<int64_t>({ws.proj_pool, 64 * (int64_t)nq, 1 << 16});
-    const int hard_cap = 4 * nq + 4096;
+    int64_t pool = fuse ? 1 : std::max<int64_t>({ws.proj_pool, 64 * nq_tot, 1 << 16});
+    static const bool dbg_stats = std::getenv("ORBX_PROJ_STATS") != nullptr;
     for (int attempt = 0; attempt < 2; ++attempt) {
         Layout L;   // inputs, then outputs, then device-only scratch
-        const size_t o_k = L.add(sizeof(orbx_keypoint) * n), o_d = L.add(32 * (size_t)n),
-                     o_ur = F->uright ? L.add(4 * (size_t)n) : 0, o_ms = F->mp_state ? L.add((size_t)n) : 0,
-                     o_isg = nlev ? L.add(4 * (size_t)nlev) : 0, o_q = L.add(sizeof(orbx_proj_query) * nq),
-                     o_qd = L.add(32 * (size_t)nq);
-        const size_t o_ptop = L.add(16);   // pool_top, hard_cnt: zeros from the host, read back after
+        Dedup dd;
+        struct Off { size_t k, d, ur, ms, isg, q, qd, qi, qdist, kf, nm, top, len, base, hard, und; int nlev, hard_cap; };
+        std::vector<Off> o(nl);
+        std::vector<bool> up(5 * nl);
+        for (int t = 0; t < nl; ++t) {
+            const orbx_proj_problem &pr = P[live[t]];
+            const orbx_match_frame *F = &pr.frame;
+            const int n = F->n;
+            bool f;
+            o[t].nlev = F->inv_sigma2 ? std::max(F->nlevels, 0) : 0;
+            o[t].k = dd.add(L, F->keys, sizeof(orbx_keypoint) * n, f); up[5 * t] = f;
+            o[t].d = dd.add(L, F->desc, 32 * (size_t)n, f); up[5 * t + 1] = f;
+            o[t].ur = F->uright ? dd.add(L, F->uright, 4 * (size_t)n, f) : 0; up[5 * t + 2] = F->uright && f;
+            o[t].ms = F->mp_state ? dd.add(L, F->mp_state, (size_t)n, f) : 0; up[5 * t + 3] = F->mp_state && f;
+            o[t].isg = o[t].nlev ? dd.add(L, F->inv_sigma2, 4 * (size_t)o[t].nlev, f) : 0; up[5 * t + 4] = o[t].nlev && f;
+            o[t].q = L.add(sizeof(orbx_proj_query) * pr.nq);
+            o[t].qd = L.add(32 * (size_t)pr.nq);
+        }
+        const size_t o_pa = L.add(sizeof(ProjBufs) * nl);
+        const size_t o_cnt = L.add(8 + 8 * (size_t)nl);   // pool_top, then hard_cnt per problem: zeros from the host
         const size_t in_bytes = L.size;
-        const size_t o_qi = L.add(4 * (size_t)nq), o_qdist = L.add(4 * (size_t)nq), o_kf = L.add(4 * (size_t)n),
-                     o_nm = L.add(4);
+        for (int t = 0; t < nl; ++t) {
+            const int n = P[live[t]].frame.n, nq = P[live[t]].nq;
+            o[t].qi = L.add(4 * (size_t)nq); o[t].qdist = L.add(4 * (size_t)nq);
+            o[t].kf = L.add(4 * (size_t)n); o[t].nm = L.add(4);
+        }
         const size_t out_end = L.size;
-        const size_t o_top = L.add(16 * (size_t)nq), o_len = L.add(4 * (size_t)nq), o_base = L.add(4 * (size_t)nq),
-                     o_pool = L.add(4 * (size_t)pool), o_hard = L.add(8 * (size_t)hard_cap), o_und = L.add((size_t)nq), o_stats = L.add(64);
+        for (int t = 0; t < nl; ++t) {
+            const int nq = P[live[t]].nq;
+            o[t].hard_cap = 4 * nq + 4096;
+            o[t].top = L.add(16 * (size_t)nq); o[t].len = L.add(4 * (size_t)nq); o[t].base = L.add(4 * (size_t)nq);
+            o[t].hard = L.add(8 * (size_t)o[t].hard_cap); o[t].und = L.add((size_t)nq);
+        }
+        const size_t o_pool = L.add(4 * (size_t)pool), o_stats = L.add(64);
         int rc = ws_reserve(ws, L.size);
         if (rc) return rc;
-        put(ws, o_k, F->keys, sizeof(orbx_keypoint) * n);
-        put(ws, o_d, F->desc, 32 * (size_t)n);
-        if (F->uright) put(ws, o_ur, F->uright, 4 * (size_t)n);
-        if (F->mp_state) put(ws, o_ms, F->mp_state, (size_t)n);
-        if (nlev) put(ws, o_isg, F->inv_sigma2, 4 * (size_t)nlev);
-        put(ws, o_q, queries, sizeof(orbx_proj_query) * nq);
-        put(ws, o_qd, qdesc, 32 * (size_t)nq);
-        std::memset(ws.host + o_ptop, 0, 16);
-        if (hipMemcpyAsync(ws.dev, ws.host, in_bytes, hipMemcpyHostToDevice, ws.st) != hipSuccess) return ORBX_EIO;
-        ProjBufs a{};
         uint8_t *D = ws.dev;
-        a.keys = at<orbx_keypoint>(D, o_k); a.desc = D + o_d;
-        a.uright = F->uright ? at<float>(D, o_ur) : nullptr;
-        a.mp_state = F->mp_state ? D + o_ms : nullptr;
-        a.inv_sigma2 = nlev ? at<float>(D, o_isg) : nullptr;
-        a.n = n; a.nlevels = nlev;
-        a.min_x = F->min_x; a.max_x = F->max_x; a.min_y = F->min_y; a.max_y = F->max_y;
-        a.q = at<orbx_proj_query>(D, o_q); a.qdesc = D + o_qd; a.nq = nq;
-        a.variant = variant; a.th_dist = th_dist; a.nnratio = nnratio; a.check_ori = check_ori;
-        a.q_idx = at<int32_t>(D, o_qi); a.q_dist = at<int32_t>(D, o_qdist); a.kp_final = at<int32_t>(D, o_kf);
-        a.nmatches = at<int32_t>(D, o_nm);
-        a.qtop = at<uint32_t>(D, o_top); a.qlen = at<int32_t>(D, o_len); a.qbase = at<int32_t>(D, o_base);
-        a.pool = at<uint32_t>(D, o_pool); a.pool_cap = pool;
-        a.pool_top = at<unsigned long long>(D, o_ptop); a.hard_cnt = at<uint32_t>(D, o_ptop + 8);
-        a.hard = at<uint2>(D, o_hard); a.hard_cap = hard_cap; a.und = D + o_und;
-        static const bool dbg_stats = std::getenv("ORBX_PROJ_STATS") != nullptr;
-        a.stats = dbg_stats ? at<int32_t>(D, o_stats) : nullptr;
-        if (launch_proj(a, ws.st) != hipSuccess ||
-            hipMemcpyAsync(ws.host + o_ptop, D + o_ptop, out_end - o_ptop, hipMemcpyDeviceToHost, ws.st) != hipSuccess ||
+        std::vector<ProjBufs> hb(nl);
+        for (int t = 0; t < nl; ++t) {
+            const orbx_proj_problem &pr = P[live[t]];
+            const orbx_match_frame *F = &pr.frame;
+            const int n = F->n, nq = pr.nq;
+            if (up[5 * t]) put(ws, o[t].k, F->keys, sizeof(orbx_keypoint) * n);
+            if (up[5 * t + 1]) put(ws, o[t].d, F->desc, 32 * (size_t)n);
+            if (up[5 * t + 2]) put(ws, o[t].ur, F->uright, 4 * (size_t)n);
+            if (up[5 * t + 3]) put(ws, o[t].ms, F->mp_state, (size_t)n);
+            if (up[5 * t + 4]) put(ws, o[t].isg, F->inv_sigma2, 4 * (size_t)o[t].nlev);
+            put(ws, o[t].q, pr.queries, sizeof(orbx_proj_query) * nq);
+            put(ws, o[t].qd, pr.qdesc, 32 * (size_t)nq);
+            ProjBufs &a = hb[t];
+            a = ProjBufs{};
+            a.keys = at<orbx_keypoint>(D, o[t].k); a.desc = D + o[t].d;
+            a.uright = F->uright ? at<float>(D, o[t].ur) : nullptr;
+            a.mp_state = F->mp_state ? D + o[t].ms : nullptr;
+            a.inv_sigma2 = o[t].nlev ? at<float>(D, o[t].isg) : nullptr;
+            a.n = n; a.nlevels = o[t].nlev;
+            a.min_x = F->min_x; a.max_x = F->max_x; a.min_y = F->min_y; a.max_y = F->max_y;
+            a.q = at<orbx_proj_query>(D, o[t].q); a.qdesc = D + o[t].qd; a.nq = nq;
+            a.variant = variant; a.th_dist = th_dist; a.nnratio = nnratio; a.check_ori = check_ori;
+            a.q_idx = at<int32_t>(D, o[t].qi); a.q_dist = at<int32_t>(D, o[t].qdist);
+            a.kp_final = at<int32_t>(D, o[t].kf); a.nmatches = at<int32_t>(D, o[t].nm);
+            a.qtop = at<uint32_t>(D, o[t].top); a.qlen = at<int32_t>(D, o[t].len); a.qbase = at<int32_t>(D, o[t].base);
+            a.pool = at<uint32_t>(D, o_pool); a.pool_cap = pool;
+            a.pool_top = at<unsigned long long>(D, o_cnt); a.hard_cnt = at<uint32_t>(D, o_cnt + 8 + 8 * (size_t)t);
+            a.hard = at<uint2>(D, o[t].hard); a.hard_cap = o[t].hard_cap; a.und = D + o[t].und;
+            a.stats = dbg_stats && t == 0 ? at<int32_t>(D, o_stats) : nullptr;
+            a.nblk = proj_blocks(nq);
+        }
+        put(ws, o_pa, hb.data(), sizeof(ProjBufs) * nl);
+        std::memset(ws.host + o_cnt, 0, 8 + 8 * (size_t)nl);
+        if (hipMemcpyAsync(D, ws.host, in_bytes, hipMemcpyHostToDevice, ws.st) != hipSuccess) return ORBX_EIO;
+        if (launch_proj(hb.data(), at<ProjBufs>(D, o_pa), nl, ws.st) != hipSuccess ||
+            hipMemcpyAsync(ws.host + o_cnt, D + o_cnt, out_end - o_cnt, hipMemcpyDeviceToHost, ws.st) != hipSuccess ||
             hipStreamSynchronize(ws.st) != hipSuccess)
             return ORBX_EIO;
         unsigned long long used = 0;
-        get(ws, o_ptop, &used, 8);
-        if (a.stats) {
+        get(ws, o_cnt, &used, 8);
+        if (dbg_stats) {
             int32_t st2[6] = {};
-            if (hipMemcpy(st2, a.stats, sizeof(st2), hipMemcpyDeviceToHost) == hipSuccess)
-                std::fprintf(stderr, "orbx proj: variant %d nq %d rounds %d in-order %d pool %llu | 10ns: init %d rounds %d end %d\n",
-                             variant, nq, st2[0], st2[1], used, st2[2], st2[3], st2[5]);
+            if (hipMemcpy(st2, D + o_stats, sizeof(st2), hipMemcpyDeviceToHost) == hipSuccess)
+                std::fprintf(stderr, "orbx proj: variant %d problems %d rounds %d in-order %d pool %llu | 10ns: init %d rounds %d end %d\n",
+                             variant, nl, st2[0], st2[1], used, st2[2], st2[3], st2[5]);
         }
         if (!fuse) ws.proj_pool = std::max<int64_t>(ws.proj_pool, (int64_t)used);
         if (!fuse && (int64_t)used > pool) {
@@ -1296,18 +1358,43 @@ int orbx_search_by_projection(int device, int variant, const orbx_match_frame *F
             pool = (int64_t)used;
             continue;
         }
-        get(ws, o_qi, q_idx, 4 * (size_t)nq);
-        get(ws, o_qdist, q_dist, 4 * (size_t)nq);
-        get(ws, o_kf, kp_final, 4 * (size_t)n);
-        get(ws, o_nm, nmatches, 4);
+        for (int t = 0; t < nl; ++t) {
+            orbx_proj_problem &pr = P[live[t]];
+            get(ws, o[t].qi, pr.q_idx, 4 * (size_t)pr.nq);
+            get(ws, o[t].qdist, pr.q_dist, 4 * (size_t)pr.nq);
+            get(ws, o[t].kf, pr.kp_final, 4 * (size_t)pr.frame.n);
+            get(ws, o[t].nm, &pr.nmatches, 4);
+        }
         return ORBX_OK;
     }
     return ORBX_EIO;
 }
 
-int orbx_search_by_bow(int device, int variant, const orbx_bow_side *A, const orbx_bow_side *B, float nnratio,
-                       int check_ori, const float *tri, int nlevels, int32_t *match_a, int32_t *match_b,
-                       int *nmatches) {
+}  // namespace
+
+int orbx_search_by_projection(int device, int variant, const orbx_match_frame *F, const orbx_proj_query *queries,
+                              const uint8_t *qdesc, int nq, int th_dist, float nnratio, int check_ori,
+                              int32_t *q_idx, int32_t *q_dist, int32_t *kp_final, int *nmatches) {
+    if (!F || !nmatches) return ORBX_EINVAL;
+    orbx_proj_problem pr{};
+    pr.frame = *F;
+    pr.queries = queries; pr.qdesc = qdesc; pr.nq = nq;
+    pr.q_idx = q_idx; pr.q_dist = q_dist; pr.kp_final = kp_final;
+    const int rc = proj_run(device, variant, &pr, 1, th_dist, nnratio, check_ori);
+    *nmatches = rc == ORBX_OK ? pr.nmatches : 0;
+    return rc;
+}
+
+int orbx_search_by_projection_batch(int device, int variant, orbx_proj_problem *problems, int nproblems, int th_dist,
+                                    float nnratio, int check_ori) {
+    return proj_run(device, variant, problems, nproblems, th_dist, nnratio, check_ori);
+}
+
+namespace {
+
+// Checks one vocabulary-node problem; 1 = nothing to search (outputs filled).
+int bow_check(int variant, const orbx_bow_side *A, const orbx_bow_side *B, const float *tri, int nlevels,
+              int32_t *match_a, int32_t *match_b, int *nmatches) {
     if (!A || !B || !nmatches || variant < ORBX_BOW_KF_FRAME || variant > ORBX_BOW_TRIANGULATION) return ORBX_EINVAL;
     if (A->n < 0 || B->n < 0 || A->nnodes < 0 || B->nnodes < 0 || (A->n && !match_a) || (B->n && !match_b))
         return ORBX_EINVAL;
@@ -1329,71 +1416,159 @@ int orbx_search_by_bow(int device, int variant, const orbx_bow_side *A, const or
     *nmatches = 0;
     for (int i = 0; i < A->n; ++i) match_a[i] = -1;
     for (int i = 0; i < B->n; ++i) match_b[i] = -1;
-    if (A->n == 0 || B->n == 0 || A->nnodes == 0 || B->nnodes == 0) return ORBX_OK;
+    return (A->n == 0 || B->n == 0 || A->nnodes == 0 || B->nnodes == 0) ? 1 : ORBX_OK;
+}
+
+int bow_run(int device, int variant, orbx_bow_problem *P, int np, float nnratio, int check_ori, int nlevels) {
+    if (np < 0 || (np && !P)) return ORBX_EINVAL;
+    std::vector<int> live;
+    for (int k = 0; k < np; ++k) {
+        const int rc = bow_check(variant, &P[k].a, &P[k].b, P[k].tri, nlevels, P[k].match_a, P[k].match_b,
+                                 &P[k].nmatches);
+        if (rc < 0) return rc;
+        if (rc == 0) live.push_back(k);
+    }
+    if (live.empty()) return ORBX_OK;
     if (hipSetDevice(device) != hipSuccess) return ORBX_ENODEV;
-    const int nfa = A->node_offsets[A->nnodes], nfb = B->node_offsets[B->nnodes];
+    const int nl = (int)live.size();
     const int ntri = variant == ORBX_BOW_TRIANGULATION ? 11 + 2 * nlevels : 0;
     Layout L;
-    size_t o_side[2][6];
-    for (int k = 0; k < 2; ++k) {
-        const orbx_bow_side *S = k ? B : A;
-        const int nf = k ? nfb : nfa;
-        o_side[k][0] = L.add(sizeof(orbx_keypoint) * S->n);
-        o_side[k][1] = L.add(32 * (size_t)S->n);
-        o_side[k][2] = L.add((size_t)S->n);
-        o_side[k][3] = L.add(4 * (size_t)S->nnodes);
-        o_side[k][4] = L.add(4 * (size_t)(S->nnodes + 1));
-        o_side[k][5] = L.add(4 * (size_t)std::max(nf, 1));
+    Dedup dd;
+    struct Off { size_t side[2][6]; size_t tri, ma, mb, cnt, bin; };
+    std::vector<Off> o(nl);
+    std::vector<uint8_t> up(12 * nl);
+    for (int t = 0; t < nl; ++t) {
+        const orbx_bow_problem &pr = P[live[t]];
+        for (int k = 0; k < 2; ++k) {
+            const orbx_bow_side *S = k ? &pr.b : &pr.a;
+            const int nf = S->node_offsets[S->nnodes];
+            bool f;
+            o[t].side[k][0] = dd.add(L, S->keys, sizeof(orbx_keypoint) * S->n, f); up[12 * t + 6 * k] = f;
+            o[t].side[k][1] = dd.add(L, S->desc, 32 * (size_t)S->n, f); up[12 * t + 6 * k + 1] = f;
+            o[t].side[k][2] = dd.add(L, S->flags, (size_t)S->n, f); up[12 * t + 6 * k + 2] = f;
+            o[t].side[k][3] = dd.add(L, S->node_ids, 4 * (size_t)S->nnodes, f); up[12 * t + 6 * k + 3] = f;
+            o[t].side[k][4] = dd.add(L, S->node_offsets, 4 * (size_t)(S->nnodes + 1), f); up[12 * t + 6 * k + 4] = f;
+            o[t].side[k][5] = dd.add(L, S->node_features, 4 * (size_t)std::max(nf, 1), f); up[12 * t + 6 * k + 5] = f;
+        }
+        o[t].tri = ntri ? L.add(4 * (size_t)ntri) : 0;
     }
-    const size_t o_tri = ntri ? L.add(4 * (size_t)ntri) : 0;
-    const size_t o_ma = L.add(4 * (size_t)A->n), o_mb = L.add(4 * (size_t)B->n);
-    const size_t in_bytes = L.size;   // match arrays start as -1 (host copies)
-    const size_t o_cnt = L.add(4 * 34);   // hist[32] + counts[2]
-    const size_t out_end = L.size;
-    const size_t o_bin = L.add((size_t)A->n);
+    const size_t o_pa = L.add(sizeof(BowBufs) * nl);
+    for (int t = 0; t < nl; ++t) {   // match arrays start as -1 (host copies), counters zeroed on the device
+        o[t].ma = L.add(4 * (size_t)P[live[t]].a.n);
+        o[t].mb = L.add(4 * (size_t)P[live[t]].b.n);
+    }
+    const size_t in_bytes = L.size;
+    for (int t = 0; t < nl; ++t) o[t].cnt = L.add(4 * 34);   // hist[32] + counts[2]
+    const size_t cnt_end = L.size;
+    for (int t = 0; t < nl; ++t) o[t].bin = L.add((size_t)P[live[t]].a.n);
     CallWs &ws = call_ws(device);
     std::lock_guard<std::mutex> lock(ws.mu);
     int rc = ws_reserve(ws, L.size);
     if (rc) return rc;
-    for (int k = 0; k < 2; ++k) {
-        const orbx_bow_side *S = k ? B : A;
-        const int nf = k ? nfb : nfa;
-        put(ws, o_side[k][0], S->keys, sizeof(orbx_keypoint) * S->n);
-        put(ws, o_side[k][1], S->desc, 32 * (size_t)S->n);
-        put(ws, o_side[k][2], S->flags, (size_t)S->n);
-        put(ws, o_side[k][3], S->node_ids, 4 * (size_t)S->nnodes);
-        put(ws, o_side[k][4], S->node_offsets, 4 * (size_t)(S->nnodes + 1));
-        put(ws, o_side[k][5], S->node_features, 4 * (size_t)nf);
-    }
-    if (ntri) put(ws, o_tri, tri, 4 * (size_t)ntri);
-    put(ws, o_ma, match_a, 4 * (size_t)A->n);
-    put(ws, o_mb, match_b, 4 * (size_t)B->n);
     uint8_t *D = ws.dev;
-    if (hipMemcpyAsync(D, ws.host, in_bytes, hipMemcpyHostToDevice, ws.st) != hipSuccess ||
-        hipMemsetAsync(D + o_cnt, 0, 4 * 34, ws.st) != hipSuccess)
-        return ORBX_EIO;
-    BowBufs a{};
-    for (int k = 0; k < 2; ++k) {
-        const orbx_bow_side *S = k ? B : A;
-        BowSideDev &d = k ? a.B : a.A;
-        d = BowSideDev{at<orbx_keypoint>(D, o_side[k][0]), D + o_side[k][1], D + o_side[k][2], S->n,
-                       at<uint32_t>(D, o_side[k][3]), at<int32_t>(D, o_side[k][4]), at<int32_t>(D, o_side[k][5]),
-                       S->nnodes};
+    std::vector<BowBufs> hb(nl);
+    for (int t = 0; t < nl; ++t) {
+        const orbx_bow_problem &pr = P[live[t]];
+        BowBufs &a = hb[t];
+        a = BowBufs{};
+        for (int k = 0; k < 2; ++k) {
+            const orbx_bow_side *S = k ? &pr.b : &pr.a;
+            const int nf = S->node_offsets[S->nnodes];
+            const size_t *so = o[t].side[k];
+            const uint8_t *u = &up[12 * t + 6 * k];
+            if (u[0]) put(ws, so[0], S->keys, sizeof(orbx_keypoint) * S->n);
+            if (u[1]) put(ws, so[1], S->desc, 32 * (size_t)S->n);
+            if (u[2]) put(ws, so[2], S->flags, (size_t)S->n);
+            if (u[3]) put(ws, so[3], S->node_ids, 4 * (size_t)S->nnodes);
+            if (u[4]) put(ws, so[4], S->node_offsets, 4 * (size_t)(S->nnodes + 1));
+            if (u[5]) put(ws, so[5], S->node_features, 4 * (size_t)nf);
+            BowSideDev &d = k ? a.B : a.A;
+            d = BowSideDev{at<orbx_keypoint>(D, so[0]), D + so[1], D + so[2], S->n, at<uint32_t>(D, so[3]),
+                           at<int32_t>(D, so[4]), at<int32_t>(D, so[5]), S->nnodes};
+        }
+        if (ntri) put(ws, o[t].tri, pr.tri, 4 * (size_t)ntri);
+        put(ws, o[t].ma, pr.match_a, 4 * (size_t)pr.a.n);
+        put(ws, o[t].mb, pr.match_b, 4 * (size_t)pr.b.n);
+        a.variant = variant; a.nnratio = nnratio; a.check_ori = check_ori;
+        a.tri = ntri ? at<float>(D, o[t].tri) : nullptr;
+        a.ex = ntri ? pr.tri[9] : 0.f; a.ey = ntri ? pr.tri[10] : 0.f;
+        a.nlevels = nlevels;
+        a.match_a = at<int32_t>(D, o[t].ma); a.match_b = at<int32_t>(D, o[t].mb); a.bin_a = at<int8_t>(D, o[t].bin);
+        a.hist = at<int32_t>(D, o[t].cnt); a.counts = at<int32_t>(D, o[t].cnt) + 32;
     }
-    a.variant = variant; a.nnratio = nnratio; a.check_ori = check_ori;
-    a.tri = ntri ? at<float>(D, o_tri) : nullptr; a.ex = ntri ? tri[9] : 0.f; a.ey = ntri ? tri[10] : 0.f;
-    a.nlevels = nlevels;
-    a.match_a = at<int32_t>(D, o_ma); a.match_b = at<int32_t>(D, o_mb); a.bin_a = at<int8_t>(D, o_bin);
-    a.hist = at<int32_t>(D, o_cnt); a.counts = at<int32_t>(D, o_cnt) + 32;
-    if (launch_bow(a, ws.st) != hipSuccess ||
-        hipMemcpyAsync(ws.host + o_ma, D + o_ma, out_end - o_ma, hipMemcpyDeviceToHost, ws.st) != hipSuccess ||
+    put(ws, o_pa, hb.data(), sizeof(BowBufs) * nl);
+    if (hipMemcpyAsync(D, ws.host, in_bytes, hipMemcpyHostToDevice, ws.st) != hipSuccess ||
+        hipMemsetAsync(D + in_bytes, 0, cnt_end - in_bytes, ws.st) != hipSuccess)
+        return ORBX_EIO;
+    const size_t o_out = o[0].ma;   // match arrays and counters are one contiguous run
+    if (launch_bow(hb.data(), at<BowBufs>(D, o_pa), nl, ws.st) != hipSuccess ||
+        hipMemcpyAsync(ws.host + o_out, D + o_out, cnt_end - o_out, hipMemcpyDeviceToHost, ws.st) != hipSuccess ||
         hipStreamSynchronize(ws.st) != hipSuccess)
         return ORBX_EIO;
-    get(ws, o_ma, match_a, 4 * (size_t)A->n);
-    get(ws, o_mb, match_b, 4 * (size_t)B->n);
-    int32_t counts[2];
-    get(ws, o_cnt + 4 * 32, counts, sizeof(counts));
-    *nmatches = counts[1];
+    for (int t = 0; t < nl; ++t) {
+        orbx_bow_problem &pr = P[live[t]];
+        get(ws, o[t].ma, pr.match_a, 4 * (size_t)pr.a.n);
+        get(ws, o[t].mb, pr.match_b, 4 * (size_t)pr.b.n);
+        int32_t counts[2];
+        get(ws, o[t].cnt + 4 * 32, counts, sizeof(counts));
+        pr.nmatches = counts[1];
+    }
+    return ORBX_OK;
+}
+
+}  // namespace
+
+int orbx_search_by_bow(int device, int variant, const orbx_bow_side *A, const orbx_bow_side *B, float nnratio,
+                       int check_ori, const float *tri, int nlevels, int32_t *match_a, int32_t *match_b,
+                       int *nmatches) {
+    if (!A || !B || !nmatches) return ORBX_EINVAL;
+    orbx_bow_problem pr{};
+    pr.a = *A; pr.b = *B; pr.tri = tri; pr.match_a = match_a; pr.match_b = match_b;
+    const int rc = bow_run(device, variant, &pr, 1, nnratio, check_ori, nlevels);
+    *nmatches = rc == ORBX_OK ? pr.nmatches : 0;
+    return rc;
+}
+
+int orbx_search_by_bow_batch(int device, int variant, orbx_bow_problem *problems, int nproblems, float nnratio,
+                             int check_ori, int nlevels) {
+    return bow_run(device, variant, problems, nproblems, nnratio, check_ori, nlevels);
+}
+
+int orbx_rotation_filter(const orbx_keypoint *ka, const orbx_keypoint *kb, int32_t *match_a, int na,
+                         const uint8_t *exclude, int *nmatches) {
+    if (na < 0 || !nmatches || (na && (!ka || !kb || !match_a))) return ORBX_EINVAL;
+    constexpr int kHist = 30;
+    std::vector<int> bins(na, -1);
+    int hist[kHist] = {};
+    const float factor = 1.0f / kHist;
+    for (int i = 0; i < na; ++i) {
+        if (match_a[i] < 0) continue;
+        if (exclude && exclude[i]) { match_a[i] = -1; continue; }
+        float rot = ka[i].angle - kb[match_a[i]].angle;
+        if (rot < 0.0f) rot += 360.0f;
+        int bin = (int)std::round(rot * factor);
+        if (bin == kHist) bin = 0;
+        if (bin < 0 || bin >= kHist) return ORBX_EINVAL;   // angles outside [0, 360)
+        bins[i] = bin;
+        ++hist[bin];
+    }
+    // ComputeThreeMaxima (ORBmatcher.cc:1603-1644)
+    int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+    for (int b = 0; b < kHist; ++b) {
+        const int sz = hist[b];
+        if (sz > max1) { max3 = max2; max2 = max1; max1 = sz; ind3 = ind2; ind2 = ind1; ind1 = b; }
+        else if (sz > max2) { max3 = max2; max2 = sz; ind3 = ind2; ind2 = b; }
+        else if (sz > max3) { max3 = sz; ind3 = b; }
+    }
+    if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+    else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+    int kept = 0;
+    for (int i = 0; i < na; ++i) {
+        if (match_a[i] < 0) continue;
+        if (bins[i] != ind1 && bins[i] != ind2 && bins[i] != ind3) { match_a[i] = -1; continue; }
+        ++kept;
+    }
+    *nmatches = kept;
     return ORBX_OK;
 }
 
@@ -1403,13 +1578,14 @@ int orbx_search_by_sim3(int device, const orbx_match_frame *kf1, const orbx_matc
     if (!kf1 || !kf2 || !nfound || kf1->n < 0 || kf2->n < 0 || (kf1->n && !matches12)) return ORBX_EINVAL;
     const int n1 = kf1->n, n2 = kf2->n;
     std::vector<int32_t> m1(n1), d1(n1), m2(n2), d2(n2), f1(n1), f2(n2);
-    int nm = 0;
-    // pKF1's points into pKF2, then pKF2's into pKF1 (ORBmatcher.cc:1147-1219, 1222-1294)
-    int rc = orbx_search_by_projection(device, ORBX_PROJ_FUSE_SIM3, kf2, q1, qdesc1, n1, th_dist, 1.0f, 0,
-                                       m1.data(), d1.data(), f2.data(), &nm);
-    if (rc) return rc;
-    rc = orbx_search_by_projection(device, ORBX_PROJ_FUSE_SIM3, kf1, q2, qdesc2, n2, th_dist, 1.0f, 0, m2.data(),
-                                   d2.data(), f1.data(), &nm);
+    // pKF1's points into pKF2 and pKF2's into pKF1 (ORBmatcher.cc:1147-1219,
+    // 1222-1294), one batch of two problems
+    orbx_proj_problem pr[2] = {};
+    pr[0].frame = *kf2; pr[0].queries = q1; pr[0].qdesc = qdesc1; pr[0].nq = n1;
+    pr[0].q_idx = m1.data(); pr[0].q_dist = d1.data(); pr[0].kp_final = f2.data();
+    pr[1].frame = *kf1; pr[1].queries = q2; pr[1].qdesc = qdesc2; pr[1].nq = n2;
+    pr[1].q_idx = m2.data(); pr[1].q_dist = d2.data(); pr[1].kp_final = f1.data();
+    const int rc = proj_run(device, ORBX_PROJ_FUSE_SIM3, pr, 2, th_dist, 1.0f, 0);
     if (rc) return rc;
     // agreement check (:1297-1315)
     int found = 0;

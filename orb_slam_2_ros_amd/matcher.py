@@ -17,7 +17,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import KEYPOINT_DTYPE, PROJ_QUERY_DTYPE, BowSide, MatchFrame, check, ptr
+from ._lib import KEYPOINT_DTYPE, PROJ_QUERY_DTYPE, BowProblem, BowSide, MatchFrame, ProjProblem, check, load, ptr
 
 # orbx_search_by_projection variants (include/orbx.h)
 PROJ_VARIANTS = {"localmap": 0, "lastframe": 1, "keyframe": 2, "sim3": 3, "fuse": 4, "fuse_sim3": 5}
@@ -103,7 +103,100 @@ class ORBmatcher:
                                                   ctypes.byref(nm)), "SearchByProjection")
         return nm.value, qi[:len(q)].copy(), qdist[:len(q)].copy(), kf[:len(keys)].copy()
 
+    def search_by_projection_batch(self, variant, problems, th_dist=None):
+        """Several search_by_projection calls of one variant in one launch pair
+        (orbx_search_by_projection_batch): Fuse over a keyframe's neighbours
+        (LocalMapping.cc:537), relocalisation's SearchByProjection over the
+        candidates (Tracking.cc:1667).  problems: dicts with the keyword
+        arguments of search_by_projection (keys, desc, queries, qdesc, bounds,
+        uright, mp_state, inv_sigma2); arrays that are the same object are
+        uploaded once.  Returns one (nmatches, q_idx, q_dist, kp_final) per problem."""
+        v = PROJ_VARIANTS[variant] if isinstance(variant, str) else int(variant)
+        if th_dist is None:
+            th_dist = self.TH_HIGH if v in (0, 1) else self.TH_LOW
+        arr = (ProjProblem * max(len(problems), 1))()
+        keep, outs, conv = [], [], {}
+
+        def c(a, dt, shape=None):   # same source object -> same converted array (uploaded once)
+            if a is None:
+                return None
+            key = (id(a), dt)
+            if key not in conv:
+                x = np.ascontiguousarray(a, dt)
+                conv[key] = (a, x.reshape(shape) if shape else x)
+            return conv[key][1]
+        for k, P in enumerate(problems):
+            keys = c(P["keys"], KEYPOINT_DTYPE)
+            desc = c(P["desc"], np.uint8, (-1, 32))
+            q = c(P["queries"], PROJ_QUERY_DTYPE)
+            qd = c(P["qdesc"], np.uint8, (-1, 32))
+            if len(keys) != len(desc) or len(q) != len(qd):
+                raise ValueError("rows of keys/desc or queries/qdesc differ")
+            ur, ms, isg = c(P.get("uright"), np.float32), c(P.get("mp_state"), np.uint8), c(P.get("inv_sigma2"), np.float32)
+            qi = np.full(max(len(q), 1), -1, np.int32)
+            qdist = np.full(max(len(q), 1), -1, np.int32)
+            kf = np.full(max(len(keys), 1), -1, np.int32)
+            keep.extend([keys, desc, q, qd, ur, ms, isg])
+            outs.append((qi, qdist, kf, len(q), len(keys)))
+            f = MatchFrame(ptr(keys), ptr(desc), ptr(ur), ptr(ms), ptr(isg), len(keys),
+                           0 if isg is None else len(isg), *[float(b) for b in P["bounds"]])
+            arr[k] = ProjProblem(f, ptr(q), ptr(qd), len(q), ptr(qi), ptr(qdist), ptr(kf), 0)
+        check(self._lib.orbx_search_by_projection_batch(self.device, v, arr, len(problems), int(th_dist),
+                                                        ctypes.c_float(self.mfNNratio), int(self.mbCheckOrientation)),
+              "SearchByProjection batch")
+        return [(arr[k].nmatches, qi[:nq].copy(), qd[:nq].copy(), kf[:n].copy())
+                for k, (qi, qd, kf, nq, n) in enumerate(outs)]
+
     # -- vocabulary-node searches (ORBmatcher.cc:160-289, 524-657, 659-825) --
+    @staticmethod
+    def _bow_side(S, keep):
+        arrs = (np.ascontiguousarray(S["keys"], KEYPOINT_DTYPE), np.ascontiguousarray(S["desc"], np.uint8),
+                np.ascontiguousarray(S["flags"], np.uint8), np.ascontiguousarray(S["ids"], np.uint32),
+                np.ascontiguousarray(S["off"], np.int32), np.ascontiguousarray(S["feat"], np.int32))
+        keep.append(arrs)
+        k, d, f, i, o, e = arrs
+        return BowSide(ptr(k), ptr(d), ptr(f), len(k), ptr(i), ptr(o), ptr(e), len(i))
+
+    def search_by_bow_batch(self, variant, problems, nlevels=8):
+        """Several search_by_bow calls of one variant in one launch pair
+        (orbx_search_by_bow_batch), e.g. SearchForTriangulation of a new
+        keyframe against its covisible neighbours (LocalMapping.cc:276-315).
+        problems: dicts with A, B (as search_by_bow) and tri.  A side dict that
+        is the same object in several problems is uploaded once.  Returns one
+        (nmatches, match_a, match_b) per problem."""
+        v = BOW_VARIANTS[variant] if isinstance(variant, str) else int(variant)
+        arr = (BowProblem * max(len(problems), 1))()
+        keep, outs, sides = [], [], {}
+        for k, P in enumerate(problems):
+            for S in (P["A"], P["B"]):
+                if id(S) not in sides:
+                    sides[id(S)] = (S, self._bow_side(S, keep), len(keep) - 1)
+            sa, ia = sides[id(P["A"])][1:]
+            sb, ib = sides[id(P["B"])][1:]
+            na, nb = len(keep[ia][0]), len(keep[ib][0])
+            t = None if P.get("tri") is None else np.ascontiguousarray(P["tri"], np.float32)
+            ma = np.full(max(na, 1), -1, np.int32)
+            mb = np.full(max(nb, 1), -1, np.int32)
+            keep.append((t,))
+            outs.append((ma, mb, na, nb))
+            arr[k] = BowProblem(sa, sb, ptr(t), ptr(ma), ptr(mb), 0)
+        check(self._lib.orbx_search_by_bow_batch(self.device, v, arr, len(problems), ctypes.c_float(self.mfNNratio),
+                                                 int(self.mbCheckOrientation), int(nlevels)), "SearchByBoW batch")
+        return [(arr[k].nmatches, ma[:na].copy(), mb[:nb].copy()) for k, (ma, mb, na, nb) in enumerate(outs)]
+
+    @staticmethod
+    def rotation_filter(ka, kb, match_a, exclude=None):
+        """orbx_rotation_filter: the reference's rotation-consistency pass over
+        the pairs (i, match_a[i]), skipping A features flagged in exclude.
+        Returns (nmatches, filtered match_a)."""
+        ka = np.ascontiguousarray(ka, KEYPOINT_DTYPE)
+        kb = np.ascontiguousarray(kb, KEYPOINT_DTYPE)
+        m = np.array(match_a, np.int32, copy=True)
+        ex = None if exclude is None else np.ascontiguousarray(exclude, np.uint8)
+        nm = ctypes.c_int(0)
+        check(load().orbx_rotation_filter(ptr(ka), ptr(kb), ptr(m), len(m), ptr(ex), ctypes.byref(nm)),
+              "rotation filter")
+        return nm.value, m
     def search_by_bow(self, variant, A, B, tri=None, nlevels=8):
         """SearchByBoW(KF, F) ("kf_frame"), SearchByBoW(KF1, KF2) ("kf_kf") or
         SearchForTriangulation ("triangulation").  A, B: dicts with keys, desc,
@@ -112,15 +205,7 @@ class ORBmatcher:
         Returns (nmatches, match_a, match_b)."""
         v = BOW_VARIANTS[variant] if isinstance(variant, str) else int(variant)
         keep = []
-
-        def side(S):
-            arrs = (np.ascontiguousarray(S["keys"], KEYPOINT_DTYPE), np.ascontiguousarray(S["desc"], np.uint8),
-                    np.ascontiguousarray(S["flags"], np.uint8), np.ascontiguousarray(S["ids"], np.uint32),
-                    np.ascontiguousarray(S["off"], np.int32), np.ascontiguousarray(S["feat"], np.int32))
-            keep.append(arrs)
-            k, d, f, i, o, e = arrs
-            return BowSide(ptr(k), ptr(d), ptr(f), len(k), ptr(i), ptr(o), ptr(e), len(i))
-        sa, sb = side(A), side(B)
+        sa, sb = self._bow_side(A, keep), self._bow_side(B, keep)
         t = None if tri is None else np.ascontiguousarray(tri, np.float32)
         na, nb = len(keep[0][0]), len(keep[1][0])
         ma = np.full(max(na, 1), -1, np.int32)
