@@ -6,20 +6,26 @@
 // cpp:78-91).  SURVEY.md §8 f2, config C4.
 //
 // Device work per LM trial, all FP64:
-//   k_ba_errors      thread per edge: error, chi2, Huber rho (computeActiveErrors)
-//   k_ba_linearize   thread per edge: Jacobians and the edge's J^T W J / J^T W r blocks
-//   k_ba_reduce      wave per vertex: sums of its edges' blocks, in edge order
-//   k_ba_point       thread per point: (Hll + lambda I)^-1, db, then per edge B Dinv and B db
-//   k_ba_pairs       wave per camera pair: S_ij -= B_i Dinv B_j^T over shared points, point order
-//   k_ba_chol        one workgroup: dense Cholesky of the reduced camera system and the solve
-//   k_ba_backsub     thread per point: xl = Dinv (bl - sum_e B_e^T xp)
-//   k_ba_update      poses exp(dx) * T (SE3Quat), points += dx
+//   k_ba_errors        thread per edge: error, chi2, Huber rho (computeActiveErrors)
+//   k_ba_linearize     thread per edge: Jacobians and the edge's J^T W J / J^T W r blocks
+//   k_ba_ordered_sums  block per free camera: Hpp / bp (and the reduced right-hand side
+//                      bp - sum B Dinv bl) as sums over its edges in edge order, the
+//                      edge records staged through LDS by three waves while one adds
+//   k_ba_reduce        wave per point: Hll / bl, edge order
+//   k_ba_point         thread per point: (Hll + lambda I)^-1 and Dinv bl
+//   k_ba_point_edges   thread per edge: B Dinv and B Dinv bl
+//   k_ba_pairs(_map)   wave per camera pair: S_ij -= B_i Dinv B_j^T over shared points, point order
+//   k_ba_chol_lds      one workgroup: blocked dense Cholesky of the reduced camera system and
+//                      the solves (k_ba_chol beyond 128 unknowns)
+//   k_ba_backsub       thread per point: xl = Dinv (bl - sum_e B_e^T xp)
+//   k_ba_update        poses exp(dx) * T (SE3Quat), points += dx
 // Every sum runs in a fixed order (edge order per vertex, ascending point per
 // camera pair, ascending column in the Cholesky), so a run is deterministic
 // and matches the oracle's CPU restatement of the same order.  g2o's own order
 // is unspecified (it sorts edges with equal ids), so parity with it is to
 // rounding only.  The LM control (lambda, rho, trials, termination) runs on
-// the host as in the reference.
+// the host as in the reference, with one stream synchronisation per trial
+// (lm_optimize).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -141,11 +147,13 @@ __device__ inline void edge_error(const EdgeD &e, const Pose &T, const double *X
     }
 }
 
+// gate (optional): run only when *gate != 0 (a trial whose solve failed
+// leaves the estimate and the errors alone)
 __global__ void k_ba_errors(const Pose *poses, const double *pts, const EdgeD *edges, int ne, const uint8_t *active,
                             int robust, int front_only, double *err_out, double *chi2_out, double *rho_out,
-                            uint8_t *front_out) {
+                            uint8_t *front_out, double *rho0_out, const int *gate) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= ne) return;
+    if (i >= ne || (gate && !*gate)) return;
     const EdgeD e = edges[i];
     double err[3];
     bool front;
@@ -168,6 +176,7 @@ __global__ void k_ba_errors(const Pose *poses, const double *pts, const EdgeD *e
     chi2_out[i] = chi2;
     rho_out[2 * (int64_t)i] = rho0;
     rho_out[2 * (int64_t)i + 1] = rho1;
+    if (rho0_out) rho0_out[i] = rho0;   // (contiguous, for the host's ordered sum)
 }
 
 __global__ void k_ba_linearize(const Pose *poses, const double *pts, const EdgeD *edges, int ne, const uint8_t *active,
@@ -301,9 +310,8 @@ __device__ inline double cof(const double *m, int i, int j) {
     return m[3 * i1 + j1] * m[3 * i2 + j2] - m[3 * i1 + j2] * m[3 * i2 + j1];
 }
 
-__global__ void k_ba_point(const double *Hll, const double *bl, int npt, double lambda, const EdgeOut *eo,
-                           const int32_t *offs, const int32_t *list, const uint8_t *usable, double *dinv_out,
-                           double *bdinv, double *bdb) {
+__global__ void k_ba_point(const double *Hll, const double *bl, int npt, double lambda, double *dinv_out,
+                           double *db_out) {
     const int pt = blockIdx.x * blockDim.x + threadIdx.x;
     if (pt >= npt) return;
     double m[9];
@@ -317,32 +325,36 @@ __global__ void k_ba_point(const double *Hll, const double *bl, int npt, double 
     D[3] = cof(m, 0, 1) * invdet; D[4] = cof(m, 1, 1) * invdet; D[5] = cof(m, 2, 1) * invdet;
     D[6] = cof(m, 0, 2) * invdet; D[7] = cof(m, 1, 2) * invdet; D[8] = cof(m, 2, 2) * invdet;
     for (int k = 0; k < 9; ++k) dinv_out[9 * (int64_t)pt + k] = D[k];
-    double db[3];
     for (int r = 0; r < 3; ++r) {
         double acc = 0;
         for (int c = 0; c < 3; ++c) acc = acc + D[3 * r + c] * bl[3 * (int64_t)pt + c];
-        db[r] = acc;
-    }
-    for (int t = offs[pt]; t < offs[pt + 1]; ++t) {
-        const int ei = list[t];
-        if (!usable[ei]) continue;
-        const double *B = eo[ei].hpl;
-        for (int r = 0; r < 6; ++r) {
-            for (int c = 0; c < 3; ++c) {
-                double acc = 0;
-                for (int k = 0; k < 3; ++k) acc = acc + B[3 * r + k] * D[3 * k + c];
-                bdinv[18 * (int64_t)ei + 3 * r + c] = acc;
-            }
-            double acc = 0;
-            for (int k = 0; k < 3; ++k) acc = acc + B[3 * r + k] * db[k];
-            bdb[6 * (int64_t)ei + r] = acc;
-        }
+        db_out[3 * (int64_t)pt + r] = acc;
     }
 }
 
-// S block (i1, i2), i1 <= i2: Hpp(+lambda on the diagonal) - sum over shared
-// points (ascending) of BDinv_e1 * B_e2^T.  Wave per pair, lane per entry.
-// Camera lists hold the usable edges sorted by point.
+// per usable edge: B Dinv (6x3) and B Dinv bl (6) of its point (thread per
+// edge, so the work spreads over every edge, not over the points' lists)
+__global__ void k_ba_point_edges(const EdgeOut *eo, const int32_t *epoint, const uint8_t *usable, int ne,
+                                 const double *dinv, const double *db, double *bdinv, double *bdb) {
+    const int ei = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ei >= ne || !usable[ei]) return;
+    const int pt = epoint[ei];
+    double D[9], d3[3];
+    for (int k = 0; k < 9; ++k) D[k] = dinv[9 * (int64_t)pt + k];
+    for (int k = 0; k < 3; ++k) d3[k] = db[3 * (int64_t)pt + k];
+    const double *B = eo[ei].hpl;
+    for (int r = 0; r < 6; ++r) {
+        for (int c = 0; c < 3; ++c) {
+            double acc = 0;
+            for (int k = 0; k < 3; ++k) acc = acc + B[3 * r + k] * D[3 * k + c];
+            bdinv[18 * (int64_t)ei + 3 * r + c] = acc;
+        }
+        double acc = 0;
+        for (int k = 0; k < 3; ++k) acc = acc + B[3 * r + k] * d3[k];
+        bdb[6 * (int64_t)ei + r] = acc;
+    }
+}
+
 __global__ void k_ba_pairs(const int2 *pairs, int npairs, const int32_t *coffs, const int32_t *clist,
                            const int32_t *epoint, const EdgeOut *eo, const double *bdinv, const double *Hpp,
                            double lambda, int nf, double *S) {
@@ -433,25 +445,95 @@ __global__ __launch_bounds__(256) void k_ba_pairs_map(const int2 *pairs, int npa
     S[(int64_t)(6 * i2 + c) * n + 6 * i1 + r] = acc;   // mirror (the solver reads the full matrix)
 }
 
-// bschur = bp - sum over the camera's usable edges (point order) of B db.
-__global__ void k_ba_bschur(const double *bp, const int32_t *coffs, const int32_t *clist, const double *bdb, int nf,
-                            double *bs) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= 6 * nf) return;
-    const int cam = i / 6, r = i % 6;
-    double coef = 0;
-    int t = coffs[cam];
-    const int te = coffs[cam + 1];
-    for (; t + 8 <= te; t += 8) {   // 8 loads in flight, summed in order
-        double val[8];
+// Ordered sums per vertex with the edge records staged through LDS: out[v][f]
+// = sum over t in [offs[v], offs[v+1]) of rec[list[t]][fo[f]] (edges with
+// pred[e] == 0 skipped), each field summed one edge at a time in list order
+// -- the order the sequential restatement uses.  One block per vertex: waves
+// 1..3 stage the next chunk of records while wave 0 (lane = field) adds the
+// current one, so the adds wait on LDS, not on a global round trip per edge.
+// minus != nullptr: out = minus - sum (the reduced right-hand side).
+constexpr int kSumChunk = 128;
+// NF fields per record; layout 1: EdgeOut's hpp (36) then bp (6), layout 0:
+// record fields 0..NF-1.
+template <int NF, int LAYOUT>
+__global__ __launch_bounds__(256) void k_ba_ordered_sums(const double *rec, int stride, const int32_t *offs,
+                                                         const int32_t *list, const uint8_t *pred, const double *minus,
+                                                         double *out_a, int na, double *out_b) {
+    extern __shared__ double sbuf[];   // 2 x kSumChunk x NF, 4 x 64 edge ids, 2 x kSumChunk flags
+    int32_t *ids = reinterpret_cast<int32_t *>(sbuf + 2 * kSumChunk * NF);
+    uint8_t *okf = reinterpret_cast<uint8_t *>(ids + 4 * 64);
+    const int v = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int t0 = offs[v], te = offs[v + 1];
+    const int nch = (te - t0 + kSumChunk - 1) / kSumChunk;
+    // a wave stages edges jw, jw + nwv, ... (at most 64) of chunk c: one id per
+    // lane, then the (edge, field) elements spread over the lanes, so a lane's
+    // loads are independent of each other
+    auto stage = [&](int c, int jw, int nwv) {
+        const int base = t0 + c * kSumChunk, cnt = min(kSumChunk, te - base);
+        double *b = sbuf + (c & 1) * kSumChunk * NF;
+        uint8_t *o = okf + (c & 1) * kSumChunk;
+        const int nj = cnt > jw ? (cnt - jw + nwv - 1) / nwv : 0;
+        int32_t *wid = ids + 64 * w;   // this wave's edge ids
+        if (lane < nj) {
+            const int eid = list[base + jw + lane * nwv];
+            wid[lane] = eid;
+            o[jw + lane * nwv] = pred ? pred[eid] : 1;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int total = nj * NF;
+        for (int k0 = lane; k0 < total; k0 += 64 * 8) {   // 8 loads in flight per lane
+            double x[8];
+            int dst[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) val[j] = bdb[6 * (int64_t)clist[t + j] + r];
+            for (int q = 0; q < 8; ++q) {
+                const int k = k0 + 64 * q;
+                dst[q] = -1;
+                if (k < total) {
+                    const int jl = k / NF, f = k - jl * NF;
+                    const int off = LAYOUT == 1 && f >= 36 ? 63 + (f - 36) : f;   // EdgeOut::bp at 63
+                    x[q] = rec[(int64_t)wid[jl] * stride + off];
+                    dst[q] = (jw + jl * nwv) * NF + f;
+                }
+            }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) coef = coef + val[j];
+            for (int q = 0; q < 8; ++q)
+                if (dst[q] >= 0) b[dst[q]] = x[q];
+        }
+    };
+    if (nch > 0) stage(0, w, 4);
+    __syncthreads();
+    double acc = 0;
+    for (int c = 0; c < nch; ++c) {
+        if (w > 0) {
+            if (c + 1 < nch) stage(c + 1, w - 1, 3);
+        } else if (lane < NF) {
+            const int cnt = min(kSumChunk, te - (t0 + c * kSumChunk));
+            const double *b = sbuf + (c & 1) * kSumChunk * NF;
+            const uint8_t *o = okf + (c & 1) * kSumChunk;
+            // 8 records' loads in flight, then their adds in order (a skipped
+            // edge leaves acc as it is)
+            int j = 0;
+            for (; j + 8 <= cnt; j += 8) {
+                double x[8];
+                uint8_t f[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) { f[q] = o[j + q]; x[q] = b[(j + q) * NF + lane]; }
+#pragma unroll
+                for (int q = 0; q < 8; ++q) acc = f[q] ? acc + x[q] : acc;
+            }
+            for (; j < cnt; ++j) acc = o[j] ? acc + b[j * NF + lane] : acc;
+        }
+        __syncthreads();
     }
-    for (; t < te; ++t) coef = coef + bdb[6 * (int64_t)clist[t] + r];
-    bs[i] = bp[i] - coef;
+    if (w != 0 || lane >= NF) return;
+    if (lane < na) out_a[(int64_t)v * na + lane] = minus ? minus[(int64_t)v * na + lane] - acc : acc;
+    else out_b[(int64_t)v * (NF - na) + lane - na] = acc;
 }
+
+inline size_t ordered_sums_lds(int nfld) { return 16 * kSumChunk * (size_t)nfld + 4 * 64 * 4 + 2 * kSumChunk; }
+
 
 // Dense Cholesky S = L L^T (lower, in place, column by column) and the two
 // triangular solves for x; one workgroup.  ok = 0 if S is not positive definite.
@@ -502,68 +584,94 @@ __device__ inline double readlane_f64(double v, int l) {
     return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 
-// The same factorisation and solves with S held in LDS (n <= kCholLds), with
-// the work spread over the workgroup instead of one thread:
-//  - right-looking: at column k every wave scales the column in registers
-//    (lane t holds L(k+1+t, k)) and the trailing lower triangle is updated
-//    row per wave, lane per column.  Each entry still receives its terms
-//    L(i,m) L(j,m) in ascending m, so the factor equals the column-by-column
-//    one bit for bit; one barrier per column.  Column k of L is kept in the
-//    upper triangle's row k (untouched by the trailing updates), the
-//    diagonal in dg[].
+// The same factorisation and solves with S held in LDS (n <= kCholLds),
+// blocked right-looking in panels of kPanel columns:
+//  - wave 0 factors a panel alone (lane t owns rows k+1+t and k+65+t of each
+//    column k: scale by the diagonal, then the panel's own later columns get
+//    their term L(i,k) L(j,k)); no workgroup barrier inside a panel;
+//  - then all waves apply the panel to the trailing lower triangle, each entry
+//    receiving the panel's kPanel terms one by one in ascending column.
+// Every entry therefore receives its terms L(i,m) L(j,m) in ascending m, each
+// as its own multiply and subtract, exactly as the column-by-column factor
+// (the oracle's): bit-identical, with two barriers per panel instead of one
+// per column.  L stays in the lower triangle (row stride n+1: odd, so column
+// reads spread over banks), the diagonal also in dg[].
 //  - the solves run column-sweep in one wave (lane r owns rows r and r+64):
 //    the forward terms arrive in ascending k as in the row loop, the
 //    backward terms in descending k (the order the oracle uses).
-// Row stride n+1 keeps the backward solve's column reads off one bank.
 constexpr int kCholLds = 128;
+constexpr int kPanel = 8;
 __global__ __launch_bounds__(512) void k_ba_chol_lds(const double *S, int n, const double *bs, double *x, int *ok) {
     extern __shared__ double L[];   // n rows of n+1, then dg (n)
+    __shared__ int bad;
     const int ld = n + 1;
     double *dg = L + n * ld;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
     for (int r = w; r < n; r += nw)
         for (int c = lane; c <= r; c += 64) L[r * ld + c] = S[(int64_t)r * n + c];
+    if (tid == 0) bad = 0;
     __syncthreads();
-    bool good = true;
-    const int i0 = lane, i1 = lane + 64;   // (rows relative to k + 1)
-    for (int k = 0; k < n; ++k) {
-        const double d = L[k * ld + k];
-        if (!(d > 0)) {   // (every thread reads the same d: the break is uniform)
-            good = false;
-            break;
-        }
-        const double g = sqrt(d);
-        const int r0 = k + 1 + i0, r1 = k + 1 + i1;
-        const double a0 = r0 < n ? L[r0 * ld + k] / g : 0.0;
-        const double a1 = r1 < n ? L[r1 * ld + k] / g : 0.0;
+    for (int k0 = 0; k0 < n; k0 += kPanel) {
+        const int k1 = min(k0 + kPanel, n);
         if (w == 0) {
-            if (lane == 0) dg[k] = g;
-            if (r0 < n) L[k * ld + r0] = a0;
-            if (r1 < n) L[k * ld + r1] = a1;
+            for (int k = k0; k < k1; ++k) {
+                const double d = L[k * ld + k];
+                if (!(d > 0)) {   // (uniform over the wave)
+                    if (lane == 0) bad = 1;
+                    break;
+                }
+                const double g = sqrt(d);
+                const int r0 = k + 1 + lane, r1 = k + 65 + lane;
+                const double a0 = r0 < n ? L[r0 * ld + k] / g : 0.0;
+                const double a1 = r1 < n ? L[r1 * ld + k] / g : 0.0;
+                if (lane == 0) dg[k] = g;
+                if (r0 < n) L[r0 * ld + k] = a0;
+                if (r1 < n) L[r1 * ld + k] = a1;
+                for (int j = k + 1; j < k1; ++j) {   // the panel's later columns
+                    const int t = j - k - 1;
+                    const double aj = t < 64 ? readlane_f64(a0, t) : readlane_f64(a1, t - 64);
+                    if (r0 >= j && r0 < n) L[r0 * ld + j] = L[r0 * ld + j] - a0 * aj;
+                    if (r1 >= j && r1 < n) L[r1 * ld + j] = L[r1 * ld + j] - a1 * aj;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
         }
-        for (int i = k + 1 + w; i < n; i += nw) {
-            const int t = i - k - 1;
-            const double ai = t < 64 ? readlane_f64(a0, t) : readlane_f64(a1, t - 64);
-            if (r0 <= i) L[i * ld + r0] = L[i * ld + r0] - ai * a0;
-            if (r1 <= i) L[i * ld + r1] = L[i * ld + r1] - ai * a1;
+        __syncthreads();
+        if (bad) break;
+        // trailing update: rows i >= k1 by wave, columns j in [k1, i] by lane
+        for (int i = k1 + w; i < n; i += nw) {
+            double li[kPanel];
+#pragma unroll
+            for (int m = 0; m < kPanel; ++m) li[m] = k0 + m < k1 ? L[i * ld + k0 + m] : 0.0;
+            for (int j = k1 + lane; j <= i; j += 64) {
+                double v = L[i * ld + j];
+#pragma unroll
+                for (int m = 0; m < kPanel; ++m)
+                    if (k0 + m < k1) v = v - li[m] * L[j * ld + k0 + m];
+                L[i * ld + j] = v;
+            }
         }
         __syncthreads();
     }
     if (w != 0) return;
+    const bool good = !bad;
     if (lane == 0) *ok = good;
     if (!good) return;
+    const int i0 = lane, i1 = lane + 64;
     double s0 = i0 < n ? bs[i0] : 0.0, s1 = i1 < n ? bs[i1] : 0.0;
     for (int k = 0; k < n; ++k) {   // L y = b
         const double yk = (k < 64 ? readlane_f64(s0, k) : readlane_f64(s1, k - 64)) / dg[k];
         if (lane == (k & 63)) (k < 64 ? s0 : s1) = yk;
-        if (i0 > k && i0 < n) s0 = s0 - L[k * ld + i0] * yk;
-        if (i1 > k && i1 < n) s1 = s1 - L[k * ld + i1] * yk;
+        if (i0 > k && i0 < n) s0 = s0 - L[i0 * ld + k] * yk;
+        if (i1 > k && i1 < n) s1 = s1 - L[i1 * ld + k] * yk;
     }
     for (int k = n - 1; k >= 0; --k) {   // L^T x = y
         const double xk = (k < 64 ? readlane_f64(s0, k) : readlane_f64(s1, k - 64)) / dg[k];
         if (lane == (k & 63)) (k < 64 ? s0 : s1) = xk;
-        if (i0 < k) s0 = s0 - L[i0 * ld + k] * xk;
-        if (i1 < k) s1 = s1 - L[i1 * ld + k] * xk;
+        if (i0 < k) s0 = s0 - L[k * ld + i0] * xk;
+        if (i1 < k) s1 = s1 - L[k * ld + i1] * xk;
     }
     if (i0 < n) x[i0] = s0;
     if (i1 < n) x[i1] = s1;
@@ -597,8 +705,10 @@ __global__ void k_ba_backsub(const double *dinv, const double *bl, int npt, cons
 }
 
 // SE3Quat::exp(update) * estimate (se3quat.h:223-258, :104-110); points += dx
-__global__ void k_ba_update(Pose *poses, int ncam, double *pts, int npt, const double *xp, const double *xl) {
+__global__ void k_ba_update(Pose *poses, int ncam, double *pts, int npt, const double *xp, const double *xl,
+                            const int *gate) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gate && !*gate) return;
     if (i < npt)
         for (int k = 0; k < 3; ++k) pts[3 * (int64_t)i + k] = pts[3 * (int64_t)i + k] + xl[3 * (int64_t)i + k];
     if (i < ncam && poses[i].free_idx >= 0) {
@@ -698,10 +808,24 @@ public:
     int solve(double lambda, int *ok);
     double scale(double lambda);
     int update();
+    // the LM driver's asynchronous pieces: launches and readbacks into pinned
+    // host buffers, one stream synchronisation per trial
+    int errors_async(bool robust, const int *gate);
+    int solve_async(double lambda);
+    int update_gated();
+    int read_errors();
+    int read_diag();
+    int read_trial();
+    double chi_sum_host() const;
+    double max_diag_host() const;
+    double scale_host(double lambda) const;
     int push();
     int pop();
     int download(double *pts, std::vector<double> &chi2, std::vector<uint8_t> &front);
-    ~BA() { if (buf_) (void)hipFree(buf_); }
+    ~BA() {
+        if (buf_) (void)hipFree(buf_);
+        if (hbuf_) (void)hipHostFree(hbuf_);
+    }
 
     Graph &g_;
     hipStream_t st_;
@@ -717,12 +841,16 @@ public:
     int2 *d_pairs = nullptr;
     int npairs = 0;
     double *d_Hpp = nullptr, *d_bp = nullptr, *d_Hll = nullptr, *d_bl = nullptr, *d_dinv = nullptr,
-           *d_bdinv = nullptr, *d_bdb = nullptr, *d_S = nullptr, *d_bs = nullptr, *d_x = nullptr;
+           *d_bdinv = nullptr, *d_bdb = nullptr, *d_S = nullptr, *d_bs = nullptr, *d_x = nullptr, *d_db = nullptr;
     int *d_ok = nullptr;
     int32_t *d_cmap = nullptr;   // free camera x point -> position in its usable list (-1)
     bool use_map = false;        // every (camera, point) observed at most once
     std::vector<uint8_t> act_;
     std::vector<int32_t> cv_offs_, cv_list_;   // all edges per free camera (reduce), edge order
+    double *d_rho0 = nullptr;                  // rho[0] per edge, contiguous
+    uint8_t *hbuf_ = nullptr;                  // pinned readbacks
+    double *h_rho0 = nullptr, *h_x = nullptr, *h_b = nullptr, *h_hpp = nullptr, *h_hll = nullptr;
+    int *h_ok = nullptr;
 };
 
 int BA::alloc() {
@@ -765,7 +893,7 @@ int BA::alloc() {
                          8 * ne * 6 + sizeof(EdgeOut) * ne + 4 * (nf + 1 + ne + np + 1 + ne + ne + nf + 1 + ne) +
                          sizeof(int2) * std::max(npairs, 1) + 8 * (36 * nf + 6 * nf + 9 * np + 3 * np + 9 * np +
                                                                    18 * ne + 6 * ne + n * n + n + n + 3 * np) +
-                         4 * nf * np + 256 * 2;
+                         4 * nf * np + 8 * ne + 8 * 3 * np + 256 * 4;
     if (hipMalloc(reinterpret_cast<void **>(&buf_), bytes) != hipSuccess) return ORBX_ENOMEM;
     uint8_t *p = buf_;
     d_pose = carve<Pose>(p, nc); d_pose_bk = carve<Pose>(p, nc);
@@ -784,7 +912,18 @@ int BA::alloc() {
     d_S = carve<double>(p, n * n); d_bs = carve<double>(p, n); d_x = carve<double>(p, n + 3 * np);
     d_ok = carve<int>(p, 1);
     d_cmap = carve<int32_t>(p, nf * np);
+    d_rho0 = carve<double>(p, ne);
+    d_db = carve<double>(p, 3 * np);
     if ((size_t)(p - buf_) > bytes) return ORBX_ENOMEM;
+    {
+        const size_t m = n + 3 * np;
+        const size_t hb = 8 * (ne + 2 * m + 36 * nf + 9 * np) + 64 + 256 * 6;
+        if (hipHostMalloc(reinterpret_cast<void **>(&hbuf_), hb, hipHostMallocDefault) != hipSuccess) return ORBX_ENOMEM;
+        uint8_t *h = hbuf_;
+        h_rho0 = carve<double>(h, ne); h_x = carve<double>(h, m); h_b = carve<double>(h, m);
+        h_hpp = carve<double>(h, 36 * nf); h_hll = carve<double>(h, 9 * np); h_ok = carve<int>(h, 1);
+        if ((size_t)(h - hbuf_) > hb) return ORBX_ENOMEM;
+    }
     auto up = [&](void *d, const void *h, size_t b) {
         return b == 0 || hipMemcpyAsync(d, h, b, hipMemcpyHostToDevice, st_) == hipSuccess;
     };
@@ -844,7 +983,7 @@ void BA::set_active(const std::vector<uint8_t> &act) {
 int BA::errors(bool robust, double *chi_sum) {
     const int ne = g_.ne;
     if (ne) hipLaunchKernelGGL(k_ba_errors, dim3((ne + 255) / 256), dim3(256), 0, st_, d_pose, d_pts, d_edges, ne,
-                               d_active, robust ? 1 : 0, 0, d_err, d_chi2, d_rho, d_front);
+                               d_active, robust ? 1 : 0, 0, d_err, d_chi2, d_rho, d_front, nullptr, nullptr);
     std::vector<double> rho(2 * (size_t)std::max(ne, 1));
     if (hipGetLastError() != hipSuccess ||
         (ne && hipMemcpyAsync(rho.data(), d_rho, 16 * (size_t)ne, hipMemcpyDeviceToHost, st_) != hipSuccess) ||
@@ -861,8 +1000,16 @@ int BA::build() {
     const Graph &g = g_;
     if (g.ne) hipLaunchKernelGGL(k_ba_linearize, dim3((g.ne + 255) / 256), dim3(256), 0, st_, d_pose, d_pts, d_edges,
                                  g.ne, d_active, d_err, d_rho, d_eo);
-    if (g.nf) hipLaunchKernelGGL(k_ba_reduce, dim3((g.nf + 3) / 4), dim3(256), 0, st_, d_eo, d_cvoffs, d_cvlist,
-                                 d_active, g.nf, 0, d_Hpp, d_bp);
+    if (g.nf) {   // Hpp and bp of each free camera over all its edges, edge order
+        constexpr int kEo = sizeof(EdgeOut) / sizeof(double);
+        const size_t lb = ordered_sums_lds(42);
+        if (lb > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void *>(k_ba_ordered_sums<42, 1>),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb) != hipSuccess)
+            return ORBX_EIO;
+        hipLaunchKernelGGL((k_ba_ordered_sums<42, 1>), dim3(g.nf), dim3(256), lb, st_,
+                           reinterpret_cast<const double *>(d_eo), kEo, d_cvoffs, d_cvlist, d_active, nullptr, d_Hpp, 36,
+                           d_bp);
+    }
     if (g.npt) hipLaunchKernelGGL(k_ba_reduce, dim3((g.npt + 3) / 4), dim3(256), 0, st_, d_eo, d_poffs, d_plist,
                                   d_active, g.npt, 1, d_Hll, d_bl);
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
@@ -889,8 +1036,13 @@ int BA::solve(double lambda, int *ok) {
     const int n = 6 * g.nf;
     // (the previous factorisation left L in place, also outside the pair blocks)
     if (n && hipMemsetAsync(d_S, 0, 8 * (size_t)n * n, st_) != hipSuccess) return ORBX_EIO;
-    if (g.npt) hipLaunchKernelGGL(k_ba_point, dim3((g.npt + 255) / 256), dim3(256), 0, st_, d_Hll, d_bl, g.npt, lambda,
-                                  d_eo, d_poffs, d_plist, d_usable, d_dinv, d_bdinv, d_bdb);
+    if (g.npt) {
+        hipLaunchKernelGGL(k_ba_point, dim3((g.npt + 255) / 256), dim3(256), 0, st_, d_Hll, d_bl, g.npt, lambda, d_dinv,
+                           d_db);
+        if (g.ne)
+            hipLaunchKernelGGL(k_ba_point_edges, dim3((g.ne + 255) / 256), dim3(256), 0, st_, d_eo, d_epoint, d_usable,
+                               g.ne, d_dinv, d_db, d_bdinv, d_bdb);
+    }
     if (g.nf) {
         if (use_map)
             hipLaunchKernelGGL(k_ba_pairs_map, dim3((npairs + 3) / 4), dim3(256), 0, st_, d_pairs, npairs, d_coffs,
@@ -898,8 +1050,9 @@ int BA::solve(double lambda, int *ok) {
         else
             hipLaunchKernelGGL(k_ba_pairs, dim3((npairs + 3) / 4), dim3(256), 0, st_, d_pairs, npairs, d_coffs,
                                d_clist, d_epoint, d_eo, d_bdinv, d_Hpp, lambda, g.nf, d_S);
-        hipLaunchKernelGGL(k_ba_bschur, dim3((n + 255) / 256), dim3(256), 0, st_, d_bp, d_coffs, d_clist, d_bdb, g.nf,
-                           d_bs);
+        // bs = bp - sum over the camera's usable edges of B Dinv bl, edge order
+        hipLaunchKernelGGL((k_ba_ordered_sums<6, 0>), dim3(g.nf), dim3(256), ordered_sums_lds(6), st_, d_bdb, 6,
+                           d_coffs, d_clist, nullptr, d_bp, d_bs, 6, nullptr);
         // (blocks of camera pairs without a shared point stay as the memset left them)
         if (n <= kCholLds) {
             const int lb = 8 * (n * (n + 1) + n);
@@ -938,8 +1091,107 @@ double BA::scale(double lambda) {
 int BA::update() {
     const int n = std::max(g_.ncam, g_.npt);
     hipLaunchKernelGGL(k_ba_update, dim3((n + 255) / 256), dim3(256), 0, st_, d_pose, g_.ncam, d_pts, g_.npt, d_x,
-                       d_x + 6 * g_.nf);
+                       d_x + 6 * g_.nf, nullptr);
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
+}
+
+int BA::errors_async(bool robust, const int *gate) {
+    const int ne = g_.ne;
+    if (ne) hipLaunchKernelGGL(k_ba_errors, dim3((ne + 255) / 256), dim3(256), 0, st_, d_pose, d_pts, d_edges, ne,
+                               d_active, robust ? 1 : 0, 0, d_err, d_chi2, d_rho, d_front, d_rho0, gate);
+    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
+}
+
+// solve() without the readback: d_ok says whether the Cholesky succeeded
+int BA::solve_async(double lambda) {
+    const Graph &g = g_;
+    const int n = 6 * g.nf;
+    if (n && hipMemsetAsync(d_S, 0, 8 * (size_t)n * n, st_) != hipSuccess) return ORBX_EIO;
+    if (!g.nf && hipMemsetAsync(d_ok, 0xFF, 4, st_) != hipSuccess) return ORBX_EIO;   // (nothing to factor: ok)
+    if (g.npt) {
+        hipLaunchKernelGGL(k_ba_point, dim3((g.npt + 255) / 256), dim3(256), 0, st_, d_Hll, d_bl, g.npt, lambda, d_dinv,
+                           d_db);
+        if (g.ne)
+            hipLaunchKernelGGL(k_ba_point_edges, dim3((g.ne + 255) / 256), dim3(256), 0, st_, d_eo, d_epoint, d_usable,
+                               g.ne, d_dinv, d_db, d_bdinv, d_bdb);
+    }
+    if (g.nf) {
+        if (use_map)
+            hipLaunchKernelGGL(k_ba_pairs_map, dim3((npairs + 3) / 4), dim3(256), 0, st_, d_pairs, npairs, d_coffs,
+                               d_clist, d_epoint, d_cmap, g.npt, d_eo, d_bdinv, d_Hpp, lambda, g.nf, d_S);
+        else
+            hipLaunchKernelGGL(k_ba_pairs, dim3((npairs + 3) / 4), dim3(256), 0, st_, d_pairs, npairs, d_coffs,
+                               d_clist, d_epoint, d_eo, d_bdinv, d_Hpp, lambda, g.nf, d_S);
+        // bs = bp - sum over the camera's usable edges of B Dinv bl, edge order
+        hipLaunchKernelGGL((k_ba_ordered_sums<6, 0>), dim3(g.nf), dim3(256), ordered_sums_lds(6), st_, d_bdb, 6,
+                           d_coffs, d_clist, nullptr, d_bp, d_bs, 6, nullptr);
+        if (n <= kCholLds) {
+            const int lb = 8 * (n * (n + 1) + n);
+            if (lb > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void *>(k_ba_chol_lds),
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize, lb) != hipSuccess)
+                return ORBX_EIO;
+            hipLaunchKernelGGL(k_ba_chol_lds, dim3(1), dim3(512), lb, st_, d_S, n, d_bs, d_x, d_ok);
+        } else {
+            hipLaunchKernelGGL(k_ba_chol, dim3(1), dim3(1024), 0, st_, d_S, n, d_bs, d_x, d_ok);
+        }
+    }
+    if (g.npt) hipLaunchKernelGGL(k_ba_backsub, dim3((g.npt + 255) / 256), dim3(256), 0, st_, d_dinv, d_bl, g.npt,
+                                  d_eo, d_poffs, d_plist, d_usable, d_edges, d_pose, d_x, d_x + n);
+    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
+}
+
+int BA::update_gated() {
+    const int n = std::max(g_.ncam, g_.npt);
+    hipLaunchKernelGGL(k_ba_update, dim3((n + 255) / 256), dim3(256), 0, st_, d_pose, g_.ncam, d_pts, g_.npt, d_x,
+                       d_x + 6 * g_.nf, d_ok);
+    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
+}
+
+int BA::read_errors() {
+    return (g_.ne && hipMemcpyAsync(h_rho0, d_rho0, 8 * (size_t)g_.ne, hipMemcpyDeviceToHost, st_) != hipSuccess)
+               ? ORBX_EIO : ORBX_OK;
+}
+
+int BA::read_diag() {
+    if ((g_.nf && hipMemcpyAsync(h_hpp, d_Hpp, 8 * 36 * (size_t)g_.nf, hipMemcpyDeviceToHost, st_) != hipSuccess) ||
+        (g_.npt && hipMemcpyAsync(h_hll, d_Hll, 8 * 9 * (size_t)g_.npt, hipMemcpyDeviceToHost, st_) != hipSuccess))
+        return ORBX_EIO;
+    return ORBX_OK;
+}
+
+// a trial's readback: the solve flag, the errors at the trial estimate, and
+// x and b for computeScale
+int BA::read_trial() {
+    const int n = 6 * g_.nf, m = n + 3 * g_.npt;
+    if (hipMemcpyAsync(h_ok, d_ok, 4, hipMemcpyDeviceToHost, st_) != hipSuccess || read_errors() != ORBX_OK ||
+        (m && hipMemcpyAsync(h_x, d_x, 8 * (size_t)m, hipMemcpyDeviceToHost, st_) != hipSuccess) ||
+        (n && hipMemcpyAsync(h_b, d_bp, 8 * (size_t)n, hipMemcpyDeviceToHost, st_) != hipSuccess) ||
+        (g_.npt && hipMemcpyAsync(h_b + n, d_bl, 8 * 3 * (size_t)g_.npt, hipMemcpyDeviceToHost, st_) != hipSuccess))
+        return ORBX_EIO;
+    return ORBX_OK;
+}
+
+double BA::chi_sum_host() const {   // activeRobustChi2: active edges in order
+    double s = 0;
+    for (int e = 0; e < g_.ne; ++e)
+        if (act_[e]) s += h_rho0[e];
+    return s;
+}
+
+double BA::max_diag_host() const {   // computeLambdaInit: max |diagonal| over the free vertices
+    double mx = 0.;
+    for (int f = 0; f < g_.nf; ++f)
+        for (int j = 0; j < 6; ++j) mx = std::max(std::fabs(h_hpp[36 * (size_t)f + 7 * j]), mx);
+    for (int p = 0; p < g_.npt; ++p)
+        for (int j = 0; j < 3; ++j) mx = std::max(std::fabs(h_hll[9 * (size_t)p + 4 * j]), mx);
+    return mx;
+}
+
+double BA::scale_host(double lambda) const {   // computeScale: x (lambda x + b), poses then points
+    const int m = 6 * g_.nf + 3 * g_.npt;
+    double s = 0.;
+    for (int j = 0; j < m; ++j) s += h_x[j] * (lambda * h_x[j] + h_b[j]);
+    return s;
 }
 
 int BA::push() {
@@ -960,7 +1212,7 @@ int BA::pop() {
 // a rejected trial's errors stay), the depth test at the current estimate
 int BA::download(double *pts, std::vector<double> &chi2, std::vector<uint8_t> &front) {
     if (g_.ne) hipLaunchKernelGGL(k_ba_errors, dim3((g_.ne + 255) / 256), dim3(256), 0, st_, d_pose, d_pts, d_edges,
-                                  g_.ne, d_active, 0, 1, d_err, d_chi2, d_rho, d_front);
+                                  g_.ne, d_active, 0, 1, d_err, d_chi2, d_rho, d_front, nullptr, nullptr);
     chi2.resize(std::max(g_.ne, 1));
     front.resize(std::max(g_.ne, 1));
     if (hipMemcpyAsync(g_.poses.data(), d_pose, sizeof(Pose) * g_.ncam, hipMemcpyDeviceToHost, st_) != hipSuccess ||
@@ -974,36 +1226,44 @@ int BA::download(double *pts, std::vector<double> &chi2, std::vector<uint8_t> &f
 
 // OptimizationAlgorithmLevenberg::solve over `iters` iterations
 // (optimization_algorithm_levenberg.cpp:60-145); returns iterations run.
+// One stream synchronisation per trial: the trial's solve, update and errors
+// are enqueued together (update and errors gated on the solve's flag on the
+// device) and read back at once.  An iteration that follows an accepted trial
+// reuses that trial's errors, which are the errors of the current estimate
+// (g2o recomputes them: same values, same sum).
 int lm_optimize(BA &ba, int iters, bool robust, int *rc_out) {
-    double lambda = 0, ni = 2;
+    double lambda = 0, ni = 2, currentChi = 0;
     int nBad = 0, it = 0;
+    bool fresh = false;   // the device errors are the current estimate's and currentChi their sum
     *rc_out = ORBX_OK;
+    auto fail = [&](int rc) { *rc_out = rc; return it; };
     for (; it < iters; ++it) {
-        double currentChi = 0;
-        int rc = ba.errors(robust, &currentChi);
-        if (!rc) rc = ba.build();
-        if (rc) { *rc_out = rc; return it; }
-        const double iniChi = currentChi;
-        if (it == 0) {
-            double md = 0;
-            if ((rc = ba.max_diag(&md))) { *rc_out = rc; return it; }
-            lambda = 1e-5 * md;   // _tau * maxDiagonal
-            ni = 2;
-            nBad = 0;
+        int rc;
+        if (!fresh && (rc = ba.errors_async(robust, nullptr))) return fail(rc);
+        if ((rc = ba.build())) return fail(rc);
+        if (!fresh || it == 0) {
+            if ((!fresh && (rc = ba.read_errors())) || (it == 0 && (rc = ba.read_diag()))) return fail(rc);
+            if (hipStreamSynchronize(ba.st_) != hipSuccess) return fail(ORBX_EIO);
+            if (!fresh) currentChi = ba.chi_sum_host();
+            if (it == 0) {
+                lambda = 1e-5 * ba.max_diag_host();   // _tau * maxDiagonal
+                ni = 2;
+                nBad = 0;
+            }
         }
+        const double iniChi = currentChi;
         double rho = 0;
         int qmax = 0;
         do {
-            int ok = 0;
-            if ((rc = ba.push()) || (rc = ba.solve(lambda, &ok))) { *rc_out = rc; return it; }
-            double tempChi = 0;
-            if (ok) {
-                if ((rc = ba.update()) || (rc = ba.errors(robust, &tempChi))) { *rc_out = rc; return it; }
-            } else {
-                tempChi = DBL_MAX;   // (the reference updates with an unsolved x; the step is rejected either way)
-            }
+            if ((rc = ba.push()) || (rc = ba.solve_async(lambda)) || (rc = ba.update_gated()) ||
+                (rc = ba.errors_async(robust, ba.d_ok)) || (rc = ba.read_trial()))
+                return fail(rc);
+            if (hipStreamSynchronize(ba.st_) != hipSuccess) return fail(ORBX_EIO);
+            const bool ok = *ba.h_ok != 0;
+            // (the reference updates with an unsolved x; the step is rejected either way)
+            const double tempChi = ok ? ba.chi_sum_host() : DBL_MAX;
             rho = currentChi - tempChi;
-            double sc = ok ? ba.scale(lambda) : 0.0;
+            double sc = ok ? ba.scale_host(lambda) : 0.0;
             sc += 1e-3;
             rho /= sc;
             if (rho > 0 && std::isfinite(tempChi)) {
@@ -1013,10 +1273,12 @@ int lm_optimize(BA &ba, int iters, bool robust, int *rc_out) {
                 lambda *= scaleFactor;
                 ni = 2;
                 currentChi = tempChi;
+                fresh = true;
             } else {
                 lambda *= ni;
                 ni *= 2;
-                if ((rc = ba.pop())) { *rc_out = rc; return it; }
+                fresh = false;
+                if ((rc = ba.pop())) return fail(rc);
             }
             qmax++;
         } while (rho < 0 && qmax < 10);

@@ -11,21 +11,29 @@
 // recovered exactly: a keyframe is first met at its first shared query word,
 // and among keyframes first met at the same word, in add order.  So the key
 // (rank of that word, add sequence) sorts them as the reference lists them.
-// The L1 scores of the retained keyframes are a second pass (a wave per
-// keyframe; the common-word terms are summed in ascending word order, as the
-// reference's merge adds them).  The per-keyframe query state (mnLoopQuery,
-// mnLoopWords, mLoopScore and the reloc trio) persists across queries on the
-// host exactly as in the reference, and the covisibility accumulation and the
-// retention run there too (a few hundred scalars).
+// The per-keyframe query state (mnLoopQuery, mnLoopWords, mLoopScore and the
+// reloc trio) lives on the device beside the arena, one record per slot, and
+// is updated by the counting pass exactly as the walk updates it; the same
+// pass lists the keyframes the walk would add to lKFsSharingWords.  The L1
+// scores of the retained ones are a second pass (a wave per keyframe; the
+// common-word terms are summed in ascending word order, as the reference's
+// merge adds them), which also appends the survivors of the score threshold.
+// Only those come back to the host, in a fixed-size buffer, with the state of
+// the covisible neighbours the accumulation reads (KeyFrameDatabase.cc:151-185
+// / 287-318: the covisibility graph is the caller's, through a callback).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <list>
 #include <mutex>
 #include <set>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
+
+#include <hipcub/hipcub.hpp>
 
 #include "orbx_device.h"
 #include "orbx_wave.h"
@@ -54,71 +62,270 @@ __device__ inline int find_word(const uint32_t *qw, int nq, uint32_t w) {
     return -1;
 }
 
-// Per keyframe: the number of query words it contains and the rank of the
-// first one (the query word at which the inverted-file walk first meets it).
-__global__ __launch_bounds__(kKT) void k_kfdb_count(const SlotDev *slots, int nslots, const uint32_t *words,
-                                                    const uint32_t *qw_g, int nq, int2 *out) {
-    __shared__ uint32_t qs[kQLds];
-    const bool staged = nq <= kQLds;
-    if (staged)
-        for (int i = threadIdx.x; i < nq; i += kKT) qs[i] = qw_g[i];
-    __syncthreads();
-    const uint32_t *qw = staged ? qs : qw_g;
-    const int lane = threadIdx.x & 63;
-    const int s = blockIdx.x * (kKT / 64) + (threadIdx.x >> 6);
+// Per-keyframe query state (KeyFrame.h: mnLoopQuery, mnLoopWords,
+// mLoopScore, mnRelocQuery, mnRelocWords, mRelocScore), by slot.
+struct KState {
+    uint64_t loop_query, reloc_query;
+    int32_t loop_words, reloc_words;
+    float loop_score, reloc_score;
+};
+
+// A keyframe the walk lists (lKFsSharingWords), for the scoring pass.
+struct Listed {
+    uint32_t first;   // rank of its first shared query word: the walk's order
+    int32_t slot;
+    float score;
+};
+
+struct QueryDev {
+    uint64_t qid;
+    int reloc;
+    int nconn;           // connected keyframes (slots, ascending)
+    float min_score;
+    int32_t *max_words;  // [0] maxCommonWords over the listed ones, [1] survivors
+    int list_cap;
+    uint32_t stamp;      // this query's number
+    int4 *rec;           // per slot, written for the keyframes met: (stamp, words, score bits, query == qid)
+};
+
+// ---- the inverted file on the device
+// Postings of the keyframes added before the last build, as CSR over word
+// ids (csr_off[V + 1], csr_slot[]): a query walks only its words' lists, as
+// the reference walks mvInvertedFile.  Keyframes added since (the "delta",
+// kept small by rebuilding) are counted by brute force against the query.
+// The order inside a list does not matter: a keyframe's count and first
+// shared word, and its state update, do not depend on it.
+
+// build: postings per word, then their placement (wave per slot)
+__global__ __launch_bounds__(kKT) void k_csr_count(const SlotDev *slots, int nslots, const uint32_t *words,
+                                                   uint32_t *counts) {
+    const int s = blockIdx.x * (kKT / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (s >= nslots) return;
     const SlotDev sl = slots[s];
-    int cnt = 0;
-    uint32_t first = ~0u;
-    if (sl.alive) {
-        for (int i = lane; i < sl.n; i += 64) {
-            const int r = find_word(qw, nq, words[sl.off + i]);
-            if (r >= 0) { ++cnt; first = min(first, (uint32_t)r); }
+    for (int i = lane; i < sl.n; i += 64) atomicAdd(&counts[words[sl.off + i]], 1u);
+}
+
+__global__ __launch_bounds__(kKT) void k_csr_fill(const SlotDev *slots, int nslots, const uint32_t *words,
+                                                  const uint32_t *off, uint32_t *fill, int32_t *post) {
+    const int s = blockIdx.x * (kKT / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (s >= nslots) return;
+    const SlotDev sl = slots[s];
+    for (int i = lane; i < sl.n; i += 64) {
+        const uint32_t w = words[sl.off + i];
+        post[off[w] + atomicAdd(&fill[w], 1u)] = s;
+    }
+}
+
+struct TouchDev {
+    const uint32_t *csr_off; const int32_t *csr_slot; uint32_t V;
+    int delta0, nslots;          // brute-force slots [delta0, nslots)
+    int32_t *qcnt; uint32_t *qfirst;   // per slot, 0 / ~0 between queries
+    int32_t *touched; int32_t *ntouched;
+};
+
+// Shared words of a keyframe with the query and the rank of the first one
+// (both lists ascend: each lane merges a contiguous run of the keyframe's
+// words with the query's, from the run's lower bound).
+__device__ inline void count_slot(const SlotDev &sl, const uint32_t *words, const uint32_t *qw, int nq, int lane,
+                                  int &cnt, uint32_t &first) {
+    cnt = 0;
+    first = ~0u;
+    if (sl.alive && sl.n > 0) {
+        const int per = (sl.n + 63) >> 6;
+        const int i0 = min(lane * per, sl.n), i1 = min(i0 + per, sl.n);
+        if (i0 < i1) {
+            const uint32_t *kw = words + sl.off;
+            uint32_t w = kw[i0];
+            int lo = 0, hi = nq;   // lower_bound(qw, w)
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (qw[mid] < w) lo = mid + 1; else hi = mid;
+            }
+            int i = i0, r = lo;
+            while (r < nq) {
+                const uint32_t q = qw[r];
+                while (w < q && ++i < i1) w = kw[i];
+                if (i >= i1) break;
+                if (w == q) {
+                    ++cnt;
+                    first = min(first, (uint32_t)r);
+                    if (++i >= i1) break;
+                    w = kw[i];
+                }
+                ++r;
+            }
         }
     }
     cnt = wave_sum_i32(cnt);
     first = wave_min_u32(first);
-    if (lane == 0) out[s] = make_int2(cnt, (int)first);
 }
 
-// L1Scoring::score(query, keyframe) for the listed slots, in double.
-__global__ __launch_bounds__(kKT) void k_kfdb_score(const SlotDev *slots, const int32_t *list, int nlist,
-                                                    const uint32_t *words, const double *values, const uint32_t *qw_g,
-                                                    const double *qv_g, int nq, double *score) {
-    __shared__ uint32_t qs[kQLds];
+// Pass 1 (persistent grid, wave per work item): items [0, nq) walk the
+// posting list of query word r; items past nq count one delta keyframe.
+// Every keyframe met goes once to the touched list.
+__global__ __launch_bounds__(kKT) void k_kfdb_touch(const SlotDev *slots, const uint32_t *words, const uint32_t *qw_g,
+                                                    int nq, TouchDev t) {
+    extern __shared__ uint32_t qs[];
     const bool staged = nq <= kQLds;
     if (staged)
         for (int i = threadIdx.x; i < nq; i += kKT) qs[i] = qw_g[i];
     __syncthreads();
     const uint32_t *qw = staged ? qs : qw_g;
     const int lane = threadIdx.x & 63;
-    const int li = blockIdx.x * (kKT / 64) + (threadIdx.x >> 6);
-    if (li >= nlist) return;
-    const SlotDev sl = slots[list[li]];
-    double acc = 0;
-    for (int c0 = 0; c0 < sl.n; c0 += 64) {
-        const int i = c0 + lane;
-        double term = 0;
-        bool hit = false;
-        if (i < sl.n) {
-            const int r = find_word(qw, nq, words[sl.off + i]);
-            if (r >= 0) {
-                const double vi = qv_g[r], wi = values[sl.off + i];
-                term = __dsub_rn(__dsub_rn(fabs(__dsub_rn(vi, wi)), fabs(vi)), fabs(wi));
-                hit = true;
+    const int nw = gridDim.x * (kKT / 64);
+    const int items = nq + (t.nslots - t.delta0);
+    for (int it = blockIdx.x * (kKT / 64) + (threadIdx.x >> 6); it < items; it += nw) {
+        if (it < nq) {
+            const uint32_t w = qw[it];
+            if (w >= t.V) continue;
+            const uint32_t b = t.csr_off[w], e = t.csr_off[w + 1];
+            for (uint32_t i = b + lane; i < e; i += 64) {
+                const int s = t.csr_slot[i];
+                if (!slots[s].alive) continue;
+                atomicMin(&t.qfirst[s], (uint32_t)it);
+                if (atomicAdd(&t.qcnt[s], 1) == 0) t.touched[atomicAdd(t.ntouched, 1)] = s;
+            }
+        } else {
+            const int s = t.delta0 + (it - nq);
+            int c;
+            uint32_t f;
+            count_slot(slots[s], words, qw, nq, lane, c, f);
+            if (lane == 0 && c > 0) {
+                t.qcnt[s] = c;
+                t.qfirst[s] = f;
+                t.touched[atomicAdd(t.ntouched, 1)] = s;
             }
         }
-        // add the terms in ascending word order (the keyframe's words are sorted)
-        for (uint64_t b = __ballot(hit); b; b &= b - 1) {
-            const int j = (int)__builtin_ctzll(b);
-            const uint64_t bits = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)__double_as_longlong(term), j) |
-                                  ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(
-                                       (int)(uint32_t)((uint64_t)__double_as_longlong(term) >> 32), j)
-                                   << 32);
-            acc = __dadd_rn(acc, __longlong_as_double((long long)bits));
+    }
+}
+
+// Pass 2 (thread per touched keyframe): the walk's state update
+// (KeyFrameDatabase.cc:95-119 / 234-251):
+//   loop:  not met by this query yet -> connected: words = 1 (it is reset at
+//          every meeting and ends at 1); else query = qid, words = count, listed;
+//          met before (same query id) -> words += count;
+//   reloc: not met -> query = qid, words = count, listed; else words += count.
+// Resets the per-slot scratch for the next query.
+__global__ __launch_bounds__(kKT) void k_kfdb_list(TouchDev t, const int32_t *conn, QueryDev qd, KState *state,
+                                                   int4 *listed) {
+    const int n = *t.ntouched;
+    for (int k = blockIdx.x * kKT + threadIdx.x; k < n; k += gridDim.x * kKT) {
+        const int s = t.touched[k];
+        const int cnt = t.qcnt[s];
+        const uint32_t first = t.qfirst[s];
+        t.qcnt[s] = 0;
+        t.qfirst[s] = ~0u;
+        int lst = 0;
+        KState &st = state[s];
+        if (!qd.reloc) {
+            if (st.loop_query != qd.qid) {
+                int lo = 0, hi = qd.nconn - 1;
+                bool connected = false;
+                while (lo <= hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (conn[mid] == s) { connected = true; break; }
+                    if (conn[mid] < s) lo = mid + 1; else hi = mid - 1;
+                }
+                if (connected) {
+                    st.loop_words = 1;
+                } else {
+                    st.loop_query = qd.qid;
+                    st.loop_words = cnt;
+                    lst = 1;
+                }
+            } else {
+                st.loop_words += cnt;
+            }
+        } else {
+            if (st.reloc_query != qd.qid) {
+                st.reloc_query = qd.qid;
+                st.reloc_words = cnt;
+                lst = 1;
+            } else {
+                st.reloc_words += cnt;
+            }
+        }
+        if (lst) atomicMax(qd.max_words, cnt);
+        listed[k] = make_int4(lst ? cnt : 0, (int)first, s, 0);
+        // what the accumulation may read of this keyframe as a neighbour
+        qd.rec[s] = qd.reloc ? make_int4((int)qd.stamp, st.reloc_words, __float_as_int(st.reloc_score),
+                                         st.reloc_query == qd.qid)
+                             : make_int4((int)qd.stamp, st.loop_words, __float_as_int(st.loop_score),
+                                         st.loop_query == qd.qid);
+    }
+}
+
+// Pass 3 (persistent grid, wave per touched keyframe): L1Scoring::score of
+// the listed keyframes above minCommonWords = maxCommonWords * 0.8f
+// (KeyFrameDatabase.cc:124-149 / 259-284), in double; the score goes to the
+// keyframe's state and the keyframes the reference keeps (loop: score >=
+// minScore; reloc: all) are appended to the output.
+__global__ __launch_bounds__(kKT) void k_kfdb_score(const SlotDev *slots, const int32_t *ntouched, const int4 *listed,
+                                                    const uint32_t *words, const double *values, const uint32_t *qw_g,
+                                                    const double *qv_g, int nq, QueryDev qd, KState *state,
+                                                    Listed *list) {
+    extern __shared__ uint32_t qs[];   // the query's words (nq <= kQLds), else read from global
+    const bool staged = nq <= kQLds;
+    if (staged)
+        for (int i = threadIdx.x; i < nq; i += kKT) qs[i] = qw_g[i];
+    __syncthreads();
+    const uint32_t *qw = staged ? qs : qw_g;
+    const int n = *ntouched;
+    const int min_words = (int)((float)*qd.max_words * 0.8f);
+    const int lane = threadIdx.x & 63;
+    const int nw = gridDim.x * (kKT / 64);
+    for (int k = blockIdx.x * (kKT / 64) + (threadIdx.x >> 6); k < n; k += nw) {
+        const int4 L = listed[k];
+        if (L.x <= min_words) continue;   // not listed (0) or too few words
+        const int s = L.z;
+        const SlotDev sl = slots[s];
+        double acc = 0;
+        for (int c0 = 0; c0 < sl.n; c0 += 64) {
+            const int i = c0 + lane;
+            double term = 0;
+            bool hit = false;
+            if (i < sl.n) {
+                const int r = find_word(qw, nq, words[sl.off + i]);
+                if (r >= 0) {
+                    const double vi = qv_g[r], wi = values[sl.off + i];
+                    term = __dsub_rn(__dsub_rn(fabs(__dsub_rn(vi, wi)), fabs(vi)), fabs(wi));
+                    hit = true;
+                }
+            }
+            // add the terms in ascending word order (the keyframe's words are sorted)
+            for (uint64_t b = __ballot(hit); b; b &= b - 1) {
+                const int j = (int)__builtin_ctzll(b);
+                const uint64_t bits =
+                    (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)__double_as_longlong(term), j) |
+                    ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(
+                         (int)(uint32_t)((uint64_t)__double_as_longlong(term) >> 32), j)
+                     << 32);
+                acc = __dadd_rn(acc, __longlong_as_double((long long)bits));
+            }
+        }
+        if (lane != 0) continue;
+        const float si = (float)(-acc / 2.0);
+        if (qd.reloc) state[s].reloc_score = si; else state[s].loop_score = si;
+        qd.rec[s].z = __float_as_int(si);
+        if (qd.reloc || si >= qd.min_score) {
+            const int at = atomicAdd(qd.max_words + 1, 1);
+            if (at < qd.list_cap) list[at] = Listed{(uint32_t)L.y, s, si};
         }
     }
-    if (lane == 0) score[li] = -acc / 2.0;
+}
+
+// New slots: a re-added keyframe keeps its query state (the reference's
+// KeyFrame object keeps its members), a new one starts at zero.
+__global__ void k_kfdb_seed(KState *state, int first, int count, const int32_t *src) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const int p = src[i];
+    state[first + i] = p >= 0 ? state[p] : KState{0, 0, 0, 0, 0.f, 0.f};
+}
+
+__global__ void k_kfdb_gather(const KState *state, const int32_t *slots, int n, KState *out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = state[slots[i]];
 }
 
 }  // namespace
@@ -127,11 +334,6 @@ __global__ __launch_bounds__(kKT) void k_kfdb_score(const SlotDev *slots, const 
 using namespace orbx;
 
 namespace {
-struct KFState {
-    uint64_t loop_query = 0, reloc_query = 0;   // KeyFrame.cc:41
-    int loop_words = 0, reloc_words = 0;
-    float loop_score = 0, reloc_score = 0;      // uninitialised in the reference
-};
 struct Slot {
     uint64_t id;
     int64_t off;
@@ -146,12 +348,26 @@ struct orbx_kfdb {
     hipStream_t st = nullptr;
     std::vector<Slot> slots;                      // add order
     std::unordered_map<uint64_t, int> live;       // id -> alive slot
-    std::unordered_map<uint64_t, KFState> state;  // persists across erase / re-add
+    std::unordered_map<uint64_t, int> last_slot;  // id -> its newest slot (its query state), erased or not
+    std::vector<int32_t> seed_src;                // per slot not yet on the device: slot whose state it inherits, or -1
     std::vector<uint32_t> h_words;                // host mirror of the arena (compaction)
     std::vector<double> h_values;
     uint32_t *d_words = nullptr;
     double *d_values = nullptr;
     SlotDev *d_slots = nullptr;
+    KState *d_state = nullptr;
+    int32_t *d_qcnt = nullptr, *d_touched = nullptr;   // per-slot query scratch
+    uint32_t *d_qfirst = nullptr;
+    // the device inverted file over slots [0, csr_ns): postings by word id
+    uint32_t *d_csr_off = nullptr, *d_csr_cnt = nullptr;
+    int32_t *d_csr_slot = nullptr;
+    uint32_t csr_V = 0;
+    int csr_ns = 0;
+    int64_t csr_cap_post = 0, csr_cap_V = 0;
+    uint32_t max_word = 0;
+    int4 *d_rec = nullptr;                        // per slot: what the last query met (QueryDev::rec)
+    uint32_t stamp = 0;
+    std::unordered_set<uint64_t> loop_qids, reloc_qids;   // query ids used so far
     int64_t cap_words = 0, dev_words = 0;        // arena capacity / words on the device
     int cap_slots = 0, dev_slots = 0;             // slot table capacity / rows on the device
     bool slots_dirty = false;
@@ -159,8 +375,10 @@ struct orbx_kfdb {
 
 namespace {
 
+constexpr int kListCap = 1024;   // scored keyframes brought back with the first copy
+
 int kfdb_sync(orbx_kfdb *db) {
-    // grow-and-upload the arena tail and the slot table
+    // grow-and-upload the arena tail and the slot table; seed new slots' state
     const int64_t need_w = (int64_t)db->h_words.size();
     if (need_w > db->cap_words) {
         const int64_t cap = std::max<int64_t>(need_w * 2, 1 << 16);
@@ -194,22 +412,98 @@ int kfdb_sync(orbx_kfdb *db) {
     if (ns > db->cap_slots) {
         const int cap = std::max(ns * 2, 1024);
         SlotDev *d = nullptr;
-        if (hipMalloc(reinterpret_cast<void **>(&d), sizeof(SlotDev) * cap) != hipSuccess) return ORBX_ENOMEM;
+        KState *k = nullptr;
+        if (hipMalloc(reinterpret_cast<void **>(&d), sizeof(SlotDev) * cap) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void **>(&k), sizeof(KState) * cap) != hipSuccess)
+            return ORBX_ENOMEM;
+        if (db->dev_slots &&
+            hipMemcpyAsync(k, db->d_state, sizeof(KState) * db->dev_slots, hipMemcpyDeviceToDevice, db->st) != hipSuccess)
+            return ORBX_EIO;
         (void)hipStreamSynchronize(db->st);
         if (db->d_slots) (void)hipFree(db->d_slots);
+        if (db->d_state) (void)hipFree(db->d_state);
+        for (void *x : {(void *)db->d_qcnt, (void *)db->d_qfirst, (void *)db->d_touched, (void *)db->d_rec})
+            if (x) (void)hipFree(x);
         db->d_slots = d;
+        db->d_state = k;
+        db->d_qcnt = db->d_touched = nullptr;
+        db->d_qfirst = nullptr;
+        db->d_rec = nullptr;
+        if (hipMalloc(reinterpret_cast<void **>(&db->d_rec), sizeof(int4) * (size_t)cap) != hipSuccess ||
+            hipMemsetAsync(db->d_rec, 0, sizeof(int4) * (size_t)cap, db->st) != hipSuccess)
+            return ORBX_ENOMEM;
+        if (hipMalloc(reinterpret_cast<void **>(&db->d_qcnt), 4 * (size_t)cap) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void **>(&db->d_qfirst), 4 * (size_t)cap) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void **>(&db->d_touched), 4 * (size_t)cap) != hipSuccess)
+            return ORBX_ENOMEM;
+        if (hipMemsetAsync(db->d_qcnt, 0, 4 * (size_t)cap, db->st) != hipSuccess ||
+            hipMemsetAsync(db->d_qfirst, 0xFF, 4 * (size_t)cap, db->st) != hipSuccess)
+            return ORBX_EIO;
         db->cap_slots = cap;
         db->slots_dirty = true;
     }
     if (db->slots_dirty || ns > db->dev_slots) {
         std::vector<SlotDev> t(ns);
         for (int i = 0; i < ns; ++i) t[i] = {db->slots[i].off, db->slots[i].n, db->slots[i].alive ? 1 : 0};
+        const int fresh = ns - db->dev_slots;
         if (ns && hipMemcpyAsync(db->d_slots, t.data(), sizeof(SlotDev) * ns, hipMemcpyHostToDevice, db->st) !=
                       hipSuccess)
             return ORBX_EIO;
-        (void)hipStreamSynchronize(db->st);   // (t is a host temporary)
+        int32_t *d_src = nullptr;
+        if (fresh > 0) {
+            if (hipMalloc(reinterpret_cast<void **>(&d_src), 4 * (size_t)fresh) != hipSuccess) return ORBX_ENOMEM;
+            if (hipMemcpyAsync(d_src, db->seed_src.data(), 4 * (size_t)fresh, hipMemcpyHostToDevice, db->st) !=
+                hipSuccess)
+                return ORBX_EIO;
+            hipLaunchKernelGGL(k_kfdb_seed, dim3((fresh + 255) / 256), dim3(256), 0, db->st, db->d_state,
+                               db->dev_slots, fresh, d_src);
+            if (hipGetLastError() != hipSuccess) return ORBX_EIO;
+        }
+        (void)hipStreamSynchronize(db->st);   // (t and seed_src are host temporaries)
+        if (d_src) (void)hipFree(d_src);
+        db->seed_src.clear();
         db->dev_slots = ns;
         db->slots_dirty = false;
+    }
+    // rebuild the inverted file once the brute-force delta has grown
+    if (ns - db->csr_ns > std::max(256, db->csr_ns / 8)) {
+        const int64_t V = (int64_t)db->max_word + 1, P = std::max<int64_t>(db->dev_words, 1);
+        if (V + 1 > db->csr_cap_V) {
+            const int64_t cap = (V + 1) * 2;
+            for (uint32_t **x : {&db->d_csr_off, &db->d_csr_cnt})
+                if (*x) { (void)hipStreamSynchronize(db->st); (void)hipFree(*x); *x = nullptr; }
+            if (hipMalloc(reinterpret_cast<void **>(&db->d_csr_off), 4 * cap) != hipSuccess ||
+                hipMalloc(reinterpret_cast<void **>(&db->d_csr_cnt), 4 * cap) != hipSuccess)
+                return ORBX_ENOMEM;
+            db->csr_cap_V = cap;
+        }
+        if (P > db->csr_cap_post) {
+            const int64_t cap = P * 2;
+            if (db->d_csr_slot) { (void)hipStreamSynchronize(db->st); (void)hipFree(db->d_csr_slot); }
+            if (hipMalloc(reinterpret_cast<void **>(&db->d_csr_slot), 4 * cap) != hipSuccess) return ORBX_ENOMEM;
+            db->csr_cap_post = cap;
+        }
+        const dim3 grid((ns + kKT / 64 - 1) / (kKT / 64));
+        if (hipMemsetAsync(db->d_csr_cnt, 0, 4 * (size_t)(V + 1), db->st) != hipSuccess) return ORBX_EIO;
+        hipLaunchKernelGGL(k_csr_count, grid, dim3(kKT), 0, db->st, db->d_slots, ns, db->d_words, db->d_csr_cnt);
+        size_t tmp = 0;
+        if (hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, db->d_csr_cnt, db->d_csr_off, (int)(V + 1), db->st) !=
+            hipSuccess)
+            return ORBX_EIO;
+        void *d_tmp = nullptr;
+        if (hipMalloc(&d_tmp, std::max<size_t>(tmp, 16)) != hipSuccess) return ORBX_ENOMEM;
+        const bool ok =
+            hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp, db->d_csr_cnt, db->d_csr_off, (int)(V + 1), db->st) ==
+                hipSuccess &&
+            hipMemsetAsync(db->d_csr_cnt, 0, 4 * (size_t)(V + 1), db->st) == hipSuccess;
+        if (ok)
+            hipLaunchKernelGGL(k_csr_fill, grid, dim3(kKT), 0, db->st, db->d_slots, ns, db->d_words, db->d_csr_off,
+                               db->d_csr_cnt, db->d_csr_slot);
+        (void)hipStreamSynchronize(db->st);
+        (void)hipFree(d_tmp);
+        if (!ok || hipGetLastError() != hipSuccess) return ORBX_EIO;
+        db->csr_ns = ns;
+        db->csr_V = (uint32_t)V;
     }
     return ORBX_OK;
 }
@@ -251,124 +545,147 @@ int detect(orbx_kfdb *db, bool reloc, uint64_t qid, const uint32_t *words, const
     if (!db->st && hipStreamCreateWithFlags(&db->st, hipStreamNonBlocking) != hipSuccess) return ORBX_EIO;
     int rc = kfdb_sync(db);
     if (rc) return rc;
-    // pass 1: shared-word counts and first shared word of every keyframe
+    // connected keyframes the walk can meet: their alive slots, ascending
+    std::vector<int32_t> conn;
+    if (!reloc)
+        for (int i = 0; i < n_connected; ++i) {
+            auto it = db->live.find(connected[i]);
+            if (it != db->live.end()) conn.push_back(it->second);
+        }
+    std::sort(conn.begin(), conn.end());
+    conn.erase(std::unique(conn.begin(), conn.end()), conn.end());
     Layout L;
-    const size_t o_qw = L.add(4 * (size_t)n), o_qv = L.add(8 * (size_t)n), o_cnt = L.add(8 * (size_t)ns);
-    const size_t o_list = L.add(4 * (size_t)ns), o_sc = L.add(8 * (size_t)ns);
+    const size_t o_qw = L.add(4 * (size_t)n), o_qv = L.add(8 * (size_t)n), o_conn = L.add(4 * (conn.size() + 1));
+    const size_t in_bytes = L.size;
+    const size_t o_mw = L.add(16), o_list = L.add(sizeof(Listed) * kListCap);   // brought back together
+    const size_t o_lst = L.add(16 * (size_t)ns), o_rec = L.add(sizeof(int4) * (size_t)ns);
+    const bool repeated = !(reloc ? db->reloc_qids : db->loop_qids).insert(qid).second;
+    if (++db->stamp == 0) ++db->stamp;   // (0: never written)
     CallWs &ws = call_ws(db->device);
     std::lock_guard<std::mutex> wl(ws.mu);
     rc = ws_reserve(ws, L.size);
     if (rc) return rc;
     put(ws, o_qw, words, 4 * (size_t)n);
     put(ws, o_qv, values, 8 * (size_t)n);
+    put(ws, o_conn, conn.data(), 4 * conn.size());
     uint8_t *D = ws.dev;
+    QueryDev qd;
+    qd.qid = qid;
+    qd.reloc = reloc;
+    qd.nconn = (int)conn.size();
+    qd.min_score = minScore;
+    qd.max_words = at<int32_t>(D, o_mw);   // [0] maxCommonWords, [1] kept, [2] touched
+    qd.list_cap = kListCap;
+    qd.stamp = db->stamp;
+    qd.rec = db->d_rec;
+    TouchDev t;
+    t.csr_off = db->d_csr_off; t.csr_slot = db->d_csr_slot; t.V = db->csr_ns ? db->csr_V : 0;
+    t.delta0 = db->csr_ns; t.nslots = ns;
+    t.qcnt = db->d_qcnt; t.qfirst = db->d_qfirst; t.touched = db->d_touched; t.ntouched = qd.max_words + 2;
+    // pass 1: the query words' posting lists + the delta keyframes; pass 2:
+    // state update and the walk's list; pass 3: scores above minCommonWords
+    const size_t qlds = n <= kQLds ? 4 * (size_t)n : 0;
+    const int items = n + (ns - db->csr_ns);
     if (hipStreamSynchronize(db->st) != hipSuccess ||
-        hipMemcpyAsync(D, ws.host, o_cnt, hipMemcpyHostToDevice, ws.st) != hipSuccess)
+        hipMemcpyAsync(D, ws.host, in_bytes, hipMemcpyHostToDevice, ws.st) != hipSuccess ||
+        hipMemsetAsync(D + o_mw, 0, 16, ws.st) != hipSuccess)
         return ORBX_EIO;
-    hipLaunchKernelGGL(k_kfdb_count, dim3((ns + kKT / 64 - 1) / (kKT / 64)), dim3(kKT), 0, ws.st, db->d_slots, ns,
-                       db->d_words, at<uint32_t>(D, o_qw), n, at<int2>(D, o_cnt));
+    hipLaunchKernelGGL(k_kfdb_touch, dim3(std::min(1024, (items + 3) / 4)), dim3(kKT), qlds, ws.st, db->d_slots,
+                       db->d_words, at<uint32_t>(D, o_qw), n, t);
+    hipLaunchKernelGGL(k_kfdb_list, dim3(std::min(256, (ns + kKT - 1) / kKT)), dim3(kKT), 0, ws.st, t,
+                       at<int32_t>(D, o_conn), qd, db->d_state, at<int4>(D, o_lst));
+    // few keyframes pass minCommonWords: a small persistent grid, each block
+    // with the query words in LDS
+    hipLaunchKernelGGL(k_kfdb_score, dim3(std::min(64, (ns + 3) / 4)), dim3(kKT), qlds, ws.st, db->d_slots,
+                       t.ntouched, at<int4>(D, o_lst), db->d_words, db->d_values, at<uint32_t>(D, o_qw),
+                       at<double>(D, o_qv), n, qd, db->d_state, at<Listed>(D, o_list));
     if (hipGetLastError() != hipSuccess ||
-        hipMemcpyAsync(ws.host + o_cnt, D + o_cnt, 8 * (size_t)ns, hipMemcpyDeviceToHost, ws.st) != hipSuccess ||
+        hipMemcpyAsync(ws.host + o_mw, D + o_mw, o_lst - o_mw, hipMemcpyDeviceToHost, ws.st) != hipSuccess ||
+        hipMemcpyAsync(ws.host + o_rec, db->d_rec, sizeof(int4) * (size_t)ns, hipMemcpyDeviceToHost, ws.st) !=
+            hipSuccess ||
         hipStreamSynchronize(ws.st) != hipSuccess)
         return ORBX_EIO;
-    const int2 *cnt = at<int2>(ws.host, o_cnt);
-    // the inverted-file walk's visiting order: (first shared query word, add order)
-    std::vector<int> met;
-    for (int s = 0; s < ns; ++s)
-        if (cnt[s].x > 0) met.push_back(s);
-    std::stable_sort(met.begin(), met.end(), [&](int a, int b) { return cnt[a].y < cnt[b].y; });
-    std::set<uint64_t> conn;
-    if (!reloc) conn.insert(connected, connected + n_connected);
-    std::vector<int> sharing;   // slots in lKFsSharingWords order
-    for (int s : met) {
-        KFState &k = db->state[db->slots[s].id];
-        const int c = cnt[s].x;
-        if (!reloc) {
-            // the walk meets the keyframe c times: the first meeting resets the
-            // count (unless already met by this query id) and lists it unless
-            // connected; a connected keyframe is reset at every meeting
-            if (k.loop_query != qid) {
-                if (!conn.count(db->slots[s].id)) {
-                    k.loop_query = qid;
-                    k.loop_words = c;
-                    sharing.push_back(s);
-                } else {
-                    k.loop_words = 1;
-                }
-            } else {
-                k.loop_words += c;
-            }
-        } else {
-            if (k.reloc_query != qid) {
-                k.reloc_query = qid;
-                k.reloc_words = c;
-                sharing.push_back(s);
-            } else {
-                k.reloc_words += c;
-            }
-        }
-    }
-    if (sharing.empty()) return ORBX_OK;
-    int maxCommonWords = 0;
-    for (int s : sharing) {
-        const KFState &k = db->state[db->slots[s].id];
-        maxCommonWords = std::max(maxCommonWords, reloc ? k.reloc_words : k.loop_words);
-    }
-    const int minCommonWords = maxCommonWords * 0.8f;
-    // pass 2: L1 scores of the keyframes above minCommonWords
-    std::vector<int> to_score;
-    for (int s : sharing) {
-        const KFState &k = db->state[db->slots[s].id];
-        if ((reloc ? k.reloc_words : k.loop_words) > minCommonWords) to_score.push_back(s);
-    }
-    const int nsc = (int)to_score.size();
-    put(ws, o_list, to_score.data(), 4 * (size_t)nsc);
-    if (hipMemcpyAsync(D + o_list, ws.host + o_list, 4 * (size_t)nsc, hipMemcpyHostToDevice, ws.st) != hipSuccess)
+    const int4 *rec = at<int4>(ws.host, o_rec);
+    int32_t mw[2];
+    get(ws, o_mw, mw, 8);
+    const int nsc = mw[1];
+    if (nsc > kListCap &&
+        (hipMemcpyAsync(ws.host + o_list, D + o_list, sizeof(Listed) * (size_t)nsc, hipMemcpyDeviceToHost, ws.st) !=
+             hipSuccess ||
+         hipStreamSynchronize(ws.st) != hipSuccess))
         return ORBX_EIO;
-    hipLaunchKernelGGL(k_kfdb_score, dim3((nsc + kKT / 64 - 1) / (kKT / 64)), dim3(kKT), 0, ws.st, db->d_slots,
-                       at<int32_t>(D, o_list), nsc, db->d_words, db->d_values, at<uint32_t>(D, o_qw),
-                       at<double>(D, o_qv), n, at<double>(D, o_sc));
-    if (hipGetLastError() != hipSuccess ||
-        hipMemcpyAsync(ws.host + o_sc, D + o_sc, 8 * (size_t)nsc, hipMemcpyDeviceToHost, ws.st) != hipSuccess ||
-        hipStreamSynchronize(ws.st) != hipSuccess)
-        return ORBX_EIO;
-    const double *sc = at<double>(ws.host, o_sc);
-    std::vector<std::pair<float, int>> scored;
+    if (nsc == 0) return ORBX_OK;
+    // the kept keyframes in the walk's order: (first shared word, add order)
+    std::vector<Listed> scored(at<Listed>(ws.host, o_list), at<Listed>(ws.host, o_list) + nsc);
+    std::sort(scored.begin(), scored.end(), [](const Listed &a, const Listed &b) {
+        return a.first != b.first ? a.first < b.first : a.slot < b.slot;
+    });
+    const int minCommonWords = mw[0] * 0.8f;
+    // covisible neighbours (KeyFrameDatabase.cc:151-185 / 287-318).  The
+    // state the accumulation reads came back with the query for every
+    // keyframe this query met; one that it did not meet matches the query id
+    // only if an earlier query used the same id -- then it is gathered.
+    struct NState { bool match; int words; float score; };
+    std::vector<uint64_t> nid;
+    std::vector<int> nfirst(nsc + 1, 0);
+    std::vector<NState> nst;
+    std::vector<int32_t> gslot;
+    std::vector<int> gpos;
+    uint64_t neigh[64];
     for (int i = 0; i < nsc; ++i) {
-        KFState &k = db->state[db->slots[to_score[i]].id];
-        const float si = (float)sc[i];
-        if (reloc) {
-            k.reloc_score = si;
-            scored.emplace_back(si, to_score[i]);
-        } else {
-            k.loop_score = si;
-            if (si >= minScore) scored.emplace_back(si, to_score[i]);
+        const int nn = std::min(covis(ctx, db->slots[scored[i].slot].id, neigh, 10), 10);
+        for (int t = 0; t < nn; ++t) {
+            auto it = db->last_slot.find(neigh[t]);
+            const int sl = it == db->last_slot.end() ? -1 : it->second;   // never in the database: no state
+            NState x{false, 0, 0.f};
+            if (sl >= 0 && (uint32_t)rec[sl].x == db->stamp) {
+                float sc;
+                std::memcpy(&sc, &rec[sl].z, 4);
+                x = NState{rec[sl].w != 0, rec[sl].y, sc};
+            } else if (sl >= 0 && repeated) {
+                gslot.push_back(sl);
+                gpos.push_back((int)nst.size());
+            }
+            nid.push_back(neigh[t]);
+            nst.push_back(x);
+        }
+        nfirst[i + 1] = (int)nid.size();
+    }
+    if (!gslot.empty()) {
+        std::vector<KState> gst(gslot.size());
+        Layout G;
+        const size_t o_gs = G.add(4 * gslot.size()), o_go = G.add(sizeof(KState) * gslot.size());
+        rc = ws_reserve(ws, G.size);
+        if (rc) return rc;
+        D = ws.dev;
+        put(ws, o_gs, gslot.data(), 4 * gslot.size());
+        if (hipMemcpyAsync(D + o_gs, ws.host + o_gs, 4 * gslot.size(), hipMemcpyHostToDevice, ws.st) != hipSuccess)
+            return ORBX_EIO;
+        hipLaunchKernelGGL(k_kfdb_gather, dim3(((int)gslot.size() + 255) / 256), dim3(256), 0, ws.st, db->d_state,
+                           at<int32_t>(D, o_gs), (int)gslot.size(), at<KState>(D, o_go));
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpyAsync(ws.host + o_go, D + o_go, sizeof(KState) * gslot.size(), hipMemcpyDeviceToHost, ws.st) !=
+                hipSuccess ||
+            hipStreamSynchronize(ws.st) != hipSuccess)
+            return ORBX_EIO;
+        get(ws, o_go, gst.data(), sizeof(KState) * gslot.size());
+        for (size_t g = 0; g < gslot.size(); ++g) {
+            const KState &k = gst[g];
+            nst[gpos[g]] = reloc ? NState{k.reloc_query == qid, k.reloc_words, k.reloc_score}
+                                 : NState{k.loop_query == qid, k.loop_words, k.loop_score};
         }
     }
-    if (scored.empty()) return ORBX_OK;
-    // covisibility accumulation (KeyFrameDatabase.cc:151-185 / 287-318)
     std::vector<std::pair<float, uint64_t>> acc;
     float bestAccScore = reloc ? 0 : minScore;
-    uint64_t neigh[64];
-    for (auto &sm : scored) {
-        const uint64_t kid = db->slots[sm.second].id;
-        const int nn = std::min(covis(ctx, kid, neigh, 10), 10);
-        float bestScore = sm.first, accScore = sm.first;
+    for (int i = 0; i < nsc; ++i) {
+        const uint64_t kid = db->slots[scored[i].slot].id;
+        float bestScore = scored[i].score, accScore = scored[i].score;
         uint64_t best = kid;
-        for (int t = 0; t < nn; ++t) {
-            auto it = db->state.find(neigh[t]);
-            if (it == db->state.end()) continue;   // never in the database: no query state
-            const KFState &k2 = it->second;
-            if (!reloc) {
-                if (k2.loop_query == qid && k2.loop_words > minCommonWords) {
-                    accScore += k2.loop_score;
-                    if (k2.loop_score > bestScore) { best = neigh[t]; bestScore = k2.loop_score; }
-                }
-            } else {
-                if (k2.reloc_query != qid) continue;
-                accScore += k2.reloc_score;
-                if (k2.reloc_score > bestScore) { best = neigh[t]; bestScore = k2.reloc_score; }
-            }
+        for (int t = nfirst[i]; t < nfirst[i + 1]; ++t) {
+            const NState &k2 = nst[t];
+            if (!k2.match || (!reloc && k2.words <= minCommonWords)) continue;
+            accScore += k2.score;
+            if (k2.score > bestScore) { best = nid[t]; bestScore = k2.score; }
         }
         acc.emplace_back(accScore, best);
         if (accScore > bestAccScore) bestAccScore = accScore;
@@ -406,6 +723,10 @@ void orbx_kfdb_destroy(orbx_kfdb *db) {
     if (db->d_words) (void)hipFree(db->d_words);
     if (db->d_values) (void)hipFree(db->d_values);
     if (db->d_slots) (void)hipFree(db->d_slots);
+    if (db->d_state) (void)hipFree(db->d_state);
+    for (void *x : {(void *)db->d_qcnt, (void *)db->d_qfirst, (void *)db->d_touched, (void *)db->d_rec, (void *)db->d_csr_off,
+                    (void *)db->d_csr_cnt, (void *)db->d_csr_slot})
+        if (x) (void)hipFree(x);
     if (db->st) (void)hipStreamDestroy(db->st);
     delete db;
 }
@@ -415,11 +736,19 @@ int orbx_kfdb_add(orbx_kfdb *db, uint64_t kf_id, const uint32_t *words, const do
     std::lock_guard<std::mutex> lock(db->mu);
     if (db->live.count(kf_id)) return ORBX_EINVAL;   // the reference would list it twice per word
     Slot s{kf_id, (int64_t)db->h_words.size(), n, true};
+    if (n) db->max_word = std::max(db->max_word, words[n - 1]);
     db->h_words.insert(db->h_words.end(), words, words + n);
     db->h_values.insert(db->h_values.end(), values, values + n);
-    db->live[kf_id] = (int)db->slots.size();
+    const int slot = (int)db->slots.size();
+    // a re-added keyframe keeps its query state: the state of its previous
+    // slot, or of that slot's own source while it is not on the device yet
+    auto prev = db->last_slot.find(kf_id);
+    int src = prev == db->last_slot.end() ? -1 : prev->second;
+    if (src >= db->dev_slots) src = db->seed_src[src - db->dev_slots];
+    db->seed_src.push_back(src);
+    db->live[kf_id] = slot;
+    db->last_slot[kf_id] = slot;
     db->slots.push_back(s);
-    db->state.emplace(kf_id, KFState());
     return ORBX_OK;
 }
 

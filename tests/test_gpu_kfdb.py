@@ -60,3 +60,40 @@ def test_kfdb_add_rejects_duplicates():
     db.erase(7)
     db.add(7, np.array([2], np.uint32), np.array([1.0]))
     assert db.size() == 1
+
+
+def test_kfdb_state_across_readd_chains(oracle_mod):
+    """Device-resident query state: keyframes queried, then erased and re-added
+    twice with no query in between (the new slots inherit the state through a
+    slot that never reached the device), then queried again with the same and
+    with new query ids -- candidate lists equal the oracle's."""
+    from orb_slam_2_ros_amd.synth_vocab import make_keyframe_bows
+    bows, covis = make_keyframe_bows(n_kf=300, n_words=20000, words_per_kf=300, seed=17, loop_every=40)
+    g, o = KeyFrameDatabase(), oracle_mod.KeyFrameDB(20000)
+    cv = lambda k: covis.get(k, [])   # noqa: E731
+    res_g, res_o = [], []
+
+    def both(kind, qid, i, ms=0.01):
+        w, v = bows[i]
+        if kind == "loop":
+            res_g.append(g.DetectLoopCandidates(qid, w, v, covis[i], ms, cv))
+            res_o.append(o.detect(False, qid, w, v, covis[i], ms, cv))
+        else:
+            res_g.append(g.DetectRelocalizationCandidates(qid, w, v, cv))
+            res_o.append(o.detect(True, qid, w, v, None, 0.0, cv))
+    for i in range(200):
+        g.add(i, *bows[i]); o.add(i, *bows[i])
+    for i in range(40, 200, 9):
+        both("loop", i, i)
+        both("reloc", 5000 + i, i)
+    for k in range(30, 90, 3):   # erase, re-add, erase, re-add: no query in between
+        for _ in range(2):
+            g.erase(k); o.erase(k)
+            g.add(k, *bows[k]); o.add(k, *bows[k])
+    for i in range(200, 300):
+        g.add(i, *bows[i]); o.add(i, *bows[i])
+    for i in range(45, 300, 7):
+        both("loop", i, i, 0.005)                  # some ids repeat earlier queries
+        both("reloc", 5000 + (i // 2) * 2, i)
+    assert res_g == res_o
+    assert sum(len(x) > 0 for x in res_o) > 20
