@@ -8,13 +8,16 @@
 // Device work per LM trial, all FP64:
 //   k_ba_errors        thread per edge: error, chi2, Huber rho (computeActiveErrors)
 //   k_ba_linearize     thread per edge: Jacobians and the edge's J^T W J / J^T W r blocks
-//   k_ba_ordered_sums  block per free camera: Hpp / bp (and the reduced right-hand side
-//                      bp - sum B Dinv bl) as sums over its edges in edge order, the
-//                      edge records staged through LDS by three waves while one adds
+//   k_ba_gather_rows / k_ba_stream_sums
+//                      Hpp / bp of each free camera (and the reduced right-hand side
+//                      bp - sum B Dinv bl) as sums over its edges in edge order: the
+//                      records gathered into list order, then a wave per camera adds
 //   k_ba_reduce        wave per point: Hll / bl, edge order
 //   k_ba_point         thread per point: (Hll + lambda I)^-1 and Dinv bl
 //   k_ba_point_edges   thread per edge: B Dinv and B Dinv bl
-//   k_ba_pairs(_map)   wave per camera pair: S_ij -= B_i Dinv B_j^T over shared points, point order
+//   k_ba_pair_terms    thread per (shared point, entry) of every camera pair: B_i Dinv B_j^T terms
+//   k_ba_pairs_sum     wave per camera pair: S_ij -= its terms in point order (pairs listed once
+//                      per set of active edges); k_ba_pairs merge walk for repeated observations
 //   k_ba_chol_lds      one workgroup: blocked dense Cholesky of the reduced camera system and
 //                      the solves (k_ba_chol beyond 128 unknowns)
 //   k_ba_backsub       thread per point: xl = Dinv (bl - sum_e B_e^T xp)
@@ -385,32 +388,23 @@ __global__ void k_ba_pairs(const int2 *pairs, int npairs, const int32_t *coffs, 
     S[(int64_t)(6 * i2 + c) * n + 6 * i1 + r] = acc;   // mirror (the solver reads the full matrix)
 }
 
-// The same blocks with the shared points found lane-parallel: a wave walks
-// camera i1's list 64 entries at a time and looks each point up in camera
-// i2's point -> list-position map (cmap, -1: not observed).  Each matched
-// lane copies its operands (B Dinv and B rows) into LDS at its rank, so one
-// global round trip serves the chunk; the 36 entry lanes then subtract the
-// shared points in ascending point order.  Needs each (camera, point)
-// observed at most once (checked on the host).
-__global__ __launch_bounds__(256) void k_ba_pairs_map(const int2 *pairs, int npairs, const int32_t *coffs,
-                                                      const int32_t *clist, const int32_t *epoint, const int32_t *cmap,
-                                                      int npt, const EdgeOut *eo, const double *bdinv,
-                                                      const double *Hpp, double lambda, int nf, double *S) {
-    // per wave: the chunk's matched B Dinv (6x3) and B (hpl, 6x3) rows
-    __shared__ double ops[4][64][36];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int pi = blockIdx.x * (blockDim.x / 64) + w;
+// The shared points of each camera pair as (edge of i1, edge of i2) in
+// ascending point order, found lane-parallel: a wave walks camera i1's list
+// 64 entries at a time and looks each point up in camera i2's point ->
+// list-position map (cmap, -1: not observed; needs each (camera, point)
+// observed at most once, checked on the host).  A count pass
+// (moffs == nullptr: counts out) and a fill pass at the scanned offsets.
+// Built once per set of active edges; the per-trial Schur pass then streams
+// the list with independent loads.
+__global__ __launch_bounds__(256) void k_ba_pair_matches(const int2 *pairs, int npairs, const int32_t *coffs,
+                                                         const int32_t *clist, const int32_t *epoint,
+                                                         const int32_t *cmap, int npt, const int32_t *moffs,
+                                                         int32_t *counts, int2 *mlist) {
+    const int lane = threadIdx.x & 63, pi = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (pi >= npairs) return;
     const int i1 = pairs[pi].x, i2 = pairs[pi].y;
-    const int r = min(lane, 35) / 6, c = min(lane, 35) % 6;
-    double acc = 0;
-    if (i1 == i2) {
-        acc = Hpp[36 * (int64_t)i1 + min(lane, 35)];
-        if (r == c) acc = acc + lambda;
-    }
     const int32_t *map2 = cmap + (int64_t)i2 * npt;
-    constexpr int kEo = sizeof(EdgeOut) / sizeof(double);
-    double (*op)[36] = ops[w];
+    int at = moffs ? moffs[pi] : 0;
     for (int a0 = coffs[i1]; a0 < coffs[i1 + 1]; a0 += 64) {
         const int a = a0 + lane;
         int e1 = -1, e2 = -1;
@@ -420,119 +414,107 @@ __global__ __launch_bounds__(256) void k_ba_pairs_map(const int2 *pairs, int npa
             if (pos >= 0) e2 = clist[pos];
         }
         const uint64_t m = __ballot(e2 >= 0);
-        const int nm = __popcll(m);
-        if (e2 >= 0) {   // this lane's match goes to slot = its rank (point order)
-            const int slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            const double *bd = bdinv + 18 * (int64_t)e1;
-            const double *hp = reinterpret_cast<const double *>(eo) + (int64_t)e2 * kEo + 45;   // EdgeOut::hpl
-#pragma unroll
-            for (int k = 0; k < 18; ++k) { op[slot][k] = bd[k]; op[slot][18 + k] = hp[k]; }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        // S_rc -= sum_k BDinv_1[r][k] B_2[c][k], shared points in ascending order
-        for (int t = 0; t < nm; ++t) {
-            double sj = 0;
-            for (int k = 0; k < 3; ++k) sj = sj + op[t][3 * r + k] * op[t][18 + 3 * c + k];
-            acc = acc - sj;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
+        if (moffs && e2 >= 0)
+            mlist[at + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+                make_int2(e1, e2);
+        at += __popcll(m);
     }
+    if (!moffs && lane == 0) counts[pi] = at;
+}
+
+// S_{i1 i2} (+ lambda I on the diagonal blocks) -= sum over the pair's shared
+// points, in point order, of (B Dinv)_{i1} B_{i2}^T, in two passes:
+//  k_ba_pair_terms: every (shared point, block entry) term of every pair,
+//    thread per term (the 3-term dot product in the sequential order);
+//  k_ba_pairs_sum: wave per pair, lane = block entry, subtracts its terms in
+//    point order, streaming them with the loads 16 deep.
+// Only the subtractions are sequential, so the longest pair (a camera with
+// itself: all its points) costs a chain of dependent adds, not of loads.
+__global__ void k_ba_pair_terms(const int2 *mlist, int64_t nterms, const EdgeOut *eo, const double *bdinv,
+                                double *terms) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= nterms) return;
+    const int64_t t = idx / 36;
+    const int e = (int)(idx - t * 36), r = e / 6, c = e % 6;
+    const int2 mt = mlist[t];
+    const double *bd = bdinv + 18 * (int64_t)mt.x + 3 * r;
+    const double *hp = eo[mt.y].hpl + 3 * c;
+    double sj = 0;
+    for (int k = 0; k < 3; ++k) sj = sj + bd[k] * hp[k];
+    terms[idx] = sj;
+}
+
+__global__ __launch_bounds__(64) void k_ba_pairs_sum(const int2 *pairs, const int32_t *moffs, const double *terms,
+                                                     const double *Hpp, double lambda, int nf, double *S) {
+    const int pi = blockIdx.x, lane = threadIdx.x;
     if (lane >= 36) return;
+    const int i1 = pairs[pi].x, i2 = pairs[pi].y, r = lane / 6, c = lane % 6;
+    double acc = 0;
+    if (i1 == i2) {
+        acc = Hpp[36 * (int64_t)i1 + lane];
+        if (r == c) acc = acc + lambda;
+    }
+    const double *tp = terms + lane;
+    int t = moffs[pi];
+    const int te = moffs[pi + 1];
+    for (; t + 16 <= te; t += 16) {
+        double x[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) x[q] = tp[36 * (int64_t)(t + q)];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc = acc - x[q];
+    }
+    for (; t < te; ++t) acc = acc - tp[36 * (int64_t)t];
     const int n = 6 * nf;
     S[(int64_t)(6 * i1 + r) * n + 6 * i2 + c] = acc;
     S[(int64_t)(6 * i2 + c) * n + 6 * i1 + r] = acc;   // mirror (the solver reads the full matrix)
 }
 
-// Ordered sums per vertex with the edge records staged through LDS: out[v][f]
-// = sum over t in [offs[v], offs[v+1]) of rec[list[t]][fo[f]] (edges with
-// pred[e] == 0 skipped), each field summed one edge at a time in list order
-// -- the order the sequential restatement uses.  One block per vertex: waves
-// 1..3 stage the next chunk of records while wave 0 (lane = field) adds the
-// current one, so the adds wait on LDS, not on a global round trip per edge.
+// Ordered sums per vertex, out[v][f] = sum over t in [offs[v], offs[v+1]) of
+// rec[list[t]][field f] in list order (edges with pred[e] == 0 add nothing),
+// in two passes:
+//  k_ba_gather_rows: thread per (list entry, field) copies the records into
+//    list order (+0.0 for a skipped edge: the running sum starts at +0.0 and
+//    never becomes -0.0 under round-to-nearest, so adding +0.0 leaves it as it
+//    is);
+//  k_ba_stream_sums: wave per vertex, lane = field, adds its column in list
+//    order with the loads 16 deep -- a chain of dependent adds, no dependent
+//    loads.
 // minus != nullptr: out = minus - sum (the reduced right-hand side).
-constexpr int kSumChunk = 128;
-// NF fields per record; layout 1: EdgeOut's hpp (36) then bp (6), layout 0:
-// record fields 0..NF-1.
+// NF fields per record; LAYOUT 1: EdgeOut's hpp (36) then bp (6), 0: record
+// fields 0..NF-1.
 template <int NF, int LAYOUT>
-__global__ __launch_bounds__(256) void k_ba_ordered_sums(const double *rec, int stride, const int32_t *offs,
-                                                         const int32_t *list, const uint8_t *pred, const double *minus,
-                                                         double *out_a, int na, double *out_b) {
-    extern __shared__ double sbuf[];   // 2 x kSumChunk x NF, 4 x 64 edge ids, 2 x kSumChunk flags
-    int32_t *ids = reinterpret_cast<int32_t *>(sbuf + 2 * kSumChunk * NF);
-    uint8_t *okf = reinterpret_cast<uint8_t *>(ids + 4 * 64);
-    const int v = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int t0 = offs[v], te = offs[v + 1];
-    const int nch = (te - t0 + kSumChunk - 1) / kSumChunk;
-    // a wave stages edges jw, jw + nwv, ... (at most 64) of chunk c: one id per
-    // lane, then the (edge, field) elements spread over the lanes, so a lane's
-    // loads are independent of each other
-    auto stage = [&](int c, int jw, int nwv) {
-        const int base = t0 + c * kSumChunk, cnt = min(kSumChunk, te - base);
-        double *b = sbuf + (c & 1) * kSumChunk * NF;
-        uint8_t *o = okf + (c & 1) * kSumChunk;
-        const int nj = cnt > jw ? (cnt - jw + nwv - 1) / nwv : 0;
-        int32_t *wid = ids + 64 * w;   // this wave's edge ids
-        if (lane < nj) {
-            const int eid = list[base + jw + lane * nwv];
-            wid[lane] = eid;
-            o[jw + lane * nwv] = pred ? pred[eid] : 1;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const int total = nj * NF;
-        for (int k0 = lane; k0 < total; k0 += 64 * 8) {   // 8 loads in flight per lane
-            double x[8];
-            int dst[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int k = k0 + 64 * q;
-                dst[q] = -1;
-                if (k < total) {
-                    const int jl = k / NF, f = k - jl * NF;
-                    const int off = LAYOUT == 1 && f >= 36 ? 63 + (f - 36) : f;   // EdgeOut::bp at 63
-                    x[q] = rec[(int64_t)wid[jl] * stride + off];
-                    dst[q] = (jw + jl * nwv) * NF + f;
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < 8; ++q)
-                if (dst[q] >= 0) b[dst[q]] = x[q];
-        }
-    };
-    if (nch > 0) stage(0, w, 4);
-    __syncthreads();
+__global__ void k_ba_gather_rows(const double *rec, int stride, const int32_t *list, int n, const uint8_t *pred,
+                                 double *out) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (int64_t)n * NF) return;
+    const int t = (int)(idx / NF), f = (int)(idx - (int64_t)t * NF);
+    const int e = list[t];
+    const int off = LAYOUT == 1 && f >= 36 ? 63 + (f - 36) : f;   // EdgeOut::bp at 63
+    out[idx] = (pred && !pred[e]) ? 0.0 : rec[(int64_t)e * stride + off];
+}
+
+template <int NF>
+__global__ __launch_bounds__(64) void k_ba_stream_sums(const double *rows, const int32_t *offs, const double *minus,
+                                                       double *out_a, int na, double *out_b) {
+    const int v = blockIdx.x, lane = threadIdx.x;
+    if (lane >= NF) return;
+    const double *col = rows + lane;
     double acc = 0;
-    for (int c = 0; c < nch; ++c) {
-        if (w > 0) {
-            if (c + 1 < nch) stage(c + 1, w - 1, 3);
-        } else if (lane < NF) {
-            const int cnt = min(kSumChunk, te - (t0 + c * kSumChunk));
-            const double *b = sbuf + (c & 1) * kSumChunk * NF;
-            const uint8_t *o = okf + (c & 1) * kSumChunk;
-            // 8 records' loads in flight, then their adds in order (a skipped
-            // edge leaves acc as it is)
-            int j = 0;
-            for (; j + 8 <= cnt; j += 8) {
-                double x[8];
-                uint8_t f[8];
+    int t = offs[v];
+    const int te = offs[v + 1];
+    for (; t + 16 <= te; t += 16) {
+        double x[16];
 #pragma unroll
-                for (int q = 0; q < 8; ++q) { f[q] = o[j + q]; x[q] = b[(j + q) * NF + lane]; }
+        for (int q = 0; q < 16; ++q) x[q] = col[(int64_t)(t + q) * NF];
 #pragma unroll
-                for (int q = 0; q < 8; ++q) acc = f[q] ? acc + x[q] : acc;
-            }
-            for (; j < cnt; ++j) acc = o[j] ? acc + b[j * NF + lane] : acc;
-        }
-        __syncthreads();
+        for (int q = 0; q < 16; ++q) acc = acc + x[q];
     }
-    if (w != 0 || lane >= NF) return;
+    for (; t < te; ++t) acc = acc + col[(int64_t)t * NF];
     if (lane < na) out_a[(int64_t)v * na + lane] = minus ? minus[(int64_t)v * na + lane] - acc : acc;
     else out_b[(int64_t)v * (NF - na) + lane - na] = acc;
 }
 
-inline size_t ordered_sums_lds(int nfld) { return 16 * kSumChunk * (size_t)nfld + 4 * 64 * 4 + 2 * kSumChunk; }
 
 
 // Dense Cholesky S = L L^T (lower, in place, column by column) and the two
@@ -607,35 +589,69 @@ __global__ __launch_bounds__(512) void k_ba_chol_lds(const double *S, int n, con
     const int ld = n + 1;
     double *dg = L + n * ld;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
-    for (int r = w; r < n; r += nw)
-        for (int c = lane; c <= r; c += 64) L[r * ld + c] = S[(int64_t)r * n + c];
+    {   // the lower triangle, 8 loads in flight per thread
+        const int tot = n * (n + 1) / 2;
+        for (int q0 = tid; q0 < tot; q0 += 512 * 8) {
+            double v[8];
+            int at[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int q = q0 + 512 * u;
+                at[u] = -1;
+                if (q < tot) {
+                    const int r = (int)((sqrt(8.0 * q + 1.0) - 1.0) * 0.5);   // row of packed index q
+                    const int rr = r + (q >= (r + 1) * (r + 2) / 2) - (q < r * (r + 1) / 2);
+                    const int c = q - rr * (rr + 1) / 2;
+                    v[u] = S[(int64_t)rr * n + c];
+                    at[u] = rr * ld + c;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (at[u] >= 0) L[at[u]] = v[u];
+        }
+    }
     if (tid == 0) bad = 0;
     __syncthreads();
     for (int k0 = 0; k0 < n; k0 += kPanel) {
         const int k1 = min(k0 + kPanel, n);
         if (w == 0) {
-            for (int k = k0; k < k1; ++k) {
-                const double d = L[k * ld + k];
+            // lane owns rows k0 + lane and k0 + 64 + lane; the panel's columns
+            // of those rows stay in registers until the panel is done
+            const int q0 = k0 + lane, q1 = k0 + 64 + lane;
+            double p0[kPanel], p1[kPanel];
+#pragma unroll
+            for (int m = 0; m < kPanel; ++m) {
+                p0[m] = (q0 < n && k0 + m < k1 && k0 + m <= q0) ? L[q0 * ld + k0 + m] : 0.0;
+                p1[m] = (q1 < n && k0 + m < k1) ? L[q1 * ld + k0 + m] : 0.0;
+            }
+#pragma unroll
+            for (int m = 0; m < kPanel; ++m) {
+                const int k = k0 + m;
+                if (k >= k1) break;
+                const double d = readlane_f64(p0[m], m);   // row k's diagonal entry (lane m)
                 if (!(d > 0)) {   // (uniform over the wave)
                     if (lane == 0) bad = 1;
                     break;
                 }
                 const double g = sqrt(d);
-                const int r0 = k + 1 + lane, r1 = k + 65 + lane;
-                const double a0 = r0 < n ? L[r0 * ld + k] / g : 0.0;
-                const double a1 = r1 < n ? L[r1 * ld + k] / g : 0.0;
                 if (lane == 0) dg[k] = g;
-                if (r0 < n) L[r0 * ld + k] = a0;
-                if (r1 < n) L[r1 * ld + k] = a1;
-                for (int j = k + 1; j < k1; ++j) {   // the panel's later columns
-                    const int t = j - k - 1;
-                    const double aj = t < 64 ? readlane_f64(a0, t) : readlane_f64(a1, t - 64);
-                    if (r0 >= j && r0 < n) L[r0 * ld + j] = L[r0 * ld + j] - a0 * aj;
-                    if (r1 >= j && r1 < n) L[r1 * ld + j] = L[r1 * ld + j] - a1 * aj;
+                // column k below the diagonal: rows > k of this lane
+                if (q0 > k) p0[m] = p0[m] / g;
+                p1[m] = p1[m] / g;   // (q1 > k always)
+#pragma unroll
+                for (int jm = m + 1; jm < kPanel; ++jm) {   // the panel's later columns
+                    if (k0 + jm >= k1) break;
+                    const double aj = readlane_f64(p0[m], jm);   // L(k0 + jm, k): row k0 + jm is lane jm's q0
+                    if (q0 >= k0 + jm) p0[jm] = p0[jm] - p0[m] * aj;
+                    p1[jm] = p1[jm] - p1[m] * aj;
                 }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+#pragma unroll
+            for (int m = 0; m < kPanel; ++m) {
+                if (k0 + m >= k1) break;
+                if (q0 < n && q0 > k0 + m) L[q0 * ld + k0 + m] = p0[m];
+                if (q1 < n) L[q1 * ld + k0 + m] = p1[m];
             }
         }
         __syncthreads();
@@ -824,6 +840,9 @@ public:
     int download(double *pts, std::vector<double> &chi2, std::vector<uint8_t> &front);
     ~BA() {
         if (buf_) (void)hipFree(buf_);
+        if (d_moffs) (void)hipFree(d_moffs);
+        if (d_mlist) (void)hipFree(d_mlist);
+        if (d_terms) (void)hipFree(d_terms);
         if (hbuf_) (void)hipHostFree(hbuf_);
     }
 
@@ -848,6 +867,12 @@ public:
     std::vector<uint8_t> act_;
     std::vector<int32_t> cv_offs_, cv_list_;   // all edges per free camera (reduce), edge order
     double *d_rho0 = nullptr;                  // rho[0] per edge, contiguous
+    int32_t *d_moffs = nullptr;                // camera pairs' shared-point lists (k_ba_pair_matches)
+    int2 *d_mlist = nullptr;
+    double *d_terms = nullptr;                 // 36 per shared point of each pair (k_ba_pair_terms)
+    double *d_rows = nullptr;                  // records gathered in list order (k_ba_gather_rows), 42 per edge
+    int nusable_ = 0;
+    int64_t mcap_ = 0, nmatch_ = 0;
     uint8_t *hbuf_ = nullptr;                  // pinned readbacks
     double *h_rho0 = nullptr, *h_x = nullptr, *h_b = nullptr, *h_hpp = nullptr, *h_hll = nullptr;
     int *h_ok = nullptr;
@@ -893,7 +918,7 @@ int BA::alloc() {
                          8 * ne * 6 + sizeof(EdgeOut) * ne + 4 * (nf + 1 + ne + np + 1 + ne + ne + nf + 1 + ne) +
                          sizeof(int2) * std::max(npairs, 1) + 8 * (36 * nf + 6 * nf + 9 * np + 3 * np + 9 * np +
                                                                    18 * ne + 6 * ne + n * n + n + n + 3 * np) +
-                         4 * nf * np + 8 * ne + 8 * 3 * np + 256 * 4;
+                         4 * nf * np + 8 * ne + 8 * 3 * np + 8 * 42 * ne + 256 * 5;
     if (hipMalloc(reinterpret_cast<void **>(&buf_), bytes) != hipSuccess) return ORBX_ENOMEM;
     uint8_t *p = buf_;
     d_pose = carve<Pose>(p, nc); d_pose_bk = carve<Pose>(p, nc);
@@ -914,6 +939,7 @@ int BA::alloc() {
     d_cmap = carve<int32_t>(p, nf * np);
     d_rho0 = carve<double>(p, ne);
     d_db = carve<double>(p, 3 * np);
+    d_rows = carve<double>(p, 42 * ne);
     if ((size_t)(p - buf_) > bytes) return ORBX_ENOMEM;
     {
         const size_t m = n + 3 * np;
@@ -962,7 +988,7 @@ void BA::set_active(const std::vector<uint8_t> &act) {
             const int e = g.plist[t];
             if (usable[e]) clist[fill[g.poses[g.edges[e].cam].free_idx]++] = e;
         }
-    // point -> list position per free camera, for k_ba_pairs_map
+    // point -> list position per free camera, for k_ba_pair_matches
     std::vector<int32_t> cmap((size_t)g.nf * g.npt, -1);
     use_map = true;
     for (int f = 0; f < g.nf && use_map; ++f)
@@ -975,14 +1001,47 @@ void BA::set_active(const std::vector<uint8_t> &act) {
     (void)hipMemcpyAsync(d_usable, usable.data(), g.ne, hipMemcpyHostToDevice, st_);
     (void)hipMemcpyAsync(d_coffs, coffs.data(), 4 * (g.nf + 1), hipMemcpyHostToDevice, st_);
     (void)hipMemcpyAsync(d_clist, clist.data(), 4 * clist.size(), hipMemcpyHostToDevice, st_);
+    nusable_ = coffs[g.nf];
     if (use_map && !cmap.empty())
         (void)hipMemcpyAsync(d_cmap, cmap.data(), 4 * cmap.size(), hipMemcpyHostToDevice, st_);
+    if (use_map && npairs > 0) {   // the pairs' shared-point lists: count, scan on the host, fill
+        if (!d_moffs && hipMalloc(reinterpret_cast<void **>(&d_moffs), 4 * (size_t)(npairs + 1)) != hipSuccess)
+            use_map = false;
+        std::vector<int32_t> cnt(npairs), offs(npairs + 1, 0);
+        if (use_map) {
+            hipLaunchKernelGGL(k_ba_pair_matches, dim3((npairs + 3) / 4), dim3(256), 0, st_, d_pairs, npairs, d_coffs,
+                               d_clist, d_epoint, d_cmap, g.npt, nullptr, d_moffs, nullptr);
+            if (hipMemcpyAsync(cnt.data(), d_moffs, 4 * (size_t)npairs, hipMemcpyDeviceToHost, st_) != hipSuccess ||
+                hipStreamSynchronize(st_) != hipSuccess)
+                use_map = false;
+        }
+        for (int k = 0; k < npairs && use_map; ++k) offs[k + 1] = offs[k] + cnt[k];
+        if (use_map && offs[npairs] > mcap_) {
+            for (void *x : {(void *)d_mlist, (void *)d_terms})
+                if (x) (void)hipFree(x);
+            d_mlist = nullptr;
+            d_terms = nullptr;
+            mcap_ = 0;
+            const size_t m = (size_t)std::max(offs[npairs], 1);
+            if (hipMalloc(reinterpret_cast<void **>(&d_mlist), sizeof(int2) * m) == hipSuccess &&
+                hipMalloc(reinterpret_cast<void **>(&d_terms), 36 * sizeof(double) * m) == hipSuccess)
+                mcap_ = (int64_t)m;
+            else
+                use_map = false;
+        }
+        nmatch_ = use_map ? offs[npairs] : 0;
+        if (use_map) {
+            (void)hipMemcpyAsync(d_moffs, offs.data(), 4 * (size_t)(npairs + 1), hipMemcpyHostToDevice, st_);
+            hipLaunchKernelGGL(k_ba_pair_matches, dim3((npairs + 3) / 4), dim3(256), 0, st_, d_pairs, npairs, d_coffs,
+                               d_clist, d_epoint, d_cmap, g.npt, d_moffs, nullptr, d_mlist);
+        }
+    }
     (void)hipStreamSynchronize(st_);
 }
 
 int BA::errors(bool robust, double *chi_sum) {
     const int ne = g_.ne;
-    if (ne) hipLaunchKernelGGL(k_ba_errors, dim3((ne + 255) / 256), dim3(256), 0, st_, d_pose, d_pts, d_edges, ne,
+    if (ne) hipLaunchKernelGGL(k_ba_errors, dim3((ne + 63) / 64), dim3(64), 0, st_, d_pose, d_pts, d_edges, ne,
                                d_active, robust ? 1 : 0, 0, d_err, d_chi2, d_rho, d_front, nullptr, nullptr);
     std::vector<double> rho(2 * (size_t)std::max(ne, 1));
     if (hipGetLastError() != hipSuccess ||
@@ -998,16 +1057,15 @@ int BA::errors(bool robust, double *chi_sum) {
 
 int BA::build() {
     const Graph &g = g_;
-    if (g.ne) hipLaunchKernelGGL(k_ba_linearize, dim3((g.ne + 255) / 256), dim3(256), 0, st_, d_pose, d_pts, d_edges,
+    if (g.ne) hipLaunchKernelGGL(k_ba_linearize, dim3((g.ne + 63) / 64), dim3(64), 0, st_, d_pose, d_pts, d_edges,
                                  g.ne, d_active, d_err, d_rho, d_eo);
     if (g.nf) {   // Hpp and bp of each free camera over all its edges, edge order
         constexpr int kEo = sizeof(EdgeOut) / sizeof(double);
-        const size_t lb = ordered_sums_lds(42);
-        if (lb > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void *>(k_ba_ordered_sums<42, 1>),
-                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb) != hipSuccess)
-            return ORBX_EIO;
-        hipLaunchKernelGGL((k_ba_ordered_sums<42, 1>), dim3(g.nf), dim3(256), lb, st_,
-                           reinterpret_cast<const double *>(d_eo), kEo, d_cvoffs, d_cvlist, d_active, nullptr, d_Hpp, 36,
+        const int nl = cv_offs_[g.nf];
+        if (nl)
+            hipLaunchKernelGGL((k_ba_gather_rows<42, 1>), dim3((unsigned)(((int64_t)nl * 42 + 255) / 256)), dim3(256), 0,
+                               st_, reinterpret_cast<const double *>(d_eo), kEo, d_cvlist, nl, d_active, d_rows);
+        hipLaunchKernelGGL((k_ba_stream_sums<42>), dim3(g.nf), dim3(64), 0, st_, d_rows, d_cvoffs, nullptr, d_Hpp, 36,
                            d_bp);
     }
     if (g.npt) hipLaunchKernelGGL(k_ba_reduce, dim3((g.npt + 3) / 4), dim3(256), 0, st_, d_eo, d_poffs, d_plist,
@@ -1040,19 +1098,27 @@ int BA::solve(double lambda, int *ok) {
         hipLaunchKernelGGL(k_ba_point, dim3((g.npt + 255) / 256), dim3(256), 0, st_, d_Hll, d_bl, g.npt, lambda, d_dinv,
                            d_db);
         if (g.ne)
-            hipLaunchKernelGGL(k_ba_point_edges, dim3((g.ne + 255) / 256), dim3(256), 0, st_, d_eo, d_epoint, d_usable,
+            hipLaunchKernelGGL(k_ba_point_edges, dim3((g.ne + 63) / 64), dim3(64), 0, st_, d_eo, d_epoint, d_usable,
                                g.ne, d_dinv, d_db, d_bdinv, d_bdb);
     }
     if (g.nf) {
-        if (use_map)
-            hipLaunchKernelGGL(k_ba_pairs_map, dim3((npairs + 3) / 4), dim3(256), 0, st_, d_pairs, npairs, d_coffs,
-                               d_clist, d_epoint, d_cmap, g.npt, d_eo, d_bdinv, d_Hpp, lambda, g.nf, d_S);
+        if (use_map) {
+            const int64_t nterms = 36 * nmatch_;
+            if (nterms)
+                hipLaunchKernelGGL(k_ba_pair_terms, dim3((unsigned)((nterms + 255) / 256)), dim3(256), 0, st_, d_mlist,
+                                   nterms, d_eo, d_bdinv, d_terms);
+            hipLaunchKernelGGL(k_ba_pairs_sum, dim3(npairs), dim3(64), 0, st_, d_pairs, d_moffs, d_terms, d_Hpp,
+                               lambda, g.nf, d_S);
+        }
         else
             hipLaunchKernelGGL(k_ba_pairs, dim3((npairs + 3) / 4), dim3(256), 0, st_, d_pairs, npairs, d_coffs,
                                d_clist, d_epoint, d_eo, d_bdinv, d_Hpp, lambda, g.nf, d_S);
         // bs = bp - sum over the camera's usable edges of B Dinv bl, edge order
-        hipLaunchKernelGGL((k_ba_ordered_sums<6, 0>), dim3(g.nf), dim3(256), ordered_sums_lds(6), st_, d_bdb, 6,
-                           d_coffs, d_clist, nullptr, d_bp, d_bs, 6, nullptr);
+        if (nusable_)
+            hipLaunchKernelGGL((k_ba_gather_rows<6, 0>), dim3((unsigned)(((int64_t)nusable_ * 6 + 255) / 256)),
+                               dim3(256), 0, st_, d_bdb, 6, d_clist, nusable_, nullptr, d_rows);
+        hipLaunchKernelGGL((k_ba_stream_sums<6>), dim3(g.nf), dim3(64), 0, st_, d_rows, d_coffs, d_bp, d_bs, 6,
+                           nullptr);
         // (blocks of camera pairs without a shared point stay as the memset left them)
         if (n <= kCholLds) {
             const int lb = 8 * (n * (n + 1) + n);
@@ -1064,7 +1130,7 @@ int BA::solve(double lambda, int *ok) {
             hipLaunchKernelGGL(k_ba_chol, dim3(1), dim3(1024), 0, st_, d_S, n, d_bs, d_x, d_ok);
         }
     }
-    if (g.npt) hipLaunchKernelGGL(k_ba_backsub, dim3((g.npt + 255) / 256), dim3(256), 0, st_, d_dinv, d_bl, g.npt,
+    if (g.npt) hipLaunchKernelGGL(k_ba_backsub, dim3((g.npt + 63) / 64), dim3(64), 0, st_, d_dinv, d_bl, g.npt,
                                   d_eo, d_poffs, d_plist, d_usable, d_edges, d_pose, d_x, d_x + n);
     int okv = 1;
     if (hipGetLastError() != hipSuccess ||
@@ -1097,7 +1163,7 @@ int BA::update() {
 
 int BA::errors_async(bool robust, const int *gate) {
     const int ne = g_.ne;
-    if (ne) hipLaunchKernelGGL(k_ba_errors, dim3((ne + 255) / 256), dim3(256), 0, st_, d_pose, d_pts, d_edges, ne,
+    if (ne) hipLaunchKernelGGL(k_ba_errors, dim3((ne + 63) / 64), dim3(64), 0, st_, d_pose, d_pts, d_edges, ne,
                                d_active, robust ? 1 : 0, 0, d_err, d_chi2, d_rho, d_front, d_rho0, gate);
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
 }
@@ -1112,19 +1178,27 @@ int BA::solve_async(double lambda) {
         hipLaunchKernelGGL(k_ba_point, dim3((g.npt + 255) / 256), dim3(256), 0, st_, d_Hll, d_bl, g.npt, lambda, d_dinv,
                            d_db);
         if (g.ne)
-            hipLaunchKernelGGL(k_ba_point_edges, dim3((g.ne + 255) / 256), dim3(256), 0, st_, d_eo, d_epoint, d_usable,
+            hipLaunchKernelGGL(k_ba_point_edges, dim3((g.ne + 63) / 64), dim3(64), 0, st_, d_eo, d_epoint, d_usable,
                                g.ne, d_dinv, d_db, d_bdinv, d_bdb);
     }
     if (g.nf) {
-        if (use_map)
-            hipLaunchKernelGGL(k_ba_pairs_map, dim3((npairs + 3) / 4), dim3(256), 0, st_, d_pairs, npairs, d_coffs,
-                               d_clist, d_epoint, d_cmap, g.npt, d_eo, d_bdinv, d_Hpp, lambda, g.nf, d_S);
+        if (use_map) {
+            const int64_t nterms = 36 * nmatch_;
+            if (nterms)
+                hipLaunchKernelGGL(k_ba_pair_terms, dim3((unsigned)((nterms + 255) / 256)), dim3(256), 0, st_, d_mlist,
+                                   nterms, d_eo, d_bdinv, d_terms);
+            hipLaunchKernelGGL(k_ba_pairs_sum, dim3(npairs), dim3(64), 0, st_, d_pairs, d_moffs, d_terms, d_Hpp,
+                               lambda, g.nf, d_S);
+        }
         else
             hipLaunchKernelGGL(k_ba_pairs, dim3((npairs + 3) / 4), dim3(256), 0, st_, d_pairs, npairs, d_coffs,
                                d_clist, d_epoint, d_eo, d_bdinv, d_Hpp, lambda, g.nf, d_S);
         // bs = bp - sum over the camera's usable edges of B Dinv bl, edge order
-        hipLaunchKernelGGL((k_ba_ordered_sums<6, 0>), dim3(g.nf), dim3(256), ordered_sums_lds(6), st_, d_bdb, 6,
-                           d_coffs, d_clist, nullptr, d_bp, d_bs, 6, nullptr);
+        if (nusable_)
+            hipLaunchKernelGGL((k_ba_gather_rows<6, 0>), dim3((unsigned)(((int64_t)nusable_ * 6 + 255) / 256)),
+                               dim3(256), 0, st_, d_bdb, 6, d_clist, nusable_, nullptr, d_rows);
+        hipLaunchKernelGGL((k_ba_stream_sums<6>), dim3(g.nf), dim3(64), 0, st_, d_rows, d_coffs, d_bp, d_bs, 6,
+                           nullptr);
         if (n <= kCholLds) {
             const int lb = 8 * (n * (n + 1) + n);
             if (lb > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void *>(k_ba_chol_lds),
@@ -1135,7 +1209,7 @@ int BA::solve_async(double lambda) {
             hipLaunchKernelGGL(k_ba_chol, dim3(1), dim3(1024), 0, st_, d_S, n, d_bs, d_x, d_ok);
         }
     }
-    if (g.npt) hipLaunchKernelGGL(k_ba_backsub, dim3((g.npt + 255) / 256), dim3(256), 0, st_, d_dinv, d_bl, g.npt,
+    if (g.npt) hipLaunchKernelGGL(k_ba_backsub, dim3((g.npt + 63) / 64), dim3(64), 0, st_, d_dinv, d_bl, g.npt,
                                   d_eo, d_poffs, d_plist, d_usable, d_edges, d_pose, d_x, d_x + n);
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
 }
@@ -1211,7 +1285,7 @@ int BA::pop() {
 // chi2 as last computed (an edge's error is only refreshed while active, and
 // a rejected trial's errors stay), the depth test at the current estimate
 int BA::download(double *pts, std::vector<double> &chi2, std::vector<uint8_t> &front) {
-    if (g_.ne) hipLaunchKernelGGL(k_ba_errors, dim3((g_.ne + 255) / 256), dim3(256), 0, st_, d_pose, d_pts, d_edges,
+    if (g_.ne) hipLaunchKernelGGL(k_ba_errors, dim3((g_.ne + 63) / 64), dim3(64), 0, st_, d_pose, d_pts, d_edges,
                                   g_.ne, d_active, 0, 1, d_err, d_chi2, d_rho, d_front, nullptr, nullptr);
     chi2.resize(std::max(g_.ne, 1));
     front.resize(std::max(g_.ne, 1));
