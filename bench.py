@@ -85,7 +85,7 @@ def measured_traffic(stage: str, frames_per_launch: float):
         # template instantiations are listed as k_name<args>; the whole-batch
         # launch is the <false> one
         keys = [k for k in prof["kernels"] if k == name or k.startswith(name + "<") or k.startswith(name + "_w<")]
-        keys.sort(key=lambda k: "<false>" not in k)
+        keys.sort(key=lambda k: "<false" not in k)
         k = prof["kernels"][keys[0]]
         per_frame = k["hbm_bytes_per_dispatch"] / prof["frames_per_dispatch"]
         return round(per_frame * frames_per_launch), str(TRAFFIC_FILE.relative_to(ROOT))
@@ -114,7 +114,7 @@ def measured_valu(stage: str, frames_per_launch: float):
         prof = json.loads(TRAFFIC_FILE.read_text())
         name = STAGE_KERNEL[stage]
         keys = [k for k in prof["kernels"] if k == name or k.startswith(name + "<") or k.startswith(name + "_w<")]
-        keys.sort(key=lambda k: "<false>" not in k)
+        keys.sort(key=lambda k: "<false" not in k)
         k = prof["kernels"][keys[0]]
         return round(k["valu_insts_per_dispatch"] / prof["frames_per_dispatch"] * frames_per_launch)
     except (OSError, KeyError, ValueError, ZeroDivisionError, IndexError):
