@@ -215,6 +215,56 @@ struct OrbxMatcher {
         return nm;
     }
 
+    // The per-keyframe loops in one launch pair: problem k searches frame
+    // F[k] with queries q[k] / qdesc[k], exactly as SearchByProjectionTable
+    // would (Fuse over LocalMapping's neighbours, relocalisation's candidates;
+    // include/orbx.h orbx_search_by_projection_batch).  Returns each problem's
+    // count.
+    static std::vector<int> SearchByProjectionBatch(int variant, const std::vector<ProjFrame> &F,
+                                                    const std::vector<std::vector<orbx_proj_query>> &q,
+                                                    const std::vector<cv::Mat> &qdesc, int th_dist, float nnratio,
+                                                    bool checkOri, std::vector<std::vector<int>> &q_idx,
+                                                    std::vector<std::vector<int>> &q_dist,
+                                                    std::vector<std::vector<int>> &kp_final) {
+        const size_t np = F.size();
+        std::vector<std::vector<orbx_keypoint>> k(np);
+        std::vector<cv::Mat> d(np), qd(np);
+        std::vector<orbx_proj_problem> pr(np);
+        q_idx.assign(np, {});
+        q_dist.assign(np, {});
+        kp_final.assign(np, {});
+        for (size_t i = 0; i < np; ++i) {
+            k[i] = orbx_detail::pack(*F[i].keys);
+            d[i] = F[i].desc->isContinuous() ? *F[i].desc : F[i].desc->clone();
+            qd[i] = qdesc[i].isContinuous() ? qdesc[i] : qdesc[i].clone();
+            orbx_match_frame &mf = pr[i].frame;
+            mf = orbx_match_frame{};
+            mf.keys = k[i].data();
+            mf.desc = d[i].data;
+            mf.uright = F[i].uright && !F[i].uright->empty() ? F[i].uright->data() : nullptr;
+            mf.mp_state = F[i].mp_state && !F[i].mp_state->empty() ? F[i].mp_state->data() : nullptr;
+            mf.inv_sigma2 = F[i].inv_sigma2 ? F[i].inv_sigma2->data() : nullptr;
+            mf.n = (int)k[i].size();
+            mf.nlevels = F[i].inv_sigma2 ? (int)F[i].inv_sigma2->size() : 0;
+            mf.min_x = F[i].min_x; mf.max_x = F[i].max_x; mf.min_y = F[i].min_y; mf.max_y = F[i].max_y;
+            q_idx[i].assign(q[i].size(), -1);
+            q_dist[i].assign(q[i].size(), -1);
+            kp_final[i].assign(k[i].size(), -1);
+            pr[i].queries = q[i].data();
+            pr[i].qdesc = qd[i].data;
+            pr[i].nq = (int)q[i].size();
+            pr[i].q_idx = q_idx[i].data();
+            pr[i].q_dist = q_dist[i].data();
+            pr[i].kp_final = kp_final[i].data();
+        }
+        orbx_detail::check(orbx_search_by_projection_batch(orbx_detail::device_index(), variant, pr.data(), (int)np,
+                                                           th_dist, nnratio, checkOri ? 1 : 0),
+                           "SearchByProjection batch");
+        std::vector<int> nm(np);
+        for (size_t i = 0; i < np; ++i) nm[i] = pr[i].nmatches;
+        return nm;
+    }
+
     // SearchByBoW x2 / SearchForTriangulation (ORBmatcher.cc:160-289, 524-825)
     // on two sides given as orbx_bow_side (FeatureVector as CSR).
     static int SearchByBoWTable(int variant, const orbx_bow_side &A, const orbx_bow_side &B, float nnratio,
@@ -227,6 +277,36 @@ struct OrbxMatcher {
                                               tri.empty() ? nullptr : tri.data(), nlevels, match_a.data(),
                                               match_b.data(), &nm),
                            "SearchByBoW");
+        return nm;
+    }
+
+    // SearchForTriangulation of one keyframe against its neighbours (or any
+    // set of SearchByBoW calls) in one launch pair: problem k = (A[k], B[k],
+    // tri[k]); include/orbx.h orbx_search_by_bow_batch for the neighbour-order
+    // rule LocalMapping::CreateNewMapPoints needs.  Returns each count.
+    static std::vector<int> SearchByBoWBatch(int variant, const std::vector<orbx_bow_side> &A,
+                                             const std::vector<orbx_bow_side> &B,
+                                             const std::vector<std::vector<float>> &tri, int nlevels, float nnratio,
+                                             bool checkOri, std::vector<std::vector<int>> &match_a,
+                                             std::vector<std::vector<int>> &match_b) {
+        const size_t np = A.size();
+        std::vector<orbx_bow_problem> pr(np);
+        match_a.assign(np, {});
+        match_b.assign(np, {});
+        for (size_t i = 0; i < np; ++i) {
+            match_a[i].assign(A[i].n, -1);
+            match_b[i].assign(B[i].n, -1);
+            pr[i].a = A[i];
+            pr[i].b = B[i];
+            pr[i].tri = i < tri.size() && !tri[i].empty() ? tri[i].data() : nullptr;
+            pr[i].match_a = match_a[i].data();
+            pr[i].match_b = match_b[i].data();
+        }
+        orbx_detail::check(orbx_search_by_bow_batch(orbx_detail::device_index(), variant, pr.data(), (int)np, nnratio,
+                                                    checkOri ? 1 : 0, nlevels),
+                           "SearchByBoW batch");
+        std::vector<int> nm(np);
+        for (size_t i = 0; i < np; ++i) nm[i] = pr[i].nmatches;
         return nm;
     }
 };

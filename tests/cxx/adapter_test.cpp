@@ -11,7 +11,8 @@
 //        desc, nkept, mvuRight, mvDepth.
 //   adapter_test proj variant th ratio ori frame.bin queries.bin out.bin
 //        OrbxMatcher::SearchByProjectionTable on raw tables (see test): writes
-//        nmatches, q_idx, q_dist, kp_final.
+//        nmatches, q_idx, q_dist, kp_final; also runs the table twice through
+//        OrbxMatcher::SearchByProjectionBatch and exits 3 if a copy differs.
 //   adapter_test rgbd W H img.raw depth.raw mbf out.bin
 //        extracts the image and runs OrbxFrame::ComputeStereoFromRGBD:
 //        n, kps, desc, mvuRight, mvDepth.
@@ -116,6 +117,17 @@ int main(int argc, char **argv) {
         const int nm = OrbxMatcher::SearchByProjectionTable(std::atoi(argv[2]), F, q, qd, std::atoi(argv[3]),
                                                             (float)std::atof(argv[4]), std::atoi(argv[5]) != 0, qi,
                                                             qdist, kf);
+        // the same problem twice through the batch entry point: both copies
+        // must equal the single call (a non-zero exit says they do not)
+        std::vector<std::vector<int>> bqi, bqd, bkf;
+        const std::vector<int> bnm = OrbxMatcher::SearchByProjectionBatch(
+            std::atoi(argv[2]), {F, F}, {q, q}, {qd, qd}, std::atoi(argv[3]), (float)std::atof(argv[4]),
+            std::atoi(argv[5]) != 0, bqi, bqd, bkf);
+        for (int i = 0; i < 2; ++i)
+            if (bnm[i] != nm || bqi[i] != qi || bqd[i] != qdist || bkf[i] != kf) {
+                std::cerr << "batch problem " << i << " differs from the single call\n";
+                return 3;
+            }
         std::ofstream out(argv[8], std::ios::binary);
         out.write(reinterpret_cast<const char *>(&nm), 4);
         out.write(reinterpret_cast<const char *>(qi.data()), 4 * qi.size());
