@@ -33,6 +33,9 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <mutex>
@@ -573,19 +576,26 @@ __device__ inline double readlane_f64(double v, int l) {
 //    their term L(i,k) L(j,k)); no workgroup barrier inside a panel;
 //  - then all waves apply the panel to the trailing lower triangle, each entry
 //    receiving the panel's kPanel terms one by one in ascending column.
+//    Look-ahead: the next panel's columns get the terms first (all waves),
+//    then wave 0 factors the next panel while waves 1.. update the rest, and
+//    the last wave also runs the panel's forward-solve steps.
 // Every entry therefore receives its terms L(i,m) L(j,m) in ascending m, each
 // as its own multiply and subtract, exactly as the column-by-column factor
 // (the oracle's): bit-identical, with two barriers per panel instead of one
 // per column.  L stays in the lower triangle (row stride n+1: odd, so column
 // reads spread over banks), the diagonal also in dg[].
-//  - the solves run column-sweep in one wave (lane r owns rows r and r+64):
+//  - the solves run column-sweep in one wave (lane r owns rows r and r+64),
+//    the backward one after the factor:
 //    the forward terms arrive in ascending k as in the row loop, the
 //    backward terms in descending k (the order the oracle uses).
 constexpr int kCholLds = 128;
 constexpr int kPanel = 8;
-__global__ __launch_bounds__(512) void k_ba_chol_lds(const double *S, int n, const double *bs, double *x, int *ok) {
+__global__ __launch_bounds__(512) void k_ba_chol_lds(const double *S, int n, const double *bs, double *x, int *ok,
+                                                     unsigned long long *clk) {
     extern __shared__ double L[];   // n rows of n+1, then dg (n)
     __shared__ int bad;
+    // clk (diagnostics, ORBX_BA_CLOCKS): wave 0's cycles in load / panel factor / next-panel update, then the backward solve
+    unsigned long long c_t = clk ? __builtin_amdgcn_s_memtime() : 0, c_f = 0, c_u = 0, c_f2 = 0;
     const int ld = n + 1;
     double *dg = L + n * ld;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
@@ -613,84 +623,160 @@ __global__ __launch_bounds__(512) void k_ba_chol_lds(const double *S, int n, con
     }
     if (tid == 0) bad = 0;
     __syncthreads();
-    for (int k0 = 0; k0 < n; k0 += kPanel) {
+    if (clk && tid == 0) { clk[0] += __builtin_amdgcn_s_memtime() - c_t; c_t = __builtin_amdgcn_s_memtime(); }
+    // wave 0 factors the panel [k0, k0 + kPanel): lane owns rows k0 + lane and
+    // k0 + 64 + lane, the panel's columns of those rows in registers
+    auto factor = [&](int k0) {
         const int k1 = min(k0 + kPanel, n);
-        if (w == 0) {
-            // lane owns rows k0 + lane and k0 + 64 + lane; the panel's columns
-            // of those rows stay in registers until the panel is done
-            const int q0 = k0 + lane, q1 = k0 + 64 + lane;
-            double p0[kPanel], p1[kPanel];
+        const int q0 = k0 + lane, q1 = k0 + 64 + lane;
+        double p0[kPanel], p1[kPanel];
 #pragma unroll
-            for (int m = 0; m < kPanel; ++m) {
-                p0[m] = (q0 < n && k0 + m < k1 && k0 + m <= q0) ? L[q0 * ld + k0 + m] : 0.0;
-                p1[m] = (q1 < n && k0 + m < k1) ? L[q1 * ld + k0 + m] : 0.0;
-            }
+        for (int m = 0; m < kPanel; ++m) {
+            p0[m] = (q0 < n && k0 + m < k1 && k0 + m <= q0) ? L[q0 * ld + k0 + m] : 0.0;
+            p1[m] = (q1 < n && k0 + m < k1) ? L[q1 * ld + k0 + m] : 0.0;
+        }
+        // branch-free over the panel so the compiler can overlap column m's
+        // tail with column m + 1's chain: a column past k1 (last panel only)
+        // is all zeros with diagonal 1, so its terms subtract +0 (no-ops)
+        bool good = true;
+        double gl = 1.0;
 #pragma unroll
-            for (int m = 0; m < kPanel; ++m) {
-                const int k = k0 + m;
-                if (k >= k1) break;
-                const double d = readlane_f64(p0[m], m);   // row k's diagonal entry (lane m)
-                if (!(d > 0)) {   // (uniform over the wave)
-                    if (lane == 0) bad = 1;
-                    break;
-                }
-                const double g = sqrt(d);
-                if (lane == 0) dg[k] = g;
-                // column k below the diagonal: rows > k of this lane
-                if (q0 > k) p0[m] = p0[m] / g;
-                p1[m] = p1[m] / g;   // (q1 > k always)
+        for (int m = 0; m < kPanel; ++m) {
+            const int k = k0 + m;
+            const double d = readlane_f64(p0[m], m);   // row k's diagonal entry (lane m)
+            good = good && (k >= k1 || d > 0);
+            const double g = sqrt(k < k1 ? d : 1.0);
+            gl = lane == m ? g : gl;
+            // column k below the diagonal: rows > k of this lane
+            const double c0 = p0[m] / g;
+            p0[m] = q0 > k ? c0 : p0[m];
+            p1[m] = p1[m] / g;   // (q1 > k always)
 #pragma unroll
-                for (int jm = m + 1; jm < kPanel; ++jm) {   // the panel's later columns
-                    if (k0 + jm >= k1) break;
-                    const double aj = readlane_f64(p0[m], jm);   // L(k0 + jm, k): row k0 + jm is lane jm's q0
-                    if (q0 >= k0 + jm) p0[jm] = p0[jm] - p0[m] * aj;
-                    p1[jm] = p1[jm] - p1[m] * aj;
-                }
-            }
-#pragma unroll
-            for (int m = 0; m < kPanel; ++m) {
-                if (k0 + m >= k1) break;
-                if (q0 < n && q0 > k0 + m) L[q0 * ld + k0 + m] = p0[m];
-                if (q1 < n) L[q1 * ld + k0 + m] = p1[m];
+            for (int jm = m + 1; jm < kPanel; ++jm) {   // the panel's later columns
+                const double aj = readlane_f64(p0[m], jm);   // L(k0 + jm, k): row k0 + jm is lane jm's q0
+                const double u0 = p0[jm] - p0[m] * aj;
+                p0[jm] = q0 >= k0 + jm ? u0 : p0[jm];
+                p1[jm] = p1[jm] - p1[m] * aj;
             }
         }
-        __syncthreads();
-        if (bad) break;
-        // trailing update: rows i >= k1 by wave, columns j in [k1, i] by lane
-        for (int i = k1 + w; i < n; i += nw) {
-            double li[kPanel];
+        if (!good && lane == 0) bad = 1;
+        if (lane < k1 - k0) dg[k0 + lane] = gl;
 #pragma unroll
-            for (int m = 0; m < kPanel; ++m) li[m] = k0 + m < k1 ? L[i * ld + k0 + m] : 0.0;
-            for (int j = k1 + lane; j <= i; j += 64) {
-                double v = L[i * ld + j];
-#pragma unroll
-                for (int m = 0; m < kPanel; ++m)
-                    if (k0 + m < k1) v = v - li[m] * L[j * ld + k0 + m];
-                L[i * ld + j] = v;
-            }
+        for (int m = 0; m < kPanel; ++m) {
+            if (k0 + m >= k1) break;
+            if (q0 < n && q0 > k0 + m) L[q0 * ld + k0 + m] = p0[m];
+            if (q1 < n) L[q1 * ld + k0 + m] = p1[m];
         }
-        __syncthreads();
+    };
+    // the panel [k0, k1)'s terms for rows i .. i+3, columns [c0, row]: four
+    // independent chains per lane sharing the column's panel values
+    auto trail = [&](int i, int k0, int k1, int c0) {
+        double li[4][kPanel];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int m = 0; m < kPanel; ++m) li[r][m] = (i + r < n && k0 + m < k1) ? L[(i + r) * ld + k0 + m] : 0.0;
+        const int ie = min(i + 3, n - 1);
+        for (int j = c0 + lane; j <= ie; j += 64) {
+            double lj[kPanel], v[4];
+#pragma unroll
+            for (int m = 0; m < kPanel; ++m) lj[m] = k0 + m < k1 ? L[j * ld + k0 + m] : 0.0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = (j <= i + r && i + r < n) ? L[(i + r) * ld + j] : 0.0;
+#pragma unroll
+            for (int m = 0; m < kPanel; ++m)
+                if (k0 + m < k1) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = v[r] - li[r][m] * lj[m];
+                }
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (j <= i + r && i + r < n) L[(i + r) * ld + j] = v[r];
+        }
+    };
+    // the forward solve L y = b rides along in wave ws: panel [k0, k1)'s
+    // steps run while wave 0 factors the next panel (lane r owns rows r and
+    // r + 64; each s_i receives its terms in ascending k, as in the row loop)
+    const int ws = nw / 2, i0 = lane, i1 = lane + 64, r0 = min(i0, n - 1), r1 = min(i1, n - 1);
+    double s0 = 0.0, s1 = 0.0;
+    if (w == ws) {
+        s0 = i0 < n ? bs[i0] : 0.0;
+        s1 = i1 < n ? bs[i1] : 0.0;
     }
-    if (w != 0) return;
+    auto forward = [&](int k0, int k1) {
+        double a0[kPanel], a1[kPanel], dk[kPanel];
+#pragma unroll
+        for (int m = 0; m < kPanel; ++m) {
+            const int kk = min(k0 + m, n - 1);
+            dk[m] = dg[kk];
+            a0[m] = L[r0 * ld + kk];
+            a1[m] = L[r1 * ld + kk];
+        }
+#pragma unroll
+        for (int m = 0; m < kPanel; ++m) {
+            const int k = k0 + m;
+            if (k >= k1) break;
+            const double yk = (k < 64 ? readlane_f64(s0, k) : readlane_f64(s1, k - 64)) / dk[m];
+            if (lane == (k & 63)) (k < 64 ? s0 : s1) = yk;
+            if (i0 > k && i0 < n) s0 = s0 - a0[m] * yk;
+            if (i1 > k && i1 < n) s1 = s1 - a1[m] * yk;
+        }
+    };
+    // look-ahead: while wave 0 factors panel p + 1, the other waves apply panel
+    // p to the columns past it (the next panel's columns got panel p's terms
+    // first, from every wave)
+    if (w == 0) factor(0);
+    __syncthreads();
+    if (clk && tid == 0) { const unsigned long long t = __builtin_amdgcn_s_memtime(); c_f += t - c_t; c_t = t; }
+    for (int k0 = 0; k0 < n && !bad; k0 += kPanel) {
+        const int k1 = min(k0 + kPanel, n), k2 = min(k1 + kPanel, n), pw = k2 - k1;
+        for (int e = tid; e < (n - k1) * pw; e += blockDim.x) {   // next panel's columns, rows >= k1
+            const int i = k1 + e / pw, j = k1 + e % pw;
+            if (j > i) continue;
+            double v = L[i * ld + j];
+#pragma unroll
+            for (int m = 0; m < kPanel; ++m)
+                if (k0 + m < k1) v = v - L[i * ld + k0 + m] * L[j * ld + k0 + m];
+            L[i * ld + j] = v;
+        }
+        __syncthreads();
+        if (clk && tid == 0) { const unsigned long long t = __builtin_amdgcn_s_memtime(); c_u += t - c_t; c_t = t; }
+        const unsigned long long c_w = clk ? __builtin_amdgcn_s_memtime() : 0;
+        if (w == 0) {
+            if (k1 < n) factor(k1);
+            if (clk && lane == 0) c_f2 += __builtin_amdgcn_s_memtime() - c_w;
+        } else {
+            if (w == ws) forward(k0, k1);
+            else   // (waves other than 0 and ws)
+                for (int i = k2 + 4 * (w - 1 - (w > ws)); i < n; i += 4 * (nw - 2)) trail(i, k0, k1, k2);
+            if (clk && lane == 0) c_f2 += __builtin_amdgcn_s_memtime() - c_w;
+        }
+        __syncthreads();
+        if (clk && tid == 0) { const unsigned long long t = __builtin_amdgcn_s_memtime(); c_f += t - c_t; c_t = t; }
+    }
+    if (clk && tid == 0) { clk[1] += c_f; clk[2] += c_u; }
+    if (clk && lane == 0 && (w == 0 || w == 1 || w == ws)) atomicAdd(clk + (w == 0 ? 5 : w == 1 ? 6 : 7), c_f2);
+    if (w != ws) return;
+    if (clk) c_t = __builtin_amdgcn_s_memtime();
     const bool good = !bad;
     if (lane == 0) *ok = good;
     if (!good) return;
-    const int i0 = lane, i1 = lane + 64;
-    double s0 = i0 < n ? bs[i0] : 0.0, s1 = i1 < n ? bs[i1] : 0.0;
-    for (int k = 0; k < n; ++k) {   // L y = b
-        const double yk = (k < 64 ? readlane_f64(s0, k) : readlane_f64(s1, k - 64)) / dg[k];
-        if (lane == (k & 63)) (k < 64 ? s0 : s1) = yk;
-        if (i0 > k && i0 < n) s0 = s0 - L[i0 * ld + k] * yk;
-        if (i1 > k && i1 < n) s1 = s1 - L[i1 * ld + k] * yk;
-    }
+    double dk, a0, a1;
+    dk = dg[n - 1];
+    a0 = L[(n - 1) * ld + r0];
+    a1 = L[(n - 1) * ld + r1];
     for (int k = n - 1; k >= 0; --k) {   // L^T x = y
-        const double xk = (k < 64 ? readlane_f64(s0, k) : readlane_f64(s1, k - 64)) / dg[k];
+        const int kn = max(k - 1, 0);
+        const double dn = dg[kn], a0n = L[kn * ld + r0], a1n = L[kn * ld + r1];
+        const double xk = (k < 64 ? readlane_f64(s0, k) : readlane_f64(s1, k - 64)) / dk;
         if (lane == (k & 63)) (k < 64 ? s0 : s1) = xk;
-        if (i0 < k) s0 = s0 - L[k * ld + i0] * xk;
-        if (i1 < k) s1 = s1 - L[k * ld + i1] * xk;
+        if (i0 < k) s0 = s0 - a0 * xk;
+        if (i1 < k) s1 = s1 - a1 * xk;
+        dk = dn; a0 = a0n; a1 = a1n;
     }
     if (i0 < n) x[i0] = s0;
     if (i1 < n) x[i1] = s1;
+    if (clk && lane == 0) { clk[3] += __builtin_amdgcn_s_memtime() - c_t; clk[4] += 1; }
 }
 
 // xl = Dinv (bl - sum over the point's usable edges (camera order) of B^T xp)
@@ -812,9 +898,62 @@ struct Graph {
     std::vector<int32_t> coffs, clist, poffs, plist, epoint;   // camera lists: usable edges by point; point lists: edges by camera
 };
 
+// Per-device workspace kept across calls (LocalMapping runs a BA per
+// keyframe): the stream, the device arena, the pinned readback buffers and
+// the pair lists, grown on demand.  Allocating and freeing them per call cost
+// ~5 ms of the ~15 ms a KITTI-size call took.
+struct BAWs {
+    std::mutex mu;
+    hipStream_t st = nullptr;
+    uint8_t *dev = nullptr, *host = nullptr;
+    size_t cap = 0, hcap = 0;
+    int32_t *moffs = nullptr;
+    size_t moffs_cap = 0;
+    int2 *mlist = nullptr;
+    double *terms = nullptr;
+    int64_t mcap = 0;
+};
+
+BAWs &ba_ws(int device) {
+    static BAWs ws[64];
+    return ws[device & 63];
+}
+
+template <typename T>
+bool grow_dev(T *&p, size_t &cap, size_t need) {
+    if (need <= cap && p) return true;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipMalloc(reinterpret_cast<void **>(&p), sizeof(T) * need) != hipSuccess) return false;
+    cap = need;
+    return true;
+}
+
+// ORBX_BA_CLOCKS: k_ba_chol_lds phase cycles, summed over the process and
+// printed at exit (diagnostics)
+unsigned long long *chol_clk() {
+    static unsigned long long *p = nullptr;
+    static bool init = false;
+    if (!init) {
+        init = true;
+        if (std::getenv("ORBX_BA_CLOCKS") && hipMallocManaged(reinterpret_cast<void **>(&p), 64) == hipSuccess) {
+            std::memset(p, 0, 64);
+            std::atexit([] {
+                (void)hipDeviceSynchronize();
+                std::fprintf(stderr, "k_ba_chol_lds cycles per call: load %llu panel %llu trailing %llu solves %llu (%llu calls); factor %llu trail(w1) %llu fwd(ws) %llu\n",
+                             p[0] / std::max(p[4], 1ull), p[1] / std::max(p[4], 1ull), p[2] / std::max(p[4], 1ull),
+                             p[3] / std::max(p[4], 1ull), p[4], p[5] / std::max(p[4], 1ull), p[6] / std::max(p[4], 1ull),
+                             p[7] / std::max(p[4], 1ull));
+            });
+        }
+    }
+    return p;
+}
+
 class BA {
 public:
-    explicit BA(Graph &g, hipStream_t st) : g_(g), st_(st) {}
+    BA(Graph &g, BAWs &ws) : g_(g), st_(ws.st), ws_(ws) {}
     int alloc();
     int upload(const double *pts);
     void set_active(const std::vector<uint8_t> &act);
@@ -838,16 +977,11 @@ public:
     int push();
     int pop();
     int download(double *pts, std::vector<double> &chi2, std::vector<uint8_t> &front);
-    ~BA() {
-        if (buf_) (void)hipFree(buf_);
-        if (d_moffs) (void)hipFree(d_moffs);
-        if (d_mlist) (void)hipFree(d_mlist);
-        if (d_terms) (void)hipFree(d_terms);
-        if (hbuf_) (void)hipHostFree(hbuf_);
-    }
+    // (the buffers belong to the workspace)
 
     Graph &g_;
     hipStream_t st_;
+    BAWs &ws_;
     uint8_t *buf_ = nullptr;
     Pose *d_pose = nullptr, *d_pose_bk = nullptr;
     double *d_pts = nullptr, *d_pts_bk = nullptr;
@@ -872,7 +1006,7 @@ public:
     double *d_terms = nullptr;                 // 36 per shared point of each pair (k_ba_pair_terms)
     double *d_rows = nullptr;                  // records gathered in list order (k_ba_gather_rows), 42 per edge
     int nusable_ = 0;
-    int64_t mcap_ = 0, nmatch_ = 0;
+    int64_t nmatch_ = 0;
     uint8_t *hbuf_ = nullptr;                  // pinned readbacks
     double *h_rho0 = nullptr, *h_x = nullptr, *h_b = nullptr, *h_hpp = nullptr, *h_hll = nullptr;
     int *h_ok = nullptr;
@@ -882,7 +1016,8 @@ int BA::alloc() {
     const Graph &g = g_;
     const size_t ne = std::max(g.ne, 1), nc = std::max(g.ncam, 1), np = std::max(g.npt, 1), nf = std::max(g.nf, 1);
     // the camera-pair list: free cameras sharing a point (structure of the reduced system)
-    std::set<std::pair<int, int>> pairset;
+    // (a dense nf x nf mark table: nf <= 170; pairs in lexicographic order)
+    std::vector<uint8_t> mark((size_t)g.nf * g.nf, 0);
     std::vector<int> fcams;
     for (int p = 0; p < g.npt; ++p) {
         fcams.clear();
@@ -892,11 +1027,13 @@ int BA::alloc() {
         }
         for (size_t a = 0; a < fcams.size(); ++a)
             for (size_t b = 0; b < fcams.size(); ++b)
-                if (fcams[a] <= fcams[b]) pairset.insert({fcams[a], fcams[b]});
+                if (fcams[a] <= fcams[b]) mark[(size_t)fcams[a] * g.nf + fcams[b]] = 1;
     }
-    for (int f = 0; f < g.nf; ++f) pairset.insert({f, f});
+    for (int f = 0; f < g.nf; ++f) mark[(size_t)f * g.nf + f] = 1;
     std::vector<int2> pairs;
-    for (auto &pr : pairset) pairs.push_back(make_int2(pr.first, pr.second));
+    for (int a = 0; a < g.nf; ++a)
+        for (int b = a; b < g.nf; ++b)
+            if (mark[(size_t)a * g.nf + b]) pairs.push_back(make_int2(a, b));
     npairs = (int)pairs.size();
     // all edges of each free camera in edge order (for Hpp / bp)
     cv_offs_.assign(g.nf + 1, 0);
@@ -919,7 +1056,15 @@ int BA::alloc() {
                          sizeof(int2) * std::max(npairs, 1) + 8 * (36 * nf + 6 * nf + 9 * np + 3 * np + 9 * np +
                                                                    18 * ne + 6 * ne + n * n + n + n + 3 * np) +
                          4 * nf * np + 8 * ne + 8 * 3 * np + 8 * 42 * ne + 256 * 5;
-    if (hipMalloc(reinterpret_cast<void **>(&buf_), bytes) != hipSuccess) return ORBX_ENOMEM;
+    if (ws_.cap < bytes) {
+        (void)hipStreamSynchronize(st_);
+        if (ws_.dev) (void)hipFree(ws_.dev);
+        ws_.dev = nullptr;
+        ws_.cap = 0;
+        if (hipMalloc(reinterpret_cast<void **>(&ws_.dev), bytes + bytes / 4) != hipSuccess) return ORBX_ENOMEM;
+        ws_.cap = bytes + bytes / 4;
+    }
+    buf_ = ws_.dev;
     uint8_t *p = buf_;
     d_pose = carve<Pose>(p, nc); d_pose_bk = carve<Pose>(p, nc);
     d_pts = carve<double>(p, 3 * np); d_pts_bk = carve<double>(p, 3 * np);
@@ -944,7 +1089,15 @@ int BA::alloc() {
     {
         const size_t m = n + 3 * np;
         const size_t hb = 8 * (ne + 2 * m + 36 * nf + 9 * np) + 64 + 256 * 6;
-        if (hipHostMalloc(reinterpret_cast<void **>(&hbuf_), hb, hipHostMallocDefault) != hipSuccess) return ORBX_ENOMEM;
+        if (ws_.hcap < hb) {
+            if (ws_.host) (void)hipHostFree(ws_.host);
+            ws_.host = nullptr;
+            ws_.hcap = 0;
+            if (hipHostMalloc(reinterpret_cast<void **>(&ws_.host), hb + hb / 4, hipHostMallocDefault) != hipSuccess)
+                return ORBX_ENOMEM;
+            ws_.hcap = hb + hb / 4;
+        }
+        hbuf_ = ws_.host;
         uint8_t *h = hbuf_;
         h_rho0 = carve<double>(h, ne); h_x = carve<double>(h, m); h_b = carve<double>(h, m);
         h_hpp = carve<double>(h, 36 * nf); h_hll = carve<double>(h, 9 * np); h_ok = carve<int>(h, 1);
@@ -1005,8 +1158,8 @@ void BA::set_active(const std::vector<uint8_t> &act) {
     if (use_map && !cmap.empty())
         (void)hipMemcpyAsync(d_cmap, cmap.data(), 4 * cmap.size(), hipMemcpyHostToDevice, st_);
     if (use_map && npairs > 0) {   // the pairs' shared-point lists: count, scan on the host, fill
-        if (!d_moffs && hipMalloc(reinterpret_cast<void **>(&d_moffs), 4 * (size_t)(npairs + 1)) != hipSuccess)
-            use_map = false;
+        if (!grow_dev(ws_.moffs, ws_.moffs_cap, (size_t)npairs + 1)) use_map = false;
+        d_moffs = ws_.moffs;
         std::vector<int32_t> cnt(npairs), offs(npairs + 1, 0);
         if (use_map) {
             hipLaunchKernelGGL(k_ba_pair_matches, dim3((npairs + 3) / 4), dim3(256), 0, st_, d_pairs, npairs, d_coffs,
@@ -1016,19 +1169,22 @@ void BA::set_active(const std::vector<uint8_t> &act) {
                 use_map = false;
         }
         for (int k = 0; k < npairs && use_map; ++k) offs[k + 1] = offs[k] + cnt[k];
-        if (use_map && offs[npairs] > mcap_) {
-            for (void *x : {(void *)d_mlist, (void *)d_terms})
+        if (use_map && offs[npairs] > ws_.mcap) {
+            (void)hipStreamSynchronize(st_);
+            for (void *x : {(void *)ws_.mlist, (void *)ws_.terms})
                 if (x) (void)hipFree(x);
-            d_mlist = nullptr;
-            d_terms = nullptr;
-            mcap_ = 0;
-            const size_t m = (size_t)std::max(offs[npairs], 1);
-            if (hipMalloc(reinterpret_cast<void **>(&d_mlist), sizeof(int2) * m) == hipSuccess &&
-                hipMalloc(reinterpret_cast<void **>(&d_terms), 36 * sizeof(double) * m) == hipSuccess)
-                mcap_ = (int64_t)m;
+            ws_.mlist = nullptr;
+            ws_.terms = nullptr;
+            ws_.mcap = 0;
+            const size_t m = (size_t)std::max(offs[npairs], 1) * 5 / 4;
+            if (hipMalloc(reinterpret_cast<void **>(&ws_.mlist), sizeof(int2) * m) == hipSuccess &&
+                hipMalloc(reinterpret_cast<void **>(&ws_.terms), 36 * sizeof(double) * m) == hipSuccess)
+                ws_.mcap = (int64_t)m;
             else
                 use_map = false;
         }
+        d_mlist = ws_.mlist;
+        d_terms = ws_.terms;
         nmatch_ = use_map ? offs[npairs] : 0;
         if (use_map) {
             (void)hipMemcpyAsync(d_moffs, offs.data(), 4 * (size_t)(npairs + 1), hipMemcpyHostToDevice, st_);
@@ -1125,7 +1281,7 @@ int BA::solve(double lambda, int *ok) {
             if (lb > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void *>(k_ba_chol_lds),
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, lb) != hipSuccess)
                 return ORBX_EIO;
-            hipLaunchKernelGGL(k_ba_chol_lds, dim3(1), dim3(512), lb, st_, d_S, n, d_bs, d_x, d_ok);
+            hipLaunchKernelGGL(k_ba_chol_lds, dim3(1), dim3(512), lb, st_, d_S, n, d_bs, d_x, d_ok, chol_clk());
         } else {
             hipLaunchKernelGGL(k_ba_chol, dim3(1), dim3(1024), 0, st_, d_S, n, d_bs, d_x, d_ok);
         }
@@ -1204,7 +1360,7 @@ int BA::solve_async(double lambda) {
             if (lb > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void *>(k_ba_chol_lds),
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, lb) != hipSuccess)
                 return ORBX_EIO;
-            hipLaunchKernelGGL(k_ba_chol_lds, dim3(1), dim3(512), lb, st_, d_S, n, d_bs, d_x, d_ok);
+            hipLaunchKernelGGL(k_ba_chol_lds, dim3(1), dim3(512), lb, st_, d_S, n, d_bs, d_x, d_ok, chol_clk());
         } else {
             hipLaunchKernelGGL(k_ba_chol, dim3(1), dim3(1024), 0, st_, d_S, n, d_bs, d_x, d_ok);
         }
@@ -1410,30 +1566,51 @@ int orbx_local_ba(int device, const float *Tcw, const uint8_t *fixed, int ncam, 
     if (ncam < 0 || npt < 0 || ne < 0 || iters1 < 0 || iters2 < 0 || (ncam && (!Tcw || !fixed || !Tcw_out)) ||
         (npt && (!Xw || !Xw_out)) || (ne && (!edges || !outlier)))
         return ORBX_EINVAL;
+    // ORBX_BA_TIMING: host-side phase times of this call on stderr (diagnostics)
+    static const bool timing = std::getenv("ORBX_BA_TIMING") != nullptr;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto t_last = now();
+    char tbuf[512];
+    int tlen = 0;
+    auto lap = [&](const char *what) {
+        if (!timing) return;
+        (void)hipDeviceSynchronize();
+        const auto t = now();
+        tlen += std::snprintf(tbuf + tlen, sizeof(tbuf) - tlen, " %s %.3f", what,
+                              std::chrono::duration<double, std::milli>(t - t_last).count());
+        t_last = t;
+    };
     Graph g;
     int rc = build_graph(Tcw, fixed, ncam, npt, edges, ne, g);
     if (rc) return rc;
+    lap("graph");
     if (g.nf > 170) return ORBX_EINVAL;   // dense reduced system: 6 x 170 rows in one workgroup
     if (hipSetDevice(device) != hipSuccess) return ORBX_ENODEV;
-    hipStream_t st;
-    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return ORBX_EIO;
+    BAWs &ws = ba_ws(device);
+    std::lock_guard<std::mutex> lock(ws.mu);
+    if (!ws.st && hipStreamCreateWithFlags(&ws.st, hipStreamNonBlocking) != hipSuccess) return ORBX_EIO;
+    const hipStream_t st = ws.st;
     std::vector<double> pts(3 * (size_t)std::max(npt, 1));
     for (size_t i = 0; i < 3 * (size_t)npt; ++i) pts[i] = Xw[i];
     std::vector<uint8_t> out_flags(std::max(ne, 1), 0);
     int its[2] = {0, 0};
     {
-        BA ba(g, st);
-        if ((rc = ba.alloc()) || (rc = ba.upload(pts.data()))) { (void)hipStreamDestroy(st); return rc; }
+        BA ba(g, ws);
+        if ((rc = ba.alloc()) || (rc = ba.upload(pts.data()))) return rc;
+        lap("alloc+upload");
         (void)hipMemsetAsync(ba.d_chi2, 0, 8 * (size_t)std::max(ne, 1), st);
         (void)hipMemsetAsync(ba.d_rho, 0, 16 * (size_t)std::max(ne, 1), st);
         (void)hipMemsetAsync(ba.d_err, 0, 24 * (size_t)std::max(ne, 1), st);
         // optimizer.optimize(5) with Huber kernels on every edge (Optimizer.cc:779-781)
         std::vector<uint8_t> act(std::max(ne, 1), 1);
         ba.set_active(act);
+        lap("active1");
         its[0] = lm_optimize(ba, iters1, true, &rc);
+        lap("lm1");
         std::vector<double> chi2;
         std::vector<uint8_t> front;
         if (!rc) rc = ba.download(pts.data(), chi2, front);
+        lap("download1");
         if (!rc && iters2 > 0) {
             // outliers leave the second pass (setLevel(1)); every kernel is dropped (:791-826)
             for (int e = 0; e < ne; ++e) {
@@ -1441,8 +1618,11 @@ int orbx_local_ba(int device, const float *Tcw, const uint8_t *fixed, int ncam, 
                 if (chi2[e] > th || !front[e]) act[e] = 0;
             }
             ba.set_active(act);
+            lap("active2");
             its[1] = lm_optimize(ba, iters2, false, &rc);
+            lap("lm2");
             if (!rc) rc = ba.download(pts.data(), chi2, front);
+            lap("download2");
         }
         if (!rc)   // the inlier check of :838-870 (an inactive edge keeps its last error)
             for (int e = 0; e < ne; ++e) {
@@ -1450,7 +1630,9 @@ int orbx_local_ba(int device, const float *Tcw, const uint8_t *fixed, int ncam, 
                 out_flags[e] = chi2[e] > th || !front[e];
             }
     }
-    (void)hipStreamDestroy(st);
+    (void)hipStreamSynchronize(st);
+    lap("end");
+    if (timing) std::fprintf(stderr, "orbx_local_ba ms:%s\n", tbuf);
     if (rc) return rc;
     for (int c = 0; c < ncam; ++c) pose_to_cv(g.poses[c], Tcw_out + 12 * (size_t)c);
     for (size_t i = 0; i < 3 * (size_t)npt; ++i) Xw_out[i] = (float)pts[i];
@@ -1473,12 +1655,13 @@ int orbx_ba_debug_step(int device, const float *Tcw, const uint8_t *fixed, int n
     if (rc) return rc;
     if (g.nf > 170) return ORBX_EINVAL;
     if (hipSetDevice(device) != hipSuccess) return ORBX_ENODEV;
-    hipStream_t st;
-    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return ORBX_EIO;
+    BAWs &ws = ba_ws(device);
+    std::lock_guard<std::mutex> lock(ws.mu);
+    if (!ws.st && hipStreamCreateWithFlags(&ws.st, hipStreamNonBlocking) != hipSuccess) return ORBX_EIO;
     std::vector<double> pts(3 * (size_t)std::max(npt, 1));
     for (size_t i = 0; i < 3 * (size_t)npt; ++i) pts[i] = Xw[i];
     {
-        BA ba(g, st);
+        BA ba(g, ws);
         std::vector<uint8_t> act(std::max(ne, 1), 1);
         if (!(rc = ba.alloc()) && !(rc = ba.upload(pts.data()))) {
             ba.set_active(act);
@@ -1488,7 +1671,6 @@ int orbx_ba_debug_step(int device, const float *Tcw, const uint8_t *fixed, int n
             }
         }
     }
-    (void)hipStreamDestroy(st);
     return rc;
 }
 
