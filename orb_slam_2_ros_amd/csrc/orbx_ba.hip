@@ -185,32 +185,33 @@ __global__ void k_ba_errors(const Pose *poses, const double *pts, const EdgeD *e
     if (rho0_out) rho0_out[i] = rho0;   // (contiguous, for the host's ordered sum)
 }
 
-__global__ void k_ba_linearize(const Pose *poses, const double *pts, const EdgeD *edges, int ne, const uint8_t *active,
-                               const double *err_in, const double *rho_in, EdgeOut *out) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= ne || !active[i]) return;
-    const EdgeD e = edges[i];
-    const Pose T = poses[e.cam];
-    double p[3];
-    se3_map(T, pts + 3 * (int64_t)e.point, p);
+// One edge's blocks (D = 2 mono, 3 stereo: compile-time, so the Jacobians
+// stay in registers), stored field by field into out
+template <int D>
+__device__ inline void linearize_edge(const EdgeD &e, const Pose &T, const double *p, double rho1, const double *err,
+                                      double *out) {
     const double x = p[0], y = p[1], z = p[2], z_2 = z * z;
     double R[9];
     quat_to_R(T.q, R);
-    double A[3][3], B[3][6];   // d e / d point, d e / d pose (rows: error components)
-    if (!e.stereo) {
+    double A[D][3], B[D][6];   // d e / d point, d e / d pose (rows: error components)
+    if (D == 2) {
         const double tmp[2][3] = {{e.fx, 0, -x / z * e.fx}, {0, e.fy, -y / z * e.fy}};
         const double s = -1. / z;
+#pragma unroll
         for (int r = 0; r < 2; ++r)
+#pragma unroll
             for (int c = 0; c < 3; ++c) {
                 double acc = 0;
+#pragma unroll
                 for (int k = 0; k < 3; ++k) acc = acc + (s * tmp[r][k]) * R[3 * k + c];
                 A[r][c] = acc;
             }
     } else {
+#pragma unroll
         for (int c = 0; c < 3; ++c) {
             A[0][c] = -e.fx * R[c] / z + e.fx * x * R[6 + c] / z_2;
             A[1][c] = -e.fy * R[3 + c] / z + e.fy * y * R[6 + c] / z_2;
-            A[2][c] = A[0][c] - e.bf * R[6 + c] / z_2;
+            A[D - 1][c] = A[0][c] - e.bf * R[6 + c] / z_2;
         }
     }
     B[0][0] = x * y / z_2 * e.fx;
@@ -225,51 +226,76 @@ __global__ void k_ba_linearize(const Pose *poses, const double *pts, const EdgeD
     B[1][3] = 0;
     B[1][4] = -1. / z * e.fy;
     B[1][5] = y / z_2 * e.fy;
-    if (e.stereo) {
-        B[2][0] = B[0][0] - e.bf * y / z_2;
-        B[2][1] = B[0][1] + e.bf * x / z_2;
-        B[2][2] = B[0][2];
-        B[2][3] = B[0][3];
-        B[2][4] = 0;
-        B[2][5] = B[0][5] - e.bf / z_2;
+    if (D == 3) {
+        B[D - 1][0] = B[0][0] - e.bf * y / z_2;
+        B[D - 1][1] = B[0][1] + e.bf * x / z_2;
+        B[D - 1][2] = B[0][2];
+        B[D - 1][3] = B[0][3];
+        B[D - 1][4] = 0;
+        B[D - 1][5] = B[0][5] - e.bf / z_2;
     }
-    const int D = e.stereo ? 3 : 2;
-    const double rho1 = rho_in[2 * (int64_t)i + 1];
     const double w = rho1 * e.omega;   // robustInformation = rho[1] * information (rho1 = 1 without a kernel)
-    double omr[3];
-    for (int k = 0; k < D; ++k) omr[k] = -(e.omega * err_in[3 * (int64_t)i + k]) * rho1;
-    EdgeOut o;
+    double omr[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) omr[k] = -(e.omega * err[k]) * rho1;
+    double *hpp = out, *hll = out + 36, *hpl = out + 45, *bp = out + 63, *bl = out + 69;   // EdgeOut's fields
+#pragma unroll
     for (int a = 0; a < 3; ++a)
+#pragma unroll
         for (int b = 0; b < 3; ++b) {
             double acc = 0;
+#pragma unroll
             for (int k = 0; k < D; ++k) acc = acc + (A[k][a] * w) * A[k][b];
-            o.hll[3 * a + b] = acc;
+            hll[3 * a + b] = acc;
         }
     const bool pose_free = T.free_idx >= 0;
+#pragma unroll
     for (int a = 0; a < 6; ++a) {
+#pragma unroll
         for (int b = 0; b < 6; ++b) {
             double acc = 0;
             if (pose_free)
+#pragma unroll
                 for (int k = 0; k < D; ++k) acc = acc + (B[k][a] * w) * B[k][b];
-            o.hpp[6 * a + b] = acc;
+            hpp[6 * a + b] = acc;
         }
+#pragma unroll
         for (int c = 0; c < 3; ++c) {   // (A^T W B)^T: pose row a, point column c
             double acc = 0;
             if (pose_free)
+#pragma unroll
                 for (int k = 0; k < D; ++k) acc = acc + (A[k][c] * w) * B[k][a];
-            o.hpl[3 * a + c] = acc;
+            hpl[3 * a + c] = acc;
         }
         double acc = 0;
         if (pose_free)
+#pragma unroll
             for (int k = 0; k < D; ++k) acc = acc + B[k][a] * omr[k];
-        o.bp[a] = acc;
+        bp[a] = acc;
     }
+#pragma unroll
     for (int c = 0; c < 3; ++c) {
         double acc = 0;
+#pragma unroll
         for (int k = 0; k < D; ++k) acc = acc + A[k][c] * omr[k];
-        o.bl[c] = acc;
+        bl[c] = acc;
     }
-    out[i] = o;
+}
+
+__global__ void k_ba_linearize(const Pose *poses, const double *pts, const EdgeD *edges, int ne, const uint8_t *active,
+                               const double *err_in, const double *rho_in, EdgeOut *out) {
+    static_assert(sizeof(EdgeOut) == 72 * sizeof(double), "EdgeOut layout");
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ne || !active[i]) return;
+    const EdgeD e = edges[i];
+    const Pose T = poses[e.cam];
+    double p[3];
+    se3_map(T, pts + 3 * (int64_t)e.point, p);
+    const double rho1 = rho_in[2 * (int64_t)i + 1];
+    const double *err = err_in + 3 * (int64_t)i;
+    double *o = reinterpret_cast<double *>(out + i);
+    if (e.stereo) linearize_edge<3>(e, T, p, rho1, err, o);
+    else linearize_edge<2>(e, T, p, rho1, err, o);
 }
 
 // Vertex blocks: wave per vertex, lane = one matrix entry, edges in order.
@@ -425,18 +451,51 @@ __global__ __launch_bounds__(256) void k_ba_pair_matches(const int2 *pairs, int 
     if (!moffs && lane == 0) counts[pi] = at;
 }
 
+// point -> position in camera f's usable list (the map k_ba_pair_matches reads)
+__global__ void k_ba_cmap(const int32_t *coffs, const int32_t *clist, const int32_t *epoint, int npt, int32_t *cmap) {
+    const int f = blockIdx.x;
+    for (int t = coffs[f] + (int)threadIdx.x; t < coffs[f + 1]; t += blockDim.x)
+        cmap[(int64_t)f * npt + epoint[clist[t]]] = t;
+}
+
+// offs[0..n] = exclusive scan of cnt[0..n) (one workgroup of 1024: a
+// contiguous range per thread, then a scan of the 1024 range sums)
+__global__ __launch_bounds__(1024) void k_ba_scan_counts(const int32_t *cnt, int n, int32_t *offs) {
+    __shared__ int32_t wsum[16];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int per = (n + 1023) / 1024, b = min(tid * per, n), e = min(b + per, n);
+    int32_t sum = 0;
+    for (int i = b; i < e; ++i) sum += cnt[i];
+    int32_t incl = sum;   // inclusive scan over the wave
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int32_t v = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += v;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    int32_t base = 0;
+    for (int k = 0; k < w; ++k) base += wsum[k];
+    int32_t at = base + incl - sum;
+    for (int i = b; i < e; ++i) {
+        offs[i] = at;
+        at += cnt[i];
+    }
+    if (tid == 1023) offs[n] = at;   // (the last thread's range ends at n)
+}
+
 // S_{i1 i2} (+ lambda I on the diagonal blocks) -= sum over the pair's shared
 // points, in point order, of (B Dinv)_{i1} B_{i2}^T, in two passes:
 //  k_ba_pair_terms: every (shared point, block entry) term of every pair,
 //    thread per term (the 3-term dot product in the sequential order);
-//  k_ba_pairs_sum: wave per pair, lane = block entry, subtracts its terms in
-//    point order, streaming them with the loads 16 deep.
+//  k_ba_pairs_sum: workgroup per pair, lane = block entry, subtracts its
+//    terms in point order (ordered_colsum: LDS-staged, double-buffered).
 // Only the subtractions are sequential, so the longest pair (a camera with
 // itself: all its points) costs a chain of dependent adds, not of loads.
-__global__ void k_ba_pair_terms(const int2 *mlist, int64_t nterms, const EdgeOut *eo, const double *bdinv,
-                                double *terms) {
+__global__ void k_ba_pair_terms(const int2 *mlist, int64_t nterms, const int32_t *total, const EdgeOut *eo,
+                                const double *bdinv, double *terms) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= nterms) return;
+    if (idx >= nterms || idx >= 36 * (int64_t)*total) return;   // (launched over a bound; total: the lists' length)
     const int64_t t = idx / 36;
     const int e = (int)(idx - t * 36), r = e / 6, c = e % 6;
     const int2 mt = mlist[t];
@@ -447,32 +506,6 @@ __global__ void k_ba_pair_terms(const int2 *mlist, int64_t nterms, const EdgeOut
     terms[idx] = sj;
 }
 
-__global__ __launch_bounds__(64) void k_ba_pairs_sum(const int2 *pairs, const int32_t *moffs, const double *terms,
-                                                     const double *Hpp, double lambda, int nf, double *S) {
-    const int pi = blockIdx.x, lane = threadIdx.x;
-    if (lane >= 36) return;
-    const int i1 = pairs[pi].x, i2 = pairs[pi].y, r = lane / 6, c = lane % 6;
-    double acc = 0;
-    if (i1 == i2) {
-        acc = Hpp[36 * (int64_t)i1 + lane];
-        if (r == c) acc = acc + lambda;
-    }
-    const double *tp = terms + lane;
-    int t = moffs[pi];
-    const int te = moffs[pi + 1];
-    for (; t + 16 <= te; t += 16) {
-        double x[16];
-#pragma unroll
-        for (int q = 0; q < 16; ++q) x[q] = tp[36 * (int64_t)(t + q)];
-#pragma unroll
-        for (int q = 0; q < 16; ++q) acc = acc - x[q];
-    }
-    for (; t < te; ++t) acc = acc - tp[36 * (int64_t)t];
-    const int n = 6 * nf;
-    S[(int64_t)(6 * i1 + r) * n + 6 * i2 + c] = acc;
-    S[(int64_t)(6 * i2 + c) * n + 6 * i1 + r] = acc;   // mirror (the solver reads the full matrix)
-}
-
 // Ordered sums per vertex, out[v][f] = sum over t in [offs[v], offs[v+1]) of
 // rec[list[t]][field f] in list order (edges with pred[e] == 0 add nothing),
 // in two passes:
@@ -480,8 +513,8 @@ __global__ __launch_bounds__(64) void k_ba_pairs_sum(const int2 *pairs, const in
 //    list order (+0.0 for a skipped edge: the running sum starts at +0.0 and
 //    never becomes -0.0 under round-to-nearest, so adding +0.0 leaves it as it
 //    is);
-//  k_ba_stream_sums: wave per vertex, lane = field, adds its column in list
-//    order with the loads 16 deep -- a chain of dependent adds, no dependent
+//  k_ba_stream_sums: workgroup per vertex, lane = field, adds its column in
+//    list order (ordered_colsum) -- a chain of dependent adds, no dependent
 //    loads.
 // minus != nullptr: out = minus - sum (the reduced right-hand side).
 // NF fields per record; LAYOUT 1: EdgeOut's hpp (36) then bp (6), 0: record
@@ -497,28 +530,125 @@ __global__ void k_ba_gather_rows(const double *rec, int stride, const int32_t *l
     out[idx] = (pred && !pred[e]) ? 0.0 : rec[(int64_t)e * stride + off];
 }
 
-template <int NF>
-__global__ __launch_bounds__(64) void k_ba_stream_sums(const double *rows, const int32_t *offs, const double *minus,
-                                                       double *out_a, int na, double *out_b) {
-    const int v = blockIdx.x, lane = threadIdx.x;
-    if (lane >= NF) return;
-    const double *col = rows + lane;
-    double acc = 0;
-    int t = offs[v];
-    const int te = offs[v + 1];
-    for (; t + 16 <= te; t += 16) {
-        double x[16];
+// The ordered column sums of one vertex's rows (contiguous: nrows x NF
+// doubles at base), acc_f = init_f (+|-) row_0[f] (+|-) row_1[f] ... in row
+// order, in lane f < NF of wave 0.  One workgroup of kSumThreads per vertex
+// streams the rows through two LDS buffers of kSumElems: every thread loads
+// its share of chunk k + 1 into registers, wave 0 adds chunk k from LDS, then
+// the registers go to the other buffer -- the chain of dependent adds runs
+// while the next chunk is in flight (a wave alone kept too few loads in flight
+// to cover the latency).
+constexpr int kSumThreads = 1024, kSumElems = 8192, kSumPer = kSumElems / kSumThreads;
+constexpr size_t kSumLds = 2 * kSumElems * sizeof(double);
+template <int NF, bool SUB>
+__device__ double ordered_colsum(const double *base, int nrows, double acc, double *buf) {
+    constexpr int kRows = kSumElems / NF, kE = kRows * NF;   // whole rows per chunk
+    const int tid = threadIdx.x, total = nrows * NF, nch = (nrows + kRows - 1) / kRows;
+    double r[kSumPer];
+    auto fetch = [&](int k) {
 #pragma unroll
-        for (int q = 0; q < 16; ++q) x[q] = col[(int64_t)(t + q) * NF];
+        for (int j = 0; j < kSumPer; ++j) {
+            const int i = tid + j * kSumThreads;
+            r[j] = (i < kE && k * kE + i < total) ? base[(int64_t)k * kE + i] : 0.0;
+        }
+    };
+    auto put = [&](int k) {
+        double *d = buf + (k & 1) * kSumElems;
 #pragma unroll
-        for (int q = 0; q < 16; ++q) acc = acc + x[q];
+        for (int j = 0; j < kSumPer; ++j) {
+            const int i = tid + j * kSumThreads;
+            if (i < kE) d[i] = r[j];
+        }
+    };
+    if (nch) {
+        fetch(0);
+        put(0);
     }
-    for (; t < te; ++t) acc = acc + col[(int64_t)t * NF];
+    __syncthreads();
+    for (int k = 0; k < nch; ++k) {
+        if (k + 1 < nch) fetch(k + 1);
+        if (tid < NF) {
+            const double *src = buf + (k & 1) * kSumElems + tid;
+            const int nr = min(kRows, nrows - k * kRows);
+            int q = 0;
+            if (nr >= 8) {   // the reads of rows q + 8 .. q + 15 go out before the adds of rows q .. q + 7
+                double a[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) a[u] = src[u * NF];
+                for (; q + 16 <= nr; q += 8) {
+                    double b[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) b[u] = src[(q + 8 + u) * NF];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) acc = SUB ? acc - a[u] : acc + a[u];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) a[u] = b[u];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc = SUB ? acc - a[u] : acc + a[u];
+                q += 8;
+            }
+            for (; q < nr; ++q) acc = SUB ? acc - src[q * NF] : acc + src[q * NF];
+        }
+        if (k + 1 < nch) put(k + 1);
+        __syncthreads();
+    }
+    return acc;
+}
+
+// S_{i1 i2} (+ lambda I on the diagonal blocks) - the pair's terms in point
+// order, written with its mirror (the solver reads the full matrix)
+__global__ __launch_bounds__(kSumThreads) void k_ba_pairs_sum(const int2 *pairs, const int32_t *moffs,
+                                                              const double *terms, const double *Hpp, double lambda,
+                                                              int nf, double *S) {
+    extern __shared__ double sbuf[];
+    const int pi = blockIdx.x, lane = threadIdx.x;
+    const int i1 = pairs[pi].x, i2 = pairs[pi].y, r = lane / 6, c = lane % 6;
+    double acc = 0;
+    if (i1 == i2 && lane < 36) {
+        acc = Hpp[36 * (int64_t)i1 + lane];
+        if (r == c) acc = acc + lambda;
+    }
+    const int t0 = moffs[pi];
+    acc = ordered_colsum<36, true>(terms + 36 * (int64_t)t0, moffs[pi + 1] - t0, acc, sbuf);
+    if (lane >= 36) return;
+    const int n = 6 * nf;
+    S[(int64_t)(6 * i1 + r) * n + 6 * i2 + c] = acc;
+    S[(int64_t)(6 * i2 + c) * n + 6 * i1 + r] = acc;
+}
+
+// out[v] = (minus[v] -) the ordered sum of the vertex's rows; fields [0, na)
+// to out_a, the rest to out_b
+template <int NF>
+__global__ __launch_bounds__(kSumThreads) void k_ba_stream_sums(const double *rows, const int32_t *offs,
+                                                                const double *minus, double *out_a, int na,
+                                                                double *out_b) {
+    extern __shared__ double sbuf[];
+    const int v = blockIdx.x, lane = threadIdx.x;
+    const int t0 = offs[v];
+    const double acc = ordered_colsum<NF, false>(rows + NF * (int64_t)t0, offs[v + 1] - t0, 0.0, sbuf);
+    if (lane >= NF) return;
     if (lane < na) out_a[(int64_t)v * na + lane] = minus ? minus[(int64_t)v * na + lane] - acc : acc;
     else out_b[(int64_t)v * (NF - na) + lane - na] = acc;
 }
 
+// (the ordered-sum kernels take 128 KB of LDS: raised once per kernel)
+template <typename K>
+bool sum_lds(K kernel) {
+    return hipFuncSetAttribute(reinterpret_cast<const void *>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)kSumLds) == hipSuccess;
+}
+bool sums_ready() {
+    static const bool ok = sum_lds(k_ba_pairs_sum) && sum_lds(k_ba_stream_sums<6>) && sum_lds(k_ba_stream_sums<42>);
+    return ok;
+}
 
+__global__ void k_ba_restore(Pose *poses, int ncam, double *pts, int npt, const Pose *pose_bk, const double *pts_bk) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < ncam) poses[i] = pose_bk[i];
+    if (i < npt)
+        for (int k = 0; k < 3; ++k) pts[3 * (int64_t)i + k] = pts_bk[3 * (int64_t)i + k];
+}
 
 // Dense Cholesky S = L L^T (lower, in place, column by column) and the two
 // triangular solves for x; one workgroup.  ok = 0 if S is not positive definite.
@@ -779,6 +909,22 @@ __global__ __launch_bounds__(512) void k_ba_chol_lds(const double *S, int n, con
     if (clk && lane == 0) { clk[3] += __builtin_amdgcn_s_memtime() - c_t; clk[4] += 1; }
 }
 
+// the caller's edges as EdgeD (float -> double: exact) and the edge -> point list
+__global__ void k_ba_edges(const orbx_ba_edge *in, int ne, double th_mono, double th_stereo, EdgeD *out,
+                           int32_t *epoint) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= ne) return;
+    const orbx_ba_edge s = in[e];
+    EdgeD d;
+    d.cam = s.cam; d.point = s.point; d.stereo = s.ur >= 0 ? 1 : 0; d.pad = 0;
+    d.obs[0] = s.u; d.obs[1] = s.v; d.obs[2] = d.stereo ? s.ur : 0.0;
+    d.omega = s.inv_sigma2;
+    d.fx = s.fx; d.fy = s.fy; d.cx = s.cx; d.cy = s.cy; d.bf = s.bf;
+    d.delta = d.stereo ? th_stereo : th_mono;
+    out[e] = d;
+    epoint[e] = s.point;
+}
+
 // xl = Dinv (bl - sum over the point's usable edges (camera order) of B^T xp)
 __global__ void k_ba_backsub(const double *dinv, const double *bl, int npt, const EdgeOut *eo, const int32_t *offs,
                              const int32_t *list, const uint8_t *usable, const EdgeD *edges, const Pose *poses,
@@ -807,10 +953,17 @@ __global__ void k_ba_backsub(const double *dinv, const double *bl, int npt, cons
 }
 
 // SE3Quat::exp(update) * estimate (se3quat.h:223-258, :104-110); points += dx
+// bk (nullable): the estimate before the step is saved first (the trial's
+// push(); a rejected trial that ran the step restores it with k_ba_restore)
 __global__ void k_ba_update(Pose *poses, int ncam, double *pts, int npt, const double *xp, const double *xl,
-                            const int *gate) {
+                            const int *gate, Pose *pose_bk, double *pts_bk) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (gate && !*gate) return;
+    if (pose_bk) {
+        if (i < ncam) pose_bk[i] = poses[i];
+        if (i < npt)
+            for (int k = 0; k < 3; ++k) pts_bk[3 * (int64_t)i + k] = pts[3 * (int64_t)i + k];
+    }
     if (i < npt)
         for (int k = 0; k < 3; ++k) pts[3 * (int64_t)i + k] = pts[3 * (int64_t)i + k] + xl[3 * (int64_t)i + k];
     if (i < ncam && poses[i].free_idx >= 0) {
@@ -894,7 +1047,7 @@ T *carve(uint8_t *&p, size_t n) {
 struct Graph {
     int ncam, npt, ne, nf;
     std::vector<Pose> poses;
-    std::vector<EdgeD> edges;
+    const orbx_ba_edge *raw;   // the caller's edges (converted to EdgeD on the device)
     std::vector<int32_t> coffs, clist, poffs, plist, epoint;   // camera lists: usable edges by point; point lists: edges by camera
 };
 
@@ -974,7 +1127,6 @@ public:
     double chi_sum_host() const;
     double max_diag_host() const;
     double scale_host(double lambda) const;
-    int push();
     int pop();
     int download(double *pts, std::vector<double> &chi2, std::vector<uint8_t> &front);
     // (the buffers belong to the workspace)
@@ -986,6 +1138,7 @@ public:
     Pose *d_pose = nullptr, *d_pose_bk = nullptr;
     double *d_pts = nullptr, *d_pts_bk = nullptr;
     EdgeD *d_edges = nullptr;
+    orbx_ba_edge *d_raw = nullptr;
     uint8_t *d_active = nullptr, *d_usable = nullptr, *d_front = nullptr;
     double *d_err = nullptr, *d_chi2 = nullptr, *d_rho = nullptr;
     EdgeOut *d_eo = nullptr;
@@ -1001,44 +1154,56 @@ public:
     std::vector<uint8_t> act_;
     std::vector<int32_t> cv_offs_, cv_list_;   // all edges per free camera (reduce), edge order
     double *d_rho0 = nullptr;                  // rho[0] per edge, contiguous
-    int32_t *d_moffs = nullptr;                // camera pairs' shared-point lists (k_ba_pair_matches)
+    int32_t *d_moffs = nullptr, *d_mcnt = nullptr;   // camera pairs' shared-point lists (k_ba_pair_matches)
     int2 *d_mlist = nullptr;
     double *d_terms = nullptr;                 // 36 per shared point of each pair (k_ba_pair_terms)
     double *d_rows = nullptr;                  // records gathered in list order (k_ba_gather_rows), 42 per edge
     int nusable_ = 0;
-    int64_t nmatch_ = 0;
+    int64_t nmatch_ = 0, mbound_ = 0;   // nmatch_: capacity the shared-point kernels are launched over
     uint8_t *hbuf_ = nullptr;                  // pinned readbacks
-    double *h_rho0 = nullptr, *h_x = nullptr, *h_b = nullptr, *h_hpp = nullptr, *h_hll = nullptr;
+    double *h_rho0 = nullptr, *h_x = nullptr, *h_bp = nullptr, *h_bl = nullptr, *h_hpp = nullptr, *h_hll = nullptr;
+    size_t span_ = 0;      // bytes from d_ok to the end of d_bl
+    bool s_zero_ = false;  // d_S's non-pair blocks are zero
     int *h_ok = nullptr;
+    uint8_t *h_stage = nullptr;                // set_active's uploads: flags, then h_coffs_ | clist
+    int32_t *h_coffs_ = nullptr;
 };
 
 int BA::alloc() {
     const Graph &g = g_;
     const size_t ne = std::max(g.ne, 1), nc = std::max(g.ncam, 1), np = std::max(g.npt, 1), nf = std::max(g.nf, 1);
-    // the camera-pair list: free cameras sharing a point (structure of the reduced system)
-    // (a dense nf x nf mark table: nf <= 170; pairs in lexicographic order)
-    std::vector<uint8_t> mark((size_t)g.nf * g.nf, 0);
-    std::vector<int> fcams;
+    // the camera-pair list: free cameras sharing a point (structure of the
+    // reduced system), from per-camera bitmasks of the cameras it shares a
+    // point with (nf <= 170: three words); pairs in lexicographic order.
+    // mbound_: the shared-point list length with every edge active (a bound
+    // for any active subset)
+    constexpr int kW = 3;
+    std::vector<uint64_t> rows((size_t)std::max(g.nf, 1) * kW, 0);
+    mbound_ = 0;
     for (int p = 0; p < g.npt; ++p) {
-        fcams.clear();
+        uint64_t pm[kW] = {0, 0, 0};
+        int64_t k = 0;
         for (int t = g.poffs[p]; t < g.poffs[p + 1]; ++t) {
-            const int f = g.poses[g.edges[g.plist[t]].cam].free_idx;
-            if (f >= 0) fcams.push_back(f);
+            const int f = g.poses[g.raw[g.plist[t]].cam].free_idx;
+            if (f >= 0) { pm[f >> 6] |= 1ull << (f & 63); ++k; }
         }
-        for (size_t a = 0; a < fcams.size(); ++a)
-            for (size_t b = 0; b < fcams.size(); ++b)
-                if (fcams[a] <= fcams[b]) mark[(size_t)fcams[a] * g.nf + fcams[b]] = 1;
+        mbound_ += k * (k + 1) / 2;
+        if (!k) continue;
+        for (int t = g.poffs[p]; t < g.poffs[p + 1]; ++t) {
+            const int f = g.poses[g.raw[g.plist[t]].cam].free_idx;
+            if (f >= 0)
+                for (int w = 0; w < kW; ++w) rows[(size_t)f * kW + w] |= pm[w];
+        }
     }
-    for (int f = 0; f < g.nf; ++f) mark[(size_t)f * g.nf + f] = 1;
     std::vector<int2> pairs;
     for (int a = 0; a < g.nf; ++a)
         for (int b = a; b < g.nf; ++b)
-            if (mark[(size_t)a * g.nf + b]) pairs.push_back(make_int2(a, b));
+            if (b == a || (rows[(size_t)a * kW + (b >> 6)] >> (b & 63) & 1)) pairs.push_back(make_int2(a, b));
     npairs = (int)pairs.size();
     // all edges of each free camera in edge order (for Hpp / bp)
     cv_offs_.assign(g.nf + 1, 0);
     for (int e = 0; e < g.ne; ++e) {
-        const int f = g.poses[g.edges[e].cam].free_idx;
+        const int f = g.poses[g.raw[e].cam].free_idx;
         if (f >= 0) ++cv_offs_[f + 1];
     }
     for (int f = 0; f < g.nf; ++f) cv_offs_[f + 1] += cv_offs_[f];
@@ -1046,7 +1211,7 @@ int BA::alloc() {
     {
         std::vector<int> fill(cv_offs_.begin(), cv_offs_.end() - 1);
         for (int e = 0; e < g.ne; ++e) {
-            const int f = g.poses[g.edges[e].cam].free_idx;
+            const int f = g.poses[g.raw[e].cam].free_idx;
             if (f >= 0) cv_list_[fill[f]++] = e;
         }
     }
@@ -1055,7 +1220,7 @@ int BA::alloc() {
                          8 * ne * 6 + sizeof(EdgeOut) * ne + 4 * (nf + 1 + ne + np + 1 + ne + ne + nf + 1 + ne) +
                          sizeof(int2) * std::max(npairs, 1) + 8 * (36 * nf + 6 * nf + 9 * np + 3 * np + 9 * np +
                                                                    18 * ne + 6 * ne + n * n + n + n + 3 * np) +
-                         4 * nf * np + 8 * ne + 8 * 3 * np + 8 * 42 * ne + 256 * 5;
+                         4 * nf * np + 8 * ne + 8 * 3 * np + 8 * 42 * ne + sizeof(orbx_ba_edge) * ne + 256 * 6;
     if (ws_.cap < bytes) {
         (void)hipStreamSynchronize(st_);
         if (ws_.dev) (void)hipFree(ws_.dev);
@@ -1076,19 +1241,25 @@ int BA::alloc() {
     d_poffs = carve<int32_t>(p, np + 1); d_plist = carve<int32_t>(p, ne); d_epoint = carve<int32_t>(p, ne);
     d_cvoffs = carve<int32_t>(p, nf + 1); d_cvlist = carve<int32_t>(p, ne);
     d_pairs = carve<int2>(p, std::max(npairs, 1));
-    d_Hpp = carve<double>(p, 36 * nf); d_bp = carve<double>(p, 6 * nf);
-    d_Hll = carve<double>(p, 9 * np); d_bl = carve<double>(p, 3 * np); d_dinv = carve<double>(p, 9 * np);
+    d_Hpp = carve<double>(p, 36 * nf);
+    d_Hll = carve<double>(p, 9 * np); d_dinv = carve<double>(p, 9 * np);
     d_bdinv = carve<double>(p, 18 * ne); d_bdb = carve<double>(p, 6 * ne);
-    d_S = carve<double>(p, n * n); d_bs = carve<double>(p, n); d_x = carve<double>(p, n + 3 * np);
+    d_S = carve<double>(p, n * n); d_bs = carve<double>(p, n);
+    // a trial's readback, one span mirrored in the pinned buffer: ok, rho0, x, bp, bl
     d_ok = carve<int>(p, 1);
-    d_cmap = carve<int32_t>(p, nf * np);
     d_rho0 = carve<double>(p, ne);
+    d_x = carve<double>(p, n + 3 * np);
+    d_bp = carve<double>(p, 6 * nf);
+    d_bl = carve<double>(p, 3 * np);
+    span_ = (size_t)(p - reinterpret_cast<uint8_t *>(d_ok));
+    d_cmap = carve<int32_t>(p, nf * np);
     d_db = carve<double>(p, 3 * np);
     d_rows = carve<double>(p, 42 * ne);
+    d_raw = carve<orbx_ba_edge>(p, ne);
     if ((size_t)(p - buf_) > bytes) return ORBX_ENOMEM;
     {
         const size_t m = n + 3 * np;
-        const size_t hb = 8 * (ne + 2 * m + 36 * nf + 9 * np) + 64 + 256 * 6;
+        const size_t hb = 8 * (ne + 2 * m + 36 * nf + 9 * np) + 64 + 2 * ne + 4 * (nf + 1 + ne) + 256 * 10;
         if (ws_.hcap < hb) {
             if (ws_.host) (void)hipHostFree(ws_.host);
             ws_.host = nullptr;
@@ -1099,19 +1270,42 @@ int BA::alloc() {
         }
         hbuf_ = ws_.host;
         uint8_t *h = hbuf_;
-        h_rho0 = carve<double>(h, ne); h_x = carve<double>(h, m); h_b = carve<double>(h, m);
-        h_hpp = carve<double>(h, 36 * nf); h_hll = carve<double>(h, 9 * np); h_ok = carve<int>(h, 1);
+        h_ok = carve<int>(h, 1); h_rho0 = carve<double>(h, ne); h_x = carve<double>(h, m);
+        h_bp = carve<double>(h, 6 * nf); h_bl = carve<double>(h, 3 * np);
+        h_hpp = carve<double>(h, 36 * nf); h_hll = carve<double>(h, 9 * np);
+        h_stage = carve<uint8_t>(h, 2 * ne); h_coffs_ = carve<int32_t>(h, nf + 1 + ne);
         if ((size_t)(h - hbuf_) > hb) return ORBX_ENOMEM;
     }
+    // the pairs' shared-point lists (set_active), sized for every edge active
+    if (!grow_dev(ws_.moffs, ws_.moffs_cap, 2 * ((size_t)npairs + 1))) return ORBX_ENOMEM;
+    d_moffs = ws_.moffs;
+    d_mcnt = ws_.moffs + npairs + 1;
+    if (mbound_ > ws_.mcap) {
+        for (void *x : {(void *)ws_.mlist, (void *)ws_.terms})
+            if (x) (void)hipFree(x);
+        ws_.mlist = nullptr;
+        ws_.terms = nullptr;
+        ws_.mcap = 0;
+        const size_t m = (size_t)mbound_ * 9 / 8;
+        if (hipMalloc(reinterpret_cast<void **>(&ws_.mlist), sizeof(int2) * m) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void **>(&ws_.terms), 36 * sizeof(double) * m) != hipSuccess)
+            return ORBX_ENOMEM;
+        ws_.mcap = (int64_t)m;
+    }
+    d_mlist = ws_.mlist;
+    d_terms = ws_.terms;
     auto up = [&](void *d, const void *h, size_t b) {
         return b == 0 || hipMemcpyAsync(d, h, b, hipMemcpyHostToDevice, st_) == hipSuccess;
     };
-    std::vector<int32_t> ep(g.ne);
-    for (int e = 0; e < g.ne; ++e) ep[e] = g.edges[e].point;
-    if (!up(d_edges, g.edges.data(), sizeof(EdgeD) * g.ne) || !up(d_poffs, g.poffs.data(), 4 * (g.npt + 1)) ||
-        !up(d_plist, g.plist.data(), 4 * g.ne) || !up(d_epoint, ep.data(), 4 * g.ne) ||
-        !up(d_pairs, pairs.data(), sizeof(int2) * npairs) || !up(d_cvoffs, cv_offs_.data(), 4 * (g.nf + 1)) ||
-        !up(d_cvlist, cv_list_.data(), 4 * cv_list_.size()) || hipStreamSynchronize(st_) != hipSuccess)
+    // the caller's 44-byte edges go up as they are; EdgeD (96 bytes) and the
+    // edge -> point list are made on the device
+    if (!up(d_raw, g.raw, sizeof(orbx_ba_edge) * g.ne)) return ORBX_EIO;
+    if (g.ne)
+        hipLaunchKernelGGL(k_ba_edges, dim3((g.ne + 255) / 256), dim3(256), 0, st_, d_raw, g.ne,
+                           (double)(float)std::sqrt(5.991), (double)(float)std::sqrt(7.815), d_edges, d_epoint);
+    if (hipGetLastError() != hipSuccess || !up(d_poffs, g.poffs.data(), 4 * (g.npt + 1)) ||
+        !up(d_plist, g.plist.data(), 4 * g.ne) || !up(d_pairs, pairs.data(), sizeof(int2) * npairs) ||
+        !up(d_cvoffs, cv_offs_.data(), 4 * (g.nf + 1)) || !up(d_cvlist, cv_list_.data(), 4 * cv_list_.size()))
         return ORBX_EIO;
     return ORBX_OK;
 }
@@ -1123,76 +1317,60 @@ int BA::upload(const double *pts) {
     return ORBX_OK;
 }
 
-// active edges; usable = active with a free camera, sorted per camera by point
+// active edges; usable = active with a free camera, sorted per camera by
+// point.  Host: the flags and per-camera lists, written into pinned staging
+// (the caller synchronises the stream before the next set_active); device:
+// the point -> list-position map, the pairs' shared-point counts, their scan
+// and the lists.  Nothing waits here.
 void BA::set_active(const std::vector<uint8_t> &act) {
     act_ = act;
+    s_zero_ = false;
     const Graph &g = g_;
-    std::vector<uint8_t> usable(g.ne);
-    for (int e = 0; e < g.ne; ++e) usable[e] = act[e] && g.poses[g.edges[e].cam].free_idx >= 0;
-    std::vector<int32_t> coffs(g.nf + 1, 0), clist;
-    for (int e = 0; e < g.ne; ++e)
-        if (usable[e]) ++coffs[g.poses[g.edges[e].cam].free_idx + 1];
-    for (int f = 0; f < g.nf; ++f) coffs[f + 1] += coffs[f];
-    clist.assign(std::max(coffs[g.nf], 1), 0);
-    std::vector<int> fill(coffs.begin(), coffs.end() - 1);
-    // point-major walk: each camera's list comes out in ascending point order
-    for (int p = 0; p < g.npt; ++p)
+    uint8_t *h_act = h_stage, *h_us = h_stage + g.ne;
+    int32_t *h_coffs = h_coffs_, *h_clist = h_coffs_ + g.nf + 1;
+    std::fill(h_coffs, h_coffs + g.nf + 1, 0);
+    for (int e = 0; e < g.ne; ++e) {
+        const int f = g.poses[g.raw[e].cam].free_idx;
+        h_act[e] = act[e];
+        h_us[e] = act[e] && f >= 0;
+        if (h_us[e]) ++h_coffs[f + 1];
+    }
+    for (int f = 0; f < g.nf; ++f) h_coffs[f + 1] += h_coffs[f];
+    std::vector<int> fill(h_coffs, h_coffs + std::max(g.nf, 1));
+    // point-major walk: each camera's list comes out in ascending point order;
+    // a camera seeing a point twice (adjacent: plist is by camera) needs the
+    // merge kernel instead of the map
+    use_map = true;
+    for (int p = 0; p < g.npt; ++p) {
+        int last = -1;
         for (int t = g.poffs[p]; t < g.poffs[p + 1]; ++t) {
             const int e = g.plist[t];
-            if (usable[e]) clist[fill[g.poses[g.edges[e].cam].free_idx]++] = e;
-        }
-    // point -> list position per free camera, for k_ba_pair_matches
-    std::vector<int32_t> cmap((size_t)g.nf * g.npt, -1);
-    use_map = true;
-    for (int f = 0; f < g.nf && use_map; ++f)
-        for (int t = coffs[f]; t < coffs[f + 1]; ++t) {
-            int32_t &m = cmap[(size_t)f * g.npt + g.edges[clist[t]].point];
-            if (m >= 0) { use_map = false; break; }   // a point seen twice by one camera: merge kernel
-            m = t;
-        }
-    (void)hipMemcpyAsync(d_active, act.data(), g.ne, hipMemcpyHostToDevice, st_);
-    (void)hipMemcpyAsync(d_usable, usable.data(), g.ne, hipMemcpyHostToDevice, st_);
-    (void)hipMemcpyAsync(d_coffs, coffs.data(), 4 * (g.nf + 1), hipMemcpyHostToDevice, st_);
-    (void)hipMemcpyAsync(d_clist, clist.data(), 4 * clist.size(), hipMemcpyHostToDevice, st_);
-    nusable_ = coffs[g.nf];
-    if (use_map && !cmap.empty())
-        (void)hipMemcpyAsync(d_cmap, cmap.data(), 4 * cmap.size(), hipMemcpyHostToDevice, st_);
-    if (use_map && npairs > 0) {   // the pairs' shared-point lists: count, scan on the host, fill
-        if (!grow_dev(ws_.moffs, ws_.moffs_cap, (size_t)npairs + 1)) use_map = false;
-        d_moffs = ws_.moffs;
-        std::vector<int32_t> cnt(npairs), offs(npairs + 1, 0);
-        if (use_map) {
-            hipLaunchKernelGGL(k_ba_pair_matches, dim3((npairs + 3) / 4), dim3(256), 0, st_, d_pairs, npairs, d_coffs,
-                               d_clist, d_epoint, d_cmap, g.npt, nullptr, d_moffs, nullptr);
-            if (hipMemcpyAsync(cnt.data(), d_moffs, 4 * (size_t)npairs, hipMemcpyDeviceToHost, st_) != hipSuccess ||
-                hipStreamSynchronize(st_) != hipSuccess)
-                use_map = false;
-        }
-        for (int k = 0; k < npairs && use_map; ++k) offs[k + 1] = offs[k] + cnt[k];
-        if (use_map && offs[npairs] > ws_.mcap) {
-            (void)hipStreamSynchronize(st_);
-            for (void *x : {(void *)ws_.mlist, (void *)ws_.terms})
-                if (x) (void)hipFree(x);
-            ws_.mlist = nullptr;
-            ws_.terms = nullptr;
-            ws_.mcap = 0;
-            const size_t m = (size_t)std::max(offs[npairs], 1) * 5 / 4;
-            if (hipMalloc(reinterpret_cast<void **>(&ws_.mlist), sizeof(int2) * m) == hipSuccess &&
-                hipMalloc(reinterpret_cast<void **>(&ws_.terms), 36 * sizeof(double) * m) == hipSuccess)
-                ws_.mcap = (int64_t)m;
-            else
-                use_map = false;
-        }
-        d_mlist = ws_.mlist;
-        d_terms = ws_.terms;
-        nmatch_ = use_map ? offs[npairs] : 0;
-        if (use_map) {
-            (void)hipMemcpyAsync(d_moffs, offs.data(), 4 * (size_t)(npairs + 1), hipMemcpyHostToDevice, st_);
-            hipLaunchKernelGGL(k_ba_pair_matches, dim3((npairs + 3) / 4), dim3(256), 0, st_, d_pairs, npairs, d_coffs,
-                               d_clist, d_epoint, d_cmap, g.npt, d_moffs, nullptr, d_mlist);
+            if (!h_us[e]) continue;
+            const int f = g.poses[g.raw[e].cam].free_idx;
+            if (f == last) use_map = false;
+            last = f;
+            h_clist[fill[f]++] = e;
         }
     }
-    (void)hipStreamSynchronize(st_);
+    nusable_ = h_coffs[g.nf];
+    (void)hipMemcpyAsync(d_active, h_act, g.ne, hipMemcpyHostToDevice, st_);
+    (void)hipMemcpyAsync(d_usable, h_us, g.ne, hipMemcpyHostToDevice, st_);
+    (void)hipMemcpyAsync(d_coffs, h_coffs, 4 * (size_t)(g.nf + 1), hipMemcpyHostToDevice, st_);
+    if (nusable_) (void)hipMemcpyAsync(d_clist, h_clist, 4 * (size_t)nusable_, hipMemcpyHostToDevice, st_);
+    nmatch_ = 0;
+    if (!use_map || !g.nf) return;
+    if (g.npt) {
+        (void)hipMemsetAsync(d_cmap, 0xFF, 4 * (size_t)g.nf * g.npt, st_);
+        hipLaunchKernelGGL(k_ba_cmap, dim3(g.nf), dim3(256), 0, st_, d_coffs, d_clist, d_epoint, g.npt, d_cmap);
+    }
+    if (npairs > 0) {   // the pairs' shared-point lists: count, scan, fill
+        hipLaunchKernelGGL(k_ba_pair_matches, dim3((npairs + 3) / 4), dim3(256), 0, st_, d_pairs, npairs, d_coffs,
+                           d_clist, d_epoint, d_cmap, g.npt, nullptr, d_mcnt, nullptr);
+        hipLaunchKernelGGL(k_ba_scan_counts, dim3(1), dim3(1024), 0, st_, d_mcnt, npairs, d_moffs);
+        hipLaunchKernelGGL(k_ba_pair_matches, dim3((npairs + 3) / 4), dim3(256), 0, st_, d_pairs, npairs, d_coffs,
+                           d_clist, d_epoint, d_cmap, g.npt, d_moffs, nullptr, d_mlist);
+        nmatch_ = mbound_;
+    }
 }
 
 int BA::errors(bool robust, double *chi_sum) {
@@ -1221,7 +1399,8 @@ int BA::build() {
         if (nl)
             hipLaunchKernelGGL((k_ba_gather_rows<42, 1>), dim3((unsigned)(((int64_t)nl * 42 + 255) / 256)), dim3(256), 0,
                                st_, reinterpret_cast<const double *>(d_eo), kEo, d_cvlist, nl, d_active, d_rows);
-        hipLaunchKernelGGL((k_ba_stream_sums<42>), dim3(g.nf), dim3(64), 0, st_, d_rows, d_cvoffs, nullptr, d_Hpp, 36,
+        if (!sums_ready()) return ORBX_EIO;
+        hipLaunchKernelGGL((k_ba_stream_sums<42>), dim3(g.nf), dim3(kSumThreads), kSumLds, st_, d_rows, d_cvoffs, nullptr, d_Hpp, 36,
                            d_bp);
     }
     if (g.npt) hipLaunchKernelGGL(k_ba_reduce, dim3((g.npt + 3) / 4), dim3(256), 0, st_, d_eo, d_poffs, d_plist,
@@ -1262,8 +1441,8 @@ int BA::solve(double lambda, int *ok) {
             const int64_t nterms = 36 * nmatch_;
             if (nterms)
                 hipLaunchKernelGGL(k_ba_pair_terms, dim3((unsigned)((nterms + 255) / 256)), dim3(256), 0, st_, d_mlist,
-                                   nterms, d_eo, d_bdinv, d_terms);
-            hipLaunchKernelGGL(k_ba_pairs_sum, dim3(npairs), dim3(64), 0, st_, d_pairs, d_moffs, d_terms, d_Hpp,
+                                   nterms, d_moffs + npairs, d_eo, d_bdinv, d_terms);
+            hipLaunchKernelGGL(k_ba_pairs_sum, dim3(npairs), dim3(kSumThreads), kSumLds, st_, d_pairs, d_moffs, d_terms, d_Hpp,
                                lambda, g.nf, d_S);
         }
         else
@@ -1273,7 +1452,7 @@ int BA::solve(double lambda, int *ok) {
         if (nusable_)
             hipLaunchKernelGGL((k_ba_gather_rows<6, 0>), dim3((unsigned)(((int64_t)nusable_ * 6 + 255) / 256)),
                                dim3(256), 0, st_, d_bdb, 6, d_clist, nusable_, nullptr, d_rows);
-        hipLaunchKernelGGL((k_ba_stream_sums<6>), dim3(g.nf), dim3(64), 0, st_, d_rows, d_coffs, d_bp, d_bs, 6,
+        hipLaunchKernelGGL((k_ba_stream_sums<6>), dim3(g.nf), dim3(kSumThreads), kSumLds, st_, d_rows, d_coffs, d_bp, d_bs, 6,
                            nullptr);
         // (blocks of camera pairs without a shared point stay as the memset left them)
         if (n <= kCholLds) {
@@ -1313,7 +1492,7 @@ double BA::scale(double lambda) {
 int BA::update() {
     const int n = std::max(g_.ncam, g_.npt);
     hipLaunchKernelGGL(k_ba_update, dim3((n + 255) / 256), dim3(256), 0, st_, d_pose, g_.ncam, d_pts, g_.npt, d_x,
-                       d_x + 6 * g_.nf, nullptr);
+                       d_x + 6 * g_.nf, nullptr, nullptr, nullptr);
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
 }
 
@@ -1328,7 +1507,12 @@ int BA::errors_async(bool robust, const int *gate) {
 int BA::solve_async(double lambda) {
     const Graph &g = g_;
     const int n = 6 * g.nf;
-    if (n && hipMemsetAsync(d_S, 0, 8 * (size_t)n * n, st_) != hipSuccess) return ORBX_EIO;
+    // every solve rewrites the pair blocks; the others stay zero unless the
+    // in-place factor (n > kCholLds) overwrote them
+    if (n && (n > kCholLds || !s_zero_)) {
+        if (hipMemsetAsync(d_S, 0, 8 * (size_t)n * n, st_) != hipSuccess) return ORBX_EIO;
+        s_zero_ = true;
+    }
     if (!g.nf && hipMemsetAsync(d_ok, 0xFF, 4, st_) != hipSuccess) return ORBX_EIO;   // (nothing to factor: ok)
     if (g.npt) {
         hipLaunchKernelGGL(k_ba_point, dim3((g.npt + 255) / 256), dim3(256), 0, st_, d_Hll, d_bl, g.npt, lambda, d_dinv,
@@ -1342,8 +1526,8 @@ int BA::solve_async(double lambda) {
             const int64_t nterms = 36 * nmatch_;
             if (nterms)
                 hipLaunchKernelGGL(k_ba_pair_terms, dim3((unsigned)((nterms + 255) / 256)), dim3(256), 0, st_, d_mlist,
-                                   nterms, d_eo, d_bdinv, d_terms);
-            hipLaunchKernelGGL(k_ba_pairs_sum, dim3(npairs), dim3(64), 0, st_, d_pairs, d_moffs, d_terms, d_Hpp,
+                                   nterms, d_moffs + npairs, d_eo, d_bdinv, d_terms);
+            hipLaunchKernelGGL(k_ba_pairs_sum, dim3(npairs), dim3(kSumThreads), kSumLds, st_, d_pairs, d_moffs, d_terms, d_Hpp,
                                lambda, g.nf, d_S);
         }
         else
@@ -1353,7 +1537,7 @@ int BA::solve_async(double lambda) {
         if (nusable_)
             hipLaunchKernelGGL((k_ba_gather_rows<6, 0>), dim3((unsigned)(((int64_t)nusable_ * 6 + 255) / 256)),
                                dim3(256), 0, st_, d_bdb, 6, d_clist, nusable_, nullptr, d_rows);
-        hipLaunchKernelGGL((k_ba_stream_sums<6>), dim3(g.nf), dim3(64), 0, st_, d_rows, d_coffs, d_bp, d_bs, 6,
+        hipLaunchKernelGGL((k_ba_stream_sums<6>), dim3(g.nf), dim3(kSumThreads), kSumLds, st_, d_rows, d_coffs, d_bp, d_bs, 6,
                            nullptr);
         if (n <= kCholLds) {
             const int lb = 8 * (n * (n + 1) + n);
@@ -1370,10 +1554,11 @@ int BA::solve_async(double lambda) {
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
 }
 
-int BA::update_gated() {
+int BA::update_gated() {   // (with the push: the backup is written by the update itself)
     const int n = std::max(g_.ncam, g_.npt);
+    if (!n) return ORBX_OK;
     hipLaunchKernelGGL(k_ba_update, dim3((n + 255) / 256), dim3(256), 0, st_, d_pose, g_.ncam, d_pts, g_.npt, d_x,
-                       d_x + 6 * g_.nf, d_ok);
+                       d_x + 6 * g_.nf, d_ok, d_pose_bk, d_pts_bk);
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
 }
 
@@ -1392,13 +1577,7 @@ int BA::read_diag() {
 // a trial's readback: the solve flag, the errors at the trial estimate, and
 // x and b for computeScale
 int BA::read_trial() {
-    const int n = 6 * g_.nf, m = n + 3 * g_.npt;
-    if (hipMemcpyAsync(h_ok, d_ok, 4, hipMemcpyDeviceToHost, st_) != hipSuccess || read_errors() != ORBX_OK ||
-        (m && hipMemcpyAsync(h_x, d_x, 8 * (size_t)m, hipMemcpyDeviceToHost, st_) != hipSuccess) ||
-        (n && hipMemcpyAsync(h_b, d_bp, 8 * (size_t)n, hipMemcpyDeviceToHost, st_) != hipSuccess) ||
-        (g_.npt && hipMemcpyAsync(h_b + n, d_bl, 8 * 3 * (size_t)g_.npt, hipMemcpyDeviceToHost, st_) != hipSuccess))
-        return ORBX_EIO;
-    return ORBX_OK;
+    return hipMemcpyAsync(h_ok, d_ok, span_, hipMemcpyDeviceToHost, st_) == hipSuccess ? ORBX_OK : ORBX_EIO;
 }
 
 double BA::chi_sum_host() const {   // activeRobustChi2: active edges in order
@@ -1420,22 +1599,16 @@ double BA::max_diag_host() const {   // computeLambdaInit: max |diagonal| over t
 double BA::scale_host(double lambda) const {   // computeScale: x (lambda x + b), poses then points
     const int m = 6 * g_.nf + 3 * g_.npt;
     double s = 0.;
-    for (int j = 0; j < m; ++j) s += h_x[j] * (lambda * h_x[j] + h_b[j]);
+    const int n = 6 * g_.nf;
+    for (int j = 0; j < m; ++j) s += h_x[j] * (lambda * h_x[j] + (j < n ? h_bp[j] : h_bl[j - n]));
     return s;
 }
 
-int BA::push() {
-    if (hipMemcpyAsync(d_pose_bk, d_pose, sizeof(Pose) * g_.ncam, hipMemcpyDeviceToDevice, st_) != hipSuccess ||
-        (g_.npt && hipMemcpyAsync(d_pts_bk, d_pts, 24 * (size_t)g_.npt, hipMemcpyDeviceToDevice, st_) != hipSuccess))
-        return ORBX_EIO;
-    return ORBX_OK;
-}
-
 int BA::pop() {
-    if (hipMemcpyAsync(d_pose, d_pose_bk, sizeof(Pose) * g_.ncam, hipMemcpyDeviceToDevice, st_) != hipSuccess ||
-        (g_.npt && hipMemcpyAsync(d_pts, d_pts_bk, 24 * (size_t)g_.npt, hipMemcpyDeviceToDevice, st_) != hipSuccess))
-        return ORBX_EIO;
-    return ORBX_OK;
+    const int n = std::max(g_.ncam, g_.npt);
+    if (n) hipLaunchKernelGGL(k_ba_restore, dim3((n + 255) / 256), dim3(256), 0, st_, d_pose, g_.ncam, d_pts, g_.npt,
+                              d_pose_bk, d_pts_bk);
+    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
 }
 
 // chi2 as last computed (an edge's error is only refreshed while active, and
@@ -1485,7 +1658,7 @@ int lm_optimize(BA &ba, int iters, bool robust, int *rc_out) {
         double rho = 0;
         int qmax = 0;
         do {
-            if ((rc = ba.push()) || (rc = ba.solve_async(lambda)) || (rc = ba.update_gated()) ||
+            if ((rc = ba.solve_async(lambda)) || (rc = ba.update_gated()) ||
                 (rc = ba.errors_async(robust, ba.d_ok)) || (rc = ba.read_trial()))
                 return fail(rc);
             if (hipStreamSynchronize(ba.st_) != hipSuccess) return fail(ORBX_EIO);
@@ -1508,7 +1681,7 @@ int lm_optimize(BA &ba, int iters, bool robust, int *rc_out) {
                 lambda *= ni;
                 ni *= 2;
                 fresh = false;
-                if ((rc = ba.pop())) return fail(rc);
+                if (ok && (rc = ba.pop())) return fail(rc);   // (a failed solve left the estimate alone)
             }
             qmax++;
         } while (rho < 0 && qmax < 10);
@@ -1522,7 +1695,7 @@ int lm_optimize(BA &ba, int iters, bool robust, int *rc_out) {
 
 int build_graph(const float *Tcw, const uint8_t *fixed, int ncam, int npt, const orbx_ba_edge *edges, int ne,
                 Graph &g) {
-    g.ncam = ncam; g.npt = npt; g.ne = ne;
+    g.ncam = ncam; g.npt = npt; g.ne = ne; g.raw = edges;
     g.poses.resize(ncam);
     int nf = 0;
     for (int c = 0; c < ncam; ++c) {
@@ -1531,28 +1704,23 @@ int build_graph(const float *Tcw, const uint8_t *fixed, int ncam, int npt, const
         g.poses[c].pad = 0;
     }
     g.nf = nf;
-    g.edges.resize(ne);
-    const double thMono = (double)(float)std::sqrt(5.991), thStereo = (double)(float)std::sqrt(7.815);
-    for (int e = 0; e < ne; ++e) {
-        const orbx_ba_edge &s = edges[e];
-        if (s.cam < 0 || s.cam >= ncam || s.point < 0 || s.point >= npt) return ORBX_EINVAL;
-        EdgeD &d = g.edges[e];
-        d.cam = s.cam; d.point = s.point; d.stereo = s.ur >= 0 ? 1 : 0; d.pad = 0;
-        d.obs[0] = s.u; d.obs[1] = s.v; d.obs[2] = d.stereo ? s.ur : 0.0;
-        d.omega = s.inv_sigma2;
-        d.fx = s.fx; d.fy = s.fy; d.cx = s.cx; d.cy = s.cy; d.bf = s.bf;
-        d.delta = d.stereo ? thStereo : thMono;
-    }
-    // edges per point, by camera index (stable)
+    for (int e = 0; e < ne; ++e)
+        if (edges[e].cam < 0 || edges[e].cam >= ncam || edges[e].point < 0 || edges[e].point >= npt) return ORBX_EINVAL;
+    // edges per point, by camera index (stable): bucket by camera, then by point
+    std::vector<int> cfill(ncam + 1, 0);
+    for (int e = 0; e < ne; ++e) ++cfill[edges[e].cam + 1];
+    for (int c = 0; c < ncam; ++c) cfill[c + 1] += cfill[c];
+    std::vector<int32_t> bycam(std::max(ne, 1));
+    for (int e = 0; e < ne; ++e) bycam[cfill[edges[e].cam]++] = e;
     g.poffs.assign(npt + 1, 0);
     for (int e = 0; e < ne; ++e) ++g.poffs[edges[e].point + 1];
     for (int p = 0; p < npt; ++p) g.poffs[p + 1] += g.poffs[p];
     g.plist.assign(std::max(ne, 1), 0);
     std::vector<int> fill(g.poffs.begin(), g.poffs.end() - 1);
-    for (int e = 0; e < ne; ++e) g.plist[fill[edges[e].point]++] = e;
-    for (int p = 0; p < npt; ++p)
-        std::stable_sort(g.plist.begin() + g.poffs[p], g.plist.begin() + g.poffs[p + 1],
-                         [&](int a, int b) { return edges[a].cam < edges[b].cam; });
+    for (int t = 0; t < ne; ++t) {
+        const int e = bycam[t];
+        g.plist[fill[edges[e].point]++] = e;
+    }
     return ORBX_OK;
 }
 
@@ -1614,7 +1782,7 @@ int orbx_local_ba(int device, const float *Tcw, const uint8_t *fixed, int ncam, 
         if (!rc && iters2 > 0) {
             // outliers leave the second pass (setLevel(1)); every kernel is dropped (:791-826)
             for (int e = 0; e < ne; ++e) {
-                const double th = g.edges[e].stereo ? 7.815 : 5.991;
+                const double th = g.raw[e].ur >= 0 ? 7.815 : 5.991;
                 if (chi2[e] > th || !front[e]) act[e] = 0;
             }
             ba.set_active(act);
@@ -1626,7 +1794,7 @@ int orbx_local_ba(int device, const float *Tcw, const uint8_t *fixed, int ncam, 
         }
         if (!rc)   // the inlier check of :838-870 (an inactive edge keeps its last error)
             for (int e = 0; e < ne; ++e) {
-                const double th = g.edges[e].stereo ? 7.815 : 5.991;
+                const double th = g.raw[e].ur >= 0 ? 7.815 : 5.991;
                 out_flags[e] = chi2[e] > th || !front[e];
             }
     }
