@@ -403,8 +403,23 @@ def kfdb_latency(n_kf=10000, words=1000, reps=10):
         b = o.detect(False, q, *bows[q], covis[q], 0.01, cv)
         to.append(time.perf_counter() - t0)
         assert a == b
+    # steady state: each side's queries back to back (fresh query ids, the
+    # same sequence on both; the answers are compared too)
+    tgb, tob, ga, oa = [], [], [], []
+    for k in range(3 * reps):
+        q = n_kf + k % reps
+        t0 = time.perf_counter()
+        ga.append(g.DetectLoopCandidates(200000 + k, *bows[q], covis[q], 0.01, cv))
+        tgb.append(time.perf_counter() - t0)
+    for k in range(3 * reps):
+        q = n_kf + k % reps
+        t0 = time.perf_counter()
+        oa.append(o.detect(False, 200000 + k, *bows[q], covis[q], 0.01, cv))
+        tob.append(time.perf_counter() - t0)
+    assert ga == oa
     return {"keyframes": n_kf, "words_per_keyframe": words, "gpu_ms": round(1e3 * float(np.median(tg)), 4),
-            "cpu_ms": round(1e3 * float(np.median(to)), 4), "cpu_kind": "port, 1 thread, inverted file"}
+            "cpu_ms": round(1e3 * float(np.median(to)), 4), "gpu_ms_back_to_back": round(1e3 * float(np.median(tgb)), 4),
+            "cpu_ms_back_to_back": round(1e3 * float(np.median(tob)), 4), "cpu_kind": "port, 1 thread, inverted file"}
 
 
 def local_ba_latency(reps=3):

@@ -24,6 +24,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <list>
@@ -44,6 +47,7 @@ namespace {
 
 constexpr int kKT = 256;
 constexpr int kQLds = 8192;   // query words (and values) staged in LDS; more: read from global
+constexpr int kScoreChunk = 1024;   // keyframe words scored per wave step (16 per lane)
 
 struct SlotDev {
     int64_t off;   // first word in the arena
@@ -120,7 +124,6 @@ struct TouchDev {
     const uint32_t *csr_off; const int32_t *csr_slot; uint32_t V;
     int delta0, nslots;          // brute-force slots [delta0, nslots)
     int32_t *qcnt; uint32_t *qfirst;   // per slot, 0 / ~0 between queries
-    int32_t *touched; int32_t *ntouched;
 };
 
 // Shared words of a keyframe with the query and the rank of the first one
@@ -162,18 +165,20 @@ __device__ inline void count_slot(const SlotDev &sl, const uint32_t *words, cons
 
 // Pass 1 (persistent grid, wave per work item): items [0, nq) walk the
 // posting list of query word r; items past nq count one delta keyframe.
-// Every keyframe met goes once to the touched list.
+// The per-slot counts are fire-and-forget atomics (no return value waited on).
 __global__ __launch_bounds__(kKT) void k_kfdb_touch(const SlotDev *slots, const uint32_t *words, const uint32_t *qw_g,
                                                     int nq, TouchDev t) {
     extern __shared__ uint32_t qs[];
-    const bool staged = nq <= kQLds;
-    if (staged)
+    // (only the delta keyframes' merges read the whole query: staged for them)
+    const int items = nq + (t.nslots - t.delta0);
+    const bool staged = nq <= kQLds && items > nq;
+    if (staged) {
         for (int i = threadIdx.x; i < nq; i += kKT) qs[i] = qw_g[i];
-    __syncthreads();
+        __syncthreads();
+    }
     const uint32_t *qw = staged ? qs : qw_g;
     const int lane = threadIdx.x & 63;
     const int nw = gridDim.x * (kKT / 64);
-    const int items = nq + (t.nslots - t.delta0);
     for (int it = blockIdx.x * (kKT / 64) + (threadIdx.x >> 6); it < items; it += nw) {
         if (it < nq) {
             const uint32_t w = qw[it];
@@ -183,7 +188,7 @@ __global__ __launch_bounds__(kKT) void k_kfdb_touch(const SlotDev *slots, const 
                 const int s = t.csr_slot[i];
                 if (!slots[s].alive) continue;
                 atomicMin(&t.qfirst[s], (uint32_t)it);
-                if (atomicAdd(&t.qcnt[s], 1) == 0) t.touched[atomicAdd(t.ntouched, 1)] = s;
+                atomicAdd(&t.qcnt[s], 1);
             }
         } else {
             const int s = t.delta0 + (it - nq);
@@ -193,13 +198,12 @@ __global__ __launch_bounds__(kKT) void k_kfdb_touch(const SlotDev *slots, const 
             if (lane == 0 && c > 0) {
                 t.qcnt[s] = c;
                 t.qfirst[s] = f;
-                t.touched[atomicAdd(t.ntouched, 1)] = s;
             }
         }
     }
 }
 
-// Pass 2 (thread per touched keyframe): the walk's state update
+// Pass 2 (thread per slot; the keyframes the query met: count > 0): the walk's state update
 // (KeyFrameDatabase.cc:95-119 / 234-251):
 //   loop:  not met by this query yet -> connected: words = 1 (it is reset at
 //          every meeting and ends at 1); else query = qid, words = count, listed;
@@ -208,10 +212,12 @@ __global__ __launch_bounds__(kKT) void k_kfdb_touch(const SlotDev *slots, const 
 // Resets the per-slot scratch for the next query.
 __global__ __launch_bounds__(kKT) void k_kfdb_list(TouchDev t, const int32_t *conn, QueryDev qd, KState *state,
                                                    int4 *listed) {
-    const int n = *t.ntouched;
-    for (int k = blockIdx.x * kKT + threadIdx.x; k < n; k += gridDim.x * kKT) {
-        const int s = t.touched[k];
+    for (int s = blockIdx.x * kKT + threadIdx.x; s < t.nslots; s += gridDim.x * kKT) {
         const int cnt = t.qcnt[s];
+        if (cnt == 0) {
+            listed[s] = make_int4(0, 0, s, 0);
+            continue;
+        }
         const uint32_t first = t.qfirst[s];
         t.qcnt[s] = 0;
         t.qfirst[s] = ~0u;
@@ -246,7 +252,7 @@ __global__ __launch_bounds__(kKT) void k_kfdb_list(TouchDev t, const int32_t *co
             }
         }
         if (lst) atomicMax(qd.max_words, cnt);
-        listed[k] = make_int4(lst ? cnt : 0, (int)first, s, 0);
+        listed[s] = make_int4(lst ? cnt : 0, (int)first, s, 0);
         // what the accumulation may read of this keyframe as a neighbour
         qd.rec[s] = qd.reloc ? make_int4((int)qd.stamp, st.reloc_words, __float_as_int(st.reloc_score),
                                          st.reloc_query == qd.qid)
@@ -255,61 +261,91 @@ __global__ __launch_bounds__(kKT) void k_kfdb_list(TouchDev t, const int32_t *co
     }
 }
 
-// Pass 3 (persistent grid, wave per touched keyframe): L1Scoring::score of
+// Pass 3 (persistent grid, a wave per 64 slots): L1Scoring::score of
 // the listed keyframes above minCommonWords = maxCommonWords * 0.8f
 // (KeyFrameDatabase.cc:124-149 / 259-284), in double; the score goes to the
 // keyframe's state and the keyframes the reference keeps (loop: score >=
 // minScore; reloc: all) are appended to the output.
-__global__ __launch_bounds__(kKT) void k_kfdb_score(const SlotDev *slots, const int32_t *ntouched, const int4 *listed,
+__global__ __launch_bounds__(kKT) void k_kfdb_score(const SlotDev *slots, int n, const int4 *listed,
                                                     const uint32_t *words, const double *values, const uint32_t *qw_g,
                                                     const double *qv_g, int nq, QueryDev qd, KState *state,
                                                     Listed *list) {
+    __shared__ double tbuf[kKT / 64][kScoreChunk];   // per wave: a chunk's terms
     extern __shared__ uint32_t qs[];   // the query's words (nq <= kQLds), else read from global
     const bool staged = nq <= kQLds;
     if (staged)
         for (int i = threadIdx.x; i < nq; i += kKT) qs[i] = qw_g[i];
     __syncthreads();
     const uint32_t *qw = staged ? qs : qw_g;
-    const int n = *ntouched;
+    double *trow = tbuf[threadIdx.x >> 6];
     const int min_words = (int)((float)*qd.max_words * 0.8f);
     const int lane = threadIdx.x & 63;
     const int nw = gridDim.x * (kKT / 64);
-    for (int k = blockIdx.x * (kKT / 64) + (threadIdx.x >> 6); k < n; k += nw) {
-        const int4 L = listed[k];
-        if (L.x <= min_words) continue;   // not listed (0) or too few words
-        const int s = L.z;
-        const SlotDev sl = slots[s];
-        double acc = 0;
-        for (int c0 = 0; c0 < sl.n; c0 += 64) {
-            const int i = c0 + lane;
-            double term = 0;
-            bool hit = false;
-            if (i < sl.n) {
-                const int r = find_word(qw, nq, words[sl.off + i]);
-                if (r >= 0) {
-                    const double vi = qv_g[r], wi = values[sl.off + i];
-                    term = __dsub_rn(__dsub_rn(fabs(__dsub_rn(vi, wi)), fabs(vi)), fabs(wi));
-                    hit = true;
+    // the wave reads 64 list entries at once and scores the ones above the
+    // threshold one after another
+    for (int k0 = (blockIdx.x * (kKT / 64) + (threadIdx.x >> 6)) * 64; k0 < n; k0 += nw * 64) {
+        const int4 Lk = k0 + lane < n ? listed[k0 + lane] : make_int4(0, 0, 0, 0);
+        for (uint64_t pass = __ballot(Lk.x > min_words); pass; pass &= pass - 1) {   // not listed (0) or too few words
+            const int j = (int)__builtin_ctzll(pass);
+            const int s = __shfl(Lk.z, j), first = __shfl(Lk.y, j);
+            const SlotDev sl = slots[s];
+            // 1024 words at a time: every lane loads and looks up 16 words at
+            // once (branch-free searches in lock step), the common words'
+            // terms go to the wave's LDS row in word order, then lane 0 adds
+            // them in order
+            double acc = 0;
+            for (int c0 = 0; c0 < sl.n; c0 += kScoreChunk) {
+                uint32_t w[16];
+                int pos[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    const int i = c0 + u * 64 + lane;
+                    w[u] = i < sl.n ? words[sl.off + i] : 0u;
+                    pos[u] = 0;
+                }
+                for (int len = nq; len > 1;) {
+                    const int half = len >> 1;
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) pos[u] = qw[pos[u] + half] <= w[u] ? pos[u] + half : pos[u];
+                    len -= half;
+                }
+                int m = 0;   // the common words' terms, compacted in word order
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    const int i = c0 + u * 64 + lane;
+                    const bool hit = i < sl.n && qw[pos[u]] == w[u];
+                    const uint64_t hm = __ballot(hit);
+                    if (hit) {
+                        const double vi = qv_g[pos[u]], wi = values[sl.off + i];
+                        const int at = m + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32),
+                                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
+                        trow[at] = __dsub_rn(__dsub_rn(fabs(__dsub_rn(vi, wi)), fabs(vi)), fabs(wi));
+                    }
+                    m += __popcll(hm);
+                }
+                wave_lds_fence();
+                if (lane == 0) {
+                    int q = 0;
+                    for (; q + 8 <= m; q += 8) {
+                        double x[8];
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) x[u] = trow[q + u];
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) acc = __dadd_rn(acc, x[u]);
+                    }
+                    for (; q < m; ++q) acc = __dadd_rn(acc, trow[q]);
+                }
+                wave_lds_fence();
+            }
+            if (lane == 0) {
+                const float si = (float)(-acc / 2.0);
+                if (qd.reloc) state[s].reloc_score = si; else state[s].loop_score = si;
+                qd.rec[s].z = __float_as_int(si);
+                if (qd.reloc || si >= qd.min_score) {
+                    const int at = atomicAdd(qd.max_words + 1, 1);
+                    if (at < qd.list_cap) list[at] = Listed{(uint32_t)first, s, si};
                 }
             }
-            // add the terms in ascending word order (the keyframe's words are sorted)
-            for (uint64_t b = __ballot(hit); b; b &= b - 1) {
-                const int j = (int)__builtin_ctzll(b);
-                const uint64_t bits =
-                    (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)__double_as_longlong(term), j) |
-                    ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(
-                         (int)(uint32_t)((uint64_t)__double_as_longlong(term) >> 32), j)
-                     << 32);
-                acc = __dadd_rn(acc, __longlong_as_double((long long)bits));
-            }
-        }
-        if (lane != 0) continue;
-        const float si = (float)(-acc / 2.0);
-        if (qd.reloc) state[s].reloc_score = si; else state[s].loop_score = si;
-        qd.rec[s].z = __float_as_int(si);
-        if (qd.reloc || si >= qd.min_score) {
-            const int at = atomicAdd(qd.max_words + 1, 1);
-            if (at < qd.list_cap) list[at] = Listed{(uint32_t)L.y, s, si};
         }
     }
 }
@@ -356,7 +392,7 @@ struct orbx_kfdb {
     double *d_values = nullptr;
     SlotDev *d_slots = nullptr;
     KState *d_state = nullptr;
-    int32_t *d_qcnt = nullptr, *d_touched = nullptr;   // per-slot query scratch
+    int32_t *d_qcnt = nullptr;   // per-slot query scratch
     uint32_t *d_qfirst = nullptr;
     // the device inverted file over slots [0, csr_ns): postings by word id
     uint32_t *d_csr_off = nullptr, *d_csr_cnt = nullptr;
@@ -422,19 +458,18 @@ int kfdb_sync(orbx_kfdb *db) {
         (void)hipStreamSynchronize(db->st);
         if (db->d_slots) (void)hipFree(db->d_slots);
         if (db->d_state) (void)hipFree(db->d_state);
-        for (void *x : {(void *)db->d_qcnt, (void *)db->d_qfirst, (void *)db->d_touched, (void *)db->d_rec})
+        for (void *x : {(void *)db->d_qcnt, (void *)db->d_qfirst, (void *)db->d_rec})
             if (x) (void)hipFree(x);
         db->d_slots = d;
         db->d_state = k;
-        db->d_qcnt = db->d_touched = nullptr;
+        db->d_qcnt = nullptr;
         db->d_qfirst = nullptr;
         db->d_rec = nullptr;
         if (hipMalloc(reinterpret_cast<void **>(&db->d_rec), sizeof(int4) * (size_t)cap) != hipSuccess ||
             hipMemsetAsync(db->d_rec, 0, sizeof(int4) * (size_t)cap, db->st) != hipSuccess)
             return ORBX_ENOMEM;
         if (hipMalloc(reinterpret_cast<void **>(&db->d_qcnt), 4 * (size_t)cap) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void **>(&db->d_qfirst), 4 * (size_t)cap) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void **>(&db->d_touched), 4 * (size_t)cap) != hipSuccess)
+            hipMalloc(reinterpret_cast<void **>(&db->d_qfirst), 4 * (size_t)cap) != hipSuccess)
             return ORBX_ENOMEM;
         if (hipMemsetAsync(db->d_qcnt, 0, 4 * (size_t)cap, db->st) != hipSuccess ||
             hipMemsetAsync(db->d_qfirst, 0xFF, 4 * (size_t)cap, db->st) != hipSuccess)
@@ -538,6 +573,10 @@ int detect(orbx_kfdb *db, bool reloc, uint64_t qid, const uint32_t *words, const
         (cap > 0 && !out) || !sorted_unique(words, n))
         return ORBX_EINVAL;
     *n_out = 0;
+    // ORBX_KFDB_TIMING: phase times of this query on stderr (diagnostics)
+    static const bool timing = std::getenv("ORBX_KFDB_TIMING") != nullptr;
+    auto tms = [] { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double t_a = timing ? tms() : 0;
     std::lock_guard<std::mutex> lock(db->mu);
     const int ns = (int)db->slots.size();
     if (n == 0 || ns == 0) return ORBX_OK;
@@ -556,7 +595,6 @@ int detect(orbx_kfdb *db, bool reloc, uint64_t qid, const uint32_t *words, const
     conn.erase(std::unique(conn.begin(), conn.end()), conn.end());
     Layout L;
     const size_t o_qw = L.add(4 * (size_t)n), o_qv = L.add(8 * (size_t)n), o_conn = L.add(4 * (conn.size() + 1));
-    const size_t in_bytes = L.size;
     const size_t o_mw = L.add(16), o_list = L.add(sizeof(Listed) * kListCap);   // brought back together
     const size_t o_lst = L.add(16 * (size_t)ns), o_rec = L.add(sizeof(int4) * (size_t)ns);
     const bool repeated = !(reloc ? db->reloc_qids : db->loop_qids).insert(qid).second;
@@ -568,27 +606,27 @@ int detect(orbx_kfdb *db, bool reloc, uint64_t qid, const uint32_t *words, const
     put(ws, o_qw, words, 4 * (size_t)n);
     put(ws, o_qv, values, 8 * (size_t)n);
     put(ws, o_conn, conn.data(), 4 * conn.size());
+    std::memset(ws.host + o_mw, 0, 16);   // (the counters go up zeroed with the query)
     uint8_t *D = ws.dev;
     QueryDev qd;
     qd.qid = qid;
     qd.reloc = reloc;
     qd.nconn = (int)conn.size();
     qd.min_score = minScore;
-    qd.max_words = at<int32_t>(D, o_mw);   // [0] maxCommonWords, [1] kept, [2] touched
+    qd.max_words = at<int32_t>(D, o_mw);   // [0] maxCommonWords, [1] kept
     qd.list_cap = kListCap;
     qd.stamp = db->stamp;
     qd.rec = db->d_rec;
     TouchDev t;
     t.csr_off = db->d_csr_off; t.csr_slot = db->d_csr_slot; t.V = db->csr_ns ? db->csr_V : 0;
     t.delta0 = db->csr_ns; t.nslots = ns;
-    t.qcnt = db->d_qcnt; t.qfirst = db->d_qfirst; t.touched = db->d_touched; t.ntouched = qd.max_words + 2;
+    t.qcnt = db->d_qcnt; t.qfirst = db->d_qfirst;
     // pass 1: the query words' posting lists + the delta keyframes; pass 2:
     // state update and the walk's list; pass 3: scores above minCommonWords
     const size_t qlds = n <= kQLds ? 4 * (size_t)n : 0;
     const int items = n + (ns - db->csr_ns);
     if (hipStreamSynchronize(db->st) != hipSuccess ||
-        hipMemcpyAsync(D, ws.host, in_bytes, hipMemcpyHostToDevice, ws.st) != hipSuccess ||
-        hipMemsetAsync(D + o_mw, 0, 16, ws.st) != hipSuccess)
+        hipMemcpyAsync(D, ws.host, o_mw + 16, hipMemcpyHostToDevice, ws.st) != hipSuccess)
         return ORBX_EIO;
     hipLaunchKernelGGL(k_kfdb_touch, dim3(std::min(1024, (items + 3) / 4)), dim3(kKT), qlds, ws.st, db->d_slots,
                        db->d_words, at<uint32_t>(D, o_qw), n, t);
@@ -597,7 +635,7 @@ int detect(orbx_kfdb *db, bool reloc, uint64_t qid, const uint32_t *words, const
     // few keyframes pass minCommonWords: a small persistent grid, each block
     // with the query words in LDS
     hipLaunchKernelGGL(k_kfdb_score, dim3(std::min(64, (ns + 3) / 4)), dim3(kKT), qlds, ws.st, db->d_slots,
-                       t.ntouched, at<int4>(D, o_lst), db->d_words, db->d_values, at<uint32_t>(D, o_qw),
+                       ns, at<int4>(D, o_lst), db->d_words, db->d_values, at<uint32_t>(D, o_qw),
                        at<double>(D, o_qv), n, qd, db->d_state, at<Listed>(D, o_list));
     if (hipGetLastError() != hipSuccess ||
         hipMemcpyAsync(ws.host + o_mw, D + o_mw, o_lst - o_mw, hipMemcpyDeviceToHost, ws.st) != hipSuccess ||
@@ -605,6 +643,7 @@ int detect(orbx_kfdb *db, bool reloc, uint64_t qid, const uint32_t *words, const
             hipSuccess ||
         hipStreamSynchronize(ws.st) != hipSuccess)
         return ORBX_EIO;
+    const double t_b = timing ? tms() : 0;
     const int4 *rec = at<int4>(ws.host, o_rec);
     int32_t mw[2];
     get(ws, o_mw, mw, 8);
@@ -651,6 +690,7 @@ int detect(orbx_kfdb *db, bool reloc, uint64_t qid, const uint32_t *words, const
         }
         nfirst[i + 1] = (int)nid.size();
     }
+    const double t_c = timing ? tms() : 0;
     if (!gslot.empty()) {
         std::vector<KState> gst(gslot.size());
         Layout G;
@@ -701,6 +741,9 @@ int detect(orbx_kfdb *db, bool reloc, uint64_t qid, const uint32_t *words, const
         }
     }
     *n_out = m;
+    if (timing)
+        std::fprintf(stderr, "kfdb query us: pre+gpu %.1f covis(%d kept) %.1f post %.1f\n", t_b - t_a, nsc, t_c - t_b,
+                     tms() - t_c);
     return m > cap ? ORBX_ERANGE : ORBX_OK;
 }
 
@@ -724,7 +767,7 @@ void orbx_kfdb_destroy(orbx_kfdb *db) {
     if (db->d_values) (void)hipFree(db->d_values);
     if (db->d_slots) (void)hipFree(db->d_slots);
     if (db->d_state) (void)hipFree(db->d_state);
-    for (void *x : {(void *)db->d_qcnt, (void *)db->d_qfirst, (void *)db->d_touched, (void *)db->d_rec, (void *)db->d_csr_off,
+    for (void *x : {(void *)db->d_qcnt, (void *)db->d_qfirst, (void *)db->d_rec, (void *)db->d_csr_off,
                     (void *)db->d_csr_cnt, (void *)db->d_csr_slot})
         if (x) (void)hipFree(x);
     if (db->st) (void)hipStreamDestroy(db->st);
