@@ -11,16 +11,17 @@
 //   k_ba_gather_rows / k_ba_stream_sums
 //                      Hpp / bp of each free camera (and the reduced right-hand side
 //                      bp - sum B Dinv bl) as sums over its edges in edge order: the
-//                      records gathered into list order, then a wave per camera adds
+//                      records gathered into list order, then a workgroup per camera adds
 //   k_ba_reduce        wave per point: Hll / bl, edge order
 //   k_ba_point         thread per point: (Hll + lambda I)^-1 and Dinv bl
 //   k_ba_point_edges   thread per edge: B Dinv and B Dinv bl
 //   k_ba_pair_terms    thread per (shared point, entry) of every camera pair: B_i Dinv B_j^T terms
-//   k_ba_pairs_sum     wave per camera pair: S_ij -= its terms in point order (pairs listed once
+//   k_ba_pairs_sum     workgroup per camera pair: S_ij -= its terms in point order (pairs listed once
 //                      per set of active edges); k_ba_pairs merge walk for repeated observations
 //   k_ba_chol_lds      one workgroup: blocked dense Cholesky of the reduced camera system and
 //                      the solves (k_ba_chol beyond 128 unknowns)
-//   k_ba_backsub       thread per point: xl = Dinv (bl - sum_e B_e^T xp)
+//   k_ba_backsub_terms / k_ba_backsub
+//                      xl = Dinv (bl - sum_e B_e^T xp): per-edge terms, then thread per point
 //   k_ba_update        poses exp(dx) * T (SE3Quat), points += dx
 // Every sum runs in a fixed order (edge order per vertex, ascending point per
 // camera pair, ascending column in the Cholesky), so a run is deterministic
@@ -926,23 +927,50 @@ __global__ void k_ba_edges(const orbx_ba_edge *in, int ne, double th_mono, doubl
 }
 
 // xl = Dinv (bl - sum over the point's usable edges (camera order) of B^T xp)
-__global__ void k_ba_backsub(const double *dinv, const double *bl, int npt, const EdgeOut *eo, const int32_t *offs,
-                             const int32_t *list, const uint8_t *usable, const EdgeD *edges, const Pose *poses,
-                             const double *xp, double *xl) {
+// The back substitution in two passes:
+//  k_ba_backsub_terms: thread per (point, edge) list entry: s = B^T (-xp) of a
+//    usable edge (each component its own 6-term sum from 0), flagged;
+//  k_ba_backsub: thread per point: cl = bl + the flagged terms in list order,
+//    xl = Dinv cl -- the loads contiguous per point and off the add chain.
+__global__ void k_ba_backsub_terms(int ne, const int32_t *list, const uint8_t *usable, const EdgeOut *eo,
+                                   const EdgeD *edges, const Pose *poses, const double *xp, double *terms,
+                                   uint8_t *flag) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ne) return;
+    const int ei = list[t];
+    const bool u = usable[ei];
+    flag[t] = u;
+    if (!u) return;
+    const int f = poses[edges[ei].cam].free_idx;
+    const double *B = eo[ei].hpl;
+    for (int c = 0; c < 3; ++c) {
+        double a = 0;
+        for (int r = 0; r < 6; ++r) a = a + B[3 * r + c] * -xp[6 * f + r];
+        terms[3 * (int64_t)t + c] = a;
+    }
+}
+
+__global__ void k_ba_backsub(const double *dinv, const double *bl, int npt, const int32_t *offs,
+                             const double *terms, const uint8_t *flag, double *xl) {
     const int pt = blockIdx.x * blockDim.x + threadIdx.x;
     if (pt >= npt) return;
     double cl[3];
     for (int k = 0; k < 3; ++k) cl[k] = bl[3 * (int64_t)pt + k];
-    for (int t = offs[pt]; t < offs[pt + 1]; ++t) {
-        const int ei = list[t];
-        if (!usable[ei]) continue;
-        const int f = poses[edges[ei].cam].free_idx;
-        const double *B = eo[ei].hpl;
-        for (int c = 0; c < 3; ++c) {
-            double s = 0;
-            for (int r = 0; r < 6; ++r) s = s + B[3 * r + c] * -xp[6 * f + r];
-            cl[c] = cl[c] + s;
+    const int te = offs[pt + 1];
+    for (int t = offs[pt]; t < te; t += 4) {
+        bool u[4];
+        double s[4][3];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            u[j] = t + j < te && flag[t + j];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) s[j][c] = u[j] ? terms[3 * (int64_t)(t + j) + c] : 0.0;
         }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (u[j])
+#pragma unroll
+                for (int c = 0; c < 3; ++c) cl[c] = cl[c] + s[j][c];
     }
     const double *D = dinv + 9 * (int64_t)pt;
     for (int r = 0; r < 3; ++r) {
@@ -1465,8 +1493,15 @@ int BA::solve(double lambda, int *ok) {
             hipLaunchKernelGGL(k_ba_chol, dim3(1), dim3(1024), 0, st_, d_S, n, d_bs, d_x, d_ok);
         }
     }
-    if (g.npt) hipLaunchKernelGGL(k_ba_backsub, dim3((g.npt + 63) / 64), dim3(64), 0, st_, d_dinv, d_bl, g.npt,
-                                  d_eo, d_poffs, d_plist, d_usable, d_edges, d_pose, d_x, d_x + n);
+    if (g.npt) {
+        double *terms = d_rows;   // (free after the reduced right-hand side)
+        uint8_t *flag = reinterpret_cast<uint8_t *>(d_rows + 3 * (size_t)std::max(g.ne, 1));
+        if (g.ne)
+            hipLaunchKernelGGL(k_ba_backsub_terms, dim3((g.ne + 255) / 256), dim3(256), 0, st_, g.ne, d_plist,
+                               d_usable, d_eo, d_edges, d_pose, d_x, terms, flag);
+        hipLaunchKernelGGL(k_ba_backsub, dim3((g.npt + 63) / 64), dim3(64), 0, st_, d_dinv, d_bl, g.npt, d_poffs,
+                           terms, flag, d_x + n);
+    }
     int okv = 1;
     if (hipGetLastError() != hipSuccess ||
         (g.nf && hipMemcpyAsync(&okv, d_ok, 4, hipMemcpyDeviceToHost, st_) != hipSuccess) ||
@@ -1549,8 +1584,15 @@ int BA::solve_async(double lambda) {
             hipLaunchKernelGGL(k_ba_chol, dim3(1), dim3(1024), 0, st_, d_S, n, d_bs, d_x, d_ok);
         }
     }
-    if (g.npt) hipLaunchKernelGGL(k_ba_backsub, dim3((g.npt + 63) / 64), dim3(64), 0, st_, d_dinv, d_bl, g.npt,
-                                  d_eo, d_poffs, d_plist, d_usable, d_edges, d_pose, d_x, d_x + n);
+    if (g.npt) {
+        double *terms = d_rows;   // (free after the reduced right-hand side)
+        uint8_t *flag = reinterpret_cast<uint8_t *>(d_rows + 3 * (size_t)std::max(g.ne, 1));
+        if (g.ne)
+            hipLaunchKernelGGL(k_ba_backsub_terms, dim3((g.ne + 255) / 256), dim3(256), 0, st_, g.ne, d_plist,
+                               d_usable, d_eo, d_edges, d_pose, d_x, terms, flag);
+        hipLaunchKernelGGL(k_ba_backsub, dim3((g.npt + 63) / 64), dim3(64), 0, st_, d_dinv, d_bl, g.npt, d_poffs,
+                           terms, flag, d_x + n);
+    }
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
 }
 
