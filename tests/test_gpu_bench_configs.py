@@ -84,7 +84,7 @@ def test_mono_bench_config_b1024_split2(oracle_mod):
 STEREO_CONFIGS = [   # bench.py EXTRAS: (w, h, nfeatures, pairs)
     (752, 480, 1200, 128),
     (1241, 376, 2000, 96),
-    (1920, 1080, 1000, 128),
+    (1920, 1080, 1000, 192),
 ]
 
 
