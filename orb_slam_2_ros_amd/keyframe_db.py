@@ -44,6 +44,10 @@ class KeyFrameDatabase:
     def __init__(self, device: int = 0):
         self._h = ctypes.c_void_p()
         check(load().orbx_kfdb_create(int(device), ctypes.byref(self._h)), "orbx_kfdb_create")
+        self._out = np.empty(64, np.uint64)   # candidates (grown with the database, reused)
+        self._cb_for = None                   # the last covisibility callable and its C callback
+        self._cb = None
+        self._n = ctypes.c_int(0)
 
     def __del__(self):
         try:
@@ -68,10 +72,14 @@ class KeyFrameDatabase:
     def _detect(self, reloc, qid, words, values, connected, min_score, covis):
         w, v = _bow(words, values)
         conn = np.ascontiguousarray(sorted(connected or []), np.uint64)
-        cb = _covis_cb(covis)
-        cap = max(self.size(), 1)
-        out = np.zeros(cap, np.uint64)
-        n = ctypes.c_int(0)
+        if covis is not self._cb_for:   # (one C callback per covisibility callable)
+            self._cb_for, self._cb = covis, _covis_cb(covis)
+        cb = self._cb
+        cap = max(self.size(), 1)   # every live keyframe could be a candidate
+        if len(self._out) < cap:
+            self._out = np.empty(max(cap, 2 * len(self._out)), np.uint64)
+        out, cap = self._out, len(self._out)
+        n = self._n
         if reloc:
             rc = load().orbx_kfdb_detect_relocalization_candidates(self._h, int(qid), ptr(w), ptr(v), len(w), cb,
                                                                    None, ptr(out), cap, ctypes.byref(n))
