@@ -1140,10 +1140,7 @@ public:
     void set_active(const std::vector<uint8_t> &act);
     int errors(bool robust, double *chi_sum);
     int build();
-    int max_diag(double *m);
     int solve(double lambda, int *ok);
-    double scale(double lambda);
-    int update();
     // the LM driver's asynchronous pieces: launches and readbacks into pinned
     // host buffers, one stream synchronisation per trial
     int errors_async(bool robust, const int *gate);
@@ -1436,99 +1433,15 @@ int BA::build() {
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
 }
 
-// computeLambdaInit: max |diagonal| over the free vertices
-int BA::max_diag(double *m) {
-    std::vector<double> hpp(36 * (size_t)std::max(g_.nf, 1)), hll(9 * (size_t)std::max(g_.npt, 1));
-    if ((g_.nf && hipMemcpyAsync(hpp.data(), d_Hpp, 8 * 36 * (size_t)g_.nf, hipMemcpyDeviceToHost, st_) != hipSuccess) ||
-        (g_.npt && hipMemcpyAsync(hll.data(), d_Hll, 8 * 9 * (size_t)g_.npt, hipMemcpyDeviceToHost, st_) != hipSuccess) ||
-        hipStreamSynchronize(st_) != hipSuccess)
-        return ORBX_EIO;
-    double mx = 0.;
-    for (int f = 0; f < g_.nf; ++f)
-        for (int j = 0; j < 6; ++j) mx = std::max(std::fabs(hpp[36 * (size_t)f + 7 * j]), mx);
-    for (int p = 0; p < g_.npt; ++p)
-        for (int j = 0; j < 3; ++j) mx = std::max(std::fabs(hll[9 * (size_t)p + 4 * j]), mx);
-    *m = mx;
-    return ORBX_OK;
-}
-
-int BA::solve(double lambda, int *ok) {
-    const Graph &g = g_;
-    const int n = 6 * g.nf;
-    // (the previous factorisation left L in place, also outside the pair blocks)
-    if (n && hipMemsetAsync(d_S, 0, 8 * (size_t)n * n, st_) != hipSuccess) return ORBX_EIO;
-    if (g.npt) {
-        hipLaunchKernelGGL(k_ba_point, dim3((g.npt + 255) / 256), dim3(256), 0, st_, d_Hll, d_bl, g.npt, lambda, d_dinv,
-                           d_db);
-        if (g.ne)
-            hipLaunchKernelGGL(k_ba_point_edges, dim3((g.ne + 63) / 64), dim3(64), 0, st_, d_eo, d_epoint, d_usable,
-                               g.ne, d_dinv, d_db, d_bdinv, d_bdb);
-    }
-    if (g.nf) {
-        if (use_map) {
-            const int64_t nterms = 36 * nmatch_;
-            if (nterms)
-                hipLaunchKernelGGL(k_ba_pair_terms, dim3((unsigned)((nterms + 255) / 256)), dim3(256), 0, st_, d_mlist,
-                                   nterms, d_moffs + npairs, d_eo, d_bdinv, d_terms);
-            hipLaunchKernelGGL(k_ba_pairs_sum, dim3(npairs), dim3(kSumThreads), kSumLds, st_, d_pairs, d_moffs, d_terms, d_Hpp,
-                               lambda, g.nf, d_S);
-        }
-        else
-            hipLaunchKernelGGL(k_ba_pairs, dim3((npairs + 3) / 4), dim3(256), 0, st_, d_pairs, npairs, d_coffs,
-                               d_clist, d_epoint, d_eo, d_bdinv, d_Hpp, lambda, g.nf, d_S);
-        // bs = bp - sum over the camera's usable edges of B Dinv bl, edge order
-        if (nusable_)
-            hipLaunchKernelGGL((k_ba_gather_rows<6, 0>), dim3((unsigned)(((int64_t)nusable_ * 6 + 255) / 256)),
-                               dim3(256), 0, st_, d_bdb, 6, d_clist, nusable_, nullptr, d_rows);
-        hipLaunchKernelGGL((k_ba_stream_sums<6>), dim3(g.nf), dim3(kSumThreads), kSumLds, st_, d_rows, d_coffs, d_bp, d_bs, 6,
-                           nullptr);
-        // (blocks of camera pairs without a shared point stay as the memset left them)
-        if (n <= kCholLds) {
-            const int lb = 8 * (n * (n + 1) + n);
-            if (lb > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void *>(k_ba_chol_lds),
-                                                      hipFuncAttributeMaxDynamicSharedMemorySize, lb) != hipSuccess)
-                return ORBX_EIO;
-            hipLaunchKernelGGL(k_ba_chol_lds, dim3(1), dim3(512), lb, st_, d_S, n, d_bs, d_x, d_ok, chol_clk());
-        } else {
-            hipLaunchKernelGGL(k_ba_chol, dim3(1), dim3(1024), 0, st_, d_S, n, d_bs, d_x, d_ok);
-        }
-    }
-    if (g.npt) {
-        double *terms = d_rows;   // (free after the reduced right-hand side)
-        uint8_t *flag = reinterpret_cast<uint8_t *>(d_rows + 3 * (size_t)std::max(g.ne, 1));
-        if (g.ne)
-            hipLaunchKernelGGL(k_ba_backsub_terms, dim3((g.ne + 255) / 256), dim3(256), 0, st_, g.ne, d_plist,
-                               d_usable, d_eo, d_edges, d_pose, d_x, terms, flag);
-        hipLaunchKernelGGL(k_ba_backsub, dim3((g.npt + 63) / 64), dim3(64), 0, st_, d_dinv, d_bl, g.npt, d_poffs,
-                           terms, flag, d_x + n);
-    }
+int BA::solve(double lambda, int *ok) {   // solve_async and its flag, synchronously
+    int rc = solve_async(lambda);
+    if (rc) return rc;
     int okv = 1;
-    if (hipGetLastError() != hipSuccess ||
-        (g.nf && hipMemcpyAsync(&okv, d_ok, 4, hipMemcpyDeviceToHost, st_) != hipSuccess) ||
+    if ((g_.nf && hipMemcpyAsync(&okv, d_ok, 4, hipMemcpyDeviceToHost, st_) != hipSuccess) ||
         hipStreamSynchronize(st_) != hipSuccess)
         return ORBX_EIO;
     *ok = okv;
     return ORBX_OK;
-}
-
-// computeScale: sum over the solution of x (lambda x + b), poses then points
-double BA::scale(double lambda) {
-    const int n = 6 * g_.nf, m = n + 3 * g_.npt;
-    std::vector<double> x(std::max(m, 1)), b(std::max(m, 1));
-    (void)hipMemcpyAsync(x.data(), d_x, 8 * (size_t)m, hipMemcpyDeviceToHost, st_);
-    if (n) (void)hipMemcpyAsync(b.data(), d_bp, 8 * (size_t)n, hipMemcpyDeviceToHost, st_);
-    if (g_.npt) (void)hipMemcpyAsync(b.data() + n, d_bl, 8 * 3 * (size_t)g_.npt, hipMemcpyDeviceToHost, st_);
-    (void)hipStreamSynchronize(st_);
-    double s = 0.;
-    for (int j = 0; j < m; ++j) s += x[j] * (lambda * x[j] + b[j]);
-    return s;
-}
-
-int BA::update() {
-    const int n = std::max(g_.ncam, g_.npt);
-    hipLaunchKernelGGL(k_ba_update, dim3((n + 255) / 256), dim3(256), 0, st_, d_pose, g_.ncam, d_pts, g_.npt, d_x,
-                       d_x + 6 * g_.nf, nullptr, nullptr, nullptr);
-    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
 }
 
 int BA::errors_async(bool robust, const int *gate) {
@@ -1538,10 +1451,11 @@ int BA::errors_async(bool robust, const int *gate) {
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
 }
 
-// solve() without the readback: d_ok says whether the Cholesky succeeded
+// The damped system's solve, enqueued: d_ok says whether the Cholesky succeeded
 int BA::solve_async(double lambda) {
     const Graph &g = g_;
     const int n = 6 * g.nf;
+    if (g.nf && !sums_ready()) return ORBX_EIO;
     // every solve rewrites the pair blocks; the others stay zero unless the
     // in-place factor (n > kCholLds) overwrote them
     if (n && (n > kCholLds || !s_zero_)) {
@@ -1596,7 +1510,7 @@ int BA::solve_async(double lambda) {
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
 }
 
-int BA::update_gated() {   // (with the push: the backup is written by the update itself)
+int BA::update_gated() {   // (the trial's backup of the estimate is written by the update itself)
     const int n = std::max(g_.ncam, g_.npt);
     if (!n) return ORBX_OK;
     hipLaunchKernelGGL(k_ba_update, dim3((n + 255) / 256), dim3(256), 0, st_, d_pose, g_.ncam, d_pts, g_.npt, d_x,
