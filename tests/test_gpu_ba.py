@@ -59,3 +59,20 @@ def test_local_ba_repeated_observation(oracle_mod):
     To, Xo, oo, io = oracle_mod.local_ba(P["Tcw"], P["fixed"], P["Xw"], e)
     assert ig == io and np.array_equal(og, oo)
     assert np.array_equal(Tg, To) and np.array_equal(Xg, Xo)
+
+
+def test_local_ba_workspace_reuse(oracle_mod):
+    """The per-device workspace across calls: problems that grow, shrink and
+    cross the LDS / global-memory Cholesky boundary (21 and 22 free
+    keyframes: 126 / 132 unknowns) in turn, a repeated observation in
+    between; every call identical to the oracle."""
+    seq = [(22, 2000, 31), (5, 400, 32), (21, 1800, 33), (6, 600, 9), (22, 2000, 34), (21, 1800, 33)]
+    for k, (n_local, n_points, seed) in enumerate(seq):
+        P = make_ba_problem(n_local=n_local, n_fixed=3, n_points=n_points, seed=seed)
+        e = P["edges"]
+        if k == 3:
+            e = np.concatenate([e, e[7:8]])
+        Tg, Xg, og, ig = local_bundle_adjustment(P["Tcw"], P["fixed"], P["Xw"], e)
+        To, Xo, oo, io = oracle_mod.local_ba(P["Tcw"], P["fixed"], P["Xw"], e)
+        assert ig == io and np.array_equal(og, oo), k
+        assert np.array_equal(Tg, To) and np.array_equal(Xg, Xo), k
