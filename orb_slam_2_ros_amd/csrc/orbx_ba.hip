@@ -543,6 +543,7 @@ constexpr int kSumThreads = 1024, kSumElems = 8192, kSumPer = kSumElems / kSumTh
 constexpr size_t kSumLds = 2 * kSumElems * sizeof(double);
 template <int NF, bool SUB>
 __device__ double ordered_colsum(const double *base, int nrows, double acc, double *buf) {
+    constexpr int kAhead = 16;   // LDS reads in flight ahead of the adds (8 left the chain waiting on them)
     constexpr int kRows = kSumElems / NF, kE = kRows * NF;   // whole rows per chunk
     const int tid = threadIdx.x, total = nrows * NF, nch = (nrows + kRows - 1) / kRows;
     double r[kSumPer];
@@ -572,22 +573,22 @@ __device__ double ordered_colsum(const double *base, int nrows, double acc, doub
             const double *src = buf + (k & 1) * kSumElems + tid;
             const int nr = min(kRows, nrows - k * kRows);
             int q = 0;
-            if (nr >= 8) {   // the reads of rows q + 8 .. q + 15 go out before the adds of rows q .. q + 7
-                double a[8];
+            if (nr >= kAhead) {   // the reads of the next kAhead rows go out before this group's adds
+                double a[kAhead];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) a[u] = src[u * NF];
-                for (; q + 16 <= nr; q += 8) {
-                    double b[8];
+                for (int u = 0; u < kAhead; ++u) a[u] = src[u * NF];
+                for (; q + 2 * kAhead <= nr; q += kAhead) {
+                    double b[kAhead];
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) b[u] = src[(q + 8 + u) * NF];
+                    for (int u = 0; u < kAhead; ++u) b[u] = src[(q + kAhead + u) * NF];
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) acc = SUB ? acc - a[u] : acc + a[u];
+                    for (int u = 0; u < kAhead; ++u) acc = SUB ? acc - a[u] : acc + a[u];
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) a[u] = b[u];
+                    for (int u = 0; u < kAhead; ++u) a[u] = b[u];
                 }
 #pragma unroll
-                for (int u = 0; u < 8; ++u) acc = SUB ? acc - a[u] : acc + a[u];
-                q += 8;
+                for (int u = 0; u < kAhead; ++u) acc = SUB ? acc - a[u] : acc + a[u];
+                q += kAhead;
             }
             for (; q < nr; ++q) acc = SUB ? acc - src[q * NF] : acc + src[q * NF];
         }
