@@ -87,7 +87,8 @@ struct QueryDev {
     int nconn;           // connected keyframes (slots, ascending)
     float min_score;
     int32_t *max_words;  // [0] maxCommonWords over the listed ones, [1] survivors
-    int list_cap;
+    int list_cap;        // survivors past list_cap go to over[]
+    Listed *over;
     uint32_t stamp;      // this query's number
     int4 *rec;           // per slot, written for the keyframes met: (stamp, words, score bits, query == qid)
 };
@@ -167,8 +168,12 @@ __device__ inline void count_slot(const SlotDev &sl, const uint32_t *words, cons
 // posting list of query word r; items past nq count one delta keyframe.
 // The per-slot counts are fire-and-forget atomics (no return value waited on).
 __global__ __launch_bounds__(kKT) void k_kfdb_touch(const SlotDev *slots, const uint32_t *words, const uint32_t *qw_g,
-                                                    int nq, TouchDev t) {
+                                                    int nq, TouchDev t, int32_t *counters) {
     extern __shared__ uint32_t qs[];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {   // the list / score passes' counters (they run after this pass)
+        counters[0] = 0;
+        counters[1] = 0;
+    }
     // (only the delta keyframes' merges read the whole query: staged for them)
     const int items = nq + (t.nslots - t.delta0);
     const bool staged = nq <= kQLds && items > nq;
@@ -344,6 +349,7 @@ __global__ __launch_bounds__(kKT) void k_kfdb_score(const SlotDev *slots, int n,
                 if (qd.reloc || si >= qd.min_score) {
                     const int at = atomicAdd(qd.max_words + 1, 1);
                     if (at < qd.list_cap) list[at] = Listed{(uint32_t)first, s, si};
+                    else qd.over[at - qd.list_cap] = Listed{(uint32_t)first, s, si};
                 }
             }
         }
@@ -401,7 +407,13 @@ struct orbx_kfdb {
     int csr_ns = 0;
     int64_t csr_cap_post = 0, csr_cap_V = 0;
     uint32_t max_word = 0;
-    int4 *d_rec = nullptr;                        // per slot: what the last query met (QueryDev::rec)
+    // one buffer per database, brought back by one copy per query: the
+    // counters (16 B), the first kListCap survivors, the per-slot records
+    // (what the last query met, QueryDev::rec); then the survivors past
+    // kListCap (rarely copied)
+    uint8_t *d_qbuf = nullptr;
+    int4 *d_rec = nullptr;
+    Listed *d_over = nullptr;
     uint32_t stamp = 0;
     std::unordered_set<uint64_t> loop_qids, reloc_qids;   // query ids used so far
     int64_t cap_words = 0, dev_words = 0;        // arena capacity / words on the device
@@ -412,6 +424,7 @@ struct orbx_kfdb {
 namespace {
 
 constexpr int kListCap = 1024;   // scored keyframes brought back with the first copy
+constexpr size_t kQHdr = (16 + sizeof(Listed) * kListCap + 255) & ~size_t(255);   // counters + first survivors
 
 int kfdb_sync(orbx_kfdb *db) {
     // grow-and-upload the arena tail and the slot table; seed new slots' state
@@ -458,16 +471,21 @@ int kfdb_sync(orbx_kfdb *db) {
         (void)hipStreamSynchronize(db->st);
         if (db->d_slots) (void)hipFree(db->d_slots);
         if (db->d_state) (void)hipFree(db->d_state);
-        for (void *x : {(void *)db->d_qcnt, (void *)db->d_qfirst, (void *)db->d_rec})
+        for (void *x : {(void *)db->d_qcnt, (void *)db->d_qfirst, (void *)db->d_qbuf})
             if (x) (void)hipFree(x);
         db->d_slots = d;
         db->d_state = k;
         db->d_qcnt = nullptr;
         db->d_qfirst = nullptr;
+        db->d_qbuf = nullptr;
         db->d_rec = nullptr;
-        if (hipMalloc(reinterpret_cast<void **>(&db->d_rec), sizeof(int4) * (size_t)cap) != hipSuccess ||
-            hipMemsetAsync(db->d_rec, 0, sizeof(int4) * (size_t)cap, db->st) != hipSuccess)
+        db->d_over = nullptr;
+        if (hipMalloc(reinterpret_cast<void **>(&db->d_qbuf), kQHdr + (sizeof(int4) + sizeof(Listed)) * (size_t)cap) !=
+                hipSuccess)
             return ORBX_ENOMEM;
+        db->d_rec = reinterpret_cast<int4 *>(db->d_qbuf + kQHdr);
+        db->d_over = reinterpret_cast<Listed *>(db->d_qbuf + kQHdr + sizeof(int4) * (size_t)cap);
+        if (hipMemsetAsync(db->d_rec, 0, sizeof(int4) * (size_t)cap, db->st) != hipSuccess) return ORBX_ENOMEM;
         if (hipMalloc(reinterpret_cast<void **>(&db->d_qcnt), 4 * (size_t)cap) != hipSuccess ||
             hipMalloc(reinterpret_cast<void **>(&db->d_qfirst), 4 * (size_t)cap) != hipSuccess)
             return ORBX_ENOMEM;
@@ -595,8 +613,10 @@ int detect(orbx_kfdb *db, bool reloc, uint64_t qid, const uint32_t *words, const
     conn.erase(std::unique(conn.begin(), conn.end()), conn.end());
     Layout L;
     const size_t o_qw = L.add(4 * (size_t)n), o_qv = L.add(8 * (size_t)n), o_conn = L.add(4 * (conn.size() + 1));
-    const size_t o_mw = L.add(16), o_list = L.add(sizeof(Listed) * kListCap);   // brought back together
-    const size_t o_lst = L.add(16 * (size_t)ns), o_rec = L.add(sizeof(int4) * (size_t)ns);
+    const size_t in_bytes = L.size;
+    const size_t o_lst = L.add(16 * (size_t)ns);                          // the walk's list (device only)
+    const size_t o_rb = L.add(kQHdr + sizeof(int4) * (size_t)ns);          // the readback (host only)
+    const size_t o_ov = L.add(sizeof(Listed) * (size_t)std::max(ns - kListCap, 0));
     const bool repeated = !(reloc ? db->reloc_qids : db->loop_qids).insert(qid).second;
     if (++db->stamp == 0) ++db->stamp;   // (0: never written)
     CallWs &ws = call_ws(db->device);
@@ -606,15 +626,15 @@ int detect(orbx_kfdb *db, bool reloc, uint64_t qid, const uint32_t *words, const
     put(ws, o_qw, words, 4 * (size_t)n);
     put(ws, o_qv, values, 8 * (size_t)n);
     put(ws, o_conn, conn.data(), 4 * conn.size());
-    std::memset(ws.host + o_mw, 0, 16);   // (the counters go up zeroed with the query)
     uint8_t *D = ws.dev;
     QueryDev qd;
     qd.qid = qid;
     qd.reloc = reloc;
     qd.nconn = (int)conn.size();
     qd.min_score = minScore;
-    qd.max_words = at<int32_t>(D, o_mw);   // [0] maxCommonWords, [1] kept
+    qd.max_words = reinterpret_cast<int32_t *>(db->d_qbuf);   // [0] maxCommonWords, [1] kept (zeroed by touch)
     qd.list_cap = kListCap;
+    qd.over = db->d_over;
     qd.stamp = db->stamp;
     qd.rec = db->d_rec;
     TouchDev t;
@@ -626,36 +646,38 @@ int detect(orbx_kfdb *db, bool reloc, uint64_t qid, const uint32_t *words, const
     const size_t qlds = n <= kQLds ? 4 * (size_t)n : 0;
     const int items = n + (ns - db->csr_ns);
     if (hipStreamSynchronize(db->st) != hipSuccess ||
-        hipMemcpyAsync(D, ws.host, o_mw + 16, hipMemcpyHostToDevice, ws.st) != hipSuccess)
+        hipMemcpyAsync(D, ws.host, in_bytes, hipMemcpyHostToDevice, ws.st) != hipSuccess)
         return ORBX_EIO;
     hipLaunchKernelGGL(k_kfdb_touch, dim3(std::min(1024, (items + 3) / 4)), dim3(kKT), qlds, ws.st, db->d_slots,
-                       db->d_words, at<uint32_t>(D, o_qw), n, t);
+                       db->d_words, at<uint32_t>(D, o_qw), n, t, qd.max_words);
     hipLaunchKernelGGL(k_kfdb_list, dim3(std::min(256, (ns + kKT - 1) / kKT)), dim3(kKT), 0, ws.st, t,
                        at<int32_t>(D, o_conn), qd, db->d_state, at<int4>(D, o_lst));
     // few keyframes pass minCommonWords: a small persistent grid, each block
     // with the query words in LDS
     hipLaunchKernelGGL(k_kfdb_score, dim3(std::min(64, (ns + 3) / 4)), dim3(kKT), qlds, ws.st, db->d_slots,
                        ns, at<int4>(D, o_lst), db->d_words, db->d_values, at<uint32_t>(D, o_qw),
-                       at<double>(D, o_qv), n, qd, db->d_state, at<Listed>(D, o_list));
+                       at<double>(D, o_qv), n, qd, db->d_state, reinterpret_cast<Listed *>(db->d_qbuf + 16));
     if (hipGetLastError() != hipSuccess ||
-        hipMemcpyAsync(ws.host + o_mw, D + o_mw, o_lst - o_mw, hipMemcpyDeviceToHost, ws.st) != hipSuccess ||
-        hipMemcpyAsync(ws.host + o_rec, db->d_rec, sizeof(int4) * (size_t)ns, hipMemcpyDeviceToHost, ws.st) !=
+        hipMemcpyAsync(ws.host + o_rb, db->d_qbuf, kQHdr + sizeof(int4) * (size_t)ns, hipMemcpyDeviceToHost, ws.st) !=
             hipSuccess ||
         hipStreamSynchronize(ws.st) != hipSuccess)
         return ORBX_EIO;
     const double t_b = timing ? tms() : 0;
-    const int4 *rec = at<int4>(ws.host, o_rec);
+    const int4 *rec = at<int4>(ws.host, o_rb + kQHdr);
     int32_t mw[2];
-    get(ws, o_mw, mw, 8);
+    get(ws, o_rb, mw, 8);
     const int nsc = mw[1];
     if (nsc > kListCap &&
-        (hipMemcpyAsync(ws.host + o_list, D + o_list, sizeof(Listed) * (size_t)nsc, hipMemcpyDeviceToHost, ws.st) !=
-             hipSuccess ||
+        (hipMemcpyAsync(ws.host + o_ov, db->d_over, sizeof(Listed) * (size_t)(nsc - kListCap), hipMemcpyDeviceToHost,
+                        ws.st) != hipSuccess ||
          hipStreamSynchronize(ws.st) != hipSuccess))
         return ORBX_EIO;
     if (nsc == 0) return ORBX_OK;
     // the kept keyframes in the walk's order: (first shared word, add order)
-    std::vector<Listed> scored(at<Listed>(ws.host, o_list), at<Listed>(ws.host, o_list) + nsc);
+    const Listed *first = at<Listed>(ws.host, o_rb + 16);
+    std::vector<Listed> scored(first, first + std::min(nsc, kListCap));
+    if (nsc > kListCap)
+        scored.insert(scored.end(), at<Listed>(ws.host, o_ov), at<Listed>(ws.host, o_ov) + (nsc - kListCap));
     std::sort(scored.begin(), scored.end(), [](const Listed &a, const Listed &b) {
         return a.first != b.first ? a.first < b.first : a.slot < b.slot;
     });
@@ -767,7 +789,7 @@ void orbx_kfdb_destroy(orbx_kfdb *db) {
     if (db->d_values) (void)hipFree(db->d_values);
     if (db->d_slots) (void)hipFree(db->d_slots);
     if (db->d_state) (void)hipFree(db->d_state);
-    for (void *x : {(void *)db->d_qcnt, (void *)db->d_qfirst, (void *)db->d_rec, (void *)db->d_csr_off,
+    for (void *x : {(void *)db->d_qcnt, (void *)db->d_qfirst, (void *)db->d_qbuf, (void *)db->d_csr_off,
                     (void *)db->d_csr_cnt, (void *)db->d_csr_slot})
         if (x) (void)hipFree(x);
     if (db->st) (void)hipStreamDestroy(db->st);

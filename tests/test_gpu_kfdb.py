@@ -124,3 +124,28 @@ def test_kfdb_long_keyframes_and_many_slots(oracle_mod):
             o.add(i, *bows[i])
         assert res_g == res_o
         assert sum(len(x) > 0 for x in res_o) > 3
+
+
+def test_kfdb_more_candidates_than_the_first_copy(oracle_mod):
+    """More than 1,024 scored keyframes (the list the first copy brings back):
+    1,500 keyframes sharing most of their words with the query, so the
+    relocalisation query scores and keeps all of them."""
+    rng = np.random.default_rng(41)
+    base = np.sort(rng.choice(5000, 300, replace=False)).astype(np.uint32)
+    g, o = KeyFrameDatabase(), oracle_mod.KeyFrameDB(5000)
+    covis = {}
+    for i in range(1500):
+        w = np.unique(np.concatenate([base[rng.random(len(base)) < 0.95], rng.choice(5000, 20).astype(np.uint32)]))
+        v = rng.random(len(w)) + 0.1
+        v /= v.sum()
+        g.add(i, w, v)
+        o.add(i, w, v)
+        covis[i] = [j for j in (i - 1, i + 1, i + 7) if 0 <= j < 1500]
+    cv = lambda k: covis.get(k, [])   # noqa: E731
+    v = np.full(len(base), 1.0 / len(base))
+    a = g.DetectRelocalizationCandidates(99999, base, v, cv)
+    b = o.detect(True, 99999, base, v, None, 0.0, cv)
+    assert a == b and len(b) > 0
+    a = g.DetectLoopCandidates(99998, base, v, [3, 5], 0.0, cv)
+    b = o.detect(False, 99998, base, v, [3, 5], 0.0, cv)
+    assert a == b and len(b) > 0
