@@ -1393,6 +1393,7 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
     constexpr uint32_t kW0 = (uint32_t)kGaussTaps[0] | (uint32_t)kGaussTaps[1] << 8 |
                              (uint32_t)kGaussTaps[2] << 16 | (uint32_t)kGaussTaps[3] << 24;
     constexpr uint32_t kW1 = (uint32_t)kGaussTaps[4] | (uint32_t)kGaussTaps[5] << 8 | (uint32_t)kGaussTaps[6] << 16;
+    constexpr u16x2 kK01 = {(unsigned short)k0, (unsigned short)k1}, kK23 = {(unsigned short)k2, (unsigned short)k3};
     // One task = 8 consecutive outputs of one row at patch-aligned columns
     // 8s..8s+7 (window column = patch column - o): the 14 source bytes lie in
     // four aligned dwords, every 4-byte window of them one v_alignbyte.
@@ -1446,12 +1447,12 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
         // mul24u sees the low 24 bits of rb + kBlurR: 0x400000 + r + kBlurR (r, cc in [-18, 18])
         const int roff = (int)mul24u(rb + kBlurR, kRowS) - kRowS * 0x400000;
         const uint16_t *w = rowp + roff + (cc + kBlurR + o);
-        // k0 (w0 + w6) + k1 (w1 + w5) + k2 (w2 + w4) + k3 w3: symmetric pairs
-        // added first (full-rate adds), then 24-bit multiply-adds -- exact
-        // integers (each pair < 2^17, the sum < 2^24), so any grouping agrees
-        const uint32_t a06 = (uint32_t)w[0] + w[6 * kRowS], a15 = (uint32_t)w[kRowS] + w[5 * kRowS],
-                       a24 = (uint32_t)w[2 * kRowS] + w[4 * kRowS];
-        sums[k] = (int)(__umul24(a06, k0) + __umul24(a15, k1) + __umul24(a24, k2) + __umul24(w[3 * kRowS], k3));
+        // k0 (w0 + w6) + k1 (w1 + w5) + k2 (w2 + w4) + k3 w3 as three u16-pair dot products
+        // (the pairs are loaded straight into register halves)
+        const u16x2 r01 = {w[0], w[kRowS]}, r65 = {w[6 * kRowS], w[5 * kRowS]}, r23 = {w[2 * kRowS], w[3 * kRowS]};
+        sums[k] = (int)__builtin_amdgcn_udot2(
+            r01, kK01, __builtin_amdgcn_udot2(r65, kK01, __builtin_amdgcn_udot2(r23, kK23, mul24u(k2, w[4 * kRowS]), false), false),
+            false);
     }
     PHASE_MARK(1, 3);   // sincos + sample offsets + column pass
     int val[8];
