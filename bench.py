@@ -680,7 +680,7 @@ def run_config(torch, dist, rank, world, dev, w, h, nfeatures, streams, steps, w
         from orb_slam_2_ros_amd import ORBextractor
         ex = ORBextractor(nfeatures, 1.2, 8, 20, 7, device=dev.index)
     ex.reserve(w, h, 2 * batch if mode == "stereo" else batch)
-    if mode == "mono" and batch >= 64 and "ORBX_SPLIT" not in os.environ:
+    if batch >= 64 and "ORBX_SPLIT" not in os.environ:
         # two half-batches on forked streams: one half's latency-bound quadtree /
         # matcher launches overlap the other half's VALU-bound ones
         ex.split(2)

@@ -1038,7 +1038,11 @@ int orbx_stereo_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t
     if (rc) return rc;
     const int next = ex->cur ^ 1;
     prof_begin(ex);
-    rc = run_extract(ex, next, d_images, frame_stride, pitch, 2 * pairs, st);
+    {   // (a split batch joins before the pairs are matched: a part boundary may cut a pair)
+        const Parts P = fork_parts(ex, st, 2 * pairs);
+        rc = run_extract(ex, next, d_images, frame_stride, pitch, 2 * pairs, P);
+        if (!rc) rc = join_parts(ex, st, P);
+    }
     if (rc) return rc;
     ex->cur = next;
     ++ex->steps;
@@ -1074,7 +1078,11 @@ int orbx_rgbd_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t f
     if (rc) return rc;
     const int next = ex->cur ^ 1;
     prof_begin(ex);
-    rc = run_extract(ex, next, d_images, frame_stride, pitch, batch, st);
+    {
+        const Parts P = fork_parts(ex, st, batch);
+        rc = run_extract(ex, next, d_images, frame_stride, pitch, batch, P);
+        if (!rc) rc = join_parts(ex, st, P);
+    }
     if (rc) return rc;
     ex->cur = next;
     ++ex->steps;

@@ -95,6 +95,7 @@ def test_stereo_bench_configs(w, h, nf, P, oracle_mod):
     host, _, fr, _ = _frames(torch, "stereo", w, h, streams)
     ex = ORBextractor(nf, 1.2, 8, 20, 7)
     ex.reserve(w, h, 2 * P)
+    ex.split(2)   # (as bench.py times it)
     ex.stereo_step_device(fr[1].data_ptr(), w * h, w, P, BF, MB)
     torch.cuda.synchronize()
     deps = [ex.depth_download(p) for p in range(P)]
@@ -129,6 +130,7 @@ def test_rgbd_fhd_bench_configs(B, oracle_mod):
     host, depth, fr, dm = _frames(torch, "rgbd", w, h, streams)
     ex = ORBextractor(1000, 1.2, 8, 20, 7)
     ex.reserve(w, h, B)
+    ex.split(2)   # (as bench.py times it)
     ex.rgbd_step_device(fr[2].data_ptr(), w * h, w, B, dm.data_ptr(), 4 * w * h, 4 * w, BF)
     torch.cuda.synchronize()
     for b in [0, 1, B // 2 - 1, B // 2, B - 1]:
