@@ -669,7 +669,7 @@ class StubExtractor:
 
 
 def run_config(torch, dist, rank, world, dev, w, h, nfeatures, streams, steps, warmup, profile, mode="mono",
-               stub=None):
+               stub=None, split=2):
     """Times `steps` front-end steps of this rank's `streams` (global stream
     ids: mono / RGB-D frames or stereo pairs, one per stream per step); returns
     (max-over-ranks seconds, stage ms, kps, sanity, frames per launch, extractor)."""
@@ -683,7 +683,7 @@ def run_config(torch, dist, rank, world, dev, w, h, nfeatures, streams, steps, w
     if batch >= 64 and "ORBX_SPLIT" not in os.environ:
         # two half-batches on forked streams: one half's latency-bound quadtree /
         # matcher launches overlap the other half's VALU-bound ones
-        ex.split(2)
+        ex.split(split)
     host, depth = _resident_frames(mode, w, h, streams)
     frames = torch.from_numpy(host).to(dev)
     dmaps = torch.from_numpy(depth).to(dev) if depth is not None else None
@@ -744,6 +744,12 @@ EXTRAS = [
     ("stereo_fhd_1920x1080", "stereo", 1920, 1080, 1000, 192, "stereo pairs/s"),
     ("rgbd_fhd_1920x1080", "rgbd", 1920, 1080, 1000, 128, "frames/s"),
 ]
+
+# Batch split per extra where it does not pay: KITTI stereo at 96 pairs
+# measured 48.4 k pairs/s unsplit, 38.8 k split in two (the level pipeline
+# costs it 25 % the same way); every other config gains or is
+# neutral (EuRoC 106.4 / 107.8 k, FHD stereo 28.1 / 29.8 k, FHD RGB-D 56.2 / 58.6 k).
+EXTRA_SPLIT = {"stereo_kitti_1241x376": 1}
 
 # Config C5 (BASELINE.json configs[4]): 64 FHD RGB-D streams over the job's
 # GPUs (stream s -> rank s mod G), plus the cross-stream keyframe exchange.
@@ -892,7 +898,8 @@ def main() -> int:
             if key == args.extra:
                 streams = stream_partition(eb * world, world, rank)
                 el2, st2, nk2, sane2, _, ex2 = run_config(torch, dist, rank, world, dev, ew, eh, enf, streams,
-                                                          args.steps, args.warmup, profile, mode, stub(ew, eh))
+                                                          args.steps, args.warmup, profile, mode, stub(ew, eh),
+                                                          EXTRA_SPLIT.get(key, 2))
                 ex2.close()
                 res = {"value": round(world * eb * args.steps / el2, 2), "unit": unit, "stage_ms": st2,
                        "kps_last_frame": nk2}
@@ -929,7 +936,7 @@ def main() -> int:
             es = max(5, args.steps // 4)
             est = stream_partition(eb * world, world, rank)
             el2, st2, nk2, sane2, _, ex2 = run_config(torch, dist, rank, world, dev, ew, eh, enf, est, es, 2, profile,
-                                                      mode)
+                                                      mode, None, EXTRA_SPLIT.get(key, 2))
             ex2.close()
             extras[key] = {"value": round(world * eb * es / el2, 2), "unit": unit, "mode": mode,
                            "streams_per_gpu": eb, "nfeatures": enf, "stage_ms": st2,
