@@ -636,6 +636,7 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
             if (rl >= R) vmask = 0;   // (tail lanes: rows of the next pass)
             const uint8_t *q0 = patch + mul24u(3 + rl, PS) + qc0 + 4 * qi;
             const u16x2 thv = {(unsigned short)th, (unsigned short)th};
+            const u16x2 thv8 = {(unsigned short)(th << 8), (unsigned short)(th << 8)};
             int e = (rl << 8) + xx0;
             for (int y0 = 0; y0 < ch; y0 += R, e += R << 8) {
                 uint32_t cand = 0;
@@ -647,12 +648,16 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
                     const uint32_t up = *reinterpret_cast<const uint32_t *>(q - 3 * PS);
                     const uint32_t dn = *reinterpret_cast<const uint32_t *>(q + 3 * PS);
                     // pixel pairs (0, 2) and (1, 3) of the quad as u16 halves, straight from
-                    // the aligned dwords: v_perm picks any two bytes of (lo, hi) dword pairs
-                    auto half = [&](uint32_t sel, uint32_t sel4, uint32_t sel12) -> u16x2 {   // 1: candidate
-                        const u16x2 v = as_u16x2(__builtin_amdgcn_perm(0u, c, sel));
-                        const u16x2 a0 = as_u16x2(__builtin_amdgcn_perm(0u, dn, sel));
+                    // the aligned dwords (v_perm picks the +-3 column bytes of (lo, hi) dword
+                    // pairs); even pixels: bytes 0 / 2 as the low bytes of the halves (an AND
+                    // for the aligned dwords); odd pixels: bytes 1 / 3 left in the high
+                    // bytes, every value and the threshold scaled by 256 -- the same
+                    // comparisons, without the shift
+                    auto half = [&](uint32_t mask, uint32_t sel4, uint32_t sel12, u16x2 thv) -> u16x2 {   // 1: candidate
+                        const u16x2 v = as_u16x2(c & mask);
+                        const u16x2 a0 = as_u16x2(dn & mask);
                         const u16x2 a4 = as_u16x2(__builtin_amdgcn_perm(r, c, sel4));     // x + 3
-                        const u16x2 a8 = as_u16x2(__builtin_amdgcn_perm(0u, up, sel));
+                        const u16x2 a8 = as_u16x2(up & mask);
                         const u16x2 a12 = as_u16x2(__builtin_amdgcn_perm(c, l, sel12));   // x - 3
                         // max over the cyclic pairs of the pair's min, and min of the max:
                         // max(min(a,b), min(b,c), min(c,d), min(d,a)) = min(max(a,c), max(b,d))
@@ -668,8 +673,9 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
                         asm("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(d), "s"(0x00010001u));
                         return m;
                     };
-                    cand = (__builtin_bit_cast(uint32_t, half(0x0c020c00u, 0x0c050c03u, 0x0c030c01u)) |
-                            (__builtin_bit_cast(uint32_t, half(0x0c030c01u, 0x0c060c04u, 0x0c040c02u)) << 1)) & vmask;
+                    cand = (__builtin_bit_cast(uint32_t, half(0x00FF00FFu, 0x0c050c03u, 0x0c030c01u, thv)) |
+                            (__builtin_bit_cast(uint32_t, half(0xFF00FF00u, 0x060c040cu, 0x040c020cu, thv8)) << 1)) &
+                           vmask;
                 }
                 // compaction in row-major order: the lanes' counts (0..4) by their
                 // binary digits, one ballot each, then each lane's bits
