@@ -745,11 +745,10 @@ EXTRAS = [
     ("rgbd_fhd_1920x1080", "rgbd", 1920, 1080, 1000, 128, "frames/s"),
 ]
 
-# Batch split per extra where it does not pay: KITTI stereo at 96 pairs
-# measured 48.4 k pairs/s unsplit, 38.8 k split in two (the level pipeline
-# costs it 25 % the same way); every other config gains or is
-# neutral (EuRoC 106.4 / 107.8 k, FHD stereo 28.1 / 29.8 k, FHD RGB-D 56.2 / 58.6 k).
-EXTRA_SPLIT = {"stereo_kitti_1241x376": 1}
+# Batch split per extra (2 unless listed): every extra gains from the split or
+# is neutral (KITTI stereo 65.6 / 67.2 k unsplit / split, EuRoC 106.4 / 107.8 k,
+# FHD stereo 28.1 / 29.8 k, FHD RGB-D 56.2 / 58.6 k pairs or frames/s).
+EXTRA_SPLIT = {}
 
 # Config C5 (BASELINE.json configs[4]): 64 FHD RGB-D streams over the job's
 # GPUs (stream s -> rank s mod G), plus the cross-stream keyframe exchange.

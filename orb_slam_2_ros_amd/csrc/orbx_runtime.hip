@@ -565,6 +565,24 @@ int validate_batch(orbx_extractor *ex, const uint8_t *d_images, int pitch, int b
 // The kernels stage level 0 with aligned dword loads: base, pitch and frame
 // stride must be multiples of 4.  Other layouts are first copied (on the
 // stream) into an aligned staging buffer.
+// Level 0 repacked to a 4-aligned pitch, all frames in one launch: a
+// workgroup per (row, frame), a thread per destination dword (the source row
+// may start at any byte: four byte loads, one dword store).
+__global__ __launch_bounds__(256) void k_align_rows(const uint8_t *src, int64_t stride, int pitch, uint8_t *dst,
+                                                    int64_t fs, int dp, int w, int h) {
+    const int y = blockIdx.x, b = blockIdx.y;
+    const uint8_t *s = src + stride * b + (int64_t)pitch * y;
+    uint32_t *d = reinterpret_cast<uint32_t *>(dst + fs * b + (int64_t)dp * y);
+    for (int q = threadIdx.x; 4 * q < w; q += blockDim.x) {
+        const int x = 4 * q;
+        uint32_t v = s[x];
+        if (x + 1 < w) v |= (uint32_t)s[x + 1] << 8;
+        if (x + 2 < w) v |= (uint32_t)s[x + 2] << 16;
+        if (x + 3 < w) v |= (uint32_t)s[x + 3] << 24;
+        d[q] = v;
+    }
+}
+
 int align_level0(orbx_extractor *ex, const uint8_t **d_images, int64_t *stride, int *pitch, int batch,
                  hipStream_t st) {
     if ((((uintptr_t)*d_images) | (uintptr_t)*stride | (uintptr_t)*pitch) % 4 == 0) return ORBX_OK;
@@ -576,10 +594,9 @@ int align_level0(orbx_extractor *ex, const uint8_t **d_images, int64_t *stride, 
         if (dalloc(&ex->d_img, need) != hipSuccess) return ORBX_ENOMEM;
         ex->d_img_bytes = need;
     }
-    for (int b = 0; b < batch; ++b)
-        if (hipMemcpy2DAsync(ex->d_img + fs * b, dp, *d_images + *stride * b, *pitch, w, h, hipMemcpyDeviceToDevice,
-                             st) != hipSuccess)
-            return ORBX_EIO;
+    hipLaunchKernelGGL(k_align_rows, dim3(h, batch), dim3(256), 0, st, *d_images, *stride, *pitch, ex->d_img,
+                       (int64_t)fs, (int)dp, w, h);
+    if (hipGetLastError() != hipSuccess) return ORBX_EIO;
     *d_images = ex->d_img;
     *stride = (int64_t)fs;
     *pitch = (int)dp;

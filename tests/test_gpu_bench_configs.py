@@ -83,7 +83,7 @@ def test_mono_bench_config_b1536_split2(oracle_mod):
 
 STEREO_CONFIGS = [   # bench.py EXTRAS: (w, h, nfeatures, pairs, split as bench.py runs it)
     (752, 480, 1200, 128, 2),
-    (1241, 376, 2000, 96, 1),
+    (1241, 376, 2000, 96, 2),
     (1920, 1080, 1000, 192, 2),
 ]
 
