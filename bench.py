@@ -669,7 +669,7 @@ class StubExtractor:
 
 
 def run_config(torch, dist, rank, world, dev, w, h, nfeatures, streams, steps, warmup, profile, mode="mono",
-               stub=None, split=2):
+               stub=None, split=2, pipeline=0):
     """Times `steps` front-end steps of this rank's `streams` (global stream
     ids: mono / RGB-D frames or stereo pairs, one per stream per step); returns
     (max-over-ranks seconds, stage ms, kps, sanity, frames per launch, extractor)."""
@@ -684,6 +684,8 @@ def run_config(torch, dist, rank, world, dev, w, h, nfeatures, streams, steps, w
         # two half-batches on forked streams: one half's latency-bound quadtree /
         # matcher launches overlap the other half's VALU-bound ones
         ex.split(split)
+    if pipeline and stub is None and "ORBX_PIPELINE" not in os.environ:
+        ex.pipeline(1)   # level pipeline: on where it measured faster
     host, depth = _resident_frames(mode, w, h, streams)
     frames = torch.from_numpy(host).to(dev)
     dmaps = torch.from_numpy(depth).to(dev) if depth is not None else None
@@ -749,6 +751,12 @@ EXTRAS = [
 # is neutral (KITTI stereo 65.6 / 67.2 k unsplit / split, EuRoC 106.4 / 107.8 k,
 # FHD stereo 28.1 / 29.8 k, FHD RGB-D 56.2 / 58.6 k pairs or frames/s).
 EXTRA_SPLIT = {}
+# Level pipeline per config (off unless listed), on / off measured on one box:
+# VGA 1536 streams 318.0 / 314.5 k, FHD stereo 31.2 / 29.9 k pairs/s -- and
+# off elsewhere: FHD 53.1 / 57.4 k, HD 116.0 / 123.9 k, FHD RGB-D 54.2 / 58.3 k,
+# EuRoC 98.5 / 108.2 k, KITTI 62.0 / 67.3 k
+EXTRA_PIPE = {"stereo_fhd_1920x1080": 1}
+HEADLINE_PIPE = 1
 
 # Config C5 (BASELINE.json configs[4]): 64 FHD RGB-D streams over the job's
 # GPUs (stream s -> rank s mod G), plus the cross-stream keyframe exchange.
@@ -898,7 +906,7 @@ def main() -> int:
                 streams = stream_partition(eb * world, world, rank)
                 el2, st2, nk2, sane2, _, ex2 = run_config(torch, dist, rank, world, dev, ew, eh, enf, streams,
                                                           args.steps, args.warmup, profile, mode, stub(ew, eh),
-                                                          EXTRA_SPLIT.get(key, 2))
+                                                          EXTRA_SPLIT.get(key, 2), EXTRA_PIPE.get(key, 0))
                 ex2.close()
                 res = {"value": round(world * eb * args.steps / el2, 2), "unit": unit, "stage_ms": st2,
                        "kps_last_frame": nk2}
@@ -911,7 +919,8 @@ def main() -> int:
     w, h, nf, B = args.width, args.height, args.nfeatures, args.batch
     streams = stream_partition(B * world, world, rank)          # weak scaling: B streams per GPU
     el, stages, nkp_last, nm_last, frames_per_launch, ex = run_config(
-        torch, dist, rank, world, dev, w, h, nf, streams, args.steps, args.warmup, profile, "mono", stub(w, h))
+        torch, dist, rank, world, dev, w, h, nf, streams, args.steps, args.warmup, profile, "mono", stub(w, h), 2,
+        HEADLINE_PIPE)
     ex.close()
     frames_total = world * B * args.steps
     value = frames_total / el
@@ -935,7 +944,7 @@ def main() -> int:
             es = max(5, args.steps // 4)
             est = stream_partition(eb * world, world, rank)
             el2, st2, nk2, sane2, _, ex2 = run_config(torch, dist, rank, world, dev, ew, eh, enf, est, es, 2, profile,
-                                                      mode, None, EXTRA_SPLIT.get(key, 2))
+                                                      mode, None, EXTRA_SPLIT.get(key, 2), EXTRA_PIPE.get(key, 0))
             ex2.close()
             extras[key] = {"value": round(world * eb * es / el2, 2), "unit": unit, "mode": mode,
                            "streams_per_gpu": eb, "nfeatures": enf, "stage_ms": st2,

@@ -59,6 +59,7 @@ def test_mono_bench_config_b1536_split2(oracle_mod):
     ex = ORBextractor(1000, 1.2, 8, 20, 7)
     ex.reserve(w, h, B)
     ex.split(2)
+    ex.pipeline(bench.HEADLINE_PIPE)   # (as bench.py times it)
     assert ex.split() == 2
     for t in range(2):
         ex.mono_step_device(fr[t].data_ptr(), w * h, w, B, 100, 0.9, True)
@@ -81,21 +82,22 @@ def test_mono_bench_config_b1536_split2(oracle_mod):
     ex.close()
 
 
-STEREO_CONFIGS = [   # bench.py EXTRAS: (w, h, nfeatures, pairs, split as bench.py runs it)
-    (752, 480, 1200, 128, 2),
-    (1241, 376, 2000, 96, 2),
-    (1920, 1080, 1000, 192, 2),
+STEREO_CONFIGS = [   # bench.py EXTRAS: (w, h, nfeatures, pairs, split, level pipeline as bench.py runs it)
+    (752, 480, 1200, 128, 2, 0),
+    (1241, 376, 2000, 96, 2, 0),
+    (1920, 1080, 1000, 192, 2, 1),
 ]
 
 
-@pytest.mark.parametrize("w,h,nf,P,split", STEREO_CONFIGS)
-def test_stereo_bench_configs(w, h, nf, P, split, oracle_mod):
+@pytest.mark.parametrize("w,h,nf,P,split,pipe", STEREO_CONFIGS)
+def test_stereo_bench_configs(w, h, nf, P, split, pipe, oracle_mod):
     import torch
     streams = list(range(P))
     host, _, fr, _ = _frames(torch, "stereo", w, h, streams)
     ex = ORBextractor(nf, 1.2, 8, 20, 7)
     ex.reserve(w, h, 2 * P)
     ex.split(split)   # (as bench.py times it)
+    ex.pipeline(pipe)
     ex.stereo_step_device(fr[1].data_ptr(), w * h, w, P, BF, MB)
     torch.cuda.synchronize()
     deps = [ex.depth_download(p) for p in range(P)]

@@ -10,8 +10,9 @@ R=$(pwd)
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-# whole-batch launches (bench.py otherwise splits the timed batch in two)
-export ORBX_SPLIT=1
+# whole-batch, unpipelined launches (bench.py otherwise splits the timed batch
+# in two and pipelines the levels)
+export ORBX_SPLIT=1 ORBX_PIPELINE=0
 B=(python "$R/bench.py" --steps 5 --warmup 2 --cpu-seconds 0 --no-extras --no-profile "$@")
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o trace -- "${B[@]}" > "$OUT/trace.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o pmc -- "${B[@]}" > "$OUT/fetch.log" 2>&1
