@@ -480,7 +480,7 @@ def stream_scene(s: int) -> int:
     """Synthetic scene of global stream s: the content is a function of the
     stream id alone, so a stream's frames (and outputs) do not depend on how
     many ranks share the job.  UNIQUE_SCENES distinct scenes keep the set-up
-    cheap at 1536 streams per GPU."""
+    cheap at 3072 streams per GPU."""
     return s % UNIQUE_SCENES
 
 
@@ -857,8 +857,9 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    # VGA streams per GPU swept (split 2): 1024 -> 306k, 1536 -> 311.5-313.3k, 2048 -> 310.8-311.7k frames/s
-    ap.add_argument("--batch", type=int, default=1536, help="streams (frames per step) per GPU")
+    # VGA streams per GPU swept (split 2, level pipeline on): 1536 -> 315.1-316.6k, 2048 -> 318.5-319.5k,
+    # 2560 -> 319.5-320.3k, 3072 -> 321.5-321.7k frames/s (split 2, pipeline off: 1024 -> 306k, 1536 -> 312k)
+    ap.add_argument("--batch", type=int, default=3072, help="streams (frames per step) per GPU")
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--nfeatures", type=int, default=1000)

@@ -49,11 +49,11 @@ def _frames(torch, mode, w, h, streams):
     return host, depth, fr, dm
 
 
-def test_mono_bench_config_b1536_split2(oracle_mod):
-    """The headline timed region: 1536 VGA streams, split 2, two steps (the
-    second matches against the first)."""
+def test_mono_bench_config_b3072_split2(oracle_mod):
+    """The headline timed region: 3072 VGA streams, split 2, level pipeline on,
+    two steps (the second matches against the first)."""
     import torch
-    w, h, B = 640, 480, 1536
+    w, h, B = 640, 480, 3072
     streams = list(range(B))
     host, _, fr, _ = _frames(torch, "mono", w, h, streams)
     ex = ORBextractor(1000, 1.2, 8, 20, 7)
