@@ -858,7 +858,8 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     # VGA streams per GPU swept (split 2, level pipeline on): 1536 -> 315.1-316.6k, 2048 -> 318.5-319.5k,
-    # 2560 -> 319.5-320.3k, 3072 -> 321.5-321.7k frames/s (split 2, pipeline off: 1024 -> 306k, 1536 -> 312k)
+    # 2560 -> 319.5-320.3k, 3072 -> 321.5-322.3k, 4096 -> 323.7-324.2k frames/s (split 2, pipeline off:
+    # 1024 -> 306k, 1536 -> 312k); 3072 keeps the resident frames at 3.8 GB per rank
     ap.add_argument("--batch", type=int, default=3072, help="streams (frames per step) per GPU")
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
