@@ -487,7 +487,11 @@ typedef int (*orbx_covis_fn)(void *ctx, uint64_t kf_id, uint64_t *out, int cap);
 int orbx_kfdb_create(int device, orbx_kfdb **out);
 void orbx_kfdb_destroy(orbx_kfdb *db);
 /* add (:37-44) / erase (:46-67) / clear (:69-73).  Adding an id that is in the
- * database is ORBX_EINVAL (the reference would list it twice). */
+ * database is ORBX_EINVAL (the reference would list it twice), and so is a
+ * word id >= ORBX_KFDB_MAX_WORDS (the inverted file is indexed by word id;
+ * ORBvoc has 10^6 words).  A query id of 0 matches every keyframe never
+ * queried (the reference's mnLoopQuery / mnRelocQuery start at 0). */
+#define ORBX_KFDB_MAX_WORDS (1u << 26)
 int orbx_kfdb_add(orbx_kfdb *db, uint64_t kf_id, const uint32_t *words, const double *values, int n);
 int orbx_kfdb_erase(orbx_kfdb *db, uint64_t kf_id);
 int orbx_kfdb_clear(orbx_kfdb *db);

@@ -15,6 +15,7 @@
 #include "orbx_oracle.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cfloat>
 #include <climits>
 #include <cmath>
@@ -406,7 +407,29 @@ void divide(const QNode &p, const std::vector<Corner> &c, QNode ch[4]) {
     for (int q = 0; q < 4; ++q) ch[q].no_more = ch[q].keys.size() == 1;
 }
 
+// Diagnostic (tools/tie_exposure.py): how often the reference's pointer tie
+// rule could matter.  [0] levels, [1] levels with a final phase, [2] final
+// rounds, [3] rounds splitting >= 2 equal-size nodes (their children's list
+// order follows the tie rule), [4] nodes in those groups, [5] rounds whose
+// cutoff falls inside a group of equal-size nodes (which of them are split
+// follows the tie rule), [6] nodes in those groups, [7] levels with [3] or
+// [5], [8] levels with [5].
+static std::atomic<long> g_tie[9];   // (the CPU baseline runs the oracle on many threads)
+// Tie order of the final-phase sort: 0 creation order (the restatement's rule),
+// 1 reverse creation order, k >= 2 a seeded pseudo-random order -- other heap
+// layouts the reference could meet (diagnostic only: tools/tie_exposure.py).
+static std::atomic<int> g_tie_mode{0};
+static inline unsigned long tie_key(long seq, int mode) {
+    if (mode == 0) return (unsigned long)seq;
+    if (mode == 1) return ~(unsigned long)seq;
+    unsigned long z = (unsigned long)seq * 0x9E3779B97F4A7C15ull + (unsigned long)mode * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 31)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 29);
+}
+
 std::vector<int> distribute(const std::vector<Corner> &c, int w, int h, int N) {
+    ++g_tie[0];
+    bool lv_any = false, lv_set = false, lv_final = false;
     const int minX = 16, maxX = w - 16, minY = 16, maxY = h - 16;
     std::vector<int> result;
     if (c.empty()) return result;
@@ -469,20 +492,47 @@ std::vector<int> distribute(const std::vector<Corner> &c, int w, int h, int N) {
                 const int prev = (int)L.size();
                 std::vector<Expand> todo = expand;
                 expand.clear();
-                std::sort(todo.begin(), todo.end(), [](const Expand &a, const Expand &b) {
-                    return a.size != b.size ? a.size < b.size : a.seq < b.seq;
+                const int tm = g_tie_mode.load(std::memory_order_relaxed);
+                std::sort(todo.begin(), todo.end(), [tm](const Expand &a, const Expand &b) {
+                    return a.size != b.size ? a.size < b.size : tie_key(a.seq, tm) < tie_key(b.seq, tm);
                 });
+                int jb = 0;   // lowest split index
                 for (int j = (int)todo.size() - 1; j >= 0; --j) {
                     QNode ch[4];
                     divide(*todo[j].node, c, ch);
                     push_children(ch, false, nullptr);
                     L.erase(todo[j].node->self);
+                    jb = j;
                     if ((int)L.size() >= N) break;
+                }
+                if (!lv_final) { lv_final = true; ++g_tie[1]; }
+                ++g_tie[2];
+                {   // tie groups among the split nodes todo[jb..]
+                    bool ord = false;
+                    long ord_nodes = 0;
+                    for (int a = jb; a < (int)todo.size();) {
+                        int e = a;
+                        while (e + 1 < (int)todo.size() && todo[e + 1].size == todo[a].size) ++e;
+                        const int lo = std::max(a, jb);
+                        if (e - lo + 1 >= 2) { ord = true; ord_nodes += e - lo + 1; }
+                        a = e + 1;
+                    }
+                    if (ord) { ++g_tie[3]; g_tie[4] += ord_nodes; lv_any = true; }
+                    if (jb > 0 && todo[jb - 1].size == todo[jb].size) {
+                        int a = jb, e = jb;
+                        while (a > 0 && todo[a - 1].size == todo[jb].size) --a;
+                        while (e + 1 < (int)todo.size() && todo[e + 1].size == todo[jb].size) ++e;
+                        ++g_tie[5];
+                        g_tie[6] += e - a + 1;
+                        lv_any = lv_set = true;
+                    }
                 }
                 if ((int)L.size() >= N || (int)L.size() == prev) finish = true;
             }
         }
     }
+    if (lv_any) ++g_tie[7];
+    if (lv_set) ++g_tie[8];
     for (const QNode &n : L) {
         int best = n.keys[0];
         for (size_t k = 1; k < n.keys.size(); ++k)
@@ -630,6 +680,12 @@ int orbo_level_candidates(const uint8_t *lvl, int w, int h, int iniTh, int minTh
         xys[3 * i] = c[i].x; xys[3 * i + 1] = c[i].y; xys[3 * i + 2] = c[i].score;
     }
     return n;
+}
+
+void orbo_set_tie_mode(int mode) { g_tie_mode = mode; }
+
+void orbo_tie_stats(int64_t out[9], int reset) {
+    for (int i = 0; i < 9; ++i) out[i] = reset ? g_tie[i].exchange(0) : g_tie[i].load();
 }
 
 int orbo_distribute(const int32_t *xys, int n, int w, int h, int N, int32_t *sel) {

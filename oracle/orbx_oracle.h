@@ -64,6 +64,8 @@ int   orbo_level_candidates(const uint8_t *lvl, int w, int h, int iniTh, int min
                             int32_t *xys, int cap);
 /* DistributeOctTree on a candidate list (ORBextractor.cc:561-787): writes the
  * selected candidate indices in output order; returns the count. */
+void  orbo_tie_stats(int64_t out[9], int reset);   /* diagnostic, see orbx_oracle.cpp */
+void  orbo_set_tie_mode(int mode);                  /* diagnostic: 0 = the restatement's rule */
 int   orbo_distribute(const int32_t *xys, int n, int w, int h, int N, int32_t *sel);
 /* Full operator() (ORBextractor.cc:1083-1149).  Returns 0, or -1 if cap is
  * too small (then *n_out holds the required count). */

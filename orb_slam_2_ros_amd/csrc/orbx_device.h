@@ -36,6 +36,7 @@ struct DevPlan {
     const ResizeTap *xtaps;
     const ResizeTap *ytaps;
     const int4 *blur_tiles;   // (level, x0, y0, 0) per 64x16 output tile
+    const uint32_t *slot_level;  // level of each output slot (out_cap entries): k_describe's one scalar load
     int nlevels, ncells, nblur_tiles;
     int gauss[7];
     int umax[16];

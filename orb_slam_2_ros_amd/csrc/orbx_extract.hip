@@ -95,7 +95,8 @@ __device__ inline const uint8_t *level_ptr(const DevPlan &p, const FrameBufs &fb
 // (overlapping cell rings / keypoint patches hit instead of refetching).
 constexpr int kXcds = 8;
 __device__ inline int xcd_logical_block(int j, int n) {
-    const int per = n / kXcds, rem = n % kXcds, xcd = j % kXcds, idx = j / kXcds;
+    const int per = (int)((uint32_t)n / kXcds), rem = (int)((uint32_t)n % kXcds), xcd = (int)((uint32_t)j % kXcds),
+              idx = (int)((uint32_t)j / kXcds);
     return xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
 }
 
@@ -107,6 +108,17 @@ __device__ inline void xcd_block_2d(int &bx, int &by) {
     // results back to the scalar unit, so the code that depends on them stays SALU)
     by = __builtin_amdgcn_readfirstlane(L / gridDim.x);
     bx = __builtin_amdgcn_readfirstlane(L - by * gridDim.x);
+}
+
+// The same with the division by gridDim.x as a multiply-high by a host-made
+// magic ceil(2^32 / gridDim.x), exact while (blocks) x gridDim.x < 2^32
+// (checked by the launcher; magic 0 = divide): 3 scalar instructions instead of
+// the ~20 of a 32-bit division.
+__device__ inline void xcd_block_2d(int &bx, int &by, uint32_t magic) {
+    const int n = gridDim.x * gridDim.y;
+    const int L = xcd_logical_block(blockIdx.y * gridDim.x + blockIdx.x, n);
+    by = magic ? (int)__umulhi((uint32_t)L, magic) : L / (int)gridDim.x;
+    bx = L - by * (int)gridDim.x;
 }
 
 // The wave's index in its workgroup as a scalar: the compiler cannot prove
@@ -1266,76 +1278,112 @@ __global__ __launch_bounds__(kThreads, 6) void k_quadtree(DevPlan p, FrameBufs f
 // ===========================================================================
 constexpr int kDescR = 21;                  // patch radius = 18 (samples) + 3 (blur taps)
 constexpr int kDescP = 2 * kDescR + 1;      // 43
-constexpr int kDescPS = 52;                 // patch row stride (bytes): 43 + align offset + row-pass overread
+#ifndef ORBX_ROWPASS_DOT4
+constexpr int kDescPS = 48;                 // patch row stride (bytes): 43 + align offset, 8-aligned rows
+#else
+constexpr int kDescPS = 52;                 // 43 + align offset + dot4 row-pass overread
+#endif
 constexpr int kBlurR = 18;
-constexpr int kRowS = 40;                   // row-pass stride (u16): 10 groups of 4 outputs
-constexpr int kDescRowOff = (kDescP * kDescPS + 15) & ~15;          // row-pass buffer, 16-aligned
-constexpr int kDescWaveLds = kDescRowOff + kDescP * kRowS * 2;        // 5680 B
+constexpr int kRowS = 40;                   // row-pass stride (u16): outputs at patch columns 0..39
+// The row-pass buffer follows the patch directly.  The MFMA row pass reads
+// 48 rows x 64 columns at the patch stride (rows 43..47, and columns past 45
+// that wrap into the next row, are either multiplied by zero taps or feed
+// outputs that are never stored), so those reads may run into the row
+// buffer: they all precede the wave's stores.
+constexpr int kDescRowOff = (kDescP * kDescPS + 15) & ~15;             // 2064
+constexpr int kDescWaveLds = kDescRowOff + kDescP * kRowS * 2;        // 5504 B
+constexpr int kDescWaveStride = (kDescWaveLds + 15) & ~15;
+static_assert(47 * kDescPS + 63 < kDescWaveLds, "MFMA row-pass reads stay inside the wave's LDS");
+// LDS is allocated per workgroup in 512-byte granules: 4 waves + 48 B of
+// shared angle records must fit 7 workgroups in a CU's 160 KB
+static_assert(7 * ((4 * kDescWaveStride + 48 + 511) & ~511) <= 160 * 1024, "k_describe: 7 workgroups per CU");
+
+// The row pass as an int8 matrix product (v_mfma_i32_16x16x32_i8): outputs
+// j = 0..15 of a 16-column tile from the tile's 32 input columns,
+//   R[r][16 t + j] = sum_c T[j][c] P[r][16 t + c],  T[j][c] = w[c - j] (0 <= c - j <= 6).
+// T is the A operand, lane l holds T[l & 15][8 (l >> 4) + 0..7] (8 bytes, i8:
+// the taps are <= 55).  The pixels go in as P - 128 (xor 0x80), so the
+// accumulator starts at 128 * sum(w) = 128 * 257 = 32896, and the exact i32
+// result is the reference's integer row sum (<= 65535).
+struct RowTaps {
+    uint64_t t[64];
+    constexpr RowTaps() : t() {
+        for (int l = 0; l < 64; ++l) {
+            uint64_t v = 0;
+            for (int jj = 0; jj < 8; ++jj) {
+                const int d = 8 * (l >> 4) + jj - (l & 15);
+                if (d >= 0 && d <= 6) v |= (uint64_t)kGaussTaps[d] << (8 * jj);
+            }
+            t[l] = v;
+        }
+    }
+};
+__constant__ RowTaps c_row_taps = RowTaps();
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 template <bool PIPE>
-__global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs fb, int s0, int ns, int write_total) {
-    __shared__ __align__(16) uint8_t lds[4 * ((kDescWaveLds + 15) & ~15)];
+__global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs fb, int s0, int ns, int write_total,
+                                                           uint32_t gmagic) {
+    __shared__ __align__(16) uint8_t lds[4 * kDescWaveStride];
+    __shared__ int s_mom[4][2];      // each wave's (m01, m10)
+    __shared__ float s_ang[4][3];    // each wave's (angle, sin, cos), computed by wave 0
     PHASE_START();
     const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
     // this lane's 4 pattern pairs (bytes x0 y0 x1 y1 of pairs 2j, 2j + 1,
     // j = 64 grp + lane), fetched first so the loads overlap the staging
     float4 pat[4];
     uint32_t dmask[4];
+#ifndef ORBX_ROWPASS_DOT4
+    const long row_taps = (long)c_row_taps.t[lane];
+#endif
 #pragma unroll
     for (int grp = 0; grp < 4; ++grp) pat[grp] = reinterpret_cast<const float4 *>(c_pattern_f)[grp * 64 + lane];
 #pragma unroll
     for (int i = 0; i < 4; ++i) dmask[i] = c_disc_mask.m[(lane >> 3) + 8 * i][lane & 7];
     int bx, b;
-    xcd_block_2d(bx, b);
-    const int32_t *lc = fb.level_count + (int64_t)b * kMaxLevels;
+    xcd_block_2d(bx, b, gmagic);
     const int slot = s0 + bx * 4 + wave;
-    // level of this slot from the kernel-argument offsets; the key and the
-    // level counts are independent loads issued together
-    // (scalar compare-selects: the compiler turns `(a && b) ? 1 : 0` on
-    // wave-uniform values into lane masks and v_cndmask + readfirstlane)
-    auto s_ge = [](int a, int b) {
-        int r;
-        asm("s_cmp_ge_i32 %1, %2\n\ts_cselect_b32 %0, 1, 0" : "=s"(r) : "s"(a), "s"(b) : "scc");
-        return r;
-    };
-    int l = 0;
-#pragma unroll
-    for (int q = 1; q < kMaxLevels; ++q) l += s_ge(p.nlevels - 1, q) & s_ge(slot, p.la[q].out_off);
-    const uint32_t key = slot < p.out_cap ? __builtin_amdgcn_readfirstlane(fb.sel[(int64_t)b * p.out_cap + slot]) : 0u;
-    // all kMaxLevels counts loaded unconditionally (one scalar burst, no
-    // load-wait chain), the levels past nlevels masked afterwards
-    int cnt[kMaxLevels];
-#pragma unroll
-    for (int q = 0; q < kMaxLevels; ++q) cnt[q] = lc[q];
-#pragma unroll
-    for (int q = 0; q < kMaxLevels; ++q) cnt[q] = q < p.nlevels ? max(cnt[q], 0) : 0;
-    if (write_total && bx == 0 && tid == 0) {
-        int total = 0;
-#pragma unroll
-        for (int q = 0; q < kMaxLevels; ++q) total += cnt[q];
-        fb.nkps[b] = total;
-    }
-    if (slot >= p.out_cap || bx * 4 + wave >= ns) return;
+    const bool in_range = slot < p.out_cap && bx * 4 + wave < ns;
+    // level of this slot (plan table) and the selected key: scalar loads
+    const int l = in_range ? (int)p.slot_level[slot] : 0;
+    const uint32_t key = in_range ? __builtin_amdgcn_readfirstlane(fb.sel[(int64_t)b * p.out_cap + slot]) : 0u;
+    // the frame's level counts: lane q < nlevels holds count q; the slot's
+    // output offset is the prefix below its level (16-lane DPP scan)
+    const int32_t *lc = fb.level_count + (int64_t)b * kMaxLevels;
+    const int lq = lane & (kMaxLevels - 1);
+    const int cq = lane < p.nlevels ? max(lc[lq], 0) : 0;
+    static_assert(kMaxLevels == 16, "one DPP row");
+    uint32_t scan = (uint32_t)cq;
+    scan += dpp_or<kRowShr1>(0u, scan);
+    scan += dpp_or<kRowShr2>(0u, scan);
+    scan += dpp_or<kRowShr4>(0u, scan);
+    scan += dpp_or<kRowShr8>(0u, scan);
+    const int cl = __builtin_amdgcn_readlane(cq, l);
+    const int off = __builtin_amdgcn_readlane((int)scan, l) - cl;
+    if (write_total && bx == 0 && tid == 0) fb.nkps[b] = __builtin_amdgcn_readlane((int)scan, kMaxLevels - 1);
+    // (no early exit: every wave reaches the block's two barriers)
     const LevelArgs g = p.la[l];
     const int i = slot - g.out_off;
-    int off = 0, cl = 0;
-#pragma unroll
-    for (int q = 0; q < kMaxLevels; ++q) {
-        off += q < l ? cnt[q] : 0;
-        cl = q == l ? cnt[q] : cl;
-    }
-    if (i >= cl) return;
+    const bool valid = in_range && i < cl;
     const int x = (int)(key & 0xFFF), y = (int)((key >> 12) & 0xFFF), score = (int)(key >> 24);
 
-    uint8_t *lbase = lds + wave * ((kDescWaveLds + 15) & ~15);
+    uint8_t *lbase = lds + wave * kDescWaveStride;
     uint16_t *rowp = reinterpret_cast<uint16_t *>(lbase + kDescRowOff);
+    // taps of getGaussianKernel(7, 2) x256 (checked against the plan on the host)
+    constexpr int k0 = kGaussTaps[0], k1 = kGaussTaps[1], k2 = kGaussTaps[2], k3 = kGaussTaps[3];
+    // Taps as byte vectors for v_dot4_u32_u8: out[j] = dot4(px[j..j+3], W0) + dot4(px[j+4..j+7], W1).
+    constexpr uint32_t kW0 = (uint32_t)kGaussTaps[0] | (uint32_t)kGaussTaps[1] << 8 |
+                             (uint32_t)kGaussTaps[2] << 16 | (uint32_t)kGaussTaps[3] << 24;
+    constexpr uint32_t kW1 = (uint32_t)kGaussTaps[4] | (uint32_t)kGaussTaps[5] << 8 | (uint32_t)kGaussTaps[6] << 16;
+    constexpr u16x2 kK01 = {(unsigned short)k0, (unsigned short)k1}, kK23 = {(unsigned short)k2, (unsigned short)k3};
+    int o = 0;
+    if (valid) {
 
     // 1. stage the 43x43 unblurred neighbourhood: aligned dword loads when it
     //    lies inside the level, else byte loads with reflect-101 at the borders
     int spitch;
     const uint8_t *img = level_ptr(p, fb, l, b, spitch);
     const int px0 = x - kDescR, py0 = y - kDescR;
-    int o = 0;
     if (px0 >= 0 && py0 >= 0 && x + kDescR < g.w && y + kDescR < g.h &&
         (px0 & ~3) + 4 * (((px0 & 3) + kDescP + 3) >> 2) <= spitch) {
         o = wave_stage_rows<(kDescP + 4) / 5>(lbase, kDescPS, img, spitch, py0, px0, kDescP, kDescP, lane);   // 5 rows a pass
@@ -1387,19 +1435,50 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
     }
     m10 = wave_sum_i32(m10);
     m01 = wave_sum_i32(m01);
-    const float angle = fast_atan2_deg((float)m01, (float)m10);
-    PHASE_MARK(1, 1);   // moments + atan
+    if (lane == 0) {
+        s_mom[wave][0] = m01;
+        s_mom[wave][1] = m10;
+    }
+    PHASE_MARK(1, 1);   // moments
 
     // 3. Gaussian 7x7 restricted to the 37x37 sample window: row pass over all
     //    43 rows (8-wide segments slide along a row), then the column pass with
     //    OpenCV 3.2's per-column rounding (half-even below w & ~3, else half-up).
-    // taps of getGaussianKernel(7, 2) x256 (checked against the plan on the host)
-    constexpr int k0 = kGaussTaps[0], k1 = kGaussTaps[1], k2 = kGaussTaps[2], k3 = kGaussTaps[3];
-    // Taps as byte vectors for v_dot4_u32_u8: out[j] = dot4(px[j..j+3], W0) + dot4(px[j+4..j+7], W1).
-    constexpr uint32_t kW0 = (uint32_t)kGaussTaps[0] | (uint32_t)kGaussTaps[1] << 8 |
-                             (uint32_t)kGaussTaps[2] << 16 | (uint32_t)kGaussTaps[3] << 24;
-    constexpr uint32_t kW1 = (uint32_t)kGaussTaps[4] | (uint32_t)kGaussTaps[5] << 8 | (uint32_t)kGaussTaps[6] << 16;
-    constexpr u16x2 kK01 = {(unsigned short)k0, (unsigned short)k1}, kK23 = {(unsigned short)k2, (unsigned short)k3};
+#ifndef ORBX_ROWPASS_DOT4
+    // Nine 16 x 16 output tiles (rows 16 rt.., patch columns 16 ct..; window
+    // column = patch column - o) as int8 MFMAs.  B operand: lane l holds
+    // P[16 rt + (l & 15)][16 ct + 8 (l >> 4) + 0..7] - 128, one ds_read_b64;
+    // the result D[j][r] puts outputs 16 ct + 4 (l >> 4) + 0..3 of row
+    // 16 rt + (l & 15) in the lane's 4 accumulators: one 8-byte store.
+    // Only rows < 43 and columns < 40 are stored.
+    {
+        const int rl = lane & 15, q = lane >> 4;
+        const uint8_t *bsrc = lbase + rl * kDescPS + 8 * q;
+        uint64_t px[3][3];
+#pragma unroll
+        for (int rt = 0; rt < 3; ++rt)
+#pragma unroll
+            for (int ct = 0; ct < 3; ++ct)
+                px[rt][ct] = *reinterpret_cast<const uint64_t *>(bsrc + 16 * rt * kDescPS + 16 * ct) ^
+                             0x8080808080808080ull;
+        const i32x4 bias = {128 * 257, 128 * 257, 128 * 257, 128 * 257};
+        static_assert(kGaussTaps[0] + kGaussTaps[1] + kGaussTaps[2] + kGaussTaps[3] + kGaussTaps[4] +
+                          kGaussTaps[5] + kGaussTaps[6] == 257, "bias = 128 * sum of the taps");
+        uint16_t *dst = rowp + rl * kRowS + 4 * q;
+#pragma unroll
+        for (int rt = 0; rt < 3; ++rt)
+#pragma unroll
+            for (int ct = 0; ct < 3; ++ct) {
+                const i32x4 d = __builtin_amdgcn_mfma_i32_16x16x32_i8(row_taps, (long)px[rt][ct], bias, 0, 0, 0);
+                if ((rt < 2 || rl < kDescP - 32) && (ct < 2 || q < 2)) {
+                    uint2 w;
+                    w.x = (uint32_t)d[0] | ((uint32_t)d[1] << 16);
+                    w.y = (uint32_t)d[2] | ((uint32_t)d[3] << 16);
+                    *reinterpret_cast<uint2 *>(dst + 16 * rt * kRowS + 16 * ct) = w;
+                }
+            }
+    }
+#else
     // One task = 8 consecutive outputs of one row at patch-aligned columns
     // 8s..8s+7 (window column = patch column - o): the 14 source bytes lie in
     // four aligned dwords, every 4-byte window of them one v_alignbyte.
@@ -1423,16 +1502,29 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
         packed.w = out[6] | (out[7] << 16);
         *reinterpret_cast<uint4 *>(rowp + r * kRowS + 8 * sgi) = packed;
     }
-    wave_lds_fence();
+#endif
     PHASE_MARK(1, 2);   // row pass
+    }   // valid
+    // The orientation (fastAtan2) and its sincosf are wave-uniform scalar
+    // chains of ~90 VALU each: wave 0 evaluates the block's four at once (lane
+    // = wave), instead of every wave issuing the chain for one value.
+    __syncthreads();
+    if (wave == 0 && lane < 4) {
+        const float a = fast_atan2_deg((float)s_mom[lane][0], (float)s_mom[lane][1]);
+        float sa, ca;
+        glibc_sincosf(__fmul_rn(a, (float)(3.14159265358979323846 / 180.f)), &sa, &ca);
+        s_ang[lane][0] = a;
+        s_ang[lane][1] = sa;
+        s_ang[lane][2] = ca;
+    }
+    __syncthreads();
+    if (!valid) return;
+    const float angle = s_ang[wave][0], sa = s_ang[wave][1], ca = s_ang[wave][2];
 
     // 4. computeOrbDescriptor (ORBextractor.cc:106-147) on the blurred level:
     //    each sample's blurred value is the column pass evaluated at that pixel
     //    from the row-pass buffer, with OpenCV 3.2's per-column rounding
     //    (half-even below w & ~3, else half-up).
-    const float factor_pi = (float)(3.14159265358979323846 / 180.f);
-    float sa, ca;
-    glibc_sincosf(__fmul_rn(angle, factor_pi), &sa, &ca);
     const int xs = g.w & ~3;
     // whole sample window left of w & ~3 (almost every keypoint): half-even
     // rounding everywhere, (s + 0x7FFF + bit16) >> 16, no per-column test
@@ -1612,8 +1704,19 @@ hipError_t launch_quadtree_level(const DevPlan &p, const FrameBufs &fb, int B, h
     return hipGetLastError();
 }
 
+namespace {
+// Magic for xcd_block_2d(bx, by, magic): ceil(2^32 / gx), exact for every
+// block index L with L * gx < 2^32; 0 (divide) when that does not hold.
+uint32_t grid_magic(uint32_t gx, uint32_t gy) {
+    if (gx <= 1 || (uint64_t)gx * gy * gx >= (1ull << 32)) return 0;
+    return (uint32_t)(((1ull << 32) + gx - 1) / gx);
+}
+}  // namespace
+
 hipError_t launch_describe(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t st) {
-    hipLaunchKernelGGL(k_describe<false>, dim3((p.out_cap + 3) / 4, B), dim3(kThreads), 0, st, p, fb, 0, p.out_cap, 1);
+    const uint32_t gx = (p.out_cap + 3) / 4;
+    hipLaunchKernelGGL(k_describe<false>, dim3(gx, B), dim3(kThreads), 0, st, p, fb, 0, p.out_cap, 1,
+                       grid_magic(gx, B));
     return hipGetLastError();
 }
 
@@ -1622,8 +1725,9 @@ hipError_t launch_describe(const DevPlan &p, const FrameBufs &fb, int B, hipStre
 hipError_t launch_describe_level(const DevPlan &p, const Plan &hp, const FrameBufs &fb, int B, hipStream_t st, int l,
                                  int l_end) {
     const int s0 = hp.lv[l].out_off, ns = hp.lv[l_end - 1].out_off + hp.lv[l_end - 1].out_cap - s0;
-    hipLaunchKernelGGL(k_describe<true>, dim3((ns + 3) / 4, B), dim3(kThreads), 0, st, p, fb, s0, ns,
-                       l_end == hp.nlevels ? 1 : 0);
+    const uint32_t gx = (ns + 3) / 4;
+    hipLaunchKernelGGL(k_describe<true>, dim3(gx, B), dim3(kThreads), 0, st, p, fb, s0, ns,
+                       l_end == hp.nlevels ? 1 : 0, grid_magic(gx, B));
     return hipGetLastError();
 }
 

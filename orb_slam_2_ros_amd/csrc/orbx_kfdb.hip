@@ -617,7 +617,9 @@ int detect(orbx_kfdb *db, bool reloc, uint64_t qid, const uint32_t *words, const
     const size_t o_lst = L.add(16 * (size_t)ns);                          // the walk's list (device only)
     const size_t o_rb = L.add(kQHdr + sizeof(int4) * (size_t)ns);          // the readback (host only)
     const size_t o_ov = L.add(sizeof(Listed) * (size_t)std::max(ns - kListCap, 0));
-    const bool repeated = !(reloc ? db->reloc_qids : db->loop_qids).insert(qid).second;
+    // a keyframe never queried has query id 0 (KeyFrame.cc's initialiser), so
+    // a query with id 0 matches every such neighbour, as a repeated id would
+    const bool repeated = !(reloc ? db->reloc_qids : db->loop_qids).insert(qid).second || qid == 0;
     if (++db->stamp == 0) ++db->stamp;   // (0: never written)
     CallWs &ws = call_ws(db->device);
     std::lock_guard<std::mutex> wl(ws.mu);
@@ -657,11 +659,21 @@ int detect(orbx_kfdb *db, bool reloc, uint64_t qid, const uint32_t *words, const
     hipLaunchKernelGGL(k_kfdb_score, dim3(std::min(64, (ns + 3) / 4)), dim3(kKT), qlds, ws.st, db->d_slots,
                        ns, at<int4>(D, o_lst), db->d_words, db->d_values, at<uint32_t>(D, o_qw),
                        at<double>(D, o_qv), n, qd, db->d_state, reinterpret_cast<Listed *>(db->d_qbuf + 16));
+    // k_kfdb_list clears the per-slot scratch k_kfdb_touch filled; a query that
+    // fails in between clears it here, so later queries start from zero counts
+    auto fail_scratch = [&]() {
+        (void)hipGetLastError();
+        (void)hipStreamSynchronize(ws.st);
+        (void)hipMemset(db->d_qcnt, 0, sizeof(*db->d_qcnt) * (size_t)ns);
+        (void)hipMemset(db->d_qfirst, 0xFF, sizeof(*db->d_qfirst) * (size_t)ns);
+        (void)hipDeviceSynchronize();
+        return ORBX_EIO;
+    };
     if (hipGetLastError() != hipSuccess ||
         hipMemcpyAsync(ws.host + o_rb, db->d_qbuf, kQHdr + sizeof(int4) * (size_t)ns, hipMemcpyDeviceToHost, ws.st) !=
             hipSuccess ||
         hipStreamSynchronize(ws.st) != hipSuccess)
-        return ORBX_EIO;
+        return fail_scratch();
     const double t_b = timing ? tms() : 0;
     const int4 *rec = at<int4>(ws.host, o_rb + kQHdr);
     int32_t mw[2];
@@ -798,6 +810,8 @@ void orbx_kfdb_destroy(orbx_kfdb *db) {
 
 int orbx_kfdb_add(orbx_kfdb *db, uint64_t kf_id, const uint32_t *words, const double *values, int n) {
     if (!db || n < 0 || (n && (!words || !values)) || !sorted_unique(words, n)) return ORBX_EINVAL;
+    // the inverted file is indexed by word id: bounded (ORBvoc has 10^6 words)
+    if (n && words[n - 1] >= ORBX_KFDB_MAX_WORDS) return ORBX_EINVAL;
     std::lock_guard<std::mutex> lock(db->mu);
     if (db->live.count(kf_id)) return ORBX_EINVAL;   // the reference would list it twice per word
     Slot s{kf_id, (int64_t)db->h_words.size(), n, true};

@@ -186,8 +186,17 @@ int upload_plan(orbx_extractor *ex) {
     const size_t b_xt = sizeof(ResizeTap) * p.xtaps.size();
     const size_t b_yt = sizeof(ResizeTap) * p.ytaps.size();
     const size_t b_tiles = sizeof(int4) * tiles.size();
+    // level of every output slot (the last level whose range starts at or before it)
+    std::vector<uint32_t> slot_level((size_t)std::max(p.out_cap, 0) + 4, 0);
+    for (int s = 0; s < p.out_cap; ++s) {
+        int l = 0;
+        for (int q = 1; q < p.nlevels; ++q)
+            if (s >= p.lv[q].out_off) l = q;
+        slot_level[s] = (uint32_t)l;
+    }
+    const size_t b_sl = sizeof(uint32_t) * slot_level.size();
     auto al = [](size_t v) { return (v + 255) & ~size_t(255); };
-    const size_t total = al(b_lv) + al(b_cells) + al(b_xt) + al(b_yt) + al(b_tiles) + 256;
+    const size_t total = al(b_lv) + al(b_cells) + al(b_xt) + al(b_yt) + al(b_tiles) + al(b_sl) + 256;
     std::vector<uint8_t> host(total, 0);
     size_t o = 0;
     const size_t o_lv = o; std::memcpy(&host[o], p.lv.data(), b_lv); o += al(b_lv);
@@ -195,6 +204,7 @@ int upload_plan(orbx_extractor *ex) {
     const size_t o_xt = o; if (b_xt) std::memcpy(&host[o], p.xtaps.data(), b_xt); o += al(b_xt);
     const size_t o_yt = o; if (b_yt) std::memcpy(&host[o], p.ytaps.data(), b_yt); o += al(b_yt);
     const size_t o_tiles = o; if (b_tiles) std::memcpy(&host[o], tiles.data(), b_tiles); o += al(b_tiles);
+    const size_t o_sl = o; std::memcpy(&host[o], slot_level.data(), b_sl); o += al(b_sl);
     if (dalloc(&ex->d_tables, total) != hipSuccess) return ORBX_ENOMEM;
     if (hipMemcpy(ex->d_tables, host.data(), total, hipMemcpyHostToDevice) != hipSuccess) return ORBX_EIO;
     DevPlan &d = ex->dp;
@@ -203,6 +213,7 @@ int upload_plan(orbx_extractor *ex) {
     d.xtaps = reinterpret_cast<const ResizeTap *>(ex->d_tables + o_xt);
     d.ytaps = reinterpret_cast<const ResizeTap *>(ex->d_tables + o_yt);
     d.blur_tiles = reinterpret_cast<const int4 *>(ex->d_tables + o_tiles);
+    d.slot_level = reinterpret_cast<const uint32_t *>(ex->d_tables + o_sl);
     d.nlevels = p.nlevels;
     for (int l = 0; l < kMaxLevels; ++l) {
         LevelArgs &a = d.la[l];

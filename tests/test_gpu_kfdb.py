@@ -149,3 +149,35 @@ def test_kfdb_more_candidates_than_the_first_copy(oracle_mod):
     a = g.DetectLoopCandidates(99998, base, v, [3, 5], 0.0, cv)
     b = o.detect(False, 99998, base, v, [3, 5], 0.0, cv)
     assert a == b and len(b) > 0
+
+
+def test_kfdb_query_id_zero_matches_never_queried(oracle_mod):
+    """A query whose id is 0 matches every keyframe that was never queried
+    (KeyFrame.cc initialises mnLoopQuery / mnRelocQuery to 0), including
+    covisible neighbours the query's own walk did not meet: the candidate
+    lists equal the oracle's (the device path used to gather those
+    neighbours' state only for an id used before)."""
+    from orb_slam_2_ros_amd.synth_vocab import make_keyframe_bows
+    bows, covis = make_keyframe_bows(n_kf=300, n_words=4000, words_per_kf=150, seed=21, loop_every=40)
+    # every keyframe's covisibility also names far keyframes that share few words
+    cov = {k: list(covis.get(k, [])) + [(k + 97) % 300, (k + 151) % 300] for k in range(300)}
+    cv = lambda k: cov.get(k, [])   # noqa: E731
+    g, o = KeyFrameDatabase(), oracle_mod.KeyFrameDB(4000)
+    for i, (w, v) in enumerate(bows[:250]):
+        g.add(i, w, v)
+        o.add(i, w, v)
+    for qi in (250, 260, 280):
+        w, v = bows[qi]
+        assert g.DetectLoopCandidates(0, w, v, cov[qi][:3], 0.0, cv) == o.detect(False, 0, w, v, cov[qi][:3], 0.0, cv)
+        assert g.DetectRelocalizationCandidates(0, w, v, cv) == o.detect(True, 0, w, v, None, 0.0, cv)
+
+
+def test_kfdb_rejects_word_ids_past_the_bound():
+    from orb_slam_2_ros_amd import OrbxError
+    db = KeyFrameDatabase()
+    db.add(1, np.array([3, (1 << 26) - 1], np.uint32), np.array([0.5, 0.5]))
+    with pytest.raises(OrbxError):
+        db.add(2, np.array([3, 1 << 26], np.uint32), np.array([0.5, 0.5]))
+    with pytest.raises(OrbxError):
+        db.add(3, np.array([0xFFFFFFFF], np.uint32), np.array([1.0]))
+    assert db.size() == 1
