@@ -121,3 +121,38 @@ def test_triangulation_batch_sequential_exclusion(oracle_mod):
             # this neighbour's new map points bar their A features from the next
             flags = flags.copy()
             flags[np.nonzero(mine >= 0)[0][::2]] &= 0xFE
+
+
+def test_fuse_neighbours_batched_with_research(oracle_mod):
+    """Fuse over the neighbours as ONE device batch with the
+    starting descriptors, then the edits neighbour by neighbour, re-searching
+    (one-row device call) every point whose descriptor a Replace changed
+    before its turn -- the final map state equals the sequential reference
+    (oracle, one query at a time with the current descriptor)."""
+    from fuse_world import TH_LOW, distinctive, make_world, problems, run
+    from proj_cases import VARIANT_ARGS
+    th, ratio, ori, _ = VARIANT_ARGS["fuse"]
+    w = make_world(7, kp_flips=(20, 40), row_flips=(10, 25))
+
+    def oracle_search(j, i, d):
+        F = w["frames"][j - 1]
+        _, qi, qd, _ = oracle_mod.search_by_projection("fuse", F["keys"], F["desc"], w["queries"][j - 1][i:i + 1],
+                                                       d.reshape(1, 32), w["bounds"], None, None, w["inv_sigma2"],
+                                                       TH_LOW, ratio, ori)
+        return int(qi[0]), int(qd[0])
+    m = ORBmatcher(ratio, ori)
+
+    def gpu_search(j, i, d):
+        F = w["frames"][j - 1]
+        _, qi, qd, _ = m.search_by_projection("fuse", F["keys"], F["desc"], w["queries"][j - 1][i:i + 1],
+                                              d.reshape(1, 32), w["bounds"], None, None, w["inv_sigma2"], TH_LOW)
+        return int(qi[0]), int(qd[0])
+    seq, _ = run(w, "sequential", oracle_search, oracle_mod=oracle_mod)
+    starts = {i: distinctive([w["rows"][(kf, w["obs"][i][kf])] for kf in sorted(w["obs"][i])], oracle_mod)
+              for i in range(w["n_cur"])}
+    batch = m.search_by_projection_batch("fuse", problems(w, starts), TH_LOW)
+    got, nre = run(w, "batched", gpu_search, batch, oracle_mod=oracle_mod)
+    naive, _ = run(w, "naive", gpu_search, batch, oracle_mod=oracle_mod)
+    assert nre > 0
+    assert got == seq
+    assert naive != seq
