@@ -669,11 +669,16 @@ class StubExtractor:
 
 
 def run_config(torch, dist, rank, world, dev, w, h, nfeatures, streams, steps, warmup, profile, mode="mono",
-               stub=None, split=2, pipeline=0):
+               stub=None, split=2, pipeline=0, kframes=1):
     """Times `steps` front-end steps of this rank's `streams` (global stream
     ids: mono / RGB-D frames or stereo pairs, one per stream per step); returns
-    (max-over-ranks seconds, stage ms, kps, sanity, frames per launch, extractor)."""
-    batch = len(streams)
+    (max-over-ranks seconds, stage ms, kps, sanity, frames per launch, extractor).
+    kframes (RGB-D only): K consecutive frames of every stream in one launch
+    (a step is then K frames per stream; RGB-D frames are independent, the
+    depth lookup reads only the frame's own depth map)."""
+    assert kframes == 1 or mode == "rgbd"
+    nstreams = len(streams)
+    batch = nstreams * kframes
     if stub is not None:
         ex = stub
     else:
@@ -687,6 +692,12 @@ def run_config(torch, dist, rank, world, dev, w, h, nfeatures, streams, steps, w
     if pipeline and stub is None and "ORBX_PIPELINE" not in os.environ:
         ex.pipeline(1)   # level pipeline: on where it measured faster
     host, depth = _resident_frames(mode, w, h, streams)
+    if kframes > 1:
+        # launch u holds times u K .. u K + K - 1 (mod the resident frames) of
+        # every stream, time-major; each frame keeps its stream's depth map
+        host = np.stack([np.concatenate([host[(u * kframes + j) % FRAMES_PER_STREAM] for j in range(kframes)])
+                         for u in range(FRAMES_PER_STREAM)])
+        depth = np.concatenate([depth] * kframes)
     frames = torch.from_numpy(host).to(dev)
     dmaps = torch.from_numpy(depth).to(dev) if depth is not None else None
     del host, depth
@@ -818,17 +829,24 @@ def keyframe_publish(torch, dist, world, dev, ex, reps=10):
             "streams_received": len(counts), "min_keypoints_per_stream": min(counts) if counts else None}
 
 
-def c5_config(torch, dist, rank, world, dev, steps, warmup, profile, stub=None, w=1920, h=1080):
+def c5_config(torch, dist, rank, world, dev, steps, warmup, profile, stub=None, w=1920, h=1080, total=None,
+              kframes=None, exchange=True):
     """C5 as configured: 64 FHD RGB-D streams in total, s -> rank s mod G, one
-    extract + ComputeStereoFromRGBD per stream per step (strong scaling inside
-    the config: the stream count is fixed); then the keyframe all-gather."""
-    streams = stream_partition(C5_STREAMS, world, rank)
+    extract + ComputeStereoFromRGBD per stream per frame (strong scaling inside
+    the config: the stream count is fixed); then the keyframe all-gather.
+    Each launch takes K consecutive frames of every stream of the rank, K =
+    64 / streams per rank by default (1 on one GPU, 8 at eight: a rank's launch
+    stays 64 frames, which a GPU needs to fill)."""
+    total = total or C5_STREAMS
+    streams = stream_partition(total, world, rank)
+    k = kframes or max(1, C5_STREAMS // max(1, len(streams)))
     el, st, nk, sane, _, ex = run_config(torch, dist, rank, world, dev, w, h, 1000, streams, steps, warmup,
-                                         profile, "rgbd", stub)
-    xchg = keyframe_publish(torch, dist, world, dev, ex)
+                                         profile, "rgbd", stub, kframes=k)
+    xchg = keyframe_publish(torch, dist, world, dev, ex) if exchange else None
     ex.close()
-    return {"value": round(C5_STREAMS * steps / el, 2), "unit": "frames/s", "mode": "rgbd", "streams_total": C5_STREAMS,
-            "streams_per_gpu": len(streams), "workload": f"rgbd {w}x{h}", "scaling": "strong", "stage_ms": st, "kps_last_frame": nk,
+    return {"value": round(total * k * steps / el, 2), "unit": "frames/s", "mode": "rgbd", "streams_total": total,
+            "streams_per_gpu": len(streams), "frames_per_stream_per_launch": k, "frames_per_launch": len(streams) * k,
+            "workload": f"rgbd {w}x{h}", "scaling": "strong", "stage_ms": st, "kps_last_frame": nk,
             "depths_last_frame": sane, "keyframe_all_gather": xchg}
 
 
@@ -868,7 +886,8 @@ def main() -> int:
                     help="skip the secondary FHD / stereo / RGB-D / C5 configurations")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-profile", action="store_true")
-    ap.add_argument("--extra", default=None, help="time only this EXTRAS config or 'c5' (diagnostics; prints its dict)")
+    ap.add_argument("--extra", default=None,
+                    help="time only this EXTRAS config, 'c5' or 'dropin' (diagnostics; prints its dict)")
     ap.add_argument("--stub", action="store_true",
                     help="CPU / gloo dry run of the launcher, stream partition and batch shapes (tests)")
     args = ap.parse_args()
@@ -903,6 +922,11 @@ def main() -> int:
         res = None
         if args.extra == "c5":
             res = c5_config(torch, dist, rank, world, dev, args.steps, args.warmup, profile, *c5_args)
+        if args.extra == "dropin":
+            res = dropin_latency(torch, dev)
+        if args.extra in ("c5_rank8", "c5_rank8_k8"):   # one rank's share of C5 at 8 GPUs
+            res = c5_config(torch, dist, rank, world, dev, args.steps, args.warmup, profile, *c5_args, total=8,
+                            kframes=8 if args.extra.endswith("k8") else 1, exchange=False)
         for key, mode, ew, eh, enf, eb, unit in EXTRAS:
             if key == args.extra:
                 streams = stream_partition(eb * world, world, rank)
@@ -997,6 +1021,12 @@ def main() -> int:
         full = world == 1 and not args.no_extras and not args.stub
         matchers = matcher_latencies() if full else None
         if full:
+            # one rank's share of C5 at 8 GPUs (8 streams), one frame per stream
+            # per launch and K = 8 consecutive frames per stream per launch
+            for kk in (1, 8):
+                extras[f"c5_rank_share_8_streams_k{kk}"] = c5_config(
+                    torch, dist, rank, world, dev, max(5, args.steps // 4), 2, profile, total=8, kframes=kk,
+                    exchange=False)
             extras["dropin_latency"] = dropin_latency(torch, dev)
             extras["bow_transform_orbvoc"] = bow_transform_throughput(torch)
             extras["keyframe_db_loop_query"] = kfdb_latency()

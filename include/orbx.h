@@ -280,10 +280,18 @@ int orbx_search_by_projection(int device, int variant, const orbx_match_frame *f
  *     (Tracking.cc:1667, 1685; ORBX_PROJ_KEYFRAME).
  * Each problem is exactly one orbx_search_by_projection call (same inputs,
  * same outputs, filled in place including nmatches); problems may share a
- * frame's arrays (uploaded once).  Fuse's candidate search reads no map
- * state, so a neighbour's results stay exact when the caller applies the map
- * edits neighbour by neighbour and re-checks pMP->isBad() / IsInKeyFrame()
- * before each edit, as Fuse itself does at the top of its loop.
+ * frame's arrays (uploaded once).  Fuse's candidate search reads one piece
+ * of map state: the query point's descriptor (pMP->GetDescriptor(),
+ * ORBmatcher.cc:901).  A Replace in an earlier neighbour (or earlier in the
+ * same one) recomputes the surviving point's descriptor (MapPoint.cc:254),
+ * and the sequential reference searches later neighbours with the new one.
+ * So the caller applies the edits neighbour by neighbour in query order,
+ * re-checks pMP->isBad() / IsInKeyFrame() before each edit (as Fuse does at
+ * the top of its loop), and for a point whose descriptor changed since the
+ * batch ran, re-runs that one row (orbx_search_by_projection, nq = 1,
+ * current descriptor) instead of using the batch's result.  Position, normal
+ * and scale are untouched by Replace, so the query rows stay valid
+ * (tests/test_gpu_batch_match.py::test_fuse_neighbours_batched_with_research).
  * Synchronous. */
 typedef struct orbx_proj_problem {
     orbx_match_frame frame;

@@ -215,6 +215,19 @@ struct OrbxMatcher {
         return nm;
     }
 
+    // One row of a projection search with the point's current descriptor: the
+    // re-search the batched Fuse recipe needs for a point whose descriptor a
+    // Replace changed after the batch ran (include/orbx.h).  idx / dist as
+    // q_idx[0] / q_dist[0] of SearchByProjectionTable.
+    static void SearchOneRow(int variant, const ProjFrame &F, const orbx_proj_query &q, const cv::Mat &desc,
+                             int th_dist, float nnratio, int &idx, int &dist) {
+        std::vector<int> qi, qdist, kf;
+        SearchByProjectionTable(variant, F, std::vector<orbx_proj_query>(1, q), desc, th_dist, nnratio, false, qi,
+                                qdist, kf);
+        idx = qi[0];
+        dist = qdist[0];
+    }
+
     // The per-keyframe loops in one launch pair: problem k searches frame
     // F[k] with queries q[k] / qdesc[k], exactly as SearchByProjectionTable
     // would (Fuse over LocalMapping's neighbours, relocalisation's candidates;
@@ -227,29 +240,41 @@ struct OrbxMatcher {
                                                     std::vector<std::vector<int>> &q_dist,
                                                     std::vector<std::vector<int>> &kp_final) {
         const size_t np = F.size();
+        // one packed copy per distinct frame: problems that search the same
+        // frame (relocalisation: one current frame, many candidates) pass the
+        // same host pointers, which the runtime uploads once
         std::vector<std::vector<orbx_keypoint>> k(np);
+        std::vector<const std::vector<orbx_keypoint> *> kp(np);
         std::vector<cv::Mat> d(np), qd(np);
         std::vector<orbx_proj_problem> pr(np);
         q_idx.assign(np, {});
         q_dist.assign(np, {});
         kp_final.assign(np, {});
         for (size_t i = 0; i < np; ++i) {
-            k[i] = orbx_detail::pack(*F[i].keys);
-            d[i] = F[i].desc->isContinuous() ? *F[i].desc : F[i].desc->clone();
+            size_t src = i;
+            for (size_t j = 0; j < i; ++j)
+                if (F[j].keys == F[i].keys && F[j].desc == F[i].desc) { src = j; break; }
+            if (src == i) {
+                k[i] = orbx_detail::pack(*F[i].keys);
+                d[i] = F[i].desc->isContinuous() ? *F[i].desc : F[i].desc->clone();
+            } else {
+                d[i] = d[src];   // shares the same buffer (cv::Mat header copy)
+            }
+            kp[i] = src == i ? &k[i] : kp[src];
             qd[i] = qdesc[i].isContinuous() ? qdesc[i] : qdesc[i].clone();
             orbx_match_frame &mf = pr[i].frame;
             mf = orbx_match_frame{};
-            mf.keys = k[i].data();
+            mf.keys = kp[i]->data();
             mf.desc = d[i].data;
             mf.uright = F[i].uright && !F[i].uright->empty() ? F[i].uright->data() : nullptr;
             mf.mp_state = F[i].mp_state && !F[i].mp_state->empty() ? F[i].mp_state->data() : nullptr;
             mf.inv_sigma2 = F[i].inv_sigma2 ? F[i].inv_sigma2->data() : nullptr;
-            mf.n = (int)k[i].size();
+            mf.n = (int)kp[i]->size();
             mf.nlevels = F[i].inv_sigma2 ? (int)F[i].inv_sigma2->size() : 0;
             mf.min_x = F[i].min_x; mf.max_x = F[i].max_x; mf.min_y = F[i].min_y; mf.max_y = F[i].max_y;
             q_idx[i].assign(q[i].size(), -1);
             q_dist[i].assign(q[i].size(), -1);
-            kp_final[i].assign(k[i].size(), -1);
+            kp_final[i].assign(kp[i]->size(), -1);
             pr[i].queries = q[i].data();
             pr[i].qdesc = qd[i].data;
             pr[i].nq = (int)q[i].size();

@@ -624,6 +624,21 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
     PHASE_MARK(0, 0);   // prologue + staging
     uint32_t *out_i = fb.cand + (int64_t)b * p.cand_cap + c.slot;
     uint32_t *out_m = fb.cand2 + (int64_t)b * p.cand_cap + c.slot;
+    // The compass pass's lane geometry (both passes): lane = (row in pass,
+    // quad of the row), 64 / nq rows per pass; a lane keeps its quad column,
+    // so its interior mask is fixed.
+    const int qc0 = (o + 3) & ~3;                           // patch column of the first quad
+    const int nq = ((o + 2 + cw) >> 2) - (qc0 >> 2) + 1;   // quads per row
+    const int R = __builtin_amdgcn_readfirstlane(div_small(64, nq));
+    const int rl = div_small(lane, nq), qi = lane - mul24u(rl, nq);
+    const int xx0 = qc0 - o - 3 + 4 * qi;   // interior x of the quad's byte 0
+    // candidate word: pixel j of the quad at bit 16 (j >> 1) + (j & 1)
+    uint32_t vmask = 0;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+        if (xx0 + jj >= 0 && xx0 + jj < cw) vmask |= 1u << (16 * (jj >> 1) + (jj & 1));
+    if (rl >= R) vmask = 0;   // (tail lanes: rows of the next pass)
+    const uint8_t *q0 = patch + mul24u(3 + rl, PS) + qc0 + 4 * qi;
 
     // One FAST pass at threshold th: returns the keypoints kept after NMS,
     // written to out.  The reference runs iniThFAST first and minThFAST only
@@ -644,20 +659,6 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
         //    odd pixels); survivors are compacted in row-major order.
         int nsurv = 0;
         {
-            // lane = (row in pass, quad of the row), 64 / nq rows per pass: a
-            // lane keeps its quad column, so its interior mask is fixed
-            const int qc0 = (o + 3) & ~3;                           // patch column of the first quad
-            const int nq = ((o + 2 + cw) >> 2) - (qc0 >> 2) + 1;   // quads per row
-            const int R = __builtin_amdgcn_readfirstlane(div_small(64, nq));
-            const int rl = div_small(lane, nq), qi = lane - mul24u(rl, nq);
-            const int xx0 = qc0 - o - 3 + 4 * qi;   // interior x of the quad's byte 0
-            // candidate word: pixel j of the quad at bit 16 (j >> 1) + (j & 1)
-            uint32_t vmask = 0;
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj)
-                if (xx0 + jj >= 0 && xx0 + jj < cw) vmask |= 1u << (16 * (jj >> 1) + (jj & 1));
-            if (rl >= R) vmask = 0;   // (tail lanes: rows of the next pass)
-            const uint8_t *q0 = patch + mul24u(3 + rl, PS) + qc0 + 4 * qi;
             const u16x2 thv = {(unsigned short)th, (unsigned short)th};
             const u16x2 thv8 = {(unsigned short)(th << 8), (unsigned short)(th << 8)};
             int e = (rl << 8) + xx0;
@@ -700,21 +701,19 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
                             (__builtin_bit_cast(uint32_t, half(0xFF00FF00u, 0x060c040cu, 0x040c020cu, thv8)) << 1)) &
                            vmask;
                 }
-                // compaction in row-major order: the lanes' counts (0..4) by their
-                // binary digits, one ballot each, then each lane's bits
+                // compaction in row-major order: an inclusive DPP scan of the
+                // lanes' counts (0..4) places each lane's run, then its bits
                 const int cnt = __builtin_popcount(cand);
-                const uint64_t c1 = __ballot(cnt & 1), c2 = __ballot(cnt & 2), c4 = __ballot(cnt & 4);
-                if (c1 | c2 | c4) {
-                    auto below_cnt = [&](uint64_t m) {
-                        return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                    };
-                    int pos = nsurv + below_cnt(c1) + 2 * below_cnt(c2) + 4 * below_cnt(c4);
+                const int incl = wave_incl_scan_i32(cnt);
+                const int total = __builtin_amdgcn_readlane(incl, 63);
+                if (total) {
+                    int pos = nsurv + incl - cnt;
                     while (cand) {
                         const int bt = __builtin_ctz(cand);
                         list[pos++] = (uint16_t)(e + ((bt >> 3) | (bt & 1)));
                         cand &= cand - 1u;
                     }
-                    nsurv += __popcll(c1) + 2 * __popcll(c2) + 4 * __popcll(c4);
+                    nsurv += total;
                 }
             }
         }
@@ -1289,20 +1288,20 @@ __global__ __launch_bounds__(kThreads, 6) void k_quadtree(DevPlan p, FrameBufs f
 // ===========================================================================
 constexpr int kDescR = 21;                  // patch radius = 18 (samples) + 3 (blur taps)
 constexpr int kDescP = 2 * kDescR + 1;      // 43
-#ifndef ORBX_ROWPASS_DOT4
 constexpr int kDescPS = 48;                 // patch row stride (bytes): 43 + align offset, 8-aligned rows
-#else
-constexpr int kDescPS = 52;                 // 43 + align offset + dot4 row-pass overread
-#endif
 constexpr int kBlurR = 18;
-constexpr int kRowS = 40;                   // row-pass stride (u16): outputs at patch columns 0..39
-// The row-pass buffer follows the patch directly.  The MFMA row pass reads
-// 48 rows x 64 columns at the patch stride (rows 43..47, and columns past 45
-// that wrap into the next row, are either multiplied by zero taps or feed
-// outputs that are never stored), so those reads may run into the row
-// buffer: they all precede the wave's stores.
+constexpr int kRowCols = 40;                // row-pass outputs at patch columns 0..39
+constexpr int kColS = 44;                   // column-major row-pass buffer: stride (u16) of a column, rows 0..43
+// The row-pass buffer follows the patch directly, column-major: a sample's
+// seven column-pass inputs (rows r..r+6 of one column) are 14 contiguous
+// bytes, one unaligned ds_read_b128 (row 43 is padding the read may cover).
+// The MFMA row pass reads 48 rows x 64 columns at the patch stride (rows
+// 43..47, and columns past 45 that wrap into the next row, are either
+// multiplied by zero taps or feed outputs that are never stored), so those
+// reads may run into the row buffer: they all precede the wave's stores.
 constexpr int kDescRowOff = (kDescP * kDescPS + 15) & ~15;             // 2064
-constexpr int kDescWaveLds = kDescRowOff + kDescP * kRowS * 2;        // 5504 B
+constexpr int kDescWaveLds = kDescRowOff + kRowCols * kColS * 2;      // 5584 B
+static_assert((kDescR - 3 + kBlurR) + 7 < kColS, "a sample's 16-byte read stays in its column");
 constexpr int kDescWaveStride = (kDescWaveLds + 15) & ~15;
 static_assert(47 * kDescPS + 63 < kDescWaveLds, "MFMA row-pass reads stay inside the wave's LDS");
 // LDS is allocated per workgroup in 512-byte granules: 4 waves + 48 B of
@@ -1344,9 +1343,7 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
     // j = 64 grp + lane), fetched first so the loads overlap the staging
     float4 pat[4];
     uint32_t dmask[4];
-#ifndef ORBX_ROWPASS_DOT4
     const long row_taps = (long)c_row_taps.t[lane];
-#endif
 #pragma unroll
     for (int grp = 0; grp < 4; ++grp) pat[grp] = reinterpret_cast<const float4 *>(c_pattern_f)[grp * 64 + lane];
 #pragma unroll
@@ -1382,11 +1379,9 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
     uint16_t *rowp = reinterpret_cast<uint16_t *>(lbase + kDescRowOff);
     // taps of getGaussianKernel(7, 2) x256 (checked against the plan on the host)
     constexpr int k0 = kGaussTaps[0], k1 = kGaussTaps[1], k2 = kGaussTaps[2], k3 = kGaussTaps[3];
-    // Taps as byte vectors for v_dot4_u32_u8: out[j] = dot4(px[j..j+3], W0) + dot4(px[j+4..j+7], W1).
-    constexpr uint32_t kW0 = (uint32_t)kGaussTaps[0] | (uint32_t)kGaussTaps[1] << 8 |
-                             (uint32_t)kGaussTaps[2] << 16 | (uint32_t)kGaussTaps[3] << 24;
-    constexpr uint32_t kW1 = (uint32_t)kGaussTaps[4] | (uint32_t)kGaussTaps[5] << 8 | (uint32_t)kGaussTaps[6] << 16;
-    constexpr u16x2 kK01 = {(unsigned short)k0, (unsigned short)k1}, kK23 = {(unsigned short)k2, (unsigned short)k3};
+    // column-pass taps as u16 pairs for v_dot2_u32_u16 over rows (r, r+1), (r+2, r+3), (r+4, r+5), (r+6, r+7)
+    constexpr u16x2 kK01 = {(unsigned short)k0, (unsigned short)k1}, kK23 = {(unsigned short)k2, (unsigned short)k3},
+                    kK21 = {(unsigned short)k2, (unsigned short)k1}, kK0z = {(unsigned short)k0, 0};
     int o = 0;
     if (valid) {
 
@@ -1455,13 +1450,13 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
     // 3. Gaussian 7x7 restricted to the 37x37 sample window: row pass over all
     //    43 rows (8-wide segments slide along a row), then the column pass with
     //    OpenCV 3.2's per-column rounding (half-even below w & ~3, else half-up).
-#ifndef ORBX_ROWPASS_DOT4
     // Nine 16 x 16 output tiles (rows 16 rt.., patch columns 16 ct..; window
-    // column = patch column - o) as int8 MFMAs.  B operand: lane l holds
-    // P[16 rt + (l & 15)][16 ct + 8 (l >> 4) + 0..7] - 128, one ds_read_b64;
-    // the result D[j][r] puts outputs 16 ct + 4 (l >> 4) + 0..3 of row
-    // 16 rt + (l & 15) in the lane's 4 accumulators: one 8-byte store.
-    // Only rows < 43 and columns < 40 are stored.
+    // column = patch column - o) as int8 MFMAs, D = P T: A operand, lane l
+    // holds P[16 rt + (l & 15)][16 ct + 8 (l >> 4) + 0..7] - 128 (one
+    // ds_read_b64); B = the Toeplitz taps.  D's lane l holds rows
+    // 16 rt + 4 (l >> 4) + 0..3 of output column 16 ct + (l & 15): one 8-byte
+    // store into the column-major buffer.  Only columns < 40 and rows < 44 are
+    // stored (row 43 is padding).
     {
         const int rl = lane & 15, q = lane >> 4;
         const uint8_t *bsrc = lbase + rl * kDescPS + 8 * q;
@@ -1475,45 +1470,20 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
         const i32x4 bias = {128 * 257, 128 * 257, 128 * 257, 128 * 257};
         static_assert(kGaussTaps[0] + kGaussTaps[1] + kGaussTaps[2] + kGaussTaps[3] + kGaussTaps[4] +
                           kGaussTaps[5] + kGaussTaps[6] == 257, "bias = 128 * sum of the taps");
-        uint16_t *dst = rowp + rl * kRowS + 4 * q;
+        uint16_t *dst = rowp + rl * kColS + 4 * q;
 #pragma unroll
         for (int rt = 0; rt < 3; ++rt)
 #pragma unroll
             for (int ct = 0; ct < 3; ++ct) {
-                const i32x4 d = __builtin_amdgcn_mfma_i32_16x16x32_i8(row_taps, (long)px[rt][ct], bias, 0, 0, 0);
-                if ((rt < 2 || rl < kDescP - 32) && (ct < 2 || q < 2)) {
+                const i32x4 d = __builtin_amdgcn_mfma_i32_16x16x32_i8((long)px[rt][ct], row_taps, bias, 0, 0, 0);
+                if ((rt < 2 || q < 3) && (ct < 2 || rl < kRowCols - 32)) {
                     uint2 w;
                     w.x = (uint32_t)d[0] | ((uint32_t)d[1] << 16);
                     w.y = (uint32_t)d[2] | ((uint32_t)d[3] << 16);
-                    *reinterpret_cast<uint2 *>(dst + 16 * rt * kRowS + 16 * ct) = w;
+                    *reinterpret_cast<uint2 *>(dst + 16 * ct * kColS + 16 * rt) = w;
                 }
             }
     }
-#else
-    // One task = 8 consecutive outputs of one row at patch-aligned columns
-    // 8s..8s+7 (window column = patch column - o): the 14 source bytes lie in
-    // four aligned dwords, every 4-byte window of them one v_alignbyte.
-    // Window columns 0..36 are patch columns o..o+36, within the 40 computed;
-    // the others are padding.
-    for (int t = lane; t < kDescP * 5; t += 64) {
-        const int r = (t * 205) >> 10, sgi = t - r * 5;   // t / 5 for t < 215
-        const uint32_t *ap = reinterpret_cast<const uint32_t *>(lbase + r * kDescPS + 8 * sgi);
-        const uint32_t d[4] = {ap[0], ap[1], ap[2], ap[3]};
-        auto win = [&](int k) {   // source bytes k..k+3
-            return (k & 3) ? __builtin_amdgcn_alignbyte(d[(k >> 2) + 1], d[k >> 2], k & 3) : d[k >> 2];
-        };
-        uint32_t out[8];
-#pragma unroll
-        for (int m = 0; m < 8; ++m)
-            out[m] = __builtin_amdgcn_udot4(win(m), kW0, __builtin_amdgcn_udot4(win(m + 4), kW1, 0u, false), false);
-        uint4 packed;
-        packed.x = out[0] | (out[1] << 16);
-        packed.y = out[2] | (out[3] << 16);
-        packed.z = out[4] | (out[5] << 16);
-        packed.w = out[6] | (out[7] << 16);
-        *reinterpret_cast<uint4 *>(rowp + r * kRowS + 8 * sgi) = packed;
-    }
-#endif
     PHASE_MARK(1, 2);   // row pass
     }   // valid
     // The orientation (fastAtan2) and its sincosf are wave-uniform scalar
@@ -1542,25 +1512,42 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
     const bool all_even = x + kBlurR < xs;
     // all 8 of the lane's samples: offsets, then every column-pass read in
     // flight at once, then the rounding
-    int sums[8], cols[8];
+    // A sample at window offset (r, c) reads column c + kBlurR + o, rows
+    // r + kBlurR .. +6 of the column-major buffer: byte offset
+    // 2 kColS (c + kBlurR + o) + 2 (r + kBlurR), from the cvRound'ed float
+    // bits (0x4B400000 + n, below) as one 24-bit multiply-add and one
+    // shift-add; the constant folds the bias bits away (mod 2^32).  The read
+    // is the four dwords from the one holding row r down (two ds_read2_b32;
+    // unaligned ds_read_b128 measured 470 stall cycles a wave), and an odd
+    // row's pairs are realigned by 16 bits (v_alignbit by a per-lane shift).
+    const uint32_t kOff = (uint32_t)(kDescRowOff + 2 * kColS * (kBlurR + o) + 2 * kBlurR) -
+                          (uint32_t)(2 * kColS) * 0x400000u - 2u * 0x4B400000u;
+    static_assert((kDescRowOff & 3) == 0 && (kColS & 1) == 0, "dword-aligned column starts");
+    typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+    int sums[8], cbs[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         const float px = (k & 1) ? pat[k >> 1].z : pat[k >> 1].x, py = (k & 1) ? pat[k >> 1].w : pat[k >> 1].y;
         // cvRound by the 1.5 * 2^23 bias: the float add rounds to the nearest
         // integer, ties to even, and the bits are then 0x4B400000 + n (|n| < 2^22)
         constexpr float kRndBias = 12582912.f;
-        const int rb = __float_as_int(__fadd_rn(__fadd_rn(__fmul_rn(px, sa), __fmul_rn(py, ca)), kRndBias));
-        const int cb = __float_as_int(__fadd_rn(__fsub_rn(__fmul_rn(px, ca), __fmul_rn(py, sa)), kRndBias));
-        const int cc = cb - 0x4B400000;
-        cols[k] = cc;
-        // mul24u sees the low 24 bits of rb + kBlurR: 0x400000 + r + kBlurR (r, cc in [-18, 18])
-        const int roff = (int)mul24u(rb + kBlurR, kRowS) - kRowS * 0x400000;
-        const uint16_t *w = rowp + roff + (cc + kBlurR + o);
-        // k0 (w0 + w6) + k1 (w1 + w5) + k2 (w2 + w4) + k3 w3 as three u16-pair dot products
-        // (the pairs are loaded straight into register halves)
-        const u16x2 r01 = {w[0], w[kRowS]}, r65 = {w[6 * kRowS], w[5 * kRowS]}, r23 = {w[2 * kRowS], w[3 * kRowS]};
+        const uint32_t rb = __float_as_uint(__fadd_rn(__fadd_rn(__fmul_rn(px, sa), __fmul_rn(py, ca)), kRndBias));
+        const uint32_t cb = __float_as_uint(__fadd_rn(__fsub_rn(__fmul_rn(px, ca), __fmul_rn(py, sa)), kRndBias));
+        cbs[k] = (int)cb;
+        // (__umul24 reads the low 24 bits of cb: 0x400000 + c, c in [-18, 18])
+        const uint32_t off = __umul24(cb, 2 * kColS) + ((rb << 1) + kOff);
+        const u32x4a v = *reinterpret_cast<const u32x4a *>(lbase + (off & ~3u));
+        const uint32_t sh = off & 2u ? 16u : 0u;   // odd row (the low bit of rb)
+        // k0 R0 + k1 R1 + k2 R2 + k3 R3 + k2 R4 + k1 R5 + k0 R6 as four u16-pair dot products
+        const uint32_t e0 = __builtin_amdgcn_alignbit(v.y, v.x, sh), e1 = __builtin_amdgcn_alignbit(v.z, v.y, sh),
+                       e2 = __builtin_amdgcn_alignbit(v.w, v.z, sh), e3 = __builtin_amdgcn_alignbit(v.w, v.w, sh);
         sums[k] = (int)__builtin_amdgcn_udot2(
-            r01, kK01, __builtin_amdgcn_udot2(r65, kK01, __builtin_amdgcn_udot2(r23, kK23, mul24u(k2, w[4 * kRowS]), false), false),
+            as_u16x2(e0), kK01,
+            __builtin_amdgcn_udot2(as_u16x2(e1), kK23,
+                                   __builtin_amdgcn_udot2(as_u16x2(e2), kK21,
+                                                          __builtin_amdgcn_udot2(as_u16x2(e3), kK0z, 0u, false),
+                                                          false),
+                                   false),
             false);
     }
     PHASE_MARK(1, 3);   // sincos + sample offsets + column pass
@@ -1573,7 +1560,7 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
         for (int k = 0; k < 8; ++k) {
             const int sum = sums[k];
             int qv;
-            if (x + cols[k] < xs) {
+            if (x + (cbs[k] - 0x4B400000) < xs) {
                 qv = sum >> 16;
                 const int rem = sum & 0xFFFF;
                 qv += (rem > 0x8000) | ((rem == 0x8000) & (qv & 1));

@@ -92,6 +92,34 @@ struct orbx_extractor {
     uint8_t *d_img = nullptr;   // staging for the host API
     size_t d_img_bytes = 0;
 
+    // Host-API fast path (orbx_extract, one frame per call as Frame::ExtractORB
+    // makes it): the upload, the extraction and the result downloads captured
+    // once per plan as a hipGraph on `stream`, replayed per call from pinned
+    // staging buffers -- one launch and one synchronisation instead of ~15
+    // launches and four blocking copies.  ORBX_HOST_GRAPH=0 turns it off.
+    hipGraphExec_t host_graph = nullptr;
+    int graph_w = 0, graph_h = 0;
+    uint8_t *h_img = nullptr, *h_out = nullptr;   // pinned
+    size_t h_img_bytes = 0, h_out_bytes = 0;
+    bool host_result_valid = false;   // slot 0 still holds what h_out holds (no extraction since)
+
+    // orbx_compute_stereo_matches workspace (this extractor as the left one),
+    // kept across calls: uploads of host keypoints that are not the right /
+    // left extractor's own last results, the outputs, a pinned readback.
+    struct StereoWs {
+        orbx_keypoint *kl = nullptr, *kr = nullptr;
+        uint8_t *dl = nullptr, *dr = nullptr;
+        int32_t *n = nullptr, *sad = nullptr, *nk = nullptr;
+        float *ur = nullptr, *depth = nullptr;
+        int cap_l = 0, cap_r = 0;
+        uint8_t *h_res = nullptr;   // pinned: ur[cap_l], depth[cap_l], nkept
+        size_t h_bytes = 0;
+        void free_dev() {
+            dfree(kl); dfree(kr); dfree(dl); dfree(dr); dfree(n); dfree(sad); dfree(nk); dfree(ur); dfree(depth);
+            cap_l = cap_r = 0;
+        }
+    } sws;
+
     hipStream_t stream = nullptr;
 
     // Batch split: a large batch runs as `split` interleaved sub-batches on
@@ -133,6 +161,10 @@ struct orbx_extractor {
 
     ~orbx_extractor() {
         release();
+        if (h_img) (void)hipHostFree(h_img);
+        if (h_out) (void)hipHostFree(h_out);
+        sws.free_dev();
+        if (sws.h_res) (void)hipHostFree(sws.h_res);
         if (stream) (void)hipStreamDestroy(stream);
         for (auto &ps : part_stream)
             if (ps) (void)hipStreamDestroy(ps);
@@ -152,6 +184,9 @@ struct orbx_extractor {
     }
 
     void release() {
+        if (host_graph) (void)hipGraphExecDestroy(host_graph);
+        host_graph = nullptr;
+        graph_w = graph_h = 0;
         dfree(d_tables); dfree(d_pyr); dfree(d_blur); dfree(d_cand); dfree(d_cand2); dfree(d_keys); dfree(d_sel);
         dfree(d_cell_count); dfree(d_level_count); dfree(d_key_node); dfree(d_key_q);
         for (auto &s : slot) { dfree(s.kps); dfree(s.desc); dfree(s.nkps); s.batch = 0; }
@@ -503,6 +538,7 @@ int run_extract_pipe(orbx_extractor *ex, const FrameBufs &fb, int nb, hipStream_
 // a level pipeline per part (stage marks then cover only the match).
 int run_extract(orbx_extractor *ex, int si, const uint8_t *d_images, int64_t stride, int pitch, int batch,
                 const Parts &P) {
+    ex->host_result_valid = false;
     auto &s = ex->slot[si];
     s.img0 = d_images;
     s.img0_stride = stride;
@@ -770,6 +806,87 @@ int orbx_batch_download(orbx_extractor *ex, int frame, orbx_keypoint *kps, uint8
     return ORBX_OK;
 }
 
+namespace {
+
+// Layout of the host graph's pinned download: [0] keypoint count, [16..80) the
+// level counts, then max_kps keypoint records and max_kps descriptors.
+constexpr size_t kOutKps = 128;
+size_t out_desc_off(const orbx_extractor *ex) {
+    return kOutKps + sizeof(orbx_keypoint) * (size_t)ex->plan.max_kps;
+}
+
+bool host_graph_enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("ORBX_HOST_GRAPH");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// Captures upload + extraction (result slot 0, unsplit, no level pipeline, no
+// stage marks) + downloads for a width x height frame.
+int build_host_graph(orbx_extractor *ex, int width, int height) {
+    if (ex->host_graph) (void)hipGraphExecDestroy(ex->host_graph);
+    ex->host_graph = nullptr;
+    const size_t dp = (size_t)pitch_of(width), need = dp * height;
+    const size_t out_bytes = out_desc_off(ex) + 32 * (size_t)ex->plan.max_kps;
+    if (ex->h_img_bytes < need) {
+        if (ex->h_img) (void)hipHostFree(ex->h_img);
+        ex->h_img = nullptr;
+        ex->h_img_bytes = 0;
+        if (hipHostMalloc(reinterpret_cast<void **>(&ex->h_img), need, hipHostMallocDefault) != hipSuccess)
+            return ORBX_ENOMEM;
+        ex->h_img_bytes = need;
+    }
+    if (ex->h_out_bytes < out_bytes) {
+        if (ex->h_out) (void)hipHostFree(ex->h_out);
+        ex->h_out = nullptr;
+        ex->h_out_bytes = 0;
+        if (hipHostMalloc(reinterpret_cast<void **>(&ex->h_out), out_bytes, hipHostMallocDefault) != hipSuccess)
+            return ORBX_ENOMEM;
+        ex->h_out_bytes = out_bytes;
+    }
+    hipStream_t st = ex->stream;
+    const int pipe = ex->pipeline;
+    hipEvent_t *ev = ex->cur_ev;
+    bool *valid = ex->cur_valid;
+    ex->pipeline = 0;
+    ex->cur_ev = nullptr;
+    ex->cur_valid = nullptr;
+    auto restore = [&] { ex->pipeline = pipe; ex->cur_ev = ev; ex->cur_valid = valid; };
+    // one eager run first: lazy attributes (LDS limits) are set outside the capture
+    int rc = run_extract(ex, 0, ex->d_img, (int64_t)need, (int)dp, 1, st);
+    if (rc || hipStreamSynchronize(st) != hipSuccess) { restore(); return rc ? rc : ORBX_EIO; }
+    hipGraph_t g = nullptr;
+    if (hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) { restore(); return ORBX_EIO; }
+    const auto &s0 = ex->slot[0];
+    const int K = ex->plan.max_kps;
+    bool ok = hipMemcpyAsync(ex->d_img, ex->h_img, need, hipMemcpyHostToDevice, st) == hipSuccess;
+    ok = ok && run_extract(ex, 0, ex->d_img, (int64_t)need, (int)dp, 1, st) == ORBX_OK;
+    ok = ok && hipMemcpyAsync(ex->h_out, s0.nkps, sizeof(int32_t), hipMemcpyDeviceToHost, st) == hipSuccess;
+    ok = ok && hipMemcpyAsync(ex->h_out + 16, ex->d_level_count, sizeof(int32_t) * kMaxLevels,
+                              hipMemcpyDeviceToHost, st) == hipSuccess;
+    ok = ok && hipMemcpyAsync(ex->h_out + kOutKps, s0.kps, sizeof(orbx_keypoint) * (size_t)K, hipMemcpyDeviceToHost,
+                              st) == hipSuccess;
+    ok = ok && hipMemcpyAsync(ex->h_out + out_desc_off(ex), s0.desc, 32 * (size_t)K, hipMemcpyDeviceToHost, st) ==
+                   hipSuccess;
+    const bool ended = hipStreamEndCapture(st, &g) == hipSuccess;
+    restore();
+    if (!ok || !ended || !g) {
+        if (g) (void)hipGraphDestroy(g);
+        (void)hipGetLastError();
+        return ORBX_EIO;
+    }
+    const bool inst = hipGraphInstantiate(&ex->host_graph, g, nullptr, nullptr, 0) == hipSuccess;
+    (void)hipGraphDestroy(g);
+    if (!inst) { ex->host_graph = nullptr; return ORBX_EIO; }
+    ex->graph_w = width;
+    ex->graph_h = height;
+    return ORBX_OK;
+}
+
+}  // namespace
+
 int orbx_extract(orbx_extractor *ex, const uint8_t *image, int width, int height, size_t pitch,
                  orbx_keypoint *kps, uint8_t *desc, int cap, int *n) {
     if (!ex || !n) return ORBX_EINVAL;
@@ -781,9 +898,33 @@ int orbx_extract(orbx_extractor *ex, const uint8_t *image, int width, int height
     const size_t dp = (size_t)pitch_of(width);
     const size_t need = dp * height;
     if (ex->d_img_bytes < need) {
+        if (ex->host_graph) (void)hipGraphExecDestroy(ex->host_graph);
+        ex->host_graph = nullptr;
         dfree(ex->d_img);
         if (dalloc(&ex->d_img, need) != hipSuccess) return ORBX_ENOMEM;
         ex->d_img_bytes = need;
+    }
+    if (host_graph_enabled()) {
+        if (!ex->host_graph || ex->graph_w != width || ex->graph_h != height) {
+            rc = build_host_graph(ex, width, height);
+            if (rc) return rc;
+        }
+        for (int r = 0; r < height; ++r) std::memcpy(ex->h_img + r * dp, image + r * pitch, (size_t)width);
+        if (hipGraphLaunch(ex->host_graph, ex->stream) != hipSuccess || hipStreamSynchronize(ex->stream) != hipSuccess)
+            return ORBX_EIO;
+        ex->cur = 0;
+        ex->match_batch = 0;
+        ex->host_result_valid = true;
+        int32_t cnt, lc[kMaxLevels];
+        std::memcpy(&cnt, ex->h_out, sizeof(cnt));
+        std::memcpy(lc, ex->h_out + 16, sizeof(lc));
+        for (int l = 0; l < ex->nlevels; ++l)
+            if (lc[l] < 0) return ORBX_EIO;   // quadtree capacity guard tripped
+        *n = cnt;
+        if (cnt > cap) return ORBX_ERANGE;
+        if (cnt > 0 && kps) std::memcpy(kps, ex->h_out + kOutKps, sizeof(orbx_keypoint) * (size_t)cnt);
+        if (cnt > 0 && desc) std::memcpy(desc, ex->h_out + out_desc_off(ex), 32 * (size_t)cnt);
+        return ORBX_OK;
     }
     if (hipMemcpy2DAsync(ex->d_img, dp, image, pitch, width, height, hipMemcpyHostToDevice, ex->stream) != hipSuccess)
         return ORBX_EIO;
@@ -1000,6 +1141,18 @@ int orbx_extractor_stage_times(orbx_extractor *ex, float *ms, int cap) {
     return nw;
 }
 
+namespace {
+// The host arrays are the extractor's own last host-API result (Frame passes
+// the mvKeys / mDescriptors ExtractORB just returned): its device copies serve.
+bool same_as_last_host_result(const orbx_extractor *ex, const orbx_keypoint *k, const uint8_t *d, int n) {
+    if (!ex->host_result_valid || ex->cur != 0 || !ex->h_out) return false;
+    int32_t cnt;
+    std::memcpy(&cnt, ex->h_out, sizeof(cnt));
+    return cnt == n && (n == 0 || (std::memcmp(k, ex->h_out + kOutKps, sizeof(orbx_keypoint) * (size_t)n) == 0 &&
+                                   std::memcmp(d, ex->h_out + out_desc_off(ex), 32 * (size_t)n) == 0));
+}
+}  // namespace
+
 int orbx_compute_stereo_matches(orbx_extractor *left, orbx_extractor *right, const orbx_keypoint *kl,
                                 const uint8_t *dl, int nl, const orbx_keypoint *kr, const uint8_t *dr, int nr,
                                 float mbf, float mb, float *uright, float *depth, int *nkept) {
@@ -1016,41 +1169,69 @@ int orbx_compute_stereo_matches(orbx_extractor *left, orbx_extractor *right, con
     if (hipSetDevice(left->device) != hipSuccess) return ORBX_ENODEV;
     if (hipStreamSynchronize(right->stream) != hipSuccess || hipStreamSynchronize(left->stream) != hipSuccess)
         return ORBX_EIO;
-    orbx_keypoint *dkl = nullptr, *dkr = nullptr;
-    uint8_t *ddl = nullptr, *ddr = nullptr;
-    int32_t *dn = nullptr, *dsad = nullptr, *dnk = nullptr;
-    float *dur = nullptr, *ddp = nullptr;
-    int rc = ORBX_OK;
-    const bool ok = dalloc(&dkl, nl) == hipSuccess && dalloc(&dkr, ncap) == hipSuccess &&
-                    dalloc(&ddl, 32 * (size_t)nl) == hipSuccess && dalloc(&ddr, 32 * (size_t)ncap) == hipSuccess &&
-                    dalloc(&dn, 2) == hipSuccess && dalloc(&dsad, nl) == hipSuccess && dalloc(&dnk, 1) == hipSuccess &&
-                    dalloc(&dur, nl) == hipSuccess && dalloc(&ddp, nl) == hipSuccess;
-    if (!ok) rc = ORBX_ENOMEM;
-    const int32_t ns[2] = {nl, nr};
-    if (!rc && (hipMemcpy(dkl, kl, sizeof(orbx_keypoint) * nl, hipMemcpyHostToDevice) != hipSuccess ||
-                hipMemcpy(ddl, dl, 32 * (size_t)nl, hipMemcpyHostToDevice) != hipSuccess ||
-                (nr && hipMemcpy(dkr, kr, sizeof(orbx_keypoint) * nr, hipMemcpyHostToDevice) != hipSuccess) ||
-                (nr && hipMemcpy(ddr, dr, 32 * (size_t)nr, hipMemcpyHostToDevice) != hipSuccess) ||
-                hipMemcpy(dn, ns, sizeof(ns), hipMemcpyHostToDevice) != hipSuccess))
-        rc = ORBX_EIO;
-    if (!rc) {
-        StereoBufs a{};
-        a.lv = left->dp.lv; a.nlevels = left->nlevels; a.rows = rows;
-        a.left = pyr_view(left, left->cur); a.right = pyr_view(right, right->cur);
-        a.left_f0 = 0; a.right_f0 = 0; a.fstep = 0;
-        a.kl = dkl; a.dl = ddl; a.nl = dn; a.kr = dkr; a.dr = ddr; a.nr = dn + 1;
-        a.kstride = 0; a.nstride = 0; a.nr_cap = ncap;
-        a.mbf = mbf; a.maxd = mbf / mb;
-        a.ur = dur; a.depth = ddp; a.sad = dsad; a.ostride = 0; a.nkept = dnk;
-        if (launch_stereo(a, 1, nl, left->stream) != hipSuccess || hipStreamSynchronize(left->stream) != hipSuccess)
-            rc = ORBX_EIO;
+    auto &w = left->sws;
+    if (nl > w.cap_l || ncap > w.cap_r) {
+        w.free_dev();
+        const int cl = std::max(nl, left->plan.max_kps), cr = std::max(ncap, left->plan.max_kps);
+        if (dalloc(&w.kl, cl) != hipSuccess || dalloc(&w.dl, 32 * (size_t)cl) != hipSuccess ||
+            dalloc(&w.kr, cr) != hipSuccess || dalloc(&w.dr, 32 * (size_t)cr) != hipSuccess ||
+            dalloc(&w.n, 2) != hipSuccess || dalloc(&w.sad, cl) != hipSuccess || dalloc(&w.nk, 1) != hipSuccess ||
+            dalloc(&w.ur, cl) != hipSuccess || dalloc(&w.depth, cl) != hipSuccess) {
+            w.free_dev();
+            return ORBX_ENOMEM;
+        }
+        w.cap_l = cl;
+        w.cap_r = cr;
     }
-    if (!rc && (hipMemcpy(uright, dur, 4 * (size_t)nl, hipMemcpyDeviceToHost) != hipSuccess ||
-                hipMemcpy(depth, ddp, 4 * (size_t)nl, hipMemcpyDeviceToHost) != hipSuccess ||
-                hipMemcpy(nkept, dnk, sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess))
-        rc = ORBX_EIO;
-    dfree(dkl); dfree(dkr); dfree(ddl); dfree(ddr); dfree(dn); dfree(dsad); dfree(dnk); dfree(dur); dfree(ddp);
-    return rc;
+    const size_t hb = 8 * (size_t)w.cap_l + 16;
+    if (w.h_bytes < hb) {
+        if (w.h_res) (void)hipHostFree(w.h_res);
+        w.h_res = nullptr;
+        w.h_bytes = 0;
+        if (hipHostMalloc(reinterpret_cast<void **>(&w.h_res), hb, hipHostMallocDefault) != hipSuccess)
+            return ORBX_ENOMEM;
+        w.h_bytes = hb;
+    }
+    hipStream_t st = left->stream;
+    StereoBufs a{};
+    a.lv = left->dp.lv; a.nlevels = left->nlevels; a.rows = rows;
+    a.left = pyr_view(left, left->cur); a.right = pyr_view(right, right->cur);
+    a.left_f0 = 0; a.right_f0 = 0; a.fstep = 0;
+    a.kstride = 0; a.nstride = 0; a.nr_cap = ncap;
+    // each side: the extractor's resident result when the host arrays are it,
+    // else an upload (with the counts in the workspace)
+    const bool lhit = same_as_last_host_result(left, kl, dl, nl), rhit = same_as_last_host_result(right, kr, dr, nr);
+    const int32_t ns[2] = {nl, nr};
+    bool ok = true;
+    if (!lhit || !rhit) ok = hipMemcpyAsync(w.n, ns, sizeof(ns), hipMemcpyHostToDevice, st) == hipSuccess;
+    if (lhit) {
+        a.kl = left->slot[0].kps; a.dl = left->slot[0].desc; a.nl = left->slot[0].nkps;
+    } else {
+        ok = ok && hipMemcpyAsync(w.kl, kl, sizeof(orbx_keypoint) * nl, hipMemcpyHostToDevice, st) == hipSuccess &&
+             hipMemcpyAsync(w.dl, dl, 32 * (size_t)nl, hipMemcpyHostToDevice, st) == hipSuccess;
+        a.kl = w.kl; a.dl = w.dl; a.nl = w.n;
+    }
+    if (rhit) {
+        a.kr = right->slot[0].kps; a.dr = right->slot[0].desc; a.nr = right->slot[0].nkps;
+    } else {
+        ok = ok && (nr == 0 || (hipMemcpyAsync(w.kr, kr, sizeof(orbx_keypoint) * nr, hipMemcpyHostToDevice, st) ==
+                                    hipSuccess &&
+                                hipMemcpyAsync(w.dr, dr, 32 * (size_t)nr, hipMemcpyHostToDevice, st) == hipSuccess));
+        a.kr = w.kr; a.dr = w.dr; a.nr = w.n + 1;
+    }
+    a.mbf = mbf; a.maxd = mbf / mb;
+    a.ur = w.ur; a.depth = w.depth; a.sad = w.sad; a.ostride = 0; a.nkept = w.nk;
+    ok = ok && launch_stereo(a, 1, nl, st) == hipSuccess &&
+         hipMemcpyAsync(w.h_res, w.ur, 4 * (size_t)nl, hipMemcpyDeviceToHost, st) == hipSuccess &&
+         hipMemcpyAsync(w.h_res + 4 * (size_t)w.cap_l, w.depth, 4 * (size_t)nl, hipMemcpyDeviceToHost, st) ==
+             hipSuccess &&
+         hipMemcpyAsync(w.h_res + 8 * (size_t)w.cap_l, w.nk, sizeof(int32_t), hipMemcpyDeviceToHost, st) == hipSuccess &&
+         hipStreamSynchronize(st) == hipSuccess;
+    if (!ok) return ORBX_EIO;
+    std::memcpy(uright, w.h_res, 4 * (size_t)nl);
+    std::memcpy(depth, w.h_res + 4 * (size_t)w.cap_l, 4 * (size_t)nl);
+    std::memcpy(nkept, w.h_res + 8 * (size_t)w.cap_l, sizeof(int32_t));
+    return ORBX_OK;
 }
 
 int orbx_stereo_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t frame_stride, int pitch, int pairs,

@@ -24,16 +24,30 @@ __device__ inline void wave_lds_fence() {
 constexpr int kRowShr1 = 0x111, kRowShr2 = 0x112, kRowShr4 = 0x114, kRowShr8 = 0x118;
 constexpr int kRowBcast15 = 0x142, kRowBcast31 = 0x143;
 
-// Inclusive prefix sum over the 64 lanes.
+// Inclusive prefix sum over the 64 lanes: six in-place v_add_u32_dpp.  (The
+// compiler's form of the same DPP sums is a v_mov 0, a v_mov_dpp and a v_add
+// per step when it does not fold them: 3x the VALU.)  A lane without a
+// row_shr source adds 0 (bound_ctrl); rows outside a row_bcast's row_mask are
+// not written, i.e. keep their sum.  The s_nop 1 before each step covers the
+// two wait states a DPP read of a VGPR the previous VALU wrote needs (the
+// compiler inserts none inside asm).
 __device__ inline int wave_incl_scan_i32(int v) {
-    uint32_t u = (uint32_t)v;
-    u += dpp_or<kRowShr1>(0u, u);
-    u += dpp_or<kRowShr2>(0u, u);
-    u += dpp_or<kRowShr4>(0u, u);
-    u += dpp_or<kRowShr8>(0u, u);
-    u += dpp_or<kRowBcast15, 0xA>(0u, u);
-    u += dpp_or<kRowBcast31, 0xC>(0u, u);
-    return (int)u;
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_add_u32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "s_nop 1\n\t"
+        "v_add_u32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "s_nop 1\n\t"
+        "v_add_u32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "s_nop 1\n\t"
+        "v_add_u32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "s_nop 1\n\t"
+        "v_add_u32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_add_u32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+        "s_nop 1"
+        : "+v"(v));
+    return v;
 }
 
 // Inclusive prefix sum of packed pairs of 32-bit counters (the halves are
