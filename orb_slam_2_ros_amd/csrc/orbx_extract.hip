@@ -283,14 +283,26 @@ __device__ inline int wave_stage_rows(uint8_t *dst, int ds, const uint8_t *img, 
     const int rl = div_small(lane, nd), k = lane - mul24u(rl, nd);
     const int voff = mul24u(rl, pitch) + 4 * k, loff = mul24u(rl, ds) + 4 * k;
     const int rmax = rl < R ? nr - rl : 0;   // this lane loads rows r0 + j R < rmax
-    for (int r0 = 0; r0 < nr; r0 += NB * R) {
+    // the row offsets as scalar multiples of R * pitch (a v_mul_lo_u32 per
+    // load otherwise: quarter rate, then a readfirstlane)
+    const int Rp = __builtin_amdgcn_readfirstlane(R * pitch);
+    for (int r0 = 0, s0 = 0; r0 < nr; r0 += NB * R, s0 += NB * Rp) {
         uint32_t v[NB];
 #pragma unroll
-        for (int j = 0; j < NB; ++j)
-            if (r0 + j * R < rmax) v[j] = load(voff, r0 + j * R);
+        for (int j = 0; j < NB; ++j) {
+            if constexpr (BUF) {
+                if (r0 + mul24u(j, R) < rmax) v[j] = buf_ld32(src, voff, s0 + j * Rp);
+            } else {
+                if (r0 + j * R < rmax) v[j] = load(voff, r0 + j * R);
+            }
+        }
 #pragma unroll
         for (int j = 0; j < NB; ++j)
-            if (r0 + j * R < rmax) *reinterpret_cast<uint32_t *>(dst + mul24u(r0 + j * R, ds) + loff) = v[j];
+            if constexpr (BUF) {
+                if (r0 + mul24u(j, R) < rmax) *reinterpret_cast<uint32_t *>(dst + mul24u(r0 + mul24u(j, R), ds) + loff) = v[j];
+            } else {
+                if (r0 + j * R < rmax) *reinterpret_cast<uint32_t *>(dst + mul24u(r0 + j * R, ds) + loff) = v[j];
+            }
     }
     return o;
 }
@@ -733,11 +745,11 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
                 const int ey = e >> 8, ex = e & 0xFF;
                 const uint8_t *q = pc + mul24u(ey, PS) + ex;
                 const int v = q[0];
-                const int pr[16] = {q[3 * PS],  q[3 * PS + 1],  q[2 * PS + 2],  q[PS + 3],
-                                    q[3],       q[-PS + 3],     q[-2 * PS + 2], q[-3 * PS + 1],
-                                    q[-3 * PS], q[-3 * PS - 1], q[-2 * PS - 2], q[-PS - 3],
-                                    q[-3],      q[PS - 3],      q[2 * PS - 2],  q[3 * PS - 1]};
-                const int S = arc_score_bytes(pr, v);
+                const uint32_t pr[16] = {q[3 * PS],  q[3 * PS + 1],  q[2 * PS + 2],  q[PS + 3],
+                                         q[3],       q[-PS + 3],     q[-2 * PS + 2], q[-3 * PS + 1],
+                                         q[-3 * PS], q[-3 * PS - 1], q[-2 * PS - 2], q[-PS - 3],
+                                         q[-3],      q[PS - 3],      q[2 * PS - 2],  q[3 * PS - 1]};
+                const int S = arc_score_bytes(reinterpret_cast<const int *>(pr), v);
                 corner = S > th;
                 if (corner) scm[mul24u(ey + 1, SW) + ex + 1] = (uint8_t)(S - 1);
             }
@@ -1537,7 +1549,8 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
         // (__umul24 reads the low 24 bits of cb: 0x400000 + c, c in [-18, 18])
         const uint32_t off = __umul24(cb, 2 * kColS) + ((rb << 1) + kOff);
         const u32x4a v = *reinterpret_cast<const u32x4a *>(lbase + (off & ~3u));
-        const uint32_t sh = off & 2u ? 16u : 0u;   // odd row (the low bit of rb)
+        // odd row (the low bit of rb): shift 16; v_alignbit reads its shift's low 5 bits
+        const uint32_t sh = rb << 4;
         // k0 R0 + k1 R1 + k2 R2 + k3 R3 + k2 R4 + k1 R5 + k0 R6 as four u16-pair dot products
         const uint32_t e0 = __builtin_amdgcn_alignbit(v.y, v.x, sh), e1 = __builtin_amdgcn_alignbit(v.z, v.y, sh),
                        e2 = __builtin_amdgcn_alignbit(v.w, v.z, sh), e3 = __builtin_amdgcn_alignbit(v.w, v.w, sh);
