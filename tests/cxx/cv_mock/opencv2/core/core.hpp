@@ -3,6 +3,7 @@
 // exercised in this OpenCV-free container.  Test scaffolding for OUR adapter
 // only (nothing of the reference is built against it).
 #pragma once
+#include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <memory>
@@ -35,6 +36,9 @@ struct KeyPoint {
         : pt(p), size(s), angle(a), response(r), octave(o), class_id(c) {}
 };
 
+class Mat;
+Mat operator*(const Mat &a, const Mat &b);
+
 class Mat {
 public:
     int rows = 0, cols = 0;
@@ -59,6 +63,49 @@ public:
     template <typename T> T *ptr(int r = 0) { return reinterpret_cast<T *>(data + r * step); }
     template <typename T> const T *ptr(int r = 0) const { return reinterpret_cast<const T *>(data + r * step); }
     template <typename T> const T &at(int r, int c) const { return ptr<T>(r)[c]; }
+    template <typename T> T &at(int r, int c) { return ptr<T>(r)[c]; }
+    // single index: element i of a row or column vector
+    template <typename T> T &at(int i) { return rows == 1 ? ptr<T>(0)[i] : ptr<T>(i)[0]; }
+    template <typename T> const T &at(int i) const { return rows == 1 ? ptr<T>(0)[i] : ptr<T>(i)[0]; }
+    // --- float matrix arithmetic (CV_32F) for the ORB-SLAM2 forwarder tests ---
+    Mat(int r, int c, int t, float fill) {
+        create(r, c, t);
+        for (int i = 0; i < r; ++i)
+            for (int j = 0; j < c; ++j) at<float>(i, j) = fill;
+    }
+    static Mat zeros(int r, int c, int t) { return Mat(r, c, t, 0.f); }
+    static Mat eye(int r, int c, int t) {
+        Mat m(r, c, t, 0.f);
+        for (int i = 0; i < r && i < c; ++i) m.at<float>(i, i) = 1.f;
+        return m;
+    }
+    Mat row(int i) const { return rowRange(i, i + 1); }
+    Mat col(int j) const { return colRange(j, j + 1); }
+    Mat colRange(int a, int b) const { Mat m = *this; m.data = data + a * elemSize(); m.cols = b - a; return m; }
+    Mat t() const {
+        Mat m(cols, rows, type_);
+        for (int i = 0; i < rows; ++i)
+            for (int j = 0; j < cols; ++j) m.at<float>(j, i) = at<float>(i, j);
+        return m;
+    }
+    double dot(const Mat &o) const {
+        double s = 0;
+        for (int i = 0; i < rows; ++i)
+            for (int j = 0; j < cols; ++j) s += (double)at<float>(i, j) * (double)o.at<float>(i, j);
+        return s;
+    }
+    template <typename F> Mat map(F f) const {
+        Mat m(rows, cols, type_);
+        for (int i = 0; i < rows; ++i)
+            for (int j = 0; j < cols; ++j) m.at<float>(i, j) = f(at<float>(i, j), i, j);
+        return m;
+    }
+    Mat operator-() const { return map([](float v, int, int) { return -v; }); }
+    Mat operator/(float s) const { return map([s](float v, int, int) { return v / s; }); }
+    Mat operator+(const Mat &o) const { return map([&o](float v, int i, int j) { return v + o.at<float>(i, j); }); }
+    Mat operator-(const Mat &o) const { return map([&o](float v, int i, int j) { return v - o.at<float>(i, j); }); }
+    friend Mat operator*(float s, const Mat &m) { return m.map([s](float v, int, int) { return s * v; }); }
+    Mat operator*(float s) const { return map([s](float v, int, int) { return v * s; }); }
     Mat rowRange(int a, int b) const { Mat m = *this; m.data = data + a * step; m.rows = b - a; return m; }
     Mat operator()(Rect r) const {
         Mat m = *this; m.data = data + r.y * step + r.x * elemSize(); m.rows = r.height; m.cols = r.width; return m;
@@ -72,6 +119,23 @@ public:
         for (int i = 0; i < rows; ++i) std::memcpy(dst.data + i * dst.step, data + i * step, cols * elemSize());
     }
 };
+
+inline Mat operator*(const Mat &a, const Mat &b) {
+    Mat m(a.rows, b.cols, CV_32F);
+    for (int i = 0; i < a.rows; ++i)
+        for (int j = 0; j < b.cols; ++j) {
+            float s = 0.f;
+            for (int k = 0; k < a.cols; ++k) s += a.at<float>(i, k) * b.at<float>(k, j);
+            m.at<float>(i, j) = s;
+        }
+    return m;
+}
+inline double norm(const Mat &m) {
+    double s = 0;
+    for (int i = 0; i < m.rows; ++i)
+        for (int j = 0; j < m.cols; ++j) s += (double)m.at<float>(i, j) * (double)m.at<float>(i, j);
+    return std::sqrt(s);
+}
 
 class _InputArray {
 public:

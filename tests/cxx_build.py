@@ -14,3 +14,32 @@ def build_adapter_test() -> Path:
                     f"-I{ROOT / 'tests' / 'cxx' / 'cv_mock'}", str(ROOT / "tests" / "cxx" / "adapter_test.cpp"),
                     f"-L{lib_dir}", "-lorbx", f"-Wl,-rpath,{lib_dir}", "-o", str(out)], check=True)
     return out
+
+
+FORWARDERS = ["integration/ORBmatcher_orbx.cc", "integration/Optimizer_orbx.cc",
+              "integration/KeyFrameDatabase_orbx.cc", "integration/Frame_orbx.cc", "integration/LocalMapping_orbx.cc",
+              "tests/cxx/orbslam_mock/mock_impl.cpp", "tests/cxx/forwarders_test.cpp"]
+
+
+def build_forwarders_test(backend: str) -> Path:
+    """tests/cxx/forwarders_test: the reference-side forwarders of integration/
+    compiled against the test stand-ins of the reference headers.  backend
+    "liborbx" links the product library (the GPU run); "oracle" answers the
+    orbx_* calls with the CPU oracle (tests/cxx/orbx_oracle_shim.cpp), so the
+    forwarders' own logic is checked without a GPU."""
+    out = Path(tempfile.mkdtemp(prefix="orbx_fwd_")) / f"forwarders_test_{backend}"
+    lib_dir, oracle_dir = ROOT / "orb_slam_2_ros_amd", ROOT / "oracle"
+    srcs = [str(ROOT / s) for s in FORWARDERS]
+    if backend == "oracle":
+        srcs.append(str(ROOT / "tests" / "cxx" / "orbx_oracle_shim.cpp"))
+        libs = []
+    elif backend == "liborbx":
+        libs = [f"-L{lib_dir}", "-lorbx", f"-Wl,-rpath,{lib_dir}"]
+    else:
+        raise ValueError(backend)
+    inc = [ROOT / "integration", ROOT / "tests" / "cxx" / "orbslam_mock", ROOT / "tests" / "cxx" / "cv_mock",
+           ROOT / "include", oracle_dir]
+    subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", "-Werror", *[f"-I{i}" for i in inc], *srcs,
+                    *libs, f"-L{oracle_dir}", "-lorbx_oracle", f"-Wl,-rpath,{oracle_dir}", "-o", str(out)],
+                   check=True)
+    return out
