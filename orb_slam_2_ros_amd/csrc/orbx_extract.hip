@@ -45,6 +45,37 @@ struct DiscMask {
 };
 __constant__ DiscMask c_disc_mask = DiscMask();
 
+// IC_Angle's moments on the matrix cores (k_describe): six int8 MFMAs over the
+// staged patch (rows 0..47 as three 16-row tiles, patch columns 0..63 as two
+// 32-column halves; the disc is rows 6..36, columns 6 + o .. 36 + o for the
+// staging offset o).  Per (o, row tile rt, half h, lane):
+//   mask: the A-operand bytes kept, patch row 16 rt + (l & 15), columns
+//         32 h + 8 (l >> 4) + 0..7, inside the disc (kUmax);
+//   b:    the B-operand bytes, k = 8 (l >> 4) + 0..7, output column j = l & 15:
+//         j = 15: u = 32 h + k - 21 - o (m10), j = 12 + rt: 1 (the rows' sums,
+//         weighted by their v afterwards: m01), others 0.
+struct MomTables {
+    uint64_t mb[4][3][2][64][2];   // (mask, b): one 16-byte load a product
+    constexpr MomTables() : mb() {
+        for (int o = 0; o < 4; ++o)
+            for (int rt = 0; rt < 3; ++rt)
+                for (int h = 0; h < 2; ++h)
+                    for (int l = 0; l < 64; ++l) {
+                        uint64_t mk = 0, bb = 0;
+                        const int v = 16 * rt + (l & 15) - 21, av = v < 0 ? -v : v, j = l & 15;
+                        for (int jj = 0; jj < 8; ++jj) {
+                            const int u = 32 * h + 8 * (l >> 4) + jj - 21 - o, au = u < 0 ? -u : u;
+                            if (av <= 15 && au <= kUmax[av]) mk |= 0xFFull << (8 * jj);
+                            const int w = j == 15 ? u : (j == 12 + rt ? 1 : 0);
+                            bb |= (uint64_t)(uint8_t)(int8_t)w << (8 * jj);
+                        }
+                        mb[o][rt][h][l][0] = mk;
+                        mb[o][rt][h][l][1] = bb;
+                    }
+    }
+};
+__constant__ MomTables c_mom = MomTables();
+
 // Phase profiling (diagnostic build only, -DORBX_PHASE_PROF: tools/phase_prof.py):
 // each wave adds the s_memtime cycles of its phases to g_phase[kernel][phase]
 // (lane 0, vector atomics).  The product build compiles the marks away.
@@ -65,6 +96,21 @@ __device__ unsigned long long g_phase[3][8][256];
 #define PHASE_START() uint64_t phase_t_ = 0; (void)phase_t_
 #define PHASE_MARK(K, I) (void)0
 #endif
+
+// Per-phase instruction counts (tools/phase_valu.sh): a build with
+// -DORBX_STOP_FAST=N / -DORBX_STOP_DESC=N compiles k_fast / k_describe only up
+// to the end of phase N (k_fast: 1 staging, 2 iniThFAST compass + compaction,
+// 3 its arc scores, 4 its NMS + output, no minThFAST pass; k_describe:
+// 1 staging, 2 moments + row pass, 4 orientation + sample offsets + column
+// pass), so SQ_INSTS_* differences between builds split the counts by phase.
+// Results of such builds are wrong by design; 0 = the product.
+#ifndef ORBX_STOP_FAST
+#define ORBX_STOP_FAST 0
+#endif
+#ifndef ORBX_STOP_DESC
+#define ORBX_STOP_DESC 0
+#endif
+constexpr int kStopFast = ORBX_STOP_FAST, kStopDesc = ORBX_STOP_DESC;
 
 namespace {
 
@@ -248,9 +294,11 @@ __device__ inline uint32_t buf_ld32(__amdgpu_buffer_rsrc_t r, int voff, int soff
 // buffer loads, the row offset a scalar operand and the lane offset a 32-bit
 // VGPR (k_fast, k_describe: -2 % time); the resize windows (up to 24
 // rows in flight) measured 2 % slower that way and keep global loads.
-template <int NB = 8, bool BUF = true>
+// X80: the bytes are stored XOR 0x80 (as signed I - 128, k_describe's int8 MFMAs).
+template <int NB = 8, bool BUF = true, bool X80 = false>
 __device__ inline int wave_stage_rows(uint8_t *dst, int ds, const uint8_t *img, int pitch, int y0, int x0, int nr,
                                       int nc, int lane) {
+    constexpr uint32_t kX = X80 ? 0x80808080u : 0u;
     // (all wave-uniform: row offsets then come from the scalar unit)
     pitch = __builtin_amdgcn_readfirstlane(pitch);
     ds = __builtin_amdgcn_readfirstlane(ds);
@@ -274,7 +322,7 @@ __device__ inline int wave_stage_rows(uint8_t *dst, int ds, const uint8_t *img, 
                     if (on && r0 + j < nr) v[j] = load(voff, r0 + j);
 #pragma unroll
                 for (int j = 0; j < NB; ++j)
-                    if (on && r0 + j < nr) *reinterpret_cast<uint32_t *>(dst + mul24u(r0 + j, ds) + voff) = v[j];
+                    if (on && r0 + j < nr) *reinterpret_cast<uint32_t *>(dst + mul24u(r0 + j, ds) + voff) = v[j] ^ kX;
             }
         }
         return o;
@@ -299,9 +347,9 @@ __device__ inline int wave_stage_rows(uint8_t *dst, int ds, const uint8_t *img, 
 #pragma unroll
         for (int j = 0; j < NB; ++j)
             if constexpr (BUF) {
-                if (r0 + mul24u(j, R) < rmax) *reinterpret_cast<uint32_t *>(dst + mul24u(r0 + mul24u(j, R), ds) + loff) = v[j];
+                if (r0 + mul24u(j, R) < rmax) *reinterpret_cast<uint32_t *>(dst + mul24u(r0 + mul24u(j, R), ds) + loff) = v[j] ^ kX;
             } else {
-                if (r0 + j * R < rmax) *reinterpret_cast<uint32_t *>(dst + mul24u(r0 + j * R, ds) + loff) = v[j];
+                if (r0 + j * R < rmax) *reinterpret_cast<uint32_t *>(dst + mul24u(r0 + j * R, ds) + loff) = v[j] ^ kX;
             }
     }
     return o;
@@ -634,6 +682,10 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
     const uint8_t *pc = patch + 3 * PS + o + 3;         // interior pixel (0, 0)
     const uint64_t below = (1ull << lane) - 1;
     PHASE_MARK(0, 0);   // prologue + staging
+    if constexpr (kStopFast == 1) {
+        if (lane == 0) *count_out = 0;
+        return;
+    }
     uint32_t *out_i = fb.cand + (int64_t)b * p.cand_cap + c.slot;
     uint32_t *out_m = fb.cand2 + (int64_t)b * p.cand_cap + c.slot;
     // The compass pass's lane geometry (both passes): lane = (row in pass,
@@ -641,16 +693,21 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
     // so its interior mask is fixed.
     const int qc0 = (o + 3) & ~3;                           // patch column of the first quad
     const int nq = ((o + 2 + cw) >> 2) - (qc0 >> 2) + 1;   // quads per row
-    const int R = __builtin_amdgcn_readfirstlane(div_small(64, nq));
-    const int rl = div_small(lane, nq), qi = lane - mul24u(rl, nq);
-    const int xx0 = qc0 - o - 3 + 4 * qi;   // interior x of the quad's byte 0
-    // candidate word: pixel j of the quad at bit 16 (j >> 1) + (j & 1)
-    uint32_t vmask = 0;
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj)
-        if (xx0 + jj >= 0 && xx0 + jj < cw) vmask |= 1u << (16 * (jj >> 1) + (jj & 1));
+    // a lane takes two adjacent quads (8 pixels) of one row: the loads, the
+    // loop and the compaction scan are shared by twice the pixels
+    const int np = (nq + 1) >> 1;                           // quad pairs per row
+    const int R = __builtin_amdgcn_readfirstlane(div_small(64, np));
+    const int rl = div_small(lane, np), pi = lane - mul24u(rl, np);
+    const int xx0 = qc0 - o - 3 + 8 * pi;   // interior x of the pair's byte 0
+    // candidate byte: bit j = pixel j of the pair; the interior pixels
+    // [lo, hi) of the pair as one bit field
+    const int vlo = min(max(-xx0, 0), 8), vhi = min(max(cw - xx0, 0), 8);
+    uint32_t vmask = __builtin_amdgcn_ubfe(0xFFu << vlo, 0, (uint32_t)vhi);   // bits [lo, hi)
     if (rl >= R) vmask = 0;   // (tail lanes: rows of the next pass)
-    const uint8_t *q0 = patch + mul24u(3 + rl, PS) + qc0 + 4 * qi;
+    // the lane's pair in LDS, 3 rows up (every load a non-negative offset from
+    // it; 32-bit address arithmetic), and its row limit
+    const lds_u8 *qb0 = (const lds_u8 *)(patch + mul24u(rl, PS) + qc0 + 8 * pi);
+    const int rlim = mul24u(max(ch - rl, 0), PS);   // (row offsets in bytes: the loop runs on scalars)
 
     // One FAST pass at threshold th: returns the keypoints kept after NMS,
     // written to out.  The reference runs iniThFAST first and minThFAST only
@@ -673,56 +730,73 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
         {
             const u16x2 thv = {(unsigned short)th, (unsigned short)th};
             const u16x2 thv8 = {(unsigned short)(th << 8), (unsigned short)(th << 8)};
-            int e = (rl << 8) + xx0;
-            for (int y0 = 0; y0 < ch; y0 += R, e += R << 8) {
+            typedef __attribute__((address_space(3))) const uint32_t lds_u32c;
+            const int e = (rl << 8) + xx0;
+            const int RPS = __builtin_amdgcn_readfirstlane(R * PS), R8 = __builtin_amdgcn_readfirstlane(R << 8);
+            const int chps = __builtin_amdgcn_readfirstlane(ch * PS);
+            for (int yo = 0, ys = 0; yo < chps; yo += RPS, ys += R8) {
                 uint32_t cand = 0;
-                if (rl + y0 < ch) {
-                    const uint8_t *q = q0 + mul24u(y0, PS);
-                    const uint32_t c = *reinterpret_cast<const uint32_t *>(q);
-                    const uint32_t l = *reinterpret_cast<const uint32_t *>(q - 4);
-                    const uint32_t r = *reinterpret_cast<const uint32_t *>(q + 4);
-                    const uint32_t up = *reinterpret_cast<const uint32_t *>(q - 3 * PS);
-                    const uint32_t dn = *reinterpret_cast<const uint32_t *>(q + 3 * PS);
-                    // pixel pairs (0, 2) and (1, 3) of the quad as u16 halves, straight from
-                    // the aligned dwords (v_perm picks the +-3 column bytes of (lo, hi) dword
-                    // pairs); even pixels: bytes 0 / 2 as the low bytes of the halves (an AND
-                    // for the aligned dwords); odd pixels: bytes 1 / 3 left in the high
-                    // bytes, every value and the threshold scaled by 256 -- the same
-                    // comparisons, without the shift
-                    auto half = [&](uint32_t mask, uint32_t sel4, uint32_t sel12, u16x2 thv) -> u16x2 {   // 1: candidate
-                        const u16x2 v = as_u16x2(c & mask);
-                        const u16x2 a0 = as_u16x2(dn & mask);
-                        const u16x2 a4 = as_u16x2(__builtin_amdgcn_perm(r, c, sel4));     // x + 3
-                        const u16x2 a8 = as_u16x2(up & mask);
-                        const u16x2 a12 = as_u16x2(__builtin_amdgcn_perm(c, l, sel12));   // x - 3
-                        // max over the cyclic pairs of the pair's min, and min of the max:
-                        // max(min(a,b), min(b,c), min(c,d), min(d,a)) = min(max(a,c), max(b,d))
-                        const u16x2 hi = __builtin_elementwise_min(__builtin_elementwise_max(a0, a8),
-                                                                   __builtin_elementwise_max(a4, a12));
-                        const u16x2 lo = __builtin_elementwise_max(__builtin_elementwise_min(a0, a8),
-                                                                   __builtin_elementwise_min(a4, a12));
-                        // hi > v + th  or  lo + th < v  <=>  max(hi - v, v - lo) > th (saturating)
-                        const u16x2 d = __builtin_elementwise_sub_sat(
-                            __builtin_elementwise_max(__builtin_elementwise_sub_sat(hi, v), __builtin_elementwise_sub_sat(v, lo)),
-                            thv);
-                        u16x2 m;   // min(d, 1) per half, kept one packed op
-                        asm("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(d), "s"(0x00010001u));
-                        return m;
+                if (yo < rlim) {
+                    const lds_u8 *qb = qb0 + yo;
+                    // the pair's dwords c0 c1, their row neighbours l r and the
+                    // rows 3 up / down
+                    const uint32_t l = *reinterpret_cast<lds_u32c *>(qb + 3 * PS - 4);
+                    const uint32_t c0 = *reinterpret_cast<lds_u32c *>(qb + 3 * PS);
+                    const uint32_t c1 = *reinterpret_cast<lds_u32c *>(qb + 3 * PS + 4);
+                    const uint32_t r = *reinterpret_cast<lds_u32c *>(qb + 3 * PS + 8);
+                    const uint32_t up0 = *reinterpret_cast<lds_u32c *>(qb);
+                    const uint32_t up1 = *reinterpret_cast<lds_u32c *>(qb + 4);
+                    const uint32_t dn0 = *reinterpret_cast<lds_u32c *>(qb + 6 * PS);
+                    const uint32_t dn1 = *reinterpret_cast<lds_u32c *>(qb + 6 * PS + 4);
+                    // one quad: pixel pairs (0, 2) and (1, 3) as u16 halves, straight
+                    // from the aligned dwords (v_perm picks the +-3 column bytes of
+                    // (lo, hi) dword pairs); even pixels: bytes 0 / 2 as the low bytes
+                    // of the halves (an AND for the aligned dwords); odd pixels: bytes
+                    // 1 / 3 left in the high bytes, every value and the threshold
+                    // scaled by 256 -- the same comparisons, without the shift
+                    auto quad = [&](uint32_t c, uint32_t lft, uint32_t rgt, uint32_t up, uint32_t dn) -> uint32_t {
+                        auto half = [&](uint32_t mask, uint32_t sel4, uint32_t sel12, u16x2 thv) -> u16x2 {   // 1: candidate
+                            const u16x2 v = as_u16x2(c & mask);
+                            const u16x2 a0 = as_u16x2(dn & mask);
+                            const u16x2 a4 = as_u16x2(__builtin_amdgcn_perm(rgt, c, sel4));    // x + 3
+                            const u16x2 a8 = as_u16x2(up & mask);
+                            const u16x2 a12 = as_u16x2(__builtin_amdgcn_perm(c, lft, sel12));  // x - 3
+                            // max over the cyclic pairs of the pair's min, and min of the max:
+                            // max(min(a,b), min(b,c), min(c,d), min(d,a)) = min(max(a,c), max(b,d))
+                            const u16x2 hi = __builtin_elementwise_min(__builtin_elementwise_max(a0, a8),
+                                                                       __builtin_elementwise_max(a4, a12));
+                            const u16x2 lo = __builtin_elementwise_max(__builtin_elementwise_min(a0, a8),
+                                                                       __builtin_elementwise_min(a4, a12));
+                            // hi > v + th  or  lo + th < v  <=>  max(hi - v, v - lo) > th (saturating)
+                            const u16x2 d = __builtin_elementwise_sub_sat(
+                                __builtin_elementwise_max(__builtin_elementwise_sub_sat(hi, v),
+                                                          __builtin_elementwise_sub_sat(v, lo)),
+                                thv);
+                            u16x2 m;   // min(d, 1) per half, kept one packed op
+                            asm("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(d), "s"(0x00010001u));
+                            return m;
+                        };
+                        // pixels 0 / 2 at bits 0 / 16, 1 / 3 at bits 1 / 17
+                        return __builtin_bit_cast(uint32_t, half(0x00FF00FFu, 0x0c050c03u, 0x0c030c01u, thv)) |
+                               (__builtin_bit_cast(uint32_t, half(0xFF00FF00u, 0x060c040cu, 0x040c020cu, thv8)) << 1);
                     };
-                    cand = (__builtin_bit_cast(uint32_t, half(0x00FF00FFu, 0x0c050c03u, 0x0c030c01u, thv)) |
-                            (__builtin_bit_cast(uint32_t, half(0xFF00FF00u, 0x060c040cu, 0x040c020cu, thv8)) << 1)) &
-                           vmask;
+                    const uint32_t q0b = quad(c0, l, c1, up0, dn0), q1b = quad(c1, c0, r, up1, dn1);
+                    // folded to bits 0..3 and 4..7
+                    const uint32_t b8 = q0b | (q1b << 4);
+                    cand = (b8 | (b8 >> 14)) & vmask;
                 }
                 // compaction in row-major order: an inclusive DPP scan of the
-                // lanes' counts (0..4) places each lane's run, then its bits
+                // lanes' counts (0..8) places each lane's run, then its bits
                 const int cnt = __builtin_popcount(cand);
-                const int incl = wave_incl_scan_i32(cnt);
+                const int incl = wave_incl_scan_i32_to(cnt);
                 const int total = __builtin_amdgcn_readlane(incl, 63);
                 if (total) {
-                    int pos = nsurv + incl - cnt;
+                    typedef __attribute__((address_space(3))) uint16_t lds_u16;
+                    lds_u16 *dst = (lds_u16 *)list + nsurv + (incl - cnt);
+                    const int ey = e + ys;
                     while (cand) {
-                        const int bt = __builtin_ctz(cand);
-                        list[pos++] = (uint16_t)(e + ((bt >> 3) | (bt & 1)));
+                        *dst = (uint16_t)(ey + __builtin_ctz(cand));
+                        ++dst;
                         cand &= cand - 1u;
                     }
                     nsurv += total;
@@ -731,6 +805,7 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
         }
         wave_lds_fence();
         PHASE_MARK(0, ph);       // score-map zeroing + compass pre-test + compaction
+        if constexpr (kStopFast == 2) return 0;
         // B. arc score of every survivor: S = max(M1 - v, v - M2), M1 = max over
         //    the 16 nine-pixel arcs of the arc's minimum, M2 = min over arcs of the
         //    arc's maximum, side by side as packed u16 lanes (p, 255 - p) through
@@ -760,6 +835,7 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
         }
         wave_lds_fence();
         PHASE_MARK(0, ph + 1);   // arc scores
+        if constexpr (kStopFast == 3) return 0;
         // C. strict 3x3 NMS inside the cell (outside neighbours and non-corners
         //    score 0), compacted in row-major order.
         int base = 0;
@@ -785,7 +861,7 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
     };
     const int n_ini = pass(p.ini_th, out_i, 1);
     int32_t cnt;
-    if (n_ini > 0) {
+    if (n_ini > 0 || (kStopFast >= 2 && kStopFast <= 4)) {
         cnt = min(n_ini, c.cap);
     } else {
         wave_lds_fence();
@@ -1354,12 +1430,9 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
     // this lane's 4 pattern pairs (bytes x0 y0 x1 y1 of pairs 2j, 2j + 1,
     // j = 64 grp + lane), fetched first so the loads overlap the staging
     float4 pat[4];
-    uint32_t dmask[4];
     const long row_taps = (long)c_row_taps.t[lane];
 #pragma unroll
     for (int grp = 0; grp < 4; ++grp) pat[grp] = reinterpret_cast<const float4 *>(c_pattern_f)[grp * 64 + lane];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) dmask[i] = c_disc_mask.m[(lane >> 3) + 8 * i][lane & 7];
     int bx, b;
     xcd_block_2d(bx, b, gmagic);
     const int slot = s0 + bx * 4 + wave;
@@ -1402,9 +1475,19 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
     int spitch;
     const uint8_t *img = level_ptr(p, fb, l, b, spitch);
     const int px0 = x - kDescR, py0 = y - kDescR;
-    if (px0 >= 0 && py0 >= 0 && x + kDescR < g.w && y + kDescR < g.h &&
-        (px0 & ~3) + 4 * (((px0 & 3) + kDescP + 3) >> 2) <= spitch) {
-        o = wave_stage_rows<(kDescP + 4) / 5>(lbase, kDescPS, img, spitch, py0, px0, kDescP, kDescP, lane);   // 5 rows a pass
+    const bool inside = px0 >= 0 && py0 >= 0 && x + kDescR < g.w && y + kDescR < g.h &&
+                        (px0 & ~3) + 4 * (((px0 & 3) + kDescP + 3) >> 2) <= spitch;
+    // the moment products' operand tables for this staging offset, loaded
+    // ahead of the patch so their latency hides under the staging's
+    typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+    u64x2 mom[6];
+    {
+        const u64x2 *mt = reinterpret_cast<const u64x2 *>(&c_mom.mb[inside ? px0 & 3 : 0][0][0][lane][0]);
+#pragma unroll
+        for (int t = 0; t < 6; ++t) mom[t] = mt[t * 64];
+    }
+    if (inside) {
+        o = wave_stage_rows<(kDescP + 4) / 5, true, true>(lbase, kDescPS, img, spitch, py0, px0, kDescP, kDescP, lane);   // 5 rows a pass
     } else {
         // near a level border: lane = patch column (its reflect-101 column fixed),
         // the rows in turn (the row's reflection is wave-uniform)
@@ -1415,60 +1498,18 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
         for (int r = 0; r < kDescP; ++r) {
             const int yy = reflect101(py0 + r, g.h);
             const uint8_t v = img[(int64_t)yy * sp + xx];
-            if (lane < kDescP) lbase[r * kDescPS + lane] = v;
+            if (lane < kDescP) lbase[r * kDescPS + lane] = v ^ 0x80;
         }
     }
-    const uint8_t *patch = lbase + o;
     wave_lds_fence();
     PHASE_MARK(1, 0);   // prologue + staging
 
-    // 2. IC_Angle (ORBextractor.cc:77-104): exact integer moments on the disc.
-    //    A task = 4 consecutive disc columns of one row (31 rows x 8 groups,
-    //    columns -16..15): m10 += sum((u + 16) * I) - 16 sum(I), m01 += v sum(I),
-    //    with v_dot4 on the realigned dword and the bytes outside the row's
-    //    |u| <= umax[|v|] masked off.
-    // The lane's column group g = lane & 7 is the same in every iteration (row
-    // ri = lane / 8 + 8 i), so the weights and the LDS offsets are fixed.
-    const uint8_t *center = patch + kDescR * kDescPS + kDescR;
-    int m10, m01 = 0;
-    {
-        const int g4 = lane & 7, u0 = 4 * g4 - 16, r0 = lane >> 3;
-        const uint32_t wu = (uint32_t)(u0 + 16) | (uint32_t)(u0 + 17) << 8 | (uint32_t)(u0 + 18) << 16 |
-                            (uint32_t)(u0 + 19) << 24;
-        const int addr = (int)(center - lbase) + (r0 - 15) * kDescPS + u0;   // byte offset of column u0, row r0 - 15
-        const uint32_t *ap = reinterpret_cast<const uint32_t *>(lbase + (addr & ~3));
-        const int sh = addr & 3;
-        uint32_t s1 = 0, s0 = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int ri = r0 + 8 * i;   // < 32; row 31 has an all-zero mask
-            const uint32_t px = __builtin_amdgcn_alignbyte(ap[i * 2 * kDescPS + 1], ap[i * 2 * kDescPS], sh);
-            const uint32_t pm = px & dmask[i];
-            const uint32_t si = __builtin_amdgcn_udot4(pm, 0x01010101u, 0u, false);
-            s1 = __builtin_amdgcn_udot4(pm, wu, s1, false);
-            s0 += si;
-            m01 += __mul24(ri - 15, (int)si);   // |ri - 15| <= 16, si <= 1020: 24-bit multiply
-        }
-        m10 = (int)s1 - 16 * (int)s0;
-    }
-    m10 = wave_sum_i32(m10);
-    m01 = wave_sum_i32(m01);
-    if (lane == 0) {
-        s_mom[wave][0] = m01;
-        s_mom[wave][1] = m10;
-    }
-    PHASE_MARK(1, 1);   // moments
-
-    // 3. Gaussian 7x7 restricted to the 37x37 sample window: row pass over all
-    //    43 rows (8-wide segments slide along a row), then the column pass with
-    //    OpenCV 3.2's per-column rounding (half-even below w & ~3, else half-up).
-    // Nine 16 x 16 output tiles (rows 16 rt.., patch columns 16 ct..; window
-    // column = patch column - o) as int8 MFMAs, D = P T: A operand, lane l
-    // holds P[16 rt + (l & 15)][16 ct + 8 (l >> 4) + 0..7] - 128 (one
-    // ds_read_b64); B = the Toeplitz taps.  D's lane l holds rows
-    // 16 rt + 4 (l >> 4) + 0..3 of output column 16 ct + (l & 15): one 8-byte
-    // store into the column-major buffer.  Only columns < 40 and rows < 44 are
-    // stored (row 43 is padding).
+    if constexpr (kStopDesc == 0 || kStopDesc >= 2) {
+    // 2. IC_Angle's moments (ORBextractor.cc:77-104) and the horizontal pass of
+    //    the 7x7 Gaussian, both as int8 MFMAs on the same pixel tiles.  The patch
+    //    was staged as I - 128 (XOR 0x80); the moments over the disc do not see
+    //    that bias (sum u = sum v = 0 over the symmetric disc) and the row pass's
+    //    accumulator starts at 128 * sum(w) to undo it.
     {
         const int rl = lane & 15, q = lane >> 4;
         const uint8_t *bsrc = lbase + rl * kDescPS + 8 * q;
@@ -1477,8 +1518,52 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
         for (int rt = 0; rt < 3; ++rt)
 #pragma unroll
             for (int ct = 0; ct < 3; ++ct)
-                px[rt][ct] = *reinterpret_cast<const uint64_t *>(bsrc + 16 * rt * kDescPS + 16 * ct) ^
-                             0x8080808080808080ull;
+                px[rt][ct] = *reinterpret_cast<const uint64_t *>(bsrc + 16 * rt * kDescPS + 16 * ct);
+        // moments: A = the disc's pixels of tiles (rt, ct = 0 / 2), B = c_mom.b;
+        // D[i][15] = sum of u I over row i, D[i][12 + rt] = sum of I over row
+        // 16 rt + i, summed over the six products (lane l: D[4 (l >> 4) + ii][l & 15])
+        {
+            i32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+            for (int rt = 0; rt < 3; ++rt)
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    acc = __builtin_amdgcn_mfma_i32_16x16x32_i8((long)(px[rt][2 * h] & mom[2 * rt + h].x),
+                                                                (long)mom[2 * rt + h].y, acc, 0, 0, 0);
+            // m10: lane 15 of each row, S; m01: lanes 12..14, v-weighted rows
+            // (v = 16 (j - 12) + 4 (l >> 4) + ii - 21), folded into lane 15
+            const int j = rl;
+            const int S = acc[0] + acc[1] + acc[2] + acc[3];
+            const int T = acc[1] + 2 * acc[2] + 3 * acc[3];
+            const bool rows = j >= 12 && j <= 14;
+            int y = rows ? __mul24(16 * (j - 12) + 4 * q - 21, S) + T : 0;
+            int x = S;
+            asm volatile(
+                "s_nop 1\n\t"
+                "v_add_u32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+                "s_nop 1\n\t"
+                "v_add_u32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+                "s_nop 1\n\t"
+                "v_add_u32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+                "v_add_u32_dpp %1, %1, %1 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+                "s_nop 1\n\t"
+                "v_add_u32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+                "v_add_u32_dpp %1, %1, %1 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+                "s_nop 1"
+                : "+v"(y), "+v"(x));
+            if (lane == 0) {
+                s_mom[wave][0] = __builtin_amdgcn_readlane(y, 63);
+                s_mom[wave][1] = __builtin_amdgcn_readlane(x, 63);
+            }
+        }
+        PHASE_MARK(1, 1);   // moments
+        // row pass: nine 16 x 16 output tiles (rows 16 rt.., patch columns
+        // 16 ct..; window column = patch column - o), D = P T: A operand, lane
+        // l holds P[16 rt + (l & 15)][16 ct + 8 (l >> 4) + 0..7] - 128 (one
+        // ds_read_b64); B = the Toeplitz taps.  D's lane l holds rows
+        // 16 rt + 4 (l >> 4) + 0..3 of output column 16 ct + (l & 15): one
+        // 8-byte store into the column-major buffer.  Only columns < 40 and
+        // rows < 44 are stored (row 43 is padding).
         const i32x4 bias = {128 * 257, 128 * 257, 128 * 257, 128 * 257};
         static_assert(kGaussTaps[0] + kGaussTaps[1] + kGaussTaps[2] + kGaussTaps[3] + kGaussTaps[4] +
                           kGaussTaps[5] + kGaussTaps[6] == 257, "bias = 128 * sum of the taps");
@@ -1497,6 +1582,7 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
             }
     }
     PHASE_MARK(1, 2);   // row pass
+    }   // kStopDesc
     }   // valid
     // The orientation (fastAtan2) and its sincosf are wave-uniform scalar
     // chains of ~90 VALU each: wave 0 evaluates the block's four at once (lane
@@ -1513,6 +1599,27 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
     __syncthreads();
     if (!valid) return;
     const float angle = s_ang[wave][0], sa = s_ang[wave][1], ca = s_ang[wave][2];
+    const int64_t kp_index = (int64_t)b * p.max_kps + off + i;
+    // the keypoint record (the matchers downstream index their grids with it)
+    auto write_record = [&]() {
+        if (lane == 0) {
+            orbx_keypoint kp;
+            float fx = (float)x, fy = (float)y;
+            if (l != 0) { fx = __fmul_rn(fx, g.scale); fy = __fmul_rn(fy, g.scale); }
+            kp.x = fx;
+            kp.y = fy;
+            kp.size = g.patch_size;
+            kp.angle = angle;
+            kp.response = (float)score;
+            kp.octave = l;
+            kp.class_id = -1;
+            fb.kps[kp_index] = kp;
+        }
+    };
+    if constexpr (kStopDesc != 0 && kStopDesc < 4) {
+        write_record();
+        return;
+    }
 
     // 4. computeOrbDescriptor (ORBextractor.cc:106-147) on the blurred level:
     //    each sample's blurred value is the column pass evaluated at that pixel
@@ -1536,6 +1643,10 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
                           (uint32_t)(2 * kColS) * 0x400000u - 2u * 0x4B400000u;
     static_assert((kDescRowOff & 3) == 0 && (kColS & 1) == 0, "dword-aligned column starts");
     typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+    typedef __attribute__((address_space(3))) const u32x4a lds_u32x4a;
+    // the LDS address of the wave's buffer folded into the constant: the
+    // address is then one v_lshl_add and one v_mad_u32_u24 from the bits
+    const uint32_t kOffL = __builtin_amdgcn_readfirstlane(kOff + (uint32_t)(uintptr_t)(const lds_u8 *)lbase);
     int sums[8], cbs[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -1547,8 +1658,10 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
         const uint32_t cb = __float_as_uint(__fadd_rn(__fsub_rn(__fmul_rn(px, ca), __fmul_rn(py, sa)), kRndBias));
         cbs[k] = (int)cb;
         // (__umul24 reads the low 24 bits of cb: 0x400000 + c, c in [-18, 18])
-        const uint32_t off = __umul24(cb, 2 * kColS) + ((rb << 1) + kOff);
-        const u32x4a v = *reinterpret_cast<const u32x4a *>(lbase + (off & ~3u));
+        uint32_t t, off;
+        asm("v_lshl_add_u32 %0, %1, 1, %2" : "=v"(t) : "v"(rb), "s"(kOffL));
+        asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(off) : "v"(cb), "s"(2u * kColS), "v"(t));
+        const u32x4a v = *reinterpret_cast<lds_u32x4a *>((uintptr_t)(off & ~3u));
         // odd row (the low bit of rb): shift 16; v_alignbit reads its shift's low 5 bits
         const uint32_t sh = rb << 4;
         // k0 R0 + k1 R1 + k2 R2 + k3 R3 + k2 R4 + k1 R5 + k0 R6 as four u16-pair dot products
@@ -1564,6 +1677,14 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
             false);
     }
     PHASE_MARK(1, 3);   // sincos + sample offsets + column pass
+    if constexpr (kStopDesc == 4) {   // keep the column pass: its sums reach LDS
+        int acc = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc ^= sums[k] + cbs[k];
+        if (acc == 0x7FFFFFFF) lbase[0] = 1;
+        write_record();
+        return;
+    }
     int val[8];
     if (all_even) {
 #pragma unroll
@@ -1583,7 +1704,6 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
             val[k] = min(qv, 255);
         }
     }
-    const int64_t kp_index = (int64_t)b * p.max_kps + off + i;
     uint64_t m[4];
 #pragma unroll
     for (int grp = 0; grp < 4; ++grp) m[grp] = __ballot(val[2 * grp] < val[2 * grp + 1]);
@@ -1592,19 +1712,7 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
         dout[0] = make_ulonglong2(m[0], m[1]);
         dout[1] = make_ulonglong2(m[2], m[3]);
     }
-    if (lane == 0) {
-        orbx_keypoint kp;
-        float fx = (float)x, fy = (float)y;
-        if (l != 0) { fx = __fmul_rn(fx, g.scale); fy = __fmul_rn(fy, g.scale); }
-        kp.x = fx;
-        kp.y = fy;
-        kp.size = g.patch_size;
-        kp.angle = angle;
-        kp.response = (float)score;
-        kp.octave = l;
-        kp.class_id = -1;
-        fb.kps[kp_index] = kp;
-    }
+    write_record();
     PHASE_MARK(1, 4);   // rounding + ballots + records
 }
 

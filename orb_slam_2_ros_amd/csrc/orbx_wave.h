@@ -50,6 +50,29 @@ __device__ inline int wave_incl_scan_i32(int v) {
     return v;
 }
 
+// The same scan into a new register, leaving v as it was (no copy when the
+// caller still needs the lane's own count).
+__device__ inline int wave_incl_scan_i32_to(int v) {
+    int r;
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_add_u32_dpp %0, %1, %1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "s_nop 1\n\t"
+        "v_add_u32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "s_nop 1\n\t"
+        "v_add_u32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "s_nop 1\n\t"
+        "v_add_u32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "s_nop 1\n\t"
+        "v_add_u32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_add_u32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+        "s_nop 1"
+        : "=&v"(r)
+        : "v"(v));
+    return r;
+}
+
 // Inclusive prefix sum of packed pairs of 32-bit counters (the halves are
 // scanned independently: callers pack counts that never carry into bit 32).
 __device__ inline uint64_t wave_incl_scan_u64(uint64_t v) {

@@ -156,6 +156,8 @@ def _run_streams(torch, mode, w, h, nf, streams, steps):
     for t in range(steps):
         if mode == "mono":
             ex.mono_step_device(fr[t].data_ptr(), w * h, w, n, 100, 0.9, True)
+        elif mode == "rgbd":
+            ex.rgbd_step_device(fr[t].data_ptr(), w * h, w, n, dm.data_ptr(), 4 * w * h, 4 * w, BF)
         else:
             ex.stereo_step_device(fr[t].data_ptr(), w * h, w, n, BF, MB)
     torch.cuda.synchronize()
@@ -165,6 +167,10 @@ def _run_streams(torch, mode, w, h, nf, streams, steps):
             k, d = ex.batch_download(b)
             m, nm = ex.mono_matches_download(b)
             out[s] = (k.tobytes(), d.tobytes(), m.tobytes(), nm)
+        elif mode == "rgbd":
+            k, d = ex.batch_download(b)
+            ur, dp, kept = ex.depth_download(b)
+            out[s] = (k.tobytes(), d.tobytes(), ur.tobytes(), dp.tobytes(), kept)
         else:
             k, d = ex.batch_download(2 * b)
             ur, dp, kept = ex.depth_download(b)
@@ -175,18 +181,51 @@ def _run_streams(torch, mode, w, h, nf, streams, steps):
 
 @pytest.mark.parametrize("mode,w,h,nf,total,world", [("mono", 640, 480, 1000, 16, 2),
                                                       ("mono", 640, 480, 1000, 16, 4),
-                                                      ("stereo", 752, 480, 1200, 8, 2)])
+                                                      ("stereo", 752, 480, 1200, 8, 2),
+                                                      ("rgbd", 1920, 1080, 1000, 64, 8)])
 def test_sharding_changes_no_stream(mode, w, h, nf, total, world):
     """per-frame outputs at G ranks are byte-identical to
     G = 1.  Each rank's share (stream s -> rank s mod G, bench.stream_partition)
-    runs as its own batch, as bench.py's ranks run it; streams are distinct
-    scenes."""
+    runs as its own batch, as bench.py's ranks run it.  The RGB-D case is C5's
+    64 FHD streams as 1 x 64 against 8 x 8 (streams past the 32 scenes repeat
+    them)."""
     import torch
-    assert total <= bench.UNIQUE_SCENES
     whole = _run_streams(torch, mode, w, h, nf, list(range(total)), 3)
     for r in range(world):
         part = bench.stream_partition(total, world, r)
         got = _run_streams(torch, mode, w, h, nf, part, 3)
         for s in part:
             assert got[s] == whole[s], f"stream {s} differs on rank {r} of {world}"
-    assert len({v[0] for v in whole.values()}) == total       # the streams really are distinct
+    # the streams really are distinct (up to the scene count)
+    assert len({v[0] for v in whole.values()}) == min(total, bench.UNIQUE_SCENES)
+
+
+def test_pack_device_equals_download():
+    """orbx_batch_pack_device (the keyframe exchange's send buffer, config C5)
+    holds exactly what orbx_batch_download returns for every stream: counts,
+    then keypoint records and descriptors at kp_stride per stream."""
+    import torch
+    w, h, B = 1920, 1080, 8
+    host, depth, fr, dm = _frames(torch, "rgbd", w, h, list(range(B)))
+    ex = ORBextractor(1000, 1.2, 8, 20, 7)
+    ex.reserve(w, h, B)
+    ex.rgbd_step_device(fr[0].data_ptr(), w * h, w, B, dm.data_ptr(), 4 * w * h, 4 * w, BF)
+    nbytes = ex.pack_bytes()
+    buf = torch.full((nbytes + 256,), 0xAB, dtype=torch.uint8, device="cuda:0")
+    assert ex.pack_device(buf.data_ptr(), nbytes) == nbytes
+    torch.cuda.synchronize()
+    raw = buf.cpu().numpy()
+    assert (raw[nbytes:] == 0xAB).all()                 # nothing past the reported size
+    K = ex.kp_stride()
+    from orb_slam_2_ros_amd._lib import KEYPOINT_DTYPE
+    coff = ((4 * B + 63) // 64) * 64
+    counts = raw[:4 * B].view(np.int32)
+    kps = raw[coff:coff + B * K * KEYPOINT_DTYPE.itemsize].view(KEYPOINT_DTYPE).reshape(B, K)
+    desc = raw[coff + B * K * KEYPOINT_DTYPE.itemsize:nbytes].reshape(B, K, 32)
+    assert nbytes == coff + B * K * (KEYPOINT_DTYPE.itemsize + 32)
+    for b in range(B):
+        k, d = ex.batch_download(b)
+        assert counts[b] == len(k) > 0, f"stream {b}"
+        assert kps[b, :len(k)].tobytes() == k.tobytes(), f"stream {b} keypoints"
+        assert np.array_equal(desc[b, :len(k)], d), f"stream {b} descriptors"
+    ex.close()
