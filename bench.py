@@ -926,7 +926,7 @@ def main() -> int:
             res = dropin_latency(torch, dev)
         if args.extra in ("c5_rank8", "c5_rank8_k8"):   # one rank's share of C5 at 8 GPUs
             res = c5_config(torch, dist, rank, world, dev, args.steps, args.warmup, profile, *c5_args, total=8,
-                            kframes=8 if args.extra.endswith("k8") else 1, exchange=False)
+                            kframes=8 if args.extra == "c5_rank8_k8" else 1, exchange=False)
         for key, mode, ew, eh, enf, eb, unit in EXTRAS:
             if key == args.extra:
                 streams = stream_partition(eb * world, world, rank)
