@@ -693,20 +693,21 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
     // so its interior mask is fixed.
     const int qc0 = (o + 3) & ~3;                           // patch column of the first quad
     const int nq = ((o + 2 + cw) >> 2) - (qc0 >> 2) + 1;   // quads per row
-    // a lane takes two adjacent quads (8 pixels) of one row: the loads, the
-    // loop and the compaction scan are shared by twice the pixels
-    const int np = (nq + 1) >> 1;                           // quad pairs per row
+    // a lane takes kFQ adjacent quads (4 kFQ pixels) of one row: the loads,
+    // the loop and the compaction scan are shared by that many pixels
+    constexpr int kFQ = 2, kFP = 4 * kFQ;   // (3: 706 VALU per wave against 698, same time)
+    const int np = kFQ == 2 ? (nq + 1) >> 1 : div_small(nq + kFQ - 1, kFQ);   // quad groups per row
     const int R = __builtin_amdgcn_readfirstlane(div_small(64, np));
     const int rl = div_small(lane, np), pi = lane - mul24u(rl, np);
-    const int xx0 = qc0 - o - 3 + 8 * pi;   // interior x of the pair's byte 0
-    // candidate byte: bit j = pixel j of the pair; the interior pixels
-    // [lo, hi) of the pair as one bit field
-    const int vlo = min(max(-xx0, 0), 8), vhi = min(max(cw - xx0, 0), 8);
-    uint32_t vmask = __builtin_amdgcn_ubfe(0xFFu << vlo, 0, (uint32_t)vhi);   // bits [lo, hi)
+    const int xx0 = qc0 - o - 3 + kFP * pi;   // interior x of the group's byte 0
+    // candidate bits: bit j = pixel j of the group; the interior pixels
+    // [lo, hi) of the group as one bit field
+    const int vlo = min(max(-xx0, 0), kFP), vhi = min(max(cw - xx0, 0), kFP);
+    uint32_t vmask = __builtin_amdgcn_ubfe(((1u << kFP) - 1u) << vlo, 0, (uint32_t)vhi);   // bits [lo, hi)
     if (rl >= R) vmask = 0;   // (tail lanes: rows of the next pass)
-    // the lane's pair in LDS, 3 rows up (every load a non-negative offset from
-    // it; 32-bit address arithmetic), and its row limit
-    const lds_u8 *qb0 = (const lds_u8 *)(patch + mul24u(rl, PS) + qc0 + 8 * pi);
+    // the lane's group in LDS, 3 rows up (every load a non-negative offset
+    // from it; 32-bit address arithmetic), and its row limit
+    const lds_u8 *qb0 = (const lds_u8 *)(patch + mul24u(rl, PS) + qc0 + kFP * pi);
     const int rlim = mul24u(max(ch - rl, 0), PS);   // (row offsets in bytes: the loop runs on scalars)
 
     // One FAST pass at threshold th: returns the keypoints kept after NMS,
@@ -738,16 +739,16 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
                 uint32_t cand = 0;
                 if (yo < rlim) {
                     const lds_u8 *qb = qb0 + yo;
-                    // the pair's dwords c0 c1, their row neighbours l r and the
-                    // rows 3 up / down
-                    const uint32_t l = *reinterpret_cast<lds_u32c *>(qb + 3 * PS - 4);
-                    const uint32_t c0 = *reinterpret_cast<lds_u32c *>(qb + 3 * PS);
-                    const uint32_t c1 = *reinterpret_cast<lds_u32c *>(qb + 3 * PS + 4);
-                    const uint32_t r = *reinterpret_cast<lds_u32c *>(qb + 3 * PS + 8);
-                    const uint32_t up0 = *reinterpret_cast<lds_u32c *>(qb);
-                    const uint32_t up1 = *reinterpret_cast<lds_u32c *>(qb + 4);
-                    const uint32_t dn0 = *reinterpret_cast<lds_u32c *>(qb + 6 * PS);
-                    const uint32_t dn1 = *reinterpret_cast<lds_u32c *>(qb + 6 * PS + 4);
+                    // the group's dwords c[0..kFQ), their row neighbours c[-1] and
+                    // c[kFQ], and the rows 3 up / down
+                    uint32_t c[kFQ + 2], up[kFQ], dn[kFQ];
+#pragma unroll
+                    for (int k = 0; k < kFQ + 2; ++k) c[k] = *reinterpret_cast<lds_u32c *>(qb + 3 * PS - 4 + 4 * k);
+#pragma unroll
+                    for (int k = 0; k < kFQ; ++k) {
+                        up[k] = *reinterpret_cast<lds_u32c *>(qb + 4 * k);
+                        dn[k] = *reinterpret_cast<lds_u32c *>(qb + 6 * PS + 4 * k);
+                    }
                     // one quad: pixel pairs (0, 2) and (1, 3) as u16 halves, straight
                     // from the aligned dwords (v_perm picks the +-3 column bytes of
                     // (lo, hi) dword pairs); even pixels: bytes 0 / 2 as the low bytes
@@ -780,13 +781,15 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
                         return __builtin_bit_cast(uint32_t, half(0x00FF00FFu, 0x0c050c03u, 0x0c030c01u, thv)) |
                                (__builtin_bit_cast(uint32_t, half(0xFF00FF00u, 0x060c040cu, 0x040c020cu, thv8)) << 1);
                     };
-                    const uint32_t q0b = quad(c0, l, c1, up0, dn0), q1b = quad(c1, c0, r, up1, dn1);
-                    // folded to bits 0..3 and 4..7
-                    const uint32_t b8 = q0b | (q1b << 4);
-                    cand = (b8 | (b8 >> 14)) & vmask;
+                    // quad k's pixels 0 / 2 at bits 4k / 4k + 16, 1 / 3 at 4k + 1 / 4k + 17,
+                    // folded to bits 4k .. 4k + 3
+                    uint32_t bits = 0;
+#pragma unroll
+                    for (int k = 0; k < kFQ; ++k) bits |= quad(c[k + 1], c[k], c[k + 2], up[k], dn[k]) << (4 * k);
+                    cand = (bits | (bits >> 14)) & vmask;
                 }
                 // compaction in row-major order: an inclusive DPP scan of the
-                // lanes' counts (0..8) places each lane's run, then its bits
+                // lanes' counts (0..4 kFQ) places each lane's run, then its bits
                 const int cnt = __builtin_popcount(cand);
                 const int incl = wave_incl_scan_i32_to(cnt);
                 const int total = __builtin_amdgcn_readlane(incl, 63);
