@@ -46,6 +46,8 @@ struct DevPlan {
     int node_cap;             // quadtree node capacity (max over levels)
     int node_lds_bytes;       // dynamic LDS of the quadtree kernel
     int dbg_stop;             // diagnostics only (ORBX_DBG_STOP): end k_quadtree after phase n (0 = off)
+    const int4 *pyr_rgn;      // Plan::rgn (k_pyramid_rgn)
+    int pyr_rgn_half;
 };
 
 // Per-batch device buffers.  Frame b of a batch uses the b-th slice of each.
@@ -102,6 +104,7 @@ struct StereoBufs {
     int nr_cap;               // right keypoints indexed per pair (LDS capacity)
     float mbf, maxd;          // maxD = mbf / mb (Frame.cc:532-534)
     float *ur, *depth; int32_t *sad; int64_t ostride; int32_t *nkept;
+    float *hout; int64_t hcap;   // optional host-visible copy of one pair's results (k_stereo_cut)
 };
 
 // Projection searches (ORBmatcher SearchByProjection x4, Fuse x2): one frame
@@ -191,5 +194,7 @@ int quadtree_lds_bytes(int node_cap);
 constexpr int kQuadRegKeys = 8 * 256;   // keys k_quadtree keeps in registers (8 per thread)
 bool resize_window_fits(const Plan &hp);
 bool plan_resize_waves(Plan &hp);   // fills hp.rw, or leaves it empty (block kernel)
+bool plan_pyr_regions(Plan &hp);   // fills hp.rgn, or leaves rgn_n = 0
+bool use_pyr_regions(const Plan &hp, int B);
 
 }  // namespace orbx

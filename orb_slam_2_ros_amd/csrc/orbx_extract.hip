@@ -552,6 +552,84 @@ __global__ __launch_bounds__(kThreads) void k_resize_w(DevPlan p, FrameBufs fb, 
 }
 
 // ===========================================================================
+// K1 (regions): the whole pyramid of a frame in one launch for small batches.
+// Block (region r, frame b) computes levels 1.. of its region with the level
+// before each held in LDS: the level-l rectangle R_l it computes is its owned
+// rectangle O_l plus what R_{l+1} reads (host plan, plan_pyr_regions), so the
+// regions recompute their halos instead of waiting for each other, and only
+// O_l is written to the pyramid.  Every pixel is the same fixed-point
+// function of the same source pixels as in k_resize (identical output); the
+// chain of 7 dependent launches becomes one.
+// ===========================================================================
+constexpr int kRgnThreads = 1024;
+constexpr int kRgnCols = 4;   // computed rectangles are at most 64 * kRgnCols wide (plan_pyr_regions)
+
+__global__ __launch_bounds__(kRgnThreads) void k_pyramid_rgn(DevPlan p, FrameBufs fb) {
+    extern __shared__ __align__(16) uint8_t lds[];
+    const int r = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    constexpr int kWaves = kRgnThreads / 64;
+    const int4 *T = p.pyr_rgn + (int64_t)r * 2 * kMaxLevels;   // [l] = R_l, [kMaxLevels + l] = O_l
+    uint8_t *cur = lds, *nxt = lds + p.pyr_rgn_half;
+    // R_0 from level 0, dword-aligned rows (level 0's base and pitch are dword multiples)
+    int4 R = T[0];
+    int ox = R.x & ~3, oy = R.y;
+    int stride;
+    {
+        int sp;
+        const uint8_t *src = level_ptr(p, fb, 0, b, sp);
+        const int ndw = ((R.z - ox) >> 2) + 1, nrows = R.w - R.y + 1;
+        stride = 4 * ndw + 4;
+        for (int row = wave; row < nrows; row += kWaves) {
+            const uint32_t *s32 = reinterpret_cast<const uint32_t *>(src + (int64_t)(oy + row) * sp + ox);
+            uint32_t *d32 = reinterpret_cast<uint32_t *>(cur + row * stride);
+            for (int d = lane; d < ndw; d += 64) d32[d] = s32[d];
+        }
+    }
+    __syncthreads();
+    for (int l = 1; l < p.nlevels; ++l) {
+        const int4 Rl = T[l], Ol = T[kMaxLevels + l];
+        const LevelGeom g = p.lv[l];
+        const int gsh = p.la[l - 1].h;
+        const ResizeTap *xt = p.xtaps + g.xtab_off;
+        const ResizeTap *yt = p.ytaps + g.ytab_off;
+        const int w = Rl.z - Rl.x + 1, h = Rl.w - Rl.y + 1;
+        const int dstride = (w + 4 + 3) & ~3;
+        uint8_t *dst = fb.pyr + (int64_t)b * p.pyr_bytes + g.pyr_off;
+        // this lane's columns lane + 64 k (k < kRgnCols: the plan bounds the
+        // widths) and their taps, loaded once for all rows
+        ResizeTap tx[kRgnCols];
+#pragma unroll
+        for (int k = 0; k < kRgnCols; ++k) tx[k] = xt[Rl.x + min(lane + 64 * k, w - 1)];
+        for (int row = wave; row < h; row += kWaves) {
+            const int y = Rl.y + row;
+            const ResizeTap ty = yt[y];
+            const int s0 = min(max((int)ty.src, 0), gsh - 1) - oy, s1 = min(max((int)ty.src + 1, 0), gsh - 1) - oy;
+            const uint8_t *S0 = cur + s0 * stride - ox, *S1 = cur + s1 * stride - ox;
+            const int b0 = ty.a0, b1 = ty.a1;
+            const bool own_row = y >= Ol.y && y <= Ol.w;
+#pragma unroll
+            for (int k = 0; k < kRgnCols; ++k) {
+                const int col = lane + 64 * k;
+                if (col >= w) break;
+                const int x = Rl.x + col;
+                const int sx = tx[k].src;
+                const int h0 = mul24u(S0[sx], tx[k].a0) + mul24u(S0[sx + 1], tx[k].a1);
+                const int h1 = mul24u(S1[sx], tx[k].a0) + mul24u(S1[sx + 1], tx[k].a1);
+                const int v_simd = ((mul24u(h0 >> 4, b0) >> 16) + (mul24u(h1 >> 4, b1) >> 16) + 2) >> 2;
+                const int v_tail = (mul24u(h0, b0) + mul24u(h1, b1) + (1 << 21)) >> 22;
+                const uint8_t v = (uint8_t)min(max((tx[k].mode & 2) ? v_simd : v_tail, 0), 255);
+                nxt[row * dstride + col] = v;
+                if (own_row && x >= Ol.x && x <= Ol.z) dst[(int64_t)y * g.pitch + x] = v;
+            }
+        }
+        __syncthreads();
+        uint8_t *t = cur; cur = nxt; nxt = t;
+        stride = dstride; ox = Rl.x; oy = Rl.y;
+    }
+}
+
+// ===========================================================================
 // K2: Gaussian 7x7, sigma 2, BORDER_REFLECT_101 on each level (OpenCV 3.2
 // fixed-point separable filter).  The SSE2 column pass accumulates exactly in
 // float and rounds half-to-even; the scalar tail adds 2^15 and shifts: both are
@@ -1749,6 +1827,17 @@ hipError_t launch_resize_level(const DevPlan &p, const Plan &hp, const FrameBufs
 }
 
 hipError_t launch_resize(const DevPlan &p, const Plan &hp, const FrameBufs &fb, int B, hipStream_t st) {
+    if (use_pyr_regions(hp, B)) {
+        static bool lds_set = false;   // (one attribute per process; the size bound is the plan check's)
+        if (!lds_set) {
+            if (hipFuncSetAttribute(reinterpret_cast<const void *>(k_pyramid_rgn),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+                return hipErrorInvalidValue;
+            lds_set = true;
+        }
+        hipLaunchKernelGGL(k_pyramid_rgn, dim3(hp.rgn_n, B), dim3(kRgnThreads), 2 * hp.rgn_half, st, p, fb);
+        return hipGetLastError();
+    }
     for (int l = 1; l < hp.nlevels; ++l)
         if (launch_resize_level(p, hp, fb, B, st, l) != hipSuccess) return hipErrorLaunchFailure;
     return hipSuccess;
@@ -1860,6 +1949,78 @@ hipError_t launch_trig_check(const float *in, float *s, float *c, float *atan_ou
     if (total <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_trig, dim3((total + 255) / 256), dim3(256), 0, st, in, s, c, n, ay, ax, atan_out, m);
     return hipGetLastError();
+}
+
+// Region pyramid plan (k_pyramid_rgn): level 1 cut into ~96 x 96 owned
+// rectangles, every level cut at the same fractions; each region's computed
+// rectangles grow from the coarsest level down by what the next level reads.
+// False (rgn_n = 0) when a region's level buffers exceed the LDS.
+bool plan_pyr_regions(Plan &hp) {
+    hp.rgn.clear();
+    hp.rgn_n = 0;
+    hp.rgn_half = 0;
+    const int n = hp.nlevels;
+    if (n < 2 || n > kMaxLevels) return false;
+    const int gx = std::max(1, (hp.lv[1].w + 95) / 96), gy = std::max(1, (hp.lv[1].h + 95) / 96);
+    // the source rectangle of level-l output rectangle q (as k_resize reads it)
+    auto src_of = [&](int l, const RgnRect &q) {
+        const LevelGeom &g = hp.lv[l], &gs = hp.lv[l - 1];
+        const ResizeTap *xt = hp.xtaps.data() + g.xtab_off;
+        const ResizeTap *yt = hp.ytaps.data() + g.ytab_off;
+        RgnRect s{INT_MAX, INT_MAX, -1, -1};
+        for (int x = q.x0; x <= q.x1; ++x) {
+            s.x0 = std::min(s.x0, (int)xt[x].src);
+            s.x1 = std::max(s.x1, std::min((int)xt[x].src + 1, gs.w - 1));
+        }
+        for (int y = q.y0; y <= q.y1; ++y) {
+            s.y0 = std::min(s.y0, std::min(std::max((int)yt[y].src, 0), gs.h - 1));
+            s.y1 = std::max(s.y1, std::min(std::max((int)yt[y].src + 1, 0), gs.h - 1));
+        }
+        return s;
+    };
+    auto unite = [](const RgnRect &a, const RgnRect &b) {
+        return RgnRect{std::min(a.x0, b.x0), std::min(a.y0, b.y0), std::max(a.x1, b.x1), std::max(a.y1, b.y1)};
+    };
+    std::vector<RgnRect> out((size_t)gx * gy * 2 * kMaxLevels, RgnRect{0, 0, -1, -1});
+    size_t half = 0;
+    for (int ry = 0; ry < gy; ++ry)
+        for (int rx = 0; rx < gx; ++rx) {
+            RgnRect *T = out.data() + ((size_t)ry * gx + rx) * 2 * kMaxLevels;
+            for (int l = 1; l < n; ++l) {
+                const LevelGeom &g = hp.lv[l];
+                T[kMaxLevels + l] = RgnRect{(int)((int64_t)rx * g.w / gx), (int)((int64_t)ry * g.h / gy),
+                                            (int)((int64_t)(rx + 1) * g.w / gx) - 1,
+                                            (int)((int64_t)(ry + 1) * g.h / gy) - 1};
+                const RgnRect &o = T[kMaxLevels + l];
+                if (o.x1 < o.x0 || o.y1 < o.y0) return false;   // a level narrower than the cut
+            }
+            T[n - 1] = T[kMaxLevels + n - 1];
+            for (int l = n - 2; l >= 1; --l) T[l] = unite(T[kMaxLevels + l], src_of(l + 1, T[l + 1]));
+            T[0] = src_of(1, T[1]);
+            for (int l = 0; l < n; ++l) {
+                const RgnRect &q = T[l];
+                if (l > 0 && q.x1 - q.x0 + 1 > 64 * kRgnCols) return false;
+                const size_t stride = l == 0 ? 4 * (size_t)(((q.x1 - (q.x0 & ~3)) >> 2) + 1) + 4
+                                             : (size_t)((q.x1 - q.x0 + 1 + 4 + 3) & ~3);
+                half = std::max(half, stride * (q.y1 - q.y0 + 1));
+            }
+        }
+    half = (half + 15) & ~size_t(15);
+    if (2 * half > 160 * 1024) return false;
+    hp.rgn = std::move(out);
+    hp.rgn_n = gx * gy;
+    hp.rgn_half = (int)half;
+    return true;
+}
+
+// The region pyramid while one block per region and frame still leaves the
+// chip short of a block per CU (ORBX_PYR_RGN=0 turns it off).
+bool use_pyr_regions(const Plan &hp, int B) {
+    static const bool on = [] {
+        const char *e = std::getenv("ORBX_PYR_RGN");
+        return !(e && e[0] == '0');
+    }();
+    return on && hp.rgn_n > 0 && (int64_t)B * hp.rgn_n <= 256;
 }
 
 // Wave-tile geometry of every level (ResizeWave).  False when some level does

@@ -93,6 +93,11 @@ struct ResizeWave {
     int xtab_off = 0, ytab_off = 0;   // the level's tap tables
 };
 
+// A pixel rectangle, inclusive bounds (an int4 on the device).
+struct RgnRect {
+    int x0, y0, x1, y1;
+};
+
 struct Plan {
     int width = 0, height = 0;
     int nfeatures = 0, nlevels = 0, ini_th = 0, min_th = 0;
@@ -109,6 +114,12 @@ struct Plan {
     int max_kps = 0;          // keypoint capacity per frame
     int max_quota = 0;
     std::vector<ResizeWave> rw;   // per level (index 0 unused); empty: k_resize_lds path
+    // Region pyramid (k_pyramid_rgn, small batches): per region 2 x kMaxLevels
+    // rectangles, [l] = the level-l pixels it computes (level 0: reads),
+    // [kMaxLevels + l] = the ones it owns and writes.  rgn_n = 0: not used.
+    std::vector<RgnRect> rgn;
+    int rgn_n = 0;
+    int rgn_half = 0;   // LDS bytes of one of the kernel's two level buffers
 };
 
 inline int pitch_of(int w) { return (w + 63) & ~63; }

@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <atomic>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -101,6 +102,7 @@ struct orbx_extractor {
     int graph_w = 0, graph_h = 0;
     uint8_t *h_img = nullptr, *h_out = nullptr;   // pinned
     size_t h_img_bytes = 0, h_out_bytes = 0;
+    uint32_t *d_pack_ctr = nullptr;   // k_pack_host's block count (the last block raises the done flag)
     bool host_result_valid = false;   // slot 0 still holds what h_out holds (no extraction since)
 
     // orbx_compute_stereo_matches workspace (this extractor as the left one),
@@ -190,7 +192,7 @@ struct orbx_extractor {
         dfree(d_tables); dfree(d_pyr); dfree(d_blur); dfree(d_cand); dfree(d_cand2); dfree(d_keys); dfree(d_sel);
         dfree(d_cell_count); dfree(d_level_count); dfree(d_key_node); dfree(d_key_q);
         for (auto &s : slot) { dfree(s.kps); dfree(s.desc); dfree(s.nkps); s.batch = 0; }
-        dfree(d_prev); dfree(d_m12); dfree(d_nmatch); dfree(d_img);
+        dfree(d_prev); dfree(d_m12); dfree(d_nmatch); dfree(d_img); dfree(d_pack_ctr);
         dfree(d_ur); dfree(d_depth); dfree(d_sad); dfree(d_nkept);
         depth_mode = 0;
         depth_count = 0;
@@ -230,8 +232,9 @@ int upload_plan(orbx_extractor *ex) {
         slot_level[s] = (uint32_t)l;
     }
     const size_t b_sl = sizeof(uint32_t) * slot_level.size();
+    const size_t b_rgn = sizeof(RgnRect) * p.rgn.size();
     auto al = [](size_t v) { return (v + 255) & ~size_t(255); };
-    const size_t total = al(b_lv) + al(b_cells) + al(b_xt) + al(b_yt) + al(b_tiles) + al(b_sl) + 256;
+    const size_t total = al(b_lv) + al(b_cells) + al(b_xt) + al(b_yt) + al(b_tiles) + al(b_sl) + al(b_rgn) + 256;
     std::vector<uint8_t> host(total, 0);
     size_t o = 0;
     const size_t o_lv = o; std::memcpy(&host[o], p.lv.data(), b_lv); o += al(b_lv);
@@ -240,6 +243,7 @@ int upload_plan(orbx_extractor *ex) {
     const size_t o_yt = o; if (b_yt) std::memcpy(&host[o], p.ytaps.data(), b_yt); o += al(b_yt);
     const size_t o_tiles = o; if (b_tiles) std::memcpy(&host[o], tiles.data(), b_tiles); o += al(b_tiles);
     const size_t o_sl = o; std::memcpy(&host[o], slot_level.data(), b_sl); o += al(b_sl);
+    const size_t o_rgn = o; if (b_rgn) std::memcpy(&host[o], p.rgn.data(), b_rgn); o += al(b_rgn);
     if (dalloc(&ex->d_tables, total) != hipSuccess) return ORBX_ENOMEM;
     if (hipMemcpy(ex->d_tables, host.data(), total, hipMemcpyHostToDevice) != hipSuccess) return ORBX_EIO;
     DevPlan &d = ex->dp;
@@ -249,6 +253,8 @@ int upload_plan(orbx_extractor *ex) {
     d.ytaps = reinterpret_cast<const ResizeTap *>(ex->d_tables + o_yt);
     d.blur_tiles = reinterpret_cast<const int4 *>(ex->d_tables + o_tiles);
     d.slot_level = reinterpret_cast<const uint32_t *>(ex->d_tables + o_sl);
+    d.pyr_rgn = reinterpret_cast<const int4 *>(ex->d_tables + o_rgn);
+    d.pyr_rgn_half = p.rgn_half;
     d.nlevels = p.nlevels;
     for (int l = 0; l < kMaxLevels; ++l) {
         LevelArgs &a = d.la[l];
@@ -308,6 +314,7 @@ int reserve(orbx_extractor *ex, int w, int h, int max_batch) {
     }
     if (!resize_window_fits(ex->plan)) return ORBX_EINVAL;
     if (!plan_resize_waves(ex->plan) || std::getenv("ORBX_RESIZE_BLOCKS")) ex->plan.rw.clear();
+    (void)plan_pyr_regions(ex->plan);
     int rc = upload_plan(ex);
     if (rc) return rc;
     const Plan &p = ex->plan;
@@ -814,10 +821,15 @@ constexpr size_t kOutKps = 128;
 
 // Frame 0's results written straight into the pinned (device-visible) host
 // buffer: one small kernel instead of four blit copies (~5 us each at B = 1).
-// Dwords: [0] count, [4..20) level counts, then the first `count` keypoint
-// records and descriptors (the host reads no further).
+// Dwords: [0] count, [2] done flag, [4..20) level counts, then the first
+// `count` keypoint records and descriptors (the host reads no further).  The
+// last block to finish raises the flag after every block's writes are
+// visible system-wide, so the host can poll it instead of sleeping in a
+// stream synchronisation (~10 us of wake-up at B = 1).
+constexpr int kOutFlag = 2;
 __global__ __launch_bounds__(256) void k_pack_host(const int32_t *nkps, const int32_t *lc, const uint32_t *kps,
-                                                   const uint32_t *desc, int nlevels, int kdesc_dw, uint32_t *out) {
+                                                   const uint32_t *desc, int nlevels, int kdesc_dw, uint32_t *out,
+                                                   uint32_t *ctr) {
     const int n = max(nkps[0], 0);
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t == 0) out[0] = (uint32_t)nkps[0];
@@ -825,6 +837,13 @@ __global__ __launch_bounds__(256) void k_pack_host(const int32_t *nkps, const in
     const int nk = n * (int)(sizeof(orbx_keypoint) / 4), nd = n * 8;
     for (int i = t; i < nk; i += gridDim.x * blockDim.x) out[kOutKps / 4 + i] = kps[i];
     for (int i = t; i < nd; i += gridDim.x * blockDim.x) out[kdesc_dw + i] = desc[i];
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0 && atomicAdd(ctr, 1u) == gridDim.x - 1) {
+        *ctr = 0;   // (for the next replay; every block has counted)
+        __threadfence_system();
+        __hip_atomic_store(out + kOutFlag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 size_t out_desc_off(const orbx_extractor *ex) {
     return kOutKps + sizeof(orbx_keypoint) * (size_t)ex->plan.max_kps;
@@ -861,14 +880,22 @@ int build_host_graph(orbx_extractor *ex, int width, int height) {
             return ORBX_ENOMEM;
         ex->h_out_bytes = out_bytes;
     }
+    if (!ex->d_pack_ctr) {
+        if (dalloc(&ex->d_pack_ctr, 1) != hipSuccess) return ORBX_ENOMEM;
+        if (hipMemset(ex->d_pack_ctr, 0, sizeof(uint32_t)) != hipSuccess) return ORBX_EIO;
+    }
     hipStream_t st = ex->stream;
     const int pipe = ex->pipeline;
     hipEvent_t *ev = ex->cur_ev;
     bool *valid = ex->cur_valid;
-    // level 0's FAST / quadtree / describe on a forked branch beside the
-    // resize chain (the level pipeline): at B = 1 the chain's launches are
-    // latency-bound, so the branches overlap
-    ex->pipeline = make_pipe(ex) ? 1 : 0;
+    // one linear chain: a graph with the level pipeline's forked branch
+    // (ORBX_HOST_PIPE=1) replays its cross-queue joins at ~10-20 us each and
+    // measured slower at B = 1 (VGA 0.159 vs 0.141 ms)
+    static const bool host_pipe = [] {
+        const char *e = std::getenv("ORBX_HOST_PIPE");
+        return e && e[0] == '1';
+    }();
+    ex->pipeline = host_pipe && make_pipe(ex) ? 1 : 0;
     ex->cur_ev = nullptr;
     ex->cur_valid = nullptr;
     auto restore = [&] { ex->pipeline = pipe; ex->cur_ev = ev; ex->cur_valid = valid; };
@@ -887,7 +914,7 @@ int build_host_graph(orbx_extractor *ex, int width, int height) {
         hipLaunchKernelGGL(k_pack_host, dim3(std::max(1, (K * 8 + 255) / 256)), dim3(256), 0, st, s0.nkps,
                            ex->d_level_count, reinterpret_cast<const uint32_t *>(s0.kps),
                            reinterpret_cast<const uint32_t *>(s0.desc), ex->nlevels, (int)(out_desc_off(ex) / 4),
-                           reinterpret_cast<uint32_t *>(dout));
+                           reinterpret_cast<uint32_t *>(dout), ex->d_pack_ctr);
         ok = hipGetLastError() == hipSuccess;
     }
     const bool ended = hipStreamEndCapture(st, &g) == hipSuccess;
@@ -930,8 +957,18 @@ int orbx_extract(orbx_extractor *ex, const uint8_t *image, int width, int height
             if (rc) return rc;
         }
         for (int r = 0; r < height; ++r) std::memcpy(ex->h_img + r * dp, image + r * pitch, (size_t)width);
-        if (hipGraphLaunch(ex->host_graph, ex->stream) != hipSuccess || hipStreamSynchronize(ex->stream) != hipSuccess)
-            return ORBX_EIO;
+        volatile uint32_t *flag = reinterpret_cast<volatile uint32_t *>(ex->h_out) + kOutFlag;
+        *flag = 0;
+        std::atomic_thread_fence(std::memory_order_seq_cst);
+        if (hipGraphLaunch(ex->host_graph, ex->stream) != hipSuccess) return ORBX_EIO;
+        // poll the pack kernel's flag; the stream's state ends the wait on an error
+        for (uint32_t i = 1; !*flag; ++i) {
+            if ((i & 255) == 0 && hipStreamQuery(ex->stream) != hipErrorNotReady) break;
+            __builtin_ia32_pause();
+        }
+        if (!*flag && hipStreamSynchronize(ex->stream) != hipSuccess) return ORBX_EIO;
+        if (!*flag) return ORBX_EIO;
+        std::atomic_thread_fence(std::memory_order_acquire);
         ex->cur = 0;
         ex->match_batch = 0;
         ex->host_result_valid = true;
@@ -1241,12 +1278,12 @@ int orbx_compute_stereo_matches(orbx_extractor *left, orbx_extractor *right, con
     }
     a.mbf = mbf; a.maxd = mbf / mb;
     a.ur = w.ur; a.depth = w.depth; a.sad = w.sad; a.ostride = 0; a.nkept = w.nk;
-    ok = ok && launch_stereo(a, 1, nl, st) == hipSuccess &&
-         hipMemcpyAsync(w.h_res, w.ur, 4 * (size_t)nl, hipMemcpyDeviceToHost, st) == hipSuccess &&
-         hipMemcpyAsync(w.h_res + 4 * (size_t)w.cap_l, w.depth, 4 * (size_t)nl, hipMemcpyDeviceToHost, st) ==
-             hipSuccess &&
-         hipMemcpyAsync(w.h_res + 8 * (size_t)w.cap_l, w.nk, sizeof(int32_t), hipMemcpyDeviceToHost, st) == hipSuccess &&
-         hipStreamSynchronize(st) == hipSuccess;
+    // k_stereo_cut writes the results straight into the pinned buffer
+    void *hdev = nullptr;
+    ok = ok && hipHostGetDevicePointer(&hdev, w.h_res, 0) == hipSuccess;
+    a.hout = static_cast<float *>(hdev);
+    a.hcap = w.cap_l;
+    ok = ok && launch_stereo(a, 1, nl, st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess;
     if (!ok) return ORBX_EIO;
     std::memcpy(uright, w.h_res, 4 * (size_t)nl);
     std::memcpy(depth, w.h_res + 4 * (size_t)w.cap_l, 4 * (size_t)nl);

@@ -6,7 +6,9 @@
 //   k_stereo_cut     the median cut of Frame.cc:662-675.
 //   k_rgbd_depth     Frame::ComputeStereoFromRGBD (Frame.cc:679-701).
 //
-// One block of k_stereo_band covers 256 left keypoints of one stereo pair.  It
+// One block of k_stereo_band covers 256 left keypoints of one stereo pair
+// (k_stereo_band_g: 16, a group of 16 lanes per keypoint, for launches too
+// small to fill the chip, e.g. the single pair of the host-array call).  It
 // first counting-sorts the pair's right keypoints by the first row of their
 // band (vRowIndices of Frame.cc:512-529 without the per-row copies) into LDS,
 // then every thread walks the bands that can contain its keypoint's row.  The
@@ -16,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include "orbx_device.h"
+#include "orbx_wave.h"
 
 namespace orbx {
 namespace {
@@ -102,32 +105,46 @@ __device__ inline void load_rows(const uint8_t *lrow, int c0, const uint8_t *rro
     }
 }
 
-__global__ __launch_bounds__(kST) void k_stereo_band(StereoBufs a) {
-    extern __shared__ __align__(16) uint8_t lds[];
-    __shared__ int ws[4];
-    __shared__ int s_span;
-    const int b = blockIdx.y, tid = threadIdx.x;
-    const int nl = a.nl[(int64_t)b * a.nstride];
-    const int i0 = blockIdx.x * kST;
-    if (i0 >= nl) return;
+// 11 pixels of a row from column c0, from dword-aligned loads.
+__device__ inline void load_row11(const uint8_t *row, int c0, int px[11]) {
+    const uint32_t o = (uint32_t)(reinterpret_cast<uintptr_t>(row + c0) & 3);
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(row + c0 - o);
+    uint32_t d[4], e[3];
+    d[0] = p[0]; d[1] = p[1]; d[2] = p[2];
+    d[3] = o >= 2 ? p[3] : 0u;   // byte o + 10 lies in dword 3 only then
+    realign<3>(d, o, e);
+#pragma unroll
+    for (int j = 0; j < 11; ++j) px[j] = byte_of(e, j);
+}
+
+// The pair's right keypoints counting-sorted by the first row of their band
+// (vRowIndices, Frame.cc:512-529) into LDS; returns the widest band - 1.
+struct Bands {
+    int *rend;        // H + 1 counters, then bucket ends
+    float *sx;        // right u, in band order
+    int16_t *smaxr;   // last row of the band
+    uint16_t *sidx;
+    int8_t *soct;
+};
+
+__device__ inline Bands bands_in(uint8_t *lds, const StereoBufs &a) {
+    Bands d;
+    d.rend = reinterpret_cast<int *>(lds);
+    d.sx = reinterpret_cast<float *>(d.rend + a.rows + 1);
+    d.smaxr = reinterpret_cast<int16_t *>(d.sx + a.nr_cap);
+    d.sidx = reinterpret_cast<uint16_t *>(d.smaxr + a.nr_cap);
+    d.soct = reinterpret_cast<int8_t *>(d.sidx + a.nr_cap);
+    return d;
+}
+
+__device__ int band_sort(const StereoBufs &a, int b, const Bands &d, int *ws, int *s_span) {
+    const int tid = threadIdx.x;
     const int nr = min(a.nr[(int64_t)b * a.nstride], a.nr_cap);
     const int H = a.rows;
-    const orbx_keypoint *kl = a.kl + (int64_t)b * a.kstride;
     const orbx_keypoint *kr = a.kr + (int64_t)b * a.kstride;
-    const uint8_t *dl = a.dl + (int64_t)b * a.kstride * 32;
-    const uint8_t *dr = a.dr + (int64_t)b * a.kstride * 32;
-
-    int *rend = reinterpret_cast<int *>(lds);                       // H + 1 counters / bucket ends
-    float *sx = reinterpret_cast<float *>(rend + H + 1);            // right u, by band order
-    int16_t *smaxr = reinterpret_cast<int16_t *>(sx + a.nr_cap);    // last row of the band
-    uint16_t *sidx = reinterpret_cast<uint16_t *>(smaxr + a.nr_cap);
-    int8_t *soct = reinterpret_cast<int8_t *>(sidx + a.nr_cap);
-
-    // 1. vRowIndices (Frame.cc:517-529): right keypoint iR lies in rows
-    //    [floor(y - r), ceil(y + r)], r = 2 * scale[octave].  Rows outside the
-    //    image (undefined behaviour in the reference) are dropped.
-    for (int i = tid; i <= H; i += kST) rend[i] = 0;
-    if (tid == 0) s_span = 0;
+    // Rows outside the image (undefined behaviour in the reference) are dropped.
+    for (int i = tid; i <= H; i += kST) d.rend[i] = 0;
+    if (tid == 0) *s_span = 0;
     __syncthreads();
     int span = 0;
     for (int iR = tid; iR < nr; iR += kST) {
@@ -137,12 +154,12 @@ __global__ __launch_bounds__(kST) void k_stereo_band(StereoBufs a) {
         const int maxr = (int)ceilf(__fadd_rn(k.y, r)), minr = (int)floorf(__fsub_rn(k.y, r));
         const int lo = max(minr, 0), hi = min(maxr, H - 1);
         if (lo > hi) continue;
-        atomicAdd(&rend[lo], 1);
+        atomicAdd(&d.rend[lo], 1);
         span = max(span, hi - lo);
     }
-    atomicMax(&s_span, span);
+    atomicMax(s_span, span);
     __syncthreads();
-    block_scan_lds(rend, H + 1, ws);
+    block_scan_lds(d.rend, H + 1, ws);
     for (int iR = tid; iR < nr; iR += kST) {
         const orbx_keypoint k = kr[iR];
         if (k.octave < 0 || k.octave >= a.nlevels) continue;
@@ -150,14 +167,38 @@ __global__ __launch_bounds__(kST) void k_stereo_band(StereoBufs a) {
         const int maxr = (int)ceilf(__fadd_rn(k.y, r)), minr = (int)floorf(__fsub_rn(k.y, r));
         const int lo = max(minr, 0), hi = min(maxr, H - 1);
         if (lo > hi) continue;
-        const int pos = atomicAdd(&rend[lo], 1);   // afterwards rend[m] = end of band m
-        sx[pos] = k.x;
-        smaxr[pos] = (int16_t)hi;
-        sidx[pos] = (uint16_t)iR;
-        soct[pos] = (int8_t)k.octave;
+        const int pos = atomicAdd(&d.rend[lo], 1);   // afterwards rend[m] = end of band m
+        d.sx[pos] = k.x;
+        d.smaxr[pos] = (int16_t)hi;
+        d.sidx[pos] = (uint16_t)iR;
+        d.soct[pos] = (int8_t)k.octave;
     }
     __syncthreads();
-    span = s_span;
+    return *s_span;
+}
+
+__global__ __launch_bounds__(kST) void k_stereo_band(StereoBufs a) {
+    extern __shared__ __align__(16) uint8_t lds[];
+    __shared__ int ws[4];
+    __shared__ int s_span;
+    const int b = blockIdx.y, tid = threadIdx.x;
+    const int nl = a.nl[(int64_t)b * a.nstride];
+    const int i0 = blockIdx.x * kST;
+    if (i0 >= nl) return;
+    const int H = a.rows;
+    const orbx_keypoint *kl = a.kl + (int64_t)b * a.kstride;
+    const orbx_keypoint *kr = a.kr + (int64_t)b * a.kstride;
+    const uint8_t *dl = a.dl + (int64_t)b * a.kstride * 32;
+    const uint8_t *dr = a.dr + (int64_t)b * a.kstride * 32;
+    // 1. vRowIndices (Frame.cc:517-529): right keypoint iR lies in rows
+    //    [floor(y - r), ceil(y + r)], r = 2 * scale[octave].
+    const Bands bd = bands_in(lds, a);
+    const int span = band_sort(a, b, bd, ws, &s_span);
+    const int *rend = bd.rend;
+    const float *sx = bd.sx;
+    const int16_t *smaxr = bd.smaxr;
+    const uint16_t *sidx = bd.sidx;
+    const int8_t *soct = bd.soct;
 
     const int iL = i0 + tid;
     if (iL >= nl) return;
@@ -254,76 +295,219 @@ __global__ __launch_bounds__(kST) void k_stereo_band(StereoBufs a) {
     }
 }
 
+// The same search with a group of kG lanes per left keypoint (kST / kG
+// keypoints per block): the lanes stride over the keypoint's band range and
+// reduce (distance, index) to its lexicographic minimum; lane i < 11 of the
+// group sums the SAD of offset i.  For launches of few pairs, where one lane
+// per keypoint leaves the chip idle and each lane's serial search is the
+// latency.
+constexpr int kG = 16;
+
+__device__ inline uint32_t group_min_u32(uint32_t v) {
+#pragma unroll
+    for (int o = kG / 2; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o));
+    return v;
+}
+
+__global__ __launch_bounds__(kST) void k_stereo_band_g(StereoBufs a) {
+    extern __shared__ __align__(16) uint8_t lds[];
+    __shared__ int ws[4];
+    __shared__ int s_span;
+    constexpr int kPer = kST / kG;
+    const int b = blockIdx.y, tid = threadIdx.x;
+    const int nl = a.nl[(int64_t)b * a.nstride];
+    const int i0 = blockIdx.x * kPer;
+    if (i0 >= nl) return;
+    const int H = a.rows;
+    const orbx_keypoint *kl = a.kl + (int64_t)b * a.kstride;
+    const orbx_keypoint *kr = a.kr + (int64_t)b * a.kstride;
+    const uint8_t *dl = a.dl + (int64_t)b * a.kstride * 32;
+    const uint8_t *dr = a.dr + (int64_t)b * a.kstride * 32;
+    const Bands bd = bands_in(lds, a);
+    const int span = band_sort(a, b, bd, ws, &s_span);
+
+    const int g = tid & (kG - 1);
+    const int iL = i0 + tid / kG;
+    if (iL >= nl) return;   // (whole groups leave together)
+    float *ur_out = a.ur + (int64_t)b * a.ostride;
+    float *dp_out = a.depth + (int64_t)b * a.ostride;
+    int32_t *sad_out = a.sad + (int64_t)b * a.ostride;
+    if (g == 0) {
+        ur_out[iL] = -1.0f;
+        dp_out[iL] = -1.0f;
+        sad_out[iL] = -1;
+    }
+    const orbx_keypoint kL = kl[iL];
+    const float vL = kL.y, uL = kL.x;
+    const int levelL = kL.octave;
+    if (!(vL >= 0.0f) || vL >= (float)H || levelL < 0 || levelL >= a.nlevels) return;
+    const int v = (int)vL;
+    const float minU = __fsub_rn(uL, a.maxd), maxU = uL;
+    if (maxU < 0.0f) return;
+
+    // 2. best Hamming distance over the band (Frame.cc:556-585): the bands
+    //    starting in rows [v - span, v] are one contiguous range of the sort
+    uint32_t q[8];
+    {
+        const uint4 q0 = *reinterpret_cast<const uint4 *>(dl + 32 * (int64_t)iL);
+        const uint4 q1 = *reinterpret_cast<const uint4 *>(dl + 32 * (int64_t)iL + 16);
+        q[0] = q0.x; q[1] = q0.y; q[2] = q0.z; q[3] = q0.w;
+        q[4] = q1.x; q[5] = q1.y; q[6] = q1.z; q[7] = q1.w;
+    }
+    const int m0 = max(0, v - span);
+    const int p0 = m0 ? bd.rend[m0 - 1] : 0, p1 = bd.rend[v];
+    uint32_t bk = 100u << 16;   // (distance << 16) | index; TH_HIGH, index 0
+    for (int pos = p0 + g; pos < p1; pos += kG) {
+        if (bd.smaxr[pos] < v) continue;
+        const int o = bd.soct[pos];
+        if (o < levelL - 1 || o > levelL + 1) continue;
+        const float uR = bd.sx[pos];
+        if (!(uR >= minU && uR <= maxU)) continue;
+        const int iR = bd.sidx[pos];
+        bk = min(bk, ((uint32_t)hamming(q, dr + 32 * (int64_t)iR) << 16) | (uint32_t)iR);
+    }
+    bk = group_min_u32(bk);
+    const int best = (int)(bk >> 16), bidx = (int)(bk & 0xFFFF);
+    if (best >= kThOrbDist) return;
+
+    // 3. SAD over 11 offsets (Frame.cc:587-629), offset g on lane g
+    const LevelGeom lg = a.lv[levelL];
+    const float sf = lg.inv_scale;
+    const float suL = roundf(__fmul_rn(uL, sf)), svL = roundf(__fmul_rn(vL, sf));
+    const float suR0 = roundf(__fmul_rn(kr[bidx].x, sf));
+    if (svL - kSadW < 0.0f || svL + kSadW + 1 > (float)lg.h || suL - kSadW < 0.0f || suL + kSadW + 1 > (float)lg.w)
+        return;
+    const float iniu = suR0 + kSadL - kSadW, endu = suR0 + kSadL + kSadW + 1;
+    if (iniu < 0.0f || endu >= (float)lg.w) return;
+    if (suR0 - kSadL - kSadW < 0.0f) return;
+    int lp, rp;
+    const uint8_t *IL = view_level(a.left, lg, levelL, a.left_f0 + b * a.fstep, lp);
+    const uint8_t *IR = view_level(a.right, lg, levelL, a.right_f0 + b * a.fstep, rp);
+    const int r0 = (int)svL - kSadW, cl0 = (int)suL - kSadW, cr0 = (int)suR0 - kSadL - kSadW;
+    // this lane's offset: the right window starts i columns further (lanes
+    // 11..15 repeat offset 10 and drop out of the minimum)
+    const int i = min(g, 2 * kSadL);
+    int l[11], r[11];
+    load_row11(IL + (int64_t)(r0 + kSadW) * lp, cl0, l);
+    load_row11(IR + (int64_t)(r0 + kSadW) * rp, cr0 + i, r);
+    const int kc = l[kSadW] - r[kSadW];   // IL(w,w) - IR(w,w) at this offset
+    int sad = 0;
+    for (int rr = 0; rr < 2 * kSadW + 1; ++rr) {
+        load_row11(IL + (int64_t)(r0 + rr) * lp, cl0, l);
+        load_row11(IR + (int64_t)(r0 + rr) * rp, cr0 + i, r);
+#pragma unroll
+        for (int c = 0; c < 11; ++c) sad += abs(l[c] - r[c] - kc);
+    }
+    // first strict minimum over the 11 offsets
+    const uint32_t sk = group_min_u32(g <= 2 * kSadL ? ((uint32_t)sad << 4) | (uint32_t)g : 0xFFFFFFFFu);
+    const int bestSad = (int)(sk >> 4), bestInc = (int)(sk & 15);
+    const int gb = tid & ~(kG - 1) & 63;   // the group's first lane in the wave
+    const int s1 = __shfl(sad, gb + max(bestInc - 1, 0)), s3 = __shfl(sad, gb + min(bestInc + 1, 2 * kSadL));
+    if (g != 0 || bestInc == 0 || bestInc == 2 * kSadL) return;
+    const float d1 = (float)s1, d2 = (float)bestSad, d3 = (float)s3;
+    // 4. parabola fit and depth (Frame.cc:631-657)
+    const float deltaR = __fdiv_rn(__fsub_rn(d1, d3), __fmul_rn(2.0f, __fsub_rn(__fadd_rn(d1, d3), __fmul_rn(2.0f, d2))));
+    if (deltaR < -1.0f || deltaR > 1.0f) return;
+    float bestuR = __fmul_rn(lg.scale, __fadd_rn(__fadd_rn(suR0, (float)(bestInc - kSadL)), deltaR));
+    float disparity = __fsub_rn(uL, bestuR);
+    if (disparity >= 0.0f && disparity < a.maxd) {
+        if (disparity <= 0.0f) {
+            disparity = 0.01f;
+            bestuR = (float)__dsub_rn((double)uL, 0.01);
+        }
+        dp_out[iL] = __fdiv_rn(a.mbf, disparity);
+        ur_out[iL] = bestuR;
+        sad_out[iL] = bestSad;
+    }
+}
+
 // Median cut (Frame.cc:662-675): entries with SAD >= 1.5f*1.4f*median are
 // dropped; the median is element size/2 of the ascending SAD order.  SADs are
-// < 2^16 (121 * 510), so the median is a two-pass 8-bit radix select.
+// < 2^16 (121 * 510), so the median is a two-pass 8-bit radix select; each
+// pass finds its bucket by a block scan of the 256-bin histogram (thread t
+// owns bin t).  With `hout` set (one pair, the host-array call) the block also
+// writes the results into that host-visible buffer: uRight at [0, nl), depth
+// at [hcap, hcap + nl), the kept count at 2 * hcap.
+__device__ inline int hist_select(const int *hist, int k, int *ws, int *s_sel, int *s_rank) {
+    const int tid = threadIdx.x;
+    const int h = hist[tid];
+    const int incl = wave_incl_scan_i32(h);
+    if ((tid & 63) == 63) ws[tid >> 6] = incl;
+    if (tid == 0) *s_sel = -1;
+    __syncthreads();
+    int base = 0;
+    for (int w = 0; w < (tid >> 6); ++w) base += ws[w];
+    const int ex = base + incl - h;   // bins before t
+    if (h > 0 && ex <= k && k < ex + h) { *s_sel = tid; *s_rank = k - ex; }
+    const int total = ws[0] + ws[1] + ws[2] + ws[3];
+    __syncthreads();
+    return total;
+}
+
 __global__ __launch_bounds__(kST) void k_stereo_cut(StereoBufs a) {
     __shared__ int hist[256];
+    __shared__ int ws[4];
     __shared__ int s_sel, s_rank, s_kept;
     const int b = blockIdx.x, tid = threadIdx.x;
     const int nl = a.nl[(int64_t)b * a.nstride];
     float *ur = a.ur + (int64_t)b * a.ostride;
     float *dp = a.depth + (int64_t)b * a.ostride;
     const int32_t *sad = a.sad + (int64_t)b * a.ostride;
-    int cnt = 0;
     hist[tid] = 0;
     __syncthreads();
     for (int i = tid; i < nl; i += kST) {
         const int s = sad[i];
-        if (s >= 0) { ++cnt; atomicAdd(&hist[s >> 8], 1); }
+        if (s >= 0) atomicAdd(&hist[s >> 8], 1);
     }
     __syncthreads();
-    if (tid == 0) {
-        int total = 0;
-        for (int i = 0; i < 256; ++i) total += hist[i];
-        const int k = total / 2;
-        int acc = 0, sel = -1;
-        for (int i = 0; i < 256 && sel < 0; ++i) {
-            if (acc + hist[i] > k) sel = i;
-            else acc += hist[i];
+    // (with nothing to cut, k = 0 finds no bin: the reference reads an empty vector)
+    int total = 0;
+    {
+        int probe = hist[tid];
+        probe = wave_sum_i32(probe);
+        if ((tid & 63) == 0) ws[tid >> 6] = probe;
+        __syncthreads();
+        total = ws[0] + ws[1] + ws[2] + ws[3];
+        __syncthreads();
+    }
+    int kept = total;
+    if (total > 0) {
+        (void)hist_select(hist, total / 2, ws, &s_sel, &s_rank);
+        const int hi = s_sel, rank = s_rank;
+        hist[tid] = 0;
+        __syncthreads();
+        for (int i = tid; i < nl; i += kST) {
+            const int s = sad[i];
+            if (s >= 0 && (s >> 8) == hi) atomicAdd(&hist[s & 0xFF], 1);
         }
-        s_sel = sel;
-        s_rank = k - acc;
-        s_kept = total;
-    }
-    __syncthreads();
-    if (s_sel < 0) {   // no depth at all: nothing to cut (the reference reads an empty vector)
-        if (tid == 0) a.nkept[b] = 0;
-        return;
-    }
-    const int hi = s_sel, rank = s_rank;
-    __syncthreads();
-    hist[tid] = 0;
-    __syncthreads();
-    for (int i = tid; i < nl; i += kST) {
-        const int s = sad[i];
-        if (s >= 0 && (s >> 8) == hi) atomicAdd(&hist[s & 0xFF], 1);
-    }
-    __syncthreads();
-    if (tid == 0) {
-        int acc = 0, sel = 0;
-        for (int i = 0; i < 256; ++i) {
-            if (acc + hist[i] > rank) { sel = i; break; }
-            acc += hist[i];
+        __syncthreads();
+        (void)hist_select(hist, rank, ws, &s_sel, &s_rank);
+        const int med = (hi << 8) | s_sel;
+        constexpr float kCut = 1.5f * 1.4f;   // folded in float, as the reference's constant product
+        const float thDist = __fmul_rn(kCut, (float)med);
+        if (tid == 0) s_kept = total;
+        __syncthreads();
+        int dropped = 0;
+        for (int i = tid; i < nl; i += kST) {
+            const int s = sad[i];
+            if (s >= 0 && !((float)s < thDist)) {
+                ur[i] = -1.0f;
+                dp[i] = -1.0f;
+                ++dropped;
+            }
         }
-        s_sel = (hi << 8) | sel;
+        if (dropped) atomicSub(&s_kept, dropped);
+        __syncthreads();
+        kept = s_kept;
     }
-    __syncthreads();
-    constexpr float kCut = 1.5f * 1.4f;   // folded in float, as the reference's constant product
-    const float thDist = __fmul_rn(kCut, (float)s_sel);
-    int dropped = 0;
-    for (int i = tid; i < nl; i += kST) {
-        const int s = sad[i];
-        if (s >= 0 && !((float)s < thDist)) {
-            ur[i] = -1.0f;
-            dp[i] = -1.0f;
-            ++dropped;
+    if (tid == 0) a.nkept[b] = kept;
+    if (a.hout) {
+        for (int i = tid; i < nl; i += kST) {   // (each thread rereads only its own entries)
+            a.hout[i] = ur[i];
+            a.hout[a.hcap + i] = dp[i];
         }
+        if (tid == 0) reinterpret_cast<int32_t *>(a.hout)[2 * a.hcap] = kept;
     }
-    (void)cnt;
-    if (dropped) atomicSub(&s_kept, dropped);
-    __syncthreads();
-    if (tid == 0) a.nkept[b] = s_kept;
 }
 
 // Frame::ComputeStereoFromRGBD (Frame.cc:679-701) for undistorted frames
@@ -364,11 +548,16 @@ int stereo_lds_bytes(int rows, int nr_cap) {
 hipError_t launch_stereo(const StereoBufs &a, int pairs, int nl_cap, hipStream_t st) {
     if (pairs <= 0) return hipSuccess;
     const int bytes = stereo_lds_bytes(a.rows, a.nr_cap);
-    if (bytes > 64 * 1024 &&
-        hipFuncSetAttribute(reinterpret_cast<const void *>(k_stereo_band), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            bytes) != hipSuccess)
+    // a lane per keypoint while that fills the chip, else a group of kG lanes
+    const bool grouped = (int64_t)pairs * ((nl_cap + kST - 1) / kST) < 256;
+    const void *fn = grouped ? reinterpret_cast<const void *>(k_stereo_band_g)
+                             : reinterpret_cast<const void *>(k_stereo_band);
+    if (bytes > 64 * 1024 && hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_stereo_band, dim3((nl_cap + kST - 1) / kST, pairs), dim3(kST), bytes, st, a);
+    if (grouped)
+        hipLaunchKernelGGL(k_stereo_band_g, dim3((nl_cap + kST / kG - 1) / (kST / kG), pairs), dim3(kST), bytes, st, a);
+    else
+        hipLaunchKernelGGL(k_stereo_band, dim3((nl_cap + kST - 1) / kST, pairs), dim3(kST), bytes, st, a);
     hipLaunchKernelGGL(k_stereo_cut, dim3(pairs), dim3(kST), 0, st, a);
     return hipGetLastError();
 }

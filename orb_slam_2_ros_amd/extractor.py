@@ -93,8 +93,8 @@ class ORBextractor:
         h, w = img.shape
         cap = self.nfeatures + 16 * self.nlevels + 64
         while True:
-            kps = np.zeros(cap, dtype=KEYPOINT_DTYPE)
-            desc = np.zeros((cap, 32), dtype=np.uint8)
+            kps = np.empty(cap, dtype=KEYPOINT_DTYPE)
+            desc = np.empty((cap, 32), dtype=np.uint8)
             n = ctypes.c_int(0)
             rc = self._lib.orbx_extract(self._h, ptr(img), w, h, img.strides[0], ptr(kps), ptr(desc), cap,
                                         ctypes.byref(n))
@@ -105,7 +105,7 @@ class ORBextractor:
             break
         self._last_shape = (h, w)
         nk = n.value
-        return kps[:nk].copy(), desc[:nk].copy()
+        return kps[:nk], desc[:nk]   # (views of this call's own arrays)
 
     @property
     def mvImagePyramid(self) -> list:
