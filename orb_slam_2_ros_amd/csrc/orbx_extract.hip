@@ -563,6 +563,14 @@ __global__ __launch_bounds__(kThreads) void k_resize_w(DevPlan p, FrameBufs fb, 
 // ===========================================================================
 constexpr int kRgnThreads = 1024;
 constexpr int kRgnCols = 4;   // computed rectangles are at most 64 * kRgnCols wide (plan_pyr_regions)
+constexpr int kRgnTapRows = 64 * kRgnCols;   // and at most this tall
+// LDS of the taps of levels 1.. (columns then rows of each)
+constexpr int rgn_tap_bytes(int nlevels) { return (int)sizeof(ResizeTap) * 2 * kRgnTapRows * (nlevels - 1); }
+
+// A workgroup barrier that orders LDS only: the kernel's global stores are
+// read by later launches, so waiting for them at every level (as
+// __syncthreads' release does) would only add their write latency.
+__device__ inline void lds_barrier() { __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __global__ __launch_bounds__(kRgnThreads) void k_pyramid_rgn(DevPlan p, FrameBufs fb) {
     extern __shared__ __align__(16) uint8_t lds[];
@@ -571,6 +579,20 @@ __global__ __launch_bounds__(kRgnThreads) void k_pyramid_rgn(DevPlan p, FrameBuf
     constexpr int kWaves = kRgnThreads / 64;
     const int4 *T = p.pyr_rgn + (int64_t)r * 2 * kMaxLevels;   // [l] = R_l, [kMaxLevels + l] = O_l
     uint8_t *cur = lds, *nxt = lds + p.pyr_rgn_half;
+    // every level's taps for this region's columns and rows, staged with R_0 so
+    // the level loop issues no global loads (on gfx9 a wait for a load also
+    // waits for the level's earlier global stores)
+    ResizeTap *sxt = reinterpret_cast<ResizeTap *>(lds + 2 * p.pyr_rgn_half);
+    ResizeTap *syt = sxt + kRgnTapRows * (p.nlevels - 1);
+    for (int i = tid; i < 2 * kRgnTapRows * (p.nlevels - 1); i += kRgnThreads) {
+        const int ly = i >= kRgnTapRows * (p.nlevels - 1);
+        const int j = i - ly * kRgnTapRows * (p.nlevels - 1);
+        const int l = 1 + j / kRgnTapRows, k = j - (l - 1) * kRgnTapRows;
+        const int4 Rl = T[l];
+        const LevelGeom &g = p.lv[l];
+        if (!ly && k <= Rl.z - Rl.x) sxt[j] = p.xtaps[g.xtab_off + Rl.x + k];
+        if (ly && k <= Rl.w - Rl.y) syt[j] = p.ytaps[g.ytab_off + Rl.y + k];
+    }
     // R_0 from level 0, dword-aligned rows (level 0's base and pitch are dword multiples)
     int4 R = T[0];
     int ox = R.x & ~3, oy = R.y;
@@ -586,24 +608,24 @@ __global__ __launch_bounds__(kRgnThreads) void k_pyramid_rgn(DevPlan p, FrameBuf
             for (int d = lane; d < ndw; d += 64) d32[d] = s32[d];
         }
     }
-    __syncthreads();
+    lds_barrier();
     for (int l = 1; l < p.nlevels; ++l) {
         const int4 Rl = T[l], Ol = T[kMaxLevels + l];
-        const LevelGeom g = p.lv[l];
+        const LevelArgs g = p.la[l];
         const int gsh = p.la[l - 1].h;
-        const ResizeTap *xt = p.xtaps + g.xtab_off;
-        const ResizeTap *yt = p.ytaps + g.ytab_off;
+        const ResizeTap *xt = sxt + kRgnTapRows * (l - 1);
+        const ResizeTap *yt = syt + kRgnTapRows * (l - 1);
         const int w = Rl.z - Rl.x + 1, h = Rl.w - Rl.y + 1;
         const int dstride = (w + 4 + 3) & ~3;
         uint8_t *dst = fb.pyr + (int64_t)b * p.pyr_bytes + g.pyr_off;
         // this lane's columns lane + 64 k (k < kRgnCols: the plan bounds the
-        // widths) and their taps, loaded once for all rows
+        // widths) and their taps, read once for all rows
         ResizeTap tx[kRgnCols];
 #pragma unroll
-        for (int k = 0; k < kRgnCols; ++k) tx[k] = xt[Rl.x + min(lane + 64 * k, w - 1)];
+        for (int k = 0; k < kRgnCols; ++k) tx[k] = xt[min(lane + 64 * k, w - 1)];
         for (int row = wave; row < h; row += kWaves) {
             const int y = Rl.y + row;
-            const ResizeTap ty = yt[y];
+            const ResizeTap ty = yt[row];
             const int s0 = min(max((int)ty.src, 0), gsh - 1) - oy, s1 = min(max((int)ty.src + 1, 0), gsh - 1) - oy;
             const uint8_t *S0 = cur + s0 * stride - ox, *S1 = cur + s1 * stride - ox;
             const int b0 = ty.a0, b1 = ty.a1;
@@ -623,7 +645,7 @@ __global__ __launch_bounds__(kRgnThreads) void k_pyramid_rgn(DevPlan p, FrameBuf
                 if (own_row && x >= Ol.x && x <= Ol.z) dst[(int64_t)y * g.pitch + x] = v;
             }
         }
-        __syncthreads();
+        lds_barrier();
         uint8_t *t = cur; cur = nxt; nxt = t;
         stride = dstride; ox = Rl.x; oy = Rl.y;
     }
@@ -1835,7 +1857,8 @@ hipError_t launch_resize(const DevPlan &p, const Plan &hp, const FrameBufs &fb, 
                 return hipErrorInvalidValue;
             lds_set = true;
         }
-        hipLaunchKernelGGL(k_pyramid_rgn, dim3(hp.rgn_n, B), dim3(kRgnThreads), 2 * hp.rgn_half, st, p, fb);
+        hipLaunchKernelGGL(k_pyramid_rgn, dim3(hp.rgn_n, B), dim3(kRgnThreads), 2 * hp.rgn_half + rgn_tap_bytes(hp.nlevels), st,
+                           p, fb);
         return hipGetLastError();
     }
     for (int l = 1; l < hp.nlevels; ++l)
@@ -1999,14 +2022,14 @@ bool plan_pyr_regions(Plan &hp) {
             T[0] = src_of(1, T[1]);
             for (int l = 0; l < n; ++l) {
                 const RgnRect &q = T[l];
-                if (l > 0 && q.x1 - q.x0 + 1 > 64 * kRgnCols) return false;
+                if (l > 0 && (q.x1 - q.x0 + 1 > 64 * kRgnCols || q.y1 - q.y0 + 1 > kRgnTapRows)) return false;
                 const size_t stride = l == 0 ? 4 * (size_t)(((q.x1 - (q.x0 & ~3)) >> 2) + 1) + 4
                                              : (size_t)((q.x1 - q.x0 + 1 + 4 + 3) & ~3);
                 half = std::max(half, stride * (q.y1 - q.y0 + 1));
             }
         }
     half = (half + 15) & ~size_t(15);
-    if (2 * half > 160 * 1024) return false;
+    if (2 * half + rgn_tap_bytes(n) > 160 * 1024) return false;
     hp.rgn = std::move(out);
     hp.rgn_n = gx * gy;
     hp.rgn_half = (int)half;
