@@ -102,7 +102,6 @@ struct orbx_extractor {
     int graph_w = 0, graph_h = 0;
     uint8_t *h_img = nullptr, *h_out = nullptr;   // pinned
     size_t h_img_bytes = 0, h_out_bytes = 0;
-    uint32_t *d_pack_ctr = nullptr;   // k_pack_host's block count (the last block raises the done flag)
     bool host_result_valid = false;   // slot 0 still holds what h_out holds (no extraction since)
 
     // orbx_compute_stereo_matches workspace (this extractor as the left one),
@@ -192,7 +191,7 @@ struct orbx_extractor {
         dfree(d_tables); dfree(d_pyr); dfree(d_blur); dfree(d_cand); dfree(d_cand2); dfree(d_keys); dfree(d_sel);
         dfree(d_cell_count); dfree(d_level_count); dfree(d_key_node); dfree(d_key_q);
         for (auto &s : slot) { dfree(s.kps); dfree(s.desc); dfree(s.nkps); s.batch = 0; }
-        dfree(d_prev); dfree(d_m12); dfree(d_nmatch); dfree(d_img); dfree(d_pack_ctr);
+        dfree(d_prev); dfree(d_m12); dfree(d_nmatch); dfree(d_img);
         dfree(d_ur); dfree(d_depth); dfree(d_sad); dfree(d_nkept);
         depth_mode = 0;
         depth_count = 0;
@@ -822,28 +821,24 @@ constexpr size_t kOutKps = 128;
 // Frame 0's results written straight into the pinned (device-visible) host
 // buffer: one small kernel instead of four blit copies (~5 us each at B = 1).
 // Dwords: [0] count, [2] done flag, [4..20) level counts, then the first
-// `count` keypoint records and descriptors (the host reads no further).  The
-// last block to finish raises the flag after every block's writes are
-// visible system-wide, so the host can poll it instead of sleeping in a
-// stream synchronisation (~10 us of wake-up at B = 1).
-constexpr int kOutFlag = 2;
-__global__ __launch_bounds__(256) void k_pack_host(const int32_t *nkps, const int32_t *lc, const uint32_t *kps,
-                                                   const uint32_t *desc, int nlevels, int kdesc_dw, uint32_t *out,
-                                                   uint32_t *ctr) {
+// `count` keypoint records and descriptors (the host reads no further).  One
+// workgroup: after its writes are visible system-wide it raises the flag, so
+// the host can poll it instead of sleeping in a stream synchronisation (~10
+// us of wake-up at B = 1).
+constexpr int kOutFlag = 2, kPackThreads = 1024;
+__global__ __launch_bounds__(kPackThreads) void k_pack_host(const int32_t *nkps, const int32_t *lc,
+                                                            const uint32_t *kps, const uint32_t *desc, int nlevels,
+                                                            int kdesc_dw, uint32_t *out) {
     const int n = max(nkps[0], 0);
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int t = threadIdx.x;
     if (t == 0) out[0] = (uint32_t)nkps[0];
     if (t < kMaxLevels) out[4 + t] = t < nlevels ? (uint32_t)lc[t] : 0u;
     const int nk = n * (int)(sizeof(orbx_keypoint) / 4), nd = n * 8;
-    for (int i = t; i < nk; i += gridDim.x * blockDim.x) out[kOutKps / 4 + i] = kps[i];
-    for (int i = t; i < nd; i += gridDim.x * blockDim.x) out[kdesc_dw + i] = desc[i];
+    for (int i = t; i < nk; i += kPackThreads) out[kOutKps / 4 + i] = kps[i];
+    for (int i = t; i < nd; i += kPackThreads) out[kdesc_dw + i] = desc[i];
     __threadfence_system();
     __syncthreads();
-    if (threadIdx.x == 0 && atomicAdd(ctr, 1u) == gridDim.x - 1) {
-        *ctr = 0;   // (for the next replay; every block has counted)
-        __threadfence_system();
-        __hip_atomic_store(out + kOutFlag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    if (t == 0) __hip_atomic_store(out + kOutFlag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 size_t out_desc_off(const orbx_extractor *ex) {
     return kOutKps + sizeof(orbx_keypoint) * (size_t)ex->plan.max_kps;
@@ -880,10 +875,6 @@ int build_host_graph(orbx_extractor *ex, int width, int height) {
             return ORBX_ENOMEM;
         ex->h_out_bytes = out_bytes;
     }
-    if (!ex->d_pack_ctr) {
-        if (dalloc(&ex->d_pack_ctr, 1) != hipSuccess) return ORBX_ENOMEM;
-        if (hipMemset(ex->d_pack_ctr, 0, sizeof(uint32_t)) != hipSuccess) return ORBX_EIO;
-    }
     hipStream_t st = ex->stream;
     const int pipe = ex->pipeline;
     hipEvent_t *ev = ex->cur_ev;
@@ -905,16 +896,14 @@ int build_host_graph(orbx_extractor *ex, int width, int height) {
     hipGraph_t g = nullptr;
     if (hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) { restore(); return ORBX_EIO; }
     const auto &s0 = ex->slot[0];
-    const int K = ex->plan.max_kps;
     bool ok = hipMemcpyAsync(ex->d_img, ex->h_img, need, hipMemcpyHostToDevice, st) == hipSuccess;
     ok = ok && run_extract(ex, 0, ex->d_img, (int64_t)need, (int)dp, 1, st) == ORBX_OK;
     void *dout = nullptr;   // the pinned buffer's device address
     ok = ok && hipHostGetDevicePointer(&dout, ex->h_out, 0) == hipSuccess;
     if (ok) {
-        hipLaunchKernelGGL(k_pack_host, dim3(std::max(1, (K * 8 + 255) / 256)), dim3(256), 0, st, s0.nkps,
-                           ex->d_level_count, reinterpret_cast<const uint32_t *>(s0.kps),
-                           reinterpret_cast<const uint32_t *>(s0.desc), ex->nlevels, (int)(out_desc_off(ex) / 4),
-                           reinterpret_cast<uint32_t *>(dout), ex->d_pack_ctr);
+        hipLaunchKernelGGL(k_pack_host, dim3(1), dim3(kPackThreads), 0, st, s0.nkps, ex->d_level_count,
+                           reinterpret_cast<const uint32_t *>(s0.kps), reinterpret_cast<const uint32_t *>(s0.desc),
+                           ex->nlevels, (int)(out_desc_off(ex) / 4), reinterpret_cast<uint32_t *>(dout));
         ok = hipGetLastError() == hipSuccess;
     }
     const bool ended = hipStreamEndCapture(st, &g) == hipSuccess;
@@ -940,22 +929,36 @@ int orbx_extract(orbx_extractor *ex, const uint8_t *image, int width, int height
     if (!image || width <= 0 || height <= 0) { *n = -1; return ORBX_OK; }  // ORBextractor.cc:1086-1087
     if (pitch < (size_t)width) return ORBX_EINVAL;
     if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
-    int rc = reserve(ex, width, height, std::max(1, ex->max_batch));
-    if (rc) return rc;
     const size_t dp = (size_t)pitch_of(width);
     const size_t need = dp * height;
-    if (ex->d_img_bytes < need) {
-        if (ex->host_graph) (void)hipGraphExecDestroy(ex->host_graph);
-        ex->host_graph = nullptr;
-        dfree(ex->d_img);
-        if (dalloc(&ex->d_img, need) != hipSuccess) return ORBX_ENOMEM;
-        ex->d_img_bytes = need;
-    }
-    if (host_graph_enabled()) {
-        if (!ex->host_graph || ex->graph_w != width || ex->graph_h != height) {
+    const bool graph = host_graph_enabled();
+    {
+        // Setup (plan upload, allocations, graph capture) under one process-wide
+        // lock: extractors driven from several threads (Frame's stereo
+        // constructor runs two) must not make a synchronous runtime call while
+        // another thread's stream is being captured.
+        static std::mutex setup_mu;
+        std::unique_lock<std::mutex> lk(setup_mu, std::defer_lock);
+        const bool ready = ex->planned && ex->plan.width == width && ex->plan.height == height &&
+                           ex->d_img_bytes >= need &&
+                           (!graph || (ex->host_graph && ex->graph_w == width && ex->graph_h == height));
+        if (!ready) lk.lock();
+        int rc = reserve(ex, width, height, std::max(1, ex->max_batch));
+        if (rc) return rc;
+        if (ex->d_img_bytes < need) {
+            if (ex->host_graph) (void)hipGraphExecDestroy(ex->host_graph);
+            ex->host_graph = nullptr;
+            dfree(ex->d_img);
+            if (dalloc(&ex->d_img, need) != hipSuccess) return ORBX_ENOMEM;
+            ex->d_img_bytes = need;
+        }
+        if (graph && (!ex->host_graph || ex->graph_w != width || ex->graph_h != height)) {
             rc = build_host_graph(ex, width, height);
             if (rc) return rc;
         }
+    }
+    int rc = ORBX_OK;
+    if (graph) {
         for (int r = 0; r < height; ++r) std::memcpy(ex->h_img + r * dp, image + r * pitch, (size_t)width);
         volatile uint32_t *flag = reinterpret_cast<volatile uint32_t *>(ex->h_out) + kOutFlag;
         *flag = 0;
@@ -966,8 +969,11 @@ int orbx_extract(orbx_extractor *ex, const uint8_t *image, int width, int height
             if ((i & 255) == 0 && hipStreamQuery(ex->stream) != hipErrorNotReady) break;
             __builtin_ia32_pause();
         }
-        if (!*flag && hipStreamSynchronize(ex->stream) != hipSuccess) return ORBX_EIO;
-        if (!*flag) return ORBX_EIO;
+        if (!*flag) {   // the stream has ended: a failure, or the flag's write still in flight
+            if (hipStreamSynchronize(ex->stream) != hipSuccess) return ORBX_EIO;
+            for (int i = 0; i < (1 << 20) && !*flag; ++i) __builtin_ia32_pause();
+            if (!*flag) return ORBX_EIO;
+        }
         std::atomic_thread_fence(std::memory_order_acquire);
         ex->cur = 0;
         ex->match_batch = 0;
