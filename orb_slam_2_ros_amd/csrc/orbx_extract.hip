@@ -2037,14 +2037,8 @@ bool plan_pyr_regions(Plan &hp) {
 }
 
 // The region pyramid while one block per region and frame still leaves the
-// chip short of a block per CU (ORBX_PYR_RGN=0 turns it off).
-bool use_pyr_regions(const Plan &hp, int B) {
-    static const bool on = [] {
-        const char *e = std::getenv("ORBX_PYR_RGN");
-        return !(e && e[0] == '0');
-    }();
-    return on && hp.rgn_n > 0 && (int64_t)B * hp.rgn_n <= 256;
-}
+// chip short of a block per CU.
+bool use_pyr_regions(const Plan &hp, int B) { return hp.rgn_n > 0 && (int64_t)B * hp.rgn_n <= 256; }
 
 // Wave-tile geometry of every level (ResizeWave).  False when some level does
 // not fit the wave kernel (a column group spanning more than 7 source bytes,

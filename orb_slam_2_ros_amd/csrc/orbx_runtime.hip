@@ -313,7 +313,8 @@ int reserve(orbx_extractor *ex, int w, int h, int max_batch) {
     }
     if (!resize_window_fits(ex->plan)) return ORBX_EINVAL;
     if (!plan_resize_waves(ex->plan) || std::getenv("ORBX_RESIZE_BLOCKS")) ex->plan.rw.clear();
-    (void)plan_pyr_regions(ex->plan);
+    const char *rg = std::getenv("ORBX_PYR_RGN");   // =0: the per-level resize kernels at every batch
+    if (!(rg && rg[0] == '0')) (void)plan_pyr_regions(ex->plan);
     int rc = upload_plan(ex);
     if (rc) return rc;
     const Plan &p = ex->plan;

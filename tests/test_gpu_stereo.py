@@ -213,3 +213,41 @@ def test_cpp_adapter_stereo_and_rgbd(tmp_path, oracle_mod):
     our, odp = oracle_mod.stereo_from_rgbd(k, dm, float(np.float32(bf)))
     assert np.array_equal(ur.view(np.uint32), our.view(np.uint32))
     assert np.array_equal(dp.view(np.uint32), odp.view(np.uint32))
+
+
+def test_stereo_pair_on_two_threads(oracle_mod):
+    """Frame's stereo constructor extracts left and right on two threads
+    (Frame.cc:79-82): two fresh extractors whose first calls (plan upload,
+    graph capture) run concurrently, then repeated concurrent calls; every
+    result is the oracle's."""
+    import threading
+    w, h, nf = 752, 480, 1200
+    L, R = synth.stereo_pair(w, h, 61, 0, 20)
+    ko_l, do_l = oracle_mod.extract(L, nf)
+    ko_r, do_r = oracle_mod.extract(R, nf)
+    for rep in range(3):
+        exl, exr = ORBextractor(nf, 1.2, 8, 20, 7), ORBextractor(nf, 1.2, 8, 20, 7)
+        out = {}
+        go = threading.Barrier(2)
+
+        def run(name, ex, img):
+            go.wait()
+            out[name] = [ex(img) for _ in range(4)]
+        ts = [threading.Thread(target=run, args=("l", exl, L)), threading.Thread(target=run, args=("r", exr, R))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        for (k, d) in out["l"]:
+            assert len(k) == len(ko_l) and (k == ko_l).all() and np.array_equal(d, do_l)
+        for (k, d) in out["r"]:
+            assert len(k) == len(ko_r) and (k == ko_r).all() and np.array_equal(d, do_r)
+        bf, fx = 47.9, 435.2
+        kl, dl = out["l"][-1]
+        kr, dr = out["r"][-1]
+        ur, dp, kept = compute_stereo_matches(exl, exr, kl, dl, kr, dr, bf, _mb(bf, fx))
+        our, odp, okept = oracle_mod.compute_stereo_matches(oracle_mod.pyramid(L), oracle_mod.pyramid(R), kl, dl, kr,
+                                                            dr, bf, _mb(bf, fx))
+        assert kept == okept and np.array_equal(ur.view(np.uint32), our.view(np.uint32))
+        exl.close()
+        exr.close()
