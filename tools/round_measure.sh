@@ -5,7 +5,7 @@
 set -uo pipefail
 TAG=$1
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gputest_$TAG.log 2>&1 || { tail -5 gpurun_out/gputest_$TAG.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gputest_$TAG.log 2>&1 || { tail -5 gpurun_out/gputest_$TAG.log; exit 1; }
 tail -1 gpurun_out/gputest_$TAG.log
 timeout -k 10 400 bash tools/profile.sh $TAG || exit 1
 P=gpurun_out/prof_$TAG
