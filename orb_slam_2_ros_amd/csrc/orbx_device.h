@@ -25,6 +25,7 @@ struct FastLds {
     int ps;            // patch row stride (dword multiple)
     int patch_bytes, score_bytes, per_wave;
     int sw;            // score-map row stride (largest cell width + 2)
+    int list_cap;      // survivor-list entries (k_fast flushes before overflowing it)
 };
 FastLds fast_lds(int mw, int mh);
 

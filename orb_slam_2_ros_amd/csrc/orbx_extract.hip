@@ -820,6 +820,83 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
             for (int i = lane; i < nz; i += 64) z0[i] = make_uint4(0u, 0u, 0u, 0u);
         }
         wave_lds_fence();
+        // The list holds, in row-major order, the corners still waiting for
+        // their NMS (list[0, npend): the last scored row's) and then the
+        // compass survivors of the rows since (list[npend, npend + nsurv)).
+        // It has room for fl.list_cap entries (8 workgroups per CU at VGA,
+        // 6 with a list for every pixel of the cell); before a compass step
+        // could overflow it, the survivors so far are scored and the corners
+        // of every finished row are suppressed and written (flush).
+        int npend = 0, nsurv = 0, base = 0;
+        // B + C for the survivors in list[npend, npend + nsurv), rows [0, ydone)
+        // compass-tested; final: every remaining corner is decided.
+        auto flush = [&](int ydone, bool final) {
+            // B. arc score of every survivor: S = max(M1 - v, v - M2), M1 = max over
+            //    the 16 nine-pixel arcs of the arc's minimum, M2 = min over arcs of the
+            //    arc's maximum, side by side as packed u16 lanes (p, 255 - p) through
+            //    sliding-window minima (2, 4, 8, 9).  A corner at th iff S > th; its
+            //    FAST score S - 1 goes to the map, corners compacted in place.
+            int ncorner = npend;
+            for (int i0 = 0; i0 < nsurv; i0 += 64) {
+                bool corner = false;
+                int e = 0;
+                if (i0 + lane < nsurv) {
+                    e = list[npend + i0 + lane];
+                    const int ey = e >> 8, ex = e & 0xFF;
+                    const uint8_t *q = pc + mul24u(ey, PS) + ex;
+                    const int v = q[0];
+                    const uint32_t pr[16] = {q[3 * PS],  q[3 * PS + 1],  q[2 * PS + 2],  q[PS + 3],
+                                             q[3],       q[-PS + 3],     q[-2 * PS + 2], q[-3 * PS + 1],
+                                             q[-3 * PS], q[-3 * PS - 1], q[-2 * PS - 2], q[-PS - 3],
+                                             q[-3],      q[PS - 3],      q[2 * PS - 2],  q[3 * PS - 1]};
+                    const int S = arc_score_bytes(reinterpret_cast<const int *>(pr), v);
+                    corner = S > th;
+                    if (corner) scm[mul24u(ey + 1, SW) + ex + 1] = (uint8_t)(S - 1);
+                }
+                const uint64_t m = __ballot(corner);
+                wave_lds_fence();   // all survivor reads of this chunk precede the in-place writes
+                if (corner) list[ncorner + __popcll(m & below)] = (uint16_t)e;
+                ncorner += __popcll(m);
+            }
+            nsurv = 0;
+            wave_lds_fence();
+            PHASE_MARK(0, ph + 1);   // arc scores
+            if constexpr (kStopFast == 3) { npend = 0; return; }
+            // C. strict 3x3 NMS inside the cell (outside neighbours and non-corners
+            //    score 0), compacted in row-major order; a corner of row ydone - 1
+            //    waits for the next rows' scores unless final.
+            const int ylast = final ? INT_MAX : ydone - 1;
+            int nfin = 0;
+            for (int i0 = 0; i0 < ncorner; i0 += 64) {
+                bool keep = false, fin = false;
+                int ey = 0, ex = 0, sv = 0;
+                if (i0 + lane < ncorner) {
+                    const int e = list[i0 + lane];
+                    ey = e >> 8;
+                    ex = e & 0xFF;
+                    fin = ey < ylast;
+                    const int si = mul24u(ey + 1, SW) + ex + 1;
+                    sv = scm[si];
+                    keep = fin && sv > scm[si - 1] && sv > scm[si + 1] && sv > scm[si - SW - 1] &&
+                           sv > scm[si - SW] && sv > scm[si - SW + 1] && sv > scm[si + SW - 1] && sv > scm[si + SW] &&
+                           sv > scm[si + SW + 1];
+                }
+                const uint64_t mk = __ballot(keep);
+                const int pk = base + __popcll(mk & below);
+                if (keep && pk < c.cap) out[pk] = pack_key(c.x0 + ex, c.y0 + ey, sv);
+                base += __popcll(mk);
+                nfin += __popcll(__ballot(fin));
+            }
+            // the waiting corners (one row: < 64) to the front
+            npend = ncorner - nfin;
+            if (npend) {
+                const int e = lane < npend ? list[nfin + lane] : 0;
+                wave_lds_fence();
+                if (lane < npend) list[lane] = (uint16_t)e;
+                wave_lds_fence();
+            }
+            PHASE_MARK(0, ph + 2);   // NMS + output
+        };
         // A. compass pre-test: an arc of 9 covers two cyclically adjacent points
         //    of {0, 4, 8, 12}, so a pixel is a corner candidate only if some
         //    adjacent pair is all brighter (min of the pair > v + th) or all
@@ -827,7 +904,6 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
         //    quad of 4 pixels from 5 aligned LDS dwords (the +-3 column
         //    neighbours by byte alignment), as two packed u16 pairs (even and
         //    odd pixels); survivors are compacted in row-major order.
-        int nsurv = 0;
         {
             const u16x2 thv = {(unsigned short)th, (unsigned short)th};
             const u16x2 thv8 = {(unsigned short)(th << 8), (unsigned short)(th << 8)};
@@ -836,6 +912,11 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
             const int RPS = __builtin_amdgcn_readfirstlane(R * PS), R8 = __builtin_amdgcn_readfirstlane(R << 8);
             const int chps = __builtin_amdgcn_readfirstlane(ch * PS);
             for (int yo = 0, ys = 0; yo < chps; yo += RPS, ys += R8) {
+                // survivors this step can add: its rows' pixels (wave-uniform)
+                if (npend + nsurv + min(R, ch - (ys >> 8)) * cw > fl.list_cap) {
+                    if constexpr (kStopFast == 2) nsurv = 0;
+                    else flush(ys >> 8, false);
+                }
                 uint32_t cand = 0;
                 if (yo < rlim) {
                     const lds_u8 *qb = qb0 + yo;
@@ -895,7 +976,7 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
                 const int total = __builtin_amdgcn_readlane(incl, 63);
                 if (total) {
                     typedef __attribute__((address_space(3))) uint16_t lds_u16;
-                    lds_u16 *dst = (lds_u16 *)list + nsurv + (incl - cnt);
+                    lds_u16 *dst = (lds_u16 *)list + npend + nsurv + (incl - cnt);
                     const int ey = e + ys;
                     while (cand) {
                         *dst = (uint16_t)(ey + __builtin_ctz(cand));
@@ -909,57 +990,7 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
         wave_lds_fence();
         PHASE_MARK(0, ph);       // score-map zeroing + compass pre-test + compaction
         if constexpr (kStopFast == 2) return 0;
-        // B. arc score of every survivor: S = max(M1 - v, v - M2), M1 = max over
-        //    the 16 nine-pixel arcs of the arc's minimum, M2 = min over arcs of the
-        //    arc's maximum, side by side as packed u16 lanes (p, 255 - p) through
-        //    sliding-window minima (2, 4, 8, 9).  A corner at th iff S > th; its
-        //    FAST score S - 1 goes to the map, corners compacted in place.
-        int ncorner = 0;
-        for (int i0 = 0; i0 < nsurv; i0 += 64) {
-            bool corner = false;
-            int e = 0;
-            if (i0 + lane < nsurv) {
-                e = list[i0 + lane];
-                const int ey = e >> 8, ex = e & 0xFF;
-                const uint8_t *q = pc + mul24u(ey, PS) + ex;
-                const int v = q[0];
-                const uint32_t pr[16] = {q[3 * PS],  q[3 * PS + 1],  q[2 * PS + 2],  q[PS + 3],
-                                         q[3],       q[-PS + 3],     q[-2 * PS + 2], q[-3 * PS + 1],
-                                         q[-3 * PS], q[-3 * PS - 1], q[-2 * PS - 2], q[-PS - 3],
-                                         q[-3],      q[PS - 3],      q[2 * PS - 2],  q[3 * PS - 1]};
-                const int S = arc_score_bytes(reinterpret_cast<const int *>(pr), v);
-                corner = S > th;
-                if (corner) scm[mul24u(ey + 1, SW) + ex + 1] = (uint8_t)(S - 1);
-            }
-            const uint64_t m = __ballot(corner);
-            wave_lds_fence();   // all survivor reads of this chunk precede the in-place writes
-            if (corner) list[ncorner + __popcll(m & below)] = (uint16_t)e;
-            ncorner += __popcll(m);
-        }
-        wave_lds_fence();
-        PHASE_MARK(0, ph + 1);   // arc scores
-        if constexpr (kStopFast == 3) return 0;
-        // C. strict 3x3 NMS inside the cell (outside neighbours and non-corners
-        //    score 0), compacted in row-major order.
-        int base = 0;
-        for (int i0 = 0; i0 < ncorner; i0 += 64) {
-            bool keep = false;
-            int ey = 0, ex = 0, sv = 0;
-            if (i0 + lane < ncorner) {
-                const int e = list[i0 + lane];
-                ey = e >> 8;
-                ex = e & 0xFF;
-                const int si = mul24u(ey + 1, SW) + ex + 1;
-                sv = scm[si];
-                keep = sv > scm[si - 1] && sv > scm[si + 1] && sv > scm[si - SW - 1] && sv > scm[si - SW] &&
-                       sv > scm[si - SW + 1] && sv > scm[si + SW - 1] && sv > scm[si + SW] && sv > scm[si + SW + 1];
-            }
-            const uint64_t mk = __ballot(keep);
-            const int pk = base + __popcll(mk & below);
-            if (keep && pk < c.cap) out[pk] = pack_key(c.x0 + ex, c.y0 + ey, sv);
-            base += __popcll(mk);
-        }
-        PHASE_MARK(0, ph + 2);   // NMS + output
+        flush(ch, true);
         return base;
     };
     const int n_ini = pass(p.ini_th, out_i, 1);
@@ -1882,12 +1913,15 @@ uint32_t grid_magic(uint32_t gx, uint32_t gy) {
 
 FastLds fast_lds(int mw, int mh) {
     FastLds f;
+    // survivor-list capacity: every pixel of the largest cell, or 640 (room
+    // for a step's 512 plus a row of waiting corners; k_fast flushes before)
+    f.list_cap = std::min(mw * mh, 640);
     f.ps = (mw + 6 + 3 + 3) & ~3;   // + alignment offset, dword rows
     f.sw = mw + 2;
     if (f.ps <= 64) f.ps = f.sw = f.ps <= 48 ? 48 : 64;   // k_fast's constant-stride instantiations
     f.patch_bytes = (f.ps * (mh + 6) + 15) & ~15;
     f.score_bytes = (f.sw * (mh + 2) + 15) & ~15;
-    f.per_wave = f.patch_bytes + f.score_bytes + ((2 * mw * mh + 15) & ~15);
+    f.per_wave = f.patch_bytes + f.score_bytes + ((2 * f.list_cap + 15) & ~15);
     return f;
 }
 
