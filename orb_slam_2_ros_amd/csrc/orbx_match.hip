@@ -34,19 +34,20 @@ constexpr int kMT = 256;                        // threads per frame pair
 constexpr int kMW = kMT / 64;                   // waves
 
 // LDS layout of one frame pair, indexed by grid position (F2 octave-0
-// keypoints, < maxc) or query rank (F1 octave-0 keypoints, < maxq) only, so a
-// pair needs ~40 KB at VGA and four pairs share a CU (16-B aligned arrays first).
+// keypoints, < maxc) or query rank (F1 octave-0 keypoints, < maxq) only, with
+// 16-bit cell starts, distances and indices, so a pair needs ~31 KB at VGA
+// and five pairs share a CU (16-B aligned arrays first).
 struct MLds {
     uint4 *gd;       // maxc x 2: F2 octave-0 descriptors in grid order
     uint4 *qd;       // maxq x 2: F1 octave-0 (query) descriptors in query order
     float2 *gxy;     // maxc: F2 positions in grid order
     float2 *qxy;     // maxq: query centres (vbPrevMatched)
     uint32_t *top4;  // maxq x 4: (grid position << 16 | dist) of the 4 smallest (dist, list position)
-    int *gstart;     // kGridCells + 1: first grid position of each cell
-    int *mdist;      // maxc: vMatchedDistance by grid position
-    int *m21;        // maxc: vnMatches21 (query rank) by grid position
     uint32_t *claim; // maxc: (replay batch << 16 | (255 - lane) << 8 | dist) of a batch's first acceptor
-    int *m12;        // maxq: vnMatches12 (grid position) by query rank
+    uint16_t *gstart;   // kGridCells + 1 (+1 pad): first grid position of each cell (dword-aligned pairs)
+    int16_t *mdist;  // maxc: vMatchedDistance by grid position (kNoDist: none)
+    int16_t *m21;    // maxc: vnMatches21 (query rank) by grid position
+    int16_t *m12;    // maxq: vnMatches12 (grid position) by query rank
     int16_t *glist;  // maxc: F2 index by grid position
     int16_t *qidx;   // maxq: F1 index of each query
     int16_t *live;   // maxq: queries that can be accepted, in order
@@ -62,11 +63,11 @@ __device__ inline MLds carve(uint8_t *ptr, int maxq, int maxc) {
     s.qxy = reinterpret_cast<float2 *>(ptr); ptr += sizeof(float2) * maxq;
     ptr += 8 * ((maxc + maxq) & 1);   // top4 rows are read as uint4
     s.top4 = reinterpret_cast<uint32_t *>(ptr); ptr += sizeof(uint32_t) * 4 * maxq;
-    s.gstart = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * (kGridCells + 1);
-    s.mdist = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * maxc;
-    s.m21 = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * maxc;
     s.claim = reinterpret_cast<uint32_t *>(ptr); ptr += sizeof(uint32_t) * maxc;
-    s.m12 = reinterpret_cast<int *>(ptr); ptr += sizeof(int) * maxq;
+    s.gstart = reinterpret_cast<uint16_t *>(ptr); ptr += sizeof(uint16_t) * (kGridCells + 2);
+    s.mdist = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * ((maxc + 1) & ~1);
+    s.m21 = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * ((maxc + 1) & ~1);
+    s.m12 = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * ((maxq + 1) & ~1);
     s.glist = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * ((maxc + 1) & ~1);
     s.qidx = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * ((maxq + 1) & ~1);
     s.live = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * ((maxq + 1) & ~1);
@@ -74,6 +75,17 @@ __device__ inline MLds carve(uint8_t *ptr, int maxq, int maxc) {
     s.rbin = reinterpret_cast<int8_t *>(ptr);
     return s;
 }
+
+// atomicAdd on one 16-bit cell start: LDS atomics are 32-bit, so the pair
+// holding it takes the add in its half (counts stay < 2^16: no carry).
+// Returns the half's old value.
+__device__ inline int gstart_add(uint16_t *gstart, int cell, int v) {
+    uint32_t *w = reinterpret_cast<uint32_t *>(gstart) + (cell >> 1);
+    const int sh = 16 * (cell & 1);
+    return (int)((atomicAdd(w, (uint32_t)v << sh) >> sh) & 0xFFFFu);
+}
+
+constexpr int kNoDist = 0x7FFF;   // vMatchedDistance's INT_MAX (distances are <= 256)
 
 __device__ inline int hamming_regs(const uint4 a0, const uint4 a1, const uint4 b0, const uint4 b1) {
     return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
@@ -129,8 +141,8 @@ __global__ __launch_bounds__(kMT) void k_search_init(MatchBufs mb, int maxq, int
     if (clk) { mb.clocks[0] = clock64(); mb.clocks[6] = 0; mb.clocks[7] = 0; }
 
     // ---- 0. init; every output defaults to "no match"
-    for (int i = tid; i <= kGridCells; i += kMT) s.gstart[i] = 0;
-    for (int i = tid; i < maxc; i += kMT) { s.mdist[i] = INT_MAX; s.m21[i] = -1; s.claim[i] = 0; }
+    for (int i = tid; i < (kGridCells + 2) / 2; i += kMT) reinterpret_cast<uint32_t *>(s.gstart)[i] = 0;
+    for (int i = tid; i < maxc; i += kMT) { s.mdist[i] = kNoDist; s.m21[i] = -1; s.claim[i] = 0; }
     for (int i = tid; i < maxq; i += kMT) { s.m12[i] = -1; s.rbin[i] = -1; s.acc[i] = -1; }
     for (int i = tid; i < n1; i += kMT) {
         out12[i] = -1;
@@ -147,7 +159,7 @@ __global__ __launch_bounds__(kMT) void k_search_init(MatchBufs mb, int maxq, int
     for (int i = tid; i < n2; i += kMT) {
         if (k2[i].octave != 0) continue;
         const int cell = grid_cell(k2[i].x, k2[i].y, invW, invH);
-        if (cell >= 0) atomicAdd(&s.gstart[cell], 1);
+        if (cell >= 0) gstart_add(s.gstart, cell, 1);
     }
     __syncthreads();
     constexpr int kPer = kGridCells / kMT;   // 12 cells per thread, contiguous
@@ -158,10 +170,10 @@ __global__ __launch_bounds__(kMT) void k_search_init(MatchBufs mb, int maxq, int
         int run = block_scan_i32(local, &tot, ws);
         for (int i = 0; i < kPer; ++i) {
             const int v = s.gstart[tid * kPer + i];
-            s.gstart[tid * kPer + i] = run;
+            s.gstart[tid * kPer + i] = (uint16_t)run;
             run += v;
         }
-        if (tid == kMT - 1) s.gstart[kGridCells] = run;
+        if (tid == kMT - 1) s.gstart[kGridCells] = (uint16_t)min(run, 0xFFFF);
         if (tid == 0 && tot > maxc) sh_err = 1;
         __syncthreads();
     }
@@ -169,7 +181,7 @@ __global__ __launch_bounds__(kMT) void k_search_init(MatchBufs mb, int maxq, int
         if (k2[i].octave != 0) continue;
         const int cell = grid_cell(k2[i].x, k2[i].y, invW, invH);
         if (cell >= 0) {
-            const int pos = atomicAdd(&s.gstart[cell], 1);
+            const int pos = gstart_add(s.gstart, cell, 1);
             if (pos < maxc) s.glist[pos] = (int16_t)i;
         }
     }
@@ -183,7 +195,7 @@ __global__ __launch_bounds__(kMT) void k_search_init(MatchBufs mb, int maxq, int
         }
         __syncthreads();
 #pragma unroll
-        for (int i = 0; i < kPer; ++i) s.gstart[tid * kPer + i] = v[i];
+        for (int i = 0; i < kPer; ++i) s.gstart[tid * kPer + i] = (uint16_t)v[i];
         __syncthreads();
     }
     // each cell's list in keypoint-index order (mGrid push_back order)
@@ -372,9 +384,9 @@ __global__ __launch_bounds__(kMT) void k_search_init(MatchBufs mb, int maxq, int
             if (ok && lane < cut) {
                 const int old = s.m21[best_g];
                 if (old >= 0) s.m12[old] = -1;
-                s.m12[q] = best_g;
-                s.m21[best_g] = q;
-                s.mdist[best_g] = best;
+                s.m12[q] = (int16_t)best_g;
+                s.m21[best_g] = (int16_t)q;
+                s.mdist[best_g] = (int16_t)best;
                 s.acc[q] = (int16_t)best_g;   // binned in phase 4 (stolen pairs keep their bin)
             }
             wave_lds_fence();
@@ -420,9 +432,9 @@ __global__ __launch_bounds__(kMT) void k_search_init(MatchBufs mb, int maxq, int
                 if (fbest <= kThLow && (float)fbest < __fmul_rn((float)fbest2, nnr) && lane == 0) {
                     const int old = s.m21[fg];
                     if (old >= 0) s.m12[old] = -1;
-                    s.m12[qf] = fg;
-                    s.m21[fg] = qf;
-                    s.mdist[fg] = fbest;
+                    s.m12[qf] = (int16_t)fg;
+                    s.m21[fg] = (int16_t)qf;
+                    s.mdist[fg] = (int16_t)fbest;
                     s.acc[qf] = (int16_t)fg;
                 }
                 wave_lds_fence();
@@ -491,8 +503,8 @@ __global__ __launch_bounds__(kMT) void k_search_init(MatchBufs mb, int maxq, int
 // is indexed by query rank and grid position only).
 int match_lds_bytes(int n1cap, int n2cap, int maxq, int maxc) {
     (void)n1cap; (void)n2cap;
-    return (int)(40 * (maxc + maxq) + 8 + 16 * maxq + sizeof(int) * (kGridCells + 1) + 12 * maxc + 4 * maxq +
-                 sizeof(int16_t) * (((maxc + 1) & ~1) + 3 * ((maxq + 1) & ~1)) + maxq + 64);
+    return (int)(40 * (maxc + maxq) + 8 + 16 * maxq + 4 * maxc + sizeof(uint16_t) * (kGridCells + 2) +
+                 sizeof(int16_t) * (3 * ((maxc + 1) & ~1) + 4 * ((maxq + 1) & ~1)) + maxq + 64);
 }
 
 constexpr int kMatchLdsMax = 160 * 1024 - 1024;   // dynamic LDS; the kernel's static LDS needs < 1 KiB
