@@ -1289,14 +1289,21 @@ __device__ void quadtree_rounds(const DevPlan &p, const FrameBufs &fb, QLds &s, 
         // (all distinct) by rank counting: one barrier instead of a bitonic
         // network's log^2 stages; zeros (unsplittable) stay behind, in b64
         {
-            const int S2r = (S + 1) & ~1;   // a64[S] is 0 when S is odd (np2 is an even power of two)
+            // eight entries per step, their four reads issued together (one LDS
+            // round trip per step instead of per pair); a64[S, np2) is 0 and np2
+            // a power of two >= 8
+            const int S8 = (S + 7) & ~7;
             for (int i = tid; i < S; i += kThreads) {
                 const uint64_t v = s.a64[i];
                 if (v == 0) continue;
                 int r = 0;
-                for (int j = 0; j < S2r; j += 2) {
-                    const ulonglong2 w = *reinterpret_cast<const ulonglong2 *>(s.a64 + j);
-                    r += (w.x > v) + (w.y > v);
+                for (int j = 0; j < S8; j += 8) {
+                    const ulonglong2 w0 = *reinterpret_cast<const ulonglong2 *>(s.a64 + j);
+                    const ulonglong2 w1 = *reinterpret_cast<const ulonglong2 *>(s.a64 + j + 2);
+                    const ulonglong2 w2 = *reinterpret_cast<const ulonglong2 *>(s.a64 + j + 4);
+                    const ulonglong2 w3 = *reinterpret_cast<const ulonglong2 *>(s.a64 + j + 6);
+                    r += (w0.x > v) + (w0.y > v) + (w1.x > v) + (w1.y > v) + (w2.x > v) + (w2.y > v) +
+                         (w3.x > v) + (w3.y > v);
                 }
                 s.b64[r] = v;
             }
