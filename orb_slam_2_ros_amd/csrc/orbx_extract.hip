@@ -1120,6 +1120,14 @@ __device__ inline void zero_children(const QLds &s, int S) {
     for (int i = threadIdx.x; i < 4 * S; i += kThreads) { s.ccnt[i] = 0; s.cbest[i] = 0; }
 }
 
+// A node that keeps its keys maps all four quadrant slots to its new index,
+// so a key's next node is one read, nidx_c[4 node + quadrant], split or not
+// (an unsplit node's keys carry a stale quadrant; every slot agrees).
+__device__ inline void set_all_quads(int16_t *nidx_c, int i, int ni) {
+    const uint32_t v = ((uint32_t)ni & 0xFFFFu) * 0x10001u;
+    *reinterpret_cast<uint2 *>(nidx_c + 4 * i) = make_uint2(v, v);
+}
+
 __device__ inline QNode make_child(const QLds &s, const QNode &parent, int i, int q, int seq) {
     QNode c = child_of(parent, q);
     c.count = (int32_t)s.ccnt[4 * i + q];
@@ -1244,14 +1252,11 @@ __device__ void quadtree_rounds(const DevPlan &p, const FrameBufs &fb, QLds &s, 
             } else {
                 const int ni = C + (int)((pre >> 21) & 0x1FFFFF);
                 s.nxt[ni] = nd;
-                s.nidx_s[i] = (int16_t)ni;
+                set_all_quads(s.nidx_c, i, ni);
             }
         }
         __syncthreads();
-        K.each([&](int j, int k) {
-            const int nd = K.node(j, k);
-            K.set_node(j, k, s.cur[nd].count > 1 ? s.nidx_c[4 * nd + K.quad(j, k)] : s.nidx_s[nd]);
-        });
+        K.each([&](int j, int k) { K.set_node(j, k, s.nidx_c[4 * K.node(j, k) + K.quad(j, k)]); });
         zero_children(s, S2);
         {
             QNode *t = s.cur; s.cur = s.nxt; s.nxt = t;
@@ -1373,13 +1378,10 @@ __device__ void quadtree_rounds(const DevPlan &p, const FrameBufs &fb, QLds &s, 
             if (s.mark[i]) continue;
             const int ni = CC + (int)s.b64[i];
             s.nxt[ni] = s.cur[i];
-            s.nidx_s[i] = (int16_t)ni;
+            set_all_quads(s.nidx_c, i, ni);
         }
         __syncthreads();
-        K.each([&](int j, int k) {
-            const int nd = K.node(j, k);
-            K.set_node(j, k, s.mark[nd] ? s.nidx_c[4 * nd + K.quad(j, k)] : s.nidx_s[nd]);
-        });
+        K.each([&](int j, int k) { K.set_node(j, k, s.nidx_c[4 * K.node(j, k) + K.quad(j, k)]); });
         zero_children(s, S2);
         {
             QNode *t = s.cur; s.cur = s.nxt; s.nxt = t;
