@@ -1149,20 +1149,38 @@ __device__ void quadtree_rounds(const DevPlan &p, const FrameBufs &fb, QLds &s, 
 
     // ---- 2. root nodes (ORBextractor.cc:566-613)
     const int nini = g.nini;
-    for (int i = tid; i < nini; i += kThreads) { s.ccnt[i] = 0; s.cbest[i] = 0; }
-    __syncthreads();
     if (nini == 1) {
-        // one root (every 4:3 or squarer level): its count is the key count and
-        // its best key a block maximum, no per-key atomics on one address
+        // one root (every 4:3 or squarer level): every key's node is 0, its
+        // count the key count and its best key a block maximum (wave maxima
+        // through LDS: no per-key atomics, no serial pass)
+        __shared__ uint32_t ws_root[kThreads / 64];
         uint32_t bm = 0;
         K.each([&](int j, int k) {
             K.set_node(j, k, 0);
             bm = max(bm, best_pack(K.get_key(j, k), k));
         });
         bm = wave_max_u32(bm);
-        if ((tid & 63) == 0) atomicMax(&s.cbest[0], bm);
-        if (tid == 0) s.ccnt[0] = (uint32_t)K.n;
+        if ((tid & 63) == 0) ws_root[tid >> 6] = bm;
+        zero_children(s, 1);
+        __syncthreads();
+        if (tid == 0) {
+            QNode nd;
+            nd.x0 = (int16_t)(int)__fmul_rn(g.hx, 0.0f);
+            nd.x1 = (int16_t)(int)__fmul_rn(g.hx, 1.0f);
+            nd.y0 = 0;
+            nd.y1 = (int16_t)(g.h - 2 * kBorder);
+            nd.count = (int32_t)K.n;
+            uint32_t best = 0;
+            for (int w = 0; w < kThreads / 64; ++w) best = max(best, ws_root[w]);
+            nd.best = best;
+            nd.seq = 0;
+            s.cur[0] = nd;
+            sh_S = 1;
+        }
+        __syncthreads();
     } else {
+        for (int i = tid; i < nini; i += kThreads) { s.ccnt[i] = 0; s.cbest[i] = 0; }
+        __syncthreads();
         K.each([&](int j, int k) {
             const uint32_t key = K.get_key(j, k);
             const float rx = (float)((int)(key & 0xFFF) - kBorder);
@@ -1172,30 +1190,30 @@ __device__ void quadtree_rounds(const DevPlan &p, const FrameBufs &fb, QLds &s, 
             atomicAdd(&s.ccnt[r], 1u);
             atomicMax(&s.cbest[r], best_pack(key, k));
         });
-    }
-    __syncthreads();
-    if (tid == 0) {
-        int S = 0;
-        for (int r = 0; r < nini; ++r) {
-            if (s.ccnt[r] == 0) continue;
-            QNode nd;
-            nd.x0 = (int16_t)(int)__fmul_rn(g.hx, (float)r);
-            nd.x1 = (int16_t)(int)__fmul_rn(g.hx, (float)(r + 1));
-            nd.y0 = 0;
-            nd.y1 = (int16_t)(g.h - 2 * kBorder);
-            nd.count = (int32_t)s.ccnt[r];
-            nd.best = s.cbest[r];
-            nd.seq = 0;
-            s.cur[S] = nd;
-            s.nidx_s[r] = (int16_t)S;
-            ++S;
+        __syncthreads();
+        if (tid == 0) {
+            int S = 0;
+            for (int r = 0; r < nini; ++r) {
+                if (s.ccnt[r] == 0) continue;
+                QNode nd;
+                nd.x0 = (int16_t)(int)__fmul_rn(g.hx, (float)r);
+                nd.x1 = (int16_t)(int)__fmul_rn(g.hx, (float)(r + 1));
+                nd.y0 = 0;
+                nd.y1 = (int16_t)(g.h - 2 * kBorder);
+                nd.count = (int32_t)s.ccnt[r];
+                nd.best = s.cbest[r];
+                nd.seq = 0;
+                s.cur[S] = nd;
+                s.nidx_s[r] = (int16_t)S;
+                ++S;
+            }
+            sh_S = S;
         }
-        sh_S = S;
+        __syncthreads();
+        K.each([&](int j, int k) { K.set_node(j, k, s.nidx_s[K.node(j, k)]); });
+        zero_children(s, sh_S);   // (the roots' counts were read before the barrier above)
+        __syncthreads();
     }
-    __syncthreads();
-    K.each([&](int j, int k) { K.set_node(j, k, s.nidx_s[K.node(j, k)]); });
-    zero_children(s, sh_S);   // (the roots' counts were read before the barrier above)
-    __syncthreads();
     PHASE_MARK(2, 1);   // roots
 
     if (p.dbg_stop == 2) return;
