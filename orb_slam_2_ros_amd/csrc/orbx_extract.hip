@@ -1450,7 +1450,6 @@ __global__ __launch_bounds__(kThreads, 6) void k_quadtree(DevPlan p, FrameBufs f
     s.nidx_c = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * 4 * NC;
     s.nidx_s = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * NC;
     s.mark = ptr;
-    __shared__ int ws32[4];
 
     const int64_t kbase = (int64_t)b * p.cand_cap + g.cand_off;
     uint32_t *keys = fb.keys + kbase;
@@ -1464,16 +1463,35 @@ __global__ __launch_bounds__(kThreads, 6) void k_quadtree(DevPlan p, FrameBufs f
     const int ncell = g.cell_end - g.cell_begin;
     int *cell_off = reinterpret_cast<int *>(lds);            // ncell + 1
     int *cell_src = cell_off + ncell + 1;                    // slot | bit 31: minThFAST list
+    // key k's source (slot index | bit 31: minThFAST list), for the first
+    // kQuadRegKeys keys: each cell's thread writes its keys' entries right after
+    // the scan, so the keys load with one LDS read each after one barrier
+    uint32_t *kaddr = reinterpret_cast<uint32_t *>(cell_src + ncell);
+    __shared__ int ws2[2 * (kThreads / 64)];   // scan partials, alternating per chunk
     int base = 0;
-    for (int c0 = 0; c0 < ncell; c0 += kThreads) {
+    for (int c0 = 0, chunk = 0; c0 < ncell; c0 += kThreads, ++chunk) {
         const int c = c0 + tid;
-        const int word = c < ncell ? fb.cell_count[(int64_t)b * p.ncells + g.cell_begin + c] : 0;
-        const int cnt = word & 0x7FFFFFFF;
-        int tot;
-        const int ex = block_excl_scan_i32(cnt, &tot, ws32);
+        int word = 0, slot = 0;
         if (c < ncell) {
-            cell_off[c] = base + ex;
-            cell_src[c] = p.cells[g.cell_begin + c].slot | (word < 0 ? (int)0x80000000 : 0);
+            word = fb.cell_count[(int64_t)b * p.ncells + g.cell_begin + c];
+            slot = p.cells[g.cell_begin + c].slot;
+        }
+        const int cnt = word & 0x7FFFFFFF;
+        int *ws = ws2 + (chunk & 1) * (kThreads / 64);
+        const int incl = wave_incl_scan_i32(cnt);
+        if ((tid & 63) == 63) ws[tid >> 6] = incl;
+        __syncthreads();
+        int pre = 0, tot = 0;
+        for (int w = 0; w < kThreads / 64; ++w) {
+            if (w < (tid >> 6)) pre += ws[w];
+            tot += ws[w];
+        }
+        if (c < ncell) {
+            const int off = base + pre + incl - cnt;
+            const uint32_t src = (uint32_t)slot | (word < 0 ? 0x80000000u : 0u);
+            cell_off[c] = off;
+            cell_src[c] = (int)src;
+            for (int i = 0; i < cnt && off + i < kQuadRegKeys; ++i) kaddr[off + i] = src + (uint32_t)i;
         }
         base += tot;
     }
@@ -1498,18 +1516,11 @@ __global__ __launch_bounds__(kThreads, 6) void k_quadtree(DevPlan p, FrameBufs f
     };
     // up to kQRegKeys keys per thread stay in registers through the rounds
     if (n <= kQRegKeys * kThreads) {
-        // key k -> its cell by a scatter of the cell ranges (u16 per key)
-        // instead of a bisection per key
-        uint16_t *kcell = reinterpret_cast<uint16_t *>(cell_src + ncell);
-        for (int c = tid; c < ncell; c += kThreads)
-            for (int k = cell_off[c]; k < cell_off[c + 1]; ++k) kcell[k] = (uint16_t)c;
-        __syncthreads();
         QKeys<kQRegKeys> K;
         K.gkeys = nullptr; K.gnode = knode; K.gq = kq; K.n = n;
         K.each([&](int j, int k) {
-            const int c = kcell[k];
-            const int src = cell_src[c];
-            K.key[j] = ((src < 0) ? cand2 : cand)[(src & 0x7FFFFFFF) + (k - cell_off[c])];
+            const uint32_t a = kaddr[k];
+            K.key[j] = ((int)a < 0 ? cand2 : cand)[a & 0x7FFFFFFFu];
             K.nq[j] = 0;
         });
         __syncthreads();   // the cell tables are dead from here

@@ -287,10 +287,10 @@ int upload_plan(orbx_extractor *ex) {
     if (mw > 255 || mh > 255) return ORBX_EINVAL;   // survivor list packs (y << 8 | x)
     if (4 * fast_lds(mw, mh).per_wave > 64 * 1024) return ORBX_EINVAL;   // k_fast's LDS for the largest cell
     d.node_lds_bytes = quadtree_lds_bytes(node_cap);
-    // phase 1 of k_quadtree keeps two ints per cell of a level and a u16 cell
-    // index per register-held key (kQuadRegKeys per thread) in the same LDS
+    // phase 1 of k_quadtree keeps two ints per cell of a level and a u32 key
+    // source per register-held key (kQuadRegKeys in all) in the same LDS
     for (const LevelGeom &g : p.lv)
-        d.node_lds_bytes = std::max(d.node_lds_bytes, (int)(8 * (g.cell_end - g.cell_begin) + 16 + 2 * kQuadRegKeys));
+        d.node_lds_bytes = std::max(d.node_lds_bytes, (int)(8 * (g.cell_end - g.cell_begin) + 16 + 4 * kQuadRegKeys));
     d.dbg_stop = std::getenv("ORBX_DBG_STOP") ? std::atoi(std::getenv("ORBX_DBG_STOP")) : 0;
     if (d.node_lds_bytes > 160 * 1024) return ORBX_EINVAL;
     return ORBX_OK;
