@@ -1431,7 +1431,7 @@ __device__ void quadtree_rounds(const DevPlan &p, const FrameBufs &fb, QLds &s, 
 }
 
 template <bool PIPE>
-__global__ __launch_bounds__(kThreads, 6) void k_quadtree(DevPlan p, FrameBufs fb, int l0) {
+__global__ __launch_bounds__(kThreads, 7) void k_quadtree(DevPlan p, FrameBufs fb, int l0) {
     extern __shared__ __align__(16) uint8_t lds[];
     PHASE_START();
     const int l = l0 + blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
