@@ -192,7 +192,7 @@ hipError_t launch_vocab_transform(const VocabDev &v, const uint8_t *feat, int n,
                                   double *o_weight, uint32_t *o_node, hipStream_t s);
 int match_lds_bytes(int n1cap, int n2cap, int maxq, int maxc);
 int quadtree_lds_bytes(int node_cap);
-constexpr int kQuadRegKeys = 6 * 256;   // keys k_quadtree keeps in registers (6 per thread)
+constexpr int kQuadRegKeys = 8 * 256;   // keys k_quadtree can keep in registers (6 or 8 per thread)
 bool resize_window_fits(const Plan &hp);
 bool plan_resize_waves(Plan &hp);   // fills hp.rw, or leaves it empty (block kernel)
 bool plan_pyr_regions(Plan &hp);   // fills hp.rgn, or leaves rgn_n = 0

@@ -1059,7 +1059,9 @@ struct QLds {
 // The level's keys, each with its node index and quadrant.  R > 0: thread t
 // holds keys t + 256 j (j < R) in registers for the whole distribution (the
 // rounds then touch no global memory); R == 0: they stay in global scratch.
-constexpr int kQRegKeys = kQuadRegKeys / kThreads;
+// 6 keys per thread cover the bench levels (VGA level 0: ~1300 keys) in 72
+// VGPRs (7 waves per SIMD); levels up to kQuadRegKeys take 8 (with spills)
+constexpr int kQRegKeys = 6, kQRegKeysWide = kQuadRegKeys / kThreads;
 template <int R>
 struct QKeys {
     uint32_t key[R > 0 ? R : 1];
@@ -1514,9 +1516,9 @@ __global__ __launch_bounds__(kThreads, 7) void k_quadtree(DevPlan p, FrameBufs f
         const int src = cell_src[lo];
         return ((src < 0) ? cand2 : cand)[(src & 0x7FFFFFFF) + (k - cell_off[lo])];
     };
-    // up to kQRegKeys keys per thread stay in registers through the rounds
-    if (n <= kQRegKeys * kThreads) {
-        QKeys<kQRegKeys> K;
+    // up to kQRegKeys (kQRegKeysWide) keys per thread stay in registers
+    // through the rounds
+    auto in_registers = [&](auto &K) {
         K.gkeys = nullptr; K.gnode = knode; K.gq = kq; K.n = n;
         K.each([&](int j, int k) {
             const uint32_t a = kaddr[k];
@@ -1526,6 +1528,13 @@ __global__ __launch_bounds__(kThreads, 7) void k_quadtree(DevPlan p, FrameBufs f
         __syncthreads();   // the cell tables are dead from here
         PHASE_MARK(2, 0);   // gather
         quadtree_rounds(p, fb, s, g, b, l, K, phase_t_);
+    };
+    if (n <= kQRegKeys * kThreads) {
+        QKeys<kQRegKeys> K;
+        in_registers(K);
+    } else if (n <= kQRegKeysWide * kThreads) {
+        QKeys<kQRegKeysWide> K;
+        in_registers(K);
     } else {
         QKeys<0> K;
         K.gkeys = keys; K.gnode = knode; K.gq = kq; K.n = n;
