@@ -26,7 +26,15 @@ namespace orbx {
 namespace {
 
 constexpr int kGridCols = 64, kGridRows = 48;  // Frame.h:37-38
-constexpr int kGridCells = kGridCols * kGridRows;
+// The F2 grid is kept as column buckets of kBucketRows cells: a window's
+// bucket range per column holds its cells' entries in the same order (cell,
+// then index), plus entries of up to kBucketRows - 1 cells above and below
+// the window, which lie at least half a cell outside the window's rows and so
+// fail GetFeaturesInArea's |dy| < r test like any non-candidate (the list
+// positions stay monotone, which is all the tie order needs).
+constexpr int kBucketRows = 8, kColBuckets = kGridRows / kBucketRows;   // 6
+constexpr int kBuckets = kGridCols * kColBuckets;                        // 384
+static_assert(kGridRows % kBucketRows == 0, "whole buckets per column");
 constexpr int kHisto = 30;                      // ORBmatcher::HISTO_LENGTH
 constexpr int kThLow = 50;                      // ORBmatcher::TH_LOW
 constexpr int kSkip = 0xFFFF;
@@ -35,8 +43,8 @@ constexpr int kMW = kMT / 64;                   // waves
 
 // LDS layout of one frame pair, indexed by grid position (F2 octave-0
 // keypoints, < maxc) or query rank (F1 octave-0 keypoints, < maxq) only, with
-// 16-bit cell starts, distances and indices, so a pair needs ~31 KB at VGA
-// and five pairs share a CU (16-B aligned arrays first).
+// 16-bit bucket starts, distances and indices, so a pair needs ~26.6 KB at
+// VGA and six pairs share a CU (16-B aligned arrays first).
 struct MLds {
     uint4 *gd;       // maxc x 2: F2 octave-0 descriptors in grid order
     uint4 *qd;       // maxq x 2: F1 octave-0 (query) descriptors in query order
@@ -44,7 +52,8 @@ struct MLds {
     float2 *qxy;     // maxq: query centres (vbPrevMatched)
     uint32_t *top4;  // maxq x 4: (grid position << 16 | dist) of the 4 smallest (dist, list position)
     uint32_t *claim; // maxc: (replay batch << 16 | (255 - lane) << 8 | dist) of a batch's first acceptor
-    uint16_t *gstart;   // kGridCells + 1 (+1 pad): first grid position of each cell (dword-aligned pairs)
+    uint16_t *gstart;   // kBuckets + 1 (+1 pad): first grid position of each bucket (dword-aligned pairs)
+    uint16_t *gcell; // maxc: grid cell of each grid position (the in-bucket sort key)
     int16_t *mdist;  // maxc: vMatchedDistance by grid position (kNoDist: none)
     int16_t *m21;    // maxc: vnMatches21 (query rank) by grid position
     int16_t *m12;    // maxq: vnMatches12 (grid position) by query rank
@@ -64,7 +73,8 @@ __device__ inline MLds carve(uint8_t *ptr, int maxq, int maxc) {
     ptr += 8 * ((maxc + maxq) & 1);   // top4 rows are read as uint4
     s.top4 = reinterpret_cast<uint32_t *>(ptr); ptr += sizeof(uint32_t) * 4 * maxq;
     s.claim = reinterpret_cast<uint32_t *>(ptr); ptr += sizeof(uint32_t) * maxc;
-    s.gstart = reinterpret_cast<uint16_t *>(ptr); ptr += sizeof(uint16_t) * (kGridCells + 2);
+    s.gstart = reinterpret_cast<uint16_t *>(ptr); ptr += sizeof(uint16_t) * (kBuckets + 2);
+    s.gcell = reinterpret_cast<uint16_t *>(ptr); ptr += sizeof(uint16_t) * ((maxc + 1) & ~1);
     s.mdist = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * ((maxc + 1) & ~1);
     s.m21 = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * ((maxc + 1) & ~1);
     s.m12 = reinterpret_cast<int16_t *>(ptr); ptr += sizeof(int16_t) * ((maxq + 1) & ~1);
@@ -110,6 +120,10 @@ __device__ inline int block_scan_i32(int v, int *total, int *ws) {
 
 // PosInGrid (Frame.cc:415-425) for an undistorted image: round(), cell
 // ix * 48 + iy, or -1 outside the grid.
+__device__ inline int bucket_of(int cell) {
+    const int ix = cell / kGridRows;
+    return ix * kColBuckets + (cell - ix * kGridRows) / kBucketRows;
+}
 __device__ inline int grid_cell(float x, float y, float invW, float invH) {
     const int px = (int)roundf(__fmul_rn(x, invW));
     const int py = (int)roundf(__fmul_rn(y, invH));
@@ -141,7 +155,7 @@ __global__ __launch_bounds__(kMT) void k_search_init(MatchBufs mb, int maxq, int
     if (clk) { mb.clocks[0] = clock64(); mb.clocks[6] = 0; mb.clocks[7] = 0; }
 
     // ---- 0. init; every output defaults to "no match"
-    for (int i = tid; i < (kGridCells + 2) / 2; i += kMT) reinterpret_cast<uint32_t *>(s.gstart)[i] = 0;
+    for (int i = tid; i < (kBuckets + 2) / 2; i += kMT) reinterpret_cast<uint32_t *>(s.gstart)[i] = 0;
     for (int i = tid; i < maxc; i += kMT) { s.mdist[i] = kNoDist; s.m21[i] = -1; s.claim[i] = 0; }
     for (int i = tid; i < maxq; i += kMT) { s.m12[i] = -1; s.rbin[i] = -1; s.acc[i] = -1; }
     for (int i = tid; i < n1; i += kMT) {
@@ -153,27 +167,29 @@ __global__ __launch_bounds__(kMT) void k_search_init(MatchBufs mb, int maxq, int
     __syncthreads();
     if (clk) mb.clocks[1] = clock64();
 
-    // ---- 1. F2 grid of octave-0 keypoints: counts, exclusive scan, then
-    //         placement by a second atomic pass on the starts (which leaves
-    //         gstart[c] at the end of cell c, i.e. the start of c + 1)
+    // ---- 1. F2 grid of octave-0 keypoints by bucket: counts, exclusive scan,
+    //         then placement by a second atomic pass on the starts (which
+    //         leaves gstart[c] at the end of bucket c, i.e. the start of c + 1)
     for (int i = tid; i < n2; i += kMT) {
         if (k2[i].octave != 0) continue;
         const int cell = grid_cell(k2[i].x, k2[i].y, invW, invH);
-        if (cell >= 0) gstart_add(s.gstart, cell, 1);
+        if (cell >= 0) gstart_add(s.gstart, bucket_of(cell), 1);
     }
     __syncthreads();
-    constexpr int kPer = kGridCells / kMT;   // 12 cells per thread, contiguous
+    constexpr int kPer = (kBuckets + kMT - 1) / kMT;   // 2 buckets per thread, contiguous
     {
         int local = 0;
-        for (int i = 0; i < kPer; ++i) local += s.gstart[tid * kPer + i];
+        for (int i = 0; i < kPer; ++i)
+            if (tid * kPer + i < kBuckets) local += s.gstart[tid * kPer + i];
         int tot;
         int run = block_scan_i32(local, &tot, ws);
         for (int i = 0; i < kPer; ++i) {
+            if (tid * kPer + i >= kBuckets) break;
             const int v = s.gstart[tid * kPer + i];
             s.gstart[tid * kPer + i] = (uint16_t)run;
             run += v;
         }
-        if (tid == kMT - 1) s.gstart[kGridCells] = (uint16_t)min(run, 0xFFFF);
+        if (tid == kMT - 1) s.gstart[kBuckets] = (uint16_t)min(tot, 0xFFFF);
         if (tid == 0 && tot > maxc) sh_err = 1;
         __syncthreads();
     }
@@ -181,8 +197,11 @@ __global__ __launch_bounds__(kMT) void k_search_init(MatchBufs mb, int maxq, int
         if (k2[i].octave != 0) continue;
         const int cell = grid_cell(k2[i].x, k2[i].y, invW, invH);
         if (cell >= 0) {
-            const int pos = gstart_add(s.gstart, cell, 1);
-            if (pos < maxc) s.glist[pos] = (int16_t)i;
+            const int pos = gstart_add(s.gstart, bucket_of(cell), 1);
+            if (pos < maxc) {
+                s.glist[pos] = (int16_t)i;
+                s.gcell[pos] = (uint16_t)cell;
+            }
         }
     }
     __syncthreads();
@@ -191,25 +210,33 @@ __global__ __launch_bounds__(kMT) void k_search_init(MatchBufs mb, int maxq, int
 #pragma unroll
         for (int i = 0; i < kPer; ++i) {
             const int c = tid * kPer + i;
-            v[i] = c == 0 ? 0 : s.gstart[c - 1];
+            v[i] = c == 0 || c >= kBuckets ? 0 : s.gstart[c - 1];
         }
         __syncthreads();
 #pragma unroll
-        for (int i = 0; i < kPer; ++i) s.gstart[tid * kPer + i] = (uint16_t)v[i];
+        for (int i = 0; i < kPer; ++i)
+            if (tid * kPer + i < kBuckets) s.gstart[tid * kPer + i] = (uint16_t)v[i];
         __syncthreads();
     }
-    // each cell's list in keypoint-index order (mGrid push_back order)
-    for (int c = tid; c < kGridCells; c += kMT) {
-        const int st = s.gstart[c], en = min(s.gstart[c + 1], maxc);
+    // each bucket's list in (cell, keypoint index) order: mGrid's cells in
+    // window order, each in push_back (index) order
+    for (int c = tid; c < kBuckets; c += kMT) {
+        const int st = s.gstart[c], en = min((int)s.gstart[c + 1], maxc);
         for (int a = st + 1; a < en; ++a) {
             const int16_t v = s.glist[a];
+            const uint16_t vc = s.gcell[a];
             int j = a - 1;
-            while (j >= st && s.glist[j] > v) { s.glist[j + 1] = s.glist[j]; --j; }
+            while (j >= st && (s.gcell[j] > vc || (s.gcell[j] == vc && s.glist[j] > v))) {
+                s.glist[j + 1] = s.glist[j];
+                s.gcell[j + 1] = s.gcell[j];
+                --j;
+            }
             s.glist[j + 1] = v;
+            s.gcell[j + 1] = vc;
         }
     }
     __syncthreads();
-    const int ngrid = min(s.gstart[kGridCells], maxc);
+    const int ngrid = min((int)s.gstart[kBuckets], maxc);
     for (int pos = tid; pos < ngrid; pos += kMT) {
         const int i2 = s.glist[pos];
         s.gxy[pos] = make_float2(k2[i2].x, k2[i2].y);
@@ -273,8 +300,9 @@ __global__ __launch_bounds__(kMT) void k_search_init(MatchBufs mb, int maxq, int
             const uint4 qa = s.qd[2 * q], qb = s.qd[2 * q + 1];
             int pos = 0;
             for (int ix = cx0; ix <= cx1; ++ix) {
-                const int col = ix * kGridRows;
-                const int st = s.gstart[col + cy0], en = min(s.gstart[col + cy1 + 1], maxc);
+                const int col = ix * kColBuckets;
+                const int st = s.gstart[col + cy0 / kBucketRows];
+                const int en = min((int)s.gstart[col + cy1 / kBucketRows + 1], maxc);
                 for (int gp = st; gp < en; ++gp, ++pos) {
                     const int dist = entry_dist(gp, c.x, c.y, qa, qb);
                     if (dist == kSkip || pos >= maxc) continue;
@@ -400,9 +428,9 @@ __global__ __launch_bounds__(kMT) void k_search_init(MatchBufs mb, int maxq, int
                 const float2 c = s.qxy[qf];
                 int cx0, cx1, cy0, cy1, st = 0, cc = 0;
                 if (cells_of(c.x, c.y, cx0, cx1, cy0, cy1) && lane < cx1 - cx0 + 1) {
-                    const int col = (cx0 + lane) * kGridRows;
-                    st = s.gstart[col + cy0];
-                    cc = max(min(s.gstart[col + cy1 + 1], maxc) - st, 0);
+                    const int col = (cx0 + lane) * kColBuckets;
+                    st = s.gstart[col + cy0 / kBucketRows];
+                    cc = max(min((int)s.gstart[col + cy1 / kBucketRows + 1], maxc) - st, 0);
                 }
                 const int pos0 = wave_incl_scan_i32(cc) - cc;
                 const uint4 qa = s.qd[2 * qf], qb = s.qd[2 * qf + 1];
@@ -503,8 +531,8 @@ __global__ __launch_bounds__(kMT) void k_search_init(MatchBufs mb, int maxq, int
 // is indexed by query rank and grid position only).
 int match_lds_bytes(int n1cap, int n2cap, int maxq, int maxc) {
     (void)n1cap; (void)n2cap;
-    return (int)(40 * (maxc + maxq) + 8 + 16 * maxq + 4 * maxc + sizeof(uint16_t) * (kGridCells + 2) +
-                 sizeof(int16_t) * (3 * ((maxc + 1) & ~1) + 4 * ((maxq + 1) & ~1)) + maxq + 64);
+    return (int)(40 * (maxc + maxq) + 8 + 16 * maxq + 4 * maxc + sizeof(uint16_t) * (kBuckets + 2) +
+                 sizeof(int16_t) * (4 * ((maxc + 1) & ~1) + 4 * ((maxq + 1) & ~1)) + maxq + 64);
 }
 
 constexpr int kMatchLdsMax = 160 * 1024 - 1024;   // dynamic LDS; the kernel's static LDS needs < 1 KiB
