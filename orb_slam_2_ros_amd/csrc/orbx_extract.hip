@@ -1102,8 +1102,76 @@ struct QKeys {
 // Child counts / best keys of the splittable nodes.  ccnt / cbest[0, 4S)
 // were zeroed by the step that produced the current nodes (zero_children),
 // ordered by that step's closing barrier.  Ends with a barrier.
+#ifndef ORBX_QT_AGG
+#define ORBX_QT_AGG 2   // 1: lane quads only, 2: quads, then rows of 16 lanes
+#endif
+// Adds each lane's (slot, bp) to cnt[slot] += 1, best[slot] = max(., bp)
+// (slot ~0u: nothing) with LDS atomics pre-aggregated over neighbouring
+// lanes.  The quadtree's keys sit in cell order, so neighbouring lanes mostly
+// hit one slot, and same-address atomics within an instruction serialise in
+// the LDS (68 % of the kernel's cycles went there).  A lane row (16 lanes) or
+// quad whose lanes all carry one slot adds its count and maximum from its
+// first lane.  Every lane of the wave must call it (DPP).
+__device__ inline void agg_atomics(uint32_t *cnt, uint32_t *best, uint32_t slot, uint32_t bp) {
+    constexpr int kQX1 = 0xB1, kQX2 = 0x4E;   // quad_perm [1,0,3,2], [2,3,0,1]
+    uint32_t lo = min(slot, dpp_or<kQX1>(0u, slot)), hi = max(slot, dpp_or<kQX1>(0u, slot));
+    lo = min(lo, dpp_or<kQX2>(0u, lo));
+    hi = max(hi, dpp_or<kQX2>(0u, hi));
+    uint32_t b4 = max(bp, dpp_or<kQX1>(0u, bp));
+    b4 = max(b4, dpp_or<kQX2>(0u, b4));
+    const bool quad = lo == hi && slot != ~0u;   // (a mixed quad has lo < hi)
+    const int lane = (int)threadIdx.x & 63;
+#if ORBX_QT_AGG >= 2
+    constexpr int kRor4 = 0x124, kRor8 = 0x128;   // row_ror:4, row_ror:8
+    uint32_t rlo = min(lo, dpp_or<kRor4>(0u, lo)), rhi = max(hi, dpp_or<kRor4>(0u, hi));
+    rlo = min(rlo, dpp_or<kRor8>(0u, rlo));
+    rhi = max(rhi, dpp_or<kRor8>(0u, rhi));
+    uint32_t b16 = max(b4, dpp_or<kRor4>(0u, b4));
+    b16 = max(b16, dpp_or<kRor8>(0u, b16));
+    if (rlo == rhi && slot != ~0u) {
+        if ((lane & 15) == 0) {
+            atomicAdd(&cnt[slot], 16u);
+            atomicMax(&best[slot], b16);
+        }
+        return;
+    }
+#endif
+    if (quad) {
+        if ((lane & 3) == 0) {
+            atomicAdd(&cnt[slot], 4u);
+            atomicMax(&best[slot], b4);
+        }
+    } else if (slot != ~0u) {
+        atomicAdd(&cnt[slot], 1u);
+        atomicMax(&best[slot], bp);
+    }
+}
+
 template <int R>
 __device__ void child_stats(const QLds &s, QKeys<R> &K) {
+    if constexpr (R > 0) {
+        // register keys: every lane runs each register's aggregation
+        // (lanes past the key count carry slot ~0u)
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const int k = (int)threadIdx.x + j * kThreads;
+            uint32_t slot = ~0u, bp = 0;
+            if (k < K.n) {
+                const int nd = K.node(j, k);
+                const QNode node = s.cur[nd];
+                if (node.count > 1) {
+                    const uint32_t key = K.get_key(j, k);
+                    const int q = quadrant_of(node, key);
+                    K.set_quad(j, k, q);
+                    slot = 4u * (uint32_t)nd + (uint32_t)q;
+                    bp = best_pack(key, k);
+                }
+            }
+            agg_atomics(s.ccnt, s.cbest, slot, bp);
+        }
+        __syncthreads();
+        return;
+    }
     K.each([&](int j, int k) {
         const int nd = K.node(j, k);
         const QNode node = s.cur[nd];
@@ -1183,15 +1251,33 @@ __device__ void quadtree_rounds(const DevPlan &p, const FrameBufs &fb, QLds &s, 
     } else {
         for (int i = tid; i < nini; i += kThreads) { s.ccnt[i] = 0; s.cbest[i] = 0; }
         __syncthreads();
-        K.each([&](int j, int k) {
-            const uint32_t key = K.get_key(j, k);
+        auto root_of = [&](uint32_t key) {
             const float rx = (float)((int)(key & 0xFFF) - kBorder);
-            int r = (int)__fdiv_rn(rx, g.hx);
-            r = min(r, nini - 1);
-            K.set_node(j, k, r);
-            atomicAdd(&s.ccnt[r], 1u);
-            atomicMax(&s.cbest[r], best_pack(key, k));
-        });
+            return min((int)__fdiv_rn(rx, g.hx), nini - 1);
+        };
+        if constexpr (NR > 0) {
+#pragma unroll
+            for (int j = 0; j < NR; ++j) {
+                const int k = tid + j * kThreads;
+                uint32_t slot = ~0u, bp = 0;
+                if (k < K.n) {
+                    const uint32_t key = K.get_key(j, k);
+                    const int r = root_of(key);
+                    K.set_node(j, k, r);
+                    slot = (uint32_t)r;
+                    bp = best_pack(key, k);
+                }
+                agg_atomics(s.ccnt, s.cbest, slot, bp);
+            }
+        } else {
+            K.each([&](int j, int k) {
+                const uint32_t key = K.get_key(j, k);
+                const int r = root_of(key);
+                K.set_node(j, k, r);
+                atomicAdd(&s.ccnt[r], 1u);
+                atomicMax(&s.cbest[r], best_pack(key, k));
+            });
+        }
         __syncthreads();
         if (tid == 0) {
             int S = 0;
