@@ -43,11 +43,12 @@ constexpr int kMW = kMT / 64;                   // waves
 
 // LDS layout of one frame pair, indexed by grid position (F2 octave-0
 // keypoints, < maxc) or query rank (F1 octave-0 keypoints, < maxq) only, with
-// 16-bit bucket starts, distances and indices, so a pair needs ~26.6 KB at
-// VGA and six pairs share a CU (16-B aligned arrays first).
+// 16-bit bucket starts, distances and indices; the query descriptors stay in
+// global memory (each is read once, by its query's lane, into registers), so a
+// pair needs ~19 KB at VGA and eight pairs share a CU (16-B aligned arrays
+// first).
 struct MLds {
     uint4 *gd;       // maxc x 2: F2 octave-0 descriptors in grid order
-    uint4 *qd;       // maxq x 2: F1 octave-0 (query) descriptors in query order
     float2 *gxy;     // maxc: F2 positions in grid order
     float2 *qxy;     // maxq: query centres (vbPrevMatched)
     uint32_t *top4;  // maxq x 4: (grid position << 16 | dist) of the 4 smallest (dist, list position)
@@ -67,7 +68,6 @@ struct MLds {
 __device__ inline MLds carve(uint8_t *ptr, int maxq, int maxc) {
     MLds s;
     s.gd = reinterpret_cast<uint4 *>(ptr); ptr += sizeof(uint4) * 2 * maxc;
-    s.qd = reinterpret_cast<uint4 *>(ptr); ptr += sizeof(uint4) * 2 * maxq;
     s.gxy = reinterpret_cast<float2 *>(ptr); ptr += sizeof(float2) * maxc;
     s.qxy = reinterpret_cast<float2 *>(ptr); ptr += sizeof(float2) * maxq;
     ptr += 8 * ((maxc + maxq) & 1);   // top4 rows are read as uint4
@@ -257,9 +257,6 @@ __global__ __launch_bounds__(kMT) void k_search_init(MatchBufs mb, int maxq, int
             if (run < maxq) {
                 s.qidx[run] = (int16_t)i;
                 s.qxy[run] = make_float2(prev[2 * i], prev[2 * i + 1]);
-                const uint4 *dp = reinterpret_cast<const uint4 *>(d1 + (int64_t)i * 32);
-                s.qd[2 * run] = dp[0];
-                s.qd[2 * run + 1] = dp[1];
             }
             ++run;
         }
@@ -297,7 +294,8 @@ __global__ __launch_bounds__(kMT) void k_search_init(MatchBufs mb, int maxq, int
         int cx0, cx1, cy0, cy1;
         const float2 c = s.qxy[q];
         if (cells_of(c.x, c.y, cx0, cx1, cy0, cy1)) {
-            const uint4 qa = s.qd[2 * q], qb = s.qd[2 * q + 1];
+            const uint4 *qp = reinterpret_cast<const uint4 *>(d1 + (int64_t)s.qidx[q] * 32);
+            const uint4 qa = qp[0], qb = qp[1];
             int pos = 0;
             for (int ix = cx0; ix <= cx1; ++ix) {
                 const int col = ix * kColBuckets;
@@ -433,7 +431,8 @@ __global__ __launch_bounds__(kMT) void k_search_init(MatchBufs mb, int maxq, int
                     cc = max(min((int)s.gstart[col + cy1 / kBucketRows + 1], maxc) - st, 0);
                 }
                 const int pos0 = wave_incl_scan_i32(cc) - cc;
-                const uint4 qa = s.qd[2 * qf], qb = s.qd[2 * qf + 1];
+                const uint4 *qp = reinterpret_cast<const uint4 *>(d1 + (int64_t)s.qidx[qf] * 32);
+                const uint4 qa = qp[0], qb = qp[1];
                 uint32_t k1 = ~0u;
                 int d2 = INT_MAX, ga = 0;
                 for (int e = 0; e < cc; ++e) {
@@ -531,7 +530,7 @@ __global__ __launch_bounds__(kMT) void k_search_init(MatchBufs mb, int maxq, int
 // is indexed by query rank and grid position only).
 int match_lds_bytes(int n1cap, int n2cap, int maxq, int maxc) {
     (void)n1cap; (void)n2cap;
-    return (int)(40 * (maxc + maxq) + 8 + 16 * maxq + 4 * maxc + sizeof(uint16_t) * (kBuckets + 2) +
+    return (int)(40 * maxc + 8 * maxq + 8 + 16 * maxq + 4 * maxc + sizeof(uint16_t) * (kBuckets + 2) +
                  sizeof(int16_t) * (4 * ((maxc + 1) & ~1) + 4 * ((maxq + 1) & ~1)) + maxq + 64);
 }
 
