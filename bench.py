@@ -800,6 +800,12 @@ EXTRA_SPLIT = {}
 # EuRoC 98.5 / 108.2 k, KITTI 62.0 / 67.3 k
 EXTRA_PIPE = {"stereo_fhd_1920x1080": 1}
 HEADLINE_PIPE = 1
+# Batch split of the VGA headline: with the quadtree's child counts aggregated
+# (0.61 -> 0.38 ms) there is less latency-bound work to hide behind the other
+# half, and one launch per stage measured faster on one box over two rounds
+# (split / pipeline 1/1: 375.8-376.3 k, 2/1: 373.7-374.2 k, 2/0: 372.2-373.1 k,
+# 1/0: 369.0-370.4 k frames/s; profiles/r03_split_sweep.txt)
+HEADLINE_SPLIT = 1
 
 # Config C5 (BASELINE.json configs[4]): 64 FHD RGB-D streams over the job's
 # GPUs (stream s -> rank s mod G), plus the cross-stream keyframe exchange.
@@ -977,8 +983,8 @@ def main() -> int:
     w, h, nf, B = args.width, args.height, args.nfeatures, args.batch
     streams = stream_partition(B * world, world, rank)          # weak scaling: B streams per GPU
     el, stages, nkp_last, nm_last, frames_per_launch, ex = run_config(
-        torch, dist, rank, world, dev, w, h, nf, streams, args.steps, args.warmup, profile, "mono", stub(w, h), 2,
-        HEADLINE_PIPE)
+        torch, dist, rank, world, dev, w, h, nf, streams, args.steps, args.warmup, profile, "mono", stub(w, h),
+        HEADLINE_SPLIT, HEADLINE_PIPE)
     ex.close()
     frames_total = world * B * args.steps
     value = frames_total / el

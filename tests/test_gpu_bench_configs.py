@@ -49,18 +49,18 @@ def _frames(torch, mode, w, h, streams):
     return host, depth, fr, dm
 
 
-def test_mono_bench_config_b3072_split2(oracle_mod):
-    """The headline timed region: 3072 VGA streams, split 2, level pipeline on,
-    two steps (the second matches against the first)."""
+def test_mono_bench_config_b3072(oracle_mod):
+    """The headline timed region: 3072 VGA streams, split and level pipeline as
+    bench.py runs them, two steps (the second matches against the first)."""
     import torch
     w, h, B = 640, 480, 3072
     streams = list(range(B))
     host, _, fr, _ = _frames(torch, "mono", w, h, streams)
     ex = ORBextractor(1000, 1.2, 8, 20, 7)
     ex.reserve(w, h, B)
-    ex.split(2)
+    ex.split(bench.HEADLINE_SPLIT)
     ex.pipeline(bench.HEADLINE_PIPE)   # (as bench.py times it)
-    assert ex.split() == 2
+    assert ex.split() == bench.HEADLINE_SPLIT
     for t in range(2):
         ex.mono_step_device(fr[t].data_ptr(), w * h, w, B, 100, 0.9, True)
     torch.cuda.synchronize()
