@@ -1169,20 +1169,27 @@ __device__ void child_stats(const QLds &s, QKeys<R> &K) {
             }
             agg_atomics(s.ccnt, s.cbest, slot, bp);
         }
-        __syncthreads();
-        return;
-    }
-    K.each([&](int j, int k) {
-        const int nd = K.node(j, k);
-        const QNode node = s.cur[nd];
-        if (node.count > 1) {
-            const uint32_t key = K.get_key(j, k);
-            const int q = quadrant_of(node, key);
-            K.set_quad(j, k, q);
-            atomicAdd(&s.ccnt[4 * nd + q], 1u);
-            atomicMax(&s.cbest[4 * nd + q], best_pack(key, k));
+    } else {
+        // keys in global scratch (levels past kQuadRegKeys, e.g. FHD's first
+        // ones): the block steps through them together, so every lane of a
+        // wave reaches the aggregation
+        for (int k0 = 0; k0 < K.n; k0 += kThreads) {
+            const int k = k0 + (int)threadIdx.x;
+            uint32_t slot = ~0u, bp = 0;
+            if (k < K.n) {
+                const int nd = K.node(0, k);
+                const QNode node = s.cur[nd];
+                if (node.count > 1) {
+                    const uint32_t key = K.get_key(0, k);
+                    const int q = quadrant_of(node, key);
+                    K.set_quad(0, k, q);
+                    slot = 4u * (uint32_t)nd + (uint32_t)q;
+                    bp = best_pack(key, k);
+                }
+            }
+            agg_atomics(s.ccnt, s.cbest, slot, bp);
         }
-    });
+    }
     __syncthreads();
 }
 
@@ -1270,13 +1277,18 @@ __device__ void quadtree_rounds(const DevPlan &p, const FrameBufs &fb, QLds &s, 
                 agg_atomics(s.ccnt, s.cbest, slot, bp);
             }
         } else {
-            K.each([&](int j, int k) {
-                const uint32_t key = K.get_key(j, k);
-                const int r = root_of(key);
-                K.set_node(j, k, r);
-                atomicAdd(&s.ccnt[r], 1u);
-                atomicMax(&s.cbest[r], best_pack(key, k));
-            });
+            for (int k0 = 0; k0 < K.n; k0 += kThreads) {
+                const int k = k0 + tid;
+                uint32_t slot = ~0u, bp = 0;
+                if (k < K.n) {
+                    const uint32_t key = K.get_key(0, k);
+                    const int r = root_of(key);
+                    K.set_node(0, k, r);
+                    slot = (uint32_t)r;
+                    bp = best_pack(key, k);
+                }
+                agg_atomics(s.ccnt, s.cbest, slot, bp);
+            }
         }
         __syncthreads();
         if (tid == 0) {
