@@ -264,3 +264,37 @@ def test_cpp_dropin_adapter_end_to_end(tmp_path, oracle_mod):
     assert nm == nm_o and np.array_equal(m12, m_o) and np.array_equal(prev, prev_o)
     ref1 = np.pad(oracle_mod.pyramid(fr[1])[1], 19, mode="reflect")   # numpy "reflect" == REFLECT_101
     assert np.array_equal(lvl1, ref1)
+
+
+def _clustered(w, h, seed, kind):
+    """synth.frame with the texture kept only in one region (flat grey elsewhere),
+    so the quadtree's keys crowd one child (whole lane quads / rows / waves on
+    one counter slot) or straddle a split line (mixed quads)."""
+    img = synth.frame(w, h, seed).copy()
+    keep = np.zeros((h, w), bool)
+    if kind == "quadrant":      # top-left quarter only: round 1 puts every key in one child,
+        keep[: h // 2, : w // 2] = True   # the node count stays 1 and the level keeps one key
+    elif kind == "corner":      # left 30 %, top 70 %: two children, one holding most keys
+        keep[: int(0.7 * h), : int(0.3 * w)] = True
+    elif kind == "stripe":      # a vertical band across the first split line
+        keep[:, int(0.45 * w): int(0.55 * w) + 1] = True
+    else:                       # a horizontal band across the other split line
+        keep[int(0.45 * h): int(0.55 * h) + 1, :] = True
+    img[~keep] = 128
+    return img
+
+
+@pytest.mark.parametrize("w,h,nfeat", [(640, 480, 1000), (1241, 376, 2000), (1920, 1080, 1000)])
+@pytest.mark.parametrize("kind", ["quadrant", "corner", "stripe", "band"])
+def test_quadtree_clustered_keys(w, h, nfeat, kind, extractors, oracle_mod):
+    """k_quadtree's child / root counts are summed over lane quads and rows before
+    their LDS atomics (register keys at VGA, the wide register path and three
+    roots at KITTI, global-scratch keys and two roots at FHD); clustered and
+    split-straddling keys exercise the uniform and the mixed groups."""
+    img = _clustered(w, h, 41, kind)
+    kg, dg = extractors(nfeat)(img)
+    ko, do = oracle_mod.extract(img, nfeat)
+    assert len(kg) == len(ko) and len(ko) > 0
+    for f in ko.dtype.names:
+        assert np.array_equal(kg[f], ko[f]), f"keypoint field {f} differs at {_first_diff(kg[f], ko[f])}"
+    assert np.array_equal(dg, do), f"descriptors differ at {_first_diff(dg, do)}"
