@@ -216,6 +216,18 @@ int orbx_search_for_initialization(int device, const orbx_keypoint *k1, const ui
                                    int n1, const orbx_keypoint *k2, const uint8_t *d2, int n2,
                                    int img_w, int img_h, float *prev_xy, int32_t *matches12,
                                    int window, float nnratio, int check_ori, int *nmatches);
+/* The same over the Frame's image bounds (mnMinX, mnMaxX, mnMinY, mnMaxY,
+ * Frame::ComputeImageBounds, Frame.cc:475-499): a distorted camera's bounds
+ * are non-zero and non-integer, and the grid is PosInGrid's
+ * round((x - mnMinX) * mfGridElementWidthInv) (Frame.cc:415-425) with
+ * GetFeaturesInArea's floor / ceil((x - mnMinX -/+ r) * inv) windows
+ * (:361-373).  orbx_search_for_initialization is this with (0, img_w, 0, img_h).
+ * ORBX_EINVAL unless max > min on both axes. */
+int orbx_search_for_initialization_bounds(int device, const orbx_keypoint *k1, const uint8_t *d1, int n1,
+                                          const orbx_keypoint *k2, const uint8_t *d2, int n2, float min_x,
+                                          float max_x, float min_y, float max_y, float *prev_xy,
+                                          int32_t *matches12, int window, float nnratio, int check_ori,
+                                          int *nmatches);
 
 /* ORBmatcher projection searches: SearchByProjection x4 and the candidate
  * search of Fuse x2 (ORBmatcher.cc:45-129, 291-404, 827-1102, 1330-1601).

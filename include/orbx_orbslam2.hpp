@@ -149,10 +149,22 @@ struct OrbxMatcher {
     }
 
     // ORBmatcher.cc:406-521 for frames given by (mvKeysUn, mDescriptors) and the
-    // undistorted image size that sizes Frame's 64x48 grid.
+    // undistorted image size that sizes Frame's 64x48 grid (mnMinX = mnMinY = 0).
     static int SearchForInitialization(const std::vector<cv::KeyPoint> &keys1, const cv::Mat &desc1,
                                        const std::vector<cv::KeyPoint> &keys2, const cv::Mat &desc2, int img_w,
                                        int img_h, std::vector<cv::Point2f> &vbPrevMatched,
+                                       std::vector<int> &vnMatches12, int windowSize, float nnratio,
+                                       bool checkOri) {
+        return SearchForInitialization(keys1, desc1, keys2, desc2, 0.f, (float)img_w, 0.f, (float)img_h,
+                                       vbPrevMatched, vnMatches12, windowSize, nnratio, checkOri);
+    }
+
+    // The same over the Frame's grid bounds mnMinX, mnMaxX, mnMinY, mnMaxY
+    // (Frame::ComputeImageBounds, Frame.cc:475-499: non-zero and non-integer
+    // for a distorted camera).
+    static int SearchForInitialization(const std::vector<cv::KeyPoint> &keys1, const cv::Mat &desc1,
+                                       const std::vector<cv::KeyPoint> &keys2, const cv::Mat &desc2, float min_x,
+                                       float max_x, float min_y, float max_y, std::vector<cv::Point2f> &vbPrevMatched,
                                        std::vector<int> &vnMatches12, int windowSize, float nnratio,
                                        bool checkOri) {
         const std::vector<orbx_keypoint> k1 = orbx_detail::pack(keys1), k2 = orbx_detail::pack(keys2);
@@ -162,10 +174,11 @@ struct OrbxMatcher {
         for (size_t i = 0; i < keys1.size(); ++i) { prev[2 * i] = vbPrevMatched[i].x; prev[2 * i + 1] = vbPrevMatched[i].y; }
         vnMatches12.assign(keys1.size(), -1);
         int nm = 0;
-        orbx_detail::check(orbx_search_for_initialization(orbx_detail::device_index(), k1.data(), d1.data,
-                                                          (int)k1.size(), k2.data(), d2.data, (int)k2.size(),
-                                                          img_w, img_h, prev.data(), vnMatches12.data(),
-                                                          windowSize, nnratio, checkOri ? 1 : 0, &nm),
+        orbx_detail::check(orbx_search_for_initialization_bounds(orbx_detail::device_index(), k1.data(), d1.data,
+                                                                 (int)k1.size(), k2.data(), d2.data, (int)k2.size(),
+                                                                 min_x, max_x, min_y, max_y, prev.data(),
+                                                                 vnMatches12.data(), windowSize, nnratio,
+                                                                 checkOri ? 1 : 0, &nm),
                            "SearchForInitialization");
         for (size_t i = 0; i < keys1.size(); ++i) vbPrevMatched[i] = cv::Point2f(prev[2 * i], prev[2 * i + 1]);
         return nm;

@@ -186,12 +186,12 @@ int ORBmatcher::SearchByBoW(KeyFrame *pKF1, KeyFrame *pKF2, std::vector<MapPoint
     return n;
 }
 
-// ---- SearchForInitialization  ORBmatcher.cc:406-521 (undistorted cameras: mnMinX == 0)
+// ---- SearchForInitialization  ORBmatcher.cc:406-521 (F2's grid: its bounds mnMinX..mnMaxY, Frame.cc:475-499)
 int ORBmatcher::SearchForInitialization(Frame &F1, Frame &F2, std::vector<cv::Point2f> &vbPrevMatched,
                                         std::vector<int> &vnMatches12, int windowSize) {
     return OrbxMatcher::SearchForInitialization(F1.mvKeysUn, F1.mDescriptors, F2.mvKeysUn, F2.mDescriptors,
-                                                (int)(F1.mnMaxX - F1.mnMinX), (int)(F1.mnMaxY - F1.mnMinY),
-                                                vbPrevMatched, vnMatches12, windowSize, mfNNratio, mbCheckOrientation);
+                                                F2.mnMinX, F2.mnMaxX, F2.mnMinY, F2.mnMaxY, vbPrevMatched,
+                                                vnMatches12, windowSize, mfNNratio, mbCheckOrientation);
 }
 
 // ---- SearchForTriangulation  ORBmatcher.cc:659-825

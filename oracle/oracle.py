@@ -39,6 +39,7 @@ _SIG = {
     "orbo_distribute": (I32, [P, I32, I32, I32, I32, P]),
     "orbo_extract": (I32, [P, I32, I32, SZ, I32, F32, I32, I32, I32, P, P, I32, P]),
     "orbo_search_for_initialization": (I32, [P, P, I32, P, P, I32, I32, I32, P, P, I32, F32, I32]),
+    "orbo_search_for_initialization_bounds": (I32, [P, P, I32, P, P, I32, F32, F32, F32, F32, P, P, I32, F32, I32]),
     "orbo_compute_stereo_matches": (I32, [P, P, P, P, I32, P, P, P, P, I32, P, P, I32, F32, F32, P, P]),
     "orbo_stereo_from_rgbd": (None, [P, P, I32, P, I32, I32, SZ, F32, P, P]),
 }
@@ -178,13 +179,20 @@ def extract(img: np.ndarray, nfeatures=1000, scale=1.2, nlevels=8, ini=20, mn=7)
     return kps[:n.value].copy(), desc[:n.value].copy()
 
 
-def search_for_initialization(k1, d1, k2, d2, w, h, prev_xy, window=100, nnratio=0.9, check_ori=True):
+def search_for_initialization(k1, d1, k2, d2, w, h, prev_xy, window=100, nnratio=0.9, check_ori=True,
+                              bounds=None):
+    """bounds: (mnMinX, mnMaxX, mnMinY, mnMaxY); None = (0, w, 0, h)."""
     k1 = np.ascontiguousarray(k1, KEYPOINT_DTYPE); k2 = np.ascontiguousarray(k2, KEYPOINT_DTYPE)
     d1 = np.ascontiguousarray(d1, np.uint8); d2 = np.ascontiguousarray(d2, np.uint8)
     prev = np.ascontiguousarray(prev_xy, np.float32).copy()
     m12 = np.full(max(len(k1), 1), -1, np.int32)
-    nm = lib().orbo_search_for_initialization(_p(k1), _p(d1), len(k1), _p(k2), _p(d2), len(k2), w, h,
-                                              _p(prev), _p(m12), window, nnratio, int(check_ori))
+    if bounds is None:
+        nm = lib().orbo_search_for_initialization(_p(k1), _p(d1), len(k1), _p(k2), _p(d2), len(k2), w, h,
+                                                  _p(prev), _p(m12), window, nnratio, int(check_ori))
+    else:
+        nm = lib().orbo_search_for_initialization_bounds(_p(k1), _p(d1), len(k1), _p(k2), _p(d2), len(k2),
+                                                         *[float(b) for b in bounds], _p(prev), _p(m12), window,
+                                                         nnratio, int(check_ori))
     return nm, m12[:len(k1)].copy(), prev
 
 

@@ -746,8 +746,16 @@ int orbo_search_for_initialization(const orbo_keypoint *k1, const uint8_t *d1, i
                                    const orbo_keypoint *k2, const uint8_t *d2, int n2,
                                    int img_w, int img_h, float *prev_xy, int32_t *m12,
                                    int window, float nnratio, int check_ori) {
+    return orbo_search_for_initialization_bounds(k1, d1, n1, k2, d2, n2, 0.f, (float)img_w, 0.f, (float)img_h,
+                                                 prev_xy, m12, window, nnratio, check_ori);
+}
+
+// The grid over the Frame's image bounds (static mnMinX .. mnMaxY, Frame.cc:475-499).
+int orbo_search_for_initialization_bounds(const orbo_keypoint *k1, const uint8_t *d1, int n1,
+                                          const orbo_keypoint *k2, const uint8_t *d2, int n2,
+                                          float minX, float maxX, float minY, float maxY, float *prev_xy,
+                                          int32_t *m12, int window, float nnratio, int check_ori) {
     const int GC = 64, GR = 48, HL = 30, TH_LOW = 50;
-    const float minX = 0.f, maxX = (float)img_w, minY = 0.f, maxY = (float)img_h;
     const float invW = (float)GC / (maxX - minX), invH = (float)GR / (maxY - minY);
     std::vector<std::vector<int>> grid((size_t)GC * GR);
     for (int i = 0; i < n2; ++i) {

@@ -85,6 +85,13 @@ int   orbo_search_for_initialization(const orbo_keypoint *k1, const uint8_t *d1,
                                      int img_w, int img_h,
                                      float *prev_xy, int32_t *matches12,
                                      int window, float nnratio, int check_ori);
+/* The same over explicit bounds (mnMinX, mnMaxX, mnMinY, mnMaxY; a distorted
+ * camera's, Frame::ComputeImageBounds, Frame.cc:475-499). */
+int   orbo_search_for_initialization_bounds(const orbo_keypoint *k1, const uint8_t *d1, int n1,
+                                            const orbo_keypoint *k2, const uint8_t *d2, int n2,
+                                            float min_x, float max_x, float min_y, float max_y,
+                                            float *prev_xy, int32_t *matches12,
+                                            int window, float nnratio, int check_ori);
 
 /* ---- stereo (Frame::ComputeStereoMatches, Frame.cc:502-676) ----
  * pyrL / pyrR: all levels packed as orbo_pyramid writes them, level sizes

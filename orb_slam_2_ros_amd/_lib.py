@@ -116,6 +116,8 @@ _SIGNATURES = {
     "orbx_search_by_bow": (I32, [I32, I32, P, P, F32, I32, P, I32, P, P, P]),
     "orbx_descriptor_distance": (I32, [P, P]),
     "orbx_search_for_initialization": (I32, [I32, P, P, I32, P, P, I32, I32, I32, P, P, I32, F32, I32, P]),
+    "orbx_search_for_initialization_bounds": (I32, [I32, P, P, I32, P, P, I32, F32, F32, F32, F32, P, P, I32, F32,
+                                                    I32, P]),
     "orbx_debug_trig": (I32, [I32, P, P, P, I32, P, P, P, I32]),
     "orbx_vocab_create": (I32, [I32, I32, I32, I32, I32, I32, P, P, P, P, P]),
     "orbx_vocab_load": (I32, [I32, ctypes.c_char_p, I32, P]),

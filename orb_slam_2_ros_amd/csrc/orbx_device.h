@@ -78,7 +78,8 @@ struct MatchBufs {
     float *prev_xy;           // B * k1_stride * 2, in/out
     int32_t *matches12;       // B * k1_stride
     int32_t *nmatches;        // B
-    int img_w, img_h, window;
+    float min_x, max_x, min_y, max_y;   // mnMinX, mnMaxX, mnMinY, mnMaxY: the 64 x 48 grid
+    int window;
     float nnratio;
     int check_ori;
     int reset_prev;           // 1: prev_xy := F1 keypoint positions before matching

@@ -8,7 +8,8 @@
 //   k_describe (one wave/kp)  IC_Angle + computeOrbDescriptor + scaling,
 //                             ORBextractor.cc:77-147, 1116-1148
 // Every launch covers a whole batch of frames (grid.y / grid.z = frame).
-// All of this is integer / byte work bound by HBM or by latency; no MFMA.
+// Integer / byte work bound by HBM, VALU issue or latency; k_describe runs its
+// orientation moments and blur row pass as int8 MFMAs (15 per keypoint).
 #include <hip/hip_runtime.h>
 
 #include "orbx_device.h"

@@ -664,9 +664,11 @@ int detect(orbx_kfdb *db, bool reloc, uint64_t qid, const uint32_t *words, const
     auto fail_scratch = [&]() {
         (void)hipGetLastError();
         (void)hipStreamSynchronize(ws.st);
-        (void)hipMemset(db->d_qcnt, 0, sizeof(*db->d_qcnt) * (size_t)ns);
-        (void)hipMemset(db->d_qfirst, 0xFF, sizeof(*db->d_qfirst) * (size_t)ns);
-        (void)hipDeviceSynchronize();
+        // (on the query's own stream: no legacy-stream or device-wide sync that
+        // could break another thread's graph capture)
+        (void)hipMemsetAsync(db->d_qcnt, 0, sizeof(*db->d_qcnt) * (size_t)ns, ws.st);
+        (void)hipMemsetAsync(db->d_qfirst, 0xFF, sizeof(*db->d_qfirst) * (size_t)ns, ws.st);
+        (void)hipStreamSynchronize(ws.st);
         return ORBX_EIO;
     };
     if (hipGetLastError() != hipSuccess ||

@@ -124,9 +124,9 @@ __device__ inline int bucket_of(int cell) {
     const int ix = cell / kGridRows;
     return ix * kColBuckets + (cell - ix * kGridRows) / kBucketRows;
 }
-__device__ inline int grid_cell(float x, float y, float invW, float invH) {
-    const int px = (int)roundf(__fmul_rn(x, invW));
-    const int py = (int)roundf(__fmul_rn(y, invH));
+__device__ inline int grid_cell(float x, float y, float minX, float minY, float invW, float invH) {
+    const int px = (int)roundf(__fmul_rn(__fsub_rn(x, minX), invW));
+    const int py = (int)roundf(__fmul_rn(__fsub_rn(y, minY), invH));
     return (px >= 0 && px < kGridCols && py >= 0 && py < kGridRows) ? px * kGridRows + py : -1;
 }
 
@@ -146,10 +146,11 @@ __global__ __launch_bounds__(kMT) void k_search_init(MatchBufs mb, int maxq, int
     __shared__ int sh_top[3];
     __shared__ int sh_err, sh_nq;
 
-    // Frame grid constants for an undistorted img_w x img_h image
-    // (Frame.cc:218-220, ComputeImageBounds with k1 == 0: minX = minY = 0).
-    const float invW = __fdiv_rn((float)kGridCols, (float)mb.img_w);
-    const float invH = __fdiv_rn((float)kGridRows, (float)mb.img_h);
+    // Frame grid constants (Frame.cc:218-221 over ComputeImageBounds, :487-497;
+    // an undistorted camera has minX = minY = 0, maxX / maxY the image size)
+    const float minX = mb.min_x, minY = mb.min_y;
+    const float invW = __fdiv_rn((float)kGridCols, __fsub_rn(mb.max_x, minX));
+    const float invH = __fdiv_rn((float)kGridRows, __fsub_rn(mb.max_y, minY));
     const float r = (float)mb.window;
     const bool clk = mb.clocks && b == 0 && tid == 0;
     if (clk) { mb.clocks[0] = clock64(); mb.clocks[6] = 0; mb.clocks[7] = 0; }
@@ -172,7 +173,7 @@ __global__ __launch_bounds__(kMT) void k_search_init(MatchBufs mb, int maxq, int
     //         leaves gstart[c] at the end of bucket c, i.e. the start of c + 1)
     for (int i = tid; i < n2; i += kMT) {
         if (k2[i].octave != 0) continue;
-        const int cell = grid_cell(k2[i].x, k2[i].y, invW, invH);
+        const int cell = grid_cell(k2[i].x, k2[i].y, minX, minY, invW, invH);
         if (cell >= 0) gstart_add(s.gstart, bucket_of(cell), 1);
     }
     __syncthreads();
@@ -195,7 +196,7 @@ __global__ __launch_bounds__(kMT) void k_search_init(MatchBufs mb, int maxq, int
     }
     for (int i = tid; i < n2; i += kMT) {
         if (k2[i].octave != 0) continue;
-        const int cell = grid_cell(k2[i].x, k2[i].y, invW, invH);
+        const int cell = grid_cell(k2[i].x, k2[i].y, minX, minY, invW, invH);
         if (cell >= 0) {
             const int pos = gstart_add(s.gstart, bucket_of(cell), 1);
             if (pos < maxc) {
@@ -268,10 +269,11 @@ __global__ __launch_bounds__(kMT) void k_search_init(MatchBufs mb, int maxq, int
 
     // GetFeaturesInArea's cell window (Frame.cc:354-412) of a query centre
     auto cells_of = [&](float x, float y, int &cx0, int &cx1, int &cy0, int &cy1) {
-        cx0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(x, r), invW)));
-        cx1 = min(kGridCols - 1, (int)ceilf(__fmul_rn(__fadd_rn(x, r), invW)));
-        cy0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(y, r), invH)));
-        cy1 = min(kGridRows - 1, (int)ceilf(__fmul_rn(__fadd_rn(y, r), invH)));
+        const float ux = __fsub_rn(x, minX), uy = __fsub_rn(y, minY);   // (x - mnMinX) -/+ r, Frame.cc:361-373
+        cx0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(ux, r), invW)));
+        cx1 = min(kGridCols - 1, (int)ceilf(__fmul_rn(__fadd_rn(ux, r), invW)));
+        cy0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(uy, r), invH)));
+        cy1 = min(kGridRows - 1, (int)ceilf(__fmul_rn(__fadd_rn(uy, r), invH)));
         return !(cx0 >= kGridCols || cx1 < 0 || cy0 >= kGridRows || cy1 < 0 || cx1 < cx0 || cy1 < cy0);
     };
     // distance of grid entry gp to query q's descriptor; kSkip outside the window

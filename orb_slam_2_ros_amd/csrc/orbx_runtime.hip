@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <atomic>
@@ -187,6 +188,7 @@ struct orbx_extractor {
     void release() {
         if (host_graph) (void)hipGraphExecDestroy(host_graph);
         host_graph = nullptr;
+        host_result_valid = false;   // the result slots are freed: h_out no longer mirrors slot 0
         graph_w = graph_h = 0;
         dfree(d_tables); dfree(d_pyr); dfree(d_blur); dfree(d_cand); dfree(d_cand2); dfree(d_keys); dfree(d_sel);
         dfree(d_cell_count); dfree(d_level_count); dfree(d_key_node); dfree(d_key_q);
@@ -1120,8 +1122,8 @@ int orbx_mono_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t f
     mb.prev_xy = ex->d_prev;
     mb.matches12 = ex->d_m12;
     mb.nmatches = ex->d_nmatch;
-    mb.img_w = ex->plan.width;
-    mb.img_h = ex->plan.height;
+    mb.min_x = 0.f; mb.max_x = (float)ex->plan.width;    // undistorted frames (Frame.cc:495-497)
+    mb.min_y = 0.f; mb.max_y = (float)ex->plan.height;
     mb.window = window;
     mb.nnratio = nnratio;
     mb.check_ori = check_ori;
@@ -1442,7 +1444,20 @@ int orbx_search_for_initialization(int device, const orbx_keypoint *k1, const ui
                                    const orbx_keypoint *k2, const uint8_t *d2, int n2, int img_w, int img_h,
                                    float *prev_xy, int32_t *matches12, int window, float nnratio, int check_ori,
                                    int *nmatches) {
-    if (n1 < 0 || n2 < 0 || n1 > 32767 || n2 > 32767 || img_w <= 0 || img_h <= 0 || !nmatches) return ORBX_EINVAL;
+    if (img_w <= 0 || img_h <= 0) return ORBX_EINVAL;
+    return orbx_search_for_initialization_bounds(device, k1, d1, n1, k2, d2, n2, 0.f, (float)img_w, 0.f,
+                                                 (float)img_h, prev_xy, matches12, window, nnratio, check_ori,
+                                                 nmatches);
+}
+
+int orbx_search_for_initialization_bounds(int device, const orbx_keypoint *k1, const uint8_t *d1, int n1,
+                                          const orbx_keypoint *k2, const uint8_t *d2, int n2, float min_x,
+                                          float max_x, float min_y, float max_y, float *prev_xy, int32_t *matches12,
+                                          int window, float nnratio, int check_ori, int *nmatches) {
+    if (n1 < 0 || n2 < 0 || n1 > 32767 || n2 > 32767 || !nmatches) return ORBX_EINVAL;
+    if (!(max_x > min_x) || !(max_y > min_y) || !std::isfinite(min_x) || !std::isfinite(max_x) ||
+        !std::isfinite(min_y) || !std::isfinite(max_y))
+        return ORBX_EINVAL;
     if ((n1 && (!k1 || !d1 || !prev_xy || !matches12)) || (n2 && (!k2 || !d2))) return ORBX_EINVAL;
     if (hipSetDevice(device) != hipSuccess) return ORBX_ENODEV;
     int q = 0, c = 0;
@@ -1476,7 +1491,8 @@ int orbx_search_for_initialization(int device, const orbx_keypoint *k1, const ui
     mb.k1 = at<orbx_keypoint>(D, o_k1); mb.d1 = D + o_d1; mb.n1 = at<int32_t>(D, o_ns); mb.k1_stride = n1c;
     mb.k2 = at<orbx_keypoint>(D, o_k2); mb.d2 = D + o_d2; mb.n2 = at<int32_t>(D, o_ns) + 1; mb.k2_stride = n2c;
     mb.prev_xy = at<float>(D, o_prev); mb.matches12 = at<int32_t>(D, o_m); mb.nmatches = at<int32_t>(D, o_nm);
-    mb.img_w = img_w; mb.img_h = img_h; mb.window = window; mb.nnratio = nnratio;
+    mb.min_x = min_x; mb.max_x = max_x; mb.min_y = min_y; mb.max_y = max_y;
+    mb.window = window; mb.nnratio = nnratio;
     mb.check_ori = check_ori; mb.reset_prev = 0; mb.clocks = nullptr;
     if (launch_match(mb, 1, n1c, n2c, q, c, ws.st) != hipSuccess ||
         hipMemcpyAsync(ws.host + o_prev, D + o_prev, out_end - o_prev, hipMemcpyDeviceToHost, ws.st) != hipSuccess ||

@@ -26,7 +26,11 @@ BOW_VARIANTS = {"kf_frame": 0, "kf_kf": 1, "triangulation": 2}
 
 
 class Frame:
-    def __init__(self, keypoints: np.ndarray, descriptors: np.ndarray, width: int, height: int):
+    """bounds: (mnMinX, mnMaxX, mnMinY, mnMaxY) as Frame::ComputeImageBounds
+    leaves them (Frame.cc:475-499); None = an undistorted camera's
+    (0, width, 0, height)."""
+
+    def __init__(self, keypoints: np.ndarray, descriptors: np.ndarray, width: int, height: int, bounds=None):
         self.mvKeysUn = np.ascontiguousarray(keypoints, dtype=KEYPOINT_DTYPE)
         self.mvKeys = self.mvKeysUn
         self.mDescriptors = np.ascontiguousarray(descriptors, dtype=np.uint8).reshape(-1, 32)
@@ -34,6 +38,8 @@ class Frame:
             raise ValueError("keypoints and descriptors differ in length")
         self.N = len(self.mvKeysUn)
         self.width, self.height = int(width), int(height)
+        b = (0.0, float(width), 0.0, float(height)) if bounds is None else tuple(float(v) for v in bounds)
+        self.mnMinX, self.mnMaxX, self.mnMinY, self.mnMaxY = (float(np.float32(v)) for v in b)
 
 
 class ORBmatcher:
@@ -62,9 +68,11 @@ class ORBmatcher:
             raise ValueError("vbPrevMatched must be a C-contiguous (N1, 2) float32 array")
         m12 = np.full(max(F1.N, 1), -1, dtype=np.int32)
         nm = ctypes.c_int(0)
-        check(self._lib.orbx_search_for_initialization(
+        # the grid is F2's (the reference's bounds are static Frame members)
+        check(self._lib.orbx_search_for_initialization_bounds(
             self.device, ptr(F1.mvKeysUn), ptr(F1.mDescriptors), F1.N,
-            ptr(F2.mvKeysUn), ptr(F2.mDescriptors), F2.N, F2.width, F2.height,
+            ptr(F2.mvKeysUn), ptr(F2.mDescriptors), F2.N, ctypes.c_float(F2.mnMinX), ctypes.c_float(F2.mnMaxX),
+            ctypes.c_float(F2.mnMinY), ctypes.c_float(F2.mnMaxY),
             ptr(vbPrevMatched), ptr(m12), int(windowSize), ctypes.c_float(self.mfNNratio),
             int(self.mbCheckOrientation), ctypes.byref(nm)), "SearchForInitialization")
         return nm.value, m12[:F1.N].copy()

@@ -953,8 +953,14 @@ int main() {
                                    std::vector<int64_t> r{n}; for (auto x : ids(m)) r.push_back(x); return r; },
                    [&](World &w) { std::vector<MapPoint *> m; int n = ref::BoWKF(nn, true, w.kfs[0].get(), w.kfs[2].get(), m);
                                    std::vector<int64_t> r{n}; for (auto x : ids(m)) r.push_back(x); return r; });
-        for (bool ori : {true, false}) {
-            auto init = [ori](World &w, bool gpu) {
+        for (int variant : {0, 1, 2}) {
+            const bool ori = variant != 1, distorted = variant == 2;
+            auto init = [ori, distorted](World &w, bool gpu) {
+                if (distorted)   // a distorted camera's ComputeImageBounds (Frame.cc:475-499): non-zero, non-integer
+                    for (Frame *f : {w.last.get(), w.cur.get()}) {
+                        f->mnMinX = -13.37f; f->mnMaxX = kW + 21.61f; f->mnMinY = 7.25f; f->mnMaxY = kH - 3.83f;
+                        f->AssignFeaturesToGrid();
+                    }
                 std::vector<cv::Point2f> prev;
                 for (auto &k : w.last->mvKeysUn) prev.push_back(k.pt);
                 std::vector<int> m;
@@ -965,7 +971,8 @@ int main() {
                 for (auto &p : prev) { int32_t b[2]; std::memcpy(b, &p, 8); r.push_back(b[0]); r.push_back(b[1]); }
                 return r;
             };
-            check_case(name(ori ? "SearchForInitialization" : "SearchForInitialization(noori)"), mk,
+            check_case(name(distorted ? "SearchForInitialization(bounds)"
+                                      : ori ? "SearchForInitialization" : "SearchForInitialization(noori)"), mk,
                        [&](World &w) { return init(w, true); }, [&](World &w) { return init(w, false); });
         }
         auto f12 = [](KeyFrame *k1, KeyFrame *k2) {

@@ -34,6 +34,15 @@ int orbx_search_for_initialization(int, const orbx_keypoint *k1, const uint8_t *
     return ORBX_OK;
 }
 
+int orbx_search_for_initialization_bounds(int, const orbx_keypoint *k1, const uint8_t *d1, int n1,
+                                          const orbx_keypoint *k2, const uint8_t *d2, int n2, float min_x,
+                                          float max_x, float min_y, float max_y, float *prev_xy, int32_t *matches12,
+                                          int window, float nnratio, int check_ori, int *nmatches) {
+    *nmatches = orbo_search_for_initialization_bounds(K(k1), d1, n1, K(k2), d2, n2, min_x, max_x, min_y, max_y,
+                                                      prev_xy, matches12, window, nnratio, check_ori);
+    return ORBX_OK;
+}
+
 int orbx_search_by_projection(int, int variant, const orbx_match_frame *f, const orbx_proj_query *q,
                               const uint8_t *qdesc, int nq, int th_dist, float nnratio, int check_ori, int32_t *q_idx,
                               int32_t *q_dist, int32_t *kp_final, int *nmatches) {
