@@ -36,6 +36,7 @@ _SIG = {
     "orbo_levels": (None, [I32, I32, I32, F32, I32, P, P, P, P]),
     "orbo_pyramid": (SZ, [P, I32, I32, SZ, F32, I32, P]),
     "orbo_level_candidates": (I32, [P, I32, I32, I32, I32, P, I32]),
+    "orbo_level_candidates_cells": (I32, [P, I32, I32, I32, I32, P, I32, P, I32, P]),
     "orbo_distribute": (I32, [P, I32, I32, I32, I32, P]),
     "orbo_extract": (I32, [P, I32, I32, SZ, I32, F32, I32, I32, I32, P, P, I32, P]),
     "orbo_search_for_initialization": (I32, [P, P, I32, P, P, I32, I32, I32, P, P, I32, F32, I32]),
@@ -156,6 +157,19 @@ def level_candidates(lvl: np.ndarray, ini=20, mn=7) -> np.ndarray:
     n = lib().orbo_level_candidates(_p(lvl), lvl.shape[1], lvl.shape[0], ini, mn, _p(out), cap)
     assert n >= 0
     return out[:3 * n].reshape(n, 3)
+
+
+def level_candidates_cells(lvl: np.ndarray, ini=20, mn=7):
+    """(candidates, per-cell corner counts in the reference's cell order)."""
+    lvl = np.ascontiguousarray(lvl)
+    cap = lvl.size
+    out = np.zeros(3 * cap, np.int32)
+    cells = np.zeros(65536, np.int32)
+    nc = ctypes.c_int(0)
+    n = lib().orbo_level_candidates_cells(_p(lvl), lvl.shape[1], lvl.shape[0], ini, mn, _p(out), cap, _p(cells),
+                                          len(cells), ctypes.byref(nc))
+    assert n >= 0
+    return out[:3 * n].reshape(n, 3), cells[:nc.value].copy()
 
 
 def distribute(cands: np.ndarray, w: int, h: int, N: int) -> np.ndarray:

@@ -343,8 +343,9 @@ Geometry make_geometry(int W, int H, int nfeatures, float scaleFactorF, int nlev
 // Cell loop of ComputeKeyPointsOctTree (ORBextractor.cc:796-863).
 // ---------------------------------------------------------------------------
 void level_candidates(const uint8_t *lvl, int w, int h, size_t step, int iniTh, int minTh,
-                      std::vector<Corner> &cands) {
+                      std::vector<Corner> &cands, std::vector<int> *cell_counts = nullptr) {
     cands.clear();
+    if (cell_counts) cell_counts->clear();
     const float W = 30;
     const int minBX = 19 - 3, minBY = minBX;
     const int maxBX = w - 19 + 3, maxBY = h - 19 + 3;
@@ -369,6 +370,7 @@ void level_candidates(const uint8_t *lvl, int w, int h, size_t step, int iniTh, 
             fast9(sub, sw, sh, step, iniTh, cell);
             if (cell.empty()) fast9(sub, sw, sh, step, minTh, cell);
             for (const Corner &c : cell) cands.push_back({c.x + x0, c.y + y0, c.score});
+            if (cell_counts) cell_counts->push_back((int)cell.size());
         }
     }
 }
@@ -679,6 +681,24 @@ int orbo_level_candidates(const uint8_t *lvl, int w, int h, int iniTh, int minTh
     for (int i = 0; i < n; ++i) {
         xys[3 * i] = c[i].x; xys[3 * i + 1] = c[i].y; xys[3 * i + 2] = c[i].score;
     }
+    return n;
+}
+
+// The same with the corner count of every visited cell, in the reference's
+// cell order (tools/tie_heap: the per-cell vector<KeyPoint> allocations).
+// Returns the candidate count, or -(count) if cap or cell_cap is too small.
+int orbo_level_candidates_cells(const uint8_t *lvl, int w, int h, int iniTh, int minTh, int32_t *xys, int cap,
+                                int32_t *cell_counts, int cell_cap, int *ncells) {
+    std::vector<Corner> c;
+    std::vector<int> cc;
+    level_candidates(lvl, w, h, w, iniTh, minTh, c, &cc);
+    const int n = (int)c.size();
+    *ncells = (int)cc.size();
+    if (n > cap || (int)cc.size() > cell_cap) return -n;
+    for (int i = 0; i < n; ++i) {
+        xys[3 * i] = c[i].x; xys[3 * i + 1] = c[i].y; xys[3 * i + 2] = c[i].score;
+    }
+    for (size_t i = 0; i < cc.size(); ++i) cell_counts[i] = cc[i];
     return n;
 }
 

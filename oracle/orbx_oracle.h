@@ -62,6 +62,10 @@ size_t orbo_pyramid(const uint8_t *img, int w, int h, size_t step,
  * order the reference pushes them.  Returns the count (or -needed if > cap). */
 int   orbo_level_candidates(const uint8_t *lvl, int w, int h, int iniTh, int minTh,
                             int32_t *xys, int cap);
+/* The same plus each visited cell's corner count, in cell order (diagnostic:
+ * tools/tie_heap replays the per-cell vector<KeyPoint> allocations). */
+int   orbo_level_candidates_cells(const uint8_t *lvl, int w, int h, int iniTh, int minTh,
+                                  int32_t *xys, int cap, int32_t *cell_counts, int cell_cap, int *ncells);
 /* DistributeOctTree on a candidate list (ORBextractor.cc:561-787): writes the
  * selected candidate indices in output order; returns the count. */
 void  orbo_tie_stats(int64_t out[9], int reset);   /* diagnostic, see orbx_oracle.cpp */
