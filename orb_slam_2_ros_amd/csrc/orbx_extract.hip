@@ -1063,14 +1063,49 @@ struct QLds {
 // 6 keys per thread cover the bench levels (VGA level 0: ~1300 keys) in 72
 // VGPRs (7 waves per SIMD); levels up to kQuadRegKeys take 8 (with spills)
 constexpr int kQRegKeys = 6, kQRegKeysWide = kQuadRegKeys / kThreads;
+// R == 0 (keys in global scratch): a pass walks the keys kQU per thread at a
+// time, the chunk's loads issued together into a register cache (key k =
+// k0 + u kThreads + tid: every pass maps a key to the same thread, so its node
+// and quadrant need no cross-thread ordering), then the chunk's node and
+// quadrant written back.  A key pass is then ~n / (kQU kThreads) L2 round
+// trips instead of n / kThreads (FHD level 0: ~9.6 k keys, 5 instead of 38).
+#ifndef ORBX_QT_QU
+#define ORBX_QT_QU 4
+#endif
+constexpr int kQU = ORBX_QT_QU;
 template <int R>
 struct QKeys {
-    uint32_t key[R > 0 ? R : 1];
-    uint32_t nq[R > 0 ? R : 1];   // node | quadrant << 16
+    static constexpr int C = R > 0 ? R : kQU;   // registers: the keys, or the chunk cache
+    uint32_t key[C];
+    uint32_t nq[C];   // node | quadrant << 16
     uint32_t *gkeys;
     uint16_t *gnode;
     uint8_t *gq;
     int n;
+    // the chunk at k0 into the cache (R == 0)
+    __device__ inline void load(int k0) {
+#pragma unroll
+        for (int u = 0; u < C; ++u) {
+            const int k = k0 + u * kThreads + (int)threadIdx.x;
+            if (k < n) {
+                key[u] = gkeys[k];
+                // (a key's quadrant is 0..3; masked, as the scratch starts
+                // unwritten and an unsplit node's keys read any of its 4 slots)
+                nq[u] = (uint32_t)gnode[k] | ((uint32_t)(gq[k] & 3) << 16);
+            }
+        }
+    }
+    __device__ inline void store(int k0) {
+#pragma unroll
+        for (int u = 0; u < C; ++u) {
+            const int k = k0 + u * kThreads + (int)threadIdx.x;
+            if (k < n) {
+                gnode[k] = (uint16_t)(nq[u] & 0xFFFF);
+                gq[k] = (uint8_t)(nq[u] >> 16);
+            }
+        }
+    }
+    // f(j, k) for every key this thread owns
     template <typename F>
     __device__ inline void each(F f) {
         if constexpr (R > 0) {
@@ -1080,24 +1115,43 @@ struct QKeys {
                 if (k < n) f(j, k);
             }
         } else {
-            for (int k = threadIdx.x; k < n; k += kThreads) f(0, k);
+            for (int k0 = 0; k0 < n; k0 += kThreads * kQU) {
+                load(k0);
+#pragma unroll
+                for (int u = 0; u < kQU; ++u) {
+                    const int k = k0 + u * kThreads + (int)threadIdx.x;
+                    if (k < n) f(u, k);
+                }
+                store(k0);
+            }
         }
     }
-    __device__ inline uint32_t get_key(int j, int k) const {
-        if constexpr (R > 0) return key[j]; else return gkeys[k];
+    // f(j, k, valid) on every lane for every key slot (bodies with DPP)
+    template <typename F>
+    __device__ inline void each_all(F f) {
+        if constexpr (R > 0) {
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                const int k = (int)threadIdx.x + j * kThreads;
+                f(j, k, k < n);
+            }
+        } else {
+            for (int k0 = 0; k0 < n; k0 += kThreads * kQU) {
+                load(k0);
+#pragma unroll
+                for (int u = 0; u < kQU; ++u) {
+                    const int k = k0 + u * kThreads + (int)threadIdx.x;
+                    f(u, k, k < n);
+                }
+                store(k0);
+            }
+        }
     }
-    __device__ inline int node(int j, int k) const {
-        if constexpr (R > 0) return (int)(nq[j] & 0xFFFF); else return gnode[k];
-    }
-    __device__ inline int quad(int j, int k) const {
-        if constexpr (R > 0) return (int)(nq[j] >> 16); else return gq[k];
-    }
-    __device__ inline void set_node(int j, int k, int nd) {
-        if constexpr (R > 0) nq[j] = (nq[j] & 0xFFFF0000u) | (uint32_t)nd; else gnode[k] = (uint16_t)nd;
-    }
-    __device__ inline void set_quad(int j, int k, int q) {
-        if constexpr (R > 0) nq[j] = (nq[j] & 0xFFFFu) | ((uint32_t)q << 16); else gq[k] = (uint8_t)q;
-    }
+    __device__ inline uint32_t get_key(int j, int) const { return key[j]; }
+    __device__ inline int node(int j, int) const { return (int)(nq[j] & 0xFFFF); }
+    __device__ inline int quad(int j, int) const { return (int)(nq[j] >> 16); }
+    __device__ inline void set_node(int j, int, int nd) { nq[j] = (nq[j] & 0xFFFF0000u) | (uint32_t)nd; }
+    __device__ inline void set_quad(int j, int, int q) { nq[j] = (nq[j] & 0xFFFFu) | ((uint32_t)q << 16); }
 };
 
 #ifndef ORBX_QT_AGG
@@ -1150,48 +1204,24 @@ __device__ inline void agg_atomics(uint32_t *cnt, uint32_t *best, uint32_t slot,
 // were zeroed by the step that produced the current nodes (zero_children),
 // ordered by that step's closing barrier.  Ends with a barrier.
 template <int R>
-__device__ void child_stats(const QLds &s, QKeys<R> &K) {
-    if constexpr (R > 0) {
-        // register keys: every lane runs each register's aggregation
-        // (lanes past the key count carry slot ~0u)
-#pragma unroll
-        for (int j = 0; j < R; ++j) {
-            const int k = (int)threadIdx.x + j * kThreads;
-            uint32_t slot = ~0u, bp = 0;
-            if (k < K.n) {
-                const int nd = K.node(j, k);
-                const QNode node = s.cur[nd];
-                if (node.count > 1) {
-                    const uint32_t key = K.get_key(j, k);
-                    const int q = quadrant_of(node, key);
-                    K.set_quad(j, k, q);
-                    slot = 4u * (uint32_t)nd + (uint32_t)q;
-                    bp = best_pack(key, k);
-                }
+__device__ __attribute__((always_inline)) void child_stats(const QLds &s, QKeys<R> &K) {
+    // every lane runs each slot's aggregation (lanes past the key count carry
+    // slot ~0u)
+    K.each_all([&](int j, int k, bool valid) {
+        uint32_t slot = ~0u, bp = 0;
+        if (valid) {
+            const int nd = K.node(j, k);
+            const QNode node = s.cur[nd];
+            if (node.count > 1) {
+                const uint32_t key = K.get_key(j, k);
+                const int q = quadrant_of(node, key);
+                K.set_quad(j, k, q);
+                slot = 4u * (uint32_t)nd + (uint32_t)q;
+                bp = best_pack(key, k);
             }
-            agg_atomics(s.ccnt, s.cbest, slot, bp);
         }
-    } else {
-        // keys in global scratch (levels past kQuadRegKeys, e.g. FHD's first
-        // ones): the block steps through them together, so every lane of a
-        // wave reaches the aggregation
-        for (int k0 = 0; k0 < K.n; k0 += kThreads) {
-            const int k = k0 + (int)threadIdx.x;
-            uint32_t slot = ~0u, bp = 0;
-            if (k < K.n) {
-                const int nd = K.node(0, k);
-                const QNode node = s.cur[nd];
-                if (node.count > 1) {
-                    const uint32_t key = K.get_key(0, k);
-                    const int q = quadrant_of(node, key);
-                    K.set_quad(0, k, q);
-                    slot = 4u * (uint32_t)nd + (uint32_t)q;
-                    bp = best_pack(key, k);
-                }
-            }
-            agg_atomics(s.ccnt, s.cbest, slot, bp);
-        }
-    }
+        agg_atomics(s.ccnt, s.cbest, slot, bp);
+    });
     __syncthreads();
 }
 
@@ -1217,7 +1247,7 @@ __device__ inline QNode make_child(const QLds &s, const QNode &parent, int i, in
 
 // Phases 2-5 of k_quadtree on the gathered keys (ORBextractor.cc:566-784).
 template <int NR>
-__device__ void quadtree_rounds(const DevPlan &p, const FrameBufs &fb, QLds &s, const LevelGeom &g, int b, int l,
+__device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p, const FrameBufs &fb, QLds &s, const LevelGeom &g, int b, int l,
                                 QKeys<NR> &K, uint64_t &phase_t_) {
     const int tid = threadIdx.x;
     const int N = g.quota, NC = p.node_cap;
@@ -1264,34 +1294,17 @@ __device__ void quadtree_rounds(const DevPlan &p, const FrameBufs &fb, QLds &s, 
             const float rx = (float)((int)(key & 0xFFF) - kBorder);
             return min((int)__fdiv_rn(rx, g.hx), nini - 1);
         };
-        if constexpr (NR > 0) {
-#pragma unroll
-            for (int j = 0; j < NR; ++j) {
-                const int k = tid + j * kThreads;
-                uint32_t slot = ~0u, bp = 0;
-                if (k < K.n) {
-                    const uint32_t key = K.get_key(j, k);
-                    const int r = root_of(key);
-                    K.set_node(j, k, r);
-                    slot = (uint32_t)r;
-                    bp = best_pack(key, k);
-                }
-                agg_atomics(s.ccnt, s.cbest, slot, bp);
+        K.each_all([&](int j, int k, bool valid) {
+            uint32_t slot = ~0u, bp = 0;
+            if (valid) {
+                const uint32_t key = K.get_key(j, k);
+                const int r = root_of(key);
+                K.set_node(j, k, r);
+                slot = (uint32_t)r;
+                bp = best_pack(key, k);
             }
-        } else {
-            for (int k0 = 0; k0 < K.n; k0 += kThreads) {
-                const int k = k0 + tid;
-                uint32_t slot = ~0u, bp = 0;
-                if (k < K.n) {
-                    const uint32_t key = K.get_key(0, k);
-                    const int r = root_of(key);
-                    K.set_node(0, k, r);
-                    slot = (uint32_t)r;
-                    bp = best_pack(key, k);
-                }
-                agg_atomics(s.ccnt, s.cbest, slot, bp);
-            }
-        }
+            agg_atomics(s.ccnt, s.cbest, slot, bp);
+        });
         __syncthreads();
         if (tid == 0) {
             int S = 0;
@@ -1606,16 +1619,6 @@ __global__ __launch_bounds__(kThreads, 7) void k_quadtree(DevPlan p, FrameBufs f
         return;
     }
     const uint32_t *cand = fb.cand + (int64_t)b * p.cand_cap, *cand2 = fb.cand2 + (int64_t)b * p.cand_cap;
-    // key k: the cell whose range [off[c], off[c+1]) holds it, by bisection
-    auto fetch = [&](int k) {
-        int lo = 0, hi = ncell - 1;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (cell_off[mid] <= k) lo = mid; else hi = mid - 1;
-        }
-        const int src = cell_src[lo];
-        return ((src < 0) ? cand2 : cand)[(src & 0x7FFFFFFF) + (k - cell_off[lo])];
-    };
     // up to kQRegKeys (kQRegKeysWide) keys per thread stay in registers
     // through the rounds
     auto in_registers = [&](auto &K) {
@@ -1638,7 +1641,35 @@ __global__ __launch_bounds__(kThreads, 7) void k_quadtree(DevPlan p, FrameBufs f
     } else {
         QKeys<0> K;
         K.gkeys = keys; K.gnode = knode; K.gq = kq; K.n = n;
-        for (int k = tid; k < n; k += kThreads) keys[k] = fetch(k);
+        // kQU keys per thread at a time (the chunk mapping of QKeys<0>): their
+        // bisections interleave, and their candidate loads go out together
+        for (int k0 = 0; k0 < n; k0 += kThreads * kQU) {
+            int lo[kQU], hi[kQU];
+#pragma unroll
+            for (int u = 0; u < kQU; ++u) { lo[u] = 0; hi[u] = ncell - 1; }
+            for (int step = ncell; step > 1; step = (step + 1) >> 1) {
+#pragma unroll
+                for (int u = 0; u < kQU; ++u) {
+                    const int k = k0 + u * kThreads + tid;
+                    if (lo[u] < hi[u]) {
+                        const int mid = (lo[u] + hi[u] + 1) >> 1;
+                        if (cell_off[mid] <= k) lo[u] = mid; else hi[u] = mid - 1;
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kQU; ++u) {
+                const int k = k0 + u * kThreads + tid;
+                while (lo[u] < hi[u]) {   // (the halving bound above covers every bisection; kept for safety)
+                    const int mid = (lo[u] + hi[u] + 1) >> 1;
+                    if (cell_off[mid] <= k) lo[u] = mid; else hi[u] = mid - 1;
+                }
+                if (k < n) {
+                    const int src = cell_src[lo[u]];
+                    keys[k] = ((src < 0) ? cand2 : cand)[(src & 0x7FFFFFFF) + (k - cell_off[lo[u]])];
+                }
+            }
+        }
         __syncthreads();
         PHASE_MARK(2, 0);
         quadtree_rounds(p, fb, s, g, b, l, K, phase_t_);
