@@ -580,6 +580,7 @@ def dropin_latency(torch, dev, reps=100):
     out["stereo_pair_host_euroc"] = {"gpu_ms": round(med(pair, reps), 4), "cpu_ms": round(med(pair_cpu, 3), 3)}
     exl.close()
     exr.close()
+    out.update(cxx_dropin_latency(L, R, bf, mb, reps))
     # batched device step, VGA mono (extract + SearchForInitialization)
     w, h = 640, 480
     base = synth.frames(w, h, 4244, FRAMES_PER_STREAM)
@@ -608,6 +609,54 @@ def dropin_latency(torch, dev, reps=100):
         ex.close()
         del fr
     out["mono_step_device_vga_batch_sweep"] = sweep
+    return out
+
+
+def cxx_dropin_latency(L, R, bf, mb, reps):
+    """The C++ drop-in (include/orbx_orbslam2.hpp) as a reference tree would
+    link it, timed by orb_slam_2_ros_amd/bin/adapter_test (built by
+    __graft_entry__.build()): ORBextractor::operator() at VGA / FHD (and the
+    first mvImagePyramid read after a call), Frame's stereo constructor (two
+    threads started per frame, Frame.cc:79-82, + ComputeStereoMatches through
+    OrbxFrame) at EuRoC size, and the RGB-D frame (extract +
+    ComputeStereoFromRGBD) at FHD."""
+    import subprocess
+    import tempfile
+    from orb_slam_2_ros_amd import synth
+    exe = Path(__file__).resolve().parent / "orb_slam_2_ros_amd" / "bin" / "adapter_test"
+    if not exe.exists():
+        sys.path.insert(0, str(Path(__file__).resolve().parent / "tests"))
+        from cxx_build import build_adapter_test
+        build_adapter_test(exe)
+
+    def run(*args):
+        r = subprocess.run([str(exe), *map(str, args)], capture_output=True, text=True, timeout=300, check=True)
+        return {ln.split()[0]: float(ln.split()[1]) for ln in r.stdout.splitlines() if ln.endswith(tuple("0123456789")) and
+                ln.split()[0].endswith("_ms")}
+
+    out = {}
+    with tempfile.TemporaryDirectory() as td:
+        td = Path(td)
+        for key, w, h in (("vga", 640, 480), ("fhd", 1920, 1080)):
+            p = td / f"{key}.raw"
+            synth.frame(w, h, 4242).tofile(p)
+            t = run("time", w, h, p, 1000, reps)
+            out[f"cxx_extract_{key}"] = {"gpu_ms": t["extract_ms"], "pyramid_read_ms": t["pyramid_read_ms"]}
+        pl, pr = td / "l.raw", td / "r.raw"
+        np.ascontiguousarray(L).tofile(pl)
+        np.ascontiguousarray(R).tofile(pr)
+        t = run("time_stereo", L.shape[1], L.shape[0], pl, pr, 1200, bf, mb, reps)
+        out["cxx_stereo_pair_euroc"] = {"gpu_ms": t["pair_ms"]}
+        w, h = 1920, 1080
+        img = synth.frame(w, h, 4245)
+        rng = np.random.default_rng(5)
+        dmap = rng.uniform(0.5, 8.0, (h, w)).astype(np.float32)
+        dmap[rng.random((h, w)) < 0.2] = 0.0
+        pi, pd = td / "rgbd.raw", td / "depth.raw"
+        img.tofile(pi)
+        dmap.tofile(pd)
+        t = run("time_rgbd", w, h, pi, pd, 40.0, reps)
+        out["cxx_rgbd_fhd"] = {"frame_ms": t["rgbd_frame_ms"], "depth_ms": t["rgbd_depth_ms"]}
     return out
 
 

@@ -79,6 +79,11 @@ int orbx_extract(orbx_extractor *ex, const uint8_t *image, int width, int height
  * at `out_pitch` stride when out != NULL; always reports w, h. */
 int orbx_extractor_pyramid_level(orbx_extractor *ex, int level, uint8_t *out,
                                  size_t out_pitch, int *w, int *h);
+/* The same for levels 0 .. nlevels-1 at once (out[l] rows of level l's width
+ * at out_pitch[l]): one stream-ordered copy of every level into pinned
+ * staging and one wait -- what an mvImagePyramid read costs after a call. */
+int orbx_extractor_pyramid_host(orbx_extractor *ex, uint8_t *const *out, const size_t *out_pitch,
+                                int nlevels);
 
 /* ---- batched device API (many cameras / frames per launch) ------------- */
 

@@ -43,6 +43,52 @@ inline std::vector<orbx_keypoint> pack(const std::vector<cv::KeyPoint> &ks) {
 }
 }  // namespace orbx_detail
 
+// mvImagePyramid (ORBextractor.h:85) as a lazily filled container: each level
+// an ROI of a buffer with a 19-px reflect-101 border, as ComputePyramid builds
+// it (ORBextractor.cc:1152-1185), copied from the device on the first access
+// after an extraction (orbx_extractor_pyramid_host: one stream-ordered copy of
+// every level).  The reference reads it only in Frame::ComputeStereoMatches
+// (Frame.cc:509, 599-616), which Frame_orbx.cc forwards to the device
+// pyramids, so with the forwarder in place no call pays for it.  operator[],
+// size(), begin()/end() read as std::vector<cv::Mat> does.
+class OrbxPyramid {
+public:
+    cv::Mat &operator[](size_t l) { fill(); return lv_[l]; }
+    const cv::Mat &operator[](size_t l) const { fill(); return lv_[l]; }
+    size_t size() const { return lv_.size(); }
+    bool empty() const { return lv_.empty(); }
+    std::vector<cv::Mat>::iterator begin() { fill(); return lv_.begin(); }
+    std::vector<cv::Mat>::iterator end() { fill(); return lv_.end(); }
+    std::vector<cv::Mat>::const_iterator begin() const { fill(); return lv_.begin(); }
+    std::vector<cv::Mat>::const_iterator end() const { fill(); return lv_.end(); }
+    void resize(size_t n) { lv_.resize(n); whole_.resize(n); }
+
+private:
+    friend class ORBextractor;
+    void fill() const {
+        if (!stale_) return;
+        const int E = 19;   // EDGE_THRESHOLD
+        const int n = (int)lv_.size();
+        std::vector<uint8_t *> ptr(n);
+        std::vector<size_t> pitch(n);
+        for (int l = 0; l < n; ++l) {
+            int w = 0, h = 0;
+            orbx_detail::check(orbx_extractor_pyramid_level(h_, l, nullptr, 0, &w, &h), "pyramid level");
+            whole_[l].create(h + 2 * E, w + 2 * E, CV_8U);   // (reused while the size holds)
+            lv_[l] = whole_[l](cv::Rect(E, E, w, h));
+            ptr[l] = lv_[l].data;
+            pitch[l] = lv_[l].step;
+        }
+        orbx_detail::check(orbx_extractor_pyramid_host(h_, ptr.data(), pitch.data(), n), "pyramid");
+        for (int l = 0; l < n; ++l)
+            cv::copyMakeBorder(lv_[l], whole_[l], E, E, E, E, cv::BORDER_REFLECT_101 + cv::BORDER_ISOLATED);
+        stale_ = false;
+    }
+    orbx_extractor *h_ = nullptr;
+    mutable std::vector<cv::Mat> lv_, whole_;
+    mutable bool stale_ = false;
+};
+
 class ORBextractor {
 public:
     enum { HARRIS_SCORE = 0, FAST_SCORE = 1 };
@@ -57,6 +103,7 @@ public:
         mvInvScaleFactor = table(1);
         mvLevelSigma2 = table(2);
         mvInvLevelSigma2 = table(3);
+        mvImagePyramid.h_ = h_;
         mvImagePyramid.resize(nlevels);
     }
     ~ORBextractor() { orbx_extractor_destroy(h_); }
@@ -95,7 +142,7 @@ public:
             _descriptors.create(n, 32, CV_8U);
             desc.rowRange(0, n).copyTo(_descriptors.getMat());
         }
-        fill_pyramid();
+        mvImagePyramid.stale_ = true;   // filled from the device when read
     }
 
     int inline GetLevels() { return nlevels_; }
@@ -107,30 +154,14 @@ public:
     std::vector<float> inline GetScaleSigmaSquares() { return mvLevelSigma2; }
     std::vector<float> inline GetInverseScaleSigmaSquares() { return mvInvLevelSigma2; }
 
-    // ORBextractor.h:85 -- each level as an ROI of a buffer with a 19-px
-    // reflect-101 border, as ComputePyramid builds it (ORBextractor.cc:1152-1185);
-    // Frame::ComputeStereoMatches reads it (Frame.cc:509, 599-616).
-    std::vector<cv::Mat> mvImagePyramid;
+    // ORBextractor.h:85 (see OrbxPyramid)
+    OrbxPyramid mvImagePyramid;
 
 protected:
     std::vector<float> table(int which) {
         std::vector<float> v(nlevels_);
         orbx_detail::check(orbx_extractor_get_scale_table(h_, which, v.data(), nlevels_), "scale table");
         return v;
-    }
-
-    void fill_pyramid() {
-        const int E = 19;   // EDGE_THRESHOLD
-        for (int l = 0; l < nlevels_; ++l) {
-            int w = 0, h = 0;
-            orbx_detail::check(orbx_extractor_pyramid_level(h_, l, nullptr, 0, &w, &h), "pyramid level");
-            cv::Mat whole(h + 2 * E, w + 2 * E, CV_8U);
-            cv::Mat roi = whole(cv::Rect(E, E, w, h));
-            orbx_detail::check(orbx_extractor_pyramid_level(h_, l, roi.data, roi.step, nullptr, nullptr),
-                               "pyramid level");
-            cv::copyMakeBorder(roi, whole, E, E, E, E, cv::BORDER_REFLECT_101 + cv::BORDER_ISOLATED);
-            mvImagePyramid[l] = roi;
-        }
     }
 
     orbx_extractor *h_ = nullptr;

@@ -90,6 +90,7 @@ _SIGNATURES = {
     "orbx_extractor_get_level_quotas": (I32, [P, P, I32]),
     "orbx_extract": (I32, [P, P, I32, I32, SZ, P, P, I32, P]),
     "orbx_extractor_pyramid_level": (I32, [P, I32, P, SZ, P, P]),
+    "orbx_extractor_pyramid_host": (I32, [P, P, P, I32]),
     "orbx_extractor_reserve": (I32, [P, I32, I32, I32]),
     "orbx_extractor_kp_stride": (I32, [P]),
     "orbx_extract_batch_device": (I32, [P, P, I64, I32, I32, P]),

@@ -168,6 +168,8 @@ hipError_t launch_trig_check(const float *in, float *s, float *c, float *atan_ou
                              const float *ay, const float *ax, int n, int m, hipStream_t st);
 hipError_t launch_stereo(const StereoBufs &a, int pairs, int nl_cap, hipStream_t s);
 int stereo_lds_bytes(int rows, int nr_cap);
+hipError_t launch_rgbd_samples(const float *dsample, const orbx_keypoint *kun, int n, float mbf, float *ur, float *depth,
+                               int32_t *nkept, hipStream_t st);
 hipError_t launch_rgbd(const orbx_keypoint *kps, const orbx_keypoint *kun, const int32_t *nkps, int64_t kstride,
                        int kcap, const float *dmap, int64_t dstride, int dpitch, int w, int h, float mbf, float *ur,
                        float *depth, int64_t ostride, int32_t *nkept, int B, hipStream_t s);

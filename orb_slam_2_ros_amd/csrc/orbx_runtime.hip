@@ -123,6 +123,16 @@ struct orbx_extractor {
     } sws;
 
     hipStream_t stream = nullptr;
+    // The current results' completion: recorded on the launch stream at the end
+    // of every device step (the caller's stream, or `stream`), so the download
+    // calls wait for exactly that work -- no device-wide synchronisation, which
+    // would also wait for (and serialise with) other extractors' streams, e.g.
+    // the two extraction threads of Frame's stereo constructor.
+    hipEvent_t res_ev = nullptr;
+    bool res_pending = false;
+    // pinned staging of the host pyramid copy (orbx_extractor_pyramid_host)
+    uint8_t *h_pyr = nullptr;
+    size_t h_pyr_bytes = 0;
 
     // Batch split: a large batch runs as `split` interleaved sub-batches on
     // their own streams (forked from / joined to the launch stream), so the
@@ -165,6 +175,8 @@ struct orbx_extractor {
         release();
         if (h_img) (void)hipHostFree(h_img);
         if (h_out) (void)hipHostFree(h_out);
+        if (h_pyr) (void)hipHostFree(h_pyr);
+        if (res_ev) (void)hipEventDestroy(res_ev);
         sws.free_dev();
         if (sws.h_res) (void)hipHostFree(sws.h_res);
         if (stream) (void)hipStreamDestroy(stream);
@@ -189,6 +201,7 @@ struct orbx_extractor {
         if (host_graph) (void)hipGraphExecDestroy(host_graph);
         host_graph = nullptr;
         host_result_valid = false;   // the result slots are freed: h_out no longer mirrors slot 0
+        res_pending = false;
         graph_w = graph_h = 0;
         dfree(d_tables); dfree(d_pyr); dfree(d_blur); dfree(d_cand); dfree(d_cand2); dfree(d_keys); dfree(d_sel);
         dfree(d_cell_count); dfree(d_level_count); dfree(d_key_node); dfree(d_key_q);
@@ -211,6 +224,37 @@ int check(hipError_t e) { return e == hipSuccess ? ORBX_OK : ORBX_EIO; }
 hipStream_t stream_of(orbx_extractor *ex, void *s) {
     return s ? reinterpret_cast<hipStream_t>(s) : ex->stream;
 }
+
+// End of a device step on st: its results are complete when res_ev is.
+void note_results(orbx_extractor *ex, hipStream_t st) {
+    if (!ex->res_ev && hipEventCreateWithFlags(&ex->res_ev, hipEventDisableTiming) != hipSuccess) {
+        ex->res_ev = nullptr;
+        (void)hipStreamSynchronize(st);   // (no event: wait here instead)
+        ex->res_pending = false;
+        return;
+    }
+    ex->res_pending = hipEventRecord(ex->res_ev, st) == hipSuccess;
+    if (!ex->res_pending) (void)hipStreamSynchronize(st);
+}
+
+// Waits for the current results; the copies that follow go on ex->stream.
+int sync_results(orbx_extractor *ex) {
+    if (ex->res_pending) {
+        if (hipEventSynchronize(ex->res_ev) != hipSuccess) return ORBX_EIO;
+        ex->res_pending = false;
+    }
+    return ORBX_OK;
+}
+
+// Device -> host copies on the extractor's stream, then one wait for them.
+struct D2H {
+    orbx_extractor *ex;
+    bool ok = true;
+    void operator()(void *dst, const void *src, size_t n) {
+        if (ok && n) ok = hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, ex->stream) == hipSuccess;
+    }
+    bool wait() { return ok && hipStreamSynchronize(ex->stream) == hipSuccess; }
+};
 
 int upload_plan(orbx_extractor *ex) {
     Plan &p = ex->plan;
@@ -662,6 +706,49 @@ int align_level0(orbx_extractor *ex, const uint8_t **d_images, int64_t *stride, 
 }  // namespace
 
 // =============================================================================
+namespace orbx {
+
+namespace {
+constexpr int kToHostThreads = 1024;
+__global__ __launch_bounds__(kToHostThreads) void k_to_host(const uint4 *src, uint4 *dst, int n16, uint32_t *flag) {
+    for (int i = threadIdx.x; i < n16; i += kToHostThreads) dst[i] = src[i];
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+}  // namespace
+
+int ws_finish(CallWs &ws, size_t off, size_t bytes) {
+    const size_t n16 = (bytes + 15) / 16;
+    if (bytes == 0) return hipStreamSynchronize(ws.st) == hipSuccess ? ORBX_OK : ORBX_EIO;
+    const bool direct = ws.host_d && ws.flag_d && (off & 15) == 0 && n16 * 16 + off <= ws.cap && bytes <= (256u << 10);
+    if (!direct) {
+        if (hipMemcpyAsync(ws.host + off, ws.dev + off, bytes, hipMemcpyDeviceToHost, ws.st) != hipSuccess ||
+            hipStreamSynchronize(ws.st) != hipSuccess)
+            return ORBX_EIO;
+        return ORBX_OK;
+    }
+    volatile uint32_t *flag = ws.flag;
+    *flag = 0;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    hipLaunchKernelGGL(k_to_host, dim3(1), dim3(kToHostThreads), 0, ws.st, reinterpret_cast<const uint4 *>(ws.dev + off),
+                       reinterpret_cast<uint4 *>(ws.host_d + off), (int)n16, ws.flag_d);
+    if (hipGetLastError() != hipSuccess) return ORBX_EIO;
+    for (uint32_t i = 1; !*flag; ++i) {   // the stream's state ends the wait on an error
+        if ((i & 255) == 0 && hipStreamQuery(ws.st) != hipErrorNotReady) break;
+        __builtin_ia32_pause();
+    }
+    if (!*flag) {
+        if (hipStreamSynchronize(ws.st) != hipSuccess) return ORBX_EIO;
+        for (int i = 0; i < (1 << 20) && !*flag; ++i) __builtin_ia32_pause();
+        if (!*flag) return ORBX_EIO;
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    return ORBX_OK;
+}
+
+}  // namespace orbx
+
 extern "C" {
 
 const char *orbx_strerror(int code) {
@@ -755,6 +842,7 @@ int orbx_extract_batch_device(orbx_extractor *ex, const uint8_t *d_images, int64
     rc = run_extract(ex, next, d_images, frame_stride, pitch, batch, st);
     if (rc) return rc;
     mark(ex, kNumStages, st);
+    note_results(ex, st);
     ex->cur = next;
     ex->match_batch = 0;
     return ORBX_OK;
@@ -796,23 +884,21 @@ int orbx_batch_download(orbx_extractor *ex, int frame, orbx_keypoint *kps, uint8
     const auto &s = ex->slot[ex->cur];
     if (frame < 0 || frame >= s.batch) return ORBX_EINVAL;
     if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
-    if (hipDeviceSynchronize() != hipSuccess) return ORBX_EIO;
+    if (sync_results(ex)) return ORBX_EIO;
     int32_t cnt = 0;
     int32_t lc[kMaxLevels];
-    if (hipMemcpy(&cnt, s.nkps + frame, sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess) return ORBX_EIO;
-    if (hipMemcpy(lc, ex->d_level_count + (size_t)frame * kMaxLevels, sizeof(lc), hipMemcpyDeviceToHost) != hipSuccess)
-        return ORBX_EIO;
+    D2H copy{ex};
+    copy(&cnt, s.nkps + frame, sizeof(int32_t));
+    copy(lc, ex->d_level_count + (size_t)frame * kMaxLevels, sizeof(lc));
+    if (!copy.wait()) return ORBX_EIO;
     for (int l = 0; l < ex->nlevels; ++l)
         if (lc[l] < 0) return ORBX_EIO;   // quadtree capacity guard tripped
     *n = cnt;
     if (cnt > cap) return ORBX_ERANGE;
     const size_t base = (size_t)frame * ex->plan.max_kps;
-    if (cnt > 0 && kps &&
-        hipMemcpy(kps, s.kps + base, sizeof(orbx_keypoint) * cnt, hipMemcpyDeviceToHost) != hipSuccess)
-        return ORBX_EIO;
-    if (cnt > 0 && desc && hipMemcpy(desc, s.desc + base * 32, 32 * (size_t)cnt, hipMemcpyDeviceToHost) != hipSuccess)
-        return ORBX_EIO;
-    return ORBX_OK;
+    if (cnt > 0 && kps) copy(kps, s.kps + base, sizeof(orbx_keypoint) * cnt);
+    if (cnt > 0 && desc) copy(desc, s.desc + base * 32, 32 * (size_t)cnt);
+    return copy.wait() ? ORBX_OK : ORBX_EIO;
 }
 
 namespace {
@@ -979,6 +1065,7 @@ int orbx_extract(orbx_extractor *ex, const uint8_t *image, int width, int height
         }
         std::atomic_thread_fence(std::memory_order_acquire);
         ex->cur = 0;
+        ex->res_pending = false;   // (the graph's work is complete: its last kernel raised the flag)
         ex->match_batch = 0;
         ex->host_result_valid = true;
         int32_t cnt, lc[kMaxLevels];
@@ -1009,10 +1096,52 @@ int orbx_extractor_pyramid_level(orbx_extractor *ex, int level, uint8_t *out, si
     const auto &s = ex->slot[ex->cur];
     if (s.batch <= 0) return ORBX_EINVAL;
     if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
-    if (hipDeviceSynchronize() != hipSuccess) return ORBX_EIO;
+    if (sync_results(ex)) return ORBX_EIO;
     const uint8_t *src = level == 0 ? s.img0 : ex->d_pyr + g.pyr_off;
     const size_t sp = level == 0 ? (size_t)s.img0_pitch : (size_t)g.pitch;
-    return check(hipMemcpy2D(out, out_pitch, src, sp, g.w, g.h, hipMemcpyDeviceToHost));
+    if (hipMemcpy2DAsync(out, out_pitch, src, sp, g.w, g.h, hipMemcpyDeviceToHost, ex->stream) != hipSuccess)
+        return ORBX_EIO;
+    return check(hipStreamSynchronize(ex->stream));
+}
+
+int orbx_extractor_pyramid_host(orbx_extractor *ex, uint8_t *const *out, const size_t *out_pitch, int nlevels) {
+    if (!ex || !ex->planned || !out || !out_pitch || nlevels < 1 || nlevels > ex->nlevels) return ORBX_EINVAL;
+    const auto &s = ex->slot[ex->cur];
+    if (s.batch <= 0) return ORBX_EINVAL;
+    size_t total = 0;
+    for (int l = 0; l < nlevels; ++l) {
+        if (!out[l] || out_pitch[l] < (size_t)ex->plan.lv[l].w) return ORBX_EINVAL;
+        total += (size_t)ex->plan.lv[l].w * ex->plan.lv[l].h;
+    }
+    if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
+    if (ex->h_pyr_bytes < total) {
+        if (ex->h_pyr) (void)hipHostFree(ex->h_pyr);
+        ex->h_pyr = nullptr;
+        ex->h_pyr_bytes = 0;
+        if (hipHostMalloc(reinterpret_cast<void **>(&ex->h_pyr), total, hipHostMallocDefault) != hipSuccess)
+            return ORBX_ENOMEM;
+        ex->h_pyr_bytes = total;
+    }
+    if (sync_results(ex)) return ORBX_EIO;
+    // every level into the pinned staging in one stream-ordered chain, one wait
+    size_t off = 0;
+    for (int l = 0; l < nlevels; ++l) {
+        const LevelGeom &g = ex->plan.lv[l];
+        const uint8_t *src = l == 0 ? s.img0 : ex->d_pyr + g.pyr_off;
+        const size_t sp = l == 0 ? (size_t)s.img0_pitch : (size_t)g.pitch;
+        if (hipMemcpy2DAsync(ex->h_pyr + off, g.w, src, sp, g.w, g.h, hipMemcpyDeviceToHost, ex->stream) !=
+            hipSuccess)
+            return ORBX_EIO;
+        off += (size_t)g.w * g.h;
+    }
+    if (hipStreamSynchronize(ex->stream) != hipSuccess) return ORBX_EIO;
+    off = 0;
+    for (int l = 0; l < nlevels; ++l) {
+        const LevelGeom &g = ex->plan.lv[l];
+        for (int r = 0; r < g.h; ++r) std::memcpy(out[l] + (size_t)r * out_pitch[l], ex->h_pyr + off + (size_t)r * g.w, g.w);
+        off += (size_t)g.w * g.h;
+    }
+    return ORBX_OK;
 }
 
 int orbx_extractor_debug_fetch(orbx_extractor *ex, int frame, int level, int what, void *out, int64_t cap) {
@@ -1020,7 +1149,7 @@ int orbx_extractor_debug_fetch(orbx_extractor *ex, int frame, int level, int wha
     const auto &s = ex->slot[ex->cur];
     if (frame < 0 || frame >= s.batch) return ORBX_EINVAL;
     if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
-    if (hipDeviceSynchronize() != hipSuccess) return ORBX_EIO;
+    if (sync_results(ex)) return ORBX_EIO;
     const Plan &p = ex->plan;
     const LevelGeom &g = p.lv[level];
     if (what == 0 || what == 1) {
@@ -1112,6 +1241,7 @@ int orbx_mono_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t f
     if (!have_prev) {
         if ((rc = join_parts(ex, st, P))) return rc;
         mark(ex, kNumStages, st);
+        note_results(ex, st);
         return ORBX_OK;
     }
     MatchBufs mb;
@@ -1150,6 +1280,7 @@ int orbx_mono_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t f
         (void)hipFree(dclk);
     }
     mark(ex, kNumStages, st);
+    note_results(ex, st);
     mark_valid(ex, kStageMatch);
     ex->match_batch = batch;
     return ORBX_OK;
@@ -1158,20 +1289,19 @@ int orbx_mono_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t f
 int orbx_mono_matches_download(orbx_extractor *ex, int frame, int32_t *matches12, int cap, int *n1, int *nmatches) {
     if (!ex || !ex->planned || frame < 0 || frame >= ex->match_batch) return ORBX_EINVAL;
     if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
-    if (hipDeviceSynchronize() != hipSuccess) return ORBX_EIO;
+    if (sync_results(ex)) return ORBX_EIO;
     const int prev = ex->cur ^ 1;
     int32_t cnt = 0, nm = 0;
-    if (hipMemcpy(&cnt, ex->slot[prev].nkps + frame, sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess) return ORBX_EIO;
-    if (hipMemcpy(&nm, ex->d_nmatch + frame, sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess) return ORBX_EIO;
+    D2H copy{ex};
+    copy(&cnt, ex->slot[prev].nkps + frame, sizeof(int32_t));
+    copy(&nm, ex->d_nmatch + frame, sizeof(int32_t));
+    if (!copy.wait()) return ORBX_EIO;
     if (nm < 0) return ORBX_EIO;
     if (n1) *n1 = cnt;
     if (nmatches) *nmatches = nm;
     if (cnt > cap) return ORBX_ERANGE;
-    if (cnt > 0 && matches12 &&
-        hipMemcpy(matches12, ex->d_m12 + (size_t)frame * ex->plan.max_kps, sizeof(int32_t) * cnt,
-                  hipMemcpyDeviceToHost) != hipSuccess)
-        return ORBX_EIO;
-    return ORBX_OK;
+    if (cnt > 0 && matches12) copy(matches12, ex->d_m12 + (size_t)frame * ex->plan.max_kps, sizeof(int32_t) * cnt);
+    return copy.wait() ? ORBX_OK : ORBX_EIO;
 }
 
 int orbx_extractor_pipeline(orbx_extractor *ex, int on) {
@@ -1334,6 +1464,7 @@ int orbx_stereo_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t
     a.ur = ex->d_ur; a.depth = ex->d_depth; a.sad = ex->d_sad; a.ostride = kcap; a.nkept = ex->d_nkept;
     if (launch_stereo(a, pairs, kcap, st) != hipSuccess) return ORBX_EIO;
     mark(ex, kNumStages, st);
+    note_results(ex, st);
     mark_valid(ex, kStageMatch);
     ex->depth_mode = 1;
     ex->depth_count = pairs;
@@ -1368,6 +1499,7 @@ int orbx_rgbd_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t f
                     ex->plan.height, mbf, ex->d_ur, ex->d_depth, kcap, ex->d_nkept, batch, st) != hipSuccess)
         return ORBX_EIO;
     mark(ex, kNumStages, st);
+    note_results(ex, st);
     mark_valid(ex, kStageMatch);
     ex->depth_mode = 2;
     ex->depth_count = batch;
@@ -1377,21 +1509,20 @@ int orbx_rgbd_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t f
 int orbx_depth_download(orbx_extractor *ex, int index, float *uright, float *depth, int cap, int *n, int *nkept) {
     if (!ex || !ex->planned || !n || ex->depth_mode == 0 || index < 0 || index >= ex->depth_count) return ORBX_EINVAL;
     if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
-    if (hipDeviceSynchronize() != hipSuccess) return ORBX_EIO;
+    if (sync_results(ex)) return ORBX_EIO;
     const int frame = ex->depth_mode == 1 ? 2 * index : index;
     int32_t cnt = 0, nk = 0;
-    if (hipMemcpy(&cnt, ex->slot[ex->cur].nkps + frame, sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemcpy(&nk, ex->d_nkept + index, sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
-        return ORBX_EIO;
+    D2H copy{ex};
+    copy(&cnt, ex->slot[ex->cur].nkps + frame, sizeof(int32_t));
+    copy(&nk, ex->d_nkept + index, sizeof(int32_t));
+    if (!copy.wait()) return ORBX_EIO;
     *n = cnt;
     if (nkept) *nkept = nk;
     if (cnt > cap) return ORBX_ERANGE;
     const size_t base = (size_t)index * ex->plan.max_kps;
-    if (cnt > 0 && uright && hipMemcpy(uright, ex->d_ur + base, 4 * (size_t)cnt, hipMemcpyDeviceToHost) != hipSuccess)
-        return ORBX_EIO;
-    if (cnt > 0 && depth && hipMemcpy(depth, ex->d_depth + base, 4 * (size_t)cnt, hipMemcpyDeviceToHost) != hipSuccess)
-        return ORBX_EIO;
-    return ORBX_OK;
+    if (cnt > 0 && uright) copy(uright, ex->d_ur + base, 4 * (size_t)cnt);
+    if (cnt > 0 && depth) copy(depth, ex->d_depth + base, 4 * (size_t)cnt);
+    return copy.wait() ? ORBX_OK : ORBX_EIO;
 }
 
 int orbx_stereo_from_rgbd(int device, const orbx_keypoint *kps, const orbx_keypoint *kps_un, int n,
@@ -1403,29 +1534,36 @@ int orbx_stereo_from_rgbd(int device, const orbx_keypoint *kps, const orbx_keypo
     *nkept = 0;
     if (n == 0) return ORBX_OK;
     if (hipSetDevice(device) != hipSuccess) return ORBX_ENODEV;
-    orbx_keypoint *dk = nullptr, *dku = nullptr;
-    float *dmap = nullptr, *dur = nullptr, *ddp = nullptr;
-    int32_t *dn = nullptr, *dnk = nullptr;
-    int rc = ORBX_OK;
-    const bool ok = dalloc(&dk, n) == hipSuccess && dalloc(&dku, n) == hipSuccess &&
-                    dalloc(&dmap, (pitch / 4) * (size_t)height) == hipSuccess && dalloc(&dur, n) == hipSuccess &&
-                    dalloc(&ddp, n) == hipSuccess && dalloc(&dn, 1) == hipSuccess && dalloc(&dnk, 1) == hipSuccess;
-    if (!ok) rc = ORBX_ENOMEM;
-    if (!rc && (hipMemcpy(dk, kps, sizeof(orbx_keypoint) * n, hipMemcpyHostToDevice) != hipSuccess ||
-                hipMemcpy(dku, kps_un ? kps_un : kps, sizeof(orbx_keypoint) * n, hipMemcpyHostToDevice) != hipSuccess ||
-                hipMemcpy(dmap, depth_map, pitch * (size_t)height, hipMemcpyHostToDevice) != hipSuccess ||
-                hipMemcpy(dn, &n, sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess))
-        rc = ORBX_EIO;
-    if (!rc && (launch_rgbd(dk, dku, dn, n, n, dmap, 0, (int)pitch, width, height, mbf, dur, ddp, n, dnk, 1,
-                            nullptr) != hipSuccess ||
-                hipDeviceSynchronize() != hipSuccess))
-        rc = ORBX_EIO;
-    if (!rc && (hipMemcpy(uright, dur, 4 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess ||
-                hipMemcpy(depth, ddp, 4 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess ||
-                hipMemcpy(nkept, dnk, sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess))
-        rc = ORBX_EIO;
-    dfree(dk); dfree(dku); dfree(dmap); dfree(dur); dfree(ddp); dfree(dn); dfree(dnk);
-    return rc;
+    // the per-call workspace (no allocation per call); inputs: mvKeysUn and the
+    // depth samples imDepth.at<float>(v, u) at the mvKeys positions (an
+    // out-of-image keypoint, undefined in the reference, gets 0: no depth)
+    Layout L;
+    const size_t o_k = L.add(sizeof(orbx_keypoint) * (size_t)n), o_s = L.add(4 * (size_t)n);
+    const size_t o_nk = L.add(4), in_end = L.size;
+    const size_t o_ur = L.add(4 * (size_t)n), o_d = L.add(4 * (size_t)n), out_end = L.size;
+    CallWs &ws = call_ws(device);
+    std::lock_guard<std::mutex> lock(ws.mu);
+    int rc = ws_reserve(ws, L.size);
+    if (rc) return rc;
+    put(ws, o_k, kps_un ? kps_un : kps, sizeof(orbx_keypoint) * (size_t)n);
+    float *samp = reinterpret_cast<float *>(ws.host + o_s);
+    const size_t pf = pitch / 4;
+    for (int i = 0; i < n; ++i) {
+        const int v = (int)kps[i].y, u = (int)kps[i].x;
+        samp[i] = (v >= 0 && v < height && u >= 0 && u < width) ? depth_map[(size_t)v * pf + u] : 0.0f;
+    }
+    std::memset(ws.host + o_nk, 0, 4);
+    uint8_t *D = ws.dev;
+    if (hipMemcpyAsync(D, ws.host, in_end, hipMemcpyHostToDevice, ws.st) != hipSuccess ||
+        launch_rgbd_samples(at<float>(D, o_s), at<orbx_keypoint>(D, o_k), n, mbf, at<float>(D, o_ur),
+                            at<float>(D, o_d), at<int32_t>(D, o_nk), ws.st) != hipSuccess)
+        return ORBX_EIO;
+    // (the count sits just before the outputs: one contiguous run back)
+    if (ws_finish(ws, o_nk, out_end - o_nk)) return ORBX_EIO;
+    get(ws, o_ur, uright, 4 * (size_t)n);
+    get(ws, o_d, depth, 4 * (size_t)n);
+    get(ws, o_nk, nkept, 4);
+    return ORBX_OK;
 }
 
 int orbx_descriptor_distance(const uint8_t *a, const uint8_t *b) {
@@ -1494,10 +1632,8 @@ int orbx_search_for_initialization_bounds(int device, const orbx_keypoint *k1, c
     mb.min_x = min_x; mb.max_x = max_x; mb.min_y = min_y; mb.max_y = max_y;
     mb.window = window; mb.nnratio = nnratio;
     mb.check_ori = check_ori; mb.reset_prev = 0; mb.clocks = nullptr;
-    if (launch_match(mb, 1, n1c, n2c, q, c, ws.st) != hipSuccess ||
-        hipMemcpyAsync(ws.host + o_prev, D + o_prev, out_end - o_prev, hipMemcpyDeviceToHost, ws.st) != hipSuccess ||
-        hipStreamSynchronize(ws.st) != hipSuccess)
-        return ORBX_EIO;
+    if (launch_match(mb, 1, n1c, n2c, q, c, ws.st) != hipSuccess) return ORBX_EIO;
+    if (ws_finish(ws, o_prev, out_end - o_prev)) return ORBX_EIO;
     int32_t nm = 0;
     get(ws, o_nm, &nm, 4);
     if (nm < 0) return ORBX_EIO;
@@ -1637,10 +1773,8 @@ int proj_run(int device, int variant, orbx_proj_problem *P, int np, int th_dist,
         put(ws, o_pa, hb.data(), sizeof(ProjBufs) * nl);
         std::memset(ws.host + o_cnt, 0, 8 + 8 * (size_t)nl);
         if (hipMemcpyAsync(D, ws.host, in_bytes, hipMemcpyHostToDevice, ws.st) != hipSuccess) return ORBX_EIO;
-        if (launch_proj(hb.data(), at<ProjBufs>(D, o_pa), nl, ws.st) != hipSuccess ||
-            hipMemcpyAsync(ws.host + o_cnt, D + o_cnt, out_end - o_cnt, hipMemcpyDeviceToHost, ws.st) != hipSuccess ||
-            hipStreamSynchronize(ws.st) != hipSuccess)
-            return ORBX_EIO;
+        if (launch_proj(hb.data(), at<ProjBufs>(D, o_pa), nl, ws.st) != hipSuccess) return ORBX_EIO;
+        if (ws_finish(ws, o_cnt, out_end - o_cnt)) return ORBX_EIO;
         unsigned long long used = 0;
         get(ws, o_cnt, &used, 8);
         if (dbg_stats) {
@@ -1794,14 +1928,11 @@ int bow_run(int device, int variant, orbx_bow_problem *P, int np, float nnratio,
         a.hist = at<int32_t>(D, o[t].cnt); a.counts = at<int32_t>(D, o[t].cnt) + 32;
     }
     put(ws, o_pa, hb.data(), sizeof(BowBufs) * nl);
-    if (hipMemcpyAsync(D, ws.host, in_bytes, hipMemcpyHostToDevice, ws.st) != hipSuccess ||
-        hipMemsetAsync(D + in_bytes, 0, cnt_end - in_bytes, ws.st) != hipSuccess)
-        return ORBX_EIO;
+    std::memset(ws.host + in_bytes, 0, cnt_end - in_bytes);   // the counters go up as zeros with the inputs
+    if (hipMemcpyAsync(D, ws.host, cnt_end, hipMemcpyHostToDevice, ws.st) != hipSuccess) return ORBX_EIO;
     const size_t o_out = o[0].ma;   // match arrays and counters are one contiguous run
-    if (launch_bow(hb.data(), at<BowBufs>(D, o_pa), nl, ws.st) != hipSuccess ||
-        hipMemcpyAsync(ws.host + o_out, D + o_out, cnt_end - o_out, hipMemcpyDeviceToHost, ws.st) != hipSuccess ||
-        hipStreamSynchronize(ws.st) != hipSuccess)
-        return ORBX_EIO;
+    if (launch_bow(hb.data(), at<BowBufs>(D, o_pa), nl, ws.st) != hipSuccess) return ORBX_EIO;
+    if (ws_finish(ws, o_out, cnt_end - o_out)) return ORBX_EIO;
     for (int t = 0; t < nl; ++t) {
         orbx_bow_problem &pr = P[live[t]];
         get(ws, o[t].ma, pr.match_a, 4 * (size_t)pr.a.n);

@@ -539,6 +539,28 @@ __global__ __launch_bounds__(kST) void k_rgbd_depth(const orbx_keypoint *kps, co
     if ((threadIdx.x & 63) == 0 && m) atomicAdd(&nkept[b], __popcll(m));
 }
 
+// The host call's form: the depth samples at the keypoints (imDepth.at<float>(v, u),
+// gathered by the host so the map itself never crosses PCIe: 4 B per keypoint
+// instead of the whole CV_32F image), then the same arithmetic as k_rgbd_depth.
+__global__ __launch_bounds__(kST) void k_rgbd_samples(const float *dsample, const orbx_keypoint *kun, int n, float mbf,
+                                                      float *ur, float *depth, int32_t *nkept) {
+    const int i = blockIdx.x * kST + threadIdx.x;
+    bool got = false;
+    if (i < n) {
+        const float d = dsample[i];
+        float u_out = -1.0f, d_out = -1.0f;
+        if (d > 0.0f) {
+            d_out = d;
+            u_out = __fsub_rn(kun[i].x, __fdiv_rn(mbf, d));
+            got = true;
+        }
+        ur[i] = u_out;
+        depth[i] = d_out;
+    }
+    const uint64_t m = __ballot(got);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(nkept, __popcll(m));
+}
+
 }  // namespace
 
 int stereo_lds_bytes(int rows, int nr_cap) {
@@ -559,6 +581,14 @@ hipError_t launch_stereo(const StereoBufs &a, int pairs, int nl_cap, hipStream_t
     else
         hipLaunchKernelGGL(k_stereo_band, dim3((nl_cap + kST - 1) / kST, pairs), dim3(kST), bytes, st, a);
     hipLaunchKernelGGL(k_stereo_cut, dim3(pairs), dim3(kST), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_rgbd_samples(const float *dsample, const orbx_keypoint *kun, int n, float mbf, float *ur, float *depth,
+                               int32_t *nkept, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rgbd_samples, dim3((n + kST - 1) / kST), dim3(kST), 0, st, dsample, kun, n, mbf, ur, depth,
+                       nkept);
     return hipGetLastError();
 }
 

@@ -23,6 +23,9 @@ struct CallWs {
     std::mutex mu;
     hipStream_t st = nullptr;
     uint8_t *dev = nullptr, *host = nullptr;
+    uint8_t *host_d = nullptr;    // the pinned arena's device address (ws_finish writes there)
+    uint32_t *flag = nullptr;     // pinned done flag of ws_finish
+    uint32_t *flag_d = nullptr;
     size_t cap = 0;
     int64_t proj_pool = 0;   // projection candidate-list entries the last calls needed
 };
@@ -44,6 +47,10 @@ struct Layout {
 // Ensures stream and capacity (caller holds ws.mu and has set the device).
 inline int ws_reserve(CallWs &ws, size_t bytes) {
     if (!ws.st && hipStreamCreateWithFlags(&ws.st, hipStreamNonBlocking) != hipSuccess) return ORBX_EIO;
+    if (!ws.flag) {
+        if (hipHostMalloc(reinterpret_cast<void **>(&ws.flag), 64, hipHostMallocDefault) != hipSuccess) return ORBX_ENOMEM;
+        if (hipHostGetDevicePointer(reinterpret_cast<void **>(&ws.flag_d), ws.flag, 0) != hipSuccess) ws.flag_d = nullptr;
+    }
     if (ws.cap >= bytes) return ORBX_OK;
     (void)hipStreamSynchronize(ws.st);
     if (ws.dev) (void)hipFree(ws.dev);
@@ -57,9 +64,18 @@ inline int ws_reserve(CallWs &ws, size_t bytes) {
         ws.dev = nullptr;
         return ORBX_ENOMEM;
     }
+    if (hipHostGetDevicePointer(reinterpret_cast<void **>(&ws.host_d), ws.host, 0) != hipSuccess) ws.host_d = nullptr;
     ws.cap = cap;
     return ORBX_OK;
 }
+
+// Brings [off, off + bytes) of the device arena into the pinned arena after
+// the work queued on ws.st, and waits for it: a one-workgroup kernel writes
+// the bytes straight into the (device-visible) pinned buffer and then raises
+// a flag the host polls, instead of a copy plus a stream synchronisation
+// (about 10 us of wake-up for a call of ~50 us).  Large outputs take the copy.
+// Caller holds ws.mu.
+int ws_finish(CallWs &ws, size_t off, size_t bytes);
 
 template <typename T>
 inline T *at(uint8_t *base, size_t off) { return reinterpret_cast<T *>(base + off); }

@@ -24,7 +24,22 @@
 //        OrbxFrameAux::ToGray (3-channel RGB image) and UndistortKeyPoints
 //        (TUM1 camera) of the keypoints file (n, then n x 28 B): writes the
 //        gray image (W x H) and the undistorted (x, y) pairs.
+//   adapter_test time W H img.raw nfeatures reps
+//        the drop-in as Frame::ExtractORB calls it (Frame.cc:259-265): prints
+//        "extract_ms <median>" of ORBextractor::operator(), then
+//        "pyramid_read_ms <median>" of an mvImagePyramid read after a call.
+//   adapter_test time_stereo W H left.raw right.raw nfeatures mbf mb reps
+//        Frame's stereo constructor: both images extracted on two threads
+//        started per frame (Frame.cc:79-82), then ComputeStereoMatches through
+//        OrbxFrame (Frame_orbx.cc): prints "pair_ms <median>".
+//   adapter_test time_rgbd W H img.raw depth.raw mbf reps
+//        Frame's RGB-D constructor: extraction, then ComputeStereoFromRGBD
+//        (Frame.cc:679-701) through OrbxFrame: prints "rgbd_frame_ms <median>"
+//        and "rgbd_depth_ms <median>" (the depth call alone).
+#include <algorithm>
+#include <chrono>
 #include <cstdio>
+#include <thread>
 #include <cstring>
 #include <map>
 #include <fstream>
@@ -54,7 +69,84 @@ static void put_kps(std::ofstream &out, const std::vector<cv::KeyPoint> &ks, con
     for (int r = 0; r < n; ++r) out.write(reinterpret_cast<const char *>(d.ptr<uint8_t>(r)), 32);
 }
 
+template <class F>
+static double median_ms(int reps, F f) {
+    std::vector<double> t(reps);
+    for (int i = 0; i < reps; ++i) {
+        const auto t0 = std::chrono::steady_clock::now();
+        f();
+        t[i] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    std::sort(t.begin(), t.end());
+    return t[reps / 2];
+}
+
 int main(int argc, char **argv) {
+    if (argc == 7 && std::string(argv[1]) == "time") {
+        const int w = std::atoi(argv[2]), h = std::atoi(argv[3]), reps = std::atoi(argv[6]);
+        cv::Mat im = load(argv[4], w, h);
+        ORBextractor ex(std::atoi(argv[5]), 1.2f, 8, 20, 7);
+        std::vector<cv::KeyPoint> k;
+        cv::Mat d;
+        for (int i = 0; i < 5; ++i) ex(im, cv::Mat(), k, d);
+        std::printf("extract_ms %.4f\n", median_ms(reps, [&] { ex(im, cv::Mat(), k, d); }));
+        int rows = 0;
+        std::vector<double> t(reps);
+        for (int i = 0; i < reps; ++i) {   // a call, then the first read of the pyramid
+            ex(im, cv::Mat(), k, d);
+            const auto t0 = std::chrono::steady_clock::now();
+            rows += ex.mvImagePyramid[0].rows;
+            t[i] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        }
+        std::sort(t.begin(), t.end());
+        std::printf("pyramid_read_ms %.4f\n", t[reps / 2]);
+        std::printf("keypoints %zu rows %d\n", k.size(), rows / reps);
+        return 0;
+    }
+    if (argc == 10 && std::string(argv[1]) == "time_stereo") {
+        const int w = std::atoi(argv[2]), h = std::atoi(argv[3]), nf = std::atoi(argv[6]), reps = std::atoi(argv[9]);
+        const float mbf = (float)std::atof(argv[7]), mb = (float)std::atof(argv[8]);
+        cv::Mat il = load(argv[4], w, h), ir = load(argv[5], w, h);
+        ORBextractor exl(nf, 1.2f, 8, 20, 7), exr(nf, 1.2f, 8, 20, 7);
+        std::vector<cv::KeyPoint> kl, kr;
+        cv::Mat dl, dr;
+        std::vector<float> ur, dp;
+        int kept = 0;
+        auto pair = [&] {
+            std::thread tl([&] { exl(il, cv::Mat(), kl, dl); });
+            std::thread tr([&] { exr(ir, cv::Mat(), kr, dr); });
+            tl.join();
+            tr.join();
+            kept = OrbxFrame::ComputeStereoMatches(exl, exr, kl, dl, kr, dr, mbf, mb, ur, dp);
+        };
+        for (int i = 0; i < 5; ++i) pair();
+        std::printf("pair_ms %.4f\n", median_ms(reps, pair));
+        std::printf("keypoints %zu %zu kept %d\n", kl.size(), kr.size(), kept);
+        return 0;
+    }
+    if (argc == 8 && std::string(argv[1]) == "time_rgbd") {
+        const int w = std::atoi(argv[2]), h = std::atoi(argv[3]), reps = std::atoi(argv[7]);
+        const float mbf = (float)std::atof(argv[6]);
+        cv::Mat im = load(argv[4], w, h);
+        cv::Mat dm(h, w, CV_32F);
+        {
+            std::ifstream f(argv[5], std::ios::binary);
+            f.read(reinterpret_cast<char *>(dm.data), (std::streamsize)w * h * 4);
+        }
+        ORBextractor ex(1000, 1.2f, 8, 20, 7);
+        std::vector<cv::KeyPoint> k;
+        cv::Mat d;
+        std::vector<float> ur, dp;
+        auto depth = [&] { OrbxFrame::ComputeStereoFromRGBD(k, k, dm, mbf, ur, dp); };
+        auto frame = [&] { ex(im, cv::Mat(), k, d); depth(); };
+        for (int i = 0; i < 5; ++i) frame();
+        std::printf("rgbd_frame_ms %.4f\n", median_ms(reps, frame));
+        std::printf("rgbd_depth_ms %.4f\n", median_ms(reps, depth));
+        int nd = 0;
+        for (float v : dp) nd += v > 0;
+        std::printf("keypoints %zu depths %d\n", k.size(), nd);
+        return 0;
+    }
     if (argc >= 2 && std::string(argv[1]) == "probe") {
         try {
             ORBextractor ex(1000, 1.2f, 8, 20, 7);

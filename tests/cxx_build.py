@@ -7,8 +7,9 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 
 
-def build_adapter_test() -> Path:
-    out = Path(tempfile.mkdtemp(prefix="orbx_cxx_")) / "adapter_test"
+def build_adapter_test(out: Path = None) -> Path:
+    out = Path(out) if out is not None else Path(tempfile.mkdtemp(prefix="orbx_cxx_")) / "adapter_test"
+    out.parent.mkdir(parents=True, exist_ok=True)
     lib_dir = ROOT / "orb_slam_2_ros_amd"
     subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", "-Werror", f"-I{ROOT / 'include'}",
                     f"-I{ROOT / 'tests' / 'cxx' / 'cv_mock'}", str(ROOT / "tests" / "cxx" / "adapter_test.cpp"),
