@@ -226,12 +226,34 @@ def max_over_ranks(torch, dist, world, el, device):
     return float(t.item())
 
 
+def write_bow_case(path, variant: int, A, B, tri, nnratio: float, check_ori: bool, nlevels: int = 8):
+    """One SearchByBoW problem as adapter_test time_bow reads it."""
+    from orb_slam_2_ros_amd._lib import KEYPOINT_DTYPE
+    t = np.zeros(0, np.float32) if tri is None else np.ascontiguousarray(tri, np.float32)
+    with open(path, "wb") as f:
+        f.write(np.array([variant, nlevels, int(check_ori), len(t), 0], np.int32).tobytes())
+        f.write(np.float32(nnratio).tobytes())
+        f.write(t.tobytes())
+        for S in (A, B):
+            k = np.ascontiguousarray(S["keys"], KEYPOINT_DTYPE)
+            ids = np.ascontiguousarray(S["ids"], np.uint32)
+            feat = np.ascontiguousarray(S["feat"], np.int32)
+            f.write(np.array([len(k), len(ids), len(feat)], np.int32).tobytes())
+            f.write(k.tobytes())
+            f.write(np.ascontiguousarray(S["desc"], np.uint8).tobytes())
+            f.write(np.ascontiguousarray(S["flags"], np.uint8).tobytes())
+            f.write(ids.tobytes())
+            f.write(np.ascontiguousarray(S["off"], np.int32).tobytes())
+            f.write(feat.tobytes())
+
+
 def matcher_latencies(reps: int = 20):
     """Per-call latency of the drop-in ORBmatcher searches (host arrays in and
     out, as Tracking / LocalMapping / LoopClosing call them) next to the
     oracle's single-thread time on the same inputs."""
     from oracle import oracle
     from orb_slam_2_ros_amd import ORBmatcher
+    from orb_slam_2_ros_amd.matcher import BOW_VARIANTS
     from orb_slam_2_ros_amd.synth_match import (BOW_VARIANT_ARGS, PROJ_VARIANT_ARGS, make_bow_case,
                                                 make_proj_case)
 
@@ -264,6 +286,7 @@ def matcher_latencies(reps: int = 20):
         name = "SearchByBoW_kf_frame" if variant == "kf_frame" else "SearchForTriangulation"
         out[name] = {"features": na,
                      "gpu_ms": round(timed(lambda: m.search_by_bow(variant, A, B, tri), reps), 4),
+                     "cxx_ms": cxx_bow_latency(BOW_VARIANTS[variant], A, B, tri, ratio, ori, 100),
                      "cpu_ms": round(timed(lambda: oracle.search_by_bow(variant, A, B, ratio, ori, tri), 5), 4)}
     out["local_mapping_20_neighbours"] = local_mapping_matchers(reps)
     return out
@@ -612,6 +635,28 @@ def dropin_latency(torch, dev, reps=100):
     return out
 
 
+def _adapter_exe():
+    exe = Path(__file__).resolve().parent / "orb_slam_2_ros_amd" / "bin" / "adapter_test"
+    if not exe.exists():
+        sys.path.insert(0, str(Path(__file__).resolve().parent / "tests"))
+        from cxx_build import build_adapter_test
+        build_adapter_test(exe)
+    return exe
+
+
+def cxx_bow_latency(variant: int, A, B, tri, nnratio, check_ori, reps):
+    """A SearchByBoW call through the C++ forwarder's entry
+    (OrbxMatcher::SearchByBoWTable), as ORBmatcher_orbx.cc makes it: ms."""
+    import subprocess
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        p = Path(td) / "bow.bin"
+        write_bow_case(p, variant, A, B, tri, nnratio, check_ori)
+        r = subprocess.run([str(_adapter_exe()), "time_bow", str(p), str(reps)], capture_output=True, text=True,
+                           timeout=120, check=True)
+    return float(r.stdout.split("bow_ms")[1].split()[0])
+
+
 def cxx_dropin_latency(L, R, bf, mb, reps):
     """The C++ drop-in (include/orbx_orbslam2.hpp) as a reference tree would
     link it, timed by orb_slam_2_ros_amd/bin/adapter_test (built by
@@ -623,11 +668,7 @@ def cxx_dropin_latency(L, R, bf, mb, reps):
     import subprocess
     import tempfile
     from orb_slam_2_ros_amd import synth
-    exe = Path(__file__).resolve().parent / "orb_slam_2_ros_amd" / "bin" / "adapter_test"
-    if not exe.exists():
-        sys.path.insert(0, str(Path(__file__).resolve().parent / "tests"))
-        from cxx_build import build_adapter_test
-        build_adapter_test(exe)
+    exe = _adapter_exe()
 
     def run(*args):
         r = subprocess.run([str(exe), *map(str, args)], capture_output=True, text=True, timeout=300, check=True)
@@ -1011,6 +1052,8 @@ def main() -> int:
             res = c5_config(torch, dist, rank, world, dev, args.steps, args.warmup, profile, *c5_args)
         if args.extra == "dropin":
             res = dropin_latency(torch, dev)
+        if args.extra == "matchers":   # the drop-in ORBmatcher calls (host arrays), per call
+            res = matcher_latencies()
         if args.extra in ("c5_rank8", "c5_rank8_k8"):   # one rank's share of C5 at 8 GPUs
             res = c5_config(torch, dist, rank, world, dev, args.steps, args.warmup, profile, *c5_args, total=8,
                             kframes=8 if args.extra == "c5_rank8_k8" else 1, exchange=False)

@@ -107,6 +107,7 @@ struct StereoBufs {
     float mbf, maxd;          // maxD = mbf / mb (Frame.cc:532-534)
     float *ur, *depth; int32_t *sad; int64_t ostride; int32_t *nkept;
     float *hout; int64_t hcap;   // optional host-visible copy of one pair's results (k_stereo_cut)
+    uint8_t *bands; int64_t band_stride;   // optional per-pair band scratch (sorted once per pair), or nullptr
 };
 
 // Projection searches (ORBmatcher SearchByProjection x4, Fuse x2): one frame
@@ -168,6 +169,7 @@ hipError_t launch_trig_check(const float *in, float *s, float *c, float *atan_ou
                              const float *ay, const float *ax, int n, int m, hipStream_t st);
 hipError_t launch_stereo(const StereoBufs &a, int pairs, int nl_cap, hipStream_t s);
 int stereo_lds_bytes(int rows, int nr_cap);
+int64_t stereo_band_stride(int rows, int nr_cap);   // per-pair band scratch (StereoBufs::bands)
 hipError_t launch_rgbd_samples(const float *dsample, const orbx_keypoint *kun, int n, float mbf, float *ur, float *depth,
                                int32_t *nkept, hipStream_t st);
 hipError_t launch_rgbd(const orbx_keypoint *kps, const orbx_keypoint *kun, const int32_t *nkps, int64_t kstride,

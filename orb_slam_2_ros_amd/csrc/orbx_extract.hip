@@ -1073,6 +1073,9 @@ constexpr int kQRegKeys = 6, kQRegKeysWide = kQuadRegKeys / kThreads;
 #define ORBX_QT_QU 4
 #endif
 constexpr int kQU = ORBX_QT_QU;
+#ifndef ORBX_QT_PF
+#define ORBX_QT_PF 1
+#endif
 template <int R>
 struct QKeys {
     static constexpr int C = R > 0 ? R : kQU;   // registers: the keys, or the chunk cache
@@ -1095,6 +1098,40 @@ struct QKeys {
             }
         }
     }
+    // the chunk at k0 into (pk, pq) without touching the cache (prefetch)
+    __device__ inline void fetch(int k0, uint32_t *pk, uint32_t *pq) const {
+#pragma unroll
+        for (int u = 0; u < C; ++u) {
+            const int k = k0 + u * kThreads + (int)threadIdx.x;
+            if (k < n) {
+                pk[u] = gkeys[k];
+                pq[u] = (uint32_t)gnode[k] | ((uint32_t)(gq[k] & 3) << 16);
+            }
+        }
+    }
+    // body(k0) over every chunk, the next chunk's loads in flight while the
+    // body runs (ORBX_QT_PF; the loads of a chunk precede the stores of the
+    // chunk before it, and the chunks are disjoint)
+    template <typename B>
+    __device__ inline void chunks(B body) {
+#if ORBX_QT_PF
+        uint32_t pk[C], pq[C];
+        fetch(0, pk, pq);
+        for (int k0 = 0; k0 < n; k0 += kThreads * kQU) {
+#pragma unroll
+            for (int u = 0; u < C; ++u) { key[u] = pk[u]; nq[u] = pq[u]; }
+            if (k0 + kThreads * kQU < n) fetch(k0 + kThreads * kQU, pk, pq);
+            body(k0);
+            store(k0);
+        }
+#else
+        for (int k0 = 0; k0 < n; k0 += kThreads * kQU) {
+            load(k0);
+            body(k0);
+            store(k0);
+        }
+#endif
+    }
     __device__ inline void store(int k0) {
 #pragma unroll
         for (int u = 0; u < C; ++u) {
@@ -1115,15 +1152,13 @@ struct QKeys {
                 if (k < n) f(j, k);
             }
         } else {
-            for (int k0 = 0; k0 < n; k0 += kThreads * kQU) {
-                load(k0);
+            chunks([&](int k0) {
 #pragma unroll
                 for (int u = 0; u < kQU; ++u) {
                     const int k = k0 + u * kThreads + (int)threadIdx.x;
                     if (k < n) f(u, k);
                 }
-                store(k0);
-            }
+            });
         }
     }
     // f(j, k, valid) on every lane for every key slot (bodies with DPP)
@@ -1136,15 +1171,13 @@ struct QKeys {
                 f(j, k, k < n);
             }
         } else {
-            for (int k0 = 0; k0 < n; k0 += kThreads * kQU) {
-                load(k0);
+            chunks([&](int k0) {
 #pragma unroll
                 for (int u = 0; u < kQU; ++u) {
                     const int k = k0 + u * kThreads + (int)threadIdx.x;
                     f(u, k, k < n);
                 }
-                store(k0);
-            }
+            });
         }
     }
     __device__ inline uint32_t get_key(int j, int) const { return key[j]; }
@@ -1227,6 +1260,30 @@ __device__ __attribute__((always_inline)) void child_stats(const QLds &s, QKeys<
 
 __device__ inline void zero_children(const QLds &s, int S) {
     for (int i = threadIdx.x; i < 4 * S; i += kThreads) { s.ccnt[i] = 0; s.cbest[i] = 0; }
+}
+
+// One key pass per round: each key moves to its node of the round just built
+// (nidx_c[4 node + quadrant]) and, when that node is splittable, adds itself
+// to the node's child counts (as child_stats).  Ends with a barrier.
+template <int R>
+__device__ __attribute__((always_inline)) void advance_stats(const QLds &s, QKeys<R> &K) {
+    K.each_all([&](int j, int k, bool valid) {
+        uint32_t slot = ~0u, bp = 0;
+        if (valid) {
+            const int nd = s.nidx_c[4 * K.node(j, k) + K.quad(j, k)];
+            K.set_node(j, k, nd);
+            const QNode node = s.cur[nd];
+            if (node.count > 1) {
+                const uint32_t key = K.get_key(j, k);
+                const int q = quadrant_of(node, key);
+                K.set_quad(j, k, q);
+                slot = 4u * (uint32_t)nd + (uint32_t)q;
+                bp = best_pack(key, k);
+            }
+        }
+        agg_atomics(s.ccnt, s.cbest, slot, bp);
+    });
+    __syncthreads();
 }
 
 // A node that keeps its keys maps all four quadrant slots to its new index,
@@ -1332,12 +1389,18 @@ __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p,
     PHASE_MARK(2, 1);   // roots
 
     if (p.dbg_stop == 2) return;
-    // ---- 3. full rounds (ORBextractor.cc:618-696)
+    // Each round is one key pass: the pass that moves the keys into their
+    // new nodes also adds them to those nodes' child counts (advance_stats),
+    // and the child counts are re-zeroed in the round's node phase (each
+    // thread its own nodes' entries after it read them, plus [4 S, 4 S2)), so
+    // the rounds need no pass of their own for either.  The last round's move
+    // only matters to the register path's output (phase 5).
     bool final_phase = false;
+    int S = sh_S;
+    child_stats(s, K);
+    PHASE_MARK(2, 2);   // child counts
+    // ---- 3. full rounds (ORBextractor.cc:618-696)
     while (true) {
-        const int S = sh_S;
-        child_stats(s, K);
-        PHASE_MARK(2, 2);   // full rounds: child counts
         // per node: (non-empty children | single-key parents << 21 | children
         // with more than one key << 42), scanned over a contiguous node range
         // per thread, so each thread reads back only its own entries
@@ -1388,25 +1451,31 @@ __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p,
                 set_all_quads(s.nidx_c, i, ni);
             }
         }
+        // (only this thread reads its nodes' child entries)
+        for (int i = 4 * i0; i < 4 * i1; ++i) { s.ccnt[i] = 0; s.cbest[i] = 0; }
+        for (int i = 4 * S + tid; i < 4 * S2; i += kThreads) { s.ccnt[i] = 0; s.cbest[i] = 0; }
         __syncthreads();
-        K.each([&](int j, int k) { K.set_node(j, k, s.nidx_c[4 * K.node(j, k) + K.quad(j, k)]); });
-        zero_children(s, S2);
         {
             QNode *t = s.cur; s.cur = s.nxt; s.nxt = t;
         }
-        if (tid == 0) sh_S = S2;
-        __syncthreads();
         PHASE_MARK(2, 3);   // full rounds: scan + children
-        if (S2 >= N || S2 == S) break;
-        if (S2 + nexp * 3 > N) { final_phase = true; break; }
+        const bool stop = S2 >= N || S2 == S;
+        final_phase = !stop && S2 + nexp * 3 > N;
+        S = S2;
+        if (stop) {
+            if constexpr (NR > 0) K.each([&](int j, int k) { K.set_node(j, k, s.nidx_c[4 * K.node(j, k) + K.quad(j, k)]); });
+            break;
+        }
+        if (tid == 0) sh_nv = 0;   // (the final phase's count; ordered by the pass's barrier)
+        advance_stats(s, K);
+        PHASE_MARK(2, 2);   // full rounds: move + child counts
+        if (final_phase) break;
     }
 
     if (p.dbg_stop == 3) return;
-    // ---- 4. final phase (ORBextractor.cc:697-762)
+    // ---- 4. final phase (ORBextractor.cc:697-762); the child counts of the
+    //         S nodes are in place
     while (final_phase) {
-        const int S = sh_S;
-        if (tid == 0) sh_nv = 0;   // (ordered by child_stats' barrier)
-        child_stats(s, K);
         {
             int nz = 0;
             for (int i = tid; i < s.np2; i += kThreads) {
@@ -1422,7 +1491,7 @@ __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p,
         }
         for (int i = tid; i < S; i += kThreads) s.mark[i] = 0;
         __syncthreads();
-        PHASE_MARK(2, 4);   // final: child counts
+        PHASE_MARK(2, 4);   // final: node keys
         // descending order of the splittable nodes' (count, seq, index) keys
         // (all distinct) by rank counting: one barrier instead of a bitonic
         // network's log^2 stages; zeros (unsplittable) stay behind, in b64
@@ -1504,7 +1573,10 @@ __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p,
             s.mark[i] = 1;
         }
         __syncthreads();
+        // (the child entries are read no more this round: re-zeroed for the
+        // next round's counts, S2 >= S)
         for (int i = tid; i < s.np2; i += kThreads) s.b64[i] = (i < S && !s.mark[i]) ? 1 : 0;
+        zero_children(s, S2);
         __syncthreads();
         block_excl_scan_u64(s.b64, s.np2, ws64);
         for (int i = tid; i < S; i += kThreads) {
@@ -1514,19 +1586,22 @@ __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p,
             set_all_quads(s.nidx_c, i, ni);
         }
         __syncthreads();
-        K.each([&](int j, int k) { K.set_node(j, k, s.nidx_c[4 * K.node(j, k) + K.quad(j, k)]); });
-        zero_children(s, S2);
         {
             QNode *t = s.cur; s.cur = s.nxt; s.nxt = t;
         }
-        if (tid == 0) sh_S = S2;
-        __syncthreads();
         PHASE_MARK(2, 6);   // final: splits
-        if (S2 >= N || S2 == S) break;
+        const bool stop = S2 >= N || S2 == S;
+        S = S2;
+        if (stop) {
+            if constexpr (NR > 0) K.each([&](int j, int k) { K.set_node(j, k, s.nidx_c[4 * K.node(j, k) + K.quad(j, k)]); });
+            break;
+        }
+        if (tid == 0) sh_nv = 0;
+        advance_stats(s, K);
+        PHASE_MARK(2, 4);   // final: move + child counts
     }
 
     // ---- 5. best key per node, in list order (ORBextractor.cc:765-784)
-    const int S = sh_S;
     uint32_t *sel = fb.sel + (int64_t)b * p.out_cap + g.out_off;
     const int S_out = min(S, g.out_cap);
     if constexpr (NR > 0) {

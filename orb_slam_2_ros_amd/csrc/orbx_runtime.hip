@@ -88,6 +88,7 @@ struct orbx_extractor {
     // depth results of the last stereo / RGB-D step (per pair or per frame)
     float *d_ur = nullptr, *d_depth = nullptr;
     int32_t *d_sad = nullptr, *d_nkept = nullptr;
+    uint8_t *d_bands = nullptr;   // per stereo pair: the right image's sorted bands (StereoBufs::bands)
     int depth_mode = 0;         // 0 none, 1 stereo (index = pair), 2 RGB-D (index = frame)
     int depth_count = 0;
 
@@ -207,7 +208,7 @@ struct orbx_extractor {
         dfree(d_cell_count); dfree(d_level_count); dfree(d_key_node); dfree(d_key_q);
         for (auto &s : slot) { dfree(s.kps); dfree(s.desc); dfree(s.nkps); s.batch = 0; }
         dfree(d_prev); dfree(d_m12); dfree(d_nmatch); dfree(d_img);
-        dfree(d_ur); dfree(d_depth); dfree(d_sad); dfree(d_nkept);
+        dfree(d_ur); dfree(d_depth); dfree(d_sad); dfree(d_nkept); dfree(d_bands);
         depth_mode = 0;
         depth_count = 0;
         d_img_bytes = 0;
@@ -390,6 +391,8 @@ int reserve(orbx_extractor *ex, int w, int h, int max_batch) {
     ok &= dalloc(&ex->d_depth, B * p.max_kps) == hipSuccess;
     ok &= dalloc(&ex->d_sad, B * p.max_kps) == hipSuccess;
     ok &= dalloc(&ex->d_nkept, B) == hipSuccess;
+    if (B >= 4 && p.max_kps <= 65535)
+        ok &= dalloc(&ex->d_bands, (size_t)(B / 2) * stereo_band_stride(p.height, p.max_kps)) == hipSuccess;
     if (!ok) { ex->release(); return ORBX_ENOMEM; }
     ex->planned = true;
     ex->max_batch = max_batch;
@@ -1462,6 +1465,7 @@ int orbx_stereo_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t
     a.kstride = 2 * (int64_t)kcap; a.nstride = 2; a.nr_cap = kcap;
     a.mbf = mbf; a.maxd = mbf / mb;
     a.ur = ex->d_ur; a.depth = ex->d_depth; a.sad = ex->d_sad; a.ostride = kcap; a.nkept = ex->d_nkept;
+    a.bands = ex->d_bands; a.band_stride = stereo_band_stride(a.rows, kcap);
     if (launch_stereo(a, pairs, kcap, st) != hipSuccess) return ORBX_EIO;
     mark(ex, kNumStages, st);
     note_results(ex, st);

@@ -17,6 +17,8 @@
 // what the walk computes in any order.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "orbx_device.h"
 #include "orbx_wave.h"
 
@@ -126,6 +128,10 @@ struct Bands {
     uint16_t *sidx;
     int8_t *soct;
 };
+
+__host__ __device__ inline int band_bytes(int rows, int nr_cap) {
+    return ((rows + 1) * 4 + nr_cap * (4 + 2 + 2 + 1) + 15) & ~15;
+}
 
 __device__ inline Bands bands_in(uint8_t *lds, const StereoBufs &a) {
     Bands d;
@@ -309,23 +315,17 @@ __device__ inline uint32_t group_min_u32(uint32_t v) {
     return v;
 }
 
-__global__ __launch_bounds__(kST) void k_stereo_band_g(StereoBufs a) {
-    extern __shared__ __align__(16) uint8_t lds[];
-    __shared__ int ws[4];
-    __shared__ int s_span;
-    constexpr int kPer = kST / kG;
-    const int b = blockIdx.y, tid = threadIdx.x;
+// Steps 2-4 for the kPer left keypoints of this block, a group of kG lanes
+// each, over the pair's sorted bands (LDS or the pair's scratch).
+__device__ __forceinline__ void group_search(const StereoBufs &a, int b, const Bands &bd, int span) {
+    const int tid = threadIdx.x;
     const int nl = a.nl[(int64_t)b * a.nstride];
-    const int i0 = blockIdx.x * kPer;
-    if (i0 >= nl) return;
+    const int i0 = blockIdx.x * (kST / kG);
     const int H = a.rows;
     const orbx_keypoint *kl = a.kl + (int64_t)b * a.kstride;
     const orbx_keypoint *kr = a.kr + (int64_t)b * a.kstride;
     const uint8_t *dl = a.dl + (int64_t)b * a.kstride * 32;
     const uint8_t *dr = a.dr + (int64_t)b * a.kstride * 32;
-    const Bands bd = bands_in(lds, a);
-    const int span = band_sort(a, b, bd, ws, &s_span);
-
     const int g = tid & (kG - 1);
     const int iL = i0 + tid / kG;
     if (iL >= nl) return;   // (whole groups leave together)
@@ -419,6 +419,44 @@ __global__ __launch_bounds__(kST) void k_stereo_band_g(StereoBufs a) {
         ur_out[iL] = bestuR;
         sad_out[iL] = bestSad;
     }
+}
+
+__global__ __launch_bounds__(kST) void k_stereo_band_g(StereoBufs a) {
+    extern __shared__ __align__(16) uint8_t lds[];
+    __shared__ int ws[4];
+    __shared__ int s_span;
+    const int b = blockIdx.y;
+    if (blockIdx.x * (kST / kG) >= a.nl[(int64_t)b * a.nstride]) return;
+    const Bands bd = bands_in(lds, a);
+    const int span = band_sort(a, b, bd, ws, &s_span);
+    group_search(a, b, bd, span);
+}
+
+// The bands of each pair sorted once (k_band_sort: the LDS image of band_sort
+// copied to the pair's scratch, span in its last dword), then the grouped
+// search over the scratch (k_stereo_band_gs), so a batch of pairs runs the
+// 16-lane search on thousands of small blocks without every block re-sorting
+// its pair's right keypoints.
+__global__ __launch_bounds__(kST) void k_band_sort(StereoBufs a) {
+    extern __shared__ __align__(16) uint8_t lds[];
+    __shared__ int ws[4];
+    __shared__ int s_span;
+    const int b = blockIdx.x;
+    const Bands bd = bands_in(lds, a);
+    const int span = band_sort(a, b, bd, ws, &s_span);
+    const int bytes = band_bytes(a.rows, a.nr_cap);
+    uint4 *dst = reinterpret_cast<uint4 *>(a.bands + (int64_t)b * a.band_stride);
+    const uint4 *src = reinterpret_cast<const uint4 *>(lds);
+    for (int i = threadIdx.x; i < bytes / 16; i += kST) dst[i] = src[i];
+    if (threadIdx.x == 0) reinterpret_cast<int *>(a.bands + (int64_t)b * a.band_stride + bytes)[0] = span;
+}
+
+__global__ __launch_bounds__(kST) void k_stereo_band_gs(StereoBufs a) {
+    const int b = blockIdx.y;
+    if (blockIdx.x * (kST / kG) >= a.nl[(int64_t)b * a.nstride]) return;
+    uint8_t *scr = a.bands + (int64_t)b * a.band_stride;
+    const int span = reinterpret_cast<const int *>(scr + band_bytes(a.rows, a.nr_cap))[0];
+    group_search(a, b, bands_in(scr, a), span);
 }
 
 // Median cut (Frame.cc:662-675): entries with SAD >= 1.5f*1.4f*median are
@@ -563,13 +601,27 @@ __global__ __launch_bounds__(kST) void k_rgbd_samples(const float *dsample, cons
 
 }  // namespace
 
-int stereo_lds_bytes(int rows, int nr_cap) {
-    return ((rows + 1) * 4 + nr_cap * (4 + 2 + 2 + 1) + 15) & ~15;
-}
+int stereo_lds_bytes(int rows, int nr_cap) { return band_bytes(rows, nr_cap); }
+
+int64_t stereo_band_stride(int rows, int nr_cap) { return ((int64_t)stereo_lds_bytes(rows, nr_cap) + 16 + 255) & ~255; }
 
 hipError_t launch_stereo(const StereoBufs &a, int pairs, int nl_cap, hipStream_t st) {
     if (pairs <= 0) return hipSuccess;
     const int bytes = stereo_lds_bytes(a.rows, a.nr_cap);
+    static const bool sorted_once = [] {
+        const char *e = std::getenv("ORBX_STEREO_SORT_ONCE");
+        return !(e && e[0] == '0');
+    }();
+    if (a.bands && sorted_once && pairs > 1) {
+        if (bytes > 64 * 1024 &&
+            hipFuncSetAttribute(reinterpret_cast<const void *>(k_band_sort), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                bytes) != hipSuccess)
+            return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_band_sort, dim3(pairs), dim3(kST), bytes, st, a);
+        hipLaunchKernelGGL(k_stereo_band_gs, dim3((nl_cap + kST / kG - 1) / (kST / kG), pairs), dim3(kST), 0, st, a);
+        hipLaunchKernelGGL(k_stereo_cut, dim3(pairs), dim3(kST), 0, st, a);
+        return hipGetLastError();
+    }
     // a lane per keypoint while that fills the chip, else a group of kG lanes
     const bool grouped = (int64_t)pairs * ((nl_cap + kST - 1) / kST) < 256;
     const void *fn = grouped ? reinterpret_cast<const void *>(k_stereo_band_g)

@@ -109,15 +109,18 @@ class ORBextractor:
 
     @property
     def mvImagePyramid(self) -> list:
+        """The last call's pyramid (ORBextractor::mvImagePyramid without the
+        EDGE_THRESHOLD border), all levels in one orbx_extractor_pyramid_host
+        call (one stream-ordered wait)."""
         levels = []
         for l in range(self.nlevels):
             w, h = ctypes.c_int(0), ctypes.c_int(0)
             check(self._lib.orbx_extractor_pyramid_level(self._h, l, None, 0, ctypes.byref(w), ctypes.byref(h)),
                   "pyramid level")
-            out = np.zeros((h.value, w.value), dtype=np.uint8)
-            check(self._lib.orbx_extractor_pyramid_level(self._h, l, ptr(out), w.value, None, None),
-                  "pyramid level")
-            levels.append(out)
+            levels.append(np.zeros((h.value, w.value), dtype=np.uint8))
+        outs = (ctypes.c_void_p * len(levels))(*[a.ctypes.data for a in levels])
+        pitches = (ctypes.c_size_t * len(levels))(*[a.strides[0] for a in levels])
+        check(self._lib.orbx_extractor_pyramid_host(self._h, outs, pitches, len(levels)), "pyramid")
         return levels
 
     # -- batched device API -------------------------------------------------

@@ -32,6 +32,10 @@
 //        Frame's stereo constructor: both images extracted on two threads
 //        started per frame (Frame.cc:79-82), then ComputeStereoMatches through
 //        OrbxFrame (Frame_orbx.cc): prints "pair_ms <median>".
+//   adapter_test time_bow case.bin reps
+//        OrbxMatcher::SearchByBoWTable (the SearchByBoW / SearchForTriangulation
+//        forwarder, ORBmatcher_orbx.cc) on one problem from bench.py's
+//        write_bow_case(): prints "bow_ms <median>" and "matches <n>".
 //   adapter_test time_rgbd W H img.raw depth.raw mbf reps
 //        Frame's RGB-D constructor: extraction, then ComputeStereoFromRGBD
 //        (Frame.cc:679-701) through OrbxFrame: prints "rgbd_frame_ms <median>"
@@ -122,6 +126,36 @@ int main(int argc, char **argv) {
         for (int i = 0; i < 5; ++i) pair();
         std::printf("pair_ms %.4f\n", median_ms(reps, pair));
         std::printf("keypoints %zu %zu kept %d\n", kl.size(), kr.size(), kept);
+        return 0;
+    }
+    if (argc == 4 && std::string(argv[1]) == "time_bow") {
+        std::ifstream f(argv[2], std::ios::binary);
+        auto rd = [&](void *p, size_t n) { f.read(reinterpret_cast<char *>(p), (std::streamsize)n); };
+        int32_t hd[5];   // variant, nlevels, checkOri, ntri, (pad)
+        float nnratio;
+        rd(hd, sizeof(hd));
+        rd(&nnratio, 4);
+        std::vector<float> tri(hd[3]);
+        rd(tri.data(), 4 * tri.size());
+        struct Side { std::vector<orbx_keypoint> k; std::vector<uint8_t> d, fl; std::vector<uint32_t> ids;
+                      std::vector<int32_t> off, feat; orbx_bow_side s; } S[2];
+        for (Side &x : S) {
+            int32_t n, nn, nf;
+            rd(&n, 4); rd(&nn, 4); rd(&nf, 4);
+            x.k.resize(n); x.d.resize(32 * (size_t)n); x.fl.resize(n); x.ids.resize(nn); x.off.resize(nn + 1);
+            x.feat.resize(std::max(nf, 1));
+            rd(x.k.data(), sizeof(orbx_keypoint) * n); rd(x.d.data(), x.d.size()); rd(x.fl.data(), n);
+            rd(x.ids.data(), 4 * (size_t)nn); rd(x.off.data(), 4 * (size_t)(nn + 1)); rd(x.feat.data(), 4 * (size_t)nf);
+            x.s = orbx_bow_side{x.k.data(), x.d.data(), x.fl.data(), n, x.ids.data(), x.off.data(), x.feat.data(), nn};
+        }
+        if (!f) { std::fprintf(stderr, "short case file\n"); return 2; }
+        const int reps = std::atoi(argv[3]);
+        std::vector<int> ma, mb;
+        int nm = 0;
+        auto call = [&] { nm = OrbxMatcher::SearchByBoWTable(hd[0], S[0].s, S[1].s, nnratio, hd[2] != 0, tri, hd[1], ma, mb); };
+        for (int i = 0; i < 5; ++i) call();
+        std::printf("bow_ms %.4f\n", median_ms(reps, call));
+        std::printf("matches %d\n", nm);
         return 0;
     }
     if (argc == 8 && std::string(argv[1]) == "time_rgbd") {

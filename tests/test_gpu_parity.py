@@ -222,6 +222,22 @@ def test_matcher_ties_and_contention(seed, pool, window, oracle_mod):
         assert nm_g == nm_o and np.array_equal(m_g, m_o) and np.array_equal(prev, prev_o)
 
 
+@pytest.mark.parametrize("w,h,seed", [(640, 480, 31), (1241, 376, 32), (333, 250, 33)])
+def test_mvimagepyramid_one_call(w, h, seed, extractors, oracle_mod):
+    """ORBextractor.mvImagePyramid (every level in one
+    orbx_extractor_pyramid_host call) after a host extraction, vs the oracle's
+    pyramid and vs the per-level download; odd widths exercise the pitches."""
+    ex = extractors(1000)
+    img = synth.frame(w, h, seed)
+    ex(img)
+    pyr = ex.mvImagePyramid
+    ref = oracle_mod.pyramid(np.ascontiguousarray(img))
+    assert len(pyr) == ex.nlevels
+    for l, lvl in enumerate(pyr):
+        assert lvl.shape == ref[l].shape and np.array_equal(lvl, ref[l]), (l, _first_diff(lvl, ref[l]))
+        assert np.array_equal(lvl, ex.debug_fetch(0, l, 0))
+
+
 def test_cpp_dropin_adapter_end_to_end(tmp_path, oracle_mod):
     """The C++ ORB_SLAM2:: adapter (include/orbx_orbslam2.hpp) driven through
     the reference-shaped calls: keypoints, descriptors, SearchForInitialization

@@ -2,7 +2,8 @@
 # Same-box A/B of library builds on one bench extra, optionally at another
 # stream count: alternates the libraries ROUNDS times, one line each into
 # gpurun_out/ab_TAG.txt (value and per-step stage ms).
-#   tools/ab_extra.sh TAG ROUNDS KEY[:STREAMS] lib1.so lib2.so ...
+#   tools/ab_extra.sh TAG ROUNDS KEY[:STREAMS] lib1.so lib2.so@ENV=V ...
+# (lib@K=V runs that library with the environment setting K=V)
 set -uo pipefail
 TAG=$1; ROUNDS=$2; SPEC=$3; shift 3
 KEY=${SPEC%%:*}; N=${SPEC#*:}; [ "$N" = "$SPEC" ] && N=0
@@ -20,9 +21,10 @@ sys.argv = ["bench.py", "--extra", key, "--steps", "20"]
 sys.exit(bench.main())
 '
 for r in $(seq "$ROUNDS"); do
-    for lib in "$@"; do
-        line=$(ORBX_LIB=$PWD/$lib timeout -k 10 150 python -c "$CODE" "$KEY" "$N" 2>/dev/null | grep "^{" | tail -n 1) || exit 1
-        python -c "import json,sys; d=json.loads(sys.argv[2]); print(sys.argv[1], round(d['value']), [round(v, 3) for v in d.get('stage_ms', [])])" "$lib" "$line" >> "$OUT"
+    for spec in "$@"; do
+        lib=${spec%%@*}; envs=""; [ "$lib" != "$spec" ] && envs=${spec#*@}
+        line=$(env $envs ORBX_LIB=$PWD/$lib timeout -k 10 150 python -c "$CODE" "$KEY" "$N" 2>/dev/null | grep "^{" | tail -n 1) || exit 1
+        python -c "import json,sys; d=json.loads(sys.argv[2]); print(sys.argv[1], round(d['value']), [round(v, 3) for v in d.get('stage_ms', [])])" "$spec" "$line" >> "$OUT"
     done
 done
 cat "$OUT"
