@@ -180,7 +180,7 @@ __global__ __launch_bounds__(kBT) void k_bow_match(const BowBufs *pa) {
 }
 
 // ComputeThreeMaxima + removal of the matches outside the three main bins.
-__global__ __launch_bounds__(1024) void k_bow_finish(const BowBufs *pa) {   // one block per problem
+__global__ __launch_bounds__(1024) void k_bow_finish(const BowBufs *pa, HostTail tail) {   // one block per problem
     __shared__ int top[3];
     const BowBufs a = pa[blockIdx.x];
     __shared__ int removed;
@@ -214,17 +214,19 @@ __global__ __launch_bounds__(1024) void k_bow_finish(const BowBufs *pa) {   // o
     }
     __syncthreads();
     if (tid == 0) a.counts[1] = a.counts[0] - removed;
+    host_tail(tail);
 }
 
 }  // namespace
 
-hipError_t launch_bow(const BowBufs *h, const BowBufs *d, int np, hipStream_t st) {
+hipError_t launch_bow(const BowBufs *h, const BowBufs *d, int np, const HostTail &tail, hipStream_t st) {
     if (np <= 0) return hipSuccess;
+    if (tail.flag && tail.blocks != np) return hipErrorInvalidValue;
     int nodes = 0;
     for (int k = 0; k < np; ++k) nodes = std::max(nodes, h[k].A.nnodes);
     if (nodes > 0)
         hipLaunchKernelGGL(k_bow_match, dim3((nodes + kBT / 64 - 1) / (kBT / 64), np), dim3(kBT), 0, st, d);
-    hipLaunchKernelGGL(k_bow_finish, dim3(np), dim3(1024), 0, st, d);
+    hipLaunchKernelGGL(k_bow_finish, dim3(np), dim3(1024), 0, st, d, tail);
     return hipGetLastError();
 }
 

@@ -72,6 +72,34 @@ struct FrameBufs {
 };
 
 // Matcher inputs/outputs for a batch of frame pairs (F1[b] -> F2[b]).
+// The copy of a synchronous call's outputs into the pinned arena, done by the
+// last workgroup of the call's last kernel instead of a kernel of its own
+// (orbx_ws.h ws_tail): flag == nullptr means no tail.
+struct HostTail {
+    const uint4 *src; uint4 *dst; int n16;
+    uint32_t *flag;   // pinned, raised after the copy (system scope)
+    uint32_t *done;   // device counter of finished workgroups, zero before the kernel
+    int blocks;       // workgroups of the kernel
+};
+
+#ifdef __HIPCC__
+// Every thread of every workgroup of the kernel calls this last.
+__device__ inline void host_tail(const HostTail &t) {
+    if (!t.flag) return;
+    __shared__ int s_last;
+    __threadfence();   // this workgroup's results before its count
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(t.done, 1u) == (uint32_t)(t.blocks - 1);
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();   // (acquire: the other workgroups' results)
+    for (int i = threadIdx.x; i < t.n16; i += blockDim.x) t.dst[i] = t.src[i];
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(t.flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+#endif
+
 struct MatchBufs {
     const orbx_keypoint *k1; const uint8_t *d1; const int32_t *n1; int64_t k1_stride;
     const orbx_keypoint *k2; const uint8_t *d2; const int32_t *n2; int64_t k2_stride;
@@ -84,6 +112,7 @@ struct MatchBufs {
     int check_ori;
     int reset_prev;           // 1: prev_xy := F1 keypoint positions before matching
     long long *clocks;        // debug: phase timestamps of pair 0 (nullptr = off)
+    HostTail tail;            // the synchronous host call's output copy (flag nullptr: none)
 };
 
 // Where a frame's pyramid lives: level 0 is the caller's image, levels >= 1
@@ -171,15 +200,15 @@ hipError_t launch_stereo(const StereoBufs &a, int pairs, int nl_cap, hipStream_t
 int stereo_lds_bytes(int rows, int nr_cap);
 int64_t stereo_band_stride(int rows, int nr_cap);   // per-pair band scratch (StereoBufs::bands)
 hipError_t launch_rgbd_samples(const float *dsample, const orbx_keypoint *kun, int n, float mbf, float *ur, float *depth,
-                               int32_t *nkept, hipStream_t st);
+                               int32_t *nkept, const HostTail &tail, hipStream_t st);
 hipError_t launch_rgbd(const orbx_keypoint *kps, const orbx_keypoint *kun, const int32_t *nkps, int64_t kstride,
                        int kcap, const float *dmap, int64_t dstride, int dpitch, int w, int h, float mbf, float *ur,
                        float *depth, int64_t ostride, int32_t *nkept, int B, hipStream_t s);
 // A batch of independent problems: h on the host, d the same array on the device.
-hipError_t launch_proj(const ProjBufs *h, const ProjBufs *d, int np, hipStream_t s);
+hipError_t launch_proj(const ProjBufs *h, const ProjBufs *d, int np, const HostTail &tail, hipStream_t s);
 int proj_blocks(int nq);
 bool proj_fits(int n);   // the frame's grid fits the search kernel's LDS
-hipError_t launch_bow(const BowBufs *h, const BowBufs *d, int np, hipStream_t s);
+hipError_t launch_bow(const BowBufs *h, const BowBufs *d, int np, const HostTail &tail, hipStream_t s);
 
 // DBoW2 vocabulary in slot order: the children of a node occupy consecutive
 // slots (root = slot 0).  16 B per slot + 32-B descriptor + weight.

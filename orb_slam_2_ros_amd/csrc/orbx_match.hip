@@ -524,6 +524,7 @@ __global__ __launch_bounds__(kMT) void k_search_init(MatchBufs mb, int maxq, int
     block_scan_i32(local, &total, ws);
     if (tid == 0) mb.nmatches[b] = sh_err ? -1 : total;
     if (clk) mb.clocks[5] = clock64();
+    host_tail(mb.tail);
 }
 
 }  // namespace
@@ -545,6 +546,7 @@ hipError_t launch_match(const MatchBufs &mb, int B, int n1cap, int n2cap, int ma
         hipFuncSetAttribute(reinterpret_cast<const void *>(k_search_init),
                             hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess)
         return hipErrorInvalidValue;
+    if (mb.tail.flag && mb.tail.blocks != B) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_search_init, dim3(B), dim3(kMT), bytes, st, mb, maxq, maxc);
     return hipGetLastError();
 }

@@ -419,7 +419,7 @@ __device__ inline bool accept(const ProjBufs &a, bool ratio, int q, const uint32
 // rounds stop when none progresses; what is left (contention chains through
 // `hard` claims) is replayed by wave 0 in query order.
 template <bool QL>   // per-query data in LDS (else global; one instantiation each keeps ds_* loads ds_*)
-__global__ __launch_bounds__(kPT) void k_proj_replay(const ProjBufs *pa) {   // one block per problem
+__global__ __launch_bounds__(kPT) void k_proj_replay(const ProjBufs *pa, HostTail tail) {   // one block per problem
     extern __shared__ __align__(16) uint8_t lds[];
     const ProjBufs a = pa[blockIdx.x];
     const uint64_t c0 = wall_clock64();
@@ -679,6 +679,7 @@ __global__ __launch_bounds__(kPT) void k_proj_replay(const ProjBufs *pa) {   // 
     } else if (tid == 0) {
         *a.nmatches = sh_acc - sh_removed;
     }
+    host_tail(tail);
 }
 
 }  // namespace
@@ -699,8 +700,9 @@ bool proj_fits(int n) { return n <= kKPer * kPT && proj_lds_bytes(n) <= kProjLds
 int proj_blocks(int nq) { return std::max(1, std::min(512, (nq + kPW - 1) / kPW)); }
 
 // h: the problems' buffers on the host, d: the same array in device memory.
-hipError_t launch_proj(const ProjBufs *h, const ProjBufs *d, int np, hipStream_t st) {
+hipError_t launch_proj(const ProjBufs *h, const ProjBufs *d, int np, const HostTail &tail, hipStream_t st) {
     if (np <= 0) return hipSuccess;
+    if (tail.flag && tail.blocks != np) return hipErrorInvalidValue;
     int bytes = 0, nblk = 1;
     bool q_in_lds = true;
     for (int k = 0; k < np; ++k) {
@@ -723,9 +725,9 @@ hipError_t launch_proj(const ProjBufs *h, const ProjBufs *d, int np, hipStream_t
     if (rbytes > 64 * 1024 && hipFuncSetAttribute(rk, hipFuncAttributeMaxDynamicSharedMemorySize, rbytes) != hipSuccess)
         return hipErrorInvalidValue;
     if (q_in_lds)
-        hipLaunchKernelGGL(k_proj_replay<true>, dim3(np), dim3(kPT), rbytes, st, d);
+        hipLaunchKernelGGL(k_proj_replay<true>, dim3(np), dim3(kPT), rbytes, st, d, tail);
     else
-        hipLaunchKernelGGL(k_proj_replay<false>, dim3(np), dim3(kPT), rbytes, st, d);
+        hipLaunchKernelGGL(k_proj_replay<false>, dim3(np), dim3(kPT), rbytes, st, d, tail);
     return hipGetLastError();
 }
 

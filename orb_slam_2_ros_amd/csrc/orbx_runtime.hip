@@ -721,23 +721,27 @@ __global__ __launch_bounds__(kToHostThreads) void k_to_host(const uint4 *src, ui
 }
 }  // namespace
 
-int ws_finish(CallWs &ws, size_t off, size_t bytes) {
+namespace {
+bool ws_direct(const CallWs &ws, size_t off, size_t bytes) {
     const size_t n16 = (bytes + 15) / 16;
-    if (bytes == 0) return hipStreamSynchronize(ws.st) == hipSuccess ? ORBX_OK : ORBX_EIO;
-    const bool direct = ws.host_d && ws.flag_d && (off & 15) == 0 && n16 * 16 + off <= ws.cap && bytes <= (256u << 10);
-    if (!direct) {
-        if (hipMemcpyAsync(ws.host + off, ws.dev + off, bytes, hipMemcpyDeviceToHost, ws.st) != hipSuccess ||
-            hipStreamSynchronize(ws.st) != hipSuccess)
-            return ORBX_EIO;
-        return ORBX_OK;
-    }
-    volatile uint32_t *flag = ws.flag;
-    *flag = 0;
+    return bytes && ws.host_d && ws.flag_d && (off & 15) == 0 && n16 * 16 + off <= ws.cap && bytes <= (256u << 10);
+}
+
+int ws_copy_sync(CallWs &ws, size_t off, size_t bytes) {
+    if (bytes && hipMemcpyAsync(ws.host + off, ws.dev + off, bytes, hipMemcpyDeviceToHost, ws.st) != hipSuccess)
+        return ORBX_EIO;
+    return hipStreamSynchronize(ws.st) == hipSuccess ? ORBX_OK : ORBX_EIO;
+}
+
+void ws_arm(CallWs &ws) {
+    *reinterpret_cast<volatile uint32_t *>(ws.flag) = 0;
     std::atomic_thread_fence(std::memory_order_seq_cst);
-    hipLaunchKernelGGL(k_to_host, dim3(1), dim3(kToHostThreads), 0, ws.st, reinterpret_cast<const uint4 *>(ws.dev + off),
-                       reinterpret_cast<uint4 *>(ws.host_d + off), (int)n16, ws.flag_d);
-    if (hipGetLastError() != hipSuccess) return ORBX_EIO;
-    for (uint32_t i = 1; !*flag; ++i) {   // the stream's state ends the wait on an error
+}
+
+// Polls the pinned flag; the stream's state ends the wait on an error.
+int ws_poll(CallWs &ws) {
+    volatile uint32_t *flag = ws.flag;
+    for (uint32_t i = 1; !*flag; ++i) {
         if ((i & 255) == 0 && hipStreamQuery(ws.st) != hipErrorNotReady) break;
         __builtin_ia32_pause();
     }
@@ -748,6 +752,32 @@ int ws_finish(CallWs &ws, size_t off, size_t bytes) {
     }
     std::atomic_thread_fence(std::memory_order_acquire);
     return ORBX_OK;
+}
+}  // namespace
+
+int ws_finish(CallWs &ws, size_t off, size_t bytes) {
+    if (!ws_direct(ws, off, bytes)) return ws_copy_sync(ws, off, bytes);
+    ws_arm(ws);
+    hipLaunchKernelGGL(k_to_host, dim3(1), dim3(kToHostThreads), 0, ws.st, reinterpret_cast<const uint4 *>(ws.dev + off),
+                       reinterpret_cast<uint4 *>(ws.host_d + off), (int)((bytes + 15) / 16), ws.flag_d);
+    if (hipGetLastError() != hipSuccess) return ORBX_EIO;
+    return ws_poll(ws);
+}
+
+void ws_tail(CallWs &ws, size_t off, size_t bytes, uint32_t *done_d, int blocks, HostTail &t) {
+    t = HostTail{};
+    if (!ws_direct(ws, off, bytes) || !done_d || blocks <= 0) return;
+    ws_arm(ws);
+    t.src = reinterpret_cast<const uint4 *>(ws.dev + off);
+    t.dst = reinterpret_cast<uint4 *>(ws.host_d + off);
+    t.n16 = (int)((bytes + 15) / 16);
+    t.flag = ws.flag_d;
+    t.done = done_d;
+    t.blocks = blocks;
+}
+
+int ws_wait(CallWs &ws, const HostTail &t, size_t off, size_t bytes) {
+    return t.flag ? ws_poll(ws) : ws_copy_sync(ws, off, bytes);
 }
 
 }  // namespace orbx
@@ -1247,7 +1277,7 @@ int orbx_mono_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t f
         note_results(ex, st);
         return ORBX_OK;
     }
-    MatchBufs mb;
+    MatchBufs mb{};
     const auto &s1 = ex->slot[prev];
     const auto &s2 = ex->slot[next];
     mb.k1 = s1.kps; mb.d1 = s1.desc; mb.n1 = s1.nkps; mb.k1_stride = ex->plan.max_kps;
@@ -1543,7 +1573,7 @@ int orbx_stereo_from_rgbd(int device, const orbx_keypoint *kps, const orbx_keypo
     // out-of-image keypoint, undefined in the reference, gets 0: no depth)
     Layout L;
     const size_t o_k = L.add(sizeof(orbx_keypoint) * (size_t)n), o_s = L.add(4 * (size_t)n);
-    const size_t o_nk = L.add(4), in_end = L.size;
+    const size_t o_nk = L.add(16), in_end = L.size;   // nkept, then the HostTail counter
     const size_t o_ur = L.add(4 * (size_t)n), o_d = L.add(4 * (size_t)n), out_end = L.size;
     CallWs &ws = call_ws(device);
     std::lock_guard<std::mutex> lock(ws.mu);
@@ -1556,14 +1586,17 @@ int orbx_stereo_from_rgbd(int device, const orbx_keypoint *kps, const orbx_keypo
         const int v = (int)kps[i].y, u = (int)kps[i].x;
         samp[i] = (v >= 0 && v < height && u >= 0 && u < width) ? depth_map[(size_t)v * pf + u] : 0.0f;
     }
-    std::memset(ws.host + o_nk, 0, 4);
+    std::memset(ws.host + o_nk, 0, 16);
     uint8_t *D = ws.dev;
+    // (the count sits just before the outputs: one contiguous run back, by
+    // the kernel's last workgroup)
+    HostTail tail;
+    ws_tail(ws, o_nk, out_end - o_nk, at<uint32_t>(D, o_nk + 4), (n + 255) / 256, tail);
     if (hipMemcpyAsync(D, ws.host, in_end, hipMemcpyHostToDevice, ws.st) != hipSuccess ||
         launch_rgbd_samples(at<float>(D, o_s), at<orbx_keypoint>(D, o_k), n, mbf, at<float>(D, o_ur),
-                            at<float>(D, o_d), at<int32_t>(D, o_nk), ws.st) != hipSuccess)
+                            at<float>(D, o_d), at<int32_t>(D, o_nk), tail, ws.st) != hipSuccess)
         return ORBX_EIO;
-    // (the count sits just before the outputs: one contiguous run back)
-    if (ws_finish(ws, o_nk, out_end - o_nk)) return ORBX_EIO;
+    if (ws_wait(ws, tail, o_nk, out_end - o_nk)) return ORBX_EIO;
     get(ws, o_ur, uright, 4 * (size_t)n);
     get(ws, o_d, depth, 4 * (size_t)n);
     get(ws, o_nk, nkept, 4);
@@ -1613,8 +1646,8 @@ int orbx_search_for_initialization_bounds(int device, const orbx_keypoint *k1, c
     const size_t o_k1 = L.add(sizeof(orbx_keypoint) * n1c), o_d1 = L.add(32 * (size_t)n1c),
                  o_k2 = L.add(sizeof(orbx_keypoint) * n2c), o_d2 = L.add(32 * (size_t)n2c), o_ns = L.add(8);
     const size_t o_prev = L.add(8 * (size_t)n1c);   // in / out
-    const size_t in_bytes = L.size;
-    const size_t o_m = L.add(4 * (size_t)n1c), o_nm = L.add(4);
+    // outputs (uploaded with the inputs: the HostTail counter goes up as 0)
+    const size_t o_m = L.add(4 * (size_t)n1c), o_nm = L.add(16);   // nmatches, then the HostTail counter
     const size_t out_end = L.size;
     CallWs &ws = call_ws(device);
     std::lock_guard<std::mutex> lock(ws.mu);
@@ -1627,17 +1660,19 @@ int orbx_search_for_initialization_bounds(int device, const orbx_keypoint *k1, c
     put(ws, o_d2, d2, 32 * (size_t)n2);
     put(ws, o_ns, ns, sizeof(ns));
     put(ws, o_prev, prev_xy, 8 * (size_t)n1);
+    std::memset(ws.host + o_nm + 4, 0, 4);
     uint8_t *D = ws.dev;
-    if (hipMemcpyAsync(D, ws.host, in_bytes, hipMemcpyHostToDevice, ws.st) != hipSuccess) return ORBX_EIO;
-    MatchBufs mb;
+    if (hipMemcpyAsync(D, ws.host, out_end, hipMemcpyHostToDevice, ws.st) != hipSuccess) return ORBX_EIO;
+    MatchBufs mb{};
     mb.k1 = at<orbx_keypoint>(D, o_k1); mb.d1 = D + o_d1; mb.n1 = at<int32_t>(D, o_ns); mb.k1_stride = n1c;
     mb.k2 = at<orbx_keypoint>(D, o_k2); mb.d2 = D + o_d2; mb.n2 = at<int32_t>(D, o_ns) + 1; mb.k2_stride = n2c;
     mb.prev_xy = at<float>(D, o_prev); mb.matches12 = at<int32_t>(D, o_m); mb.nmatches = at<int32_t>(D, o_nm);
     mb.min_x = min_x; mb.max_x = max_x; mb.min_y = min_y; mb.max_y = max_y;
     mb.window = window; mb.nnratio = nnratio;
     mb.check_ori = check_ori; mb.reset_prev = 0; mb.clocks = nullptr;
+    ws_tail(ws, o_prev, out_end - o_prev, at<uint32_t>(D, o_nm + 4), 1, mb.tail);
     if (launch_match(mb, 1, n1c, n2c, q, c, ws.st) != hipSuccess) return ORBX_EIO;
-    if (ws_finish(ws, o_prev, out_end - o_prev)) return ORBX_EIO;
+    if (ws_wait(ws, mb.tail, o_prev, out_end - o_prev)) return ORBX_EIO;
     int32_t nm = 0;
     get(ws, o_nm, &nm, 4);
     if (nm < 0) return ORBX_EIO;
@@ -1725,7 +1760,8 @@ int proj_run(int device, int variant, orbx_proj_problem *P, int np, int th_dist,
             o[t].qd = L.add(32 * (size_t)pr.nq);
         }
         const size_t o_pa = L.add(sizeof(ProjBufs) * nl);
-        const size_t o_cnt = L.add(8 + 8 * (size_t)nl);   // pool_top, then hard_cnt per problem: zeros from the host
+        // pool_top, then hard_cnt per problem, then the HostTail counter: zeros from the host
+        const size_t o_cnt = L.add(16 + 8 * (size_t)nl);
         const size_t in_bytes = L.size;
         for (int t = 0; t < nl; ++t) {
             const int n = P[live[t]].frame.n, nq = P[live[t]].nq;
@@ -1775,10 +1811,12 @@ int proj_run(int device, int variant, orbx_proj_problem *P, int np, int th_dist,
             a.nblk = proj_blocks(nq);
         }
         put(ws, o_pa, hb.data(), sizeof(ProjBufs) * nl);
-        std::memset(ws.host + o_cnt, 0, 8 + 8 * (size_t)nl);
+        std::memset(ws.host + o_cnt, 0, 16 + 8 * (size_t)nl);
         if (hipMemcpyAsync(D, ws.host, in_bytes, hipMemcpyHostToDevice, ws.st) != hipSuccess) return ORBX_EIO;
-        if (launch_proj(hb.data(), at<ProjBufs>(D, o_pa), nl, ws.st) != hipSuccess) return ORBX_EIO;
-        if (ws_finish(ws, o_cnt, out_end - o_cnt)) return ORBX_EIO;
+        HostTail tail;
+        ws_tail(ws, o_cnt, out_end - o_cnt, at<uint32_t>(D, o_cnt + 8 + 8 * (size_t)nl), nl, tail);
+        if (launch_proj(hb.data(), at<ProjBufs>(D, o_pa), nl, tail, ws.st) != hipSuccess) return ORBX_EIO;
+        if (ws_wait(ws, tail, o_cnt, out_end - o_cnt)) return ORBX_EIO;
         unsigned long long used = 0;
         get(ws, o_cnt, &used, 8);
         if (dbg_stats) {
@@ -1894,6 +1932,7 @@ int bow_run(int device, int variant, orbx_bow_problem *P, int np, float nnratio,
     }
     const size_t in_bytes = L.size;
     for (int t = 0; t < nl; ++t) o[t].cnt = L.add(4 * 34);   // hist[32] + counts[2]
+    const size_t o_done = L.add(16);   // k_bow_finish's workgroup counter (HostTail)
     const size_t cnt_end = L.size;
     for (int t = 0; t < nl; ++t) o[t].bin = L.add((size_t)P[live[t]].a.n);
     CallWs &ws = call_ws(device);
@@ -1935,8 +1974,10 @@ int bow_run(int device, int variant, orbx_bow_problem *P, int np, float nnratio,
     std::memset(ws.host + in_bytes, 0, cnt_end - in_bytes);   // the counters go up as zeros with the inputs
     if (hipMemcpyAsync(D, ws.host, cnt_end, hipMemcpyHostToDevice, ws.st) != hipSuccess) return ORBX_EIO;
     const size_t o_out = o[0].ma;   // match arrays and counters are one contiguous run
-    if (launch_bow(hb.data(), at<BowBufs>(D, o_pa), nl, ws.st) != hipSuccess) return ORBX_EIO;
-    if (ws_finish(ws, o_out, cnt_end - o_out)) return ORBX_EIO;
+    HostTail tail;
+    ws_tail(ws, o_out, cnt_end - o_out, at<uint32_t>(D, o_done), nl, tail);
+    if (launch_bow(hb.data(), at<BowBufs>(D, o_pa), nl, tail, ws.st) != hipSuccess) return ORBX_EIO;
+    if (ws_wait(ws, tail, o_out, cnt_end - o_out)) return ORBX_EIO;
     for (int t = 0; t < nl; ++t) {
         orbx_bow_problem &pr = P[live[t]];
         get(ws, o[t].ma, pr.match_a, 4 * (size_t)pr.a.n);

@@ -581,7 +581,7 @@ __global__ __launch_bounds__(kST) void k_rgbd_depth(const orbx_keypoint *kps, co
 // gathered by the host so the map itself never crosses PCIe: 4 B per keypoint
 // instead of the whole CV_32F image), then the same arithmetic as k_rgbd_depth.
 __global__ __launch_bounds__(kST) void k_rgbd_samples(const float *dsample, const orbx_keypoint *kun, int n, float mbf,
-                                                      float *ur, float *depth, int32_t *nkept) {
+                                                      float *ur, float *depth, int32_t *nkept, HostTail tail) {
     const int i = blockIdx.x * kST + threadIdx.x;
     bool got = false;
     if (i < n) {
@@ -597,6 +597,7 @@ __global__ __launch_bounds__(kST) void k_rgbd_samples(const float *dsample, cons
     }
     const uint64_t m = __ballot(got);
     if ((threadIdx.x & 63) == 0 && m) atomicAdd(nkept, __popcll(m));
+    host_tail(tail);
 }
 
 }  // namespace
@@ -637,10 +638,11 @@ hipError_t launch_stereo(const StereoBufs &a, int pairs, int nl_cap, hipStream_t
 }
 
 hipError_t launch_rgbd_samples(const float *dsample, const orbx_keypoint *kun, int n, float mbf, float *ur, float *depth,
-                               int32_t *nkept, hipStream_t st) {
+                               int32_t *nkept, const HostTail &tail, hipStream_t st) {
     if (n <= 0) return hipSuccess;
+    if (tail.flag && tail.blocks != (n + kST - 1) / kST) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_rgbd_samples, dim3((n + kST - 1) / kST), dim3(kST), 0, st, dsample, kun, n, mbf, ur, depth,
-                       nkept);
+                       nkept, tail);
     return hipGetLastError();
 }
 

@@ -10,6 +10,7 @@
 #include <mutex>
 
 #include "../../include/orbx.h"
+#include "orbx_device.h"
 
 namespace orbx {
 
@@ -76,6 +77,12 @@ inline int ws_reserve(CallWs &ws, size_t bytes) {
 // (about 10 us of wake-up for a call of ~50 us).  Large outputs take the copy.
 // Caller holds ws.mu.
 int ws_finish(CallWs &ws, size_t off, size_t bytes);
+// The same copy done by the last workgroup of the call's last kernel
+// (HostTail, orbx_device.h): ws_tail prepares it before that launch (done_d: a
+// device counter the inputs upload as zero; blocks: the kernel's workgroups;
+// t.flag stays nullptr when the output takes the copy), ws_wait waits after.
+void ws_tail(CallWs &ws, size_t off, size_t bytes, uint32_t *done_d, int blocks, HostTail &t);
+int ws_wait(CallWs &ws, const HostTail &t, size_t off, size_t bytes);
 
 template <typename T>
 inline T *at(uint8_t *base, size_t off) { return reinterpret_cast<T *>(base + off); }
