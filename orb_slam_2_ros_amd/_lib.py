@@ -193,7 +193,8 @@ def check(code: int, what: str) -> int:
     return code
 
 
-def ptr(a: np.ndarray | None) -> ctypes.c_void_p | None:
+def ptr(a: np.ndarray | None) -> int | None:
+    """The array's data address (an int: ctypes passes it as void*)."""
     if a is None:
         return None
-    return ctypes.c_void_p(a.ctypes.data)
+    return a.__array_interface__["data"][0]

@@ -46,6 +46,7 @@ struct DevPlan {
     int out_cap, max_kps;
     int node_cap;             // quadtree node capacity (max over levels)
     int node_lds_bytes;       // dynamic LDS of the quadtree kernel
+    int node_lds_bytes_w;     // ... of its 1024-thread form (launches of few frames; > 160 KB: not used)
     int dbg_stop;             // diagnostics only (ORBX_DBG_STOP): end k_quadtree after phase n (0 = off)
     const int4 *pyr_rgn;      // Plan::rgn (k_pyramid_rgn)
     int pyr_rgn_half;
@@ -226,7 +227,8 @@ hipError_t launch_vocab_transform(const VocabDev &v, const uint8_t *feat, int n,
                                   double *o_weight, uint32_t *o_node, hipStream_t s);
 int match_lds_bytes(int n1cap, int n2cap, int maxq, int maxc);
 int quadtree_lds_bytes(int node_cap);
-constexpr int kQuadRegKeys = 8 * 256;   // keys k_quadtree can keep in registers (6 or 8 per thread)
+constexpr int kQuadRegKeys = 8 * 256;     // keys k_quadtree can keep in registers (6 or 8 per thread)
+constexpr int kQuadRegKeysW = 10 * 1024;  // the same for its 1024-thread form (4 or 10 per thread)
 bool resize_window_fits(const Plan &hp);
 bool plan_resize_waves(Plan &hp);   // fills hp.rw, or leaves it empty (block kernel)
 bool plan_pyr_regions(Plan &hp);   // fills hp.rgn, or leaves rgn_n = 0

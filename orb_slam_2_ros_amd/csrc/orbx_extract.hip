@@ -184,11 +184,12 @@ __device__ inline uint32_t pack_key(int x, int y, int score) {
 }
 
 // ---- wave / block helpers (wave64) ----------------------------------------
-// Exclusive scan of a[0..m) (uint64) in LDS by the whole 256-thread block.
-// ws: 4 uint64 of LDS scratch.  Returns the total.  Ends with a barrier.
+// Exclusive scan of a[0..m) (uint64) in LDS by the whole NT-thread block.
+// ws: NT / 64 uint64 of LDS scratch.  Returns the total.  Ends with a barrier.
+template <int NT = kThreads>
 __device__ uint64_t block_excl_scan_u64(uint64_t *a, int m, uint64_t *ws) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int per = (m + kThreads - 1) / kThreads;
+    const int per = (m + NT - 1) / NT;
     const int s = min(tid * per, m), e = min(s + per, m);
     uint64_t local = 0;
     for (int i = s; i < e; ++i) local += a[i];
@@ -196,7 +197,7 @@ __device__ uint64_t block_excl_scan_u64(uint64_t *a, int m, uint64_t *ws) {
     if (lane == 63) ws[wave] = incl;
     __syncthreads();
     uint64_t base = 0, total = 0;
-    for (int w = 0; w < kThreads / 64; ++w) {
+    for (int w = 0; w < NT / 64; ++w) {
         if (w < wave) base += ws[w];
         total += ws[w];
     }
@@ -1062,13 +1063,19 @@ struct QLds {
 // rounds then touch no global memory); R == 0: they stay in global scratch.
 // 6 keys per thread cover the bench levels (VGA level 0: ~1300 keys) in 72
 // VGPRs (7 waves per SIMD); levels up to kQuadRegKeys take 8 (with spills)
-constexpr int kQRegKeys = 6, kQRegKeysWide = kQuadRegKeys / kThreads;
+// Per workgroup size NT: register keys per thread on the narrow (R1) and wide
+// (R2) paths, the key -> source map's capacity (KR) and workgroups per CU.
+// NT = 1024 serves launches too small to fill the chip (a few frames: the
+// drop-in call, a sharded camera set), where a level's latency is the step's.
+template <int NT> struct QCfg;
+template <> struct QCfg<256> { static constexpr int R1 = 6, R2 = kQuadRegKeys / 256, KR = kQuadRegKeys, MINB = 7; };
+template <> struct QCfg<1024> { static constexpr int R1 = 4, R2 = kQuadRegKeysW / 1024, KR = kQuadRegKeysW, MINB = 1; };
 // R == 0 (keys in global scratch): a pass walks the keys kQU per thread at a
 // time, the chunk's loads issued together into a register cache (key k =
-// k0 + u kThreads + tid: every pass maps a key to the same thread, so its node
+// k0 + u NT + tid: every pass maps a key to the same thread, so its node
 // and quadrant need no cross-thread ordering), then the chunk's node and
-// quadrant written back.  A key pass is then ~n / (kQU kThreads) L2 round
-// trips instead of n / kThreads (FHD level 0: ~9.6 k keys, 5 instead of 38).
+// quadrant written back.  A key pass is then ~n / (kQU NT) L2 round
+// trips instead of n / NT (FHD level 0: ~9.6 k keys, 5 instead of 38).
 #ifndef ORBX_QT_QU
 #define ORBX_QT_QU 4
 #endif
@@ -1076,7 +1083,7 @@ constexpr int kQU = ORBX_QT_QU;
 #ifndef ORBX_QT_PF
 #define ORBX_QT_PF 1
 #endif
-template <int R>
+template <int R, int NT>
 struct QKeys {
     static constexpr int C = R > 0 ? R : kQU;   // registers: the keys, or the chunk cache
     uint32_t key[C];
@@ -1089,7 +1096,7 @@ struct QKeys {
     __device__ inline void load(int k0) {
 #pragma unroll
         for (int u = 0; u < C; ++u) {
-            const int k = k0 + u * kThreads + (int)threadIdx.x;
+            const int k = k0 + u * NT + (int)threadIdx.x;
             if (k < n) {
                 key[u] = gkeys[k];
                 // (a key's quadrant is 0..3; masked, as the scratch starts
@@ -1102,7 +1109,7 @@ struct QKeys {
     __device__ inline void fetch(int k0, uint32_t *pk, uint32_t *pq) const {
 #pragma unroll
         for (int u = 0; u < C; ++u) {
-            const int k = k0 + u * kThreads + (int)threadIdx.x;
+            const int k = k0 + u * NT + (int)threadIdx.x;
             if (k < n) {
                 pk[u] = gkeys[k];
                 pq[u] = (uint32_t)gnode[k] | ((uint32_t)(gq[k] & 3) << 16);
@@ -1117,15 +1124,15 @@ struct QKeys {
 #if ORBX_QT_PF
         uint32_t pk[C], pq[C];
         fetch(0, pk, pq);
-        for (int k0 = 0; k0 < n; k0 += kThreads * kQU) {
+        for (int k0 = 0; k0 < n; k0 += NT * kQU) {
 #pragma unroll
             for (int u = 0; u < C; ++u) { key[u] = pk[u]; nq[u] = pq[u]; }
-            if (k0 + kThreads * kQU < n) fetch(k0 + kThreads * kQU, pk, pq);
+            if (k0 + NT * kQU < n) fetch(k0 + NT * kQU, pk, pq);
             body(k0);
             store(k0);
         }
 #else
-        for (int k0 = 0; k0 < n; k0 += kThreads * kQU) {
+        for (int k0 = 0; k0 < n; k0 += NT * kQU) {
             load(k0);
             body(k0);
             store(k0);
@@ -1135,7 +1142,7 @@ struct QKeys {
     __device__ inline void store(int k0) {
 #pragma unroll
         for (int u = 0; u < C; ++u) {
-            const int k = k0 + u * kThreads + (int)threadIdx.x;
+            const int k = k0 + u * NT + (int)threadIdx.x;
             if (k < n) {
                 gnode[k] = (uint16_t)(nq[u] & 0xFFFF);
                 gq[k] = (uint8_t)(nq[u] >> 16);
@@ -1148,14 +1155,14 @@ struct QKeys {
         if constexpr (R > 0) {
 #pragma unroll
             for (int j = 0; j < R; ++j) {
-                const int k = (int)threadIdx.x + j * kThreads;
+                const int k = (int)threadIdx.x + j * NT;
                 if (k < n) f(j, k);
             }
         } else {
             chunks([&](int k0) {
 #pragma unroll
                 for (int u = 0; u < kQU; ++u) {
-                    const int k = k0 + u * kThreads + (int)threadIdx.x;
+                    const int k = k0 + u * NT + (int)threadIdx.x;
                     if (k < n) f(u, k);
                 }
             });
@@ -1167,14 +1174,14 @@ struct QKeys {
         if constexpr (R > 0) {
 #pragma unroll
             for (int j = 0; j < R; ++j) {
-                const int k = (int)threadIdx.x + j * kThreads;
+                const int k = (int)threadIdx.x + j * NT;
                 f(j, k, k < n);
             }
         } else {
             chunks([&](int k0) {
 #pragma unroll
                 for (int u = 0; u < kQU; ++u) {
-                    const int k = k0 + u * kThreads + (int)threadIdx.x;
+                    const int k = k0 + u * NT + (int)threadIdx.x;
                     f(u, k, k < n);
                 }
             });
@@ -1236,8 +1243,8 @@ __device__ inline void agg_atomics(uint32_t *cnt, uint32_t *best, uint32_t slot,
 // Child counts / best keys of the splittable nodes.  ccnt / cbest[0, 4S)
 // were zeroed by the step that produced the current nodes (zero_children),
 // ordered by that step's closing barrier.  Ends with a barrier.
-template <int R>
-__device__ __attribute__((always_inline)) void child_stats(const QLds &s, QKeys<R> &K) {
+template <int R, int NT>
+__device__ __attribute__((always_inline)) void child_stats(const QLds &s, QKeys<R, NT> &K) {
     // every lane runs each slot's aggregation (lanes past the key count carry
     // slot ~0u)
     K.each_all([&](int j, int k, bool valid) {
@@ -1258,15 +1265,16 @@ __device__ __attribute__((always_inline)) void child_stats(const QLds &s, QKeys<
     __syncthreads();
 }
 
+template <int NT>
 __device__ inline void zero_children(const QLds &s, int S) {
-    for (int i = threadIdx.x; i < 4 * S; i += kThreads) { s.ccnt[i] = 0; s.cbest[i] = 0; }
+    for (int i = threadIdx.x; i < 4 * S; i += NT) { s.ccnt[i] = 0; s.cbest[i] = 0; }
 }
 
 // One key pass per round: each key moves to its node of the round just built
 // (nidx_c[4 node + quadrant]) and, when that node is splittable, adds itself
 // to the node's child counts (as child_stats).  Ends with a barrier.
-template <int R>
-__device__ __attribute__((always_inline)) void advance_stats(const QLds &s, QKeys<R> &K) {
+template <int R, int NT>
+__device__ __attribute__((always_inline)) void advance_stats(const QLds &s, QKeys<R, NT> &K) {
     K.each_all([&](int j, int k, bool valid) {
         uint32_t slot = ~0u, bp = 0;
         if (valid) {
@@ -1303,14 +1311,14 @@ __device__ inline QNode make_child(const QLds &s, const QNode &parent, int i, in
 }
 
 // Phases 2-5 of k_quadtree on the gathered keys (ORBextractor.cc:566-784).
-template <int NR>
+template <int NR, int NT>
 __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p, const FrameBufs &fb, QLds &s, const LevelGeom &g, int b, int l,
-                                QKeys<NR> &K, uint64_t &phase_t_) {
+                                QKeys<NR, NT> &K, uint64_t &phase_t_) {
     const int tid = threadIdx.x;
     const int N = g.quota, NC = p.node_cap;
     const uint32_t *keys = K.gkeys;
     int32_t *level_count = fb.level_count + (int64_t)b * kMaxLevels + l;
-    __shared__ uint64_t ws64[4];
+    __shared__ uint64_t ws64[NT / 64];
     __shared__ int sh_S, sh_R, sh_nv;
 
     // ---- 2. root nodes (ORBextractor.cc:566-613)
@@ -1319,7 +1327,7 @@ __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p,
         // one root (every 4:3 or squarer level): every key's node is 0, its
         // count the key count and its best key a block maximum (wave maxima
         // through LDS: no per-key atomics, no serial pass)
-        __shared__ uint32_t ws_root[kThreads / 64];
+        __shared__ uint32_t ws_root[NT / 64];
         uint32_t bm = 0;
         K.each([&](int j, int k) {
             K.set_node(j, k, 0);
@@ -1327,7 +1335,7 @@ __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p,
         });
         bm = wave_max_u32(bm);
         if ((tid & 63) == 0) ws_root[tid >> 6] = bm;
-        zero_children(s, 1);
+        zero_children<NT>(s, 1);
         __syncthreads();
         if (tid == 0) {
             QNode nd;
@@ -1337,7 +1345,7 @@ __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p,
             nd.y1 = (int16_t)(g.h - 2 * kBorder);
             nd.count = (int32_t)K.n;
             uint32_t best = 0;
-            for (int w = 0; w < kThreads / 64; ++w) best = max(best, ws_root[w]);
+            for (int w = 0; w < NT / 64; ++w) best = max(best, ws_root[w]);
             nd.best = best;
             nd.seq = 0;
             s.cur[0] = nd;
@@ -1345,7 +1353,7 @@ __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p,
         }
         __syncthreads();
     } else {
-        for (int i = tid; i < nini; i += kThreads) { s.ccnt[i] = 0; s.cbest[i] = 0; }
+        for (int i = tid; i < nini; i += NT) { s.ccnt[i] = 0; s.cbest[i] = 0; }
         __syncthreads();
         auto root_of = [&](uint32_t key) {
             const float rx = (float)((int)(key & 0xFFF) - kBorder);
@@ -1383,7 +1391,7 @@ __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p,
         }
         __syncthreads();
         K.each([&](int j, int k) { K.set_node(j, k, s.nidx_s[K.node(j, k)]); });
-        zero_children(s, sh_S);   // (the roots' counts were read before the barrier above)
+        zero_children<NT>(s, sh_S);   // (the roots' counts were read before the barrier above)
         __syncthreads();
     }
     PHASE_MARK(2, 1);   // roots
@@ -1404,7 +1412,7 @@ __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p,
         // per node: (non-empty children | single-key parents << 21 | children
         // with more than one key << 42), scanned over a contiguous node range
         // per thread, so each thread reads back only its own entries
-        const int per = (S + kThreads - 1) / kThreads;
+        const int per = (S + NT - 1) / NT;
         const int i0 = min(tid * per, S), i1 = min(i0 + per, S);
         uint64_t local = 0;
         for (int i = i0; i < i1; ++i) {
@@ -1421,7 +1429,7 @@ __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p,
         if ((tid & 63) == 63) ws64[tid >> 6] = incl;
         __syncthreads();
         uint64_t run = incl - local, tot = 0;
-        for (int w = 0; w < kThreads / 64; ++w) {
+        for (int w = 0; w < NT / 64; ++w) {
             if (w < (tid >> 6)) run += ws64[w];
             tot += ws64[w];
         }
@@ -1453,7 +1461,7 @@ __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p,
         }
         // (only this thread reads its nodes' child entries)
         for (int i = 4 * i0; i < 4 * i1; ++i) { s.ccnt[i] = 0; s.cbest[i] = 0; }
-        for (int i = 4 * S + tid; i < 4 * S2; i += kThreads) { s.ccnt[i] = 0; s.cbest[i] = 0; }
+        for (int i = 4 * S + tid; i < 4 * S2; i += NT) { s.ccnt[i] = 0; s.cbest[i] = 0; }
         __syncthreads();
         {
             QNode *t = s.cur; s.cur = s.nxt; s.nxt = t;
@@ -1478,7 +1486,7 @@ __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p,
     while (final_phase) {
         {
             int nz = 0;
-            for (int i = tid; i < s.np2; i += kThreads) {
+            for (int i = tid; i < s.np2; i += NT) {
                 uint64_t v = 0;
                 if (i < S && s.cur[i].count > 1)
                     v = ((uint64_t)s.cur[i].count << 40) | ((uint64_t)s.cur[i].seq << 16) | (uint64_t)i;
@@ -1489,7 +1497,7 @@ __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p,
             nz = wave_sum_i32(nz);
             if ((tid & 63) == 0 && nz) atomicAdd(&sh_nv, nz);
         }
-        for (int i = tid; i < S; i += kThreads) s.mark[i] = 0;
+        for (int i = tid; i < S; i += NT) s.mark[i] = 0;
         __syncthreads();
         PHASE_MARK(2, 4);   // final: node keys
         // descending order of the splittable nodes' (count, seq, index) keys
@@ -1500,7 +1508,7 @@ __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p,
             // round trip per step instead of per pair); a64[S, np2) is 0 and np2
             // a power of two >= 8
             const int S8 = (S + 7) & ~7;
-            for (int i = tid; i < S; i += kThreads) {
+            for (int i = tid; i < S; i += NT) {
                 const uint64_t v = s.a64[i];
                 if (v == 0) continue;
                 int r = 0;
@@ -1519,7 +1527,7 @@ __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p,
         }
         PHASE_MARK(2, 5);   // final: sort
         // per rank: number of non-empty children (nc) and gain (nc - 1)
-        for (int r = tid; r < s.np2; r += kThreads) {
+        for (int r = tid; r < s.np2; r += NT) {
             uint64_t v = 0;
             if (s.a64[r] != 0) {
                 const int i = (int)(s.a64[r] & 0xFFFF);
@@ -1532,8 +1540,8 @@ __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p,
         if (tid == 0) sh_R = -1;
         __syncthreads();
         const int nv = sh_nv;
-        block_excl_scan_u64(s.b64, s.np2, ws64);
-        for (int r = tid; r < nv; r += kThreads) {
+        block_excl_scan_u64<NT>(s.b64, s.np2, ws64);
+        for (int r = tid; r < nv; r += NT) {
             const int i = (int)(s.a64[r] & 0xFFFF);
             int nc = 0;
             for (int q = 0; q < 4; ++q) nc += s.ccnt[4 * i + q] > 0;
@@ -1559,7 +1567,7 @@ __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p,
             if (tid == 0) *level_count = -1;
             return;
         }
-        for (int r = tid; r < R; r += kThreads) {
+        for (int r = tid; r < R; r += NT) {
             const int i = (int)(s.a64[r] & 0xFFFF);
             int cs = (int)(s.b64[r] & 0xFFFFFFFF);
             const QNode nd = s.cur[i];
@@ -1575,11 +1583,11 @@ __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p,
         __syncthreads();
         // (the child entries are read no more this round: re-zeroed for the
         // next round's counts, S2 >= S)
-        for (int i = tid; i < s.np2; i += kThreads) s.b64[i] = (i < S && !s.mark[i]) ? 1 : 0;
-        zero_children(s, S2);
+        for (int i = tid; i < s.np2; i += NT) s.b64[i] = (i < S && !s.mark[i]) ? 1 : 0;
+        zero_children<NT>(s, S2);
         __syncthreads();
-        block_excl_scan_u64(s.b64, s.np2, ws64);
-        for (int i = tid; i < S; i += kThreads) {
+        block_excl_scan_u64<NT>(s.b64, s.np2, ws64);
+        for (int i = tid; i < S; i += NT) {
             if (s.mark[i]) continue;
             const int ni = CC + (int)s.b64[i];
             s.nxt[ni] = s.cur[i];
@@ -1611,7 +1619,7 @@ __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p,
             if (nd < S_out && 0xFFFFFF - (int)(s.cur[nd].best & 0xFFFFFF) == k) sel[nd] = K.key[j];
         });
     } else {
-        for (int i = tid; i < S_out; i += kThreads) {
+        for (int i = tid; i < S_out; i += NT) {
             const int k = 0xFFFFFF - (int)(s.cur[i].best & 0xFFFFFF);
             sel[i] = keys[k];
         }
@@ -1620,8 +1628,8 @@ __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p,
     PHASE_MARK(2, 7);   // output
 }
 
-template <bool PIPE>
-__global__ __launch_bounds__(kThreads, 7) void k_quadtree(DevPlan p, FrameBufs fb, int l0) {
+template <bool PIPE, int NT>
+__global__ __launch_bounds__(NT, QCfg<NT>::MINB) void k_quadtree(DevPlan p, FrameBufs fb, int l0) {
     extern __shared__ __align__(16) uint8_t lds[];
     PHASE_START();
     const int l = l0 + blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
@@ -1654,12 +1662,12 @@ __global__ __launch_bounds__(kThreads, 7) void k_quadtree(DevPlan p, FrameBufs f
     int *cell_off = reinterpret_cast<int *>(lds);            // ncell + 1
     int *cell_src = cell_off + ncell + 1;                    // slot | bit 31: minThFAST list
     // key k's source (slot index | bit 31: minThFAST list), for the first
-    // kQuadRegKeys keys: each cell's thread writes its keys' entries right after
+    // QCfg<NT>::KR keys: each cell's thread writes its keys' entries right after
     // the scan, so the keys load with one LDS read each after one barrier
     uint32_t *kaddr = reinterpret_cast<uint32_t *>(cell_src + ncell);
-    __shared__ int ws2[2 * (kThreads / 64)];   // scan partials, alternating per chunk
+    __shared__ int ws2[2 * (NT / 64)];   // scan partials, alternating per chunk
     int base = 0;
-    for (int c0 = 0, chunk = 0; c0 < ncell; c0 += kThreads, ++chunk) {
+    for (int c0 = 0, chunk = 0; c0 < ncell; c0 += NT, ++chunk) {
         const int c = c0 + tid;
         int word = 0, slot = 0;
         if (c < ncell) {
@@ -1667,12 +1675,12 @@ __global__ __launch_bounds__(kThreads, 7) void k_quadtree(DevPlan p, FrameBufs f
             slot = p.cells[g.cell_begin + c].slot;
         }
         const int cnt = word & 0x7FFFFFFF;
-        int *ws = ws2 + (chunk & 1) * (kThreads / 64);
+        int *ws = ws2 + (chunk & 1) * (NT / 64);
         const int incl = wave_incl_scan_i32(cnt);
         if ((tid & 63) == 63) ws[tid >> 6] = incl;
         __syncthreads();
         int pre = 0, tot = 0;
-        for (int w = 0; w < kThreads / 64; ++w) {
+        for (int w = 0; w < NT / 64; ++w) {
             if (w < (tid >> 6)) pre += ws[w];
             tot += ws[w];
         }
@@ -1681,7 +1689,7 @@ __global__ __launch_bounds__(kThreads, 7) void k_quadtree(DevPlan p, FrameBufs f
             const uint32_t src = (uint32_t)slot | (word < 0 ? 0x80000000u : 0u);
             cell_off[c] = off;
             cell_src[c] = (int)src;
-            for (int i = 0; i < cnt && off + i < kQuadRegKeys; ++i) kaddr[off + i] = src + (uint32_t)i;
+            for (int i = 0; i < cnt && off + i < QCfg<NT>::KR; ++i) kaddr[off + i] = src + (uint32_t)i;
         }
         base += tot;
     }
@@ -1694,7 +1702,7 @@ __global__ __launch_bounds__(kThreads, 7) void k_quadtree(DevPlan p, FrameBufs f
         return;
     }
     const uint32_t *cand = fb.cand + (int64_t)b * p.cand_cap, *cand2 = fb.cand2 + (int64_t)b * p.cand_cap;
-    // up to kQRegKeys (kQRegKeysWide) keys per thread stay in registers
+    // up to QCfg<NT>::R1 (R2) keys per thread stay in registers
     // through the rounds
     auto in_registers = [&](auto &K) {
         K.gkeys = nullptr; K.gnode = knode; K.gq = kq; K.n = n;
@@ -1707,25 +1715,25 @@ __global__ __launch_bounds__(kThreads, 7) void k_quadtree(DevPlan p, FrameBufs f
         PHASE_MARK(2, 0);   // gather
         quadtree_rounds(p, fb, s, g, b, l, K, phase_t_);
     };
-    if (n <= kQRegKeys * kThreads) {
-        QKeys<kQRegKeys> K;
+    if (n <= QCfg<NT>::R1 * NT) {
+        QKeys<QCfg<NT>::R1, NT> K;
         in_registers(K);
-    } else if (n <= kQRegKeysWide * kThreads) {
-        QKeys<kQRegKeysWide> K;
+    } else if (n <= QCfg<NT>::R2 * NT) {
+        QKeys<QCfg<NT>::R2, NT> K;
         in_registers(K);
     } else {
-        QKeys<0> K;
+        QKeys<0, NT> K;
         K.gkeys = keys; K.gnode = knode; K.gq = kq; K.n = n;
         // kQU keys per thread at a time (the chunk mapping of QKeys<0>): their
         // bisections interleave, and their candidate loads go out together
-        for (int k0 = 0; k0 < n; k0 += kThreads * kQU) {
+        for (int k0 = 0; k0 < n; k0 += NT * kQU) {
             int lo[kQU], hi[kQU];
 #pragma unroll
             for (int u = 0; u < kQU; ++u) { lo[u] = 0; hi[u] = ncell - 1; }
             for (int step = ncell; step > 1; step = (step + 1) >> 1) {
 #pragma unroll
                 for (int u = 0; u < kQU; ++u) {
-                    const int k = k0 + u * kThreads + tid;
+                    const int k = k0 + u * NT + tid;
                     if (lo[u] < hi[u]) {
                         const int mid = (lo[u] + hi[u] + 1) >> 1;
                         if (cell_off[mid] <= k) lo[u] = mid; else hi[u] = mid - 1;
@@ -1734,7 +1742,7 @@ __global__ __launch_bounds__(kThreads, 7) void k_quadtree(DevPlan p, FrameBufs f
             }
 #pragma unroll
             for (int u = 0; u < kQU; ++u) {
-                const int k = k0 + u * kThreads + tid;
+                const int k = k0 + u * NT + tid;
                 while (lo[u] < hi[u]) {   // (the halving bound above covers every bisection; kept for safety)
                     const int mid = (lo[u] + hi[u] + 1) >> 1;
                     if (cell_off[mid] <= k) lo[u] = mid; else hi[u] = mid - 1;
@@ -2223,16 +2231,34 @@ hipError_t allow_lds(K kernel, int bytes) {
                                hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
-hipError_t launch_quadtree(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t st) {
-    if (allow_lds(k_quadtree<false>, p.node_lds_bytes) != hipSuccess) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_quadtree<false>, dim3(p.nlevels, B), dim3(kThreads), p.node_lds_bytes, st, p, fb, 0);
+// The 1024-thread form when the launch is too small to fill the chip with
+// 256-thread workgroups (ORBX_QT_WIDE=0 never, 1 always where it fits).
+bool quadtree_wide(const DevPlan &p, int blocks) {
+    const char *e = std::getenv("ORBX_QT_WIDE");   // (read per launch: tests switch it per extractor)
+    const int mode = e ? std::atoi(e) : -1;
+    if (mode == 0 || p.node_lds_bytes_w > 160 * 1024) return false;
+    return mode == 1 || blocks <= 256;
+}
+
+template <bool PIPE>
+hipError_t launch_quadtree_range(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t st, int l, int l_end) {
+    const dim3 grid(l_end - l, B);
+    if (quadtree_wide(p, (l_end - l) * B)) {
+        if (allow_lds(k_quadtree<PIPE, 1024>, p.node_lds_bytes_w) != hipSuccess) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_quadtree<PIPE, 1024>), grid, dim3(1024), p.node_lds_bytes_w, st, p, fb, l);
+    } else {
+        if (allow_lds(k_quadtree<PIPE, kThreads>, p.node_lds_bytes) != hipSuccess) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_quadtree<PIPE, kThreads>), grid, dim3(kThreads), p.node_lds_bytes, st, p, fb, l);
+    }
     return hipGetLastError();
 }
 
+hipError_t launch_quadtree(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t st) {
+    return launch_quadtree_range<false>(p, fb, B, st, 0, p.nlevels);
+}
+
 hipError_t launch_quadtree_level(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t st, int l, int l_end) {
-    if (allow_lds(k_quadtree<true>, p.node_lds_bytes) != hipSuccess) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_quadtree<true>, dim3(l_end - l, B), dim3(kThreads), p.node_lds_bytes, st, p, fb, l);
-    return hipGetLastError();
+    return launch_quadtree_range<true>(p, fb, B, st, l, l_end);
 }
 
 hipError_t launch_describe(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t st) {

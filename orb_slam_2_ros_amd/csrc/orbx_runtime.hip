@@ -336,8 +336,11 @@ int upload_plan(orbx_extractor *ex) {
     d.node_lds_bytes = quadtree_lds_bytes(node_cap);
     // phase 1 of k_quadtree keeps two ints per cell of a level and a u32 key
     // source per register-held key (kQuadRegKeys in all) in the same LDS
-    for (const LevelGeom &g : p.lv)
+    d.node_lds_bytes_w = d.node_lds_bytes;   // (the 1024-thread form's map holds kQuadRegKeysW sources)
+    for (const LevelGeom &g : p.lv) {
         d.node_lds_bytes = std::max(d.node_lds_bytes, (int)(8 * (g.cell_end - g.cell_begin) + 16 + 4 * kQuadRegKeys));
+        d.node_lds_bytes_w = std::max(d.node_lds_bytes_w, (int)(8 * (g.cell_end - g.cell_begin) + 16 + 4 * kQuadRegKeysW));
+    }
     d.dbg_stop = std::getenv("ORBX_DBG_STOP") ? std::atoi(std::getenv("ORBX_DBG_STOP")) : 0;
     if (d.node_lds_bytes > 160 * 1024) return ORBX_EINVAL;
     return ORBX_OK;

@@ -156,14 +156,24 @@ class ORBmatcher:
                 for k, (qi, qd, kf, nq, n) in enumerate(outs)]
 
     # -- vocabulary-node searches (ORBmatcher.cc:160-289, 524-657, 659-825) --
-    @staticmethod
-    def _bow_side(S, keep):
-        arrs = (np.ascontiguousarray(S["keys"], KEYPOINT_DTYPE), np.ascontiguousarray(S["desc"], np.uint8),
-                np.ascontiguousarray(S["flags"], np.uint8), np.ascontiguousarray(S["ids"], np.uint32),
-                np.ascontiguousarray(S["off"], np.int32), np.ascontiguousarray(S["feat"], np.int32))
+    _BOW_FIELDS = (("keys", KEYPOINT_DTYPE), ("desc", np.uint8), ("flags", np.uint8), ("ids", np.uint32),
+                   ("off", np.int32), ("feat", np.int32))
+    _side_cache: list = []   # (source arrays, BowSide): sides whose arrays went in unconverted
+
+    @classmethod
+    def _bow_side(cls, S, keep):
+        src = tuple(S[f] for f, _ in cls._BOW_FIELDS)
+        for c_src, side in cls._side_cache:   # the same array objects as a recent call: same addresses
+            if all(a is b for a, b in zip(c_src, src)) and side.n == len(src[0]) and side.nnodes == len(src[3]):
+                keep.append(c_src)
+                return side
+        arrs = tuple(np.ascontiguousarray(a, dt) for a, (_, dt) in zip(src, cls._BOW_FIELDS))
         keep.append(arrs)
         k, d, f, i, o, e = arrs
-        return BowSide(ptr(k), ptr(d), ptr(f), len(k), ptr(i), ptr(o), ptr(e), len(i))
+        side = BowSide(ptr(k), ptr(d), ptr(f), len(k), ptr(i), ptr(o), ptr(e), len(i))
+        if all(a is b for a, b in zip(arrs, src)):   # (a converted copy could go stale: not cached)
+            cls._side_cache = ([(src, side)] + cls._side_cache)[:8]
+        return side
 
     def search_by_bow_batch(self, variant, problems, nlevels=8):
         """Several search_by_bow calls of one variant in one launch pair
