@@ -445,6 +445,12 @@ __global__ __launch_bounds__(kThreads) void k_resize(DevPlan p, FrameBufs fb, in
 // v_dot2_u32_u16; the vertical pass is OpenCV's fixed point as above.
 // ===========================================================================
 typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+#ifndef ORBX_RS_REUSE
+#define ORBX_RS_REUSE 1
+#endif
+#ifndef ORBX_RS_MULHI
+#define ORBX_RS_MULHI 1
+#endif
 
 __host__ __device__ inline int resize_src_raw(int d, double scale) {
 #ifdef __HIP_DEVICE_COMPILE__
@@ -512,6 +518,12 @@ __device__ inline void resize_tile(const DevPlan &p, const FrameBufs &fb, int l,
                                           false);
         }
     };
+    // the horizontal pass of source row `prow` from the previous output row:
+    // the next row's first source row is usually the previous one's second
+#if ORBX_RS_REUSE
+    uint32_t hp[4] = {0u, 0u, 0u, 0u};
+    int prow = -1;
+#endif
 #pragma unroll
     for (int j = 0; j < kResizeK; ++j) {
         const int y = yb + j;
@@ -519,16 +531,41 @@ __device__ inline void resize_tile(const DevPlan &p, const FrameBufs &fb, int l,
         const int s0 = min(max((int)tyk[j].src, 0), gs.h - 1), s1 = min(max((int)tyk[j].src + 1, 0), gs.h - 1);
         const int b0 = tyk[j].a0, b1 = tyk[j].a1;
         uint32_t h0[4], h1[4];
+#if ORBX_RS_REUSE
+        if (s0 == prow) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) h0[k] = hp[k];
+        } else {
+            hrow(s0, h0);
+        }
+        hrow(s1, h1);
+        prow = s1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) hp[k] = h1[k];
+#else
         hrow(s0, h0);
         hrow(s1, h1);
+#endif
         // SSE2 columns: _mm_packs_epi32(h>>4); _mm_mulhi_epi16; _mm_adds_epi16; +2; >>2
         // (h <= 255 * 2048: no saturation, result <= 255); the last < 16 columns
         // are the scalar tail FixedPtCast<int, uchar, 22>
         uint32_t packed = 0;
         if (simd_all) {
+#if ORBX_RS_MULHI
+            // ((h >> 4) * b) >> 16 as the high half of a 24 x 24-bit product:
+            // (h & ~15) * (b << 12) = ((h >> 4) * b) << 16, both operands < 2^24
+            const uint32_t bb0 = ((uint32_t)b0 & 0xFFFu) << 12, bb1 = ((uint32_t)b1 & 0xFFFu) << 12;   // (b <= 2048)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t t0 = (uint32_t)(((uint64_t)(h0[k] & 0xFFFF0u) * bb0) >> 32);
+                const uint32_t t1 = (uint32_t)(((uint64_t)(h1[k] & 0xFFFF0u) * bb1) >> 32);
+                packed |= ((t0 + t1 + 2) >> 2) << (8 * k);
+            }
+#else
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 packed |= (((mul24u(h0[k] >> 4, b0) >> 16) + (mul24u(h1[k] >> 4, b1) >> 16) + 2) >> 2) << (8 * k);
+#endif
         } else {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {

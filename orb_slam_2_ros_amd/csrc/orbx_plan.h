@@ -80,8 +80,14 @@ struct LevelGeom {
 // Wave-tile geometry of one pyramid level's resize (k_resize): a wave owns
 // 4*twg columns x (64/twg)*kResizeK rows; lane (lr, lg) writes columns
 // x0 + 4 lg .. + 3 of rows y0 + lr kResizeK + j.  twg in {16, 32, 64} is chosen
-// per level to waste the fewest columns at the right edge.
-constexpr int kResizeK = 8;
+// per level to waste the fewest columns at the right edge.  10 rows per lane:
+// at the 1.2 scale factor the source rows advance by 6 every 5 output rows,
+// so every lane group starts at the same phase and the lanes of a wave reuse
+// the previous row's horizontal pass together (resize_tile).
+#ifndef ORBX_RS_K
+#define ORBX_RS_K 10
+#endif
+constexpr int kResizeK = ORBX_RS_K;
 struct ResizeWave {
     double sx = 0, sy = 0;     // source / destination size ratio, as make_resize_taps
     int twg = 64, twg_shift = 6;
