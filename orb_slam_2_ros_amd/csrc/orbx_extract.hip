@@ -1118,7 +1118,7 @@ template <> struct QCfg<1024> { static constexpr int R1 = 4, R2 = kQuadRegKeysW 
 #endif
 constexpr int kQU = ORBX_QT_QU;
 #ifndef ORBX_QT_PF
-#define ORBX_QT_PF 1
+#define ORBX_QT_PF 0   // (FHD quadtree 0.243 -> 0.255 ms with it, profiles/r04_ab_qt_fhd.txt)
 #endif
 template <int R, int NT>
 struct QKeys {

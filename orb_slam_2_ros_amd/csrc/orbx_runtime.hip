@@ -394,7 +394,8 @@ int reserve(orbx_extractor *ex, int w, int h, int max_batch) {
     ok &= dalloc(&ex->d_depth, B * p.max_kps) == hipSuccess;
     ok &= dalloc(&ex->d_sad, B * p.max_kps) == hipSuccess;
     ok &= dalloc(&ex->d_nkept, B) == hipSuccess;
-    if (B >= 4 && p.max_kps <= 65535)
+    const char *so = std::getenv("ORBX_STEREO_SORT_ONCE");   // (k_band_sort + k_stereo_band_gs, orbx_stereo.hip)
+    if (so && so[0] == '1' && B >= 4 && p.max_kps <= 65535)
         ok &= dalloc(&ex->d_bands, (size_t)(B / 2) * stereo_band_stride(p.height, p.max_kps)) == hipSuccess;
     if (!ok) { ex->release(); return ORBX_ENOMEM; }
     ex->planned = true;
@@ -1144,11 +1145,17 @@ int orbx_extractor_pyramid_host(orbx_extractor *ex, uint8_t *const *out, const s
     if (!ex || !ex->planned || !out || !out_pitch || nlevels < 1 || nlevels > ex->nlevels) return ORBX_EINVAL;
     const auto &s = ex->slot[ex->cur];
     if (s.batch <= 0) return ORBX_EINVAL;
-    size_t total = 0;
-    for (int l = 0; l < nlevels; ++l) {
+    for (int l = 0; l < nlevels; ++l)
         if (!out[l] || out_pitch[l] < (size_t)ex->plan.lv[l].w) return ORBX_EINVAL;
-        total += (size_t)ex->plan.lv[l].w * ex->plan.lv[l].h;
-    }
+    // two linear spans, pitches included (a 2-D copy of narrow rows runs row by
+    // row): level 0 where the last call read it, levels 1.. of frame 0 (one
+    // contiguous block of the pyramid)
+    const LevelGeom &g0 = ex->plan.lv[0], &gl = ex->plan.lv[nlevels - 1];
+    const size_t p0 = (size_t)s.img0_pitch;
+    const size_t span0 = p0 * (g0.h - 1) + g0.w;
+    const size_t base1 = nlevels > 1 ? (size_t)ex->plan.lv[1].pyr_off : 0;
+    const size_t span1 = nlevels > 1 ? (size_t)gl.pyr_off + (size_t)gl.pitch * (gl.h - 1) + gl.w - base1 : 0;
+    const size_t off1 = (span0 + 255) & ~size_t(255), total = off1 + span1;
     if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
     if (ex->h_pyr_bytes < total) {
         if (ex->h_pyr) (void)hipHostFree(ex->h_pyr);
@@ -1159,23 +1166,16 @@ int orbx_extractor_pyramid_host(orbx_extractor *ex, uint8_t *const *out, const s
         ex->h_pyr_bytes = total;
     }
     if (sync_results(ex)) return ORBX_EIO;
-    // every level into the pinned staging in one stream-ordered chain, one wait
-    size_t off = 0;
+    if (hipMemcpyAsync(ex->h_pyr, s.img0, span0, hipMemcpyDeviceToHost, ex->stream) != hipSuccess ||
+        (span1 && hipMemcpyAsync(ex->h_pyr + off1, ex->d_pyr + base1, span1, hipMemcpyDeviceToHost, ex->stream) !=
+                      hipSuccess) ||
+        hipStreamSynchronize(ex->stream) != hipSuccess)
+        return ORBX_EIO;
     for (int l = 0; l < nlevels; ++l) {
         const LevelGeom &g = ex->plan.lv[l];
-        const uint8_t *src = l == 0 ? s.img0 : ex->d_pyr + g.pyr_off;
-        const size_t sp = l == 0 ? (size_t)s.img0_pitch : (size_t)g.pitch;
-        if (hipMemcpy2DAsync(ex->h_pyr + off, g.w, src, sp, g.w, g.h, hipMemcpyDeviceToHost, ex->stream) !=
-            hipSuccess)
-            return ORBX_EIO;
-        off += (size_t)g.w * g.h;
-    }
-    if (hipStreamSynchronize(ex->stream) != hipSuccess) return ORBX_EIO;
-    off = 0;
-    for (int l = 0; l < nlevels; ++l) {
-        const LevelGeom &g = ex->plan.lv[l];
-        for (int r = 0; r < g.h; ++r) std::memcpy(out[l] + (size_t)r * out_pitch[l], ex->h_pyr + off + (size_t)r * g.w, g.w);
-        off += (size_t)g.w * g.h;
+        const uint8_t *src = l == 0 ? ex->h_pyr : ex->h_pyr + off1 + ((size_t)g.pyr_off - base1);
+        const size_t sp = l == 0 ? p0 : (size_t)g.pitch;
+        for (int r = 0; r < g.h; ++r) std::memcpy(out[l] + (size_t)r * out_pitch[l], src + (size_t)r * sp, g.w);
     }
     return ORBX_OK;
 }

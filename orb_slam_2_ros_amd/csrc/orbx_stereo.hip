@@ -436,7 +436,9 @@ __global__ __launch_bounds__(kST) void k_stereo_band_g(StereoBufs a) {
 // copied to the pair's scratch, span in its last dword), then the grouped
 // search over the scratch (k_stereo_band_gs), so a batch of pairs runs the
 // 16-lane search on thousands of small blocks without every block re-sorting
-// its pair's right keypoints.
+// its pair's right keypoints.  Measured no faster than k_stereo_band at the
+// bench's batches (EuRoC 123.6 -> 122.5 k, KITTI 77.1 -> 75.4 k pairs/s,
+// profiles/r04_ab_stereo_sort_once.txt): off unless ORBX_STEREO_SORT_ONCE=1.
 __global__ __launch_bounds__(kST) void k_band_sort(StereoBufs a) {
     extern __shared__ __align__(16) uint8_t lds[];
     __shared__ int ws[4];
@@ -609,11 +611,7 @@ int64_t stereo_band_stride(int rows, int nr_cap) { return ((int64_t)stereo_lds_b
 hipError_t launch_stereo(const StereoBufs &a, int pairs, int nl_cap, hipStream_t st) {
     if (pairs <= 0) return hipSuccess;
     const int bytes = stereo_lds_bytes(a.rows, a.nr_cap);
-    static const bool sorted_once = [] {
-        const char *e = std::getenv("ORBX_STEREO_SORT_ONCE");
-        return !(e && e[0] == '0');
-    }();
-    if (a.bands && sorted_once && pairs > 1) {
+    if (a.bands && pairs > 1) {
         if (bytes > 64 * 1024 &&
             hipFuncSetAttribute(reinterpret_cast<const void *>(k_band_sort), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 bytes) != hipSuccess)
