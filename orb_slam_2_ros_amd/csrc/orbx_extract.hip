@@ -1105,7 +1105,9 @@ struct QLds {
 // NT = 1024 serves launches too small to fill the chip (a few frames: the
 // drop-in call, a sharded camera set), where a level's latency is the step's.
 template <int NT> struct QCfg;
+constexpr int kQPreRoots = 16;   // roots the global-key gather counts itself (more: the roots' own pass)
 template <> struct QCfg<256> { static constexpr int R1 = 6, R2 = kQuadRegKeys / 256, KR = kQuadRegKeys, MINB = 7; };
+template <> struct QCfg<512> { static constexpr int R1 = 10, R2 = 2 * kQuadRegKeysW / 1024, KR = kQuadRegKeysW, MINB = 4; };
 template <> struct QCfg<1024> { static constexpr int R1 = 4, R2 = kQuadRegKeysW / 1024, KR = kQuadRegKeysW, MINB = 1; };
 // R == 0 (keys in global scratch): a pass walks the keys kQU per thread at a
 // time, the chunk's loads issued together into a register cache (key k =
@@ -1309,9 +1311,21 @@ __device__ inline void zero_children(const QLds &s, int S) {
 
 // One key pass per round: each key moves to its node of the round just built
 // (nidx_c[4 node + quadrant]) and, when that node is splittable, adds itself
-// to the node's child counts (as child_stats).  Ends with a barrier.
+// to the node's child counts (as child_stats).  Ends with a barrier.  The
+// 256-thread form with register-held keys (VGA) moves the keys in a pass of
+// their own and then counts (0.386 vs 0.403 ms fused per 3072 VGA frames,
+// profiles/r04_ab_qt_fhd2.txt): the fused pass's dependent LDS reads queue
+// behind each key's atomics; the global-key path and the wider forms gain from
+// the single pass (FHD 0.298 -> 0.243 ms).  (No barrier between the two
+// loops: the move touches registers only, and the counters were zeroed before
+// the barrier that precedes this pass.)
 template <int R, int NT>
 __device__ __attribute__((always_inline)) void advance_stats(const QLds &s, QKeys<R, NT> &K) {
+    if constexpr (NT == 256 && R > 0) {
+        K.each([&](int j, int k) { K.set_node(j, k, s.nidx_c[4 * K.node(j, k) + K.quad(j, k)]); });
+        child_stats(s, K);
+        return;
+    }
     K.each_all([&](int j, int k, bool valid) {
         uint32_t slot = ~0u, bp = 0;
         if (valid) {
@@ -1350,7 +1364,8 @@ __device__ inline QNode make_child(const QLds &s, const QNode &parent, int i, in
 // Phases 2-5 of k_quadtree on the gathered keys (ORBextractor.cc:566-784).
 template <int NR, int NT>
 __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p, const FrameBufs &fb, QLds &s, const LevelGeom &g, int b, int l,
-                                QKeys<NR, NT> &K, uint64_t &phase_t_) {
+                                QKeys<NR, NT> &K, uint64_t &phase_t_, const uint32_t *pre_cnt = nullptr,
+                                const uint32_t *pre_best = nullptr) {
     const int tid = threadIdx.x;
     const int N = g.quota, NC = p.node_cap;
     const uint32_t *keys = K.gkeys;
@@ -1360,7 +1375,32 @@ __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p,
 
     // ---- 2. root nodes (ORBextractor.cc:566-613)
     const int nini = g.nini;
-    if (nini == 1) {
+    if (pre_cnt) {
+        // counted in the gather (every key's node is its root index r, its
+        // quadrant 0): the non-empty roots in order, and root r's four slots
+        // of nidx_c map to its list position, so the first key pass moves the
+        // keys as any round's does (advance_stats)
+        for (int i = tid; i < 4 * nini; i += NT) { s.ccnt[i] = 0; s.cbest[i] = 0; }
+        if (tid == 0) {
+            int S = 0;
+            for (int r = 0; r < nini; ++r) {
+                if (pre_cnt[r] == 0) continue;
+                QNode nd;
+                nd.x0 = (int16_t)(int)__fmul_rn(g.hx, (float)r);
+                nd.x1 = (int16_t)(int)__fmul_rn(g.hx, (float)(r + 1));
+                nd.y0 = 0;
+                nd.y1 = (int16_t)(g.h - 2 * kBorder);
+                nd.count = (int32_t)pre_cnt[r];
+                nd.best = pre_best[r];
+                nd.seq = 0;
+                s.cur[S] = nd;
+                set_all_quads(s.nidx_c, r, S);
+                ++S;
+            }
+            sh_S = S;
+        }
+        __syncthreads();
+    } else if (nini == 1) {
         // one root (every 4:3 or squarer level): every key's node is 0, its
         // count the key count and its best key a block maximum (wave maxima
         // through LDS: no per-key atomics, no serial pass)
@@ -1442,7 +1482,8 @@ __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p,
     // only matters to the register path's output (phase 5).
     bool final_phase = false;
     int S = sh_S;
-    child_stats(s, K);
+    if (pre_cnt) advance_stats(s, K);
+    else child_stats(s, K);
     PHASE_MARK(2, 2);   // child counts
     // ---- 3. full rounds (ORBextractor.cc:618-696)
     while (true) {
@@ -1761,38 +1802,76 @@ __global__ __launch_bounds__(NT, QCfg<NT>::MINB) void k_quadtree(DevPlan p, Fram
     } else {
         QKeys<0, NT> K;
         K.gkeys = keys; K.gnode = knode; K.gq = kq; K.n = n;
+        // the cell of key 64 m for every m (in the key-source map's LDS,
+        // unused on this path): a wave's 64 keys (k0 is a multiple of 64)
+        // then bisect only the cells between two of them
+        const int nco = (n + 63) >> 6;
+        int *coarse = reinterpret_cast<int *>(kaddr);
+        const bool use_co = nco < QCfg<NT>::KR;
+        if (use_co) {
+            for (int c = tid; c < ncell; c += NT) {
+                const int o = cell_off[c], e = cell_off[c + 1];
+                for (int m = (o + 63) >> 6; (m << 6) < e; ++m) coarse[m] = c;
+            }
+            if (tid == 0) coarse[nco] = ncell - 1;
+        }
+        // the roots counted here when there are few (every level but the
+        // narrowest strips): count and best key per root by the aggregated
+        // atomics, each key's node = its root and quadrant 0 written with it
+        __shared__ uint32_t rcnt[kQPreRoots], rbest[kQPreRoots];
+        const int nini = g.nini;
+        const bool pre = nini <= kQPreRoots;
+        if (tid < kQPreRoots) { rcnt[tid] = 0; rbest[tid] = 0; }
+        __syncthreads();
         // kQU keys per thread at a time (the chunk mapping of QKeys<0>): their
         // bisections interleave, and their candidate loads go out together
         for (int k0 = 0; k0 < n; k0 += NT * kQU) {
             int lo[kQU], hi[kQU];
 #pragma unroll
-            for (int u = 0; u < kQU; ++u) { lo[u] = 0; hi[u] = ncell - 1; }
-            for (int step = ncell; step > 1; step = (step + 1) >> 1) {
+            for (int u = 0; u < kQU; ++u) {
+                const int m = (k0 + u * NT + tid) >> 6;   // (wave-uniform)
+                lo[u] = use_co && m < nco ? coarse[m] : 0;
+                hi[u] = use_co && m < nco ? coarse[m + 1] : ncell - 1;
+            }
+            for (bool more = true; more;) {
+                more = false;
 #pragma unroll
                 for (int u = 0; u < kQU; ++u) {
                     const int k = k0 + u * NT + tid;
                     if (lo[u] < hi[u]) {
                         const int mid = (lo[u] + hi[u] + 1) >> 1;
                         if (cell_off[mid] <= k) lo[u] = mid; else hi[u] = mid - 1;
+                        more |= lo[u] < hi[u];
                     }
                 }
             }
 #pragma unroll
             for (int u = 0; u < kQU; ++u) {
                 const int k = k0 + u * NT + tid;
-                while (lo[u] < hi[u]) {   // (the halving bound above covers every bisection; kept for safety)
-                    const int mid = (lo[u] + hi[u] + 1) >> 1;
-                    if (cell_off[mid] <= k) lo[u] = mid; else hi[u] = mid - 1;
-                }
+                uint32_t slot = ~0u, bp = 0;
                 if (k < n) {
                     const int src = cell_src[lo[u]];
-                    keys[k] = ((src < 0) ? cand2 : cand)[(src & 0x7FFFFFFF) + (k - cell_off[lo[u]])];
+                    const uint32_t key = ((src < 0) ? cand2 : cand)[(src & 0x7FFFFFFF) + (k - cell_off[lo[u]])];
+                    keys[k] = key;
+                    if (pre) {
+                        int r = 0;
+                        if (nini > 1) {
+                            const float rx = (float)((int)(key & 0xFFF) - kBorder);
+                            r = min((int)__fdiv_rn(rx, g.hx), nini - 1);
+                        }
+                        knode[k] = (uint16_t)r;
+                        kq[k] = 0;
+                        slot = (uint32_t)r;
+                        bp = best_pack(key, k);
+                    }
                 }
+                if (pre) agg_atomics(rcnt, rbest, slot, bp);   // (every lane: DPP)
             }
         }
         __syncthreads();
         PHASE_MARK(2, 0);
-        quadtree_rounds(p, fb, s, g, b, l, K, phase_t_);
+        if (pre) quadtree_rounds(p, fb, s, g, b, l, K, phase_t_, rcnt, rbest);
+        else quadtree_rounds(p, fb, s, g, b, l, K, phase_t_);
     }
 }
 
@@ -2268,24 +2347,43 @@ hipError_t allow_lds(K kernel, int bytes) {
                                hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
-// The 1024-thread form when the launch is too small to fill the chip with
-// 256-thread workgroups (ORBX_QT_WIDE=0 never, 1 always where it fits).
-bool quadtree_wide(const DevPlan &p, int blocks) {
-    const char *e = std::getenv("ORBX_QT_WIDE");   // (read per launch: tests switch it per extractor)
-    const int mode = e ? std::atoi(e) : -1;
-    if (mode == 0 || p.node_lds_bytes_w > 160 * 1024) return false;
-    return mode == 1 || blocks <= 256;
+// Workgroup size of k_quadtree for a launch of `blocks` (level, frame)
+// blocks: 1024 threads when the launch is too small to fill the chip with
+// 256-thread workgroups (a few frames: the drop-in call, a sharded camera
+// set); 512 for images of more than 0.6 MP (HD, FHD: thousands of keys on
+// every level, up to 20 per thread in registers, two workgroups per CU);
+// else 256 (VGA: <= 8 register keys per thread, 7 workgroups per CU).
+// ORBX_QT_NT=256 / 512 / 1024 forces one (where its LDS fits); ORBX_QT_WIDE=0
+// never takes 1024, =1 always (read per launch: tests switch them per extractor).
+int quadtree_nt(const DevPlan &p, int blocks) {
+    const bool wide_fits = p.node_lds_bytes_w <= 160 * 1024;
+    if (const char *e = std::getenv("ORBX_QT_NT")) {
+        const int nt = std::atoi(e);
+        if ((nt == 512 || nt == 1024) && wide_fits) return nt;
+        if (nt == 256) return 256;
+    }
+    const char *w = std::getenv("ORBX_QT_WIDE");
+    const int mode = w ? std::atoi(w) : -1;
+    if (!wide_fits) return 256;
+    if (mode == 1 || (mode != 0 && blocks <= 256)) return 1024;
+    return (int64_t)p.lv[0].w * p.lv[0].h > 600 * 1000 ? 512 : 256;
 }
 
 template <bool PIPE>
 hipError_t launch_quadtree_range(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t st, int l, int l_end) {
     const dim3 grid(l_end - l, B);
-    if (quadtree_wide(p, (l_end - l) * B)) {
-        if (allow_lds(k_quadtree<PIPE, 1024>, p.node_lds_bytes_w) != hipSuccess) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((k_quadtree<PIPE, 1024>), grid, dim3(1024), p.node_lds_bytes_w, st, p, fb, l);
-    } else {
-        if (allow_lds(k_quadtree<PIPE, kThreads>, p.node_lds_bytes) != hipSuccess) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((k_quadtree<PIPE, kThreads>), grid, dim3(kThreads), p.node_lds_bytes, st, p, fb, l);
+    switch (quadtree_nt(p, (l_end - l) * B)) {
+        case 1024:
+            if (allow_lds(k_quadtree<PIPE, 1024>, p.node_lds_bytes_w) != hipSuccess) return hipErrorInvalidValue;
+            hipLaunchKernelGGL((k_quadtree<PIPE, 1024>), grid, dim3(1024), p.node_lds_bytes_w, st, p, fb, l);
+            break;
+        case 512:
+            if (allow_lds(k_quadtree<PIPE, 512>, p.node_lds_bytes_w) != hipSuccess) return hipErrorInvalidValue;
+            hipLaunchKernelGGL((k_quadtree<PIPE, 512>), grid, dim3(512), p.node_lds_bytes_w, st, p, fb, l);
+            break;
+        default:
+            if (allow_lds(k_quadtree<PIPE, kThreads>, p.node_lds_bytes) != hipSuccess) return hipErrorInvalidValue;
+            hipLaunchKernelGGL((k_quadtree<PIPE, kThreads>), grid, dim3(kThreads), p.node_lds_bytes, st, p, fb, l);
     }
     return hipGetLastError();
 }

@@ -12,6 +12,8 @@
 // of every stream against the current one without a copy.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -1895,8 +1897,31 @@ int bow_check(int variant, const orbx_bow_side *A, const orbx_bow_side *B, const
     return (A->n == 0 || B->n == 0 || A->nnodes == 0 || B->nnodes == 0) ? 1 : ORBX_OK;
 }
 
+// ORBX_CALL_TIMING=1: a synchronous call's host phases (checks, staging,
+// enqueue, wait, readback) in microseconds on stderr (diagnostics).
+struct CallClock {
+    bool on;
+    std::chrono::steady_clock::time_point t0;
+    double us[6] = {};
+    int n = 0;
+    CallClock() : on(std::getenv("ORBX_CALL_TIMING") != nullptr), t0(std::chrono::steady_clock::now()) {}
+    void mark() {
+        if (!on || n >= 6) return;
+        const auto t = std::chrono::steady_clock::now();
+        us[n++] = std::chrono::duration<double, std::micro>(t - t0).count();
+        t0 = t;
+    }
+    void print(const char *what) const {
+        if (!on) return;
+        std::fprintf(stderr, "orbx %s us:", what);
+        for (int i = 0; i < n; ++i) std::fprintf(stderr, " %.1f", us[i]);
+        std::fprintf(stderr, "\n");
+    }
+};
+
 int bow_run(int device, int variant, orbx_bow_problem *P, int np, float nnratio, int check_ori, int nlevels) {
     if (np < 0 || (np && !P)) return ORBX_EINVAL;
+    CallClock clk;
     std::vector<int> live;
     for (int k = 0; k < np; ++k) {
         const int rc = bow_check(variant, &P[k].a, &P[k].b, P[k].tri, nlevels, P[k].match_a, P[k].match_b,
@@ -1906,6 +1931,7 @@ int bow_run(int device, int variant, orbx_bow_problem *P, int np, float nnratio,
     }
     if (live.empty()) return ORBX_OK;
     if (hipSetDevice(device) != hipSuccess) return ORBX_ENODEV;
+    clk.mark();   // checks
     const int nl = (int)live.size();
     const int ntri = variant == ORBX_BOW_TRIANGULATION ? 11 + 2 * nlevels : 0;
     Layout L;
@@ -1975,12 +2001,15 @@ int bow_run(int device, int variant, orbx_bow_problem *P, int np, float nnratio,
     }
     put(ws, o_pa, hb.data(), sizeof(BowBufs) * nl);
     std::memset(ws.host + in_bytes, 0, cnt_end - in_bytes);   // the counters go up as zeros with the inputs
+    clk.mark();   // layout + staging copies
     if (hipMemcpyAsync(D, ws.host, cnt_end, hipMemcpyHostToDevice, ws.st) != hipSuccess) return ORBX_EIO;
     const size_t o_out = o[0].ma;   // match arrays and counters are one contiguous run
     HostTail tail;
     ws_tail(ws, o_out, cnt_end - o_out, at<uint32_t>(D, o_done), nl, tail);
     if (launch_bow(hb.data(), at<BowBufs>(D, o_pa), nl, tail, ws.st) != hipSuccess) return ORBX_EIO;
+    clk.mark();   // enqueue
     if (ws_wait(ws, tail, o_out, cnt_end - o_out)) return ORBX_EIO;
+    clk.mark();   // wait
     for (int t = 0; t < nl; ++t) {
         orbx_bow_problem &pr = P[live[t]];
         get(ws, o[t].ma, pr.match_a, 4 * (size_t)pr.a.n);
@@ -1989,6 +2018,8 @@ int bow_run(int device, int variant, orbx_bow_problem *P, int np, float nnratio,
         get(ws, o[t].cnt + 4 * 32, counts, sizeof(counts));
         pr.nmatches = counts[1];
     }
+    clk.mark();   // readback
+    clk.print("bow");
     return ORBX_OK;
 }
 

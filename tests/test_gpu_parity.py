@@ -316,16 +316,16 @@ def test_quadtree_clustered_keys(w, h, nfeat, kind, extractors, oracle_mod):
     assert np.array_equal(dg, do), f"descriptors differ at {_first_diff(dg, do)}"
 
 
-@pytest.mark.parametrize("wide", ["0", "1"])
+@pytest.mark.parametrize("nt", ["256", "512", "1024"])
 @pytest.mark.parametrize("w,h,nfeat,kind", [(640, 480, 1000, "corner"), (1241, 376, 2000, "stripe"),
                                             (1920, 1080, 1000, "band"), (1920, 1080, 1000, "quadrant"),
                                             (1920, 1080, 1000, None), (2560, 1920, 2000, None)])
-def test_quadtree_workgroup_forms(w, h, nfeat, kind, wide, monkeypatch, oracle_mod):
-    """k_quadtree's 256-thread form (ORBX_QT_WIDE=0) and its 1024-thread form
-    for launches of few frames (=1): register keys (VGA, KITTI, FHD: 4 / 10
-    per thread in the wide form) and global-scratch keys (2560 x 1920: ~20 k
-    candidates on level 0, past either form's registers), bit-exact."""
-    monkeypatch.setenv("ORBX_QT_WIDE", wide)
+def test_quadtree_workgroup_forms(w, h, nfeat, kind, nt, monkeypatch, oracle_mod):
+    """k_quadtree's 256-, 512- and 1024-thread forms (ORBX_QT_NT): register
+    keys (VGA, KITTI, FHD: up to 8 / 20 / 10 per thread), global-scratch keys
+    with the roots counted in the gather (2560 x 1920: ~20 k candidates on
+    level 0, past every form's registers; FHD at 256 threads), bit-exact."""
+    monkeypatch.setenv("ORBX_QT_NT", nt)
     img = _clustered(w, h, 43, kind) if kind else synth.frame(w, h, 44)
     ex = ORBextractor(nfeat, 1.2, 8, 20, 7)
     try:
