@@ -79,102 +79,131 @@ __global__ __launch_bounds__(kBT) void k_bow_match(const BowBufs *pa) {
     // the first 64 B features stay in registers
     int i2r = -1, fbr = 0, octr = 0;
     uint4 d0r = make_uint4(0, 0, 0, 0), d1r = d0r;
-    float xr = 0.f, yr = 0.f;
+    float xr = 0.f, yr = 0.f, angr = 0.f;
     if (lane < nbk) {
         i2r = a.B.node_features[b0 + lane];
         fbr = a.B.flags[i2r];
         const uint4 *dp = reinterpret_cast<const uint4 *>(a.B.desc + 32 * (int64_t)i2r);
         d0r = dp[0]; d1r = dp[1];
         const orbx_keypoint k = a.B.keys[i2r];
-        xr = k.x; yr = k.y; octr = k.octave;
+        xr = k.x; yr = k.y; octr = k.octave; angr = k.angle;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const float *F = a.tri;
-    for (int p = a0; p < a1; ++p) {
-        const int i1 = a.A.node_features[p];
-        const int fa = a.A.flags[i1];
-        if (!(fa & 1)) continue;
-        const uint4 *ap = reinterpret_cast<const uint4 *>(a.A.desc + 32 * (int64_t)i1);
-        const uint4 qa = ap[0], qb = ap[1];
-        const orbx_keypoint k1 = a.A.keys[i1];
-        const bool st1 = (fa >> 1) & 1;
-        uint32_t k_1 = kNone, k_2 = kNone;   // running (dist << 16 | position) smallest two
-        int x_1 = -1;                         // B feature of k_1
-        for (int c0 = 0; c0 < nbk; c0 += 64) {
-            const int pos = c0 + lane;
-            int i2 = -1, fb = 0, oct = 0;
-            uint4 e0, e1;
-            float x2 = 0.f, y2 = 0.f;
-            if (c0 == 0) {
-                i2 = i2r; fb = fbr; e0 = d0r; e1 = d1r; x2 = xr; y2 = yr; oct = octr;
-            } else if (pos < nbk) {
-                i2 = a.B.node_features[b0 + pos];
-                fb = a.B.flags[i2];
-                const uint4 *dp = reinterpret_cast<const uint4 *>(a.B.desc + 32 * (int64_t)i2);
-                e0 = dp[0]; e1 = dp[1];
-                const orbx_keypoint k = a.B.keys[i2];
-                x2 = k.x; y2 = k.y; oct = k.octave;
-            }
-            uint32_t key = kNone;
-            if (pos < nbk) {
-                const bool usable = a.variant == ORBX_BOW_KF_FRAME ? true : (fb & 1);
-                if (usable && !(tri ? false : mflag[pos])) {
-                    const int dist = hamming_rr(qa, qb, e0, e1);
-                    if (!tri) {
-                        key = ((uint32_t)dist << 16) | (uint32_t)pos;
-                    } else if (dist <= kThLow) {
-                        bool ok = true;
-                        const bool st2 = (fb >> 1) & 1;
-                        const bool lv = oct >= 0 && oct < a.nlevels;
-                        if (!st1 && !st2) {
-                            const float dx = __fsub_rn(a.ex, x2), dy = __fsub_rn(a.ey, y2);
-                            const float sc = lv ? F[11 + oct] : 0.0f;
-                            if (__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)) < __fmul_rn(100.0f, sc)) ok = false;
+    // A's features walked in order, 64 at a time: lane q holds feature
+    // a0 + q's index, flags, descriptor and keypoint (one round of loads for
+    // the run instead of a dependent chain per feature), read back by readlane
+    for (int pa = a0; pa < a1; pa += 64) {
+        const int np = min(64, a1 - pa);
+        int i1l = -1, fal = 0;
+        uint4 qal = make_uint4(0, 0, 0, 0), qbl = qal;
+        float x1l = 0.f, y1l = 0.f, an1l = 0.f;
+        if (lane < np) {
+            i1l = a.A.node_features[pa + lane];
+            fal = a.A.flags[i1l];
+            const uint4 *ap = reinterpret_cast<const uint4 *>(a.A.desc + 32 * (int64_t)i1l);
+            qal = ap[0]; qbl = ap[1];
+            const orbx_keypoint k = a.A.keys[i1l];
+            x1l = k.x; y1l = k.y; an1l = k.angle;
+        }
+        for (int q = 0; q < np; ++q) {
+            const int fa = __builtin_amdgcn_readlane(fal, q);
+            if (!(fa & 1)) continue;
+            const int i1 = __builtin_amdgcn_readlane(i1l, q);
+            const uint4 qa = make_uint4(__builtin_amdgcn_readlane(qal.x, q), __builtin_amdgcn_readlane(qal.y, q),
+                                        __builtin_amdgcn_readlane(qal.z, q), __builtin_amdgcn_readlane(qal.w, q));
+            const uint4 qb = make_uint4(__builtin_amdgcn_readlane(qbl.x, q), __builtin_amdgcn_readlane(qbl.y, q),
+                                        __builtin_amdgcn_readlane(qbl.z, q), __builtin_amdgcn_readlane(qbl.w, q));
+            const float k1x = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x1l), q));
+            const float k1y = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, y1l), q));
+            const bool st1 = (fa >> 1) & 1;
+            uint32_t k_1 = kNone, k_2 = kNone;   // running (dist << 16 | position) smallest two
+            int x_1 = -1, p_1 = -1;               // B feature of k_1 and its position in the node
+            for (int c0 = 0; c0 < nbk; c0 += 64) {
+                const int pos = c0 + lane;
+                int i2 = -1, fb = 0, oct = 0;
+                uint4 e0, e1;
+                float x2 = 0.f, y2 = 0.f;
+                if (c0 == 0) {
+                    i2 = i2r; fb = fbr; e0 = d0r; e1 = d1r; x2 = xr; y2 = yr; oct = octr;
+                } else if (pos < nbk) {
+                    i2 = a.B.node_features[b0 + pos];
+                    fb = a.B.flags[i2];
+                    const uint4 *dp = reinterpret_cast<const uint4 *>(a.B.desc + 32 * (int64_t)i2);
+                    e0 = dp[0]; e1 = dp[1];
+                    const orbx_keypoint k = a.B.keys[i2];
+                    x2 = k.x; y2 = k.y; oct = k.octave;
+                }
+                uint32_t key = kNone;
+                if (pos < nbk) {
+                    const bool usable = a.variant == ORBX_BOW_KF_FRAME ? true : (fb & 1);
+                    if (usable && !(tri ? false : mflag[pos])) {
+                        const int dist = hamming_rr(qa, qb, e0, e1);
+                        if (!tri) {
+                            key = ((uint32_t)dist << 16) | (uint32_t)pos;
+                        } else if (dist <= kThLow) {
+                            bool ok = true;
+                            const bool st2 = (fb >> 1) & 1;
+                            const bool lv = oct >= 0 && oct < a.nlevels;
+                            if (!st1 && !st2) {
+                                const float dx = __fsub_rn(a.ex, x2), dy = __fsub_rn(a.ey, y2);
+                                const float sc = lv ? F[11 + oct] : 0.0f;
+                                if (__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)) < __fmul_rn(100.0f, sc)) ok = false;
+                            }
+                            if (ok && epipolar_ok(k1x, k1y, x2, y2, F, lv ? F[11 + a.nlevels + oct] : 0.0f))
+                                key = ((uint32_t)dist << 16) | (uint32_t)(0xFFFF - pos);   // last minimum wins
                         }
-                        if (ok && epipolar_ok(k1.x, k1.y, x2, y2, F, lv ? F[11 + a.nlevels + oct] : 0.0f))
-                            key = ((uint32_t)dist << 16) | (uint32_t)(0xFFFF - pos);   // last minimum wins
                     }
                 }
+                const uint32_t m1 = wave_min_u32(key);
+                if (m1 == kNone) continue;
+                const int pm = tri ? (int)(0xFFFF - (m1 & 0xFFFF)) : (int)(m1 & 0xFFFF);
+                const int w1 = __builtin_amdgcn_readlane(i2, pm - c0);
+                if (tri) {
+                    if (m1 < k_1) { k_1 = m1; x_1 = w1; p_1 = pm; }
+                    continue;
+                }
+                const uint32_t m2 = wave_min_u32(lane == pm - c0 ? kNone : key);
+                if (m1 < k_1) {
+                    k_2 = m2 < k_1 ? m2 : k_1;
+                    k_1 = m1;
+                    x_1 = w1;
+                    p_1 = pm;
+                } else if (m1 < k_2) {
+                    k_2 = m1;
+                }
             }
-            const uint32_t m1 = wave_min_u32(key);
-            if (m1 == kNone) continue;
-            const int l1 = tri ? (int)(0xFFFF - (m1 & 0xFFFF)) - c0 : (int)(m1 & 0xFFFF) - c0;
-            const int w1 = __builtin_amdgcn_readlane(i2, l1);
-            if (tri) {
-                if (m1 < k_1) { k_1 = m1; x_1 = w1; }
-                continue;
+            if (k_1 == kNone) continue;
+            const int best1 = (int)(k_1 >> 16);
+            if (!tri) {
+                const int best2 = k_2 == kNone ? 256 : (int)(k_2 >> 16);
+                const bool pass = a.variant == ORBX_BOW_KF_FRAME ? best1 <= kThLow : best1 < kThLow;
+                if (!(pass && (float)best1 < __fmul_rn(a.nnratio, (float)best2))) continue;
+                if (lane == 0) mflag[k_1 & 0xFFFF] = 1;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
-            const uint32_t m2 = wave_min_u32(lane == l1 ? kNone : key);
-            if (m1 < k_1) {
-                k_2 = m2 < k_1 ? m2 : k_1;
-                k_1 = m1;
-                x_1 = w1;
-            } else if (m1 < k_2) {
-                k_2 = m1;
-            }
-        }
-        if (k_1 == kNone) continue;
-        const int best1 = (int)(k_1 >> 16);
-        if (!tri) {
-            const int best2 = k_2 == kNone ? 256 : (int)(k_2 >> 16);
-            const bool pass = a.variant == ORBX_BOW_KF_FRAME ? best1 <= kThLow : best1 < kThLow;
-            if (!(pass && (float)best1 < __fmul_rn(a.nnratio, (float)best2))) continue;
-            if (lane == 0) mflag[k_1 & 0xFFFF] = 1;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-        if (lane == 0) {
-            a.match_a[i1] = x_1;
-            if (!tri) a.match_b[x_1] = i1;
+            // the matched B feature's angle: from its lane's registers when it is
+            // one of the node's first 64 (wave-uniform position)
+            float an1 = 0.f, an2 = 0.f;
             if (a.check_ori) {
-                const int bin = rot_bin(k1.angle, a.B.keys[x_1].angle);
-                a.bin_a[i1] = (int8_t)bin;
-                atomicAdd(&a.hist[bin], 1);
+                an1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, an1l), q));
+                if (p_1 < 64) an2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, angr), p_1));
+                else an2 = a.B.keys[x_1].angle;
             }
-            atomicAdd(&a.counts[0], 1);
+            if (lane == 0) {
+                a.match_a[i1] = x_1;
+                if (!tri) a.match_b[x_1] = i1;
+                if (a.check_ori) {
+                    const int bin = rot_bin(an1, an2);
+                    a.bin_a[i1] = (int8_t)bin;
+                    atomicAdd(&a.hist[bin], 1);
+                }
+                atomicAdd(&a.counts[0], 1);
+            }
         }
     }
 }
@@ -182,14 +211,17 @@ __global__ __launch_bounds__(kBT) void k_bow_match(const BowBufs *pa) {
 // ComputeThreeMaxima + removal of the matches outside the three main bins.
 __global__ __launch_bounds__(1024) void k_bow_finish(const BowBufs *pa, HostTail tail) {   // one block per problem
     __shared__ int top[3];
+    __shared__ int hist[kHist];
     const BowBufs a = pa[blockIdx.x];
     __shared__ int removed;
     const int tid = threadIdx.x;
+    if (tid < kHist) hist[tid] = a.hist[tid];   // (one round of loads, not a serial chain on thread 0)
+    __syncthreads();
     if (tid == 0) {
         removed = 0;
         int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
         for (int i = 0; i < kHist; ++i) {
-            const int sz = a.hist[i];
+            const int sz = hist[i];
             if (sz > max1) { max3 = max2; max2 = max1; max1 = sz; ind3 = ind2; ind2 = ind1; ind1 = i; }
             else if (sz > max2) { max3 = max2; max2 = sz; ind3 = ind2; ind2 = i; }
             else if (sz > max3) { max3 = sz; ind3 = i; }

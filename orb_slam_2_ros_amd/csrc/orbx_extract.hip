@@ -1106,7 +1106,10 @@ struct QLds {
 // drop-in call, a sharded camera set), where a level's latency is the step's.
 template <int NT> struct QCfg;
 constexpr int kQPreRoots = 16;   // roots the global-key gather counts itself (more: the roots' own pass)
-template <> struct QCfg<256> { static constexpr int R1 = 6, R2 = kQuadRegKeys / 256, KR = kQuadRegKeys, MINB = 7; };
+#ifndef ORBX_QT_R2
+#define ORBX_QT_R2 (kQuadRegKeys / 256)
+#endif
+template <> struct QCfg<256> { static constexpr int R1 = 6, R2 = ORBX_QT_R2, KR = kQuadRegKeys, MINB = 7; };
 template <> struct QCfg<512> { static constexpr int R1 = 10, R2 = 2 * kQuadRegKeysW / 1024, KR = kQuadRegKeysW, MINB = 4; };
 template <> struct QCfg<1024> { static constexpr int R1 = 4, R2 = kQuadRegKeysW / 1024, KR = kQuadRegKeysW, MINB = 1; };
 // R == 0 (keys in global scratch): a pass walks the keys kQU per thread at a
