@@ -54,13 +54,9 @@ __device__ inline bool epipolar_ok(float x1, float y1, float x2, float y2, const
     return (double)dsqr < __dmul_rn(3.84, (double)sigma2);
 }
 
-// Grid (nodes of the largest side A / 4, problems).
-__global__ __launch_bounds__(kBT) void k_bow_match(const BowBufs *pa) {
-    __shared__ uint8_t matched[kBT / 64][kBowNodeCap];
-    const BowBufs a = pa[blockIdx.y];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int na_node = blockIdx.x * (kBT / 64) + wave;
-    if (na_node >= a.A.nnodes) return;
+// One wave: node na_node of side A against its node in side B.
+__device__ __attribute__((always_inline)) void bow_match_node(const BowBufs &a, int na_node, int lane,
+                                                              uint8_t *mflag) {
     // the node in side B
     const uint32_t id = a.A.node_ids[na_node];
     int lo = 0, hi = a.B.nnodes - 1, nb_node = -1;
@@ -74,7 +70,6 @@ __global__ __launch_bounds__(kBT) void k_bow_match(const BowBufs *pa) {
     const int a0 = a.A.node_offsets[na_node], a1 = a.A.node_offsets[na_node + 1];
     const int b0 = a.B.node_offsets[nb_node], nbk = a.B.node_offsets[nb_node + 1] - b0;
     const bool tri = a.variant == ORBX_BOW_TRIANGULATION;
-    uint8_t *mflag = matched[wave];
     for (int p = lane; p < nbk; p += 64) mflag[p] = 0;
     // the first 64 B features stay in registers
     int i2r = -1, fbr = 0, octr = 0;
@@ -208,11 +203,11 @@ __global__ __launch_bounds__(kBT) void k_bow_match(const BowBufs *pa) {
     }
 }
 
-// ComputeThreeMaxima + removal of the matches outside the three main bins.
-__global__ __launch_bounds__(1024) void k_bow_finish(const BowBufs *pa, HostTail tail) {   // one block per problem
+// ComputeThreeMaxima + removal of the matches outside the three main bins,
+// by one workgroup (any size); ends with a barrier.
+__device__ __attribute__((always_inline)) void bow_finish_problem(const BowBufs &a) {
     __shared__ int top[3];
     __shared__ int hist[kHist];
-    const BowBufs a = pa[blockIdx.x];
     __shared__ int removed;
     const int tid = threadIdx.x;
     if (tid < kHist) hist[tid] = a.hist[tid];   // (one round of loads, not a serial chain on thread 0)
@@ -246,18 +241,57 @@ __global__ __launch_bounds__(1024) void k_bow_finish(const BowBufs *pa, HostTail
     }
     __syncthreads();
     if (tid == 0) a.counts[1] = a.counts[0] - removed;
+    __syncthreads();
+}
+
+// Grid (nodes of the largest side A / 4, problems).  With a host tail (one
+// problem: the drop-in call) the last workgroup to finish also runs the
+// rotation pass and copies the outputs to the host, so the call is one launch.
+__global__ __launch_bounds__(kBT) void k_bow_match(const BowBufs *pa, HostTail tail) {
+    __shared__ uint8_t matched[kBT / 64][kBowNodeCap];
+    const BowBufs a = pa[blockIdx.y];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int na_node = blockIdx.x * (kBT / 64) + wave;
+    if (na_node < a.A.nnodes) bow_match_node(a, na_node, lane, matched[wave]);
+    if (!tail.flag) return;
+    __shared__ int s_last;
+    __threadfence();   // this workgroup's matches before its count
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(tail.done, 1u) == (uint32_t)(tail.blocks - 1);
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();   // (acquire: every workgroup's matches)
+    bow_finish_problem(pa[0]);
+    for (int i = threadIdx.x; i < tail.n16; i += blockDim.x) tail.dst[i] = tail.src[i];
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(tail.flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(1024) void k_bow_finish(const BowBufs *pa, HostTail tail) {   // one block per problem
+    bow_finish_problem(pa[blockIdx.x]);
     host_tail(tail);
 }
 
 }  // namespace
 
+int bow_tail_blocks(const BowBufs *h, int np) {
+    if (np != 1) return np;   // k_bow_finish, a workgroup per problem
+    return (h[0].A.nnodes + kBT / 64 - 1) / (kBT / 64);   // k_bow_match's workgroups
+}
+
 hipError_t launch_bow(const BowBufs *h, const BowBufs *d, int np, const HostTail &tail, hipStream_t st) {
     if (np <= 0) return hipSuccess;
-    if (tail.flag && tail.blocks != np) return hipErrorInvalidValue;
+    if (tail.flag && tail.blocks != bow_tail_blocks(h, np)) return hipErrorInvalidValue;
     int nodes = 0;
     for (int k = 0; k < np; ++k) nodes = std::max(nodes, h[k].A.nnodes);
-    if (nodes > 0)
-        hipLaunchKernelGGL(k_bow_match, dim3((nodes + kBT / 64 - 1) / (kBT / 64), np), dim3(kBT), 0, st, d);
+    const dim3 grid((nodes + kBT / 64 - 1) / (kBT / 64), np);
+    if (np == 1 && tail.flag && nodes > 0) {   // one launch: matching, rotation pass, outputs
+        hipLaunchKernelGGL(k_bow_match, grid, dim3(kBT), 0, st, d, tail);
+        return hipGetLastError();
+    }
+    if (tail.flag && np == 1) return hipErrorInvalidValue;   // (no nodes: nothing to elect a last workgroup)
+    if (nodes > 0) hipLaunchKernelGGL(k_bow_match, grid, dim3(kBT), 0, st, d, HostTail{});
     hipLaunchKernelGGL(k_bow_finish, dim3(np), dim3(1024), 0, st, d, tail);
     return hipGetLastError();
 }

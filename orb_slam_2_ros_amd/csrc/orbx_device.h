@@ -210,6 +210,7 @@ hipError_t launch_proj(const ProjBufs *h, const ProjBufs *d, int np, const HostT
 int proj_blocks(int nq);
 bool proj_fits(int n);   // the frame's grid fits the search kernel's LDS
 hipError_t launch_bow(const BowBufs *h, const BowBufs *d, int np, const HostTail &tail, hipStream_t s);
+int bow_tail_blocks(const BowBufs *h, int np);   // the workgroups the host tail of launch_bow counts
 
 // DBoW2 vocabulary in slot order: the children of a node occupy consecutive
 // slots (root = slot 0).  16 B per slot + 32-B descriptor + weight.

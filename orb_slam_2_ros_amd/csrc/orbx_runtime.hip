@@ -2005,7 +2005,7 @@ int bow_run(int device, int variant, orbx_bow_problem *P, int np, float nnratio,
     if (hipMemcpyAsync(D, ws.host, cnt_end, hipMemcpyHostToDevice, ws.st) != hipSuccess) return ORBX_EIO;
     const size_t o_out = o[0].ma;   // match arrays and counters are one contiguous run
     HostTail tail;
-    ws_tail(ws, o_out, cnt_end - o_out, at<uint32_t>(D, o_done), nl, tail);
+    ws_tail(ws, o_out, cnt_end - o_out, at<uint32_t>(D, o_done), bow_tail_blocks(hb.data(), nl), tail);
     if (launch_bow(hb.data(), at<BowBufs>(D, o_pa), nl, tail, ws.st) != hipSuccess) return ORBX_EIO;
     clk.mark();   // enqueue
     if (ws_wait(ws, tail, o_out, cnt_end - o_out)) return ORBX_EIO;
