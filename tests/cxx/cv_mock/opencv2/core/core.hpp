@@ -162,8 +162,16 @@ inline void copyMakeBorder(const Mat &src, Mat &dst, int top, int bottom, int le
     auto r101 = [](int p, int n) { while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - p - 2; return p; };
     std::vector<uint8_t> tmp((size_t)src.rows * src.cols);
     for (int y = 0; y < src.rows; ++y) std::memcpy(&tmp[(size_t)y * src.cols], src.data + y * src.step, src.cols);
-    for (int y = -top; y < src.rows + bottom; ++y)
-        for (int x = -left; x < src.cols + right; ++x)
-            dst.data[(y + top) * dst.step + (x + left)] = tmp[(size_t)r101(y, src.rows) * src.cols + r101(x, src.cols)];
+    // row by row: the interior as one copy, the side borders by reflection
+    std::vector<int> lx(left), rx(right);
+    for (int x = 0; x < left; ++x) lx[x] = r101(x - left, src.cols);
+    for (int x = 0; x < right; ++x) rx[x] = r101(src.cols + x, src.cols);
+    for (int y = -top; y < src.rows + bottom; ++y) {
+        const uint8_t *s = &tmp[(size_t)r101(y, src.rows) * src.cols];
+        uint8_t *d = dst.data + (size_t)(y + top) * dst.step;
+        for (int x = 0; x < left; ++x) d[x] = s[lx[x]];
+        std::memcpy(d + left, s, src.cols);
+        for (int x = 0; x < right; ++x) d[left + src.cols + x] = s[rx[x]];
+    }
 }
 }  // namespace cv
