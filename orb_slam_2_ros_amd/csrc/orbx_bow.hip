@@ -261,7 +261,7 @@ __global__ __launch_bounds__(kBT) void k_bow_match(const BowBufs *pa, HostTail t
     __syncthreads();
     if (!s_last) return;
     __threadfence();   // (acquire: every workgroup's matches)
-    bow_finish_problem(pa[0]);
+    bow_finish_problem(a);
     for (int i = threadIdx.x; i < tail.n16; i += blockDim.x) tail.dst[i] = tail.src[i];
     __threadfence_system();
     __syncthreads();
@@ -269,7 +269,8 @@ __global__ __launch_bounds__(kBT) void k_bow_match(const BowBufs *pa, HostTail t
 }
 
 __global__ __launch_bounds__(1024) void k_bow_finish(const BowBufs *pa, HostTail tail) {   // one block per problem
-    bow_finish_problem(pa[blockIdx.x]);
+    const BowBufs a = pa[blockIdx.x];
+    bow_finish_problem(a);
     host_tail(tail);
 }
 

@@ -207,6 +207,7 @@ hipError_t launch_rgbd(const orbx_keypoint *kps, const orbx_keypoint *kun, const
                        float *depth, int64_t ostride, int32_t *nkept, int B, hipStream_t s);
 // A batch of independent problems: h on the host, d the same array on the device.
 hipError_t launch_proj(const ProjBufs *h, const ProjBufs *d, int np, const HostTail &tail, hipStream_t s);
+int proj_tail_blocks(const ProjBufs *h, int np);   // the workgroups the host tail of launch_proj counts
 int proj_blocks(int nq);
 bool proj_fits(int n);   // the frame's grid fits the search kernel's LDS
 hipError_t launch_bow(const BowBufs *h, const BowBufs *d, int np, const HostTail &tail, hipStream_t s);

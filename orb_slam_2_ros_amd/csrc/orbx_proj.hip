@@ -99,8 +99,7 @@ __device__ inline int block_scan(int v, int *total, int *ws) {
 }
 
 // Grid (max nblk, problems): problem blockIdx.y, its first a.nblk blocks.
-__global__ __launch_bounds__(kPT) void k_proj_search(const ProjBufs *pa) {
-    extern __shared__ __align__(16) uint8_t lds[];
+__device__ __attribute__((always_inline)) void proj_search(const ProjBufs *pa, uint8_t *lds) {
     const ProjBufs a = pa[blockIdx.y];
     if ((int)blockIdx.x >= a.nblk) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -335,6 +334,11 @@ __global__ __launch_bounds__(kPT) void k_proj_search(const ProjBufs *pa) {
     }
 }
 
+__global__ __launch_bounds__(kPT) void k_proj_search(const ProjBufs *pa) {
+    extern __shared__ __align__(16) uint8_t lds[];
+    proj_search(pa, lds);
+}
+
 __device__ inline bool taken_static(int st, bool occ_obs) { return occ_obs ? st == 3 : (st & 1); }
 
 constexpr int kFQ = 512;   // full-list queries a round hands to the waves
@@ -419,9 +423,7 @@ __device__ inline bool accept(const ProjBufs &a, bool ratio, int q, const uint32
 // rounds stop when none progresses; what is left (contention chains through
 // `hard` claims) is replayed by wave 0 in query order.
 template <bool QL>   // per-query data in LDS (else global; one instantiation each keeps ds_* loads ds_*)
-__global__ __launch_bounds__(kPT) void k_proj_replay(const ProjBufs *pa, HostTail tail) {   // one block per problem
-    extern __shared__ __align__(16) uint8_t lds[];
-    const ProjBufs a = pa[blockIdx.x];
+__device__ __attribute__((always_inline)) void proj_replay(const ProjBufs &a, uint8_t *lds) {
     const uint64_t c0 = wall_clock64();
     const int n = a.n, nq = a.nq;
     const int V = a.variant;
@@ -679,7 +681,37 @@ __global__ __launch_bounds__(kPT) void k_proj_replay(const ProjBufs *pa, HostTai
     } else if (tid == 0) {
         *a.nmatches = sh_acc - sh_removed;
     }
+    __syncthreads();
+}
+
+template <bool QL>
+__global__ __launch_bounds__(kPT) void k_proj_replay(const ProjBufs *pa, HostTail tail) {   // one block per problem
+    extern __shared__ __align__(16) uint8_t lds[];
+    const ProjBufs a = pa[blockIdx.x];   // (a copy: the fields in registers)
+    proj_replay<QL>(a, lds);
     host_tail(tail);
+}
+
+// The single-problem host call in one launch: the search, then its last
+// workgroup to finish runs the replay and copies the outputs to the host
+// (dynamic LDS: the larger of the two layouts).
+template <bool QL>
+__global__ __launch_bounds__(kPT) void k_proj_search_replay(const ProjBufs *pa, HostTail tail) {
+    extern __shared__ __align__(16) uint8_t lds[];
+    proj_search(pa, lds);
+    __shared__ int s_last;
+    __threadfence();   // this workgroup's lists and entries before its count
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(tail.done, 1u) == (uint32_t)(tail.blocks - 1);
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();   // (acquire: every workgroup's results)
+    const ProjBufs a = pa[0];
+    proj_replay<QL>(a, lds);
+    for (int i = threadIdx.x; i < tail.n16; i += blockDim.x) tail.dst[i] = tail.src[i];
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(tail.flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace
@@ -699,10 +731,12 @@ bool proj_fits(int n) { return n <= kKPer * kPT && proj_lds_bytes(n) <= kProjLds
 
 int proj_blocks(int nq) { return std::max(1, std::min(512, (nq + kPW - 1) / kPW)); }
 
+int proj_tail_blocks(const ProjBufs *h, int np) { return np == 1 ? h[0].nblk : np; }
+
 // h: the problems' buffers on the host, d: the same array in device memory.
 hipError_t launch_proj(const ProjBufs *h, const ProjBufs *d, int np, const HostTail &tail, hipStream_t st) {
     if (np <= 0) return hipSuccess;
-    if (tail.flag && tail.blocks != np) return hipErrorInvalidValue;
+    if (tail.flag && tail.blocks != proj_tail_blocks(h, np)) return hipErrorInvalidValue;
     int bytes = 0, nblk = 1;
     bool q_in_lds = true;
     for (int k = 0; k < np; ++k) {
@@ -711,15 +745,27 @@ hipError_t launch_proj(const ProjBufs *h, const ProjBufs *d, int np, const HostT
         q_in_lds = q_in_lds && proj_replay_lds_bytes(h[k].n, h[k].nq, true) <= kProjLdsMax;
     }
     if (bytes > kProjLdsMax) return hipErrorInvalidValue;
+    int rbytes = 0;
+    for (int k = 0; k < np; ++k) rbytes = std::max(rbytes, proj_replay_lds_bytes(h[k].n, h[k].nq, q_in_lds));
+    if (rbytes > kProjLdsMax) return hipErrorInvalidValue;
+    if (np == 1 && tail.flag) {   // the host call: one launch
+        const int fb = std::max(bytes, rbytes);
+        const void *fk = q_in_lds ? reinterpret_cast<const void *>(k_proj_search_replay<true>)
+                                  : reinterpret_cast<const void *>(k_proj_search_replay<false>);
+        if (fb > 64 * 1024 && hipFuncSetAttribute(fk, hipFuncAttributeMaxDynamicSharedMemorySize, fb) != hipSuccess)
+            return hipErrorInvalidValue;
+        if (q_in_lds)
+            hipLaunchKernelGGL(k_proj_search_replay<true>, dim3(nblk, 1), dim3(kPT), fb, st, d, tail);
+        else
+            hipLaunchKernelGGL(k_proj_search_replay<false>, dim3(nblk, 1), dim3(kPT), fb, st, d, tail);
+        return hipGetLastError();
+    }
     if (bytes > 64 * 1024 &&
         hipFuncSetAttribute(reinterpret_cast<const void *>(k_proj_search), hipFuncAttributeMaxDynamicSharedMemorySize,
                             bytes) != hipSuccess)
         return hipErrorInvalidValue;
     // each problem's queries spread over up to 512 blocks, one query per wave
     hipLaunchKernelGGL(k_proj_search, dim3(nblk, np), dim3(kPT), bytes, st, d);
-    int rbytes = 0;
-    for (int k = 0; k < np; ++k) rbytes = std::max(rbytes, proj_replay_lds_bytes(h[k].n, h[k].nq, q_in_lds));
-    if (rbytes > kProjLdsMax) return hipErrorInvalidValue;
     const void *rk = q_in_lds ? reinterpret_cast<const void *>(k_proj_replay<true>)
                               : reinterpret_cast<const void *>(k_proj_replay<false>);
     if (rbytes > 64 * 1024 && hipFuncSetAttribute(rk, hipFuncAttributeMaxDynamicSharedMemorySize, rbytes) != hipSuccess)

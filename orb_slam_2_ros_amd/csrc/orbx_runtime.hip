@@ -1819,7 +1819,8 @@ int proj_run(int device, int variant, orbx_proj_problem *P, int np, int th_dist,
         std::memset(ws.host + o_cnt, 0, 16 + 8 * (size_t)nl);
         if (hipMemcpyAsync(D, ws.host, in_bytes, hipMemcpyHostToDevice, ws.st) != hipSuccess) return ORBX_EIO;
         HostTail tail;
-        ws_tail(ws, o_cnt, out_end - o_cnt, at<uint32_t>(D, o_cnt + 8 + 8 * (size_t)nl), nl, tail);
+        ws_tail(ws, o_cnt, out_end - o_cnt, at<uint32_t>(D, o_cnt + 8 + 8 * (size_t)nl), proj_tail_blocks(hb.data(), nl),
+                tail);
         if (launch_proj(hb.data(), at<ProjBufs>(D, o_pa), nl, tail, ws.st) != hipSuccess) return ORBX_EIO;
         if (ws_wait(ws, tail, o_cnt, out_end - o_cnt)) return ORBX_EIO;
         unsigned long long used = 0;
