@@ -25,6 +25,8 @@
 // queries finish in the parallel phase.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <climits>
 
@@ -731,7 +733,16 @@ bool proj_fits(int n) { return n <= kKPer * kPT && proj_lds_bytes(n) <= kProjLds
 
 int proj_blocks(int nq) { return std::max(1, std::min(512, (nq + kPW - 1) / kPW)); }
 
-int proj_tail_blocks(const ProjBufs *h, int np) { return np == 1 ? h[0].nblk : np; }
+// The one-launch form of the single host call (k_proj_search_replay) measured
+// slower than the two launches (SearchByProjection localmap 0.115 -> 0.148 ms:
+// the search then runs with the replay's LDS and registers): off unless
+// ORBX_PROJ_ONE_LAUNCH=1.
+bool proj_one_launch() {
+    const char *e = std::getenv("ORBX_PROJ_ONE_LAUNCH");
+    return e && e[0] == '1';
+}
+
+int proj_tail_blocks(const ProjBufs *h, int np) { return np == 1 && proj_one_launch() ? h[0].nblk : np; }
 
 // h: the problems' buffers on the host, d: the same array in device memory.
 hipError_t launch_proj(const ProjBufs *h, const ProjBufs *d, int np, const HostTail &tail, hipStream_t st) {
@@ -748,7 +759,7 @@ hipError_t launch_proj(const ProjBufs *h, const ProjBufs *d, int np, const HostT
     int rbytes = 0;
     for (int k = 0; k < np; ++k) rbytes = std::max(rbytes, proj_replay_lds_bytes(h[k].n, h[k].nq, q_in_lds));
     if (rbytes > kProjLdsMax) return hipErrorInvalidValue;
-    if (np == 1 && tail.flag) {   // the host call: one launch
+    if (np == 1 && tail.flag && proj_one_launch()) {   // the host call: one launch
         const int fb = std::max(bytes, rbytes);
         const void *fk = q_in_lds ? reinterpret_cast<const void *>(k_proj_search_replay<true>)
                                   : reinterpret_cast<const void *>(k_proj_search_replay<false>);

@@ -230,20 +230,49 @@ __global__ __launch_bounds__(kST) void k_stereo_band(StereoBufs a) {
         q[0] = q0.x; q[1] = q0.y; q[2] = q0.z; q[3] = q0.w;
         q[4] = q1.x; q[5] = q1.y; q[6] = q1.z; q[7] = q1.w;
     }
-    int best = 100, bidx = 0;   // TH_HIGH
-    for (int m = max(0, v - span); m <= v; ++m) {
-        const int e = rend[m];
-        for (int pos = m ? rend[m - 1] : 0; pos < e; ++pos) {
-            if (smaxr[pos] < v) continue;
-            const int o = soct[pos];
-            if (o < levelL - 1 || o > levelL + 1) continue;
-            const float uR = sx[pos];
-            if (!(uR >= minU && uR <= maxU)) continue;
-            const int iR = sidx[pos];
-            const int dist = hamming(q, dr + 32 * (int64_t)iR);
-            if (dist < best || (dist == best && iR < bidx)) { best = dist; bidx = iR; }
+    // the bands starting in rows [v - span, v] are one contiguous range of the
+    // sort; four positions at a time, their descriptor loads issued together
+    // (the (distance, index) minimum does not depend on the visiting order)
+    const int m0 = max(0, v - span);
+    const int p0 = m0 ? rend[m0 - 1] : 0, p1 = rend[v];
+    uint32_t bk = 100u << 16;   // (distance << 16) | index; TH_HIGH, index 0
+    for (int pos = p0; pos < p1; pos += 4) {
+        bool ok[4];
+        int iR[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int pj = pos + j;
+            ok[j] = false;
+            iR[j] = 0;
+            if (pj < p1 && smaxr[pj] >= v) {
+                const int o = soct[pj];
+                const float uR = sx[pj];
+                if (o >= levelL - 1 && o <= levelL + 1 && uR >= minU && uR <= maxU) {
+                    ok[j] = true;
+                    iR[j] = sidx[pj];
+                }
+            }
+        }
+        uint4 e0[4], e1[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (ok[j]) {
+                const uint4 *dp = reinterpret_cast<const uint4 *>(dr + 32 * (int64_t)iR[j]);
+                e0[j] = dp[0];
+                e1[j] = dp[1];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (ok[j]) {
+                const int dist = __popc(q[0] ^ e0[j].x) + __popc(q[1] ^ e0[j].y) + __popc(q[2] ^ e0[j].z) +
+                                 __popc(q[3] ^ e0[j].w) + __popc(q[4] ^ e1[j].x) + __popc(q[5] ^ e1[j].y) +
+                                 __popc(q[6] ^ e1[j].z) + __popc(q[7] ^ e1[j].w);
+                bk = min(bk, ((uint32_t)dist << 16) | (uint32_t)iR[j]);
+            }
         }
     }
+    const int best = (int)(bk >> 16), bidx = (int)(bk & 0xFFFF);
     if (best >= kThOrbDist) return;
 
     // 3. SAD over 11 offsets (Frame.cc:587-629).  Windows the reference's
