@@ -1113,7 +1113,10 @@ constexpr int kQPreRoots = 16;   // roots the global-key gather counts itself (m
 #define ORBX_QT_MINB 7
 #endif
 template <> struct QCfg<256> { static constexpr int R1 = 6, R2 = ORBX_QT_R2, KR = kQuadRegKeys, MINB = ORBX_QT_MINB; };
-template <> struct QCfg<512> { static constexpr int R1 = 10, R2 = 2 * kQuadRegKeysW / 1024, KR = kQuadRegKeysW, MINB = 4; };
+#ifndef ORBX_QT_R2_512
+#define ORBX_QT_R2_512 (2 * kQuadRegKeysW / 1024)
+#endif
+template <> struct QCfg<512> { static constexpr int R1 = 10, R2 = ORBX_QT_R2_512, KR = kQuadRegKeysW, MINB = 4; };
 template <> struct QCfg<1024> { static constexpr int R1 = 4, R2 = kQuadRegKeysW / 1024, KR = kQuadRegKeysW, MINB = 1; };
 // R == 0 (keys in global scratch): a pass walks the keys kQU per thread at a
 // time, the chunk's loads issued together into a register cache (key k =

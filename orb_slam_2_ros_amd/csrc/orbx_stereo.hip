@@ -183,6 +183,11 @@ __device__ int band_sort(const StereoBufs &a, int b, const Bands &d, int *ws, in
     return *s_span;
 }
 
+#ifndef ORBX_STEREO_WALK
+#define ORBX_STEREO_WALK 4
+#endif
+constexpr int kWalk = ORBX_STEREO_WALK;   // band positions per batch of descriptor loads
+
 __global__ __launch_bounds__(kST) void k_stereo_band(StereoBufs a) {
     extern __shared__ __align__(16) uint8_t lds[];
     __shared__ int ws[4];
@@ -231,16 +236,16 @@ __global__ __launch_bounds__(kST) void k_stereo_band(StereoBufs a) {
         q[4] = q1.x; q[5] = q1.y; q[6] = q1.z; q[7] = q1.w;
     }
     // the bands starting in rows [v - span, v] are one contiguous range of the
-    // sort; four positions at a time, their descriptor loads issued together
+    // sort; kWalk positions at a time, their descriptor loads issued together
     // (the (distance, index) minimum does not depend on the visiting order)
     const int m0 = max(0, v - span);
     const int p0 = m0 ? rend[m0 - 1] : 0, p1 = rend[v];
     uint32_t bk = 100u << 16;   // (distance << 16) | index; TH_HIGH, index 0
-    for (int pos = p0; pos < p1; pos += 4) {
-        bool ok[4];
-        int iR[4];
+    for (int pos = p0; pos < p1; pos += kWalk) {
+        bool ok[kWalk];
+        int iR[kWalk];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < kWalk; ++j) {
             const int pj = pos + j;
             ok[j] = false;
             iR[j] = 0;
@@ -253,9 +258,9 @@ __global__ __launch_bounds__(kST) void k_stereo_band(StereoBufs a) {
                 }
             }
         }
-        uint4 e0[4], e1[4];
+        uint4 e0[kWalk], e1[kWalk];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < kWalk; ++j) {
             if (ok[j]) {
                 const uint4 *dp = reinterpret_cast<const uint4 *>(dr + 32 * (int64_t)iR[j]);
                 e0[j] = dp[0];
@@ -263,7 +268,7 @@ __global__ __launch_bounds__(kST) void k_stereo_band(StereoBufs a) {
             }
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < kWalk; ++j) {
             if (ok[j]) {
                 const int dist = __popc(q[0] ^ e0[j].x) + __popc(q[1] ^ e0[j].y) + __popc(q[2] ^ e0[j].z) +
                                  __popc(q[3] ^ e0[j].w) + __popc(q[4] ^ e1[j].x) + __popc(q[5] ^ e1[j].y) +
