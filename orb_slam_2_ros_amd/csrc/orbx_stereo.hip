@@ -188,6 +188,9 @@ __device__ int band_sort(const StereoBufs &a, int b, const Bands &d, int *ws, in
 #endif
 constexpr int kWalk = ORBX_STEREO_WALK;   // band positions per batch of descriptor loads
 
+// SCR: the pair's bands sorted once by k_band_sort into its scratch (read
+// from L2), instead of every block sorting them into its LDS.
+template <bool SCR>
 __global__ __launch_bounds__(kST) void k_stereo_band(StereoBufs a) {
     extern __shared__ __align__(16) uint8_t lds[];
     __shared__ int ws[4];
@@ -203,8 +206,16 @@ __global__ __launch_bounds__(kST) void k_stereo_band(StereoBufs a) {
     const uint8_t *dr = a.dr + (int64_t)b * a.kstride * 32;
     // 1. vRowIndices (Frame.cc:517-529): right keypoint iR lies in rows
     //    [floor(y - r), ceil(y + r)], r = 2 * scale[octave].
-    const Bands bd = bands_in(lds, a);
-    const int span = band_sort(a, b, bd, ws, &s_span);
+    Bands bd;
+    int span;
+    if constexpr (SCR) {
+        uint8_t *scr = a.bands + (int64_t)b * a.band_stride;
+        bd = bands_in(scr, a);
+        span = reinterpret_cast<const int *>(scr + band_bytes(a.rows, a.nr_cap))[0];
+    } else {
+        bd = bands_in(lds, a);
+        span = band_sort(a, b, bd, ws, &s_span);
+    }
     const int *rend = bd.rend;
     const float *sx = bd.sx;
     const int16_t *smaxr = bd.smaxr;
@@ -651,20 +662,27 @@ hipError_t launch_stereo(const StereoBufs &a, int pairs, int nl_cap, hipStream_t
                                 bytes) != hipSuccess)
             return hipErrorInvalidValue;
         hipLaunchKernelGGL(k_band_sort, dim3(pairs), dim3(kST), bytes, st, a);
-        hipLaunchKernelGGL(k_stereo_band_gs, dim3((nl_cap + kST / kG - 1) / (kST / kG), pairs), dim3(kST), 0, st, a);
+        static const bool grouped_scr = [] {
+            const char *e = std::getenv("ORBX_STEREO_SORT_ONCE");
+            return e && e[0] == '1' && e[1] == 'g';   // "1g": the 16-lane search over the scratch
+        }();
+        if (grouped_scr)
+            hipLaunchKernelGGL(k_stereo_band_gs, dim3((nl_cap + kST / kG - 1) / (kST / kG), pairs), dim3(kST), 0, st, a);
+        else
+            hipLaunchKernelGGL(k_stereo_band<true>, dim3((nl_cap + kST - 1) / kST, pairs), dim3(kST), 0, st, a);
         hipLaunchKernelGGL(k_stereo_cut, dim3(pairs), dim3(kST), 0, st, a);
         return hipGetLastError();
     }
     // a lane per keypoint while that fills the chip, else a group of kG lanes
     const bool grouped = (int64_t)pairs * ((nl_cap + kST - 1) / kST) < 256;
     const void *fn = grouped ? reinterpret_cast<const void *>(k_stereo_band_g)
-                             : reinterpret_cast<const void *>(k_stereo_band);
+                             : reinterpret_cast<const void *>(k_stereo_band<false>);
     if (bytes > 64 * 1024 && hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess)
         return hipErrorInvalidValue;
     if (grouped)
         hipLaunchKernelGGL(k_stereo_band_g, dim3((nl_cap + kST / kG - 1) / (kST / kG), pairs), dim3(kST), bytes, st, a);
     else
-        hipLaunchKernelGGL(k_stereo_band, dim3((nl_cap + kST - 1) / kST, pairs), dim3(kST), bytes, st, a);
+        hipLaunchKernelGGL(k_stereo_band<false>, dim3((nl_cap + kST - 1) / kST, pairs), dim3(kST), bytes, st, a);
     hipLaunchKernelGGL(k_stereo_cut, dim3(pairs), dim3(kST), 0, st, a);
     return hipGetLastError();
 }
