@@ -1104,6 +1104,10 @@ struct QLds {
 // (R2) paths, the key -> source map's capacity (KR) and workgroups per CU.
 // NT = 1024 serves launches too small to fill the chip (a few frames: the
 // drop-in call, a sharded camera set), where a level's latency is the step's.
+#ifndef ORBX_QT_R4A
+#define ORBX_QT_R4A 0
+#endif
+constexpr bool kQtRoundsR4 = ORBX_QT_R4A;   // (A/B: round 3's round structure on the 256-thread register path)
 template <int NT> struct QCfg;
 constexpr int kQPreRoots = 16;   // roots the global-key gather counts itself (more: the roots' own pass)
 #ifndef ORBX_QT_R2
@@ -1483,217 +1487,416 @@ __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p,
     PHASE_MARK(2, 1);   // roots
 
     if (p.dbg_stop == 2) return;
-    // Each round is one key pass: the pass that moves the keys into their
-    // new nodes also adds them to those nodes' child counts (advance_stats),
-    // and the child counts are re-zeroed in the round's node phase (each
-    // thread its own nodes' entries after it read them, plus [4 S, 4 S2)), so
-    // the rounds need no pass of their own for either.  The last round's move
-    // only matters to the register path's output (phase 5).
-    bool final_phase = false;
-    int S = sh_S;
-    if (pre_cnt) advance_stats(s, K);
-    else child_stats(s, K);
-    PHASE_MARK(2, 2);   // child counts
-    // ---- 3. full rounds (ORBextractor.cc:618-696)
-    while (true) {
-        // per node: (non-empty children | single-key parents << 21 | children
-        // with more than one key << 42), scanned over a contiguous node range
-        // per thread, so each thread reads back only its own entries
-        const int per = (S + NT - 1) / NT;
-        const int i0 = min(tid * per, S), i1 = min(i0 + per, S);
-        uint64_t local = 0;
-        for (int i = i0; i < i1; ++i) {
-            uint64_t v = 1ull << 21;
-            if (s.cur[i].count > 1) {
-                uint64_t nc = 0, ex = 0;
-                for (int q = 0; q < 4; ++q) { nc += s.ccnt[4 * i + q] > 0; ex += s.ccnt[4 * i + q] > 1; }
-                v = nc | (ex << 42);
-            }
-            s.a64[i] = v;
-            local += v;
-        }
-        const uint64_t incl = wave_incl_scan_u64(local);
-        if ((tid & 63) == 63) ws64[tid >> 6] = incl;
-        __syncthreads();
-        uint64_t run = incl - local, tot = 0;
-        for (int w = 0; w < NT / 64; ++w) {
-            if (w < (tid >> 6)) run += ws64[w];
-            tot += ws64[w];
-        }
-        const int C = (int)(tot & 0x1FFFFF), singles = (int)((tot >> 21) & 0x1FFFFF);
-        const int nexp = (int)(tot >> 42);
-        const int S2 = C + singles;
-        if (S2 > NC) {  // cannot happen by the bound in make_plan; fail loudly
-            if (tid == 0) *level_count = -1;
-            return;
-        }
-        for (int i = i0; i < i1; ++i) {
-            const uint64_t pre = run;
-            run += s.a64[i];
-            const QNode nd = s.cur[i];
-            if (nd.count > 1) {
-                int pos = (int)(pre & 0x1FFFFF);
-                for (int q = 0; q < 4; ++q) {
-                    if (s.ccnt[4 * i + q] == 0) continue;
-                    const int ni = C - 1 - pos;
-                    s.nxt[ni] = make_child(s, nd, i, q, pos);
-                    s.nidx_c[4 * i + q] = (int16_t)ni;
-                    ++pos;
+    int S;
+    if constexpr (kQtRoundsR4 && NT == 256 && NR > 0) {
+        // the round structure of round 3 (a stats pass at the top of each round,
+        // the move and the counters' zeroing after the node phase): ORBX_QT_R4A
+        // ---- 3. full rounds (ORBextractor.cc:618-696)
+        bool final_phase = false;
+        while (true) {
+            const int S = sh_S;
+            child_stats(s, K);
+            PHASE_MARK(2, 2);   // full rounds: child counts
+            // per node: (non-empty children | single-key parents << 21 | children
+            // with more than one key << 42), scanned over a contiguous node range
+            // per thread, so each thread reads back only its own entries
+            const int per = (S + NT - 1) / NT;
+            const int i0 = min(tid * per, S), i1 = min(i0 + per, S);
+            uint64_t local = 0;
+            for (int i = i0; i < i1; ++i) {
+                uint64_t v = 1ull << 21;
+                if (s.cur[i].count > 1) {
+                    uint64_t nc = 0, ex = 0;
+                    for (int q = 0; q < 4; ++q) { nc += s.ccnt[4 * i + q] > 0; ex += s.ccnt[4 * i + q] > 1; }
+                    v = nc | (ex << 42);
                 }
-            } else {
-                const int ni = C + (int)((pre >> 21) & 0x1FFFFF);
-                s.nxt[ni] = nd;
-                set_all_quads(s.nidx_c, i, ni);
-            }
-        }
-        // (only this thread reads its nodes' child entries)
-        for (int i = 4 * i0; i < 4 * i1; ++i) { s.ccnt[i] = 0; s.cbest[i] = 0; }
-        for (int i = 4 * S + tid; i < 4 * S2; i += NT) { s.ccnt[i] = 0; s.cbest[i] = 0; }
-        __syncthreads();
-        {
-            QNode *t = s.cur; s.cur = s.nxt; s.nxt = t;
-        }
-        PHASE_MARK(2, 3);   // full rounds: scan + children
-        const bool stop = S2 >= N || S2 == S;
-        final_phase = !stop && S2 + nexp * 3 > N;
-        S = S2;
-        if (stop) {
-            if constexpr (NR > 0) K.each([&](int j, int k) { K.set_node(j, k, s.nidx_c[4 * K.node(j, k) + K.quad(j, k)]); });
-            break;
-        }
-        if (tid == 0) sh_nv = 0;   // (the final phase's count; ordered by the pass's barrier)
-        advance_stats(s, K);
-        PHASE_MARK(2, 2);   // full rounds: move + child counts
-        if (final_phase) break;
-    }
-
-    if (p.dbg_stop == 3) return;
-    // ---- 4. final phase (ORBextractor.cc:697-762); the child counts of the
-    //         S nodes are in place
-    while (final_phase) {
-        {
-            int nz = 0;
-            for (int i = tid; i < s.np2; i += NT) {
-                uint64_t v = 0;
-                if (i < S && s.cur[i].count > 1)
-                    v = ((uint64_t)s.cur[i].count << 40) | ((uint64_t)s.cur[i].seq << 16) | (uint64_t)i;
                 s.a64[i] = v;
-                s.b64[i] = 0;
-                nz += v != 0;
+                local += v;
             }
-            nz = wave_sum_i32(nz);
-            if ((tid & 63) == 0 && nz) atomicAdd(&sh_nv, nz);
+            const uint64_t incl = wave_incl_scan_u64(local);
+            if ((tid & 63) == 63) ws64[tid >> 6] = incl;
+            __syncthreads();
+            uint64_t run = incl - local, tot = 0;
+            for (int w = 0; w < NT / 64; ++w) {
+                if (w < (tid >> 6)) run += ws64[w];
+                tot += ws64[w];
+            }
+            const int C = (int)(tot & 0x1FFFFF), singles = (int)((tot >> 21) & 0x1FFFFF);
+            const int nexp = (int)(tot >> 42);
+            const int S2 = C + singles;
+            if (S2 > NC) {  // cannot happen by the bound in make_plan; fail loudly
+                if (tid == 0) *level_count = -1;
+                return;
+            }
+            for (int i = i0; i < i1; ++i) {
+                const uint64_t pre = run;
+                run += s.a64[i];
+                const QNode nd = s.cur[i];
+                if (nd.count > 1) {
+                    int pos = (int)(pre & 0x1FFFFF);
+                    for (int q = 0; q < 4; ++q) {
+                        if (s.ccnt[4 * i + q] == 0) continue;
+                        const int ni = C - 1 - pos;
+                        s.nxt[ni] = make_child(s, nd, i, q, pos);
+                        s.nidx_c[4 * i + q] = (int16_t)ni;
+                        ++pos;
+                    }
+                } else {
+                    const int ni = C + (int)((pre >> 21) & 0x1FFFFF);
+                    s.nxt[ni] = nd;
+                    set_all_quads(s.nidx_c, i, ni);
+                }
+            }
+            __syncthreads();
+            K.each([&](int j, int k) { K.set_node(j, k, s.nidx_c[4 * K.node(j, k) + K.quad(j, k)]); });
+            zero_children<NT>(s, S2);
+            {
+                QNode *t = s.cur; s.cur = s.nxt; s.nxt = t;
+            }
+            if (tid == 0) sh_S = S2;
+            __syncthreads();
+            PHASE_MARK(2, 3);   // full rounds: scan + children
+            if (S2 >= N || S2 == S) break;
+            if (S2 + nexp * 3 > N) { final_phase = true; break; }
         }
-        for (int i = tid; i < S; i += NT) s.mark[i] = 0;
-        __syncthreads();
-        PHASE_MARK(2, 4);   // final: node keys
-        // descending order of the splittable nodes' (count, seq, index) keys
-        // (all distinct) by rank counting: one barrier instead of a bitonic
-        // network's log^2 stages; zeros (unsplittable) stay behind, in b64
-        {
-            // eight entries per step, their four reads issued together (one LDS
-            // round trip per step instead of per pair); a64[S, np2) is 0 and np2
-            // a power of two >= 8
-            const int S8 = (S + 7) & ~7;
-            for (int i = tid; i < S; i += NT) {
-                const uint64_t v = s.a64[i];
-                if (v == 0) continue;
-                int r = 0;
-                for (int j = 0; j < S8; j += 8) {
-                    const ulonglong2 w0 = *reinterpret_cast<const ulonglong2 *>(s.a64 + j);
-                    const ulonglong2 w1 = *reinterpret_cast<const ulonglong2 *>(s.a64 + j + 2);
-                    const ulonglong2 w2 = *reinterpret_cast<const ulonglong2 *>(s.a64 + j + 4);
-                    const ulonglong2 w3 = *reinterpret_cast<const ulonglong2 *>(s.a64 + j + 6);
-                    r += (w0.x > v) + (w0.y > v) + (w1.x > v) + (w1.y > v) + (w2.x > v) + (w2.y > v) +
-                         (w3.x > v) + (w3.y > v);
+
+        if (p.dbg_stop == 3) return;
+        // ---- 4. final phase (ORBextractor.cc:697-762)
+        while (final_phase) {
+            const int S = sh_S;
+            if (tid == 0) sh_nv = 0;   // (ordered by child_stats' barrier)
+            child_stats(s, K);
+            {
+                int nz = 0;
+                for (int i = tid; i < s.np2; i += NT) {
+                    uint64_t v = 0;
+                    if (i < S && s.cur[i].count > 1)
+                        v = ((uint64_t)s.cur[i].count << 40) | ((uint64_t)s.cur[i].seq << 16) | (uint64_t)i;
+                    s.a64[i] = v;
+                    s.b64[i] = 0;
+                    nz += v != 0;
+                }
+                nz = wave_sum_i32(nz);
+                if ((tid & 63) == 0 && nz) atomicAdd(&sh_nv, nz);
+            }
+            for (int i = tid; i < S; i += NT) s.mark[i] = 0;
+            __syncthreads();
+            PHASE_MARK(2, 4);   // final: child counts
+            // descending order of the splittable nodes' (count, seq, index) keys
+            // (all distinct) by rank counting: one barrier instead of a bitonic
+            // network's log^2 stages; zeros (unsplittable) stay behind, in b64
+            {
+                // eight entries per step, their four reads issued together (one LDS
+                // round trip per step instead of per pair); a64[S, np2) is 0 and np2
+                // a power of two >= 8
+                const int S8 = (S + 7) & ~7;
+                for (int i = tid; i < S; i += NT) {
+                    const uint64_t v = s.a64[i];
+                    if (v == 0) continue;
+                    int r = 0;
+                    for (int j = 0; j < S8; j += 8) {
+                        const ulonglong2 w0 = *reinterpret_cast<const ulonglong2 *>(s.a64 + j);
+                        const ulonglong2 w1 = *reinterpret_cast<const ulonglong2 *>(s.a64 + j + 2);
+                        const ulonglong2 w2 = *reinterpret_cast<const ulonglong2 *>(s.a64 + j + 4);
+                        const ulonglong2 w3 = *reinterpret_cast<const ulonglong2 *>(s.a64 + j + 6);
+                        r += (w0.x > v) + (w0.y > v) + (w1.x > v) + (w1.y > v) + (w2.x > v) + (w2.y > v) +
+                             (w3.x > v) + (w3.y > v);
+                    }
+                    s.b64[r] = v;
+                }
+                __syncthreads();
+                uint64_t *t = s.a64; s.a64 = s.b64; s.b64 = t;
+            }
+            PHASE_MARK(2, 5);   // final: sort
+            // per rank: number of non-empty children (nc) and gain (nc - 1)
+            for (int r = tid; r < s.np2; r += NT) {
+                uint64_t v = 0;
+                if (s.a64[r] != 0) {
+                    const int i = (int)(s.a64[r] & 0xFFFF);
+                    int nc = 0;
+                    for (int q = 0; q < 4; ++q) nc += s.ccnt[4 * i + q] > 0;
+                    v = (uint64_t)nc | ((uint64_t)(nc - 1) << 32);
                 }
                 s.b64[r] = v;
             }
+            if (tid == 0) sh_R = -1;
             __syncthreads();
-            uint64_t *t = s.a64; s.a64 = s.b64; s.b64 = t;
-        }
-        PHASE_MARK(2, 5);   // final: sort
-        // per rank: number of non-empty children (nc) and gain (nc - 1)
-        for (int r = tid; r < s.np2; r += NT) {
-            uint64_t v = 0;
-            if (s.a64[r] != 0) {
+            const int nv = sh_nv;
+            block_excl_scan_u64<NT>(s.b64, s.np2, ws64);
+            for (int r = tid; r < nv; r += NT) {
                 const int i = (int)(s.a64[r] & 0xFFFF);
                 int nc = 0;
                 for (int q = 0; q < 4; ++q) nc += s.ccnt[4 * i + q] > 0;
-                v = (uint64_t)nc | ((uint64_t)(nc - 1) << 32);
+                const int incl = (int)(s.b64[r] >> 32) + nc - 1;
+                const int prev = (int)(s.b64[r] >> 32);
+                if (S + incl >= N && S + prev < N) sh_R = r + 1;
             }
-            s.b64[r] = v;
+            __syncthreads();
+            const int R = sh_R < 0 ? nv : sh_R;
+            int CC;
+            {
+                if (R > 0) {
+                    const int i = (int)(s.a64[R - 1] & 0xFFFF);
+                    int nc = 0;
+                    for (int q = 0; q < 4; ++q) nc += s.ccnt[4 * i + q] > 0;
+                    CC = (int)(s.b64[R - 1] & 0xFFFFFFFF) + nc;
+                } else {
+                    CC = 0;
+                }
+            }
+            const int S2 = CC + (S - R);
+            if (S2 > NC) {
+                if (tid == 0) *level_count = -1;
+                return;
+            }
+            for (int r = tid; r < R; r += NT) {
+                const int i = (int)(s.a64[r] & 0xFFFF);
+                int cs = (int)(s.b64[r] & 0xFFFFFFFF);
+                const QNode nd = s.cur[i];
+                for (int q = 0; q < 4; ++q) {
+                    if (s.ccnt[4 * i + q] == 0) continue;
+                    const int ni = CC - 1 - cs;
+                    s.nxt[ni] = make_child(s, nd, i, q, cs);
+                    s.nidx_c[4 * i + q] = (int16_t)ni;
+                    ++cs;
+                }
+                s.mark[i] = 1;
+            }
+            __syncthreads();
+            for (int i = tid; i < s.np2; i += NT) s.b64[i] = (i < S && !s.mark[i]) ? 1 : 0;
+            __syncthreads();
+            block_excl_scan_u64<NT>(s.b64, s.np2, ws64);
+            for (int i = tid; i < S; i += NT) {
+                if (s.mark[i]) continue;
+                const int ni = CC + (int)s.b64[i];
+                s.nxt[ni] = s.cur[i];
+                set_all_quads(s.nidx_c, i, ni);
+            }
+            __syncthreads();
+            K.each([&](int j, int k) { K.set_node(j, k, s.nidx_c[4 * K.node(j, k) + K.quad(j, k)]); });
+            zero_children<NT>(s, S2);
+            {
+                QNode *t = s.cur; s.cur = s.nxt; s.nxt = t;
+            }
+            if (tid == 0) sh_S = S2;
+            __syncthreads();
+            PHASE_MARK(2, 6);   // final: splits
+            if (S2 >= N || S2 == S) break;
         }
-        if (tid == 0) sh_R = -1;
-        __syncthreads();
-        const int nv = sh_nv;
-        block_excl_scan_u64<NT>(s.b64, s.np2, ws64);
-        for (int r = tid; r < nv; r += NT) {
-            const int i = (int)(s.a64[r] & 0xFFFF);
-            int nc = 0;
-            for (int q = 0; q < 4; ++q) nc += s.ccnt[4 * i + q] > 0;
-            const int incl = (int)(s.b64[r] >> 32) + nc - 1;
-            const int prev = (int)(s.b64[r] >> 32);
-            if (S + incl >= N && S + prev < N) sh_R = r + 1;
+        S = sh_S;
+    } else {
+        // Each round is one key pass: the pass that moves the keys into their
+        // new nodes also adds them to those nodes' child counts (advance_stats),
+        // and the child counts are re-zeroed in the round's node phase (each
+        // thread its own nodes' entries after it read them, plus [4 S, 4 S2)), so
+        // the rounds need no pass of their own for either.  The last round's move
+        // only matters to the register path's output (phase 5).
+        bool final_phase = false;
+        S = sh_S;
+        if (pre_cnt) advance_stats(s, K);
+        else child_stats(s, K);
+        PHASE_MARK(2, 2);   // child counts
+        // ---- 3. full rounds (ORBextractor.cc:618-696)
+        while (true) {
+            // per node: (non-empty children | single-key parents << 21 | children
+            // with more than one key << 42), scanned over a contiguous node range
+            // per thread, so each thread reads back only its own entries
+            const int per = (S + NT - 1) / NT;
+            const int i0 = min(tid * per, S), i1 = min(i0 + per, S);
+            uint64_t local = 0;
+            for (int i = i0; i < i1; ++i) {
+                uint64_t v = 1ull << 21;
+                if (s.cur[i].count > 1) {
+                    uint64_t nc = 0, ex = 0;
+                    for (int q = 0; q < 4; ++q) { nc += s.ccnt[4 * i + q] > 0; ex += s.ccnt[4 * i + q] > 1; }
+                    v = nc | (ex << 42);
+                }
+                s.a64[i] = v;
+                local += v;
+            }
+            const uint64_t incl = wave_incl_scan_u64(local);
+            if ((tid & 63) == 63) ws64[tid >> 6] = incl;
+            __syncthreads();
+            uint64_t run = incl - local, tot = 0;
+            for (int w = 0; w < NT / 64; ++w) {
+                if (w < (tid >> 6)) run += ws64[w];
+                tot += ws64[w];
+            }
+            const int C = (int)(tot & 0x1FFFFF), singles = (int)((tot >> 21) & 0x1FFFFF);
+            const int nexp = (int)(tot >> 42);
+            const int S2 = C + singles;
+            if (S2 > NC) {  // cannot happen by the bound in make_plan; fail loudly
+                if (tid == 0) *level_count = -1;
+                return;
+            }
+            for (int i = i0; i < i1; ++i) {
+                const uint64_t pre = run;
+                run += s.a64[i];
+                const QNode nd = s.cur[i];
+                if (nd.count > 1) {
+                    int pos = (int)(pre & 0x1FFFFF);
+                    for (int q = 0; q < 4; ++q) {
+                        if (s.ccnt[4 * i + q] == 0) continue;
+                        const int ni = C - 1 - pos;
+                        s.nxt[ni] = make_child(s, nd, i, q, pos);
+                        s.nidx_c[4 * i + q] = (int16_t)ni;
+                        ++pos;
+                    }
+                } else {
+                    const int ni = C + (int)((pre >> 21) & 0x1FFFFF);
+                    s.nxt[ni] = nd;
+                    set_all_quads(s.nidx_c, i, ni);
+                }
+            }
+            // (only this thread reads its nodes' child entries)
+            for (int i = 4 * i0; i < 4 * i1; ++i) { s.ccnt[i] = 0; s.cbest[i] = 0; }
+            for (int i = 4 * S + tid; i < 4 * S2; i += NT) { s.ccnt[i] = 0; s.cbest[i] = 0; }
+            __syncthreads();
+            {
+                QNode *t = s.cur; s.cur = s.nxt; s.nxt = t;
+            }
+            PHASE_MARK(2, 3);   // full rounds: scan + children
+            const bool stop = S2 >= N || S2 == S;
+            final_phase = !stop && S2 + nexp * 3 > N;
+            S = S2;
+            if (stop) {
+                if constexpr (NR > 0) K.each([&](int j, int k) { K.set_node(j, k, s.nidx_c[4 * K.node(j, k) + K.quad(j, k)]); });
+                break;
+            }
+            if (tid == 0) sh_nv = 0;   // (the final phase's count; ordered by the pass's barrier)
+            advance_stats(s, K);
+            PHASE_MARK(2, 2);   // full rounds: move + child counts
+            if (final_phase) break;
         }
-        __syncthreads();
-        const int R = sh_R < 0 ? nv : sh_R;
-        int CC;
-        {
-            if (R > 0) {
-                const int i = (int)(s.a64[R - 1] & 0xFFFF);
+
+        if (p.dbg_stop == 3) return;
+        // ---- 4. final phase (ORBextractor.cc:697-762); the child counts of the
+        //         S nodes are in place
+        while (final_phase) {
+            {
+                int nz = 0;
+                for (int i = tid; i < s.np2; i += NT) {
+                    uint64_t v = 0;
+                    if (i < S && s.cur[i].count > 1)
+                        v = ((uint64_t)s.cur[i].count << 40) | ((uint64_t)s.cur[i].seq << 16) | (uint64_t)i;
+                    s.a64[i] = v;
+                    s.b64[i] = 0;
+                    nz += v != 0;
+                }
+                nz = wave_sum_i32(nz);
+                if ((tid & 63) == 0 && nz) atomicAdd(&sh_nv, nz);
+            }
+            for (int i = tid; i < S; i += NT) s.mark[i] = 0;
+            __syncthreads();
+            PHASE_MARK(2, 4);   // final: node keys
+            // descending order of the splittable nodes' (count, seq, index) keys
+            // (all distinct) by rank counting: one barrier instead of a bitonic
+            // network's log^2 stages; zeros (unsplittable) stay behind, in b64
+            {
+                // eight entries per step, their four reads issued together (one LDS
+                // round trip per step instead of per pair); a64[S, np2) is 0 and np2
+                // a power of two >= 8
+                const int S8 = (S + 7) & ~7;
+                for (int i = tid; i < S; i += NT) {
+                    const uint64_t v = s.a64[i];
+                    if (v == 0) continue;
+                    int r = 0;
+                    for (int j = 0; j < S8; j += 8) {
+                        const ulonglong2 w0 = *reinterpret_cast<const ulonglong2 *>(s.a64 + j);
+                        const ulonglong2 w1 = *reinterpret_cast<const ulonglong2 *>(s.a64 + j + 2);
+                        const ulonglong2 w2 = *reinterpret_cast<const ulonglong2 *>(s.a64 + j + 4);
+                        const ulonglong2 w3 = *reinterpret_cast<const ulonglong2 *>(s.a64 + j + 6);
+                        r += (w0.x > v) + (w0.y > v) + (w1.x > v) + (w1.y > v) + (w2.x > v) + (w2.y > v) +
+                             (w3.x > v) + (w3.y > v);
+                    }
+                    s.b64[r] = v;
+                }
+                __syncthreads();
+                uint64_t *t = s.a64; s.a64 = s.b64; s.b64 = t;
+            }
+            PHASE_MARK(2, 5);   // final: sort
+            // per rank: number of non-empty children (nc) and gain (nc - 1)
+            for (int r = tid; r < s.np2; r += NT) {
+                uint64_t v = 0;
+                if (s.a64[r] != 0) {
+                    const int i = (int)(s.a64[r] & 0xFFFF);
+                    int nc = 0;
+                    for (int q = 0; q < 4; ++q) nc += s.ccnt[4 * i + q] > 0;
+                    v = (uint64_t)nc | ((uint64_t)(nc - 1) << 32);
+                }
+                s.b64[r] = v;
+            }
+            if (tid == 0) sh_R = -1;
+            __syncthreads();
+            const int nv = sh_nv;
+            block_excl_scan_u64<NT>(s.b64, s.np2, ws64);
+            for (int r = tid; r < nv; r += NT) {
+                const int i = (int)(s.a64[r] & 0xFFFF);
                 int nc = 0;
                 for (int q = 0; q < 4; ++q) nc += s.ccnt[4 * i + q] > 0;
-                CC = (int)(s.b64[R - 1] & 0xFFFFFFFF) + nc;
-            } else {
-                CC = 0;
+                const int incl = (int)(s.b64[r] >> 32) + nc - 1;
+                const int prev = (int)(s.b64[r] >> 32);
+                if (S + incl >= N && S + prev < N) sh_R = r + 1;
             }
-        }
-        const int S2 = CC + (S - R);
-        if (S2 > NC) {
-            if (tid == 0) *level_count = -1;
-            return;
-        }
-        for (int r = tid; r < R; r += NT) {
-            const int i = (int)(s.a64[r] & 0xFFFF);
-            int cs = (int)(s.b64[r] & 0xFFFFFFFF);
-            const QNode nd = s.cur[i];
-            for (int q = 0; q < 4; ++q) {
-                if (s.ccnt[4 * i + q] == 0) continue;
-                const int ni = CC - 1 - cs;
-                s.nxt[ni] = make_child(s, nd, i, q, cs);
-                s.nidx_c[4 * i + q] = (int16_t)ni;
-                ++cs;
+            __syncthreads();
+            const int R = sh_R < 0 ? nv : sh_R;
+            int CC;
+            {
+                if (R > 0) {
+                    const int i = (int)(s.a64[R - 1] & 0xFFFF);
+                    int nc = 0;
+                    for (int q = 0; q < 4; ++q) nc += s.ccnt[4 * i + q] > 0;
+                    CC = (int)(s.b64[R - 1] & 0xFFFFFFFF) + nc;
+                } else {
+                    CC = 0;
+                }
             }
-            s.mark[i] = 1;
+            const int S2 = CC + (S - R);
+            if (S2 > NC) {
+                if (tid == 0) *level_count = -1;
+                return;
+            }
+            for (int r = tid; r < R; r += NT) {
+                const int i = (int)(s.a64[r] & 0xFFFF);
+                int cs = (int)(s.b64[r] & 0xFFFFFFFF);
+                const QNode nd = s.cur[i];
+                for (int q = 0; q < 4; ++q) {
+                    if (s.ccnt[4 * i + q] == 0) continue;
+                    const int ni = CC - 1 - cs;
+                    s.nxt[ni] = make_child(s, nd, i, q, cs);
+                    s.nidx_c[4 * i + q] = (int16_t)ni;
+                    ++cs;
+                }
+                s.mark[i] = 1;
+            }
+            __syncthreads();
+            // (the child entries are read no more this round: re-zeroed for the
+            // next round's counts, S2 >= S)
+            for (int i = tid; i < s.np2; i += NT) s.b64[i] = (i < S && !s.mark[i]) ? 1 : 0;
+            zero_children<NT>(s, S2);
+            __syncthreads();
+            block_excl_scan_u64<NT>(s.b64, s.np2, ws64);
+            for (int i = tid; i < S; i += NT) {
+                if (s.mark[i]) continue;
+                const int ni = CC + (int)s.b64[i];
+                s.nxt[ni] = s.cur[i];
+                set_all_quads(s.nidx_c, i, ni);
+            }
+            __syncthreads();
+            {
+                QNode *t = s.cur; s.cur = s.nxt; s.nxt = t;
+            }
+            PHASE_MARK(2, 6);   // final: splits
+            const bool stop = S2 >= N || S2 == S;
+            S = S2;
+            if (stop) {
+                if constexpr (NR > 0) K.each([&](int j, int k) { K.set_node(j, k, s.nidx_c[4 * K.node(j, k) + K.quad(j, k)]); });
+                break;
+            }
+            if (tid == 0) sh_nv = 0;
+            advance_stats(s, K);
+            PHASE_MARK(2, 4);   // final: move + child counts
         }
-        __syncthreads();
-        // (the child entries are read no more this round: re-zeroed for the
-        // next round's counts, S2 >= S)
-        for (int i = tid; i < s.np2; i += NT) s.b64[i] = (i < S && !s.mark[i]) ? 1 : 0;
-        zero_children<NT>(s, S2);
-        __syncthreads();
-        block_excl_scan_u64<NT>(s.b64, s.np2, ws64);
-        for (int i = tid; i < S; i += NT) {
-            if (s.mark[i]) continue;
-            const int ni = CC + (int)s.b64[i];
-            s.nxt[ni] = s.cur[i];
-            set_all_quads(s.nidx_c, i, ni);
-        }
-        __syncthreads();
-        {
-            QNode *t = s.cur; s.cur = s.nxt; s.nxt = t;
-        }
-        PHASE_MARK(2, 6);   // final: splits
-        const bool stop = S2 >= N || S2 == S;
-        S = S2;
-        if (stop) {
-            if constexpr (NR > 0) K.each([&](int j, int k) { K.set_node(j, k, s.nidx_c[4 * K.node(j, k) + K.quad(j, k)]); });
-            break;
-        }
-        if (tid == 0) sh_nv = 0;
-        advance_stats(s, K);
-        PHASE_MARK(2, 4);   // final: move + child counts
     }
 
     // ---- 5. best key per node, in list order (ORBextractor.cc:765-784)
