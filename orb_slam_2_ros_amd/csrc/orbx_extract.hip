@@ -1105,7 +1105,7 @@ struct QLds {
 // NT = 1024 serves launches too small to fill the chip (a few frames: the
 // drop-in call, a sharded camera set), where a level's latency is the step's.
 #ifndef ORBX_QT_R4A
-#define ORBX_QT_R4A 0
+#define ORBX_QT_R4A 1   // (0.403 -> 0.395 ms per 3072 VGA frames, profiles/r04_ab_qt_rounds_vga.txt)
 #endif
 constexpr bool kQtRoundsR4 = ORBX_QT_R4A;   // (A/B: round 3's round structure on the 256-thread register path)
 template <int NT> struct QCfg;
