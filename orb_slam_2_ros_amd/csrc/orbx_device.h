@@ -138,6 +138,7 @@ struct StereoBufs {
     float *ur, *depth; int32_t *sad; int64_t ostride; int32_t *nkept;
     float *hout; int64_t hcap;   // optional host-visible copy of one pair's results (k_stereo_cut)
     uint8_t *bands; int64_t band_stride;   // optional per-pair band scratch (sorted once per pair), or nullptr
+    int32_t *pair_done;          // optional per-pair workgroup counters (zero): the median cut fused into the search
 };
 
 // Projection searches (ORBmatcher SearchByProjection x4, Fuse x2): one frame

@@ -91,6 +91,7 @@ struct orbx_extractor {
     float *d_ur = nullptr, *d_depth = nullptr;
     int32_t *d_sad = nullptr, *d_nkept = nullptr;
     uint8_t *d_bands = nullptr;   // per stereo pair: the right image's sorted bands (StereoBufs::bands)
+    int32_t *d_pair_done = nullptr;   // per stereo pair: workgroup counter of the fused median cut
     int depth_mode = 0;         // 0 none, 1 stereo (index = pair), 2 RGB-D (index = frame)
     int depth_count = 0;
 
@@ -210,7 +211,7 @@ struct orbx_extractor {
         dfree(d_cell_count); dfree(d_level_count); dfree(d_key_node); dfree(d_key_q);
         for (auto &s : slot) { dfree(s.kps); dfree(s.desc); dfree(s.nkps); s.batch = 0; }
         dfree(d_prev); dfree(d_m12); dfree(d_nmatch); dfree(d_img);
-        dfree(d_ur); dfree(d_depth); dfree(d_sad); dfree(d_nkept); dfree(d_bands);
+        dfree(d_ur); dfree(d_depth); dfree(d_sad); dfree(d_nkept); dfree(d_bands); dfree(d_pair_done);
         depth_mode = 0;
         depth_count = 0;
         d_img_bytes = 0;
@@ -399,6 +400,10 @@ int reserve(orbx_extractor *ex, int w, int h, int max_batch) {
     const char *so = std::getenv("ORBX_STEREO_SORT_ONCE");   // (k_band_sort + k_stereo_band_gs, orbx_stereo.hip)
     if (so && so[0] == '1' && B >= 4 && p.max_kps <= 65535)
         ok &= dalloc(&ex->d_bands, (size_t)(B / 2) * stereo_band_stride(p.height, p.max_kps)) == hipSuccess;
+    if (B >= 2) {   // (zero; the fused cut's last workgroup resets its pair's counter)
+        ok &= dalloc(&ex->d_pair_done, B / 2) == hipSuccess;
+        ok &= ok && hipMemset(ex->d_pair_done, 0, sizeof(int32_t) * (B / 2)) == hipSuccess;
+    }
     if (!ok) { ex->release(); return ORBX_ENOMEM; }
     ex->planned = true;
     ex->max_batch = max_batch;
@@ -1501,6 +1506,10 @@ int orbx_stereo_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t
     a.mbf = mbf; a.maxd = mbf / mb;
     a.ur = ex->d_ur; a.depth = ex->d_depth; a.sad = ex->d_sad; a.ostride = kcap; a.nkept = ex->d_nkept;
     a.bands = ex->d_bands; a.band_stride = stereo_band_stride(a.rows, kcap);
+    {   // the median cut fused into the search (ORBX_STEREO_FUSED_CUT=0: its own launch)
+        const char *e = std::getenv("ORBX_STEREO_FUSED_CUT");
+        a.pair_done = (e && e[0] == '0') ? nullptr : ex->d_pair_done;
+    }
     if (launch_stereo(a, pairs, kcap, st) != hipSuccess) return ORBX_EIO;
     mark(ex, kNumStages, st);
     note_results(ex, st);

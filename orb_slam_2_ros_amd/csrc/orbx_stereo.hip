@@ -191,8 +191,7 @@ constexpr int kWalk = ORBX_STEREO_WALK;   // band positions per batch of descrip
 // SCR: the pair's bands sorted once by k_band_sort into its scratch (read
 // from L2), instead of every block sorting them into its LDS.
 template <bool SCR>
-__global__ __launch_bounds__(kST) void k_stereo_band(StereoBufs a) {
-    extern __shared__ __align__(16) uint8_t lds[];
+__device__ __attribute__((always_inline)) void stereo_band_body(const StereoBufs &a, uint8_t *lds) {
     __shared__ int ws[4];
     __shared__ int s_span;
     const int b = blockIdx.y, tid = threadIdx.x;
@@ -345,6 +344,13 @@ __global__ __launch_bounds__(kST) void k_stereo_band(StereoBufs a) {
         sad_out[iL] = bestSad;
     }
 }
+
+
+// With a.pair_done (batched steps) the last of a pair's workgroups to finish
+// also runs the pair's median cut (no k_stereo_cut launch); it resets the
+// pair's counter for the next step.  Defined after stereo_cut_pair.
+template <bool SCR>
+__global__ __launch_bounds__(kST) void k_stereo_band(StereoBufs a);
 
 // The same search with a group of kG lanes per left keypoint (kST / kG
 // keypoints per block): the lanes stride over the keypoint's band range and
@@ -529,11 +535,11 @@ __device__ inline int hist_select(const int *hist, int k, int *ws, int *s_sel, i
     return total;
 }
 
-__global__ __launch_bounds__(kST) void k_stereo_cut(StereoBufs a) {
+__device__ __attribute__((always_inline)) void stereo_cut_pair(const StereoBufs &a, int b) {
     __shared__ int hist[256];
     __shared__ int ws[4];
     __shared__ int s_sel, s_rank, s_kept;
-    const int b = blockIdx.x, tid = threadIdx.x;
+    const int tid = threadIdx.x;
     const int nl = a.nl[(int64_t)b * a.nstride];
     float *ur = a.ur + (int64_t)b * a.ostride;
     float *dp = a.depth + (int64_t)b * a.ostride;
@@ -593,6 +599,32 @@ __global__ __launch_bounds__(kST) void k_stereo_cut(StereoBufs a) {
         }
         if (tid == 0) reinterpret_cast<int32_t *>(a.hout)[2 * a.hcap] = kept;
     }
+}
+
+__global__ __launch_bounds__(kST) void k_stereo_cut(StereoBufs a) { stereo_cut_pair(a, blockIdx.x); }
+
+template <bool SCR>
+__global__ __launch_bounds__(kST) void k_stereo_band(StereoBufs a) {
+    extern __shared__ __align__(16) uint8_t lds[];
+    stereo_band_body<SCR>(a, lds);
+    if (!a.pair_done) return;
+    const int b = blockIdx.y;
+    const int nl = a.nl[(int64_t)b * a.nstride];
+    const int nact = (nl + kST - 1) / kST;   // the pair's workgroups that searched
+    if (nl <= 0) {
+        if (blockIdx.x != 0) return;   // (an empty pair: its first workgroup cuts)
+    } else {
+        if ((int)blockIdx.x >= nact) return;
+        __shared__ int s_last;
+        __threadfence();   // this workgroup's depths before its count
+        __syncthreads();
+        if (threadIdx.x == 0) s_last = atomicAdd(&a.pair_done[b], 1) == nact - 1;
+        __syncthreads();
+        if (!s_last) return;
+        __threadfence();   // (acquire: the pair's other workgroups' depths)
+        if (threadIdx.x == 0) a.pair_done[b] = 0;   // ready for the next step (stream order)
+    }
+    stereo_cut_pair(a, b);
 }
 
 // Frame::ComputeStereoFromRGBD (Frame.cc:679-701) for undistorted frames
@@ -668,8 +700,11 @@ hipError_t launch_stereo(const StereoBufs &a, int pairs, int nl_cap, hipStream_t
         }();
         if (grouped_scr)
             hipLaunchKernelGGL(k_stereo_band_gs, dim3((nl_cap + kST / kG - 1) / (kST / kG), pairs), dim3(kST), 0, st, a);
-        else
-            hipLaunchKernelGGL(k_stereo_band<true>, dim3((nl_cap + kST - 1) / kST, pairs), dim3(kST), 0, st, a);
+        else {
+            StereoBufs g = a;
+            g.pair_done = nullptr;
+            hipLaunchKernelGGL(k_stereo_band<true>, dim3((nl_cap + kST - 1) / kST, pairs), dim3(kST), 0, st, g);
+        }
         hipLaunchKernelGGL(k_stereo_cut, dim3(pairs), dim3(kST), 0, st, a);
         return hipGetLastError();
     }
@@ -679,10 +714,14 @@ hipError_t launch_stereo(const StereoBufs &a, int pairs, int nl_cap, hipStream_t
                              : reinterpret_cast<const void *>(k_stereo_band<false>);
     if (bytes > 64 * 1024 && hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess)
         return hipErrorInvalidValue;
-    if (grouped)
-        hipLaunchKernelGGL(k_stereo_band_g, dim3((nl_cap + kST / kG - 1) / (kST / kG), pairs), dim3(kST), bytes, st, a);
-    else
+    if (grouped) {
+        StereoBufs g = a;
+        g.pair_done = nullptr;
+        hipLaunchKernelGGL(k_stereo_band_g, dim3((nl_cap + kST / kG - 1) / (kST / kG), pairs), dim3(kST), bytes, st, g);
+    } else {
         hipLaunchKernelGGL(k_stereo_band<false>, dim3((nl_cap + kST - 1) / kST, pairs), dim3(kST), bytes, st, a);
+        if (a.pair_done) return hipGetLastError();   // (the cut ran in the search's last workgroups)
+    }
     hipLaunchKernelGGL(k_stereo_cut, dim3(pairs), dim3(kST), 0, st, a);
     return hipGetLastError();
 }
