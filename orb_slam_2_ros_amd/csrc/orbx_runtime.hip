@@ -1506,9 +1506,11 @@ int orbx_stereo_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t
     a.mbf = mbf; a.maxd = mbf / mb;
     a.ur = ex->d_ur; a.depth = ex->d_depth; a.sad = ex->d_sad; a.ostride = kcap; a.nkept = ex->d_nkept;
     a.bands = ex->d_bands; a.band_stride = stereo_band_stride(a.rows, kcap);
-    {   // the median cut fused into the search (ORBX_STEREO_FUSED_CUT=0: its own launch)
+    {   // the median cut fused into the search's last workgroups: measured slower
+        // (EuRoC depth 0.106 -> 0.23 ms, profiles/r04_ab_stereo_fused_cut.txt), so
+        // only with ORBX_STEREO_FUSED_CUT=1
         const char *e = std::getenv("ORBX_STEREO_FUSED_CUT");
-        a.pair_done = (e && e[0] == '0') ? nullptr : ex->d_pair_done;
+        a.pair_done = (e && e[0] == '1') ? ex->d_pair_done : nullptr;
     }
     if (launch_stereo(a, pairs, kcap, st) != hipSuccess) return ORBX_EIO;
     mark(ex, kNumStages, st);
