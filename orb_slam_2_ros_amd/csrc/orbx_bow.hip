@@ -54,20 +54,42 @@ __device__ inline bool epipolar_ok(float x1, float y1, float x2, float y2, const
     return (double)dsqr < __dmul_rn(3.84, (double)sigma2);
 }
 
-// One wave: node na_node of side A against its node in side B.
-__device__ __attribute__((always_inline)) void bow_match_node(const BowBufs &a, int na_node, int lane,
-                                                              uint8_t *mflag) {
-    // the node in side B
-    const uint32_t id = a.A.node_ids[na_node];
-    int lo = 0, hi = a.B.nnodes - 1, nb_node = -1;
-    while (lo <= hi) {
-        const int mid = (lo + hi) >> 1;
-        const uint32_t v = a.B.node_ids[mid];
-        if (v == id) { nb_node = mid; break; }
-        if (v < id) lo = mid + 1; else hi = mid - 1;
+// Position of id in the ascending, distinct ids[0, n), or -1, by the whole
+// wave: 64 pivots per round narrow the range 64-fold, so a side of up to 4096
+// nodes takes two rounds of loads where a binary search takes twelve
+// dependent ones (the single drop-in call waits on every round trip).
+__device__ inline int wave_find_u32(const uint32_t *ids, int n, uint32_t id, int lane) {
+    int lo = 0, hi = n;
+    while (hi - lo > 64) {
+        const int step = (hi - lo + 63) >> 6;
+        const int p = lo + lane * step;
+        const bool le = p < hi && ids[p] <= id;   // a prefix of the lanes
+        const int c = __popcll(__ballot(le));
+        if (c == 0) return -1;
+        lo += (c - 1) * step;
+        hi = min(hi, lo + step);
     }
-    if (nb_node < 0) return;
+    const int p = lo + lane;
+    const uint64_t eq = __ballot(p < hi && ids[p] == id);
+    return eq ? lo + __ffsll((unsigned long long)eq) - 1 : -1;
+}
+
+// One wave: node na_node of side A against its node in side B.
+// Accepted matches are counted in the workgroup's LDS (cnt[0, 30): rotation
+// bins, cnt[30]: matches); each workgroup stores its counts to its own slot
+// of a.part and the finish sums the slots.  (Device atomics on the problem's
+// counters -- one per match, or even one per bin per workgroup -- all land on
+// one cache line and serialise at its L2 channel: 43 -> 31 us of kernel time
+// in the drop-in call, profiles/r04_bow_call_phases3.txt.)
+__device__ __attribute__((always_inline)) void bow_match_node(const BowBufs &a, int na_node, int lane,
+                                                              uint8_t *mflag, int *cnt) {
+    const uint32_t id = a.A.node_ids[na_node];
     const int a0 = a.A.node_offsets[na_node], a1 = a.A.node_offsets[na_node + 1];
+    // A's first 64 feature indices, in flight with the search below
+    const int ia0 = lane < a1 - a0 ? a.A.node_features[a0 + lane] : -1;
+    // the node in side B
+    const int nb_node = wave_find_u32(a.B.node_ids, a.B.nnodes, id, lane);
+    if (nb_node < 0) return;
     const int b0 = a.B.node_offsets[nb_node], nbk = a.B.node_offsets[nb_node + 1] - b0;
     const bool tri = a.variant == ORBX_BOW_TRIANGULATION;
     for (int p = lane; p < nbk; p += 64) mflag[p] = 0;
@@ -96,7 +118,7 @@ __device__ __attribute__((always_inline)) void bow_match_node(const BowBufs &a, 
         uint4 qal = make_uint4(0, 0, 0, 0), qbl = qal;
         float x1l = 0.f, y1l = 0.f, an1l = 0.f;
         if (lane < np) {
-            i1l = a.A.node_features[pa + lane];
+            i1l = pa == a0 ? ia0 : a.A.node_features[pa + lane];
             fal = a.A.flags[i1l];
             const uint4 *ap = reinterpret_cast<const uint4 *>(a.A.desc + 32 * (int64_t)i1l);
             qal = ap[0]; qbl = ap[1];
@@ -195,9 +217,9 @@ __device__ __attribute__((always_inline)) void bow_match_node(const BowBufs &a, 
                 if (a.check_ori) {
                     const int bin = rot_bin(an1, an2);
                     a.bin_a[i1] = (int8_t)bin;
-                    atomicAdd(&a.hist[bin], 1);
+                    atomicAdd(&cnt[bin], 1);
                 }
-                atomicAdd(&a.counts[0], 1);
+                atomicAdd(&cnt[kHist], 1);
             }
         }
     }
@@ -207,12 +229,26 @@ __device__ __attribute__((always_inline)) void bow_match_node(const BowBufs &a, 
 // by one workgroup (any size); ends with a barrier.
 __device__ __attribute__((always_inline)) void bow_finish_problem(const BowBufs &a) {
     __shared__ int top[3];
-    __shared__ int hist[kHist];
+    __shared__ int hist[32];
     __shared__ int removed;
-    const int tid = threadIdx.x;
-    if (tid < kHist) hist[tid] = a.hist[tid];   // (one round of loads, not a serial chain on thread 0)
+    const int tid = threadIdx.x, bd = blockDim.x;
+    if (tid < 32) hist[tid] = 0;
     __syncthreads();
+    {   // the match workgroups' partial counts, eight loads in flight per thread
+        const int ne = 32 * a.nparts;
+        for (int base = tid; base < ne; base += 8 * bd) {
+            int v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = base + j * bd < ne ? a.part[base + j * bd] : 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (v[j]) atomicAdd(&hist[(base + j * bd) & 31], v[j]);
+        }
+    }
+    __syncthreads();
+    if (tid < 32) a.hist[tid] = hist[tid];
     if (tid == 0) {
+        a.counts[0] = hist[kHist];
         removed = 0;
         int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
         for (int i = 0; i < kHist; ++i) {
@@ -227,20 +263,29 @@ __device__ __attribute__((always_inline)) void bow_finish_problem(const BowBufs 
     }
     __syncthreads();
     if (a.check_ori) {
+        // eight features per thread with their loads in flight together
         int local = 0;
-        for (int i1 = tid; i1 < a.A.n; i1 += blockDim.x) {
-            const int m = a.match_a[i1];
-            if (m < 0) continue;
-            const int bin = a.bin_a[i1];
-            if (bin == top[0] || bin == top[1] || bin == top[2]) continue;
-            a.match_a[i1] = -1;
-            if (a.variant != ORBX_BOW_TRIANGULATION) a.match_b[m] = -1;
-            ++local;
+        const int n = a.A.n;
+        for (int base = tid; base < n; base += 8 * bd) {
+            int m[8], bin[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int i1 = base + j * bd;
+                m[j] = i1 < n ? a.match_a[i1] : -1;
+                bin[j] = i1 < n ? a.bin_a[i1] : 0;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (m[j] < 0 || bin[j] == top[0] || bin[j] == top[1] || bin[j] == top[2]) continue;
+                a.match_a[base + j * bd] = -1;
+                if (a.variant != ORBX_BOW_TRIANGULATION) a.match_b[m[j]] = -1;
+                ++local;
+            }
         }
         if (local) atomicAdd(&removed, local);
     }
     __syncthreads();
-    if (tid == 0) a.counts[1] = a.counts[0] - removed;
+    if (tid == 0) a.counts[1] = hist[kHist] - removed;
     __syncthreads();
 }
 
@@ -252,7 +297,19 @@ __global__ __launch_bounds__(kBT) void k_bow_match(const BowBufs *pa, HostTail t
     const BowBufs a = pa[blockIdx.y];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int na_node = blockIdx.x * (kBT / 64) + wave;
-    if (na_node < a.A.nnodes) bow_match_node(a, na_node, lane, matched[wave]);
+    const long long t0 = a.clk ? (long long)wall_clock64() : 0;
+    __shared__ int cnt[kHist + 1];
+    if (threadIdx.x <= kHist) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    if (na_node < a.A.nnodes) bow_match_node(a, na_node, lane, matched[wave], cnt);
+    __syncthreads();
+    if (threadIdx.x < 32) a.part[32 * blockIdx.x + threadIdx.x] = threadIdx.x <= kHist ? cnt[threadIdx.x] : 0;
+    if (a.clk && threadIdx.x == 0) {   // first start, last match end, longest workgroup
+        const long long t1 = (long long)wall_clock64();
+        atomicMin(&a.clk[0], t0);
+        atomicMax(&a.clk[1], t1);
+        atomicMax(&a.clk[5], t1 - t0);
+    }
     if (!tail.flag) return;
     __shared__ int s_last;
     __threadfence();   // this workgroup's matches before its count
@@ -261,10 +318,13 @@ __global__ __launch_bounds__(kBT) void k_bow_match(const BowBufs *pa, HostTail t
     __syncthreads();
     if (!s_last) return;
     __threadfence();   // (acquire: every workgroup's matches)
+    if (a.clk && threadIdx.x == 0) a.clk[2] = (long long)wall_clock64();
     bow_finish_problem(a);
-    for (int i = threadIdx.x; i < tail.n16; i += blockDim.x) tail.dst[i] = tail.src[i];
+    if (a.clk && threadIdx.x == 0) a.clk[3] = (long long)wall_clock64();
+    tail_copy(tail);
     __threadfence_system();
     __syncthreads();
+    if (a.clk && threadIdx.x == 0) a.clk[4] = (long long)wall_clock64();
     if (threadIdx.x == 0) __hip_atomic_store(tail.flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -287,6 +347,8 @@ hipError_t launch_bow(const BowBufs *h, const BowBufs *d, int np, const HostTail
     int nodes = 0;
     for (int k = 0; k < np; ++k) nodes = std::max(nodes, h[k].A.nnodes);
     const dim3 grid((nodes + kBT / 64 - 1) / (kBT / 64), np);
+    for (int k = 0; k < np; ++k)
+        if (h[k].nparts != (int)grid.x || (grid.x && !h[k].part)) return hipErrorInvalidValue;
     if (np == 1 && tail.flag && nodes > 0) {   // one launch: matching, rotation pass, outputs
         hipLaunchKernelGGL(k_bow_match, grid, dim3(kBT), 0, st, d, tail);
         return hipGetLastError();

@@ -84,6 +84,32 @@ struct HostTail {
 };
 
 #ifdef __HIPCC__
+// The copy itself, eight loads in flight per thread before their stores (a
+// loop of load -> store pairs is one memory round trip per element a thread
+// copies, and the synchronous calls wait on every one of them).
+__device__ inline void tail_copy(const HostTail &t) {
+    const int bd = blockDim.x;
+    for (int base = threadIdx.x; base < t.n16; base += 8 * bd) {
+        uint4 v0 = t.src[base], v1, v2, v3, v4, v5, v6, v7;
+        const int last = t.n16 - 1;   // (the tail of the range re-reads its last element)
+        v1 = t.src[min(base + bd, last)];
+        v2 = t.src[min(base + 2 * bd, last)];
+        v3 = t.src[min(base + 3 * bd, last)];
+        v4 = t.src[min(base + 4 * bd, last)];
+        v5 = t.src[min(base + 5 * bd, last)];
+        v6 = t.src[min(base + 6 * bd, last)];
+        v7 = t.src[min(base + 7 * bd, last)];
+        t.dst[base] = v0;
+        if (base + bd < t.n16) t.dst[base + bd] = v1;
+        if (base + 2 * bd < t.n16) t.dst[base + 2 * bd] = v2;
+        if (base + 3 * bd < t.n16) t.dst[base + 3 * bd] = v3;
+        if (base + 4 * bd < t.n16) t.dst[base + 4 * bd] = v4;
+        if (base + 5 * bd < t.n16) t.dst[base + 5 * bd] = v5;
+        if (base + 6 * bd < t.n16) t.dst[base + 6 * bd] = v6;
+        if (base + 7 * bd < t.n16) t.dst[base + 7 * bd] = v7;
+    }
+}
+
 // Every thread of every workgroup of the kernel calls this last.
 __device__ inline void host_tail(const HostTail &t) {
     if (!t.flag) return;
@@ -94,7 +120,7 @@ __device__ inline void host_tail(const HostTail &t) {
     __syncthreads();
     if (!s_last) return;
     __threadfence();   // (acquire: the other workgroups' results)
-    for (int i = threadIdx.x; i < t.n16; i += blockDim.x) t.dst[i] = t.src[i];
+    tail_copy(t);
     __threadfence_system();
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(t.flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -177,6 +203,9 @@ struct BowBufs {
     int8_t *bin_a;      // rotation bin per accepted A feature
     int32_t *hist;      // 30 bins
     int32_t *counts;    // [0] accepted, [1] nmatches after the rotation check
+    int32_t *part;      // per k_bow_match workgroup: 32 partial counts (30 bins, accepted, 0)
+    int nparts;         // k_bow_match's workgroups per problem (its grid's x)
+    long long *clk;     // debug (ORBX_BOW_CLOCKS): wall-clock marks of problem 0's one-launch call
 };
 
 enum Stage { kStageResize = 0, kStageBlur, kStageFast, kStageQuadtree, kStageDescribe, kStageMatch, kNumStages };

@@ -710,7 +710,7 @@ __global__ __launch_bounds__(kPT) void k_proj_search_replay(const ProjBufs *pa, 
     __threadfence();   // (acquire: every workgroup's results)
     const ProjBufs a = pa[0];
     proj_replay<QL>(a, lds);
-    for (int i = threadIdx.x; i < tail.n16; i += blockDim.x) tail.dst[i] = tail.src[i];
+    tail_copy(tail);
     __threadfence_system();
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(tail.flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -1976,6 +1976,9 @@ int bow_run(int device, int variant, orbx_bow_problem *P, int np, float nnratio,
     const size_t o_done = L.add(16);   // k_bow_finish's workgroup counter (HostTail)
     const size_t cnt_end = L.size;
     for (int t = 0; t < nl; ++t) o[t].bin = L.add((size_t)P[live[t]].a.n);
+    int nparts = 0;   // k_bow_match's workgroups per problem (4 side-A nodes each)
+    for (int t = 0; t < nl; ++t) nparts = std::max(nparts, (P[live[t]].a.nnodes + 3) / 4);
+    const size_t o_part = L.add(4 * 32 * (size_t)nparts * nl);
     CallWs &ws = call_ws(device);
     std::lock_guard<std::mutex> lock(ws.mu);
     int rc = ws_reserve(ws, L.size);
@@ -2010,6 +2013,14 @@ int bow_run(int device, int variant, orbx_bow_problem *P, int np, float nnratio,
         a.nlevels = nlevels;
         a.match_a = at<int32_t>(D, o[t].ma); a.match_b = at<int32_t>(D, o[t].mb); a.bin_a = at<int8_t>(D, o[t].bin);
         a.hist = at<int32_t>(D, o[t].cnt); a.counts = at<int32_t>(D, o[t].cnt) + 32;
+        a.part = at<int32_t>(D, o_part) + 32 * (size_t)nparts * t; a.nparts = nparts;
+    }
+    static const bool dbg_clk = std::getenv("ORBX_BOW_CLOCKS") != nullptr;   // diagnostic
+    static long long *dclk = nullptr;
+    if (dbg_clk && nl == 1) {
+        if (!dclk) (void)hipMalloc(reinterpret_cast<void **>(&dclk), 8 * sizeof(long long));
+        const long long init[8] = {INT64_MAX, 0, 0, 0, 0, 0, 0, 0};
+        if (dclk && hipMemcpy(dclk, init, sizeof(init), hipMemcpyHostToDevice) == hipSuccess) hb[0].clk = dclk;
     }
     put(ws, o_pa, hb.data(), sizeof(BowBufs) * nl);
     std::memset(ws.host + in_bytes, 0, cnt_end - in_bytes);   // the counters go up as zeros with the inputs
@@ -2032,6 +2043,13 @@ int bow_run(int device, int variant, orbx_bow_problem *P, int np, float nnratio,
     }
     clk.mark();   // readback
     clk.print("bow");
+    if (hb[0].clk) {
+        long long c[8];
+        if (hipMemcpy(c, hb[0].clk, sizeof(c), hipMemcpyDeviceToHost) == hipSuccess)   // 100 MHz ticks
+            std::fprintf(stderr, "orbx bow clocks us: matched %.2f elected %.2f finished %.2f copied %.2f longest wg %.2f\n",
+                         (c[1] - c[0]) / 100.0, (c[2] - c[0]) / 100.0, (c[3] - c[0]) / 100.0, (c[4] - c[0]) / 100.0,
+                         c[5] / 100.0);
+    }
     return ORBX_OK;
 }
 
