@@ -1109,6 +1109,11 @@ struct QLds {
 #endif
 constexpr bool kQtRoundsR4 = ORBX_QT_R4A;   // (A/B: round 3's round structure on the 256-thread register path)
 template <int NT> struct QCfg;
+#ifndef ORBX_QT_REGROOTS
+#define ORBX_QT_REGROOTS 0   // 1: the register paths count the roots in the gather too (slower:
+                             // FHD 0.162 -> 0.164, EuRoC 0.069 -> 0.080 ms, profiles/r04_ab_qt_regroots.txt)
+#endif
+constexpr bool kQtRegRoots = ORBX_QT_REGROOTS;
 constexpr int kQPreRoots = 16;   // roots the global-key gather counts itself (more: the roots' own pass)
 #ifndef ORBX_QT_R2
 #define ORBX_QT_R2 (kQuadRegKeys / 256)
@@ -1493,6 +1498,8 @@ __device__ __attribute__((always_inline)) void quadtree_rounds(const DevPlan &p,
         // the move and the counters' zeroing after the node phase): ORBX_QT_R4A
         // ---- 3. full rounds (ORBextractor.cc:618-696)
         bool final_phase = false;
+        if (pre_cnt)   // (roots counted in the gather: the keys move to the roots' list positions)
+            K.each([&](int j, int k) { K.set_node(j, k, s.nidx_c[4 * K.node(j, k)]); });
         while (true) {
             const int S = sh_S;
             child_stats(s, K);
@@ -1992,18 +1999,47 @@ __global__ __launch_bounds__(NT, QCfg<NT>::MINB) void k_quadtree(DevPlan p, Fram
         return;
     }
     const uint32_t *cand = fb.cand + (int64_t)b * p.cand_cap, *cand2 = fb.cand2 + (int64_t)b * p.cand_cap;
+    // the roots counted in the gather when there are few (every level but the
+    // narrowest strips; one root has its own pass without atomics): count and
+    // best key per root by the aggregated atomics, each key's node = its root
+    // and quadrant 0 set with it (no roots pass over the keys of its own)
+    __shared__ uint32_t rcnt[kQPreRoots], rbest[kQPreRoots];
+    const int nini = g.nini;
+    auto root_of = [&](uint32_t key) {
+        const float rx = (float)((int)(key & 0xFFF) - kBorder);
+        return min((int)__fdiv_rn(rx, g.hx), nini - 1);
+    };
     // up to QCfg<NT>::R1 (R2) keys per thread stay in registers
     // through the rounds
     auto in_registers = [&](auto &K) {
         K.gkeys = nullptr; K.gnode = knode; K.gq = kq; K.n = n;
-        K.each([&](int j, int k) {
-            const uint32_t a = kaddr[k];
-            K.key[j] = ((int)a < 0 ? cand2 : cand)[a & 0x7FFFFFFFu];
-            K.nq[j] = 0;
-        });
+        const bool pre = kQtRegRoots && nini > 1 && nini <= kQPreRoots;
+        if (pre) {
+            if (tid < kQPreRoots) { rcnt[tid] = 0; rbest[tid] = 0; }
+            __syncthreads();
+            K.each_all([&](int j, int k, bool valid) {
+                uint32_t slot = ~0u, bp = 0;
+                if (valid) {
+                    const uint32_t a = kaddr[k];
+                    const uint32_t key = ((int)a < 0 ? cand2 : cand)[a & 0x7FFFFFFFu];
+                    K.key[j] = key;
+                    const int r = root_of(key);
+                    K.nq[j] = (uint32_t)r;
+                    slot = (uint32_t)r;
+                    bp = best_pack(key, k);
+                }
+                agg_atomics(rcnt, rbest, slot, bp);   // (every lane: DPP)
+            });
+        } else {
+            K.each([&](int j, int k) {
+                const uint32_t a = kaddr[k];
+                K.key[j] = ((int)a < 0 ? cand2 : cand)[a & 0x7FFFFFFFu];
+                K.nq[j] = 0;
+            });
+        }
         __syncthreads();   // the cell tables are dead from here
         PHASE_MARK(2, 0);   // gather
-        quadtree_rounds(p, fb, s, g, b, l, K, phase_t_);
+        quadtree_rounds(p, fb, s, g, b, l, K, phase_t_, pre ? rcnt : nullptr, pre ? rbest : nullptr);
     };
     if (n <= QCfg<NT>::R1 * NT) {
         QKeys<QCfg<NT>::R1, NT> K;
@@ -2027,11 +2063,7 @@ __global__ __launch_bounds__(NT, QCfg<NT>::MINB) void k_quadtree(DevPlan p, Fram
             }
             if (tid == 0) coarse[nco] = ncell - 1;
         }
-        // the roots counted here when there are few (every level but the
-        // narrowest strips): count and best key per root by the aggregated
-        // atomics, each key's node = its root and quadrant 0 written with it
-        __shared__ uint32_t rcnt[kQPreRoots], rbest[kQPreRoots];
-        const int nini = g.nini;
+        // the roots counted here when there are few (rcnt / rbest above)
         const bool pre = nini <= kQPreRoots;
         if (tid < kQPreRoots) { rcnt[tid] = 0; rbest[tid] = 0; }
         __syncthreads();
@@ -2067,10 +2099,7 @@ __global__ __launch_bounds__(NT, QCfg<NT>::MINB) void k_quadtree(DevPlan p, Fram
                     keys[k] = key;
                     if (pre) {
                         int r = 0;
-                        if (nini > 1) {
-                            const float rx = (float)((int)(key & 0xFFF) - kBorder);
-                            r = min((int)__fdiv_rn(rx, g.hx), nini - 1);
-                        }
+                        if (nini > 1) r = root_of(key);
                         knode[k] = (uint16_t)r;
                         kq[k] = 0;
                         slot = (uint32_t)r;
