@@ -871,15 +871,17 @@ def run_config(torch, dist, rank, world, dev, w, h, nfeatures, streams, steps, w
 
 EXTRAS = [
     # key, mode, w, h, nfeatures, streams per GPU, unit
-    ("fhd_1920x1080", "mono", 1920, 1080, 1000, 128, "frames/s"),
-    ("hd_1280x720", "mono", 1280, 720, 1000, 256, "frames/s"),
+    # frames per GPU swept (round 4, profiles/r04_sweep_mono_streams.txt): FHD 128 / 192 / 256:
+    # 70.7k / 74.1k / 74.7k frames/s; HD 256 / 384: 144.4k / 151.1k; FHD RGB-D 128 / 192: 72.3k / 75.2k
+    ("fhd_1920x1080", "mono", 1920, 1080, 1000, 192, "frames/s"),
+    ("hd_1280x720", "mono", 1280, 720, 1000, 384, "frames/s"),
     # EuRoC pairs per GPU swept 128 / 192 / 256: 129.6k / 135.8k / 140.8k pairs/s; KITTI 96 / 144 / 192:
     # 80.6k / 84.4k / 84.9k (round 4, profiles/r04_sweep_stereo_streams.txt)
     ("stereo_euroc_752x480", "stereo", 752, 480, 1200, 256, "stereo pairs/s"),
     ("stereo_kitti_1241x376", "stereo", 1241, 376, 2000, 144, "stereo pairs/s"),
     # FHD stereo pairs per GPU swept 32 / 64 / 128 / 192 / 256: 23.9k / 27.3k / 28.2k / 28.6k / 28.4k pairs/s
     ("stereo_fhd_1920x1080", "stereo", 1920, 1080, 1000, 192, "stereo pairs/s"),
-    ("rgbd_fhd_1920x1080", "rgbd", 1920, 1080, 1000, 128, "frames/s"),
+    ("rgbd_fhd_1920x1080", "rgbd", 1920, 1080, 1000, 192, "frames/s"),
 ]
 
 # Batch split per extra (2 unless listed): every extra gains from the split or

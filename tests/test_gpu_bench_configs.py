@@ -122,9 +122,9 @@ def test_stereo_bench_configs(w, h, nf, P, split, pipe, oracle_mod):
     ex.close()
 
 
-@pytest.mark.parametrize("B", [128, 64])
+@pytest.mark.parametrize("B", [192, 64])
 def test_rgbd_fhd_bench_configs(B, oracle_mod):
-    """RGB-D FHD at the bench's 128 streams per GPU, and C5's 64 streams as
+    """RGB-D FHD at the bench's 192 streams per GPU, and C5's 64 streams as
     one GPU runs them."""
     import torch
     w, h = 1920, 1080
