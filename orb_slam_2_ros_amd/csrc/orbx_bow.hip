@@ -29,6 +29,10 @@ constexpr int kBT = 256;
 constexpr int kHist = 30;
 constexpr int kThLow = 50;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
+#ifndef ORBX_BOW_LANES_A
+#define ORBX_BOW_LANES_A 1   // nodes of <= 64 B features: lanes take A's features (0: one A feature at a time)
+#endif
+constexpr bool kBowLanesA = ORBX_BOW_LANES_A;
 
 __device__ inline int hamming_rr(const uint4 a0, const uint4 a1, const uint4 b0, const uint4 b1) {
     return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
@@ -83,14 +87,22 @@ __device__ inline int wave_find_u32(const uint32_t *ids, int n, uint32_t id, int
 // in the drop-in call, profiles/r04_bow_call_phases3.txt.)
 __device__ __attribute__((always_inline)) void bow_match_node(const BowBufs &a, int na_node, int lane,
                                                               uint8_t *mflag, int *cnt) {
-    const uint32_t id = a.A.node_ids[na_node];
-    const int a0 = a.A.node_offsets[na_node], a1 = a.A.node_offsets[na_node + 1];
-    // A's first 64 feature indices, in flight with the search below
-    const int ia0 = lane < a1 - a0 ? a.A.node_features[a0 + lane] : -1;
-    // the node in side B
-    const int nb_node = wave_find_u32(a.B.node_ids, a.B.nnodes, id, lane);
-    if (nb_node < 0) return;
-    const int b0 = a.B.node_offsets[nb_node], nbk = a.B.node_offsets[nb_node + 1] - b0;
+    int a0, a1, b0, nbk, ia0;
+    if (a.span) {   // the host's merge join of the two node lists: one load
+        const int4 sp = a.span[na_node];
+        a0 = sp.x; a1 = sp.y; b0 = sp.z; nbk = sp.w - sp.z;
+        if (nbk <= 0) return;
+        ia0 = lane < a1 - a0 ? a.A.node_features[a0 + lane] : -1;
+    } else {
+        const uint32_t id = a.A.node_ids[na_node];
+        a0 = a.A.node_offsets[na_node]; a1 = a.A.node_offsets[na_node + 1];
+        // A's first 64 feature indices, in flight with the search below
+        ia0 = lane < a1 - a0 ? a.A.node_features[a0 + lane] : -1;
+        // the node in side B
+        const int nb_node = wave_find_u32(a.B.node_ids, a.B.nnodes, id, lane);
+        if (nb_node < 0) return;
+        b0 = a.B.node_offsets[nb_node]; nbk = a.B.node_offsets[nb_node + 1] - b0;
+    }
     const bool tri = a.variant == ORBX_BOW_TRIANGULATION;
     for (int p = lane; p < nbk; p += 64) mflag[p] = 0;
     // the first 64 B features stay in registers
@@ -109,6 +121,118 @@ __device__ __attribute__((always_inline)) void bow_match_node(const BowBufs &a, 
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const float *F = a.tri;
+    if (nbk <= 64 && kBowLanesA) {
+        // The lanes take A's features (64 at a time) and B's features are
+        // broadcast one at a time from the registers above: every A feature's
+        // two best keys over all of B, with no cross-lane reduction per
+        // feature.  SearchByBoW's greedy pass then walks the features in
+        // order; a feature's two keys stand unless an earlier feature took one
+        // of their B features (then its exact pass over the untaken ones runs,
+        // the lanes holding B again).  Triangulation's features are
+        // independent: each lane writes its own.
+        uint64_t taken = 0;   // B positions matched by earlier A features (wave-uniform)
+        for (int pa = a0; pa < a1; pa += 64) {
+            const int np = min(64, a1 - pa);
+            int i1l = -1, fal = 0;
+            uint4 qal = make_uint4(0, 0, 0, 0), qbl = qal;
+            float x1l = 0.f, y1l = 0.f, an1l = 0.f;
+            if (lane < np) {
+                i1l = pa == a0 ? ia0 : a.A.node_features[pa + lane];
+                fal = a.A.flags[i1l];
+                const uint4 *ap = reinterpret_cast<const uint4 *>(a.A.desc + 32 * (int64_t)i1l);
+                qal = ap[0]; qbl = ap[1];
+                const orbx_keypoint k = a.A.keys[i1l];
+                x1l = k.x; y1l = k.y; an1l = k.angle;
+            }
+            const bool st1 = (fal >> 1) & 1;
+            uint32_t k1 = kNone, k2 = kNone;   // the lane's smallest two (dist << 16 | position) keys
+            for (int p = 0; p < nbk; ++p) {
+                const int fb = __builtin_amdgcn_readlane(fbr, p);
+                if (!(a.variant == ORBX_BOW_KF_FRAME || (fb & 1))) continue;
+                const uint4 e0 = make_uint4(__builtin_amdgcn_readlane(d0r.x, p), __builtin_amdgcn_readlane(d0r.y, p),
+                                            __builtin_amdgcn_readlane(d0r.z, p), __builtin_amdgcn_readlane(d0r.w, p));
+                const uint4 e1 = make_uint4(__builtin_amdgcn_readlane(d1r.x, p), __builtin_amdgcn_readlane(d1r.y, p),
+                                            __builtin_amdgcn_readlane(d1r.z, p), __builtin_amdgcn_readlane(d1r.w, p));
+                const int dist = hamming_rr(qal, qbl, e0, e1);
+                uint32_t key = kNone;
+                if (!tri) {
+                    key = ((uint32_t)dist << 16) | (uint32_t)p;
+                } else if (dist <= kThLow) {
+                    const float x2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, xr), p));
+                    const float y2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, yr), p));
+                    const int oct = __builtin_amdgcn_readlane(octr, p);
+                    const bool st2 = (fb >> 1) & 1;
+                    const bool lv = oct >= 0 && oct < a.nlevels;
+                    bool ok = true;
+                    if (!st1 && !st2) {
+                        const float dx = __fsub_rn(a.ex, x2), dy = __fsub_rn(a.ey, y2);
+                        const float sc = lv ? F[11 + oct] : 0.0f;
+                        if (__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)) < __fmul_rn(100.0f, sc)) ok = false;
+                    }
+                    if (ok && epipolar_ok(x1l, y1l, x2, y2, F, lv ? F[11 + a.nlevels + oct] : 0.0f))
+                        key = ((uint32_t)dist << 16) | (uint32_t)(0xFFFF - p);   // last minimum wins
+                }
+                if (key < k1) { k2 = k1; k1 = key; }
+                else if (key < k2) { k2 = key; }
+            }
+            if (tri) {
+                const int p1 = k1 == kNone ? 0 : 0xFFFF - (int)(k1 & 0xFFFF);
+                const int x_1 = __shfl(i2r, p1);   // (every lane active)
+                const float an2 = __shfl(angr, p1);
+                if (lane < np && (fal & 1) && k1 != kNone) {
+                    a.match_a[i1l] = x_1;
+                    if (a.check_ori) {
+                        const int bin = rot_bin(an1l, an2);
+                        a.bin_a[i1l] = (int8_t)bin;
+                        atomicAdd(&cnt[bin], 1);
+                    }
+                    atomicAdd(&cnt[kHist], 1);
+                }
+                continue;
+            }
+            for (int q = 0; q < np; ++q) {
+                const int fa = __builtin_amdgcn_readlane(fal, q);
+                if (!(fa & 1)) continue;
+                uint32_t c1 = (uint32_t)__builtin_amdgcn_readlane((int)k1, q);
+                uint32_t c2 = (uint32_t)__builtin_amdgcn_readlane((int)k2, q);
+                if (c1 == kNone) continue;
+                if (((taken >> (c1 & 63)) & 1) || (c2 != kNone && ((taken >> (c2 & 63)) & 1))) {
+                    const uint4 qa = make_uint4(__builtin_amdgcn_readlane(qal.x, q), __builtin_amdgcn_readlane(qal.y, q),
+                                                __builtin_amdgcn_readlane(qal.z, q), __builtin_amdgcn_readlane(qal.w, q));
+                    const uint4 qb = make_uint4(__builtin_amdgcn_readlane(qbl.x, q), __builtin_amdgcn_readlane(qbl.y, q),
+                                                __builtin_amdgcn_readlane(qbl.z, q), __builtin_amdgcn_readlane(qbl.w, q));
+                    uint32_t key = kNone;
+                    if (lane < nbk && (a.variant == ORBX_BOW_KF_FRAME || (fbr & 1)) && !((taken >> lane) & 1))
+                        key = ((uint32_t)hamming_rr(qa, qb, d0r, d1r) << 16) | (uint32_t)lane;
+                    c1 = wave_min_u32(key);
+                    if (c1 == kNone) continue;
+                    c2 = wave_min_u32(lane == (int)(c1 & 0xFFFF) ? kNone : key);
+                }
+                const int best1 = (int)(c1 >> 16), best2 = c2 == kNone ? 256 : (int)(c2 >> 16);
+                const bool pass = a.variant == ORBX_BOW_KF_FRAME ? best1 <= kThLow : best1 < kThLow;
+                if (!(pass && (float)best1 < __fmul_rn(a.nnratio, (float)best2))) continue;
+                const int p1 = (int)(c1 & 0xFFFF);
+                taken |= 1ull << p1;
+                const int x_1 = __builtin_amdgcn_readlane(i2r, p1), i1 = __builtin_amdgcn_readlane(i1l, q);
+                float an1 = 0.f, an2 = 0.f;
+                if (a.check_ori) {
+                    an1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, an1l), q));
+                    an2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, angr), p1));
+                }
+                if (lane == 0) {
+                    a.match_a[i1] = x_1;
+                    a.match_b[x_1] = i1;
+                    if (a.check_ori) {
+                        const int bin = rot_bin(an1, an2);
+                        a.bin_a[i1] = (int8_t)bin;
+                        atomicAdd(&cnt[bin], 1);
+                    }
+                    atomicAdd(&cnt[kHist], 1);
+                }
+            }
+        }
+        return;
+    }
     // A's features walked in order, 64 at a time: lane q holds feature
     // a0 + q's index, flags, descriptor and keypoint (one round of loads for
     // the run instead of a dependent chain per feature), read back by readlane

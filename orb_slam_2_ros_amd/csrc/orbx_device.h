@@ -203,6 +203,7 @@ struct BowBufs {
     int8_t *bin_a;      // rotation bin per accepted A feature
     int32_t *hist;      // 30 bins
     int32_t *counts;    // [0] accepted, [1] nmatches after the rotation check
+    const int4 *span;   // per side-A node: A's features [x, y), its side-B node's [z, w) (z == w: none)
     int32_t *part;      // per k_bow_match workgroup: 32 partial counts (30 bins, accepted, 0)
     int nparts;         // k_bow_match's workgroups per problem (its grid's x)
     long long *clk;     // debug (ORBX_BOW_CLOCKS): wall-clock marks of problem 0's one-launch call

@@ -1948,7 +1948,7 @@ int bow_run(int device, int variant, orbx_bow_problem *P, int np, float nnratio,
     const int ntri = variant == ORBX_BOW_TRIANGULATION ? 11 + 2 * nlevels : 0;
     Layout L;
     Dedup dd;
-    struct Off { size_t side[2][6]; size_t tri, ma, mb, cnt, bin; };
+    struct Off { size_t side[2][6]; size_t tri, span, ma, mb, cnt, bin; };
     std::vector<Off> o(nl);
     std::vector<uint8_t> up(12 * nl);
     for (int t = 0; t < nl; ++t) {
@@ -1965,6 +1965,7 @@ int bow_run(int device, int variant, orbx_bow_problem *P, int np, float nnratio,
             o[t].side[k][5] = dd.add(L, S->node_features, 4 * (size_t)std::max(nf, 1), f); up[12 * t + 6 * k + 5] = f;
         }
         o[t].tri = ntri ? L.add(4 * (size_t)ntri) : 0;
+        o[t].span = L.add(sizeof(int4) * (size_t)std::max(pr.a.nnodes, 1));
     }
     const size_t o_pa = L.add(sizeof(BowBufs) * nl);
     for (int t = 0; t < nl; ++t) {   // match arrays start as -1 (host copies), counters zeroed on the device
@@ -2005,6 +2006,19 @@ int bow_run(int device, int variant, orbx_bow_problem *P, int np, float nnratio,
                            at<int32_t>(D, so[4]), at<int32_t>(D, so[5]), S->nnodes};
         }
         if (ntri) put(ws, o[t].tri, pr.tri, 4 * (size_t)ntri);
+        {   // merge join of the ascending node ids: each A node's features and its B node's
+            int4 *sp = at<int4>(ws.host, o[t].span);
+            const orbx_bow_side &A = pr.a, &Bs = pr.b;
+            int j = 0;
+            for (int i = 0; i < A.nnodes; ++i) {
+                const uint32_t id = A.node_ids[i];
+                while (j < Bs.nnodes && Bs.node_ids[j] < id) ++j;
+                const bool hit = j < Bs.nnodes && Bs.node_ids[j] == id;
+                sp[i] = make_int4(A.node_offsets[i], A.node_offsets[i + 1], hit ? Bs.node_offsets[j] : 0,
+                                  hit ? Bs.node_offsets[j + 1] : 0);
+            }
+            a.span = at<int4>(D, o[t].span);
+        }
         put(ws, o[t].ma, pr.match_a, 4 * (size_t)pr.a.n);
         put(ws, o[t].mb, pr.match_b, 4 * (size_t)pr.b.n);
         a.variant = variant; a.nnratio = nnratio; a.check_ori = check_ori;
