@@ -114,8 +114,11 @@ __device__ __attribute__((always_inline)) void bow_match_node(const BowBufs &a, 
         fbr = a.B.flags[i2r];
         const uint4 *dp = reinterpret_cast<const uint4 *>(a.B.desc + 32 * (int64_t)i2r);
         d0r = dp[0]; d1r = dp[1];
-        const orbx_keypoint k = a.B.keys[i2r];
-        xr = k.x; yr = k.y; octr = k.octave; angr = k.angle;
+        if (tri) {
+            const orbx_keypoint k = a.B.keys[i2r];
+            xr = k.x; yr = k.y; octr = k.octave;
+        }
+        angr = a.B.ang[i2r];
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -141,8 +144,11 @@ __device__ __attribute__((always_inline)) void bow_match_node(const BowBufs &a, 
                 fal = a.A.flags[i1l];
                 const uint4 *ap = reinterpret_cast<const uint4 *>(a.A.desc + 32 * (int64_t)i1l);
                 qal = ap[0]; qbl = ap[1];
-                const orbx_keypoint k = a.A.keys[i1l];
-                x1l = k.x; y1l = k.y; an1l = k.angle;
+                if (tri) {
+                    const orbx_keypoint k = a.A.keys[i1l];
+                    x1l = k.x; y1l = k.y;
+                }
+                an1l = a.A.ang[i1l];
             }
             const bool st1 = (fal >> 1) & 1;
             uint32_t k1 = kNone, k2 = kNone;   // the lane's smallest two (dist << 16 | position) keys
@@ -246,8 +252,11 @@ __device__ __attribute__((always_inline)) void bow_match_node(const BowBufs &a, 
             fal = a.A.flags[i1l];
             const uint4 *ap = reinterpret_cast<const uint4 *>(a.A.desc + 32 * (int64_t)i1l);
             qal = ap[0]; qbl = ap[1];
-            const orbx_keypoint k = a.A.keys[i1l];
-            x1l = k.x; y1l = k.y; an1l = k.angle;
+            if (tri) {
+                const orbx_keypoint k = a.A.keys[i1l];
+                x1l = k.x; y1l = k.y;
+            }
+            an1l = a.A.ang[i1l];
         }
         for (int q = 0; q < np; ++q) {
             const int fa = __builtin_amdgcn_readlane(fal, q);
@@ -274,8 +283,10 @@ __device__ __attribute__((always_inline)) void bow_match_node(const BowBufs &a, 
                     fb = a.B.flags[i2];
                     const uint4 *dp = reinterpret_cast<const uint4 *>(a.B.desc + 32 * (int64_t)i2);
                     e0 = dp[0]; e1 = dp[1];
-                    const orbx_keypoint k = a.B.keys[i2];
-                    x2 = k.x; y2 = k.y; oct = k.octave;
+                    if (tri) {
+                        const orbx_keypoint k = a.B.keys[i2];
+                        x2 = k.x; y2 = k.y; oct = k.octave;
+                    }
                 }
                 uint32_t key = kNone;
                 if (pos < nbk) {
@@ -333,7 +344,7 @@ __device__ __attribute__((always_inline)) void bow_match_node(const BowBufs &a, 
             if (a.check_ori) {
                 an1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, an1l), q));
                 if (p_1 < 64) an2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, angr), p_1));
-                else an2 = a.B.keys[x_1].angle;
+                else an2 = a.B.ang[x_1];
             }
             if (lane == 0) {
                 a.match_a[i1] = x_1;

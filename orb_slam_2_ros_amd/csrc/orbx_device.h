@@ -193,6 +193,7 @@ constexpr int kBowNodeCap = 2048;   // largest side-B node (features) a wave han
 struct BowSideDev {
     const orbx_keypoint *keys; const uint8_t *desc; const uint8_t *flags; int n;
     const uint32_t *node_ids; const int32_t *node_offsets; const int32_t *node_features; int nnodes;
+    const float *ang;   // keypoint angles (keys: triangulation only, nullptr otherwise)
 };
 struct BowBufs {
     BowSideDev A, B;

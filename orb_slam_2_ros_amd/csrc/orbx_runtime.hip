@@ -1948,21 +1948,28 @@ int bow_run(int device, int variant, orbx_bow_problem *P, int np, float nnratio,
     const int ntri = variant == ORBX_BOW_TRIANGULATION ? 11 + 2 * nlevels : 0;
     Layout L;
     Dedup dd;
-    struct Off { size_t side[2][6]; size_t tri, span, ma, mb, cnt, bin; };
+    struct Off { size_t side[2][7]; size_t tri, span, ma, mb, cnt, bin; };
     std::vector<Off> o(nl);
-    std::vector<uint8_t> up(12 * nl);
+    std::vector<uint8_t> up(14 * nl);
+    // the keypoints go up whole for triangulation only; the SearchByBoW
+    // variants read just their angles (4 of 28 bytes: a third of the call's
+    // upload)
+    const bool whole_keys = variant == ORBX_BOW_TRIANGULATION;
     for (int t = 0; t < nl; ++t) {
         const orbx_bow_problem &pr = P[live[t]];
         for (int k = 0; k < 2; ++k) {
             const orbx_bow_side *S = k ? &pr.b : &pr.a;
             const int nf = S->node_offsets[S->nnodes];
             bool f;
-            o[t].side[k][0] = dd.add(L, S->keys, sizeof(orbx_keypoint) * S->n, f); up[12 * t + 6 * k] = f;
-            o[t].side[k][1] = dd.add(L, S->desc, 32 * (size_t)S->n, f); up[12 * t + 6 * k + 1] = f;
-            o[t].side[k][2] = dd.add(L, S->flags, (size_t)S->n, f); up[12 * t + 6 * k + 2] = f;
-            o[t].side[k][3] = dd.add(L, S->node_ids, 4 * (size_t)S->nnodes, f); up[12 * t + 6 * k + 3] = f;
-            o[t].side[k][4] = dd.add(L, S->node_offsets, 4 * (size_t)(S->nnodes + 1), f); up[12 * t + 6 * k + 4] = f;
-            o[t].side[k][5] = dd.add(L, S->node_features, 4 * (size_t)std::max(nf, 1), f); up[12 * t + 6 * k + 5] = f;
+            uint8_t *u = &up[14 * t + 7 * k];
+            o[t].side[k][0] = 0; u[0] = 0;
+            if (whole_keys) { o[t].side[k][0] = dd.add(L, S->keys, sizeof(orbx_keypoint) * S->n, f); u[0] = f; }
+            o[t].side[k][1] = dd.add(L, S->desc, 32 * (size_t)S->n, f); u[1] = f;
+            o[t].side[k][2] = dd.add(L, S->flags, (size_t)S->n, f); u[2] = f;
+            o[t].side[k][3] = dd.add(L, S->node_ids, 4 * (size_t)S->nnodes, f); u[3] = f;
+            o[t].side[k][4] = dd.add(L, S->node_offsets, 4 * (size_t)(S->nnodes + 1), f); u[4] = f;
+            o[t].side[k][5] = dd.add(L, S->node_features, 4 * (size_t)std::max(nf, 1), f); u[5] = f;
+            o[t].side[k][6] = dd.add(L, S->keys, 4 * (size_t)std::max(S->n, 1), f); u[6] = f;   // (angles)
         }
         o[t].tri = ntri ? L.add(4 * (size_t)ntri) : 0;
         o[t].span = L.add(sizeof(int4) * (size_t)std::max(pr.a.nnodes, 1));
@@ -1994,16 +2001,21 @@ int bow_run(int device, int variant, orbx_bow_problem *P, int np, float nnratio,
             const orbx_bow_side *S = k ? &pr.b : &pr.a;
             const int nf = S->node_offsets[S->nnodes];
             const size_t *so = o[t].side[k];
-            const uint8_t *u = &up[12 * t + 6 * k];
+            const uint8_t *u = &up[14 * t + 7 * k];
             if (u[0]) put(ws, so[0], S->keys, sizeof(orbx_keypoint) * S->n);
+            if (u[6]) {
+                float *ang = at<float>(ws.host, so[6]);
+                for (int i = 0; i < S->n; ++i) ang[i] = S->keys[i].angle;
+            }
             if (u[1]) put(ws, so[1], S->desc, 32 * (size_t)S->n);
             if (u[2]) put(ws, so[2], S->flags, (size_t)S->n);
             if (u[3]) put(ws, so[3], S->node_ids, 4 * (size_t)S->nnodes);
             if (u[4]) put(ws, so[4], S->node_offsets, 4 * (size_t)(S->nnodes + 1));
             if (u[5]) put(ws, so[5], S->node_features, 4 * (size_t)nf);
             BowSideDev &d = k ? a.B : a.A;
-            d = BowSideDev{at<orbx_keypoint>(D, so[0]), D + so[1], D + so[2], S->n, at<uint32_t>(D, so[3]),
-                           at<int32_t>(D, so[4]), at<int32_t>(D, so[5]), S->nnodes};
+            d = BowSideDev{whole_keys ? at<orbx_keypoint>(D, so[0]) : nullptr, D + so[1], D + so[2], S->n,
+                           at<uint32_t>(D, so[3]), at<int32_t>(D, so[4]), at<int32_t>(D, so[5]), S->nnodes,
+                           at<float>(D, so[6])};
         }
         if (ntri) put(ws, o[t].tri, pr.tri, 4 * (size_t)ntri);
         {   // merge join of the ascending node ids: each A node's features and its B node's
