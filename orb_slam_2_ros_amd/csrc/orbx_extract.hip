@@ -1114,6 +1114,10 @@ template <int NT> struct QCfg;
                              // FHD 0.162 -> 0.164, EuRoC 0.069 -> 0.080 ms, profiles/r04_ab_qt_regroots.txt)
 #endif
 constexpr bool kQtRegRoots = ORBX_QT_REGROOTS;
+#ifndef ORBX_QT_LEVEL_MAJOR
+#define ORBX_QT_LEVEL_MAJOR 1   // workgroups dispatched level by level (longest first), not frame by frame
+#endif
+constexpr bool kQtLevelMajor = ORBX_QT_LEVEL_MAJOR;
 constexpr int kQPreRoots = 16;   // roots the global-key gather counts itself (more: the roots' own pass)
 #ifndef ORBX_QT_R2
 #define ORBX_QT_R2 (kQuadRegKeys / 256)
@@ -1929,7 +1933,9 @@ template <bool PIPE, int NT>
 __global__ __launch_bounds__(NT, QCfg<NT>::MINB) void k_quadtree(DevPlan p, FrameBufs fb, int l0) {
     extern __shared__ __align__(16) uint8_t lds[];
     PHASE_START();
-    const int l = l0 + blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+    // (level-major grid: every frame's level 0, the longest, goes out first)
+    const int l = l0 + (kQtLevelMajor ? blockIdx.y : blockIdx.x), b = kQtLevelMajor ? blockIdx.x : blockIdx.y;
+    const int tid = threadIdx.x;
     const LevelGeom g = p.lv[l];
     const int NC = p.node_cap;
     QLds s;
@@ -2612,7 +2618,7 @@ int quadtree_nt(const DevPlan &p, int blocks) {
 
 template <bool PIPE>
 hipError_t launch_quadtree_range(const DevPlan &p, const FrameBufs &fb, int B, hipStream_t st, int l, int l_end) {
-    const dim3 grid(l_end - l, B);
+    const dim3 grid = kQtLevelMajor ? dim3(B, l_end - l) : dim3(l_end - l, B);
     switch (quadtree_nt(p, (l_end - l) * B)) {
         case 1024:
             if (allow_lds(k_quadtree<PIPE, 1024>, p.node_lds_bytes_w) != hipSuccess) return hipErrorInvalidValue;
