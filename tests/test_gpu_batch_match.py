@@ -28,7 +28,7 @@ def _same(g, o, names):
 
 @pytest.mark.parametrize("variant", ["fuse", "keyframe", "localmap", "fuse_sim3"])
 def test_projection_batch_equals_single_calls(variant, oracle_mod):
-    from proj_cases import VARIANT_ARGS, make_case
+    from orb_slam_2_ros_amd.synth_match import PROJ_VARIANT_ARGS as VARIANT_ARGS, make_proj_case as make_case
     th, ratio, ori, win = VARIANT_ARGS[variant]
     cases = [make_case(300 + k, variant, n=600 + 150 * k, nq=400 + 90 * k, stereo=k % 2 == 1, th=win)
              for k in range(6)]
@@ -46,7 +46,7 @@ def test_projection_batch_equals_single_calls(variant, oracle_mod):
 
 
 def test_projection_batch_with_empty_problems(oracle_mod):
-    from proj_cases import VARIANT_ARGS, make_case
+    from orb_slam_2_ros_amd.synth_match import PROJ_VARIANT_ARGS as VARIANT_ARGS, make_proj_case as make_case
     th, ratio, ori, win = VARIANT_ARGS["fuse"]
     a = make_case(311, "fuse", n=800, nq=500, th=win)
     b = make_case(312, "fuse", n=700, nq=400, th=win)
@@ -80,7 +80,7 @@ def _neighbours(B, count, seed):
 @pytest.mark.parametrize("variant,ori", [("triangulation", False), ("triangulation", True), ("kf_kf", True),
                                          ("kf_frame", False)])
 def test_bow_batch_equals_single_calls(variant, ori, oracle_mod):
-    from bow_cases import VARIANT_ARGS, make_case
+    from orb_slam_2_ros_amd.synth_match import BOW_VARIANT_ARGS as VARIANT_ARGS, make_bow_case as make_case
     ratio, _ = VARIANT_ARGS[variant]
     A, B, tri = make_case(400, variant, na=1200, nb=1300, nodes=90)
     # one keyframe A against 8 neighbours (the same A object: uploaded once),
@@ -100,7 +100,7 @@ def test_triangulation_batch_sequential_exclusion(oracle_mod):
     mapped by neighbours < i as unusable.  Batch once with the initial flags,
     then drop the excluded features and run the rotation pass
     (orbx_rotation_filter): equal to the oracle run with the updated flags."""
-    from bow_cases import VARIANT_ARGS, make_case
+    from orb_slam_2_ros_amd.synth_match import BOW_VARIANT_ARGS as VARIANT_ARGS, make_bow_case as make_case
     ratio, _ = VARIANT_ARGS["triangulation"]
     A, B, tri = make_case(420, "triangulation", na=1500, nb=1500, nodes=80)
     probs = [{"A": A, "B": Bk, "tri": tri} for Bk in _neighbours(B, 5, 421)]
@@ -130,7 +130,7 @@ def test_fuse_neighbours_batched_with_research(oracle_mod):
     before its turn -- the final map state equals the sequential reference
     (oracle, one query at a time with the current descriptor)."""
     from fuse_world import TH_LOW, distinctive, make_world, problems, run
-    from proj_cases import VARIANT_ARGS
+    from orb_slam_2_ros_amd.synth_match import PROJ_VARIANT_ARGS as VARIANT_ARGS
     th, ratio, ori, _ = VARIANT_ARGS["fuse"]
     w = make_world(7, kp_flips=(20, 40), row_flips=(10, 25))
 

@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("seed,na,nb,nodes,ori", [(111, 1000, 1100, 120, True), (112, 2500, 2400, 40, False),
                                                  (113, 3000, 3000, 15, True)])
 def test_bow_matchers_bit_exact(variant, seed, na, nb, nodes, ori, oracle_mod):
-    from bow_cases import VARIANT_ARGS, make_case
+    from orb_slam_2_ros_amd.synth_match import BOW_VARIANT_ARGS as VARIANT_ARGS, make_bow_case as make_case
     A, B, tri = make_case(seed, variant, na=na, nb=nb, nodes=nodes)
     ratio, _ = VARIANT_ARGS[variant]
     g = ORBmatcher(ratio, ori).search_by_bow(variant, A, B, tri)
@@ -25,7 +25,7 @@ def test_bow_matchers_bit_exact(variant, seed, na, nb, nodes, ori, oracle_mod):
 
 
 def test_bow_disjoint_and_empty(oracle_mod):
-    from bow_cases import make_case
+    from orb_slam_2_ros_amd.synth_match import make_bow_case as make_case
     A, B, _ = make_case(114, "kf_frame", na=300, nb=300, nodes=30)
     B2 = dict(B, ids=(B["ids"] + np.uint32(2_000_000)).astype(np.uint32))   # no common node
     nm, ma, mb = ORBmatcher(0.75, True).search_by_bow("kf_frame", A, B2)

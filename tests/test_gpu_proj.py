@@ -13,7 +13,7 @@ VARIANTS = ["localmap", "lastframe", "keyframe", "sim3", "fuse", "fuse_sim3"]
 
 
 def _check(c, variant, oracle_mod, th=None):
-    from proj_cases import VARIANT_ARGS
+    from orb_slam_2_ros_amd.synth_match import PROJ_VARIANT_ARGS as VARIANT_ARGS
     th_dist, ratio, ori, _ = VARIANT_ARGS[variant]
     if th is not None:
         th_dist = th
@@ -32,7 +32,7 @@ def _check(c, variant, oracle_mod, th=None):
 @pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("seed,n,nq,stereo", [(91, 1000, 800, False), (92, 2500, 2000, True)])
 def test_projection_matchers_bit_exact(variant, seed, n, nq, stereo, oracle_mod):
-    from proj_cases import VARIANT_ARGS, make_case
+    from orb_slam_2_ros_amd.synth_match import PROJ_VARIANT_ARGS as VARIANT_ARGS, make_proj_case as make_case
     c = make_case(seed, variant, n=n, nq=nq, stereo=stereo, th=VARIANT_ARGS[variant][3])
     assert _check(c, variant, oracle_mod) > 0
 
@@ -42,7 +42,7 @@ def test_projection_matchers_contention(variant, oracle_mod):
     """Wide windows over a dense frame with many near-duplicate descriptors:
     long candidate lists (LDS pool overflow into global scratch), frequent
     keypoint contention and full-list fallbacks in the greedy replay."""
-    from proj_cases import make_case
+    from orb_slam_2_ros_amd.synth_match import make_proj_case as make_case
     c = make_case(93, variant, n=6000, nq=3000, stereo=True, th=40.0)
     rng = np.random.default_rng(5)
     base = c["desc"][:40].copy()
@@ -54,7 +54,7 @@ def test_projection_matchers_contention(variant, oracle_mod):
 
 
 def test_projection_matchers_empty_and_edges(oracle_mod):
-    from proj_cases import make_case
+    from orb_slam_2_ros_amd.synth_match import make_proj_case as make_case
     c = make_case(94, "localmap", n=300, nq=200)
     m = ORBmatcher(0.8, False)
     nm, qi, qd, kf = m.search_by_projection("localmap", c["keys"][:0], c["desc"][:0], c["queries"], c["qdesc"],
@@ -70,7 +70,7 @@ def test_projection_matchers_empty_and_edges(oracle_mod):
 
 @pytest.mark.parametrize("seed", [95, 96])
 def test_search_by_sim3_bit_exact(seed, oracle_mod):
-    from proj_cases import make_sim3_case
+    from orb_slam_2_ros_amd.synth_match import make_sim3_case
     kf1, kf2, q1, qd1, q2, qd2 = make_sim3_case(seed)
     nf, m = ORBmatcher(0.75, False).search_by_sim3(kf1, kf2, q1, qd1, q2, qd2)
     onf, om = oracle_mod.search_by_sim3(kf1["keys"], kf1["desc"], kf1["bounds"], kf2["keys"], kf2["desc"],
@@ -84,7 +84,7 @@ def test_cpp_adapter_projection_table(tmp_path, oracle_mod):
     through its cv-typed signature (local-map variant, stereo) vs the oracle."""
     import subprocess
     from cxx_build import build_adapter_test
-    from proj_cases import VARIANT_ARGS, make_case
+    from orb_slam_2_ros_amd.synth_match import PROJ_VARIANT_ARGS as VARIANT_ARGS, make_proj_case as make_case
     c = make_case(98, "localmap", n=1200, nq=900, stereo=True, th=3.0)
     th, ratio, ori, _ = VARIANT_ARGS["localmap"]
     n, nq = len(c["keys"]), len(c["queries"])
@@ -113,7 +113,7 @@ def test_projection_pool_growth(oracle_mod):
     """Very wide windows over the largest frame the grid LDS holds: the
     candidate lists total millions of entries, more than the pool the earlier
     calls sized, so the call overflows it, learns the size and runs again."""
-    from proj_cases import make_case
+    from orb_slam_2_ros_amd.synth_match import make_proj_case as make_case
     c = make_case(97, "localmap", n=7000, nq=600, stereo=False, th=60.0)
     assert _check(c, "localmap", oracle_mod) > 0
     assert _check(c, "lastframe", oracle_mod, th=255) > 0
@@ -123,6 +123,6 @@ def test_projection_pool_growth(oracle_mod):
 def test_projection_many_points(variant, oracle_mod):
     """More map points than the replay keeps in LDS (their kept entries and
     status stay in global memory)."""
-    from proj_cases import VARIANT_ARGS, make_case
+    from orb_slam_2_ros_amd.synth_match import PROJ_VARIANT_ARGS as VARIANT_ARGS, make_proj_case as make_case
     c = make_case(98, variant, n=3000, nq=9000, stereo=True, th=VARIANT_ARGS[variant][3])
     assert _check(c, variant, oracle_mod) > 0

@@ -244,7 +244,7 @@ def test_stereo_from_rgbd_oracle(oracle_mod):
 @pytest.mark.parametrize("variant", ["localmap", "lastframe", "keyframe", "sim3", "fuse", "fuse_sim3"])
 @pytest.mark.parametrize("seed,stereo", [(81, False), (82, True)])
 def test_projection_matchers_vs_python(variant, seed, stereo, oracle_mod):
-    from proj_cases import VARIANT_ARGS, make_case
+    from orb_slam_2_ros_amd.synth_match import PROJ_VARIANT_ARGS as VARIANT_ARGS, make_proj_case as make_case
     th, ratio, ori, wth = VARIANT_ARGS[variant]
     c = make_case(seed, variant, n=900, nq=700, stereo=stereo, th=wth)
     a = oracle_mod.search_by_projection(variant, c["keys"], c["desc"], c["queries"], c["qdesc"], c["bounds"],
@@ -259,7 +259,7 @@ def test_projection_matchers_vs_python(variant, seed, stereo, oracle_mod):
 @pytest.mark.parametrize("variant", ["kf_frame", "kf_kf", "triangulation"])
 @pytest.mark.parametrize("seed,ori", [(101, True), (102, False)])
 def test_bow_matchers_vs_python(variant, seed, ori, oracle_mod):
-    from bow_cases import VARIANT_ARGS, make_case
+    from orb_slam_2_ros_amd.synth_match import BOW_VARIANT_ARGS as VARIANT_ARGS, make_bow_case as make_case
     A, B, tri = make_case(seed, variant, na=700, nb=650)
     ratio, _ = VARIANT_ARGS[variant]
     a = oracle_mod.search_by_bow(variant, A, B, ratio, ori, tri)
@@ -269,7 +269,7 @@ def test_bow_matchers_vs_python(variant, seed, ori, oracle_mod):
 
 
 def test_search_by_sim3_vs_python(oracle_mod):
-    from proj_cases import make_sim3_case
+    from orb_slam_2_ros_amd.synth_match import make_sim3_case
     kf1, kf2, q1, qd1, q2, qd2 = make_sim3_case(97, n1=500, n2=480)
     nf, m = oracle_mod.search_by_sim3(kf1["keys"], kf1["desc"], kf1["bounds"], kf2["keys"], kf2["desc"],
                                       kf2["bounds"], q1, qd1, q2, qd2, 100)
