@@ -891,8 +891,9 @@ EXTRA_SPLIT = {}
 # Level pipeline per config (off unless listed), on / off measured on one box:
 # VGA 1536 streams 318.0 / 314.5 k, FHD stereo 31.2 / 29.9 k pairs/s -- and
 # off elsewhere: FHD 53.1 / 57.4 k, HD 116.0 / 123.9 k, FHD RGB-D 54.2 / 58.3 k,
-# EuRoC 98.5 / 108.2 k, KITTI 62.0 / 67.3 k
-EXTRA_PIPE = {"stereo_fhd_1920x1080": 1}
+# EuRoC 98.5 / 108.2 k, KITTI 62.0 / 67.3 k.  Round 4, after the level-major quadtree grid: FHD
+# stereo on / off 37.2-37.3 / 37.9-38.0 k, so off there too (profiles/r04_ab_pipeline.txt)
+EXTRA_PIPE = {}
 HEADLINE_PIPE = 1
 # Batch split of the VGA headline: with the quadtree's child counts aggregated
 # (0.61 -> 0.38 ms) there is less latency-bound work to hide behind the other

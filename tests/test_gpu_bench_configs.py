@@ -85,7 +85,8 @@ def test_mono_bench_config_b3072(oracle_mod):
 STEREO_CONFIGS = [   # bench.py EXTRAS: (w, h, nfeatures, pairs, split, level pipeline as bench.py runs it)
     (752, 480, 1200, 256, 2, 0),
     (1241, 376, 2000, 144, 2, 0),
-    (1920, 1080, 1000, 192, 2, 1),
+    (1920, 1080, 1000, 192, 2, 0),
+    (752, 480, 1200, 32, 2, 1),   # (the level pipeline on a stereo step)
 ]
 
 
