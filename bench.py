@@ -889,8 +889,8 @@ EXTRAS = [
 # FHD stereo 28.1 / 29.8 k, FHD RGB-D 56.2 / 58.6 k pairs or frames/s).
 # Round 4, after the level-major quadtree grid (profiles/r04_ab_split.txt), unsplit measured faster for
 # FHD mono 75.1 / 75.5-75.7 k, FHD RGB-D 76.1-76.2 / 76.8-77.0 k, FHD stereo 37.7-38.0 / 38.1 k
-# (split / unsplit); EuRoC and KITTI within noise, kept split
-EXTRA_SPLIT = {"fhd_1920x1080": 1, "rgbd_fhd_1920x1080": 1, "stereo_fhd_1920x1080": 1}
+# (split / unsplit), HD 152.3 / 152.8-153.7 k; EuRoC and KITTI within noise, kept split
+EXTRA_SPLIT = {"fhd_1920x1080": 1, "hd_1280x720": 1, "rgbd_fhd_1920x1080": 1, "stereo_fhd_1920x1080": 1}
 # Level pipeline per config (off unless listed), on / off measured on one box:
 # VGA 1536 streams 318.0 / 314.5 k, FHD stereo 31.2 / 29.9 k pairs/s -- and
 # off elsewhere: FHD 53.1 / 57.4 k, HD 116.0 / 123.9 k, FHD RGB-D 54.2 / 58.3 k,
