@@ -42,6 +42,13 @@ typedef struct orbx_extractor orbx_extractor;
 const char *orbx_strerror(int code);
 int orbx_device_count(void);
 
+/* Diagnostic counters of the calling thread's last host call, for tests (no
+ * reference counterpart): "bow_repairs" -- in the last orbx_search_by_bow(_batch)
+ * call, the A features whose two best B features (of a node of <= 64 B
+ * features) included one an earlier A feature had taken, so that the exact
+ * in-order pass over the untaken ones ran.  ORBX_EINVAL for an unknown name. */
+int orbx_debug_counter(const char *name, int64_t *value);
+
 /* ---- ORB_SLAM2::ORBextractor ------------------------------------------ */
 
 /* ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST,

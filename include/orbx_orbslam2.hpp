@@ -17,6 +17,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -50,7 +51,11 @@ inline std::vector<orbx_keypoint> pack(const std::vector<cv::KeyPoint> &ks) {
 // every level).  The reference reads it only in Frame::ComputeStereoMatches
 // (Frame.cc:509, 599-616), which Frame_orbx.cc forwards to the device
 // pyramids, so with the forwarder in place no call pays for it.  operator[],
-// size(), begin()/end() read as std::vector<cv::Mat> does.
+// size(), begin()/end() read as std::vector<cv::Mat> does.  Each refill
+// allocates new level buffers, as ComputePyramid's fresh `temp` does, so a
+// cv::Mat a caller kept from an earlier frame keeps that frame's pixels.  The
+// fill is guarded by a mutex, so concurrent const reads are safe; as with
+// the reference's vector, reading while the extractor runs is not.
 class OrbxPyramid {
 public:
     cv::Mat &operator[](size_t l) { fill(); return lv_[l]; }
@@ -66,6 +71,7 @@ public:
 private:
     friend class ORBextractor;
     void fill() const {
+        std::lock_guard<std::mutex> lock(mu_);
         if (!stale_) return;
         const int E = 19;   // EDGE_THRESHOLD
         const int n = (int)lv_.size();
@@ -74,7 +80,7 @@ private:
         for (int l = 0; l < n; ++l) {
             int w = 0, h = 0;
             orbx_detail::check(orbx_extractor_pyramid_level(h_, l, nullptr, 0, &w, &h), "pyramid level");
-            whole_[l].create(h + 2 * E, w + 2 * E, CV_8U);   // (reused while the size holds)
+            whole_[l] = cv::Mat(h + 2 * E, w + 2 * E, CV_8U);   // new buffer: old ROIs keep their data
             lv_[l] = whole_[l](cv::Rect(E, E, w, h));
             ptr[l] = lv_[l].data;
             pitch[l] = lv_[l].step;
@@ -87,6 +93,7 @@ private:
     orbx_extractor *h_ = nullptr;
     mutable std::vector<cv::Mat> lv_, whole_;
     mutable bool stale_ = false;
+    mutable std::mutex mu_;
 };
 
 class ORBextractor {
@@ -142,7 +149,10 @@ public:
             _descriptors.create(n, 32, CV_8U);
             desc.rowRange(0, n).copyTo(_descriptors.getMat());
         }
-        mvImagePyramid.stale_ = true;   // filled from the device when read
+        {
+            std::lock_guard<std::mutex> lock(mvImagePyramid.mu_);
+            mvImagePyramid.stale_ = true;   // filled from the device when read
+        }
     }
 
     int inline GetLevels() { return nlevels_; }

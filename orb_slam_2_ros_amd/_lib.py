@@ -82,6 +82,7 @@ SZ = ctypes.c_size_t
 _SIGNATURES = {
     "orbx_strerror": (ctypes.c_char_p, [I32]),
     "orbx_device_count": (I32, []),
+    "orbx_debug_counter": (I32, [ctypes.c_char_p, P]),
     "orbx_extractor_create": (P, [I32, I32, F32, I32, I32, I32]),
     "orbx_extractor_destroy": (None, [P]),
     "orbx_extractor_get_levels": (I32, [P]),
@@ -198,3 +199,10 @@ def ptr(a: np.ndarray | None) -> int | None:
     if a is None:
         return None
     return a.__array_interface__["data"][0]
+
+
+def debug_counter(name: str) -> int:
+    """orbx_debug_counter: a diagnostic of this thread's last host call (tests)."""
+    v = ctypes.c_int64(0)
+    check(load().orbx_debug_counter(name.encode(), ctypes.byref(v)), f"orbx_debug_counter({name})")
+    return v.value

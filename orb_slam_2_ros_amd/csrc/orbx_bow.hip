@@ -29,6 +29,7 @@ constexpr int kBT = 256;
 constexpr int kHist = 30;
 constexpr int kThLow = 50;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr int kRepairs = kHist + 1;   // count slot of the repair passes (after the match count)
 #ifndef ORBX_BOW_LANES_A
 #define ORBX_BOW_LANES_A 1   // nodes of <= 64 B features: lanes take A's features (0: one A feature at a time)
 #endif
@@ -80,7 +81,8 @@ __device__ inline int wave_find_u32(const uint32_t *ids, int n, uint32_t id, int
 
 // One wave: node na_node of side A against its node in side B.
 // Accepted matches are counted in the workgroup's LDS (cnt[0, 30): rotation
-// bins, cnt[30]: matches); each workgroup stores its counts to its own slot
+// bins, cnt[30]: matches, cnt[31]: features that took the in-order repair
+// pass, a diagnostic the host reports through orbx_debug_counter); each workgroup stores its counts to its own slot
 // of a.part and the finish sums the slots.  (Device atomics on the problem's
 // counters -- one per match, or even one per bin per workgroup -- all land on
 // one cache line and serialise at its L2 channel: 43 -> 31 us of kernel time
@@ -203,6 +205,7 @@ __device__ __attribute__((always_inline)) void bow_match_node(const BowBufs &a, 
                 uint32_t c2 = (uint32_t)__builtin_amdgcn_readlane((int)k2, q);
                 if (c1 == kNone) continue;
                 if (((taken >> (c1 & 63)) & 1) || (c2 != kNone && ((taken >> (c2 & 63)) & 1))) {
+                    if (lane == 0) atomicAdd(&cnt[kRepairs], 1);
                     const uint4 qa = make_uint4(__builtin_amdgcn_readlane(qal.x, q), __builtin_amdgcn_readlane(qal.y, q),
                                                 __builtin_amdgcn_readlane(qal.z, q), __builtin_amdgcn_readlane(qal.w, q));
                     const uint4 qb = make_uint4(__builtin_amdgcn_readlane(qbl.x, q), __builtin_amdgcn_readlane(qbl.y, q),
@@ -433,12 +436,12 @@ __global__ __launch_bounds__(kBT) void k_bow_match(const BowBufs *pa, HostTail t
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int na_node = blockIdx.x * (kBT / 64) + wave;
     const long long t0 = a.clk ? (long long)wall_clock64() : 0;
-    __shared__ int cnt[kHist + 1];
-    if (threadIdx.x <= kHist) cnt[threadIdx.x] = 0;
+    __shared__ int cnt[32];
+    if (threadIdx.x < 32) cnt[threadIdx.x] = 0;
     __syncthreads();
     if (na_node < a.A.nnodes) bow_match_node(a, na_node, lane, matched[wave], cnt);
     __syncthreads();
-    if (threadIdx.x < 32) a.part[32 * blockIdx.x + threadIdx.x] = threadIdx.x <= kHist ? cnt[threadIdx.x] : 0;
+    if (threadIdx.x < 32) a.part[32 * blockIdx.x + threadIdx.x] = cnt[threadIdx.x];
     if (a.clk && threadIdx.x == 0) {   // first start, last match end, longest workgroup
         const long long t1 = (long long)wall_clock64();
         atomicMin(&a.clk[0], t0);

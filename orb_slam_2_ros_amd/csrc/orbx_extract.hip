@@ -297,15 +297,21 @@ __device__ inline uint32_t buf_ld32(__amdgpu_buffer_rsrc_t r, int voff, int soff
 // VGPR (k_fast, k_describe: -2 % time); the resize windows (up to 24
 // rows in flight) measured 2 % slower that way and keep global loads.
 // X80: the bytes are stored XOR 0x80 (as signed I - 128, k_describe's int8 MFMAs).
-template <int NB = 8, bool BUF = true, bool X80 = false>
+// FO >= 0 (BUF only): the rectangle lands at dst column FO whatever x0's
+// alignment (the loads are then unaligned dwords from x0 - FO; the buffer
+// base stays 4-aligned and the remainder goes into the lane offset).
+template <int NB = 8, bool BUF = true, bool X80 = false, int FO = -1>
 __device__ inline int wave_stage_rows(uint8_t *dst, int ds, const uint8_t *img, int pitch, int y0, int x0, int nr,
                                       int nc, int lane) {
     constexpr uint32_t kX = X80 ? 0x80808080u : 0u;
+    static_assert(FO < 0 || BUF, "a forced column offset needs the buffer loads");
     // (all wave-uniform: row offsets then come from the scalar unit)
     pitch = __builtin_amdgcn_readfirstlane(pitch);
     ds = __builtin_amdgcn_readfirstlane(ds);
     nr = __builtin_amdgcn_readfirstlane(nr);
-    const int xa = x0 & ~3, o = x0 - xa;
+    const int xs = FO >= 0 ? x0 - FO : x0;                  // first byte loaded
+    const int xa = xs & ~3, o = FO >= 0 ? FO : x0 - xa;
+    const int sh = FO >= 0 ? xs - xa : 0;                   // load misalignment
     const int nd = (o + nc + 3) >> 2;
     const uint8_t *gsrc = img + (int64_t)y0 * pitch + xa;
     const __amdgpu_buffer_rsrc_t src = wave_rsrc(gsrc);
@@ -316,7 +322,7 @@ __device__ inline int wave_stage_rows(uint8_t *dst, int ds, const uint8_t *img, 
     if (nd > 64) {
         for (int c0 = 0; c0 < nd; c0 += 64) {
             const bool on = c0 + lane < nd;
-            const int voff = 4 * (c0 + lane);
+            const int voff = 4 * (c0 + lane) + sh;
             for (int r0 = 0; r0 < nr; r0 += NB) {
                 uint32_t v[NB];
 #pragma unroll
@@ -324,14 +330,14 @@ __device__ inline int wave_stage_rows(uint8_t *dst, int ds, const uint8_t *img, 
                     if (on && r0 + j < nr) v[j] = load(voff, r0 + j);
 #pragma unroll
                 for (int j = 0; j < NB; ++j)
-                    if (on && r0 + j < nr) *reinterpret_cast<uint32_t *>(dst + mul24u(r0 + j, ds) + voff) = v[j] ^ kX;
+                    if (on && r0 + j < nr) *reinterpret_cast<uint32_t *>(dst + mul24u(r0 + j, ds) + voff - sh) = v[j] ^ kX;
             }
         }
         return o;
     }
     const int R = __builtin_amdgcn_readfirstlane(div_small(64, nd));   // rows per pass (wave-uniform)
     const int rl = div_small(lane, nd), k = lane - mul24u(rl, nd);
-    const int voff = mul24u(rl, pitch) + 4 * k, loff = mul24u(rl, ds) + 4 * k;
+    const int voff = mul24u(rl, pitch) + 4 * k + sh, loff = mul24u(rl, ds) + 4 * k;
     const int rmax = rl < R ? nr - rl : 0;   // this lane loads rows r0 + j R < rmax
     // the row offsets as scalar multiples of R * pitch (a v_mul_lo_u32 per
     // load otherwise: quarter rate, then a readfirstlane)
@@ -794,6 +800,11 @@ __device__ inline int arc_score_bytes(const int p[16], int v) {
 // PSC: the patch / score-map row stride as a compile-time constant (48 or 64:
 // every circle, ring and NMS neighbour offset becomes an LDS immediate), or 0
 // for the launch's runtime stride.
+#ifndef ORBX_FAST_ALIGN
+#define ORBX_FAST_ALIGN 1
+#endif
+constexpr bool kFastAlign = ORBX_FAST_ALIGN != 0;
+
 template <bool PIPE, int PSC>
 __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int c0, int nc, FastLds fl,
                                                    uint32_t gmagic) {
@@ -817,7 +828,13 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
     uint16_t *list = reinterpret_cast<uint16_t *>(scm + fl.score_bytes);   // (yy << 8 | xx), row-major
     int spitch;
     const uint8_t *img = level_ptr(p, fb, c.level, b, spitch);
-    const int o = wave_stage_rows(patch, PS, img, spitch, c.y0 - 3, c.x0 - 3, ch + 6, cw + 6, lane);
+    // (ORBX_FAST_ALIGN: the cell is staged so that interior column 0 lands on
+    // a dword boundary (patch column 4, loads unaligned): a 31-pixel cell row
+    // is then 8 quads, 4 lane groups, 16 rows per compass step, where a
+    // misaligned one took 9 quads, 5 groups, 12 rows: 2.66 -> 2.06 compass
+    // steps per VGA cell)
+    const int o = wave_stage_rows<8, true, false, kFastAlign ? 1 : -1>(patch, PS, img, spitch, c.y0 - 3, c.x0 - 3,
+                                                                        ch + 6, cw + 6, lane);
     const uint8_t *pc = patch + 3 * PS + o + 3;         // interior pixel (0, 0)
     const uint64_t below = (1ull << lane) - 1;
     PHASE_MARK(0, 0);   // prologue + staging
@@ -2541,6 +2558,9 @@ FastLds fast_lds(int mw, int mh) {
     // for a step's 512 plus a row of waiting corners; k_fast flushes before)
     f.list_cap = std::min(mw * mh, 640);
     f.ps = (mw + 6 + 3 + 3) & ~3;   // + alignment offset, dword rows
+    // the compass's last lane group reads up to column 4 + 8 ceil(mw / 8) + 3
+    // (interior column 0 at patch column 4, ORBX_FAST_ALIGN)
+    f.ps = std::max(f.ps, 8 * ((mw + 7) / 8) + 8);
     f.sw = mw + 2;
     if (f.ps <= 64) f.ps = f.sw = f.ps <= 48 ? 48 : 64;   // k_fast's constant-stride instantiations
     f.patch_bytes = (f.ps * (mh + 6) + 15) & ~15;

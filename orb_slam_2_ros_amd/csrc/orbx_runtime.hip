@@ -723,16 +723,6 @@ int align_level0(orbx_extractor *ex, const uint8_t **d_images, int64_t *stride, 
 namespace orbx {
 
 namespace {
-constexpr int kToHostThreads = 1024;
-__global__ __launch_bounds__(kToHostThreads) void k_to_host(const uint4 *src, uint4 *dst, int n16, uint32_t *flag) {
-    for (int i = threadIdx.x; i < n16; i += kToHostThreads) dst[i] = src[i];
-    __threadfence_system();
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-}  // namespace
-
-namespace {
 bool ws_direct(const CallWs &ws, size_t off, size_t bytes) {
     const size_t n16 = (bytes + 15) / 16;
     return bytes && ws.host_d && ws.flag_d && (off & 15) == 0 && n16 * 16 + off <= ws.cap && bytes <= (256u << 10);
@@ -765,15 +755,6 @@ int ws_poll(CallWs &ws) {
     return ORBX_OK;
 }
 }  // namespace
-
-int ws_finish(CallWs &ws, size_t off, size_t bytes) {
-    if (!ws_direct(ws, off, bytes)) return ws_copy_sync(ws, off, bytes);
-    ws_arm(ws);
-    hipLaunchKernelGGL(k_to_host, dim3(1), dim3(kToHostThreads), 0, ws.st, reinterpret_cast<const uint4 *>(ws.dev + off),
-                       reinterpret_cast<uint4 *>(ws.host_d + off), (int)((bytes + 15) / 16), ws.flag_d);
-    if (hipGetLastError() != hipSuccess) return ORBX_EIO;
-    return ws_poll(ws);
-}
 
 void ws_tail(CallWs &ws, size_t off, size_t bytes, uint32_t *done_d, int blocks, HostTail &t) {
     t = HostTail{};
@@ -1931,7 +1912,14 @@ struct CallClock {
     }
 };
 
+// Diagnostics of the calling thread's last host call (orbx_debug_counter).
+struct DebugCounters {
+    int64_t bow_repairs = 0;   // SearchByBoW features that took the in-order repair pass (orbx_bow.hip)
+};
+thread_local DebugCounters g_debug;
+
 int bow_run(int device, int variant, orbx_bow_problem *P, int np, float nnratio, int check_ori, int nlevels) {
+    g_debug.bow_repairs = 0;
     if (np < 0 || (np && !P)) return ORBX_EINVAL;
     CallClock clk;
     std::vector<int> live;
@@ -2042,11 +2030,13 @@ int bow_run(int device, int variant, orbx_bow_problem *P, int np, float nnratio,
         a.part = at<int32_t>(D, o_part) + 32 * (size_t)nparts * t; a.nparts = nparts;
     }
     static const bool dbg_clk = std::getenv("ORBX_BOW_CLOCKS") != nullptr;   // diagnostic
-    static long long *dclk = nullptr;
-    if (dbg_clk && nl == 1) {
-        if (!dclk) (void)hipMalloc(reinterpret_cast<void **>(&dclk), 8 * sizeof(long long));
+    struct DbgClk {   // this call's clock buffer, on the call's device, freed when the call returns
+        long long *p = nullptr;
+        ~DbgClk() { if (p) (void)hipFree(p); }
+    } dclk;
+    if (dbg_clk && nl == 1 && hipMalloc(reinterpret_cast<void **>(&dclk.p), 8 * sizeof(long long)) == hipSuccess) {
         const long long init[8] = {INT64_MAX, 0, 0, 0, 0, 0, 0, 0};
-        if (dclk && hipMemcpy(dclk, init, sizeof(init), hipMemcpyHostToDevice) == hipSuccess) hb[0].clk = dclk;
+        if (hipMemcpy(dclk.p, init, sizeof(init), hipMemcpyHostToDevice) == hipSuccess) hb[0].clk = dclk.p;
     }
     put(ws, o_pa, hb.data(), sizeof(BowBufs) * nl);
     std::memset(ws.host + in_bytes, 0, cnt_end - in_bytes);   // the counters go up as zeros with the inputs
@@ -2063,9 +2053,11 @@ int bow_run(int device, int variant, orbx_bow_problem *P, int np, float nnratio,
         orbx_bow_problem &pr = P[live[t]];
         get(ws, o[t].ma, pr.match_a, 4 * (size_t)pr.a.n);
         get(ws, o[t].mb, pr.match_b, 4 * (size_t)pr.b.n);
-        int32_t counts[2];
+        int32_t counts[2], repairs = 0;
         get(ws, o[t].cnt + 4 * 32, counts, sizeof(counts));
+        get(ws, o[t].cnt + 4 * 31, &repairs, sizeof(repairs));
         pr.nmatches = counts[1];
+        g_debug.bow_repairs += repairs;
     }
     clk.mark();   // readback
     clk.print("bow");
@@ -2095,6 +2087,12 @@ int orbx_search_by_bow(int device, int variant, const orbx_bow_side *A, const or
 int orbx_search_by_bow_batch(int device, int variant, orbx_bow_problem *problems, int nproblems, float nnratio,
                              int check_ori, int nlevels) {
     return bow_run(device, variant, problems, nproblems, nnratio, check_ori, nlevels);
+}
+
+int orbx_debug_counter(const char *name, int64_t *value) {
+    if (!name || !value) return ORBX_EINVAL;
+    if (!std::strcmp(name, "bow_repairs")) { *value = g_debug.bow_repairs; return ORBX_OK; }
+    return ORBX_EINVAL;
 }
 
 int orbx_rotation_filter(const orbx_keypoint *ka, const orbx_keypoint *kb, int32_t *match_a, int na,

@@ -24,8 +24,8 @@ struct CallWs {
     std::mutex mu;
     hipStream_t st = nullptr;
     uint8_t *dev = nullptr, *host = nullptr;
-    uint8_t *host_d = nullptr;    // the pinned arena's device address (ws_finish writes there)
-    uint32_t *flag = nullptr;     // pinned done flag of ws_finish
+    uint8_t *host_d = nullptr;    // the pinned arena's device address (the HostTail copy writes there)
+    uint32_t *flag = nullptr;     // pinned done flag the HostTail copy raises
     uint32_t *flag_d = nullptr;
     size_t cap = 0;
     int64_t proj_pool = 0;   // projection candidate-list entries the last calls needed
@@ -71,16 +71,14 @@ inline int ws_reserve(CallWs &ws, size_t bytes) {
 }
 
 // Brings [off, off + bytes) of the device arena into the pinned arena after
-// the work queued on ws.st, and waits for it: a one-workgroup kernel writes
-// the bytes straight into the (device-visible) pinned buffer and then raises
-// a flag the host polls, instead of a copy plus a stream synchronisation
-// (about 10 us of wake-up for a call of ~50 us).  Large outputs take the copy.
-// Caller holds ws.mu.
-int ws_finish(CallWs &ws, size_t off, size_t bytes);
-// The same copy done by the last workgroup of the call's last kernel
-// (HostTail, orbx_device.h): ws_tail prepares it before that launch (done_d: a
+// the call's last kernel, and waits for it: the last workgroup of that kernel
+// to finish (HostTail, orbx_device.h) writes the bytes straight into the
+// (device-visible) pinned buffer and then raises a flag the host polls,
+// instead of a copy plus a stream synchronisation (about 10 us of wake-up for
+// a call of ~50 us).  ws_tail prepares it before that launch (done_d: a
 // device counter the inputs upload as zero; blocks: the kernel's workgroups;
-// t.flag stays nullptr when the output takes the copy), ws_wait waits after.
+// t.flag stays nullptr when the output takes the copy: large outputs, no
+// device-visible pinned arena), ws_wait waits after.  Caller holds ws.mu.
 void ws_tail(CallWs &ws, size_t off, size_t bytes, uint32_t *done_d, int blocks, HostTail &t);
 int ws_wait(CallWs &ws, const HostTail &t, size_t off, size_t bytes);
 

@@ -127,9 +127,6 @@ def make_sim3_case(seed, n1=900, n2=850, w=640, h=480, th=7.5):
     return kf1, kf2, c2["queries"], c2["qdesc"], c1["queries"], c1["qdesc"]
 
 
-
-
-
 def _bow_csr(node_of, n):
     ids = np.unique(node_of).astype(np.uint32)
     off = np.zeros(len(ids) + 1, np.int32)
@@ -203,6 +200,64 @@ def make_bow_case(seed, variant, na=1000, nb=1000, nodes=120, w=640, h=480):
     if variant == "triangulation":
         ex, ey = np.float32(w * 0.5), np.float32(h * 0.5)
         tri = np.concatenate([F12.ravel(), [ex, ey], sf, sigma2]).astype(np.float32)
+    return A, B, tri
+
+
+def make_bow_contention_case(seed, variant, nb_node, na_node, nodes=12, hubs=3, w=640, h=480):
+    """Tiny descriptor pools: in each of `nodes` nodes, nb_node B features are
+    noisy copies of a few hub descriptors and na_node A features are noisy
+    copies of the same hubs, so many A features share their best and second
+    B features and the greedy "already matched" state of SearchByBoW decides
+    most of them (ORBmatcher.cc:200-250, 577-625).  Exact ties included."""
+    rng = np.random.default_rng(seed)
+    sf, _ = scale_tables(1.2, 8)
+    sigma2 = (sf * sf).astype(np.float32)
+    pool = np.sort(rng.choice(10 ** 6, nodes, replace=False)).astype(np.uint32)
+    na, nb = nodes * na_node, nodes * nb_node
+
+    def noisy(d, nbits):
+        d = d.copy()
+        for bit in rng.choice(256, nbits, replace=False):
+            d[bit >> 3] ^= np.uint8(1 << (bit & 7))
+        return d
+
+    def keys(n):
+        k = np.zeros(n, KEYPOINT_DTYPE)
+        k["x"] = rng.uniform(0, w, n).astype(np.float32)
+        k["y"] = rng.uniform(0, h, n).astype(np.float32)
+        k["octave"] = rng.choice(8, n, p=[0.3, 0.2, 0.15, 0.1, 0.1, 0.06, 0.05, 0.04])
+        k["angle"] = rng.uniform(0, 30, n).astype(np.float32)   # mostly one rotation bin
+        k["class_id"] = -1
+        return k
+    ka, kb = keys(na), keys(nb)
+    da = np.zeros((na, 32), np.uint8)
+    db = np.zeros((nb, 32), np.uint8)
+    node_a = np.repeat(pool, na_node)
+    node_b = np.repeat(pool, nb_node)
+    for t in range(nodes):
+        hub = rng.integers(0, 256, (hubs, 32)).astype(np.uint8)
+        for j in range(nb_node):
+            db[t * nb_node + j] = noisy(hub[rng.integers(hubs)], int(rng.integers(0, 24)))
+        for j in range(na_node):
+            da[t * na_node + j] = noisy(hub[rng.integers(hubs)], int(rng.integers(0, 16)))
+    dup = rng.integers(0, nb, nb // 10)
+    db[dup] = db[rng.integers(0, nb, len(dup))]          # exact ties
+    # shuffle so a node's features are not contiguous indices
+    pa, pb = rng.permutation(na), rng.permutation(nb)
+    ka, da, node_a = ka[pa], da[pa], node_a[pa]
+    kb, db, node_b = kb[pb], db[pb], node_b[pb]
+    fa = (rng.random(na) > 0.1).astype(np.uint8)
+    fb = np.ones(nb, np.uint8) if variant == "kf_frame" else (rng.random(nb) > 0.1).astype(np.uint8)
+    tri = None
+    if variant == "triangulation":
+        fa |= (2 * (rng.random(na) < 0.4)).astype(np.uint8)
+        fb |= (2 * (rng.random(nb) < 0.4)).astype(np.uint8)
+        F12 = np.array([[0.0, -2e-6, 1e-3], [2e-6, 0.0, -2e-3], [-1.2e-3, 2.1e-3, 0.05]], np.float32)
+        tri = np.concatenate([F12.ravel(), [np.float32(w * 0.5), np.float32(h * 0.5)], sf, sigma2]).astype(np.float32)
+    ia, oa, fea = _bow_csr(node_a, na)
+    ib, ob, feb = _bow_csr(node_b, nb)
+    A = dict(keys=ka, desc=da, flags=fa, ids=ia, off=oa, feat=fea)
+    B = dict(keys=kb, desc=db, flags=fb, ids=ib, off=ob, feat=feb)
     return A, B, tri
 
 
