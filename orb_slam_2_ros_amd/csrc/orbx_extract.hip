@@ -2194,6 +2194,40 @@ struct RowTaps {
 __constant__ RowTaps c_row_taps = RowTaps();
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
+#ifndef ORBX_DESC_STAGE
+#define ORBX_DESC_STAGE 1   // 0: the generic wave_stage_rows
+#endif
+// k_describe's 43 x 43 patch inside the level: a row is nd = 11 or 12 dwords,
+// so 5 rows a pass (lanes (rl, k), rl < 5) and 9 passes cover rows rl + 5 j;
+// every row lane has j < 8, rows 40..42 (j = 8) only rl < 3.  One exec region
+// for the nine loads and stores (the generic loop guards each with its own
+// compare and exec save / restore: ~70 scalar instructions a wave), row
+// offsets as scalar multiples of the pitch, LDS offsets as immediates.
+// Stored XOR 0x80 (the int8 MFMAs' I - 128).  Returns o = x0 & 3.
+__device__ inline int stage_desc_patch(uint8_t *dst, const uint8_t *img, int pitch, int y0, int x0, int lane) {
+    static_assert(kDescP == 43 && kDescPS >= 48, "5 rows of <= 12 dwords a pass");
+    pitch = __builtin_amdgcn_readfirstlane(pitch);
+    const int xa = x0 & ~3, o = x0 - xa;
+    const int nd = (o + kDescP + 3) >> 2;   // 11 or 12
+    const __amdgpu_buffer_rsrc_t src = wave_rsrc(img + (int64_t)y0 * pitch + xa);
+    const int rl = div_small(lane, nd), k = lane - mul24u(rl, nd);
+    const int voff = mul24u(rl, pitch) + 4 * k;
+    const int p5 = __builtin_amdgcn_readfirstlane(5 * pitch);
+    typedef __attribute__((address_space(3))) uint32_t lds_u32;
+    lds_u32 *d = (lds_u32 *)(dst + mul24u(rl, kDescPS) + 4 * k);
+    if (rl < 5) {
+        uint32_t v[9];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = buf_ld32(src, voff, j * p5);
+        const bool last = rl < 3;
+        if (last) v[8] = buf_ld32(src, voff, 8 * p5);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j * 5 * kDescPS / 4] = v[j] ^ 0x80808080u;
+        if (last) d[8 * 5 * kDescPS / 4] = v[8] ^ 0x80808080u;
+    }
+    return o;
+}
+
 template <bool PIPE>
 __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs fb, int s0, int ns, int write_total,
                                                            uint32_t gmagic) {
@@ -2262,7 +2296,8 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
         for (int t = 0; t < 6; ++t) mom[t] = mt[t * 64];
     }
     if (inside) {
-        o = wave_stage_rows<(kDescP + 4) / 5, true, true>(lbase, kDescPS, img, spitch, py0, px0, kDescP, kDescP, lane);   // 5 rows a pass
+        if constexpr (ORBX_DESC_STAGE) o = stage_desc_patch(lbase, img, spitch, py0, px0, lane);
+        else o = wave_stage_rows<(kDescP + 4) / 5, true, true>(lbase, kDescPS, img, spitch, py0, px0, kDescP, kDescP, lane);   // 5 rows a pass
     } else {
         // near a level border: lane = patch column (its reflect-101 column fixed),
         // the rows in turn (the row's reflection is wave-uniform)
