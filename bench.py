@@ -869,6 +869,89 @@ def run_config(torch, dist, rank, world, dev, w, h, nfeatures, streams, steps, w
     return el, stages, len(kp), sane, float(batch), ex   # the profiled launches cover the whole batch
 
 
+def host_fed(torch, dev, w, h, nfeatures, nstreams, split, pipeline, steps, warmup):
+    """The mono step fed from host memory, as a camera-fed node sees it
+    (ros/src/MonoNode.cc:38-50 -> Frame.cc:259-265: each frame arrives in a host
+    cv::Mat).  Frames sit in pinned host memory (two per stream, alternating);
+    step k's batch goes up on its own copy stream while step k - 1 computes
+    (two device input buffers), and step k's keypoints + descriptors
+    (orbx_batch_pack_device) come back on a third stream while step k + 1
+    computes.  Reports frames/s with both PCIe directions inside the timed
+    region, the host->device and device->host rates achieved, and a
+    copy-only host->device rate over the same buffers: the bound PCIe puts on
+    a host-fed front end (frames/s <= that rate / frame bytes)."""
+    from orb_slam_2_ros_amd import ORBextractor
+    streams = list(range(nstreams))
+    host, _ = _resident_frames("mono", w, h, streams)
+    src = torch.empty((2, nstreams, h, w), dtype=torch.uint8, pin_memory=True)
+    src.copy_(torch.from_numpy(host[:2]))
+    del host
+    ex = ORBextractor(nfeatures, 1.2, 8, 20, 7, device=dev.index)
+    ex.reserve(w, h, nstreams)
+    ex.split(split)
+    ex.pipeline(pipeline)
+    dbuf = torch.empty((2, nstreams, h, w), dtype=torch.uint8, device=dev)
+    s_comp = torch.cuda.current_stream(dev)
+    s_up, s_down = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    # the pack layout's size (known once a batch of this size has run)
+    ex.mono_step_device(dbuf[0].data_ptr(), h * w, w, nstreams, 100, 0.9, True, s_comp.cuda_stream)
+    torch.cuda.synchronize(dev)
+    nb = ex.pack_bytes()
+    pbuf = torch.empty((2, nb), dtype=torch.uint8, device=dev)
+    hout = torch.empty((2, nb), dtype=torch.uint8, pin_memory=True)
+    up_done = [torch.cuda.Event() for _ in range(2)]
+    comp_done = [torch.cuda.Event() for _ in range(2)]
+    down_done = [torch.cuda.Event() for _ in range(2)]
+    recorded = [False, False]
+
+    def step(k):
+        i = k % 2
+        if recorded[i]:
+            s_up.wait_event(comp_done[i])     # step k - 2 has read dbuf[i]
+        with torch.cuda.stream(s_up):
+            dbuf[i].copy_(src[i], non_blocking=True)
+            up_done[i].record(s_up)
+        s_comp.wait_event(up_done[i])
+        if recorded[i]:
+            s_comp.wait_event(down_done[i])   # pbuf[i] of step k - 2 is on the host
+        ex.mono_step_device(dbuf[i].data_ptr(), h * w, w, nstreams, 100, 0.9, True, s_comp.cuda_stream)
+        ex.pack_device(pbuf[i].data_ptr(), nb, s_comp.cuda_stream)
+        comp_done[i].record(s_comp)
+        s_down.wait_event(comp_done[i])
+        with torch.cuda.stream(s_down):
+            hout[i].copy_(pbuf[i], non_blocking=True)
+            down_done[i].record(s_down)
+        recorded[i] = True
+
+    sync = lambda: torch.cuda.synchronize(dev)   # noqa: E731
+    el = timed_region(step, steps, warmup, sync, None, 1)
+    # the copies alone over the same buffers: PCIe's own rate
+    sync()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        with torch.cuda.stream(s_up):
+            dbuf[k % 2].copy_(src[k % 2], non_blocking=True)
+    sync()
+    el_up = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    for k in range(steps):
+        with torch.cuda.stream(s_down):
+            hout[k % 2].copy_(pbuf[k % 2], non_blocking=True)
+    sync()
+    el_down = time.perf_counter() - t0
+    counts = hout[(steps - 1) % 2][:4 * nstreams].view(torch.int32)
+    ok = int(counts.min().item()) > 0
+    ex.close()
+    fb = w * h
+    up_rate = nstreams * fb * steps / el_up / 1e9
+    return {"value": round(nstreams * steps / el, 2), "unit": "frames/s", "streams_per_gpu": nstreams,
+            "ms_per_step": round(1e3 * el / steps, 4),
+            "h2d_GBs": round(nstreams * fb * steps / el / 1e9, 2), "d2h_GBs": round(nb * steps / el / 1e9, 2),
+            "d2h_bytes_per_frame": round(nb / nstreams, 1),
+            "copy_only_h2d_GBs": round(up_rate, 2), "copy_only_d2h_GBs": round(nb * steps / el_down / 1e9, 2),
+            "pcie_bound_frames_per_s": round(up_rate * 1e9 / fb, 1), "results_on_host": ok}
+
+
 EXTRAS = [
     # key, mode, w, h, nfeatures, streams per GPU, unit
     # frames per GPU swept (round 4, profiles/r04_sweep_mono_streams.txt): FHD 128 / 192 / 256:
@@ -904,6 +987,11 @@ HEADLINE_PIPE = 1
 # (split / pipeline 1/1: 375.8-376.3 k, 2/1: 373.7-374.2 k, 2/0: 372.2-373.1 k,
 # 1/0: 369.0-370.4 k frames/s; profiles/r03_split_sweep.txt)
 HEADLINE_SPLIT = 1
+
+# Host-fed runs of the mono step (frames from pinned host memory, both PCIe
+# directions in the timed region): (w, h, nfeatures, streams per GPU, split, level pipeline)
+HOST_FED = {"host_fed_vga": (640, 480, 1000, 3072, HEADLINE_SPLIT, HEADLINE_PIPE),
+            "host_fed_fhd": (1920, 1080, 1000, 192, 1, 0)}
 
 # Config C5 (BASELINE.json configs[4]): 64 FHD RGB-D streams over the job's
 # GPUs (stream s -> rank s mod G), plus the cross-stream keyframe exchange.
@@ -1062,6 +1150,8 @@ def main() -> int:
             res = dropin_latency(torch, dev)
         if args.extra == "matchers":   # the drop-in ORBmatcher calls (host arrays), per call
             res = matcher_latencies()
+        if args.extra in ("host_fed_vga", "host_fed_fhd"):
+            res = host_fed(torch, dev, *HOST_FED[args.extra], args.steps, args.warmup)
         if args.extra in ("c5_rank8", "c5_rank8_k8"):   # one rank's share of C5 at 8 GPUs
             res = c5_config(torch, dist, rank, world, dev, args.steps, args.warmup, profile, *c5_args, total=8,
                             kframes=8 if args.extra == "c5_rank8_k8" else 1, exchange=False)
@@ -1165,6 +1255,8 @@ def main() -> int:
                 extras[f"c5_rank_share_8_streams_k{kk}"] = c5_config(
                     torch, dist, rank, world, dev, max(5, args.steps // 4), 2, profile, total=8, kframes=kk,
                     exchange=False)
+            for key, cfg in HOST_FED.items():
+                extras[key] = host_fed(torch, dev, *cfg, max(8, args.steps // 4), 2)
             extras["dropin_latency"] = dropin_latency(torch, dev)
             extras["bow_transform_orbvoc"] = bow_transform_throughput(torch)
             extras["keyframe_db_loop_query"] = kfdb_latency()

@@ -36,8 +36,6 @@
 #include <unordered_set>
 #include <vector>
 
-#include <hipcub/hipcub.hpp>
-
 #include "orbx_device.h"
 #include "orbx_wave.h"
 #include "orbx_ws.h"
@@ -118,6 +116,71 @@ __global__ __launch_bounds__(kKT) void k_csr_fill(const SlotDev *slots, int nslo
     for (int i = lane; i < sl.n; i += 64) {
         const uint32_t w = words[sl.off + i];
         post[off[w] + atomicAdd(&fill[w], 1u)] = s;
+    }
+}
+
+// Exclusive prefix sum of the posting counts (n = V + 1 words, up to ~1 M for
+// ORBvoc), in three launches: tile sums (1024 threads x 4 counts a tile),
+// one workgroup scanning the tile sums, then each tile's own scan offset by
+// its tile's prefix.  Runs once per rebuild of the inverted file.
+constexpr int kScanT = 1024, kScanTile = 4 * kScanT;
+
+// exclusive scan of v over the workgroup; *total = the workgroup's sum
+__device__ inline uint32_t block_excl_scan_u32(uint32_t v, uint32_t *total, uint32_t *ws) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t incl = (uint32_t)wave_incl_scan_i32((int)v);
+    if (lane == 63) ws[w] = incl;
+    __syncthreads();
+    uint32_t base = 0, all = 0;
+    for (int k = 0; k < kScanT / 64; ++k) {
+        const uint32_t t = ws[k];
+        base += k < w ? t : 0u;
+        all += t;
+    }
+    __syncthreads();   // (ws reusable)
+    *total = all;
+    return base + incl - v;
+}
+
+__device__ inline uint4 scan_load4(const uint32_t *in, int n, int i) {
+    if (i + 3 < n) return *reinterpret_cast<const uint4 *>(in + i);
+    return make_uint4(i < n ? in[i] : 0u, i + 1 < n ? in[i + 1] : 0u, i + 2 < n ? in[i + 2] : 0u, 0u);
+}
+
+__global__ __launch_bounds__(kScanT) void k_scan_tiles(const uint32_t *in, int n, uint32_t *tsum) {
+    __shared__ uint32_t ws[kScanT / 64];
+    const uint4 v = scan_load4(in, n, blockIdx.x * kScanTile + 4 * threadIdx.x);
+    uint32_t total;
+    (void)block_excl_scan_u32(v.x + v.y + v.z + v.w, &total, ws);
+    if (threadIdx.x == 0) tsum[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kScanT) void k_scan_top(uint32_t *tsum, int nt) {
+    __shared__ uint32_t ws[kScanT / 64];
+    uint32_t carry = 0;
+    for (int b = 0; b < nt; b += kScanT) {
+        const int i = b + threadIdx.x;
+        const uint32_t v = i < nt ? tsum[i] : 0u;
+        uint32_t total;
+        const uint32_t ex = block_excl_scan_u32(v, &total, ws);
+        if (i < nt) tsum[i] = carry + ex;
+        carry += total;
+    }
+}
+
+__global__ __launch_bounds__(kScanT) void k_scan_apply(const uint32_t *in, int n, const uint32_t *tsum, uint32_t *out) {
+    __shared__ uint32_t ws[kScanT / 64];
+    const int i = blockIdx.x * kScanTile + 4 * threadIdx.x;
+    const uint4 v = scan_load4(in, n, i);
+    uint32_t total;
+    const uint32_t e0 = tsum[blockIdx.x] + block_excl_scan_u32(v.x + v.y + v.z + v.w, &total, ws);
+    const uint32_t e1 = e0 + v.x, e2 = e1 + v.y, e3 = e2 + v.z;
+    if (i + 3 < n) {
+        *reinterpret_cast<uint4 *>(out + i) = make_uint4(e0, e1, e2, e3);
+    } else {
+        if (i < n) out[i] = e0;
+        if (i + 1 < n) out[i + 1] = e1;
+        if (i + 2 < n) out[i + 2] = e2;
     }
 }
 
@@ -401,7 +464,7 @@ struct orbx_kfdb {
     int32_t *d_qcnt = nullptr;   // per-slot query scratch
     uint32_t *d_qfirst = nullptr;
     // the device inverted file over slots [0, csr_ns): postings by word id
-    uint32_t *d_csr_off = nullptr, *d_csr_cnt = nullptr;
+    uint32_t *d_csr_off = nullptr, *d_csr_cnt = nullptr, *d_csr_tsum = nullptr;   // (tsum: the scan's tile sums)
     int32_t *d_csr_slot = nullptr;
     uint32_t csr_V = 0;
     int csr_ns = 0;
@@ -523,10 +586,11 @@ int kfdb_sync(orbx_kfdb *db) {
         const int64_t V = (int64_t)db->max_word + 1, P = std::max<int64_t>(db->dev_words, 1);
         if (V + 1 > db->csr_cap_V) {
             const int64_t cap = (V + 1) * 2;
-            for (uint32_t **x : {&db->d_csr_off, &db->d_csr_cnt})
+            for (uint32_t **x : {&db->d_csr_off, &db->d_csr_cnt, &db->d_csr_tsum})
                 if (*x) { (void)hipStreamSynchronize(db->st); (void)hipFree(*x); *x = nullptr; }
             if (hipMalloc(reinterpret_cast<void **>(&db->d_csr_off), 4 * cap) != hipSuccess ||
-                hipMalloc(reinterpret_cast<void **>(&db->d_csr_cnt), 4 * cap) != hipSuccess)
+                hipMalloc(reinterpret_cast<void **>(&db->d_csr_cnt), 4 * cap) != hipSuccess ||
+                hipMalloc(reinterpret_cast<void **>(&db->d_csr_tsum), 4 * (cap / kScanTile + 1)) != hipSuccess)
                 return ORBX_ENOMEM;
             db->csr_cap_V = cap;
         }
@@ -539,21 +603,16 @@ int kfdb_sync(orbx_kfdb *db) {
         const dim3 grid((ns + kKT / 64 - 1) / (kKT / 64));
         if (hipMemsetAsync(db->d_csr_cnt, 0, 4 * (size_t)(V + 1), db->st) != hipSuccess) return ORBX_EIO;
         hipLaunchKernelGGL(k_csr_count, grid, dim3(kKT), 0, db->st, db->d_slots, ns, db->d_words, db->d_csr_cnt);
-        size_t tmp = 0;
-        if (hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, db->d_csr_cnt, db->d_csr_off, (int)(V + 1), db->st) !=
-            hipSuccess)
-            return ORBX_EIO;
-        void *d_tmp = nullptr;
-        if (hipMalloc(&d_tmp, std::max<size_t>(tmp, 16)) != hipSuccess) return ORBX_ENOMEM;
-        const bool ok =
-            hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp, db->d_csr_cnt, db->d_csr_off, (int)(V + 1), db->st) ==
-                hipSuccess &&
-            hipMemsetAsync(db->d_csr_cnt, 0, 4 * (size_t)(V + 1), db->st) == hipSuccess;
+        const int nscan = (int)(V + 1), ntile = (nscan + kScanTile - 1) / kScanTile;
+        hipLaunchKernelGGL(k_scan_tiles, dim3(ntile), dim3(kScanT), 0, db->st, db->d_csr_cnt, nscan, db->d_csr_tsum);
+        hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kScanT), 0, db->st, db->d_csr_tsum, ntile);
+        hipLaunchKernelGGL(k_scan_apply, dim3(ntile), dim3(kScanT), 0, db->st, db->d_csr_cnt, nscan, db->d_csr_tsum,
+                           db->d_csr_off);
+        const bool ok = hipMemsetAsync(db->d_csr_cnt, 0, 4 * (size_t)(V + 1), db->st) == hipSuccess;
         if (ok)
             hipLaunchKernelGGL(k_csr_fill, grid, dim3(kKT), 0, db->st, db->d_slots, ns, db->d_words, db->d_csr_off,
                                db->d_csr_cnt, db->d_csr_slot);
         (void)hipStreamSynchronize(db->st);
-        (void)hipFree(d_tmp);
         if (!ok || hipGetLastError() != hipSuccess) return ORBX_EIO;
         db->csr_ns = ns;
         db->csr_V = (uint32_t)V;
@@ -804,7 +863,7 @@ void orbx_kfdb_destroy(orbx_kfdb *db) {
     if (db->d_slots) (void)hipFree(db->d_slots);
     if (db->d_state) (void)hipFree(db->d_state);
     for (void *x : {(void *)db->d_qcnt, (void *)db->d_qfirst, (void *)db->d_qbuf, (void *)db->d_csr_off,
-                    (void *)db->d_csr_cnt, (void *)db->d_csr_slot})
+                    (void *)db->d_csr_cnt, (void *)db->d_csr_tsum, (void *)db->d_csr_slot})
         if (x) (void)hipFree(x);
     if (db->st) (void)hipStreamDestroy(db->st);
     delete db;

@@ -734,6 +734,15 @@ int ws_copy_sync(CallWs &ws, size_t off, size_t bytes) {
     return hipStreamSynchronize(ws.st) == hipSuccess ? ORBX_OK : ORBX_EIO;
 }
 
+// The same copy, its completion polled (hipStreamQuery) instead of waited for.
+int ws_copy_spin(CallWs &ws, size_t off, size_t bytes) {
+    if (bytes && hipMemcpyAsync(ws.host + off, ws.dev + off, bytes, hipMemcpyDeviceToHost, ws.st) != hipSuccess)
+        return ORBX_EIO;
+    hipError_t e;
+    while ((e = hipStreamQuery(ws.st)) == hipErrorNotReady) __builtin_ia32_pause();
+    return e == hipSuccess ? ORBX_OK : ORBX_EIO;
+}
+
 void ws_arm(CallWs &ws) {
     *reinterpret_cast<volatile uint32_t *>(ws.flag) = 0;
     std::atomic_thread_fence(std::memory_order_seq_cst);
@@ -1810,11 +1819,20 @@ int proj_run(int device, int variant, orbx_proj_problem *P, int np, int th_dist,
         put(ws, o_pa, hb.data(), sizeof(ProjBufs) * nl);
         std::memset(ws.host + o_cnt, 0, 16 + 8 * (size_t)nl);
         if (hipMemcpyAsync(D, ws.host, in_bytes, hipMemcpyHostToDevice, ws.st) != hipSuccess) return ORBX_EIO;
-        HostTail tail;
-        ws_tail(ws, o_cnt, out_end - o_cnt, at<uint32_t>(D, o_cnt + 8 + 8 * (size_t)nl), proj_tail_blocks(hb.data(), nl),
-                tail);
+        // Outputs: one copy whose completion the host polls (ORBX_PROJ_TAIL=2,
+        // the default).  The replay's workgroup writing them into pinned
+        // memory itself (1) measured 7-10 us slower a call, the copy waited
+        // for by a stream synchronisation (0) 1-3 us (profiles/r05_ab_proj_call.txt).
+        HostTail tail{};
+        static const int tail_mode = std::getenv("ORBX_PROJ_TAIL") ? std::atoi(std::getenv("ORBX_PROJ_TAIL")) : 2;
+        if (tail_mode == 1)
+            ws_tail(ws, o_cnt, out_end - o_cnt, at<uint32_t>(D, o_cnt + 8 + 8 * (size_t)nl),
+                    proj_tail_blocks(hb.data(), nl), tail);
         if (launch_proj(hb.data(), at<ProjBufs>(D, o_pa), nl, tail, ws.st) != hipSuccess) return ORBX_EIO;
-        if (ws_wait(ws, tail, o_cnt, out_end - o_cnt)) return ORBX_EIO;
+        if (tail_mode == 1 ? ws_wait(ws, tail, o_cnt, out_end - o_cnt)
+                           : tail_mode == 2 ? ws_copy_spin(ws, o_cnt, out_end - o_cnt)
+                                            : ws_copy_sync(ws, o_cnt, out_end - o_cnt))
+            return ORBX_EIO;
         unsigned long long used = 0;
         get(ws, o_cnt, &used, 8);
         if (dbg_stats) {
@@ -2043,11 +2061,17 @@ int bow_run(int device, int variant, orbx_bow_problem *P, int np, float nnratio,
     clk.mark();   // layout + staging copies
     if (hipMemcpyAsync(D, ws.host, cnt_end, hipMemcpyHostToDevice, ws.st) != hipSuccess) return ORBX_EIO;
     const size_t o_out = o[0].ma;   // match arrays and counters are one contiguous run
-    HostTail tail;
-    ws_tail(ws, o_out, cnt_end - o_out, at<uint32_t>(D, o_done), bow_tail_blocks(hb.data(), nl), tail);
+    HostTail tail{};
+    // 1: the match kernel's last workgroup runs the rotation pass and copies
+    // the outputs into pinned memory (one launch); 2: match + finish launches,
+    // then one copy whose completion the host polls
+    static const int tail_mode = std::getenv("ORBX_BOW_TAIL") ? std::atoi(std::getenv("ORBX_BOW_TAIL")) : 1;
+    if (tail_mode == 1)
+        ws_tail(ws, o_out, cnt_end - o_out, at<uint32_t>(D, o_done), bow_tail_blocks(hb.data(), nl), tail);
     if (launch_bow(hb.data(), at<BowBufs>(D, o_pa), nl, tail, ws.st) != hipSuccess) return ORBX_EIO;
     clk.mark();   // enqueue
-    if (ws_wait(ws, tail, o_out, cnt_end - o_out)) return ORBX_EIO;
+    if (tail_mode == 1 ? ws_wait(ws, tail, o_out, cnt_end - o_out) : ws_copy_spin(ws, o_out, cnt_end - o_out))
+        return ORBX_EIO;
     clk.mark();   // wait
     for (int t = 0; t < nl; ++t) {
         orbx_bow_problem &pr = P[live[t]];

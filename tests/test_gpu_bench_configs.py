@@ -82,6 +82,42 @@ def test_mono_bench_config_b3072(oracle_mod):
     ex.close()
 
 
+MONO_EXTRAS = [(w, h, nf, B) for key, mode, w, h, nf, B, _ in bench.EXTRAS if mode == "mono"]
+
+
+@pytest.mark.parametrize("w,h,nf,B", MONO_EXTRAS)
+def test_mono_extra_bench_configs(w, h, nf, B, oracle_mod):
+    """The mono extras at the batches and split / pipeline settings bench.py
+    times them (HD 1280x720 at 384 streams, FHD at 192, both unsplit): two
+    steps, every stream equal to its scene's, sampled streams vs the oracle."""
+    import torch
+    key = next(k for k, m, ww, hh, _, _, _ in bench.EXTRAS if m == "mono" and (ww, hh) == (w, h))
+    streams = list(range(B))
+    host, _, fr, _ = _frames(torch, "mono", w, h, streams)
+    ex = ORBextractor(nf, 1.2, 8, 20, 7)
+    ex.reserve(w, h, B)
+    ex.split(bench.EXTRA_SPLIT.get(key, 2))   # (as bench.py times it)
+    ex.pipeline(bench.EXTRA_PIPE.get(key, 0))
+    for t in range(2):
+        ex.mono_step_device(fr[t].data_ptr(), w * h, w, B, 100, 0.9, True)
+    torch.cuda.synchronize()
+    outs = [ex.batch_download(b) for b in range(B)]
+    matches = [ex.mono_matches_download(b) for b in range(B)]
+    for b in range(B):
+        r = bench.stream_scene(b)
+        assert _kp_equal(outs[b][0], outs[r][0]) and np.array_equal(outs[b][1], outs[r][1]), f"stream {b}"
+        assert matches[b][1] == matches[r][1] and np.array_equal(matches[b][0], matches[r][0]), f"stream {b}"
+    for b in [0, 1, B // 2 - 1, B // 2, B - 1]:
+        k1, d1 = oracle_mod.extract(host[0, b], nf)
+        k2, d2 = oracle_mod.extract(host[1, b], nf)
+        assert _kp_equal(outs[b][0], k2) and np.array_equal(outs[b][1], d2), f"stream {b} extract"
+        prev = np.ascontiguousarray(np.stack([k1["x"], k1["y"]], 1).astype(np.float32))
+        nm, m12, _ = oracle_mod.search_for_initialization(k1, d1, k2, d2, w, h, prev, 100, 0.9, True)
+        assert matches[b][1] == nm and np.array_equal(matches[b][0], m12), f"stream {b} matches"
+        assert nm > 0
+    ex.close()
+
+
 STEREO_CONFIGS = [   # bench.py EXTRAS: (w, h, nfeatures, pairs, split, level pipeline as bench.py runs it)
     (752, 480, 1200, 256, 2, 0),
     (1241, 376, 2000, 144, 2, 0),

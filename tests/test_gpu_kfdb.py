@@ -181,3 +181,24 @@ def test_kfdb_rejects_word_ids_past_the_bound():
     with pytest.raises(OrbxError):
         db.add(3, np.array([0xFFFFFFFF], np.uint32), np.array([1.0]))
     assert db.size() == 1
+
+
+def test_kfdb_orbvoc_sized_word_ids(oracle_mod):
+    """Word ids over ORBvoc's whole range (10^6 words): the inverted file's
+    count scan spans ~245 tiles of the three-launch scan; rebuilt several
+    times as keyframes arrive."""
+    from orb_slam_2_ros_amd.synth_vocab import make_keyframe_bows
+    bows, covis = make_keyframe_bows(n_kf=900, n_words=1_000_000, words_per_kf=800, seed=21, loop_every=90)
+    g, o = KeyFrameDatabase(), oracle_mod.KeyFrameDB(1_000_000)
+    cv = lambda k: covis.get(k, [])   # noqa: E731
+    hits = 0
+    for i, (w, v) in enumerate(bows):
+        if i and i % 60 == 0:
+            a = g.DetectLoopCandidates(i, w, v, covis[i], 0.01, cv)
+            assert a == o.detect(False, i, w, v, covis[i], 0.01, cv)
+            r = g.DetectRelocalizationCandidates(10_000 + i, w, v, cv)
+            assert r == o.detect(True, 10_000 + i, w, v, None, 0.0, cv)
+            hits += len(a) > 0
+        g.add(i, w, v)
+        o.add(i, w, v)
+    assert hits > 0
