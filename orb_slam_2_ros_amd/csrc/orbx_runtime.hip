@@ -401,8 +401,7 @@ int reserve(orbx_extractor *ex, int w, int h, int max_batch) {
     if (so && so[0] == '1' && B >= 4 && p.max_kps <= 65535)
         ok &= dalloc(&ex->d_bands, (size_t)(B / 2) * stereo_band_stride(p.height, p.max_kps)) == hipSuccess;
     if (B >= 2) {   // (zero; the fused cut's last workgroup resets its pair's counter)
-        ok &= dalloc(&ex->d_pair_done, B / 2) == hipSuccess;
-        ok &= ok && hipMemset(ex->d_pair_done, 0, sizeof(int32_t) * (B / 2)) == hipSuccess;
+        ok &= dalloc(&ex->d_pair_done, B / 2) == hipSuccess;   // (zeroed before each fused launch)
     }
     if (!ok) { ex->release(); return ORBX_ENOMEM; }
     ex->planned = true;
@@ -1501,6 +1500,10 @@ int orbx_stereo_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t
         // only with ORBX_STEREO_FUSED_CUT=1
         const char *e = std::getenv("ORBX_STEREO_FUSED_CUT");
         a.pair_done = (e && e[0] == '1') ? ex->d_pair_done : nullptr;
+        // each launch starts from zeroed counters (a failed launch cannot leave
+        // them counting for the next one)
+        if (a.pair_done && hipMemsetAsync(a.pair_done, 0, sizeof(int32_t) * (size_t)pairs, st) != hipSuccess)
+            return ORBX_EIO;
     }
     if (launch_stereo(a, pairs, kcap, st) != hipSuccess) return ORBX_EIO;
     mark(ex, kNumStages, st);
