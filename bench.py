@@ -455,18 +455,26 @@ def local_ba_latency(reps=3):
     P = make_ba_problem(n_local=20, n_fixed=4, n_points=3000, seed=2)
     args = (P["Tcw"], P["fixed"], P["Xw"], P["edges"])
     local_bundle_adjustment(*args)
-    tg, to = [], []
+    local_bundle_adjustment(*args, fast=True)
+    tg, tf, to = [], [], []
     for _ in range(reps):
         t0 = time.perf_counter()
         g = local_bundle_adjustment(*args)
         tg.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        f = local_bundle_adjustment(*args, fast=True)
+        tf.append(time.perf_counter() - t0)
         t0 = time.perf_counter()
         o = oracle.local_ba(*args)
         to.append(time.perf_counter() - t0)
     assert np.array_equal(g[0], o[0]) and np.array_equal(g[2], o[2])
     return {"keyframes": 24, "points": 3000, "observations": int(len(P["edges"])), "lm_iterations": list(g[3]),
             "gpu_ms": round(1e3 * float(np.median(tg)), 3), "cpu_ms": round(1e3 * float(np.median(to)), 3),
-            "cpu_kind": "port, 1 thread, same summation order"}
+            "cpu_kind": "port, 1 thread, same summation order",
+            "fast_mode": {"gpu_ms": round(1e3 * float(np.median(tf)), 3), "lm_iterations": list(f[3]),
+                          "outliers_identical": bool(np.array_equal(f[2], o[2])),
+                          "max_abs_pose_diff": float(np.abs(f[0] - o[0]).max()),
+                          "max_rel_point_diff": float(np.abs(f[1] - o[1]).max() / np.abs(o[1]).max())}}
 
 
 def keyframe_exchange(torch, dist, world, dev, kfs_per_rank=8, nkp=1000, reps=10):

@@ -145,6 +145,7 @@ _SIGNATURES = {
     "orbx_kfdb_detect_relocalization_candidates": (I32, [P, ctypes.c_uint64, P, P, I32, P, P, P, I32, P]),
     "orbx_bow_score_l1": (I32, [P, P, I32, P, P, I32, P]),
     "orbx_local_ba": (I32, [I32, P, P, I32, P, I32, P, I32, I32, I32, P, P, P, P]),
+    "orbx_local_ba_fast": (I32, [I32, P, P, I32, P, I32, P, I32, I32, I32, P, P, P, P]),
     "orbx_ba_debug_step": (I32, [I32, P, P, I32, P, I32, P, I32, I32, ctypes.c_double, P, P, P]),
 }
 
@@ -174,8 +175,14 @@ def load(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     except ImportError:
         pass
     lib = ctypes.CDLL(str(p))
+    alt = path is None and "ORBX_LIB" in os.environ
     for name, (res, args) in _SIGNATURES.items():
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            if alt:   # an older build under A/B timing may predate an entry point
+                continue
+            raise
         fn.restype = res
         fn.argtypes = args
     if path is None:

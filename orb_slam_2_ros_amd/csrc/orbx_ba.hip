@@ -598,8 +598,39 @@ __device__ double ordered_colsum(const double *base, int nrows, double acc, doub
     return acc;
 }
 
+// The fast mode's column sums (orbx_local_ba_fast): thread t adds field
+// t % NF of rows t / NF, t / NF + G, ... (G = kSumThreads / NF groups; the
+// loads coalesced, each thread's chain nrows / G long), then lane f < NF adds
+// the G partial sums.  Same terms, another order: equal to rounding.
+template <int NF, bool SUB>
+__device__ double tree_colsum(const double *base, int nrows, double acc, double *buf) {
+    constexpr int G = kSumThreads / NF;
+    const int tid = threadIdx.x, f = tid % NF, g = tid / NF;
+    double part = 0.0;
+    if (g < G) {
+        const double *src = base + f;
+        int r = g;
+        for (; r + 3 * G < nrows; r += 4 * G) {   // four rows in flight per thread
+            const double a0 = src[(int64_t)r * NF], a1 = src[(int64_t)(r + G) * NF], a2 = src[(int64_t)(r + 2 * G) * NF],
+                         a3 = src[(int64_t)(r + 3 * G) * NF];
+            part += (a0 + a1) + (a2 + a3);
+        }
+        for (; r < nrows; r += G) part += src[(int64_t)r * NF];
+        buf[g * NF + f] = part;
+    }
+    __syncthreads();
+    if (tid < NF) {
+        double s = 0.0;
+        for (int k = 0; k < G; ++k) s += buf[k * NF + tid];
+        acc = SUB ? acc - s : acc + s;
+    }
+    __syncthreads();
+    return acc;
+}
+
 // S_{i1 i2} (+ lambda I on the diagonal blocks) - the pair's terms in point
 // order, written with its mirror (the solver reads the full matrix)
+template <bool FAST>
 __global__ __launch_bounds__(kSumThreads) void k_ba_pairs_sum(const int2 *pairs, const int32_t *moffs,
                                                               const double *terms, const double *Hpp, double lambda,
                                                               int nf, double *S) {
@@ -612,7 +643,8 @@ __global__ __launch_bounds__(kSumThreads) void k_ba_pairs_sum(const int2 *pairs,
         if (r == c) acc = acc + lambda;
     }
     const int t0 = moffs[pi];
-    acc = ordered_colsum<36, true>(terms + 36 * (int64_t)t0, moffs[pi + 1] - t0, acc, sbuf);
+    if constexpr (FAST) acc = tree_colsum<36, true>(terms + 36 * (int64_t)t0, moffs[pi + 1] - t0, acc, sbuf);
+    else acc = ordered_colsum<36, true>(terms + 36 * (int64_t)t0, moffs[pi + 1] - t0, acc, sbuf);
     if (lane >= 36) return;
     const int n = 6 * nf;
     S[(int64_t)(6 * i1 + r) * n + 6 * i2 + c] = acc;
@@ -621,14 +653,15 @@ __global__ __launch_bounds__(kSumThreads) void k_ba_pairs_sum(const int2 *pairs,
 
 // out[v] = (minus[v] -) the ordered sum of the vertex's rows; fields [0, na)
 // to out_a, the rest to out_b
-template <int NF>
+template <int NF, bool FAST>
 __global__ __launch_bounds__(kSumThreads) void k_ba_stream_sums(const double *rows, const int32_t *offs,
                                                                 const double *minus, double *out_a, int na,
                                                                 double *out_b) {
     extern __shared__ double sbuf[];
     const int v = blockIdx.x, lane = threadIdx.x;
     const int t0 = offs[v];
-    const double acc = ordered_colsum<NF, false>(rows + NF * (int64_t)t0, offs[v + 1] - t0, 0.0, sbuf);
+    const double acc = FAST ? tree_colsum<NF, false>(rows + NF * (int64_t)t0, offs[v + 1] - t0, 0.0, sbuf)
+                            : ordered_colsum<NF, false>(rows + NF * (int64_t)t0, offs[v + 1] - t0, 0.0, sbuf);
     if (lane >= NF) return;
     if (lane < na) out_a[(int64_t)v * na + lane] = minus ? minus[(int64_t)v * na + lane] - acc : acc;
     else out_b[(int64_t)v * (NF - na) + lane - na] = acc;
@@ -641,7 +674,9 @@ bool sum_lds(K kernel) {
                                (int)kSumLds) == hipSuccess;
 }
 bool sums_ready() {
-    static const bool ok = sum_lds(k_ba_pairs_sum) && sum_lds(k_ba_stream_sums<6>) && sum_lds(k_ba_stream_sums<42>);
+    static const bool ok = sum_lds(k_ba_pairs_sum<false>) && sum_lds(k_ba_stream_sums<6, false>) &&
+                           sum_lds(k_ba_stream_sums<42, false>) && sum_lds(k_ba_pairs_sum<true>) &&
+                           sum_lds(k_ba_stream_sums<6, true>) && sum_lds(k_ba_stream_sums<42, true>);
     return ok;
 }
 
@@ -700,6 +735,73 @@ __device__ inline double readlane_f64(double v, int l) {
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
     return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
+
+// The fast mode's factorisation (orbx_local_ba_fast; n <= kCholLds): right-
+// looking, one column a step, every thread on the trailing update with fused
+// multiply-adds -- thread (ty, tx) of a 32 x 32 grid owns the entries
+// (i, j), i = ty mod 32, j = tx mod 32, j <= i -- and one barrier a step: the
+// column's entries are read unscaled (multiplied by 1 / L(k, k)) and the
+// scaled ones go to the unused upper triangle (U(k, i) = L(i, k)), so no
+// entry a step reads is written in it; the next diagonal's owner takes its
+// square root and reciprocal before the barrier.  Then the two solves by
+// wave 0 (lane r owns rows r and r + 64, column sweeps, readlane broadcasts).
+// Not the oracle's operation order: equal to rounding.
+__global__ __launch_bounds__(1024) void k_ba_chol_fast(const double *S, int n, const double *bs, double *x, int *ok) {
+    extern __shared__ double L[];   // n rows of n+1 (lower: the working matrix; upper: scaled columns), then dg, inv
+    __shared__ int bad;
+    const int ld = n + 1, tid = threadIdx.x, tx = tid & 31, ty = tid >> 5;
+    double *dg = L + n * ld, *inv = dg + n;
+    for (int q = tid; q < n * n; q += 1024) {
+        const int r = q / n, c = q - r * n;
+        if (c <= r) L[r * ld + c] = S[q];
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const double d0 = L[0];
+        bad = !(d0 > 0);
+        dg[0] = sqrt(d0);
+        inv[0] = 1.0 / dg[0];
+    }
+    __syncthreads();
+    for (int k = 0; k < n && !bad; ++k) {
+        const double ik = inv[k];
+        // scaled column k to the upper triangle (row k, columns > k)
+        for (int i = k + 1 + tid; i < n; i += 1024) L[k * ld + i] = L[i * ld + k] * ik;
+        const double ik2 = ik * ik;
+        const int j0 = k + 1 + ((tx - (k + 1)) & 31);   // this thread's first column > k
+        for (int i = k + 1 + ((ty - (k + 1)) & 31); i < n; i += 32) {
+            const double li = L[i * ld + k] * ik2;
+            for (int j = j0; j <= i; j += 32) L[i * ld + j] = fma(-li, L[j * ld + k], L[i * ld + j]);
+            if (i == k + 1 && j0 == k + 1) {   // the next diagonal, final now
+                const double d = L[(k + 1) * ld + k + 1];
+                if (!(d > 0)) bad = 1;
+                dg[k + 1] = sqrt(d);
+                inv[k + 1] = 1.0 / dg[k + 1];
+            }
+        }
+        __syncthreads();
+    }
+    if (tid >= 64) return;
+    if (tid == 0) *ok = !bad;
+    if (bad) return;
+    const int lane = tid;
+    double y0 = lane < n ? bs[lane] : 0.0, y1 = lane + 64 < n ? bs[lane + 64] : 0.0;
+    for (int k = 0; k < n; ++k) {   // L y = b: L(i, k) = U(k, i) = L[k * ld + i]
+        const double yk = readlane_f64(k < 64 ? y0 : y1, k & 63) * inv[k];
+        if (lane == (k & 63)) { if (k < 64) y0 = yk; else y1 = yk; }
+        if (lane > k && lane < n) y0 = fma(-L[k * ld + lane], yk, y0);
+        if (lane + 64 > k && lane + 64 < n) y1 = fma(-L[k * ld + lane + 64], yk, y1);
+    }
+    for (int k = n - 1; k >= 0; --k) {   // L^T x = y: L(k, i) for i < k = U(i, k) = L[i * ld + k]
+        const double xk = readlane_f64(k < 64 ? y0 : y1, k & 63) * inv[k];
+        if (lane == (k & 63)) { if (k < 64) y0 = xk; else y1 = xk; }
+        if (lane < k) y0 = fma(-L[lane * ld + k], xk, y0);
+        if (lane + 64 < k) y1 = fma(-L[(lane + 64) * ld + k], xk, y1);
+    }
+    if (lane < n) x[lane] = y0;
+    if (lane + 64 < n) x[lane + 64] = y1;
+}
+
 
 // The same factorisation and solves with S held in LDS (n <= kCholLds),
 // blocked right-looking in panels of kPanel columns:
@@ -1160,6 +1262,7 @@ public:
     Graph &g_;
     hipStream_t st_;
     BAWs &ws_;
+    bool fast_ = false;   // orbx_local_ba_fast: parallel sums and factorisation (equal to rounding)
     uint8_t *buf_ = nullptr;
     Pose *d_pose = nullptr, *d_pose_bk = nullptr;
     double *d_pts = nullptr, *d_pts_bk = nullptr;
@@ -1426,8 +1529,12 @@ int BA::build() {
             hipLaunchKernelGGL((k_ba_gather_rows<42, 1>), dim3((unsigned)(((int64_t)nl * 42 + 255) / 256)), dim3(256), 0,
                                st_, reinterpret_cast<const double *>(d_eo), kEo, d_cvlist, nl, d_active, d_rows);
         if (!sums_ready()) return ORBX_EIO;
-        hipLaunchKernelGGL((k_ba_stream_sums<42>), dim3(g.nf), dim3(kSumThreads), kSumLds, st_, d_rows, d_cvoffs, nullptr, d_Hpp, 36,
-                           d_bp);
+        if (fast_)
+            hipLaunchKernelGGL((k_ba_stream_sums<42, true>), dim3(g.nf), dim3(kSumThreads), kSumLds, st_, d_rows,
+                               d_cvoffs, nullptr, d_Hpp, 36, d_bp);
+        else
+            hipLaunchKernelGGL((k_ba_stream_sums<42, false>), dim3(g.nf), dim3(kSumThreads), kSumLds, st_, d_rows,
+                               d_cvoffs, nullptr, d_Hpp, 36, d_bp);
     }
     if (g.npt) hipLaunchKernelGGL(k_ba_reduce, dim3((g.npt + 3) / 4), dim3(256), 0, st_, d_eo, d_poffs, d_plist,
                                   d_active, g.npt, 1, d_Hll, d_bl);
@@ -1477,8 +1584,12 @@ int BA::solve_async(double lambda) {
             if (nterms)
                 hipLaunchKernelGGL(k_ba_pair_terms, dim3((unsigned)((nterms + 255) / 256)), dim3(256), 0, st_, d_mlist,
                                    nterms, d_moffs + npairs, d_eo, d_bdinv, d_terms);
-            hipLaunchKernelGGL(k_ba_pairs_sum, dim3(npairs), dim3(kSumThreads), kSumLds, st_, d_pairs, d_moffs, d_terms, d_Hpp,
-                               lambda, g.nf, d_S);
+            if (fast_)
+                hipLaunchKernelGGL(k_ba_pairs_sum<true>, dim3(npairs), dim3(kSumThreads), kSumLds, st_, d_pairs,
+                                   d_moffs, d_terms, d_Hpp, lambda, g.nf, d_S);
+            else
+                hipLaunchKernelGGL(k_ba_pairs_sum<false>, dim3(npairs), dim3(kSumThreads), kSumLds, st_, d_pairs,
+                                   d_moffs, d_terms, d_Hpp, lambda, g.nf, d_S);
         }
         else
             hipLaunchKernelGGL(k_ba_pairs, dim3((npairs + 3) / 4), dim3(256), 0, st_, d_pairs, npairs, d_coffs,
@@ -1487,9 +1598,19 @@ int BA::solve_async(double lambda) {
         if (nusable_)
             hipLaunchKernelGGL((k_ba_gather_rows<6, 0>), dim3((unsigned)(((int64_t)nusable_ * 6 + 255) / 256)),
                                dim3(256), 0, st_, d_bdb, 6, d_clist, nusable_, nullptr, d_rows);
-        hipLaunchKernelGGL((k_ba_stream_sums<6>), dim3(g.nf), dim3(kSumThreads), kSumLds, st_, d_rows, d_coffs, d_bp, d_bs, 6,
-                           nullptr);
-        if (n <= kCholLds) {
+        if (fast_)
+            hipLaunchKernelGGL((k_ba_stream_sums<6, true>), dim3(g.nf), dim3(kSumThreads), kSumLds, st_, d_rows,
+                               d_coffs, d_bp, d_bs, 6, nullptr);
+        else
+            hipLaunchKernelGGL((k_ba_stream_sums<6, false>), dim3(g.nf), dim3(kSumThreads), kSumLds, st_, d_rows,
+                               d_coffs, d_bp, d_bs, 6, nullptr);
+        if (fast_ && n <= kCholLds) {
+            const int lb = 8 * (n * (n + 1) + 2 * n);
+            if (lb > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void *>(k_ba_chol_fast),
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize, lb) != hipSuccess)
+                return ORBX_EIO;
+            hipLaunchKernelGGL(k_ba_chol_fast, dim3(1), dim3(1024), lb, st_, d_S, n, d_bs, d_x, d_ok);
+        } else if (n <= kCholLds) {
             const int lb = 8 * (n * (n + 1) + n);
             if (lb > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void *>(k_ba_chol_lds),
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, lb) != hipSuccess)
@@ -1685,9 +1806,9 @@ int build_graph(const float *Tcw, const uint8_t *fixed, int ncam, int npt, const
 
 extern "C" {
 
-int orbx_local_ba(int device, const float *Tcw, const uint8_t *fixed, int ncam, const float *Xw, int npt,
-                  const orbx_ba_edge *edges, int ne, int iters1, int iters2, float *Tcw_out, float *Xw_out,
-                  uint8_t *outlier, int *iterations) {
+static int local_ba(int device, bool fast, const float *Tcw, const uint8_t *fixed, int ncam, const float *Xw, int npt,
+                    const orbx_ba_edge *edges, int ne, int iters1, int iters2, float *Tcw_out, float *Xw_out,
+                    uint8_t *outlier, int *iterations) {
     if (ncam < 0 || npt < 0 || ne < 0 || iters1 < 0 || iters2 < 0 || (ncam && (!Tcw || !fixed || !Tcw_out)) ||
         (npt && (!Xw || !Xw_out)) || (ne && (!edges || !outlier)))
         return ORBX_EINVAL;
@@ -1721,6 +1842,7 @@ int orbx_local_ba(int device, const float *Tcw, const uint8_t *fixed, int ncam, 
     int its[2] = {0, 0};
     {
         BA ba(g, ws);
+        ba.fast_ = fast;
         if ((rc = ba.alloc()) || (rc = ba.upload(pts.data()))) return rc;
         lap("alloc+upload");
         (void)hipMemsetAsync(ba.d_chi2, 0, 8 * (size_t)std::max(ne, 1), st);
@@ -1764,6 +1886,20 @@ int orbx_local_ba(int device, const float *Tcw, const uint8_t *fixed, int ncam, 
     if (ne) std::memcpy(outlier, out_flags.data(), ne);
     if (iterations) { iterations[0] = its[0]; iterations[1] = its[1]; }
     return ORBX_OK;
+}
+
+int orbx_local_ba(int device, const float *Tcw, const uint8_t *fixed, int ncam, const float *Xw, int npt,
+                  const orbx_ba_edge *edges, int ne, int iters1, int iters2, float *Tcw_out, float *Xw_out,
+                  uint8_t *outlier, int *iterations) {
+    return local_ba(device, false, Tcw, fixed, ncam, Xw, npt, edges, ne, iters1, iters2, Tcw_out, Xw_out, outlier,
+                    iterations);
+}
+
+int orbx_local_ba_fast(int device, const float *Tcw, const uint8_t *fixed, int ncam, const float *Xw, int npt,
+                       const orbx_ba_edge *edges, int ne, int iters1, int iters2, float *Tcw_out, float *Xw_out,
+                       uint8_t *outlier, int *iterations) {
+    return local_ba(device, true, Tcw, fixed, ncam, Xw, npt, edges, ne, iters1, iters2, Tcw_out, Xw_out, outlier,
+                    iterations);
 }
 
 // One linear system of the first pass: computeActiveErrors, buildSystem,

@@ -12,6 +12,8 @@
 // orientation moments and blur row pass as int8 MFMAs (15 per keypoint).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "orbx_device.h"
 #include "orbx_math.h"
 #include "orbx_wave.h"
@@ -172,6 +174,10 @@ __device__ inline void xcd_block_2d(int &bx, int &by, uint32_t magic) {
 // threadIdx.x >> 6 wave-uniform, so everything derived from it would live in
 // VGPRs and branch per lane.
 __device__ inline int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+// set bits of m below this lane (v_mbcnt_lo / hi: two VALU, where a masked popcount takes four)
+__device__ inline int mbcnt64(uint64_t m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 
 __device__ inline int reflect101(int v, int n) {
     // BORDER_REFLECT_101 for the 3-px halo of a >= 4 px image.
@@ -481,13 +487,16 @@ __device__ inline void resize_tile(const DevPlan &p, const FrameBufs &fb, int l,
     const int x0 = tx * 4 * twg, y0 = ty * TH;
     const int xb = x0 + 4 * lg, yb = y0 + lr * kResizeK;
     // taps of this lane's 4 columns and kResizeK rows (independent of the window loads)
-    const ResizeTap *xt = p.xtaps + a.xtab_off;
-    const ResizeTap *yt = p.ytaps + a.ytab_off;
+    // (buffer loads: 32-bit lane offsets from the wave's table bases)
+    static_assert(sizeof(ResizeTap) == 8, "one dwordx2 a tap");
+    const __amdgpu_buffer_rsrc_t xt = wave_rsrc(p.xtaps + a.xtab_off), yt = wave_rsrc(p.ytaps + a.ytab_off);
     ResizeTap txk[4], tyk[kResizeK];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) txk[k] = xt[min(xb + k, g.w - 1)];
+    for (int k = 0; k < 4; ++k)
+        txk[k] = __builtin_bit_cast(ResizeTap, __builtin_amdgcn_raw_buffer_load_b64(xt, 8 * min(xb + k, g.w - 1), 0, 0));
 #pragma unroll
-    for (int k = 0; k < kResizeK; ++k) tyk[k] = yt[min(yb + k, g.h - 1)];
+    for (int k = 0; k < kResizeK; ++k)
+        tyk[k] = __builtin_bit_cast(ResizeTap, __builtin_amdgcn_raw_buffer_load_b64(yt, 8 * min(yb + k, g.h - 1), 0, 0));
     // the source window: columns [c_lo, c_hi], rows [r_lo, r_hi] (as the tables)
     const int xl = min(x0 + 4 * twg, g.w) - 1, yl = min(y0 + TH, g.h) - 1;
     const int c_lo = min(max(resize_src_raw(x0, a.sx), 0), gs.w - 1);
@@ -512,7 +521,9 @@ __device__ inline void resize_tile(const DevPlan &p, const FrameBufs &fb, int l,
     }
     wave_lds_fence();
     if (xb >= g.w) return;
-    uint8_t *dst = fb.pyr + (int64_t)b * p.pyr_bytes + g.pyr_off;
+    // (buffer stores: a 32-bit lane offset from the wave's level base, no
+    // 64-bit address arithmetic per row)
+    const __amdgpu_buffer_rsrc_t dst = wave_rsrc(fb.pyr + (int64_t)b * p.pyr_bytes + g.pyr_off);
     auto hrow = [&](int row, uint32_t h[4]) {
         const uint32_t *ap = reinterpret_cast<const uint32_t *>(win + mul24u(row - r_lo, a.win_stride) + q4);
         const uint32_t d0 = ap[0], d1 = ap[1], d2 = ap[2];
@@ -581,7 +592,7 @@ __device__ inline void resize_tile(const DevPlan &p, const FrameBufs &fb, int l,
                 packed |= v << (8 * k);
             }
         }
-        *reinterpret_cast<uint32_t *>(dst + mul24u(y, g.pitch) + xb) = packed;
+        __builtin_amdgcn_raw_buffer_store_b32(packed, dst, mul24u(y, g.pitch) + xb, 0, 0);
     }
 }
 
@@ -795,6 +806,47 @@ __device__ inline int arc_score_bytes(const int p[16], int v) {
     return max((int)best.x - v, v - (255 - (int)best.y));
 }
 
+// k_fast's cell + ring (ORBX_FAST_STAGE): nr rows of nd dwords from column
+// x0 - 1, so that column x0 lands at patch column 1 (interior column 0 at
+// column 4).  R rows a pass (lanes rl < R, R = 64 / nd from a table: no
+// division), 8 passes: every load is issued (the buffer's range ends at the
+// rectangle, so rows past nr read zeros -- raw buffers check the lane offset,
+// which holds the whole row offset here) and the stores of passes starting at
+// or past nr are skipped by uniform branches.  The generic loop's per-load
+// and per-store exec masks (~3 scalar instructions and a compare each) go.
+// Rows in [nr, nr + R) of the last pass land below the patch, in its spare
+// rows or the score map, which each FAST pass zeroes before use; the caller
+// checks that 8 R >= nr and that nr + R - 1 rows fit the patch + score map.
+__device__ inline int fast_stage_rows(int nd) {   // 64 / nd for nd in [1, 12], 0 past
+    return nd <= 5 ? 64 / max(nd, 1) : nd == 6 ? 10 : nd == 7 ? 9 : nd == 8 ? 8 : nd == 9 ? 7 : nd == 10 ? 6 : nd <= 12 ? 5 : 0;
+}
+__device__ inline void stage_fast_patch(uint8_t *dst, int ps, const uint8_t *img, int pitch, int y0, int x0, int nr,
+                                        int nd, int R, int lane) {
+    const int xs = x0 - 1, xa = xs & ~3, sh = xs - xa;
+    const uint64_t a = reinterpret_cast<uint64_t>(img + (int64_t)y0 * pitch + xa);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const __amdgpu_buffer_rsrc_t src = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), (short)0, nr * pitch, 0x00020000);
+    const int rl = div_small(lane, nd), k = lane - mul24u(rl, nd);
+    const int voff = mul24u(rl, pitch) + 4 * k + sh, loff = mul24u(rl, ps) + 4 * k;
+    const int Rp = R * pitch, Rs = R * ps;   // (scalar)
+    typedef __attribute__((address_space(3))) uint32_t lds_u32;
+    if (rl < R) {
+        uint32_t v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = __builtin_amdgcn_raw_buffer_load_b32(src, voff + j * Rp, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(v[j]));   // (all eight issued before any store)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (j * R < nr) *(lds_u32 *)(dst + loff + j * Rs) = v[j];
+    }
+}
+
+#ifndef ORBX_FAST_STAGE
+#define ORBX_FAST_STAGE 1   // 0: the generic wave_stage_rows
+#endif
+
 // PIPE: a level's cells in a level-pipelined step (a distinct instantiation so
 // profiles tell per-level launches from whole-batch ones).
 // PSC: the patch / score-map row stride as a compile-time constant (48 or 64:
@@ -833,10 +885,21 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
     // is then 8 quads, 4 lane groups, 16 rows per compass step, where a
     // misaligned one took 9 quads, 5 groups, 12 rows: 2.66 -> 2.06 compass
     // steps per VGA cell)
-    const int o = wave_stage_rows<8, true, false, kFastAlign ? 1 : -1>(patch, PS, img, spitch, c.y0 - 3, c.x0 - 3,
-                                                                        ch + 6, cw + 6, lane);
+    int o;
+    {
+        const int sp = __builtin_amdgcn_readfirstlane(spitch), nr = ch + 6;
+        const int nd = (1 + cw + 6 + 3) >> 2;
+        const int R = fast_stage_rows(nd);
+        if (ORBX_FAST_STAGE && kFastAlign && R && 8 * R >= nr &&
+            (nr + R - 1) * PS <= fl.patch_bytes + fl.score_bytes) {
+            stage_fast_patch(patch, PS, img, sp, c.y0 - 3, c.x0 - 3, nr, nd, R, lane);
+            o = 1;
+        } else {
+            o = wave_stage_rows<8, true, false, kFastAlign ? 1 : -1>(patch, PS, img, spitch, c.y0 - 3, c.x0 - 3,
+                                                                    nr, cw + 6, lane);
+        }
+    }
     const uint8_t *pc = patch + 3 * PS + o + 3;         // interior pixel (0, 0)
-    const uint64_t below = (1ull << lane) - 1;
     PHASE_MARK(0, 0);   // prologue + staging
     if constexpr (kStopFast == 1) {
         if (lane == 0) *count_out = 0;
@@ -911,7 +974,7 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
                 }
                 const uint64_t m = __ballot(corner);
                 wave_lds_fence();   // all survivor reads of this chunk precede the in-place writes
-                if (corner) list[ncorner + __popcll(m & below)] = (uint16_t)e;
+                if (corner) list[ncorner + mbcnt64(m)] = (uint16_t)e;
                 ncorner += __popcll(m);
             }
             nsurv = 0;
@@ -932,13 +995,16 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
                     ex = e & 0xFF;
                     fin = ey < ylast;
                     const int si = mul24u(ey + 1, SW) + ex + 1;
+                    // the centre and its 8 neighbours read together, compared
+                    // with their maximum (no short-circuit chain of dependent reads)
                     sv = scm[si];
-                    keep = fin && sv > scm[si - 1] && sv > scm[si + 1] && sv > scm[si - SW - 1] &&
-                           sv > scm[si - SW] && sv > scm[si - SW + 1] && sv > scm[si + SW - 1] && sv > scm[si + SW] &&
-                           sv > scm[si + SW + 1];
+                    const int n0 = scm[si - 1], n1 = scm[si + 1], n2 = scm[si - SW - 1], n3 = scm[si - SW],
+                              n4 = scm[si - SW + 1], n5 = scm[si + SW - 1], n6 = scm[si + SW], n7 = scm[si + SW + 1];
+                    const int mx = max(max(max(n0, n1), max(n2, n3)), max(max(n4, n5), max(n6, n7)));
+                    keep = fin & (sv > mx);
                 }
                 const uint64_t mk = __ballot(keep);
-                const int pk = base + __popcll(mk & below);
+                const int pk = base + mbcnt64(mk);
                 if (keep && pk < c.cap) out[pk] = pack_key(c.x0 + ex, c.y0 + ey, sv);
                 base += __popcll(mk);
                 nfin += __popcll(__ballot(fin));
@@ -993,11 +1059,19 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
                     // 1 / 3 left in the high bytes, every value and the threshold
                     // scaled by 256 -- the same comparisons, without the shift
                     auto quad = [&](uint32_t c, uint32_t lft, uint32_t rgt, uint32_t up, uint32_t dn) -> uint32_t {
-                        auto half = [&](uint32_t mask, uint32_t sel4, uint32_t sel12, u16x2 thv) -> u16x2 {   // 1: candidate
-                            const u16x2 v = as_u16x2(c & mask);
-                            const u16x2 a0 = as_u16x2(dn & mask);
+                        // ODD: the pixels sit in the high bytes of the halves and the low
+                        // bytes are left as they come (another pixel).  Max / min then
+                        // give the right high byte and some low byte h or l, and with the
+                        // centre as V:FF against hi and V:00 against lo,
+                        //   sat(H:h - V:FF) > th:00  <=>  H - V > th,  sat(V:00 - L:l) > th:00  <=>  V - L > th
+                        // (the low-byte terms lie in [-255, 0]): one operand op fewer a half.
+                        auto half = [&](auto odd, uint32_t sel4, uint32_t sel12, u16x2 thv) -> u16x2 {   // 1: candidate
+                            constexpr bool kOdd = decltype(odd)::value;
+                            const u16x2 vh = as_u16x2(kOdd ? (c | 0x00FF00FFu) : (c & 0x00FF00FFu));   // (v against hi)
+                            const u16x2 vl = kOdd ? as_u16x2(c & 0xFF00FF00u) : vh;                  // (v against lo)
+                            const u16x2 a0 = as_u16x2(kOdd ? dn : (dn & 0x00FF00FFu));
                             const u16x2 a4 = as_u16x2(__builtin_amdgcn_perm(rgt, c, sel4));    // x + 3
-                            const u16x2 a8 = as_u16x2(up & mask);
+                            const u16x2 a8 = as_u16x2(kOdd ? up : (up & 0x00FF00FFu));
                             const u16x2 a12 = as_u16x2(__builtin_amdgcn_perm(c, lft, sel12));  // x - 3
                             // max over the cyclic pairs of the pair's min, and min of the max:
                             // max(min(a,b), min(b,c), min(c,d), min(d,a)) = min(max(a,c), max(b,d))
@@ -1007,16 +1081,16 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
                                                                        __builtin_elementwise_min(a4, a12));
                             // hi > v + th  or  lo + th < v  <=>  max(hi - v, v - lo) > th (saturating)
                             const u16x2 d = __builtin_elementwise_sub_sat(
-                                __builtin_elementwise_max(__builtin_elementwise_sub_sat(hi, v),
-                                                          __builtin_elementwise_sub_sat(v, lo)),
+                                __builtin_elementwise_max(__builtin_elementwise_sub_sat(hi, vh),
+                                                          __builtin_elementwise_sub_sat(vl, lo)),
                                 thv);
                             u16x2 m;   // min(d, 1) per half, kept one packed op
                             asm("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(d), "s"(0x00010001u));
                             return m;
                         };
                         // pixels 0 / 2 at bits 0 / 16, 1 / 3 at bits 1 / 17
-                        return __builtin_bit_cast(uint32_t, half(0x00FF00FFu, 0x0c050c03u, 0x0c030c01u, thv)) |
-                               (__builtin_bit_cast(uint32_t, half(0xFF00FF00u, 0x060c040cu, 0x040c020cu, thv8)) << 1);
+                        return __builtin_bit_cast(uint32_t, half(std::false_type{}, 0x0c050c03u, 0x0c030c01u, thv)) |
+                               (__builtin_bit_cast(uint32_t, half(std::true_type{}, 0x060c040cu, 0x040c020cu, thv8)) << 1);
                     };
                     // quad k's pixels 0 / 2 at bits 4k / 4k + 16, 1 / 3 at 4k + 1 / 4k + 17,
                     // folded to bits 4k .. 4k + 3
@@ -2239,9 +2313,13 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
     // this lane's 4 pattern pairs (bytes x0 y0 x1 y1 of pairs 2j, 2j + 1,
     // j = 64 grp + lane), fetched first so the loads overlap the staging
     float4 pat[4];
+    // one buffer resource over the table, the loads at immediate offsets (the
+    // compiler otherwise rebuilds the symbol's address, s_getpc + add + addc, per load)
+    const __amdgpu_buffer_rsrc_t pat_rsrc = wave_rsrc(c_pattern_f);
     const long row_taps = (long)c_row_taps.t[lane];
 #pragma unroll
-    for (int grp = 0; grp < 4; ++grp) pat[grp] = reinterpret_cast<const float4 *>(c_pattern_f)[grp * 64 + lane];
+    for (int grp = 0; grp < 4; ++grp)
+        pat[grp] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(pat_rsrc, 16 * lane + 1024 * grp, 0, 0));
     int bx, b;
     xcd_block_2d(bx, b, gmagic);
     const int slot = s0 + bx * 4 + wave;

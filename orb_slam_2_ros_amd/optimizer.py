@@ -14,10 +14,11 @@ from ._lib import check, load, ptr
 from .synth_ba import BA_EDGE_DTYPE
 
 
-def local_bundle_adjustment(Tcw, fixed, Xw, edges, iters=(5, 10), device: int = 0):
+def local_bundle_adjustment(Tcw, fixed, Xw, edges, iters=(5, 10), device: int = 0, fast: bool = False):
     """Tcw (ncam, 3, 4) f32, fixed (ncam,) bool, Xw (npt, 3) f32, edges
     BA_EDGE_DTYPE.  Returns (Tcw_out, Xw_out, outlier (ne,) bool,
-    (iterations pass 1, pass 2))."""
+    (iterations pass 1, pass 2)).  fast: orbx_local_ba_fast (parallel sums
+    and factorisation; equal to the ordered mode to rounding)."""
     T = np.ascontiguousarray(Tcw, np.float32).reshape(-1, 3, 4)
     F = np.ascontiguousarray(fixed, np.uint8)
     X = np.ascontiguousarray(Xw, np.float32).reshape(-1, 3)
@@ -25,8 +26,9 @@ def local_bundle_adjustment(Tcw, fixed, Xw, edges, iters=(5, 10), device: int = 
     To, Xo = np.empty_like(T), np.empty_like(X)
     out = np.zeros(max(len(E), 1), np.uint8)
     its = np.zeros(2, np.int32)
-    check(load().orbx_local_ba(device, ptr(T), ptr(F), len(T), ptr(X), len(X), ptr(E), len(E), int(iters[0]),
-                               int(iters[1]), ptr(To), ptr(Xo), ptr(out), ptr(its)), "orbx_local_ba")
+    fn = load().orbx_local_ba_fast if fast else load().orbx_local_ba
+    check(fn(device, ptr(T), ptr(F), len(T), ptr(X), len(X), ptr(E), len(E), int(iters[0]),
+             int(iters[1]), ptr(To), ptr(Xo), ptr(out), ptr(its)), "orbx_local_ba")
     return To, Xo, out[:len(E)].astype(bool), (int(its[0]), int(its[1]))
 
 

@@ -76,3 +76,21 @@ def test_local_ba_workspace_reuse(oracle_mod):
         To, Xo, oo, io = oracle_mod.local_ba(P["Tcw"], P["fixed"], P["Xw"], e)
         assert ig == io and np.array_equal(og, oo), k
         assert np.array_equal(Tg, To) and np.array_equal(Xg, Xo), k
+
+
+@pytest.mark.parametrize("seed,n_local,n_points", [(1, 10, 1500), (2, 20, 3000), (3, 4, 300), (5, 21, 3000),
+                                                   (4, 30, 2500)])
+def test_local_ba_fast_mode_within_tolerance(seed, n_local, n_points, oracle_mod):
+    """orbx_local_ba_fast (parallel sums, parallel FMA Cholesky for <= 21 free
+    keyframes) against the ordered oracle: identical outlier flags, poses and
+    points equal to 1e-4 relative (float outputs; the double-precision LM
+    differs by rounding only)."""
+    P = make_ba_problem(n_local=n_local, n_fixed=4, n_points=n_points, seed=seed)
+    Tg, Xg, og, ig = local_bundle_adjustment(P["Tcw"], P["fixed"], P["Xw"], P["edges"], fast=True)
+    To, Xo, oo, io = oracle_mod.local_ba(P["Tcw"], P["fixed"], P["Xw"], P["edges"])
+    assert np.array_equal(og, oo), f"outlier flags differ at {np.nonzero(og != oo)[0][:8]}"
+    assert np.abs(Tg - To).max() <= 1e-4 * max(1.0, np.abs(To).max()), np.abs(Tg - To).max()
+    assert np.abs(Xg - Xo).max() <= 1e-4 * np.abs(Xo).max(), np.abs(Xg - Xo).max()
+    free = P["fixed"] == 0
+    assert np.array_equal(Tg[~free], P["Tcw"][~free])
+    assert abs(ig[0] - io[0]) <= 1 and abs(ig[1] - io[1]) <= 2, (ig, io)
