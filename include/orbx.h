@@ -569,13 +569,13 @@ typedef struct orbx_ba_edge {
 int orbx_local_ba(int device, const float *Tcw, const uint8_t *fixed, int ncam, const float *Xw, int npt,
                   const orbx_ba_edge *edges, int ne, int iters1, int iters2, float *Tcw_out, float *Xw_out,
                   uint8_t *outlier, int *iterations);
-/* The same optimisation in a fast mode: the per-vertex and per-camera-pair
- * sums as parallel reductions and the reduced camera system factored by a
- * parallel right-looking Cholesky with fused multiply-adds (systems of up to
- * 21 free cameras; larger ones as above).  Same algorithm, another
- * floating-point order: outputs equal orbx_local_ba's to rounding (tolerances
- * in tests/test_gpu_ba.py), not bit for bit.  No reference counterpart beyond
- * LocalBundleAdjustment itself, whose g2o sums are unordered too. */
+/* The same optimisation in a fast mode: the per-vertex (Hpp, bp, reduced
+ * right-hand side) and per-camera-pair (Schur complement) sums as parallel
+ * reductions instead of sequential chains in edge / point order.  Same
+ * algorithm, another floating-point order: outputs equal orbx_local_ba's to
+ * rounding (tolerances in tests/test_gpu_ba.py), not bit for bit.  No
+ * reference counterpart beyond LocalBundleAdjustment itself, whose g2o sums
+ * are unordered too. */
 int orbx_local_ba_fast(int device, const float *Tcw, const uint8_t *fixed, int ncam, const float *Xw, int npt,
                        const orbx_ba_edge *edges, int ne, int iters1, int iters2, float *Tcw_out, float *Xw_out,
                        uint8_t *outlier, int *iterations);

@@ -736,73 +736,6 @@ __device__ inline double readlane_f64(double v, int l) {
     return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 
-// The fast mode's factorisation (orbx_local_ba_fast; n <= kCholLds): right-
-// looking, one column a step, every thread on the trailing update with fused
-// multiply-adds -- thread (ty, tx) of a 32 x 32 grid owns the entries
-// (i, j), i = ty mod 32, j = tx mod 32, j <= i -- and one barrier a step: the
-// column's entries are read unscaled (multiplied by 1 / L(k, k)) and the
-// scaled ones go to the unused upper triangle (U(k, i) = L(i, k)), so no
-// entry a step reads is written in it; the next diagonal's owner takes its
-// square root and reciprocal before the barrier.  Then the two solves by
-// wave 0 (lane r owns rows r and r + 64, column sweeps, readlane broadcasts).
-// Not the oracle's operation order: equal to rounding.
-__global__ __launch_bounds__(1024) void k_ba_chol_fast(const double *S, int n, const double *bs, double *x, int *ok) {
-    extern __shared__ double L[];   // n rows of n+1 (lower: the working matrix; upper: scaled columns), then dg, inv
-    __shared__ int bad;
-    const int ld = n + 1, tid = threadIdx.x, tx = tid & 31, ty = tid >> 5;
-    double *dg = L + n * ld, *inv = dg + n;
-    for (int q = tid; q < n * n; q += 1024) {
-        const int r = q / n, c = q - r * n;
-        if (c <= r) L[r * ld + c] = S[q];
-    }
-    __syncthreads();
-    if (tid == 0) {
-        const double d0 = L[0];
-        bad = !(d0 > 0);
-        dg[0] = sqrt(d0);
-        inv[0] = 1.0 / dg[0];
-    }
-    __syncthreads();
-    for (int k = 0; k < n && !bad; ++k) {
-        const double ik = inv[k];
-        // scaled column k to the upper triangle (row k, columns > k)
-        for (int i = k + 1 + tid; i < n; i += 1024) L[k * ld + i] = L[i * ld + k] * ik;
-        const double ik2 = ik * ik;
-        const int j0 = k + 1 + ((tx - (k + 1)) & 31);   // this thread's first column > k
-        for (int i = k + 1 + ((ty - (k + 1)) & 31); i < n; i += 32) {
-            const double li = L[i * ld + k] * ik2;
-            for (int j = j0; j <= i; j += 32) L[i * ld + j] = fma(-li, L[j * ld + k], L[i * ld + j]);
-            if (i == k + 1 && j0 == k + 1) {   // the next diagonal, final now
-                const double d = L[(k + 1) * ld + k + 1];
-                if (!(d > 0)) bad = 1;
-                dg[k + 1] = sqrt(d);
-                inv[k + 1] = 1.0 / dg[k + 1];
-            }
-        }
-        __syncthreads();
-    }
-    if (tid >= 64) return;
-    if (tid == 0) *ok = !bad;
-    if (bad) return;
-    const int lane = tid;
-    double y0 = lane < n ? bs[lane] : 0.0, y1 = lane + 64 < n ? bs[lane + 64] : 0.0;
-    for (int k = 0; k < n; ++k) {   // L y = b: L(i, k) = U(k, i) = L[k * ld + i]
-        const double yk = readlane_f64(k < 64 ? y0 : y1, k & 63) * inv[k];
-        if (lane == (k & 63)) { if (k < 64) y0 = yk; else y1 = yk; }
-        if (lane > k && lane < n) y0 = fma(-L[k * ld + lane], yk, y0);
-        if (lane + 64 > k && lane + 64 < n) y1 = fma(-L[k * ld + lane + 64], yk, y1);
-    }
-    for (int k = n - 1; k >= 0; --k) {   // L^T x = y: L(k, i) for i < k = U(i, k) = L[i * ld + k]
-        const double xk = readlane_f64(k < 64 ? y0 : y1, k & 63) * inv[k];
-        if (lane == (k & 63)) { if (k < 64) y0 = xk; else y1 = xk; }
-        if (lane < k) y0 = fma(-L[lane * ld + k], xk, y0);
-        if (lane + 64 < k) y1 = fma(-L[(lane + 64) * ld + k], xk, y1);
-    }
-    if (lane < n) x[lane] = y0;
-    if (lane + 64 < n) x[lane + 64] = y1;
-}
-
-
 // The same factorisation and solves with S held in LDS (n <= kCholLds),
 // blocked right-looking in panels of kPanel columns:
 //  - wave 0 factors a panel alone (lane t owns rows k+1+t and k+65+t of each
@@ -1262,7 +1195,7 @@ public:
     Graph &g_;
     hipStream_t st_;
     BAWs &ws_;
-    bool fast_ = false;   // orbx_local_ba_fast: parallel sums and factorisation (equal to rounding)
+    bool fast_ = false;   // orbx_local_ba_fast: the per-vertex / per-pair sums as parallel reductions (equal to rounding)
     uint8_t *buf_ = nullptr;
     Pose *d_pose = nullptr, *d_pose_bk = nullptr;
     double *d_pts = nullptr, *d_pts_bk = nullptr;
@@ -1604,13 +1537,11 @@ int BA::solve_async(double lambda) {
         else
             hipLaunchKernelGGL((k_ba_stream_sums<6, false>), dim3(g.nf), dim3(kSumThreads), kSumLds, st_, d_rows,
                                d_coffs, d_bp, d_bs, 6, nullptr);
-        if (fast_ && n <= kCholLds) {
-            const int lb = 8 * (n * (n + 1) + 2 * n);
-            if (lb > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void *>(k_ba_chol_fast),
-                                                      hipFuncAttributeMaxDynamicSharedMemorySize, lb) != hipSuccess)
-                return ORBX_EIO;
-            hipLaunchKernelGGL(k_ba_chol_fast, dim3(1), dim3(1024), lb, st_, d_S, n, d_bs, d_x, d_ok);
-        } else if (n <= kCholLds) {
+        // (both modes factor with the same kernels: an unblocked parallel
+        // right-looking FMA factorisation, one barrier a column, measured 130 us
+        // against this blocked look-ahead kernel's 85 us at 120 unknowns --
+        // the per-column square root and reciprocal sit on the critical path)
+        if (n <= kCholLds) {
             const int lb = 8 * (n * (n + 1) + n);
             if (lb > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void *>(k_ba_chol_lds),
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, lb) != hipSuccess)

@@ -17,8 +17,8 @@ from .synth_ba import BA_EDGE_DTYPE
 def local_bundle_adjustment(Tcw, fixed, Xw, edges, iters=(5, 10), device: int = 0, fast: bool = False):
     """Tcw (ncam, 3, 4) f32, fixed (ncam,) bool, Xw (npt, 3) f32, edges
     BA_EDGE_DTYPE.  Returns (Tcw_out, Xw_out, outlier (ne,) bool,
-    (iterations pass 1, pass 2)).  fast: orbx_local_ba_fast (parallel sums
-    and factorisation; equal to the ordered mode to rounding)."""
+    (iterations pass 1, pass 2)).  fast: orbx_local_ba_fast (the sums as
+    parallel reductions; equal to the ordered mode to rounding)."""
     T = np.ascontiguousarray(Tcw, np.float32).reshape(-1, 3, 4)
     F = np.ascontiguousarray(fixed, np.uint8)
     X = np.ascontiguousarray(Xw, np.float32).reshape(-1, 3)

@@ -81,8 +81,8 @@ def test_local_ba_workspace_reuse(oracle_mod):
 @pytest.mark.parametrize("seed,n_local,n_points", [(1, 10, 1500), (2, 20, 3000), (3, 4, 300), (5, 21, 3000),
                                                    (4, 30, 2500)])
 def test_local_ba_fast_mode_within_tolerance(seed, n_local, n_points, oracle_mod):
-    """orbx_local_ba_fast (parallel sums, parallel FMA Cholesky for <= 21 free
-    keyframes) against the ordered oracle: identical outlier flags, poses and
+    """orbx_local_ba_fast (the per-vertex and per-pair sums as parallel
+    reductions) against the ordered oracle: identical outlier flags, poses and
     points equal to 1e-4 relative (float outputs; the double-precision LM
     differs by rounding only)."""
     P = make_ba_problem(n_local=n_local, n_fixed=4, n_points=n_points, seed=seed)
