@@ -59,8 +59,8 @@ def algorithmic_bytes(sizes, nkp: float, stage: str) -> float:
         return 2.0 * p
     if stage == "fast":        # read every level once
         return float(p)
-    if stage == "describe":    # the keypoints' neighbourhoods cover the levels: each pixel once, 60 B per kp out
-        return float(p) + nkp * 60
+    if stage == "describe":    # 60 B per keypoint out; its patch reads re-read what k_fast streamed (L2)
+        return nkp * 60
     if stage == "match":       # both frames' descriptors + keypoints read, matches written
         return nkp * (2 * 32 + 2 * 28 + 4)
     if stage == "quadtree":    # candidates in, selection out (counted in the kernel)
@@ -1223,8 +1223,14 @@ def main() -> int:
         stage_ms = None
         if stages:
             stage_ms = dict(zip(names, [round(s, 4) for s in stages]))
-            # dominant HBM-streaming kernel by time among the stages with an algorithmic byte count
-            cand = {n: s for n, s in stage_ms.items() if s and s > 0 and algorithmic_bytes(sizes, nkp_last, n) > 0}
+            # the dominant HBM-streaming kernel: by time among the stages that move a
+            # tenth or more of the frame's compulsory bytes; k_fast
+            # (reads the pyramid) and k_describe (60 B per keypoint out, its patches
+            # re-read from L2) take about equal time, and the time-dominant one of all
+            # stages is reported beside it under "dominant_by_time"
+            fb = algorithmic_bytes(sizes, nkp_last, "frame")
+            cand = {n: s for n, s in stage_ms.items()
+                    if s and s > 0 and algorithmic_bytes(sizes, nkp_last, n) >= 0.1 * fb}
             dom = max(cand, key=cand.get)
             # stage times come from the profiling pass: one whole-batch launch per
             # stage, unsplit and unpipelined, overlapping nothing
@@ -1244,6 +1250,17 @@ def main() -> int:
                                  "half_rate_peak": VALU_HALF_RATE_GINST,
                                  "frac_of_half_rate": round(ach / VALU_HALF_RATE_GINST, 4),
                                  "insts_per_launch": valu, "source": tsrc, "peak_source": VALU_PEAK_SOURCE}
+            tdom = max((n for n, t in stage_ms.items() if t and t > 0), key=lambda n: stage_ms[n])
+            if tdom != dom:
+                tb = algorithmic_bytes(sizes, nkp_last, tdom) * frames_per_launch
+                tach = tb / (stage_ms[tdom] * 1e-3) / 1e9
+                tv = measured_valu(tdom, frames_per_launch)
+                roof["dominant_by_time"] = {
+                    "kernel": tdom, "ms": stage_ms[tdom], "bytes_per_launch": tb, "achieved": round(tach, 2),
+                    "frac": round(tach / HBM_PEAK_GBS, 5),
+                    "traffic": measured_traffic(tdom, frames_per_launch)[0],
+                    "issue_frac_of_half_rate": round(tv / (stage_ms[tdom] * 1e-3) / 1e9 / VALU_HALF_RATE_GINST, 4)
+                    if tv else None}
             frame_bytes = algorithmic_bytes(sizes, nkp_last, "frame")
             roof["pipeline_GBs"] = round(frame_bytes * value / world / 1e9, 2)
             roof["pipeline_frac"] = round(frame_bytes * value / world / 1e9 / HBM_PEAK_GBS, 5)
