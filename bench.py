@@ -1281,7 +1281,7 @@ def main() -> int:
                     torch, dist, rank, world, dev, max(5, args.steps // 4), 2, profile, total=8, kframes=kk,
                     exchange=False)
             for key, cfg in HOST_FED.items():
-                extras[key] = host_fed(torch, dev, *cfg, max(8, args.steps // 4), 2)
+                extras[key] = host_fed(torch, dev, *cfg, max(20, args.steps // 2), 3)
             extras["dropin_latency"] = dropin_latency(torch, dev)
             extras["bow_transform_orbvoc"] = bow_transform_throughput(torch)
             extras["keyframe_db_loop_query"] = kfdb_latency()

@@ -235,7 +235,9 @@ __device__ int block_excl_scan_i32(int v, int *total, int *ws) {
 
 // Unsigned 24-bit multiply (v_mul_u32_u24, full rate); both operands must be
 // in [0, 2^24), which every use below guarantees.
-__device__ inline int mul24u(int a, int b) { return (int)(((uint32_t)a & 0xFFFFFFu) * ((uint32_t)b & 0xFFFFFFu)); }
+// (__umul24: the masked-product form let the compiler pick v_mul_lo_u32, a
+// quarter-rate op, whenever one operand was a scalar it had proven small)
+__device__ inline int mul24u(int a, int b) { return (int)__umul24((uint32_t)a, (uint32_t)b); }
 
 // Small exact integer division for the index walks (a < 2^15, b <= 255).
 __device__ inline int div_small(int a, int b) {
@@ -817,8 +819,9 @@ __device__ inline int arc_score_bytes(const int p[16], int v) {
 // Rows in [nr, nr + R) of the last pass land below the patch, in its spare
 // rows or the score map, which each FAST pass zeroes before use; the caller
 // checks that 8 R >= nr and that nr + R - 1 rows fit the patch + score map.
-__device__ inline int fast_stage_rows(int nd) {   // 64 / nd for nd in [1, 12], 0 past
-    return nd <= 5 ? 64 / max(nd, 1) : nd == 6 ? 10 : nd == 7 ? 9 : nd == 8 ? 8 : nd == 9 ? 7 : nd == 10 ? 6 : nd <= 12 ? 5 : 0;
+__device__ inline int fast_stage_rows(int nd) {   // 64 / nd for nd in [1, 12], 0 past (selects, no division)
+    return nd <= 1 ? 64 : nd == 2 ? 32 : nd == 3 ? 21 : nd == 4 ? 16 : nd == 5 ? 12 : nd == 6 ? 10 : nd == 7 ? 9
+         : nd == 8 ? 8 : nd == 9 ? 7 : nd == 10 ? 6 : nd <= 12 ? 5 : 0;
 }
 __device__ inline void stage_fast_patch(uint8_t *dst, int ps, const uint8_t *img, int pitch, int y0, int x0, int nr,
                                         int nd, int R, int lane) {
