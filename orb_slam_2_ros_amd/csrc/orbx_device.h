@@ -24,8 +24,9 @@ struct LevelArgs {
 struct FastLds {
     int ps;            // patch row stride (dword multiple)
     int patch_bytes, score_bytes, per_wave;
-    int sw;            // score-map row stride (largest cell width + 2)
+    int sw;            // score-map row stride (= ps: a survivor's patch offset indexes both)
     int list_cap;      // survivor-list entries (k_fast flushes before overflowing it)
+    int pmag;          // ceil(2^24 / ps): row = (offset * pmag) >> 24 for offsets < 2^16
 };
 FastLds fast_lds(int mw, int mh);
 

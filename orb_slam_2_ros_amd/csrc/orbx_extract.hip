@@ -12,6 +12,7 @@
 // orientation moments and blur row pass as int8 MFMAs (15 per keypoint).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "orbx_device.h"
@@ -20,14 +21,44 @@
 
 namespace orbx {
 
-// rBRIEF sampling points as floats (the descriptor's rotation multiplies them in float)
-__constant__ __attribute__((aligned(16))) float c_pattern_f[512][2] = {
+// rBRIEF sampling points (ORBextractor.cc:150-408)
+constexpr int kPatternPts[512][2] = {
 #define ORBX_PATTERN_BEGIN
 #define ORBX_PATTERN_END
 #include "orb_pattern.inc"
 #undef ORBX_PATTERN_BEGIN
 #undef ORBX_PATTERN_END
 };
+// The descriptor's rotation multiplies them in float; k_describe fetches them
+// as OCP fp8 e4m3fn (gfx950's format: every integer of magnitude <= 16 is
+// exact) and widens a point (x, y) to an f32 pair with one
+// v_cvt_pk_f32_fp8: lane l's 16 bytes are pairs 64 g + l, g = 0..3, as
+// (x0, y0, x1, y1) -- one 16-byte load a lane instead of four.
+constexpr uint32_t fp8_e4m3_int(int n) {   // n in [-15, 15]
+    int a = n < 0 ? -n : n, e = 0;
+    while (a >> (e + 1)) ++e;
+    return n == 0 ? 0u : (uint32_t)((n < 0 ? 0x80 : 0) | ((e + 7) << 3) | (((a << 3) >> e) & 7));
+}
+struct PatternQ {
+    uint32_t w[64][4];
+    constexpr PatternQ() : w() {
+        for (int l = 0; l < 64; ++l)
+            for (int g = 0; g < 4; ++g) {
+                const int j = 64 * g + l;
+                w[l][g] = fp8_e4m3_int(kPatternPts[2 * j][0]) | fp8_e4m3_int(kPatternPts[2 * j][1]) << 8 |
+                          fp8_e4m3_int(kPatternPts[2 * j + 1][0]) << 16 | fp8_e4m3_int(kPatternPts[2 * j + 1][1]) << 24;
+            }
+    }
+};
+constexpr bool pattern_in_fp8_range() {
+    for (int i = 0; i < 512; ++i)
+        for (int c = 0; c < 2; ++c)
+            if (kPatternPts[i][c] < -15 || kPatternPts[i][c] > 15) return false;
+    return true;
+}
+static_assert(pattern_in_fp8_range(), "the fp8 pattern table holds integers up to 15 exactly");
+static_assert(fp8_e4m3_int(1) == 0x38 && fp8_e4m3_int(13) == 0x55 && fp8_e4m3_int(-3) == 0xC4, "e4m3fn, bias 7");
+__constant__ __attribute__((aligned(16))) PatternQ c_pattern_q = PatternQ();
 
 // c_disc_mask[ri][g]: byte k kept iff column 4g - 16 + k lies in row ri - 15
 // of the orientation disc (kUmax, orbx_plan.h).
@@ -48,36 +79,35 @@ struct DiscMask {
 };
 __constant__ DiscMask c_disc_mask = DiscMask();
 
-// IC_Angle's moments on the matrix cores (k_describe): six int8 MFMAs over the
-// staged patch (rows 0..47 as three 16-row tiles, patch columns 0..63 as two
-// 32-column halves; the disc is rows 6..36, columns 6 + o .. 36 + o for the
-// staging offset o).  Per (o, row tile rt, half h, lane):
-//   mask: the A-operand bytes kept, patch row 16 rt + (l & 15), columns
-//         32 h + 8 (l >> 4) + 0..7, inside the disc (kUmax);
+// IC_Angle's moments on the matrix cores (k_describe): three int8 MFMAs over
+// the staged patch (rows 0..47 as three 16-row tiles; the keypoint at patch
+// column 23, so the disc, rows 6..36 and columns 8..38, lies in one 32-column
+// window, columns 8..39).  Per (row tile rt, lane):
+//   mask: the A-operand bytes kept, patch row 16 rt + (l & 15), window
+//         columns 8 (l >> 4) + 0..7, inside the disc (kUmax);
 //   b:    the B-operand bytes, k = 8 (l >> 4) + 0..7, output column j = l & 15:
-//         j = 15: u = 32 h + k - 21 - o (m10), j = 12 + rt: 1 (the rows' sums,
-//         weighted by their v afterwards: m01), others 0.
+//         j = 15: u = k - 15 (m10), j = 12 + rt: 1 (the rows' sums, weighted
+//         by their v afterwards: m01), others 0.
+constexpr int kDescKpCol = 23;   // the keypoint's patch column (k_describe staging)
 struct MomTables {
-    uint64_t mb[4][3][2][64][2];   // (mask, b): one 16-byte load a product
+    uint64_t mb[3][64][2];   // (mask, b): one 16-byte load a product
     constexpr MomTables() : mb() {
-        for (int o = 0; o < 4; ++o)
-            for (int rt = 0; rt < 3; ++rt)
-                for (int h = 0; h < 2; ++h)
-                    for (int l = 0; l < 64; ++l) {
-                        uint64_t mk = 0, bb = 0;
-                        const int v = 16 * rt + (l & 15) - 21, av = v < 0 ? -v : v, j = l & 15;
-                        for (int jj = 0; jj < 8; ++jj) {
-                            const int u = 32 * h + 8 * (l >> 4) + jj - 21 - o, au = u < 0 ? -u : u;
-                            if (av <= 15 && au <= kUmax[av]) mk |= 0xFFull << (8 * jj);
-                            const int w = j == 15 ? u : (j == 12 + rt ? 1 : 0);
-                            bb |= (uint64_t)(uint8_t)(int8_t)w << (8 * jj);
-                        }
-                        mb[o][rt][h][l][0] = mk;
-                        mb[o][rt][h][l][1] = bb;
-                    }
+        for (int rt = 0; rt < 3; ++rt)
+            for (int l = 0; l < 64; ++l) {
+                uint64_t mk = 0, bb = 0;
+                const int v = 16 * rt + (l & 15) - 21, av = v < 0 ? -v : v, j = l & 15;
+                for (int jj = 0; jj < 8; ++jj) {
+                    const int u = 8 + 8 * (l >> 4) + jj - kDescKpCol, au = u < 0 ? -u : u;
+                    if (av <= 15 && au <= kUmax[av]) mk |= 0xFFull << (8 * jj);
+                    const int w = j == 15 ? u : (j == 12 + rt ? 1 : 0);
+                    bb |= (uint64_t)(uint8_t)(int8_t)w << (8 * jj);
+                }
+                mb[rt][l][0] = mk;
+                mb[rt][l][1] = bb;
+            }
     }
 };
-__constant__ MomTables c_mom = MomTables();
+__constant__ __attribute__((aligned(16))) MomTables c_mom = MomTables();
 
 // Phase profiling (diagnostic build only, -DORBX_PHASE_PROF: tools/phase_prof.py):
 // each wave adds the s_memtime cycles of its phases to g_phase[kernel][phase]
@@ -877,10 +907,15 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
         if (lane == 0) *count_out = 0;
         return;
     }
-    const int PS = PSC ? PSC : fl.ps, SW = PSC ? PSC : fl.sw;
+    // the patch and the score map share the row stride (fast_lds)
+    const int PS = PSC ? PSC : fl.ps;
+    const int pmag = PSC ? (int)(((1u << 24) + PSC - 1) / (PSC ? PSC : 1)) : fl.pmag;
+    const int kxy0 = c.x0 + (c.y0 << 12);   // pack_key of interior pixel (0, 0), score 0
     uint8_t *patch = lds + (size_t)wave * fl.per_wave;
     uint8_t *scm = patch + fl.patch_bytes;   // S-1 of the pass's corners, 0 elsewhere
-    uint16_t *list = reinterpret_cast<uint16_t *>(scm + fl.score_bytes);   // (yy << 8 | xx), row-major
+    // survivors and corners as patch offsets yy * PS + xx from interior pixel
+    // (0, 0) (the score map's index of the pixel is the same + PS + 1), row-major
+    uint16_t *list = reinterpret_cast<uint16_t *>(scm + fl.score_bytes);
     int spitch;
     const uint8_t *img = level_ptr(p, fb, c.level, b, spitch);
     // (ORBX_FAST_ALIGN: the cell is staged so that interior column 0 lands on
@@ -958,23 +993,23 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
             //    arc's maximum, side by side as packed u16 lanes (p, 255 - p) through
             //    sliding-window minima (2, 4, 8, 9).  A corner at th iff S > th; its
             //    FAST score S - 1 goes to the map, corners compacted in place.
+            // (wave-uniform counts, kept in scalars: loops on scalar compares)
+            npend = __builtin_amdgcn_readfirstlane(npend);
+            nsurv = __builtin_amdgcn_readfirstlane(nsurv);
             int ncorner = npend;
             for (int i0 = 0; i0 < nsurv; i0 += 64) {
-                bool corner = false;
-                int e = 0;
-                if (i0 + lane < nsurv) {
-                    e = list[npend + i0 + lane];
-                    const int ey = e >> 8, ex = e & 0xFF;
-                    const uint8_t *q = pc + mul24u(ey, PS) + ex;
-                    const int v = q[0];
-                    const uint32_t pr[16] = {q[3 * PS],  q[3 * PS + 1],  q[2 * PS + 2],  q[PS + 3],
-                                             q[3],       q[-PS + 3],     q[-2 * PS + 2], q[-3 * PS + 1],
-                                             q[-3 * PS], q[-3 * PS - 1], q[-2 * PS - 2], q[-PS - 3],
-                                             q[-3],      q[PS - 3],      q[2 * PS - 2],  q[3 * PS - 1]};
-                    const int S = arc_score_bytes(reinterpret_cast<const int *>(pr), v);
-                    corner = S > th;
-                    if (corner) scm[mul24u(ey + 1, SW) + ex + 1] = (uint8_t)(S - 1);
-                }
+                // every lane scores (no exec region): a lane past the survivors
+                // reads a stale entry, or LDS past the list, and is masked after
+                const int e = list[npend + i0 + lane];
+                const uint8_t *q = pc + e;
+                const int v = q[0];
+                const uint32_t pr[16] = {q[3 * PS],  q[3 * PS + 1],  q[2 * PS + 2],  q[PS + 3],
+                                         q[3],       q[-PS + 3],     q[-2 * PS + 2], q[-3 * PS + 1],
+                                         q[-3 * PS], q[-3 * PS - 1], q[-2 * PS - 2], q[-PS - 3],
+                                         q[-3],      q[PS - 3],      q[2 * PS - 2],  q[3 * PS - 1]};
+                const int S = arc_score_bytes(reinterpret_cast<const int *>(pr), v);
+                const bool corner = (i0 + lane < nsurv) & (S > th);
+                if (corner) scm[e + PS + 1] = (uint8_t)(S - 1);
                 const uint64_t m = __ballot(corner);
                 wave_lds_fence();   // all survivor reads of this chunk precede the in-place writes
                 if (corner) list[ncorner + mbcnt64(m)] = (uint16_t)e;
@@ -987,28 +1022,27 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
             // C. strict 3x3 NMS inside the cell (outside neighbours and non-corners
             //    score 0), compacted in row-major order; a corner of row ydone - 1
             //    waits for the next rows' scores unless final.
-            const int ylast = final ? INT_MAX : ydone - 1;
+            // (entries are patch offsets ey * PS + ex: row ey is final below ylast * PS)
+            const int ylast = final ? INT_MAX : (ydone - 1) * PS;
             int nfin = 0;
             for (int i0 = 0; i0 < ncorner; i0 += 64) {
-                bool keep = false, fin = false;
-                int ey = 0, ex = 0, sv = 0;
-                if (i0 + lane < ncorner) {
-                    const int e = list[i0 + lane];
-                    ey = e >> 8;
-                    ex = e & 0xFF;
-                    fin = ey < ylast;
-                    const int si = mul24u(ey + 1, SW) + ex + 1;
-                    // the centre and its 8 neighbours read together, compared
-                    // with their maximum (no short-circuit chain of dependent reads)
-                    sv = scm[si];
-                    const int n0 = scm[si - 1], n1 = scm[si + 1], n2 = scm[si - SW - 1], n3 = scm[si - SW],
-                              n4 = scm[si - SW + 1], n5 = scm[si + SW - 1], n6 = scm[si + SW], n7 = scm[si + SW + 1];
-                    const int mx = max(max(max(n0, n1), max(n2, n3)), max(max(n4, n5), max(n6, n7)));
-                    keep = fin & (sv > mx);
-                }
+                // every lane reads (as in B), lanes past the corners masked after
+                const int e = list[i0 + lane];
+                const bool fin = (i0 + lane < ncorner) & (e < ylast);
+                const int si = e + PS + 1;
+                // the centre and its 8 neighbours read together, compared
+                // with their maximum (no short-circuit chain of dependent reads)
+                const int sv = scm[si];
+                const int n0 = scm[si - 1], n1 = scm[si + 1], n2 = scm[si - PS - 1], n3 = scm[si - PS],
+                          n4 = scm[si - PS + 1], n5 = scm[si + PS - 1], n6 = scm[si + PS], n7 = scm[si + PS + 1];
+                const int mx = max(max(max(n0, n1), max(n2, n3)), max(max(n4, n5), max(n6, n7)));
+                const bool keep = fin & (sv > mx);
                 const uint64_t mk = __ballot(keep);
                 const int pk = base + mbcnt64(mk);
-                if (keep && pk < c.cap) out[pk] = pack_key(c.x0 + ex, c.y0 + ey, sv);
+                // the key from the offset: ey by the 24-bit reciprocal, then
+                // x | y << 12 = x0 + (y0 << 12) + e + ey (4096 - PS)
+                const int ey = (int)(__umul24((uint32_t)e, (uint32_t)pmag) >> 24);
+                if (keep && pk < c.cap) out[pk] = (uint32_t)(kxy0 + e + mul24u(ey, 4096 - PS)) | ((uint32_t)sv << 24);
                 base += __popcll(mk);
                 nfin += __popcll(__ballot(fin));
             }
@@ -1033,14 +1067,14 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
             const u16x2 thv = {(unsigned short)th, (unsigned short)th};
             const u16x2 thv8 = {(unsigned short)(th << 8), (unsigned short)(th << 8)};
             typedef __attribute__((address_space(3))) const uint32_t lds_u32c;
-            const int e = (rl << 8) + xx0;
-            const int RPS = __builtin_amdgcn_readfirstlane(R * PS), R8 = __builtin_amdgcn_readfirstlane(R << 8);
+            const int e = mul24u(rl, PS) + xx0;   // the list entry of the group's byte 0 at yo = 0
+            const int RPS = __builtin_amdgcn_readfirstlane(R * PS);
             const int chps = __builtin_amdgcn_readfirstlane(ch * PS);
-            for (int yo = 0, ys = 0; yo < chps; yo += RPS, ys += R8) {
+            for (int yo = 0, ys = 0; yo < chps; yo += RPS, ys += R) {
                 // survivors this step can add: its rows' pixels (wave-uniform)
-                if (npend + nsurv + min(R, ch - (ys >> 8)) * cw > fl.list_cap) {
+                if (npend + nsurv + min(R, ch - ys) * cw > fl.list_cap) {
                     if constexpr (kStopFast == 2) nsurv = 0;
-                    else flush(ys >> 8, false);
+                    else flush(ys, false);
                 }
                 uint32_t cand = 0;
                 if (yo < rlim) {
@@ -1110,11 +1144,15 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
                 if (total) {
                     typedef __attribute__((address_space(3))) uint16_t lds_u16;
                     lds_u16 *dst = (lds_u16 *)list + npend + nsurv + (incl - cnt);
-                    const int ey = e + ys;
-                    while (cand) {
-                        *dst = (uint16_t)(ey + __builtin_ctz(cand));
-                        ++dst;
-                        cand &= cand - 1u;
+                    const int ey = e + yo;
+                    // the lane's k-th bit to dst[k] (LDS immediate offsets), while any lane has one
+#pragma unroll
+                    for (int k = 0; k < kFP; ++k) {
+                        if (!__builtin_amdgcn_ballot_w64(cand != 0u)) break;
+                        if (cand) {
+                            dst[k] = (uint16_t)(ey + __builtin_ctz(cand));
+                            cand &= cand - 1u;
+                        }
                     }
                     nsurv += total;
                 }
@@ -2232,21 +2270,36 @@ constexpr int kDescPS = 48;                 // patch row stride (bytes): 43 + al
 constexpr int kBlurR = 18;
 constexpr int kRowCols = 40;                // row-pass outputs at patch columns 0..39
 constexpr int kColS = 44;                   // column-major row-pass buffer: stride (u16) of a column, rows 0..43
-// The row-pass buffer follows the patch directly, column-major: a sample's
-// seven column-pass inputs (rows r..r+6 of one column) are 14 contiguous
-// bytes, one unaligned ds_read_b128 (row 43 is padding the read may cover).
+// The row-pass buffer is column-major: a sample's seven column-pass inputs
+// (rows r..r+6 of one column) are 14 contiguous bytes, one unaligned
+// ds_read_b128 (row 43 is padding the read may cover).
 // The MFMA row pass reads 48 rows x 64 columns at the patch stride (rows
 // 43..47, and columns past 45 that wrap into the next row, are either
-// multiplied by zero taps or feed outputs that are never stored), so those
-// reads may run into the row buffer: they all precede the wave's stores.
-constexpr int kDescRowOff = (kDescP * kDescPS + 15) & ~15;             // 2064
-constexpr int kDescWaveLds = kDescRowOff + kRowCols * kColS * 2;      // 5584 B
+// multiplied by zero taps or feed outputs that are never stored), all of it
+// into registers before its first store: the patch is dead by then, so the
+// row buffer overlays it (ORBX_DESC_OVERLAY; 3.5 KB a wave instead of 5.5:
+// LDS no longer caps the occupancy).  Without the overlay the buffer follows
+// the patch and the row pass's reads may run into it (they still precede
+// the wave's stores).
+#ifndef ORBX_DESC_OVERLAY
+#define ORBX_DESC_OVERLAY 1
+#endif
+#ifndef ORBX_DESC_WAVES
+#define ORBX_DESC_WAVES 8   // waves per SIMD the launch bounds ask for (VGPR budget 512 / this)
+#endif
+constexpr int kDescRowOff = ORBX_DESC_OVERLAY ? 0 : (kDescP * kDescPS + 15) & ~15;   // 0 or 2064
+constexpr int kDescWaveLds = std::max(kDescRowOff + kRowCols * kColS * 2 + 8,    // (+ 8: the row pass's spill, below)
+                                      47 * kDescPS + 64);                         // 3528 or 5592 B
 static_assert((kDescR - 3 + kBlurR) + 7 < kColS, "a sample's 16-byte read stays in its column");
-constexpr int kDescWaveStride = (kDescWaveLds + 15) & ~15;
+#ifndef ORBX_DESC_PAD
+#define ORBX_DESC_PAD 0   // (occupancy probe: extra LDS bytes a wave)
+#endif
+constexpr int kDescWaveStride = (kDescWaveLds + ORBX_DESC_PAD + 15) & ~15;
 static_assert(47 * kDescPS + 63 < kDescWaveLds, "MFMA row-pass reads stay inside the wave's LDS");
 // LDS is allocated per workgroup in 512-byte granules: 4 waves + 48 B of
-// shared angle records must fit 7 workgroups in a CU's 160 KB
-static_assert(7 * ((4 * kDescWaveStride + 48 + 511) & ~511) <= 160 * 1024, "k_describe: 7 workgroups per CU");
+// shared angle records must fit ORBX_DESC_WAVES workgroups in a CU's 160 KB
+static_assert(ORBX_DESC_WAVES * ((4 * kDescWaveStride + 48 + 511) & ~511) <= 160 * 1024,
+              "k_describe: LDS for the occupancy the launch bounds ask");
 
 // The row pass as an int8 matrix product (v_mfma_i32_16x16x32_i8): outputs
 // j = 0..15 of a 16-column tile from the tile's 32 input columns,
@@ -2271,24 +2324,31 @@ struct RowTaps {
 __constant__ RowTaps c_row_taps = RowTaps();
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
+#ifndef ORBX_DESC_NOTAB
+#define ORBX_DESC_NOTAB 0   // timing probe only (wrong descriptors): no pattern / moment table loads
+#endif
 #ifndef ORBX_DESC_STAGE
 #define ORBX_DESC_STAGE 1   // 0: the generic wave_stage_rows
 #endif
-// k_describe's 43 x 43 patch inside the level: a row is nd = 11 or 12 dwords,
+// k_describe's 43 x 43 patch inside the level, staged with its column 0 at
+// patch column 2 (the keypoint at kDescKpCol = 23: the orientation disc in one
+// 32-column MFMA window): a row is 12 dwords from x0 - 2, unaligned loads
+// (the buffer base stays 4-aligned, the misalignment in the lane offset),
 // so 5 rows a pass (lanes (rl, k), rl < 5) and 9 passes cover rows rl + 5 j;
 // every row lane has j < 8, rows 40..42 (j = 8) only rl < 3.  One exec region
 // for the nine loads and stores (the generic loop guards each with its own
 // compare and exec save / restore: ~70 scalar instructions a wave), row
 // offsets as scalar multiples of the pitch, LDS offsets as immediates.
-// Stored XOR 0x80 (the int8 MFMAs' I - 128).  Returns o = x0 & 3.
-__device__ inline int stage_desc_patch(uint8_t *dst, const uint8_t *img, int pitch, int y0, int x0, int lane) {
-    static_assert(kDescP == 43 && kDescPS >= 48, "5 rows of <= 12 dwords a pass");
+// Stored XOR 0x80 (the int8 MFMAs' I - 128).  Needs x0 >= 2, x0 + 46 <= pitch.
+constexpr int kDescCol0 = kDescKpCol - kDescR;   // 2: the patch column of the window's column 0
+__device__ inline void stage_desc_patch(uint8_t *dst, const uint8_t *img, int pitch, int y0, int x0, int lane) {
+    static_assert(kDescP == 43 && kDescPS == 48 && kDescCol0 == 2, "5 rows of 12 dwords a pass");
     pitch = __builtin_amdgcn_readfirstlane(pitch);
-    const int xa = x0 & ~3, o = x0 - xa;
-    const int nd = (o + kDescP + 3) >> 2;   // 11 or 12
+    const int xs = x0 - kDescCol0, xa = xs & ~3, sh = xs - xa;
+    constexpr int nd = kDescPS / 4;
     const __amdgpu_buffer_rsrc_t src = wave_rsrc(img + (int64_t)y0 * pitch + xa);
-    const int rl = div_small(lane, nd), k = lane - mul24u(rl, nd);
-    const int voff = mul24u(rl, pitch) + 4 * k;
+    const int rl = lane / nd, k = lane - mul24u(rl, nd);
+    const int voff = mul24u(rl, pitch) + 4 * k + sh;
     const int p5 = __builtin_amdgcn_readfirstlane(5 * pitch);
     typedef __attribute__((address_space(3))) uint32_t lds_u32;
     lds_u32 *d = (lds_u32 *)(dst + mul24u(rl, kDescPS) + 4 * k);
@@ -2302,27 +2362,24 @@ __device__ inline int stage_desc_patch(uint8_t *dst, const uint8_t *img, int pit
         for (int j = 0; j < 8; ++j) d[j * 5 * kDescPS / 4] = v[j] ^ 0x80808080u;
         if (last) d[8 * 5 * kDescPS / 4] = v[8] ^ 0x80808080u;
     }
-    return o;
 }
 
 template <bool PIPE>
-__global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs fb, int s0, int ns, int write_total,
+__global__ __launch_bounds__(kThreads, ORBX_DESC_WAVES) void k_describe(DevPlan p, FrameBufs fb, int s0, int ns, int write_total,
                                                            uint32_t gmagic) {
     __shared__ __align__(16) uint8_t lds[4 * kDescWaveStride];
     __shared__ int s_mom[4][2];      // each wave's (m01, m10)
     __shared__ float s_ang[4][3];    // each wave's (angle, sin, cos), computed by wave 0
     PHASE_START();
     const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
-    // this lane's 4 pattern pairs (bytes x0 y0 x1 y1 of pairs 2j, 2j + 1,
-    // j = 64 grp + lane), fetched first so the loads overlap the staging
-    float4 pat[4];
-    // one buffer resource over the table, the loads at immediate offsets (the
-    // compiler otherwise rebuilds the symbol's address, s_getpc + add + addc, per load)
-    const __amdgpu_buffer_rsrc_t pat_rsrc = wave_rsrc(c_pattern_f);
+    // this lane's 4 pattern pairs (pairs 64 g + lane, g = 0..3, as fp8 bytes
+    // x0 y0 x1 y1 in word g), fetched first so the load overlaps the staging;
+    // one buffer resource over each table, the loads at immediate offsets (the
+    // compiler otherwise rebuilds a symbol's address, s_getpc + add + addc, per load)
+    const __amdgpu_buffer_rsrc_t pat_rsrc = wave_rsrc(&c_pattern_q);
     const long row_taps = (long)c_row_taps.t[lane];
-#pragma unroll
-    for (int grp = 0; grp < 4; ++grp)
-        pat[grp] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(pat_rsrc, 16 * lane + 1024 * grp, 0, 0));
+    const uint4 patq = ORBX_DESC_NOTAB ? make_uint4(0x38u * lane, 0x40u, 0x48u, 0xC4u)
+                                       : __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(pat_rsrc, 16 * lane, 0, 0));
     int bx, b;
     xcd_block_2d(bx, b, gmagic);
     const int slot = s0 + bx * 4 + wave;
@@ -2357,39 +2414,44 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
     // column-pass taps as u16 pairs for v_dot2_u32_u16 over rows (r, r+1), (r+2, r+3), (r+4, r+5), (r+6, r+7)
     constexpr u16x2 kK01 = {(unsigned short)k0, (unsigned short)k1}, kK23 = {(unsigned short)k2, (unsigned short)k3},
                     kK21 = {(unsigned short)k2, (unsigned short)k1}, kK0z = {(unsigned short)k0, 0};
-    int o = 0;
     if (valid) {
 
-    // 1. stage the 43x43 unblurred neighbourhood: aligned dword loads when it
-    //    lies inside the level, else byte loads with reflect-101 at the borders
+    // 1. stage the 43x43 unblurred neighbourhood at patch columns 2..44: dword
+    //    loads when it lies inside the level, else byte loads with reflect-101
+    //    at the borders
     int spitch;
     const uint8_t *img = level_ptr(p, fb, l, b, spitch);
     const int px0 = x - kDescR, py0 = y - kDescR;
-    const bool inside = px0 >= 0 && py0 >= 0 && x + kDescR < g.w && y + kDescR < g.h &&
-                        (px0 & ~3) + 4 * (((px0 & 3) + kDescP + 3) >> 2) <= spitch;
-    // the moment products' operand tables for this staging offset, loaded
-    // ahead of the patch so their latency hides under the staging's
+    const bool inside = px0 >= kDescCol0 && py0 >= 0 && x + kDescR < g.w && y + kDescR < g.h &&
+                        px0 - kDescCol0 + kDescPS <= spitch;
+    // the moment products' operand tables, loaded ahead of the patch so their
+    // latency hides under the staging's
     typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-    u64x2 mom[6];
+    u64x2 mom[3];
     {
-        const u64x2 *mt = reinterpret_cast<const u64x2 *>(&c_mom.mb[inside ? px0 & 3 : 0][0][0][lane][0]);
+        const __amdgpu_buffer_rsrc_t mom_rsrc = wave_rsrc(&c_mom);
 #pragma unroll
-        for (int t = 0; t < 6; ++t) mom[t] = mt[t * 64];
+        for (int t = 0; t < 3; ++t)
+            mom[t] = ORBX_DESC_NOTAB ? u64x2{0x00FFFF00FF00FFFFull * (uint64_t)(lane + t), 0x0102030405060708ull + t}
+                                     : __builtin_bit_cast(u64x2, __builtin_amdgcn_raw_buffer_load_b128(mom_rsrc, 16 * lane + 1024 * t, 0, 0));
     }
     if (inside) {
-        if constexpr (ORBX_DESC_STAGE) o = stage_desc_patch(lbase, img, spitch, py0, px0, lane);
-        else o = wave_stage_rows<(kDescP + 4) / 5, true, true>(lbase, kDescPS, img, spitch, py0, px0, kDescP, kDescP, lane);   // 5 rows a pass
+        if constexpr (ORBX_DESC_STAGE) stage_desc_patch(lbase, img, spitch, py0, px0, lane);
+        else wave_stage_rows<(kDescP + 4) / 5, true, true, kDescCol0>(lbase, kDescPS, img, spitch, py0, px0, kDescP, kDescP, lane);   // 5 rows a pass
     } else {
         // near a level border: lane = patch column (its reflect-101 column fixed),
-        // the rows in turn (the row's reflection is wave-uniform)
-        const int c = min(lane, kDescP - 1);
-        const int xx = reflect101(px0 + c, g.w);
+        // the rows in turn (the row's reflection is wave-uniform); columns
+        // outside the window are not needed (multiplied by zero taps or feeding
+        // unread outputs) and stay as they are
+        const int c = min(max(lane, kDescCol0), kDescCol0 + kDescP - 1);
+        const int xx = reflect101(px0 - kDescCol0 + c, g.w);
         const int sp = __builtin_amdgcn_readfirstlane(spitch);
+        const bool col = lane >= kDescCol0 && lane < kDescCol0 + kDescP;
 #pragma unroll 11
         for (int r = 0; r < kDescP; ++r) {
             const int yy = reflect101(py0 + r, g.h);
             const uint8_t v = img[(int64_t)yy * sp + xx];
-            if (lane < kDescP) lbase[r * kDescPS + lane] = v ^ 0x80;
+            if (col) lbase[r * kDescPS + lane] = v ^ 0x80;
         }
     }
     wave_lds_fence();
@@ -2410,17 +2472,18 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
 #pragma unroll
             for (int ct = 0; ct < 3; ++ct)
                 px[rt][ct] = *reinterpret_cast<const uint64_t *>(bsrc + 16 * rt * kDescPS + 16 * ct);
-        // moments: A = the disc's pixels of tiles (rt, ct = 0 / 2), B = c_mom.b;
-        // D[i][15] = sum of u I over row i, D[i][12 + rt] = sum of I over row
-        // 16 rt + i, summed over the six products (lane l: D[4 (l >> 4) + ii][l & 15])
+        // moments: A = the disc's pixels of the window tiles (rows 16 rt..,
+        // columns 8..39), B = c_mom.b; D[i][15] = sum of u I over row i,
+        // D[i][12 + rt] = sum of I over row 16 rt + i, summed over the three
+        // products (lane l: D[4 (l >> 4) + ii][l & 15])
         {
+            static_assert(kDescKpCol - 15 == 8, "the disc's columns start the 8-aligned window");
             i32x4 acc = {0, 0, 0, 0};
 #pragma unroll
-            for (int rt = 0; rt < 3; ++rt)
-#pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    acc = __builtin_amdgcn_mfma_i32_16x16x32_i8((long)(px[rt][2 * h] & mom[2 * rt + h].x),
-                                                                (long)mom[2 * rt + h].y, acc, 0, 0, 0);
+            for (int rt = 0; rt < 3; ++rt) {
+                const uint64_t pw = *reinterpret_cast<const uint64_t *>(bsrc + 16 * rt * kDescPS + 8);
+                acc = __builtin_amdgcn_mfma_i32_16x16x32_i8((long)(pw & mom[rt].x), (long)mom[rt].y, acc, 0, 0, 0);
+            }
             // m10: lane 15 of each row, S; m01: lanes 12..14, v-weighted rows
             // (v = 16 (j - 12) + 4 (l >> 4) + ii - 21), folded into lane 15
             const int j = rl;
@@ -2458,19 +2521,31 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
         const i32x4 bias = {128 * 257, 128 * 257, 128 * 257, 128 * 257};
         static_assert(kGaussTaps[0] + kGaussTaps[1] + kGaussTaps[2] + kGaussTaps[3] + kGaussTaps[4] +
                           kGaussTaps[5] + kGaussTaps[6] == 257, "bias = 128 * sum of the taps");
+        // Every lane stores (no exec regions): the outputs outside the buffer
+        // land where a later store of the same wave rewrites them (LDS stores
+        // of a wave complete in order; compiler barriers keep that order):
+        //  - rows 44..47 (rt = 2, q = 3) are rows 0..3 of the next column,
+        //    rewritten by the rt = 0 tiles, stored last (the last column's
+        //    go to the buffer's 8 spare bytes);
+        //  - columns 40..47 (ct = 2, rl >= 8) are sent to columns 0..7 of the
+        //    same rows, rewritten by the ct = 0 tile stored after it.
+        static_assert(kRowCols == 40 && kColS == 44, "the spill targets above");
         uint16_t *dst = rowp + rl * kColS + 4 * q;
+        uint16_t *dst2 = rowp + (rl < kRowCols - 32 ? rl + 32 : rl - 8) * kColS + 4 * q;   // tile ct = 2
+        auto store = [&](int rt, int ct) {
+            const i32x4 d = __builtin_amdgcn_mfma_i32_16x16x32_i8((long)px[rt][ct], row_taps, bias, 0, 0, 0);
+            uint2 w;
+            w.x = __builtin_amdgcn_perm((uint32_t)d[1], (uint32_t)d[0], 0x05040100u);   // (d0, d1) as u16 halves
+            w.y = __builtin_amdgcn_perm((uint32_t)d[3], (uint32_t)d[2], 0x05040100u);
+            *reinterpret_cast<uint2 *>((ct == 2 ? dst2 : dst + 16 * ct * kColS) + 16 * rt) = w;
+            asm volatile("" ::: "memory");
+        };
 #pragma unroll
-        for (int rt = 0; rt < 3; ++rt)
-#pragma unroll
-            for (int ct = 0; ct < 3; ++ct) {
-                const i32x4 d = __builtin_amdgcn_mfma_i32_16x16x32_i8((long)px[rt][ct], row_taps, bias, 0, 0, 0);
-                if ((rt < 2 || q < 3) && (ct < 2 || rl < kRowCols - 32)) {
-                    uint2 w;
-                    w.x = (uint32_t)d[0] | ((uint32_t)d[1] << 16);
-                    w.y = (uint32_t)d[2] | ((uint32_t)d[3] << 16);
-                    *reinterpret_cast<uint2 *>(dst + 16 * ct * kColS + 16 * rt) = w;
-                }
-            }
+        for (int rt = 2; rt >= 0; --rt) {
+            store(rt, 2);
+            store(rt, 0);
+            store(rt, 1);
+        }
     }
     PHASE_MARK(1, 2);   // row pass
     }   // kStopDesc
@@ -2522,15 +2597,15 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
     const bool all_even = x + kBlurR < xs;
     // all 8 of the lane's samples: offsets, then every column-pass read in
     // flight at once, then the rounding
-    // A sample at window offset (r, c) reads column c + kBlurR + o, rows
+    // A sample at window offset (r, c) reads column c + kBlurR + kDescCol0, rows
     // r + kBlurR .. +6 of the column-major buffer: byte offset
-    // 2 kColS (c + kBlurR + o) + 2 (r + kBlurR), from the cvRound'ed float
+    // 2 kColS (c + kBlurR + kDescCol0) + 2 (r + kBlurR), from the cvRound'ed float
     // bits (0x4B400000 + n, below) as one 24-bit multiply-add and one
     // shift-add; the constant folds the bias bits away (mod 2^32).  The read
     // is the four dwords from the one holding row r down (two ds_read2_b32;
     // unaligned ds_read_b128 measured 470 stall cycles a wave), and an odd
     // row's pairs are realigned by 16 bits (v_alignbit by a per-lane shift).
-    const uint32_t kOff = (uint32_t)(kDescRowOff + 2 * kColS * (kBlurR + o) + 2 * kBlurR) -
+    const uint32_t kOff = (uint32_t)(kDescRowOff + 2 * kColS * (kBlurR + kDescCol0) + 2 * kBlurR) -
                           (uint32_t)(2 * kColS) * 0x400000u - 2u * 0x4B400000u;
     static_assert((kDescRowOff & 3) == 0 && (kColS & 1) == 0, "dword-aligned column starts");
     typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
@@ -2539,14 +2614,28 @@ __global__ __launch_bounds__(kThreads, 7) void k_describe(DevPlan p, FrameBufs f
     // address is then one v_lshl_add and one v_mad_u32_u24 from the bits
     const uint32_t kOffL = __builtin_amdgcn_readfirstlane(kOff + (uint32_t)(uintptr_t)(const lds_u8 *)lbase);
     int sums[8], cbs[8];
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    // cvRound by the 1.5 * 2^23 bias: the float add rounds to the nearest
+    // integer, ties to even, and the bits are then 0x4B400000 + n (|n| < 2^22)
+    constexpr float kRndBias = 12582912.f;
+    const f32x2 sc = {sa, ca}, rnd2 = {kRndBias, kRndBias};
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        const float px = (k & 1) ? pat[k >> 1].z : pat[k >> 1].x, py = (k & 1) ? pat[k >> 1].w : pat[k >> 1].y;
-        // cvRound by the 1.5 * 2^23 bias: the float add rounds to the nearest
-        // integer, ties to even, and the bits are then 0x4B400000 + n (|n| < 2^22)
-        constexpr float kRndBias = 12582912.f;
-        const uint32_t rb = __float_as_uint(__fadd_rn(__fadd_rn(__fmul_rn(px, sa), __fmul_rn(py, ca)), kRndBias));
-        const uint32_t cb = __float_as_uint(__fadd_rn(__fsub_rn(__fmul_rn(px, ca), __fmul_rn(py, sa)), kRndBias));
+        const uint32_t pw = (k >> 1) == 0 ? patq.x : (k >> 1) == 1 ? patq.y : (k >> 1) == 2 ? patq.z : patq.w;
+        // (rb, cb) side by side as packed f32 pairs (v_pk_mul / v_pk_add:
+        // the same IEEE products and sums, two per instruction):
+        //   rb = (px sa + py ca) + bias,  cb = (px ca - py sa) + bias
+        // (written out: the compiler's own packing negates and moves pairs around)
+        const f32x2 pxy = (k & 1) ? __builtin_amdgcn_cvt_pk_f32_fp8((int)pw, true)      // (x, y) of point k
+                                  : __builtin_amdgcn_cvt_pk_f32_fp8((int)pw, false);
+        f32x2 rc, py2;
+        asm("v_pk_mul_f32 %0, %2, %3 op_sel_hi:[0,1]\n\t"               // (px sa, px ca)
+            "v_pk_mul_f32 %1, %2, %3 op_sel:[1,1] op_sel_hi:[1,0]\n\t"  // (py ca, py sa)
+            "v_pk_add_f32 %0, %0, %1 neg_hi:[0,1]\n\t"                  // (px sa + py ca, px ca - py sa)
+            "v_pk_add_f32 %0, %0, %4"                                   // + (bias, bias)
+            : "=&v"(rc), "=&v"(py2)
+            : "v"(pxy), "v"(sc), "s"(rnd2));
+        const uint32_t rb = __float_as_uint(rc.x), cb = __float_as_uint(rc.y);
         cbs[k] = (int)cb;
         // (__umul24 reads the low 24 bits of cb: 0x400000 + c, c in [-18, 18])
         uint32_t t, off;
@@ -2677,8 +2766,12 @@ FastLds fast_lds(int mw, int mh) {
     // the compass's last lane group reads up to column 4 + 8 ceil(mw / 8) + 3
     // (interior column 0 at patch column 4, ORBX_FAST_ALIGN)
     f.ps = std::max(f.ps, 8 * ((mw + 7) / 8) + 8);
-    f.sw = mw + 2;
-    if (f.ps <= 64) f.ps = f.sw = f.ps <= 48 ? 48 : 64;   // k_fast's constant-stride instantiations
+    if (f.ps <= 64) f.ps = f.ps <= 48 ? 48 : 64;   // k_fast's constant-stride instantiations
+    // the score map at the patch's stride: a survivor's list entry, its patch
+    // offset ey * ps + ex from interior pixel (0, 0), also indexes the map
+    // (cells are under 60 px a side, ORBextractor.cc:796-817: offsets < 2^13)
+    f.sw = f.ps;
+    f.pmag = (int)(((1u << 24) + f.ps - 1) / f.ps);
     f.patch_bytes = (f.ps * (mh + 6) + 15) & ~15;
     f.score_bytes = (f.sw * (mh + 2) + 15) & ~15;
     f.per_wave = f.patch_bytes + f.score_bytes + ((2 * f.list_cap + 15) & ~15);

@@ -1,0 +1,15 @@
+#!/bin/bash
+# r5m: k_fast offset-encoded lists + unrolled compaction; k_describe packed-f32 sample offsets,
+# exec-free row-pass stores
+set -uo pipefail
+mkdir -p gpurun_out
+timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_golden.py "tests/test_gpu_bench_configs.py::test_mono_bench_config_b3072" -x -q -m gpu --timeout 200 --timeout-method thread > gpurun_out/r5m_parity.log 2>&1
+rc=$?; tail -3 gpurun_out/r5m_parity.log; [ $rc -eq 0 ] || exit 1
+timeout -k 10 800 bash tools/ab_bench.sh r5m 3 orb_slam_2_ros_amd/liborbx_base.so orb_slam_2_ros_amd/liborbx_f.so orb_slam_2_ros_amd/liborbx.so || exit 1
+cd /tmp && export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+for L in base new; do
+  lib=$R/orb_slam_2_ros_amd/liborbx.so; [ $L = base ] && lib=$R/orb_slam_2_ros_amd/liborbx_base.so
+  ORBX_LIB=$lib ORBX_SPLIT=1 ORBX_PIPELINE=0 timeout -k 10 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAVE_CYCLES -d $R/gpurun_out/r5m_sq_$L -o pmc -- python $R/bench.py --steps 3 --warmup 1 --cpu-seconds 0 --no-extras --no-profile > $R/gpurun_out/r5m_sq_$L.log 2>&1 || exit 1
+done
+cd $R && for L in base new; do echo "== $L"; python tools/pmc_table.py gpurun_out/r5m_sq_$L/pmc_results.db --kernels k_fast k_describe; done
