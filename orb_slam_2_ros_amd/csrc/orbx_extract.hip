@@ -2757,11 +2757,25 @@ uint32_t grid_magic(uint32_t gx, uint32_t gy) {
 }
 }  // namespace
 
+#ifndef ORBX_FAST_LIST_CAP
+#define ORBX_FAST_LIST_CAP 640   // (survivor-list entries, at least what a compass step needs)
+#endif
 FastLds fast_lds(int mw, int mh) {
     FastLds f;
-    // survivor-list capacity: every pixel of the largest cell, or 640 (room
-    // for a step's 512 plus a row of waiting corners; k_fast flushes before)
-    f.list_cap = std::min(mw * mh, 640);
+    // survivor-list capacity: every pixel of the largest cell, or 640.  It
+    // must hold a row of waiting corners plus what one compass step can add,
+    // R rows of cw pixels (k_fast flushes before a step could overflow it):
+    // R = 64 / the lane groups of a row, (quads + 1) / 2 for the aligned
+    // staging's (cw + 3) / 4 quads (the unaligned fallback has more groups,
+    // fewer rows); 527 at VGA.  (Sized to that, 528, the launch fits 9
+    // workgroups per CU instead of 8 and measured slower: 2.61 -> 2.70 ms;
+    // 7 and 6 workgroups 2.71 and 2.88, profiles/r05_ab_fast_occupancy.txt.)
+    int need = 0;
+    for (int cw = 1; cw <= mw; ++cw) {
+        const int nq = (cw + 3) >> 2, np = (nq + 1) >> 1, R = 64 / np;
+        need = std::max(need, (R + 1) * cw);
+    }
+    f.list_cap = std::min(mw * mh, std::max(ORBX_FAST_LIST_CAP, (need + 7) & ~7));
     f.ps = (mw + 6 + 3 + 3) & ~3;   // + alignment offset, dword rows
     // the compass's last lane group reads up to column 4 + 8 ceil(mw / 8) + 3
     // (interior column 0 at patch column 4, ORBX_FAST_ALIGN)
@@ -2962,7 +2976,10 @@ bool plan_pyr_regions(Plan &hp) {
 
 // The region pyramid while one block per region and frame still leaves the
 // chip short of a block per CU.
-bool use_pyr_regions(const Plan &hp, int B) { return hp.rgn_n > 0 && (int64_t)B * hp.rgn_n <= 256; }
+#ifndef ORBX_RGN_MAX
+#define ORBX_RGN_MAX 256   // (region blocks a launch may take before the per-level kernels win)
+#endif
+bool use_pyr_regions(const Plan &hp, int B) { return hp.rgn_n > 0 && (int64_t)B * hp.rgn_n <= ORBX_RGN_MAX; }
 
 // Wave-tile geometry of every level (ResizeWave).  False when some level does
 // not fit the wave kernel (a column group spanning more than 7 source bytes,
