@@ -1267,9 +1267,14 @@ def main() -> int:
         run_cpu = world == 1 and args.cpu_seconds > 0 and not args.stub
         cpu = cpu_baseline(w, h, nf, args.cpu_seconds) if run_cpu else None
         if cpu is not None:
-            # the host's share of cores (OMP_NUM_THREADS on the GPU box), all at once
-            nthr = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1), 64))
+            # the host's share of cores, all at once: the CPUs this process may
+            # run on (its affinity set), capped by OMP_NUM_THREADS where the
+            # box sets its share that way (16 of 256 on the GPU box)
+            aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+            omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+            nthr = max(1, min(aff, omp or aff, 64))
             cpu["all_cores"] = cpu_baseline_threads(w, h, nf, max(2.0, args.cpu_seconds / 2), nthr)
+            cpu["all_cores"]["threads_from"] = {"affinity_cpus": aff, "OMP_NUM_THREADS": omp or None}
             # the timing build stays selected: every CPU time in extras uses it too
         full = world == 1 and not args.no_extras and not args.stub
         matchers = matcher_latencies() if full else None
