@@ -2380,6 +2380,18 @@ __global__ __launch_bounds__(kThreads, ORBX_DESC_WAVES) void k_describe(DevPlan 
     const long row_taps = (long)c_row_taps.t[lane];
     const uint4 patq = ORBX_DESC_NOTAB ? make_uint4(0x38u * lane, 0x40u, 0x48u, 0xC4u)
                                        : __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(pat_rsrc, 16 * lane, 0, 0));
+    // the moment products' operand tables (the same for every keypoint: the
+    // patch is staged with the keypoint at a fixed column), also before the
+    // key's chain of scalar loads, so their latency hides under it and the staging
+    typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+    u64x2 mom[3];
+    {
+        const __amdgpu_buffer_rsrc_t mom_rsrc = wave_rsrc(&c_mom);
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+            mom[t] = ORBX_DESC_NOTAB ? u64x2{0x00FFFF00FF00FFFFull * (uint64_t)(lane + t), 0x0102030405060708ull + t}
+                                     : __builtin_bit_cast(u64x2, __builtin_amdgcn_raw_buffer_load_b128(mom_rsrc, 16 * lane + 1024 * t, 0, 0));
+    }
     int bx, b;
     xcd_block_2d(bx, b, gmagic);
     const int slot = s0 + bx * 4 + wave;
@@ -2424,17 +2436,6 @@ __global__ __launch_bounds__(kThreads, ORBX_DESC_WAVES) void k_describe(DevPlan 
     const int px0 = x - kDescR, py0 = y - kDescR;
     const bool inside = px0 >= kDescCol0 && py0 >= 0 && x + kDescR < g.w && y + kDescR < g.h &&
                         px0 - kDescCol0 + kDescPS <= spitch;
-    // the moment products' operand tables, loaded ahead of the patch so their
-    // latency hides under the staging's
-    typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-    u64x2 mom[3];
-    {
-        const __amdgpu_buffer_rsrc_t mom_rsrc = wave_rsrc(&c_mom);
-#pragma unroll
-        for (int t = 0; t < 3; ++t)
-            mom[t] = ORBX_DESC_NOTAB ? u64x2{0x00FFFF00FF00FFFFull * (uint64_t)(lane + t), 0x0102030405060708ull + t}
-                                     : __builtin_bit_cast(u64x2, __builtin_amdgcn_raw_buffer_load_b128(mom_rsrc, 16 * lane + 1024 * t, 0, 0));
-    }
     if (inside) {
         if constexpr (ORBX_DESC_STAGE) stage_desc_patch(lbase, img, spitch, py0, px0, lane);
         else wave_stage_rows<(kDescP + 4) / 5, true, true, kDescCol0>(lbase, kDescPS, img, spitch, py0, px0, kDescP, kDescP, lane);   // 5 rows a pass
