@@ -877,6 +877,45 @@ def run_config(torch, dist, rank, world, dev, w, h, nfeatures, streams, steps, w
     return el, stages, len(kp), sane, float(batch), ex   # the profiled launches cover the whole batch
 
 
+HOST_FED_STREAMS = "cumask"   # (tools/host_fed_probe.py: "pool" = torch's stream pool)
+_hip_rt = None
+
+
+def dedicated_stream(torch, dev):
+    """A stream on a hardware queue of its own: hipExtStreamCreateWithCUMask
+    (every CU enabled) makes the runtime create a new queue for it rather
+    than share one of the process's pooled queues."""
+    global _hip_rt
+    if HOST_FED_STREAMS == "pool":
+        return torch.cuda.Stream(dev)
+    import ctypes
+    if _hip_rt is None:
+        _hip_rt = ctypes.CDLL("libamdhip64.so")
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    words = (ncu + 31) // 32
+    mask = (ctypes.c_uint32 * words)(*([0xFFFFFFFF] * words))
+    s = ctypes.c_void_p()
+    torch.cuda.set_device(dev)
+    rc = _hip_rt.hipExtStreamCreateWithCUMask(ctypes.byref(s), ctypes.c_uint32(words), mask)
+    if rc != 0:
+        raise RuntimeError(f"hipExtStreamCreateWithCUMask: {rc}")
+    return torch.cuda.ExternalStream(s.value, device=dev)
+
+
+_hf_streams = {}
+
+
+def host_fed_streams(torch, dev):
+    """The host-fed runs' compute / upload / download streams, made once per
+    process and reused (torch keeps referring to external streams it has
+    run work on, so they are never destroyed: destroying them crashed the
+    process on exit)."""
+    key = (HOST_FED_STREAMS, dev.index)
+    if key not in _hf_streams:
+        _hf_streams[key] = tuple(dedicated_stream(torch, dev) for _ in range(3))
+    return _hf_streams[key]
+
+
 def host_fed(torch, dev, w, h, nfeatures, nstreams, split, pipeline, steps, warmup):
     """The mono step fed from host memory, as a camera-fed node sees it
     (ros/src/MonoNode.cc:38-50 -> Frame.cc:259-265: each frame arrives in a host
@@ -899,8 +938,12 @@ def host_fed(torch, dev, w, h, nfeatures, nstreams, split, pipeline, steps, warm
     ex.split(split)
     ex.pipeline(pipeline)
     dbuf = torch.empty((2, nstreams, h, w), dtype=torch.uint8, device=dev)
-    s_comp = torch.cuda.current_stream(dev)
-    s_up, s_down = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    # compute, upload and download on three streams of their own hardware
+    # queues: HIP spreads a process's streams over its few queues
+    # (GPU_MAX_HW_QUEUES), and a copy stream that shares the compute stream's
+    # queue waits behind its kernels (180 k -> 124 k frames/s,
+    # tools/host_fed_probe.py)
+    s_comp, s_up, s_down = host_fed_streams(torch, dev)
     # the pack layout's size (known once a batch of this size has run)
     ex.mono_step_device(dbuf[0].data_ptr(), h * w, w, nstreams, 100, 0.9, True, s_comp.cuda_stream)
     torch.cuda.synchronize(dev)
