@@ -482,6 +482,24 @@ struct Parts {
     hipStream_t s[orbx_extractor::kMaxParts] = {};
 };
 
+// A stream for the extractor's own forks (batch parts, level pipeline).
+// ORBX_QUEUES=dedicated: one made by hipExtStreamCreateWithCUMask (every CU),
+// which the runtime gives a hardware queue of its own, so two forks never
+// share one of the process's pooled queues (GPU_MAX_HW_QUEUES) and serialise.
+hipError_t fork_stream(hipStream_t *s) {
+    static const bool dedicated = [] {
+        const char *q = std::getenv("ORBX_QUEUES");
+        return q && std::strcmp(q, "dedicated") == 0;
+    }();
+    if (!dedicated) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+        return hipErrorInvalidValue;
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0xFFFFFFFFu);
+    return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
+}
+
 // Splits `batch` into sub-batches on the part streams (forked from st), or a
 // single part on st itself.
 Parts fork_parts(orbx_extractor *ex, hipStream_t st, int batch) {
@@ -493,7 +511,7 @@ Parts fork_parts(orbx_extractor *ex, hipStream_t st, int batch) {
     if (!ex->fork_ev) {
         bool ok = hipEventCreateWithFlags(&ex->fork_ev, hipEventDisableTiming) == hipSuccess;
         for (int k = 0; k < orbx_extractor::kMaxParts && ok; ++k)
-            ok = hipStreamCreateWithFlags(&ex->part_stream[k], hipStreamNonBlocking) == hipSuccess &&
+            ok = fork_stream(&ex->part_stream[k]) == hipSuccess &&
                  hipEventCreateWithFlags(&ex->done_ev[k], hipEventDisableTiming) == hipSuccess;
         if (!ok) { ex->split = 1; return P; }
     }
@@ -560,7 +578,7 @@ bool make_pipe(orbx_extractor *ex) {
     const unsigned f = hipEventDisableTiming;
     bool ok = true;
     for (auto &ps : ex->pipe) {
-        for (auto &x : ps.s) ok = ok && hipStreamCreateWithFlags(&x, hipStreamNonBlocking) == hipSuccess;
+        for (auto &x : ps.s) ok = ok && fork_stream(&x) == hipSuccess;
         ok = ok && hipEventCreateWithFlags(&ps.fork, f) == hipSuccess && hipEventCreateWithFlags(&ps.level0, f) == hipSuccess;
         for (auto &e : ps.done) ok = ok && hipEventCreateWithFlags(&e, f) == hipSuccess;
     }
