@@ -2372,26 +2372,6 @@ __global__ __launch_bounds__(kThreads, ORBX_DESC_WAVES) void k_describe(DevPlan 
     __shared__ float s_ang[4][3];    // each wave's (angle, sin, cos), computed by wave 0
     PHASE_START();
     const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
-    // this lane's 4 pattern pairs (pairs 64 g + lane, g = 0..3, as fp8 bytes
-    // x0 y0 x1 y1 in word g), fetched first so the load overlaps the staging;
-    // one buffer resource over each table, the loads at immediate offsets (the
-    // compiler otherwise rebuilds a symbol's address, s_getpc + add + addc, per load)
-    const __amdgpu_buffer_rsrc_t pat_rsrc = wave_rsrc(&c_pattern_q);
-    const long row_taps = (long)c_row_taps.t[lane];
-    const uint4 patq = ORBX_DESC_NOTAB ? make_uint4(0x38u * lane, 0x40u, 0x48u, 0xC4u)
-                                       : __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(pat_rsrc, 16 * lane, 0, 0));
-    // the moment products' operand tables (the same for every keypoint: the
-    // patch is staged with the keypoint at a fixed column), also before the
-    // key's chain of scalar loads, so their latency hides under it and the staging
-    typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-    u64x2 mom[3];
-    {
-        const __amdgpu_buffer_rsrc_t mom_rsrc = wave_rsrc(&c_mom);
-#pragma unroll
-        for (int t = 0; t < 3; ++t)
-            mom[t] = ORBX_DESC_NOTAB ? u64x2{0x00FFFF00FF00FFFFull * (uint64_t)(lane + t), 0x0102030405060708ull + t}
-                                     : __builtin_bit_cast(u64x2, __builtin_amdgcn_raw_buffer_load_b128(mom_rsrc, 16 * lane + 1024 * t, 0, 0));
-    }
     int bx, b;
     xcd_block_2d(bx, b, gmagic);
     const int slot = s0 + bx * 4 + wave;
@@ -2403,7 +2383,30 @@ __global__ __launch_bounds__(kThreads, ORBX_DESC_WAVES) void k_describe(DevPlan 
     // output offset is the prefix below its level (16-lane DPP scan)
     const int32_t *lc = fb.level_count + (int64_t)b * kMaxLevels;
     const int lq = lane & (kMaxLevels - 1);
-    const int cq = lane < p.nlevels ? max(lc[lq], 0) : 0;
+    const int lcv = lc[lq];   // (every lane: a frame holds kMaxLevels counts)
+    // the tables after the level counts: the scan below waits for the
+    // counts alone (vector loads complete in order), not for the tables
+    // this lane's 4 pattern pairs (pairs 64 g + lane, g = 0..3, as fp8 bytes
+    // x0 y0 x1 y1 in word g), fetched first so the load overlaps the staging;
+    // one buffer resource over each table, the loads at immediate offsets (the
+    // compiler otherwise rebuilds a symbol's address, s_getpc + add + addc, per load)
+    const __amdgpu_buffer_rsrc_t pat_rsrc = wave_rsrc(&c_pattern_q);
+    const long row_taps = (long)c_row_taps.t[lane];
+    const uint4 patq = ORBX_DESC_NOTAB ? make_uint4(0x38u * lane, 0x40u, 0x48u, 0xC4u)
+                                       : __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(pat_rsrc, 16 * lane, 0, 0));
+    // the moment products' operand tables (the same for every keypoint: the
+    // patch is staged with the keypoint at a fixed column), ahead of the
+    // key's chain of scalar loads and the staging, whose latency they hide under
+    typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+    u64x2 mom[3];
+    {
+        const __amdgpu_buffer_rsrc_t mom_rsrc = wave_rsrc(&c_mom);
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+            mom[t] = ORBX_DESC_NOTAB ? u64x2{0x00FFFF00FF00FFFFull * (uint64_t)(lane + t), 0x0102030405060708ull + t}
+                                     : __builtin_bit_cast(u64x2, __builtin_amdgcn_raw_buffer_load_b128(mom_rsrc, 16 * lane + 1024 * t, 0, 0));
+    }
+    const int cq = lane < p.nlevels ? max(lcv, 0) : 0;
     static_assert(kMaxLevels == 16, "one DPP row");
     uint32_t scan = (uint32_t)cq;
     scan += dpp_or<kRowShr1>(0u, scan);
