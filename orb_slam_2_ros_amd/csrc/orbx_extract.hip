@@ -900,7 +900,22 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
     xcd_block_2d(bx, b, gmagic);
     if (bx * 4 + wave >= nc) return;
     const int ci = c0 + bx * 4 + wave;
-    const Cell c = p.cells[ci];
+    // the cell as five dwords: scalar loads (a 16-bit field would take a
+    // vector load, and a vector round trip, ahead of the staging)
+    static_assert(sizeof(Cell) == 20, "five dwords");
+    Cell c;
+    {
+        const uint32_t *cp = reinterpret_cast<const uint32_t *>(p.cells) + 5 * ci;
+        const uint32_t w0 = cp[0], w1 = cp[1], w2 = cp[2];
+        c.level = (int16_t)(w0 & 0xFFFFu);
+        c.pad = 0;
+        c.x0 = (int16_t)(w1 & 0xFFFFu);
+        c.y0 = (int16_t)(w1 >> 16);
+        c.x1 = (int16_t)(w2 & 0xFFFFu);
+        c.y1 = (int16_t)(w2 >> 16);
+        c.slot = (int32_t)cp[3];
+        c.cap = (int32_t)cp[4];
+    }
     int32_t *count_out = fb.cell_count + (int64_t)b * p.ncells + ci;
     const int cw = c.x1 - c.x0, ch = c.y1 - c.y0;
     if (cw <= 0 || ch <= 0) {
