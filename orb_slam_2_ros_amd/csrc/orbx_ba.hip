@@ -680,6 +680,68 @@ bool sums_ready() {
     return ok;
 }
 
+// Fast mode's trial readback, reduced on the device (parallel sums: equal to
+// the host's ordered sums to rounding): out[0] = sum of rho0 over the active
+// edges (activeRobustChi2); with x: out[1] = x (lambda x + b), poses then
+// points (computeScale); out[2] = the solve flag; with Hpp: out[3] = the
+// largest |diagonal| of the free vertices (computeLambdaInit).  kFastSumBlocks
+// workgroups write partials; the last to finish (a counter it resets) folds
+// them in block order, so the result does not depend on the schedule.
+constexpr int kFastSumThreads = 256, kFastSumBlocks = 64;
+__global__ __launch_bounds__(kFastSumThreads) void k_ba_fast_sums(const double *rho0, const uint8_t *active, int ne,
+                                                                  const double *x, const double *bp, const double *bl,
+                                                                  int n, int m, double lambda, const int *ok,
+                                                                  const double *Hpp, int nf, const double *Hll, int np,
+                                                                  double *part, unsigned *counter, double *out) {
+    __shared__ double red[3][kFastSumThreads / 64];
+    __shared__ bool last;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int gt = blockIdx.x * kFastSumThreads + tid, gs = gridDim.x * kFastSumThreads;
+    double chi = 0, sc = 0, mx = 0;
+    if (rho0)
+        for (int e = gt; e < ne; e += gs)
+            if (active[e]) chi += rho0[e];
+    if (x && (!ok || *ok))
+        for (int j = gt; j < m; j += gs) {
+            const double xj = x[j];
+            sc += xj * (lambda * xj + (j < n ? bp[j] : bl[j - n]));
+        }
+    if (Hpp) {
+        for (int q = gt; q < 6 * nf; q += gs) mx = fmax(mx, fabs(Hpp[36 * (q / 6) + 7 * (q % 6)]));
+        for (int q = gt; q < 3 * np; q += gs) mx = fmax(mx, fabs(Hll[9 * (q / 3) + 4 * (q % 3)]));
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        chi += __shfl_xor(chi, o);
+        sc += __shfl_xor(sc, o);
+        mx = fmax(mx, __shfl_xor(mx, o));
+    }
+    if (lane == 0) { red[0][w] = chi; red[1][w] = sc; red[2][w] = mx; }
+    __syncthreads();
+    if (tid == 0) {
+        double c = 0, t = 0, d = 0;
+        for (int k = 0; k < kFastSumThreads / 64; ++k) { c += red[0][k]; t += red[1][k]; d = fmax(d, red[2][k]); }
+        part[3 * blockIdx.x] = c;
+        part[3 * blockIdx.x + 1] = t;
+        part[3 * blockIdx.x + 2] = d;
+        __threadfence();
+        last = atomicAdd(counter, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last || tid != 0) return;
+    __threadfence();
+    double c = 0, t = 0, d = 0;
+    for (int k = 0; k < (int)gridDim.x; ++k) {
+        c += __builtin_nontemporal_load(&part[3 * k]);
+        t += __builtin_nontemporal_load(&part[3 * k + 1]);
+        d = fmax(d, __builtin_nontemporal_load(&part[3 * k + 2]));
+    }
+    out[0] = c;
+    out[1] = t;
+    out[2] = ok ? (double)*ok : 1.0;
+    out[3] = d;
+    *counter = 0;
+}
+
 __global__ void k_ba_restore(Pose *poses, int ncam, double *pts, int npt, const Pose *pose_bk, const double *pts_bk) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < ncam) poses[i] = pose_bk[i];
@@ -1184,10 +1246,11 @@ public:
     int update_gated();
     int read_errors();
     int read_diag();
-    int read_trial();
+    int read_trial(double lambda);
     double chi_sum_host() const;
     double max_diag_host() const;
     double scale_host(double lambda) const;
+    bool trial_ok() const { return fast_ ? h_fsum[2] != 0 : *h_ok != 0; }
     int pop();
     int download(double *pts, std::vector<double> &chi2, std::vector<uint8_t> &front);
     // (the buffers belong to the workspace)
@@ -1227,6 +1290,9 @@ public:
     size_t span_ = 0;      // bytes from d_ok to the end of d_bl
     bool s_zero_ = false;  // d_S's non-pair blocks are zero
     int *h_ok = nullptr;
+    double *d_fsum = nullptr, *h_fsum = nullptr;   // fast mode's device-reduced readback (k_ba_fast_sums)
+    double *d_fpart = nullptr;                     // its per-workgroup partials
+    unsigned *d_fcount = nullptr;                  // its finished-workgroup counter (zeroed by alloc, reset by the last)
     uint8_t *h_stage = nullptr;                // set_active's uploads: flags, then h_coffs_ | clist
     int32_t *h_coffs_ = nullptr;
 };
@@ -1315,6 +1381,9 @@ int BA::alloc() {
     d_bl = carve<double>(p, 3 * np);
     span_ = (size_t)(p - reinterpret_cast<uint8_t *>(d_ok));
     d_cmap = carve<int32_t>(p, nf * np);
+    d_fsum = carve<double>(p, 4);
+    d_fpart = carve<double>(p, 3 * kFastSumBlocks);
+    d_fcount = carve<unsigned>(p, 4);
     d_db = carve<double>(p, 3 * np);
     d_rows = carve<double>(p, 42 * ne);
     d_raw = carve<orbx_ba_edge>(p, ne);
@@ -1335,6 +1404,7 @@ int BA::alloc() {
         h_ok = carve<int>(h, 1); h_rho0 = carve<double>(h, ne); h_x = carve<double>(h, m);
         h_bp = carve<double>(h, 6 * nf); h_bl = carve<double>(h, 3 * np);
         h_hpp = carve<double>(h, 36 * nf); h_hll = carve<double>(h, 9 * np);
+        h_fsum = carve<double>(h, 4);
         h_stage = carve<uint8_t>(h, 2 * ne); h_coffs_ = carve<int32_t>(h, nf + 1 + ne);
         if ((size_t)(h - hbuf_) > hb) return ORBX_ENOMEM;
     }
@@ -1373,7 +1443,8 @@ int BA::alloc() {
 }
 
 int BA::upload(const double *pts) {
-    if (hipMemcpyAsync(d_pose, g_.poses.data(), sizeof(Pose) * g_.ncam, hipMemcpyHostToDevice, st_) != hipSuccess ||
+    if ((fast_ && hipMemsetAsync(d_fcount, 0, 16, st_) != hipSuccess) ||   // (k_ba_fast_sums' counter)
+        hipMemcpyAsync(d_pose, g_.poses.data(), sizeof(Pose) * g_.ncam, hipMemcpyHostToDevice, st_) != hipSuccess ||
         (g_.npt && hipMemcpyAsync(d_pts, pts, 24 * (size_t)g_.npt, hipMemcpyHostToDevice, st_) != hipSuccess))
         return ORBX_EIO;
     return ORBX_OK;
@@ -1571,12 +1642,25 @@ int BA::update_gated() {   // (the trial's backup of the estimate is written by 
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
 }
 
+// (fast mode: the sums reduced on the device, 32 bytes back instead of the
+// per-edge errors and the step; the ordered mode sums on the host in order)
 int BA::read_errors() {
+    if (fast_) {
+        hipLaunchKernelGGL(k_ba_fast_sums, dim3(kFastSumBlocks), dim3(kFastSumThreads), 0, st_, d_rho0, d_active, g_.ne,
+                           nullptr, nullptr, nullptr, 0, 0, 0.0, nullptr, nullptr, 0, nullptr, 0, d_fpart, d_fcount, d_fsum);
+        return hipMemcpyAsync(h_fsum, d_fsum, 32, hipMemcpyDeviceToHost, st_) == hipSuccess ? ORBX_OK : ORBX_EIO;
+    }
     return (g_.ne && hipMemcpyAsync(h_rho0, d_rho0, 8 * (size_t)g_.ne, hipMemcpyDeviceToHost, st_) != hipSuccess)
                ? ORBX_EIO : ORBX_OK;
 }
 
 int BA::read_diag() {
+    if (fast_) {   // (after read_errors: the chi sum is kept)
+        hipLaunchKernelGGL(k_ba_fast_sums, dim3(kFastSumBlocks), dim3(kFastSumThreads), 0, st_, d_rho0, d_active, g_.ne,
+                           nullptr, nullptr, nullptr, 0, 0, 0.0, nullptr, d_Hpp, g_.nf, d_Hll, g_.npt, d_fpart, d_fcount,
+                           d_fsum);
+        return hipMemcpyAsync(h_fsum, d_fsum, 32, hipMemcpyDeviceToHost, st_) == hipSuccess ? ORBX_OK : ORBX_EIO;
+    }
     if ((g_.nf && hipMemcpyAsync(h_hpp, d_Hpp, 8 * 36 * (size_t)g_.nf, hipMemcpyDeviceToHost, st_) != hipSuccess) ||
         (g_.npt && hipMemcpyAsync(h_hll, d_Hll, 8 * 9 * (size_t)g_.npt, hipMemcpyDeviceToHost, st_) != hipSuccess))
         return ORBX_EIO;
@@ -1585,11 +1669,18 @@ int BA::read_diag() {
 
 // a trial's readback: the solve flag, the errors at the trial estimate, and
 // x and b for computeScale
-int BA::read_trial() {
+int BA::read_trial(double lambda) {
+    if (fast_) {
+        const int n = 6 * g_.nf, m = n + 3 * g_.npt;
+        hipLaunchKernelGGL(k_ba_fast_sums, dim3(kFastSumBlocks), dim3(kFastSumThreads), 0, st_, d_rho0, d_active, g_.ne,
+                           d_x, d_bp, d_bl, n, m, lambda, d_ok, nullptr, 0, nullptr, 0, d_fpart, d_fcount, d_fsum);
+        return hipMemcpyAsync(h_fsum, d_fsum, 32, hipMemcpyDeviceToHost, st_) == hipSuccess ? ORBX_OK : ORBX_EIO;
+    }
     return hipMemcpyAsync(h_ok, d_ok, span_, hipMemcpyDeviceToHost, st_) == hipSuccess ? ORBX_OK : ORBX_EIO;
 }
 
 double BA::chi_sum_host() const {   // activeRobustChi2: active edges in order
+    if (fast_) return h_fsum[0];
     double s = 0;
     for (int e = 0; e < g_.ne; ++e)
         if (act_[e]) s += h_rho0[e];
@@ -1597,6 +1688,7 @@ double BA::chi_sum_host() const {   // activeRobustChi2: active edges in order
 }
 
 double BA::max_diag_host() const {   // computeLambdaInit: max |diagonal| over the free vertices
+    if (fast_) return h_fsum[3];
     double mx = 0.;
     for (int f = 0; f < g_.nf; ++f)
         for (int j = 0; j < 6; ++j) mx = std::max(std::fabs(h_hpp[36 * (size_t)f + 7 * j]), mx);
@@ -1606,6 +1698,7 @@ double BA::max_diag_host() const {   // computeLambdaInit: max |diagonal| over t
 }
 
 double BA::scale_host(double lambda) const {   // computeScale: x (lambda x + b), poses then points
+    if (fast_) return h_fsum[1];
     const int m = 6 * g_.nf + 3 * g_.npt;
     double s = 0.;
     const int n = 6 * g_.nf;
@@ -1668,10 +1761,10 @@ int lm_optimize(BA &ba, int iters, bool robust, int *rc_out) {
         int qmax = 0;
         do {
             if ((rc = ba.solve_async(lambda)) || (rc = ba.update_gated()) ||
-                (rc = ba.errors_async(robust, ba.d_ok)) || (rc = ba.read_trial()))
+                (rc = ba.errors_async(robust, ba.d_ok)) || (rc = ba.read_trial(lambda)))
                 return fail(rc);
             if (hipStreamSynchronize(ba.st_) != hipSuccess) return fail(ORBX_EIO);
-            const bool ok = *ba.h_ok != 0;
+            const bool ok = ba.trial_ok();
             // (the reference updates with an unsolved x; the step is rejected either way)
             const double tempChi = ok ? ba.chi_sum_host() : DBL_MAX;
             rho = currentChi - tempChi;
