@@ -37,6 +37,8 @@ struct DevPlan {
     const Cell *cells;
     const ResizeTap *xtaps;
     const ResizeTap *ytaps;
+    const ResizeCol *rcols;   // k_resize_d column groups / rows (Plan::rcols, rrows)
+    const ResizeRow *rrows;
     const int4 *blur_tiles;   // (level, x0, y0, 0) per 64x16 output tile
     const uint32_t *slot_level;  // level of each output slot (out_cap entries): k_describe's one scalar load
     int nlevels, ncells, nblur_tiles;

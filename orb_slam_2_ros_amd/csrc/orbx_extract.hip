@@ -506,6 +506,21 @@ __host__ __device__ inline int resize_src_raw(int d, double scale) {
 #endif
 }
 
+// The SSE2 columns' vertical pass of 4 columns, packed into one dword:
+// ((h0 >> 4) b0 >> 16) + ((h1 >> 4) b1 >> 16), + 2, >> 2 (each sum <= 1022),
+// the >> 16 as the high half of (h & ~15) x (b << 12) (24-bit operands, bb =
+// b << 12).  Two sums share a dword (s0 + s1 << 16 + 0x20002, no carry between
+// the halves), one shift rounds both, one v_perm packs the four bytes.
+__device__ inline uint32_t resize_vpass_simd(const uint32_t h0[4], const uint32_t h1[4], uint32_t bb0, uint32_t bb1) {
+    uint32_t sm[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        sm[k] = (uint32_t)(((uint64_t)(h0[k] & 0xFFFF0u) * bb0) >> 32) + (uint32_t)(((uint64_t)(h1[k] & 0xFFFF0u) * bb1) >> 32);
+    const uint32_t p01 = ((sm[1] << 16) + sm[0] + 0x00020002u) >> 2;
+    const uint32_t p23 = ((sm[3] << 16) + sm[2] + 0x00020002u) >> 2;
+    return __builtin_amdgcn_perm(p23, p01, 0x06040200u);
+}
+
 // One wave tile (ResizeWave) of level l of frame b; `win` is the wave's LDS
 // slice (a.win_bytes).
 template <int NB>
@@ -604,12 +619,7 @@ __device__ inline void resize_tile(const DevPlan &p, const FrameBufs &fb, int l,
             // ((h >> 4) * b) >> 16 as the high half of a 24 x 24-bit product:
             // (h & ~15) * (b << 12) = ((h >> 4) * b) << 16, both operands < 2^24
             const uint32_t bb0 = ((uint32_t)b0 & 0xFFFu) << 12, bb1 = ((uint32_t)b1 & 0xFFFu) << 12;   // (b <= 2048)
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t t0 = (uint32_t)(((uint64_t)(h0[k] & 0xFFFF0u) * bb0) >> 32);
-                const uint32_t t1 = (uint32_t)(((uint64_t)(h1[k] & 0xFFFF0u) * bb1) >> 32);
-                packed |= ((t0 + t1 + 2) >> 2) << (8 * k);
-            }
+            packed = resize_vpass_simd(h0, h1, bb0, bb1);
 #else
 #pragma unroll
             for (int k = 0; k < 4; ++k)
@@ -637,6 +647,134 @@ __global__ __launch_bounds__(kThreads) void k_resize_w(DevPlan p, FrameBufs fb, 
     if (t >= a.ntiles * B) return;
     const int b = t / a.ntiles;
     resize_tile<NB>(p, fb, l, a, b, t - b * a.ntiles, lane, lds + wave * a.win_bytes);
+}
+
+// ===========================================================================
+// K1 (direct wave tiles): the same tiles and arithmetic without the LDS
+// window.  A lane's 4 columns read source bytes sx_0 .. sx_3 + 1, at most 7
+// apart (plan_resize_waves), so each source row is ONE dword-aligned 12-byte
+// buffer load (8 bytes from cs = min(sx_0, w_src - 8) after v_alignbyte; a
+// pair byte past them, only the last column's S[sx + 1] whose coefficient is
+// 0 there, is selected as zero).  The lane's column constants (load column,
+// realignment, v_perm selectors, coefficients) and its rows' clamped source
+// rows and vertical coefficients are host tables (ResizeCol, ResizeRow), so
+// the kernel does no tap arithmetic.  The window staging (half of
+// resize_tile's VALU: predicated loads and LDS stores a row) goes; L1/L2
+// serve the rows the lanes share.  Unaligned 8-byte loads instead of the
+// 12-byte aligned ones measured slower (resize 1.80 vs 1.52 ms a step,
+// profiles/r05_ab_resize_direct.txt).
+// ===========================================================================
+#ifndef ORBX_RS_DIRECT
+#define ORBX_RS_DIRECT 1
+#endif
+
+__device__ inline void resize_tile_direct(const DevPlan &p, const FrameBufs &fb, int l, const ResizeWave &a, int b,
+                                          int tile, int lane) {
+    const int ty = tile / a.ntx, tx = tile - ty * a.ntx;
+    const LevelArgs g = p.la[l], gs = p.la[l - 1];
+    const int twg = a.twg, lr = lane >> a.twg_shift, lg = lane & (twg - 1);
+    const int TH = (64 >> a.twg_shift) * kResizeK;
+    const int x0 = tx * 4 * twg, y0 = ty * TH;
+    const int xb = x0 + 4 * lg, yb = y0 + lr * kResizeK;
+    if (xb >= g.w) return;
+    // this lane's column group and rows (host tables: no per-lane tap arithmetic)
+    const __amdgpu_buffer_rsrc_t ct = wave_rsrc(p.rcols + a.col_off), rt = wave_rsrc(p.rrows + a.ytab_off);
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+    const u32x3 cg0 = __builtin_amdgcn_raw_buffer_load_b96(ct, 12 * xb, 0, 0);     // c, o, smask
+    const u32x4 cg1 = __builtin_amdgcn_raw_buffer_load_b128(ct, 12 * xb + 16, 0, 0);   // sel
+    const u32x4 cg2 = __builtin_amdgcn_raw_buffer_load_b128(ct, 12 * xb + 32, 0, 0);   // coef
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    u32x2 rw[kResizeK];
+#pragma unroll
+    for (int j = 0; j < kResizeK; ++j) rw[j] = __builtin_amdgcn_raw_buffer_load_b64(rt, 8 * min(yb + j, g.h - 1), 0, 0);
+    int spitch;
+    __amdgpu_buffer_rsrc_t src = wave_rsrc(level_ptr(p, fb, l - 1, b, spitch));
+    spitch = __builtin_amdgcn_readfirstlane(spitch);
+    if (l == 1) {
+        // level 0 is the caller's image: the buffer's range ends at its last
+        // row's last dword (a dword never crosses a page), so the dword loads
+        // of the last row's right end cannot fault
+        const uint64_t a0 = reinterpret_cast<uint64_t>(level_ptr(p, fb, 0, b, spitch));
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a0), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a0 >> 32));
+        src = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), (short)0,
+                                                ((gs.h - 1) * spitch + gs.w + 3) & ~3, 0x00020000);
+    }
+    const int c = (int)cg0.x, o = (int)cg0.y;
+    const uint32_t smask = cg0.z;
+    const uint32_t sel[4] = {cg1.x, cg1.y, cg1.z, cg1.w}, coef[4] = {cg2.x, cg2.y, cg2.z, cg2.w};
+    // every source row the lane needs, loaded before any is used; a row shared
+    // with the previous output row is not loaded again (at the 1.2 factor 2 of
+    // 3 output rows reuse one)
+    u32x3 d0[kResizeK], d1[kResizeK];
+    int s1p = -1;
+#pragma unroll
+    for (int j = 0; j < kResizeK; ++j) {
+        const int s0 = (int)(rw[j].x & 0xFFFFu), s1 = (int)(rw[j].x >> 16);
+        if (s0 != s1p) d0[j] = __builtin_amdgcn_raw_buffer_load_b96(src, mul24u(s0, spitch) + c, 0, 0);
+        d1[j] = __builtin_amdgcn_raw_buffer_load_b96(src, mul24u(s1, spitch) + c, 0, 0);
+        s1p = s1;
+    }
+    const __amdgpu_buffer_rsrc_t dst = wave_rsrc(fb.pyr + (int64_t)b * p.pyr_bytes + g.pyr_off);
+    auto hrow = [&](u32x3 d, uint32_t h[4]) {
+        const uint32_t w0 = __builtin_amdgcn_alignbyte(d.y, d.x, o), w1 = __builtin_amdgcn_alignbyte(d.z, d.y, o);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t pr = __builtin_amdgcn_perm(w1, w0, sel[k]);
+            h[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, pr), __builtin_bit_cast(u16x2_t, coef[k]), 0u,
+                                          false);
+        }
+    };
+    uint32_t hp[4] = {0u, 0u, 0u, 0u};
+    int prow = -1;
+#pragma unroll
+    for (int j = 0; j < kResizeK; ++j) {
+        const int y = yb + j;
+        if (y >= g.h) break;
+        const int s0 = (int)(rw[j].x & 0xFFFFu), s1 = (int)(rw[j].x >> 16);
+        const uint32_t bb0 = (rw[j].y & 0xFFFFu) << 12, bb1 = (rw[j].y >> 16) << 12;
+        uint32_t h0[4], h1[4];
+        if (s0 == prow) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) h0[k] = hp[k];
+        } else {
+            hrow(d0[j], h0);
+        }
+        hrow(d1[j], h1);
+        prow = s1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) hp[k] = h1[k];
+        uint32_t packed = 0;
+        if (smask == 0xFu) {
+            packed = resize_vpass_simd(h0, h1, bb0, bb1);
+        } else {
+            const uint32_t b0 = bb0 >> 12, b1 = bb1 >> 12;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t v = (smask >> k & 1u)
+                                       ? ((mul24u(h0[k] >> 4, b0) >> 16) + (mul24u(h1[k] >> 4, b1) >> 16) + 2) >> 2
+                                       : (mul24u(h0[k], b0) + mul24u(h1[k], b1) + (1 << 21)) >> 22;
+                packed |= v << (8 * k);
+            }
+        }
+        __builtin_amdgcn_raw_buffer_store_b32(packed, dst, mul24u(y, g.pitch) + xb, 0, 0);
+    }
+}
+
+#ifndef ORBX_RSD_WPE
+#define ORBX_RSD_WPE 0
+#endif
+__global__ __launch_bounds__(kThreads)
+#if ORBX_RSD_WPE
+__attribute__((amdgpu_waves_per_eu(ORBX_RSD_WPE)))
+#endif
+void k_resize_d(DevPlan p, FrameBufs fb, int l, ResizeWave a, int B) {
+    const int wave = wave_id(), lane = threadIdx.x & 63;
+    const int L = xcd_logical_block(blockIdx.x, gridDim.x);
+    const int t = L * 4 + wave;
+    if (t >= a.ntiles * B) return;
+    const int b = t / a.ntiles;
+    resize_tile_direct(p, fb, l, a, b, t - b * a.ntiles, lane);
 }
 
 // ===========================================================================
@@ -2729,6 +2867,10 @@ hipError_t launch_resize_level(const DevPlan &p, const Plan &hp, const FrameBufs
     if (!hp.rw.empty()) {
         const ResizeWave &a = hp.rw[l];
         const int waves = a.ntiles * B;
+        if (a.direct) {
+            hipLaunchKernelGGL(k_resize_d, dim3((waves + 3) / 4), dim3(kThreads), 0, st, p, fb, l, a, B);
+            return hipGetLastError();
+        }
         // one global round trip for the whole window: NB >= the staging's row passes
         if (a.stage_passes <= 9)
             hipLaunchKernelGGL(k_resize_w<9>, dim3((waves + 3) / 4), dim3(kThreads), 4 * a.win_bytes, st, p, fb, l, a, B);
@@ -3007,6 +3149,11 @@ bool use_pyr_regions(const Plan &hp, int B) { return hp.rgn_n > 0 && (int64_t)B 
 bool plan_resize_waves(Plan &hp) {
     hp.rw.assign(hp.nlevels, ResizeWave{});
     for (int l = 1; l < hp.nlevels; ++l) {
+        bool direct = ORBX_RS_DIRECT && hp.lv[l - 1].w >= 8 && !std::getenv("ORBX_RESIZE_LDS");   // =1: windows in LDS
+        if (l == 1) {
+            hp.rcols.clear();
+            hp.rrows.assign(hp.ytaps.size(), ResizeRow{});
+        }
         const LevelGeom &g = hp.lv[l], &gs = hp.lv[l - 1];
         const ResizeTap *xt = hp.xtaps.data() + g.xtab_off;
         const ResizeTap *yt = hp.ytaps.data() + g.ytab_off;
@@ -3026,6 +3173,7 @@ bool plan_resize_waves(Plan &hp) {
         const int nty = (g.h + TH - 1) / TH;
         a.ntiles = a.ntx * nty;
         int nd_max = 0, nd_win = 0;
+        a.col_off = (int)hp.rcols.size();   // one ResizeCol per 4 columns, x / 4
         for (int tx = 0; tx < a.ntx; ++tx) {
             const int x0 = tx * TW, xl = std::min(x0 + TW, g.w) - 1;
             const int c_lo = std::min(std::max(resize_src_raw(x0, a.sx), 0), gs.w - 1);
@@ -3038,7 +3186,28 @@ bool plan_resize_waves(Plan &hp) {
                 const int s0 = xt[xb].src, s3 = xt[std::min(xb + 3, g.w - 1)].src;
                 if (s3 - s0 + 1 > 7) return false;   // pair bytes within the 8 realigned ones
                 nd_max = std::max(nd_max, ((s0 - (c_lo & ~3)) >> 2) + 3);
+                // k_resize_d: the 8 bytes from cs = min(s0, w_src - 8) hold every
+                // pair byte whose coefficient is not 0 (resize_tile_direct)
+                const int cs = std::min(s0, gs.w - 8);
+                ResizeCol rc{};
+                rc.c = cs & ~3;
+                rc.o = cs & 3;
+                for (int k = 0; k < 4; ++k) {
+                    const ResizeTap &t = xt[std::min(xb + k, g.w - 1)];
+                    const int r = t.src - cs;
+                    if (r < 0 || r > 7 || (r == 7 && t.a1 != 0)) direct = false;
+                    rc.sel[k] = (uint32_t)(r & 7) | 0x0C00u | ((uint32_t)(r < 7 ? r + 1 : 0x0C) << 16) | 0x0C000000u;
+                    rc.coef[k] = (uint32_t)(uint16_t)t.a0 | ((uint32_t)(uint16_t)t.a1 << 16);
+                    rc.smask |= (t.mode & 2) ? 1 << k : 0;
+                }
+                hp.rcols.push_back(rc);
             }
+        }
+        for (int y = 0; y < g.h; ++y) {
+            ResizeRow &rr = hp.rrows[g.ytab_off + y];
+            rr.s01 = (uint32_t)std::min(std::max((int)yt[y].src, 0), gs.h - 1) |
+                     (uint32_t)std::min(std::max((int)yt[y].src + 1, 0), gs.h - 1) << 16;
+            rr.b01 = ((uint32_t)yt[y].a0 & 0xFFFu) | ((uint32_t)yt[y].a1 & 0xFFFu) << 16;
         }
         int nr_max = 0;
         for (int ty = 0; ty < nty; ++ty) {
@@ -3057,6 +3226,7 @@ bool plan_resize_waves(Plan &hp) {
         a.stage_passes = nd_win <= 64 ? (nr_max + 64 / nd_win - 1) / (64 / nd_win) : nr_max;
         a.win_bytes = (nr_max * a.win_stride + 15) & ~15;
         if (4 * a.win_bytes > 64 * 1024) return false;
+        a.direct = direct;
         hp.rw[l] = a;
     }
     return true;

@@ -58,6 +58,21 @@ struct ResizeTap {
     int16_t src, a0, a1, mode;
 };
 
+// k_resize_d's per-level tables (plan_resize_waves).  A column group (4
+// destination columns, one lane): its row loads start at the dword c, the 8
+// bytes it uses at c + o; sel / coef are the v_perm selectors of its 4 pixel
+// pairs within those 8 bytes and their horizontal coefficients (a0 | a1 << 16);
+// bit k of smask = column k is an SSE2 column.  A destination row: its two
+// source rows (clamped) and vertical coefficients, two 16-bit halves each.
+struct ResizeCol {
+    int c, o, smask, pad;
+    uint32_t sel[4], coef[4];
+};
+struct ResizeRow {
+    uint32_t s01;   // s0 | s1 << 16
+    uint32_t b01;   // b0 | b1 << 16
+};
+
 struct LevelGeom {
     int w, h;
     int pitch;            // row pitch of the device images (multiple of 64)
@@ -97,6 +112,8 @@ struct ResizeWave {
     int win_dwords = 0;        // largest window, in staged dwords
     int stage_passes = 0;      // row passes of the window staging (wave_stage_rows)
     int xtab_off = 0, ytab_off = 0;   // the level's tap tables
+    int direct = 0;            // k_resize_d: rows read straight from global memory (no window)
+    int col_off = 0;           // the level's ResizeCol table (k_resize_d; rows: ytab_off)
 };
 
 // A pixel rectangle, inclusive bounds (an int4 on the device).
@@ -120,6 +137,8 @@ struct Plan {
     int max_kps = 0;          // keypoint capacity per frame
     int max_quota = 0;
     std::vector<ResizeWave> rw;   // per level (index 0 unused); empty: k_resize_lds path
+    std::vector<ResizeCol> rcols;   // k_resize_d tables (rw[l].col_off; rows at lv[l].ytab_off)
+    std::vector<ResizeRow> rrows;
     // Region pyramid (k_pyramid_rgn, small batches): per region 2 x kMaxLevels
     // rectangles, [l] = the level-l pixels it computes (level 0: reads),
     // [kMaxLevels + l] = the ones it owns and writes.  rgn_n = 0: not used.

@@ -271,6 +271,8 @@ int upload_plan(orbx_extractor *ex) {
     const size_t b_cells = sizeof(Cell) * p.cells.size();
     const size_t b_xt = sizeof(ResizeTap) * p.xtaps.size();
     const size_t b_yt = sizeof(ResizeTap) * p.ytaps.size();
+    const size_t b_rc = sizeof(ResizeCol) * p.rcols.size();
+    const size_t b_rr = sizeof(ResizeRow) * p.rrows.size();
     const size_t b_tiles = sizeof(int4) * tiles.size();
     // level of every output slot (the last level whose range starts at or before it)
     std::vector<uint32_t> slot_level((size_t)std::max(p.out_cap, 0) + 4, 0);
@@ -283,13 +285,15 @@ int upload_plan(orbx_extractor *ex) {
     const size_t b_sl = sizeof(uint32_t) * slot_level.size();
     const size_t b_rgn = sizeof(RgnRect) * p.rgn.size();
     auto al = [](size_t v) { return (v + 255) & ~size_t(255); };
-    const size_t total = al(b_lv) + al(b_cells) + al(b_xt) + al(b_yt) + al(b_tiles) + al(b_sl) + al(b_rgn) + 256;
+    const size_t total = al(b_lv) + al(b_cells) + al(b_xt) + al(b_yt) + al(b_rc) + al(b_rr) + al(b_tiles) + al(b_sl) + al(b_rgn) + 256;
     std::vector<uint8_t> host(total, 0);
     size_t o = 0;
     const size_t o_lv = o; std::memcpy(&host[o], p.lv.data(), b_lv); o += al(b_lv);
     const size_t o_cells = o; if (b_cells) std::memcpy(&host[o], p.cells.data(), b_cells); o += al(b_cells);
     const size_t o_xt = o; if (b_xt) std::memcpy(&host[o], p.xtaps.data(), b_xt); o += al(b_xt);
     const size_t o_yt = o; if (b_yt) std::memcpy(&host[o], p.ytaps.data(), b_yt); o += al(b_yt);
+    const size_t o_rc = o; if (b_rc) std::memcpy(&host[o], p.rcols.data(), b_rc); o += al(b_rc);
+    const size_t o_rr = o; if (b_rr) std::memcpy(&host[o], p.rrows.data(), b_rr); o += al(b_rr);
     const size_t o_tiles = o; if (b_tiles) std::memcpy(&host[o], tiles.data(), b_tiles); o += al(b_tiles);
     const size_t o_sl = o; std::memcpy(&host[o], slot_level.data(), b_sl); o += al(b_sl);
     const size_t o_rgn = o; if (b_rgn) std::memcpy(&host[o], p.rgn.data(), b_rgn); o += al(b_rgn);
@@ -300,6 +304,8 @@ int upload_plan(orbx_extractor *ex) {
     d.cells = reinterpret_cast<const Cell *>(ex->d_tables + o_cells);
     d.xtaps = reinterpret_cast<const ResizeTap *>(ex->d_tables + o_xt);
     d.ytaps = reinterpret_cast<const ResizeTap *>(ex->d_tables + o_yt);
+    d.rcols = reinterpret_cast<const ResizeCol *>(ex->d_tables + o_rc);
+    d.rrows = reinterpret_cast<const ResizeRow *>(ex->d_tables + o_rr);
     d.blur_tiles = reinterpret_cast<const int4 *>(ex->d_tables + o_tiles);
     d.slot_level = reinterpret_cast<const uint32_t *>(ex->d_tables + o_sl);
     d.pyr_rgn = reinterpret_cast<const int4 *>(ex->d_tables + o_rgn);

@@ -77,13 +77,16 @@ PYRAMID_CASES = [
 
 
 @pytest.mark.parametrize("w,h,scale,nlev,seed", PYRAMID_CASES)
-@pytest.mark.parametrize("path", ["regions", "waves", "blocks"])
+@pytest.mark.parametrize("path", ["regions", "waves", "waves_lds", "blocks"])
 def test_pyramid_sizes_and_scales(w, h, scale, nlev, seed, path, oracle_mod, monkeypatch):
     """cv::resize chain vs the oracle: the one-launch region pyramid
-    (k_pyramid_rgn, small batches), per-level wave tiles (k_resize_w) and the
-    block kernel (k_resize)."""
+    (k_pyramid_rgn, small batches), per-level wave tiles reading rows straight
+    from global memory (k_resize_d) or from an LDS window (k_resize_w), and
+    the block kernel (k_resize)."""
     if path != "regions":
         monkeypatch.setenv("ORBX_PYR_RGN", "0")
+    if path == "waves_lds":
+        monkeypatch.setenv("ORBX_RESIZE_LDS", "1")
     if path == "blocks":
         monkeypatch.setenv("ORBX_RESIZE_BLOCKS", "1")
     img = synth.frame(w, h, seed)
