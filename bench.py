@@ -799,7 +799,7 @@ class StubExtractor:
 
 
 def run_config(torch, dist, rank, world, dev, w, h, nfeatures, streams, steps, warmup, profile, mode="mono",
-               stub=None, split=2, pipeline=0, kframes=1):
+               stub=None, split=2, pipeline=0, kframes=1, overlap=None):
     """Times `steps` front-end steps of this rank's `streams` (global stream
     ids: mono / RGB-D frames or stereo pairs, one per stream per step); returns
     (max-over-ranks seconds, stage ms, kps, sanity, frames per launch, extractor).
@@ -821,6 +821,12 @@ def run_config(torch, dist, rank, world, dev, w, h, nfeatures, streams, steps, w
         ex.split(split)
     if pipeline and stub is None and "ORBX_PIPELINE" not in os.environ:
         ex.pipeline(1)   # level pipeline: on where it measured faster
+    if overlap is None:
+        overlap = MONO_OVERLAP
+    if overlap and mode == "mono" and stub is None and "ORBX_OVERLAP_MATCH" not in os.environ:
+        # each step's matcher beside the next step's extraction (orbx_extractor_overlap_match;
+        # the timed region ends with a device-wide synchronisation, which covers it)
+        ex.overlap_match(1)
     host, depth = _resident_frames(mode, w, h, streams)
     if kframes > 1:
         # launch u holds times u K .. u K + K - 1 (mod the resident frames) of
@@ -1032,6 +1038,10 @@ EXTRA_SPLIT = {"fhd_1920x1080": 1, "hd_1280x720": 1, "rgbd_fhd_1920x1080": 1, "s
 # stereo on / off 37.2-37.3 / 37.9-38.0 k, so off there too (profiles/r04_ab_pipeline.txt)
 EXTRA_PIPE = {}
 HEADLINE_PIPE = 1
+# Matcher overlap of the mono steps (orbx_extractor_overlap_match): each step's
+# SearchForInitialization on an internal stream beside the next step's resize /
+# FAST / quadtree (profiles/r05_ab_overlap_match.txt)
+MONO_OVERLAP = 0
 # Batch split of the VGA headline: with the quadtree's child counts aggregated
 # (0.61 -> 0.38 ms) there is less latency-bound work to hide behind the other
 # half, and one launch per stage measured faster on one box over two rounds

@@ -149,6 +149,18 @@ int orbx_extractor_split(orbx_extractor *ex, int parts);
  * stages only with the pipeline off. */
 int orbx_extractor_pipeline(orbx_extractor *ex, int on);
 
+/* Matcher overlap (default off): orbx_mono_step_device's SearchForInitialization
+ * runs on an internal stream that the launch stream does not wait for, so it
+ * overlaps the next step's resize / FAST / quadtree; the next extraction's
+ * descriptor stage (the only writer of the result slot the matcher reads)
+ * waits for it.  The step's matches are complete when the device is idle or a
+ * download call (orbx_mono_matches_download) returns, not when the launch
+ * stream is; the extraction results are complete with the launch stream as
+ * before.  Outputs are identical either way.  No reference counterpart (a
+ * scheduling option of the batched step, like the split and the pipeline).
+ * on: 1 / 0 sets, -1 queries; returns the current setting. */
+int orbx_extractor_overlap_match(orbx_extractor *ex, int on);
+
 /* Per-stage device time of the last batch (HIP events on the launch stream),
  * in ms, when profiling is enabled: resize, blur, fast, quadtree, describe,
  * match.  Returns the number of stages written. */

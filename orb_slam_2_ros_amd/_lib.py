@@ -102,6 +102,7 @@ _SIGNATURES = {
     "orbx_mono_matches_download": (I32, [P, I32, P, I32, P, P]),
     "orbx_extractor_split": (I32, [P, I32]),
     "orbx_extractor_pipeline": (I32, [P, I32]),
+    "orbx_extractor_overlap_match": (I32, [P, I32]),
     "orbx_extractor_set_profiling": (I32, [P, I32]),
     "orbx_extractor_stage_times": (I32, [P, P, I32]),
     "orbx_extractor_debug_fetch": (I32, [P, I32, I32, I32, P, I64]),

@@ -162,6 +162,17 @@ struct orbx_extractor {
     int stagger = 0;
     hipEvent_t stag_ev = nullptr;
 
+    // Matcher overlap (orbx_extractor_overlap_match, default off): a mono
+    // step's SearchForInitialization runs on match_stream, which the launch
+    // stream does not wait for, so it overlaps the next step's resize / FAST /
+    // quadtree.  The next extraction's k_describe launches (the only writers of
+    // a result slot, which the matcher reads) wait for match_ev (match_gate);
+    // res_ev is recorded after the matcher, so downloads wait for it.
+    int overlap_match = 0;
+    hipStream_t match_stream = nullptr;
+    hipEvent_t ext_ev = nullptr, match_ev = nullptr;
+    bool match_gate = false;
+
     // Stage profiling: a ring of event sets, one set per step, folded into
     // per-stage sums lazily so the timed loop never waits on the host.
     static constexpr int kRing = 64;
@@ -188,6 +199,9 @@ struct orbx_extractor {
             if (ps) (void)hipStreamDestroy(ps);
         if (fork_ev) (void)hipEventDestroy(fork_ev);
         if (stag_ev) (void)hipEventDestroy(stag_ev);
+        if (match_stream) (void)hipStreamDestroy(match_stream);
+        if (ext_ev) (void)hipEventDestroy(ext_ev);
+        if (match_ev) (void)hipEventDestroy(match_ev);
         for (auto &e : done_ev)
             if (e) (void)hipEventDestroy(e);
         for (auto &set : ev)
@@ -202,6 +216,8 @@ struct orbx_extractor {
     }
 
     void release() {
+        if (match_gate && match_ev) (void)hipEventSynchronize(match_ev);   // (the matcher reads the slots freed below)
+        match_gate = false;
         if (host_graph) (void)hipGraphExecDestroy(host_graph);
         host_graph = nullptr;
         host_result_valid = false;   // the result slots are freed: h_out no longer mirrors slot 0
@@ -540,6 +556,12 @@ int join_parts(orbx_extractor *ex, hipStream_t st, const Parts &P) {
     return ORBX_OK;
 }
 
+// Before a k_describe launch on `st` (it writes the result slot): wait for a
+// matcher still reading that slot on match_stream (orbx_extractor_overlap_match).
+bool gate_describe(orbx_extractor *ex, hipStream_t st) {
+    return !ex->match_gate || hipStreamWaitEvent(st, ex->match_ev, 0) == hipSuccess;
+}
+
 void fold(orbx_extractor *ex, int set) {
     if (!ex->pending[set]) return;
     (void)hipEventSynchronize(ex->ev[set][kNumStages]);
@@ -608,14 +630,14 @@ int run_extract_pipe(orbx_extractor *ex, const FrameBufs &fb, int nb, hipStream_
         launch_quadtree_level(dp, fb, nb, ps.s[1], 0, 1) != hipSuccess)
         return ORBX_EIO;
     if (hipEventRecord(ps.level0, ps.s[1]) != hipSuccess) return ORBX_EIO;
-    if (launch_describe_level(dp, hp, fb, nb, ps.s[1], 0, 1) != hipSuccess) return ORBX_EIO;
+    if (!gate_describe(ex, ps.s[1]) || launch_describe_level(dp, hp, fb, nb, ps.s[1], 0, 1) != hipSuccess) return ORBX_EIO;
     if (n > 1) {
         if (launch_resize(dp, hp, fb, nb, ps.s[0]) != hipSuccess ||
             launch_fast_level(dp, hp, fb, nb, ps.s[0], 1, n) != hipSuccess ||
             launch_quadtree_level(dp, fb, nb, ps.s[0], 1, n) != hipSuccess)
             return ORBX_EIO;
         if (hipStreamWaitEvent(ps.s[0], ps.level0, 0) != hipSuccess) return ORBX_EIO;
-        if (launch_describe_level(dp, hp, fb, nb, ps.s[0], 1, n) != hipSuccess) return ORBX_EIO;
+        if (!gate_describe(ex, ps.s[0]) || launch_describe_level(dp, hp, fb, nb, ps.s[0], 1, n) != hipSuccess) return ORBX_EIO;
     }
     for (int i = 0; i < 2; ++i)
         if (hipEventRecord(ps.done[i], ps.s[i]) != hipSuccess || hipStreamWaitEvent(st, ps.done[i], 0) != hipSuccess)
@@ -650,7 +672,7 @@ int run_extract(orbx_extractor *ex, int si, const uint8_t *d_images, int64_t str
             case 0: return launch_resize(ex->dp, ex->plan, pf[k], P.nb[k], P.s[k]) == hipSuccess;
             case 1: return launch_fast(ex->dp, ex->plan, pf[k], P.nb[k], P.s[k]) == hipSuccess;
             case 2: return launch_quadtree(ex->dp, pf[k], P.nb[k], P.s[k]) == hipSuccess;
-            default: return launch_describe(ex->dp, pf[k], P.nb[k], P.s[k]) == hipSuccess;
+            default: return gate_describe(ex, P.s[k]) && launch_describe(ex->dp, pf[k], P.nb[k], P.s[k]) == hipSuccess;
         }
     };
     if (P.n == 2 && ex->stagger > 0 &&
@@ -678,7 +700,7 @@ int run_extract(orbx_extractor *ex, int si, const uint8_t *d_images, int64_t str
         if (launch_quadtree(ex->dp, pf[k], P.nb[k], P.s[k]) != hipSuccess) return ORBX_EIO;
     mark(ex, 4, m);
     for (int k = 0; k < P.n; ++k)
-        if (launch_describe(ex->dp, pf[k], P.nb[k], P.s[k]) != hipSuccess) return ORBX_EIO;
+        if (!gate_describe(ex, P.s[k]) || launch_describe(ex->dp, pf[k], P.nb[k], P.s[k]) != hipSuccess) return ORBX_EIO;
     mark(ex, 5, m);
     for (int i = 0; i < kStageMatch; ++i)
         if (i != kStageBlur) mark_valid(ex, i);
@@ -843,6 +865,7 @@ orbx_extractor *orbx_extractor_create(int device, int nfeatures, float scaleFact
     if (hipStreamCreateWithFlags(&ex->stream, hipStreamNonBlocking) != hipSuccess) { delete ex; return nullptr; }
     if (const char *sp = std::getenv("ORBX_SPLIT")) ex->split = std::max(1, std::min(std::atoi(sp), orbx_extractor::kMaxParts));
     if (const char *pp = std::getenv("ORBX_PIPELINE")) ex->pipeline = std::atoi(pp) != 0;
+    if (const char *om = std::getenv("ORBX_OVERLAP_MATCH")) ex->overlap_match = std::atoi(om) != 0;
     if (const char *sg = std::getenv("ORBX_STAGGER")) ex->stagger = std::max(0, std::min(std::atoi(sg), 3));
     // geometry tables for the getters are size independent; plan a nominal size
     ex->plan = make_plan(640, 480, nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST);
@@ -1109,7 +1132,7 @@ int orbx_extract(orbx_extractor *ex, const uint8_t *image, int width, int height
         volatile uint32_t *flag = reinterpret_cast<volatile uint32_t *>(ex->h_out) + kOutFlag;
         *flag = 0;
         std::atomic_thread_fence(std::memory_order_seq_cst);
-        if (hipGraphLaunch(ex->host_graph, ex->stream) != hipSuccess) return ORBX_EIO;
+        if (!gate_describe(ex, ex->stream) || hipGraphLaunch(ex->host_graph, ex->stream) != hipSuccess) return ORBX_EIO;
         // poll the pack kernel's flag; the stream's state ends the wait on an error
         for (uint32_t i = 1; !*flag; ++i) {
             if ((i & 255) == 0 && hipStreamQuery(ex->stream) != hipErrorNotReady) break;
@@ -1315,10 +1338,34 @@ int orbx_mono_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t f
     mb.check_ori = check_ori;
     mb.reset_prev = 1;
     mb.clocks = nullptr;
+    if (ex->overlap_match && !ex->profiling) {
+        // the matcher for the whole batch on match_stream, after the extraction
+        if ((rc = join_parts(ex, st, P))) return rc;
+        if (!ex->match_stream) {
+            if (fork_stream(&ex->match_stream) != hipSuccess ||
+                hipEventCreateWithFlags(&ex->ext_ev, hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&ex->match_ev, hipEventDisableTiming) != hipSuccess)
+                return ORBX_EIO;
+        }
+        if (hipEventRecord(ex->ext_ev, st) != hipSuccess || hipStreamWaitEvent(ex->match_stream, ex->ext_ev, 0) != hipSuccess)
+            return ORBX_EIO;
+        if (launch_match(mb, batch, ex->plan.max_kps, ex->plan.max_kps, ex->l0cap, ex->l0cap, ex->match_stream) != hipSuccess ||
+            hipEventRecord(ex->match_ev, ex->match_stream) != hipSuccess)
+            return ORBX_EIO;
+        ex->match_gate = true;
+        note_results(ex, ex->match_stream);
+        ex->match_batch = batch;
+        return ORBX_OK;
+    }
     static const bool dbg_clocks = std::getenv("ORBX_MATCH_CLOCKS") != nullptr;
     long long *dclk = nullptr;
     if (dbg_clocks && hipMalloc(reinterpret_cast<void **>(&dclk), 8 * sizeof(long long)) == hipSuccess)
         mb.clocks = dclk;
+    if (ex->match_gate) {   // (overlap just turned off: the last overlapped matcher writes the same state)
+        for (int k = 0; k < P.n; ++k)
+            if (hipStreamWaitEvent(P.s[k], ex->match_ev, 0) != hipSuccess) return ORBX_EIO;
+        ex->match_gate = false;
+    }
     for (int k = 0; k < P.n; ++k) {
         MatchBufs pm = offset_pairs(mb, P.b0[k]);
         if (k > 0) pm.clocks = nullptr;
@@ -1358,6 +1405,12 @@ int orbx_mono_matches_download(orbx_extractor *ex, int frame, int32_t *matches12
     if (cnt > cap) return ORBX_ERANGE;
     if (cnt > 0 && matches12) copy(matches12, ex->d_m12 + (size_t)frame * ex->plan.max_kps, sizeof(int32_t) * cnt);
     return copy.wait() ? ORBX_OK : ORBX_EIO;
+}
+
+int orbx_extractor_overlap_match(orbx_extractor *ex, int on) {
+    if (!ex || on < -1 || on > 1) return ORBX_EINVAL;
+    if (on >= 0) ex->overlap_match = on != 0;
+    return ex->overlap_match;
 }
 
 int orbx_extractor_pipeline(orbx_extractor *ex, int on) {

@@ -204,6 +204,11 @@ class ORBextractor:
         """Level-pipelined extraction on internal streams (1 on, 0 off, -1 query)."""
         return check(self._lib.orbx_extractor_pipeline(self._h, int(on)), "pipeline")
 
+    def overlap_match(self, on: int = -1) -> int:
+        """Mono-step matcher on an internal stream, overlapping the next step's
+        extraction (1 on, 0 off, -1 query; include/orbx.h)."""
+        return check(self._lib.orbx_extractor_overlap_match(self._h, int(on)), "overlap_match")
+
     def set_profiling(self, on: bool) -> None:
         check(self._lib.orbx_extractor_set_profiling(self._h, int(on)), "set_profiling")
 

@@ -82,6 +82,40 @@ def test_mono_bench_config_b3072(oracle_mod):
     ex.close()
 
 
+def test_mono_overlap_match_steps(oracle_mod):
+    """Matcher overlap (orbx_extractor_overlap_match): four mono steps issued
+    back to back, each step's matcher on the internal stream beside the next
+    step's extraction (whose descriptor stage waits for it); the last step's
+    matches and keypoints equal the oracle's on sampled streams, and the same
+    extractor without the overlap gives the same matches for every stream."""
+    import torch
+    w, h, B = 640, 480, 3072
+    host, _, fr, _ = _frames(torch, "mono", w, h, list(range(B)))
+    res = []
+    for ovl in (1, 0):
+        ex = ORBextractor(1000, 1.2, 8, 20, 7)
+        ex.reserve(w, h, B)
+        ex.split(bench.HEADLINE_SPLIT)
+        ex.pipeline(bench.HEADLINE_PIPE)
+        assert ex.overlap_match(ovl) == ovl and ex.overlap_match() == ovl
+        for t in range(4):
+            ex.mono_step_device(fr[t].data_ptr(), w * h, w, B, 100, 0.9, True)
+        torch.cuda.synchronize()
+        res.append(([ex.mono_matches_download(b) for b in range(B)], [ex.batch_download(b) for b in _samples(B)]))
+        ex.close()
+    (m_ovl, o_ovl), (m_ref, o_ref) = res
+    for b in range(B):
+        assert m_ovl[b][1] == m_ref[b][1] and np.array_equal(m_ovl[b][0], m_ref[b][0]), f"stream {b}"
+    for j, b in enumerate(_samples(B)):
+        k1, d1 = oracle_mod.extract(host[2, b])
+        k2, d2 = oracle_mod.extract(host[3, b])
+        assert _kp_equal(o_ovl[j][0], k2) and np.array_equal(o_ovl[j][1], d2), f"stream {b} extract"
+        prev = np.ascontiguousarray(np.stack([k1["x"], k1["y"]], 1).astype(np.float32))
+        nm, m12, _ = oracle_mod.search_for_initialization(k1, d1, k2, d2, w, h, prev, 100, 0.9, True)
+        assert m_ovl[b][1] == nm and np.array_equal(m_ovl[b][0], m12), f"stream {b} matches"
+        assert nm > 0
+
+
 MONO_EXTRAS = [(w, h, nf, B) for key, mode, w, h, nf, B, _ in bench.EXTRAS if mode == "mono"]
 
 
