@@ -60,6 +60,7 @@ def test_mono_bench_config_b3072(oracle_mod):
     ex.reserve(w, h, B)
     ex.split(bench.HEADLINE_SPLIT)
     ex.pipeline(bench.HEADLINE_PIPE)   # (as bench.py times it)
+    ex.overlap_match(bench.MONO_OVERLAP)
     assert ex.split() == bench.HEADLINE_SPLIT
     for t in range(2):
         ex.mono_step_device(fr[t].data_ptr(), w * h, w, B, 100, 0.9, True)
@@ -132,6 +133,7 @@ def test_mono_extra_bench_configs(w, h, nf, B, oracle_mod):
     ex.reserve(w, h, B)
     ex.split(bench.EXTRA_SPLIT.get(key, 2))   # (as bench.py times it)
     ex.pipeline(bench.EXTRA_PIPE.get(key, 0))
+    ex.overlap_match(bench.MONO_OVERLAP)
     for t in range(2):
         ex.mono_step_device(fr[t].data_ptr(), w * h, w, B, 100, 0.9, True)
     torch.cuda.synchronize()
