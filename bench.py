@@ -1036,7 +1036,10 @@ EXTRA_SPLIT = {"fhd_1920x1080": 1, "hd_1280x720": 1, "rgbd_fhd_1920x1080": 1, "s
 # off elsewhere: FHD 53.1 / 57.4 k, HD 116.0 / 123.9 k, FHD RGB-D 54.2 / 58.3 k,
 # EuRoC 98.5 / 108.2 k, KITTI 62.0 / 67.3 k.  Round 4, after the level-major quadtree grid: FHD
 # stereo on / off 37.2-37.3 / 37.9-38.0 k, so off there too (profiles/r04_ab_pipeline.txt)
-EXTRA_PIPE = {}
+# Round 5, after the LDS-free resize (k_resize_d), on / off on one box: FHD mono 89.5-90.8 / 88.2-88.5 k,
+# HD 184.0 / 180.5-180.6 k, FHD stereo 45.6-45.7 / 44.0-44.1 k, FHD RGB-D 90.8-90.9 / 89.0-89.3 k; EuRoC
+# 148.0 / 161.0-162.3 k and KITTI 87.8-88.2 / 95.2-95.3 k stay off (profiles/r05_ab_pipeline_extras.txt)
+EXTRA_PIPE = {"fhd_1920x1080": 1, "hd_1280x720": 1, "stereo_fhd_1920x1080": 1, "rgbd_fhd_1920x1080": 1}
 HEADLINE_PIPE = 1
 # Matcher overlap of the mono steps (orbx_extractor_overlap_match): each step's
 # SearchForInitialization on an internal stream beside the next step's resize /

@@ -157,8 +157,8 @@ def test_mono_extra_bench_configs(w, h, nf, B, oracle_mod):
 STEREO_CONFIGS = [   # bench.py EXTRAS: (w, h, nfeatures, pairs, split, level pipeline as bench.py runs it)
     (752, 480, 1200, 256, 2, 0),
     (1241, 376, 2000, 144, 2, 0),
-    (1920, 1080, 1000, 192, 1, 0),
-    (752, 480, 1200, 32, 2, 1),   # (the level pipeline on a stereo step)
+    (1920, 1080, 1000, 192, 1, 1),
+    (752, 480, 1200, 32, 2, 1),   # (the level pipeline on a small split stereo step)
 ]
 
 
@@ -206,6 +206,7 @@ def test_rgbd_fhd_bench_configs(B, oracle_mod):
     ex = ORBextractor(1000, 1.2, 8, 20, 7)
     ex.reserve(w, h, B)
     ex.split(bench.EXTRA_SPLIT.get("rgbd_fhd_1920x1080", 2) if B == 192 else 2)   # (as bench.py times it)
+    ex.pipeline(bench.EXTRA_PIPE.get("rgbd_fhd_1920x1080", 0) if B == 192 else 0)
     ex.rgbd_step_device(fr[2].data_ptr(), w * h, w, B, dm.data_ptr(), 4 * w * h, 4 * w, BF)
     torch.cuda.synchronize()
     for b in [0, 1, B // 2 - 1, B // 2, B - 1]:
