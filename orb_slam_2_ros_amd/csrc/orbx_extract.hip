@@ -58,7 +58,6 @@ constexpr bool pattern_in_fp8_range() {
 }
 static_assert(pattern_in_fp8_range(), "the fp8 pattern table holds integers up to 15 exactly");
 static_assert(fp8_e4m3_int(1) == 0x38 && fp8_e4m3_int(13) == 0x55 && fp8_e4m3_int(-3) == 0xC4, "e4m3fn, bias 7");
-__constant__ __attribute__((aligned(16))) PatternQ c_pattern_q = PatternQ();
 
 // c_disc_mask[ri][g]: byte k kept iff column 4g - 16 + k lies in row ri - 15
 // of the orientation disc (kUmax, orbx_plan.h).
@@ -107,7 +106,6 @@ struct MomTables {
             }
     }
 };
-__constant__ __attribute__((aligned(16))) MomTables c_mom = MomTables();
 
 // Phase profiling (diagnostic build only, -DORBX_PHASE_PROF: tools/phase_prof.py):
 // each wave adds the s_memtime cycles of its phases to g_phase[kernel][phase]
@@ -2474,7 +2472,15 @@ struct RowTaps {
         }
     }
 };
-__constant__ RowTaps c_row_taps = RowTaps();
+// k_describe's three per-lane tables in one constant block: one buffer
+// resource (one s_getpc / add / addc) serves every table load at immediate offsets
+struct DescTables {
+    MomTables mom;   // 3072 B
+    PatternQ pat;    // 1024 B
+    RowTaps taps;    // 512 B
+};
+static_assert(offsetof(DescTables, pat) == 3072 && offsetof(DescTables, taps) == 4096, "immediate offsets below");
+__constant__ __attribute__((aligned(16))) DescTables c_desc = DescTables();
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 #ifndef ORBX_DESC_NOTAB
@@ -2531,10 +2537,11 @@ __global__ __launch_bounds__(kThreads, ORBX_DESC_WAVES) void k_describe(DevPlan 
     const bool in_range = slot < p.out_cap && bx * 4 + wave < ns;
     // level of this slot (plan table) and the selected key: scalar loads
     const int l = in_range ? (int)p.slot_level[slot] : 0;
-    const uint32_t key = in_range ? __builtin_amdgcn_readfirstlane(fb.sel[(int64_t)b * p.out_cap + slot]) : 0u;
+    // (32-bit index: the plan bounds max_batch * out_cap below 2^31, orbx_runtime.hip)
+    const uint32_t key = in_range ? __builtin_amdgcn_readfirstlane(fb.sel[(uint32_t)(b * p.out_cap + slot)]) : 0u;
     // the frame's level counts: lane q < nlevels holds count q; the slot's
     // output offset is the prefix below its level (16-lane DPP scan)
-    const int32_t *lc = fb.level_count + (int64_t)b * kMaxLevels;
+    const int32_t *lc = fb.level_count + (uint32_t)(b * kMaxLevels);
     const int lq = lane & (kMaxLevels - 1);
     const int lcv = lc[lq];   // (every lane: a frame holds kMaxLevels counts)
     // the tables after the level counts: the scan below waits for the
@@ -2543,21 +2550,20 @@ __global__ __launch_bounds__(kThreads, ORBX_DESC_WAVES) void k_describe(DevPlan 
     // x0 y0 x1 y1 in word g), fetched first so the load overlaps the staging;
     // one buffer resource over each table, the loads at immediate offsets (the
     // compiler otherwise rebuilds a symbol's address, s_getpc + add + addc, per load)
-    const __amdgpu_buffer_rsrc_t pat_rsrc = wave_rsrc(&c_pattern_q);
-    const long row_taps = (long)c_row_taps.t[lane];
+    const __amdgpu_buffer_rsrc_t tab_rsrc = wave_rsrc(&c_desc);
+    const long row_taps = __builtin_bit_cast(long, __builtin_amdgcn_raw_buffer_load_b64(tab_rsrc, 8 * lane, 4096, 0));
     const uint4 patq = ORBX_DESC_NOTAB ? make_uint4(0x38u * lane, 0x40u, 0x48u, 0xC4u)
-                                       : __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(pat_rsrc, 16 * lane, 0, 0));
+                                       : __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(tab_rsrc, 16 * lane, 3072, 0));
     // the moment products' operand tables (the same for every keypoint: the
     // patch is staged with the keypoint at a fixed column), ahead of the
     // key's chain of scalar loads and the staging, whose latency they hide under
     typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
     u64x2 mom[3];
     {
-        const __amdgpu_buffer_rsrc_t mom_rsrc = wave_rsrc(&c_mom);
 #pragma unroll
         for (int t = 0; t < 3; ++t)
             mom[t] = ORBX_DESC_NOTAB ? u64x2{0x00FFFF00FF00FFFFull * (uint64_t)(lane + t), 0x0102030405060708ull + t}
-                                     : __builtin_bit_cast(u64x2, __builtin_amdgcn_raw_buffer_load_b128(mom_rsrc, 16 * lane + 1024 * t, 0, 0));
+                                     : __builtin_bit_cast(u64x2, __builtin_amdgcn_raw_buffer_load_b128(tab_rsrc, 16 * lane + 1024 * t, 0, 0));
     }
     const int cq = lane < p.nlevels ? max(lcv, 0) : 0;
     static_assert(kMaxLevels == 16, "one DPP row");
@@ -2590,8 +2596,9 @@ __global__ __launch_bounds__(kThreads, ORBX_DESC_WAVES) void k_describe(DevPlan 
     int spitch;
     const uint8_t *img = level_ptr(p, fb, l, b, spitch);
     const int px0 = x - kDescR, py0 = y - kDescR;
-    const bool inside = px0 >= kDescCol0 && py0 >= 0 && x + kDescR < g.w && y + kDescR < g.h &&
-                        px0 - kDescCol0 + kDescPS <= spitch;
+    // (every term >= 0 <=> their OR is: one scalar compare instead of five compare / select / and)
+    const bool inside = ((px0 - kDescCol0) | py0 | (g.w - 1 - kDescR - x) | (g.h - 1 - kDescR - y) |
+                         (spitch - (px0 - kDescCol0 + kDescPS))) >= 0;
     if (inside) {
         if constexpr (ORBX_DESC_STAGE) stage_desc_patch(lbase, img, spitch, py0, px0, lane);
         else wave_stage_rows<(kDescP + 4) / 5, true, true, kDescCol0>(lbase, kDescPS, img, spitch, py0, px0, kDescP, kDescP, lane);   // 5 rows a pass
@@ -2630,7 +2637,7 @@ __global__ __launch_bounds__(kThreads, ORBX_DESC_WAVES) void k_describe(DevPlan 
             for (int ct = 0; ct < 3; ++ct)
                 px[rt][ct] = *reinterpret_cast<const uint64_t *>(bsrc + 16 * rt * kDescPS + 16 * ct);
         // moments: A = the disc's pixels of the window tiles (rows 16 rt..,
-        // columns 8..39), B = c_mom.b; D[i][15] = sum of u I over row i,
+        // columns 8..39), B = c_desc.mom's b; D[i][15] = sum of u I over row i,
         // D[i][12 + rt] = sum of I over row 16 rt + i, summed over the three
         // products (lane l: D[4 (l >> 4) + ii][l & 15])
         {

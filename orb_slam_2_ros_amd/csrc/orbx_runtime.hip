@@ -394,6 +394,7 @@ int reserve(orbx_extractor *ex, int w, int h, int max_batch) {
     if (rc) return rc;
     const Plan &p = ex->plan;
     const size_t B = (size_t)max_batch;
+    if (B * (size_t)std::max(p.out_cap, 1) >= (size_t(1) << 31)) return ORBX_EINVAL;   // (k_describe's 32-bit slot index)
     bool ok = true;
     ok &= dalloc(&ex->d_pyr, B * p.pyr_bytes) == hipSuccess;
     ok &= dalloc(&ex->d_blur, B * p.blur_bytes) == hipSuccess;
