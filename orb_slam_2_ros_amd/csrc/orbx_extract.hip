@@ -3174,6 +3174,10 @@ bool plan_resize_waves(Plan &hp) {
             const int cols = 4 << sh, n = (g.w + cols - 1) / cols;
             if (best < 0 || n * cols < best) { best = n * cols; a.twg_shift = sh; }
         }
+        if (const char *e = std::getenv("ORBX_RS_TWG")) {   // (A/B probe: one column-group width for every level)
+            const int t = std::atoi(e);
+            if (t == 16 || t == 32 || t == 64) a.twg_shift = t == 16 ? 4 : t == 32 ? 5 : 6;
+        }
         a.twg = 1 << a.twg_shift;
         const int TW = 4 * a.twg, TH = (64 >> a.twg_shift) * kResizeK;
         a.ntx = (g.w + TW - 1) / TW;
