@@ -63,6 +63,10 @@ def algorithmic_bytes(sizes, nkp: float, stage: str) -> float:
         return nkp * 60
     if stage == "match":       # both frames' descriptors + keypoints read, matches written
         return nkp * (2 * 32 + 2 * 28 + 4)
+    if stage == "stereo":      # per pair: both images' keypoints + descriptors read, uR / depth / SAD written
+        return nkp * (2 * 60 + 12)
+    if stage == "rgbd":        # per frame: keypoints read, one depth sample each, uR / depth written
+        return nkp * (28 + 4 + 8)
     if stage == "quadtree":    # candidates in, selection out (counted in the kernel)
         return 0.0
     if stage == "frame":       # SURVEY.md §8(d) compulsory figure
@@ -71,16 +75,20 @@ def algorithmic_bytes(sizes, nkp: float, stage: str) -> float:
 
 
 TRAFFIC_FILE = ROOT / "profiles" / "traffic_vga.json"
+# per-workload PMC summaries (tools/profile.sh + tools/prof_summary.py --json) for the extras' rooflines
+TRAFFIC_FILES = {"fhd_1920x1080": ROOT / "profiles" / "traffic_fhd.json",
+                 "stereo_fhd_1920x1080": ROOT / "profiles" / "traffic_fhd_stereo.json"}
 STAGE_KERNEL = {"resize": "k_resize", "fast": "k_fast", "quadtree": "k_quadtree", "describe": "k_describe",
                 "match": "k_search_init"}
 
 
-def measured_traffic(stage: str, frames_per_launch: float):
+def measured_traffic(stage: str, frames_per_launch: float, path=None):
     """HBM bytes per launch of the stage's kernel from the committed rocprofv3
     PMC passes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, MI355X_MICROARCH.md),
     scaled from the profiled dispatch's frame count; (None, None) if absent."""
+    path = path or TRAFFIC_FILE
     try:
-        prof = json.loads(TRAFFIC_FILE.read_text())
+        prof = json.loads(path.read_text())
         name = STAGE_KERNEL[stage]
         # template instantiations are listed as k_name<args>; the whole-batch
         # launch is the <false> one
@@ -88,7 +96,7 @@ def measured_traffic(stage: str, frames_per_launch: float):
         keys.sort(key=lambda k: "<false" not in k)
         k = prof["kernels"][keys[0]]
         per_frame = k["hbm_bytes_per_dispatch"] / prof["frames_per_dispatch"]
-        return round(per_frame * frames_per_launch), str(TRAFFIC_FILE.relative_to(ROOT))
+        return round(per_frame * frames_per_launch), str(path.relative_to(ROOT))
     except (OSError, KeyError, ValueError, ZeroDivisionError, IndexError):
         return None, None
 
@@ -106,12 +114,13 @@ VALU_HALF_RATE_GINST = 592.9
 VALU_PEAK_SOURCE = "profiles/r02_valu_rate_clock.txt, profiles/r02_valu_ops.txt"
 
 
-def measured_valu(stage: str, frames_per_launch: float):
+def measured_valu(stage: str, frames_per_launch: float, path=None):
     """VALU wave-instructions per launch of the stage's kernel (SQ_INSTS_VALU
     from the committed PMC pass, scaled from the profiled dispatch's frame
     count); None if absent."""
+    path = path or TRAFFIC_FILE
     try:
-        prof = json.loads(TRAFFIC_FILE.read_text())
+        prof = json.loads(path.read_text())
         name = STAGE_KERNEL[stage]
         keys = [k for k in prof["kernels"] if k == name or k.startswith(name + "<") or k.startswith(name + "_w<")]
         keys.sort(key=lambda k: "<false" not in k)
@@ -119,6 +128,79 @@ def measured_valu(stage: str, frames_per_launch: float):
         return round(k["valu_insts_per_dispatch"] / prof["frames_per_dispatch"] * frames_per_launch)
     except (OSError, KeyError, ValueError, ZeroDivisionError, IndexError):
         return None
+
+
+STAGE_NAMES = ["resize", "blur", "fast", "quadtree", "describe", "match"]
+
+
+def roofline_block(sizes, nkp, stages, frames_per_launch, units_per_s_gpu, mode="mono", traffic_path=None):
+    """The `roofline` object for one workload: the dominant HBM-streaming
+    kernel (by time among the stages that move a tenth or more of the frame's
+    compulsory bytes) with its algorithmic bytes per launch
+    over its measured launch time (stage times: HIP events on the launch
+    stream, a separate unsplit, unpipelined pass, one whole-batch launch per
+    stage), its PMC traffic and VALU issue rate from the workload's committed
+    profile, the time-dominant stage beside it, and the whole unit's
+    compulsory bytes at the measured throughput (`pipeline_frac`).
+    frames_per_launch counts images (2 per stereo pair); units_per_s_gpu is
+    the workload's own unit (frames or stereo pairs) per second per GPU.
+    Returns (roofline, stage_ms)."""
+    if not stages:
+        return None, None
+    stage_ms = dict(zip(STAGE_NAMES, [round(s, 4) for s in stages]))
+    if mode == "stereo":
+        stage_ms["stereo"] = stage_ms.pop("match")
+    elif mode == "rgbd":
+        stage_ms["rgbd"] = stage_ms.pop("match")
+    fb = algorithmic_bytes(sizes, nkp, "frame")
+    # (per launch: frames for the extraction stages, pairs / frames for the last)
+    per_launch = {n: frames_per_launch / 2 if n == "stereo" else frames_per_launch for n in stage_ms}
+    cand = {n: t for n, t in stage_ms.items()
+            if t and t > 0 and algorithmic_bytes(sizes, nkp, n) >= 0.1 * fb}
+    if not cand:
+        return None, stage_ms
+    dom = max(cand, key=cand.get)
+    bytes_launch = algorithmic_bytes(sizes, nkp, dom) * per_launch[dom]
+    achieved = bytes_launch / (cand[dom] * 1e-3) / 1e9
+    traffic, tsrc = measured_traffic(dom, per_launch[dom], traffic_path)
+    roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+            "traffic_source": tsrc, "bytes_per_launch": bytes_launch, "frames_per_launch": frames_per_launch,
+            "launch_ms": cand[dom]}
+    valu = measured_valu(dom, per_launch[dom], traffic_path)
+    if valu:
+        # the same kernel against the VALU issue rate (its actual bound)
+        ach = valu / (cand[dom] * 1e-3) / 1e9
+        roof["issue"] = {"bound": "valu", "achieved": round(ach, 1), "peak": VALU_PEAK_GINST,
+                         "unit": "G wave-instr/s", "frac": round(ach / VALU_PEAK_GINST, 4),
+                         "half_rate_peak": VALU_HALF_RATE_GINST,
+                         "frac_of_half_rate": round(ach / VALU_HALF_RATE_GINST, 4),
+                         "insts_per_launch": valu, "source": tsrc, "peak_source": VALU_PEAK_SOURCE}
+    tdom = max((n for n, t in stage_ms.items() if t and t > 0), key=lambda n: stage_ms[n])
+    if tdom != dom:
+        tb = algorithmic_bytes(sizes, nkp, tdom) * per_launch[tdom]
+        tach = tb / (stage_ms[tdom] * 1e-3) / 1e9
+        tv = measured_valu(tdom, per_launch[tdom], traffic_path)
+        roof["dominant_by_time"] = {
+            "kernel": tdom, "ms": stage_ms[tdom], "bytes_per_launch": tb, "achieved": round(tach, 2),
+            "frac": round(tach / HBM_PEAK_GBS, 5),
+            "traffic": measured_traffic(tdom, per_launch[tdom], traffic_path)[0],
+            "issue_frac_of_half_rate": round(tv / (stage_ms[tdom] * 1e-3) / 1e9 / VALU_HALF_RATE_GINST, 4)
+            if tv else None}
+    # the unit's compulsory bytes (SURVEY.md §8(d)): a frame, or a stereo pair =
+    # two frames' extraction + the pair's stereo search
+    if mode == "stereo":
+        unit_bytes = 2 * algorithmic_bytes(sizes, nkp, "frame") - 2 * nkp * (2 * 32 + 4) \
+            + algorithmic_bytes(sizes, nkp, "stereo")
+    elif mode == "rgbd":
+        unit_bytes = fb - nkp * (2 * 32 + 4) + algorithmic_bytes(sizes, nkp, "rgbd")
+    else:
+        unit_bytes = fb
+    roof["unit_bytes"] = round(unit_bytes)
+    roof["pipeline_GBs"] = round(unit_bytes * units_per_s_gpu / 1e9, 2)
+    roof["pipeline_frac"] = round(unit_bytes * units_per_s_gpu / 1e9 / HBM_PEAK_GBS, 5)
+    return roof, stage_ms
+
 
 
 def cpu_model() -> str:
@@ -1228,6 +1310,10 @@ def main() -> int:
                 ex2.close()
                 res = {"value": round(world * eb * args.steps / el2, 2), "unit": unit, "stage_ms": st2,
                        "kps_last_frame": nk2}
+                if rank == 0 and st2 and not args.stub:
+                    res["roofline"], _ = roofline_block(
+                        level_geometry(ew, eh, enf), nk2, st2, (2 if mode == "stereo" else 1) * eb,
+                        eb * args.steps / el2, mode, TRAFFIC_FILES.get(key))
         if rank == 0:
             print(json.dumps({"extra": args.extra, **(res or {"error": "unknown extra"})}), flush=True)
         if world > 1:
@@ -1267,6 +1353,10 @@ def main() -> int:
             extras[key] = {"value": round(world * eb * es / el2, 2), "unit": unit, "mode": mode,
                            "streams_per_gpu": eb, "nfeatures": enf, "stage_ms": st2,
                            "kps_last_frame": nk2, ("matches" if mode == "mono" else "depths") + "_last_frame": sane2}
+            if rank == 0 and st2:
+                extras[key]["roofline"], _ = roofline_block(
+                    level_geometry(ew, eh, enf), nk2, st2, (2 if mode == "stereo" else 1) * eb, eb * es / el2, mode,
+                    TRAFFIC_FILES.get(key))
         c5 = c5_config(torch, dist, rank, world, dev, max(5, args.steps // 4), 2, profile, *c5_args)
         extras["c5_rgbd_fhd_64_streams"] = c5
         if world > 1 and not args.stub:
@@ -1274,52 +1364,7 @@ def main() -> int:
 
     if rank == 0:
         sizes = level_geometry(w, h, nf) if not args.stub else [(w, h)]
-        names = ["resize", "blur", "fast", "quadtree", "describe", "match"]
-        roof = None
-        stage_ms = None
-        if stages:
-            stage_ms = dict(zip(names, [round(s, 4) for s in stages]))
-            # the dominant HBM-streaming kernel: by time among the stages that move a
-            # tenth or more of the frame's compulsory bytes; k_fast
-            # (reads the pyramid) and k_describe (60 B per keypoint out, its patches
-            # re-read from L2) take about equal time, and the time-dominant one of all
-            # stages is reported beside it under "dominant_by_time"
-            fb = algorithmic_bytes(sizes, nkp_last, "frame")
-            cand = {n: s for n, s in stage_ms.items()
-                    if s and s > 0 and algorithmic_bytes(sizes, nkp_last, n) >= 0.1 * fb}
-            dom = max(cand, key=cand.get)
-            # stage times come from the profiling pass: one whole-batch launch per
-            # stage, unsplit and unpipelined, overlapping nothing
-            bytes_launch = algorithmic_bytes(sizes, nkp_last, dom) * frames_per_launch
-            achieved = bytes_launch / (cand[dom] * 1e-3) / 1e9
-            traffic, tsrc = measured_traffic(dom, frames_per_launch)
-            roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                    "traffic_source": tsrc, "bytes_per_launch": bytes_launch,
-                    "frames_per_launch": frames_per_launch}
-            valu = measured_valu(dom, frames_per_launch)
-            if valu:
-                # the same kernel against the VALU issue rate (its actual bound)
-                ach = valu / (cand[dom] * 1e-3) / 1e9
-                roof["issue"] = {"bound": "valu", "achieved": round(ach, 1), "peak": VALU_PEAK_GINST,
-                                 "unit": "G wave-instr/s", "frac": round(ach / VALU_PEAK_GINST, 4),
-                                 "half_rate_peak": VALU_HALF_RATE_GINST,
-                                 "frac_of_half_rate": round(ach / VALU_HALF_RATE_GINST, 4),
-                                 "insts_per_launch": valu, "source": tsrc, "peak_source": VALU_PEAK_SOURCE}
-            tdom = max((n for n, t in stage_ms.items() if t and t > 0), key=lambda n: stage_ms[n])
-            if tdom != dom:
-                tb = algorithmic_bytes(sizes, nkp_last, tdom) * frames_per_launch
-                tach = tb / (stage_ms[tdom] * 1e-3) / 1e9
-                tv = measured_valu(tdom, frames_per_launch)
-                roof["dominant_by_time"] = {
-                    "kernel": tdom, "ms": stage_ms[tdom], "bytes_per_launch": tb, "achieved": round(tach, 2),
-                    "frac": round(tach / HBM_PEAK_GBS, 5),
-                    "traffic": measured_traffic(tdom, frames_per_launch)[0],
-                    "issue_frac_of_half_rate": round(tv / (stage_ms[tdom] * 1e-3) / 1e9 / VALU_HALF_RATE_GINST, 4)
-                    if tv else None}
-            frame_bytes = algorithmic_bytes(sizes, nkp_last, "frame")
-            roof["pipeline_GBs"] = round(frame_bytes * value / world / 1e9, 2)
-            roof["pipeline_frac"] = round(frame_bytes * value / world / 1e9 / HBM_PEAK_GBS, 5)
+        roof, stage_ms = roofline_block(sizes, nkp_last, stages, frames_per_launch, value / world, "mono")
         run_cpu = world == 1 and args.cpu_seconds > 0 and not args.stub
         cpu = cpu_baseline(w, h, nf, args.cpu_seconds) if run_cpu else None
         if cpu is not None:

@@ -29,11 +29,14 @@ KeyFrameDatabase::KeyFrameDatabase(const ORBVocabulary &voc) : mpVoc(&voc) {
     orbx_detail::check(orbx_kfdb_create(orbx_detail::device_index(), &mDb), "KeyFrameDatabase");
 }
 
+// (KeyFrameDatabase.h:75, the archive's constructor)
+KeyFrameDatabase::KeyFrameDatabase() {
+    orbx_detail::check(orbx_kfdb_create(orbx_detail::device_index(), &mDb), "KeyFrameDatabase");
+}
+
 KeyFrameDatabase::~KeyFrameDatabase() { orbx_kfdb_destroy(mDb); }
 
-// :37-44
-void KeyFrameDatabase::add(KeyFrame *pKF) {
-    std::unique_lock<std::mutex> lock(mMutex);
+void KeyFrameDatabase::AddLocked(KeyFrame *pKF) {
     std::vector<uint32_t> w;
     std::vector<double> v;
     bow_arrays(pKF->mBowVec, w, v);
@@ -41,11 +44,19 @@ void KeyFrameDatabase::add(KeyFrame *pKF) {
     mKFs[pKF->mnId] = pKF;
 }
 
+// :37-44
+void KeyFrameDatabase::add(KeyFrame *pKF) {
+    std::unique_lock<std::mutex> lock(mMutex);
+    AddLocked(pKF);
+    mvpKFs.push_back(pKF);
+}
+
 // :46-67
 void KeyFrameDatabase::erase(KeyFrame *pKF) {
     std::unique_lock<std::mutex> lock(mMutex);
     if (!mKFs.erase(pKF->mnId)) return;   // not in the database: nothing to remove, as the reference
     orbx_detail::check(orbx_kfdb_erase(mDb, pKF->mnId), "KeyFrameDatabase::erase");
+    mvpKFs.erase(std::find(mvpKFs.begin(), mvpKFs.end(), pKF));
 }
 
 // :69-73
@@ -53,6 +64,34 @@ void KeyFrameDatabase::clear() {
     std::unique_lock<std::mutex> lock(mMutex);
     orbx_detail::check(orbx_kfdb_clear(mDb), "KeyFrameDatabase::clear");
     mKFs.clear();
+    mvpKFs.clear();
+}
+
+// Map serialisation (KeyFrameDatabase.cc:371-384).  The reference archives its
+// inverted file, mvInvertedFile's KeyFrame* lists, each in insertion order.
+// Here the archived state is the database's keyframes in insertion order; each
+// keyframe archives its own mBowVec (KeyFrame.cc:858), so the inverted file is
+// determined by them: adding them again in that order gives every word's
+// posting list the same keyframes in the same order.  The vocabulary is not
+// archived, as in the reference.
+template <class Archive>
+void KeyFrameDatabase::serialize(Archive &ar, const unsigned int) {
+    std::unique_lock<std::mutex> lock(mMutex);
+    ar & mvpKFs;
+}
+template void KeyFrameDatabase::serialize(boost::archive::binary_iarchive &, const unsigned int);
+template void KeyFrameDatabase::serialize(boost::archive::binary_oarchive &, const unsigned int);
+
+// (KeyFrameDatabase.h:76) System::LoadMap calls this once the map and the
+// database are loaded (System.cc:666-667): every archived keyframe is then
+// complete, and the device database is rebuilt from them.  On a live database
+// it rebuilds the same state.
+void KeyFrameDatabase::SetORBvocabulary(ORBVocabulary *porbv) {
+    std::unique_lock<std::mutex> lock(mMutex);
+    mpVoc = porbv;
+    orbx_detail::check(orbx_kfdb_clear(mDb), "KeyFrameDatabase::SetORBvocabulary");
+    mKFs.clear();
+    for (KeyFrame *pKF : mvpKFs) AddLocked(pKF);
 }
 
 // GetBestCovisibilityKeyFrames(10) of a candidate, by id (:129, :279)

@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 from pathlib import Path
 
 import numpy as np
@@ -176,14 +177,20 @@ def load(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     except ImportError:
         pass
     lib = ctypes.CDLL(str(p))
-    alt = path is None and "ORBX_LIB" in os.environ
+    # ORBX_LIB_ALLOW_MISSING=1 (A/B timing of an older build that predates an
+    # entry point): skip the missing symbols, listed on stderr.  Otherwise a
+    # stale or mismatched library fails here, with the ABI names it lacks.
+    allow = os.environ.get("ORBX_LIB_ALLOW_MISSING") == "1"
+    missing = [name for name in _SIGNATURES if not hasattr(lib, name)]
+    if missing and not allow:
+        raise OSError(f"{p}: missing entry points {missing} (stale or mismatched build; "
+                      "ORBX_LIB_ALLOW_MISSING=1 skips them for A/B timing)")
+    if missing:
+        print(f"orbx: {p} lacks {missing}; skipped (ORBX_LIB_ALLOW_MISSING=1)", file=sys.stderr)
     for name, (res, args) in _SIGNATURES.items():
-        try:
-            fn = getattr(lib, name)
-        except AttributeError:
-            if alt:   # an older build under A/B timing may predate an entry point
-                continue
-            raise
+        if name in missing:
+            continue
+        fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
     if path is None:

@@ -1404,7 +1404,7 @@ int BA::alloc() {
         h_ok = carve<int>(h, 1); h_rho0 = carve<double>(h, ne); h_x = carve<double>(h, m);
         h_bp = carve<double>(h, 6 * nf); h_bl = carve<double>(h, 3 * np);
         h_hpp = carve<double>(h, 36 * nf); h_hll = carve<double>(h, 9 * np);
-        h_fsum = carve<double>(h, 4);
+        h_fsum = carve<double>(h, 8);   // [0, 4): errors / trial sums, [4, 8): read_diag's
         h_stage = carve<uint8_t>(h, 2 * ne); h_coffs_ = carve<int32_t>(h, nf + 1 + ne);
         if ((size_t)(h - hbuf_) > hb) return ORBX_ENOMEM;
     }
@@ -1655,11 +1655,11 @@ int BA::read_errors() {
 }
 
 int BA::read_diag() {
-    if (fast_) {   // (after read_errors: the chi sum is kept)
+    if (fast_) {   // (into slots of its own: read_errors' chi sum in h_fsum[0] stays whatever the order)
         hipLaunchKernelGGL(k_ba_fast_sums, dim3(kFastSumBlocks), dim3(kFastSumThreads), 0, st_, d_rho0, d_active, g_.ne,
                            nullptr, nullptr, nullptr, 0, 0, 0.0, nullptr, d_Hpp, g_.nf, d_Hll, g_.npt, d_fpart, d_fcount,
                            d_fsum);
-        return hipMemcpyAsync(h_fsum, d_fsum, 32, hipMemcpyDeviceToHost, st_) == hipSuccess ? ORBX_OK : ORBX_EIO;
+        return hipMemcpyAsync(h_fsum + 4, d_fsum, 32, hipMemcpyDeviceToHost, st_) == hipSuccess ? ORBX_OK : ORBX_EIO;
     }
     if ((g_.nf && hipMemcpyAsync(h_hpp, d_Hpp, 8 * 36 * (size_t)g_.nf, hipMemcpyDeviceToHost, st_) != hipSuccess) ||
         (g_.npt && hipMemcpyAsync(h_hll, d_Hll, 8 * 9 * (size_t)g_.npt, hipMemcpyDeviceToHost, st_) != hipSuccess))
@@ -1688,7 +1688,7 @@ double BA::chi_sum_host() const {   // activeRobustChi2: active edges in order
 }
 
 double BA::max_diag_host() const {   // computeLambdaInit: max |diagonal| over the free vertices
-    if (fast_) return h_fsum[3];
+    if (fast_) return h_fsum[4 + 3];
     double mx = 0.;
     for (int f = 0; f < g_.nf; ++f)
         for (int j = 0; j < 6; ++j) mx = std::max(std::fabs(h_hpp[36 * (size_t)f + 7 * j]), mx);

@@ -1150,8 +1150,11 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
             int ncorner = npend;
             for (int i0 = 0; i0 < nsurv; i0 += 64) {
                 // every lane scores (no exec region): a lane past the survivors
-                // reads a stale entry, or LDS past the list, and is masked after
-                const int e = list[npend + i0 + lane];
+                // reads a stale entry, or LDS past the list, clamped to entry 0
+                // (pixel (0, 0)) so that its circle reads stay inside the patch;
+                // it is masked after
+                const bool live = i0 + lane < nsurv;
+                const int e = live ? (int)list[npend + i0 + lane] : 0;
                 const uint8_t *q = pc + e;
                 const int v = q[0];
                 const uint32_t pr[16] = {q[3 * PS],  q[3 * PS + 1],  q[2 * PS + 2],  q[PS + 3],
@@ -1159,7 +1162,7 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
                                          q[-3 * PS], q[-3 * PS - 1], q[-2 * PS - 2], q[-PS - 3],
                                          q[-3],      q[PS - 3],      q[2 * PS - 2],  q[3 * PS - 1]};
                 const int S = arc_score_bytes(reinterpret_cast<const int *>(pr), v);
-                const bool corner = (i0 + lane < nsurv) & (S > th);
+                const bool corner = live & (S > th);
                 if (corner) scm[e + PS + 1] = (uint8_t)(S - 1);
                 const uint64_t m = __ballot(corner);
                 wave_lds_fence();   // all survivor reads of this chunk precede the in-place writes
@@ -1177,9 +1180,11 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
             const int ylast = final ? INT_MAX : (ydone - 1) * PS;
             int nfin = 0;
             for (int i0 = 0; i0 < ncorner; i0 += 64) {
-                // every lane reads (as in B), lanes past the corners masked after
-                const int e = list[i0 + lane];
-                const bool fin = (i0 + lane < ncorner) & (e < ylast);
+                // every lane reads (as in B: a lane past the corners clamped to
+                // entry 0, inside the score map), masked after
+                const bool live = i0 + lane < ncorner;
+                const int e = live ? (int)list[i0 + lane] : 0;
+                const bool fin = live & (e < ylast);
                 const int si = e + PS + 1;
                 // the centre and its 8 neighbours read together, compared
                 // with their maximum (no short-circuit chain of dependent reads)

@@ -1046,6 +1046,15 @@ int build_host_graph(orbx_extractor *ex, int width, int height) {
         ex->h_out_bytes = out_bytes;
     }
     hipStream_t st = ex->stream;
+    // An overlapped matcher (orbx_extractor_overlap_match) may still read the
+    // result slots on match_stream; gate_describe would then wait on match_ev
+    // inside the capture, an event recorded outside it (a cross-capture wait
+    // invalidates the capture).  Drain it here: the capture then has no gate,
+    // and the graph's launch site gates later overlapped steps itself.
+    if (ex->match_gate) {
+        if (hipEventSynchronize(ex->match_ev) != hipSuccess) return ORBX_EIO;
+        ex->match_gate = false;
+    }
     const int pipe = ex->pipeline;
     hipEvent_t *ev = ex->cur_ev;
     bool *valid = ex->cur_valid;

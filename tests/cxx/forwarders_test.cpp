@@ -21,6 +21,7 @@
 #include <list>
 #include <memory>
 #include <set>
+#include <sstream>
 #include <string>
 #include <vector>
 
@@ -1223,6 +1224,85 @@ int main() {
             return r;
         };
         check_case(name("KeyFrameDatabase"), mk, [&](World &w) { return kfdb(w, true); }, [&](World &w) { return kfdb(w, false); });
+
+        // KeyFrameDatabase map save / load (KeyFrameDatabase.h:72-81): the
+        // database with one keyframe erased is archived with the map as
+        // System::SaveMap does (System.cc:629: the map, then the database;
+        // each keyframe archives mpKeyFrameDB, KeyFrame.cc:877), loaded into
+        // new objects as LoadMap does (System.cc:665-667, SetORBvocabulary
+        // after the load), and queried through the loaded keyframes; the
+        // reference side queries the database that was saved
+        auto kfdb_io = [](World &w, bool gpu) {
+            std::vector<int64_t> r;
+            for (auto &kf : w.kfs) kf->mvpOrderedConnectedKeyFrames.resize(std::min<size_t>(2, kf->mvpOrderedConnectedKeyFrames.size()));
+            auto push = [&r](const std::vector<uint64_t> &v) { r.push_back((int64_t)v.size()); for (auto x : v) r.push_back((int64_t)x); };
+            if (gpu) {
+                ORBVocabulary voc;
+                std::stringstream ss;
+                {
+                    KeyFrameDatabase db(voc);
+                    for (auto &kf : w.kfs) { db.add(kf.get()); kf->mpKeyFrameDB = &db; }
+                    db.erase(w.kfs[1].get());
+                    Map *mpMap = &w.map;
+                    KeyFrameDatabase *mpKeyFrameDatabase = &db;
+                    boost::archive::binary_oarchive oa(ss, boost::archive::no_header);
+                    oa << mpMap;
+                    oa << mpKeyFrameDatabase;
+                }   // (the saved database is gone before the load)
+                Map *mpMap = nullptr;
+                KeyFrameDatabase *mpKeyFrameDatabase = nullptr;
+                boost::archive::binary_iarchive ia(ss, boost::archive::no_header);
+                ia >> mpMap;
+                ia >> mpKeyFrameDatabase;
+                mpKeyFrameDatabase->SetORBvocabulary(&voc);
+                auto as_ids = [](const std::vector<KeyFrame *> &v) { std::vector<uint64_t> o; for (auto *k : v) o.push_back(k->mnId); return o; };
+                bool same_db = true;
+                for (KeyFrame *k : mpMap->keyframes) same_db = same_db && k->mpKeyFrameDB == mpKeyFrameDatabase;
+                r.push_back(same_db && mpMap->keyframes.size() == w.kfs.size());
+                for (int q : {0, 5, 3}) push(as_ids(mpKeyFrameDatabase->DetectLoopCandidates(mpMap->KeyFrameById(w.kfs[q]->mnId), 0.001f)));
+                push(as_ids(mpKeyFrameDatabase->DetectRelocalizationCandidates(w.cur.get())));
+                push(as_ids(mpKeyFrameDatabase->DetectRelocalizationCandidates(w.last.get())));
+                // the loaded database stays live: erase, add back, query
+                mpKeyFrameDatabase->erase(mpMap->KeyFrameById(w.kfs[2]->mnId));
+                mpKeyFrameDatabase->add(mpMap->KeyFrameById(w.kfs[2]->mnId));
+                push(as_ids(mpKeyFrameDatabase->DetectLoopCandidates(mpMap->KeyFrameById(w.kfs[5]->mnId), 0.001f)));
+                for (KeyFrame *k : mpMap->keyframes) delete k;
+                delete mpKeyFrameDatabase;
+                delete mpMap;
+                for (auto &kf : w.kfs) kf->mpKeyFrameDB = nullptr;
+            } else {
+                auto bowv = [](const DBoW2::BowVector &b, std::vector<uint32_t> &wd, std::vector<double> &vl) {
+                    for (auto &kv : b) { wd.push_back(kv.first); vl.push_back(kv.second); }
+                };
+                void *db = orbo_kfdb_create(409);
+                auto add = [&](KeyFrame *kf) {
+                    std::vector<uint32_t> wd; std::vector<double> vl; bowv(kf->mBowVec, wd, vl);
+                    orbo_kfdb_add(db, kf->mnId, wd.data(), vl.data(), (int)wd.size());
+                };
+                for (auto &kf : w.kfs) add(kf.get());
+                orbo_kfdb_erase(db, w.kfs[1]->mnId);
+                auto det = [&](int reloc, uint64_t qid, const DBoW2::BowVector &b, const std::set<KeyFrame *> &conn, float ms) {
+                    std::vector<uint32_t> wd; std::vector<double> vl; bowv(b, wd, vl);
+                    std::vector<uint64_t> c;
+                    for (auto *k : conn) c.push_back(k->mnId);
+                    std::vector<uint64_t> out(64);
+                    const int n = orbo_kfdb_detect(db, reloc, qid, wd.data(), vl.data(), (int)wd.size(), c.data(), (int)c.size(), ms,
+                                                   covis_cb, &w, out.data(), (int)out.size());
+                    out.resize(n);
+                    return out;
+                };
+                r.push_back(1);
+                for (int q : {0, 5, 3}) push(det(0, w.kfs[q]->mnId, w.kfs[q]->mBowVec, w.kfs[q]->GetConnectedKeyFrames(), 0.001f));
+                push(det(1, w.cur->mnId, w.cur->mBowVec, {}, 0.f));
+                push(det(1, w.last->mnId, w.last->mBowVec, {}, 0.f));
+                orbo_kfdb_erase(db, w.kfs[2]->mnId);
+                add(w.kfs[2].get());
+                push(det(0, w.kfs[5]->mnId, w.kfs[5]->mBowVec, w.kfs[5]->GetConnectedKeyFrames(), 0.001f));
+                orbo_kfdb_destroy(db);
+            }
+            return r;
+        };
+        check_case(name("KeyFrameDatabase(save/load)"), mk, [&](World &w) { return kfdb_io(w, true); }, [&](World &w) { return kfdb_io(w, false); });
     }
     std::printf("%s: %d mismatching case(s)\n", failures ? "FAIL" : "PASS", failures);
     return failures ? 1 : 0;

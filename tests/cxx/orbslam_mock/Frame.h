@@ -12,6 +12,7 @@
 
 #include <opencv2/core/core.hpp>
 
+#include "BoostArchiver.h"
 #include "MapPoint.h"
 #include "orbx_orbslam2.hpp"
 #include "Thirdparty/DBoW2/DBoW2/BowVector.h"
@@ -21,6 +22,8 @@
 #define FRAME_GRID_COLS 64
 
 namespace ORB_SLAM2 {
+
+class KeyFrameDatabase;
 
 // The members Frame and KeyFrame share (calibration, features, scale tables, grid).
 struct FeatureSet {
@@ -100,12 +103,19 @@ public:
     std::set<KeyFrame *> GetConnectedKeyFrames() const {
         return std::set<KeyFrame *>(mvpOrderedConnectedKeyFrames.begin(), mvpOrderedConnectedKeyFrames.end());
     }
+
+    // map serialisation (KeyFrame.cc:823-893): the members the keyframe
+    // database's queries read, and the database pointer as the fork archives
+    // it (`ar & mpKeyFrameDB`, KeyFrame.cc:877, after mBowVec)
+    KeyFrameDatabase *mpKeyFrameDB = nullptr;
+    template <class Archive> void serialize(Archive &ar, const unsigned int version);
 };
 
 class Map {
 public:
     std::vector<KeyFrame *> keyframes;
     std::mutex mMutexMapUpdate;
+    template <class Archive> void serialize(Archive &ar, const unsigned int version);   // (Map.cc: the keyframes)
     KeyFrame *KeyFrameById(unsigned long id) const {
         for (KeyFrame *k : keyframes)
             if (k->mnId == id) return k;

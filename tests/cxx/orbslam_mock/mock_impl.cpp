@@ -5,6 +5,7 @@
 #include <climits>
 
 #include "Frame.h"
+#include "KeyFrameDatabase.h"
 #include "MapPoint.h"
 #include "orbx.h"
 
@@ -171,5 +172,25 @@ void MapPoint::ComputeDistinctiveDescriptors() {
     mDescriptor = cv::Mat(1, 32, CV_8U);
     std::memcpy(mDescriptor.data, d[bi], 32);
 }
+
+// KeyFrame.cc:823-893 (the fields the database queries read, in the fork's
+// order: mnId, mBowVec, then mpKeyFrameDB at :877) and Map.cc's keyframe set
+template <class Archive>
+void KeyFrame::serialize(Archive &ar, const unsigned int) {
+    ar & mnId;
+    ar & mbBad;
+    ar & mBowVec;
+    ar & mvpOrderedConnectedKeyFrames;
+    ar & mpKeyFrameDB;
+}
+template void KeyFrame::serialize(boost::archive::binary_iarchive &, const unsigned int);
+template void KeyFrame::serialize(boost::archive::binary_oarchive &, const unsigned int);
+
+template <class Archive>
+void Map::serialize(Archive &ar, const unsigned int) {
+    ar & keyframes;
+}
+template void Map::serialize(boost::archive::binary_iarchive &, const unsigned int);
+template void Map::serialize(boost::archive::binary_oarchive &, const unsigned int);
 
 }  // namespace ORB_SLAM2

@@ -14,7 +14,7 @@ import pytest
 from cxx_build import build_forwarders_test
 
 ROOT = Path(__file__).resolve().parents[1]
-N_CASES = 60   # 30 per seed, two seeds
+N_CASES = 62   # 31 per seed, two seeds
 
 
 def _run(exe):

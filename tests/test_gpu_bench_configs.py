@@ -117,6 +117,67 @@ def test_mono_overlap_match_steps(oracle_mod):
         assert nm > 0
 
 
+def test_mono_overlap_transitions(oracle_mod):
+    """The matcher overlap's state changes on one extractor, each phase checked
+    against the oracle: overlapped steps, then overlap off (the matcher waits on
+    the last overlapped one), profiling on mid-sequence (falls back to the
+    non-overlapped path), overlap on again, the host-image call on the same
+    handle right after an overlapped step (its graph capture must not wait on
+    the overlapped matcher's event), then a reserve at a new batch size (frees
+    the slots the matcher reads)."""
+    import torch
+    w, h, B = 640, 480, 64
+    # 2 B resident streams (the last phase's batch); the earlier phases use the first B
+    host, _, fr, _ = _frames(torch, "mono", w, h, list(range(2 * B)))
+    ex = ORBextractor(1000, 1.2, 8, 20, 7)
+    ex.reserve(w, h, B)
+    ex.split(2)
+    smp = [0, 31, 32, 63, 64, 127]
+
+    def step_and_check(t, nb=B, tag=""):
+        ex.mono_step_device(fr[t % 4].data_ptr(), w * h, w, nb, 100, 0.9, True)
+        torch.cuda.synchronize()
+        for b in smp:
+            if b >= nb:
+                continue
+            kp, de = ex.batch_download(b)
+            m12, nm = ex.mono_matches_download(b)
+            k1, d1 = oracle_mod.extract(host[(t - 1) % 4, b])
+            k2, d2 = oracle_mod.extract(host[t % 4, b])
+            assert _kp_equal(kp, k2) and np.array_equal(de, d2), f"{tag} step {t} stream {b} extract"
+            prev = np.ascontiguousarray(np.stack([k1["x"], k1["y"]], 1).astype(np.float32))
+            onm, om12, _ = oracle_mod.search_for_initialization(k1, d1, k2, d2, w, h, prev, 100, 0.9, True)
+            assert nm == onm and np.array_equal(m12, om12), f"{tag} step {t} stream {b} matches"
+
+    ex.overlap_match(1)
+    for t in range(3):
+        ex.mono_step_device(fr[t].data_ptr(), w * h, w, B, 100, 0.9, True)
+    step_and_check(3, tag="overlap")
+    ex.overlap_match(0)
+    step_and_check(4, tag="overlap->off")
+    ex.overlap_match(1)
+    ex.mono_step_device(fr[1].data_ptr(), w * h, w, B, 100, 0.9, True)
+    ex.set_profiling(True)
+    step_and_check(6, tag="profiling")
+    assert all(x >= 0 for x in ex.stage_times()[:1])
+    ex.set_profiling(False)
+    step_and_check(7, tag="overlap again")
+    # the host-image call right after an overlapped step (no synchronisation between)
+    ex.mono_step_device(fr[0].data_ptr(), w * h, w, B, 100, 0.9, True)
+    img = np.ascontiguousarray(host[2, 5])
+    kp, de = ex(img)
+    ok, od = oracle_mod.extract(img)
+    assert _kp_equal(kp, ok) and np.array_equal(de, od), "host call after an overlapped step"
+    # and back to the device path, then a reserve at another batch size
+    ex.mono_step_device(fr[0].data_ptr(), w * h, w, B, 100, 0.9, True)
+    step_and_check(1, tag="after host call")
+    ex.mono_step_device(fr[2].data_ptr(), w * h, w, B, 100, 0.9, True)
+    ex.reserve(w, h, 2 * B)
+    ex.mono_step_device(fr[2].data_ptr(), w * h, w, 2 * B, 100, 0.9, True)
+    step_and_check(3, nb=2 * B, tag="reserve")
+    ex.close()
+
+
 MONO_EXTRAS = [(w, h, nf, B) for key, mode, w, h, nf, B, _ in bench.EXTRAS if mode == "mono"]
 
 

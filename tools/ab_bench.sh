@@ -9,7 +9,7 @@ OUT=gpurun_out/ab_$TAG.txt
 : > "$OUT"
 for r in $(seq "$ROUNDS"); do
     for lib in "$@"; do
-        line=$(ORBX_LIB=$PWD/$lib timeout -k 10 150 python bench.py --no-extras --cpu-seconds 0 --steps 40 2>/dev/null | tail -n 1) || exit 1
+        line=$(ORBX_LIB_ALLOW_MISSING=1 ORBX_LIB=$PWD/$lib timeout -k 10 150 python bench.py --no-extras --cpu-seconds 0 --steps 40 2>/dev/null | tail -n 1) || exit 1
         python -c "import json,sys; d=json.loads(sys.argv[2]); print(sys.argv[1], round(d['value']), {k: round(v, 3) for k, v in d['stage_ms_per_step'].items()})" "$lib" "$line" >> "$OUT"
     done
 done
