@@ -1015,6 +1015,9 @@ __device__ inline void stage_fast_patch(uint8_t *dst, int ps, const uint8_t *img
 #ifndef ORBX_FAST_STAGE
 #define ORBX_FAST_STAGE 1   // 0: the generic wave_stage_rows
 #endif
+#ifndef ORBX_FAST_EVEN8
+#define ORBX_FAST_EVEN8 0   // 1: the 8-even-point pre-test before the arc score (A/B, slower)
+#endif
 
 // PIPE: a level's cells in a level-pipelined step (a distinct instantiation so
 // profiles tell per-level launches from whole-batch ones).
@@ -1148,6 +1151,38 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
             npend = __builtin_amdgcn_readfirstlane(npend);
             nsurv = __builtin_amdgcn_readfirstlane(nsurv);
             int ncorner = npend;
+#if ORBX_FAST_EVEN8
+            // (A/B candidate, off) a second pre-test on the 8 even circle points:
+            // any 9-arc holds >= 4 cyclically consecutive even points, all
+            // brighter or all darker; survivors that fail it are dropped before
+            // the 16-point score (compacted in place, as the corners below)
+            {
+                int npass = npend;
+                for (int i0 = 0; i0 < nsurv; i0 += 64) {
+                    const bool live = i0 + lane < nsurv;
+                    const int e = live ? (int)list[npend + i0 + lane] : 0;
+                    const uint8_t *q = pc + e;
+                    const int v = q[0];
+                    const uint32_t pe[8] = {q[3 * PS], q[2 * PS + 2], q[3], q[-2 * PS + 2],
+                                            q[-3 * PS], q[-2 * PS - 2], q[-3], q[2 * PS - 2]};
+                    u16x2 ev[8], m2[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) ev[k] = as_u16x2(pe[k] + ((255u - pe[k]) << 16));
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) m2[k] = __builtin_elementwise_min(ev[k], ev[(k + 1) & 7]);
+                    u16x2 best = __builtin_elementwise_min(m2[0], m2[2]);
+#pragma unroll
+                    for (int k = 1; k < 8; ++k) best = __builtin_elementwise_max(best, __builtin_elementwise_min(m2[k], m2[(k + 2) & 7]));
+                    const bool pass = live & (max((int)best.x - v, v - (255 - (int)best.y)) > th);
+                    const uint64_t m = __ballot(pass);
+                    wave_lds_fence();
+                    if (pass) list[npass + mbcnt64(m)] = (uint16_t)e;
+                    npass += __popcll(m);
+                }
+                nsurv = __builtin_amdgcn_readfirstlane(npass - npend);
+                wave_lds_fence();
+            }
+#endif
             for (int i0 = 0; i0 < nsurv; i0 += 64) {
                 // every lane scores (no exec region): a lane past the survivors
                 // reads a stale entry, or LDS past the list, clamped to entry 0
