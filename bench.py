@@ -335,7 +335,7 @@ def matcher_latencies(reps: int = 20):
     oracle's single-thread time on the same inputs."""
     from oracle import oracle
     from orb_slam_2_ros_amd import ORBmatcher
-    from orb_slam_2_ros_amd.matcher import BOW_VARIANTS
+    from orb_slam_2_ros_amd.matcher import BOW_VARIANTS, PROJ_VARIANTS
     from orb_slam_2_ros_amd.synth_match import (BOW_VARIANT_ARGS, PROJ_VARIANT_ARGS, make_bow_case,
                                                 make_proj_case)
 
@@ -359,6 +359,7 @@ def matcher_latencies(reps: int = 20):
         out[f"SearchByProjection_{variant}" if "fuse" not in variant else "Fuse"] = {
             "keypoints": n, "points": nq,
             "gpu_ms": round(timed(lambda: m.search_by_projection(*args, th), reps), 4),
+            **cxx_proj_latency(PROJ_VARIANTS[variant], c, th, ratio, ori),
             "cpu_ms": round(timed(lambda: oracle.search_by_projection(*args, th, ratio, ori), 5), 4)}
     for variant, na in [("kf_frame", 2000), ("triangulation", 2000)]:
         ratio, ori = BOW_VARIANT_ARGS[variant]
@@ -745,6 +746,49 @@ def cxx_bow_latency(variant: int, A, B, tri, nnratio, check_ori, reps):
         r = subprocess.run([str(_adapter_exe()), "time_bow", str(p), str(reps)], capture_output=True, text=True,
                            timeout=120, check=True)
     return float(r.stdout.split("bow_ms")[1].split()[0])
+
+
+def write_proj_case(d: Path, c):
+    """One SearchByProjection problem as adapter_test proj / time_proj read it
+    (frame.bin, queries.bin in d)."""
+    n, nq = len(c["keys"]), len(c["queries"])
+    with open(d / "f.bin", "wb") as f:
+        f.write(np.int32(n).tobytes()); f.write(np.array(c["bounds"], np.float32).tobytes())
+        f.write(np.ascontiguousarray(c["keys"]).tobytes()); f.write(np.ascontiguousarray(c["desc"]).tobytes())
+        ur = c["uright"] if c["uright"] is not None else np.full(n, -1, np.float32)
+        f.write(np.ascontiguousarray(ur, np.float32).tobytes())
+        ms = c["mp_state"] if c["mp_state"] is not None else np.zeros(n, np.uint8)
+        f.write(np.ascontiguousarray(ms, np.uint8).tobytes())
+        isg = c["inv_sigma2"] if c["inv_sigma2"] is not None else np.zeros(0, np.float32)
+        f.write(np.int32(len(isg)).tobytes()); f.write(np.ascontiguousarray(isg, np.float32).tobytes())
+    with open(d / "q.bin", "wb") as f:
+        f.write(np.int32(nq).tobytes()); f.write(np.ascontiguousarray(c["queries"]).tobytes())
+        f.write(np.ascontiguousarray(c["qdesc"]).tobytes())
+
+
+def cxx_proj_latency(variant: int, c, th, ratio, ori, reps=1000, phase_reps=200):
+    """A SearchByProjection / Fuse call through the C++ forwarder's entry
+    (OrbxMatcher::SearchByProjectionTable, ORBmatcher_orbx.cc), host tables in
+    and out: median and minimum over `reps` calls, then the host call's phases
+    (ORBX_CALL_TIMING: checks, staging, enqueue, wait for the outputs, readback;
+    medians over `phase_reps` calls, in microseconds)."""
+    import subprocess
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        d = Path(td)
+        write_proj_case(d, c)
+        args = [str(_adapter_exe()), "time_proj", str(variant), str(th), repr(float(ratio)), str(int(ori)),
+                str(d / "f.bin"), str(d / "q.bin")]
+        r = subprocess.run(args + [str(reps)], capture_output=True, text=True, timeout=300, check=True)
+        rp = subprocess.run(args + [str(phase_reps)], capture_output=True, text=True, timeout=300, check=True,
+                            env=dict(os.environ, ORBX_CALL_TIMING="1"))
+    val = {k: float(r.stdout.split(k + " ")[1].split()[0]) for k in ("proj_ms", "proj_min_ms")}
+    ph = [[float(x) for x in ln.split(":", 1)[1].split()] for ln in rp.stderr.splitlines()
+          if ln.startswith("orbx proj us:")]
+    ph = [p for p in ph if len(p) == 5][-phase_reps:]
+    med = [round(float(np.median([p[i] for p in ph])), 2) for i in range(5)] if ph else None
+    return {"cxx_ms": val["proj_ms"], "cxx_min_ms": val["proj_min_ms"], "calls": reps,
+            "phases_us": dict(zip(["checks", "staging", "enqueue", "wait", "readback"], med)) if med else None}
 
 
 def cxx_dropin_latency(L, R, bf, mb, reps):

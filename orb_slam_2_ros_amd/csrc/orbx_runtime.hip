@@ -161,6 +161,11 @@ struct orbx_extractor {
     // meet the other part's VALU-bound ones instead of each other.
     int stagger = 0;
     hipEvent_t stag_ev = nullptr;
+    // Serial chunks (ORBX_CHUNKS=c, diagnostic): an unsplit batch runs as c
+    // chunks one after another on the launch stream, each chunk's resize,
+    // FAST, quadtree and describe back to back, so a chunk's pyramid is still
+    // in the 256 MB MALL when its describe re-reads it.
+    int chunks = 1;
 
     // Matcher overlap (orbx_extractor_overlap_match, default off): a mono
     // step's SearchForInitialization runs on match_stream, which the launch
@@ -572,6 +577,8 @@ void fold(orbx_extractor *ex, int set) {
         if (hipEventElapsedTime(&t, ex->ev[set][i], ex->ev[set][i + 1]) == hipSuccess) {
             ex->stage_sum[i] += t;
             ex->stage_cnt[i] += 1;
+        } else {
+            (void)hipGetLastError();   // (not the next launch's error)
         }
     }
     ex->pending[set] = false;
@@ -661,6 +668,21 @@ int run_extract(orbx_extractor *ex, int si, const uint8_t *d_images, int64_t str
     FrameBufs pf[orbx_extractor::kMaxParts];
     for (int k = 0; k < P.n; ++k) pf[k] = offset_frames(ex, fb, P.b0[k]);
     const hipStream_t m = P.s[0];
+    if (ex->chunks > 1 && P.n == 1 && !ex->pipeline) {
+        mark(ex, 0, m);   // (one span for the whole extraction, no per-stage times)
+        const int nc = std::min(ex->chunks, batch);
+        for (int k = 0; k < nc; ++k) {
+            const int c0 = batch * k / nc, cn = batch * (k + 1) / nc - c0;
+            const FrameBufs fc = offset_frames(ex, fb, c0);
+            if (launch_resize(ex->dp, ex->plan, fc, cn, m) != hipSuccess ||
+                launch_fast(ex->dp, ex->plan, fc, cn, m) != hipSuccess ||
+                launch_quadtree(ex->dp, fc, cn, m) != hipSuccess || !gate_describe(ex, m) ||
+                launch_describe(ex->dp, fc, cn, m) != hipSuccess)
+                return ORBX_EIO;
+        }
+        for (int i = 1; i <= kStageMatch; ++i) mark(ex, i, m);
+        return ORBX_OK;   // (no stage marks: stage times come from unchunked runs)
+    }
     if (ex->pipeline && make_pipe(ex)) {
         for (int k = 0; k < P.n; ++k) {
             const int rc = run_extract_pipe(ex, pf[k], P.nb[k], P.s[k], ex->pipe[k]);
@@ -868,6 +890,7 @@ orbx_extractor *orbx_extractor_create(int device, int nfeatures, float scaleFact
     if (const char *pp = std::getenv("ORBX_PIPELINE")) ex->pipeline = std::atoi(pp) != 0;
     if (const char *om = std::getenv("ORBX_OVERLAP_MATCH")) ex->overlap_match = std::atoi(om) != 0;
     if (const char *sg = std::getenv("ORBX_STAGGER")) ex->stagger = std::max(0, std::min(std::atoi(sg), 3));
+    if (const char *ck = std::getenv("ORBX_CHUNKS")) ex->chunks = std::max(1, std::min(std::atoi(ck), 64));
     // geometry tables for the getters are size independent; plan a nominal size
     ex->plan = make_plan(640, 480, nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST);
     return ex;
@@ -1814,8 +1837,31 @@ struct Dedup {
 };
 
 // Runs the problems (all of one variant) in one pair of launches.
+// ORBX_CALL_TIMING=1: a synchronous call's host phases (checks, staging,
+// enqueue, wait, readback) in microseconds on stderr (diagnostics).
+struct CallClock {
+    bool on;
+    std::chrono::steady_clock::time_point t0;
+    double us[6] = {};
+    int n = 0;
+    CallClock() : on(std::getenv("ORBX_CALL_TIMING") != nullptr), t0(std::chrono::steady_clock::now()) {}
+    void mark() {
+        if (!on || n >= 6) return;
+        const auto t = std::chrono::steady_clock::now();
+        us[n++] = std::chrono::duration<double, std::micro>(t - t0).count();
+        t0 = t;
+    }
+    void print(const char *what) const {
+        if (!on) return;
+        std::fprintf(stderr, "orbx %s us:", what);
+        for (int i = 0; i < n; ++i) std::fprintf(stderr, " %.1f", us[i]);
+        std::fprintf(stderr, "\n");
+    }
+};
+
 int proj_run(int device, int variant, orbx_proj_problem *P, int np, int th_dist, float nnratio, int check_ori) {
     if (np < 0 || (np && !P)) return ORBX_EINVAL;
+    CallClock clk;   // (ORBX_CALL_TIMING: checks / staging / enqueue / wait / readback)
     std::vector<int> live;
     for (int k = 0; k < np; ++k) {
         const int rc = proj_check(variant, &P[k].frame, P[k].queries, P[k].qdesc, P[k].nq, th_dist, P[k].q_idx,
@@ -1825,6 +1871,7 @@ int proj_run(int device, int variant, orbx_proj_problem *P, int np, int th_dist,
     }
     if (live.empty()) return ORBX_OK;
     if (hipSetDevice(device) != hipSuccess) return ORBX_ENODEV;
+    clk.mark();
     const bool fuse = variant == ORBX_PROJ_FUSE || variant == ORBX_PROJ_FUSE_SIM3;
     const int nl = (int)live.size();
     int64_t nq_tot = 0;
@@ -1908,6 +1955,7 @@ int proj_run(int device, int variant, orbx_proj_problem *P, int np, int th_dist,
         }
         put(ws, o_pa, hb.data(), sizeof(ProjBufs) * nl);
         std::memset(ws.host + o_cnt, 0, 16 + 8 * (size_t)nl);
+        clk.mark();
         if (hipMemcpyAsync(D, ws.host, in_bytes, hipMemcpyHostToDevice, ws.st) != hipSuccess) return ORBX_EIO;
         // Outputs: one copy whose completion the host polls (ORBX_PROJ_TAIL=2,
         // the default).  The replay's workgroup writing them into pinned
@@ -1919,10 +1967,12 @@ int proj_run(int device, int variant, orbx_proj_problem *P, int np, int th_dist,
             ws_tail(ws, o_cnt, out_end - o_cnt, at<uint32_t>(D, o_cnt + 8 + 8 * (size_t)nl),
                     proj_tail_blocks(hb.data(), nl), tail);
         if (launch_proj(hb.data(), at<ProjBufs>(D, o_pa), nl, tail, ws.st) != hipSuccess) return ORBX_EIO;
+        clk.mark();
         if (tail_mode == 1 ? ws_wait(ws, tail, o_cnt, out_end - o_cnt)
                            : tail_mode == 2 ? ws_copy_spin(ws, o_cnt, out_end - o_cnt)
                                             : ws_copy_sync(ws, o_cnt, out_end - o_cnt))
             return ORBX_EIO;
+        clk.mark();
         unsigned long long used = 0;
         get(ws, o_cnt, &used, 8);
         if (dbg_stats) {
@@ -1944,6 +1994,8 @@ int proj_run(int device, int variant, orbx_proj_problem *P, int np, int th_dist,
             get(ws, o[t].kf, pr.kp_final, 4 * (size_t)pr.frame.n);
             get(ws, o[t].nm, &pr.nmatches, 4);
         }
+        clk.mark();
+        clk.print("proj");
         return ORBX_OK;
     }
     return ORBX_EIO;
@@ -1997,28 +2049,6 @@ int bow_check(int variant, const orbx_bow_side *A, const orbx_bow_side *B, const
     for (int i = 0; i < B->n; ++i) match_b[i] = -1;
     return (A->n == 0 || B->n == 0 || A->nnodes == 0 || B->nnodes == 0) ? 1 : ORBX_OK;
 }
-
-// ORBX_CALL_TIMING=1: a synchronous call's host phases (checks, staging,
-// enqueue, wait, readback) in microseconds on stderr (diagnostics).
-struct CallClock {
-    bool on;
-    std::chrono::steady_clock::time_point t0;
-    double us[6] = {};
-    int n = 0;
-    CallClock() : on(std::getenv("ORBX_CALL_TIMING") != nullptr), t0(std::chrono::steady_clock::now()) {}
-    void mark() {
-        if (!on || n >= 6) return;
-        const auto t = std::chrono::steady_clock::now();
-        us[n++] = std::chrono::duration<double, std::micro>(t - t0).count();
-        t0 = t;
-    }
-    void print(const char *what) const {
-        if (!on) return;
-        std::fprintf(stderr, "orbx %s us:", what);
-        for (int i = 0; i < n; ++i) std::fprintf(stderr, " %.1f", us[i]);
-        std::fprintf(stderr, "\n");
-    }
-};
 
 // Diagnostics of the calling thread's last host call (orbx_debug_counter).
 struct DebugCounters {

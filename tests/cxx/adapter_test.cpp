@@ -36,6 +36,10 @@
 //        OrbxMatcher::SearchByBoWTable (the SearchByBoW / SearchForTriangulation
 //        forwarder, ORBmatcher_orbx.cc) on one problem from bench.py's
 //        write_bow_case(): prints "bow_ms <median>" and "matches <n>".
+//   adapter_test time_proj variant th ratio ori frame.bin queries.bin reps
+//        OrbxMatcher::SearchByProjectionTable (the SearchByProjection / Fuse
+//        forwarders, ORBmatcher_orbx.cc) on the files of "proj": prints
+//        "proj_ms <median>", "proj_min_ms <min>" over reps calls and "matches <n>".
 //   adapter_test time_rgbd W H img.raw depth.raw mbf reps
 //        Frame's RGB-D constructor: extraction, then ComputeStereoFromRGBD
 //        (Frame.cc:679-701) through OrbxFrame: prints "rgbd_frame_ms <median>"
@@ -209,7 +213,7 @@ int main(int argc, char **argv) {
         out.write(reinterpret_cast<const char *>(dp.data()), 4 * dp.size());
         return 0;
     }
-    if (argc == 9 && std::string(argv[1]) == "proj") {
+    if ((argc == 9 && std::string(argv[1]) == "proj") || (argc == 9 && std::string(argv[1]) == "time_proj")) {
         // frame.bin: n, min_x, max_x, min_y, max_y, n x 28 B keys, n x 32 B desc, n floats uright, n u8 state,
         //            nlev, nlev floats inv_sigma2;  queries.bin: nq, nq x 36 B rows, nq x 32 B desc
         std::ifstream ff(argv[6], std::ios::binary), fq(argv[7], std::ios::binary);
@@ -243,6 +247,19 @@ int main(int argc, char **argv) {
         const int nm = OrbxMatcher::SearchByProjectionTable(std::atoi(argv[2]), F, q, qd, std::atoi(argv[3]),
                                                             (float)std::atof(argv[4]), std::atoi(argv[5]) != 0, qi,
                                                             qdist, kf);
+        if (std::string(argv[1]) == "time_proj") {
+            const int reps = std::max(1, std::atoi(argv[8]));
+            std::vector<double> t(reps);
+            for (int i = 0; i < reps; ++i) {
+                const auto t0 = std::chrono::steady_clock::now();
+                OrbxMatcher::SearchByProjectionTable(std::atoi(argv[2]), F, q, qd, std::atoi(argv[3]),
+                                                     (float)std::atof(argv[4]), std::atoi(argv[5]) != 0, qi, qdist, kf);
+                t[i] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            }
+            std::sort(t.begin(), t.end());
+            std::printf("proj_ms %.4f\nproj_min_ms %.4f\nmatches %d\n", t[reps / 2], t[0], nm);
+            return 0;
+        }
         // the same problem twice through the batch entry point: both copies
         // must equal the single call (a non-zero exit says they do not)
         std::vector<std::vector<int>> bqi, bqd, bkf;
