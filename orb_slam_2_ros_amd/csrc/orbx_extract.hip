@@ -951,8 +951,46 @@ __device__ inline u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, 
 // The 16 arcs in pairs sharing 8 points (as OpenCV's cornerScore<16> walks
 // them): for even k, arcs k..k+8 and k+1..k+9 are the block B = k+1..k+8 plus
 // point k or point k+9.  The eight blocks (odd starts j) come from minima of
-// pairs and quads at odd starts only: 24 + 16 + 15 packed ops instead of the
-// 48 + 16 + 15 of all sixteen sliding windows.
+// pairs and quads at odd starts only: 24 + 24 packed ops (the 16 arcs' minima
+// folded per block) instead of the 48 + 16 + 15 of all sixteen sliding windows.
+#ifndef ORBX_ARC_DIST
+#define ORBX_ARC_DIST 1
+#endif
+// ORBX_ARC_F16=1: the pairs offset by K = 0x3C00 (both halves normal positive
+// f16 numbers, 1.0 .. 1.25, ordered as their bit patterns), so gfx950's packed
+// three-input v_pk_minimum3_f16 / v_pk_maximum3_f16 apply: block i's value is
+// min3(m4[i], m4[i+2], max(e[2i], e[2i+9])) (no m8 stage) and the eight block
+// values fold by max3 -- 8 + 8 + 16 + 4 packed ops against 8 + 8 + 8 + 24.
+#ifndef ORBX_ARC_F16
+#define ORBX_ARC_F16 1
+#endif
+#if ORBX_ARC_F16
+__device__ inline u16x2 pk_min3_h(u16x2 a, u16x2 b, u16x2 c) {
+    uint32_t r;
+    asm("v_pk_minimum3_f16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return as_u16x2(r);
+}
+__device__ inline u16x2 pk_max3_h(u16x2 a, u16x2 b, u16x2 c) {
+    uint32_t r;
+    asm("v_pk_maximum3_f16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return as_u16x2(r);
+}
+__device__ inline int arc_score_bytes(const int p[16], int v) {
+    constexpr uint32_t K = 0x3C00u, C = ((255u + K) << 16) + K;   // (p, 255 - p) + (K, K)
+    u16x2 e[16], m2[8], m4[8], x[8];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) e[k] = as_u16x2(C - (uint32_t)p[k] * 65535u);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) m2[i] = __builtin_elementwise_min(e[2 * i + 1], e[(2 * i + 2) & 15]);   // j, j+1
+#pragma unroll
+    for (int i = 0; i < 8; ++i) m4[i] = __builtin_elementwise_min(m2[i], m2[(i + 1) & 7]);              // j..j+3
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        x[i] = pk_min3_h(m4[i], m4[(i + 2) & 7], __builtin_elementwise_max(e[2 * i], e[(2 * i + 9) & 15]));
+    const u16x2 best = __builtin_elementwise_max(pk_max3_h(pk_max3_h(pk_max3_h(x[0], x[1], x[2]), x[3], x[4]), x[5], x[6]), x[7]);
+    return max((int)best.x - (int)K - v, v - (255 + (int)K - (int)best.y));
+}
+#else
 __device__ inline int arc_score_bytes(const int p[16], int v) {
     u16x2 e[16], m2[8], m4[8], m8[8];
 #pragma unroll
@@ -963,16 +1001,29 @@ __device__ inline int arc_score_bytes(const int p[16], int v) {
     for (int i = 0; i < 8; ++i) m4[i] = __builtin_elementwise_min(m2[i], m2[(i + 1) & 7]);              // j..j+3
 #pragma unroll
     for (int i = 0; i < 8; ++i) m8[i] = __builtin_elementwise_min(m4[i], m4[(i + 2) & 7]);              // j..j+7
-    // block i = points 2i+1 .. 2i+8: arcs starting at 2i and 2i+1
-    u16x2 best = __builtin_elementwise_min(m8[0], e[0]);
+    // block i = points 2i+1 .. 2i+8: arcs starting at 2i and 2i+1, whose
+    // minima max together as min(m8, e[2i]) v min(m8, e[2i+9]) =
+    // min(m8, max(e[2i], e[2i+9])) (min distributes over max): three packed
+    // ops a block instead of four (ORBX_ARC_DIST=0: the four)
+    u16x2 best;
+#if ORBX_ARC_DIST
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const u16x2 x = __builtin_elementwise_min(m8[i], __builtin_elementwise_max(e[2 * i], e[(2 * i + 9) & 15]));
+        best = i ? __builtin_elementwise_max(best, x) : x;
+    }
+#else
+    best = __builtin_elementwise_min(m8[0], e[0]);
     best = __builtin_elementwise_max(best, __builtin_elementwise_min(m8[0], e[9]));
 #pragma unroll
     for (int i = 1; i < 8; ++i) {
         best = __builtin_elementwise_max(best, __builtin_elementwise_min(m8[i], e[2 * i]));
         best = __builtin_elementwise_max(best, __builtin_elementwise_min(m8[i], e[(2 * i + 9) & 15]));
     }
+#endif
     return max((int)best.x - v, v - (255 - (int)best.y));
 }
+#endif
 
 // k_fast's cell + ring (ORBX_FAST_STAGE): nr rows of nd dwords from column
 // x0 - 1, so that column x0 lands at patch column 1 (interior column 0 at
