@@ -151,7 +151,14 @@ struct orbx_extractor {
     struct PipeSet {
         hipStream_t s[2] = {};
         hipEvent_t fork = nullptr, level0 = nullptr, done[2] = {};
+        hipEvent_t resized = nullptr, early = nullptr;   // (pipeline 2: levels 1..E resized / their quadtree done)
     } pipe[kMaxParts];
+    // pipeline 2: the levels FAST / quadtree take on the side stream once the
+    // resize chain has produced them (ORBX_PIPE_EARLY, 1..nlevels - 2), and
+    // whether their describe runs there too (ORBX_PIPE_DESC=1) rather than
+    // with the other levels' at the end of the main stream
+    int pipe_early = 2;
+    int pipe_desc = 0;
     bool pipe_ready = false;
     int split = 1;   // orbx_extractor_split / ORBX_SPLIT=2 turn it on
     hipStream_t part_stream[kMaxParts] = {};
@@ -215,7 +222,7 @@ struct orbx_extractor {
         for (auto &ps : pipe) {
             for (auto &x : ps.s)
                 if (x) (void)hipStreamDestroy(x);
-            for (hipEvent_t e : {ps.fork, ps.level0, ps.done[0], ps.done[1]})
+            for (hipEvent_t e : {ps.fork, ps.level0, ps.done[0], ps.done[1], ps.resized, ps.early})
                 if (e) (void)hipEventDestroy(e);
         }
     }
@@ -616,6 +623,7 @@ bool make_pipe(orbx_extractor *ex) {
     for (auto &ps : ex->pipe) {
         for (auto &x : ps.s) ok = ok && fork_stream(&x) == hipSuccess;
         ok = ok && hipEventCreateWithFlags(&ps.fork, f) == hipSuccess && hipEventCreateWithFlags(&ps.level0, f) == hipSuccess;
+        ok = ok && hipEventCreateWithFlags(&ps.resized, f) == hipSuccess && hipEventCreateWithFlags(&ps.early, f) == hipSuccess;
         for (auto &e : ps.done) ok = ok && hipEventCreateWithFlags(&e, f) == hipSuccess;
     }
     ex->pipe_ready = ok;
@@ -647,6 +655,53 @@ int run_extract_pipe(orbx_extractor *ex, const FrameBufs &fb, int nb, hipStream_
         if (hipStreamWaitEvent(ps.s[0], ps.level0, 0) != hipSuccess) return ORBX_EIO;
         if (!gate_describe(ex, ps.s[0]) || launch_describe_level(dp, hp, fb, nb, ps.s[0], 1, n) != hipSuccess) return ORBX_EIO;
     }
+    for (int i = 0; i < 2; ++i)
+        if (hipEventRecord(ps.done[i], ps.s[i]) != hipSuccess || hipStreamWaitEvent(st, ps.done[i], 0) != hipSuccess)
+            return ORBX_EIO;
+    return ORBX_OK;
+}
+
+// The deep level pipeline (pipeline 2): the side stream also takes levels
+// 1..E once the resize chain has produced them, so the rest of the chain
+// (latency- and memory-bound) runs beside their FAST (VALU-bound):
+//   stream 1: FAST + quadtree of level 0, describe of level 0, then (after
+//             `resized`) FAST + quadtree of levels 1..E (event `early`), and
+//             with ORBX_PIPE_DESC=1 their describe
+//   stream 0: resize of levels 1..E (event `resized`), resize of E+1..,
+//             FAST + quadtree of levels E+1.., then (after `early`: every
+//             count below a level is final) describe of levels 1.. (E+1..)
+// Each describe launch needs the counts of the levels below it (its output
+// offsets), which `early` covers.  Same kernels, same outputs.
+int run_extract_pipe2(orbx_extractor *ex, const FrameBufs &fb, int nb, hipStream_t st, orbx_extractor::PipeSet &ps) {
+    const Plan &hp = ex->plan;
+    const DevPlan &dp = ex->dp;
+    const int n = hp.nlevels, E = std::max(1, std::min(ex->pipe_early, n - 2));
+    if (hipEventRecord(ps.fork, st) != hipSuccess) return ORBX_EIO;
+    for (auto &x : ps.s)
+        if (hipStreamWaitEvent(x, ps.fork, 0) != hipSuccess) return ORBX_EIO;
+    if (launch_fast_level(dp, hp, fb, nb, ps.s[1], 0, 1) != hipSuccess ||
+        launch_quadtree_level(dp, fb, nb, ps.s[1], 0, 1) != hipSuccess)
+        return ORBX_EIO;
+    if (!gate_describe(ex, ps.s[1]) || launch_describe_level(dp, hp, fb, nb, ps.s[1], 0, 1) != hipSuccess) return ORBX_EIO;
+    for (int l = 1; l <= E; ++l)
+        if (launch_resize_level(dp, hp, fb, nb, ps.s[0], l) != hipSuccess) return ORBX_EIO;
+    if (hipEventRecord(ps.resized, ps.s[0]) != hipSuccess || hipStreamWaitEvent(ps.s[1], ps.resized, 0) != hipSuccess)
+        return ORBX_EIO;
+    if (launch_fast_level(dp, hp, fb, nb, ps.s[1], 1, E + 1) != hipSuccess ||
+        launch_quadtree_level(dp, fb, nb, ps.s[1], 1, E + 1) != hipSuccess)
+        return ORBX_EIO;
+    if (hipEventRecord(ps.early, ps.s[1]) != hipSuccess) return ORBX_EIO;
+    const int d0 = ex->pipe_desc ? E + 1 : 1;   // the main stream's describe levels [d0, n)
+    if (ex->pipe_desc &&
+        (!gate_describe(ex, ps.s[1]) || launch_describe_level(dp, hp, fb, nb, ps.s[1], 1, E + 1) != hipSuccess))
+        return ORBX_EIO;
+    for (int l = E + 1; l < n; ++l)
+        if (launch_resize_level(dp, hp, fb, nb, ps.s[0], l) != hipSuccess) return ORBX_EIO;
+    if (launch_fast_level(dp, hp, fb, nb, ps.s[0], E + 1, n) != hipSuccess ||
+        launch_quadtree_level(dp, fb, nb, ps.s[0], E + 1, n) != hipSuccess)
+        return ORBX_EIO;
+    if (hipStreamWaitEvent(ps.s[0], ps.early, 0) != hipSuccess) return ORBX_EIO;
+    if (!gate_describe(ex, ps.s[0]) || launch_describe_level(dp, hp, fb, nb, ps.s[0], d0, n) != hipSuccess) return ORBX_EIO;
     for (int i = 0; i < 2; ++i)
         if (hipEventRecord(ps.done[i], ps.s[i]) != hipSuccess || hipStreamWaitEvent(st, ps.done[i], 0) != hipSuccess)
             return ORBX_EIO;
@@ -685,7 +740,11 @@ int run_extract(orbx_extractor *ex, int si, const uint8_t *d_images, int64_t str
     }
     if (ex->pipeline && make_pipe(ex)) {
         for (int k = 0; k < P.n; ++k) {
-            const int rc = run_extract_pipe(ex, pf[k], P.nb[k], P.s[k], ex->pipe[k]);
+            // (the deep form needs the per-level resize kernels: not the
+            // small-batch region pyramid, and at least three levels)
+            const bool deep = ex->pipeline == 2 && ex->plan.nlevels >= 3 && !use_pyr_regions(ex->plan, P.nb[k]);
+            const int rc = deep ? run_extract_pipe2(ex, pf[k], P.nb[k], P.s[k], ex->pipe[k])
+                                : run_extract_pipe(ex, pf[k], P.nb[k], P.s[k], ex->pipe[k]);
             if (rc) return rc;
         }
         return ORBX_OK;
@@ -887,7 +946,9 @@ orbx_extractor *orbx_extractor_create(int device, int nfeatures, float scaleFact
     ex->min_th = minThFAST;
     if (hipStreamCreateWithFlags(&ex->stream, hipStreamNonBlocking) != hipSuccess) { delete ex; return nullptr; }
     if (const char *sp = std::getenv("ORBX_SPLIT")) ex->split = std::max(1, std::min(std::atoi(sp), orbx_extractor::kMaxParts));
-    if (const char *pp = std::getenv("ORBX_PIPELINE")) ex->pipeline = std::atoi(pp) != 0;
+    if (const char *pp = std::getenv("ORBX_PIPELINE")) ex->pipeline = std::max(0, std::min(std::atoi(pp), 2));
+    if (const char *pe = std::getenv("ORBX_PIPE_EARLY")) ex->pipe_early = std::max(1, std::atoi(pe));
+    if (const char *pd = std::getenv("ORBX_PIPE_DESC")) ex->pipe_desc = std::atoi(pd) != 0;
     if (const char *om = std::getenv("ORBX_OVERLAP_MATCH")) ex->overlap_match = std::atoi(om) != 0;
     if (const char *sg = std::getenv("ORBX_STAGGER")) ex->stagger = std::max(0, std::min(std::atoi(sg), 3));
     if (const char *ck = std::getenv("ORBX_CHUNKS")) ex->chunks = std::max(1, std::min(std::atoi(ck), 64));
@@ -1447,7 +1508,7 @@ int orbx_extractor_overlap_match(orbx_extractor *ex, int on) {
 }
 
 int orbx_extractor_pipeline(orbx_extractor *ex, int on) {
-    if (!ex || on < -1 || on > 1) return ORBX_EINVAL;
+    if (!ex || on < -1 || on > 2) return ORBX_EINVAL;
     if (on >= 0) ex->pipeline = on;
     return ex->pipeline;
 }

@@ -201,7 +201,7 @@ class ORBextractor:
         return check(self._lib.orbx_extractor_split(self._h, int(parts)), "split")
 
     def pipeline(self, on: int = -1) -> int:
-        """Level-pipelined extraction on internal streams (1 on, 0 off, -1 query)."""
+        """Level-pipelined extraction on internal streams (2 deep, 1 on, 0 off, -1 query)."""
         return check(self._lib.orbx_extractor_pipeline(self._h, int(on)), "pipeline")
 
     def overlap_match(self, on: int = -1) -> int:

@@ -178,6 +178,61 @@ def test_mono_overlap_transitions(oracle_mod):
     ex.close()
 
 
+@pytest.mark.parametrize("mode,w,h,nf,B", [("mono", 640, 480, 1000, 256), ("stereo", 1920, 1080, 1000, 32),
+                                            ("mono", 1241, 376, 2000, 64)])
+def test_deep_level_pipeline(mode, w, h, nf, B, oracle_mod):
+    """The deep level pipeline (orbx_extractor_pipeline(2): FAST / quadtree of
+    levels 1..E on the side stream as the resize chain produces them, E =
+    ORBX_PIPE_EARLY; their describe there too with ORBX_PIPE_DESC=1) gives
+    byte-identical keypoints, descriptors and matches / depths to the
+    unpipelined step for every stream and E in 1..3, and the oracle's on
+    sampled streams; split 2 as well (each part pipelined)."""
+    import os
+    import torch
+    host, _, fr, _ = _frames(torch, mode, w, h, list(range(B)))
+    frames = 2 * B if mode == "stereo" else B
+
+    def run(pipe, early, split, desc=0):
+        saved = {k: os.environ.get(k) for k in ("ORBX_PIPE_EARLY", "ORBX_PIPE_DESC")}
+        os.environ["ORBX_PIPE_EARLY"] = str(early)   # (read at extractor creation)
+        os.environ["ORBX_PIPE_DESC"] = str(desc)
+        try:
+            ex = ORBextractor(nf, 1.2, 8, 20, 7)
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    del os.environ[k]
+                else:
+                    os.environ[k] = v
+        ex.reserve(w, h, frames)
+        ex.split(split)
+        assert ex.pipeline(pipe) == pipe
+        for t in range(2):
+            if mode == "mono":
+                ex.mono_step_device(fr[t].data_ptr(), w * h, w, B, 100, 0.9, True)
+            else:
+                ex.stereo_step_device(fr[t].data_ptr(), w * h, w, B, BF, MB)
+        torch.cuda.synchronize()
+        kd = [ex.batch_download(b) for b in range(frames)]
+        extra = [ex.mono_matches_download(b) if mode == "mono" else ex.depth_download(b) for b in range(B)]
+        ex.close()
+        return kd, extra
+
+    ref_kd, ref_x = run(0, 2, 1)
+    for pipe, early, split, desc in [(2, 1, 1, 0), (2, 2, 1, 0), (2, 3, 1, 0), (2, 2, 2, 0), (2, 2, 1, 1), (2, 3, 2, 1)]:
+        kd, x = run(pipe, early, split, desc)
+        for b in range(frames):
+            assert _kp_equal(kd[b][0], ref_kd[b][0]) and np.array_equal(kd[b][1], ref_kd[b][1]), \
+                f"pipe {pipe} E {early} split {split} frame {b}"
+        for b in range(B):
+            assert all(np.array_equal(np.asarray(u), np.asarray(v)) for u, v in zip(x[b], ref_x[b])), \
+                f"pipe {pipe} E {early} split {split} stream {b}"
+    for b in (0, B - 1):
+        k2, d2 = oracle_mod.extract(host[1, b], nf) if mode == "mono" else oracle_mod.extract(host[1, 2 * b], nf)
+        f = b if mode == "mono" else 2 * b
+        assert _kp_equal(ref_kd[f][0], k2) and np.array_equal(ref_kd[f][1], d2), f"frame {f} vs oracle"
+
+
 MONO_EXTRAS = [(w, h, nf, B) for key, mode, w, h, nf, B, _ in bench.EXTRAS if mode == "mono"]
 
 
