@@ -946,15 +946,13 @@ def run_config(torch, dist, rank, world, dev, w, h, nfeatures, streams, steps, w
         # matcher launches overlap the other half's VALU-bound ones
         ex.split(split)
     if pipeline and stub is None and "ORBX_PIPELINE" not in os.environ:
-        ex.pipeline(pipeline)   # level pipeline (2: the deep form): on where it measured faster
+        ex.pipeline(1)   # level pipeline: on where it measured faster
     if overlap is None:
         overlap = MONO_OVERLAP
     if overlap and mode == "mono" and stub is None and "ORBX_OVERLAP_MATCH" not in os.environ:
         # each step's matcher beside the next step's extraction (orbx_extractor_overlap_match;
         # the timed region ends with a device-wide synchronisation, which covers it)
         ex.overlap_match(1)
-        if MONO_OVERLAP_DESC and "ORBX_OVERLAP_DESC" not in os.environ:
-            ex.overlap_describe(1)   # (and its last describe launch beside the next step)
     host, depth = _resident_frames(mode, w, h, streams)
     if kframes > 1:
         # launch u holds times u K .. u K + K - 1 (mod the resident frames) of
@@ -1173,9 +1171,6 @@ HEADLINE_PIPE = 1
 # SearchForInitialization on an internal stream beside the next step's resize /
 # FAST / quadtree: VGA 449.1 k -> 454.1 k frames/s on one box (profiles/r05_ab_overlap_match.txt)
 MONO_OVERLAP = 1
-# Describe overlap of the mono steps (orbx_extractor_overlap_describe, with the deep level pipeline):
-# a step's last describe launch beside the next step's level-0 FAST and resize chain
-MONO_OVERLAP_DESC = 0
 # Batch split of the VGA headline: with the quadtree's child counts aggregated
 # (0.61 -> 0.38 ms) there is less latency-bound work to hide behind the other
 # half, and one launch per stage measured faster on one box over two rounds

@@ -164,18 +164,6 @@ int orbx_extractor_pipeline(orbx_extractor *ex, int on);
  * on: 1 / 0 sets, -1 queries; returns the current setting. */
 int orbx_extractor_overlap_match(orbx_extractor *ex, int on);
 
-/* Describe overlap (default off; takes effect with the deep level pipeline,
- * orbx_extractor_pipeline(ex, 2), and the matcher overlap): a mono step's last
- * descriptor launch runs on an internal stream that the launch stream does not
- * wait for, so the next step's level-0 FAST and resize chain start beside it.
- * The step's matcher waits for it, and the step's keypoints and descriptors
- * are complete when the matches are (download calls and
- * orbx_batch_pack_device wait for them).  The pyramid, quadtree selections and
- * level counts are kept per result slot so the next step does not overwrite
- * what the deferred launch reads.  Outputs are identical either way.  No
- * reference counterpart.  on: 1 / 0 sets, -1 queries; returns the setting. */
-int orbx_extractor_overlap_describe(orbx_extractor *ex, int on);
-
 /* Per-stage device time of the last batch (HIP events on the launch stream),
  * in ms, when profiling is enabled: resize, blur, fast, quadtree, describe,
  * match.  Returns the number of stages written. */

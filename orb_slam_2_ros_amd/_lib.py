@@ -104,7 +104,6 @@ _SIGNATURES = {
     "orbx_extractor_split": (I32, [P, I32]),
     "orbx_extractor_pipeline": (I32, [P, I32]),
     "orbx_extractor_overlap_match": (I32, [P, I32]),
-    "orbx_extractor_overlap_describe": (I32, [P, I32]),
     "orbx_extractor_set_profiling": (I32, [P, I32]),
     "orbx_extractor_stage_times": (I32, [P, P, I32]),
     "orbx_extractor_debug_fetch": (I32, [P, I32, I32, I32, P, I64]),

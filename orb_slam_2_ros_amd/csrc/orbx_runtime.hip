@@ -152,20 +152,7 @@ struct orbx_extractor {
         hipStream_t s[2] = {};
         hipEvent_t fork = nullptr, level0 = nullptr, done[2] = {};
         hipEvent_t resized = nullptr, early = nullptr;   // (pipeline 2: levels 1..E resized / their quadtree done)
-        hipStream_t tail = nullptr;                      // (describe overlap: the deferred describe's stream)
-        hipEvent_t qt_done = nullptr, tail_ev = nullptr;
     } pipe[kMaxParts];
-    // Describe overlap (orbx_extractor_overlap_describe, default off; needs
-    // the deep level pipeline and the matcher overlap): a mono step's last
-    // describe launch (levels E+1.. or 1..) runs on a stream of its own that
-    // the launch stream does not wait for, so the next step's FAST of level 0
-    // and resize chain start beside it.  The step's matcher waits for it
-    // (tail_ev), and the next steps write the other result slot's pyramid,
-    // selections and level counts (slot_pyr / slot_sel / slot_lc) until the
-    // matcher's gate (match_ev) has covered this step's.
-    int overlap_desc = 0;
-    bool defer_tail = false;   // (set by orbx_mono_step_device around its extraction)
-    unsigned tail_mask = 0;    // parts whose describe is deferred in the current step
     // pipeline 2: the levels FAST / quadtree take on the side stream once the
     // resize chain has produced them (ORBX_PIPE_EARLY, 1..nlevels - 2), and
     // whether their describe runs there too (ORBX_PIPE_DESC=1) rather than
@@ -235,9 +222,8 @@ struct orbx_extractor {
         for (auto &ps : pipe) {
             for (auto &x : ps.s)
                 if (x) (void)hipStreamDestroy(x);
-            for (hipEvent_t e : {ps.fork, ps.level0, ps.done[0], ps.done[1], ps.resized, ps.early, ps.qt_done, ps.tail_ev})
+            for (hipEvent_t e : {ps.fork, ps.level0, ps.done[0], ps.done[1], ps.resized, ps.early})
                 if (e) (void)hipEventDestroy(e);
-            if (ps.tail) (void)hipStreamDestroy(ps.tail);
         }
     }
 
@@ -422,10 +408,7 @@ int reserve(orbx_extractor *ex, int w, int h, int max_batch) {
     const size_t B = (size_t)max_batch;
     if (B * (size_t)std::max(p.out_cap, 1) >= (size_t(1) << 31)) return ORBX_EINVAL;   // (k_describe's 32-bit slot index)
     bool ok = true;
-    // pyramid, selections and level counts per result slot: a step's describe
-    // may still read its slot's while the next step (the other slot) runs
-    // (orbx_extractor_overlap_describe)
-    ok &= dalloc(&ex->d_pyr, 2 * B * p.pyr_bytes) == hipSuccess;
+    ok &= dalloc(&ex->d_pyr, B * p.pyr_bytes) == hipSuccess;
     ok &= dalloc(&ex->d_blur, B * p.blur_bytes) == hipSuccess;
     ok &= dalloc(&ex->d_cand, B * p.cand_cap) == hipSuccess;
     ok &= dalloc(&ex->d_cand2, B * p.cand_cap) == hipSuccess;
@@ -433,8 +416,8 @@ int reserve(orbx_extractor *ex, int w, int h, int max_batch) {
     ok &= dalloc(&ex->d_key_node, B * p.cand_cap) == hipSuccess;
     ok &= dalloc(&ex->d_key_q, B * p.cand_cap) == hipSuccess;
     ok &= dalloc(&ex->d_cell_count, B * p.cells.size()) == hipSuccess;
-    ok &= dalloc(&ex->d_sel, 2 * B * p.out_cap) == hipSuccess;
-    ok &= dalloc(&ex->d_level_count, 2 * B * kMaxLevels) == hipSuccess;
+    ok &= dalloc(&ex->d_sel, B * p.out_cap) == hipSuccess;
+    ok &= dalloc(&ex->d_level_count, B * kMaxLevels) == hipSuccess;
     for (auto &s : ex->slot) {
         ok &= dalloc(&s.kps, B * p.max_kps) == hipSuccess;
         ok &= dalloc(&s.desc, B * p.max_kps * 32) == hipSuccess;
@@ -462,24 +445,13 @@ int reserve(orbx_extractor *ex, int w, int h, int max_batch) {
     return ORBX_OK;
 }
 
-// A result slot's pyramid (levels >= 1), quadtree selections and level counts.
-uint8_t *slot_pyr(const orbx_extractor *ex, int slot) {
-    return ex->d_pyr + (size_t)slot * ex->max_batch * ex->plan.pyr_bytes;
-}
-uint32_t *slot_sel(const orbx_extractor *ex, int slot) {
-    return ex->d_sel + (size_t)slot * ex->max_batch * ex->plan.out_cap;
-}
-int32_t *slot_lc(const orbx_extractor *ex, int slot) {
-    return ex->d_level_count + (size_t)slot * ex->max_batch * kMaxLevels;
-}
-
 FrameBufs frame_bufs(orbx_extractor *ex, int slot) {
     FrameBufs fb;
     const auto &s = ex->slot[slot];
     fb.img0 = s.img0;
     fb.img0_stride = s.img0_stride;
     fb.img0_pitch = s.img0_pitch;
-    fb.pyr = slot_pyr(ex, slot);
+    fb.pyr = ex->d_pyr;
     fb.blur = ex->d_blur;
     fb.cand = ex->d_cand;
     fb.cand2 = ex->d_cand2;
@@ -487,8 +459,8 @@ FrameBufs frame_bufs(orbx_extractor *ex, int slot) {
     fb.keys = ex->d_keys;
     fb.key_node = ex->d_key_node;
     fb.key_q = ex->d_key_q;
-    fb.sel = slot_sel(ex, slot);
-    fb.level_count = slot_lc(ex, slot);
+    fb.sel = ex->d_sel;
+    fb.level_count = ex->d_level_count;
     fb.kps = s.kps;
     fb.desc = s.desc;
     fb.nkps = s.nkps;
@@ -497,7 +469,7 @@ FrameBufs frame_bufs(orbx_extractor *ex, int slot) {
 
 PyrView pyr_view(const orbx_extractor *ex, int slot) {
     const auto &s = ex->slot[slot];
-    return PyrView{s.img0, s.img0_stride, s.img0_pitch, slot_pyr(ex, slot), ex->plan.pyr_bytes};
+    return PyrView{s.img0, s.img0_stride, s.img0_pitch, ex->d_pyr, ex->plan.pyr_bytes};
 }
 
 bool same_geometry(const Plan &a, const Plan &b) {
@@ -652,8 +624,6 @@ bool make_pipe(orbx_extractor *ex) {
         for (auto &x : ps.s) ok = ok && fork_stream(&x) == hipSuccess;
         ok = ok && hipEventCreateWithFlags(&ps.fork, f) == hipSuccess && hipEventCreateWithFlags(&ps.level0, f) == hipSuccess;
         ok = ok && hipEventCreateWithFlags(&ps.resized, f) == hipSuccess && hipEventCreateWithFlags(&ps.early, f) == hipSuccess;
-        ok = ok && fork_stream(&ps.tail) == hipSuccess && hipEventCreateWithFlags(&ps.qt_done, f) == hipSuccess &&
-             hipEventCreateWithFlags(&ps.tail_ev, f) == hipSuccess;
         for (auto &e : ps.done) ok = ok && hipEventCreateWithFlags(&e, f) == hipSuccess;
     }
     ex->pipe_ready = ok;
@@ -730,21 +700,8 @@ int run_extract_pipe2(orbx_extractor *ex, const FrameBufs &fb, int nb, hipStream
     if (launch_fast_level(dp, hp, fb, nb, ps.s[0], E + 1, n) != hipSuccess ||
         launch_quadtree_level(dp, fb, nb, ps.s[0], E + 1, n) != hipSuccess)
         return ORBX_EIO;
-    if (ex->defer_tail) {
-        // the last describe on the tail stream, after this step's quadtrees;
-        // the launch stream joins s0 / s1 without it (the matcher waits tail_ev)
-        hipStream_t t = ps.tail;
-        if (hipEventRecord(ps.qt_done, ps.s[0]) != hipSuccess || hipStreamWaitEvent(t, ps.qt_done, 0) != hipSuccess ||
-            hipStreamWaitEvent(t, ps.early, 0) != hipSuccess)
-            return ORBX_EIO;
-        if (!gate_describe(ex, t) || launch_describe_level(dp, hp, fb, nb, t, d0, n) != hipSuccess ||
-            hipEventRecord(ps.tail_ev, t) != hipSuccess)
-            return ORBX_EIO;
-        ex->tail_mask |= 1u << (unsigned)(&ps - ex->pipe);
-    } else {
-        if (hipStreamWaitEvent(ps.s[0], ps.early, 0) != hipSuccess) return ORBX_EIO;
-        if (!gate_describe(ex, ps.s[0]) || launch_describe_level(dp, hp, fb, nb, ps.s[0], d0, n) != hipSuccess) return ORBX_EIO;
-    }
+    if (hipStreamWaitEvent(ps.s[0], ps.early, 0) != hipSuccess) return ORBX_EIO;
+    if (!gate_describe(ex, ps.s[0]) || launch_describe_level(dp, hp, fb, nb, ps.s[0], d0, n) != hipSuccess) return ORBX_EIO;
     for (int i = 0; i < 2; ++i)
         if (hipEventRecord(ps.done[i], ps.s[i]) != hipSuccess || hipStreamWaitEvent(st, ps.done[i], 0) != hipSuccess)
             return ORBX_EIO;
@@ -992,7 +949,6 @@ orbx_extractor *orbx_extractor_create(int device, int nfeatures, float scaleFact
     if (const char *pp = std::getenv("ORBX_PIPELINE")) ex->pipeline = std::max(0, std::min(std::atoi(pp), 2));
     if (const char *pe = std::getenv("ORBX_PIPE_EARLY")) ex->pipe_early = std::max(1, std::atoi(pe));
     if (const char *pd = std::getenv("ORBX_PIPE_DESC")) ex->pipe_desc = std::atoi(pd) != 0;
-    if (const char *od = std::getenv("ORBX_OVERLAP_DESC")) ex->overlap_desc = std::atoi(od) != 0;
     if (const char *om = std::getenv("ORBX_OVERLAP_MATCH")) ex->overlap_match = std::atoi(om) != 0;
     if (const char *sg = std::getenv("ORBX_STAGGER")) ex->stagger = std::max(0, std::min(std::atoi(sg), 3));
     if (const char *ck = std::getenv("ORBX_CHUNKS")) ex->chunks = std::max(1, std::min(std::atoi(ck), 64));
@@ -1079,9 +1035,6 @@ int orbx_batch_pack_device(orbx_extractor *ex, void *d_out, int64_t cap, int64_t
     if (cap < need) return ORBX_ERANGE;
     if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
     hipStream_t st = stream_of(ex, stream);
-    // (the results may still be in flight on an internal stream: the matcher
-    // overlap's, the describe overlap's; res_ev follows them)
-    if (ex->res_pending && hipStreamWaitEvent(st, ex->res_ev, 0) != hipSuccess) return ORBX_EIO;
     auto *o = static_cast<uint8_t *>(d_out);
     if (hipMemcpyAsync(o, s.nkps, 4 * B, hipMemcpyDeviceToDevice, st) != hipSuccess ||
         hipMemcpyAsync(o + head, s.kps, B * K * sizeof(orbx_keypoint), hipMemcpyDeviceToDevice, st) != hipSuccess ||
@@ -1101,7 +1054,7 @@ int orbx_batch_download(orbx_extractor *ex, int frame, orbx_keypoint *kps, uint8
     int32_t lc[kMaxLevels];
     D2H copy{ex};
     copy(&cnt, s.nkps + frame, sizeof(int32_t));
-    copy(lc, slot_lc(ex, ex->cur) + (size_t)frame * kMaxLevels, sizeof(lc));
+    copy(lc, ex->d_level_count + (size_t)frame * kMaxLevels, sizeof(lc));
     if (!copy.wait()) return ORBX_EIO;
     for (int l = 0; l < ex->nlevels; ++l)
         if (lc[l] < 0) return ORBX_EIO;   // quadtree capacity guard tripped
@@ -1211,7 +1164,7 @@ int build_host_graph(orbx_extractor *ex, int width, int height) {
     void *dout = nullptr;   // the pinned buffer's device address
     ok = ok && hipHostGetDevicePointer(&dout, ex->h_out, 0) == hipSuccess;
     if (ok) {
-        hipLaunchKernelGGL(k_pack_host, dim3(1), dim3(kPackThreads), 0, st, s0.nkps, slot_lc(ex, 0),
+        hipLaunchKernelGGL(k_pack_host, dim3(1), dim3(kPackThreads), 0, st, s0.nkps, ex->d_level_count,
                            reinterpret_cast<const uint32_t *>(s0.kps), reinterpret_cast<const uint32_t *>(s0.desc),
                            ex->nlevels, (int)(out_desc_off(ex) / 4), reinterpret_cast<uint32_t *>(dout));
         ok = hipGetLastError() == hipSuccess;
@@ -1318,7 +1271,7 @@ int orbx_extractor_pyramid_level(orbx_extractor *ex, int level, uint8_t *out, si
     if (s.batch <= 0) return ORBX_EINVAL;
     if (hipSetDevice(ex->device) != hipSuccess) return ORBX_ENODEV;
     if (sync_results(ex)) return ORBX_EIO;
-    const uint8_t *src = level == 0 ? s.img0 : slot_pyr(ex, ex->cur) + g.pyr_off;
+    const uint8_t *src = level == 0 ? s.img0 : ex->d_pyr + g.pyr_off;
     const size_t sp = level == 0 ? (size_t)s.img0_pitch : (size_t)g.pitch;
     if (hipMemcpy2DAsync(out, out_pitch, src, sp, g.w, g.h, hipMemcpyDeviceToHost, ex->stream) != hipSuccess)
         return ORBX_EIO;
@@ -1351,7 +1304,7 @@ int orbx_extractor_pyramid_host(orbx_extractor *ex, uint8_t *const *out, const s
     }
     if (sync_results(ex)) return ORBX_EIO;
     if (hipMemcpyAsync(ex->h_pyr, s.img0, span0, hipMemcpyDeviceToHost, ex->stream) != hipSuccess ||
-        (span1 && hipMemcpyAsync(ex->h_pyr + off1, slot_pyr(ex, ex->cur) + base1, span1, hipMemcpyDeviceToHost, ex->stream) !=
+        (span1 && hipMemcpyAsync(ex->h_pyr + off1, ex->d_pyr + base1, span1, hipMemcpyDeviceToHost, ex->stream) !=
                       hipSuccess) ||
         hipStreamSynchronize(ex->stream) != hipSuccess)
         return ORBX_EIO;
@@ -1378,7 +1331,7 @@ int orbx_extractor_debug_fetch(orbx_extractor *ex, int frame, int level, int wha
         size_t sp;
         if (what == 0) {
             src = level == 0 ? s.img0 + (int64_t)frame * s.img0_stride
-                             : slot_pyr(ex, ex->cur) + (int64_t)frame * p.pyr_bytes + g.pyr_off;
+                             : ex->d_pyr + (int64_t)frame * p.pyr_bytes + g.pyr_off;
             sp = level == 0 ? (size_t)s.img0_pitch : (size_t)g.pitch;
         } else {
             // the hot path blurs patch-locally inside k_describe; materialise the
@@ -1422,13 +1375,13 @@ int orbx_extractor_debug_fetch(orbx_extractor *ex, int frame, int level, int wha
     }
     if (what == 3) {
         int32_t cnt = 0;
-        if (hipMemcpy(&cnt, slot_lc(ex, ex->cur) + (size_t)frame * kMaxLevels + level, sizeof(int32_t),
+        if (hipMemcpy(&cnt, ex->d_level_count + (size_t)frame * kMaxLevels + level, sizeof(int32_t),
                       hipMemcpyDeviceToHost) != hipSuccess)
             return ORBX_EIO;
         if (cnt < 0) return ORBX_EIO;
         if (3 * (int64_t)cnt > cap) return ORBX_ERANGE;
         std::vector<uint32_t> sel(cnt);
-        if (cnt && hipMemcpy(sel.data(), slot_sel(ex, ex->cur) + (size_t)frame * p.out_cap + g.out_off, sizeof(uint32_t) * cnt,
+        if (cnt && hipMemcpy(sel.data(), ex->d_sel + (size_t)frame * p.out_cap + g.out_off, sizeof(uint32_t) * cnt,
                              hipMemcpyDeviceToHost) != hipSuccess)
             return ORBX_EIO;
         for (int i = 0; i < cnt; ++i) {
@@ -1453,12 +1406,7 @@ int orbx_mono_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t f
     const bool have_prev = ex->slot[prev].batch == batch && ex->steps > 0;
     prof_begin(ex);
     const Parts P = fork_parts(ex, st, batch);
-    // describe overlap: the extraction's last describe deferred to the parts'
-    // tail streams, which only the overlapped matcher below waits for
-    ex->defer_tail = ex->overlap_desc && ex->overlap_match && !ex->profiling && have_prev && ex->pipeline == 2;
-    ex->tail_mask = 0;
     rc = run_extract(ex, next, d_images, frame_stride, pitch, batch, P);
-    ex->defer_tail = false;
     if (rc) return rc;
     ex->cur = next;
     ++ex->steps;
@@ -1495,9 +1443,6 @@ int orbx_mono_step_device(orbx_extractor *ex, const uint8_t *d_images, int64_t f
         }
         if (hipEventRecord(ex->ext_ev, st) != hipSuccess || hipStreamWaitEvent(ex->match_stream, ex->ext_ev, 0) != hipSuccess)
             return ORBX_EIO;
-        for (int k = 0; k < orbx_extractor::kMaxParts; ++k)   // (the deferred describes: the slot the matcher reads)
-            if ((ex->tail_mask >> k & 1u) && hipStreamWaitEvent(ex->match_stream, ex->pipe[k].tail_ev, 0) != hipSuccess)
-                return ORBX_EIO;
         if (launch_match(mb, batch, ex->plan.max_kps, ex->plan.max_kps, ex->l0cap, ex->l0cap, ex->match_stream) != hipSuccess ||
             hipEventRecord(ex->match_ev, ex->match_stream) != hipSuccess)
             return ORBX_EIO;
@@ -1554,12 +1499,6 @@ int orbx_mono_matches_download(orbx_extractor *ex, int frame, int32_t *matches12
     if (cnt > cap) return ORBX_ERANGE;
     if (cnt > 0 && matches12) copy(matches12, ex->d_m12 + (size_t)frame * ex->plan.max_kps, sizeof(int32_t) * cnt);
     return copy.wait() ? ORBX_OK : ORBX_EIO;
-}
-
-int orbx_extractor_overlap_describe(orbx_extractor *ex, int on) {
-    if (!ex || on < -1 || on > 1) return ORBX_EINVAL;
-    if (on >= 0) ex->overlap_desc = on;
-    return ex->overlap_desc;
 }
 
 int orbx_extractor_overlap_match(orbx_extractor *ex, int on) {

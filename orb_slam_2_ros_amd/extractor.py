@@ -209,11 +209,6 @@ class ORBextractor:
         extraction (1 on, 0 off, -1 query; include/orbx.h)."""
         return check(self._lib.orbx_extractor_overlap_match(self._h, int(on)), "overlap_match")
 
-    def overlap_describe(self, on: int = -1) -> int:
-        """A mono step's last describe launch beside the next step (with the
-        deep level pipeline and the matcher overlap; 1 on, 0 off, -1 query)."""
-        return check(self._lib.orbx_extractor_overlap_describe(self._h, int(on)), "overlap_describe")
-
     def set_profiling(self, on: bool) -> None:
         check(self._lib.orbx_extractor_set_profiling(self._h, int(on)), "set_profiling")
 

@@ -233,54 +233,6 @@ def test_deep_level_pipeline(mode, w, h, nf, B, oracle_mod):
         assert _kp_equal(ref_kd[f][0], k2) and np.array_equal(ref_kd[f][1], d2), f"frame {f} vs oracle"
 
 
-def test_mono_overlap_describe_steps(oracle_mod):
-    """Describe overlap (orbx_extractor_overlap_describe, with the deep level
-    pipeline and the matcher overlap, split 1 and 2): four mono steps back to
-    back, each step's last describe launch beside the next step; every
-    stream's matches, keypoints and descriptors equal those of the same steps
-    run without any overlap, sampled streams equal the oracle's, and the
-    device pack (orbx_batch_pack_device, on another stream, no synchronisation
-    before it) holds the final step's keypoint counts."""
-    import torch
-    w, h, B = 640, 480, 512
-    host, _, fr, _ = _frames(torch, "mono", w, h, list(range(B)))
-
-    def run(pipe, ovl, desc, split):
-        ex = ORBextractor(1000, 1.2, 8, 20, 7)
-        ex.reserve(w, h, B)
-        ex.split(split)
-        assert ex.pipeline(pipe) == pipe
-        ex.overlap_match(ovl)
-        assert ex.overlap_describe(desc) == desc and ex.overlap_describe() == desc
-        for t in range(4):
-            ex.mono_step_device(fr[t].data_ptr(), w * h, w, B, 100, 0.9, True)
-        side = torch.cuda.Stream()
-        nb = ex.pack_bytes()
-        pk = torch.empty(nb, dtype=torch.uint8, device="cuda")
-        ex.pack_device(pk.data_ptr(), nb, side.cuda_stream)
-        torch.cuda.synchronize()
-        counts = pk[:4 * B].view(torch.int32).cpu().numpy().copy()
-        out = ([ex.mono_matches_download(b) for b in range(B)], [ex.batch_download(b) for b in range(B)], counts)
-        ex.close()
-        return out
-
-    m_ref, o_ref, c_ref = run(0, 0, 0, 1)
-    assert np.array_equal(c_ref, [len(o_ref[b][0]) for b in range(B)])
-    for split in (1, 2):
-        m, o, c = run(2, 1, 1, split)
-        assert np.array_equal(c, c_ref), f"split {split}: packed counts"
-        for b in range(B):
-            assert m[b][1] == m_ref[b][1] and np.array_equal(m[b][0], m_ref[b][0]), f"split {split} stream {b} matches"
-            assert _kp_equal(o[b][0], o_ref[b][0]) and np.array_equal(o[b][1], o_ref[b][1]), f"split {split} stream {b}"
-    for b in (0, B // 2, B - 1):
-        k1, d1 = oracle_mod.extract(host[2, b])
-        k2, d2 = oracle_mod.extract(host[3, b])
-        assert _kp_equal(o_ref[b][0], k2) and np.array_equal(o_ref[b][1], d2), f"stream {b} extract"
-        prev = np.ascontiguousarray(np.stack([k1["x"], k1["y"]], 1).astype(np.float32))
-        nm, m12, _ = oracle_mod.search_for_initialization(k1, d1, k2, d2, w, h, prev, 100, 0.9, True)
-        assert m_ref[b][1] == nm and np.array_equal(m_ref[b][0], m12), f"stream {b} matches"
-
-
 MONO_EXTRAS = [(w, h, nf, B) for key, mode, w, h, nf, B, _ in bench.EXTRAS if mode == "mono"]
 
 
