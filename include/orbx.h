@@ -144,9 +144,10 @@ int orbx_extractor_split(orbx_extractor *ex, int parts);
  * on internal streams forked from and joined to the launch stream -- level 0's
  * FAST, quadtree and describe beside the resize chain and levels 1.. -- so
  * level 0's work overlaps the latency-bound resize chain.  on = 2, the deep
- * form: the side stream also takes FAST and quadtree of levels 1..E as soon as
- * the resize chain has produced them (E: environment ORBX_PIPE_EARLY, default
- * 2), so the rest of the chain runs beside them.  Outputs are identical in
+ * form: the side stream also takes FAST, quadtree and describe of levels 1..E
+ * as soon as the resize chain has produced them (E: environment
+ * ORBX_PIPE_EARLY, default 2; ORBX_PIPE_DESC=0 leaves their describe with the
+ * other levels'), so the rest of the chain runs beside them.  Outputs are identical in
  * every form.  on: 2 / 1 / 0 sets, -1 queries; returns the current setting.
  * Stage times (orbx_extractor_stage_times) cover the extractor stages only
  * with the pipeline off. */

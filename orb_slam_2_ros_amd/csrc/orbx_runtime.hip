@@ -157,8 +157,10 @@ struct orbx_extractor {
     // resize chain has produced them (ORBX_PIPE_EARLY, 1..nlevels - 2), and
     // whether their describe runs there too (ORBX_PIPE_DESC=1) rather than
     // with the other levels' at the end of the main stream
+    // (E = 2 with their describe there: VGA 467.9 k -> 484.5 k, FHD stereo 47.66 k -> 49.80 k on one box;
+    // E = 1 / 3 and the describe at the end measured lower, profiles/r06_ab_deep_pipeline.txt)
     int pipe_early = 2;
-    int pipe_desc = 0;
+    int pipe_desc = 1;
     bool pipe_ready = false;
     int split = 1;   // orbx_extractor_split / ORBX_SPLIT=2 turn it on
     hipStream_t part_stream[kMaxParts] = {};
