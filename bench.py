@@ -1165,7 +1165,10 @@ EXTRA_SPLIT = {"fhd_1920x1080": 1, "hd_1280x720": 1, "rgbd_fhd_1920x1080": 1, "s
 # Round 5, after the LDS-free resize (k_resize_d), on / off on one box: FHD mono 89.5-90.8 / 88.2-88.5 k,
 # HD 184.0 / 180.5-180.6 k, FHD stereo 45.6-45.7 / 44.0-44.1 k, FHD RGB-D 90.8-90.9 / 89.0-89.3 k; EuRoC
 # 148.0 / 161.0-162.3 k and KITTI 87.8-88.2 / 95.2-95.3 k stay off (profiles/r05_ab_pipeline_extras.txt)
-EXTRA_PIPE = {"fhd_1920x1080": 1, "hd_1280x720": 1, "stereo_fhd_1920x1080": 2, "rgbd_fhd_1920x1080": 1}
+# Round 6, the deep form (2) on one box (profiles/r06_ab_pipe_extras.txt), pipeline 0 / 1 / 2: FHD mono 92.3 / 94.9 /
+# 99.5 k, HD 188.2 / 192.3 / 197.9 k, FHD RGB-D 92.5 / 94.7 / 98.1 k frames/s; EuRoC 166.9 / 153.3 / 161.0 k and
+# KITTI 97.6 / 89.6 / 95.1 k pairs/s stay unpipelined
+EXTRA_PIPE = {"fhd_1920x1080": 2, "hd_1280x720": 2, "stereo_fhd_1920x1080": 2, "rgbd_fhd_1920x1080": 2}
 # Round 6, the deep level pipeline (2: the side stream also takes levels 1..2 as the resize chain
 # produces them, and their describe): VGA 467.9 k -> 484.5 k, FHD stereo 47.66 k -> 49.80 k pairs/s on
 # one box (profiles/r06_ab_deep_pipeline.txt)

@@ -2580,6 +2580,9 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 #ifndef ORBX_DESC_STAGE
 #define ORBX_DESC_STAGE 1   // 0: the generic wave_stage_rows
 #endif
+#ifndef ORBX_DESC_PKF32
+#define ORBX_DESC_PKF32 0   // 1: the sample offsets as packed f32 pairs (round 5's form; fewer, slower instructions)
+#endif
 // k_describe's 43 x 43 patch inside the level, staged with its column 0 at
 // patch column 2 (the keypoint at kDescKpCol = 23: the orientation disc in one
 // 32-column MFMA window): a row is 12 dwords from x0 - 2, unaligned loads
@@ -2873,7 +2876,15 @@ __global__ __launch_bounds__(kThreads, ORBX_DESC_WAVES) void k_describe(DevPlan 
     // cvRound by the 1.5 * 2^23 bias: the float add rounds to the nearest
     // integer, ties to even, and the bits are then 0x4B400000 + n (|n| < 2^22)
     constexpr float kRndBias = 12582912.f;
+#if ORBX_DESC_PKF32
     const f32x2 sc = {sa, ca}, rnd2 = {kRndBias, kRndBias};
+#else
+    // (wave-uniform, moved into VGPRs once: a VOP2 f32 op with an SGPR operand issues at half rate)
+    float sav, cav, rndv;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(sav) : "v"(sa));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(cav) : "v"(ca));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(rndv) : "v"(kRndBias));
+#endif
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         const uint32_t pw = (k >> 1) == 0 ? patq.x : (k >> 1) == 1 ? patq.y : (k >> 1) == 2 ? patq.z : patq.w;
@@ -2883,13 +2894,31 @@ __global__ __launch_bounds__(kThreads, ORBX_DESC_WAVES) void k_describe(DevPlan 
         // (written out: the compiler's own packing negates and moves pairs around)
         const f32x2 pxy = (k & 1) ? __builtin_amdgcn_cvt_pk_f32_fp8((int)pw, true)      // (x, y) of point k
                                   : __builtin_amdgcn_cvt_pk_f32_fp8((int)pw, false);
-        f32x2 rc, py2;
+        f32x2 rc;
+#if ORBX_DESC_PKF32
+        f32x2 py2;
         asm("v_pk_mul_f32 %0, %2, %3 op_sel_hi:[0,1]\n\t"               // (px sa, px ca)
             "v_pk_mul_f32 %1, %2, %3 op_sel:[1,1] op_sel_hi:[1,0]\n\t"  // (py ca, py sa)
             "v_pk_add_f32 %0, %0, %1 neg_hi:[0,1]\n\t"                  // (px sa + py ca, px ca - py sa)
             "v_pk_add_f32 %0, %0, %4"                                   // + (bias, bias)
             : "=&v"(rc), "=&v"(py2)
             : "v"(pxy), "v"(sc), "s"(rnd2));
+#else
+        // the same eight IEEE steps as unpacked VOP2 f32 ops on VGPR operands
+        // only (sa, ca and the bias held in VGPRs): ~2.2 cycles each where a
+        // packed f32 op takes ~8.4 and an SGPR operand makes any op ~4.2
+        {
+            float t0, t1, t2, t3;
+            asm("v_mul_f32 %0, %1, %2" : "=v"(t0) : "v"(pxy.x), "v"(sav));
+            asm("v_mul_f32 %0, %1, %2" : "=v"(t1) : "v"(pxy.y), "v"(cav));
+            asm("v_mul_f32 %0, %1, %2" : "=v"(t2) : "v"(pxy.x), "v"(cav));
+            asm("v_mul_f32 %0, %1, %2" : "=v"(t3) : "v"(pxy.y), "v"(sav));
+            asm("v_add_f32 %0, %1, %2" : "=v"(t0) : "v"(t0), "v"(t1));
+            asm("v_sub_f32 %0, %1, %2" : "=v"(t2) : "v"(t2), "v"(t3));
+            asm("v_add_f32 %0, %1, %2" : "=v"(rc.x) : "v"(t0), "v"(rndv));
+            asm("v_add_f32 %0, %1, %2" : "=v"(rc.y) : "v"(t2), "v"(rndv));
+        }
+#endif
         const uint32_t rb = __float_as_uint(rc.x), cb = __float_as_uint(rc.y);
         cbs[k] = (int)cb;
         // (__umul24 reads the low 24 bits of cb: 0x400000 + c, c in [-18, 18])
