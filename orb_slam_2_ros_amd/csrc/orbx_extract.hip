@@ -203,6 +203,12 @@ __device__ inline void xcd_block_2d(int &bx, int &by, uint32_t magic) {
 // VGPRs and branch per lane.
 __device__ inline int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 // set bits of m below this lane (v_mbcnt_lo / hi: two VALU, where a masked popcount takes four)
+// The lane mask of a comparison straight from its v_cmp (an SGPR pair).
+// __ballot of a bool that also steers a branch is lowered as v_cndmask 0 / 1
+// plus a second v_cmp; these keep the compare's own mask.
+__device__ inline uint64_t lanes_lt(int a, int b) { return __builtin_amdgcn_sicmp(a, b, 40); }   // ICMP_SLT
+__device__ inline uint64_t lanes_gt(int a, int b) { return __builtin_amdgcn_sicmp(a, b, 38); }   // ICMP_SGT
+
 __device__ inline int mbcnt64(uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
@@ -1249,8 +1255,8 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
                                          q[-3],      q[PS - 3],      q[2 * PS - 2],  q[3 * PS - 1]};
                 const int S = arc_score_bytes(reinterpret_cast<const int *>(pr), v);
                 const bool corner = live & (S > th);
+                const uint64_t m = lanes_lt(i0 + lane, nsurv) & lanes_gt(S, th);   // (the ballot of corner)
                 if (corner) scm[e + PS + 1] = (uint8_t)(S - 1);
-                const uint64_t m = __ballot(corner);
                 wave_lds_fence();   // all survivor reads of this chunk precede the in-place writes
                 if (corner) list[ncorner + mbcnt64(m)] = (uint16_t)e;
                 ncorner += __popcll(m);
@@ -1279,14 +1285,15 @@ __global__ __launch_bounds__(kThreads) void k_fast(DevPlan p, FrameBufs fb, int 
                           n4 = scm[si - PS + 1], n5 = scm[si + PS - 1], n6 = scm[si + PS], n7 = scm[si + PS + 1];
                 const int mx = max(max(max(n0, n1), max(n2, n3)), max(max(n4, n5), max(n6, n7)));
                 const bool keep = fin & (sv > mx);
-                const uint64_t mk = __ballot(keep);
+                const uint64_t mf = lanes_lt(i0 + lane, ncorner) & lanes_lt(e, ylast);   // (the ballots of fin, keep)
+                const uint64_t mk = mf & lanes_gt(sv, mx);
                 const int pk = base + mbcnt64(mk);
                 // the key from the offset: ey by the 24-bit reciprocal, then
                 // x | y << 12 = x0 + (y0 << 12) + e + ey (4096 - PS)
                 const int ey = (int)(__umul24((uint32_t)e, (uint32_t)pmag) >> 24);
                 if (keep && pk < c.cap) out[pk] = (uint32_t)(kxy0 + e + mul24u(ey, 4096 - PS)) | ((uint32_t)sv << 24);
                 base += __popcll(mk);
-                nfin += __popcll(__ballot(fin));
+                nfin += __popcll(mf);
             }
             // the waiting corners (one row: < 64) to the front
             npend = ncorner - nfin;
@@ -2970,7 +2977,7 @@ __global__ __launch_bounds__(kThreads, ORBX_DESC_WAVES) void k_describe(DevPlan 
     }
     uint64_t m[4];
 #pragma unroll
-    for (int grp = 0; grp < 4; ++grp) m[grp] = __ballot(val[2 * grp] < val[2 * grp + 1]);
+    for (int grp = 0; grp < 4; ++grp) m[grp] = lanes_lt(val[2 * grp], val[2 * grp + 1]);
     if (lane == 0) {
         ulonglong2 *dout = reinterpret_cast<ulonglong2 *>(fb.desc + kp_index * 32);
         dout[0] = make_ulonglong2(m[0], m[1]);
