@@ -2588,7 +2588,7 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 #define ORBX_DESC_STAGE 1   // 0: the generic wave_stage_rows
 #endif
 #ifndef ORBX_DESC_PKF32
-#define ORBX_DESC_PKF32 0   // 1: the sample offsets as packed f32 pairs (round 5's form; fewer, slower instructions)
+#define ORBX_DESC_PKF32 1   // 0: the sample offsets as eight unpacked VOP2 f32 ops (fewer issue cycles, more instructions; time neutral, profiles/r06_ab_desc_f32.txt)
 #endif
 // k_describe's 43 x 43 patch inside the level, staged with its column 0 at
 // patch column 2 (the keypoint at kDescKpCol = 23: the orientation disc in one
