@@ -946,7 +946,7 @@ def run_config(torch, dist, rank, world, dev, w, h, nfeatures, streams, steps, w
         # matcher launches overlap the other half's VALU-bound ones
         ex.split(split)
     if pipeline and stub is None and "ORBX_PIPELINE" not in os.environ:
-        ex.pipeline(1)   # level pipeline: on where it measured faster
+        ex.pipeline(pipeline)   # level pipeline (2: the deep form): on where it measured faster
     if overlap is None:
         overlap = MONO_OVERLAP
     if overlap and mode == "mono" and stub is None and "ORBX_OVERLAP_MATCH" not in os.environ:
