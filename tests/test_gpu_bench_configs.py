@@ -162,12 +162,17 @@ def test_mono_overlap_transitions(oracle_mod):
     assert all(x >= 0 for x in ex.stage_times()[:1])
     ex.set_profiling(False)
     step_and_check(7, tag="overlap again")
+    # the deep level pipeline on the same handle (and through the host call below, whose
+    # graph is captured with the pipeline off and must leave the setting as it was)
+    assert ex.pipeline(2) == 2
+    step_and_check(8, tag="deep pipeline")
     # the host-image call right after an overlapped step (no synchronisation between)
     ex.mono_step_device(fr[0].data_ptr(), w * h, w, B, 100, 0.9, True)
     img = np.ascontiguousarray(host[2, 5])
     kp, de = ex(img)
     ok, od = oracle_mod.extract(img)
     assert _kp_equal(kp, ok) and np.array_equal(de, od), "host call after an overlapped step"
+    assert ex.pipeline() == 2
     # and back to the device path, then a reserve at another batch size
     ex.mono_step_device(fr[0].data_ptr(), w * h, w, B, 100, 0.9, True)
     step_and_check(1, tag="after host call")
