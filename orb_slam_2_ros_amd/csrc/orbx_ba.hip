@@ -20,6 +20,8 @@
 //                      per set of active edges); k_ba_pairs merge walk for repeated observations
 //   k_ba_chol_lds      one workgroup: blocked dense Cholesky of the reduced camera system and
 //                      the solves (k_ba_chol beyond 128 unknowns)
+//   k_ba_chol_fast     fast mode: the augmented system on the FP64 matrix cores, tiles resident in
+//                      the accumulators, a division-free panel chain (<= 126 unknowns)
 //   k_ba_backsub_terms / k_ba_backsub
 //                      xl = Dinv (bl - sum_e B_e^T xp): per-edge terms, then thread per point
 //   k_ba_update        poses exp(dx) * T (SE3Quat), points += dx
@@ -41,6 +43,7 @@
 #include <cstring>
 #include <mutex>
 #include <set>
+#include <type_traits>
 #include <vector>
 
 #include "orbx_device.h"
@@ -1008,6 +1011,221 @@ __global__ __launch_bounds__(512) void k_ba_chol_lds(const double *S, int n, con
     if (clk && lane == 0) { clk[3] += __builtin_amdgcn_s_memtime() - c_t; clk[4] += 1; }
 }
 
+// Fast mode's factorisation (equal to rounding, not in the ordered mode's
+// term order): the augmented matrix [S b; b^T .] = L L^T, so row n of L is
+// y = L^-1 b and the forward solve comes free, right-looking in 16-column
+// panels on the FP64 matrix cores, with the latency chain cut to what the
+// panel needs:
+//  - L in LDS (16T rows of ld, T = tile rows of the n + 1 rows), the
+//    reciprocal diagonal in rinv[];
+//  - the 16x16 tiles right of the first panel live in the accumulators of
+//    waves 1..7 (tile t of the column-major lower-triangle order -> wave
+//    1 + t % 7, slot t / 7: a tile column's tiles sit in different waves), each
+//    receives panel J as four v_mfma_f64_16x16x4 with A = -L(rows of I, J),
+//    B = L(rows of K, J)^T, and goes to LDS once, when it is the next panel;
+//  - wave 0 factors a panel with its rows on the lanes (two a lane): a
+//    column's pivot by readlane, 1/sqrt as rsq plus one Newton step, the
+//    column scaled by it; the next column gets its term at once (readlane),
+//    the later ones a column later from an LDS broadcast -- no division or
+//    square root on the chain;
+//  - look-ahead: the owners of the next panel's tiles apply the panel first
+//    and store them, then wave 0 factors the next panel while the owners
+//    apply the panel to everything else: two barriers a panel;
+//  - L^T x = y column-sweep in wave 0 (x_k = s_k * rinv_k), 16 rows a block
+//    with the block's coefficients loaded together and no branch per step.
+// Measured (profiles/r06_ab_ba_chol_fast.txt): 85 -> ~50 us a factorisation,
+// fast local BA 5.0 -> 4.4 ms on one box.
+// ok = 0 if a pivot is not positive.  n <= kCholFastMax (n + 1 rows <= 128).
+constexpr int kCholFastMax = 126;
+typedef double orbx_f64x4 __attribute__((ext_vector_type(4)));
+__device__ inline double rsq_nr(double d) {   // 1/sqrt(d): the hardware estimate and one Newton step
+    const double r = __builtin_amdgcn_rsq(d);
+    const double h = 0.5 * d * r;
+    return fma(r, fma(-r, h, 0.5), r);
+}
+__device__ inline int chol_tile(int t, int T, int TC) {   // tile t (K >= 1, column-major) -> (I << 8) | K, or -1
+    for (int k = 1; k < TC; ++k) {
+        if (t < T - k) return ((k + t) << 8) | k;
+        t -= T - k;
+    }
+    return -1;
+}
+__global__ __launch_bounds__(512) void k_ba_chol_fast(const double *S, int n, const double *bs, double *x, int *ok,
+                                                      unsigned long long *clk) {
+    extern __shared__ double L[];   // 16T rows of ld, rinv (16T), the panel's column broadcasts (16 x 64)
+    __shared__ int bad;
+    constexpr int kSlots = 4;   // (T <= 8: at most 28 tiles right of the first panel, 4 a wave)
+    const int T = (n + 16) / 16, TC = (n + 15) / 16, R = 16 * T, ld = R + 1;
+    double *rinv = L + R * ld;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    // clk (diagnostics, ORBX_BA_CLOCKS): wave 0's cycles in load / factor / waits / backward solve
+    unsigned long long c_t = clk ? __builtin_amdgcn_s_memtime() : 0, c_f = 0;
+    // load: rows 0..n-1 of S's lower triangle, row n = b, zeros elsewhere
+    // (a wave's 16 rows: all 32 loads in flight, then the stores)
+    {
+        double v[16][2];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int r = w + 8 * i;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int c = lane + 64 * h;
+                v[i][h] = r < n ? (c <= r ? S[(int64_t)r * n + c] : 0.0) : (r == n && c < n ? bs[c] : 0.0);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                if (w + 8 * i < R && lane + 64 * h < R) L[(w + 8 * i) * ld + lane + 64 * h] = v[i][h];
+    }
+    if (tid == 0) bad = 0;
+    __syncthreads();
+    if (clk && tid == 0) { clk[0] += __builtin_amdgcn_s_memtime() - c_t; c_t = __builtin_amdgcn_s_memtime(); }
+    auto factor = [&](int J) {
+        const int k0 = 16 * J, q0 = k0 + lane, q1 = k0 + 64 + lane;
+        double p0[16], p1[16];
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            p0[m] = q0 < R ? L[q0 * ld + k0 + m] : 0.0;
+            p1[m] = q1 < R ? L[q1 * ld + k0 + m] : 0.0;
+        }
+        // Column m's terms reach column m + 1 at once (a readlane: the next
+        // pivot's chain) and columns m + 2.. one column later, from entries
+        // published to LDS and read back broadcast while the next pivot is
+        // worked out.  (Unpredicated: a lane's entries above the diagonal take
+        // finite garbage that only flows into its own upper entries, which are
+        // neither read back nor stored.)
+        // (Every lane publishes its entry: no exec-masked store.)
+        double *cb = rinv + R;
+        double c[16];
+        bool good = true;
+        double rl = 0.0;
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            if (k0 + m >= n) break;   // (uniform: the padding columns stay zero)
+            const double d = readlane_f64(p0[m], m);   // the pivot: row k0 + m is lane m's q0
+            good = good && d > 0;
+            const double r = rsq_nr(d);
+            rl = lane == m ? r : rl;
+            p0[m] = p0[m] * r;
+            p1[m] = p1[m] * r;
+            if (m + 1 < 16) {
+                const double a = readlane_f64(p0[m], m + 1);
+                p0[m + 1] = fma(-p0[m], a, p0[m + 1]);
+                p1[m + 1] = fma(-p1[m], a, p1[m + 1]);
+            }
+            double cn[16];
+            if (m + 2 < 16) {
+                cb[64 * m + lane] = p0[m];
+#pragma unroll
+                for (int jm = m + 2; jm < 16; ++jm) cn[jm] = cb[64 * m + jm];
+            }
+            if (m >= 1)
+#pragma unroll
+                for (int jm = m + 1; jm < 16; ++jm) {   // column m - 1's terms, read one column ago
+                    p0[jm] = fma(-p0[m - 1], c[jm], p0[jm]);
+                    p1[jm] = fma(-p1[m - 1], c[jm], p1[jm]);
+                }
+#pragma unroll
+            for (int jm = m + 2; jm < 16; ++jm) c[jm] = cn[jm];
+        }
+        if (!good && lane == 0) bad = 1;
+        if (lane < 16 && k0 + lane < n) rinv[k0 + lane] = rl;
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            if (k0 + m >= n) break;
+            if (q0 < R && q0 > k0 + m) L[q0 * ld + k0 + m] = p0[m];
+            if (q1 < R) L[q1 * ld + k0 + m] = p1[m];
+        }
+    };
+    // this wave's tiles and their accumulators (C[(l >> 4) + 4 r][l & 15] in element r)
+    int tI[kSlots], tK[kSlots];
+    orbx_f64x4 acc[kSlots];
+    const int fr = lane & 15, fk = lane >> 4;   // fragment row / k of the MFMA operands
+#pragma unroll
+    for (int s = 0; s < kSlots; ++s) {
+        const int tk = w > 0 ? chol_tile(w - 1 + 7 * s, T, TC) : -1;
+        tI[s] = tk >> 8;
+        tK[s] = tk < 0 ? -1 : tk & 255;
+        if (tK[s] >= 0)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[s][r] = L[(16 * tI[s] + fk + 4 * r) * ld + 16 * tK[s] + fr];
+    }
+    auto apply = [&](int s, int J) {   // panel J's terms into slot s
+        orbx_f64x4 c = acc[s];
+        const double *a = L + (16 * tI[s] + fr) * ld + 16 * J + fk, *b = L + (16 * tK[s] + fr) * ld + 16 * J + fk;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) c = __builtin_amdgcn_mfma_f64_16x16x4f64(-a[4 * q], b[4 * q], c, 0, 0, 0);
+        acc[s] = c;
+    };
+    if (w == 0) factor(0);
+    if (clk && tid == 0) { const unsigned long long t = __builtin_amdgcn_s_memtime(); c_f += t - c_t; }
+    __syncthreads();
+    for (int J = 0; J + 1 < TC && !bad; ++J) {
+#pragma unroll
+        for (int s = 0; s < kSlots; ++s)
+            if (tK[s] == J + 1) {   // the next panel's tiles: apply, store
+                apply(s, J);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) L[(16 * tI[s] + fk + 4 * r) * ld + 16 * tK[s] + fr] = acc[s][r];
+            }
+        __syncthreads();
+        if (w == 0) {
+            const unsigned long long c_w = clk ? __builtin_amdgcn_s_memtime() : 0;
+            factor(J + 1);
+            if (clk) c_f += __builtin_amdgcn_s_memtime() - c_w;
+        } else {
+#pragma unroll
+            for (int s = 0; s < kSlots; ++s)
+                if (tK[s] > J + 1) apply(s, J);
+        }
+        __syncthreads();
+    }
+    if (w != 0) return;
+    if (clk && lane == 0) {
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        clk[1] += t - c_t; clk[5] += c_f; c_t = t;
+    }
+    const bool good = !bad;
+    if (lane == 0) *ok = good;
+    if (!good) return;
+    // L^T x = y: lane owns rows lane and lane + 64; y = row n of L
+    const int i0 = lane, i1 = lane + 64, r0 = min(i0, n - 1), r1 = min(i1, n - 1);
+    // 16 rows a block from the bottom: the block's coefficients (zero for
+    // rows >= k) and reciprocals loaded together, then its steps from
+    // registers -- a step on the chain is readlane, multiply, FMA; x_k is kept
+    // aside
+    double s0 = i0 < n ? L[n * ld + i0] : 0.0, s1 = i1 < n ? L[n * ld + i1] : 0.0, x0 = 0.0, x1 = 0.0;
+    auto block = [&](int kb, auto hi_c) {   // rows kb..kb+15, all in one half (hi: rows 64..)
+        constexpr bool hi = decltype(hi_c)::value;
+        double a0[16], a1[16], rr[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {   // (a row past n - 1: r = 0, a no-op step)
+            const int k = min(kb + u, n - 1);
+            rr[u] = kb + u < n ? rinv[k] : 0.0;
+            a0[u] = i0 < k ? L[k * ld + r0] : 0.0;
+            a1[u] = i1 < k ? L[k * ld + r1] : 0.0;
+        }
+#pragma unroll
+        for (int u = 15; u >= 0; --u) {
+            const int k = kb + u;
+            const double xk = readlane_f64(hi ? s1 : s0, hi ? k - 64 : k) * rr[u];
+            if constexpr (hi) x1 = lane == k - 64 ? xk : x1;
+            else x0 = lane == k ? xk : x0;
+            s0 = fma(-a0[u], xk, s0);
+            s1 = fma(-a1[u], xk, s1);
+        }
+    };
+    for (int kb = (n - 1) & ~15; kb >= 0; kb -= 16) {   // (a block lies in one half: uniform branch per block)
+        if (kb >= 64) block(kb, std::true_type{});
+        else block(kb, std::false_type{});
+    }
+    if (i0 < n) x[i0] = x0;
+    if (i1 < n) x[i1] = x1;
+    if (clk && lane == 0) { clk[3] += __builtin_amdgcn_s_memtime() - c_t; clk[4] += 1; }
+}
+
 // the caller's edges as EdgeD (float -> double: exact) and the edge -> point list
 __global__ void k_ba_edges(const orbx_ba_edge *in, int ne, double th_mono, double th_stereo, EdgeD *out,
                            int32_t *epoint) {
@@ -1230,6 +1448,16 @@ unsigned long long *chol_clk() {
     return p;
 }
 
+// ORBX_BA_CHOL_FAST=0: fast mode factors with the ordered mode's kernel
+// (diagnostics, A/B)
+bool chol_fast_on() {
+    static const bool on = [] {
+        const char *e = std::getenv("ORBX_BA_CHOL_FAST");
+        return !e || std::atoi(e) != 0;
+    }();
+    return on;
+}
+
 class BA {
 public:
     BA(Graph &g, BAWs &ws) : g_(g), st_(ws.st), ws_(ws) {}
@@ -1290,7 +1518,10 @@ public:
     size_t span_ = 0;      // bytes from d_ok to the end of d_bl
     bool s_zero_ = false;  // d_S's non-pair blocks are zero
     int *h_ok = nullptr;
-    double *d_fsum = nullptr, *h_fsum = nullptr;   // fast mode's device-reduced readback (k_ba_fast_sums)
+    // fast mode's device-reduced readback (k_ba_fast_sums): written by the
+    // kernel straight into the pinned h_fsum (d_fsum = its device address),
+    // visible to the host at the stream synchronisation -- no copy a trial
+    double *d_fsum = nullptr, *h_fsum = nullptr;
     double *d_fpart = nullptr;                     // its per-workgroup partials
     unsigned *d_fcount = nullptr;                  // its finished-workgroup counter (zeroed by alloc, reset by the last)
     uint8_t *h_stage = nullptr;                // set_active's uploads: flags, then h_coffs_ | clist
@@ -1381,7 +1612,6 @@ int BA::alloc() {
     d_bl = carve<double>(p, 3 * np);
     span_ = (size_t)(p - reinterpret_cast<uint8_t *>(d_ok));
     d_cmap = carve<int32_t>(p, nf * np);
-    d_fsum = carve<double>(p, 4);
     d_fpart = carve<double>(p, 3 * kFastSumBlocks);
     d_fcount = carve<unsigned>(p, 4);
     d_db = carve<double>(p, 3 * np);
@@ -1405,6 +1635,7 @@ int BA::alloc() {
         h_bp = carve<double>(h, 6 * nf); h_bl = carve<double>(h, 3 * np);
         h_hpp = carve<double>(h, 36 * nf); h_hll = carve<double>(h, 9 * np);
         h_fsum = carve<double>(h, 8);   // [0, 4): errors / trial sums, [4, 8): read_diag's
+        if (hipHostGetDevicePointer(reinterpret_cast<void **>(&d_fsum), h_fsum, 0) != hipSuccess) return ORBX_EIO;
         h_stage = carve<uint8_t>(h, 2 * ne); h_coffs_ = carve<int32_t>(h, nf + 1 + ne);
         if ((size_t)(h - hbuf_) > hb) return ORBX_ENOMEM;
     }
@@ -1608,11 +1839,18 @@ int BA::solve_async(double lambda) {
         else
             hipLaunchKernelGGL((k_ba_stream_sums<6, false>), dim3(g.nf), dim3(kSumThreads), kSumLds, st_, d_rows,
                                d_coffs, d_bp, d_bs, 6, nullptr);
-        // (both modes factor with the same kernels: an unblocked parallel
-        // right-looking FMA factorisation, one barrier a column, measured 130 us
-        // against this blocked look-ahead kernel's 85 us at 120 unknowns --
-        // the per-column square root and reciprocal sit on the critical path)
-        if (n <= kCholLds) {
+        // (fast mode: the augmented-matrix MFMA factorisation, k_ba_chol_fast;
+        // the ordered mode keeps the oracle's term order in k_ba_chol_lds.  An
+        // unblocked parallel right-looking FMA factorisation, one barrier a
+        // column, measured 130 us against the look-ahead kernel's 85 us at 120
+        // unknowns: the per-column square root and division on the chain)
+        if (fast_ && n <= kCholFastMax && chol_fast_on()) {
+            const int R = 16 * ((n + 16) / 16), lb = 8 * (R * (R + 1) + R + 1024);
+            if (lb > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void *>(k_ba_chol_fast),
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize, lb) != hipSuccess)
+                return ORBX_EIO;
+            hipLaunchKernelGGL(k_ba_chol_fast, dim3(1), dim3(512), lb, st_, d_S, n, d_bs, d_x, d_ok, chol_clk());
+        } else if (n <= kCholLds) {
             const int lb = 8 * (n * (n + 1) + n);
             if (lb > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void *>(k_ba_chol_lds),
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, lb) != hipSuccess)
@@ -1648,7 +1886,7 @@ int BA::read_errors() {
     if (fast_) {
         hipLaunchKernelGGL(k_ba_fast_sums, dim3(kFastSumBlocks), dim3(kFastSumThreads), 0, st_, d_rho0, d_active, g_.ne,
                            nullptr, nullptr, nullptr, 0, 0, 0.0, nullptr, nullptr, 0, nullptr, 0, d_fpart, d_fcount, d_fsum);
-        return hipMemcpyAsync(h_fsum, d_fsum, 32, hipMemcpyDeviceToHost, st_) == hipSuccess ? ORBX_OK : ORBX_EIO;
+        return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
     }
     return (g_.ne && hipMemcpyAsync(h_rho0, d_rho0, 8 * (size_t)g_.ne, hipMemcpyDeviceToHost, st_) != hipSuccess)
                ? ORBX_EIO : ORBX_OK;
@@ -1658,8 +1896,8 @@ int BA::read_diag() {
     if (fast_) {   // (into slots of its own: read_errors' chi sum in h_fsum[0] stays whatever the order)
         hipLaunchKernelGGL(k_ba_fast_sums, dim3(kFastSumBlocks), dim3(kFastSumThreads), 0, st_, d_rho0, d_active, g_.ne,
                            nullptr, nullptr, nullptr, 0, 0, 0.0, nullptr, d_Hpp, g_.nf, d_Hll, g_.npt, d_fpart, d_fcount,
-                           d_fsum);
-        return hipMemcpyAsync(h_fsum + 4, d_fsum, 32, hipMemcpyDeviceToHost, st_) == hipSuccess ? ORBX_OK : ORBX_EIO;
+                           d_fsum + 4);
+        return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
     }
     if ((g_.nf && hipMemcpyAsync(h_hpp, d_Hpp, 8 * 36 * (size_t)g_.nf, hipMemcpyDeviceToHost, st_) != hipSuccess) ||
         (g_.npt && hipMemcpyAsync(h_hll, d_Hll, 8 * 9 * (size_t)g_.npt, hipMemcpyDeviceToHost, st_) != hipSuccess))
@@ -1674,7 +1912,7 @@ int BA::read_trial(double lambda) {
         const int n = 6 * g_.nf, m = n + 3 * g_.npt;
         hipLaunchKernelGGL(k_ba_fast_sums, dim3(kFastSumBlocks), dim3(kFastSumThreads), 0, st_, d_rho0, d_active, g_.ne,
                            d_x, d_bp, d_bl, n, m, lambda, d_ok, nullptr, 0, nullptr, 0, d_fpart, d_fcount, d_fsum);
-        return hipMemcpyAsync(h_fsum, d_fsum, 32, hipMemcpyDeviceToHost, st_) == hipSuccess ? ORBX_OK : ORBX_EIO;
+        return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
     }
     return hipMemcpyAsync(h_ok, d_ok, span_, hipMemcpyDeviceToHost, st_) == hipSuccess ? ORBX_OK : ORBX_EIO;
 }
