@@ -347,7 +347,7 @@ __device__ inline double cof(const double *m, int i, int j) {
 }
 
 __global__ void k_ba_point(const double *Hll, const double *bl, int npt, double lambda, double *dinv_out,
-                           double *db_out) {
+                           double *db_out, double *lu_out) {
     const int pt = blockIdx.x * blockDim.x + threadIdx.x;
     if (pt >= npt) return;
     double m[9];
@@ -365,6 +365,19 @@ __global__ void k_ba_point(const double *Hll, const double *bl, int npt, double 
         double acc = 0;
         for (int c = 0; c < 3; ++c) acc = acc + D[3 * r + c] * bl[3 * (int64_t)pt + c];
         db_out[3 * (int64_t)pt + r] = acc;
+    }
+    if (lu_out) {   // (fast mode's dense Schur product) m = L L^T: L^-1 (lower, six) and u = L^-1 bl
+        const double l00 = sqrt(m[0]), l10 = m[3] / l00, l20 = m[6] / l00;
+        const double l11 = sqrt(m[4] - l10 * l10), l21 = (m[7] - l20 * l10) / l11;
+        const double l22 = sqrt(m[8] - l20 * l20 - l21 * l21);
+        const double i00 = 1.0 / l00, i11 = 1.0 / l11, i22 = 1.0 / l22;
+        const double i10 = -l10 * i00 * i11, i21 = -l21 * i11 * i22, i20 = -(l20 * i00 + l21 * i10) * i22;
+        const double *b = bl + 3 * (int64_t)pt;
+        double *o = lu_out + 9 * (int64_t)pt;
+        o[0] = i00; o[1] = i10; o[2] = i11; o[3] = i20; o[4] = i21; o[5] = i22;
+        o[6] = i00 * b[0];
+        o[7] = i10 * b[0] + i11 * b[1];
+        o[8] = i20 * b[0] + i21 * b[1] + i22 * b[2];
     }
 }
 
@@ -652,6 +665,147 @@ __global__ __launch_bounds__(kSumThreads) void k_ba_pairs_sum(const int2 *pairs,
     const int n = 6 * nf;
     S[(int64_t)(6 * i1 + r) * n + 6 * i2 + c] = acc;
     S[(int64_t)(6 * i2 + c) * n + 6 * i1 + r] = acc;
+}
+
+typedef double orbx_f64x4 __attribute__((ext_vector_type(4)));
+
+// Fast mode's Schur complement and reduced right-hand side as one dense
+// product on the FP64 matrix cores (round 6; each (camera, point) observed at
+// most once, use_map).  With D_p = Hll_p + lambda I = L_p L_p^T (k_ba_point's
+// lu: L_p^-1 and u_p = L_p^-1 bl_p), S = Hpp + lambda I - sum_p B_p D_p^-1 B_p^T
+// = Hpp + lambda I - W^T W and bs = bp - W^T u, with W's row 3p + k the k-th
+// row of L_p^-1 B_p^T (6 columns per free camera).  One K x CT operand M holds
+// W (columns [0, 16 TCe)), u (column 16 TCe) and zeros, K = 3 npt padded to
+// whole chunks of kSchurKC rows; M^T M's needed 16x16 tiles -- S's lower
+// triangle and the u column -- go in 2x2 tile blocks (a workgroup of four
+// waves per (block, chunk), each wave a quarter of the chunk, four
+// independent accumulators), the chunk partials summed in chunk order
+// (deterministic).  It replaces the shared-point lists, the per-pair sums and
+// the per-edge B D^-1 products; equal to rounding.
+constexpr int kSchurKC = 512;
+__global__ void k_ba_schur_ops(int npt, int nf, int CT, int ucol, int kp, const int32_t *cmap, const int32_t *clist,
+                               const EdgeOut *eo, const double *lu, double *M) {
+    const int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (idx >= (int64_t)kp * CT) return;
+    const int k = (int)(idx / CT), col = (int)(idx - (int64_t)k * CT);
+    const int p = k / 3, kk = k - 3 * p;
+    double v = 0.0;
+    if (p < npt) {
+        const double *l = lu + 9 * (int64_t)p;   // L^-1 as m00, m10, m11, m20, m21, m22; then u
+        if (col < 6 * nf) {
+            const int f = col / 6, r = col - 6 * f;
+            const int pos = cmap[(int64_t)f * npt + p];
+            if (pos >= 0) {
+                const double *h = eo[clist[pos]].hpl + 3 * r;   // row r of B (6 x 3)
+                v = kk == 0 ? l[0] * h[0]
+                  : kk == 1 ? fma(l[2], h[1], l[1] * h[0])
+                            : fma(l[5], h[2], fma(l[4], h[1], l[3] * h[0]));
+            }
+        } else if (col == ucol) {
+            v = l[6 + kk];
+        }
+    }
+    M[idx] = v;
+}
+__device__ inline void schur_block(int blk, int h, int &I0, int &J0) {   // 2x2 tile block -> its first tiles
+    const int nl = h * (h + 1) / 2;
+    int ip = 0, jp = blk;
+    if (blk < nl) {
+        while (jp > ip) { jp -= ip + 1; ++ip; }
+    } else {
+        ip = blk - nl;
+        jp = h;
+    }
+    I0 = 2 * ip;
+    J0 = 2 * jp;
+}
+__global__ __launch_bounds__(256) void k_ba_schur_mfma(const double *M, int CT, int h, double *part) {
+    __shared__ double red[4][4 * 256];
+    const int blk = blockIdx.x, ch = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    int I0, J0;
+    schur_block(blk, h, I0, J0);
+    const int fr = lane & 15, fk = lane >> 4;
+    const double *base = M + (int64_t)(ch * kSchurKC + w * (kSchurKC / 4) + fk) * CT + fr;
+    const double *a0 = base + 16 * I0, *a1 = a0 + 16, *b0 = base + 16 * J0, *b1 = b0 + 16;
+    orbx_f64x4 c00 = {0.0, 0.0, 0.0, 0.0}, c01 = c00, c10 = c00, c11 = c00;
+    for (int s = 0; s < kSchurKC / 16; s += 4) {   // four K-steps' operands in flight
+        double A0[4], A1[4], B0[4], B1[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t o = (int64_t)(4 * (s + u)) * CT;
+            A0[u] = a0[o]; A1[u] = a1[o]; B0[u] = b0[o]; B1[u] = b1[o];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            c00 = __builtin_amdgcn_mfma_f64_16x16x4f64(A0[u], B0[u], c00, 0, 0, 0);
+            c01 = __builtin_amdgcn_mfma_f64_16x16x4f64(A0[u], B1[u], c01, 0, 0, 0);
+            c10 = __builtin_amdgcn_mfma_f64_16x16x4f64(A1[u], B0[u], c10, 0, 0, 0);
+            c11 = __builtin_amdgcn_mfma_f64_16x16x4f64(A1[u], B1[u], c11, 0, 0, 0);
+        }
+    }
+    // (tile q = 2 (I - I0) + (J - J0); element 4 lane + r: row (l >> 4) + 4 r, column l & 15)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        red[w][0 * 256 + 4 * lane + r] = c00[r];
+        red[w][1 * 256 + 4 * lane + r] = c01[r];
+        red[w][2 * 256 + 4 * lane + r] = c10[r];
+        red[w][3 * 256 + 4 * lane + r] = c11[r];
+    }
+    __syncthreads();
+    double *o = part + ((int64_t)ch * gridDim.x + blk) * 1024;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int e = tid + 256 * q;
+        o[e] = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+    }
+}
+// S's lower triangle = Hpp (+ lambda) on the diagonal blocks - (W^T W), and
+// bs = bp - W^T u, the chunk partials added in chunk order
+__global__ void k_ba_schur_sum(const double *part, int nch, int nblk, int h, const double *Hpp, const double *bp,
+                               double lambda, int n, double *S, double *bs) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= n * n + n) return;
+    int row, col;
+    if (idx < n * n) {
+        row = idx / n;
+        col = idx - row * n;
+        if (col > row) return;
+    } else {
+        row = idx - n * n;
+        col = -1;
+    }
+    const int I = row >> 4, ri = row & 15;
+    int blk, q, cj;
+    if (col >= 0) {
+        const int J = col >> 4;
+        blk = (I >> 1) * ((I >> 1) + 1) / 2 + (J >> 1);
+        q = 2 * (I & 1) + (J & 1);
+        cj = col & 15;
+    } else {
+        blk = h * (h + 1) / 2 + (I >> 1);
+        q = 2 * (I & 1);
+        cj = 0;
+    }
+    const int64_t off = 256 * q + 4 * (16 * (ri & 3) + cj) + (ri >> 2);
+    double sum = 0.0;
+    int c = 0;
+    for (; c + 4 <= nch; c += 4) {   // (four independent loads, added in chunk order)
+        const double v0 = part[((int64_t)c * nblk + blk) * 1024 + off], v1 = part[((int64_t)(c + 1) * nblk + blk) * 1024 + off],
+                     v2 = part[((int64_t)(c + 2) * nblk + blk) * 1024 + off], v3 = part[((int64_t)(c + 3) * nblk + blk) * 1024 + off];
+        sum = (((sum + v0) + v1) + v2) + v3;
+    }
+    for (; c < nch; ++c) sum += part[((int64_t)c * nblk + blk) * 1024 + off];
+    if (col < 0) {
+        bs[row] = bp[row] - sum;
+        return;
+    }
+    const int i = row / 6, j = col / 6;
+    double acc = 0.0;
+    if (i == j) {
+        acc = Hpp[36 * (int64_t)i + 6 * (row - 6 * i) + (col - 6 * j)];
+        if (row == col) acc = acc + lambda;
+    }
+    S[idx] = acc - sum;
 }
 
 // out[v] = (minus[v] -) the ordered sum of the vertex's rows; fields [0, na)
@@ -1037,7 +1191,6 @@ __global__ __launch_bounds__(512) void k_ba_chol_lds(const double *S, int n, con
 // fast local BA 5.0 -> 4.4 ms on one box.
 // ok = 0 if a pivot is not positive.  n <= kCholFastMax (n + 1 rows <= 128).
 constexpr int kCholFastMax = 126;
-typedef double orbx_f64x4 __attribute__((ext_vector_type(4)));
 __device__ inline double rsq_nr(double d) {   // 1/sqrt(d): the hardware estimate and one Newton step
     const double r = __builtin_amdgcn_rsq(d);
     const double h = 0.5 * d * r;
@@ -1448,13 +1601,19 @@ unsigned long long *chol_clk() {
     return p;
 }
 
-// ORBX_BA_CHOL_FAST=0: fast mode factors with the ordered mode's kernel
-// (diagnostics, A/B)
+// ORBX_BA_CHOL_FAST=0: fast mode factors with the ordered mode's kernel;
+// ORBX_BA_DENSE_SCHUR=0: fast mode's Schur pairs as shared-point lists + pair
+// sums, as the ordered mode's (diagnostics, A/B)
+bool env_on(const char *name) {
+    const char *e = std::getenv(name);
+    return !e || std::atoi(e) != 0;
+}
 bool chol_fast_on() {
-    static const bool on = [] {
-        const char *e = std::getenv("ORBX_BA_CHOL_FAST");
-        return !e || std::atoi(e) != 0;
-    }();
+    static const bool on = env_on("ORBX_BA_CHOL_FAST");
+    return on;
+}
+bool dense_schur_on() {
+    static const bool on = env_on("ORBX_BA_DENSE_SCHUR");
     return on;
 }
 
@@ -1504,6 +1663,11 @@ public:
     int *d_ok = nullptr;
     int32_t *d_cmap = nullptr;   // free camera x point -> position in its usable list (-1)
     bool use_map = false;        // every (camera, point) observed at most once
+    // fast mode's dense Schur product (k_ba_schur_*): per-point L^-1 and u,
+    // the operand M (kp_ x ct_), the chunk partials of the 2x2 tile blocks
+    double *d_lu = nullptr, *d_M = nullptr, *d_spart = nullptr;
+    int schur_ct_ = 0, schur_ucol_ = 0, schur_kp_ = 0, schur_nch_ = 0, schur_h_ = 0, schur_nblk_ = 0;
+    bool dense() const { return fast_ && use_map && dense_schur_on(); }
     std::vector<uint8_t> act_;
     std::vector<int32_t> cv_offs_, cv_list_;   // all edges per free camera (reduce), edge order
     double *d_rho0 = nullptr;                  // rho[0] per edge, contiguous
@@ -1526,6 +1690,19 @@ public:
     unsigned *d_fcount = nullptr;                  // its finished-workgroup counter (zeroed by alloc, reset by the last)
     uint8_t *h_stage = nullptr;                // set_active's uploads: flags, then h_coffs_ | clist
     int32_t *h_coffs_ = nullptr;
+    size_t schur_bytes() {   // (fast mode) sizes the dense Schur product's buffers
+        schur_ct_ = schur_ucol_ = schur_kp_ = schur_nch_ = schur_h_ = schur_nblk_ = 0;
+        if (!fast_ || !g_.nf || !dense_schur_on()) return 0;
+        const int tce = 2 * ((6 * g_.nf + 31) / 32);   // tile columns of W, even
+        schur_h_ = tce / 2;
+        schur_ucol_ = 16 * tce;
+        schur_ct_ = 16 * (tce + 2);                     // + the u tile and a zero tile (its block's pair)
+        schur_nch_ = std::max((3 * g_.npt + kSchurKC - 1) / kSchurKC, 1);
+        schur_kp_ = schur_nch_ * kSchurKC;
+        schur_nblk_ = schur_h_ * (schur_h_ + 1) / 2 + schur_h_;
+        return 8 * (9 * (size_t)std::max(g_.npt, 1) + (size_t)schur_kp_ * schur_ct_ +
+                    (size_t)schur_nch_ * schur_nblk_ * 1024) + 256 * 3;
+    }
 };
 
 int BA::alloc() {
@@ -1579,7 +1756,8 @@ int BA::alloc() {
                          8 * ne * 6 + sizeof(EdgeOut) * ne + 4 * (nf + 1 + ne + np + 1 + ne + ne + nf + 1 + ne) +
                          sizeof(int2) * std::max(npairs, 1) + 8 * (36 * nf + 6 * nf + 9 * np + 3 * np + 9 * np +
                                                                    18 * ne + 6 * ne + n * n + n + n + 3 * np) +
-                         4 * nf * np + 8 * ne + 8 * 3 * np + 8 * 42 * ne + sizeof(orbx_ba_edge) * ne + 256 * 6;
+                         4 * nf * np + 8 * ne + 8 * 3 * np + 8 * 42 * ne + sizeof(orbx_ba_edge) * ne + 256 * 6 +
+                         schur_bytes();
     if (ws_.cap < bytes) {
         (void)hipStreamSynchronize(st_);
         if (ws_.dev) (void)hipFree(ws_.dev);
@@ -1612,6 +1790,11 @@ int BA::alloc() {
     d_bl = carve<double>(p, 3 * np);
     span_ = (size_t)(p - reinterpret_cast<uint8_t *>(d_ok));
     d_cmap = carve<int32_t>(p, nf * np);
+    if (schur_ct_) {
+        d_lu = carve<double>(p, 9 * np);
+        d_M = carve<double>(p, (size_t)schur_kp_ * schur_ct_);
+        d_spart = carve<double>(p, (size_t)schur_nch_ * schur_nblk_ * 1024);
+    }
     d_fpart = carve<double>(p, 3 * kFastSumBlocks);
     d_fcount = carve<unsigned>(p, 4);
     d_db = carve<double>(p, 3 * np);
@@ -1727,7 +1910,7 @@ void BA::set_active(const std::vector<uint8_t> &act) {
         (void)hipMemsetAsync(d_cmap, 0xFF, 4 * (size_t)g.nf * g.npt, st_);
         hipLaunchKernelGGL(k_ba_cmap, dim3(g.nf), dim3(256), 0, st_, d_coffs, d_clist, d_epoint, g.npt, d_cmap);
     }
-    if (npairs > 0) {   // the pairs' shared-point lists: count, scan, fill
+    if (npairs > 0 && !dense()) {   // the pairs' shared-point lists: count, scan, fill
         hipLaunchKernelGGL(k_ba_pair_matches, dim3((npairs + 3) / 4), dim3(256), 0, st_, d_pairs, npairs, d_coffs,
                            d_clist, d_epoint, d_cmap, g.npt, nullptr, d_mcnt, nullptr);
         hipLaunchKernelGGL(k_ba_scan_counts, dim3(1), dim3(1024), 0, st_, d_mcnt, npairs, d_moffs);
@@ -1806,14 +1989,23 @@ int BA::solve_async(double lambda) {
         s_zero_ = true;
     }
     if (!g.nf && hipMemsetAsync(d_ok, 0xFF, 4, st_) != hipSuccess) return ORBX_EIO;   // (nothing to factor: ok)
+    const bool dn = g.nf && dense();
     if (g.npt) {
         hipLaunchKernelGGL(k_ba_point, dim3((g.npt + 255) / 256), dim3(256), 0, st_, d_Hll, d_bl, g.npt, lambda, d_dinv,
-                           d_db);
-        if (g.ne)
+                           d_db, dn ? d_lu : nullptr);
+        if (g.ne && !dn)
             hipLaunchKernelGGL(k_ba_point_edges, dim3((g.ne + 63) / 64), dim3(64), 0, st_, d_eo, d_epoint, d_usable,
                                g.ne, d_dinv, d_db, d_bdinv, d_bdb);
     }
-    if (g.nf) {
+    if (dn) {   // S and bs from one dense product (k_ba_schur_*)
+        const int64_t tot = (int64_t)schur_kp_ * schur_ct_;
+        hipLaunchKernelGGL(k_ba_schur_ops, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st_, g.npt, g.nf,
+                           schur_ct_, schur_ucol_, schur_kp_, d_cmap, d_clist, d_eo, d_lu, d_M);
+        hipLaunchKernelGGL(k_ba_schur_mfma, dim3(schur_nblk_, schur_nch_), dim3(256), 0, st_, d_M, schur_ct_,
+                           schur_h_, d_spart);
+        hipLaunchKernelGGL(k_ba_schur_sum, dim3((n * n + n + 255) / 256), dim3(256), 0, st_, d_spart, schur_nch_,
+                           schur_nblk_, schur_h_, d_Hpp, d_bp, lambda, n, d_S, d_bs);
+    } else if (g.nf) {
         if (use_map) {
             const int64_t nterms = 36 * nmatch_;
             if (nterms)
@@ -1839,6 +2031,8 @@ int BA::solve_async(double lambda) {
         else
             hipLaunchKernelGGL((k_ba_stream_sums<6, false>), dim3(g.nf), dim3(kSumThreads), kSumLds, st_, d_rows,
                                d_coffs, d_bp, d_bs, 6, nullptr);
+    }
+    if (g.nf) {
         // (fast mode: the augmented-matrix MFMA factorisation, k_ba_chol_fast;
         // the ordered mode keeps the oracle's term order in k_ba_chol_lds.  An
         // unblocked parallel right-looking FMA factorisation, one barrier a
