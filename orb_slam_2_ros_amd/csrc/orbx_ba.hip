@@ -1173,22 +1173,24 @@ __global__ __launch_bounds__(512) void k_ba_chol_lds(const double *S, int n, con
 //  - L in LDS (16T rows of ld, T = tile rows of the n + 1 rows), the
 //    reciprocal diagonal in rinv[];
 //  - the 16x16 tiles right of the first panel live in the accumulators of
-//    waves 1..7 (tile t of the column-major lower-triangle order -> wave
-//    1 + t % 7, slot t / 7: a tile column's tiles sit in different waves), each
-//    receives panel J as four v_mfma_f64_16x16x4 with A = -L(rows of I, J),
-//    B = L(rows of K, J)^T, and goes to LDS once, when it is the next panel;
-//  - wave 0 factors a panel with its rows on the lanes (two a lane): a
-//    column's pivot by readlane, 1/sqrt as rsq plus one Newton step, the
-//    column scaled by it; the next column gets its term at once (readlane),
-//    the later ones a column later from an LDS broadcast -- no division or
-//    square root on the chain;
+//    waves 3..7 (tile t of the column-major lower-triangle order -> wave
+//    3 + t % 5, slot t / 5), each receives panel J as four
+//    v_mfma_f64_16x16x4 with A = -L(rows of I, J), B = L(rows of K, J)^T,
+//    and goes to LDS once, when it is the next panel;
+//  - waves 0..2 factor a panel, rows on the lanes: each holds the diagonal
+//    block in lanes 0..15 and a third of the rows below in lanes 16..63, and
+//    runs the same pivot chain -- a column's pivot by readlane, 1/sqrt as rsq
+//    plus one Newton step, the column scaled by it; the next column gets its
+//    term at once (readlane), the later ones a column later from an LDS
+//    broadcast -- no division, square root or exchange between waves;
 //  - look-ahead: the owners of the next panel's tiles apply the panel first
-//    and store them, then wave 0 factors the next panel while the owners
+//    and store them, then waves 0..2 factor the next panel while the owners
 //    apply the panel to everything else: two barriers a panel;
 //  - L^T x = y column-sweep in wave 0 (x_k = s_k * rinv_k), 16 rows a block
 //    with the block's coefficients loaded together and no branch per step.
-// Measured (profiles/r06_ab_ba_chol_fast.txt): 85 -> ~50 us a factorisation,
-// fast local BA 5.0 -> 4.4 ms on one box.
+// Measured (profiles/r06_ab_ba_chol_fast.txt, r06_ab_ba_chol_3w.txt): 85 ->
+// 42 us a factorisation with wave 0 factoring alone, fast local BA 5.0 ->
+// 4.2 ms on one box; then the three factor waves.
 // ok = 0 if a pivot is not positive.  n <= kCholFastMax (n + 1 rows <= 128).
 constexpr int kCholFastMax = 126;
 __device__ inline double rsq_nr(double d) {   // 1/sqrt(d): the hardware estimate and one Newton step
@@ -1205,9 +1207,9 @@ __device__ inline int chol_tile(int t, int T, int TC) {   // tile t (K >= 1, col
 }
 __global__ __launch_bounds__(512) void k_ba_chol_fast(const double *S, int n, const double *bs, double *x, int *ok,
                                                       unsigned long long *clk) {
-    extern __shared__ double L[];   // 16T rows of ld, rinv (16T), the panel's column broadcasts (16 x 64)
+    extern __shared__ double L[];   // 16T rows of ld, rinv (16T), the factor waves' column broadcasts (3 x 16 x 64)
     __shared__ int bad;
-    constexpr int kSlots = 4;   // (T <= 8: at most 28 tiles right of the first panel, 4 a wave)
+    constexpr int kSlots = 6;   // (T <= 8: at most 28 tiles right of the first panel, 6 a wave over waves 3..7)
     const int T = (n + 16) / 16, TC = (n + 15) / 16, R = 16 * T, ld = R + 1;
     double *rinv = L + R * ld;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1235,38 +1237,37 @@ __global__ __launch_bounds__(512) void k_ba_chol_fast(const double *S, int n, co
     if (tid == 0) bad = 0;
     __syncthreads();
     if (clk && tid == 0) { clk[0] += __builtin_amdgcn_s_memtime() - c_t; c_t = __builtin_amdgcn_s_memtime(); }
+    // Waves 0..2 factor a panel together, each on its own rows and with no
+    // exchange: lanes 0..15 hold the panel's diagonal block (the same rows in
+    // all three, so each wave runs the same pivot chain), lanes 16..63 of wave
+    // f the rows k0 + 48 f + lane below it -- a third of the row updates each.
     auto factor = [&](int J) {
-        const int k0 = 16 * J, q0 = k0 + lane, q1 = k0 + 64 + lane;
-        double p0[16], p1[16];
+        const int k0 = 16 * J, q = lane < 16 ? k0 + lane : k0 + 48 * w + lane;
+        double p0[16];
 #pragma unroll
-        for (int m = 0; m < 16; ++m) {
-            p0[m] = q0 < R ? L[q0 * ld + k0 + m] : 0.0;
-            p1[m] = q1 < R ? L[q1 * ld + k0 + m] : 0.0;
-        }
+        for (int m = 0; m < 16; ++m) p0[m] = q < R ? L[q * ld + k0 + m] : 0.0;
         // Column m's terms reach column m + 1 at once (a readlane: the next
         // pivot's chain) and columns m + 2.. one column later, from entries
         // published to LDS and read back broadcast while the next pivot is
         // worked out.  (Unpredicated: a lane's entries above the diagonal take
         // finite garbage that only flows into its own upper entries, which are
-        // neither read back nor stored.)
-        // (Every lane publishes its entry: no exec-masked store.)
-        double *cb = rinv + R;
+        // neither read back nor stored.)  Every lane publishes its entry (no
+        // exec-masked store), into its wave's own 16 x 64 buffer.
+        double *cb = rinv + R + 1024 * w;
         double c[16];
         bool good = true;
         double rl = 0.0;
 #pragma unroll
         for (int m = 0; m < 16; ++m) {
             if (k0 + m >= n) break;   // (uniform: the padding columns stay zero)
-            const double d = readlane_f64(p0[m], m);   // the pivot: row k0 + m is lane m's q0
+            const double d = readlane_f64(p0[m], m);   // the pivot: row k0 + m is lane m's
             good = good && d > 0;
             const double r = rsq_nr(d);
             rl = lane == m ? r : rl;
             p0[m] = p0[m] * r;
-            p1[m] = p1[m] * r;
             if (m + 1 < 16) {
                 const double a = readlane_f64(p0[m], m + 1);
                 p0[m + 1] = fma(-p0[m], a, p0[m + 1]);
-                p1[m + 1] = fma(-p1[m], a, p1[m + 1]);
             }
             double cn[16];
             if (m + 2 < 16) {
@@ -1276,20 +1277,18 @@ __global__ __launch_bounds__(512) void k_ba_chol_fast(const double *S, int n, co
             }
             if (m >= 1)
 #pragma unroll
-                for (int jm = m + 1; jm < 16; ++jm) {   // column m - 1's terms, read one column ago
-                    p0[jm] = fma(-p0[m - 1], c[jm], p0[jm]);
-                    p1[jm] = fma(-p1[m - 1], c[jm], p1[jm]);
-                }
+                for (int jm = m + 1; jm < 16; ++jm) p0[jm] = fma(-p0[m - 1], c[jm], p0[jm]);   // column m - 1's terms
 #pragma unroll
             for (int jm = m + 2; jm < 16; ++jm) c[jm] = cn[jm];
         }
-        if (!good && lane == 0) bad = 1;
-        if (lane < 16 && k0 + lane < n) rinv[k0 + lane] = rl;
+        if (w == 0) {
+            if (!good && lane == 0) bad = 1;
+            if (lane < 16 && k0 + lane < n) rinv[k0 + lane] = rl;
+        }
 #pragma unroll
         for (int m = 0; m < 16; ++m) {
             if (k0 + m >= n) break;
-            if (q0 < R && q0 > k0 + m) L[q0 * ld + k0 + m] = p0[m];
-            if (q1 < R) L[q1 * ld + k0 + m] = p1[m];
+            if (q < R && (lane < 16 ? w == 0 && q > k0 + m : true)) L[q * ld + k0 + m] = p0[m];
         }
     };
     // this wave's tiles and their accumulators (C[(l >> 4) + 4 r][l & 15] in element r)
@@ -1298,7 +1297,7 @@ __global__ __launch_bounds__(512) void k_ba_chol_fast(const double *S, int n, co
     const int fr = lane & 15, fk = lane >> 4;   // fragment row / k of the MFMA operands
 #pragma unroll
     for (int s = 0; s < kSlots; ++s) {
-        const int tk = w > 0 ? chol_tile(w - 1 + 7 * s, T, TC) : -1;
+        const int tk = w >= 3 ? chol_tile(w - 3 + 5 * s, T, TC) : -1;
         tI[s] = tk >> 8;
         tK[s] = tk < 0 ? -1 : tk & 255;
         if (tK[s] >= 0)
@@ -1312,7 +1311,7 @@ __global__ __launch_bounds__(512) void k_ba_chol_fast(const double *S, int n, co
         for (int q = 0; q < 4; ++q) c = __builtin_amdgcn_mfma_f64_16x16x4f64(-a[4 * q], b[4 * q], c, 0, 0, 0);
         acc[s] = c;
     };
-    if (w == 0) factor(0);
+    if (w < 3) factor(0);
     if (clk && tid == 0) { const unsigned long long t = __builtin_amdgcn_s_memtime(); c_f += t - c_t; }
     __syncthreads();
     for (int J = 0; J + 1 < TC && !bad; ++J) {
@@ -1324,7 +1323,7 @@ __global__ __launch_bounds__(512) void k_ba_chol_fast(const double *S, int n, co
                 for (int r = 0; r < 4; ++r) L[(16 * tI[s] + fk + 4 * r) * ld + 16 * tK[s] + fr] = acc[s][r];
             }
         __syncthreads();
-        if (w == 0) {
+        if (w < 3) {
             const unsigned long long c_w = clk ? __builtin_amdgcn_s_memtime() : 0;
             factor(J + 1);
             if (clk) c_f += __builtin_amdgcn_s_memtime() - c_w;
@@ -2039,7 +2038,7 @@ int BA::solve_async(double lambda) {
         // column, measured 130 us against the look-ahead kernel's 85 us at 120
         // unknowns: the per-column square root and division on the chain)
         if (fast_ && n <= kCholFastMax && chol_fast_on()) {
-            const int R = 16 * ((n + 16) / 16), lb = 8 * (R * (R + 1) + R + 1024);
+            const int R = 16 * ((n + 16) / 16), lb = 8 * (R * (R + 1) + R + 3 * 1024);
             if (lb > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void *>(k_ba_chol_fast),
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, lb) != hipSuccess)
                 return ORBX_EIO;
