@@ -1579,7 +1579,7 @@ bool grow_dev(T *&p, size_t &cap, size_t need) {
     return true;
 }
 
-// ORBX_BA_CLOCKS: k_ba_chol_lds phase cycles, summed over the process and
+// ORBX_BA_CLOCKS: k_ba_chol_lds / k_ba_chol_fast phase cycles, summed over the process and
 // printed at exit (diagnostics)
 unsigned long long *chol_clk() {
     static unsigned long long *p = nullptr;
@@ -1590,7 +1590,7 @@ unsigned long long *chol_clk() {
             std::memset(p, 0, 64);
             std::atexit([] {
                 (void)hipDeviceSynchronize();
-                std::fprintf(stderr, "k_ba_chol_lds cycles per call: load %llu panel %llu trailing %llu solves %llu (%llu calls); factor %llu trail(w1) %llu fwd(ws) %llu\n",
+                std::fprintf(stderr, "cholesky cycles per call (k_ba_chol_lds / k_ba_chol_fast): load %llu panel %llu trailing %llu solves %llu (%llu calls); factor %llu trail(w1) %llu fwd(ws) %llu\n",
                              p[0] / std::max(p[4], 1ull), p[1] / std::max(p[4], 1ull), p[2] / std::max(p[4], 1ull),
                              p[3] / std::max(p[4], 1ull), p[4], p[5] / std::max(p[4], 1ull), p[6] / std::max(p[4], 1ull),
                              p[7] / std::max(p[4], 1ull));

@@ -94,3 +94,34 @@ def test_local_ba_fast_mode_within_tolerance(seed, n_local, n_points, oracle_mod
     free = P["fixed"] == 0
     assert np.array_equal(Tg[~free], P["Tcw"][~free])
     assert abs(ig[0] - io[0]) <= 1 and abs(ig[1] - io[1]) <= 2, (ig, io)
+
+
+def _fast_close(P, e, oracle_mod, tag):
+    Tg, Xg, og, ig = local_bundle_adjustment(P["Tcw"], P["fixed"], P["Xw"], e, fast=True)
+    To, Xo, oo, io = oracle_mod.local_ba(P["Tcw"], P["fixed"], P["Xw"], e)
+    assert np.array_equal(og, oo), (tag, np.nonzero(og != oo)[0][:8])
+    assert np.abs(Tg - To).max() <= 1e-4 * max(1.0, np.abs(To).max()), (tag, np.abs(Tg - To).max())
+    assert np.abs(Xg - Xo).max() <= 1e-4 * np.abs(Xo).max(), (tag, np.abs(Xg - Xo).max())
+    assert abs(ig[0] - io[0]) <= 1 and abs(ig[1] - io[1]) <= 2, (tag, ig, io)
+
+
+def test_local_ba_fast_mode_paths_and_reuse(oracle_mod):
+    """The fast mode's paths across one workspace: the dense Schur product
+    and the augmented-system Cholesky (<= 126 unknowns), the global-memory
+    Cholesky past them (22 free keyframes: 132 unknowns), a repeated (camera,
+    point) observation (no point maps: the merge-walk pairs and the ordered
+    right-hand side), growing and shrinking problems, and an ordered-mode call
+    in between (its workspace has no dense operand); every call against the
+    ordered oracle within the fast mode's tolerance."""
+    seq = [(20, 3000, 2, False), (22, 2000, 34, False), (5, 400, 32, False), (6, 600, 9, True),
+           (21, 1800, 33, False), (10, 1500, 1, False)]
+    for k, (n_local, n_points, seed, dup) in enumerate(seq):
+        P = make_ba_problem(n_local=n_local, n_fixed=3 if n_local != 20 else 4, n_points=n_points, seed=seed)
+        e = P["edges"]
+        if dup:
+            e = np.concatenate([e, e[7:8]])
+        _fast_close(P, e, oracle_mod, k)
+        if k == 2:   # an ordered call on the same workspace, bit-exact
+            Tg, Xg, og, ig = local_bundle_adjustment(P["Tcw"], P["fixed"], P["Xw"], e)
+            To, Xo, oo, io = oracle_mod.local_ba(P["Tcw"], P["fixed"], P["Xw"], e)
+            assert ig == io and np.array_equal(og, oo) and np.array_equal(Tg, To) and np.array_equal(Xg, Xo)
