@@ -125,3 +125,15 @@ def test_local_ba_fast_mode_paths_and_reuse(oracle_mod):
             Tg, Xg, og, ig = local_bundle_adjustment(P["Tcw"], P["fixed"], P["Xw"], e)
             To, Xo, oo, io = oracle_mod.local_ba(P["Tcw"], P["fixed"], P["Xw"], e)
             assert ig == io and np.array_equal(og, oo) and np.array_equal(Tg, To) and np.array_equal(Xg, Xo)
+
+
+def test_local_ba_fast_mode_mono_only_and_empty(oracle_mod):
+    """The fast mode on a monocular-only problem (2-row edges throughout) and
+    with no edges at all (nothing to optimise: the estimate comes back as
+    given, up to the float round trip)."""
+    P = make_ba_problem(n_local=5, n_fixed=2, n_points=500, seed=8, stereo_frac=0.0)
+    _fast_close(P, P["edges"], oracle_mod, "mono")
+    e = P["edges"][:0]
+    Tg, Xg, og, ig = local_bundle_adjustment(P["Tcw"], P["fixed"], P["Xw"], e, fast=True)
+    assert len(og) == 0
+    assert np.abs(Tg - P["Tcw"]).max() <= 1e-6 and np.abs(Xg - P["Xw"]).max() <= 1e-6 * np.abs(P["Xw"]).max()
