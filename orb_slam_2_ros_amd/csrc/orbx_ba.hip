@@ -286,9 +286,11 @@ __device__ inline void linearize_edge(const EdgeD &e, const Pose &T, const doubl
     }
 }
 
+// gate (fast mode's speculative build, lm_optimize): run only if *gate != 0
 __global__ void k_ba_linearize(const Pose *poses, const double *pts, const EdgeD *edges, int ne, const uint8_t *active,
-                               const double *err_in, const double *rho_in, EdgeOut *out) {
+                               const double *err_in, const double *rho_in, EdgeOut *out, const int *gate) {
     static_assert(sizeof(EdgeOut) == 72 * sizeof(double), "EdgeOut layout");
+    if (gate && !*gate) return;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= ne || !active[i]) return;
     const EdgeD e = edges[i];
@@ -305,7 +307,8 @@ __global__ void k_ba_linearize(const Pose *poses, const double *pts, const EdgeD
 // Vertex blocks: wave per vertex, lane = one matrix entry, edges in order.
 // kind 0: cameras (36 + 6 entries from hpp / bp), 1: points (9 + 3 from hll / bl).
 __global__ void k_ba_reduce(const EdgeOut *eo, const int32_t *offs, const int32_t *list, const uint8_t *active,
-                            int nv, int kind, double *H, double *b) {
+                            int nv, int kind, double *H, double *b, const int *gate) {
+    if (gate && !*gate) return;
     const int lane = threadIdx.x & 63;
     const int v = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
     if (v >= nv) return;
@@ -538,7 +541,8 @@ __global__ void k_ba_pair_terms(const int2 *mlist, int64_t nterms, const int32_t
 // fields 0..NF-1.
 template <int NF, int LAYOUT>
 __global__ void k_ba_gather_rows(const double *rec, int stride, const int32_t *list, int n, const uint8_t *pred,
-                                 double *out) {
+                                 double *out, const int *gate) {
+    if (gate && !*gate) return;
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (int64_t)n * NF) return;
     const int t = (int)(idx / NF), f = (int)(idx - (int64_t)t * NF);
@@ -813,7 +817,8 @@ __global__ void k_ba_schur_sum(const double *part, int nch, int nblk, int h, con
 template <int NF, bool FAST>
 __global__ __launch_bounds__(kSumThreads) void k_ba_stream_sums(const double *rows, const int32_t *offs,
                                                                 const double *minus, double *out_a, int na,
-                                                                double *out_b) {
+                                                                double *out_b, const int *gate) {
+    if (gate && !*gate) return;   // (uniform: before any barrier)
     extern __shared__ double sbuf[];
     const int v = blockIdx.x, lane = threadIdx.x;
     const int t0 = offs[v];
@@ -849,7 +854,8 @@ __global__ __launch_bounds__(kFastSumThreads) void k_ba_fast_sums(const double *
                                                                   const double *x, const double *bp, const double *bl,
                                                                   int n, int m, double lambda, const int *ok,
                                                                   const double *Hpp, int nf, const double *Hll, int np,
-                                                                  double *part, unsigned *counter, double *out) {
+                                                                  double *part, unsigned *counter, double *out,
+                                                                  double cur_chi, int *accept) {
     __shared__ double red[3][kFastSumThreads / 64];
     __shared__ bool last;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -896,6 +902,16 @@ __global__ __launch_bounds__(kFastSumThreads) void k_ba_fast_sums(const double *
     out[1] = t;
     out[2] = ok ? (double)*ok : 1.0;
     out[3] = d;
+    if (accept) {   // lm_optimize's acceptance of the trial, the host's arithmetic exactly
+        const bool okv = !ok || *ok != 0;
+        const double tempChi = okv ? c : DBL_MAX;
+        double rho = cur_chi - tempChi, sc = okv ? t : 0.0;
+        sc += 1e-3;
+        rho /= sc;
+        const int a = rho > 0 && __builtin_isfinite(tempChi);
+        *accept = a;
+        out[8] = a;   // (h_fsum[8]: the host checks its own decision against it)
+    }
     *counter = 0;
 }
 
@@ -1554,6 +1570,7 @@ struct Graph {
 struct BAWs {
     std::mutex mu;
     hipStream_t st = nullptr;
+    hipEvent_t ev = nullptr;   // (fast mode: the trial's readback, waited on while the speculative build runs)
     uint8_t *dev = nullptr, *host = nullptr;
     size_t cap = 0, hcap = 0;
     int32_t *moffs = nullptr;
@@ -1623,7 +1640,7 @@ public:
     int upload(const double *pts);
     void set_active(const std::vector<uint8_t> &act);
     int errors(bool robust, double *chi_sum);
-    int build();
+    int build(const int *gate = nullptr);
     int solve(double lambda, int *ok);
     // the LM driver's asynchronous pieces: launches and readbacks into pinned
     // host buffers, one stream synchronisation per trial
@@ -1632,7 +1649,7 @@ public:
     int update_gated();
     int read_errors();
     int read_diag();
-    int read_trial(double lambda);
+    int read_trial(double lambda, double cur_chi);
     double chi_sum_host() const;
     double max_diag_host() const;
     double scale_host(double lambda) const;
@@ -1662,6 +1679,19 @@ public:
     int *d_ok = nullptr;
     int32_t *d_cmap = nullptr;   // free camera x point -> position in its usable list (-1)
     bool use_map = false;        // every (camera, point) observed at most once
+    // fast mode's speculative build (lm_optimize): the second linear system
+    // (swapped in when the trial is accepted) and the device's acceptance
+    EdgeOut *d_eo2 = nullptr;
+    double *d_Hpp2 = nullptr, *d_bp2 = nullptr, *d_Hll2 = nullptr, *d_bl2 = nullptr;
+    int *d_accept = nullptr;
+    void swap_system() {
+        std::swap(d_eo, d_eo2); std::swap(d_Hpp, d_Hpp2); std::swap(d_bp, d_bp2);
+        std::swap(d_Hll, d_Hll2); std::swap(d_bl, d_bl2);
+    }
+    hipEvent_t event() {
+        if (!ws_.ev && hipEventCreateWithFlags(&ws_.ev, hipEventDisableTiming) != hipSuccess) ws_.ev = nullptr;
+        return ws_.ev;
+    }
     // fast mode's dense Schur product (k_ba_schur_*): per-point L^-1 and u,
     // the operand M (kp_ x ct_), the chunk partials of the 2x2 tile blocks
     double *d_lu = nullptr, *d_M = nullptr, *d_spart = nullptr;
@@ -1756,7 +1786,8 @@ int BA::alloc() {
                          sizeof(int2) * std::max(npairs, 1) + 8 * (36 * nf + 6 * nf + 9 * np + 3 * np + 9 * np +
                                                                    18 * ne + 6 * ne + n * n + n + n + 3 * np) +
                          4 * nf * np + 8 * ne + 8 * 3 * np + 8 * 42 * ne + sizeof(orbx_ba_edge) * ne + 256 * 6 +
-                         schur_bytes();
+                         schur_bytes() +
+                         (fast_ ? sizeof(EdgeOut) * ne + 8 * (36 * nf + 6 * nf + 9 * np + 3 * np) + 256 * 6 : 0);
     if (ws_.cap < bytes) {
         (void)hipStreamSynchronize(st_);
         if (ws_.dev) (void)hipFree(ws_.dev);
@@ -1796,6 +1827,13 @@ int BA::alloc() {
     }
     d_fpart = carve<double>(p, 3 * kFastSumBlocks);
     d_fcount = carve<unsigned>(p, 4);
+    d_eo2 = nullptr; d_Hpp2 = d_bp2 = d_Hll2 = d_bl2 = nullptr; d_accept = nullptr;
+    if (fast_) {
+        d_eo2 = carve<EdgeOut>(p, ne);
+        d_Hpp2 = carve<double>(p, 36 * nf); d_bp2 = carve<double>(p, 6 * nf);
+        d_Hll2 = carve<double>(p, 9 * np); d_bl2 = carve<double>(p, 3 * np);
+        d_accept = carve<int>(p, 1);
+    }
     d_db = carve<double>(p, 3 * np);
     d_rows = carve<double>(p, 42 * ne);
     d_raw = carve<orbx_ba_edge>(p, ne);
@@ -1816,7 +1854,7 @@ int BA::alloc() {
         h_ok = carve<int>(h, 1); h_rho0 = carve<double>(h, ne); h_x = carve<double>(h, m);
         h_bp = carve<double>(h, 6 * nf); h_bl = carve<double>(h, 3 * np);
         h_hpp = carve<double>(h, 36 * nf); h_hll = carve<double>(h, 9 * np);
-        h_fsum = carve<double>(h, 8);   // [0, 4): errors / trial sums, [4, 8): read_diag's
+        h_fsum = carve<double>(h, 12);   // [0, 4): errors / trial sums, [4, 8): read_diag's, [8]: the trial's acceptance
         if (hipHostGetDevicePointer(reinterpret_cast<void **>(&d_fsum), h_fsum, 0) != hipSuccess) return ORBX_EIO;
         h_stage = carve<uint8_t>(h, 2 * ne); h_coffs_ = carve<int32_t>(h, nf + 1 + ne);
         if ((size_t)(h - hbuf_) > hb) return ORBX_ENOMEM;
@@ -1935,26 +1973,26 @@ int BA::errors(bool robust, double *chi_sum) {
     return ORBX_OK;
 }
 
-int BA::build() {
+int BA::build(const int *gate) {
     const Graph &g = g_;
     if (g.ne) hipLaunchKernelGGL(k_ba_linearize, dim3((g.ne + 63) / 64), dim3(64), 0, st_, d_pose, d_pts, d_edges,
-                                 g.ne, d_active, d_err, d_rho, d_eo);
+                                 g.ne, d_active, d_err, d_rho, d_eo, gate);
     if (g.nf) {   // Hpp and bp of each free camera over all its edges, edge order
         constexpr int kEo = sizeof(EdgeOut) / sizeof(double);
         const int nl = cv_offs_[g.nf];
         if (nl)
             hipLaunchKernelGGL((k_ba_gather_rows<42, 1>), dim3((unsigned)(((int64_t)nl * 42 + 255) / 256)), dim3(256), 0,
-                               st_, reinterpret_cast<const double *>(d_eo), kEo, d_cvlist, nl, d_active, d_rows);
+                               st_, reinterpret_cast<const double *>(d_eo), kEo, d_cvlist, nl, d_active, d_rows, gate);
         if (!sums_ready()) return ORBX_EIO;
         if (fast_)
             hipLaunchKernelGGL((k_ba_stream_sums<42, true>), dim3(g.nf), dim3(kSumThreads), kSumLds, st_, d_rows,
-                               d_cvoffs, nullptr, d_Hpp, 36, d_bp);
+                               d_cvoffs, nullptr, d_Hpp, 36, d_bp, gate);
         else
             hipLaunchKernelGGL((k_ba_stream_sums<42, false>), dim3(g.nf), dim3(kSumThreads), kSumLds, st_, d_rows,
-                               d_cvoffs, nullptr, d_Hpp, 36, d_bp);
+                               d_cvoffs, nullptr, d_Hpp, 36, d_bp, gate);
     }
     if (g.npt) hipLaunchKernelGGL(k_ba_reduce, dim3((g.npt + 3) / 4), dim3(256), 0, st_, d_eo, d_poffs, d_plist,
-                                  d_active, g.npt, 1, d_Hll, d_bl);
+                                  d_active, g.npt, 1, d_Hll, d_bl, gate);
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
 }
 
@@ -2023,13 +2061,13 @@ int BA::solve_async(double lambda) {
         // bs = bp - sum over the camera's usable edges of B Dinv bl, edge order
         if (nusable_)
             hipLaunchKernelGGL((k_ba_gather_rows<6, 0>), dim3((unsigned)(((int64_t)nusable_ * 6 + 255) / 256)),
-                               dim3(256), 0, st_, d_bdb, 6, d_clist, nusable_, nullptr, d_rows);
+                               dim3(256), 0, st_, d_bdb, 6, d_clist, nusable_, nullptr, d_rows, nullptr);
         if (fast_)
             hipLaunchKernelGGL((k_ba_stream_sums<6, true>), dim3(g.nf), dim3(kSumThreads), kSumLds, st_, d_rows,
-                               d_coffs, d_bp, d_bs, 6, nullptr);
+                               d_coffs, d_bp, d_bs, 6, nullptr, nullptr);
         else
             hipLaunchKernelGGL((k_ba_stream_sums<6, false>), dim3(g.nf), dim3(kSumThreads), kSumLds, st_, d_rows,
-                               d_coffs, d_bp, d_bs, 6, nullptr);
+                               d_coffs, d_bp, d_bs, 6, nullptr, nullptr);
     }
     if (g.nf) {
         // (fast mode: the augmented-matrix MFMA factorisation, k_ba_chol_fast;
@@ -2078,7 +2116,8 @@ int BA::update_gated() {   // (the trial's backup of the estimate is written by 
 int BA::read_errors() {
     if (fast_) {
         hipLaunchKernelGGL(k_ba_fast_sums, dim3(kFastSumBlocks), dim3(kFastSumThreads), 0, st_, d_rho0, d_active, g_.ne,
-                           nullptr, nullptr, nullptr, 0, 0, 0.0, nullptr, nullptr, 0, nullptr, 0, d_fpart, d_fcount, d_fsum);
+                           nullptr, nullptr, nullptr, 0, 0, 0.0, nullptr, nullptr, 0, nullptr, 0, d_fpart, d_fcount, d_fsum,
+                           0.0, nullptr);
         return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
     }
     return (g_.ne && hipMemcpyAsync(h_rho0, d_rho0, 8 * (size_t)g_.ne, hipMemcpyDeviceToHost, st_) != hipSuccess)
@@ -2089,7 +2128,7 @@ int BA::read_diag() {
     if (fast_) {   // (into slots of its own: read_errors' chi sum in h_fsum[0] stays whatever the order)
         hipLaunchKernelGGL(k_ba_fast_sums, dim3(kFastSumBlocks), dim3(kFastSumThreads), 0, st_, d_rho0, d_active, g_.ne,
                            nullptr, nullptr, nullptr, 0, 0, 0.0, nullptr, d_Hpp, g_.nf, d_Hll, g_.npt, d_fpart, d_fcount,
-                           d_fsum + 4);
+                           d_fsum + 4, 0.0, nullptr);
         return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
     }
     if ((g_.nf && hipMemcpyAsync(h_hpp, d_Hpp, 8 * 36 * (size_t)g_.nf, hipMemcpyDeviceToHost, st_) != hipSuccess) ||
@@ -2100,11 +2139,12 @@ int BA::read_diag() {
 
 // a trial's readback: the solve flag, the errors at the trial estimate, and
 // x and b for computeScale
-int BA::read_trial(double lambda) {
+int BA::read_trial(double lambda, double cur_chi) {
     if (fast_) {
         const int n = 6 * g_.nf, m = n + 3 * g_.npt;
         hipLaunchKernelGGL(k_ba_fast_sums, dim3(kFastSumBlocks), dim3(kFastSumThreads), 0, st_, d_rho0, d_active, g_.ne,
-                           d_x, d_bp, d_bl, n, m, lambda, d_ok, nullptr, 0, nullptr, 0, d_fpart, d_fcount, d_fsum);
+                           d_x, d_bp, d_bl, n, m, lambda, d_ok, nullptr, 0, nullptr, 0, d_fpart, d_fcount, d_fsum,
+                           cur_chi, d_accept);
         return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
     }
     return hipMemcpyAsync(h_ok, d_ok, span_, hipMemcpyDeviceToHost, st_) == hipSuccess ? ORBX_OK : ORBX_EIO;
@@ -2167,16 +2207,29 @@ int BA::download(double *pts, std::vector<double> &chi2, std::vector<uint8_t> &f
 // device) and read back at once.  An iteration that follows an accepted trial
 // reuses that trial's errors, which are the errors of the current estimate
 // (g2o recomputes them: same values, same sum).
+// Fast mode: the device decides each trial's acceptance too (k_ba_fast_sums,
+// the host's arithmetic), and the linear system at the trial's estimate is
+// built into the second system buffers, gated on that decision, right behind
+// the trial: the host waits for the trial's sums alone (an event), and an
+// accepted trial's next iteration finds its system built (the buffers swap).
+// ORBX_BA_SPEC=0 turns it off.
+bool spec_on() {
+    static const bool on = env_on("ORBX_BA_SPEC");
+    return on;
+}
 int lm_optimize(BA &ba, int iters, bool robust, int *rc_out) {
     double lambda = 0, ni = 2, currentChi = 0;
     int nBad = 0, it = 0;
     bool fresh = false;   // the device errors are the current estimate's and currentChi their sum
+    bool built = false;   // (fast mode) the current estimate's system is built already
     *rc_out = ORBX_OK;
     auto fail = [&](int rc) { *rc_out = rc; return it; };
+    const hipEvent_t ev = ba.fast_ && ba.d_eo2 && spec_on() ? ba.event() : nullptr;
     for (; it < iters; ++it) {
         int rc;
         if (!fresh && (rc = ba.errors_async(robust, nullptr))) return fail(rc);
-        if ((rc = ba.build())) return fail(rc);
+        if (!built && (rc = ba.build())) return fail(rc);
+        built = false;
         if (!fresh || it == 0) {
             if ((!fresh && (rc = ba.read_errors())) || (it == 0 && (rc = ba.read_diag()))) return fail(rc);
             if (hipStreamSynchronize(ba.st_) != hipSuccess) return fail(ORBX_EIO);
@@ -2192,9 +2245,18 @@ int lm_optimize(BA &ba, int iters, bool robust, int *rc_out) {
         int qmax = 0;
         do {
             if ((rc = ba.solve_async(lambda)) || (rc = ba.update_gated()) ||
-                (rc = ba.errors_async(robust, ba.d_ok)) || (rc = ba.read_trial(lambda)))
+                (rc = ba.errors_async(robust, ba.d_ok)) || (rc = ba.read_trial(lambda, currentChi)))
                 return fail(rc);
-            if (hipStreamSynchronize(ba.st_) != hipSuccess) return fail(ORBX_EIO);
+            if (ev) {
+                if (hipEventRecord(ev, ba.st_) != hipSuccess) return fail(ORBX_EIO);
+                ba.swap_system();
+                rc = ba.build(ba.d_accept);
+                ba.swap_system();
+                if (rc) return fail(rc);
+                if (hipEventSynchronize(ev) != hipSuccess) return fail(ORBX_EIO);
+            } else if (hipStreamSynchronize(ba.st_) != hipSuccess) {
+                return fail(ORBX_EIO);
+            }
             const bool ok = ba.trial_ok();
             // (the reference updates with an unsolved x; the step is rejected either way)
             const double tempChi = ok ? ba.chi_sum_host() : DBL_MAX;
@@ -2210,6 +2272,10 @@ int lm_optimize(BA &ba, int iters, bool robust, int *rc_out) {
                 ni = 2;
                 currentChi = tempChi;
                 fresh = true;
+                if (ev && ba.h_fsum[8] != 0) {   // (the device agreed: its build ran)
+                    ba.swap_system();
+                    built = true;
+                }
             } else {
                 lambda *= ni;
                 ni *= 2;
