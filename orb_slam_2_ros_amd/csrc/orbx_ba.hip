@@ -1561,6 +1561,7 @@ struct Graph {
     std::vector<Pose> poses;
     const orbx_ba_edge *raw;   // the caller's edges (converted to EdgeD on the device)
     std::vector<int32_t> coffs, clist, poffs, plist, epoint;   // camera lists: usable edges by point; point lists: edges by camera
+    std::vector<int32_t> efree;   // per edge: its camera's free index (-1: fixed), for the host's list building
 };
 
 // Per-device workspace kept across calls (LocalMapping runs a BA per
@@ -1736,6 +1737,11 @@ public:
 
 int BA::alloc() {
     const Graph &g = g_;
+    // ORBX_BA_TIMING: the host phases of alloc on stderr (diagnostics)
+    static const bool timing = std::getenv("ORBX_BA_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto ms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
+    double t_pairs = 0, t_lists = 0, t_arena = 0;
     const size_t ne = std::max(g.ne, 1), nc = std::max(g.ncam, 1), np = std::max(g.npt, 1), nf = std::max(g.nf, 1);
     // the camera-pair list: free cameras sharing a point (structure of the
     // reduced system), from per-camera bitmasks of the cameras it shares a
@@ -1749,13 +1755,13 @@ int BA::alloc() {
         uint64_t pm[kW] = {0, 0, 0};
         int64_t k = 0;
         for (int t = g.poffs[p]; t < g.poffs[p + 1]; ++t) {
-            const int f = g.poses[g.raw[g.plist[t]].cam].free_idx;
+            const int f = g.efree[g.plist[t]];
             if (f >= 0) { pm[f >> 6] |= 1ull << (f & 63); ++k; }
         }
         mbound_ += k * (k + 1) / 2;
         if (!k) continue;
         for (int t = g.poffs[p]; t < g.poffs[p + 1]; ++t) {
-            const int f = g.poses[g.raw[g.plist[t]].cam].free_idx;
+            const int f = g.efree[g.plist[t]];
             if (f >= 0)
                 for (int w = 0; w < kW; ++w) rows[(size_t)f * kW + w] |= pm[w];
         }
@@ -1765,10 +1771,11 @@ int BA::alloc() {
         for (int b = a; b < g.nf; ++b)
             if (b == a || (rows[(size_t)a * kW + (b >> 6)] >> (b & 63) & 1)) pairs.push_back(make_int2(a, b));
     npairs = (int)pairs.size();
+    t_pairs = ms();
     // all edges of each free camera in edge order (for Hpp / bp)
     cv_offs_.assign(g.nf + 1, 0);
     for (int e = 0; e < g.ne; ++e) {
-        const int f = g.poses[g.raw[e].cam].free_idx;
+        const int f = g.efree[e];
         if (f >= 0) ++cv_offs_[f + 1];
     }
     for (int f = 0; f < g.nf; ++f) cv_offs_[f + 1] += cv_offs_[f];
@@ -1776,10 +1783,11 @@ int BA::alloc() {
     {
         std::vector<int> fill(cv_offs_.begin(), cv_offs_.end() - 1);
         for (int e = 0; e < g.ne; ++e) {
-            const int f = g.poses[g.raw[e].cam].free_idx;
+            const int f = g.efree[e];
             if (f >= 0) cv_list_[fill[f]++] = e;
         }
     }
+    t_lists = ms();
     const size_t n = 6 * nf;
     const size_t bytes = 256 * 40 + sizeof(Pose) * nc * 2 + 8 * 3 * np * 2 + sizeof(EdgeD) * ne + 3 * ne +
                          8 * ne * 6 + sizeof(EdgeOut) * ne + 4 * (nf + 1 + ne + np + 1 + ne + ne + nf + 1 + ne) +
@@ -1875,6 +1883,7 @@ int BA::alloc() {
             return ORBX_ENOMEM;
         ws_.mcap = (int64_t)m;
     }
+    t_arena = ms();
     d_mlist = ws_.mlist;
     d_terms = ws_.terms;
     auto up = [&](void *d, const void *h, size_t b) {
@@ -1890,6 +1899,9 @@ int BA::alloc() {
         !up(d_plist, g.plist.data(), 4 * g.ne) || !up(d_pairs, pairs.data(), sizeof(int2) * npairs) ||
         !up(d_cvoffs, cv_offs_.data(), 4 * (g.nf + 1)) || !up(d_cvlist, cv_list_.data(), 4 * cv_list_.size()))
         return ORBX_EIO;
+    if (timing)
+        std::fprintf(stderr, "orbx_local_ba alloc ms: pairs %.3f lists %.3f arena %.3f uploads %.3f\n", t_pairs,
+                     t_lists - t_pairs, t_arena - t_lists, ms() - t_arena);
     return ORBX_OK;
 }
 
@@ -1907,6 +1919,8 @@ int BA::upload(const double *pts) {
 // the point -> list-position map, the pairs' shared-point counts, their scan
 // and the lists.  Nothing waits here.
 void BA::set_active(const std::vector<uint8_t> &act) {
+    static const bool timing = std::getenv("ORBX_BA_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
     act_ = act;
     s_zero_ = false;
     const Graph &g = g_;
@@ -1914,7 +1928,7 @@ void BA::set_active(const std::vector<uint8_t> &act) {
     int32_t *h_coffs = h_coffs_, *h_clist = h_coffs_ + g.nf + 1;
     std::fill(h_coffs, h_coffs + g.nf + 1, 0);
     for (int e = 0; e < g.ne; ++e) {
-        const int f = g.poses[g.raw[e].cam].free_idx;
+        const int f = g.efree[e];
         h_act[e] = act[e];
         h_us[e] = act[e] && f >= 0;
         if (h_us[e]) ++h_coffs[f + 1];
@@ -1930,13 +1944,16 @@ void BA::set_active(const std::vector<uint8_t> &act) {
         for (int t = g.poffs[p]; t < g.poffs[p + 1]; ++t) {
             const int e = g.plist[t];
             if (!h_us[e]) continue;
-            const int f = g.poses[g.raw[e].cam].free_idx;
+            const int f = g.efree[e];
             if (f == last) use_map = false;
             last = f;
             h_clist[fill[f]++] = e;
         }
     }
     nusable_ = h_coffs[g.nf];
+    if (timing)
+        std::fprintf(stderr, "orbx_local_ba set_active host ms: %.3f\n",
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     (void)hipMemcpyAsync(d_active, h_act, g.ne, hipMemcpyHostToDevice, st_);
     (void)hipMemcpyAsync(d_usable, h_us, g.ne, hipMemcpyHostToDevice, st_);
     (void)hipMemcpyAsync(d_coffs, h_coffs, 4 * (size_t)(g.nf + 1), hipMemcpyHostToDevice, st_);
@@ -2303,8 +2320,11 @@ int build_graph(const float *Tcw, const uint8_t *fixed, int ncam, int npt, const
         g.poses[c].pad = 0;
     }
     g.nf = nf;
-    for (int e = 0; e < ne; ++e)
+    g.efree.resize(std::max(ne, 1));
+    for (int e = 0; e < ne; ++e) {
         if (edges[e].cam < 0 || edges[e].cam >= ncam || edges[e].point < 0 || edges[e].point >= npt) return ORBX_EINVAL;
+        g.efree[e] = g.poses[edges[e].cam].free_idx;
+    }
     // edges per point, by camera index (stable): bucket by camera, then by point
     std::vector<int> cfill(ncam + 1, 0);
     for (int e = 0; e < ne; ++e) ++cfill[edges[e].cam + 1];
