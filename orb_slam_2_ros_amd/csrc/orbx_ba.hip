@@ -1678,6 +1678,9 @@ public:
     double *d_Hpp = nullptr, *d_bp = nullptr, *d_Hll = nullptr, *d_bl = nullptr, *d_dinv = nullptr,
            *d_bdinv = nullptr, *d_bdb = nullptr, *d_S = nullptr, *d_bs = nullptr, *d_x = nullptr, *d_db = nullptr;
     int *d_ok = nullptr;
+    std::vector<int2> pairs_;    // the camera pairs (make_pairs; d_pairs)
+    bool pairs_made_ = false;
+    void make_pairs();
     int32_t *d_cmap = nullptr;   // free camera x point -> position in its usable list (-1)
     bool use_map = false;        // every (camera, point) observed at most once
     // fast mode's speculative build (lm_optimize): the second linear system
@@ -1735,19 +1738,13 @@ public:
     }
 };
 
-int BA::alloc() {
+// the camera-pair list: free cameras sharing a point (structure of the
+// reduced system), from per-camera bitmasks of the cameras it shares a point
+// with (nf <= 170: three words); pairs in lexicographic order.  mbound_: the
+// shared-point list length with every edge active (a bound for any active
+// subset)
+void BA::make_pairs() {
     const Graph &g = g_;
-    // ORBX_BA_TIMING: the host phases of alloc on stderr (diagnostics)
-    static const bool timing = std::getenv("ORBX_BA_TIMING") != nullptr;
-    const auto t0 = std::chrono::steady_clock::now();
-    auto ms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
-    double t_pairs = 0, t_lists = 0, t_arena = 0;
-    const size_t ne = std::max(g.ne, 1), nc = std::max(g.ncam, 1), np = std::max(g.npt, 1), nf = std::max(g.nf, 1);
-    // the camera-pair list: free cameras sharing a point (structure of the
-    // reduced system), from per-camera bitmasks of the cameras it shares a
-    // point with (nf <= 170: three words); pairs in lexicographic order.
-    // mbound_: the shared-point list length with every edge active (a bound
-    // for any active subset)
     constexpr int kW = 3;
     std::vector<uint64_t> rows((size_t)std::max(g.nf, 1) * kW, 0);
     mbound_ = 0;
@@ -1766,11 +1763,32 @@ int BA::alloc() {
                 for (int w = 0; w < kW; ++w) rows[(size_t)f * kW + w] |= pm[w];
         }
     }
-    std::vector<int2> pairs;
+    pairs_.clear();
     for (int a = 0; a < g.nf; ++a)
         for (int b = a; b < g.nf; ++b)
-            if (b == a || (rows[(size_t)a * kW + (b >> 6)] >> (b & 63) & 1)) pairs.push_back(make_int2(a, b));
-    npairs = (int)pairs.size();
+            if (b == a || (rows[(size_t)a * kW + (b >> 6)] >> (b & 63) & 1)) pairs_.push_back(make_int2(a, b));
+    npairs = (int)pairs_.size();
+    pairs_made_ = true;
+}
+
+int BA::alloc() {
+    const Graph &g = g_;
+    // ORBX_BA_TIMING: the host phases of alloc on stderr (diagnostics)
+    static const bool timing = std::getenv("ORBX_BA_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto ms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
+    double t_pairs = 0, t_lists = 0, t_arena = 0;
+    const size_t ne = std::max(g.ne, 1), nc = std::max(g.ncam, 1), np = std::max(g.npt, 1), nf = std::max(g.nf, 1);
+    // the camera pairs (make_pairs): the fast mode's dense Schur product needs
+    // none, so there they are made only if set_active falls back to the merge walk
+    const bool lazy_pairs = fast_ && dense_schur_on();
+    if (lazy_pairs) {
+        pairs_.clear();
+        npairs = 0;
+        mbound_ = 0;
+    } else {
+        make_pairs();
+    }
     t_pairs = ms();
     // all edges of each free camera in edge order (for Hpp / bp)
     cv_offs_.assign(g.nf + 1, 0);
@@ -1789,9 +1807,10 @@ int BA::alloc() {
     }
     t_lists = ms();
     const size_t n = 6 * nf;
+    const size_t pair_cap = lazy_pairs ? nf * (nf + 1) / 2 : (size_t)std::max(npairs, 1);   // (d_pairs)
     const size_t bytes = 256 * 40 + sizeof(Pose) * nc * 2 + 8 * 3 * np * 2 + sizeof(EdgeD) * ne + 3 * ne +
                          8 * ne * 6 + sizeof(EdgeOut) * ne + 4 * (nf + 1 + ne + np + 1 + ne + ne + nf + 1 + ne) +
-                         sizeof(int2) * std::max(npairs, 1) + 8 * (36 * nf + 6 * nf + 9 * np + 3 * np + 9 * np +
+                         sizeof(int2) * pair_cap + 8 * (36 * nf + 6 * nf + 9 * np + 3 * np + 9 * np +
                                                                    18 * ne + 6 * ne + n * n + n + n + 3 * np) +
                          4 * nf * np + 8 * ne + 8 * 3 * np + 8 * 42 * ne + sizeof(orbx_ba_edge) * ne + 256 * 6 +
                          schur_bytes() +
@@ -1815,7 +1834,7 @@ int BA::alloc() {
     d_coffs = carve<int32_t>(p, nf + 1); d_clist = carve<int32_t>(p, ne);
     d_poffs = carve<int32_t>(p, np + 1); d_plist = carve<int32_t>(p, ne); d_epoint = carve<int32_t>(p, ne);
     d_cvoffs = carve<int32_t>(p, nf + 1); d_cvlist = carve<int32_t>(p, ne);
-    d_pairs = carve<int2>(p, std::max(npairs, 1));
+    d_pairs = carve<int2>(p, pair_cap);
     d_Hpp = carve<double>(p, 36 * nf);
     d_Hll = carve<double>(p, 9 * np); d_dinv = carve<double>(p, 9 * np);
     d_bdinv = carve<double>(p, 18 * ne); d_bdb = carve<double>(p, 6 * ne);
@@ -1896,7 +1915,7 @@ int BA::alloc() {
         hipLaunchKernelGGL(k_ba_edges, dim3((g.ne + 255) / 256), dim3(256), 0, st_, d_raw, g.ne,
                            (double)(float)std::sqrt(5.991), (double)(float)std::sqrt(7.815), d_edges, d_epoint);
     if (hipGetLastError() != hipSuccess || !up(d_poffs, g.poffs.data(), 4 * (g.npt + 1)) ||
-        !up(d_plist, g.plist.data(), 4 * g.ne) || !up(d_pairs, pairs.data(), sizeof(int2) * npairs) ||
+        !up(d_plist, g.plist.data(), 4 * g.ne) || !up(d_pairs, pairs_.data(), sizeof(int2) * npairs) ||
         !up(d_cvoffs, cv_offs_.data(), 4 * (g.nf + 1)) || !up(d_cvlist, cv_list_.data(), 4 * cv_list_.size()))
         return ORBX_EIO;
     if (timing)
@@ -1959,6 +1978,10 @@ void BA::set_active(const std::vector<uint8_t> &act) {
     (void)hipMemcpyAsync(d_coffs, h_coffs, 4 * (size_t)(g.nf + 1), hipMemcpyHostToDevice, st_);
     if (nusable_) (void)hipMemcpyAsync(d_clist, h_clist, 4 * (size_t)nusable_, hipMemcpyHostToDevice, st_);
     nmatch_ = 0;
+    if (!use_map && g.nf && !pairs_made_) {   // (fast mode: the merge walk needs the pairs after all)
+        make_pairs();
+        if (npairs) (void)hipMemcpyAsync(d_pairs, pairs_.data(), sizeof(int2) * npairs, hipMemcpyHostToDevice, st_);
+    }
     if (!use_map || !g.nf) return;
     if (g.npt) {
         (void)hipMemsetAsync(d_cmap, 0xFF, 4 * (size_t)g.nf * g.npt, st_);
