@@ -848,7 +848,8 @@ bool sums_ready() {
 // points (computeScale); out[2] = the solve flag; with Hpp: out[3] = the
 // largest |diagonal| of the free vertices (computeLambdaInit).  kFastSumBlocks
 // workgroups write partials; the last to finish (a counter it resets) folds
-// them in block order, so the result does not depend on the schedule.
+// them in a fixed order (lanes over blocks, then a butterfly), so the result
+// does not depend on the schedule.
 constexpr int kFastSumThreads = 256, kFastSumBlocks = 64;
 __global__ __launch_bounds__(kFastSumThreads) void k_ba_fast_sums(const double *rho0, const uint8_t *active, int ne,
                                                                   const double *x, const double *bp, const double *bl,
@@ -890,14 +891,23 @@ __global__ __launch_bounds__(kFastSumThreads) void k_ba_fast_sums(const double *
         last = atomicAdd(counter, 1u) == gridDim.x - 1;
     }
     __syncthreads();
-    if (!last || tid != 0) return;
+    if (!last || w != 0) return;
     __threadfence();
+    // the last workgroup's wave 0 folds the partials: lane k takes blocks k,
+    // k + 64, ... in order, then a fixed butterfly (the result does not
+    // depend on the schedule)
     double c = 0, t = 0, d = 0;
-    for (int k = 0; k < (int)gridDim.x; ++k) {
+    for (int k = lane; k < (int)gridDim.x; k += 64) {
         c += __builtin_nontemporal_load(&part[3 * k]);
         t += __builtin_nontemporal_load(&part[3 * k + 1]);
         d = fmax(d, __builtin_nontemporal_load(&part[3 * k + 2]));
     }
+    for (int o = 32; o > 0; o >>= 1) {
+        c += __shfl_xor(c, o);
+        t += __shfl_xor(t, o);
+        d = fmax(d, __shfl_xor(d, o));
+    }
+    if (lane != 0) return;
     out[0] = c;
     out[1] = t;
     out[2] = ok ? (double)*ok : 1.0;
