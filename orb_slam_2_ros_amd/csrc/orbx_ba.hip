@@ -1474,6 +1474,36 @@ __global__ void k_ba_backsub(const double *dinv, const double *bl, int npt, cons
     }
 }
 
+// Fast mode's back substitution from the dense Schur operand (dense mode):
+// xl_p = D_p^-1 (bl_p - sum_e B_e^T xc) = L_p^-T (u_p - (W xc)_p), W's rows
+// 3p..3p+2 read once, a wave per point (lanes over the camera columns, a
+// butterfly per row).  Replaces k_ba_backsub_terms + k_ba_backsub there.
+__global__ __launch_bounds__(256) void k_ba_backsub_dense(const double *M, int CT, int ncols, const double *xc,
+                                                          const double *lu, int npt, double *xl) {
+    const int lane = threadIdx.x & 63, p = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (p >= npt) return;
+    const double *row = M + (int64_t)3 * p * CT;
+    double r0 = 0.0, r1 = 0.0, r2 = 0.0;
+    for (int c = lane; c < ncols; c += 64) {
+        const double x = xc[c];
+        r0 = fma(row[c], x, r0);
+        r1 = fma(row[CT + c], x, r1);
+        r2 = fma(row[2 * CT + c], x, r2);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        r0 += __shfl_xor(r0, o);
+        r1 += __shfl_xor(r1, o);
+        r2 += __shfl_xor(r2, o);
+    }
+    if (lane != 0) return;
+    const double *l = lu + 9 * (int64_t)p;   // L^-1 (m00, m10, m11, m20, m21, m22), then u
+    const double y0 = l[6] - r0, y1 = l[7] - r1, y2 = l[8] - r2;
+    double *o = xl + 3 * (int64_t)p;   // L^-T y
+    o[0] = l[0] * y0 + l[1] * y1 + l[3] * y2;
+    o[1] = l[2] * y1 + l[4] * y2;
+    o[2] = l[5] * y2;
+}
+
 // SE3Quat::exp(update) * estimate (se3quat.h:223-258, :104-110); points += dx
 // bk (nullable): the estimate before the step is saved first (the trial's
 // push(); a rejected trial that ran the step restores it with k_ba_restore)
@@ -2141,7 +2171,10 @@ int BA::solve_async(double lambda) {
             hipLaunchKernelGGL(k_ba_chol, dim3(1), dim3(1024), 0, st_, d_S, n, d_bs, d_x, d_ok);
         }
     }
-    if (g.npt) {
+    if (g.npt && dn) {
+        hipLaunchKernelGGL(k_ba_backsub_dense, dim3((g.npt + 3) / 4), dim3(256), 0, st_, d_M, schur_ct_, n, d_x, d_lu,
+                           g.npt, d_x + n);
+    } else if (g.npt) {
         double *terms = d_rows;   // (free after the reduced right-hand side)
         uint8_t *flag = reinterpret_cast<uint8_t *>(d_rows + 3 * (size_t)std::max(g.ne, 1));
         if (g.ne)
