@@ -157,19 +157,18 @@ __device__ inline void edge_error(const EdgeD &e, const Pose &T, const double *X
     }
 }
 
-// gate (optional): run only when *gate != 0 (a trial whose solve failed
-// leaves the estimate and the errors alone)
-__global__ void k_ba_errors(const Pose *poses, const double *pts, const EdgeD *edges, int ne, const uint8_t *active,
-                            int robust, int front_only, double *err_out, double *chi2_out, double *rho_out,
-                            uint8_t *front_out, double *rho0_out, const int *gate) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= ne || (gate && !*gate)) return;
+// One edge's error at the current estimate: front flag, and for an active
+// edge (computeActiveErrors) err, chi2, rho; returns rho0 (0 if inactive or
+// front_only)
+__device__ inline double ba_edge_error(int i, const Pose *poses, const double *pts, const EdgeD *edges,
+                                       const uint8_t *active, int robust, int front_only, double *err_out,
+                                       double *chi2_out, double *rho_out, uint8_t *front_out, double *rho0_out) {
     const EdgeD e = edges[i];
     double err[3];
     bool front;
     edge_error(e, poses[e.cam], pts + 3 * (int64_t)e.point, err, &front);
     front_out[i] = front;   // isDepthPositive() at the current estimate
-    if (front_only || !active[i]) return;   // computeActiveErrors leaves inactive edges' errors as they were
+    if (front_only || !active[i]) return 0.0;   // computeActiveErrors leaves inactive edges' errors as they were
     const int D = e.stereo ? 3 : 2;
     double chi2 = 0;
     for (int k = 0; k < D; ++k) chi2 = chi2 + err[k] * (e.omega * err[k]);
@@ -187,6 +186,18 @@ __global__ void k_ba_errors(const Pose *poses, const double *pts, const EdgeD *e
     rho_out[2 * (int64_t)i] = rho0;
     rho_out[2 * (int64_t)i + 1] = rho1;
     if (rho0_out) rho0_out[i] = rho0;   // (contiguous, for the host's ordered sum)
+    return rho0;
+}
+
+// gate (optional): run only when *gate != 0 (a trial whose solve failed
+// leaves the estimate and the errors alone)
+__global__ void k_ba_errors(const Pose *poses, const double *pts, const EdgeD *edges, int ne, const uint8_t *active,
+                            int robust, int front_only, double *err_out, double *chi2_out, double *rho_out,
+                            uint8_t *front_out, double *rho0_out, const int *gate) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ne || (gate && !*gate)) return;
+    (void)ba_edge_error(i, poses, pts, edges, active, robust, front_only, err_out, chi2_out, rho_out, front_out,
+                        rho0_out);
 }
 
 // One edge's blocks (D = 2 mono, 3 stereo: compile-time, so the Jacobians
@@ -922,6 +933,72 @@ __global__ __launch_bounds__(kFastSumThreads) void k_ba_fast_sums(const double *
         *accept = a;
         out[8] = a;   // (h_fsum[8]: the host checks its own decision against it)
     }
+    *counter = 0;
+}
+
+// Fast mode's trial tail in one kernel (k_ba_errors gated on the solve,
+// then k_ba_fast_sums' trial sums): thread per edge computes its error and
+// adds its rho0 (active edges), threads over [0, m) add x (lambda x + b);
+// each workgroup writes its two partials, the last one (a counter it
+// resets) folds them in a fixed order and writes the sums, the solve flag
+// and the acceptance (as k_ba_fast_sums does) to the pinned readback.
+constexpr int kErrSumThreads = 256;
+__global__ __launch_bounds__(kErrSumThreads) void k_ba_errors_sums(
+    const Pose *poses, const double *pts, const EdgeD *edges, int ne, const uint8_t *active, int robust,
+    double *err_out, double *chi2_out, double *rho_out, uint8_t *front_out, const int *ok, const double *x,
+    const double *bp, const double *bl, int n, int m, double lambda, double *part, unsigned *counter, double *out,
+    double cur_chi, int *accept) {
+    __shared__ double red[2][kErrSumThreads / 64];
+    __shared__ bool last;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, i = blockIdx.x * kErrSumThreads + tid;
+    const int gs = gridDim.x * kErrSumThreads;
+    const bool okv = !ok || *ok != 0;
+    double chi = 0.0, sc = 0.0;
+    if (okv) {
+        if (i < ne)
+            chi = ba_edge_error(i, poses, pts, edges, active, robust, 0, err_out, chi2_out, rho_out, front_out, nullptr);
+        for (int j = i; j < m; j += gs) {
+            const double xj = x[j];
+            sc += xj * (lambda * xj + (j < n ? bp[j] : bl[j - n]));
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        chi += __shfl_xor(chi, o);
+        sc += __shfl_xor(sc, o);
+    }
+    if (lane == 0) { red[0][w] = chi; red[1][w] = sc; }
+    __syncthreads();
+    if (tid == 0) {
+        double c = 0, t = 0;
+        for (int k = 0; k < kErrSumThreads / 64; ++k) { c += red[0][k]; t += red[1][k]; }
+        part[2 * blockIdx.x] = c;
+        part[2 * blockIdx.x + 1] = t;
+        __threadfence();
+        last = atomicAdd(counter, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last || w != 0) return;
+    __threadfence();
+    double c = 0, t = 0;
+    for (int k = lane; k < (int)gridDim.x; k += 64) {
+        c += __builtin_nontemporal_load(&part[2 * k]);
+        t += __builtin_nontemporal_load(&part[2 * k + 1]);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        c += __shfl_xor(c, o);
+        t += __shfl_xor(t, o);
+    }
+    if (lane != 0) return;
+    out[0] = c;
+    out[1] = t;
+    out[2] = ok ? (double)*ok : 1.0;
+    const double tempChi = okv ? c : DBL_MAX;
+    double rho = cur_chi - tempChi, s2 = okv ? t : 0.0;
+    s2 += 1e-3;
+    rho /= s2;
+    const int a = rho > 0 && __builtin_isfinite(tempChi);
+    if (accept) *accept = a;
+    out[8] = a;
     *counter = 0;
 }
 
@@ -1691,6 +1768,7 @@ public:
     int read_errors();
     int read_diag();
     int read_trial(double lambda, double cur_chi);
+    int errors_trial(bool robust, double lambda, double cur_chi);   // (fast mode) errors_async + read_trial in one kernel
     double chi_sum_host() const;
     double max_diag_host() const;
     double scale_host(double lambda) const;
@@ -1760,6 +1838,7 @@ public:
     // visible to the host at the stream synchronisation -- no copy a trial
     double *d_fsum = nullptr, *h_fsum = nullptr;
     double *d_fpart = nullptr;                     // its per-workgroup partials
+    double *d_epart = nullptr;                     // k_ba_errors_sums' per-workgroup partials (2 each)
     unsigned *d_fcount = nullptr;                  // its finished-workgroup counter (zeroed by alloc, reset by the last)
     uint8_t *h_stage = nullptr;                // set_active's uploads: flags, then h_coffs_ | clist
     int32_t *h_coffs_ = nullptr;
@@ -1854,7 +1933,8 @@ int BA::alloc() {
                                                                    18 * ne + 6 * ne + n * n + n + n + 3 * np) +
                          4 * nf * np + 8 * ne + 8 * 3 * np + 8 * 42 * ne + sizeof(orbx_ba_edge) * ne + 256 * 6 +
                          schur_bytes() +
-                         (fast_ ? sizeof(EdgeOut) * ne + 8 * (36 * nf + 6 * nf + 9 * np + 3 * np) + 256 * 6 : 0);
+                         (fast_ ? sizeof(EdgeOut) * ne + 8 * (36 * nf + 6 * nf + 9 * np + 3 * np) + 256 * 6 +
+                                      16 * (std::max(ne, 6 * nf + 3 * np) / kErrSumThreads + 2) + 256 : 0);
     if (ws_.cap < bytes) {
         (void)hipStreamSynchronize(st_);
         if (ws_.dev) (void)hipFree(ws_.dev);
@@ -1894,12 +1974,13 @@ int BA::alloc() {
     }
     d_fpart = carve<double>(p, 3 * kFastSumBlocks);
     d_fcount = carve<unsigned>(p, 4);
-    d_eo2 = nullptr; d_Hpp2 = d_bp2 = d_Hll2 = d_bl2 = nullptr; d_accept = nullptr;
+    d_eo2 = nullptr; d_Hpp2 = d_bp2 = d_Hll2 = d_bl2 = nullptr; d_accept = nullptr; d_epart = nullptr;
     if (fast_) {
         d_eo2 = carve<EdgeOut>(p, ne);
         d_Hpp2 = carve<double>(p, 36 * nf); d_bp2 = carve<double>(p, 6 * nf);
         d_Hll2 = carve<double>(p, 9 * np); d_bl2 = carve<double>(p, 3 * np);
         d_accept = carve<int>(p, 1);
+        d_epart = carve<double>(p, 2 * (std::max(ne, 6 * nf + 3 * np) / kErrSumThreads + 2));
     }
     d_db = carve<double>(p, 3 * np);
     d_rows = carve<double>(p, 42 * ne);
@@ -2222,6 +2303,15 @@ int BA::read_diag() {
 
 // a trial's readback: the solve flag, the errors at the trial estimate, and
 // x and b for computeScale
+int BA::errors_trial(bool robust, double lambda, double cur_chi) {
+    const int ne = g_.ne, n = 6 * g_.nf, m = n + 3 * g_.npt;
+    const int nb = std::max((std::max(ne, m) + kErrSumThreads - 1) / kErrSumThreads, 1);
+    hipLaunchKernelGGL(k_ba_errors_sums, dim3(nb), dim3(kErrSumThreads), 0, st_, d_pose, d_pts, d_edges, ne, d_active,
+                       robust ? 1 : 0, d_err, d_chi2, d_rho, d_front, d_ok, d_x, d_bp, d_bl, n, m, lambda, d_epart,
+                       d_fcount, d_fsum, cur_chi, d_accept);
+    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
+}
+
 int BA::read_trial(double lambda, double cur_chi) {
     if (fast_) {
         const int n = 6 * g_.nf, m = n + 3 * g_.npt;
@@ -2328,7 +2418,8 @@ int lm_optimize(BA &ba, int iters, bool robust, int *rc_out) {
         int qmax = 0;
         do {
             if ((rc = ba.solve_async(lambda)) || (rc = ba.update_gated()) ||
-                (rc = ba.errors_async(robust, ba.d_ok)) || (rc = ba.read_trial(lambda, currentChi)))
+                (ba.fast_ && ba.d_epart ? (rc = ba.errors_trial(robust, lambda, currentChi))
+                                        : ((rc = ba.errors_async(robust, ba.d_ok)) || (rc = ba.read_trial(lambda, currentChi)))))
                 return fail(rc);
             if (ev) {
                 if (hipEventRecord(ev, ba.st_) != hipSuccess) return fail(ORBX_EIO);
