@@ -483,10 +483,26 @@ __global__ __launch_bounds__(256) void k_ba_pair_matches(const int2 *pairs, int 
 }
 
 // point -> position in camera f's usable list (the map k_ba_pair_matches reads)
-__global__ void k_ba_cmap(const int32_t *coffs, const int32_t *clist, const int32_t *epoint, int npt, int32_t *cmap) {
+// (ids: the edge itself instead of its list position -- the fast mode's
+// dense Schur product reads the map that way)
+__global__ void k_ba_cmap(const int32_t *coffs, const int32_t *clist, const int32_t *epoint, int npt, int32_t *cmap,
+                          int ids) {
     const int f = blockIdx.x;
     for (int t = coffs[f] + (int)threadIdx.x; t < coffs[f + 1]; t += blockDim.x)
-        cmap[(int64_t)f * npt + epoint[clist[t]]] = t;
+        cmap[(int64_t)f * npt + epoint[clist[t]]] = ids ? clist[t] : t;
+}
+
+// Fast mode's active set on the device (a graph whose free cameras observe
+// each point at most once): usable = active with a free camera, and the
+// camera x point -> edge map the dense Schur product reads -- no host lists
+__global__ void k_ba_usable_map(const uint8_t *active, const int32_t *efree, const int32_t *epoint, int ne, int npt,
+                                uint8_t *usable, int32_t *cmap) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= ne) return;
+    const int f = efree[e];
+    const bool us = active[e] && f >= 0;
+    usable[e] = us;
+    if (us) cmap[(int64_t)f * npt + epoint[e]] = e;
 }
 
 // offs[0..n] = exclusive scan of cnt[0..n) (one workgroup of 1024: a
@@ -698,8 +714,8 @@ typedef double orbx_f64x4 __attribute__((ext_vector_type(4)));
 // (deterministic).  It replaces the shared-point lists, the per-pair sums and
 // the per-edge B D^-1 products; equal to rounding.
 constexpr int kSchurKC = 512;
-__global__ void k_ba_schur_ops(int npt, int nf, int CT, int ucol, int kp, const int32_t *cmap, const int32_t *clist,
-                               const EdgeOut *eo, const double *lu, double *M) {
+__global__ void k_ba_schur_ops(int npt, int nf, int CT, int ucol, int kp, const int32_t *cmap, const EdgeOut *eo,
+                               int ne, const double *lu, double *M) {
     const int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (idx >= (int64_t)kp * CT) return;
     const int k = (int)(idx / CT), col = (int)(idx - (int64_t)k * CT);
@@ -709,9 +725,9 @@ __global__ void k_ba_schur_ops(int npt, int nf, int CT, int ucol, int kp, const 
         const double *l = lu + 9 * (int64_t)p;   // L^-1 as m00, m10, m11, m20, m21, m22; then u
         if (col < 6 * nf) {
             const int f = col / 6, r = col - 6 * f;
-            const int pos = cmap[(int64_t)f * npt + p];
-            if (pos >= 0) {
-                const double *h = eo[clist[pos]].hpl + 3 * r;   // row r of B (6 x 3)
+            const int ed = cmap[(int64_t)f * npt + p];   // (the edge: k_ba_cmap / k_ba_usable_map with ids)
+            if (ed >= 0 && ed < ne) {   // (-1: none; the bound guards the read whatever the map holds)
+                const double *h = eo[ed].hpl + 3 * r;   // row r of B (6 x 3)
                 v = kk == 0 ? l[0] * h[0]
                   : kk == 1 ? fma(l[2], h[1], l[1] * h[0])
                             : fma(l[5], h[2], fma(l[4], h[1], l[3] * h[0]));
@@ -1796,6 +1812,7 @@ public:
     double *d_Hpp = nullptr, *d_bp = nullptr, *d_Hll = nullptr, *d_bl = nullptr, *d_dinv = nullptr,
            *d_bdinv = nullptr, *d_bdb = nullptr, *d_S = nullptr, *d_bs = nullptr, *d_x = nullptr, *d_db = nullptr;
     int *d_ok = nullptr;
+    int32_t *d_efree = nullptr;  // (fast dense mode on a graph without repeated observations) Graph::efree, set_active on the device
     std::vector<int2> pairs_;    // the camera pairs (make_pairs; d_pairs)
     bool pairs_made_ = false;
     void make_pairs();
@@ -1928,7 +1945,7 @@ int BA::alloc() {
     const size_t n = 6 * nf;
     const size_t pair_cap = lazy_pairs ? nf * (nf + 1) / 2 : (size_t)std::max(npairs, 1);   // (d_pairs)
     const size_t bytes = 256 * 40 + sizeof(Pose) * nc * 2 + 8 * 3 * np * 2 + sizeof(EdgeD) * ne + 3 * ne +
-                         8 * ne * 6 + sizeof(EdgeOut) * ne + 4 * (nf + 1 + ne + np + 1 + ne + ne + nf + 1 + ne) +
+                         8 * ne * 6 + sizeof(EdgeOut) * ne + 4 * (nf + 1 + ne + np + 1 + ne + ne + nf + 1 + ne + ne) + 256 +
                          sizeof(int2) * pair_cap + 8 * (36 * nf + 6 * nf + 9 * np + 3 * np + 9 * np +
                                                                    18 * ne + 6 * ne + n * n + n + n + 3 * np) +
                          4 * nf * np + 8 * ne + 8 * 3 * np + 8 * 42 * ne + sizeof(orbx_ba_edge) * ne + 256 * 6 +
@@ -1954,6 +1971,19 @@ int BA::alloc() {
     d_coffs = carve<int32_t>(p, nf + 1); d_clist = carve<int32_t>(p, ne);
     d_poffs = carve<int32_t>(p, np + 1); d_plist = carve<int32_t>(p, ne); d_epoint = carve<int32_t>(p, ne);
     d_cvoffs = carve<int32_t>(p, nf + 1); d_cvlist = carve<int32_t>(p, ne);
+    d_efree = nullptr;
+    if (lazy_pairs) {   // (each free camera observes each point at most once: point lists are by camera)
+        bool unique = true;
+        for (int q = 0; q < g.npt && unique; ++q) {
+            int last = -1;
+            for (int t = g.poffs[q]; t < g.poffs[q + 1]; ++t) {
+                const int f = g.efree[g.plist[t]];
+                if (f >= 0 && f == last) { unique = false; break; }
+                if (f >= 0) last = f;
+            }
+        }
+        if (unique) d_efree = carve<int32_t>(p, ne);
+    }
     d_pairs = carve<int2>(p, pair_cap);
     d_Hpp = carve<double>(p, 36 * nf);
     d_Hll = carve<double>(p, 9 * np); d_dinv = carve<double>(p, 9 * np);
@@ -2037,7 +2067,8 @@ int BA::alloc() {
                            (double)(float)std::sqrt(5.991), (double)(float)std::sqrt(7.815), d_edges, d_epoint);
     if (hipGetLastError() != hipSuccess || !up(d_poffs, g.poffs.data(), 4 * (g.npt + 1)) ||
         !up(d_plist, g.plist.data(), 4 * g.ne) || !up(d_pairs, pairs_.data(), sizeof(int2) * npairs) ||
-        !up(d_cvoffs, cv_offs_.data(), 4 * (g.nf + 1)) || !up(d_cvlist, cv_list_.data(), 4 * cv_list_.size()))
+        !up(d_cvoffs, cv_offs_.data(), 4 * (g.nf + 1)) || !up(d_cvlist, cv_list_.data(), 4 * cv_list_.size()) ||
+        (d_efree && !up(d_efree, g.efree.data(), 4 * (size_t)g.ne)))
         return ORBX_EIO;
     if (timing)
         std::fprintf(stderr, "orbx_local_ba alloc ms: pairs %.3f lists %.3f arena %.3f uploads %.3f\n", t_pairs,
@@ -2064,6 +2095,19 @@ void BA::set_active(const std::vector<uint8_t> &act) {
     act_ = act;
     s_zero_ = false;
     const Graph &g = g_;
+    if (d_efree) {   // (fast mode, dense product, no repeated observation: the device builds the set)
+        use_map = true;
+        nmatch_ = 0;
+        nusable_ = 0;
+        // (the map is cleared even with no edges: the dense product reads it)
+        if (g.nf && g.npt) (void)hipMemsetAsync(d_cmap, 0xFF, 4 * (size_t)g.nf * g.npt, st_);
+        if (!g.ne) return;
+        std::memcpy(h_stage, act.data(), g.ne);
+        (void)hipMemcpyAsync(d_active, h_stage, g.ne, hipMemcpyHostToDevice, st_);
+        hipLaunchKernelGGL(k_ba_usable_map, dim3((g.ne + 255) / 256), dim3(256), 0, st_, d_active, d_efree, d_epoint,
+                           g.ne, g.npt, d_usable, d_cmap);
+        return;
+    }
     uint8_t *h_act = h_stage, *h_us = h_stage + g.ne;
     int32_t *h_coffs = h_coffs_, *h_clist = h_coffs_ + g.nf + 1;
     std::fill(h_coffs, h_coffs + g.nf + 1, 0);
@@ -2106,7 +2150,8 @@ void BA::set_active(const std::vector<uint8_t> &act) {
     if (!use_map || !g.nf) return;
     if (g.npt) {
         (void)hipMemsetAsync(d_cmap, 0xFF, 4 * (size_t)g.nf * g.npt, st_);
-        hipLaunchKernelGGL(k_ba_cmap, dim3(g.nf), dim3(256), 0, st_, d_coffs, d_clist, d_epoint, g.npt, d_cmap);
+        hipLaunchKernelGGL(k_ba_cmap, dim3(g.nf), dim3(256), 0, st_, d_coffs, d_clist, d_epoint, g.npt, d_cmap,
+                           fast_ && dense_schur_on() ? 1 : 0);
     }
     if (npairs > 0 && !dense()) {   // the pairs' shared-point lists: count, scan, fill
         hipLaunchKernelGGL(k_ba_pair_matches, dim3((npairs + 3) / 4), dim3(256), 0, st_, d_pairs, npairs, d_coffs,
@@ -2198,7 +2243,7 @@ int BA::solve_async(double lambda) {
     if (dn) {   // S and bs from one dense product (k_ba_schur_*)
         const int64_t tot = (int64_t)schur_kp_ * schur_ct_;
         hipLaunchKernelGGL(k_ba_schur_ops, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st_, g.npt, g.nf,
-                           schur_ct_, schur_ucol_, schur_kp_, d_cmap, d_clist, d_eo, d_lu, d_M);
+                           schur_ct_, schur_ucol_, schur_kp_, d_cmap, d_eo, g.ne, d_lu, d_M);
         hipLaunchKernelGGL(k_ba_schur_mfma, dim3(schur_nblk_, schur_nch_), dim3(256), 0, st_, d_M, schur_ct_,
                            schur_h_, d_spart);
         hipLaunchKernelGGL(k_ba_schur_sum, dim3((n * n + n + 255) / 256), dim3(256), 0, st_, d_spart, schur_nch_,
