@@ -585,13 +585,17 @@ typedef struct orbx_ba_edge {
 int orbx_local_ba(int device, const float *Tcw, const uint8_t *fixed, int ncam, const float *Xw, int npt,
                   const orbx_ba_edge *edges, int ne, int iters1, int iters2, float *Tcw_out, float *Xw_out,
                   uint8_t *outlier, int *iterations);
-/* The same optimisation in a fast mode: the per-vertex (Hpp, bp, reduced
- * right-hand side) and per-camera-pair (Schur complement) sums as parallel
- * reductions instead of sequential chains in edge / point order.  Same
+/* The same optimisation in a fast mode: the per-vertex sums as parallel
+ * reductions instead of sequential chains in edge / point order, the Schur
+ * complement and reduced right-hand side as one dense FP64 matrix-core
+ * product (S = Hpp + lambda I - W^T W, W_p = L_p^-1 B_p^T with D_p = L_p L_p^T),
+ * the reduced system factored as an augmented matrix with its trailing tiles
+ * on the matrix cores, the trial's acceptance decided on the device.  Same
  * algorithm, another floating-point order: outputs equal orbx_local_ba's to
- * rounding (tolerances in tests/test_gpu_ba.py), not bit for bit.  No
- * reference counterpart beyond LocalBundleAdjustment itself, whose g2o sums
- * are unordered too. */
+ * rounding (tolerances in tests/test_gpu_ba.py), not bit for bit; the LM
+ * iteration counts and outlier flags came out equal on every test problem.
+ * No reference counterpart beyond LocalBundleAdjustment itself, whose g2o
+ * sums are unordered too. */
 int orbx_local_ba_fast(int device, const float *Tcw, const uint8_t *fixed, int ncam, const float *Xw, int npt,
                        const orbx_ba_edge *edges, int ne, int iters1, int iters2, float *Tcw_out, float *Xw_out,
                        uint8_t *outlier, int *iterations);
