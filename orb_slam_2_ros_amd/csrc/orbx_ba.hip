@@ -492,6 +492,17 @@ __global__ void k_ba_cmap(const int32_t *coffs, const int32_t *clist, const int3
         cmap[(int64_t)f * npt + epoint[clist[t]]] = ids ? clist[t] : t;
 }
 
+// The second pass's active set (Optimizer.cc:791-826: an observation with
+// chi2 > 5.991 (mono) / 7.815 (stereo), or behind the camera, leaves it), on
+// the device: the host's rule on the device's chi2 and front flags
+__global__ void k_ba_pass2_active(const EdgeD *edges, int ne, const double *chi2, const uint8_t *front,
+                                  uint8_t *active) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= ne) return;
+    const double th = edges[e].stereo ? 7.815 : 5.991;
+    active[e] = !(chi2[e] > th || !front[e]);
+}
+
 // Fast mode's active set on the device (a graph whose free cameras observe
 // each point at most once): usable = active with a free camera, and the
 // camera x point -> edge map the dense Schur product reads -- no host lists
@@ -1773,6 +1784,7 @@ public:
     int alloc();
     int upload(const double *pts);
     void set_active(const std::vector<uint8_t> &act);
+    int set_active_pass2();   // (fast mode, device-built sets) the second pass's set without a round trip
     int errors(bool robust, double *chi_sum);
     int build(const int *gate = nullptr);
     int solve(double lambda, int *ok);
@@ -2089,6 +2101,26 @@ int BA::upload(const double *pts) {
 // (the caller synchronises the stream before the next set_active); device:
 // the point -> list-position map, the pairs' shared-point counts, their scan
 // and the lists.  Nothing waits here.
+// the second pass's active set from the device's errors: the front flags at
+// the current estimate (download's k_ba_errors front_only), the outlier rule,
+// then the usable flags and the map (set_active's device path)
+int BA::set_active_pass2() {
+    const Graph &g = g_;
+    s_zero_ = false;
+    use_map = true;
+    nmatch_ = 0;
+    nusable_ = 0;
+    if (g.nf && g.npt && hipMemsetAsync(d_cmap, 0xFF, 4 * (size_t)g.nf * g.npt, st_) != hipSuccess) return ORBX_EIO;
+    if (!g.ne) return ORBX_OK;
+    hipLaunchKernelGGL(k_ba_errors, dim3((g.ne + 63) / 64), dim3(64), 0, st_, d_pose, d_pts, d_edges, g.ne, d_active, 0,
+                       1, d_err, d_chi2, d_rho, d_front, nullptr, nullptr);
+    hipLaunchKernelGGL(k_ba_pass2_active, dim3((g.ne + 255) / 256), dim3(256), 0, st_, d_edges, g.ne, d_chi2, d_front,
+                       d_active);
+    hipLaunchKernelGGL(k_ba_usable_map, dim3((g.ne + 255) / 256), dim3(256), 0, st_, d_active, d_efree, d_epoint, g.ne,
+                       g.npt, d_usable, d_cmap);
+    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EIO;
+}
+
 void BA::set_active(const std::vector<uint8_t> &act) {
     static const bool timing = std::getenv("ORBX_BA_TIMING") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
@@ -2599,17 +2631,24 @@ static int local_ba(int device, bool fast, const float *Tcw, const uint8_t *fixe
         lap("lm1");
         std::vector<double> chi2;
         std::vector<uint8_t> front;
-        if (!rc) rc = ba.download(pts.data(), chi2, front);
+        // (fast mode with device-built sets: the second pass's set is made on
+        // the device, with no download in between)
+        const bool dev2 = !rc && iters2 > 0 && ba.d_efree;
+        if (!rc && !dev2) rc = ba.download(pts.data(), chi2, front);
         lap("download1");
         if (!rc && iters2 > 0) {
             // outliers leave the second pass (setLevel(1)); every kernel is dropped (:791-826)
-            for (int e = 0; e < ne; ++e) {
-                const double th = g.raw[e].ur >= 0 ? 7.815 : 5.991;
-                if (chi2[e] > th || !front[e]) act[e] = 0;
+            if (dev2) {
+                rc = ba.set_active_pass2();
+            } else {
+                for (int e = 0; e < ne; ++e) {
+                    const double th = g.raw[e].ur >= 0 ? 7.815 : 5.991;
+                    if (chi2[e] > th || !front[e]) act[e] = 0;
+                }
+                ba.set_active(act);
             }
-            ba.set_active(act);
             lap("active2");
-            its[1] = lm_optimize(ba, iters2, false, &rc);
+            if (!rc) its[1] = lm_optimize(ba, iters2, false, &rc);
             lap("lm2");
             if (!rc) rc = ba.download(pts.data(), chi2, front);
             lap("download2");

@@ -39,4 +39,7 @@ print('mono', emulate(P['Tcw'], P['fixed'], P['Xw'], E))
 print('empty', emulate(P['Tcw'], P['fixed'], P['Xw'], E[:0]))
 P = make_ba_problem(n_local=20, n_fixed=4, n_points=3000, seed=2)
 print('bench', emulate(P['Tcw'], P['fixed'], P['Xw'], P['edges'][:4000]))
+# the second pass's set (set_active_pass2): a subset active, the map cleared first
+rng = np.random.default_rng(0)
+print('pass2', emulate(P['Tcw'], P['fixed'], P['Xw'], P['edges'], act=(rng.random(len(P['edges'])) > 0.1).astype(np.uint8)))
 print('index logic ok')
