@@ -2,7 +2,7 @@
 k_ba_schur_ops map reads): every map entry it reads is -1 or an edge, with and without edges.
     python tools/ba_index_check.py"""
 import sys, numpy as np
-sys.path.insert(0, '/root/repo')
+sys.path.insert(0, str(__import__('pathlib').Path(__file__).resolve().parents[1]))
 from orb_slam_2_ros_amd.synth_ba import make_ba_problem
 
 def emulate(Tcw, fixed, Xw, edges, act=None):
