@@ -345,9 +345,18 @@ __global__ void k_ba_reduce(const EdgeOut *eo, const int32_t *offs, const int32_
         for (int j = 0; j < 8; ++j)
             if (a[j]) acc = acc + val[j];
     }
-    for (; t < te; ++t) {
-        const int ei = list[t];
-        if (active[ei]) acc = acc + base[(int64_t)ei * kEo];
+    if (t < te) {   // the tail too: its loads in flight together, then added in edge order
+        const int nr = te - t;
+        int ei[8];
+        double val[8];
+        bool a[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ei[j] = list[t + (j < nr ? j : 0)];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { a[j] = j < nr && active[ei[j]]; val[j] = base[(int64_t)ei[j] * kEo]; }
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (a[j]) acc = acc + val[j];
     }
     if (lane < nh) H[(int64_t)v * nh + lane] = acc;
     else b[(int64_t)v * nb + lane - nh] = acc;
